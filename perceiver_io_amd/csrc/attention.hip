@@ -1,0 +1,488 @@
+// Flash-style multi-head attention for the Perceiver's asymmetric shapes (CDNA4 / gfx950).
+//
+// Replaces nn.MultiheadAttention's unfused core (reference perceiver/model.py:59-74,
+// SURVEY K-07/K-08): QK^T → key-padding mask → softmax → dropout → PV, never
+// materialising P.  One kernel family serves all three Perceiver attentions:
+//   * encoder cross-attention: few latent queries × many inputs (split-KV over the grid)
+//   * latent self-attention:   N × N, N ≤ 512
+//   * decoder cross-attention: many output queries × few latents (q batch-stride 0
+//     lets the batch-independent output-query projection be computed once)
+//
+// Layouts (element strides, bf16): X[b, n, h*D + j] at X + b*bstride + n*rstride + h*D + j,
+// so Q/K/V can be column slices of packed projection outputs.  O is (B, Nq, H*D) bf16,
+// LSE / delta are (B, Nq, H) fp32 in log2 units (scores are pre-multiplied by
+// scale*log2(e) so every exponential is a native v_exp_f32 = exp2).
+//
+// Forward, per wave: 32 queries.  S^T = K·Q^T (v_mfma_f32_32x32x16_bf16: keys on the
+// accumulator rows, the query on the lane) so the softmax max/sum over keys is
+// in-register + one lane^32 exchange, and P^T feeds O^T += V^T·P^T straight from the
+// accumulator registers (no LDS round trip for P).  V^T fragments come from the LDS V
+// tile with ds_read_b64_tr_b16 (hardware transpose).
+//
+// Backward, per workgroup: 128 keys (32 per wave), sweeping every query tile:
+//   S = Q·K^T, dP = dO·V^T (query rows in registers, key on the lane),
+//   dV += P^T·dO and dK += dS^T·Q from the accumulators (transpose reads of the LDS Q/dO
+//   tiles), dQ via one LDS transpose of dS, summed over the 4 waves in LDS, then one
+//   fp32 atomic add per element per workgroup (SURVEY §2.3 K-07 backward).
+// Fully-masked query rows produce O = 0 and zero gradients (defect D10 defined).
+#include "common.h"
+
+namespace pio {
+
+constexpr int KT = 64;  // keys per forward tile
+
+// A-operand read of V^T / dO^T / Q^T from an LDS tile stored [k][i] with the k order
+// permuted to match an accumulator used as the other operand (see common.h).
+__device__ __forceinline__ bf16x8 frag_ks_perm(const uint16_t* lds, int ld, int i0, int k0) {
+  const int l = lane_id();
+  const int g = l >> 4, i = l & 15, q = i >> 2, p = i & 3;
+  const uint16_t* base = lds + (k0 + 4 * (g >> 1) + q) * ld + i0 + 16 * (g & 1) + 4 * p;
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(base));
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(base + 8 * ld));
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+// pack accumulator registers 8s..8s+7 to a bf16 operand fragment
+__device__ __forceinline__ bf16x8 pack_acc(const f32x16& a, int s) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (short)f2bf(a[8 * s + j]);
+  return r;
+}
+
+struct AttnArgs {
+  const uint16_t* q; long long q_bs; int q_rs;
+  const uint16_t* k; long long k_bs; int k_rs;
+  const uint16_t* v; long long v_bs; int v_rs;
+  const uint8_t* kmask;  // (B, Nk), nonzero = padding key; may be null
+  int B, H, Nq, Nk;
+  float scale_log2;      // softmax scale * log2(e)
+  float scale;           // softmax scale (backward)
+  uint32_t drop_thresh;  // dropout probability * 2^32 (0 = off)
+  float drop_scale;      // 1 / (1 - p)
+  uint32_t seed;
+};
+
+// ------------------------------------------------------------------------------------
+// forward
+// ------------------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a, uint16_t* __restrict__ O, float* __restrict__ LSE,
+                                                       float* __restrict__ Opart, float* __restrict__ MLpart,
+                                                       int nsplit, int tiles_per_split) {
+  constexpr int LDK = D + 8;                 // K tile [key][d], 16-B padded rows
+  constexpr int LDV = (D < 32 ? 32 : D) + 8;  // V tile [key][d]; D=16 zero-padded to 32 columns
+  constexpr int NT = (D < 32) ? 1 : D / 32;   // O^T tiles of 32 rows (head-dim)
+  constexpr int KS = D / 16;                  // k-steps for QK^T
+  __shared__ __attribute__((aligned(16))) uint16_t sK[KT * LDK];
+  __shared__ __attribute__((aligned(16))) uint16_t sV[KT * LDV + 64];
+
+  const int nwaves = blockDim.x >> 6;
+  const int w = wave_id(), l = lane_id(), r = l & 31, hh = l >> 5;
+  const int h = blockIdx.y;
+  const int b = blockIdx.z / nsplit, split = blockIdx.z % nsplit;
+  const int q0 = (blockIdx.x * nwaves + w) * 32;
+  const int qi = q0 + r;
+  const int qc = qi < a.Nq ? qi : a.Nq - 1;
+
+  // this wave's Q^T operand fragments (B operand: B[k=d][col=query])
+  bf16x8 qf[KS];
+  {
+    const uint16_t* qp = a.q + (long long)b * a.q_bs + (long long)qc * a.q_rs + h * D + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qp + 16 * s);
+  }
+
+  if (D < 32) {  // zero the unused head-dim columns 16..31 of the V tile once
+    for (int i = threadIdx.x; i < KT; i += blockDim.x)
+      *reinterpret_cast<bf16x8*>(sV + i * LDV + 16) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0},
+      *reinterpret_cast<bf16x8*>(sV + i * LDV + 24) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+
+  f32x16 o[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) o[t] = f32x16{};
+  float m_run = -1e30f, l_run = 0.f;
+
+  const int ntiles = (a.Nk + KT - 1) / KT;
+  const int t_begin = split * tiles_per_split;
+  const int t_end = min(ntiles, t_begin + tiles_per_split);
+  const uint16_t* kb = a.k + (long long)b * a.k_bs + h * D;
+  const uint16_t* vb = a.v + (long long)b * a.v_bs + h * D;
+  constexpr int CH = D / 8;  // 16-byte chunks per row
+
+  for (int t = t_begin; t < t_end; ++t) {
+    const int key0 = t * KT;
+    __syncthreads();
+    for (int c = threadIdx.x; c < KT * CH; c += blockDim.x) {
+      const int kr = c / CH, col = (c % CH) * 8;
+      const int key = key0 + kr;
+      bf16x8 kv = bf16x8{0, 0, 0, 0, 0, 0, 0, 0}, vv = kv;
+      if (key < a.Nk) {
+        kv = *reinterpret_cast<const bf16x8*>(kb + (long long)key * a.k_rs + col);
+        vv = *reinterpret_cast<const bf16x8*>(vb + (long long)key * a.v_rs + col);
+      }
+      *reinterpret_cast<bf16x8*>(sK + kr * LDK + col) = kv;
+      *reinterpret_cast<bf16x8*>(sV + kr * LDV + col) = vv;
+    }
+    // key-padding bits for this tile (bit i = key0+i is padding or out of range)
+    uint64_t padbits;
+    {
+      const int key = key0 + l;
+      bool pad = key >= a.Nk;
+      if (!pad && a.kmask) pad = a.kmask[(long long)b * a.Nk + key] != 0;
+      padbits = __ballot(pad);
+    }
+    __syncthreads();
+
+    f32x16 s[2];
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      s[kh] = f32x16{};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) s[kh] = mfma32(frag_kc(sK, LDK, 32 * kh, 16 * ks), qf[ks], s[kh]);
+    }
+    // scale, mask, tile max
+    float mt = -INFINITY;
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int kr = 32 * kh + acc_row(i, hh);
+        float v = s[kh][i] * a.scale_log2;
+        v = ((padbits >> kr) & 1ull) ? -INFINITY : v;
+        s[kh][i] = v;
+        mt = fmaxf(mt, v);
+      }
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float m_new = fmaxf(m_run, mt);
+    const float alpha = exp2f(m_run - m_new);
+    m_run = m_new;
+    float ls = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float p = exp2f(s[kh][i] - m_new);
+        ls += p;
+        if (a.drop_thresh) {
+          const int key = key0 + 32 * kh + acc_row(i, hh);
+          const uint32_t idx = (uint32_t)qi * (uint32_t)a.Nk + (uint32_t)key;
+          p = keep_elem(a.seed, (uint32_t)(b * a.H + h), idx, a.drop_thresh) ? p * a.drop_scale : 0.f;
+        }
+        s[kh][i] = p;
+      }
+    l_run = l_run * alpha + ls;
+#pragma unroll
+    for (int t2 = 0; t2 < NT; ++t2)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) o[t2][i] *= alpha;
+    // O^T += V^T · P^T
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const bf16x8 pb = pack_acc(s[kh], ss);
+#pragma unroll
+        for (int t2 = 0; t2 < NT; ++t2)
+          o[t2] = mfma32(frag_ks_perm(sV, LDV, 32 * t2, 32 * kh + 16 * ss), pb, o[t2]);
+      }
+  }
+
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  if (qi >= a.Nq) return;
+  const int HD = a.H * D;
+  if (nsplit == 1) {
+    const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+    uint16_t* op = O + ((long long)b * a.Nq + qi) * HD + h * D;
+#pragma unroll
+    for (int t2 = 0; t2 < NT; ++t2)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int dd = 32 * t2 + 8 * g + 4 * hh;
+        if (dd < D) {
+          uint2 pk;
+          pk.x = pack2(o[t2][4 * g] * inv, o[t2][4 * g + 1] * inv);
+          pk.y = pack2(o[t2][4 * g + 2] * inv, o[t2][4 * g + 3] * inv);
+          *reinterpret_cast<uint2*>(op + dd) = pk;
+        }
+      }
+    if (hh == 0) LSE[((long long)b * a.Nq + qi) * a.H + h] = l_tot > 0.f ? m_run + __log2f(l_tot) : INFINITY;
+  } else {
+    // unnormalised partials: Opart[split][b][q][h][D], MLpart[split][b][q][h][2]
+    const long long row = (((long long)split * a.B + b) * a.Nq + qi) * a.H + h;
+    float* op = Opart + row * D;
+#pragma unroll
+    for (int t2 = 0; t2 < NT; ++t2)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int dd = 32 * t2 + 8 * g + 4 * hh;
+        if (dd < D)
+          *reinterpret_cast<float4*>(op + dd) = make_float4(o[t2][4 * g], o[t2][4 * g + 1], o[t2][4 * g + 2], o[t2][4 * g + 3]);
+      }
+    if (hh == 0) {
+      MLpart[row * 2] = m_run;
+      MLpart[row * 2 + 1] = l_tot;
+    }
+  }
+}
+
+// combine split-KV partials: one thread per (b, q, h, d)
+__global__ void attn_combine_kernel(const float* __restrict__ Opart, const float* __restrict__ MLpart,
+                                    uint16_t* __restrict__ O, float* __restrict__ LSE, int nsplit, int rows, int D) {
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long long)rows * D) return;
+  const long long row = idx / D;
+  const int d = idx % D;
+  float M = -1e30f;
+  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, MLpart[((long long)s * rows + row) * 2]);
+  float L = 0.f, acc = 0.f;
+  for (int s = 0; s < nsplit; ++s) {
+    const float m = MLpart[((long long)s * rows + row) * 2];
+    const float w = exp2f(m - M);
+    L += MLpart[((long long)s * rows + row) * 2 + 1] * w;
+    acc += Opart[((long long)s * rows + row) * D + d] * w;
+  }
+  O[row * D + d] = f2bf(L > 0.f ? acc / L : 0.f);  // rows ordered (b, q, h) → O[(b*Nq+q)*HD + h*D + d]
+  if (d == 0) LSE[row] = L > 0.f ? M + __log2f(L) : INFINITY;
+}
+
+// ------------------------------------------------------------------------------------
+// backward
+// ------------------------------------------------------------------------------------
+// delta[b, q, h] = sum_d dO * O (fp32), and zero dQ accumulator rows
+__global__ void attn_bwd_prep_kernel(const uint16_t* __restrict__ dO, const uint16_t* __restrict__ O,
+                                     float* __restrict__ delta, float* __restrict__ dq, int rows, int H, int D,
+                                     int dq_rs) {
+  const int row = blockIdx.x * (blockDim.x >> 6) + wave_id();
+  if (row >= rows) return;
+  const int l = lane_id();
+  const int HD = H * D;
+  for (int h = 0; h < H; ++h) {
+    float acc = 0.f;
+    for (int d = l; d < D; d += 64) acc += bf2f(dO[(long long)row * HD + h * D + d]) * bf2f(O[(long long)row * HD + h * D + d]);
+    acc = wave_sum(acc);
+    if (l == 0) delta[(long long)row * H + h] = acc;
+  }
+  for (int j = l; j < HD; j += 64) dq[(long long)row * dq_rs + j] = 0.f;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a, const uint16_t* __restrict__ dO,
+                                                       const float* __restrict__ LSE, const float* __restrict__ delta,
+                                                       float* __restrict__ dq, long long dq_bs, int dq_rs,
+                                                       float* __restrict__ dk, long long dk_bs, int dk_rs,
+                                                       float* __restrict__ dv, long long dv_bs, int dv_rs) {
+  constexpr int LD = (D < 32 ? 32 : D) + 8;  // Q / dO / K tiles [row][d] (D=16 zero-padded to 32 cols)
+  constexpr int NT = (D < 32) ? 1 : D / 32;
+  constexpr int KS = D / 16;
+  constexpr int LDS_ = 40;                   // dS tile [key][q] (32 q + pad)
+  __shared__ __attribute__((aligned(16))) uint16_t sQ[32 * LD + 64];
+  __shared__ __attribute__((aligned(16))) uint16_t sdO[32 * LD + 64];
+  __shared__ __attribute__((aligned(16))) uint16_t sK[128 * LD + 64];
+  __shared__ __attribute__((aligned(16))) uint16_t sdS[4 * 32 * LDS_];
+  __shared__ float sL[32], sDl[32];
+  __shared__ float sdQ[4][32 * (D + 1)];
+
+  const int w = wave_id(), l = lane_id(), r = l & 31, hh = l >> 5;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int kbase = blockIdx.x * 128;
+  const int key = kbase + 32 * w + r;         // this lane's key (column of S / dP)
+  const int kc = key < a.Nk ? key : a.Nk - 1;
+  bool kpad = key >= a.Nk;
+  if (!kpad && a.kmask) kpad = a.kmask[(long long)b * a.Nk + key] != 0;
+
+  // stage the block's K tile (for dQ) and zero padded columns
+  const uint16_t* kbp = a.k + (long long)b * a.k_bs + h * D;
+  const uint16_t* vbp = a.v + (long long)b * a.v_bs + h * D;
+  constexpr int CH = D / 8;
+  for (int c = threadIdx.x; c < 128 * CH; c += blockDim.x) {
+    const int kr = c / CH, col = (c % CH) * 8;
+    const int kk = kbase + kr;
+    bf16x8 kv = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (kk < a.Nk) kv = *reinterpret_cast<const bf16x8*>(kbp + (long long)kk * a.k_rs + col);
+    *reinterpret_cast<bf16x8*>(sK + kr * LD + col) = kv;
+  }
+  if (D < 32) {
+    for (int i = threadIdx.x; i < 128; i += blockDim.x) {
+      *reinterpret_cast<bf16x8*>(sK + i * LD + 16) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      *reinterpret_cast<bf16x8*>(sK + i * LD + 24) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+    for (int i = threadIdx.x; i < 32; i += blockDim.x) {
+      *reinterpret_cast<bf16x8*>(sQ + i * LD + 16) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      *reinterpret_cast<bf16x8*>(sQ + i * LD + 24) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      *reinterpret_cast<bf16x8*>(sdO + i * LD + 16) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      *reinterpret_cast<bf16x8*>(sdO + i * LD + 24) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  // K^T / V^T operand fragments for this wave's 32 keys (B operand: B[k=d][col=key])
+  bf16x8 kf[KS], vf[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    kf[s] = *reinterpret_cast<const bf16x8*>(kbp + (long long)kc * a.k_rs + 16 * s + 8 * hh);
+    vf[s] = *reinterpret_cast<const bf16x8*>(vbp + (long long)kc * a.v_rs + 16 * s + 8 * hh);
+  }
+  f32x16 dK[NT], dV[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) dK[t] = dV[t] = f32x16{};
+
+  const int HD = a.H * D;
+  const uint16_t* qbp = a.q + (long long)b * a.q_bs + h * D;
+  const uint16_t* dobp = dO + (long long)b * a.Nq * HD + h * D;
+  const int nqt = (a.Nq + 31) / 32;
+  uint16_t* mydS = sdS + w * 32 * LDS_;
+
+  for (int qt = 0; qt < nqt; ++qt) {
+    const int q0 = qt * 32;
+    __syncthreads();
+    for (int c = threadIdx.x; c < 32 * CH; c += blockDim.x) {
+      const int qr = c / CH, col = (c % CH) * 8;
+      const int qq = q0 + qr;
+      bf16x8 qv = bf16x8{0, 0, 0, 0, 0, 0, 0, 0}, dv8 = qv;
+      if (qq < a.Nq) {
+        qv = *reinterpret_cast<const bf16x8*>(qbp + (long long)qq * a.q_rs + col);
+        dv8 = *reinterpret_cast<const bf16x8*>(dobp + (long long)qq * HD + col);
+      }
+      *reinterpret_cast<bf16x8*>(sQ + qr * LD + col) = qv;
+      *reinterpret_cast<bf16x8*>(sdO + qr * LD + col) = dv8;
+    }
+    if (threadIdx.x < 32) {
+      const int qq = q0 + threadIdx.x;
+      sL[threadIdx.x] = qq < a.Nq ? LSE[((long long)b * a.Nq + qq) * a.H + h] : INFINITY;
+      sDl[threadIdx.x] = qq < a.Nq ? delta[((long long)b * a.Nq + qq) * a.H + h] : 0.f;
+    }
+    __syncthreads();
+
+    // S = Q K^T and dP = dO V^T  (rows: queries; lane: key)
+    f32x16 S = f32x16{}, dP = f32x16{};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      S = mfma32(frag_kc(sQ, LD, 0, 16 * s), kf[s], S);
+      dP = mfma32(frag_kc(sdO, LD, 0, 16 * s), vf[s], dP);
+    }
+    f32x16 P, dS;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int qr = acc_row(i, hh);
+      float p = kpad ? 0.f : exp2f(S[i] * a.scale_log2 - sL[qr]);
+      float dp = dP[i];
+      float pd = p;
+      if (a.drop_thresh) {
+        const uint32_t idx = (uint32_t)(q0 + qr) * (uint32_t)a.Nk + (uint32_t)key;
+        const bool keep = keep_elem(a.seed, (uint32_t)(b * a.H + h), idx, a.drop_thresh);
+        pd = keep ? p * a.drop_scale : 0.f;
+        dp = keep ? dp * a.drop_scale : 0.f;
+      }
+      P[i] = pd;
+      dS[i] = p * (dp - sDl[qr]);
+    }
+    // dV += P^T dO ; dK += dS^T Q   (accumulator as A operand: X^T · B)
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      const bf16x8 pa = pack_acc(P, ss), sa = pack_acc(dS, ss);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        dV[t] = mfma32(pa, frag_ks_perm(sdO, LD, 32 * t, 16 * ss), dV[t]);
+        dK[t] = mfma32(sa, frag_ks_perm(sQ, LD, 32 * t, 16 * ss), dK[t]);
+      }
+    }
+    // dS -> LDS as [key][q] (bf16) for the dQ product
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      uint2 pk;
+      pk.x = pack2(dS[4 * g], dS[4 * g + 1]);
+      pk.y = pack2(dS[4 * g + 2], dS[4 * g + 3]);
+      *reinterpret_cast<uint2*>(mydS + r * LDS_ + 8 * g + 4 * hh) = pk;
+    }
+    __syncthreads();
+    // dQ_part = dS (q × 32 keys of this wave) · K (32 keys × d)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      f32x16 dq_acc = f32x16{};
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss)
+        dq_acc = mfma32(frag_ks(mydS, LDS_, 0, 16 * ss), frag_ks(sK + (32 * w) * LD, LD, 32 * t, 16 * ss), dq_acc);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int dd = 32 * t + r;
+        if (dd < D) sdQ[w][acc_row(i, hh) * (D + 1) + dd] = dq_acc[i];
+      }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 32 * D; e += blockDim.x) {
+      const int qr = e / D, dd = e % D;
+      const int qq = q0 + qr;
+      if (qq < a.Nq) {
+        const float v = (sdQ[0][qr * (D + 1) + dd] + sdQ[1][qr * (D + 1) + dd] + sdQ[2][qr * (D + 1) + dd] +
+                         sdQ[3][qr * (D + 1) + dd]) * a.scale;
+        atomicAdd(dq + (long long)b * dq_bs + (long long)qq * dq_rs + h * D + dd, v);
+      }
+    }
+  }
+  // write dK (scaled) and dV: rows = keys (registers), lane = head-dim column
+  // accumulator: col = lane&31 = d, row = acc_row(reg) = key within the wave's 32
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int kk = kbase + 32 * w + acc_row(i, hh);
+      const int dd = 32 * t + r;
+      if (kk < a.Nk && dd < D) {
+        dk[(long long)b * dk_bs + (long long)kk * dk_rs + h * D + dd] = dK[t][i] * a.scale;
+        dv[(long long)b * dv_bs + (long long)kk * dv_rs + h * D + dd] = dV[t][i];
+      }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// host launchers
+// ------------------------------------------------------------------------------------
+template <int D>
+static void fwd_dispatch(const AttnArgs& a, uint16_t* O, float* LSE, float* Opart, float* MLpart, int nsplit,
+                         hipStream_t st) {
+  const int nwaves = a.Nq <= 32 ? 1 : (a.Nq <= 64 ? 2 : 4);
+  const int ntiles = (a.Nk + KT - 1) / KT;
+  const int tps = (ntiles + nsplit - 1) / nsplit;
+  dim3 grid((a.Nq + 32 * nwaves - 1) / (32 * nwaves), a.H, a.B * nsplit);
+  hipLaunchKernelGGL(attn_fwd_kernel<D>, grid, dim3(64 * nwaves), 0, st, a, O, LSE, Opart, MLpart, nsplit, tps);
+}
+
+void attn_fwd_launch(const AttnArgs& a, int D, uint16_t* O, float* LSE, float* Opart, float* MLpart, int nsplit,
+                     hipStream_t st) {
+  switch (D) {
+    case 16: fwd_dispatch<16>(a, O, LSE, Opart, MLpart, nsplit, st); break;
+    case 32: fwd_dispatch<32>(a, O, LSE, Opart, MLpart, nsplit, st); break;
+    case 64: fwd_dispatch<64>(a, O, LSE, Opart, MLpart, nsplit, st); break;
+    case 128: fwd_dispatch<128>(a, O, LSE, Opart, MLpart, nsplit, st); break;
+    default: break;
+  }
+  if (nsplit > 1) {
+    const long long rows = (long long)a.B * a.Nq * a.H;
+    const long long n = rows * D;
+    hipLaunchKernelGGL(attn_combine_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, Opart, MLpart, O, LSE,
+                       nsplit, (int)rows, D);
+  }
+}
+
+void attn_bwd_launch(const AttnArgs& a, int D, const uint16_t* O, const uint16_t* dO, const float* LSE, float* delta,
+                     float* dq, long long dq_bs, int dq_rs, float* dk, long long dk_bs, int dk_rs, float* dv,
+                     long long dv_bs, int dv_rs, bool dq_is_dense, hipStream_t st) {
+  // prep: delta and zero dQ (dQ buffer is (B, Nq, dq_rs) with dq_bs == Nq * dq_rs when dense)
+  const int rows = a.B * a.Nq;
+  hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, dO, O, delta, dq, rows, a.H, D,
+                     dq_rs);
+  (void)dq_is_dense;
+  dim3 grid((a.Nk + 127) / 128, a.H, a.B);
+  switch (D) {
+    case 16: hipLaunchKernelGGL(attn_bwd_kernel<16>, grid, dim3(256), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs); break;
+    case 32: hipLaunchKernelGGL(attn_bwd_kernel<32>, grid, dim3(256), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs); break;
+    case 64: hipLaunchKernelGGL(attn_bwd_kernel<64>, grid, dim3(256), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs); break;
+    case 128: hipLaunchKernelGGL(attn_bwd_kernel<128>, grid, dim3(256), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs); break;
+    default: break;
+  }
+}
+
+}  // namespace pio

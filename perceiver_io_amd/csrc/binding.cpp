@@ -1,0 +1,362 @@
+// PyTorch bindings for the Perceiver IO CDNA4 kernels.  Host-only translation unit
+// (g++): validates shapes/dtypes, allocates outputs, and launches on the current HIP
+// stream so every call is capturable in a hipGraph.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+namespace pio {
+struct AttnArgs {
+  const uint16_t* q; long long q_bs; int q_rs;
+  const uint16_t* k; long long k_bs; int k_rs;
+  const uint16_t* v; long long v_bs; int v_rs;
+  const uint8_t* kmask;
+  int B, H, Nq, Nk;
+  float scale_log2, scale;
+  uint32_t drop_thresh;
+  float drop_scale;
+  uint32_t seed;
+};
+struct ReduceJob { const float* src; float* dst; int len, nslab, accumulate; };
+struct ReduceJobs { ReduceJob j[12]; int n; };
+
+void attn_fwd_launch(const AttnArgs&, int, uint16_t*, float*, float*, float*, int, hipStream_t);
+void attn_bwd_launch(const AttnArgs&, int, const uint16_t*, const uint16_t*, const float*, float*, float*, long long,
+                     int, float*, long long, int, float*, long long, int, bool, hipStream_t);
+void ln_linear_fwd_launch(const void*, bool, int, int, int, const float*, const float*, float, const uint16_t*,
+                          const float*, int, int, const float*, int, void*, bool, int, float*, float*, hipStream_t);
+void post_attn_fwd_launch(int, const uint16_t*, const float*, const uint16_t*, const float*, const float*,
+                          const float*, float, const uint16_t*, const float*, const uint16_t*, const float*, float*,
+                          float*, float*, float*, uint16_t*, int, hipStream_t);
+void post_attn_bwd_launch(int, const float*, const float*, const float*, const float*, const uint16_t*,
+                          const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*, const float*, float*,
+                          uint16_t*, uint16_t*, float*, int, float*, float*, int, hipStream_t);
+void ln_linear_dgrad_launch(const void*, bool, int, int, const uint16_t*, int, const void*, bool, int, const float*,
+                            const float*, const float*, const float*, int, float*, int, float*, float*, int,
+                            hipStream_t);
+void wgrad_launch(const void*, bool, int, int, const void*, bool, int, int, int, const float*, const float*,
+                  const float*, const float*, int, int, float*, float*, hipStream_t);
+void slab_reduce_launch(const ReduceJobs&, hipStream_t);
+void ce_fwd_launch(int, const uint16_t*, const int64_t*, const uint16_t*, const float*, int, int, float*, float*,
+                   float*, float*, int, hipStream_t);
+int ce_num_splits(int, int);
+void ce_bwd_launch(int, const uint16_t*, const int64_t*, const uint16_t*, const float*, const float*, const float*,
+                   int, int, float*, float*, float*, int, hipStream_t);
+void embed_fwd_launch(const int64_t*, const float*, const float*, float*, long long, int, int, float, hipStream_t);
+void embed_bwd_launch(const int64_t*, const float*, float*, float*, int, int, int, float, hipStream_t);
+void text_mask_launch(const int64_t*, const bool*, const float*, const int64_t*, int64_t*, int64_t*, long long, int,
+                      int, float, hipStream_t);
+void sumsq_launch(const float*, long long, float*, hipStream_t);
+void adamw_launch(float*, const float*, float*, float*, uint16_t*, long long, const float*, float, float, float, float,
+                  hipStream_t);
+void cast_bf16_launch(const float*, uint16_t*, long long, hipStream_t);
+}  // namespace pio
+
+using torch::Tensor;
+using OptT = c10::optional<Tensor>;
+
+namespace {
+hipStream_t stream() { return at::hip::getCurrentHIPStream(); }
+
+#define CHECK_CUDA(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_DT(t, dt) TORCH_CHECK((t).scalar_type() == (dt), #t " has wrong dtype ", (t).scalar_type())
+
+const uint16_t* bfp(const Tensor& t) { CHECK_DT(t, torch::kBFloat16); return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
+uint16_t* bfp_mut(Tensor& t) { CHECK_DT(t, torch::kBFloat16); return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+const float* f32p(const Tensor& t) { CHECK_DT(t, torch::kFloat32); return t.data_ptr<float>(); }
+const float* f32o(const OptT& t) { return t.has_value() ? f32p(*t) : nullptr; }
+bool is_bf16(const Tensor& t) {
+  TORCH_CHECK(t.scalar_type() == torch::kBFloat16 || t.scalar_type() == torch::kFloat32, "expected bf16/fp32");
+  return t.scalar_type() == torch::kBFloat16;
+}
+
+// 3-D (B|1, N, >=HD) view with unit inner stride → (batch stride, row stride)
+void strides3(const Tensor& t, int B, long long& bs, int& rs) {
+  TORCH_CHECK(t.dim() == 3 && t.stride(2) == 1, "attention operand must be 3-D with unit inner stride");
+  TORCH_CHECK(t.size(0) == B || t.size(0) == 1, "batch mismatch");
+  bs = t.size(0) == 1 ? 0 : t.stride(0);
+  rs = (int)t.stride(1);
+  TORCH_CHECK(rs % 8 == 0 && (bs % 8 == 0) && (reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0),
+              "attention operands need 16-byte aligned rows");
+}
+
+pio::AttnArgs make_args(const Tensor& q, const Tensor& k, const Tensor& v, const OptT& kmask, int H, int D,
+                        double scale, double dropout_p, int64_t seed) {
+  CHECK_CUDA(q); CHECK_CUDA(k); CHECK_CUDA(v);
+  pio::AttnArgs a{};
+  a.B = (int)std::max(q.size(0), k.size(0));
+  a.H = H;
+  a.Nq = (int)q.size(1);
+  a.Nk = (int)k.size(1);
+  TORCH_CHECK(v.size(1) == a.Nk, "K/V length mismatch");
+  TORCH_CHECK(D == 16 || D == 32 || D == 64 || D == 128, "head dim must be 16/32/64/128, got ", D);
+  TORCH_CHECK(q.size(2) >= H * D && k.size(2) >= H * D && v.size(2) >= H * D, "head columns out of range");
+  TORCH_CHECK(k.size(0) == a.B && v.size(0) == a.B, "K/V must carry the full batch");
+  a.q = bfp(q); a.k = bfp(k); a.v = bfp(v);
+  strides3(q, a.B, a.q_bs, a.q_rs);
+  strides3(k, a.B, a.k_bs, a.k_rs);
+  strides3(v, a.B, a.v_bs, a.v_rs);
+  a.kmask = nullptr;
+  if (kmask.has_value()) {
+    const Tensor& m = *kmask;
+    CHECK_CUDA(m);
+    TORCH_CHECK(m.scalar_type() == torch::kBool || m.scalar_type() == torch::kUInt8, "key mask must be bool/uint8");
+    TORCH_CHECK(m.is_contiguous() && m.size(0) == a.B && m.size(1) == a.Nk, "key mask must be (B, Nk) contiguous");
+    a.kmask = reinterpret_cast<const uint8_t*>(m.data_ptr());
+  }
+  a.scale = (float)scale;
+  a.scale_log2 = (float)(scale * 1.4426950408889634);
+  a.drop_thresh = dropout_p > 0 ? (uint32_t)std::min(4294967295.0, dropout_p * 4294967296.0) : 0u;
+  a.drop_scale = dropout_p > 0 ? (float)(1.0 / (1.0 - dropout_p)) : 1.f;
+  a.seed = (uint32_t)seed;
+  return a;
+}
+}  // namespace
+
+std::vector<Tensor> attn_fwd(Tensor q, Tensor k, Tensor v, OptT kmask, int64_t H, int64_t D, double scale,
+                             double dropout_p, int64_t seed, int64_t nsplit) {
+  auto a = make_args(q, k, v, kmask, (int)H, (int)D, scale, dropout_p, seed);
+  auto opts = q.options();
+  Tensor O = torch::empty({a.B, a.Nq, H * D}, opts.dtype(torch::kBFloat16));
+  Tensor L = torch::empty({a.B, a.Nq, H}, opts.dtype(torch::kFloat32));
+  Tensor Op, ML;
+  float* opp = nullptr; float* mlp = nullptr;
+  if (nsplit > 1) {
+    Op = torch::empty({nsplit, a.B, a.Nq, H, D}, opts.dtype(torch::kFloat32));
+    ML = torch::empty({nsplit, a.B, a.Nq, H, 2}, opts.dtype(torch::kFloat32));
+    opp = Op.data_ptr<float>(); mlp = ML.data_ptr<float>();
+  }
+  pio::attn_fwd_launch(a, (int)D, bfp_mut(O), L.data_ptr<float>(), opp, mlp, (int)std::max<int64_t>(1, nsplit), stream());
+  return {O, L};
+}
+
+// returns (dq, dk, dv) fp32; dq is per batch even when q is batch-broadcast.  Optional
+// *_out tensors (B, N, >=HD views, unit inner stride) let the results land in packed buffers;
+// a dq_out view must be batch-dense (batch stride == Nq * row stride).
+std::vector<Tensor> attn_bwd(Tensor q, Tensor k, Tensor v, OptT kmask, Tensor o, Tensor dO, Tensor lse, OptT delta_in,
+                             int64_t H, int64_t D, double scale, double dropout_p, int64_t seed, OptT dq_out,
+                             OptT dk_out, OptT dv_out) {
+  auto a = make_args(q, k, v, kmask, (int)H, (int)D, scale, dropout_p, seed);
+  TORCH_CHECK(dO.is_contiguous() && o.is_contiguous(), "O / dO must be contiguous (B, Nq, H*D)");
+  auto f32 = q.options().dtype(torch::kFloat32);
+  Tensor dq = dq_out.has_value() ? *dq_out : torch::empty({a.B, a.Nq, H * D}, f32);
+  Tensor dk = dk_out.has_value() ? *dk_out : torch::empty({a.B, a.Nk, H * D}, f32);
+  Tensor dv = dv_out.has_value() ? *dv_out : torch::empty({a.B, a.Nk, H * D}, f32);
+  TORCH_CHECK(dq.stride(2) == 1 && dk.stride(2) == 1 && dv.stride(2) == 1, "dq/dk/dv need unit inner stride");
+  TORCH_CHECK(dq.size(0) == a.B && dq.stride(0) == a.Nq * dq.stride(1), "dq must be batch-dense");
+  CHECK_DT(dq, torch::kFloat32); CHECK_DT(dk, torch::kFloat32); CHECK_DT(dv, torch::kFloat32);
+  Tensor delta = torch::empty({a.B, a.Nq, H}, f32);
+  (void)delta_in;
+  pio::attn_bwd_launch(a, (int)D, bfp(o), bfp(dO), f32p(lse), delta.data_ptr<float>(), dq.data_ptr<float>(),
+                       dq.stride(0), (int)dq.stride(1), dk.data_ptr<float>(), dk.stride(0), (int)dk.stride(1),
+                       dv.data_ptr<float>(), dv.stride(0), (int)dv.stride(1), true, stream());
+  return {dq, dk, dv};
+}
+
+std::vector<Tensor> ln_linear_fwd(Tensor x, OptT lnw, OptT lnb, double eps, Tensor w, OptT bias, int64_t act, OptT res,
+                                  bool out_bf16, bool save_stats) {
+  CHECK_CUDA(x); CHECK_CUDA(w);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be 2-D rows");
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous() && w.size(1) == x.size(1), "w must be (N, Kin) contiguous");
+  const int R = (int)x.size(0), Kin = (int)x.size(1), N = (int)w.size(0);
+  TORCH_CHECK(Kin <= 256, "Kin > 256 unsupported");
+  auto opts = x.options();
+  Tensor y = torch::empty({R, N}, opts.dtype(out_bf16 ? torch::kBFloat16 : torch::kFloat32));
+  Tensor mean, rstd;
+  float *mp = nullptr, *rp = nullptr;
+  if (save_stats && lnw.has_value()) {
+    mean = torch::empty({R}, opts.dtype(torch::kFloat32));
+    rstd = torch::empty({R}, opts.dtype(torch::kFloat32));
+    mp = mean.data_ptr<float>(); rp = rstd.data_ptr<float>();
+  }
+  const float* rptr = nullptr; int res_rs = 0;
+  if (res.has_value()) { rptr = f32p(*res); res_rs = (int)res->stride(0); TORCH_CHECK(res->stride(1) == 1); }
+  pio::ln_linear_fwd_launch(x.data_ptr(), is_bf16(x), (int)x.stride(0), R, Kin, f32o(lnw), f32o(lnb), (float)eps, bfp(w),
+                            f32o(bias), N, (int)act, rptr, res_rs, y.data_ptr(), out_bf16, N, mp, rp, stream());
+  std::vector<Tensor> out{y};
+  if (mp) { out.push_back(mean); out.push_back(rstd); }
+  return out;
+}
+
+std::vector<Tensor> post_attn_fwd(Tensor o, Tensor x, Tensor wo, Tensor bo, Tensor g2, Tensor be2, double eps,
+                                  Tensor w1, Tensor b1, Tensor w2, Tensor b2) {
+  TORCH_CHECK(o.is_contiguous() && x.is_contiguous(), "o/x must be contiguous (R, C)");
+  const int R = (int)o.size(0), C = (int)o.size(1);
+  TORCH_CHECK(C == 32 || C == 64 || C == 128, "post_attn supports C in {32, 64, 128}");
+  auto f32 = x.options().dtype(torch::kFloat32);
+  Tensor z = torch::empty({R, C}, f32), y = torch::empty({R, C}, f32);
+  Tensor m = torch::empty({R}, f32), r = torch::empty({R}, f32);
+  Tensor u = torch::empty({R, C}, x.options().dtype(torch::kBFloat16));
+  pio::post_attn_fwd_launch(C, bfp(o), f32p(x), bfp(wo), f32p(bo), f32p(g2), f32p(be2), (float)eps, bfp(w1), f32p(b1),
+                            bfp(w2), f32p(b2), z.data_ptr<float>(), y.data_ptr<float>(), m.data_ptr<float>(),
+                            r.data_ptr<float>(), bfp_mut(u), R, stream());
+  return {z, y, m, r, u};
+}
+
+std::vector<Tensor> post_attn_bwd(Tensor dz, Tensor y, Tensor m2, Tensor r2, Tensor u, Tensor o, Tensor wo, Tensor w1,
+                                  Tensor w2, Tensor g2, int64_t H) {
+  TORCH_CHECK(dz.is_contiguous(), "dz must be contiguous");
+  const int R = (int)dz.size(0), C = (int)dz.size(1);
+  auto f32 = dz.options().dtype(torch::kFloat32);
+  const int nblk = (R + 63) / 64;
+  Tensor dy = torch::empty({R, C}, f32);
+  Tensor du = torch::empty({R, C}, dz.options().dtype(torch::kBFloat16));
+  Tensor dO = torch::empty({R, C}, dz.options().dtype(torch::kBFloat16));
+  Tensor delta = torch::empty({R, H}, f32);
+  Tensor sg = torch::empty({nblk, C}, f32), sb = torch::empty({nblk, C}, f32);
+  pio::post_attn_bwd_launch(C, f32p(dz), f32p(y), f32p(m2), f32p(r2), bfp(u), bfp(o), bfp(wo), bfp(w1), bfp(w2),
+                            f32p(g2), dy.data_ptr<float>(), bfp_mut(du), bfp_mut(dO), delta.data_ptr<float>(), (int)H,
+                            sg.data_ptr<float>(), sb.data_ptr<float>(), R, stream());
+  return {dy, du, dO, delta, sg, sb};
+}
+
+std::vector<Tensor> ln_linear_dgrad(Tensor g, Tensor w, OptT x, OptT mean, OptT rstd, OptT lnw, OptT dres, bool need_dx) {
+  TORCH_CHECK(g.dim() == 2 && g.stride(1) == 1, "g must be 2-D rows");
+  const int R = (int)g.size(0), N = (int)g.size(1), Kin = (int)w.size(1);
+  TORCH_CHECK(w.size(0) == N, "w rows must match g columns");
+  TORCH_CHECK(Kin <= 160, "dgrad supports Kin <= 160");
+  auto f32 = g.options().dtype(torch::kFloat32);
+  Tensor dx, sg, sb;
+  float *dxp = nullptr, *sgp = nullptr, *sbp = nullptr;
+  if (need_dx) { dx = torch::empty({R, Kin}, f32); dxp = dx.data_ptr<float>(); }
+  const int nblk = (R + 63) / 64;
+  if (lnw.has_value()) {
+    sg = torch::empty({nblk, Kin}, f32); sb = torch::empty({nblk, Kin}, f32);
+    sgp = sg.data_ptr<float>(); sbp = sb.data_ptr<float>();
+  }
+  const void* xp = nullptr; bool xb = false; int xrs = 0;
+  if (x.has_value()) { xp = x->data_ptr(); xb = is_bf16(*x); xrs = (int)x->stride(0); }
+  const float* dr = nullptr; int drs = 0;
+  if (dres.has_value()) { dr = f32p(*dres); drs = (int)dres->stride(0); }
+  pio::ln_linear_dgrad_launch(g.data_ptr(), is_bf16(g), (int)g.stride(0), N, bfp(w), Kin, xp, xb, xrs, f32o(mean),
+                              f32o(rstd), f32o(lnw), dr, drs, dxp, Kin, sgp, sbp, R, stream());
+  return {dx, sg, sb};
+}
+
+std::vector<Tensor> wgrad(Tensor g, Tensor a, int64_t amode, OptT mean, OptT rstd, OptT lnw, OptT lnb, int64_t nsplit,
+                          bool with_bias) {
+  TORCH_CHECK(g.dim() == 2 && a.dim() == 2 && g.stride(1) == 1 && a.stride(1) == 1, "2-D row tensors expected");
+  const int R = (int)g.size(0), N = (int)g.size(1), Kin = (int)a.size(1);
+  TORCH_CHECK(a.size(0) == R, "row mismatch");
+  TORCH_CHECK(Kin <= 160, "wgrad supports Kin <= 160");
+  auto f32 = g.options().dtype(torch::kFloat32);
+  Tensor sw = torch::empty({nsplit, N, Kin}, f32);
+  Tensor sb;
+  float* sbp = nullptr;
+  if (with_bias) { sb = torch::empty({nsplit, N}, f32); sbp = sb.data_ptr<float>(); }
+  pio::wgrad_launch(g.data_ptr(), is_bf16(g), (int)g.stride(0), N, a.data_ptr(), is_bf16(a), (int)a.stride(0), Kin,
+                    (int)amode, f32o(mean), f32o(rstd), f32o(lnw), f32o(lnb), R, (int)nsplit, sw.data_ptr<float>(), sbp,
+                    stream());
+  return {sw, sb};
+}
+
+// jobs: list of (slab [S, ...], dst (numel = slab[0].numel()), accumulate)
+void slab_reduce(std::vector<Tensor> slabs, std::vector<Tensor> dsts, std::vector<bool> acc) {
+  TORCH_CHECK(slabs.size() == dsts.size() && slabs.size() == acc.size());
+  size_t i = 0;
+  while (i < slabs.size()) {
+    pio::ReduceJobs jobs{};
+    jobs.n = 0;
+    for (; i < slabs.size() && jobs.n < 12; ++i) {
+      Tensor& s = slabs[i];
+      Tensor& d = dsts[i];
+      TORCH_CHECK(s.is_contiguous() && d.is_contiguous(), "slab_reduce needs contiguous tensors");
+      const long long len = d.numel();
+      TORCH_CHECK(s.numel() % len == 0, "slab size mismatch");
+      jobs.j[jobs.n++] = pio::ReduceJob{f32p(s), d.data_ptr<float>(), (int)len, (int)(s.numel() / len), acc[i] ? 1 : 0};
+    }
+    pio::slab_reduce_launch(jobs, stream());
+  }
+}
+
+std::vector<Tensor> ce_fwd(Tensor h, Tensor labels, Tensor w, Tensor bias) {
+  TORCH_CHECK(h.is_contiguous() && w.is_contiguous() && labels.is_contiguous());
+  CHECK_DT(labels, torch::kInt64);
+  const int M = (int)h.size(0), C = (int)h.size(1), V = (int)w.size(0);
+  TORCH_CHECK(w.size(1) == C && (C == 32 || C == 64 || C == 128), "bad vocab head shape");
+  auto f32 = h.options().dtype(torch::kFloat32);
+  const int ns = pio::ce_num_splits(M, V);
+  Tensor part = torch::empty({ns, M, 2}, f32), picked = torch::zeros({M}, f32);
+  Tensor loss = torch::empty({M}, f32), lse = torch::empty({M}, f32);
+  pio::ce_fwd_launch(C, bfp(h), labels.data_ptr<int64_t>(), bfp(w), f32p(bias), M, V, part.data_ptr<float>(),
+                     picked.data_ptr<float>(), loss.data_ptr<float>(), lse.data_ptr<float>(), ns, stream());
+  return {loss, lse};
+}
+
+void ce_bwd(Tensor h, Tensor labels, Tensor w, Tensor bias, Tensor lse, Tensor gscale, Tensor dH, Tensor dW, Tensor db,
+            bool accumulate) {
+  const int M = (int)h.size(0), C = (int)h.size(1), V = (int)w.size(0);
+  TORCH_CHECK(dH.is_contiguous() && dW.is_contiguous() && db.is_contiguous());
+  pio::ce_bwd_launch(C, bfp(h), labels.data_ptr<int64_t>(), bfp(w), f32p(bias), f32p(lse), f32p(gscale), M, V,
+                     dH.data_ptr<float>(), dW.data_ptr<float>(), db.data_ptr<float>(), accumulate ? 1 : 0, stream());
+}
+
+Tensor embed_fwd(Tensor ids, Tensor E, Tensor P, double scale) {
+  TORCH_CHECK(ids.is_contiguous() && E.is_contiguous() && P.is_contiguous());
+  CHECK_DT(ids, torch::kInt64);
+  const long long rows = ids.numel();
+  const int L = (int)ids.size(1), C = (int)E.size(1);
+  TORCH_CHECK(C % 4 == 0, "embedding width must be a multiple of 4");
+  Tensor out = torch::empty({ids.size(0), L, C}, E.options());
+  pio::embed_fwd_launch(ids.data_ptr<int64_t>(), f32p(E), f32p(P), out.data_ptr<float>(), rows, L, C, (float)scale, stream());
+  return out;
+}
+
+void embed_bwd(Tensor ids, Tensor g, OptT dE, OptT dP, double scale) {
+  TORCH_CHECK(g.is_contiguous() && ids.is_contiguous());
+  const int B = (int)ids.size(0), L = (int)ids.size(1), C = (int)g.size(2);
+  pio::embed_bwd_launch(ids.data_ptr<int64_t>(), f32p(g), dE.has_value() ? dE->data_ptr<float>() : nullptr,
+                        dP.has_value() ? dP->data_ptr<float>() : nullptr, B, L, C, (float)scale, stream());
+}
+
+std::vector<Tensor> text_mask(Tensor x, OptT pad, Tensor u, Tensor rid, int64_t unk, int64_t mask, double p) {
+  TORCH_CHECK(x.is_contiguous() && u.is_contiguous() && rid.is_contiguous());
+  const long long n = x.numel();
+  TORCH_CHECK(u.numel() == 3 * n && rid.numel() == n);
+  Tensor xm = torch::empty_like(x), lab = torch::empty_like(x);
+  const bool* pp = nullptr;
+  if (pad.has_value()) { CHECK_DT(*pad, torch::kBool); pp = pad->data_ptr<bool>(); }
+  pio::text_mask_launch(x.data_ptr<int64_t>(), pp, f32p(u), rid.data_ptr<int64_t>(), xm.data_ptr<int64_t>(),
+                        lab.data_ptr<int64_t>(), n, (int)unk, (int)mask, (float)p, stream());
+  return {xm, lab};
+}
+
+void sumsq(Tensor g, Tensor out) { pio::sumsq_launch(f32p(g), g.numel(), out.data_ptr<float>(), stream()); }
+
+void adamw(Tensor p, Tensor g, Tensor m, Tensor v, OptT shadow, Tensor hyper, double eps, double wd, double clip,
+           double gscale) {
+  TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && m.is_contiguous() && v.is_contiguous());
+  TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel());
+  uint16_t* sp = nullptr;
+  if (shadow.has_value()) { TORCH_CHECK(shadow->numel() == p.numel()); sp = reinterpret_cast<uint16_t*>(shadow->data_ptr()); }
+  pio::adamw_launch(p.data_ptr<float>(), f32p(g), m.data_ptr<float>(), v.data_ptr<float>(), sp, p.numel(), f32p(hyper),
+                    (float)eps, (float)wd, (float)clip, (float)gscale, stream());
+}
+
+void cast_bf16(Tensor x, Tensor y) {
+  TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && x.numel() == y.numel());
+  pio::cast_bf16_launch(f32p(x), reinterpret_cast<uint16_t*>(y.data_ptr()), x.numel(), stream());
+}
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "Perceiver IO CDNA4 (gfx950) kernels";
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
+  m.def("ln_linear_fwd", &ln_linear_fwd);
+  m.def("post_attn_fwd", &post_attn_fwd);
+  m.def("post_attn_bwd", &post_attn_bwd);
+  m.def("ln_linear_dgrad", &ln_linear_dgrad);
+  m.def("wgrad", &wgrad);
+  m.def("slab_reduce", &slab_reduce);
+  m.def("ce_fwd", &ce_fwd);
+  m.def("ce_bwd", &ce_bwd);
+  m.def("embed_fwd", &embed_fwd);
+  m.def("embed_bwd", &embed_bwd);
+  m.def("text_mask", &text_mask);
+  m.def("sumsq", &sumsq);
+  m.def("adamw", &adamw);
+  m.def("cast_bf16", &cast_bf16);
+  m.attr("arch") = "gfx950";
+}

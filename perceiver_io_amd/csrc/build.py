@@ -1,0 +1,107 @@
+"""Build the in-tree HIP extension ``perceiver_io_amd/_C*.so`` for gfx950.
+
+Kernels (``*.hip``) are compiled with ``hipcc --offload-arch=gfx950`` and contain no
+PyTorch headers (fast, parallel, cached by content hash); only ``binding.cpp`` sees
+the torch headers (host compiler).  No hipify pass, no JIT cache outside the tree:
+the resulting ``.so`` travels with the repository snapshot to the GPU box.
+
+    python -m perceiver_io_amd.csrc.build [--force] [--jobs N] [--debug]
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import os
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+PKG = HERE.parent
+BUILD = PKG.parent / "build" / "csrc"
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def _torch_paths():
+    import torch.utils.cpp_extension as ce
+
+    inc = ce.include_paths()
+    libdir = os.path.join(os.path.dirname(ce.__file__), "..", "lib")
+    return inc, os.path.abspath(libdir)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(" ".join(cmd) + "\n" + r.stdout)
+        raise RuntimeError(f"command failed ({r.returncode}): {cmd[0]} … {cmd[-1]}")
+    return r.stdout
+
+
+def _digest(paths, flags):
+    h = hashlib.sha256(" ".join(flags).encode())
+    for p in paths:
+        h.update(Path(p).read_bytes())
+    return h.hexdigest()[:16]
+
+
+def ext_path() -> Path:
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    return PKG / f"_C{suffix}"
+
+
+def build(force: bool = False, jobs: int = 0, debug: bool = False, verbose: bool = True) -> Path:
+    BUILD.mkdir(parents=True, exist_ok=True)
+    headers = sorted(HERE.glob("*.h"))
+    hip_srcs = sorted(HERE.glob("*.hip"))
+    opt = ["-O0", "-g"] if debug else ["-O3"]
+    hip_flags = [f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-ffp-contract=fast", "-munsafe-fp-atomics",
+                 "-Wno-unused-result"] + opt
+    objs = []
+    todo = []
+    for src in hip_srcs:
+        obj = BUILD / f"{src.stem}.{_digest([src] + headers, hip_flags)}.o"
+        objs.append(obj)
+        if force or not obj.exists():
+            todo.append([HIPCC, *hip_flags, "-I", str(HERE), "-c", str(src), "-o", str(obj)])
+    inc, libdir = _torch_paths()
+    py_inc = sysconfig.get_paths()["include"]
+    cxx_flags = ["-O2", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+                 "-DTORCH_API_INCLUDE_EXTENSION_H", "-DTORCH_EXTENSION_NAME=_C", "-D_GLIBCXX_USE_CXX11_ABI=1",
+                 "-isystem", "/opt/rocm/include", "-isystem", py_inc] + sum((["-isystem", p] for p in inc), [])
+    bsrc = HERE / "binding.cpp"
+    bobj = BUILD / f"binding.{_digest([bsrc], cxx_flags)}.o"
+    if force or not bobj.exists():
+        todo.append(["g++", *cxx_flags, "-c", str(bsrc), "-o", str(bobj)])
+    if todo:
+        n = jobs or min(len(todo), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)))
+        if verbose:
+            print(f"[perceiver_io_amd] compiling {len(todo)} translation unit(s) for {ARCH} with {n} job(s)")
+        with ThreadPoolExecutor(max_workers=n) as ex:
+            list(ex.map(_run, todo))
+    out = ext_path()
+    link = ["g++", "-shared", "-o", str(out), str(bobj), *map(str, objs), f"-L{libdir}", "-L/opt/rocm/lib",
+            "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lamdhip64", "-lc10_hip", "-ltorch_hip",
+            f"-Wl,-rpath,{libdir}", "-Wl,-rpath,/opt/rocm/lib"]
+    newest = max(p.stat().st_mtime for p in objs + [bobj])
+    if force or todo or not out.exists() or out.stat().st_mtime < newest:
+        _run(link)
+        if verbose:
+            print(f"[perceiver_io_amd] linked {out.relative_to(PKG.parent)}")
+    return out
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--jobs", type=int, default=0)
+    ap.add_argument("--debug", action="store_true")
+    a = ap.parse_args(argv)
+    build(force=a.force, jobs=a.jobs, debug=a.debug)
+
+
+if __name__ == "__main__":
+    main()

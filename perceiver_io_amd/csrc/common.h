@@ -1,0 +1,102 @@
+// Shared device helpers for the Perceiver IO CDNA4 (gfx950) kernels.
+//
+// Conventions (all kernels):
+//   * wave = 64 lanes; blocks are multiples of 64 threads.
+//   * matrix products use v_mfma_f32_32x32x16_bf16 (fp32 accumulate).
+//     operand lane map (lane l, r = l & 31, h = l >> 5):
+//        A[row r][k = 8h + j], B[k = 8h + j][col r], j = 0..7
+//     accumulator map: col = l & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * h.
+//   * an operand tile lives in LDS either "k-contiguous" (row-major with the
+//     contraction index innermost → one ds_read_b128 per fragment) or
+//     "k-strided" (contraction index = LDS row → two ds_read_b64_tr_b16).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pio {
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+__device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+__device__ __forceinline__ float bf2f(short v) { return bf2f((uint16_t)v); }
+
+// round-to-nearest-even f32 -> bf16 (NaN stays NaN via the cast path hipcc lowers to v_cvt_pk_bf16_f32)
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return *reinterpret_cast<uint16_t*>(&b);
+}
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+
+// accumulator register -> row within the 32x32 tile
+__device__ __forceinline__ int acc_row(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
+
+// ---- LDS operand reads ------------------------------------------------------------
+// k-contiguous: element (idx, k) at base[idx * ld + k]; fragment for tile origin (i0, k0)
+__device__ __forceinline__ bf16x8 frag_kc(const uint16_t* lds, int ld, int i0, int k0) {
+  const int l = lane_id();
+  return *reinterpret_cast<const bf16x8*>(lds + (i0 + (l & 31)) * ld + k0 + 8 * (l >> 5));
+}
+
+// k-strided: element (idx, k) at base[k * ld + idx] — hardware transpose read.
+// Lane group g = l>>4 covers idx i0 + 16*(g&1) + 0..15 and k rows k0 + 8*(g>>1) + 0..7.
+__device__ __forceinline__ bf16x8 frag_ks(const uint16_t* lds, int ld, int i0, int k0) {
+  const int l = lane_id();
+  const int g = l >> 4, i = l & 15, q = i >> 2, p = i & 3;
+  const uint16_t* base = lds + (k0 + 8 * (g >> 1) + q) * ld + i0 + 16 * (g & 1) + 4 * p;
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(base));
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(base + 4 * ld));
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+// ---- reductions ---------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---- GELU (erf form, nn.GELU default) ------------------------------------------------
+__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad(float x) {
+  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+// ---- counter-based RNG for dropout (regenerated in backward, no mask storage) -------
+__device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
+  // a few rounds of a murmur-style mixer over (seed, stream, index)
+  uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u);
+  h ^= c * 0x85EBCA77u;
+  h ^= h >> 15; h *= 0x2C1B3C6Du;
+  h ^= h >> 12; h *= 0x297A2D39u;
+  h ^= h >> 15;
+  return h;
+}
+// keep with probability (1-p): threshold = p * 2^32
+__device__ __forceinline__ bool keep_elem(uint32_t seed, uint32_t stream, uint32_t idx, uint32_t thresh) {
+  return hash3(seed, stream, idx) >= thresh;
+}
+
+}  // namespace pio

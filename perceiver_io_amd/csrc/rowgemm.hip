@@ -1,0 +1,583 @@
+// Row-local fused GEMM kernels for the Perceiver's narrow layers (C = 64..133 channels).
+//
+// With C ≤ 133 every projection in the model is a skinny GEMM (K-dim 64–160) whose cost is
+// moving activations, not MFMA time, so these kernels fuse everything
+// that is row-local around the attention core:
+//   ln_linear_fwd   : LayerNorm prologue (fp32 stats) → X·Wᵀ + b (+GELU) (+residual)
+//                     (reference mlp/q_norm/kv_norm/norm + MHA in-proj, model.py:20-26,89-99,108-116)
+//   post_attn_fwd   : out-proj + bias + residual → LN2 → W1 + b1 → GELU → W2 + b2 + residual,
+//                     one kernel per 64-row tile, intermediates in LDS (Residual(attn) →
+//                     Residual(mlp), model.py:29-56)
+//   post_attn_bwd   : the reverse chain for one 64-row tile: dZ → dH → dU (GELU') → LN2 bwd →
+//                     dY → dO (+ softmax delta = rowsum(dO∘O) for the attention backward)
+//   ln_linear_dgrad : dX = LN_bwd(dY·W) (+ residual grad), LN param partials
+//   wgrad           : dW = Σ_rows Gᵀ·A and db = Σ_rows G as per-split fp32 slabs, A optionally
+//                     recomputed on the fly (LN(x) or GELU(u)) instead of stored
+//   slab_reduce     : deterministic sum of the slabs into the (flat) fp32 grad buffer
+// All GEMMs are v_mfma_f32_32x32x16_bf16 on LDS tiles (common.h operand helpers); a 64-row
+// tile spans four waves, each owning whole 32×32 output sub-tiles.
+#include "common.h"
+
+namespace pio {
+
+__device__ __forceinline__ float ldf(const float* p) { return *p; }
+__device__ __forceinline__ float ldf(const uint16_t* p) { return bf2f(*p); }
+__device__ __forceinline__ void stf(float* p, float v) { *p = v; }
+__device__ __forceinline__ void stf(uint16_t* p, float v) { *p = f2bf(v); }
+
+// C (+)= A·B over K on LDS tiles; sub-tile tg = w + 4t of a (BM/32)×(BN/32) grid.
+// A_KC: A stored [m][k] (else [k][m]); B_KC: B stored [n][k] (else [k][n]).
+template <int MAXT, bool A_KC, bool B_KC>
+__device__ __forceinline__ void tile_gemm(const uint16_t* sA, int lda, const uint16_t* sB, int ldb, int BM, int BN,
+                                          int K, f32x16 (&acc)[MAXT]) {
+  const int w = wave_id();
+  const int ntn = BN / 32, nt = (BM / 32) * ntn;
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) {
+    const int tg = w + 4 * t;
+    if (tg < nt) {  // wave-uniform
+      const int m0 = 32 * (tg / ntn), n0 = 32 * (tg % ntn);
+      for (int k0 = 0; k0 < K; k0 += 16) {
+        const bf16x8 a = A_KC ? frag_kc(sA, lda, m0, k0) : frag_ks(sA, lda, m0, k0);
+        const bf16x8 b = B_KC ? frag_kc(sB, ldb, n0, k0) : frag_ks(sB, ldb, n0, k0);
+        acc[t] = mfma32(a, b, acc[t]);
+      }
+    }
+  }
+}
+
+// visit every element of this wave's accumulator sub-tiles: f(t, m, n, reg)
+template <int MAXT, typename F>
+__device__ __forceinline__ void for_acc(int BM, int BN, F&& f) {
+  const int w = wave_id(), l = lane_id(), hh = l >> 5;
+  const int ntn = BN / 32, nt = (BM / 32) * ntn;
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) {
+    const int tg = w + 4 * t;
+    if (tg < nt) {
+      const int m0 = 32 * (tg / ntn), n0 = 32 * (tg % ntn);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) f(t, m0 + acc_row(i, hh), n0 + (l & 31), i);
+    }
+  }
+}
+
+// stage rows [r0, r0+rows) × cols [c0, c0+cols) of a row-major matrix into an LDS bf16
+// tile [rows][ld] (zero outside the matrix).
+template <typename T>
+__device__ __forceinline__ void stage(uint16_t* s, int ld, const T* g, long long g_rs, int r0, int R, int c0, int Cmax,
+                                      int rows, int cols) {
+  for (int e = threadIdx.x; e < rows * cols; e += blockDim.x) {
+    const int rr = e / cols, cc = e % cols;
+    const int gr = r0 + rr, gc = c0 + cc;
+    float v = 0.f;
+    if (gr < R && gc < Cmax) v = ldf(g + (long long)gr * g_rs + gc);
+    s[rr * ld + cc] = f2bf(v);
+  }
+}
+
+__host__ __device__ __forceinline__ int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+// ------------------------------------------------------------------------------------
+// LayerNorm(+)Linear forward
+// ------------------------------------------------------------------------------------
+template <typename TIn, typename TOut>
+__global__ __launch_bounds__(256) void ln_linear_fwd_kernel(const TIn* __restrict__ X, int x_rs, int R, int Kin,
+                                                            const float* __restrict__ lnw, const float* __restrict__ lnb,
+                                                            float eps, const uint16_t* __restrict__ W,
+                                                            const float* __restrict__ bias, int N, int act,
+                                                            const float* __restrict__ res, int res_rs,
+                                                            TOut* __restrict__ Y, int y_rs, float* __restrict__ mean_out,
+                                                            float* __restrict__ rstd_out) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int KP = round_up(Kin, 16), ld = KP + 8;
+  uint16_t* sA = smem;
+  uint16_t* sB = smem + 64 * ld;
+  const int m0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
+  const int w = wave_id(), l = lane_id();
+
+  stage(sB, ld, W, Kin, n0, N, 0, Kin, 64, KP);
+  // LN prologue: one wave per row
+  for (int rr = w; rr < 64; rr += 4) {
+    const int gr = m0 + rr;
+    if (gr < R) {
+      const TIn* xr = X + (long long)gr * x_rs;
+      float mean = 0.f, rstd = 1.f;
+      if (lnw) {
+        float s = 0.f;
+        for (int k = l; k < Kin; k += 64) s += ldf(xr + k);
+        mean = wave_sum(s) / Kin;
+        float v = 0.f;
+        for (int k = l; k < Kin; k += 64) { const float d = ldf(xr + k) - mean; v += d * d; }
+        rstd = rsqrtf(wave_sum(v) / Kin + eps);
+        if (blockIdx.y == 0 && l == 0 && mean_out) { mean_out[gr] = mean; rstd_out[gr] = rstd; }
+      }
+      for (int k = l; k < KP; k += 64) {
+        float v = 0.f;
+        if (k < Kin) {
+          v = ldf(xr + k);
+          if (lnw) v = (v - mean) * rstd * lnw[k] + lnb[k];
+        }
+        sA[rr * ld + k] = f2bf(v);
+      }
+    } else {
+      for (int k = l; k < KP; k += 64) sA[rr * ld + k] = 0;
+    }
+  }
+  __syncthreads();
+  f32x16 acc[1] = {f32x16{}};
+  tile_gemm<1, true, true>(sA, ld, sB, ld, 64, 64, KP, acc);
+  for_acc<1>(64, 64, [&](int t, int m, int n, int i) {
+    const int gr = m0 + m, gc = n0 + n;
+    if (gr < R && gc < N) {
+      float v = acc[t][i] + (bias ? bias[gc] : 0.f);
+      if (act == 1) v = gelu_f(v);
+      if (res) v += res[(long long)gr * res_rs + gc];
+      stf(Y + (long long)gr * y_rs + gc, v);
+    }
+  });
+}
+
+// ------------------------------------------------------------------------------------
+// post-attention block forward: Z = Y + W2·gelu(W1·LN2(Y) + b1) + b2, Y = X + Wo·O + bo
+// ------------------------------------------------------------------------------------
+template <int C>
+__global__ __launch_bounds__(256) void post_attn_fwd_kernel(
+    const uint16_t* __restrict__ O, const float* __restrict__ X, const uint16_t* __restrict__ Wo,
+    const float* __restrict__ bo, const float* __restrict__ g2, const float* __restrict__ be2, float eps,
+    const uint16_t* __restrict__ W1, const float* __restrict__ b1, const uint16_t* __restrict__ W2,
+    const float* __restrict__ b2, float* __restrict__ Z, float* __restrict__ Ysave, float* __restrict__ mean2,
+    float* __restrict__ rstd2, uint16_t* __restrict__ Usave, int R) {
+  constexpr int LD = C + 8, LDF = C + 4, MAXT = (2 * C / 32 + 3) / 4;
+  __shared__ __attribute__((aligned(16))) uint16_t sA[64 * LD];
+  __shared__ __attribute__((aligned(16))) uint16_t sW[C * LD];
+  __shared__ __attribute__((aligned(16))) float sY[64 * LDF];
+  const int m0 = blockIdx.x * 64;
+  const int w = wave_id(), l = lane_id();
+
+  stage(sA, LD, O, C, m0, R, 0, C, 64, C);
+  stage(sW, LD, Wo, C, 0, C, 0, C, C, C);
+  __syncthreads();
+  f32x16 acc[MAXT];
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
+  tile_gemm<MAXT, true, true>(sA, LD, sW, LD, 64, C, C, acc);
+  for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) {
+    const int gr = m0 + m;
+    float y = 0.f;
+    if (gr < R) {
+      y = X[(long long)gr * C + n] + acc[t][i] + bo[n];
+      Ysave[(long long)gr * C + n] = y;
+    }
+    sY[m * LDF + n] = y;
+  });
+  __syncthreads();
+  // LN2 (one wave per row) → sA ; W1 → sW
+  for (int rr = w; rr < 64; rr += 4) {
+    float s = 0.f;
+    for (int k = l; k < C; k += 64) s += sY[rr * LDF + k];
+    const float mean = wave_sum(s) / C;
+    float v = 0.f;
+    for (int k = l; k < C; k += 64) { const float d = sY[rr * LDF + k] - mean; v += d * d; }
+    const float rstd = rsqrtf(wave_sum(v) / C + eps);
+    const int gr = m0 + rr;
+    if (l == 0 && gr < R) { mean2[gr] = mean; rstd2[gr] = rstd; }
+    for (int k = l; k < C; k += 64) sA[rr * LD + k] = f2bf((sY[rr * LDF + k] - mean) * rstd * g2[k] + be2[k]);
+  }
+  stage(sW, LD, W1, C, 0, C, 0, C, C, C);
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
+  tile_gemm<MAXT, true, true>(sA, LD, sW, LD, 64, C, C, acc);
+  __syncthreads();  // everyone done reading sA / sW
+  for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) {
+    const int gr = m0 + m;
+    const float u = acc[t][i] + b1[n];
+    if (gr < R) Usave[(long long)gr * C + n] = f2bf(u);
+    sA[m * LD + n] = f2bf(gelu_f(u));
+  });
+  stage(sW, LD, W2, C, 0, C, 0, C, C, C);
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
+  tile_gemm<MAXT, true, true>(sA, LD, sW, LD, 64, C, C, acc);
+  for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) {
+    const int gr = m0 + m;
+    if (gr < R) Z[(long long)gr * C + n] = sY[m * LDF + n] + acc[t][i] + b2[n];
+  });
+}
+
+// ------------------------------------------------------------------------------------
+// post-attention block backward (row-local part)
+// ------------------------------------------------------------------------------------
+template <int C>
+__global__ __launch_bounds__(256) void post_attn_bwd_kernel(
+    const float* __restrict__ dZ, const float* __restrict__ Ysave, const float* __restrict__ mean2,
+    const float* __restrict__ rstd2, const uint16_t* __restrict__ U, const uint16_t* __restrict__ O,
+    const uint16_t* __restrict__ Wo, const uint16_t* __restrict__ W1, const uint16_t* __restrict__ W2,
+    const float* __restrict__ g2, float* __restrict__ dY, uint16_t* __restrict__ dU, uint16_t* __restrict__ dO,
+    float* __restrict__ delta, int H, float* __restrict__ slab_g2, float* __restrict__ slab_b2, int R) {
+  constexpr int LD = C + 8, LDF = C + 4, MAXT = (2 * C / 32 + 3) / 4;
+  __shared__ __attribute__((aligned(16))) uint16_t sA[64 * LD];
+  __shared__ __attribute__((aligned(16))) uint16_t sW[C * LD];
+  __shared__ __attribute__((aligned(16))) float sF[64 * LDF];
+  __shared__ float sPart[2][4][C];
+  const int m0 = blockIdx.x * 64;
+  const int w = wave_id(), l = lane_id();
+
+  // dH = dZ · W2   (B[k=n][col=c] = W2[n][c] → W2 tile k-strided)
+  stage(sA, LD, dZ, C, m0, R, 0, C, 64, C);
+  stage(sW, LD, W2, C, 0, C, 0, C, C, C);
+  __syncthreads();
+  f32x16 acc[MAXT];
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
+  tile_gemm<MAXT, true, false>(sA, LD, sW, LD, 64, C, C, acc);
+  __syncthreads();
+  for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) {
+    const int gr = m0 + m;
+    float du = 0.f;
+    if (gr < R) {
+      du = acc[t][i] * gelu_grad(bf2f(U[(long long)gr * C + n]));
+      dU[(long long)gr * C + n] = f2bf(du);
+    }
+    sA[m * LD + n] = f2bf(du);
+  });
+  stage(sW, LD, W1, C, 0, C, 0, C, C, C);
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
+  tile_gemm<MAXT, true, false>(sA, LD, sW, LD, 64, C, C, acc);  // dXn2 = dU · W1
+  for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) { sF[m * LDF + n] = acc[t][i]; });
+  __syncthreads();
+  // LN2 backward → dY = dZ + LN_bwd ; param partials
+  float pg[(C + 63) / 64], pb[(C + 63) / 64];
+#pragma unroll
+  for (int j = 0; j < (C + 63) / 64; ++j) pg[j] = pb[j] = 0.f;
+  for (int rr = w; rr < 64; rr += 4) {
+    const int gr = m0 + rr;
+    if (gr >= R) {
+      for (int k = l; k < C; k += 64) sA[rr * LD + k] = 0;
+      continue;
+    }
+    const float mean = mean2[gr], rstd = rstd2[gr];
+    float s1 = 0.f, s2 = 0.f;
+    for (int k = l; k < C; k += 64) {
+      const float xh = (Ysave[(long long)gr * C + k] - mean) * rstd;
+      const float g = sF[rr * LDF + k] * g2[k];
+      s1 += g;
+      s2 += g * xh;
+    }
+    s1 = wave_sum(s1) / C;
+    s2 = wave_sum(s2) / C;
+#pragma unroll
+    for (int j = 0; j < (C + 63) / 64; ++j) {
+      const int k = l + 64 * j;
+      if (k < C) {
+        const float xh = (Ysave[(long long)gr * C + k] - mean) * rstd;
+        const float dxn = sF[rr * LDF + k];
+        const float d = dZ[(long long)gr * C + k] + rstd * (dxn * g2[k] - s1 - xh * s2);
+        dY[(long long)gr * C + k] = d;
+        sA[rr * LD + k] = f2bf(d);
+        pg[j] += dxn * xh;
+        pb[j] += dxn;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < (C + 63) / 64; ++j) {
+    const int k = l + 64 * j;
+    if (k < C) { sPart[0][w][k] = pg[j]; sPart[1][w][k] = pb[j]; }
+  }
+  stage(sW, LD, Wo, C, 0, C, 0, C, C, C);
+  __syncthreads();
+  for (int k = threadIdx.x; k < C; k += blockDim.x) {
+    slab_g2[(long long)blockIdx.x * C + k] = sPart[0][0][k] + sPart[0][1][k] + sPart[0][2][k] + sPart[0][3][k];
+    slab_b2[(long long)blockIdx.x * C + k] = sPart[1][0][k] + sPart[1][1][k] + sPart[1][2][k] + sPart[1][3][k];
+  }
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
+  tile_gemm<MAXT, true, false>(sA, LD, sW, LD, 64, C, C, acc);  // dO = dY · Wo
+  for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) {
+    const int gr = m0 + m;
+    const uint16_t d = f2bf(acc[t][i]);
+    sF[m * LDF + n] = bf2f(d);
+    if (gr < R) dO[(long long)gr * C + n] = d;
+  });
+  __syncthreads();
+  // delta[r, h] = sum_d dO * O over the head's columns (bf16 values as the attention sees them)
+  const int D = C / H;
+  for (int e = threadIdx.x; e < 64 * H; e += blockDim.x) {
+    const int rr = e / H, h = e % H;
+    const int gr = m0 + rr;
+    if (gr < R) {
+      float s = 0.f;
+      for (int d = 0; d < D; ++d) s += sF[rr * LDF + h * D + d] * bf2f(O[(long long)gr * C + h * D + d]);
+      delta[(long long)gr * H + h] = s;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// dX = LN_bwd(G · W) (+ dres) ; LN param partial slabs
+// ------------------------------------------------------------------------------------
+template <typename TG, typename TX>
+__global__ __launch_bounds__(256) void ln_linear_dgrad_kernel(
+    const TG* __restrict__ G, int g_rs, int N, const uint16_t* __restrict__ W, int Kin, const TX* __restrict__ X,
+    int x_rs, const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ lnw,
+    const float* __restrict__ dres, int dres_rs, float* __restrict__ dX, int dx_rs, float* __restrict__ slab_g,
+    float* __restrict__ slab_b, int R) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int KP = round_up(Kin, 32), ld = KP + 8, ldg = 64 + 8, ldF = KP + 4;
+  uint16_t* sG = smem;                 // [64 rows][64 n]
+  uint16_t* sW = sG + 64 * ldg;        // [64 n][KP]
+  float* sF = reinterpret_cast<float*>(sW + 64 * ld);  // [64][KP] fp32
+  float* sPart = sF + 64 * ldF;        // [2][4][KP]
+  const int m0 = blockIdx.x * 64;
+  const int w = wave_id(), l = lane_id();
+  constexpr int MAXT = 3;  // (64/32)*(KP/32) ≤ 10 sub-tiles (KP ≤ 160)
+  f32x16 acc[MAXT];
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
+  for (int nc = 0; nc < N; nc += 64) {
+    __syncthreads();
+    stage(sG, ldg, G, g_rs, m0, R, nc, N, 64, 64);
+    stage(sW, ld, W, Kin, nc, N, 0, Kin, 64, KP);
+    __syncthreads();
+    tile_gemm<MAXT, true, false>(sG, ldg, sW, ld, 64, KP, 64, acc);
+  }
+  for_acc<MAXT>(64, KP, [&](int t, int m, int n, int i) { sF[m * ldF + n] = acc[t][i]; });
+  __syncthreads();
+  const int NJ = (KP + 63) / 64;
+  float pg[3] = {0.f, 0.f, 0.f}, pb[3] = {0.f, 0.f, 0.f};
+  for (int rr = w; rr < 64; rr += 4) {
+    const int gr = m0 + rr;
+    if (gr >= R) continue;
+    if (lnw) {
+      const float mu = mean[gr], rs = rstd[gr];
+      float s1 = 0.f, s2 = 0.f;
+      for (int k = l; k < Kin; k += 64) {
+        const float xh = (ldf(X + (long long)gr * x_rs + k) - mu) * rs;
+        const float g = sF[rr * ldF + k] * lnw[k];
+        s1 += g;
+        s2 += g * xh;
+      }
+      s1 = wave_sum(s1) / Kin;
+      s2 = wave_sum(s2) / Kin;
+      for (int j = 0; j < NJ; ++j) {
+        const int k = l + 64 * j;
+        if (k < Kin) {
+          const float xh = (ldf(X + (long long)gr * x_rs + k) - mu) * rs;
+          const float dxn = sF[rr * ldF + k];
+          pg[j] += dxn * xh;
+          pb[j] += dxn;
+          if (dX) {
+            float d = rs * (dxn * lnw[k] - s1 - xh * s2);
+            if (dres) d += dres[(long long)gr * dres_rs + k];
+            dX[(long long)gr * dx_rs + k] = d;
+          }
+        }
+      }
+    } else if (dX) {
+      for (int k = l; k < Kin; k += 64) {
+        float d = sF[rr * ldF + k];
+        if (dres) d += dres[(long long)gr * dres_rs + k];
+        dX[(long long)gr * dx_rs + k] = d;
+      }
+    }
+  }
+  if (lnw && slab_g) {
+    for (int j = 0; j < NJ; ++j) {
+      const int k = l + 64 * j;
+      if (k < Kin) { sPart[(0 * 4 + w) * KP + k] = pg[j]; sPart[(1 * 4 + w) * KP + k] = pb[j]; }
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < Kin; k += blockDim.x) {
+      float a = 0.f, b = 0.f;
+      for (int ww = 0; ww < 4; ++ww) { a += sPart[ww * KP + k]; b += sPart[(4 + ww) * KP + k]; }
+      slab_g[(long long)blockIdx.x * Kin + k] = a;
+      slab_b[(long long)blockIdx.x * Kin + k] = b;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// weight gradient slabs: slab[s][n][k] = Σ_{rows of split s} G[r][n] · A[r][k]
+// A modes: 0 plain bf16, 1 LN(x) recomputed (x fp32), 2 GELU(u) recomputed (u bf16)
+// ------------------------------------------------------------------------------------
+template <typename TG, typename TA>
+__global__ __launch_bounds__(256) void wgrad_kernel(const TG* __restrict__ G, int g_rs, int N, const TA* __restrict__ A,
+                                                    int a_rs, int Kin, int amode, const float* __restrict__ mean,
+                                                    const float* __restrict__ rstd, const float* __restrict__ lnw,
+                                                    const float* __restrict__ lnb, int R, int rows_per_split,
+                                                    float* __restrict__ slab_w, float* __restrict__ slab_b) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int KP = round_up(Kin, 32), lda = KP + 8, ldg = 64 + 8;
+  uint16_t* sG = smem;           // [64 rows][64 n]
+  uint16_t* sA = sG + 64 * ldg;  // [64 rows][KP]
+  const int n0 = blockIdx.x * 64, s = blockIdx.y;
+  const int r_begin = s * rows_per_split, r_end = min(R, r_begin + rows_per_split);
+  constexpr int MAXT = 3;
+  f32x16 acc[MAXT];
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
+  float bsum = 0.f;  // thread n = threadIdx.x (< 64)
+  for (int r0 = r_begin; r0 < r_end; r0 += 64) {
+    __syncthreads();
+    const int rows = min(64, r_end - r0);
+    stage(sG, ldg, G, g_rs, r0, r_begin + (r_end - r_begin), n0, N, 64, 64);
+    for (int e = threadIdx.x; e < 64 * KP; e += blockDim.x) {
+      const int rr = e / KP, k = e % KP;
+      const int gr = r0 + rr;
+      float v = 0.f;
+      if (rr < rows && k < Kin) {
+        v = ldf(A + (long long)gr * a_rs + k);
+        if (amode == 1) v = (v - mean[gr]) * rstd[gr] * lnw[k] + lnb[k];
+        else if (amode == 2) v = gelu_f(v);
+      }
+      sA[rr * lda + k] = f2bf(v);
+    }
+    __syncthreads();
+    if (threadIdx.x < 64 && n0 + threadIdx.x < N)
+      for (int rr = 0; rr < rows; ++rr) bsum += ldf(G + (long long)(r0 + rr) * g_rs + n0 + threadIdx.x);
+    tile_gemm<MAXT, false, false>(sG, ldg, sA, lda, 64, KP, 64, acc);
+  }
+  float* out = slab_w + (long long)s * N * Kin;
+  for_acc<MAXT>(64, KP, [&](int t, int m, int n, int i) {
+    const int gn = n0 + m;
+    if (gn < N && n < Kin) out[(long long)gn * Kin + n] = acc[t][i];
+  });
+  if (slab_b && threadIdx.x < 64 && n0 + threadIdx.x < N) slab_b[(long long)s * N + n0 + threadIdx.x] = bsum;
+}
+
+// ------------------------------------------------------------------------------------
+// batched slab reduction: dst[i] (+)= Σ_s src[s * len + i]
+// ------------------------------------------------------------------------------------
+struct ReduceJob {
+  const float* src;
+  float* dst;
+  int len, nslab, accumulate;
+};
+struct ReduceJobs {
+  ReduceJob j[12];
+  int n;
+};
+
+__global__ void slab_reduce_kernel(ReduceJobs jobs) {
+  const ReduceJob& jb = jobs.j[blockIdx.y];
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < jb.len; i += gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < jb.nslab; ++k) s += jb.src[(long long)k * jb.len + i];
+    jb.dst[i] = jb.accumulate ? jb.dst[i] + s : s;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------
+// kernels whose dynamic LDS can exceed 64 KiB: raise the per-function limit once (gfx950: 160 KiB/CU)
+static void set_smem_once(const void* fn) {
+  static const void* done[8] = {nullptr};
+  for (auto& d : done) {
+    if (d == fn) return;
+    if (d == nullptr) {
+      (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      d = fn;
+      return;
+    }
+  }
+}
+
+void ln_linear_fwd_launch(const void* X, bool x_bf16, int x_rs, int R, int Kin, const float* lnw, const float* lnb,
+                          float eps, const uint16_t* W, const float* bias, int N, int act, const float* res,
+                          int res_rs, void* Y, bool y_bf16, int y_rs, float* mean, float* rstd, hipStream_t st) {
+  const int KP = round_up(Kin, 16);
+  const size_t smem = 2 * 64 * (KP + 8) * sizeof(uint16_t);
+  dim3 grid((R + 63) / 64, (N + 63) / 64);
+#define LNL(TI, TO)                                                                                         \
+  hipLaunchKernelGGL((ln_linear_fwd_kernel<TI, TO>), grid, dim3(256), smem, st, (const TI*)X, x_rs, R, Kin, \
+                     lnw, lnb, eps, W, bias, N, act, res, res_rs, (TO*)Y, y_rs, mean, rstd)
+  if (x_bf16 && y_bf16) LNL(uint16_t, uint16_t);
+  else if (x_bf16) LNL(uint16_t, float);
+  else if (y_bf16) LNL(float, uint16_t);
+  else LNL(float, float);
+#undef LNL
+}
+
+void post_attn_fwd_launch(int C, const uint16_t* O, const float* X, const uint16_t* Wo, const float* bo,
+                          const float* g2, const float* be2, float eps, const uint16_t* W1, const float* b1,
+                          const uint16_t* W2, const float* b2, float* Z, float* Ysave, float* mean2, float* rstd2,
+                          uint16_t* Usave, int R, hipStream_t st) {
+  dim3 grid((R + 63) / 64);
+  if (C == 64)
+    hipLaunchKernelGGL(post_attn_fwd_kernel<64>, grid, dim3(256), 0, st, O, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2,
+                       Z, Ysave, mean2, rstd2, Usave, R);
+  else if (C == 128)
+    hipLaunchKernelGGL(post_attn_fwd_kernel<128>, grid, dim3(256), 0, st, O, X, Wo, bo, g2, be2, eps, W1, b1, W2,
+                       b2, Z, Ysave, mean2, rstd2, Usave, R);
+  else if (C == 32)
+    hipLaunchKernelGGL(post_attn_fwd_kernel<32>, grid, dim3(256), 0, st, O, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2,
+                       Z, Ysave, mean2, rstd2, Usave, R);
+}
+
+void post_attn_bwd_launch(int C, const float* dZ, const float* Ysave, const float* mean2, const float* rstd2,
+                          const uint16_t* U, const uint16_t* O, const uint16_t* Wo, const uint16_t* W1,
+                          const uint16_t* W2, const float* g2, float* dY, uint16_t* dU, uint16_t* dO, float* delta,
+                          int H, float* slab_g2, float* slab_b2, int R, hipStream_t st) {
+  dim3 grid((R + 63) / 64);
+#define PAB(CC)                                                                                                  \
+  hipLaunchKernelGGL(post_attn_bwd_kernel<CC>, grid, dim3(256), 0, st, dZ, Ysave, mean2, rstd2, U, O, Wo, W1, W2, \
+                     g2, dY, dU, dO, delta, H, slab_g2, slab_b2, R)
+  if (C == 64) PAB(64);
+  else if (C == 128) PAB(128);
+  else if (C == 32) PAB(32);
+#undef PAB
+}
+
+void ln_linear_dgrad_launch(const void* G, bool g_bf16, int g_rs, int N, const uint16_t* W, int Kin, const void* X,
+                            bool x_bf16, int x_rs, const float* mean, const float* rstd, const float* lnw,
+                            const float* dres, int dres_rs, float* dX, int dx_rs, float* slab_g, float* slab_b, int R,
+                            hipStream_t st) {
+  const int KP = round_up(Kin, 32);
+  const size_t smem = 64 * (64 + 8) * 2 + 64 * (KP + 8) * 2 + 64 * (KP + 4) * 4 + 2 * 4 * KP * 4;
+  dim3 grid((R + 63) / 64);
+#define LDG(TG, TX)                                                                                             \
+  do {                                                                                                          \
+    set_smem_once((const void*)ln_linear_dgrad_kernel<TG, TX>);                                                 \
+    hipLaunchKernelGGL((ln_linear_dgrad_kernel<TG, TX>), grid, dim3(256), smem, st, (const TG*)G, g_rs, N, W,   \
+                       Kin, (const TX*)X, x_rs, mean, rstd, lnw, dres, dres_rs, dX, dx_rs, slab_g, slab_b, R);  \
+  } while (0)
+  if (g_bf16 && x_bf16) LDG(uint16_t, uint16_t);
+  else if (g_bf16) LDG(uint16_t, float);
+  else if (x_bf16) LDG(float, uint16_t);
+  else LDG(float, float);
+#undef LDG
+}
+
+void wgrad_launch(const void* G, bool g_bf16, int g_rs, int N, const void* A, bool a_bf16, int a_rs, int Kin,
+                  int amode, const float* mean, const float* rstd, const float* lnw, const float* lnb, int R,
+                  int nsplit, float* slab_w, float* slab_b, hipStream_t st) {
+  const int KP = round_up(Kin, 32);
+  const size_t smem = (64 * (64 + 8) + 64 * (KP + 8)) * 2;
+  int rps = (R + nsplit - 1) / nsplit;
+  rps = round_up(rps, 64);
+  dim3 grid((N + 63) / 64, nsplit);
+#define WG(TG, TA)                                                                                                 \
+  hipLaunchKernelGGL((wgrad_kernel<TG, TA>), grid, dim3(256), smem, st, (const TG*)G, g_rs, N, (const TA*)A, a_rs, \
+                     Kin, amode, mean, rstd, lnw, lnb, R, rps, slab_w, slab_b)
+  if (g_bf16 && a_bf16) WG(uint16_t, uint16_t);
+  else if (g_bf16) WG(uint16_t, float);
+  else if (a_bf16) WG(float, uint16_t);
+  else WG(float, float);
+#undef WG
+}
+
+void slab_reduce_launch(const ReduceJobs& jobs, hipStream_t st) {
+  if (jobs.n == 0) return;
+  int maxlen = 0;
+  for (int i = 0; i < jobs.n; ++i) maxlen = jobs.j[i].len > maxlen ? jobs.j[i].len : maxlen;
+  dim3 grid(min((maxlen + 255) / 256, 64), jobs.n);
+  hipLaunchKernelGGL(slab_reduce_kernel, grid, dim3(256), 0, st, jobs);
+}
+
+}  // namespace pio

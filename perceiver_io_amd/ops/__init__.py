@@ -1,0 +1,55 @@
+"""Op layer: hand-written HIP/CDNA4 kernels (``perceiver_io_amd/csrc``) behind
+autograd Functions, plus the eager PyTorch oracle used on CPU and in tests.
+
+Backend selection (``PERCEIVER_BACKEND`` env or :func:`set_backend`):
+  * ``auto``  — HIP kernels for CUDA(HIP) tensors, eager PyTorch on CPU.  On a GPU
+    box a missing/broken extension raises instead of silently falling back.
+  * ``hip``   — force the kernels (error if unavailable).
+  * ``torch`` — eager PyTorch everywhere (this framework's own eager oracle).
+  * ``reference`` — eager PyTorch with the reference's exact compute: ``nn.MultiheadAttention``
+    math (``F.multi_head_attention_forward``, need_weights=True), full ``(B, V, L)`` logits
+    cross-entropy and sync-ing boolean-index masking.  Used to measure the baseline.
+"""
+from __future__ import annotations
+
+import os
+from contextlib import contextmanager
+
+import torch
+
+from . import ext  # noqa: F401  (extension loader)
+
+_BACKEND = os.environ.get("PERCEIVER_BACKEND", "auto")
+_VALID = ("auto", "hip", "torch", "reference")
+
+
+def set_backend(name: str) -> None:
+    global _BACKEND
+    if name not in _VALID:
+        raise ValueError(f"backend must be one of {_VALID}, got {name!r}")
+    _BACKEND = name
+
+
+def get_backend() -> str:
+    return _BACKEND
+
+
+@contextmanager
+def backend(name: str):
+    prev = get_backend()
+    set_backend(name)
+    try:
+        yield
+    finally:
+        set_backend(prev)
+
+
+def use_hip(t: torch.Tensor) -> bool:
+    """True when ``t`` should be processed by the HIP kernels."""
+    if _BACKEND in ("torch", "reference") or not t.is_cuda:
+        return False
+    ext.require()  # raises loudly if the extension is missing on a GPU
+    return True
+
+
+from . import attention, fused, masking, mlm_head, optim  # noqa: E402,F401

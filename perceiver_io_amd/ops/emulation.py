@@ -1,0 +1,260 @@
+"""Plain-PyTorch emulation of every HIP kernel entry point (same signatures as ``_C``).
+
+Two uses: (1) the fused executor runs on CPU through this module, so its bookkeeping
+(strides, packed buffers, batch-broadcast queries, slab reductions, weight sharing) is
+covered by the CPU test-suite; (2) it is the fp32 oracle the GPU numerics tests compare
+the hand-written kernels against.  Rounding points mirror the kernels: GEMM operands are
+rounded to bf16 exactly where the kernels stage bf16 tiles, accumulation is fp32.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional
+
+import torch
+import torch.nn.functional as F
+
+LOG2E = 1.4426950408889634
+
+
+def _bf(x):
+    return x.to(torch.bfloat16).to(torch.float32)
+
+
+def _ln(x, w, b, eps):
+    mean = x.mean(-1)
+    var = x.var(-1, unbiased=False)
+    rstd = torch.rsqrt(var + eps)
+    return (x - mean[:, None]) * rstd[:, None] * w + b, mean, rstd
+
+
+def ln_linear_fwd(x, lnw, lnb, eps, w, bias, act, res, out_bf16, save_stats):
+    xf = x.float()
+    mean = rstd = None
+    if lnw is not None:
+        xn, mean, rstd = _ln(xf, lnw, lnb, eps)
+    else:
+        xn = xf
+    y = _bf(xn) @ _bf(w.float()).t()
+    if bias is not None:
+        y = y + bias
+    if act == 1:
+        y = F.gelu(y)
+    if res is not None:
+        y = y + res
+    y = y.to(torch.bfloat16) if out_bf16 else y
+    out = [y]
+    if save_stats and lnw is not None:
+        out += [mean, rstd]
+    return out
+
+
+def _heads(x, H):
+    b, n, _ = x.shape
+    return x[:, :, : x.shape[2]].reshape(b, n, H, -1).permute(0, 2, 1, 3)
+
+
+def _qkv(q, k, v, H, D):
+    B = max(q.shape[0], k.shape[0])
+    qf = q[:, :, : H * D].float().expand(B, -1, -1).reshape(B, q.shape[1], H, D).permute(0, 2, 1, 3)
+    kf = k[:, :, : H * D].float().reshape(B, k.shape[1], H, D).permute(0, 2, 1, 3)
+    vf = v[:, :, : H * D].float().reshape(B, v.shape[1], H, D).permute(0, 2, 1, 3)
+    return B, qf, kf, vf
+
+
+def _scores(qf, kf, kmask, scale):
+    s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
+    if kmask is not None:
+        s = s.masked_fill(kmask.view(kmask.shape[0], 1, 1, -1).bool(), float("-inf"))
+    return s
+
+
+def attn_fwd(q, k, v, kmask, H, D, scale, dropout_p, seed, nsplit):
+    if dropout_p > 0:
+        raise NotImplementedError("emulation: attention dropout uses the kernel's hash RNG (GPU only)")
+    B, qf, kf, vf = _qkv(q, k, v, H, D)
+    s = _scores(qf, kf, kmask, scale)
+    lse = torch.logsumexp(s, -1)  # (B, H, Nq), -inf for dead rows
+    p = torch.exp(s - lse[..., None])
+    p = torch.nan_to_num(p, nan=0.0)
+    o = torch.matmul(_bf(p), vf)
+    lse2 = torch.where(torch.isfinite(lse), lse * LOG2E, torch.full_like(lse, float("inf")))
+    o = o.permute(0, 2, 1, 3).reshape(B, q.shape[1], H * D).to(torch.bfloat16)
+    return o, lse2.permute(0, 2, 1).contiguous()
+
+
+def attn_bwd(q, k, v, kmask, o, dO, lse, delta_in, H, D, scale, dropout_p, seed, dq_out, dk_out, dv_out):
+    B, qf, kf, vf = _qkv(q, k, v, H, D)
+    s = _scores(qf, kf, kmask, scale)
+    l2 = lse.permute(0, 2, 1)  # (B, H, Nq)
+    p = torch.exp2(s * LOG2E - l2[..., None])
+    p = torch.nan_to_num(p, nan=0.0)
+    dof = dO.float().reshape(B, -1, H, D).permute(0, 2, 1, 3)
+    of = o.float().reshape(B, -1, H, D).permute(0, 2, 1, 3)
+    delta = (dof * of).sum(-1, keepdim=True)
+    dp = torch.matmul(dof, vf.transpose(-1, -2))
+    ds = p * (dp - delta)
+    dq = torch.matmul(ds, kf) * scale
+    dk = torch.matmul(ds.transpose(-1, -2), qf) * scale
+    dv = torch.matmul(p.transpose(-1, -2), dof)
+
+    def merge(t):
+        return t.permute(0, 2, 1, 3).reshape(B, t.shape[2], H * D)
+
+    res = []
+    for t, out in ((dq, dq_out), (dk, dk_out), (dv, dv_out)):
+        t = merge(t)
+        if out is not None:
+            out[:, :, : H * D].copy_(t)
+            t = out
+        res.append(t)
+    return res
+
+
+def post_attn_fwd(o, x, wo, bo, g2, be2, eps, w1, b1, w2, b2):
+    y = x + _bf(o.float()) @ _bf(wo.float()).t() + bo
+    xn, m, r = _ln(y, g2, be2, eps)
+    u = _bf(xn) @ _bf(w1.float()).t() + b1
+    h = F.gelu(u)
+    z = y + _bf(h) @ _bf(w2.float()).t() + b2
+    return z, y, m, r, u.to(torch.bfloat16)
+
+
+def _gelu_grad(u):
+    cdf = 0.5 * (1.0 + torch.erf(u * 0.7071067811865476))
+    pdf = 0.3989422804014327 * torch.exp(-0.5 * u * u)
+    return cdf + u * pdf
+
+
+def _ln_bwd(dxn, x, mean, rstd, w):
+    xh = (x - mean[:, None]) * rstd[:, None]
+    g = dxn * w
+    s1 = g.mean(-1, keepdim=True)
+    s2 = (g * xh).mean(-1, keepdim=True)
+    return rstd[:, None] * (g - s1 - xh * s2), xh
+
+
+def post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, H):
+    dh = _bf(dz) @ _bf(w2.float())
+    du = dh * _gelu_grad(u.float())
+    du_b = du.to(torch.bfloat16)
+    dxn = _bf(du) @ _bf(w1.float())
+    dln, xh = _ln_bwd(dxn, y, m2, r2, g2)
+    dy = dz + dln
+    do = (_bf(dy) @ _bf(wo.float())).to(torch.bfloat16)
+    R, C = dz.shape
+    D = C // H
+    delta = (do.float().view(R, H, D) * o.float().view(R, H, D)).sum(-1)
+    sg = (dxn * xh).sum(0, keepdim=True)
+    sb = dxn.sum(0, keepdim=True)
+    return dy, du_b, do, delta, sg, sb
+
+
+def ln_linear_dgrad(g, w, x, mean, rstd, lnw, dres, need_dx):
+    dxn = _bf(g.float()) @ _bf(w.float())
+    dx = sg = sb = None
+    if lnw is not None:
+        d, xh = _ln_bwd(dxn, x.float(), mean, rstd, lnw)
+        sg = (dxn * xh).sum(0, keepdim=True)
+        sb = dxn.sum(0, keepdim=True)
+    else:
+        d = dxn
+    if need_dx:
+        dx = d + dres if dres is not None else d
+    return dx, sg, sb
+
+
+def wgrad(g, a, amode, mean, rstd, lnw, lnb, nsplit, with_bias):
+    af = a.float()
+    if amode == 1:
+        af = (af - mean[:, None]) * rstd[:, None] * lnw + lnb
+    elif amode == 2:
+        af = F.gelu(af)
+    sw = (_bf(g.float()).t() @ _bf(af)).unsqueeze(0)
+    sb = g.float().sum(0, keepdim=True) if with_bias else None
+    return sw, sb
+
+
+def slab_reduce(slabs: List[torch.Tensor], dsts: List[torch.Tensor], acc: List[bool]):
+    for s, d, a in zip(slabs, dsts, acc):
+        v = s.reshape(-1, d.numel()).sum(0).view(d.shape)
+        if a:
+            d.add_(v)
+        else:
+            d.copy_(v)
+
+
+def ce_fwd(h, labels, w, bias):
+    logits = _bf(h.float()) @ _bf(w.float()).t() + bias
+    lse = torch.logsumexp(logits, -1)
+    valid = labels >= 0
+    picked = logits.gather(1, labels.clamp(min=0)[:, None])[:, 0]
+    loss = torch.where(valid, lse - picked, torch.zeros_like(lse))
+    return loss, lse
+
+
+def ce_bwd(h, labels, w, bias, lse, gscale, dH, dW, db, accumulate):
+    logits = _bf(h.float()) @ _bf(w.float()).t() + bias
+    p = torch.exp(logits - lse[:, None])
+    valid = (labels >= 0).float()[:, None]
+    onehot = F.one_hot(labels.clamp(min=0), w.shape[0]).float()
+    dl = (p - onehot) * valid * gscale
+    dH.add_(_bf(dl) @ _bf(w.float()))
+    gw = _bf(dl).t() @ _bf(h.float())
+    gb = dl.sum(0)
+    if accumulate:
+        dW.add_(gw)
+        db.add_(gb)
+    else:
+        dW.copy_(gw)
+        db.copy_(gb)
+
+
+def embed_fwd(ids, E, P, scale):
+    return E[ids] * scale + P[: ids.shape[1]].unsqueeze(0)
+
+
+def embed_bwd(ids, g, dE, dP, scale):
+    C = g.shape[-1]
+    if dE is not None:
+        dE.index_add_(0, ids.reshape(-1), g.reshape(-1, C) * scale)
+    if dP is not None:
+        dP[: ids.shape[1]] += g.sum(0)
+
+
+def text_mask(x, pad, u, rid, unk, mask, p):
+    special = x == unk
+    if pad is not None:
+        special = special | pad
+    sel = ~special & (u[0] < p)
+    msk = sel & (u[1] < 0.9)
+    rnd = msk & (u[2] < 1.0 / 9.0)
+    xm = torch.where(rnd, rid, torch.where(msk, torch.full_like(x, mask), x))
+    return xm, torch.where(sel, x, torch.full_like(x, -100))
+
+
+def sumsq(g, out):
+    out += (g.float() ** 2).sum()
+
+
+def adamw(p, g, m, v, shadow, hyper, eps, wd, clip, gscale):
+    lr, step, b1, b2 = float(hyper[0]), float(hyper[1]), float(hyper[3]), float(hyper[4])
+    gs = gscale
+    if clip > 0:
+        norm = math.sqrt(float(hyper[2]))
+        f = clip / (norm + 1e-6)
+        if f < 1:
+            gs *= f
+    gg = g * gs
+    p.mul_(1 - lr * wd)
+    m.mul_(b1).add_(gg, alpha=1 - b1)
+    v.mul_(b2).addcmul_(gg, gg, value=1 - b2)
+    bc1, bc2 = 1 - b1 ** step, 1 - b2 ** step
+    denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
+    p.addcdiv_(m, denom, value=-lr / bc1)
+    if shadow is not None:
+        shadow.copy_(p.to(shadow.dtype))
+
+
+def cast_bf16(x, y):
+    y.copy_(x.to(torch.bfloat16).view(y.shape))

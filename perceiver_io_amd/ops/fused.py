@@ -1,0 +1,378 @@
+"""Fused layer executor: one autograd node per Perceiver sublayer.
+
+The module tree (``models/blocks.py``) only holds parameters.  On an MI355X each
+``Residual(attention) → Residual(mlp)`` pair (reference ``perceiver/model.py:29-44``) runs as
+a single :class:`_LayerFn` whose forward is
+
+    LN+QKV projection (ln_linear_fwd) → flash attention (attn_fwd) →
+    out-proj + residual + LN2 + MLP(GELU) + residual (post_attn_fwd)
+
+i.e. 3 kernel launches, and whose backward is the hand-written reverse chain
+(post_attn_bwd → attn_bwd → ln_linear_dgrad + wgrad slabs → slab_reduce).  Activations
+kept for backward: the bf16 Q/K/V and attention output, fp32 post-attention residual,
+LN statistics, the bf16 pre-GELU tensor — LN outputs and GELU outputs are recomputed.
+
+Encoder-specific savings over the reference forward:
+  * the learned latent array enters the first layer un-expanded (batch stride 0): its
+    LayerNorm + Q projection runs on N rows instead of B·N (SURVEY K-04);
+  * the decoder's output queries likewise (K rows, not B·K).
+
+``kernels`` is either the HIP extension or :mod:`.emulation` (same signatures in plain
+PyTorch), so the executor's bookkeeping is testable on CPU.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import List, Optional
+
+import torch
+
+from . import emulation, ext
+
+EPS = 1e-5
+
+
+def kernels(t: torch.Tensor):
+    return ext.require() if t.is_cuda else emulation
+
+
+# ------------------------------------------------------------------------------------------
+# bf16 weight shadows
+# ------------------------------------------------------------------------------------------
+class WeightCache:
+    """bf16 copies of fp32 parameters used as GEMM operands.
+
+    An entry is refreshed when the parameter's version counter or storage changes.  The
+    fused optimizer (``ops.optim.FusedAdamW``) writes shadows in the same pass as the
+    parameter update and binds them here, so steady-state training never re-casts.
+    """
+
+    def __init__(self):
+        self._d = {}
+
+    def bind(self, p: torch.Tensor, shadow: torch.Tensor):
+        self._d[id(p)] = [p._version, p.data_ptr(), shadow, p]
+        with torch.no_grad():
+            shadow.copy_(p.detach().reshape(shadow.shape))
+
+    def get(self, p: torch.Tensor) -> torch.Tensor:
+        ent = self._d.get(id(p))
+        if ent is not None and ent[3] is p and ent[0] == p._version and ent[1] == p.data_ptr():
+            return ent[2]
+        with torch.no_grad():
+            if ent is not None and ent[3] is p and ent[2].shape == p.shape:
+                ent[2].copy_(p.detach())
+                ent[0], ent[1] = p._version, p.data_ptr()
+                return ent[2]
+            t = p.detach().to(torch.bfloat16).contiguous()
+        self._d[id(p)] = [p._version, p.data_ptr(), t, p]
+        return t
+
+    def clear(self):
+        self._d.clear()
+
+
+weight_cache = WeightCache()
+
+
+# ------------------------------------------------------------------------------------------
+# layer specs
+# ------------------------------------------------------------------------------------------
+@dataclass(frozen=True)
+class LayerSpec:
+    cross: bool
+    packed: bool      # packed in_proj_weight (kdim == vdim == embed_dim)
+    C: int            # embed / latent channels
+    heads: int
+    dropout: float
+
+
+def layer_spec_and_params(layer):
+    att = layer.attn
+    mha = att.attention.attention
+    m = layer.mlp
+    cross = hasattr(att, "q_norm")
+    packed = mha._qkv_same_embed_dim
+    spec = LayerSpec(cross=cross, packed=packed, C=mha.embed_dim, heads=mha.num_heads, dropout=float(mha.dropout))
+    ps: List[torch.Tensor] = []
+    if cross:
+        ps += [att.q_norm.weight, att.q_norm.bias, att.kv_norm.weight, att.kv_norm.bias]
+    else:
+        ps += [att.norm.weight, att.norm.bias]
+    if packed:
+        ps += [mha.in_proj_weight]
+    else:
+        ps += [mha.q_proj_weight, mha.k_proj_weight, mha.v_proj_weight]
+    ps += [mha.in_proj_bias, mha.out_proj.weight, mha.out_proj.bias,
+           m[0].weight, m[0].bias, m[1].weight, m[1].bias, m[3].weight, m[3].bias]
+    return spec, ps
+
+
+def _bf16_weights(spec: LayerSpec, ps):
+    """bf16 GEMM operands: (w_q_or_qkv, w_kv or None, w_o, w_1, w_2)."""
+    wc = weight_cache
+    if spec.cross:
+        if spec.packed:
+            win = wc.get(ps[4])
+            wq, wkv = win[: spec.C], win[spec.C:]
+            rest = ps[5:]
+        else:
+            wq = wc.get(ps[4])
+            wkv = torch.cat([wc.get(ps[5]), wc.get(ps[6])], 0)
+            rest = ps[7:]
+    else:
+        wq, wkv = wc.get(ps[2]), None
+        rest = ps[3:]
+    # rest = [bin, Wo, bo, g2, be2, W1, b1, W2, b2]
+    return wq, wkv, wc.get(rest[1]), wc.get(rest[5]), wc.get(rest[7])
+
+
+def _wgrad_splits(rows: int, n: int) -> int:
+    return int(max(1, min(rows // 128, 256 // max(1, (n + 63) // 64))))
+
+
+class _LayerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, spec: LayerSpec, bw, seed, p_attn, x_q, x_kv, kmask, *ps):
+        K = kernels(x_q)
+        C, H = spec.C, spec.heads
+        D = C // H
+        scale = 1.0 / math.sqrt(D)
+        wq, wkv, wo, w1, w2 = bw
+        if spec.cross:
+            g_q, b_q, g_kv, b_kv = ps[0:4]
+            rest = ps[5:] if spec.packed else ps[7:]
+        else:
+            g_q, b_q = ps[0:2]
+            rest = ps[3:]
+        bin_, _, bo, g2, be2, _, b1, _, b2 = rest
+        Bq, Nq = x_q.shape[0], x_q.shape[1]
+        xq2 = x_q.reshape(Bq * Nq, C)
+        if not xq2.is_contiguous():
+            xq2 = xq2.contiguous()
+        if spec.cross:
+            B, M, Ckv = x_kv.shape
+            xkv2 = x_kv.reshape(B * M, Ckv)
+            q, mean_q, rstd_q = K.ln_linear_fwd(xq2, g_q, b_q, EPS, wq, bin_[:C], 0, None, True, True)
+            kv, mean_kv, rstd_kv = K.ln_linear_fwd(xkv2, g_kv, b_kv, EPS, wkv, bin_[C:], 0, None, True, True)
+            q3 = q.view(Bq, Nq, C)
+            kv3 = kv.view(B, M, 2 * C)
+            k3, v3 = kv3[:, :, :C], kv3[:, :, C:]
+        else:
+            B = Bq
+            qkv, mean_q, rstd_q = K.ln_linear_fwd(xq2, g_q, b_q, EPS, wq, bin_, 0, None, True, True)
+            qkv3 = qkv.view(B, Nq, 3 * C)
+            q3, k3, v3 = qkv3[:, :, :C], qkv3[:, :, C:2 * C], qkv3[:, :, 2 * C:]
+            xkv2 = kv = mean_kv = rstd_kv = None
+        from .attention import pick_splits
+
+        nsplit = pick_splits(B, H, Nq, k3.shape[1])
+        o, lse = K.attn_fwd(q3, k3, v3, kmask, H, D, scale, p_attn, seed, nsplit)
+        o2 = o.view(B * Nq, C)
+        xres = xq2 if Bq == B else x_q.expand(B, Nq, C).reshape(B * Nq, C).contiguous()
+        z, y, m2, r2, u = K.post_attn_fwd(o2, xres, wo, bo, g2, be2, EPS, w1, b1, w2, b2)
+        ctx.spec, ctx.bw, ctx.seed, ctx.p_attn = spec, bw, seed, p_attn
+        ctx.dims = (B, Bq, Nq, C, H, D, scale)
+        ctx.kv_grad = x_kv is not None and ctx.needs_input_grad[5]
+        ctx.has_mask = kmask is not None
+        ctx.save_for_backward(xq2, xkv2 if xkv2 is not None else torch.empty(0), q3 if spec.cross else qkv,
+                              kv if kv is not None else torch.empty(0), o, lse, y, m2, r2, u, mean_q, rstd_q,
+                              mean_kv if mean_kv is not None else torch.empty(0),
+                              rstd_kv if rstd_kv is not None else torch.empty(0),
+                              kmask if kmask is not None else torch.empty(0), *ps)
+        return z.view(B, Nq, C)
+
+    @staticmethod
+    def backward(ctx, dz):
+        K = kernels(dz)
+        spec = ctx.spec
+        B, Bq, Nq, C, H, D, scale = ctx.dims
+        (xq2, xkv2, qx, kv, o, lse, y, m2, r2, u, mean_q, rstd_q, mean_kv, rstd_kv, kmask, *ps) = ctx.saved_tensors
+        kmask = kmask if ctx.has_mask else None
+        wq, wkv, wo, w1, w2 = ctx.bw
+        if spec.cross:
+            g_q, b_q, g_kv, b_kv = ps[0:4]
+            rest = ps[5:] if spec.packed else ps[7:]
+        else:
+            g_q, b_q = ps[0:2]
+            rest = ps[3:]
+        bin_, Wo, bo, g2, be2, W1, b1, W2, b2 = rest
+        dz2 = dz.reshape(B * Nq, C)
+        if not dz2.is_contiguous():
+            dz2 = dz2.contiguous()
+        o2 = o.view(B * Nq, C)
+        dy, du, do, _delta, sg2, sb2 = K.post_attn_bwd(dz2, y, m2, r2, u, o2, wo, w1, w2, g2, H)
+        dev = dz.device
+        f32 = dict(device=dev, dtype=torch.float32)
+        R = B * Nq
+        slabs, dsts = [], []
+        grads = [None] * len(ps)
+
+        def red(slab, dst):
+            slabs.append(slab)
+            dsts.append(dst)
+
+        # --- attention backward -------------------------------------------------------
+        if spec.cross:
+            q3 = qx
+            M = kv.shape[0] // B
+            kv3 = kv.view(B, M, 2 * C)
+            dkv = torch.empty((B, M, 2 * C), **f32)
+            dq, _, _ = K.attn_bwd(q3, kv3[:, :, :C], kv3[:, :, C:], kmask, o, do.view(B, Nq, C), lse, None, H, D,
+                                  scale, ctx.p_attn, ctx.seed, None, dkv[:, :, :C], dkv[:, :, C:])
+            dq2 = dq.reshape(B * Nq, C)
+            dres = dy
+            if Bq == 1 and B > 1:
+                dq2 = dq.sum(0)
+                dres = dy.view(B, Nq, C).sum(0)
+            dx_q, sgq, sbq = K.ln_linear_dgrad(dq2, wq, xq2, mean_q, rstd_q, g_q, dres, True)
+            dkv2 = dkv.view(B * M, 2 * C)
+            dx_kv, sgk, sbk = K.ln_linear_dgrad(dkv2, wkv, xkv2, mean_kv, rstd_kv, g_kv, None, ctx.kv_grad)
+            grads[0], grads[1] = torch.empty(C, **f32), torch.empty(C, **f32)
+            red(sgq, grads[0]); red(sbq, grads[1])
+            ckv = xkv2.shape[1]
+            grads[2], grads[3] = torch.empty(ckv, **f32), torch.empty(ckv, **f32)
+            red(sgk, grads[2]); red(sbk, grads[3])
+            rq = dq2.shape[0]
+            swq, sbq_ = K.wgrad(dq2, xq2, 1, mean_q, rstd_q, g_q, b_q, _wgrad_splits(rq, C), True)
+            swk, sbk_ = K.wgrad(dkv2, xkv2, 1, mean_kv, rstd_kv, g_kv, b_kv, _wgrad_splits(B * M, 2 * C), True)
+            gbin = torch.empty(3 * C, **f32)
+            if spec.packed:
+                gin = torch.empty((3 * C, C), **f32)
+                red(swq, gin[:C]); red(swk, gin[C:])
+                grads[4] = gin
+                ibias = 5
+            else:
+                gkv = torch.empty((2 * C, ckv), **f32)
+                grads[4] = torch.empty((C, C), **f32)
+                red(swq, grads[4]); red(swk, gkv)
+                grads[5], grads[6] = gkv[:C], gkv[C:]
+                ibias = 7
+            red(sbq_, gbin[:C]); red(sbk_, gbin[C:])
+            grads[ibias] = gbin
+            dx_q = dx_q.view(Bq, Nq, C)
+            dx_kv = dx_kv.view(B, M, -1) if ctx.kv_grad else None
+        else:
+            qkv3 = qx.view(B, Nq, 3 * C)
+            dqkv = torch.empty((B, Nq, 3 * C), **f32)
+            K.attn_bwd(qkv3[:, :, :C], qkv3[:, :, C:2 * C], qkv3[:, :, 2 * C:], kmask, o, do.view(B, Nq, C), lse, None,
+                       H, D, scale, ctx.p_attn, ctx.seed, dqkv[:, :, :C], dqkv[:, :, C:2 * C], dqkv[:, :, 2 * C:])
+            dqkv2 = dqkv.view(R, 3 * C)
+            dx_q, sg1, sb1 = K.ln_linear_dgrad(dqkv2, wq, xq2, mean_q, rstd_q, g_q, dy, True)
+            grads[0], grads[1] = torch.empty(C, **f32), torch.empty(C, **f32)
+            red(sg1, grads[0]); red(sb1, grads[1])
+            sw, sb = K.wgrad(dqkv2, xq2, 1, mean_q, rstd_q, g_q, b_q, _wgrad_splits(R, 3 * C), True)
+            grads[2], grads[3] = torch.empty((3 * C, C), **f32), torch.empty(3 * C, **f32)
+            red(sw, grads[2]); red(sb, grads[3])
+            ibias = 3
+            dx_q = dx_q.view(B, Nq, C)
+            dx_kv = None
+        # --- post-attention weights -------------------------------------------------------
+        i0 = ibias + 1  # index of Wo in ps
+        ns = _wgrad_splits(R, C)
+        swo, sbo = K.wgrad(dy, o2, 0, None, None, None, None, ns, True)
+        sw1, sb1m = K.wgrad(du, y, 1, m2, r2, g2, be2, ns, True)
+        sw2, sb2m = K.wgrad(dz2, u, 2, None, None, None, None, ns, True)
+        for j, sl in ((0, swo), (1, sbo), (2, sg2), (3, sb2), (4, sw1), (5, sb1m), (6, sw2), (7, sb2m)):
+            grads[i0 + j] = torch.empty(ps[i0 + j].shape, **f32)
+            red(sl, grads[i0 + j])
+        K.slab_reduce(slabs, dsts, [False] * len(slabs))
+        return (None, None, None, None, dx_q, dx_kv, None, *grads)
+
+
+def _seed(spec: LayerSpec, training: bool) -> int:
+    if spec.dropout > 0.0 and training:
+        return int(torch.randint(0, 2**31 - 1, (1,)).item())
+    return 0
+
+
+def _run_layer(layer, x_q, x_kv=None, pad_mask=None):
+    spec, ps = layer_spec_and_params(layer)
+    if spec.dropout > 0.0 and layer.training:
+        raise NotImplementedError("fused path: dropout > 0 handled by the eager path")
+    kmask = pad_mask.to(torch.bool).contiguous() if pad_mask is not None else None
+    bw = _bf16_weights(spec, ps)
+    p_attn = spec.dropout if layer.training else 0.0
+    if x_q.dtype != torch.float32:
+        x_q = x_q.float()
+    if x_kv is not None and x_kv.dtype != torch.float32:
+        x_kv = x_kv.float()
+    return _LayerFn.apply(spec, bw, _seed(spec, layer.training), p_attn, x_q, x_kv, kmask, *ps)
+
+
+def _fusable(layer, x=None) -> bool:
+    spec, _ = layer_spec_and_params(layer)
+    d = spec.C // spec.heads
+    return (spec.C in (32, 64, 128) and d in (16, 32, 64, 128) and not (spec.dropout > 0.0 and layer.training))
+
+
+def can_fuse(layer, x_kv=None) -> bool:
+    return _fusable(layer) and (x_kv is None or x_kv.shape[-1] <= 160)
+
+
+def self_attention_layer(layer, x):
+    if not _fusable(layer, x):
+        return layer.eager_forward(x)
+    return _run_layer(layer, x)
+
+
+def cross_attention_layer(layer, x_q, x_kv, pad_mask=None):
+    if not can_fuse(layer, x_kv):
+        return layer.eager_forward(x_q, x_kv, pad_mask)
+    if x_q.dim() == 3 and x_q.shape[0] > 1 and x_q.stride(0) == 0:
+        x_q = x_q[:1]  # batch-broadcast queries (decoder output array): project once
+    return _run_layer(layer, x_q, x_kv, pad_mask)
+
+
+# ------------------------------------------------------------------------------------------
+# text embedding
+# ------------------------------------------------------------------------------------------
+class _TextEmbedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, emb, pos, scale):
+        K = kernels(emb)
+        ids = ids.contiguous()
+        out = K.embed_fwd(ids, emb, pos[: ids.shape[1]].contiguous(), scale)
+        ctx.save_for_backward(ids)
+        ctx.scale, ctx.shapes = scale, (emb.shape, pos.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (ids,) = ctx.saved_tensors
+        K = kernels(g)
+        es, ps_ = ctx.shapes
+        de = torch.zeros(es, device=g.device, dtype=torch.float32) if ctx.needs_input_grad[1] else None
+        dp = torch.zeros(ps_, device=g.device, dtype=torch.float32) if ctx.needs_input_grad[2] else None
+        K.embed_bwd(ids, g.contiguous(), de, dp, ctx.scale)
+        return None, de, dp, None
+
+
+def text_embed(adapter, ids):
+    return _TextEmbedFn.apply(ids, adapter.text_embedding.weight, adapter.pos_encoding, float(adapter.scale))
+
+
+# ------------------------------------------------------------------------------------------
+# encoder
+# ------------------------------------------------------------------------------------------
+def encoder_forward(encoder, x, pad_mask=None):
+    from ..models.adapters import TextInputAdapter
+
+    ad = encoder.input_adapter
+    if isinstance(ad, TextInputAdapter):
+        xin = text_embed(ad, x)
+    else:
+        xin = ad(x)
+    lat = encoder.latent.unsqueeze(0)  # (1, N, C): projected once, broadcast inside the kernels
+    b = xin.shape[0]
+    for layer in encoder.layers():
+        cross, block = layer[0], layer[1]
+        if lat.shape[0] == 1 and not can_fuse(cross, xin):
+            lat = lat.expand(b, -1, -1)
+        lat = cross_attention_layer(cross, lat, xin, pad_mask)
+        if lat.shape[0] == 1 and b > 1:
+            lat = lat.expand(b, -1, -1)
+        for sa in block:
+            lat = self_attention_layer(sa, lat)
+    return lat

@@ -1,0 +1,196 @@
+"""Flat parameter space + fused AdamW (SURVEY K-15, §5.8).
+
+``FlatParameterSpace`` re-homes every trainable parameter into ONE contiguous fp32 buffer
+(and its gradient into one fp32 buffer, with a bf16 shadow of the weights for the GEMM
+kernels).  Consequences on MI355X:
+  * the data-parallel all-reduce is one (or a few bucketed) RCCL call(s) over a flat
+    buffer instead of ~190 per-tensor collectives (``parallel/reducer.py``);
+  * the optimizer is a single kernel launch over the flat buffers that also refreshes the
+    bf16 shadow (no per-step weight casts);
+  * zeroing gradients is one memset.
+
+``FusedAdamW`` is a ``torch.optim.Optimizer`` (so ``torch.optim.lr_scheduler`` schedulers
+such as ``OneCycleLR`` drive it through ``param_groups``) with torch.optim.AdamW semantics
+and a torch-compatible ``state_dict`` layout (``exp_avg``/``exp_avg_sq``/``step`` per
+parameter), so Lightning-layout checkpoints round-trip.  lr/betas/step live in a small
+device tensor refreshed before each step, which keeps the update capturable in a hipGraph.
+"""
+from __future__ import annotations
+
+import math
+from typing import Iterable, List, Optional
+
+import torch
+
+from . import emulation, ext
+
+ALIGN = 64  # elements; keeps every parameter view 256-byte aligned
+
+
+class FlatParameterSpace:
+    def __init__(self, params: Iterable[torch.nn.Parameter], with_shadow: Optional[bool] = None):
+        self.params: List[torch.nn.Parameter] = [p for p in params if p.requires_grad]
+        if not self.params:
+            raise ValueError("no trainable parameters")
+        dev = self.params[0].device
+        self.device = dev
+        self.offsets = []
+        off = 0
+        for p in self.params:
+            self.offsets.append(off)
+            off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
+        self.numel = off
+        self.data = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(off, dtype=torch.float32, device=dev)
+        if with_shadow is None:
+            with_shadow = dev.type == "cuda"
+        self.shadow = torch.zeros(off, dtype=torch.bfloat16, device=dev) if with_shadow else None
+        with torch.no_grad():
+            for p, o in zip(self.params, self.offsets):
+                n = p.numel()
+                self.data[o:o + n].copy_(p.detach().reshape(-1).float())
+                p.data = self.data[o:o + n].view_as(p)
+                p.grad = self.grad[o:o + n].view_as(p)
+        if self.shadow is not None:
+            from .fused import weight_cache
+
+            for p, o in zip(self.params, self.offsets):
+                weight_cache.bind(p, self.shadow[o:o + p.numel()].view(p.shape))
+
+    def views(self, buf: torch.Tensor):
+        return [buf[o:o + p.numel()].view(p.shape) for p, o in zip(self.params, self.offsets)]
+
+    def zero_grad(self):
+        self.grad.zero_()
+        # re-attach views autograd may have replaced (e.g. a grad that was set to None)
+        for p, o in zip(self.params, self.offsets):
+            g = p.grad
+            if g is None or g.data_ptr() != self.grad[o:o + 1].data_ptr():
+                p.grad = self.grad[o:o + p.numel()].view_as(p)
+
+    def check_views(self) -> bool:
+        return all(p.grad is not None and p.grad.data_ptr() == self.grad[o:o + 1].data_ptr()
+                   for p, o in zip(self.params, self.offsets))
+
+    def bucket_ranges(self, bucket_bytes: int):
+        """Split [0, numel) into contiguous ranges of ≤ bucket_bytes in reverse parameter
+        order (gradients of late parameters are produced first in backward)."""
+        cap = max(ALIGN, bucket_bytes // 4)
+        ends = self.offsets[1:] + [self.numel]
+        ranges = []
+        hi = self.numel
+        for o in reversed(self.offsets):
+            if hi - o >= cap:
+                ranges.append((o, hi))
+                hi = o
+        if hi > 0:
+            ranges.append((0, hi))
+        del ends
+        return ranges
+
+
+class _HostRing:
+    """Pinned host staging slots for per-step device hyper-parameters (no reuse before the
+    copy that read a slot has completed)."""
+
+    def __init__(self, n: int, width: int, device):
+        self.slots = [torch.zeros(width, dtype=torch.float32).pin_memory() for _ in range(n)]
+        self.events = [None] * n
+        self.i = 0
+
+    def push(self, values, dst: torch.Tensor):
+        i = self.i
+        self.i = (self.i + 1) % len(self.slots)
+        if self.events[i] is not None:
+            self.events[i].synchronize()
+        s = self.slots[i]
+        for j, v in enumerate(values):
+            s[j] = float(v)
+        dst.copy_(s, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.events[i] = ev
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    """AdamW over a :class:`FlatParameterSpace` in one kernel (HIP) or its emulation (CPU)."""
+
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 1e-2,
+                 amsgrad: bool = False, max_grad_norm: float = 0.0, flat: Optional[FlatParameterSpace] = None):
+        if amsgrad:
+            raise NotImplementedError("amsgrad is not supported by the fused optimizer")
+        params = list(params)
+        defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, amsgrad=False,
+                        maximize=False, foreach=None, capturable=False, differentiable=False, fused=None)
+        super().__init__(params, defaults)
+        if len(self.param_groups) != 1:
+            raise ValueError("FusedAdamW supports a single parameter group")
+        self.flat = flat if flat is not None else FlatParameterSpace(self.param_groups[0]["params"])
+        dev = self.flat.device
+        self.exp_avg = torch.zeros(self.flat.numel, dtype=torch.float32, device=dev)
+        self.exp_avg_sq = torch.zeros(self.flat.numel, dtype=torch.float32, device=dev)
+        self.hyper = torch.zeros(8, dtype=torch.float32, device=dev)
+        self.max_grad_norm = float(max_grad_norm)
+        self._step = 0
+        self._ring = _HostRing(8, 8, dev) if dev.type == "cuda" else None
+        self.grad_scale = 1.0
+
+    # -- the update ---------------------------------------------------------------------
+    def stage_hyper(self):
+        """Write lr / step / betas for the NEXT update into device memory (outside any graph)."""
+        g = self.param_groups[0]
+        b1, b2 = g["betas"]
+        vals = [g["lr"], self._step + 1, 0.0, b1, b2]
+        if self._ring is not None:
+            self._ring.push(vals, self.hyper[:5])
+        else:
+            self.hyper[:5] = torch.tensor(vals)
+
+    def device_update(self):
+        """The capturable part: (grad-norm) + fused AdamW kernel over the flat buffers."""
+        K = ext.require() if self.flat.device.type == "cuda" else emulation
+        g = self.param_groups[0]
+        if self.max_grad_norm > 0:
+            self.hyper[2:3].zero_()
+            K.sumsq(self.flat.grad, self.hyper[2:3])
+        K.adamw(self.flat.data, self.flat.grad, self.exp_avg, self.exp_avg_sq, self.flat.shadow, self.hyper,
+                g["eps"], g["weight_decay"], self.max_grad_norm, self.grad_scale)
+
+    @torch.no_grad()
+    def step(self, closure=None, staged: bool = False):
+        loss = closure() if closure is not None else None
+        if not staged:
+            self.stage_hyper()
+        self.device_update()
+        self._step += 1
+        return loss
+
+    def zero_grad(self, set_to_none: bool = False):
+        self.flat.zero_grad()
+
+    # -- torch-compatible state dict ------------------------------------------------------
+    def state_dict(self):
+        sd = super().state_dict()
+        state = {}
+        ea, es = self.flat.views(self.exp_avg), self.flat.views(self.exp_avg_sq)
+        for i in range(len(self.flat.params)):
+            state[i] = {"step": torch.tensor(float(self._step)), "exp_avg": ea[i].clone(), "exp_avg_sq": es[i].clone()}
+        sd["state"] = state
+        return sd
+
+    def load_state_dict(self, state_dict):
+        state = state_dict.get("state", {})
+        groups = state_dict["param_groups"]
+        for g, sg in zip(self.param_groups, groups):
+            for k, v in sg.items():
+                if k != "params":
+                    g[k] = v
+        ea, es = self.flat.views(self.exp_avg), self.flat.views(self.exp_avg_sq)
+        step = 0
+        for i, st in state.items():
+            i = int(i)
+            if "exp_avg" in st:
+                ea[i].copy_(st["exp_avg"])
+                es[i].copy_(st["exp_avg_sq"])
+            step = int(float(st.get("step", 0)))
+        self._step = step

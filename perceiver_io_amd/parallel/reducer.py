@@ -1,0 +1,84 @@
+"""Data-parallel gradient reducer over the flat gradient buffer (SURVEY C-01..C-03, §5.8).
+
+Replaces the DDP Reducer the reference gets from Lightning (``trainer.yaml:47``):
+  * parameters and buffers are broadcast once from rank 0 as flat tensors (C-01); the
+    deterministic Fourier position-encoding buffer is *not* re-broadcast every step (C-02);
+  * gradients live in ONE contiguous fp32 buffer (``ops.optim.FlatParameterSpace``), reduced
+    by a few large RCCL all-reduces instead of per-parameter buckets.  Per-step gradient
+    volume is 4–11 MB, so on xGMI the collective is latency-bound: 1–2 buckets is optimal
+    and more, smaller buckets only add ring-hop latency;
+  * the average (÷ world) is folded into the fused optimizer's gradient scale (no extra pass);
+  * optional overlap: ``ready(range)`` launches a bucket's all-reduce on a side HIP stream
+    as soon as the backward has produced it (the decoder/head grads are produced first);
+    ``finish()`` makes the main stream wait on the side stream.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+class FlatGradReducer:
+    def __init__(self, flat, bucket_bytes: int = 32 << 20, overlap: bool = False, wire_dtype: Optional[torch.dtype] = None):
+        self.flat = flat
+        self.world = dist.get_world_size() if (dist.is_available() and dist.is_initialized()) else 1
+        self.buckets: List[Tuple[int, int]] = flat.bucket_ranges(bucket_bytes)
+        self.overlap = overlap and flat.device.type == "cuda"
+        self.wire_dtype = wire_dtype
+        self._side = torch.cuda.Stream() if self.overlap else None
+        self._launched = set()
+
+    @property
+    def enabled(self) -> bool:
+        return self.world > 1
+
+    def broadcast_parameters(self, module: torch.nn.Module, src: int = 0):
+        """C-01: one broadcast of the flat parameter buffer + remaining buffers."""
+        if not self.enabled:
+            return
+        dist.broadcast(self.flat.data, src=src)
+        flat_ptrs = {p.data_ptr() for p in self.flat.params}
+        for name, b in module.named_buffers():
+            if name.endswith("position_encoding"):
+                continue  # deterministic (C-02)
+            dist.broadcast(b, src=src)
+        for p in module.parameters():
+            if p.data_ptr() not in flat_ptrs:
+                dist.broadcast(p.data, src=src)
+
+    def _reduce(self, lo: int, hi: int):
+        g = self.flat.grad[lo:hi]
+        if self.wire_dtype is not None and self.wire_dtype != g.dtype:
+            w = g.to(self.wire_dtype)
+            dist.all_reduce(w)
+            g.copy_(w)
+        else:
+            dist.all_reduce(g)
+
+    def ready(self, bucket: int):
+        """Launch one bucket's all-reduce (side stream when overlapping)."""
+        if not self.enabled or bucket in self._launched:
+            return
+        self._launched.add(bucket)
+        lo, hi = self.buckets[bucket]
+        if self._side is not None:
+            self._side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(self._side):
+                self._reduce(lo, hi)
+        else:
+            self._reduce(lo, hi)
+
+    def finish(self):
+        """All remaining buckets, then join the side stream."""
+        if not self.enabled:
+            return
+        for i in range(len(self.buckets)):
+            self.ready(i)
+        if self._side is not None:
+            torch.cuda.current_stream().wait_stream(self._side)
+        self._launched.clear()
+
+    def grad_scale(self) -> float:
+        return 1.0 / self.world

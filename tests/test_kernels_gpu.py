@@ -1,0 +1,224 @@
+"""Numerics of every HIP kernel against its plain-PyTorch fp32 emulation (ops/emulation.py).
+
+Each test feeds identical inputs to ``perceiver_io_amd._C`` and ``ops.emulation`` and
+compares with tolerances scaled to the output magnitude (bf16 operands, fp32 accumulate).
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _ext():
+    from perceiver_io_amd.ops import ext
+
+    return ext.require()
+
+
+def _emu():
+    from perceiver_io_amd.ops import emulation
+
+    return emulation
+
+
+def close(a, b, rel=2e-2, name=""):
+    a, b = a.float().cpu(), b.float().cpu()
+    assert a.shape == b.shape, (name, a.shape, b.shape)
+    fin = torch.isfinite(b)
+    assert torch.equal(torch.isfinite(a), fin), f"{name}: non-finite pattern differs"
+    a, b = a[fin], b[fin]
+    if b.numel() == 0:
+        return
+    scale = b.abs().max().item() + 1e-6
+    err = (a - b).abs().max().item()
+    assert err <= rel * scale, f"{name}: max err {err:.3e} vs scale {scale:.3e}"
+
+
+def bf(x):
+    return x.to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("R,Kin,N,xbf", [(200, 64, 192, False), (130, 131, 128, False), (64, 64, 64, True)])
+def test_ln_linear_fwd(R, Kin, N, xbf):
+    torch.manual_seed(0)
+    x = torch.randn(R, Kin, device=DEV) * 2 + 0.5
+    if xbf:
+        x = bf(x)
+    w = bf(torch.randn(N, Kin, device=DEV) / math.sqrt(Kin))
+    lw, lb = torch.randn(Kin, device=DEV), torch.randn(Kin, device=DEV)
+    b = torch.randn(N, device=DEV)
+    res = torch.randn(R, N, device=DEV)
+    for act, r, ob in ((0, None, True), (1, res, False)):
+        y1 = _ext().ln_linear_fwd(x, lw, lb, 1e-5, w, b, act, r, ob, True)
+        y2 = _emu().ln_linear_fwd(x, lw, lb, 1e-5, w, b, act, r, ob, True)
+        close(y1[0], y2[0], name="y")
+        close(y1[1], y2[1], 1e-4, "mean")
+        close(y1[2], y2[2], 1e-3, "rstd")
+
+
+def _attn_inputs(B, Bq, Nq, Nk, H, D, packed=True, mask=True):
+    E = H * D
+    q = bf(torch.randn(Bq, Nq, 3 * E if packed else E, device=DEV))
+    kv = bf(torch.randn(B, Nk, 2 * E, device=DEV))
+    qv = q[:, :, :E]
+    k, v = kv[:, :, :E], kv[:, :, E:]
+    km = None
+    if mask:
+        km = torch.rand(B, Nk, device=DEV) < 0.3
+        km[0] = True  # a fully padded batch row (defect D10: defined as zero output)
+    return qv, k, v, km
+
+
+@pytest.mark.parametrize("B,Bq,Nq,Nk,H,D,ns", [
+    (3, 3, 70, 100, 4, 16, 1),
+    (2, 1, 40, 300, 4, 16, 1),
+    (2, 2, 32, 1000, 4, 32, 4),
+    (2, 2, 96, 64, 2, 64, 1),
+    (2, 2, 33, 80, 1, 128, 2),
+])
+def test_attention_fwd_bwd(B, Bq, Nq, Nk, H, D, ns):
+    torch.manual_seed(1)
+    q, k, v, km = _attn_inputs(B, Bq, Nq, Nk, H, D)
+    scale = 1.0 / math.sqrt(D)
+    o1, l1 = _ext().attn_fwd(q, k, v, km, H, D, scale, 0.0, 0, ns)
+    o2, l2 = _emu().attn_fwd(q, k, v, km, H, D, scale, 0.0, 0, ns)
+    close(o1, o2, name="O")
+    close(l1, l2, 1e-3, "lse")
+    assert o1[0].abs().max().item() == 0.0  # fully masked rows → 0
+    do = bf(torch.randn(B, Nq, H * D, device=DEV))
+    g1 = _ext().attn_bwd(q, k, v, km, o1, do, l1, None, H, D, scale, 0.0, 0, None, None, None)
+    g2 = _emu().attn_bwd(q, k, v, km, o1, do, l1, None, H, D, scale, 0.0, 0, None, None, None)
+    for a, b, n in zip(g1, g2, ("dq", "dk", "dv")):
+        close(a, b, 3e-2, n)
+
+
+def test_attention_dropout_statistics():
+    torch.manual_seed(2)
+    B, Nq, Nk, H, D = 2, 64, 256, 4, 16
+    q, k, v, _ = _attn_inputs(B, B, Nq, Nk, H, D, mask=False)
+    v = torch.ones_like(v)
+    o, _ = _ext().attn_fwd(q, k, v, None, H, D, 0.25, 0.25, 123, 1)
+    # E[dropout(P)·1] = 1 per row; rows average close to 1
+    m = o.float().mean().item()
+    assert abs(m - 1.0) < 0.05, m
+    o2, _ = _ext().attn_fwd(q, k, v, None, H, D, 0.25, 0.25, 123, 1)
+    assert torch.equal(o, o2)  # deterministic for a given seed
+
+
+@pytest.mark.parametrize("C,H", [(64, 4), (128, 4), (32, 1)])
+def test_post_attn(C, H):
+    torch.manual_seed(3)
+    R = 150
+    o = bf(torch.randn(R, C, device=DEV))
+    x = torch.randn(R, C, device=DEV)
+    ws = [bf(torch.randn(C, C, device=DEV) / math.sqrt(C)) for _ in range(3)]
+    bo, b1, b2 = (torch.randn(C, device=DEV) * 0.1 for _ in range(3))
+    g2, be2 = torch.randn(C, device=DEV), torch.randn(C, device=DEV)
+    a = _ext().post_attn_fwd(o, x, ws[0], bo, g2, be2, 1e-5, ws[1], b1, ws[2], b2)
+    b = _emu().post_attn_fwd(o, x, ws[0], bo, g2, be2, 1e-5, ws[1], b1, ws[2], b2)
+    for t1, t2, n in zip(a, b, ("z", "y", "mean", "rstd", "u")):
+        close(t1, t2, 2e-2, n)
+    z, y, m, r, u = b
+    dz = torch.randn(R, C, device=DEV)
+    ga = _ext().post_attn_bwd(dz, y, m, r, u, o, ws[0], ws[1], ws[2], g2, H)
+    gb = _emu().post_attn_bwd(dz, y, m, r, u, o, ws[0], ws[1], ws[2], g2, H)
+    close(ga[0], gb[0], 3e-2, "dy")
+    close(ga[1], gb[1], 3e-2, "du")
+    close(ga[2], gb[2], 3e-2, "dO")
+    close(ga[3], gb[3], 3e-2, "delta")
+    close(ga[4].sum(0), gb[4].sum(0), 3e-2, "dgamma")
+    close(ga[5].sum(0), gb[5].sum(0), 3e-2, "dbeta")
+
+
+@pytest.mark.parametrize("R,N,Kin,gbf", [(300, 192, 64, False), (200, 128, 131, False), (129, 64, 64, True)])
+def test_dgrad_wgrad(R, N, Kin, gbf):
+    torch.manual_seed(4)
+    g = torch.randn(R, N, device=DEV)
+    if gbf:
+        g = bf(g)
+    w = bf(torch.randn(N, Kin, device=DEV) / math.sqrt(Kin))
+    x = torch.randn(R, Kin, device=DEV) * 1.5 + 0.2
+    lw, lb = torch.randn(Kin, device=DEV), torch.randn(Kin, device=DEV)
+    mean = x.mean(-1)
+    rstd = torch.rsqrt(x.var(-1, unbiased=False) + 1e-5)
+    dres = torch.randn(R, Kin, device=DEV)
+    a = _ext().ln_linear_dgrad(g, w, x, mean, rstd, lw, dres, True)
+    b = _emu().ln_linear_dgrad(g, w, x, mean, rstd, lw, dres, True)
+    close(a[0], b[0], 3e-2, "dx")
+    close(a[1].sum(0), b[1].sum(0), 3e-2, "dgamma")
+    close(a[2].sum(0), b[2].sum(0), 3e-2, "dbeta")
+    u = bf(torch.randn(R, Kin, device=DEV))
+    for mode, A in ((0, x), (1, x), (2, u)):
+        sa = _ext().wgrad(g, A, mode, mean, rstd, lw, lb, 4, True)
+        sb = _emu().wgrad(g, A, mode, mean, rstd, lw, lb, 4, True)
+        close(sa[0].sum(0), sb[0].sum(0), 3e-2, f"dW mode {mode}")
+        close(sa[1].sum(0), sb[1].sum(0), 1e-4, f"db mode {mode}")
+    slabs = [torch.randn(5, 7, 3, device=DEV), torch.randn(3, 11, device=DEV)]
+    dsts = [torch.ones(7, 3, device=DEV), torch.ones(11, device=DEV)]
+    _ext().slab_reduce(slabs, dsts, [True, False])
+    close(dsts[0], slabs[0].sum(0) + 1, 1e-5, "reduce acc")
+    close(dsts[1], slabs[1].sum(0), 1e-5, "reduce")
+
+
+@pytest.mark.parametrize("M,V,C", [(300, 1000, 64), (77, 10003, 64), (64, 257, 128)])
+def test_fused_cross_entropy(M, V, C):
+    torch.manual_seed(5)
+    h = bf(torch.randn(M, C, device=DEV))
+    w = bf(torch.randn(V, C, device=DEV) * 0.3)
+    bias = torch.randn(V, device=DEV) * 0.1
+    lab = torch.randint(0, V, (M,), device=DEV)
+    lab[::7] = -100
+    l1, s1 = _ext().ce_fwd(h, lab, w, bias)
+    l2, s2 = _emu().ce_fwd(h, lab, w, bias)
+    close(l1, l2, 1e-2, "loss")
+    close(s1, s2, 1e-3, "lse")
+    gs = torch.tensor([0.37], device=DEV)
+    outs = []
+    for K in (_ext(), _emu()):
+        dH = torch.zeros(M, C, device=DEV)
+        dW = torch.zeros(V, C, device=DEV)
+        db = torch.zeros(V, device=DEV)
+        K.ce_bwd(h, lab, w, bias, s2, gs, dH, dW, db, False)
+        outs.append((dH, dW, db))
+    for a, b, n in zip(outs[0], outs[1], ("dH", "dW", "db")):
+        close(a, b, 3e-2, n)
+
+
+def test_embed_mask_adamw():
+    torch.manual_seed(6)
+    B, L, V, C = 4, 50, 300, 64
+    ids = torch.randint(0, V, (B, L), device=DEV)
+    E, P = torch.randn(V, C, device=DEV), torch.randn(64, C, device=DEV)
+    close(_ext().embed_fwd(ids, E, P[:L].contiguous(), 8.0), _emu().embed_fwd(ids, E, P[:L].contiguous(), 8.0), 1e-6, "emb")
+    g = torch.randn(B, L, C, device=DEV)
+    r = []
+    for K in (_ext(), _emu()):
+        dE, dP = torch.zeros(V, C, device=DEV), torch.zeros(64, C, device=DEV)
+        K.embed_bwd(ids, g, dE, dP, 8.0)
+        r.append((dE, dP))
+    close(r[0][0], r[1][0], 1e-5, "dE")
+    close(r[0][1], r[1][1], 1e-5, "dP")
+    x = torch.randint(0, V, (B, L), device=DEV)
+    pad = torch.rand(B, L, device=DEV) < 0.2
+    u = torch.rand(3, B, L, device=DEV)
+    rid = torch.randint(3, V, (B, L), device=DEV)
+    a = _ext().text_mask(x, pad, u, rid, 1, 2, 0.15)
+    b = _emu().text_mask(x, pad, u, rid, 1, 2, 0.15)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    n = 10000
+    res = []
+    for K in (_ext(), _emu()):
+        torch.manual_seed(7)
+        p, gg = torch.randn(n, device=DEV), torch.randn(n, device=DEV)
+        m, v = torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+        sh = torch.zeros(n, device=DEV, dtype=torch.bfloat16)
+        hyper = torch.tensor([1e-3, 1.0, 0.0, 0.9, 0.999, 0, 0, 0], device=DEV)
+        K.sumsq(gg, hyper[2:3])
+        K.adamw(p, gg, m, v, sh, hyper, 1e-8, 0.01, 1.0, 1.0)
+        res.append((p, m, v, sh))
+    for a_, b_, nme in zip(res[0], res[1], ("p", "m", "v", "shadow")):
+        close(a_, b_, 1e-5, nme)

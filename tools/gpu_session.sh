@@ -1,0 +1,35 @@
+#!/bin/bash
+# Staged GPU session for gpurun: each GPU step has its own time limit; a step that faults,
+# aborts, segfaults or times out ends the session (exit codes 124/134/137/139 or >128).
+# Pytest failures (exit 1) are numerics findings and do not stop later steps.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+export TMPDIR=/tmp
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+mkdir -p gpurun_out
+run() {  # run <name> <timeout-s> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "=== $name ($(date +%T))" | tee -a gpurun_out/session.log
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a gpurun_out/session.log
+  tail -5 "gpurun_out/$name.log" | tee -a gpurun_out/session.log
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ] && [ $rc -ne 2 ] && [ $rc -ne 5 ]; then
+    echo "stopping session after $name (rc=$rc)" | tee -a gpurun_out/session.log
+    exit $rc
+  fi
+  return 0
+}
+for step in "$@"; do
+  case "$step" in
+    smoke)    run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    kernels)  run kernels 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    kernels_all) run kernels_all 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    ref)      run bench_ref 600 python bench.py --backend reference --steps 5 --warmup 2 ;;
+    ref32)    run bench_ref32 600 python bench.py --backend reference --dtype fp32 --steps 5 --warmup 2 ;;
+    eager)    run bench_eager 600 python bench.py --no-graph --steps 10 --warmup 3 ;;
+    bench)    run bench 600 python bench.py --steps 20 --warmup 5 ;;
+    prof)     run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 3 ;;
+    *) echo "unknown step $step" ;;
+  esac
+done
+echo "session done"
