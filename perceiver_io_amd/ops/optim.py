@@ -140,11 +140,11 @@ class FusedAdamW(torch.optim.Optimizer):
         """Write lr / step / betas for the NEXT update into device memory (outside any graph)."""
         g = self.param_groups[0]
         b1, b2 = g["betas"]
-        vals = [g["lr"], self._step + 1, 0.0, b1, b2]
+        vals = [g["lr"], self._step + 1, 0.0, b1, b2, 0.0, 0.0, 0.0]
         if self._ring is not None:
-            self._ring.push(vals, self.hyper[:5])
+            self._ring.push(vals, self.hyper)
         else:
-            self.hyper[:5] = torch.tensor(vals)
+            self.hyper.copy_(torch.tensor(vals))
 
     def device_update(self):
         """The capturable part: (grad-norm) + fused AdamW kernel over the flat buffers."""

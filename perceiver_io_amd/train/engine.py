@@ -75,6 +75,10 @@ class StepEngine:
         self._static_loss = None
         self._eager_steps = 0
         self._micro = 0
+        # every step (eager warmups, capture, replays) runs on ONE dedicated stream: autograd's
+        # AccumulateGrad nodes bind to the stream they were created on, and a capture whose
+        # accumulations land on another stream silently leaves them outside the graph
+        self.stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
         if self.fused and reducer is not None and reducer.enabled:
             optimizer.grad_scale = reducer.grad_scale()
         self.grad_scale_base = getattr(optimizer, "grad_scale", 1.0)
@@ -105,19 +109,15 @@ class StepEngine:
     def _capture(self, batch):
         opt = self.opt
         self._static_batch = _clone_to(batch, self.device)
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        # side-stream warmup (required before capture: allocator + lazy init)
-        with torch.cuda.stream(s):
-            for _ in range(2):
-                opt.flat.grad.zero_()
-                loss = self.loss_fn(self._static_batch)
-                loss.backward()
-        torch.cuda.current_stream().wait_stream(s)
+        # warmup on the capture stream (allocator + lazy init); no optimizer update → nothing to undo
+        for _ in range(2):
+            opt.flat.grad.zero_()
+            loss = self.loss_fn(self._static_batch)
+            loss.backward()
+            del loss
         opt.flat.grad.zero_()
-        # restore parameters touched by warmup? warmup has no optimizer update → nothing to undo
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, stream=self.stream):
             opt.flat.grad.zero_()
             loss = self.loss_fn(self._static_batch)
             loss.backward()
@@ -135,6 +135,16 @@ class StepEngine:
 
     def step(self, batch):
         """One optimizer step (``accumulate`` micro-batches must be passed as a list)."""
+        if self.stream is None:
+            return self._step(batch)
+        cur = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            out = self._step(batch)
+        cur.wait_stream(self.stream)
+        return out
+
+    def _step(self, batch):
         batches = batch if (self.accumulate > 1 and isinstance(batch, list)) else [batch]
         if self.graph_enabled and self.accumulate == 1:
             b = batches[0]

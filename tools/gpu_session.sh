@@ -19,6 +19,7 @@ run() {  # run <name> <timeout-s> <cmd...>
   fi
   return 0
 }
+run build 900 python -m perceiver_io_amd.csrc.build
 for step in "$@"; do
   case "$step" in
     smoke)    run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
@@ -29,6 +30,8 @@ for step in "$@"; do
     eager)    run bench_eager 600 python bench.py --no-graph --steps 10 --warmup 3 ;;
     bench)    run bench 600 python bench.py --steps 20 --warmup 5 ;;
     prof)     run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 3 ;;
+    dbg0)     run dbg0 300 env AMD_SERIALIZE_KERNEL=3 python tools/debug_engine.py 0 ;;
+    dbg1)     run dbg1 300 python tools/debug_engine.py 1 ;;
     *) echo "unknown step $step" ;;
   esac
 done
