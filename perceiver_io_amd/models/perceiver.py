@@ -65,6 +65,8 @@ class PerceiverEncoder(nn.Module):
 
     def layers(self):
         """The layer sequence actually executed (``layer_n`` repeated)."""
+        if self.num_layers <= 1:
+            return [self.layer_1]
         return [self.layer_1] + [self.layer_n] * (self.num_layers - 1)
 
     def forward(self, x, pad_mask=None, attn_mask=None):

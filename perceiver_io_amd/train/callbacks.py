@@ -80,9 +80,9 @@ class ModelCheckpoint(Callback):
 
     def _dir(self, trainer) -> str:
         if self.dirpath:
-            return self.dirpath
+            return os.path.abspath(self.dirpath)
         base = trainer.logger.log_dir if trainer.logger is not None else trainer.default_root_dir
-        return os.path.join(base, "checkpoints")
+        return os.path.abspath(os.path.join(base, "checkpoints"))
 
     def format_name(self, metrics: Dict[str, float], epoch: int, step: int) -> str:
         fn = self.filename or ("{epoch}-{step}" if self.monitor is None else "{epoch}-{step}")

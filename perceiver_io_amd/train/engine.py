@@ -103,7 +103,10 @@ class StepEngine:
             self.opt.step()
         if self.sched is not None:
             self.sched.step()
-        self.opt.zero_grad()
+        if self.reducer is not None:
+            self.reducer.flat.zero_grad()  # keep .grad as views of the flat buffer (never None)
+        else:
+            self.opt.zero_grad()
 
     # -- graph -----------------------------------------------------------------------------
     def _capture(self, batch):

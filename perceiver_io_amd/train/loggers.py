@@ -116,7 +116,7 @@ class TensorBoardLogger:
     def __init__(self, save_dir: str = "logs", name: Optional[str] = "default", version: Optional[Any] = None,
                  log_graph: bool = False, default_hp_metric: bool = True, prefix: str = "", sub_dir: Optional[str] = None,
                  **_):
-        self.save_dir = save_dir
+        self.save_dir = os.path.abspath(save_dir or ".")
         self.name = name or ""
         self._version = version
         self._writer = None

@@ -421,7 +421,10 @@ class Trainer:
         opt.step()
         for s in self.lr_schedulers:
             s.step()
-        opt.zero_grad()
+        if self._engine.reducer is not None:
+            self._engine.reducer.flat.zero_grad()
+        else:
+            opt.zero_grad()
         return loss.detach()
 
     @torch.no_grad()

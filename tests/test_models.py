@@ -1,0 +1,192 @@
+"""Model semantics on CPU: checkpoint key layout, adapters, masking, encoder
+weight sharing, MLM loss parity with the full-logits reference path, fused-executor parity
+through the kernel emulation."""
+import math
+
+import pytest
+import torch
+
+from perceiver_io_amd import ops
+from perceiver_io_amd.models import (ClassificationOutputAdapter, ImageInputAdapter, PerceiverDecoder, PerceiverEncoder,
+                                     PerceiverIO, PerceiverMLM, SemanticSegOutputAdapter, TextInputAdapter, TextMasking,
+                                     TextOutputAdapter)
+
+
+def mnist_model(latents=32, c=128, layers=3, sa=3):
+    enc = PerceiverEncoder(ImageInputAdapter((28, 28, 1), 32), (latents, c), layers, num_self_attention_layers_per_block=sa)
+    dec = PerceiverDecoder(ClassificationOutputAdapter(10, num_output_channels=c), (latents, c), num_cross_attention_heads=1)
+    return PerceiverIO(enc, dec)
+
+
+def mlm_model(v=300, L=64, n=16, c=64, layers=2, sa=2):
+    enc = PerceiverEncoder(TextInputAdapter(v, L, c), (n, c), layers, num_self_attention_layers_per_block=sa)
+    dec = PerceiverDecoder(TextOutputAdapter(v, L, c), (n, c))
+    return PerceiverMLM(enc, dec, TextMasking(v))
+
+
+def test_state_dict_layout_image():
+    keys = set(mnist_model().state_dict())
+    # separate q/k/v projection weights in the image encoder cross-attention (Cin != C)
+    assert "0.layer_1.0.0.module.attention.attention.q_proj_weight" in keys
+    assert "0.layer_1.0.0.module.attention.attention.k_proj_weight" in keys
+    assert "0.layer_1.0.0.module.attention.attention.in_proj_bias" in keys
+    assert "0.layer_1.0.0.module.q_norm.weight" in keys and "0.layer_1.0.0.module.kv_norm.bias" in keys
+    assert "0.layer_1.0.1.module.0.weight" in keys and "0.layer_1.0.1.module.3.bias" in keys
+    assert "0.layer_1.1.2.0.module.norm.weight" in keys
+    assert "0.layer_1.1.2.0.module.attention.attention.in_proj_weight" in keys
+    assert "0.layer_n.1.0.1.module.1.weight" in keys
+    assert "0.input_adapter.position_encoding" in keys and "0.latent" in keys
+    assert "1.output" in keys and "1.output_adapter.linear.weight" in keys
+    assert "1.cross_attention.0.module.attention.attention.in_proj_weight" in keys
+    assert "1.cross_attention.1.module.3.weight" in keys
+    assert not any("in_proj_weight" in k and "layer_1.0.0" in k for k in keys)
+
+
+def test_state_dict_layout_mlm_and_aliases():
+    m = mlm_model()
+    keys = set(m.state_dict())
+    assert "encoder.input_adapter.text_embedding.weight" in keys
+    assert "encoder.input_adapter.pos_encoding" in keys
+    assert "encoder.layer_1.0.0.module.attention.attention.in_proj_weight" in keys
+    assert "decoder.output_adapter.linear.bias" in keys
+    io = PerceiverIO(m.encoder, m.decoder)
+    assert io.encoder is io[0] and io.decoder is io[1]  # defect D3
+    assert set(io.state_dict()) == {k.replace("encoder.", "0.", 1).replace("decoder.", "1.", 1) for k in keys}
+
+
+def test_param_counts_match_survey():
+    # SURVEY §6.3 parameter counts (MNIST 32x128: 904,086; MLM 64x64 vocab 10003 L 512: 1,738,643)
+    assert sum(p.numel() for p in mnist_model().parameters()) == 904_086
+    m = mlm_model(v=10003, L=512, n=64, c=64, layers=3, sa=6)
+    assert sum(p.numel() for p in m.parameters()) == 1_738_643
+
+
+def test_fourier_encoding_layout():
+    ad = ImageInputAdapter((28, 28, 1), 32)
+    assert ad.num_input_channels == 1 + 2 * (2 * 32 + 1)
+    pe = ad.position_encoding
+    assert pe.shape == (784, 130)
+    # positions first (row-major ij grid in [-1, 1]); then sin for dim0 bands, sin dim1, cos dim0, cos dim1
+    assert torch.allclose(pe[0, :2], torch.tensor([-1.0, -1.0]))
+    assert torch.allclose(pe[27, :2], torch.tensor([-1.0, 1.0]))
+    f0 = torch.linspace(1.0, 14.0, 32)
+    p = pe[5, 0]
+    assert torch.allclose(pe[5, 2:34], torch.sin(math.pi * p * f0), atol=1e-5)
+    assert torch.allclose(pe[5, 66:98], torch.cos(math.pi * p * f0), atol=1e-5)
+    x = torch.randn(2, 28, 28, 1)
+    y = ad(x)
+    assert y.shape == (2, 784, 131) and torch.equal(y[:, :, 0], x.reshape(2, -1))
+    with pytest.raises(ValueError):
+        ad(torch.randn(2, 27, 28, 1))
+
+
+def test_text_adapter_and_masking_semantics():
+    torch.manual_seed(0)
+    ad = TextInputAdapter(100, 16, 8)
+    ids = torch.randint(0, 100, (3, 10))
+    y = ad(ids)
+    assert torch.allclose(y, ad.text_embedding.weight[ids] * math.sqrt(8) + ad.pos_encoding[:10])
+    mk = TextMasking(1000)
+    x = torch.randint(3, 1000, (64, 512))
+    x[:, -50:] = 0
+    x[:, :5] = 1  # UNK never selected
+    pad = x == 0
+    x0 = x.clone()
+    xm, lab = mk(x, pad)
+    assert torch.equal(x, x0)  # out of place (defect D4)
+    sel = lab != -100
+    assert not sel[pad].any() and not sel[:, :5].any()
+    frac = sel.float().sum() / (~pad & (x != 1)).float().sum()
+    assert abs(frac.item() - 0.15) < 0.01
+    masked = (xm == 2) & sel
+    assert abs(masked.float().sum().item() / sel.float().sum().item() - 0.8) < 0.03
+    assert torch.equal(lab[sel], x[sel]) and torch.equal(xm[~sel], x[~sel])
+    rnd = sel & (xm != 2) & (xm != x)
+    assert rnd.any() and (xm[rnd] >= 3).all()
+
+
+def test_encoder_weight_sharing():
+    enc = PerceiverEncoder(TextInputAdapter(50, 16, 32), (8, 32), 4, num_self_attention_layers_per_block=1)
+    layers = enc.layers()
+    assert len(layers) == 4 and layers[1] is layers[2] is layers[3] is enc.layer_n
+
+
+def test_decoder_latent_shape_check():
+    dec = PerceiverDecoder(ClassificationOutputAdapter(5, num_output_channels=16), (8, 16))
+    with pytest.raises(ValueError):
+        dec(torch.randn(2, 7, 16))
+    assert dec(torch.randn(2, 8, 16)).shape == (2, 5)
+
+
+def test_semantic_seg_adapter_identity():
+    ad = SemanticSegOutputAdapter(3, num_outputs=4, num_output_channels=8)
+    x = torch.randn(2, 4, 8)
+    assert ad(x) is x
+
+
+def test_all_masked_rows_are_zero_not_nan():
+    q = torch.randn(2, 4, 16)
+    k = torch.randn(2, 6, 16)
+    pad = torch.zeros(2, 6, dtype=torch.bool)
+    pad[0] = True
+    o = ops.attention.mha_core(q, k, k, 4, key_padding_mask=pad)
+    assert torch.isfinite(o).all() and o[0].abs().max() == 0
+
+
+def test_mlm_loss_matches_full_logit_reference():
+    torch.manual_seed(1)
+    m = mlm_model()
+    x = torch.randint(3, 300, (4, 64))
+    pad = torch.zeros(4, 64, dtype=torch.bool)
+    pad[1, 40:] = True
+    xm, lab = m.masking(x, pad)
+    fast = m.loss(x, pad, labels=lab, x_masked=xm)
+    with ops.backend("reference"):
+        ref = m.loss(x, pad, labels=lab, x_masked=xm)
+        logits, _ = m(xm, pad, masking=False)
+    full = torch.nn.functional.cross_entropy(logits.transpose(1, 2), lab, ignore_index=-100)
+    assert torch.allclose(fast, ref, atol=1e-5) and torch.allclose(fast, full, atol=1e-5)
+
+
+def test_reference_backend_matches_nn_multihead_attention():
+    torch.manual_seed(2)
+    from perceiver_io_amd.models.blocks import MultiHeadAttention
+
+    mha = MultiHeadAttention(32, 48, 4, 0.0)
+    ref = torch.nn.MultiheadAttention(32, 4, kdim=48, vdim=48, batch_first=True)
+    ref.load_state_dict(mha.attention.state_dict())
+    q, kv = torch.randn(2, 5, 32), torch.randn(2, 7, 48)
+    pad = torch.zeros(2, 7, dtype=torch.bool)
+    pad[1, 4:] = True
+    want = ref(q, kv, kv, key_padding_mask=pad)[0]
+    assert torch.allclose(mha(q, kv, pad), want, atol=1e-5)
+    with ops.backend("reference"):
+        assert torch.allclose(mha(q, kv, pad), want, atol=1e-6)
+
+
+@pytest.mark.parametrize("kind", ["mlm", "image"])
+def test_fused_executor_matches_eager_via_emulation(kind):
+    torch.manual_seed(3)
+    if kind == "mlm":
+        m = mlm_model()
+        x = torch.randint(3, 300, (3, 64))
+        pad = torch.zeros(3, 64, dtype=torch.bool)
+        pad[2, 30:] = True
+        enc = m.encoder
+    else:
+        m = mnist_model(latents=16, c=64, layers=2, sa=1)
+        x = torch.randn(2, 28, 28, 1)
+        pad = None
+        enc = m.encoder
+    ref = enc(x, pad)[0]
+    fused = ops.fused.encoder_forward(enc, x, pad)
+    w = torch.randn_like(ref)
+    (ref * w).sum().backward()
+    g_ref = {n: p.grad.clone() for n, p in enc.named_parameters() if p.grad is not None}
+    enc.zero_grad()
+    (fused * w).sum().backward()
+    assert (fused - ref).abs().max() < 0.03 * ref.abs().max()
+    gmax = max(g.abs().max() for g in g_ref.values())
+    for n, p in enc.named_parameters():
+        if n in g_ref:
+            assert (p.grad - g_ref[n]).abs().max() < 0.03 * gmax, n

@@ -1,0 +1,150 @@
+"""Training stack on CPU: CLI parsing + links, Trainer fit/validate/test on synthetic data
+(BASELINE config 1: MNIST img_clf, 32×128 latents, batch 8), Lightning-layout checkpoints,
+MLM → text-classifier transfer with a frozen encoder, fused optimizer, loggers."""
+import json
+import os
+import struct
+
+import pytest
+import torch
+
+from perceiver_io_amd.cli.tasks import main as cli_main
+from perceiver_io_amd.train.checkpoint import load_checkpoint
+
+PL_KEYS = {"epoch", "global_step", "pytorch-lightning_version", "state_dict", "callbacks", "optimizer_states",
+           "lr_schedulers", "hparams_name", "hyper_parameters"}
+
+
+def run_cli(task, tmp_path, *flags):
+    old = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        return cli_main(task, list(flags))
+    finally:
+        os.chdir(old)
+
+
+def test_cli_parse_links_and_defaults(tmp_path):
+    from perceiver_io_amd.cli.tasks import task_cli
+    from perceiver_io_amd.tasks import LitMaskedLanguageModel
+
+    cls = task_cli("mlm")
+    cli = cls.__new__(cls)
+    from perceiver_io_amd.cli import CLIParser
+
+    cli.parser = CLIParser()
+    cli.add_default_arguments_to_parser(cli.parser)
+    cli.add_arguments_to_parser(cli.parser)
+    sub, cfg = cli.parse(["fit", "--model.dropout=0.0", "--data=IMDBDataModule", "--data.max_seq_len=512",
+                          "--data.batch_size=64", "--optimizer.lr=0.003", "--optimizer.weight_decay=0.0",
+                          "--lr_scheduler.pct_start=0.1", "--trainer.accelerator=gpu", "--trainer.devices=-1",
+                          "--trainer.max_steps=50000",
+                          "--model.masked_samples=['i have watched this <MASK> and it was awesome']"])
+    assert sub == "fit"
+    assert cfg["data"]["class"] == "IMDBDataModule" and cfg["data"]["max_seq_len"] == 512
+    assert cfg["lr_scheduler"]["total_steps"] == 50000 and cfg["lr_scheduler"]["max_lr"] == 0.003
+    assert cfg["lr_scheduler"]["cycle_momentum"] is False and cfg["lr_scheduler"]["pct_start"] == 0.1
+    assert cfg["logger"]["name"] == "mlm" and cfg["logger"]["save_dir"] == "logs"
+    assert cfg["model"]["masked_samples"] == ["i have watched this <MASK> and it was awesome"]
+    assert cfg["trainer"]["devices"] == -1 and cfg["optimizer"]["weight_decay"] == 0.0
+    assert LitMaskedLanguageModel  # import ok
+
+
+def test_img_clf_fit_batch8_cpu_writes_loadable_checkpoint(tmp_path):
+    """BASELINE config 1 plumbing: MNIST img_clf, latent 32×128, batch 8 on CPU."""
+    cli = run_cli("img_clf", tmp_path, "fit", "--data=MNISTDataModule", "--data.synthetic=true",
+                  "--data.synthetic_size=96", "--data.batch_size=8", "--data.num_workers=0", "--data.val_split=16",
+                  "--optimizer.lr=0.001", "--optimizer.weight_decay=0.01", "--trainer.max_epochs=1",
+                  "--trainer.limit_train_batches=3", "--trainer.limit_val_batches=2", "--trainer.log_every_n_steps=1",
+                  "--model.num_encoder_layers=2", "--model.num_encoder_self_attention_layers_per_block=1")
+    tr = cli.trainer
+    assert tr.global_step == 3
+    ck = [c for c in tr.callbacks if type(c).__name__ == "ModelCheckpoint"][0]
+    assert ck.best_model_path and os.path.exists(ck.best_model_path)
+    assert os.path.basename(ck.best_model_path).startswith("epoch=000-val_loss=")
+    ckpt = load_checkpoint(ck.best_model_path)
+    assert PL_KEYS <= set(ckpt)
+    assert ckpt["hyper_parameters"]["num_latents"] == 32 and ckpt["hyper_parameters"]["image_shape"] == [28, 28, 1]
+    from perceiver_io_amd.tasks import LitImageClassifier
+
+    m = LitImageClassifier.load_from_checkpoint(ck.best_model_path)
+    sd = cli.model.state_dict()
+    assert all(torch.equal(v.cpu(), sd[k].cpu()) for k, v in m.state_dict().items())
+    logdir = tr.logger.log_dir
+    assert os.path.exists(os.path.join(logdir, "config.yaml"))
+    recs = [json.loads(l) for l in open(os.path.join(logdir, "metrics.jsonl"))]
+    assert any("train_loss" in r for r in recs) and any("val_loss" in r for r in recs)
+    assert any(k.startswith("lr-") for r in recs for k in r)
+    ev = [f for f in os.listdir(logdir) if f.startswith("events.out.tfevents")]
+    assert ev and _tfrecords_valid(os.path.join(logdir, ev[0]))
+
+
+def _tfrecords_valid(path):
+    from perceiver_io_amd.train.loggers import _crc32c, _masked
+
+    data = open(path, "rb").read()
+    i, n = 0, 0
+    while i < len(data):
+        (ln,) = struct.unpack("<Q", data[i:i + 8])
+        (hc,) = struct.unpack("<I", data[i + 8:i + 12])
+        if _masked(_crc32c(data[i:i + 8])) != hc:
+            return False
+        body = data[i + 12:i + 12 + ln]
+        (bc,) = struct.unpack("<I", data[i + 12 + ln:i + 16 + ln])
+        if _masked(_crc32c(body)) != bc:
+            return False
+        i += 16 + ln
+        n += 1
+    return n > 1
+
+
+def test_mlm_then_frozen_seq_clf_transfer_and_resume(tmp_path):
+    common = ["--data=IMDBDataModule", "--data.synthetic=true", "--data.synthetic_size=48", "--data.vocab_size=400",
+              "--data.max_seq_len=48", "--data.batch_size=8", "--data.num_workers=0", "--data.data_dir=" + str(tmp_path / "cache"),
+              "--model.num_latents=16", "--model.num_encoder_layers=2",
+              "--model.num_encoder_self_attention_layers_per_block=1", "--trainer.limit_val_batches=1"]
+    mlm = run_cli("mlm", tmp_path, "fit", *common, "--optimizer.lr=0.003", "--trainer.max_epochs=1",
+                  "--trainer.max_steps=4", "--trainer.val_check_interval=2",
+                  "--model.masked_samples=['w17 w18 <MASK> w19']", "--model.num_predictions=2")
+    ck = [c for c in mlm.trainer.callbacks if type(c).__name__ == "ModelCheckpoint"][0]
+    assert os.path.exists(ck.best_model_path)
+    texts = os.path.join(mlm.trainer.logger.log_dir, "text.jsonl")
+    assert os.path.exists(texts)  # sample predictions logged after validation
+    clf = run_cli("seq_clf", tmp_path, "fit", *common, f"--model.mlm_ckpt={ck.best_model_path}",
+                  "--model.freeze_encoder=true", "--trainer.max_epochs=1", "--trainer.limit_train_batches=2")
+    enc_ref = mlm.model.model.encoder.state_dict()
+    enc_clf = clf.model.model.encoder.state_dict()
+    assert all(torch.equal(enc_ref[k].cpu(), enc_clf[k].cpu()) for k in enc_ref)  # frozen + transferred
+    assert not any(p.requires_grad for p in clf.model.model.encoder.parameters())
+    ck2 = [c for c in clf.trainer.callbacks if type(c).__name__ == "ModelCheckpoint"][0]
+    # resume: continues from the stored global step
+    res = run_cli("seq_clf", tmp_path, "fit", *common, f"--trainer.resume_from_checkpoint={ck2.best_model_path}",
+                  "--trainer.max_epochs=2", "--trainer.limit_train_batches=2")
+    assert res.trainer.global_step == clf.trainer.global_step + 2
+
+
+def test_fused_adamw_matches_torch_adamw():
+    from perceiver_io_amd.ops.optim import FusedAdamW
+
+    torch.manual_seed(0)
+    a = torch.nn.Linear(7, 5)
+    b = torch.nn.Linear(7, 5)
+    b.load_state_dict(a.state_dict())
+    oa = torch.optim.AdamW(a.parameters(), lr=1e-2, weight_decay=0.1)
+    ob = FusedAdamW(b.parameters(), lr=1e-2, weight_decay=0.1)
+    sa = torch.optim.lr_scheduler.OneCycleLR(oa, max_lr=1e-2, total_steps=10, cycle_momentum=False)
+    sb = torch.optim.lr_scheduler.OneCycleLR(ob, max_lr=1e-2, total_steps=10, cycle_momentum=False)
+    for _ in range(5):
+        x = torch.randn(3, 7)
+        for m, o, s in ((a, oa, sa), (b, ob, sb)):
+            o.zero_grad()
+            m(x).pow(2).sum().backward()
+            o.step()
+            s.step()
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        assert torch.allclose(pa, pb, atol=1e-6)
+    sd = ob.state_dict()
+    assert set(sd["state"][0]) == {"step", "exp_avg", "exp_avg_sq"}
+    ob2 = FusedAdamW(torch.nn.Linear(7, 5).parameters(), lr=1.0)
+    ob2.load_state_dict(sd)
+    assert ob2._step == 5 and torch.allclose(ob2.exp_avg, ob.exp_avg)
