@@ -267,7 +267,8 @@ __global__ void attn_bwd_prep_kernel(const uint16_t* __restrict__ dO, const uint
     acc = wave_sum(acc);
     if (l == 0) delta[(long long)row * H + h] = acc;
   }
-  for (int j = l; j < HD; j += 64) dq[(long long)row * dq_rs + j] = 0.f;
+  if (dq)
+    for (int j = l; j < HD; j += 64) dq[(long long)row * dq_rs + j] = 0.f;
 }
 
 template <int D>
@@ -469,12 +470,13 @@ void attn_fwd_launch(const AttnArgs& a, int D, uint16_t* O, float* LSE, float* O
 
 void attn_bwd_launch(const AttnArgs& a, int D, const uint16_t* O, const uint16_t* dO, const float* LSE, float* delta,
                      float* dq, long long dq_bs, int dq_rs, float* dk, long long dk_bs, int dk_rs, float* dv,
-                     long long dv_bs, int dv_rs, bool dq_is_dense, hipStream_t st) {
-  // prep: delta and zero dQ (dQ buffer is (B, Nq, dq_rs) with dq_bs == Nq * dq_rs when dense)
+                     long long dv_bs, int dv_rs, bool compute_delta, hipStream_t st) {
+  // dQ must arrive zero-filled (it is accumulated with atomics).  delta = rowsum(dO∘O) is
+  // normally produced by the post-attention backward kernel; compute it here otherwise.
   const int rows = a.B * a.Nq;
-  hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, dO, O, delta, dq, rows, a.H, D,
-                     dq_rs);
-  (void)dq_is_dense;
+  if (compute_delta)
+    hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, dO, O, delta, (float*)nullptr,
+                       rows, a.H, D, dq_rs);
   dim3 grid((a.Nk + 127) / 128, a.H, a.B);
   switch (D) {
     case 16: hipLaunchKernelGGL(attn_bwd_kernel<16>, grid, dim3(256), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs); break;

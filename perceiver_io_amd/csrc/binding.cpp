@@ -134,24 +134,32 @@ std::vector<Tensor> attn_fwd(Tensor q, Tensor k, Tensor v, OptT kmask, int64_t H
 
 // returns (dq, dk, dv) fp32; dq is per batch even when q is batch-broadcast.  Optional
 // *_out tensors (B, N, >=HD views, unit inner stride) let the results land in packed buffers;
-// a dq_out view must be batch-dense (batch stride == Nq * row stride).
+// a dq_out view must be batch-dense (batch stride == Nq * row stride) and ZERO-FILLED (dQ is
+// accumulated with atomics).  delta_in ((B, Nq, H) fp32 rowsum(dO∘O), e.g. from post_attn_bwd)
+// skips the delta pass.
 std::vector<Tensor> attn_bwd(Tensor q, Tensor k, Tensor v, OptT kmask, Tensor o, Tensor dO, Tensor lse, OptT delta_in,
                              int64_t H, int64_t D, double scale, double dropout_p, int64_t seed, OptT dq_out,
                              OptT dk_out, OptT dv_out) {
   auto a = make_args(q, k, v, kmask, (int)H, (int)D, scale, dropout_p, seed);
   TORCH_CHECK(dO.is_contiguous() && o.is_contiguous(), "O / dO must be contiguous (B, Nq, H*D)");
   auto f32 = q.options().dtype(torch::kFloat32);
-  Tensor dq = dq_out.has_value() ? *dq_out : torch::empty({a.B, a.Nq, H * D}, f32);
+  Tensor dq = dq_out.has_value() ? *dq_out : torch::zeros({a.B, a.Nq, H * D}, f32);
   Tensor dk = dk_out.has_value() ? *dk_out : torch::empty({a.B, a.Nk, H * D}, f32);
   Tensor dv = dv_out.has_value() ? *dv_out : torch::empty({a.B, a.Nk, H * D}, f32);
   TORCH_CHECK(dq.stride(2) == 1 && dk.stride(2) == 1 && dv.stride(2) == 1, "dq/dk/dv need unit inner stride");
   TORCH_CHECK(dq.size(0) == a.B && dq.stride(0) == a.Nq * dq.stride(1), "dq must be batch-dense");
   CHECK_DT(dq, torch::kFloat32); CHECK_DT(dk, torch::kFloat32); CHECK_DT(dv, torch::kFloat32);
-  Tensor delta = torch::empty({a.B, a.Nq, H}, f32);
-  (void)delta_in;
+  Tensor delta;
+  if (delta_in.has_value()) {
+    delta = *delta_in;
+    TORCH_CHECK(delta.is_contiguous() && delta.numel() == (int64_t)a.B * a.Nq * H, "delta must be (B, Nq, H)");
+    CHECK_DT(delta, torch::kFloat32);
+  } else {
+    delta = torch::empty({a.B, a.Nq, H}, f32);
+  }
   pio::attn_bwd_launch(a, (int)D, bfp(o), bfp(dO), f32p(lse), delta.data_ptr<float>(), dq.data_ptr<float>(),
                        dq.stride(0), (int)dq.stride(1), dk.data_ptr<float>(), dk.stride(0), (int)dk.stride(1),
-                       dv.data_ptr<float>(), dv.stride(0), (int)dv.stride(1), true, stream());
+                       dv.data_ptr<float>(), dv.stride(0), (int)dv.stride(1), !delta_in.has_value(), stream());
   return {dq, dk, dv};
 }
 
@@ -195,36 +203,39 @@ std::vector<Tensor> post_attn_fwd(Tensor o, Tensor x, Tensor wo, Tensor bo, Tens
   return {z, y, m, r, u};
 }
 
+// the three backward entry points below ACCUMULATE parameter gradients into caller-provided fp32
+// tensors (normally views of the flat gradient buffer) with device atomics: no partial slabs,
+// no reduction pass, no autograd AccumulateGrad adds
 std::vector<Tensor> post_attn_bwd(Tensor dz, Tensor y, Tensor m2, Tensor r2, Tensor u, Tensor o, Tensor wo, Tensor w1,
-                                  Tensor w2, Tensor g2, int64_t H) {
+                                  Tensor w2, Tensor g2, int64_t H, Tensor dg2, Tensor db2) {
   TORCH_CHECK(dz.is_contiguous(), "dz must be contiguous");
   const int R = (int)dz.size(0), C = (int)dz.size(1);
+  TORCH_CHECK(dg2.is_contiguous() && db2.is_contiguous() && dg2.numel() == C && db2.numel() == C, "bad LN2 grad targets");
   auto f32 = dz.options().dtype(torch::kFloat32);
-  const int nblk = (R + 63) / 64;
   Tensor dy = torch::empty({R, C}, f32);
   Tensor du = torch::empty({R, C}, dz.options().dtype(torch::kBFloat16));
   Tensor dO = torch::empty({R, C}, dz.options().dtype(torch::kBFloat16));
   Tensor delta = torch::empty({R, H}, f32);
-  Tensor sg = torch::empty({nblk, C}, f32), sb = torch::empty({nblk, C}, f32);
   pio::post_attn_bwd_launch(C, f32p(dz), f32p(y), f32p(m2), f32p(r2), bfp(u), bfp(o), bfp(wo), bfp(w1), bfp(w2),
                             f32p(g2), dy.data_ptr<float>(), bfp_mut(du), bfp_mut(dO), delta.data_ptr<float>(), (int)H,
-                            sg.data_ptr<float>(), sb.data_ptr<float>(), R, stream());
-  return {dy, du, dO, delta, sg, sb};
+                            dg2.data_ptr<float>(), db2.data_ptr<float>(), R, stream());
+  return {dy, du, dO, delta};
 }
 
-std::vector<Tensor> ln_linear_dgrad(Tensor g, Tensor w, OptT x, OptT mean, OptT rstd, OptT lnw, OptT dres, bool need_dx) {
+OptT ln_linear_dgrad(Tensor g, Tensor w, OptT x, OptT mean, OptT rstd, OptT lnw, OptT dres, bool need_dx, OptT dg,
+                     OptT db) {
   TORCH_CHECK(g.dim() == 2 && g.stride(1) == 1, "g must be 2-D rows");
   const int R = (int)g.size(0), N = (int)g.size(1), Kin = (int)w.size(1);
   TORCH_CHECK(w.size(0) == N, "w rows must match g columns");
   TORCH_CHECK(Kin <= 160, "dgrad supports Kin <= 160");
   auto f32 = g.options().dtype(torch::kFloat32);
-  Tensor dx, sg, sb;
+  Tensor dx;
   float *dxp = nullptr, *sgp = nullptr, *sbp = nullptr;
   if (need_dx) { dx = torch::empty({R, Kin}, f32); dxp = dx.data_ptr<float>(); }
-  const int nblk = (R + 63) / 64;
   if (lnw.has_value()) {
-    sg = torch::empty({nblk, Kin}, f32); sb = torch::empty({nblk, Kin}, f32);
-    sgp = sg.data_ptr<float>(); sbp = sb.data_ptr<float>();
+    TORCH_CHECK(dg.has_value() && db.has_value() && dg->numel() == Kin && db->numel() == Kin && dg->is_contiguous() &&
+                db->is_contiguous(), "LN grad targets required");
+    sgp = dg->data_ptr<float>(); sbp = db->data_ptr<float>();
   }
   const void* xp = nullptr; bool xb = false; int xrs = 0;
   if (x.has_value()) { xp = x->data_ptr(); xb = is_bf16(*x); xrs = (int)x->stride(0); }
@@ -232,24 +243,22 @@ std::vector<Tensor> ln_linear_dgrad(Tensor g, Tensor w, OptT x, OptT mean, OptT 
   if (dres.has_value()) { dr = f32p(*dres); drs = (int)dres->stride(0); }
   pio::ln_linear_dgrad_launch(g.data_ptr(), is_bf16(g), (int)g.stride(0), N, bfp(w), Kin, xp, xb, xrs, f32o(mean),
                               f32o(rstd), f32o(lnw), dr, drs, dxp, Kin, sgp, sbp, R, stream());
-  return {dx, sg, sb};
+  if (need_dx) return dx;
+  return c10::nullopt;
 }
 
-std::vector<Tensor> wgrad(Tensor g, Tensor a, int64_t amode, OptT mean, OptT rstd, OptT lnw, OptT lnb, int64_t nsplit,
-                          bool with_bias) {
+void wgrad(Tensor g, Tensor a, int64_t amode, OptT mean, OptT rstd, OptT lnw, OptT lnb, int64_t rows_per_wg, Tensor dW,
+           OptT db) {
   TORCH_CHECK(g.dim() == 2 && a.dim() == 2 && g.stride(1) == 1 && a.stride(1) == 1, "2-D row tensors expected");
   const int R = (int)g.size(0), N = (int)g.size(1), Kin = (int)a.size(1);
   TORCH_CHECK(a.size(0) == R, "row mismatch");
   TORCH_CHECK(Kin <= 160, "wgrad supports Kin <= 160");
-  auto f32 = g.options().dtype(torch::kFloat32);
-  Tensor sw = torch::empty({nsplit, N, Kin}, f32);
-  Tensor sb;
-  float* sbp = nullptr;
-  if (with_bias) { sb = torch::empty({nsplit, N}, f32); sbp = sb.data_ptr<float>(); }
+  TORCH_CHECK(dW.is_contiguous() && dW.numel() == (int64_t)N * Kin, "dW must be a contiguous (N, Kin) fp32 target");
+  float* dbp = nullptr;
+  if (db.has_value()) { TORCH_CHECK(db->is_contiguous() && db->numel() == N); dbp = db->data_ptr<float>(); }
   pio::wgrad_launch(g.data_ptr(), is_bf16(g), (int)g.stride(0), N, a.data_ptr(), is_bf16(a), (int)a.stride(0), Kin,
-                    (int)amode, f32o(mean), f32o(rstd), f32o(lnw), f32o(lnb), R, (int)nsplit, sw.data_ptr<float>(), sbp,
-                    stream());
-  return {sw, sb};
+                    (int)amode, f32o(mean), f32o(rstd), f32o(lnw), f32o(lnb), R, (int)rows_per_wg,
+                    dW.data_ptr<float>(), dbp, stream());
 }
 
 // jobs: list of (slab [S, ...], dst (numel = slab[0].numel()), accumulate)

@@ -64,9 +64,39 @@ __device__ __forceinline__ void for_acc(int BM, int BN, F&& f) {
 
 // stage rows [r0, r0+rows) × cols [c0, c0+cols) of a row-major matrix into an LDS bf16
 // tile [rows][ld] (zero outside the matrix).
+__device__ __forceinline__ bf16x8 load8(const uint16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
+__device__ __forceinline__ bf16x8 load8(const float* p) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  bf16x8 r;
+  r[0] = (short)f2bf(a.x); r[1] = (short)f2bf(a.y); r[2] = (short)f2bf(a.z); r[3] = (short)f2bf(a.w);
+  r[4] = (short)f2bf(b.x); r[5] = (short)f2bf(b.y); r[6] = (short)f2bf(b.z); r[7] = (short)f2bf(b.w);
+  return r;
+}
+
 template <typename T>
 __device__ __forceinline__ void stage(uint16_t* s, int ld, const T* g, long long g_rs, int r0, int R, int c0, int Cmax,
                                       int rows, int cols) {
+  // 16-byte path (8 elements per access) when the layout allows it, scalar otherwise
+  if ((cols & 7) == 0 && (ld & 7) == 0 && (g_rs & 7) == 0 && (c0 & 7) == 0 &&
+      (reinterpret_cast<uintptr_t>(g) & 15) == 0) {
+    const int cpr = cols >> 3;
+    for (int e = threadIdx.x; e < rows * cpr; e += blockDim.x) {
+      const int rr = e / cpr, cc = (e % cpr) * 8;
+      const int gr = r0 + rr, gc = c0 + cc;
+      bf16x8 v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (gr < R) {
+        const T* p = g + (long long)gr * g_rs + gc;
+        if (gc + 8 <= Cmax) {
+          v = load8(p);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = gc + j < Cmax ? (short)f2bf(ldf(p + j)) : (short)0;
+        }
+      }
+      *reinterpret_cast<bf16x8*>(s + rr * ld + cc) = v;
+    }
+    return;
+  }
   for (int e = threadIdx.x; e < rows * cols; e += blockDim.x) {
     const int rr = e / cols, cc = e % cols;
     const int gr = r0 + rr, gc = c0 + cc;
@@ -93,49 +123,60 @@ __global__ __launch_bounds__(256) void ln_linear_fwd_kernel(const TIn* __restric
   const int KP = round_up(Kin, 16), ld = KP + 8;
   uint16_t* sA = smem;
   uint16_t* sB = smem + 64 * ld;
-  const int m0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
+  const int m0 = blockIdx.x * 64;
   const int w = wave_id(), l = lane_id();
 
-  stage(sB, ld, W, Kin, n0, N, 0, Kin, 64, KP);
-  // LN prologue: one wave per row
+  // LN prologue once per 64-row tile (one wave per row, x row cached in registers), then all
+  // N columns of the output are produced 64 at a time against the resident normalised tile
+  float gw[4], gb[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k = l + 64 * j;
+    gw[j] = (lnw && k < Kin) ? lnw[k] : 1.f;
+    gb[j] = (lnw && k < Kin) ? lnb[k] : 0.f;
+  }
   for (int rr = w; rr < 64; rr += 4) {
     const int gr = m0 + rr;
+    float xv[4] = {0.f, 0.f, 0.f, 0.f};
     if (gr < R) {
       const TIn* xr = X + (long long)gr * x_rs;
-      float mean = 0.f, rstd = 1.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (l + 64 * j < Kin) xv[j] = ldf(xr + l + 64 * j);
       if (lnw) {
-        float s = 0.f;
-        for (int k = l; k < Kin; k += 64) s += ldf(xr + k);
-        mean = wave_sum(s) / Kin;
+        const float mean = wave_sum(xv[0] + xv[1] + xv[2] + xv[3]) / Kin;
         float v = 0.f;
-        for (int k = l; k < Kin; k += 64) { const float d = ldf(xr + k) - mean; v += d * d; }
-        rstd = rsqrtf(wave_sum(v) / Kin + eps);
-        if (blockIdx.y == 0 && l == 0 && mean_out) { mean_out[gr] = mean; rstd_out[gr] = rstd; }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (l + 64 * j < Kin) v += (xv[j] - mean) * (xv[j] - mean);
+        const float rstd = rsqrtf(wave_sum(v) / Kin + eps);
+        if (l == 0 && mean_out) { mean_out[gr] = mean; rstd_out[gr] = rstd; }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xv[j] = (xv[j] - mean) * rstd * gw[j] + gb[j];
       }
-      for (int k = l; k < KP; k += 64) {
-        float v = 0.f;
-        if (k < Kin) {
-          v = ldf(xr + k);
-          if (lnw) v = (v - mean) * rstd * lnw[k] + lnb[k];
-        }
-        sA[rr * ld + k] = f2bf(v);
-      }
-    } else {
-      for (int k = l; k < KP; k += 64) sA[rr * ld + k] = 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = l + 64 * j;
+      if (k < KP) sA[rr * ld + k] = (gr < R && k < Kin) ? f2bf(xv[j]) : (uint16_t)0;
     }
   }
-  __syncthreads();
-  f32x16 acc[1] = {f32x16{}};
-  tile_gemm<1, true, true>(sA, ld, sB, ld, 64, 64, KP, acc);
-  for_acc<1>(64, 64, [&](int t, int m, int n, int i) {
-    const int gr = m0 + m, gc = n0 + n;
-    if (gr < R && gc < N) {
-      float v = acc[t][i] + (bias ? bias[gc] : 0.f);
-      if (act == 1) v = gelu_f(v);
-      if (res) v += res[(long long)gr * res_rs + gc];
-      stf(Y + (long long)gr * y_rs + gc, v);
-    }
-  });
+  for (int n0 = 0; n0 < N; n0 += 64) {
+    stage(sB, ld, W, Kin, n0, N, 0, Kin, 64, KP);
+    __syncthreads();
+    f32x16 acc[1] = {f32x16{}};
+    tile_gemm<1, true, true>(sA, ld, sB, ld, 64, 64, KP, acc);
+    for_acc<1>(64, 64, [&](int t, int m, int n, int i) {
+      const int gr = m0 + m, gc = n0 + n;
+      if (gr < R && gc < N) {
+        float v = acc[t][i] + (bias ? bias[gc] : 0.f);
+        if (act == 1) v = gelu_f(v);
+        if (res) v += res[(long long)gr * res_rs + gc];
+        stf(Y + (long long)gr * y_rs + gc, v);
+      }
+    });
+    __syncthreads();
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -291,9 +332,9 @@ __global__ __launch_bounds__(256) void post_attn_bwd_kernel(
   }
   stage(sW, LD, Wo, C, 0, C, 0, C, C, C);
   __syncthreads();
-  for (int k = threadIdx.x; k < C; k += blockDim.x) {
-    slab_g2[(long long)blockIdx.x * C + k] = sPart[0][0][k] + sPart[0][1][k] + sPart[0][2][k] + sPart[0][3][k];
-    slab_b2[(long long)blockIdx.x * C + k] = sPart[1][0][k] + sPart[1][1][k] + sPart[1][2][k] + sPart[1][3][k];
+  for (int k = threadIdx.x; k < C; k += blockDim.x) {  // LN2 param grads straight into the fp32 grads
+    atomicAdd(slab_g2 + k, sPart[0][0][k] + sPart[0][1][k] + sPart[0][2][k] + sPart[0][3][k]);
+    atomicAdd(slab_b2 + k, sPart[1][0][k] + sPart[1][1][k] + sPart[1][2][k] + sPart[1][3][k]);
   }
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
@@ -350,29 +391,38 @@ __global__ __launch_bounds__(256) void ln_linear_dgrad_kernel(
   __syncthreads();
   const int NJ = (KP + 63) / 64;
   float pg[3] = {0.f, 0.f, 0.f}, pb[3] = {0.f, 0.f, 0.f};
+  float gw[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) gw[j] = (lnw && l + 64 * j < Kin) ? lnw[l + 64 * j] : 0.f;
   for (int rr = w; rr < 64; rr += 4) {
     const int gr = m0 + rr;
     if (gr >= R) continue;
     if (lnw) {
       const float mu = mean[gr], rs = rstd[gr];
+      float xh[3], dxn[3];
       float s1 = 0.f, s2 = 0.f;
-      for (int k = l; k < Kin; k += 64) {
-        const float xh = (ldf(X + (long long)gr * x_rs + k) - mu) * rs;
-        const float g = sF[rr * ldF + k] * lnw[k];
-        s1 += g;
-        s2 += g * xh;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int k = l + 64 * j;
+        xh[j] = dxn[j] = 0.f;
+        if (j < NJ && k < Kin) {
+          xh[j] = (ldf(X + (long long)gr * x_rs + k) - mu) * rs;
+          dxn[j] = sF[rr * ldF + k];
+          const float g = dxn[j] * gw[j];
+          s1 += g;
+          s2 += g * xh[j];
+        }
       }
       s1 = wave_sum(s1) / Kin;
       s2 = wave_sum(s2) / Kin;
-      for (int j = 0; j < NJ; ++j) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
         const int k = l + 64 * j;
-        if (k < Kin) {
-          const float xh = (ldf(X + (long long)gr * x_rs + k) - mu) * rs;
-          const float dxn = sF[rr * ldF + k];
-          pg[j] += dxn * xh;
-          pb[j] += dxn;
+        if (j < NJ && k < Kin) {
+          pg[j] += dxn[j] * xh[j];
+          pb[j] += dxn[j];
           if (dX) {
-            float d = rs * (dxn * lnw[k] - s1 - xh * s2);
+            float d = rs * (dxn[j] * gw[j] - s1 - xh[j] * s2);
             if (dres) d += dres[(long long)gr * dres_rs + k];
             dX[(long long)gr * dx_rs + k] = d;
           }
@@ -392,11 +442,12 @@ __global__ __launch_bounds__(256) void ln_linear_dgrad_kernel(
       if (k < Kin) { sPart[(0 * 4 + w) * KP + k] = pg[j]; sPart[(1 * 4 + w) * KP + k] = pb[j]; }
     }
     __syncthreads();
+    // accumulate straight into the (flat) fp32 gradient: one atomic per element per workgroup
     for (int k = threadIdx.x; k < Kin; k += blockDim.x) {
       float a = 0.f, b = 0.f;
       for (int ww = 0; ww < 4; ++ww) { a += sPart[ww * KP + k]; b += sPart[(4 + ww) * KP + k]; }
-      slab_g[(long long)blockIdx.x * Kin + k] = a;
-      slab_b[(long long)blockIdx.x * Kin + k] = b;
+      atomicAdd(slab_g + k, a);
+      atomicAdd(slab_b + k, b);
     }
   }
 }
@@ -422,32 +473,66 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const TG* __restrict__ G, in
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
   float bsum = 0.f;  // thread n = threadIdx.x (< 64)
+  const bool avec = (Kin & 7) == 0 && (a_rs & 7) == 0 && (reinterpret_cast<uintptr_t>(A) & 15) == 0;
   for (int r0 = r_begin; r0 < r_end; r0 += 64) {
     __syncthreads();
     const int rows = min(64, r_end - r0);
-    stage(sG, ldg, G, g_rs, r0, r_begin + (r_end - r_begin), n0, N, 64, 64);
-    for (int e = threadIdx.x; e < 64 * KP; e += blockDim.x) {
-      const int rr = e / KP, k = e % KP;
-      const int gr = r0 + rr;
-      float v = 0.f;
-      if (rr < rows && k < Kin) {
-        v = ldf(A + (long long)gr * a_rs + k);
-        if (amode == 1) v = (v - mean[gr]) * rstd[gr] * lnw[k] + lnb[k];
-        else if (amode == 2) v = gelu_f(v);
+    stage(sG, ldg, G, g_rs, r0, r_end, n0, N, 64, 64);
+    if (avec) {  // 8 elements per access, transform applied in registers
+      const int cpr = KP >> 3;
+      for (int e = threadIdx.x; e < 64 * cpr; e += blockDim.x) {
+        const int rr = e / cpr, k = (e % cpr) * 8;
+        const int gr = r0 + rr;
+        bf16x8 o = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        if (rr < rows && k < Kin) {
+          const TA* p = A + (long long)gr * a_rs + k;
+          float v[8];
+          if constexpr (sizeof(TA) == 2) {
+            const bf16x8 b = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = bf2f(b[j]);
+          } else {
+            const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+          }
+          if (amode == 1) {
+            const float mu = mean[gr], rs = rstd[gr];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = (v[j] - mu) * rs * lnw[k + j] + lnb[k + j];
+          } else if (amode == 2) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = gelu_f(v[j]);
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = (short)f2bf(v[j]);
+        }
+        *reinterpret_cast<bf16x8*>(sA + rr * lda + k) = o;
       }
-      sA[rr * lda + k] = f2bf(v);
+    } else {
+      for (int e = threadIdx.x; e < 64 * KP; e += blockDim.x) {
+        const int rr = e / KP, k = e % KP;
+        const int gr = r0 + rr;
+        float v = 0.f;
+        if (rr < rows && k < Kin) {
+          v = ldf(A + (long long)gr * a_rs + k);
+          if (amode == 1) v = (v - mean[gr]) * rstd[gr] * lnw[k] + lnb[k];
+          else if (amode == 2) v = gelu_f(v);
+        }
+        sA[rr * lda + k] = f2bf(v);
+      }
     }
     __syncthreads();
     if (threadIdx.x < 64 && n0 + threadIdx.x < N)
       for (int rr = 0; rr < rows; ++rr) bsum += ldf(G + (long long)(r0 + rr) * g_rs + n0 + threadIdx.x);
     tile_gemm<MAXT, false, false>(sG, ldg, sA, lda, 64, KP, 64, acc);
   }
-  float* out = slab_w + (long long)s * N * Kin;
+  // accumulate into the fp32 gradient (slab_w: [N][Kin], slab_b: [N]); each wave-instruction
+  // adds two 128-byte row segments — the full-rate atomic shape on gfx950
   for_acc<MAXT>(64, KP, [&](int t, int m, int n, int i) {
     const int gn = n0 + m;
-    if (gn < N && n < Kin) out[(long long)gn * Kin + n] = acc[t][i];
+    if (gn < N && n < Kin) atomicAdd(slab_w + (long long)gn * Kin + n, acc[t][i]);
   });
-  if (slab_b && threadIdx.x < 64 && n0 + threadIdx.x < N) slab_b[(long long)s * N + n0 + threadIdx.x] = bsum;
+  if (slab_b && threadIdx.x < 64 && n0 + threadIdx.x < N) atomicAdd(slab_b + n0 + threadIdx.x, bsum);
 }
 
 // ------------------------------------------------------------------------------------
@@ -493,7 +578,7 @@ void ln_linear_fwd_launch(const void* X, bool x_bf16, int x_rs, int R, int Kin, 
                           int res_rs, void* Y, bool y_bf16, int y_rs, float* mean, float* rstd, hipStream_t st) {
   const int KP = round_up(Kin, 16);
   const size_t smem = 2 * 64 * (KP + 8) * sizeof(uint16_t);
-  dim3 grid((R + 63) / 64, (N + 63) / 64);
+  dim3 grid((R + 63) / 64);
 #define LNL(TI, TO)                                                                                         \
   hipLaunchKernelGGL((ln_linear_fwd_kernel<TI, TO>), grid, dim3(256), smem, st, (const TI*)X, x_rs, R, Kin, \
                      lnw, lnb, eps, W, bias, N, act, res, res_rs, (TO*)Y, y_rs, mean, rstd)
@@ -556,15 +641,14 @@ void ln_linear_dgrad_launch(const void* G, bool g_bf16, int g_rs, int N, const u
 
 void wgrad_launch(const void* G, bool g_bf16, int g_rs, int N, const void* A, bool a_bf16, int a_rs, int Kin,
                   int amode, const float* mean, const float* rstd, const float* lnw, const float* lnb, int R,
-                  int nsplit, float* slab_w, float* slab_b, hipStream_t st) {
+                  int rows_per_wg, float* dW, float* db, hipStream_t st) {
   const int KP = round_up(Kin, 32);
   const size_t smem = (64 * (64 + 8) + 64 * (KP + 8)) * 2;
-  int rps = (R + nsplit - 1) / nsplit;
-  rps = round_up(rps, 64);
-  dim3 grid((N + 63) / 64, nsplit);
+  const int rps = round_up(rows_per_wg > 0 ? rows_per_wg : 256, 64);
+  dim3 grid((N + 63) / 64, (R + rps - 1) / rps);
 #define WG(TG, TA)                                                                                                 \
   hipLaunchKernelGGL((wgrad_kernel<TG, TA>), grid, dim3(256), smem, st, (const TG*)G, g_rs, N, (const TA*)A, a_rs, \
-                     Kin, amode, mean, rstd, lnw, lnb, R, rps, slab_w, slab_b)
+                     Kin, amode, mean, rstd, lnw, lnb, R, rps, dW, db)
   if (g_bf16 && a_bf16) WG(uint16_t, uint16_t);
   else if (g_bf16) WG(uint16_t, float);
   else if (a_bf16) WG(float, uint16_t);

@@ -134,7 +134,8 @@ def _ln_bwd(dxn, x, mean, rstd, w):
     return rstd[:, None] * (g - s1 - xh * s2), xh
 
 
-def post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, H):
+def post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, H, dg2, db2):
+    """Returns (dy, du, dO, delta); LN2 parameter grads are ACCUMULATED into dg2 / db2."""
     dh = _bf(dz) @ _bf(w2.float())
     du = dh * _gelu_grad(u.float())
     du_b = du.to(torch.bfloat16)
@@ -145,34 +146,35 @@ def post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, H):
     R, C = dz.shape
     D = C // H
     delta = (do.float().view(R, H, D) * o.float().view(R, H, D)).sum(-1)
-    sg = (dxn * xh).sum(0, keepdim=True)
-    sb = dxn.sum(0, keepdim=True)
-    return dy, du_b, do, delta, sg, sb
+    dg2 += (dxn * xh).sum(0).view(dg2.shape)
+    db2 += dxn.sum(0).view(db2.shape)
+    return dy, du_b, do, delta
 
 
-def ln_linear_dgrad(g, w, x, mean, rstd, lnw, dres, need_dx):
+def ln_linear_dgrad(g, w, x, mean, rstd, lnw, dres, need_dx, dg=None, db=None):
+    """Returns dX (or None); LN parameter grads are ACCUMULATED into dg / db."""
     dxn = _bf(g.float()) @ _bf(w.float())
-    dx = sg = sb = None
     if lnw is not None:
         d, xh = _ln_bwd(dxn, x.float(), mean, rstd, lnw)
-        sg = (dxn * xh).sum(0, keepdim=True)
-        sb = dxn.sum(0, keepdim=True)
+        dg += (dxn * xh).sum(0).view(dg.shape)
+        db += dxn.sum(0).view(db.shape)
     else:
         d = dxn
     if need_dx:
-        dx = d + dres if dres is not None else d
-    return dx, sg, sb
+        return d + dres if dres is not None else d
+    return None
 
 
-def wgrad(g, a, amode, mean, rstd, lnw, lnb, nsplit, with_bias):
+def wgrad(g, a, amode, mean, rstd, lnw, lnb, rows_per_wg, dW, db=None):
+    """dW += Gᵀ·A(transformed), db += Σ_rows G (accumulated in place)."""
     af = a.float()
     if amode == 1:
         af = (af - mean[:, None]) * rstd[:, None] * lnw + lnb
     elif amode == 2:
         af = F.gelu(af)
-    sw = (_bf(g.float()).t() @ _bf(af)).unsqueeze(0)
-    sb = g.float().sum(0, keepdim=True) if with_bias else None
-    return sw, sb
+    dW += (_bf(g.float()).t() @ _bf(af)).view(dW.shape)
+    if db is not None:
+        db += g.float().sum(0).view(db.shape)
 
 
 def slab_reduce(slabs: List[torch.Tensor], dsts: List[torch.Tensor], acc: List[bool]):

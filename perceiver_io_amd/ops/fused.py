@@ -8,7 +8,9 @@ a single :class:`_LayerFn` whose forward is
     out-proj + residual + LN2 + MLP(GELU) + residual (post_attn_fwd)
 
 i.e. 3 kernel launches, and whose backward is the hand-written reverse chain
-(post_attn_bwd → attn_bwd → ln_linear_dgrad + wgrad slabs → slab_reduce).  Activations
+(post_attn_bwd → attn_bwd → ln_linear_dgrad + wgrad), whose parameter gradients are
+accumulated by the kernels straight into ``p.grad`` (views of the flat gradient buffer) with
+device atomics — no per-parameter autograd accumulation, no reduction pass.  Activations
 kept for backward: the bf16 Q/K/V and attention output, fp32 post-attention residual,
 LN statistics, the bf16 pre-GELU tensor — LN outputs and GELU outputs are recomputed.
 
@@ -128,8 +130,10 @@ def _bf16_weights(spec: LayerSpec, ps):
     return wq, wkv, wc.get(rest[1]), wc.get(rest[5]), wc.get(rest[7])
 
 
-def _wgrad_splits(rows: int, n: int) -> int:
-    return int(max(1, min(rows // 128, 256 // max(1, (n + 63) // 64))))
+def _rows_per_wg(rows: int) -> int:
+    """Rows per weight-gradient workgroup: ~64–256 workgroups per GEMM, ≥ 256 rows each so
+    the per-workgroup atomic flush stays small next to the streamed activations."""
+    return int(max(256, ((rows + 255) // 256 + 63) // 64 * 64))
 
 
 class _LayerFn(torch.autograd.Function):
@@ -194,91 +198,79 @@ class _LayerFn(torch.autograd.Function):
         if spec.cross:
             g_q, b_q, g_kv, b_kv = ps[0:4]
             rest = ps[5:] if spec.packed else ps[7:]
+            ibias = 5 if spec.packed else 7
         else:
             g_q, b_q = ps[0:2]
             rest = ps[3:]
+            ibias = 3
         bin_, Wo, bo, g2, be2, W1, b1, W2, b2 = rest
         dz2 = dz.reshape(B * Nq, C)
         if not dz2.is_contiguous():
             dz2 = dz2.contiguous()
         o2 = o.view(B * Nq, C)
-        dy, du, do, _delta, sg2, sb2 = K.post_attn_bwd(dz2, y, m2, r2, u, o2, wo, w1, w2, g2, H)
-        dev = dz.device
-        f32 = dict(device=dev, dtype=torch.float32)
         R = B * Nq
-        slabs, dsts = [], []
-        grads = [None] * len(ps)
+        f32 = dict(device=dz.device, dtype=torch.float32)
+        scratch = {}
 
-        def red(slab, dst):
-            slabs.append(slab)
-            dsts.append(dst)
+        def gb(p):
+            """Gradient target of parameter p (its .grad, normally a view of the flat buffer);
+            kernels accumulate into it directly.  Frozen parameters get a throw-away buffer."""
+            if not p.requires_grad:
+                t = scratch.get(id(p))
+                if t is None:
+                    t = scratch[id(p)] = torch.zeros(p.shape, **f32)
+                return t
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            return p.grad
 
-        # --- attention backward -------------------------------------------------------
+        dy, du, do, delta = K.post_attn_bwd(dz2, y, m2, r2, u, o2, wo, w1, w2, g2, H, gb(g2), gb(be2))
+        delta3 = delta.view(B, Nq, H)
+        rpw = _rows_per_wg(R)
+        # --- attention backward + input-side projections -----------------------------------------
         if spec.cross:
-            q3 = qx
             M = kv.shape[0] // B
             kv3 = kv.view(B, M, 2 * C)
             dkv = torch.empty((B, M, 2 * C), **f32)
-            dq, _, _ = K.attn_bwd(q3, kv3[:, :, :C], kv3[:, :, C:], kmask, o, do.view(B, Nq, C), lse, None, H, D,
+            dq, _, _ = K.attn_bwd(qx, kv3[:, :, :C], kv3[:, :, C:], kmask, o, do.view(B, Nq, C), lse, delta3, H, D,
                                   scale, ctx.p_attn, ctx.seed, None, dkv[:, :, :C], dkv[:, :, C:])
-            dq2 = dq.reshape(B * Nq, C)
-            dres = dy
+            dq2, dres = dq.reshape(B * Nq, C), dy
             if Bq == 1 and B > 1:
-                dq2 = dq.sum(0)
-                dres = dy.view(B, Nq, C).sum(0)
-            dx_q, sgq, sbq = K.ln_linear_dgrad(dq2, wq, xq2, mean_q, rstd_q, g_q, dres, True)
+                dq2, dres = dq.sum(0), dy.view(B, Nq, C).sum(0)
+            dx_q = K.ln_linear_dgrad(dq2, wq, xq2, mean_q, rstd_q, g_q, dres, True, gb(g_q), gb(b_q))
             dkv2 = dkv.view(B * M, 2 * C)
-            dx_kv, sgk, sbk = K.ln_linear_dgrad(dkv2, wkv, xkv2, mean_kv, rstd_kv, g_kv, None, ctx.kv_grad)
-            grads[0], grads[1] = torch.empty(C, **f32), torch.empty(C, **f32)
-            red(sgq, grads[0]); red(sbq, grads[1])
-            ckv = xkv2.shape[1]
-            grads[2], grads[3] = torch.empty(ckv, **f32), torch.empty(ckv, **f32)
-            red(sgk, grads[2]); red(sbk, grads[3])
-            rq = dq2.shape[0]
-            swq, sbq_ = K.wgrad(dq2, xq2, 1, mean_q, rstd_q, g_q, b_q, _wgrad_splits(rq, C), True)
-            swk, sbk_ = K.wgrad(dkv2, xkv2, 1, mean_kv, rstd_kv, g_kv, b_kv, _wgrad_splits(B * M, 2 * C), True)
-            gbin = torch.empty(3 * C, **f32)
+            dx_kv = K.ln_linear_dgrad(dkv2, wkv, xkv2, mean_kv, rstd_kv, g_kv, None, ctx.kv_grad, gb(g_kv), gb(b_kv))
+            gbias = gb(bin_)
             if spec.packed:
-                gin = torch.empty((3 * C, C), **f32)
-                red(swq, gin[:C]); red(swk, gin[C:])
-                grads[4] = gin
-                ibias = 5
+                gin = gb(ps[4])
+                gwq, gwkv = gin[:C], gin[C:]
             else:
-                gkv = torch.empty((2 * C, ckv), **f32)
-                grads[4] = torch.empty((C, C), **f32)
-                red(swq, grads[4]); red(swk, gkv)
-                grads[5], grads[6] = gkv[:C], gkv[C:]
-                ibias = 7
-            red(sbq_, gbin[:C]); red(sbk_, gbin[C:])
-            grads[ibias] = gbin
+                gwq = gb(ps[4])
+                gwkv = torch.zeros((2 * C, xkv2.shape[1]), **f32)
+            K.wgrad(dq2, xq2, 1, mean_q, rstd_q, g_q, b_q, _rows_per_wg(dq2.shape[0]), gwq, gbias[:C])
+            K.wgrad(dkv2, xkv2, 1, mean_kv, rstd_kv, g_kv, b_kv, _rows_per_wg(B * M), gwkv, gbias[C:])
+            if not spec.packed:
+                gb(ps[5]).add_(gwkv[:C])
+                gb(ps[6]).add_(gwkv[C:])
             dx_q = dx_q.view(Bq, Nq, C)
             dx_kv = dx_kv.view(B, M, -1) if ctx.kv_grad else None
         else:
             qkv3 = qx.view(B, Nq, 3 * C)
-            dqkv = torch.empty((B, Nq, 3 * C), **f32)
-            K.attn_bwd(qkv3[:, :, :C], qkv3[:, :, C:2 * C], qkv3[:, :, 2 * C:], kmask, o, do.view(B, Nq, C), lse, None,
-                       H, D, scale, ctx.p_attn, ctx.seed, dqkv[:, :, :C], dqkv[:, :, C:2 * C], dqkv[:, :, 2 * C:])
+            dqkv = torch.zeros((B, Nq, 3 * C), **f32)  # dQ third is accumulated with atomics
+            K.attn_bwd(qkv3[:, :, :C], qkv3[:, :, C:2 * C], qkv3[:, :, 2 * C:], kmask, o, do.view(B, Nq, C), lse,
+                       delta3, H, D, scale, ctx.p_attn, ctx.seed, dqkv[:, :, :C], dqkv[:, :, C:2 * C],
+                       dqkv[:, :, 2 * C:])
             dqkv2 = dqkv.view(R, 3 * C)
-            dx_q, sg1, sb1 = K.ln_linear_dgrad(dqkv2, wq, xq2, mean_q, rstd_q, g_q, dy, True)
-            grads[0], grads[1] = torch.empty(C, **f32), torch.empty(C, **f32)
-            red(sg1, grads[0]); red(sb1, grads[1])
-            sw, sb = K.wgrad(dqkv2, xq2, 1, mean_q, rstd_q, g_q, b_q, _wgrad_splits(R, 3 * C), True)
-            grads[2], grads[3] = torch.empty((3 * C, C), **f32), torch.empty(3 * C, **f32)
-            red(sw, grads[2]); red(sb, grads[3])
-            ibias = 3
+            dx_q = K.ln_linear_dgrad(dqkv2, wq, xq2, mean_q, rstd_q, g_q, dy, True, gb(g_q), gb(b_q))
+            K.wgrad(dqkv2, xq2, 1, mean_q, rstd_q, g_q, b_q, rpw, gb(ps[2]), gb(ps[3]))
             dx_q = dx_q.view(B, Nq, C)
             dx_kv = None
-        # --- post-attention weights -------------------------------------------------------
-        i0 = ibias + 1  # index of Wo in ps
-        ns = _wgrad_splits(R, C)
-        swo, sbo = K.wgrad(dy, o2, 0, None, None, None, None, ns, True)
-        sw1, sb1m = K.wgrad(du, y, 1, m2, r2, g2, be2, ns, True)
-        sw2, sb2m = K.wgrad(dz2, u, 2, None, None, None, None, ns, True)
-        for j, sl in ((0, swo), (1, sbo), (2, sg2), (3, sb2), (4, sw1), (5, sb1m), (6, sw2), (7, sb2m)):
-            grads[i0 + j] = torch.empty(ps[i0 + j].shape, **f32)
-            red(sl, grads[i0 + j])
-        K.slab_reduce(slabs, dsts, [False] * len(slabs))
-        return (None, None, None, None, dx_q, dx_kv, None, *grads)
+        # --- post-attention weights (out-proj, MLP) -------------------------------------------------
+        K.wgrad(dy, o2, 0, None, None, None, None, rpw, gb(Wo), gb(bo))
+        K.wgrad(du, y, 1, m2, r2, g2, be2, rpw, gb(W1), gb(b1))
+        K.wgrad(dz2, u, 2, None, None, None, None, rpw, gb(W2), gb(b2))
+        # parameter gradients were accumulated in place (no autograd AccumulateGrad pass)
+        return (None, None, None, None, dx_q, dx_kv, None) + (None,) * len(ps)
 
 
 def _seed(spec: LayerSpec, training: bool) -> int:
@@ -335,18 +327,21 @@ class _TextEmbedFn(torch.autograd.Function):
         ids = ids.contiguous()
         out = K.embed_fwd(ids, emb, pos[: ids.shape[1]].contiguous(), scale)
         ctx.save_for_backward(ids)
-        ctx.scale, ctx.shapes = scale, (emb.shape, pos.shape)
+        ctx.scale, ctx.emb, ctx.pos = scale, emb, pos
         return out
 
     @staticmethod
     def backward(ctx, g):
         (ids,) = ctx.saved_tensors
         K = kernels(g)
-        es, ps_ = ctx.shapes
-        de = torch.zeros(es, device=g.device, dtype=torch.float32) if ctx.needs_input_grad[1] else None
-        dp = torch.zeros(ps_, device=g.device, dtype=torch.float32) if ctx.needs_input_grad[2] else None
-        K.embed_bwd(ids, g.contiguous(), de, dp, ctx.scale)
-        return None, de, dp, None
+        targets = []
+        for p, need in ((ctx.emb, ctx.needs_input_grad[1]), (ctx.pos, ctx.needs_input_grad[2])):
+            if need and p.grad is None:
+                p.grad = torch.zeros_like(p)
+            targets.append(p.grad if need else None)
+        # scatter-add straight into the (flat-buffer) gradients
+        K.embed_bwd(ids, g.contiguous(), targets[0], targets[1], ctx.scale)
+        return None, None, None, None
 
 
 def text_embed(adapter, ids):

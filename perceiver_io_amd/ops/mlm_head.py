@@ -43,20 +43,24 @@ class _MaskedCE(torch.autograd.Function):
         denom = count.clamp(min=1).to(torch.float32)
         ctx.save_for_backward(hs, wb, bias, lse, idx, labels_c, denom)
         ctx.hshape = h.shape
+        ctx.weight, ctx.bias_p = weight, bias
         return loss_rows.sum() / denom
 
     @staticmethod
     def backward(ctx, g):
         hs, wb, bias, lse, idx, labels_c, denom = ctx.saved_tensors
+        weight = ctx.weight
         gscale = (g.to(torch.float32) / denom).reshape(1).contiguous()
         d_rows = torch.zeros(hs.shape, device=hs.device, dtype=torch.float32)
-        dw = torch.empty(wb.shape, device=hs.device, dtype=torch.float32)
-        db = torch.empty(bias.shape, device=hs.device, dtype=torch.float32)
-        ext.ce_bwd(hs, labels_c, wb, bias.contiguous(), lse, gscale, d_rows, dw, db, False)
+        # vocab-head parameter gradients are accumulated in place into .grad (flat buffer views)
+        for p in (weight, ctx.bias_p):
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        ext.ce_bwd(hs, labels_c, wb, bias.contiguous(), lse, gscale, d_rows, weight.grad, ctx.bias_p.grad, True)
         shp = ctx.hshape
         dh = torch.zeros((shp[0] * shp[1], shp[2]), device=hs.device, dtype=torch.float32)
         dh.index_add_(0, idx, d_rows)
-        return dh.view(shp), dw, db, None, None, None
+        return dh.view(shp), None, None, None, None, None
 
 
 def compact_rows(labels: torch.Tensor, cap: int):

@@ -112,9 +112,9 @@ def test_mlm_then_frozen_seq_clf_transfer_and_resume(tmp_path):
     assert os.path.exists(texts)  # sample predictions logged after validation
     clf = run_cli("seq_clf", tmp_path, "fit", *common, f"--model.mlm_ckpt={ck.best_model_path}",
                   "--model.freeze_encoder=true", "--trainer.max_epochs=1", "--trainer.limit_train_batches=2")
-    enc_ref = mlm.model.model.encoder.state_dict()
+    best = load_checkpoint(ck.best_model_path)["state_dict"]
     enc_clf = clf.model.model.encoder.state_dict()
-    assert all(torch.equal(enc_ref[k].cpu(), enc_clf[k].cpu()) for k in enc_ref)  # frozen + transferred
+    assert all(torch.equal(best["model.encoder." + k].cpu(), v.cpu()) for k, v in enc_clf.items())  # frozen + transferred
     assert not any(p.requires_grad for p in clf.model.model.encoder.parameters())
     ck2 = [c for c in clf.trainer.callbacks if type(c).__name__ == "ModelCheckpoint"][0]
     # resume: continues from the stored global step
