@@ -19,8 +19,7 @@ struct AttnArgs {
   float drop_scale;
   uint32_t seed;
 };
-struct ReduceJob { const float* src; float* dst; int len, nslab, accumulate; };
-struct ReduceJobs { ReduceJob j[12]; int n; };
+struct PostAttnGrads { float *dWo, *dbo, *dg2, *dbe2, *dW1, *db1, *dW2, *db2; };
 
 void attn_fwd_launch(const AttnArgs&, int, uint16_t*, float*, float*, float*, int, hipStream_t);
 void attn_bwd_launch(const AttnArgs&, int, const uint16_t*, const uint16_t*, const float*, float*, float*, long long,
@@ -31,14 +30,13 @@ void post_attn_fwd_launch(int, const uint16_t*, const float*, const uint16_t*, c
                           const float*, float, const uint16_t*, const float*, const uint16_t*, const float*, float*,
                           float*, float*, float*, uint16_t*, int, hipStream_t);
 void post_attn_bwd_launch(int, const float*, const float*, const float*, const float*, const uint16_t*,
-                          const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*, const float*, float*,
-                          uint16_t*, uint16_t*, float*, int, float*, float*, int, hipStream_t);
-void ln_linear_dgrad_launch(const void*, bool, int, int, const uint16_t*, int, const void*, bool, int, const float*,
-                            const float*, const float*, const float*, int, float*, int, float*, float*, int,
-                            hipStream_t);
+                          const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*, const float*,
+                          const float*, float*, uint16_t*, float*, int, const PostAttnGrads&, int, hipStream_t);
+void ln_linear_bwd_launch(const void*, bool, int, int, const uint16_t*, int, const void*, bool, int, const float*,
+                          const float*, const float*, const float*, const float*, int, float*, int, float*, float*,
+                          float*, float*, int, hipStream_t);
 void wgrad_launch(const void*, bool, int, int, const void*, bool, int, int, int, const float*, const float*,
                   const float*, const float*, int, int, float*, float*, hipStream_t);
-void slab_reduce_launch(const ReduceJobs&, hipStream_t);
 void ce_fwd_launch(int, const uint16_t*, const int64_t*, const uint16_t*, const float*, int, int, float*, float*,
                    float*, float*, int, hipStream_t);
 int ce_num_splits(int, int);
@@ -203,46 +201,67 @@ std::vector<Tensor> post_attn_fwd(Tensor o, Tensor x, Tensor wo, Tensor bo, Tens
   return {z, y, m, r, u};
 }
 
-// the three backward entry points below ACCUMULATE parameter gradients into caller-provided fp32
+// the backward entry points below ACCUMULATE parameter gradients into caller-provided fp32
 // tensors (normally views of the flat gradient buffer) with device atomics: no partial slabs,
 // no reduction pass, no autograd AccumulateGrad adds
+namespace {
+float* grad_target(Tensor& t, int64_t numel, const char* what) {
+  TORCH_CHECK(t.is_contiguous() && t.numel() == numel, "bad gradient target ", what);
+  CHECK_DT(t, torch::kFloat32);
+  return t.data_ptr<float>();
+}
+}  // namespace
+
+// grads = [dWo, dbo, dg2, dbe2, dW1, db1, dW2, db2]; returns (dy, dO, delta)
 std::vector<Tensor> post_attn_bwd(Tensor dz, Tensor y, Tensor m2, Tensor r2, Tensor u, Tensor o, Tensor wo, Tensor w1,
-                                  Tensor w2, Tensor g2, int64_t H, Tensor dg2, Tensor db2) {
-  TORCH_CHECK(dz.is_contiguous(), "dz must be contiguous");
+                                  Tensor w2, Tensor g2, Tensor be2, int64_t H, std::vector<Tensor> grads) {
+  TORCH_CHECK(dz.is_contiguous() && y.is_contiguous() && u.is_contiguous() && o.is_contiguous(),
+              "post_attn_bwd operands must be contiguous (R, C)");
   const int R = (int)dz.size(0), C = (int)dz.size(1);
-  TORCH_CHECK(dg2.is_contiguous() && db2.is_contiguous() && dg2.numel() == C && db2.numel() == C, "bad LN2 grad targets");
+  TORCH_CHECK(C == 32 || C == 64 || C == 128, "post_attn supports C in {32, 64, 128}");
+  TORCH_CHECK(H > 0 && C % H == 0, "heads must divide C");
+  TORCH_CHECK(grads.size() == 8, "post_attn_bwd needs 8 gradient targets");
+  const int64_t CC = (int64_t)C * C;
+  pio::PostAttnGrads pg{grad_target(grads[0], CC, "dWo"), grad_target(grads[1], C, "dbo"),
+                        grad_target(grads[2], C, "dg2"), grad_target(grads[3], C, "dbe2"),
+                        grad_target(grads[4], CC, "dW1"), grad_target(grads[5], C, "db1"),
+                        grad_target(grads[6], CC, "dW2"), grad_target(grads[7], C, "db2")};
   auto f32 = dz.options().dtype(torch::kFloat32);
   Tensor dy = torch::empty({R, C}, f32);
-  Tensor du = torch::empty({R, C}, dz.options().dtype(torch::kBFloat16));
   Tensor dO = torch::empty({R, C}, dz.options().dtype(torch::kBFloat16));
   Tensor delta = torch::empty({R, H}, f32);
   pio::post_attn_bwd_launch(C, f32p(dz), f32p(y), f32p(m2), f32p(r2), bfp(u), bfp(o), bfp(wo), bfp(w1), bfp(w2),
-                            f32p(g2), dy.data_ptr<float>(), bfp_mut(du), bfp_mut(dO), delta.data_ptr<float>(), (int)H,
-                            dg2.data_ptr<float>(), db2.data_ptr<float>(), R, stream());
-  return {dy, du, dO, delta};
+                            f32p(g2), f32p(be2), dy.data_ptr<float>(), bfp_mut(dO), delta.data_ptr<float>(), (int)H,
+                            pg, R, stream());
+  return {dy, dO, delta};
 }
 
-OptT ln_linear_dgrad(Tensor g, Tensor w, OptT x, OptT mean, OptT rstd, OptT lnw, OptT dres, bool need_dx, OptT dg,
-                     OptT db) {
-  TORCH_CHECK(g.dim() == 2 && g.stride(1) == 1, "g must be 2-D rows");
+// dX = LN_bwd(g·w) (+ dres); accumulates dγ/dβ (dlnw/dlnb, needed when lnw is given) and, when
+// dW is given, dW += gᵀ·LN(x) and db += Σ_rows g.  Returns dX when need_dx.
+OptT ln_linear_bwd(Tensor g, Tensor w, Tensor x, OptT mean, OptT rstd, OptT lnw, OptT lnb, OptT dres, bool need_dx,
+                   OptT dlnw, OptT dlnb, OptT dW, OptT db) {
+  TORCH_CHECK(g.dim() == 2 && g.stride(1) == 1 && x.dim() == 2 && x.stride(1) == 1, "g / x must be 2-D rows");
   const int R = (int)g.size(0), N = (int)g.size(1), Kin = (int)w.size(1);
-  TORCH_CHECK(w.size(0) == N, "w rows must match g columns");
-  TORCH_CHECK(Kin <= 160, "dgrad supports Kin <= 160");
+  TORCH_CHECK(w.size(0) == N && w.is_contiguous(), "w must be (N, Kin) contiguous, N = g columns");
+  TORCH_CHECK(x.size(0) == R && x.size(1) == Kin, "x must be (R, Kin)");
+  TORCH_CHECK(Kin <= 160, "ln_linear_bwd supports Kin <= 160");
   auto f32 = g.options().dtype(torch::kFloat32);
   Tensor dx;
-  float *dxp = nullptr, *sgp = nullptr, *sbp = nullptr;
+  float *dxp = nullptr, *dgp = nullptr, *dbp = nullptr, *dwp = nullptr, *dbiasp = nullptr;
   if (need_dx) { dx = torch::empty({R, Kin}, f32); dxp = dx.data_ptr<float>(); }
   if (lnw.has_value()) {
-    TORCH_CHECK(dg.has_value() && db.has_value() && dg->numel() == Kin && db->numel() == Kin && dg->is_contiguous() &&
-                db->is_contiguous(), "LN grad targets required");
-    sgp = dg->data_ptr<float>(); sbp = db->data_ptr<float>();
+    TORCH_CHECK(lnb.has_value() && mean.has_value() && rstd.has_value(), "LN weight needs bias and row stats");
+    TORCH_CHECK(dlnw.has_value() && dlnb.has_value(), "LN grad targets required");
+    dgp = grad_target(*dlnw, Kin, "dlnw");
+    dbp = grad_target(*dlnb, Kin, "dlnb");
   }
-  const void* xp = nullptr; bool xb = false; int xrs = 0;
-  if (x.has_value()) { xp = x->data_ptr(); xb = is_bf16(*x); xrs = (int)x->stride(0); }
+  if (dW.has_value()) dwp = grad_target(*dW, (int64_t)N * Kin, "dW");
+  if (db.has_value()) { TORCH_CHECK(dW.has_value(), "db needs dW"); dbiasp = grad_target(*db, N, "db"); }
   const float* dr = nullptr; int drs = 0;
-  if (dres.has_value()) { dr = f32p(*dres); drs = (int)dres->stride(0); }
-  pio::ln_linear_dgrad_launch(g.data_ptr(), is_bf16(g), (int)g.stride(0), N, bfp(w), Kin, xp, xb, xrs, f32o(mean),
-                              f32o(rstd), f32o(lnw), dr, drs, dxp, Kin, sgp, sbp, R, stream());
+  if (dres.has_value()) { dr = f32p(*dres); drs = (int)dres->stride(0); TORCH_CHECK(dres->stride(1) == 1); }
+  pio::ln_linear_bwd_launch(g.data_ptr(), is_bf16(g), (int)g.stride(0), N, bfp(w), Kin, x.data_ptr(), is_bf16(x),
+                            (int)x.stride(0), f32o(mean), f32o(rstd), f32o(lnw), f32o(lnb), dr, drs, dxp, Kin, dgp, dbp,
+                            dwp, dbiasp, R, stream());
   if (need_dx) return dx;
   return c10::nullopt;
 }
@@ -253,31 +272,12 @@ void wgrad(Tensor g, Tensor a, int64_t amode, OptT mean, OptT rstd, OptT lnw, Op
   const int R = (int)g.size(0), N = (int)g.size(1), Kin = (int)a.size(1);
   TORCH_CHECK(a.size(0) == R, "row mismatch");
   TORCH_CHECK(Kin <= 160, "wgrad supports Kin <= 160");
-  TORCH_CHECK(dW.is_contiguous() && dW.numel() == (int64_t)N * Kin, "dW must be a contiguous (N, Kin) fp32 target");
-  float* dbp = nullptr;
-  if (db.has_value()) { TORCH_CHECK(db->is_contiguous() && db->numel() == N); dbp = db->data_ptr<float>(); }
+  TORCH_CHECK(amode != 1 || (mean.has_value() && rstd.has_value() && lnw.has_value() && lnb.has_value()),
+              "LN mode needs stats and affine");
+  float* dwp = grad_target(dW, (int64_t)N * Kin, "dW");
+  float* dbp = db.has_value() ? grad_target(*db, N, "db") : nullptr;
   pio::wgrad_launch(g.data_ptr(), is_bf16(g), (int)g.stride(0), N, a.data_ptr(), is_bf16(a), (int)a.stride(0), Kin,
-                    (int)amode, f32o(mean), f32o(rstd), f32o(lnw), f32o(lnb), R, (int)rows_per_wg,
-                    dW.data_ptr<float>(), dbp, stream());
-}
-
-// jobs: list of (slab [S, ...], dst (numel = slab[0].numel()), accumulate)
-void slab_reduce(std::vector<Tensor> slabs, std::vector<Tensor> dsts, std::vector<bool> acc) {
-  TORCH_CHECK(slabs.size() == dsts.size() && slabs.size() == acc.size());
-  size_t i = 0;
-  while (i < slabs.size()) {
-    pio::ReduceJobs jobs{};
-    jobs.n = 0;
-    for (; i < slabs.size() && jobs.n < 12; ++i) {
-      Tensor& s = slabs[i];
-      Tensor& d = dsts[i];
-      TORCH_CHECK(s.is_contiguous() && d.is_contiguous(), "slab_reduce needs contiguous tensors");
-      const long long len = d.numel();
-      TORCH_CHECK(s.numel() % len == 0, "slab size mismatch");
-      jobs.j[jobs.n++] = pio::ReduceJob{f32p(s), d.data_ptr<float>(), (int)len, (int)(s.numel() / len), acc[i] ? 1 : 0};
-    }
-    pio::slab_reduce_launch(jobs, stream());
-  }
+                    (int)amode, f32o(mean), f32o(rstd), f32o(lnw), f32o(lnb), R, (int)rows_per_wg, dwp, dbp, stream());
 }
 
 std::vector<Tensor> ce_fwd(Tensor h, Tensor labels, Tensor w, Tensor bias) {
@@ -356,9 +356,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ln_linear_fwd", &ln_linear_fwd);
   m.def("post_attn_fwd", &post_attn_fwd);
   m.def("post_attn_bwd", &post_attn_bwd);
-  m.def("ln_linear_dgrad", &ln_linear_dgrad);
+  m.def("ln_linear_bwd", &ln_linear_bwd);
   m.def("wgrad", &wgrad);
-  m.def("slab_reduce", &slab_reduce);
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);
   m.def("embed_fwd", &embed_fwd);

@@ -9,11 +9,12 @@
 //                     one kernel per 64-row tile, intermediates in LDS (Residual(attn) →
 //                     Residual(mlp), model.py:29-56)
 //   post_attn_bwd   : the reverse chain for one 64-row tile: dZ → dH → dU (GELU') → LN2 bwd →
-//                     dY → dO (+ softmax delta = rowsum(dO∘O) for the attention backward)
-//   ln_linear_dgrad : dX = LN_bwd(dY·W) (+ residual grad), LN param partials
-//   wgrad           : dW = Σ_rows Gᵀ·A and db = Σ_rows G as per-split fp32 slabs, A optionally
-//                     recomputed on the fly (LN(x) or GELU(u)) instead of stored
-//   slab_reduce     : deterministic sum of the slabs into the (flat) fp32 grad buffer
+//                     dY → dO (+ softmax delta = rowsum(dO∘O) for the attention backward), with
+//                     the Wo/W1/W2/bias/LN2 parameter gradients computed from the resident tiles
+//   ln_linear_bwd   : dX = LN_bwd(G·W) (+ residual grad) plus dW = Gᵀ·LN(X), db, dγ, dβ
+//   wgrad           : standalone dW = Σ_rows Gᵀ·A', db = Σ_rows G, A' recomputed on load
+// Parameter gradients are accumulated with fp32 atomics straight into the caller's gradient
+// tensors (views of the flat gradient buffer): no partial slabs, no reduction launches.
 // All GEMMs are v_mfma_f32_32x32x16_bf16 on LDS tiles (common.h operand helpers); a 64-row
 // tile spans four waves, each owning whole 32×32 output sub-tiles.
 #include "common.h"
@@ -105,6 +106,11 @@ __device__ __forceinline__ void stage(uint16_t* s, int ld, const T* g, long long
     s[rr * ld + cc] = f2bf(v);
   }
 }
+
+// fp32 gradient targets of the post-attention block (views of the flat gradient buffer)
+struct PostAttnGrads {
+  float *dWo, *dbo, *dg2, *dbe2, *dW1, *db1, *dW2, *db2;
+};
 
 __host__ __device__ __forceinline__ int round_up(int x, int m) { return (x + m - 1) / m * m; }
 
@@ -249,96 +255,202 @@ __global__ __launch_bounds__(256) void post_attn_fwd_kernel(
 }
 
 // ------------------------------------------------------------------------------------
-// post-attention block backward (row-local part)
+// activation tile staging with the forward transform re-applied on load:
+// mode 0 plain, 1 LayerNorm (row stats + affine), 2 GELU.  Rows ≥ R and cols ≥ Kin are zero.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ void xform8(float (&v)[8], int amode, int gr, int k, const float* mean, const float* rstd,
+                                       const float* lnw, const float* lnb) {
+  if (amode == 1) {
+    const float mu = mean[gr], rs = rstd[gr];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (v[j] - mu) * rs * lnw[k + j] + lnb[k + j];
+  } else if (amode == 2) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = gelu_f(v[j]);
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void stage_act(uint16_t* s, int ld, const T* A, long long a_rs, int r0, int R, int Kin,
+                                          int cols, int amode, const float* mean, const float* rstd,
+                                          const float* lnw, const float* lnb) {
+  if ((Kin & 7) == 0 && (a_rs & 7) == 0 && (cols & 7) == 0 && (reinterpret_cast<uintptr_t>(A) & 15) == 0) {
+    const int cpr = cols >> 3;
+    for (int e = threadIdx.x; e < 64 * cpr; e += blockDim.x) {
+      const int rr = e / cpr, k = (e % cpr) * 8;
+      const int gr = r0 + rr;
+      bf16x8 o = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (gr < R && k < Kin) {
+        const T* p = A + (long long)gr * a_rs + k;
+        float v[8];
+        if constexpr (sizeof(T) == 2) {
+          const bf16x8 b = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = bf2f(b[j]);
+        } else {
+          const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+          v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        }
+        xform8(v, amode, gr, k, mean, rstd, lnw, lnb);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (short)f2bf(v[j]);
+      }
+      *reinterpret_cast<bf16x8*>(s + rr * ld + k) = o;
+    }
+    return;
+  }
+  for (int e = threadIdx.x; e < 64 * cols; e += blockDim.x) {
+    const int rr = e / cols, k = e % cols;
+    const int gr = r0 + rr;
+    float v = 0.f;
+    if (gr < R && k < Kin) {
+      v = ldf(A + (long long)gr * a_rs + k);
+      if (amode == 1) v = (v - mean[gr]) * rstd[gr] * lnw[k] + lnb[k];
+      else if (amode == 2) v = gelu_f(v);
+    }
+    s[rr * ld + k] = f2bf(v);
+  }
+}
+
+// weight-gradient partial of one 64-row tile, flushed with atomics into the fp32 gradient:
+// dW[n][k] += Σ_r sG[r][n] · sX[r][k]  (both tiles row-major [r][·] in LDS → k-strided
+// operands).  Each wave instruction adds two 128-byte row segments: the full-rate atomic shape.
+template <int MAXW>
+__device__ __forceinline__ void wgrad_tile(const uint16_t* sG, int ldg, const uint16_t* sX, int ldx, int NG, int KX,
+                                           int Nvalid, int Kvalid, float* __restrict__ dW, int dw_rs) {
+  f32x16 acc[MAXW];
+#pragma unroll
+  for (int t = 0; t < MAXW; ++t) acc[t] = f32x16{};
+  tile_gemm<MAXW, false, false>(sG, ldg, sX, ldx, NG, KX, 64, acc);
+  for_acc<MAXW>(NG, KX, [&](int t, int m, int n, int i) {
+    if (m < Nvalid && n < Kvalid) atomicAdd(dW + (long long)m * dw_rs + n, acc[t][i]);
+  });
+}
+
+// ------------------------------------------------------------------------------------
+// post-attention block backward, one 64-row tile, weight gradients included:
+//   dH = dZ·W2, dW2 += dZᵀ·GELU(U), db2 += Σ dZ
+//   dU = dH∘GELU'(U), dXn2 = dU·W1, dW1 += dUᵀ·LN2(Y), db1 += Σ dU
+//   dY = dZ + LN2_bwd(dXn2), dγ2/dβ2 partials
+//   dO = dY·Wo, dWo += dYᵀ·O, dbo += Σ dY, delta = rowsum_head(dO∘O)
+// The gradient tile (sG) and its matching activation tile (sX) sit side by side in LDS, so
+// each weight gradient is one extra MFMA pass over tiles that are already resident.
 // ------------------------------------------------------------------------------------
 template <int C>
 __global__ __launch_bounds__(256) void post_attn_bwd_kernel(
     const float* __restrict__ dZ, const float* __restrict__ Ysave, const float* __restrict__ mean2,
     const float* __restrict__ rstd2, const uint16_t* __restrict__ U, const uint16_t* __restrict__ O,
     const uint16_t* __restrict__ Wo, const uint16_t* __restrict__ W1, const uint16_t* __restrict__ W2,
-    const float* __restrict__ g2, float* __restrict__ dY, uint16_t* __restrict__ dU, uint16_t* __restrict__ dO,
-    float* __restrict__ delta, int H, float* __restrict__ slab_g2, float* __restrict__ slab_b2, int R) {
-  constexpr int LD = C + 8, LDF = C + 4, MAXT = (2 * C / 32 + 3) / 4;
-  __shared__ __attribute__((aligned(16))) uint16_t sA[64 * LD];
-  __shared__ __attribute__((aligned(16))) uint16_t sW[C * LD];
+    const float* __restrict__ g2, const float* __restrict__ be2, float* __restrict__ dY, uint16_t* __restrict__ dO,
+    float* __restrict__ delta, int H, PostAttnGrads gr_out, int R) {
+  constexpr int LD = C + 8, LDF = C + 4, MAXT = (2 * C / 32 + 3) / 4, MAXW = ((C / 32) * (C / 32) + 3) / 4;
+  constexpr int NJ = (C + 63) / 64, GRP = 256 / C, RPG = 64 / GRP;
+  __shared__ __attribute__((aligned(16))) uint16_t sG[64 * LD];  // dZ → dU → dY
+  __shared__ __attribute__((aligned(16))) uint16_t sX[64 * LD];  // GELU(U) → LN2(Y) → O
+  __shared__ __attribute__((aligned(16))) uint16_t sW[C * LD];   // W2 → W1 → Wo
   __shared__ __attribute__((aligned(16))) float sF[64 * LDF];
-  __shared__ float sPart[2][4][C];
+  __shared__ float sPart[4][4][C];  // per-wave column partials: dγ2, dβ2, Σ dY, Σ dZ
   const int m0 = blockIdx.x * 64;
   const int w = wave_id(), l = lane_id();
 
-  // dH = dZ · W2   (B[k=n][col=c] = W2[n][c] → W2 tile k-strided)
-  stage(sA, LD, dZ, C, m0, R, 0, C, 64, C);
+  // ---- MLP output layer
+  stage(sG, LD, dZ, C, m0, R, 0, C, 64, C);
+  stage_act(sX, LD, U, C, m0, R, C, C, 2, nullptr, nullptr, nullptr, nullptr);
   stage(sW, LD, W2, C, 0, C, 0, C, C, C);
   __syncthreads();
   f32x16 acc[MAXT];
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
-  tile_gemm<MAXT, true, false>(sA, LD, sW, LD, 64, C, C, acc);
-  __syncthreads();
+  tile_gemm<MAXT, true, false>(sG, LD, sW, LD, 64, C, C, acc);  // dH
+  wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, gr_out.dW2, C);
   for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) {
     const int gr = m0 + m;
-    float du = 0.f;
-    if (gr < R) {
-      du = acc[t][i] * gelu_grad(bf2f(U[(long long)gr * C + n]));
-      dU[(long long)gr * C + n] = f2bf(du);
-    }
-    sA[m * LD + n] = f2bf(du);
+    sF[m * LDF + n] = gr < R ? acc[t][i] * gelu_grad(bf2f(U[(long long)gr * C + n])) : 0.f;
   });
+  __syncthreads();
+  // ---- MLP hidden layer: db1 column sums (fp32), dU → bf16 tile, LN2(Y) tile, W1
+  {
+    const int c = threadIdx.x % C, g = threadIdx.x / C;
+    float s = 0.f;
+#pragma unroll 4
+    for (int r = g * RPG; r < (g + 1) * RPG; ++r) s += sF[r * LDF + c];
+    atomicAdd(gr_out.db1 + c, s);
+  }
+  for (int e = threadIdx.x; e < 64 * C / 4; e += blockDim.x) {
+    const int r = e / (C / 4), c = (e % (C / 4)) * 4;
+    const float4 v = *reinterpret_cast<const float4*>(sF + r * LDF + c);
+    *reinterpret_cast<uint32_t*>(sG + r * LD + c) = pack2(v.x, v.y);
+    *reinterpret_cast<uint32_t*>(sG + r * LD + c + 2) = pack2(v.z, v.w);
+  }
+  stage_act(sX, LD, Ysave, C, m0, R, C, C, 1, mean2, rstd2, g2, be2);
   stage(sW, LD, W1, C, 0, C, 0, C, C, C);
   __syncthreads();
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
-  tile_gemm<MAXT, true, false>(sA, LD, sW, LD, 64, C, C, acc);  // dXn2 = dU · W1
+  tile_gemm<MAXT, true, false>(sG, LD, sW, LD, 64, C, C, acc);  // dXn2 = dU · W1
+  wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, gr_out.dW1, C);
   for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) { sF[m * LDF + n] = acc[t][i]; });
   __syncthreads();
-  // LN2 backward → dY = dZ + LN_bwd ; param partials
-  float pg[(C + 63) / 64], pb[(C + 63) / 64];
+  // ---- LN2 backward → dY = dZ + LN_bwd ; column partials
+  float pg[NJ], pb[NJ], py[NJ], pz[NJ];
 #pragma unroll
-  for (int j = 0; j < (C + 63) / 64; ++j) pg[j] = pb[j] = 0.f;
+  for (int j = 0; j < NJ; ++j) pg[j] = pb[j] = py[j] = pz[j] = 0.f;
   for (int rr = w; rr < 64; rr += 4) {
     const int gr = m0 + rr;
     if (gr >= R) {
-      for (int k = l; k < C; k += 64) sA[rr * LD + k] = 0;
+      for (int k = l; k < C; k += 64) sG[rr * LD + k] = 0;
       continue;
     }
     const float mean = mean2[gr], rstd = rstd2[gr];
+    float xh[NJ], dxn[NJ], dz[NJ];
     float s1 = 0.f, s2 = 0.f;
-    for (int k = l; k < C; k += 64) {
-      const float xh = (Ysave[(long long)gr * C + k] - mean) * rstd;
-      const float g = sF[rr * LDF + k] * g2[k];
-      s1 += g;
-      s2 += g * xh;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int k = l + 64 * j;
+      xh[j] = dxn[j] = dz[j] = 0.f;
+      if (k < C) {
+        xh[j] = (Ysave[(long long)gr * C + k] - mean) * rstd;
+        dxn[j] = sF[rr * LDF + k];
+        dz[j] = dZ[(long long)gr * C + k];
+        const float g = dxn[j] * g2[k];
+        s1 += g;
+        s2 += g * xh[j];
+      }
     }
     s1 = wave_sum(s1) / C;
     s2 = wave_sum(s2) / C;
 #pragma unroll
-    for (int j = 0; j < (C + 63) / 64; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       const int k = l + 64 * j;
       if (k < C) {
-        const float xh = (Ysave[(long long)gr * C + k] - mean) * rstd;
-        const float dxn = sF[rr * LDF + k];
-        const float d = dZ[(long long)gr * C + k] + rstd * (dxn * g2[k] - s1 - xh * s2);
+        const float d = dz[j] + rstd * (dxn[j] * g2[k] - s1 - xh[j] * s2);
         dY[(long long)gr * C + k] = d;
-        sA[rr * LD + k] = f2bf(d);
-        pg[j] += dxn * xh;
-        pb[j] += dxn;
+        sG[rr * LD + k] = f2bf(d);
+        pg[j] += dxn[j] * xh[j];
+        pb[j] += dxn[j];
+        py[j] += d;
+        pz[j] += dz[j];
       }
     }
   }
 #pragma unroll
-  for (int j = 0; j < (C + 63) / 64; ++j) {
+  for (int j = 0; j < NJ; ++j) {
     const int k = l + 64 * j;
-    if (k < C) { sPart[0][w][k] = pg[j]; sPart[1][w][k] = pb[j]; }
+    if (k < C) { sPart[0][w][k] = pg[j]; sPart[1][w][k] = pb[j]; sPart[2][w][k] = py[j]; sPart[3][w][k] = pz[j]; }
   }
+  // ---- out-projection
+  stage(sX, LD, O, C, m0, R, 0, C, 64, C);
   stage(sW, LD, Wo, C, 0, C, 0, C, C, C);
   __syncthreads();
-  for (int k = threadIdx.x; k < C; k += blockDim.x) {  // LN2 param grads straight into the fp32 grads
-    atomicAdd(slab_g2 + k, sPart[0][0][k] + sPart[0][1][k] + sPart[0][2][k] + sPart[0][3][k]);
-    atomicAdd(slab_b2 + k, sPart[1][0][k] + sPart[1][1][k] + sPart[1][2][k] + sPart[1][3][k]);
+  for (int e = threadIdx.x; e < 4 * C; e += blockDim.x) {
+    const int q = e / C, k = e % C;
+    float* dst = q == 0 ? gr_out.dg2 : q == 1 ? gr_out.dbe2 : q == 2 ? gr_out.dbo : gr_out.db2;
+    atomicAdd(dst + k, sPart[q][0][k] + sPart[q][1][k] + sPart[q][2][k] + sPart[q][3][k]);
   }
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
-  tile_gemm<MAXT, true, false>(sA, LD, sW, LD, 64, C, C, acc);  // dO = dY · Wo
+  tile_gemm<MAXT, true, false>(sG, LD, sW, LD, 64, C, C, acc);  // dO = dY · Wo
+  wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, gr_out.dWo, C);
   for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) {
     const int gr = m0 + m;
     const uint16_t d = f2bf(acc[t][i]);
@@ -346,37 +458,41 @@ __global__ __launch_bounds__(256) void post_attn_bwd_kernel(
     if (gr < R) dO[(long long)gr * C + n] = d;
   });
   __syncthreads();
-  // delta[r, h] = sum_d dO * O over the head's columns (bf16 values as the attention sees them)
+  // delta[r, h] = Σ_d dO·O over the head's columns (bf16 values, as the attention sees them)
   const int D = C / H;
   for (int e = threadIdx.x; e < 64 * H; e += blockDim.x) {
     const int rr = e / H, h = e % H;
     const int gr = m0 + rr;
     if (gr < R) {
       float s = 0.f;
-      for (int d = 0; d < D; ++d) s += sF[rr * LDF + h * D + d] * bf2f(O[(long long)gr * C + h * D + d]);
+      for (int d = 0; d < D; ++d) s += sF[rr * LDF + h * D + d] * bf2f(sX[rr * LD + h * D + d]);
       delta[(long long)gr * H + h] = s;
     }
   }
 }
 
 // ------------------------------------------------------------------------------------
-// dX = LN_bwd(G · W) (+ dres) ; LN param partial slabs
+// LayerNorm(+)Linear backward, one 64-row tile:
+//   dXn = G·W (N streamed in 64-column chunks), dW += Gᵀ·LN(X), db += Σ G (per chunk, atomics)
+//   dX = LN_bwd(dXn) (+ dres), dγ/dβ partials (atomics)
 // ------------------------------------------------------------------------------------
 template <typename TG, typename TX>
-__global__ __launch_bounds__(256) void ln_linear_dgrad_kernel(
+__global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
     const TG* __restrict__ G, int g_rs, int N, const uint16_t* __restrict__ W, int Kin, const TX* __restrict__ X,
     int x_rs, const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ lnw,
-    const float* __restrict__ dres, int dres_rs, float* __restrict__ dX, int dx_rs, float* __restrict__ slab_g,
-    float* __restrict__ slab_b, int R) {
+    const float* __restrict__ lnb, const float* __restrict__ dres, int dres_rs, float* __restrict__ dX, int dx_rs,
+    float* __restrict__ dlnw, float* __restrict__ dlnb, float* __restrict__ dW, float* __restrict__ db, int R) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   const int KP = round_up(Kin, 32), ld = KP + 8, ldg = 64 + 8, ldF = KP + 4;
   uint16_t* sG = smem;                 // [64 rows][64 n]
   uint16_t* sW = sG + 64 * ldg;        // [64 n][KP]
-  float* sF = reinterpret_cast<float*>(sW + 64 * ld);  // [64][KP] fp32
+  uint16_t* sXn = sW + 64 * ld;        // [64 rows][KP]  LN(X), the forward GEMM's A operand
+  float* sF = reinterpret_cast<float*>(sXn + 64 * ld);  // [64][KP] fp32
   float* sPart = sF + 64 * ldF;        // [2][4][KP]
   const int m0 = blockIdx.x * 64;
   const int w = wave_id(), l = lane_id();
   constexpr int MAXT = 3;  // (64/32)*(KP/32) ≤ 10 sub-tiles (KP ≤ 160)
+  if (dW) stage_act(sXn, ld, X, x_rs, m0, R, Kin, KP, lnw ? 1 : 0, mean, rstd, lnw, lnb);
   f32x16 acc[MAXT];
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
@@ -386,6 +502,18 @@ __global__ __launch_bounds__(256) void ln_linear_dgrad_kernel(
     stage(sW, ld, W, Kin, nc, N, 0, Kin, 64, KP);
     __syncthreads();
     tile_gemm<MAXT, true, false>(sG, ldg, sW, ld, 64, KP, 64, acc);
+    if (dW) {
+      wgrad_tile<MAXT>(sG, ldg, sXn, ld, 64, KP, N - nc, Kin, dW + (long long)nc * Kin, Kin);
+      if (db) {  // fp32 column sums of this G chunk: 4 row-quarters per column
+        const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
+        if (nc + c < N) {
+          float s = 0.f;
+#pragma unroll 4
+          for (int r = m0 + 16 * q; r < min(R, m0 + 16 * q + 16); ++r) s += ldf(G + (long long)r * g_rs + nc + c);
+          atomicAdd(db + nc + c, s);
+        }
+      }
+    }
   }
   for_acc<MAXT>(64, KP, [&](int t, int m, int n, int i) { sF[m * ldF + n] = acc[t][i]; });
   __syncthreads();
@@ -436,32 +564,32 @@ __global__ __launch_bounds__(256) void ln_linear_dgrad_kernel(
       }
     }
   }
-  if (lnw && slab_g) {
+  if (lnw && dlnw) {
     for (int j = 0; j < NJ; ++j) {
       const int k = l + 64 * j;
       if (k < Kin) { sPart[(0 * 4 + w) * KP + k] = pg[j]; sPart[(1 * 4 + w) * KP + k] = pb[j]; }
     }
     __syncthreads();
-    // accumulate straight into the (flat) fp32 gradient: one atomic per element per workgroup
     for (int k = threadIdx.x; k < Kin; k += blockDim.x) {
       float a = 0.f, b = 0.f;
       for (int ww = 0; ww < 4; ++ww) { a += sPart[ww * KP + k]; b += sPart[(4 + ww) * KP + k]; }
-      atomicAdd(slab_g + k, a);
-      atomicAdd(slab_b + k, b);
+      atomicAdd(dlnw + k, a);
+      atomicAdd(dlnb + k, b);
     }
   }
 }
 
 // ------------------------------------------------------------------------------------
-// weight gradient slabs: slab[s][n][k] = Σ_{rows of split s} G[r][n] · A[r][k]
-// A modes: 0 plain bf16, 1 LN(x) recomputed (x fp32), 2 GELU(u) recomputed (u bf16)
+// standalone weight gradient (for projections without a fused backward producer):
+// dW[n][k] += Σ_rows G[r][n] · A'[r][k], db[n] += Σ_rows G[r][n], A' = A | LN(A) | GELU(A)
+// grid (N/64, row splits); partials flushed with atomics
 // ------------------------------------------------------------------------------------
 template <typename TG, typename TA>
 __global__ __launch_bounds__(256) void wgrad_kernel(const TG* __restrict__ G, int g_rs, int N, const TA* __restrict__ A,
                                                     int a_rs, int Kin, int amode, const float* __restrict__ mean,
                                                     const float* __restrict__ rstd, const float* __restrict__ lnw,
                                                     const float* __restrict__ lnb, int R, int rows_per_split,
-                                                    float* __restrict__ slab_w, float* __restrict__ slab_b) {
+                                                    float* __restrict__ dW, float* __restrict__ db) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   const int KP = round_up(Kin, 32), lda = KP + 8, ldg = 64 + 8;
   uint16_t* sG = smem;           // [64 rows][64 n]
@@ -473,88 +601,20 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const TG* __restrict__ G, in
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
   float bsum = 0.f;  // thread n = threadIdx.x (< 64)
-  const bool avec = (Kin & 7) == 0 && (a_rs & 7) == 0 && (reinterpret_cast<uintptr_t>(A) & 15) == 0;
   for (int r0 = r_begin; r0 < r_end; r0 += 64) {
     __syncthreads();
-    const int rows = min(64, r_end - r0);
     stage(sG, ldg, G, g_rs, r0, r_end, n0, N, 64, 64);
-    if (avec) {  // 8 elements per access, transform applied in registers
-      const int cpr = KP >> 3;
-      for (int e = threadIdx.x; e < 64 * cpr; e += blockDim.x) {
-        const int rr = e / cpr, k = (e % cpr) * 8;
-        const int gr = r0 + rr;
-        bf16x8 o = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-        if (rr < rows && k < Kin) {
-          const TA* p = A + (long long)gr * a_rs + k;
-          float v[8];
-          if constexpr (sizeof(TA) == 2) {
-            const bf16x8 b = *reinterpret_cast<const bf16x8*>(p);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = bf2f(b[j]);
-          } else {
-            const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
-            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-          }
-          if (amode == 1) {
-            const float mu = mean[gr], rs = rstd[gr];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = (v[j] - mu) * rs * lnw[k + j] + lnb[k + j];
-          } else if (amode == 2) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = gelu_f(v[j]);
-          }
-#pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = (short)f2bf(v[j]);
-        }
-        *reinterpret_cast<bf16x8*>(sA + rr * lda + k) = o;
-      }
-    } else {
-      for (int e = threadIdx.x; e < 64 * KP; e += blockDim.x) {
-        const int rr = e / KP, k = e % KP;
-        const int gr = r0 + rr;
-        float v = 0.f;
-        if (rr < rows && k < Kin) {
-          v = ldf(A + (long long)gr * a_rs + k);
-          if (amode == 1) v = (v - mean[gr]) * rstd[gr] * lnw[k] + lnb[k];
-          else if (amode == 2) v = gelu_f(v);
-        }
-        sA[rr * lda + k] = f2bf(v);
-      }
-    }
+    stage_act(sA, lda, A, a_rs, r0, r_end, Kin, KP, amode, mean, rstd, lnw, lnb);
     __syncthreads();
     if (threadIdx.x < 64 && n0 + threadIdx.x < N)
-      for (int rr = 0; rr < rows; ++rr) bsum += ldf(G + (long long)(r0 + rr) * g_rs + n0 + threadIdx.x);
+      for (int rr = r0; rr < min(r_end, r0 + 64); ++rr) bsum += ldf(G + (long long)rr * g_rs + n0 + threadIdx.x);
     tile_gemm<MAXT, false, false>(sG, ldg, sA, lda, 64, KP, 64, acc);
   }
-  // accumulate into the fp32 gradient (slab_w: [N][Kin], slab_b: [N]); each wave-instruction
-  // adds two 128-byte row segments — the full-rate atomic shape on gfx950
   for_acc<MAXT>(64, KP, [&](int t, int m, int n, int i) {
     const int gn = n0 + m;
-    if (gn < N && n < Kin) atomicAdd(slab_w + (long long)gn * Kin + n, acc[t][i]);
+    if (gn < N && n < Kin) atomicAdd(dW + (long long)gn * Kin + n, acc[t][i]);
   });
-  if (slab_b && threadIdx.x < 64 && n0 + threadIdx.x < N) atomicAdd(slab_b + n0 + threadIdx.x, bsum);
-}
-
-// ------------------------------------------------------------------------------------
-// batched slab reduction: dst[i] (+)= Σ_s src[s * len + i]
-// ------------------------------------------------------------------------------------
-struct ReduceJob {
-  const float* src;
-  float* dst;
-  int len, nslab, accumulate;
-};
-struct ReduceJobs {
-  ReduceJob j[12];
-  int n;
-};
-
-__global__ void slab_reduce_kernel(ReduceJobs jobs) {
-  const ReduceJob& jb = jobs.j[blockIdx.y];
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < jb.len; i += gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int k = 0; k < jb.nslab; ++k) s += jb.src[(long long)k * jb.len + i];
-    jb.dst[i] = jb.accumulate ? jb.dst[i] + s : s;
-  }
+  if (db && threadIdx.x < 64 && n0 + threadIdx.x < N) atomicAdd(db + n0 + threadIdx.x, bsum);
 }
 
 // ------------------------------------------------------------------------------------
@@ -607,30 +667,30 @@ void post_attn_fwd_launch(int C, const uint16_t* O, const float* X, const uint16
 
 void post_attn_bwd_launch(int C, const float* dZ, const float* Ysave, const float* mean2, const float* rstd2,
                           const uint16_t* U, const uint16_t* O, const uint16_t* Wo, const uint16_t* W1,
-                          const uint16_t* W2, const float* g2, float* dY, uint16_t* dU, uint16_t* dO, float* delta,
-                          int H, float* slab_g2, float* slab_b2, int R, hipStream_t st) {
+                          const uint16_t* W2, const float* g2, const float* be2, float* dY, uint16_t* dO,
+                          float* delta, int H, const PostAttnGrads& grads, int R, hipStream_t st) {
   dim3 grid((R + 63) / 64);
 #define PAB(CC)                                                                                                  \
   hipLaunchKernelGGL(post_attn_bwd_kernel<CC>, grid, dim3(256), 0, st, dZ, Ysave, mean2, rstd2, U, O, Wo, W1, W2, \
-                     g2, dY, dU, dO, delta, H, slab_g2, slab_b2, R)
+                     g2, be2, dY, dO, delta, H, grads, R)
   if (C == 64) PAB(64);
   else if (C == 128) PAB(128);
   else if (C == 32) PAB(32);
 #undef PAB
 }
 
-void ln_linear_dgrad_launch(const void* G, bool g_bf16, int g_rs, int N, const uint16_t* W, int Kin, const void* X,
-                            bool x_bf16, int x_rs, const float* mean, const float* rstd, const float* lnw,
-                            const float* dres, int dres_rs, float* dX, int dx_rs, float* slab_g, float* slab_b, int R,
-                            hipStream_t st) {
+void ln_linear_bwd_launch(const void* G, bool g_bf16, int g_rs, int N, const uint16_t* W, int Kin, const void* X,
+                          bool x_bf16, int x_rs, const float* mean, const float* rstd, const float* lnw,
+                          const float* lnb, const float* dres, int dres_rs, float* dX, int dx_rs, float* dlnw,
+                          float* dlnb, float* dW, float* db, int R, hipStream_t st) {
   const int KP = round_up(Kin, 32);
-  const size_t smem = 64 * (64 + 8) * 2 + 64 * (KP + 8) * 2 + 64 * (KP + 4) * 4 + 2 * 4 * KP * 4;
+  const size_t smem = 64 * (64 + 8) * 2 + 2 * 64 * (KP + 8) * 2 + 64 * (KP + 4) * 4 + 2 * 4 * KP * 4;
   dim3 grid((R + 63) / 64);
-#define LDG(TG, TX)                                                                                             \
-  do {                                                                                                          \
-    set_smem_once((const void*)ln_linear_dgrad_kernel<TG, TX>);                                                 \
-    hipLaunchKernelGGL((ln_linear_dgrad_kernel<TG, TX>), grid, dim3(256), smem, st, (const TG*)G, g_rs, N, W,   \
-                       Kin, (const TX*)X, x_rs, mean, rstd, lnw, dres, dres_rs, dX, dx_rs, slab_g, slab_b, R);  \
+#define LDG(TG, TX)                                                                                              \
+  do {                                                                                                           \
+    set_smem_once((const void*)ln_linear_bwd_kernel<TG, TX>);                                                    \
+    hipLaunchKernelGGL((ln_linear_bwd_kernel<TG, TX>), grid, dim3(256), smem, st, (const TG*)G, g_rs, N, W, Kin, \
+                       (const TX*)X, x_rs, mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, dlnw, dlnb, dW, db, R); \
   } while (0)
   if (g_bf16 && x_bf16) LDG(uint16_t, uint16_t);
   else if (g_bf16) LDG(uint16_t, float);
@@ -654,14 +714,6 @@ void wgrad_launch(const void* G, bool g_bf16, int g_rs, int N, const void* A, bo
   else if (a_bf16) WG(float, uint16_t);
   else WG(float, float);
 #undef WG
-}
-
-void slab_reduce_launch(const ReduceJobs& jobs, hipStream_t st) {
-  if (jobs.n == 0) return;
-  int maxlen = 0;
-  for (int i = 0; i < jobs.n; ++i) maxlen = jobs.j[i].len > maxlen ? jobs.j[i].len : maxlen;
-  dim3 grid(min((maxlen + 255) / 256, 64), jobs.n);
-  hipLaunchKernelGGL(slab_reduce_kernel, grid, dim3(256), 0, st, jobs);
 }
 
 }  // namespace pio

@@ -1,7 +1,7 @@
 """Plain-PyTorch emulation of every HIP kernel entry point (same signatures as ``_C``).
 
 Two uses: (1) the fused executor runs on CPU through this module, so its bookkeeping
-(strides, packed buffers, batch-broadcast queries, slab reductions, weight sharing) is
+(strides, packed buffers, batch-broadcast queries, in-place gradient accumulation) is
 covered by the CPU test-suite; (2) it is the fp32 oracle the GPU numerics tests compare
 the hand-written kernels against.  Rounding points mirror the kernels: GEMM operands are
 rounded to bf16 exactly where the kernels stage bf16 tiles, accumulation is fp32.
@@ -9,8 +9,6 @@ rounded to bf16 exactly where the kernels stage bf16 tiles, accumulation is fp32
 from __future__ import annotations
 
 import math
-from typing import List, Optional
-
 import torch
 import torch.nn.functional as F
 
@@ -134,30 +132,47 @@ def _ln_bwd(dxn, x, mean, rstd, w):
     return rstd[:, None] * (g - s1 - xh * s2), xh
 
 
-def post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, H, dg2, db2):
-    """Returns (dy, du, dO, delta); LN2 parameter grads are ACCUMULATED into dg2 / db2."""
+def post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, be2, H, grads):
+    """Returns (dy, dO, delta); parameter grads are ACCUMULATED into
+    grads = [dWo, dbo, dg2, dbe2, dW1, db1, dW2, db2]."""
+    dWo, dbo, dg2, dbe2, dW1, db1, dW2, db2 = grads
+    uf = u.float()
     dh = _bf(dz) @ _bf(w2.float())
-    du = dh * _gelu_grad(u.float())
-    du_b = du.to(torch.bfloat16)
+    dW2 += (_bf(dz).t() @ _bf(F.gelu(uf))).view(dW2.shape)
+    db2 += dz.sum(0).view(db2.shape)
+    du = dh * _gelu_grad(uf)
     dxn = _bf(du) @ _bf(w1.float())
+    xn = (y - m2[:, None]) * r2[:, None] * g2 + be2
+    dW1 += (_bf(du).t() @ _bf(xn)).view(dW1.shape)
+    db1 += du.sum(0).view(db1.shape)
     dln, xh = _ln_bwd(dxn, y, m2, r2, g2)
     dy = dz + dln
     do = (_bf(dy) @ _bf(wo.float())).to(torch.bfloat16)
+    dWo += (_bf(dy).t() @ _bf(o.float())).view(dWo.shape)
+    dbo += dy.sum(0).view(dbo.shape)
     R, C = dz.shape
     D = C // H
     delta = (do.float().view(R, H, D) * o.float().view(R, H, D)).sum(-1)
     dg2 += (dxn * xh).sum(0).view(dg2.shape)
-    db2 += dxn.sum(0).view(db2.shape)
-    return dy, du_b, do, delta
+    dbe2 += dxn.sum(0).view(dbe2.shape)
+    return dy, do, delta
 
 
-def ln_linear_dgrad(g, w, x, mean, rstd, lnw, dres, need_dx, dg=None, db=None):
-    """Returns dX (or None); LN parameter grads are ACCUMULATED into dg / db."""
-    dxn = _bf(g.float()) @ _bf(w.float())
+def ln_linear_bwd(g, w, x, mean, rstd, lnw, lnb, dres, need_dx, dlnw=None, dlnb=None, dW=None, db=None):
+    """Returns dX (or None); LN grads accumulate into dlnw / dlnb and, when given,
+    dW += gᵀ·LN(x), db += Σ_rows g."""
+    gf = g.float()
+    dxn = _bf(gf) @ _bf(w.float())
+    xf = x.float()
+    if dW is not None:
+        xn = (xf - mean[:, None]) * rstd[:, None] * lnw + lnb if lnw is not None else xf
+        dW += (_bf(gf).t() @ _bf(xn)).view(dW.shape)
+        if db is not None:
+            db += gf.sum(0).view(db.shape)
     if lnw is not None:
-        d, xh = _ln_bwd(dxn, x.float(), mean, rstd, lnw)
-        dg += (dxn * xh).sum(0).view(dg.shape)
-        db += dxn.sum(0).view(db.shape)
+        d, xh = _ln_bwd(dxn, xf, mean, rstd, lnw)
+        dlnw += (dxn * xh).sum(0).view(dlnw.shape)
+        dlnb += dxn.sum(0).view(dlnb.shape)
     else:
         d = dxn
     if need_dx:
@@ -175,15 +190,6 @@ def wgrad(g, a, amode, mean, rstd, lnw, lnb, rows_per_wg, dW, db=None):
     dW += (_bf(g.float()).t() @ _bf(af)).view(dW.shape)
     if db is not None:
         db += g.float().sum(0).view(db.shape)
-
-
-def slab_reduce(slabs: List[torch.Tensor], dsts: List[torch.Tensor], acc: List[bool]):
-    for s, d, a in zip(slabs, dsts, acc):
-        v = s.reshape(-1, d.numel()).sum(0).view(d.shape)
-        if a:
-            d.add_(v)
-        else:
-            d.copy_(v)
 
 
 def ce_fwd(h, labels, w, bias):

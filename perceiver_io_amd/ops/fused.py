@@ -8,8 +8,9 @@ a single :class:`_LayerFn` whose forward is
     out-proj + residual + LN2 + MLP(GELU) + residual (post_attn_fwd)
 
 i.e. 3 kernel launches, and whose backward is the hand-written reverse chain
-(post_attn_bwd → attn_bwd → ln_linear_dgrad + wgrad), whose parameter gradients are
-accumulated by the kernels straight into ``p.grad`` (views of the flat gradient buffer) with
+(post_attn_bwd → attn_bwd → ln_linear_bwd), 3 launches as well: each weight gradient is an
+extra MFMA pass over LDS tiles the producing kernel already holds, and all parameter gradients
+are accumulated by the kernels straight into ``p.grad`` (views of the flat gradient buffer) with
 device atomics — no per-parameter autograd accumulation, no reduction pass.  Activations
 kept for backward: the bf16 Q/K/V and attention output, fp32 post-attention residual,
 LN statistics, the bf16 pre-GELU tensor — LN outputs and GELU outputs are recomputed.
@@ -130,12 +131,6 @@ def _bf16_weights(spec: LayerSpec, ps):
     return wq, wkv, wc.get(rest[1]), wc.get(rest[5]), wc.get(rest[7])
 
 
-def _rows_per_wg(rows: int) -> int:
-    """Rows per weight-gradient workgroup: ~64–256 workgroups per GEMM, ≥ 256 rows each so
-    the per-workgroup atomic flush stays small next to the streamed activations."""
-    return int(max(256, ((rows + 255) // 256 + 63) // 64 * 64))
-
-
 class _LayerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, spec: LayerSpec, bw, seed, p_attn, x_q, x_kv, kmask, *ps):
@@ -224,10 +219,10 @@ class _LayerFn(torch.autograd.Function):
                 p.grad = torch.zeros_like(p)
             return p.grad
 
-        dy, du, do, delta = K.post_attn_bwd(dz2, y, m2, r2, u, o2, wo, w1, w2, g2, H, gb(g2), gb(be2))
+        dy, do, delta = K.post_attn_bwd(dz2, y, m2, r2, u, o2, wo, w1, w2, g2, be2, H,
+                                        [gb(Wo), gb(bo), gb(g2), gb(be2), gb(W1), gb(b1), gb(W2), gb(b2)])
         delta3 = delta.view(B, Nq, H)
-        rpw = _rows_per_wg(R)
-        # --- attention backward + input-side projections -----------------------------------------
+        # --- attention backward + input-side projections (weight grads fused into ln_linear_bwd) ----
         if spec.cross:
             M = kv.shape[0] // B
             kv3 = kv.view(B, M, 2 * C)
@@ -237,9 +232,6 @@ class _LayerFn(torch.autograd.Function):
             dq2, dres = dq.reshape(B * Nq, C), dy
             if Bq == 1 and B > 1:
                 dq2, dres = dq.sum(0), dy.view(B, Nq, C).sum(0)
-            dx_q = K.ln_linear_dgrad(dq2, wq, xq2, mean_q, rstd_q, g_q, dres, True, gb(g_q), gb(b_q))
-            dkv2 = dkv.view(B * M, 2 * C)
-            dx_kv = K.ln_linear_dgrad(dkv2, wkv, xkv2, mean_kv, rstd_kv, g_kv, None, ctx.kv_grad, gb(g_kv), gb(b_kv))
             gbias = gb(bin_)
             if spec.packed:
                 gin = gb(ps[4])
@@ -247,8 +239,11 @@ class _LayerFn(torch.autograd.Function):
             else:
                 gwq = gb(ps[4])
                 gwkv = torch.zeros((2 * C, xkv2.shape[1]), **f32)
-            K.wgrad(dq2, xq2, 1, mean_q, rstd_q, g_q, b_q, _rows_per_wg(dq2.shape[0]), gwq, gbias[:C])
-            K.wgrad(dkv2, xkv2, 1, mean_kv, rstd_kv, g_kv, b_kv, _rows_per_wg(B * M), gwkv, gbias[C:])
+            dx_q = K.ln_linear_bwd(dq2, wq, xq2, mean_q, rstd_q, g_q, b_q, dres, True, gb(g_q), gb(b_q), gwq,
+                                   gbias[:C])
+            dkv2 = dkv.view(B * M, 2 * C)
+            dx_kv = K.ln_linear_bwd(dkv2, wkv, xkv2, mean_kv, rstd_kv, g_kv, b_kv, None, ctx.kv_grad, gb(g_kv),
+                                    gb(b_kv), gwkv, gbias[C:])
             if not spec.packed:
                 gb(ps[5]).add_(gwkv[:C])
                 gb(ps[6]).add_(gwkv[C:])
@@ -260,15 +255,10 @@ class _LayerFn(torch.autograd.Function):
             K.attn_bwd(qkv3[:, :, :C], qkv3[:, :, C:2 * C], qkv3[:, :, 2 * C:], kmask, o, do.view(B, Nq, C), lse,
                        delta3, H, D, scale, ctx.p_attn, ctx.seed, dqkv[:, :, :C], dqkv[:, :, C:2 * C],
                        dqkv[:, :, 2 * C:])
-            dqkv2 = dqkv.view(R, 3 * C)
-            dx_q = K.ln_linear_dgrad(dqkv2, wq, xq2, mean_q, rstd_q, g_q, dy, True, gb(g_q), gb(b_q))
-            K.wgrad(dqkv2, xq2, 1, mean_q, rstd_q, g_q, b_q, rpw, gb(ps[2]), gb(ps[3]))
+            dx_q = K.ln_linear_bwd(dqkv.view(R, 3 * C), wq, xq2, mean_q, rstd_q, g_q, b_q, dy, True, gb(g_q), gb(b_q),
+                                   gb(ps[2]), gb(ps[3]))
             dx_q = dx_q.view(B, Nq, C)
             dx_kv = None
-        # --- post-attention weights (out-proj, MLP) -------------------------------------------------
-        K.wgrad(dy, o2, 0, None, None, None, None, rpw, gb(Wo), gb(bo))
-        K.wgrad(du, y, 1, m2, r2, g2, be2, rpw, gb(W1), gb(b1))
-        K.wgrad(dz2, u, 2, None, None, None, None, rpw, gb(W2), gb(b2))
         # parameter gradients were accumulated in place (no autograd AccumulateGrad pass)
         return (None, None, None, None, dx_q, dx_kv, None) + (None,) * len(ps)
 

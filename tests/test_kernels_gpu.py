@@ -124,18 +124,18 @@ def test_post_attn(C, H):
         close(t1, t2, 2e-2, n)
     z, y, m, r, u = b
     dz = torch.randn(R, C, device=DEV)
-    ga = _ext().post_attn_bwd(dz, y, m, r, u, o, ws[0], ws[1], ws[2], g2, H)
-    gb = _emu().post_attn_bwd(dz, y, m, r, u, o, ws[0], ws[1], ws[2], g2, H)
-    close(ga[0], gb[0], 3e-2, "dy")
-    close(ga[1], gb[1], 3e-2, "du")
-    close(ga[2], gb[2], 3e-2, "dO")
-    close(ga[3], gb[3], 3e-2, "delta")
-    close(ga[4].sum(0), gb[4].sum(0), 3e-2, "dgamma")
-    close(ga[5].sum(0), gb[5].sum(0), 3e-2, "dbeta")
+    outs = []
+    names = ("dWo", "dbo", "dg2", "dbe2", "dW1", "db1", "dW2", "db2")
+    for K in (_ext(), _emu()):
+        grads = [torch.full((C, C) if n.startswith("dW") else (C,), 0.5, device=DEV) for n in names]  # accumulate
+        outs.append(tuple(K.post_attn_bwd(dz, y, m, r, u, o, ws[0], ws[1], ws[2], g2, be2, H, grads)) + tuple(grads))
+    ga, gb = outs
+    for i, n in enumerate(("dy", "dO", "delta") + names):
+        close(ga[i], gb[i], 3e-2, n)
 
 
 @pytest.mark.parametrize("R,N,Kin,gbf", [(300, 192, 64, False), (200, 128, 131, False), (129, 64, 64, True)])
-def test_dgrad_wgrad(R, N, Kin, gbf):
+def test_ln_linear_bwd_and_wgrad(R, N, Kin, gbf):
     torch.manual_seed(4)
     g = torch.randn(R, N, device=DEV)
     if gbf:
@@ -146,22 +146,29 @@ def test_dgrad_wgrad(R, N, Kin, gbf):
     mean = x.mean(-1)
     rstd = torch.rsqrt(x.var(-1, unbiased=False) + 1e-5)
     dres = torch.randn(R, Kin, device=DEV)
-    a = _ext().ln_linear_dgrad(g, w, x, mean, rstd, lw, dres, True)
-    b = _emu().ln_linear_dgrad(g, w, x, mean, rstd, lw, dres, True)
-    close(a[0], b[0], 3e-2, "dx")
-    close(a[1].sum(0), b[1].sum(0), 3e-2, "dgamma")
-    close(a[2].sum(0), b[2].sum(0), 3e-2, "dbeta")
+    res = []
+    for K in (_ext(), _emu()):
+        dg, db = torch.zeros(Kin, device=DEV), torch.zeros(Kin, device=DEV)
+        dW, dbias = torch.ones(N, Kin, device=DEV), torch.ones(N, device=DEV)  # accumulate onto existing grads
+        dx = K.ln_linear_bwd(g, w, x, mean, rstd, lw, lb, dres, True, dg, db, dW, dbias)
+        res.append((dx, dg, db, dW, dbias))
+    for i, n in enumerate(("dx", "dgamma", "dbeta", "dW", "dbias")):
+        close(res[0][i], res[1][i], 3e-2 if i < 4 else 1e-4, n)
+    # no-dx / no-LN variants
+    for K in (_ext(), _emu()):
+        assert K.ln_linear_bwd(g, w, x, None, None, None, None, None, False, None, None, None, None) is None
+    d1 = _ext().ln_linear_bwd(g, w, x, None, None, None, None, None, True, None, None, None, None)
+    d2 = _emu().ln_linear_bwd(g, w, x, None, None, None, None, None, True, None, None, None, None)
+    close(d1, d2, 3e-2, "dx no-LN")
     u = bf(torch.randn(R, Kin, device=DEV))
     for mode, A in ((0, x), (1, x), (2, u)):
-        sa = _ext().wgrad(g, A, mode, mean, rstd, lw, lb, 4, True)
-        sb = _emu().wgrad(g, A, mode, mean, rstd, lw, lb, 4, True)
-        close(sa[0].sum(0), sb[0].sum(0), 3e-2, f"dW mode {mode}")
-        close(sa[1].sum(0), sb[1].sum(0), 1e-4, f"db mode {mode}")
-    slabs = [torch.randn(5, 7, 3, device=DEV), torch.randn(3, 11, device=DEV)]
-    dsts = [torch.ones(7, 3, device=DEV), torch.ones(11, device=DEV)]
-    _ext().slab_reduce(slabs, dsts, [True, False])
-    close(dsts[0], slabs[0].sum(0) + 1, 1e-5, "reduce acc")
-    close(dsts[1], slabs[1].sum(0), 1e-5, "reduce")
+        outs = []
+        for K in (_ext(), _emu()):
+            dW, db = torch.ones(N, Kin, device=DEV), torch.ones(N, device=DEV)
+            K.wgrad(g, A, mode, mean, rstd, lw, lb, 64, dW, db)
+            outs.append((dW, db))
+        close(outs[0][0], outs[1][0], 3e-2, f"dW mode {mode}")
+        close(outs[0][1], outs[1][1], 1e-4, f"db mode {mode}")
 
 
 @pytest.mark.parametrize("M,V,C", [(300, 1000, 64), (77, 10003, 64), (64, 257, 128)])
