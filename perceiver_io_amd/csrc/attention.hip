@@ -22,8 +22,10 @@
 // Backward, per workgroup: 128 keys (32 per wave), sweeping every query tile:
 //   S = Q·K^T, dP = dO·V^T (query rows in registers, key on the lane),
 //   dV += P^T·dO and dK += dS^T·Q from the accumulators (transpose reads of the LDS Q/dO
-//   tiles), dQ via one LDS transpose of dS, summed over the 4 waves in LDS, then one
-//   fp32 atomic add per element per workgroup (SURVEY §2.3 K-07 backward).
+//   tiles), dQ via one LDS transpose of dS, summed over the waves in LDS; a single key block
+//   (Nk ≤ 256 for d ≤ 32) stores dQ outright, several add with fp32 atomics.
+// Both directions stage the next K/V (forward) or Q/dO (backward) tile in registers while
+// the current tile's MFMAs run, so global latency is paid once per kernel, not per tile.
 // Fully-masked query rows produce O = 0 and zero gradients (defect D10 defined).
 #include "common.h"
 
@@ -69,22 +71,25 @@ struct AttnArgs {
 // ------------------------------------------------------------------------------------
 // forward
 // ------------------------------------------------------------------------------------
-template <int D>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a, uint16_t* __restrict__ O, float* __restrict__ LSE,
-                                                       float* __restrict__ Opart, float* __restrict__ MLpart,
-                                                       int nsplit, int tiles_per_split) {
+template <int D, int NWV>
+__global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(AttnArgs a, uint16_t* __restrict__ O,
+                                                            float* __restrict__ LSE, float* __restrict__ Opart,
+                                                            float* __restrict__ MLpart, int nsplit,
+                                                            int tiles_per_split) {
   constexpr int LDK = D + 8;                 // K tile [key][d], 16-B padded rows
   constexpr int LDV = (D < 32 ? 32 : D) + 8;  // V tile [key][d]; D=16 zero-padded to 32 columns
   constexpr int NT = (D < 32) ? 1 : D / 32;   // O^T tiles of 32 rows (head-dim)
   constexpr int KS = D / 16;                  // k-steps for QK^T
+  constexpr int CH = D / 8;                   // 16-byte chunks per K/V row
+  constexpr int NTH = 64 * NWV, NI = (KT * CH + NTH - 1) / NTH;
+  constexpr bool PF = NI <= 4;  // next K/V tile prefetched into registers during this tile's math
   __shared__ __attribute__((aligned(16))) uint16_t sK[KT * LDK];
   __shared__ __attribute__((aligned(16))) uint16_t sV[KT * LDV + 64];
 
-  const int nwaves = blockDim.x >> 6;
   const int w = wave_id(), l = lane_id(), r = l & 31, hh = l >> 5;
   const int h = blockIdx.y;
   const int b = blockIdx.z / nsplit, split = blockIdx.z % nsplit;
-  const int q0 = (blockIdx.x * nwaves + w) * 32;
+  const int q0 = (blockIdx.x * NWV + w) * 32;
   const int qi = q0 + r;
   const int qc = qi < a.Nq ? qi : a.Nq - 1;
 
@@ -97,7 +102,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a, uint16_t* __r
   }
 
   if (D < 32) {  // zero the unused head-dim columns 16..31 of the V tile once
-    for (int i = threadIdx.x; i < KT; i += blockDim.x)
+    for (int i = threadIdx.x; i < KT; i += NTH)
       *reinterpret_cast<bf16x8*>(sV + i * LDV + 16) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0},
       *reinterpret_cast<bf16x8*>(sV + i * LDV + 24) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
   }
@@ -112,31 +117,61 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a, uint16_t* __r
   const int t_end = min(ntiles, t_begin + tiles_per_split);
   const uint16_t* kb = a.k + (long long)b * a.k_bs + h * D;
   const uint16_t* vb = a.v + (long long)b * a.v_bs + h * D;
-  constexpr int CH = D / 8;  // 16-byte chunks per row
+
+  // K/V tile staging: items c = tid + NTH·i of the tile's KT × CH 16-byte chunks
+  bf16x8 kreg[PF ? NI : 1], vreg[PF ? NI : 1];
+  bool pad_next = true;
+  auto fetch = [&](int t) {
+    const int key0 = t * KT;
+#pragma unroll
+    for (int i = 0; i < (PF ? NI : 1); ++i) {
+      const int c = threadIdx.x + NTH * i, key = key0 + c / CH, col = (c % CH) * 8;
+      kreg[i] = vreg[i] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (c < KT * CH && key < a.Nk) {
+        kreg[i] = *reinterpret_cast<const bf16x8*>(kb + (long long)key * a.k_rs + col);
+        vreg[i] = *reinterpret_cast<const bf16x8*>(vb + (long long)key * a.v_rs + col);
+      }
+    }
+    const int key = key0 + l;
+    pad_next = key >= a.Nk;
+    if (!pad_next && a.kmask) pad_next = a.kmask[(long long)b * a.Nk + key] != 0;
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < (PF ? NI : 1); ++i) {
+      const int c = threadIdx.x + NTH * i, kr = c / CH, col = (c % CH) * 8;
+      if (c < KT * CH) {
+        *reinterpret_cast<bf16x8*>(sK + kr * LDK + col) = kreg[i];
+        *reinterpret_cast<bf16x8*>(sV + kr * LDV + col) = vreg[i];
+      }
+    }
+  };
+  if (PF && t_begin < t_end) fetch(t_begin);
 
   for (int t = t_begin; t < t_end; ++t) {
     const int key0 = t * KT;
     __syncthreads();
-    for (int c = threadIdx.x; c < KT * CH; c += blockDim.x) {
-      const int kr = c / CH, col = (c % CH) * 8;
-      const int key = key0 + kr;
-      bf16x8 kv = bf16x8{0, 0, 0, 0, 0, 0, 0, 0}, vv = kv;
-      if (key < a.Nk) {
-        kv = *reinterpret_cast<const bf16x8*>(kb + (long long)key * a.k_rs + col);
-        vv = *reinterpret_cast<const bf16x8*>(vb + (long long)key * a.v_rs + col);
+    if constexpr (PF) {
+      store();
+    } else {
+      for (int c = threadIdx.x; c < KT * CH; c += NTH) {
+        const int kr = c / CH, col = (c % CH) * 8, key = key0 + kr;
+        bf16x8 kv = bf16x8{0, 0, 0, 0, 0, 0, 0, 0}, vv = kv;
+        if (key < a.Nk) {
+          kv = *reinterpret_cast<const bf16x8*>(kb + (long long)key * a.k_rs + col);
+          vv = *reinterpret_cast<const bf16x8*>(vb + (long long)key * a.v_rs + col);
+        }
+        *reinterpret_cast<bf16x8*>(sK + kr * LDK + col) = kv;
+        *reinterpret_cast<bf16x8*>(sV + kr * LDV + col) = vv;
       }
-      *reinterpret_cast<bf16x8*>(sK + kr * LDK + col) = kv;
-      *reinterpret_cast<bf16x8*>(sV + kr * LDV + col) = vv;
+      const int key = key0 + l;
+      pad_next = key >= a.Nk;
+      if (!pad_next && a.kmask) pad_next = a.kmask[(long long)b * a.Nk + key] != 0;
     }
     // key-padding bits for this tile (bit i = key0+i is padding or out of range)
-    uint64_t padbits;
-    {
-      const int key = key0 + l;
-      bool pad = key >= a.Nk;
-      if (!pad && a.kmask) pad = a.kmask[(long long)b * a.Nk + key] != 0;
-      padbits = __ballot(pad);
-    }
+    const uint64_t padbits = __ballot(pad_next);
     __syncthreads();
+    if (PF && t + 1 < t_end) fetch(t + 1);
 
     f32x16 s[2];
 #pragma unroll
@@ -271,36 +306,76 @@ __global__ void attn_bwd_prep_kernel(const uint16_t* __restrict__ dO, const uint
     for (int j = l; j < HD; j += 64) dq[(long long)row * dq_rs + j] = 0.f;
 }
 
-template <int D>
-__global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a, const uint16_t* __restrict__ dO,
-                                                       const float* __restrict__ LSE, const float* __restrict__ delta,
-                                                       float* __restrict__ dq, long long dq_bs, int dq_rs,
-                                                       float* __restrict__ dk, long long dk_bs, int dk_rs,
-                                                       float* __restrict__ dv, long long dv_bs, int dv_rs) {
+template <int D, int NW>
+__global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uint16_t* __restrict__ dO,
+                                                           const float* __restrict__ LSE,
+                                                           const float* __restrict__ delta, float* __restrict__ dq,
+                                                           long long dq_bs, int dq_rs, float* __restrict__ dk,
+                                                           long long dk_bs, int dk_rs, float* __restrict__ dv,
+                                                           long long dv_bs, int dv_rs, int dq_atomic) {
   constexpr int LD = (D < 32 ? 32 : D) + 8;  // Q / dO / K tiles [row][d] (D=16 zero-padded to 32 cols)
   constexpr int NT = (D < 32) ? 1 : D / 32;
   constexpr int KS = D / 16;
   constexpr int LDS_ = 40;                   // dS tile [key][q] (32 q + pad)
-  __shared__ __attribute__((aligned(16))) uint16_t sQ[32 * LD + 64];
-  __shared__ __attribute__((aligned(16))) uint16_t sdO[32 * LD + 64];
-  __shared__ __attribute__((aligned(16))) uint16_t sK[128 * LD + 64];
-  __shared__ __attribute__((aligned(16))) uint16_t sdS[4 * 32 * LDS_];
-  __shared__ float sL[32], sDl[32];
-  __shared__ float sdQ[4][32 * (D + 1)];
+  constexpr int KB = 32 * NW;                // keys per workgroup
+  constexpr int NTH = 64 * NW, CH = D / 8;
+  constexpr int NI = (2 * 32 * CH + NTH - 1) / NTH;  // Q + dO tile 16-B items per thread
+  __shared__ __attribute__((aligned(16))) uint16_t sQ[2][32 * LD + 64];
+  __shared__ __attribute__((aligned(16))) uint16_t sdO[2][32 * LD + 64];
+  __shared__ __attribute__((aligned(16))) uint16_t sK[KB * LD + 64];
+  __shared__ __attribute__((aligned(16))) uint16_t sdS[NW * 32 * LDS_];
+  __shared__ float sL[2][32], sDl[2][32];
+  __shared__ float sdQ[NW][32 * (D + 1)];
 
   const int w = wave_id(), l = lane_id(), r = l & 31, hh = l >> 5;
   const int h = blockIdx.y, b = blockIdx.z;
-  const int kbase = blockIdx.x * 128;
-  const int key = kbase + 32 * w + r;         // this lane's key (column of S / dP)
+  const int kbase = blockIdx.x * KB;
+  const int key = kbase + 32 * w + r;  // this lane's key (column of S / dP)
   const int kc = key < a.Nk ? key : a.Nk - 1;
   bool kpad = key >= a.Nk;
   if (!kpad && a.kmask) kpad = a.kmask[(long long)b * a.Nk + key] != 0;
 
-  // stage the block's K tile (for dQ) and zero padded columns
+  const int HD = a.H * D;
   const uint16_t* kbp = a.k + (long long)b * a.k_bs + h * D;
   const uint16_t* vbp = a.v + (long long)b * a.v_bs + h * D;
-  constexpr int CH = D / 8;
-  for (int c = threadIdx.x; c < 128 * CH; c += blockDim.x) {
+  const uint16_t* qbp = a.q + (long long)b * a.q_bs + h * D;
+  const uint16_t* dobp = dO + (long long)b * a.Nq * HD + h * D;
+  const int nqt = (a.Nq + 31) / 32;
+
+  // per-tile register staging: items c < 32·CH are Q chunks, the next 32·CH dO chunks;
+  // threads [0, 32) also carry the tile's LSE, [32, 64) its delta
+  bf16x8 qreg[NI];
+  float lreg = 0.f;
+  auto fetch = [&](int qt) {
+    const int q0 = qt * 32;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int c = threadIdx.x + NTH * i, isdo = c >= 32 * CH, cc = isdo ? c - 32 * CH : c;
+      const int qq = q0 + cc / CH, col = (cc % CH) * 8;
+      qreg[i] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (c < 64 * CH && qq < a.Nq)
+        qreg[i] = isdo ? *reinterpret_cast<const bf16x8*>(dobp + (long long)qq * HD + col)
+                       : *reinterpret_cast<const bf16x8*>(qbp + (long long)qq * a.q_rs + col);
+    }
+    if (threadIdx.x < 64) {
+      const int qq = q0 + (threadIdx.x & 31);
+      const long long idx = ((long long)b * a.Nq + qq) * a.H + h;
+      lreg = threadIdx.x < 32 ? (qq < a.Nq ? LSE[idx] : INFINITY) : (qq < a.Nq ? delta[idx] : 0.f);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int c = threadIdx.x + NTH * i, isdo = c >= 32 * CH, cc = isdo ? c - 32 * CH : c;
+      if (c < 64 * CH) *reinterpret_cast<bf16x8*>((isdo ? sdO[buf] : sQ[buf]) + (cc / CH) * LD + (cc % CH) * 8) = qreg[i];
+    }
+    if (threadIdx.x < 32) sL[buf][threadIdx.x] = lreg;
+    else if (threadIdx.x < 64) sDl[buf][threadIdx.x - 32] = lreg;
+  };
+  if (nqt > 0) fetch(0);
+
+  // stage the block's K tile (for dQ) and zero padded columns
+  for (int c = threadIdx.x; c < KB * CH; c += NTH) {
     const int kr = c / CH, col = (c % CH) * 8;
     const int kk = kbase + kr;
     bf16x8 kv = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
@@ -308,15 +383,16 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a, const uint16_
     *reinterpret_cast<bf16x8*>(sK + kr * LD + col) = kv;
   }
   if (D < 32) {
-    for (int i = threadIdx.x; i < 128; i += blockDim.x) {
+    for (int i = threadIdx.x; i < KB; i += NTH) {
       *reinterpret_cast<bf16x8*>(sK + i * LD + 16) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
       *reinterpret_cast<bf16x8*>(sK + i * LD + 24) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
     }
-    for (int i = threadIdx.x; i < 32; i += blockDim.x) {
-      *reinterpret_cast<bf16x8*>(sQ + i * LD + 16) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      *reinterpret_cast<bf16x8*>(sQ + i * LD + 24) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      *reinterpret_cast<bf16x8*>(sdO + i * LD + 16) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      *reinterpret_cast<bf16x8*>(sdO + i * LD + 24) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = threadIdx.x; i < 64; i += NTH) {
+      const int bb = i >> 5, rr = i & 31;
+      *reinterpret_cast<bf16x8*>(sQ[bb] + rr * LD + 16) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      *reinterpret_cast<bf16x8*>(sQ[bb] + rr * LD + 24) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      *reinterpret_cast<bf16x8*>(sdO[bb] + rr * LD + 16) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      *reinterpret_cast<bf16x8*>(sdO[bb] + rr * LD + 24) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
     }
   }
   // K^T / V^T operand fragments for this wave's 32 keys (B operand: B[k=d][col=key])
@@ -329,46 +405,28 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a, const uint16_
   f32x16 dK[NT], dV[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) dK[t] = dV[t] = f32x16{};
-
-  const int HD = a.H * D;
-  const uint16_t* qbp = a.q + (long long)b * a.q_bs + h * D;
-  const uint16_t* dobp = dO + (long long)b * a.Nq * HD + h * D;
-  const int nqt = (a.Nq + 31) / 32;
   uint16_t* mydS = sdS + w * 32 * LDS_;
 
   for (int qt = 0; qt < nqt; ++qt) {
-    const int q0 = qt * 32;
-    __syncthreads();
-    for (int c = threadIdx.x; c < 32 * CH; c += blockDim.x) {
-      const int qr = c / CH, col = (c % CH) * 8;
-      const int qq = q0 + qr;
-      bf16x8 qv = bf16x8{0, 0, 0, 0, 0, 0, 0, 0}, dv8 = qv;
-      if (qq < a.Nq) {
-        qv = *reinterpret_cast<const bf16x8*>(qbp + (long long)qq * a.q_rs + col);
-        dv8 = *reinterpret_cast<const bf16x8*>(dobp + (long long)qq * HD + col);
-      }
-      *reinterpret_cast<bf16x8*>(sQ + qr * LD + col) = qv;
-      *reinterpret_cast<bf16x8*>(sdO + qr * LD + col) = dv8;
-    }
-    if (threadIdx.x < 32) {
-      const int qq = q0 + threadIdx.x;
-      sL[threadIdx.x] = qq < a.Nq ? LSE[((long long)b * a.Nq + qq) * a.H + h] : INFINITY;
-      sDl[threadIdx.x] = qq < a.Nq ? delta[((long long)b * a.Nq + qq) * a.H + h] : 0.f;
-    }
-    __syncthreads();
+    const int q0 = qt * 32, buf = qt & 1;
+    store(buf);
+    __syncthreads();  // tile qt visible; last iteration's dQ reduction finished
+    if (qt + 1 < nqt) fetch(qt + 1);
+    const uint16_t* tQ = sQ[buf];
+    const uint16_t* tdO = sdO[buf];
 
     // S = Q K^T and dP = dO V^T  (rows: queries; lane: key)
     f32x16 S = f32x16{}, dP = f32x16{};
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      S = mfma32(frag_kc(sQ, LD, 0, 16 * s), kf[s], S);
-      dP = mfma32(frag_kc(sdO, LD, 0, 16 * s), vf[s], dP);
+      S = mfma32(frag_kc(tQ, LD, 0, 16 * s), kf[s], S);
+      dP = mfma32(frag_kc(tdO, LD, 0, 16 * s), vf[s], dP);
     }
     f32x16 P, dS;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int qr = acc_row(i, hh);
-      float p = kpad ? 0.f : exp2f(S[i] * a.scale_log2 - sL[qr]);
+      float p = kpad ? 0.f : exp2f(S[i] * a.scale_log2 - sL[buf][qr]);
       float dp = dP[i];
       float pd = p;
       if (a.drop_thresh) {
@@ -378,7 +436,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a, const uint16_
         dp = keep ? dp * a.drop_scale : 0.f;
       }
       P[i] = pd;
-      dS[i] = p * (dp - sDl[qr]);
+      dS[i] = p * (dp - sDl[buf][qr]);
     }
     // dV += P^T dO ; dK += dS^T Q   (accumulator as A operand: X^T · B)
 #pragma unroll
@@ -386,11 +444,12 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a, const uint16_
       const bf16x8 pa = pack_acc(P, ss), sa = pack_acc(dS, ss);
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        dV[t] = mfma32(pa, frag_ks_perm(sdO, LD, 32 * t, 16 * ss), dV[t]);
-        dK[t] = mfma32(sa, frag_ks_perm(sQ, LD, 32 * t, 16 * ss), dK[t]);
+        dV[t] = mfma32(pa, frag_ks_perm(tdO, LD, 32 * t, 16 * ss), dV[t]);
+        dK[t] = mfma32(sa, frag_ks_perm(tQ, LD, 32 * t, 16 * ss), dK[t]);
       }
     }
-    // dS -> LDS as [key][q] (bf16) for the dQ product
+    // this wave's dQ partial = dS (32 q × its 32 keys) · K (32 keys × d): dS goes through the
+    // wave's own LDS slab (no barrier needed), the partial into sdQ[w]
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       uint2 pk;
@@ -398,8 +457,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a, const uint16_
       pk.y = pack2(dS[4 * g + 2], dS[4 * g + 3]);
       *reinterpret_cast<uint2*>(mydS + r * LDS_ + 8 * g + 4 * hh) = pk;
     }
-    __syncthreads();
-    // dQ_part = dS (q × 32 keys of this wave) · K (32 keys × d)
+    asm volatile("" ::: "memory");  // keep the slab reads behind the writes (one wave: LDS is in order)
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       f32x16 dq_acc = f32x16{};
@@ -413,13 +471,17 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a, const uint16_
       }
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < 32 * D; e += blockDim.x) {
+    // Σ over the waves' key slices; a single key block owns dQ outright (plain store)
+    for (int e = threadIdx.x; e < 32 * D; e += NTH) {
       const int qr = e / D, dd = e % D;
       const int qq = q0 + qr;
       if (qq < a.Nq) {
-        const float v = (sdQ[0][qr * (D + 1) + dd] + sdQ[1][qr * (D + 1) + dd] + sdQ[2][qr * (D + 1) + dd] +
-                         sdQ[3][qr * (D + 1) + dd]) * a.scale;
-        atomicAdd(dq + (long long)b * dq_bs + (long long)qq * dq_rs + h * D + dd, v);
+        float v = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < NW; ++ww) v += sdQ[ww][qr * (D + 1) + dd];
+        float* dst = dq + (long long)b * dq_bs + (long long)qq * dq_rs + h * D + dd;
+        if (dq_atomic) atomicAdd(dst, v * a.scale);
+        else *dst = v * a.scale;
       }
     }
   }
@@ -438,17 +500,34 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a, const uint16_
     }
 }
 
+// zero rows of a strided fp32 (B, N, W) view (dQ accumulator when several key blocks add into it)
+__global__ void zero_rows_kernel(float* __restrict__ p, long long bs, int rs, int N, int W, long long total) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const long long row = i / W;
+    const int c = (int)(i - row * W);
+    const long long bb = row / N;
+    p[bb * bs + (row - bb * N) * rs + c] = 0.f;
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------
+template <int D, int NWV>
+static void fwd_launch_t(const AttnArgs& a, uint16_t* O, float* LSE, float* Opart, float* MLpart, int nsplit,
+                         hipStream_t st) {
+  const int ntiles = (a.Nk + KT - 1) / KT;
+  const int tps = (ntiles + nsplit - 1) / nsplit;
+  dim3 grid((a.Nq + 32 * NWV - 1) / (32 * NWV), a.H, a.B * nsplit);
+  hipLaunchKernelGGL((attn_fwd_kernel<D, NWV>), grid, dim3(64 * NWV), 0, st, a, O, LSE, Opart, MLpart, nsplit, tps);
+}
+
 template <int D>
 static void fwd_dispatch(const AttnArgs& a, uint16_t* O, float* LSE, float* Opart, float* MLpart, int nsplit,
                          hipStream_t st) {
-  const int nwaves = a.Nq <= 32 ? 1 : (a.Nq <= 64 ? 2 : 4);
-  const int ntiles = (a.Nk + KT - 1) / KT;
-  const int tps = (ntiles + nsplit - 1) / nsplit;
-  dim3 grid((a.Nq + 32 * nwaves - 1) / (32 * nwaves), a.H, a.B * nsplit);
-  hipLaunchKernelGGL(attn_fwd_kernel<D>, grid, dim3(64 * nwaves), 0, st, a, O, LSE, Opart, MLpart, nsplit, tps);
+  if (a.Nq <= 32) fwd_launch_t<D, 1>(a, O, LSE, Opart, MLpart, nsplit, st);
+  else if (a.Nq <= 64) fwd_launch_t<D, 2>(a, O, LSE, Opart, MLpart, nsplit, st);
+  else fwd_launch_t<D, 4>(a, O, LSE, Opart, MLpart, nsplit, st);
 }
 
 void attn_fwd_launch(const AttnArgs& a, int D, uint16_t* O, float* LSE, float* Opart, float* MLpart, int nsplit,
@@ -468,21 +547,35 @@ void attn_fwd_launch(const AttnArgs& a, int D, uint16_t* O, float* LSE, float* O
   }
 }
 
+template <int D, int NW>
+static void bwd_launch_t(const AttnArgs& a, const uint16_t* dO, const float* LSE, float* delta, float* dq,
+                         long long dq_bs, int dq_rs, float* dk, long long dk_bs, int dk_rs, float* dv, long long dv_bs,
+                         int dv_rs, hipStream_t st) {
+  const int nkb = (a.Nk + 32 * NW - 1) / (32 * NW);
+  if (nkb > 1) {  // several key blocks accumulate into dQ
+    const long long total = (long long)a.B * a.Nq * a.H * D;
+    hipLaunchKernelGGL(zero_rows_kernel, dim3((unsigned)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096)), dim3(256), 0,
+                       st, dq, dq_bs, dq_rs, a.Nq, a.H * D, total);
+  }
+  dim3 grid(nkb, a.H, a.B);
+  hipLaunchKernelGGL((attn_bwd_kernel<D, NW>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs, dk,
+                     dk_bs, dk_rs, dv, dv_bs, dv_rs, nkb > 1 ? 1 : 0);
+}
+
 void attn_bwd_launch(const AttnArgs& a, int D, const uint16_t* O, const uint16_t* dO, const float* LSE, float* delta,
                      float* dq, long long dq_bs, int dq_rs, float* dk, long long dk_bs, int dk_rs, float* dv,
                      long long dv_bs, int dv_rs, bool compute_delta, hipStream_t st) {
-  // dQ must arrive zero-filled (it is accumulated with atomics).  delta = rowsum(dO∘O) is
-  // normally produced by the post-attention backward kernel; compute it here otherwise.
+  // delta = rowsum(dO∘O) is normally produced by the post-attention backward kernel;
+  // compute it here otherwise.  dQ needs no zero fill from the caller.
   const int rows = a.B * a.Nq;
   if (compute_delta)
     hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, dO, O, delta, (float*)nullptr,
                        rows, a.H, D, dq_rs);
-  dim3 grid((a.Nk + 127) / 128, a.H, a.B);
-  switch (D) {
-    case 16: hipLaunchKernelGGL(attn_bwd_kernel<16>, grid, dim3(256), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs); break;
-    case 32: hipLaunchKernelGGL(attn_bwd_kernel<32>, grid, dim3(256), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs); break;
-    case 64: hipLaunchKernelGGL(attn_bwd_kernel<64>, grid, dim3(256), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs); break;
-    case 128: hipLaunchKernelGGL(attn_bwd_kernel<128>, grid, dim3(256), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs); break;
+  switch (D) {  // waves per workgroup: 8 for d ≤ 32, 4 above (keys per block = 32 × waves)
+    case 16: bwd_launch_t<16, 8>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, st); break;
+    case 32: bwd_launch_t<32, 8>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, st); break;
+    case 64: bwd_launch_t<64, 4>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, st); break;
+    case 128: bwd_launch_t<128, 4>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, st); break;
     default: break;
   }
 }

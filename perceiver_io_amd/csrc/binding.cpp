@@ -132,8 +132,8 @@ std::vector<Tensor> attn_fwd(Tensor q, Tensor k, Tensor v, OptT kmask, int64_t H
 
 // returns (dq, dk, dv) fp32; dq is per batch even when q is batch-broadcast.  Optional
 // *_out tensors (B, N, >=HD views, unit inner stride) let the results land in packed buffers;
-// a dq_out view must be batch-dense (batch stride == Nq * row stride) and ZERO-FILLED (dQ is
-// accumulated with atomics).  delta_in ((B, Nq, H) fp32 rowsum(dO∘O), e.g. from post_attn_bwd)
+// a dq_out view must be batch-dense (batch stride == Nq * row stride); it needs no zero fill
+// (the launcher clears it itself when several key blocks accumulate into it).  delta_in ((B, Nq, H) fp32 rowsum(dO∘O), e.g. from post_attn_bwd)
 // skips the delta pass.
 std::vector<Tensor> attn_bwd(Tensor q, Tensor k, Tensor v, OptT kmask, Tensor o, Tensor dO, Tensor lse, OptT delta_in,
                              int64_t H, int64_t D, double scale, double dropout_p, int64_t seed, OptT dq_out,
@@ -141,7 +141,7 @@ std::vector<Tensor> attn_bwd(Tensor q, Tensor k, Tensor v, OptT kmask, Tensor o,
   auto a = make_args(q, k, v, kmask, (int)H, (int)D, scale, dropout_p, seed);
   TORCH_CHECK(dO.is_contiguous() && o.is_contiguous(), "O / dO must be contiguous (B, Nq, H*D)");
   auto f32 = q.options().dtype(torch::kFloat32);
-  Tensor dq = dq_out.has_value() ? *dq_out : torch::zeros({a.B, a.Nq, H * D}, f32);
+  Tensor dq = dq_out.has_value() ? *dq_out : torch::empty({a.B, a.Nq, H * D}, f32);
   Tensor dk = dk_out.has_value() ? *dk_out : torch::empty({a.B, a.Nk, H * D}, f32);
   Tensor dv = dv_out.has_value() ? *dv_out : torch::empty({a.B, a.Nk, H * D}, f32);
   TORCH_CHECK(dq.stride(2) == 1 && dk.stride(2) == 1 && dv.stride(2) == 1, "dq/dk/dv need unit inner stride");

@@ -115,9 +115,209 @@ struct PostAttnGrads {
 __host__ __device__ __forceinline__ int round_up(int x, int m) { return (x + m - 1) / m * m; }
 
 // ------------------------------------------------------------------------------------
-// LayerNorm(+)Linear forward
+// row-pass layout
+// A 256-thread block owns a 64-row tile.  For row-wise work (LayerNorm statistics and
+// backward, residual adds, vectorised loads/stores) thread t owns row t >> 2 and the
+// 8-column chunks (t & 3) + 4j, j < NCH = ceil(K / 32).  Lanes 4r + p of wave w hold tile
+// row 16w + r, so a row reduction is two DPP quad permutes and a column reduction over the
+// wave's 16 rows is two DPP row rotations plus two cross-row shuffles.  Every global load of
+// a phase is issued before its first use, so a kernel pays the memory latency once per
+// phase instead of once per row.
 // ------------------------------------------------------------------------------------
-template <typename TIn, typename TOut>
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float quad_sum(float v) {  // over lanes 4r .. 4r+3
+  v += dpp<0xB1>(v);                                    // quad_perm [1,0,3,2]
+  v += dpp<0x4E>(v);                                    // quad_perm [2,3,0,1]
+  return v;
+}
+__device__ __forceinline__ float rows16_sum(float v) {  // over lanes ≡ l (mod 4)
+  v += dpp<0x124>(v);                                     // row_ror:4
+  v += dpp<0x128>(v);                                     // row_ror:8
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+__device__ __forceinline__ int rp_row() { return threadIdx.x >> 2; }
+__device__ __forceinline__ int rp_col(int j) { return 8 * ((threadIdx.x & 3) + 4 * j); }
+__device__ __forceinline__ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// row gr (< R) of a row-major [.. × K] matrix, this thread's chunks; zero outside
+template <int NCH, typename T>
+__device__ __forceinline__ void row_load(float (&v)[NCH][8], const T* __restrict__ base, long long rs, int gr, int R,
+                                         int K, bool vec) {
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    const int c = rp_col(j);
+    const T* src = base + (long long)gr * rs + c;
+    if (vec && gr < R && c + 8 <= K) {
+      if constexpr (sizeof(T) == 2) {
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(src);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[j][e] = bf2f(b[e]);
+      } else {
+        const float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
+        v[j][0] = a.x; v[j][1] = a.y; v[j][2] = a.z; v[j][3] = a.w;
+        v[j][4] = b.x; v[j][5] = b.y; v[j][6] = b.z; v[j][7] = b.w;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[j][e] = (gr < R && c + e < K) ? ldf(src + e) : 0.f;
+    }
+  }
+}
+
+template <int NCH, typename T>
+__device__ __forceinline__ void row_store(const float (&v)[NCH][8], T* __restrict__ base, long long rs, int gr, int R,
+                                          int K, bool vec) {
+  if (gr >= R) return;
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    const int c = rp_col(j);
+    if (c >= K) continue;
+    T* dst = base + (long long)gr * rs + c;
+    if (vec && c + 8 <= K) {
+      if constexpr (sizeof(T) == 2) {
+        bf16x8 b;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) b[e] = (short)f2bf(v[j][e]);
+        *reinterpret_cast<bf16x8*>(dst) = b;
+      } else {
+        *reinterpret_cast<float4*>(dst) = make_float4(v[j][0], v[j][1], v[j][2], v[j][3]);
+        *reinterpret_cast<float4*>(dst + 4) = make_float4(v[j][4], v[j][5], v[j][6], v[j][7]);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (c + e < K) stf(dst + e, v[j][e]);
+    }
+  }
+}
+
+// LDS row access (this thread's row and chunks); tiles are ≥ 32·NCH columns wide
+template <int NCH>
+__device__ __forceinline__ void lds_row_read(float (&v)[NCH][8], const float* s, int ld) {
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    const float* p = s + rp_row() * ld + rp_col(j);
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    v[j][0] = a.x; v[j][1] = a.y; v[j][2] = a.z; v[j][3] = a.w;
+    v[j][4] = b.x; v[j][5] = b.y; v[j][6] = b.z; v[j][7] = b.w;
+  }
+}
+template <int NCH>
+__device__ __forceinline__ void lds_row_write(float* s, int ld, const float (&v)[NCH][8]) {
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    float* p = s + rp_row() * ld + rp_col(j);
+    *reinterpret_cast<float4*>(p) = make_float4(v[j][0], v[j][1], v[j][2], v[j][3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(v[j][4], v[j][5], v[j][6], v[j][7]);
+  }
+}
+template <int NCH>
+__device__ __forceinline__ void lds_row_write_bf16(uint16_t* s, int ld, const float (&v)[NCH][8]) {
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    bf16x8 b;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) b[e] = (short)f2bf(v[j][e]);
+    *reinterpret_cast<bf16x8*>(s + rp_row() * ld + rp_col(j)) = b;
+  }
+}
+
+// per-thread column values → per-wave column sums in sPart[w][·] (KP-strided); callers
+// barrier, then colsum_flush adds the four wave partials into the fp32 gradient
+template <int NCH>
+__device__ __forceinline__ void colsum_partial(const float (&v)[NCH][8], float* sPart, int KP) {
+  const int l = lane_id(), w = wave_id();
+#pragma unroll
+  for (int j = 0; j < NCH; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float s = rows16_sum(v[j][e]);
+      if (l < 4) sPart[w * KP + rp_col(j) + e] = s;
+    }
+}
+__device__ __forceinline__ void colsum_flush(const float* sPart, int KP, float* __restrict__ dst, int K) {
+  for (int k = threadIdx.x; k < K; k += blockDim.x)
+    atomicAdd(dst + k, sPart[k] + sPart[KP + k] + sPart[2 * KP + k] + sPart[3 * KP + k]);
+}
+
+// rows [r0, r0 + rows) × cols [0, KP) of a bf16 row-major matrix → registers (zero beyond
+// Rmax rows / K cols), then → an LDS tile [rows][ld]; NI = ceil(rows·KP / 2048)
+template <int NI>
+__device__ __forceinline__ void tile_fetch(bf16x8 (&b)[NI], const uint16_t* __restrict__ src, long long rs, int r0,
+                                           int Rmax, int rows, int K, int KP, bool vec) {
+  const int cpr = KP >> 3;
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int e = threadIdx.x + 256 * i, rr = e / cpr, cc = (e - rr * cpr) * 8, gr = r0 + rr;
+    b[i] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (rr < rows && gr < Rmax && cc < K) {
+      const uint16_t* p = src + (long long)gr * rs + cc;
+      if (vec && cc + 8 <= K) {
+        b[i] = *reinterpret_cast<const bf16x8*>(p);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) b[i][q] = cc + q < K ? (short)p[q] : (short)0;
+      }
+    }
+  }
+}
+template <int NI>
+__device__ __forceinline__ void tile_store(const bf16x8 (&b)[NI], uint16_t* s, int ld, int rows, int KP) {
+  const int cpr = KP >> 3;
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int e = threadIdx.x + 256 * i, rr = e / cpr, cc = (e - rr * cpr) * 8;
+    if (rr < rows) *reinterpret_cast<bf16x8*>(s + rr * ld + cc) = b[i];
+  }
+}
+
+// 64 × 64 chunk of a gradient matrix G (cols [nc, nc+64)) in the staging layout
+// (thread t: rows t>>3 and 32 + (t>>3), cols 8(t&7) .. +8), kept in fp32 for the bias sums
+template <typename TG>
+__device__ __forceinline__ void g_fetch(float (&v)[2][8], const TG* __restrict__ G, int g_rs, int m0, int R, int nc,
+                                        int N, bool vec) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int rr = (threadIdx.x >> 3) + 32 * i, cc = (threadIdx.x & 7) * 8, gr = m0 + rr, gc = nc + cc;
+    const TG* p = G + (long long)gr * g_rs + gc;
+    if (vec && gr < R && gc + 8 <= N) {
+      if constexpr (sizeof(TG) == 2) {
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[i][e] = bf2f(b[e]);
+      } else {
+        const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+        v[i][0] = a.x; v[i][1] = a.y; v[i][2] = a.z; v[i][3] = a.w;
+        v[i][4] = b.x; v[i][5] = b.y; v[i][6] = b.z; v[i][7] = b.w;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[i][e] = (gr < R && gc + e < N) ? ldf(p + e) : 0.f;
+    }
+  }
+}
+__device__ __forceinline__ void g_store(const float (&v)[2][8], uint16_t* sG, int ldg) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    bf16x8 b;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) b[e] = (short)f2bf(v[i][e]);
+    *reinterpret_cast<bf16x8*>(sG + ((threadIdx.x >> 3) + 32 * i) * ldg + (threadIdx.x & 7) * 8) = b;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// LayerNorm(+)Linear forward: Y = act(LN(X)·Wᵀ + b) (+ res), one 64-row tile per block.
+// Phase 0 issues the X rows, LN affine and the first 64-row W chunk together; LN runs in
+// registers (row-pass layout) into a resident bf16 tile; W chunks are double-buffered
+// through registers; each 64-column output chunk leaves through LDS as 16-byte row stores.
+// ------------------------------------------------------------------------------------
+template <typename TIn, typename TOut, int NCH>
 __global__ __launch_bounds__(256) void ln_linear_fwd_kernel(const TIn* __restrict__ X, int x_rs, int R, int Kin,
                                                             const float* __restrict__ lnw, const float* __restrict__ lnb,
                                                             float eps, const uint16_t* __restrict__ W,
@@ -125,68 +325,80 @@ __global__ __launch_bounds__(256) void ln_linear_fwd_kernel(const TIn* __restric
                                                             const float* __restrict__ res, int res_rs,
                                                             TOut* __restrict__ Y, int y_rs, float* __restrict__ mean_out,
                                                             float* __restrict__ rstd_out) {
+  constexpr int KP = 32 * NCH, LD = KP + 8, LDO = 64 + 4;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  const int KP = round_up(Kin, 16), ld = KP + 8;
-  uint16_t* sA = smem;
-  uint16_t* sB = smem + 64 * ld;
-  const int m0 = blockIdx.x * 64;
-  const int w = wave_id(), l = lane_id();
+  uint16_t* sA = smem;                                  // [64][LD]  LN(X), bf16
+  uint16_t* sW = sA + 64 * LD;                          // [64][LD]  W chunk
+  float* sO = reinterpret_cast<float*>(sW + 64 * LD);   // [64][LDO] output chunk
+  const int m0 = blockIdx.x * 64, gr = m0 + rp_row(), w = wave_id(), l = lane_id();
+  const bool wvec = (Kin & 7) == 0 && aligned16(W);
+  const bool yvec = (N & 7) == 0 && (y_rs & 7) == 0 && aligned16(Y);
 
-  // LN prologue once per 64-row tile (one wave per row, x row cached in registers), then all
-  // N columns of the output are produced 64 at a time against the resident normalised tile
-  float gw[4], gb[4];
+  float xv[NCH][8];
+  row_load<NCH>(xv, X, x_rs, gr, R, Kin, (Kin & 7) == 0 && (x_rs & 7) == 0 && aligned16(X));
+  bf16x8 wb[NCH];
+  tile_fetch<NCH>(wb, W, Kin, 0, N, 64, Kin, KP, wvec);
+  if (lnw) {
+    float gw[NCH][8], gb[NCH][8];
+    const bool pvec = (Kin & 7) == 0 && aligned16(lnw) && aligned16(lnb);
+    row_load<NCH>(gw, lnw, 0, 0, 1, Kin, pvec);
+    row_load<NCH>(gb, lnb, 0, 0, 1, Kin, pvec);
+    float s = 0.f;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int k = l + 64 * j;
-    gw[j] = (lnw && k < Kin) ? lnw[k] : 1.f;
-    gb[j] = (lnw && k < Kin) ? lnb[k] : 0.f;
-  }
-  for (int rr = w; rr < 64; rr += 4) {
-    const int gr = m0 + rr;
-    float xv[4] = {0.f, 0.f, 0.f, 0.f};
-    if (gr < R) {
-      const TIn* xr = X + (long long)gr * x_rs;
+    for (int j = 0; j < NCH; ++j)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (l + 64 * j < Kin) xv[j] = ldf(xr + l + 64 * j);
-      if (lnw) {
-        const float mean = wave_sum(xv[0] + xv[1] + xv[2] + xv[3]) / Kin;
-        float v = 0.f;
+      for (int e = 0; e < 8; ++e) s += xv[j][e];
+    const float mean = quad_sum(s) / Kin;
+    float q = 0.f;
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (l + 64 * j < Kin) v += (xv[j] - mean) * (xv[j] - mean);
-        const float rstd = rsqrtf(wave_sum(v) / Kin + eps);
-        if (l == 0 && mean_out) { mean_out[gr] = mean; rstd_out[gr] = rstd; }
+    for (int j = 0; j < NCH; ++j)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) xv[j] = (xv[j] - mean) * rstd * gw[j] + gb[j];
+      for (int e = 0; e < 8; ++e) {
+        const float d = rp_col(j) + e < Kin ? xv[j][e] - mean : 0.f;
+        q += d * d;
       }
-    }
+    const float rstd = rsqrtf(quad_sum(q) / Kin + eps);
+    if ((threadIdx.x & 3) == 0 && gr < R && mean_out) { mean_out[gr] = mean; rstd_out[gr] = rstd; }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int k = l + 64 * j;
-      if (k < KP) sA[rr * ld + k] = (gr < R && k < Kin) ? f2bf(xv[j]) : (uint16_t)0;
-    }
+    for (int j = 0; j < NCH; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xv[j][e] = (xv[j][e] - mean) * rstd * gw[j][e] + gb[j][e];
   }
+  lds_row_write_bf16<NCH>(sA, LD, xv);
+
   for (int n0 = 0; n0 < N; n0 += 64) {
-    stage(sB, ld, W, Kin, n0, N, 0, Kin, 64, KP);
+    tile_store<NCH>(wb, sW, LD, 64, KP);
     __syncthreads();
+    if (n0 + 64 < N) tile_fetch<NCH>(wb, W, Kin, n0 + 64, N, 64, Kin, KP, wvec);
+    const int bc = n0 + 32 * (w & 1) + (l & 31);
+    const float bv = (bias && bc < N) ? bias[bc] : 0.f;
     f32x16 acc[1] = {f32x16{}};
-    tile_gemm<1, true, true>(sA, ld, sB, ld, 64, 64, KP, acc);
+    tile_gemm<1, true, true>(sA, LD, sW, LD, 64, 64, KP, acc);
     for_acc<1>(64, 64, [&](int t, int m, int n, int i) {
-      const int gr = m0 + m, gc = n0 + n;
-      if (gr < R && gc < N) {
-        float v = acc[t][i] + (bias ? bias[gc] : 0.f);
-        if (act == 1) v = gelu_f(v);
-        if (res) v += res[(long long)gr * res_rs + gc];
-        stf(Y + (long long)gr * y_rs + gc, v);
-      }
+      float v = acc[t][i] + bv;
+      if (act == 1) v = gelu_f(v);
+      sO[m * LDO + n] = v;
     });
     __syncthreads();
+    float ov[2][8];
+    lds_row_read<2>(ov, sO, LDO);
+    if (res) {
+      float rv[2][8];
+      row_load<2>(rv, res + n0, res_rs, gr, R, N - n0, false);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ov[j][e] += rv[j][e];
+    }
+    row_store<2>(ov, Y + n0, y_rs, gr, R, N - n0, yvec && aligned16(Y + n0));
   }
 }
 
 // ------------------------------------------------------------------------------------
 // post-attention block forward: Z = Y + W2·gelu(W1·LN2(Y) + b1) + b2, Y = X + Wo·O + bo
+// Phase 0 fetches the O tile, the X rows and (C ≤ 64) all three weights; the three GEMMs
+// then run back to back on LDS with row-pass epilogues (LN2 in registers, 16-byte stores).
+// For C = 128 the weights share one LDS buffer, each fetched during the previous GEMM.
 // ------------------------------------------------------------------------------------
 template <int C>
 __global__ __launch_bounds__(256) void post_attn_fwd_kernel(
@@ -195,63 +407,101 @@ __global__ __launch_bounds__(256) void post_attn_fwd_kernel(
     const uint16_t* __restrict__ W1, const float* __restrict__ b1, const uint16_t* __restrict__ W2,
     const float* __restrict__ b2, float* __restrict__ Z, float* __restrict__ Ysave, float* __restrict__ mean2,
     float* __restrict__ rstd2, uint16_t* __restrict__ Usave, int R) {
-  constexpr int LD = C + 8, LDF = C + 4, MAXT = (2 * C / 32 + 3) / 4;
-  __shared__ __attribute__((aligned(16))) uint16_t sA[64 * LD];
-  __shared__ __attribute__((aligned(16))) uint16_t sW[C * LD];
-  __shared__ __attribute__((aligned(16))) float sY[64 * LDF];
-  const int m0 = blockIdx.x * 64;
-  const int w = wave_id(), l = lane_id();
+  constexpr int LD = C + 8, LDF = C + 4, MAXT = (2 * C / 32 + 3) / 4, NCH = C / 32;
+  constexpr int NWB = C <= 64 ? 3 : 1, NIW = (C * C / 8 + 255) / 256;
+  __shared__ __attribute__((aligned(16))) uint16_t sA[64 * LD];   // O → LN2(Y) → GELU(U)
+  __shared__ __attribute__((aligned(16))) uint16_t sW[NWB][C * LD];
+  __shared__ __attribute__((aligned(16))) float sF[64 * LDF];
+  __shared__ float sP[5][C];  // bo, b1, b2, γ2, β2
+  const int m0 = blockIdx.x * 64, gr = m0 + rp_row();
+  const bool av = aligned16(O) && aligned16(X) && aligned16(Z) && aligned16(Ysave) && aligned16(Usave) &&
+                  aligned16(Wo) && aligned16(W1) && aligned16(W2);
 
-  stage(sA, LD, O, C, m0, R, 0, C, 64, C);
-  stage(sW, LD, Wo, C, 0, C, 0, C, C, C);
+  bf16x8 ob[NCH];
+  tile_fetch<NCH>(ob, O, C, m0, R, 64, C, C, av);
+  bf16x8 wr[NWB][NIW];
+  tile_fetch<NIW>(wr[0], Wo, C, 0, C, C, C, C, av);
+  if constexpr (NWB == 3) {
+    tile_fetch<NIW>(wr[1], W1, C, 0, C, C, C, C, av);
+    tile_fetch<NIW>(wr[2], W2, C, 0, C, C, C, C, av);
+  }
+  float yv[NCH][8];
+  row_load<NCH>(yv, X, C, gr, R, C, av);
+  for (int k = threadIdx.x; k < C; k += blockDim.x) {
+    sP[0][k] = bo[k]; sP[1][k] = b1[k]; sP[2][k] = b2[k]; sP[3][k] = g2[k]; sP[4][k] = be2[k];
+  }
+  tile_store<NCH>(ob, sA, LD, 64, C);
+#pragma unroll
+  for (int b = 0; b < NWB; ++b) tile_store<NIW>(wr[b], sW[b], LD, C, C);
   __syncthreads();
+  if constexpr (NWB == 1) tile_fetch<NIW>(wr[0], W1, C, 0, C, C, C, C, av);
   f32x16 acc[MAXT];
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
-  tile_gemm<MAXT, true, true>(sA, LD, sW, LD, 64, C, C, acc);
-  for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) {
-    const int gr = m0 + m;
-    float y = 0.f;
-    if (gr < R) {
-      y = X[(long long)gr * C + n] + acc[t][i] + bo[n];
-      Ysave[(long long)gr * C + n] = y;
-    }
-    sY[m * LDF + n] = y;
-  });
+  tile_gemm<MAXT, true, true>(sA, LD, sW[0], LD, 64, C, C, acc);
+  for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) { sF[m * LDF + n] = acc[t][i] + sP[0][n]; });
   __syncthreads();
-  // LN2 (one wave per row) → sA ; W1 → sW
-  for (int rr = w; rr < 64; rr += 4) {
+  if constexpr (NWB == 1) tile_store<NIW>(wr[0], sW[0], LD, C, C);
+  // Y = X + attn-out; LN2 → sA
+  {
+    float t[NCH][8];
+    lds_row_read<NCH>(t, sF, LDF);
     float s = 0.f;
-    for (int k = l; k < C; k += 64) s += sY[rr * LDF + k];
-    const float mean = wave_sum(s) / C;
-    float v = 0.f;
-    for (int k = l; k < C; k += 64) { const float d = sY[rr * LDF + k] - mean; v += d * d; }
-    const float rstd = rsqrtf(wave_sum(v) / C + eps);
-    const int gr = m0 + rr;
-    if (l == 0 && gr < R) { mean2[gr] = mean; rstd2[gr] = rstd; }
-    for (int k = l; k < C; k += 64) sA[rr * LD + k] = f2bf((sY[rr * LDF + k] - mean) * rstd * g2[k] + be2[k]);
+#pragma unroll
+    for (int j = 0; j < NCH; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { yv[j][e] += t[j][e]; s += yv[j][e]; }
+    row_store<NCH>(yv, Ysave, C, gr, R, C, av);
+    const float mean = quad_sum(s) / C;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < NCH; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { const float d = yv[j][e] - mean; q += d * d; }
+    const float rstd = rsqrtf(quad_sum(q) / C + eps);
+    if ((threadIdx.x & 3) == 0 && gr < R) { mean2[gr] = mean; rstd2[gr] = rstd; }
+#pragma unroll
+    for (int j = 0; j < NCH; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = rp_col(j) + e;
+        t[j][e] = (yv[j][e] - mean) * rstd * sP[3][c] + sP[4][c];
+      }
+    lds_row_write_bf16<NCH>(sA, LD, t);
   }
-  stage(sW, LD, W1, C, 0, C, 0, C, C, C);
+  __syncthreads();
+  if constexpr (NWB == 1) tile_fetch<NIW>(wr[0], W2, C, 0, C, C, C, C, av);
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
+  tile_gemm<MAXT, true, true>(sA, LD, sW[NWB == 3 ? 1 : 0], LD, 64, C, C, acc);
+  for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) { sF[m * LDF + n] = acc[t][i] + sP[1][n]; });
+  __syncthreads();
+  if constexpr (NWB == 1) tile_store<NIW>(wr[0], sW[0], LD, C, C);
+  {
+    float u[NCH][8];
+    lds_row_read<NCH>(u, sF, LDF);
+    row_store<NCH>(u, Usave, C, gr, R, C, av);
+#pragma unroll
+    for (int j = 0; j < NCH; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) u[j][e] = gelu_f(u[j][e]);
+    lds_row_write_bf16<NCH>(sA, LD, u);
+  }
   __syncthreads();
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
-  tile_gemm<MAXT, true, true>(sA, LD, sW, LD, 64, C, C, acc);
-  __syncthreads();  // everyone done reading sA / sW
-  for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) {
-    const int gr = m0 + m;
-    const float u = acc[t][i] + b1[n];
-    if (gr < R) Usave[(long long)gr * C + n] = f2bf(u);
-    sA[m * LD + n] = f2bf(gelu_f(u));
-  });
-  stage(sW, LD, W2, C, 0, C, 0, C, C, C);
+  tile_gemm<MAXT, true, true>(sA, LD, sW[NWB == 3 ? 2 : 0], LD, 64, C, C, acc);
+  for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) { sF[m * LDF + n] = acc[t][i] + sP[2][n]; });
   __syncthreads();
+  {
+    float z[NCH][8];
+    lds_row_read<NCH>(z, sF, LDF);
 #pragma unroll
-  for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
-  tile_gemm<MAXT, true, true>(sA, LD, sW, LD, 64, C, C, acc);
-  for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) {
-    const int gr = m0 + m;
-    if (gr < R) Z[(long long)gr * C + n] = sY[m * LDF + n] + acc[t][i] + b2[n];
-  });
+    for (int j = 0; j < NCH; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) z[j][e] += yv[j][e];
+    row_store<NCH>(z, Z, C, gr, R, C, av);
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -331,10 +581,12 @@ __device__ __forceinline__ void wgrad_tile(const uint16_t* sG, int ldg, const ui
 // post-attention block backward, one 64-row tile, weight gradients included:
 //   dH = dZ·W2, dW2 += dZᵀ·GELU(U), db2 += Σ dZ
 //   dU = dH∘GELU'(U), dXn2 = dU·W1, dW1 += dUᵀ·LN2(Y), db1 += Σ dU
-//   dY = dZ + LN2_bwd(dXn2), dγ2/dβ2 partials
+//   dY = dZ + LN2_bwd(dXn2), dγ2 += Σ dXn2∘Ŷ, dβ2 += Σ dXn2
 //   dO = dY·Wo, dWo += dYᵀ·O, dbo += Σ dY, delta = rowsum_head(dO∘O)
 // The gradient tile (sG) and its matching activation tile (sX) sit side by side in LDS, so
-// each weight gradient is one extra MFMA pass over tiles that are already resident.
+// each weight gradient is one extra MFMA pass over resident tiles.  Phase 0 fetches dZ, Y,
+// U, O and (C ≤ 64) all weights at once; the rest of the kernel touches global memory only
+// to store results and to add parameter gradients.
 // ------------------------------------------------------------------------------------
 template <int C>
 __global__ __launch_bounds__(256) void post_attn_bwd_kernel(
@@ -344,238 +596,319 @@ __global__ __launch_bounds__(256) void post_attn_bwd_kernel(
     const float* __restrict__ g2, const float* __restrict__ be2, float* __restrict__ dY, uint16_t* __restrict__ dO,
     float* __restrict__ delta, int H, PostAttnGrads gr_out, int R) {
   constexpr int LD = C + 8, LDF = C + 4, MAXT = (2 * C / 32 + 3) / 4, MAXW = ((C / 32) * (C / 32) + 3) / 4;
-  constexpr int NJ = (C + 63) / 64, GRP = 256 / C, RPG = 64 / GRP;
+  constexpr int NCH = C / 32, NWB = C <= 64 ? 3 : 1, NIW = (C * C / 8 + 255) / 256;
   __shared__ __attribute__((aligned(16))) uint16_t sG[64 * LD];  // dZ → dU → dY
   __shared__ __attribute__((aligned(16))) uint16_t sX[64 * LD];  // GELU(U) → LN2(Y) → O
-  __shared__ __attribute__((aligned(16))) uint16_t sW[C * LD];   // W2 → W1 → Wo
-  __shared__ __attribute__((aligned(16))) float sF[64 * LDF];
-  __shared__ float sPart[4][4][C];  // per-wave column partials: dγ2, dβ2, Σ dY, Σ dZ
-  const int m0 = blockIdx.x * 64;
-  const int w = wave_id(), l = lane_id();
+  __shared__ __attribute__((aligned(16))) uint16_t sW[NWB][C * LD];  // W2, W1, Wo
+  __shared__ __attribute__((aligned(16))) float sF[64 * LDF];    // GELU'(U) → dU → dXn2 → dO
+  __shared__ __attribute__((aligned(16))) float sPart[4][4 * C];  // wave partials: Σ dZ, dγ2, dβ2, Σ dY
+  __shared__ float sDb1[2][C];
+  __shared__ float sP[2][C];  // γ2, β2
+  const int m0 = blockIdx.x * 64, gr = m0 + rp_row(), w = wave_id(), l = lane_id();
+  const bool av = aligned16(dZ) && aligned16(Ysave) && aligned16(U) && aligned16(O) && aligned16(dY) &&
+                  aligned16(dO) && aligned16(Wo) && aligned16(W1) && aligned16(W2);
+
+  // ---- phase 0: every input of the tile in flight at once
+  float dz[NCH][8], yv[NCH][8], t0[NCH][8];
+  row_load<NCH>(dz, dZ, C, gr, R, C, av);
+  row_load<NCH>(yv, Ysave, C, gr, R, C, av);
+  row_load<NCH>(t0, U, C, gr, R, C, av);
+  bf16x8 ob[NCH];
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    ob[j] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (gr < R) ob[j] = *reinterpret_cast<const bf16x8*>(O + (long long)gr * C + rp_col(j));
+  }
+  const float mu = gr < R ? mean2[gr] : 0.f, rs = gr < R ? rstd2[gr] : 0.f;
+  bf16x8 wr[NWB][NIW];
+  tile_fetch<NIW>(wr[0], W2, C, 0, C, C, C, C, av);
+  if constexpr (NWB == 3) {
+    tile_fetch<NIW>(wr[1], W1, C, 0, C, C, C, C, av);
+    tile_fetch<NIW>(wr[2], Wo, C, 0, C, C, C, C, av);
+  }
+  for (int k = threadIdx.x; k < C; k += blockDim.x) { sP[0][k] = g2[k]; sP[1][k] = be2[k]; }
+  lds_row_write_bf16<NCH>(sG, LD, dz);
+  {
+    float gp[NCH][8];
+#pragma unroll
+    for (int j = 0; j < NCH; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { gp[j][e] = gelu_grad(t0[j][e]); t0[j][e] = gelu_f(t0[j][e]); }
+    lds_row_write_bf16<NCH>(sX, LD, t0);
+    lds_row_write<NCH>(sF, LDF, gp);
+  }
+#pragma unroll
+  for (int b = 0; b < NWB; ++b) tile_store<NIW>(wr[b], sW[b], LD, C, C);
+  colsum_partial<NCH>(dz, sPart[0], C);
+  __syncthreads();
+  if constexpr (NWB == 1) tile_fetch<NIW>(wr[0], W1, C, 0, C, C, C, C, av);
 
   // ---- MLP output layer
-  stage(sG, LD, dZ, C, m0, R, 0, C, 64, C);
-  stage_act(sX, LD, U, C, m0, R, C, C, 2, nullptr, nullptr, nullptr, nullptr);
-  stage(sW, LD, W2, C, 0, C, 0, C, C, C);
-  __syncthreads();
   f32x16 acc[MAXT];
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
-  tile_gemm<MAXT, true, false>(sG, LD, sW, LD, 64, C, C, acc);  // dH
+  tile_gemm<MAXT, true, false>(sG, LD, sW[0], LD, 64, C, C, acc);  // dH = dZ · W2
   wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, gr_out.dW2, C);
-  for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) {
-    const int gr = m0 + m;
-    sF[m * LDF + n] = gr < R ? acc[t][i] * gelu_grad(bf2f(U[(long long)gr * C + n])) : 0.f;
-  });
-  __syncthreads();
-  // ---- MLP hidden layer: db1 column sums (fp32), dU → bf16 tile, LN2(Y) tile, W1
   {
-    const int c = threadIdx.x % C, g = threadIdx.x / C;
-    float s = 0.f;
-#pragma unroll 4
-    for (int r = g * RPG; r < (g + 1) * RPG; ++r) s += sF[r * LDF + c];
-    atomicAdd(gr_out.db1 + c, s);
+    constexpr int NTN = C / 32;
+#pragma unroll
+    for (int t = 0; t < MAXT; ++t) {
+      const int tg = w + 4 * t;
+      if (tg < 2 * NTN) {
+        const int mt = tg / NTN, n0 = 32 * (tg % NTN), hh = l >> 5;
+        float cs = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int m = 32 * mt + acc_row(i, hh), n = n0 + (l & 31);
+          const float du = acc[t][i] * sF[m * LDF + n];
+          sF[m * LDF + n] = du;
+          cs += du;
+        }
+        cs += __shfl_xor(cs, 32, 64);
+        if (l < 32) sDb1[mt][n0 + l] = cs;
+      }
+    }
   }
-  for (int e = threadIdx.x; e < 64 * C / 4; e += blockDim.x) {
-    const int r = e / (C / 4), c = (e % (C / 4)) * 4;
-    const float4 v = *reinterpret_cast<const float4*>(sF + r * LDF + c);
-    *reinterpret_cast<uint32_t*>(sG + r * LD + c) = pack2(v.x, v.y);
-    *reinterpret_cast<uint32_t*>(sG + r * LD + c + 2) = pack2(v.z, v.w);
-  }
-  stage_act(sX, LD, Ysave, C, m0, R, C, C, 1, mean2, rstd2, g2, be2);
-  stage(sW, LD, W1, C, 0, C, 0, C, C, C);
   __syncthreads();
+  for (int k = threadIdx.x; k < C; k += blockDim.x) {
+    atomicAdd(gr_out.db1 + k, sDb1[0][k] + sDb1[1][k]);
+    atomicAdd(gr_out.db2 + k, sPart[0][k] + sPart[0][C + k] + sPart[0][2 * C + k] + sPart[0][3 * C + k]);
+  }
+  if constexpr (NWB == 1) tile_store<NIW>(wr[0], sW[0], LD, C, C);
+  {
+    float du[NCH][8];
+    lds_row_read<NCH>(du, sF, LDF);
+    lds_row_write_bf16<NCH>(sG, LD, du);
+#pragma unroll
+    for (int j = 0; j < NCH; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = rp_col(j) + e;
+        t0[j][e] = (yv[j][e] - mu) * rs * sP[0][c] + sP[1][c];
+      }
+    lds_row_write_bf16<NCH>(sX, LD, t0);
+  }
+  __syncthreads();
+  if constexpr (NWB == 1) tile_fetch<NIW>(wr[0], Wo, C, 0, C, C, C, C, av);
+
+  // ---- MLP hidden layer
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
-  tile_gemm<MAXT, true, false>(sG, LD, sW, LD, 64, C, C, acc);  // dXn2 = dU · W1
+  tile_gemm<MAXT, true, false>(sG, LD, sW[NWB == 3 ? 1 : 0], LD, 64, C, C, acc);  // dXn2 = dU · W1
   wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, gr_out.dW1, C);
   for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) { sF[m * LDF + n] = acc[t][i]; });
   __syncthreads();
-  // ---- LN2 backward → dY = dZ + LN_bwd ; column partials
-  float pg[NJ], pb[NJ], py[NJ], pz[NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) pg[j] = pb[j] = py[j] = pz[j] = 0.f;
-  for (int rr = w; rr < 64; rr += 4) {
-    const int gr = m0 + rr;
-    if (gr >= R) {
-      for (int k = l; k < C; k += 64) sG[rr * LD + k] = 0;
-      continue;
-    }
-    const float mean = mean2[gr], rstd = rstd2[gr];
-    float xh[NJ], dxn[NJ], dz[NJ];
+  if constexpr (NWB == 1) tile_store<NIW>(wr[0], sW[0], LD, C, C);
+  // ---- LN2 backward → dY = dZ + LN_bwd(dXn2); the O tile replaces LN2(Y) in sX
+  {
+    float dxn[NCH][8];
+    lds_row_read<NCH>(dxn, sF, LDF);
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int k = l + 64 * j;
-      xh[j] = dxn[j] = dz[j] = 0.f;
-      if (k < C) {
-        xh[j] = (Ysave[(long long)gr * C + k] - mean) * rstd;
-        dxn[j] = sF[rr * LDF + k];
-        dz[j] = dZ[(long long)gr * C + k];
-        const float g = dxn[j] * g2[k];
+    for (int j = 0; j < NCH; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        yv[j][e] = (yv[j][e] - mu) * rs;  // ŷ
+        const float g = dxn[j][e] * sP[0][rp_col(j) + e];
         s1 += g;
-        s2 += g * xh[j];
+        s2 += g * yv[j][e];
       }
-    }
-    s1 = wave_sum(s1) / C;
-    s2 = wave_sum(s2) / C;
+    s1 = quad_sum(s1) / C;
+    s2 = quad_sum(s2) / C;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int k = l + 64 * j;
-      if (k < C) {
-        const float d = dz[j] + rstd * (dxn[j] * g2[k] - s1 - xh[j] * s2);
-        dY[(long long)gr * C + k] = d;
-        sG[rr * LD + k] = f2bf(d);
-        pg[j] += dxn[j] * xh[j];
-        pb[j] += dxn[j];
-        py[j] += d;
-        pz[j] += dz[j];
+    for (int j = 0; j < NCH; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        dz[j][e] += rs * (dxn[j][e] * sP[0][rp_col(j) + e] - s1 - yv[j][e] * s2);  // dY
+        yv[j][e] *= dxn[j][e];                                                      // dγ2 terms
       }
-    }
-  }
+    colsum_partial<NCH>(yv, sPart[1], C);
+    colsum_partial<NCH>(dxn, sPart[2], C);
+    colsum_partial<NCH>(dz, sPart[3], C);
+    row_store<NCH>(dz, dY, C, gr, R, C, av);
+    lds_row_write_bf16<NCH>(sG, LD, dz);
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int k = l + 64 * j;
-    if (k < C) { sPart[0][w][k] = pg[j]; sPart[1][w][k] = pb[j]; sPart[2][w][k] = py[j]; sPart[3][w][k] = pz[j]; }
+    for (int j = 0; j < NCH; ++j) *reinterpret_cast<bf16x8*>(sX + rp_row() * LD + rp_col(j)) = ob[j];
   }
-  // ---- out-projection
-  stage(sX, LD, O, C, m0, R, 0, C, 64, C);
-  stage(sW, LD, Wo, C, 0, C, 0, C, C, C);
   __syncthreads();
-  for (int e = threadIdx.x; e < 4 * C; e += blockDim.x) {
-    const int q = e / C, k = e % C;
-    float* dst = q == 0 ? gr_out.dg2 : q == 1 ? gr_out.dbe2 : q == 2 ? gr_out.dbo : gr_out.db2;
-    atomicAdd(dst + k, sPart[q][0][k] + sPart[q][1][k] + sPart[q][2][k] + sPart[q][3][k]);
+  for (int k = threadIdx.x; k < C; k += blockDim.x) {
+    atomicAdd(gr_out.dg2 + k, sPart[1][k] + sPart[1][C + k] + sPart[1][2 * C + k] + sPart[1][3 * C + k]);
+    atomicAdd(gr_out.dbe2 + k, sPart[2][k] + sPart[2][C + k] + sPart[2][2 * C + k] + sPart[2][3 * C + k]);
+    atomicAdd(gr_out.dbo + k, sPart[3][k] + sPart[3][C + k] + sPart[3][2 * C + k] + sPart[3][3 * C + k]);
   }
+
+  // ---- out-projection
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
-  tile_gemm<MAXT, true, false>(sG, LD, sW, LD, 64, C, C, acc);  // dO = dY · Wo
+  tile_gemm<MAXT, true, false>(sG, LD, sW[NWB == 3 ? 2 : 0], LD, 64, C, C, acc);  // dO = dY · Wo
   wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, gr_out.dWo, C);
-  for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) {
-    const int gr = m0 + m;
-    const uint16_t d = f2bf(acc[t][i]);
-    sF[m * LDF + n] = bf2f(d);
-    if (gr < R) dO[(long long)gr * C + n] = d;
-  });
+  for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) { sF[m * LDF + n] = bf2f(f2bf(acc[t][i])); });
   __syncthreads();
-  // delta[r, h] = Σ_d dO·O over the head's columns (bf16 values, as the attention sees them)
-  const int D = C / H;
-  for (int e = threadIdx.x; e < 64 * H; e += blockDim.x) {
-    const int rr = e / H, h = e % H;
-    const int gr = m0 + rr;
-    if (gr < R) {
+  {
+    float dov[NCH][8];
+    lds_row_read<NCH>(dov, sF, LDF);
+    row_store<NCH>(dov, dO, C, gr, R, C, av);
+    // delta[r, h] = Σ_d dO·O over head h's columns (bf16 values, as the attention sees them);
+    // every 8-column chunk lies inside one head (D ≥ 8)
+    const int D = C / H;
+    for (int h = 0; h < H; ++h) {
       float s = 0.f;
-      for (int d = 0; d < D; ++d) s += sF[rr * LDF + h * D + d] * bf2f(sX[rr * LD + h * D + d]);
-      delta[(long long)gr * H + h] = s;
+#pragma unroll
+      for (int j = 0; j < NCH; ++j)
+        if (rp_col(j) / D == h) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) s += dov[j][e] * bf2f(ob[j][e]);
+        }
+      s = quad_sum(s);
+      if ((threadIdx.x & 3) == 0 && gr < R) delta[(long long)gr * H + h] = s;
     }
   }
 }
 
 // ------------------------------------------------------------------------------------
 // LayerNorm(+)Linear backward, one 64-row tile:
-//   dXn = G·W (N streamed in 64-column chunks), dW += Gᵀ·LN(X), db += Σ G (per chunk, atomics)
-//   dX = LN_bwd(dXn) (+ dres), dγ/dβ partials (atomics)
+//   dXn = G·W (N streamed in 64-column chunks, double-buffered through registers),
+//   dW += Gᵀ·LN(X), db += Σ G (per chunk, atomics), dX = LN_bwd(dXn) (+ dres), dγ/dβ.
 // ------------------------------------------------------------------------------------
-template <typename TG, typename TX>
+template <typename TG, typename TX, int NCH>
 __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
     const TG* __restrict__ G, int g_rs, int N, const uint16_t* __restrict__ W, int Kin, const TX* __restrict__ X,
     int x_rs, const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ lnw,
     const float* __restrict__ lnb, const float* __restrict__ dres, int dres_rs, float* __restrict__ dX, int dx_rs,
     float* __restrict__ dlnw, float* __restrict__ dlnb, float* __restrict__ dW, float* __restrict__ db, int R) {
+  constexpr int KP = 32 * NCH, LD = KP + 8, LDG = 64 + 8, LDF = KP + 4;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  const int KP = round_up(Kin, 32), ld = KP + 8, ldg = 64 + 8, ldF = KP + 4;
-  uint16_t* sG = smem;                 // [64 rows][64 n]
-  uint16_t* sW = sG + 64 * ldg;        // [64 n][KP]
-  uint16_t* sXn = sW + 64 * ld;        // [64 rows][KP]  LN(X), the forward GEMM's A operand
-  float* sF = reinterpret_cast<float*>(sXn + 64 * ld);  // [64][KP] fp32
-  float* sPart = sF + 64 * ldF;        // [2][4][KP]
-  const int m0 = blockIdx.x * 64;
-  const int w = wave_id(), l = lane_id();
-  constexpr int MAXT = 3;  // (64/32)*(KP/32) ≤ 10 sub-tiles (KP ≤ 160)
-  if (dW) stage_act(sXn, ld, X, x_rs, m0, R, Kin, KP, lnw ? 1 : 0, mean, rstd, lnw, lnb);
+  uint16_t* sG = smem;                                   // [64][LDG]  G chunk
+  uint16_t* sW = sG + 64 * LDG;                          // [64][LD]   W chunk
+  uint16_t* sXn = sW + 64 * LD;                          // [64][LD]   LN(X)
+  float* sF = reinterpret_cast<float*>(sXn + 64 * LD);   // [64][LDF]  dXn
+  float* sPart = sF + 64 * LDF;                          // [2][4][KP]
+  float* sPb = sPart + 8 * KP;                           // [4][64]
+  const int m0 = blockIdx.x * 64, gr = m0 + rp_row(), w = wave_id(), l = lane_id();
+  const bool gvec = (N & 7) == 0 && (g_rs & 7) == 0 && aligned16(G);
+  const bool wvec = (Kin & 7) == 0 && aligned16(W);
+  const bool kvec = (Kin & 7) == 0;
+
+  // ---- phase 0
+  float xv[NCH][8], gw[NCH][8];
+  row_load<NCH>(xv, X, x_rs, gr, R, Kin, kvec && (x_rs & 7) == 0 && aligned16(X));
+  float mu = 0.f, rs = 1.f;
+  if (lnw) {
+    row_load<NCH>(gw, lnw, 0, 0, 1, Kin, kvec && aligned16(lnw));
+    if (gr < R) { mu = mean[gr]; rs = rstd[gr]; }
+  }
+  float gv[2][8];
+  g_fetch<TG>(gv, G, g_rs, m0, R, 0, N, gvec);
+  bf16x8 wb[NCH];
+  tile_fetch<NCH>(wb, W, Kin, 0, N, 64, Kin, KP, wvec);
+  if (dW) {  // LN(X), the forward GEMM's A operand, for the weight gradient
+    float xn[NCH][8];
+    if (lnw) {
+      row_load<NCH>(xn, lnb, 0, 0, 1, Kin, kvec && aligned16(lnb));
+#pragma unroll
+      for (int j = 0; j < NCH; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xn[j][e] += (xv[j][e] - mu) * rs * gw[j][e];
+    } else {
+#pragma unroll
+      for (int j = 0; j < NCH; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xn[j][e] = xv[j][e];
+    }
+    lds_row_write_bf16<NCH>(sXn, LD, xn);
+  }
+
+  constexpr int MAXT = 3;  // (64/32)·(KP/32) ≤ 10 sub-tiles (KP ≤ 160)
   f32x16 acc[MAXT];
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
   for (int nc = 0; nc < N; nc += 64) {
+    g_store(gv, sG, LDG);
+    tile_store<NCH>(wb, sW, LD, 64, KP);
+    float cs[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cs[e] = gv[0][e] + gv[1][e];
     __syncthreads();
-    stage(sG, ldg, G, g_rs, m0, R, nc, N, 64, 64);
-    stage(sW, ld, W, Kin, nc, N, 0, Kin, 64, KP);
-    __syncthreads();
-    tile_gemm<MAXT, true, false>(sG, ldg, sW, ld, 64, KP, 64, acc);
+    if (nc + 64 < N) {
+      g_fetch<TG>(gv, G, g_rs, m0, R, nc + 64, N, gvec);
+      tile_fetch<NCH>(wb, W, Kin, nc + 64, N, 64, Kin, KP, wvec);
+    }
+    tile_gemm<MAXT, true, false>(sG, LDG, sW, LD, 64, KP, 64, acc);
     if (dW) {
-      wgrad_tile<MAXT>(sG, ldg, sXn, ld, 64, KP, N - nc, Kin, dW + (long long)nc * Kin, Kin);
-      if (db) {  // fp32 column sums of this G chunk: 4 row-quarters per column
-        const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
-        if (nc + c < N) {
-          float s = 0.f;
-#pragma unroll 4
-          for (int r = m0 + 16 * q; r < min(R, m0 + 16 * q + 16); ++r) s += ldf(G + (long long)r * g_rs + nc + c);
-          atomicAdd(db + nc + c, s);
+      wgrad_tile<MAXT>(sG, LDG, sXn, LD, 64, KP, N - nc, Kin, dW + (long long)nc * Kin, Kin);
+      if (db) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float s = cs[e] + dpp<0x128>(cs[e]);  // lanes i, i ± 8 share a column group
+          s += __shfl_xor(s, 16, 64);
+          s += __shfl_xor(s, 32, 64);
+          if (l < 8) sPb[w * 64 + 8 * l + e] = s;
         }
       }
+    }
+    __syncthreads();
+    if (dW && db && threadIdx.x < 64 && nc + (int)threadIdx.x < N) {
+      const int t = threadIdx.x;
+      atomicAdd(db + nc + t, sPb[t] + sPb[64 + t] + sPb[128 + t] + sPb[192 + t]);
     }
   }
-  for_acc<MAXT>(64, KP, [&](int t, int m, int n, int i) { sF[m * ldF + n] = acc[t][i]; });
+  for_acc<MAXT>(64, KP, [&](int t, int m, int n, int i) { sF[m * LDF + n] = acc[t][i]; });
   __syncthreads();
-  const int NJ = (KP + 63) / 64;
-  float pg[3] = {0.f, 0.f, 0.f}, pb[3] = {0.f, 0.f, 0.f};
-  float gw[3];
+
+  // ---- row pass: LN backward, residual gradient, LN parameter gradients
+  float dr[NCH][8];
+  if (dres) row_load<NCH>(dr, dres, dres_rs, gr, R, Kin, kvec && (dres_rs & 7) == 0 && aligned16(dres));
+  float dxn[NCH][8];
+  lds_row_read<NCH>(dxn, sF, LDF);
+  if (lnw) {
+    float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-  for (int j = 0; j < 3; ++j) gw[j] = (lnw && l + 64 * j < Kin) ? lnw[l + 64 * j] : 0.f;
-  for (int rr = w; rr < 64; rr += 4) {
-    const int gr = m0 + rr;
-    if (gr >= R) continue;
-    if (lnw) {
-      const float mu = mean[gr], rs = rstd[gr];
-      float xh[3], dxn[3];
-      float s1 = 0.f, s2 = 0.f;
+    for (int j = 0; j < NCH; ++j)
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const int k = l + 64 * j;
-        xh[j] = dxn[j] = 0.f;
-        if (j < NJ && k < Kin) {
-          xh[j] = (ldf(X + (long long)gr * x_rs + k) - mu) * rs;
-          dxn[j] = sF[rr * ldF + k];
-          const float g = dxn[j] * gw[j];
-          s1 += g;
-          s2 += g * xh[j];
-        }
+      for (int e = 0; e < 8; ++e) {
+        xv[j][e] = rp_col(j) + e < Kin ? (xv[j][e] - mu) * rs : 0.f;  // x̂
+        const float g = dxn[j][e] * gw[j][e];
+        s1 += g;
+        s2 += g * xv[j][e];
       }
-      s1 = wave_sum(s1) / Kin;
-      s2 = wave_sum(s2) / Kin;
+    s1 = quad_sum(s1) / Kin;
+    s2 = quad_sum(s2) / Kin;
+    if (dlnw) {
+      colsum_partial<NCH>(dxn, sPart + 4 * KP, KP);
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const int k = l + 64 * j;
-        if (j < NJ && k < Kin) {
-          pg[j] += dxn[j] * xh[j];
-          pb[j] += dxn[j];
-          if (dX) {
-            float d = rs * (dxn[j] * gw[j] - s1 - xh[j] * s2);
-            if (dres) d += dres[(long long)gr * dres_rs + k];
-            dX[(long long)gr * dx_rs + k] = d;
-          }
-        }
-      }
-    } else if (dX) {
-      for (int k = l; k < Kin; k += 64) {
-        float d = sF[rr * ldF + k];
-        if (dres) d += dres[(long long)gr * dres_rs + k];
-        dX[(long long)gr * dx_rs + k] = d;
-      }
+      for (int j = 0; j < NCH; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) gw[j][e] = rs * (dxn[j][e] * gw[j][e] - s1 - xv[j][e] * s2);  // dX (LN part)
+#pragma unroll
+      for (int j = 0; j < NCH; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dxn[j][e] *= xv[j][e];
+      colsum_partial<NCH>(dxn, sPart, KP);
+    } else {
+#pragma unroll
+      for (int j = 0; j < NCH; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) gw[j][e] = rs * (dxn[j][e] * gw[j][e] - s1 - xv[j][e] * s2);
     }
+  } else {
+#pragma unroll
+    for (int j = 0; j < NCH; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) gw[j][e] = dxn[j][e];
+  }
+  if (dX) {
+    if (dres) {
+#pragma unroll
+      for (int j = 0; j < NCH; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) gw[j][e] += dr[j][e];
+    }
+    row_store<NCH>(gw, dX, dx_rs, gr, R, Kin, kvec && (dx_rs & 7) == 0 && aligned16(dX));
   }
   if (lnw && dlnw) {
-    for (int j = 0; j < NJ; ++j) {
-      const int k = l + 64 * j;
-      if (k < Kin) { sPart[(0 * 4 + w) * KP + k] = pg[j]; sPart[(1 * 4 + w) * KP + k] = pb[j]; }
-    }
     __syncthreads();
-    for (int k = threadIdx.x; k < Kin; k += blockDim.x) {
-      float a = 0.f, b = 0.f;
-      for (int ww = 0; ww < 4; ++ww) { a += sPart[ww * KP + k]; b += sPart[(4 + ww) * KP + k]; }
-      atomicAdd(dlnw + k, a);
-      atomicAdd(dlnb + k, b);
-    }
+    colsum_flush(sPart, KP, dlnw, Kin);
+    colsum_flush(sPart + 4 * KP, KP, dlnb, Kin);
   }
 }
 
@@ -622,7 +955,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const TG* __restrict__ G, in
 // ------------------------------------------------------------------------------------
 // kernels whose dynamic LDS can exceed 64 KiB: raise the per-function limit once (gfx950: 160 KiB/CU)
 static void set_smem_once(const void* fn) {
-  static const void* done[8] = {nullptr};
+  static const void* done[64] = {nullptr};
   for (auto& d : done) {
     if (d == fn) return;
     if (d == nullptr) {
@@ -633,15 +966,45 @@ static void set_smem_once(const void* fn) {
   }
 }
 
+// row-pass chunk count for a K-wide row: K ≤ 32·NCH, NCH ∈ {1, 2, 4, 5, 8}
+static int pick_nch(int K) {
+  const int n = (K + 31) / 32;
+  return n <= 2 ? n : n <= 4 ? 4 : n <= 5 ? 5 : 8;
+}
+
+template <typename TI, typename TO, int NCH>
+static void ln_linear_fwd_t(const void* X, int x_rs, int R, int Kin, const float* lnw, const float* lnb, float eps,
+                            const uint16_t* W, const float* bias, int N, int act, const float* res, int res_rs,
+                            void* Y, int y_rs, float* mean, float* rstd, hipStream_t st) {
+  constexpr int KP = 32 * NCH;
+  const size_t smem = 2 * 64 * (KP + 8) * sizeof(uint16_t) + 64 * 68 * sizeof(float);
+  auto fn = ln_linear_fwd_kernel<TI, TO, NCH>;
+  set_smem_once((const void*)fn);
+  hipLaunchKernelGGL(fn, dim3((R + 63) / 64), dim3(256), smem, st, (const TI*)X, x_rs, R, Kin, lnw, lnb, eps, W, bias,
+                     N, act, res, res_rs, (TO*)Y, y_rs, mean, rstd);
+}
+
+template <typename TI, typename TO>
+static void ln_linear_fwd_n(int nch, const void* X, int x_rs, int R, int Kin, const float* lnw, const float* lnb,
+                            float eps, const uint16_t* W, const float* bias, int N, int act, const float* res,
+                            int res_rs, void* Y, int y_rs, float* mean, float* rstd, hipStream_t st) {
+#define LNF(K) ln_linear_fwd_t<TI, TO, K>(X, x_rs, R, Kin, lnw, lnb, eps, W, bias, N, act, res, res_rs, Y, y_rs, mean, rstd, st)
+  switch (nch) {
+    case 1: LNF(1); break;
+    case 2: LNF(2); break;
+    case 4: LNF(4); break;
+    case 5: LNF(5); break;
+    default: LNF(8); break;
+  }
+#undef LNF
+}
+
 void ln_linear_fwd_launch(const void* X, bool x_bf16, int x_rs, int R, int Kin, const float* lnw, const float* lnb,
                           float eps, const uint16_t* W, const float* bias, int N, int act, const float* res,
                           int res_rs, void* Y, bool y_bf16, int y_rs, float* mean, float* rstd, hipStream_t st) {
-  const int KP = round_up(Kin, 16);
-  const size_t smem = 2 * 64 * (KP + 8) * sizeof(uint16_t);
-  dim3 grid((R + 63) / 64);
-#define LNL(TI, TO)                                                                                         \
-  hipLaunchKernelGGL((ln_linear_fwd_kernel<TI, TO>), grid, dim3(256), smem, st, (const TI*)X, x_rs, R, Kin, \
-                     lnw, lnb, eps, W, bias, N, act, res, res_rs, (TO*)Y, y_rs, mean, rstd)
+  const int nch = pick_nch(Kin);
+#define LNL(TI, TO) \
+  ln_linear_fwd_n<TI, TO>(nch, X, x_rs, R, Kin, lnw, lnb, eps, W, bias, N, act, res, res_rs, Y, y_rs, mean, rstd, st)
   if (x_bf16 && y_bf16) LNL(uint16_t, uint16_t);
   else if (x_bf16) LNL(uint16_t, float);
   else if (y_bf16) LNL(float, uint16_t);
@@ -654,15 +1017,13 @@ void post_attn_fwd_launch(int C, const uint16_t* O, const float* X, const uint16
                           const uint16_t* W2, const float* b2, float* Z, float* Ysave, float* mean2, float* rstd2,
                           uint16_t* Usave, int R, hipStream_t st) {
   dim3 grid((R + 63) / 64);
-  if (C == 64)
-    hipLaunchKernelGGL(post_attn_fwd_kernel<64>, grid, dim3(256), 0, st, O, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2,
-                       Z, Ysave, mean2, rstd2, Usave, R);
-  else if (C == 128)
-    hipLaunchKernelGGL(post_attn_fwd_kernel<128>, grid, dim3(256), 0, st, O, X, Wo, bo, g2, be2, eps, W1, b1, W2,
-                       b2, Z, Ysave, mean2, rstd2, Usave, R);
-  else if (C == 32)
-    hipLaunchKernelGGL(post_attn_fwd_kernel<32>, grid, dim3(256), 0, st, O, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2,
-                       Z, Ysave, mean2, rstd2, Usave, R);
+#define PAF(CC)                                                                                                     \
+  hipLaunchKernelGGL(post_attn_fwd_kernel<CC>, grid, dim3(256), 0, st, O, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, \
+                     Z, Ysave, mean2, rstd2, Usave, R)
+  if (C == 64) PAF(64);
+  else if (C == 128) PAF(128);
+  else if (C == 32) PAF(32);
+#undef PAF
 }
 
 void post_attn_bwd_launch(int C, const float* dZ, const float* Ysave, const float* mean2, const float* rstd2,
@@ -679,19 +1040,44 @@ void post_attn_bwd_launch(int C, const float* dZ, const float* Ysave, const floa
 #undef PAB
 }
 
+template <typename TG, typename TX, int NCH>
+static void ln_linear_bwd_t(const void* G, int g_rs, int N, const uint16_t* W, int Kin, const void* X, int x_rs,
+                            const float* mean, const float* rstd, const float* lnw, const float* lnb, const float* dres,
+                            int dres_rs, float* dX, int dx_rs, float* dlnw, float* dlnb, float* dW, float* db, int R,
+                            hipStream_t st) {
+  constexpr int KP = 32 * NCH;
+  const size_t smem = 64 * 72 * 2 + 2 * 64 * (KP + 8) * 2 + 64 * (KP + 4) * 4 + 8 * KP * 4 + 4 * 64 * 4;
+  auto fn = ln_linear_bwd_kernel<TG, TX, NCH>;
+  set_smem_once((const void*)fn);
+  hipLaunchKernelGGL(fn, dim3((R + 63) / 64), dim3(256), smem, st, (const TG*)G, g_rs, N, W, Kin, (const TX*)X, x_rs,
+                     mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, dlnw, dlnb, dW, db, R);
+}
+
+template <typename TG, typename TX>
+static void ln_linear_bwd_n(int nch, const void* G, int g_rs, int N, const uint16_t* W, int Kin, const void* X,
+                            int x_rs, const float* mean, const float* rstd, const float* lnw, const float* lnb,
+                            const float* dres, int dres_rs, float* dX, int dx_rs, float* dlnw, float* dlnb, float* dW,
+                            float* db, int R, hipStream_t st) {
+#define LNB(K)                                                                                                    \
+  ln_linear_bwd_t<TG, TX, K>(G, g_rs, N, W, Kin, X, x_rs, mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, dlnw, \
+                             dlnb, dW, db, R, st)
+  switch (nch) {
+    case 1: LNB(1); break;
+    case 2: LNB(2); break;
+    case 4: LNB(4); break;
+    default: LNB(5); break;
+  }
+#undef LNB
+}
+
 void ln_linear_bwd_launch(const void* G, bool g_bf16, int g_rs, int N, const uint16_t* W, int Kin, const void* X,
                           bool x_bf16, int x_rs, const float* mean, const float* rstd, const float* lnw,
                           const float* lnb, const float* dres, int dres_rs, float* dX, int dx_rs, float* dlnw,
                           float* dlnb, float* dW, float* db, int R, hipStream_t st) {
-  const int KP = round_up(Kin, 32);
-  const size_t smem = 64 * (64 + 8) * 2 + 2 * 64 * (KP + 8) * 2 + 64 * (KP + 4) * 4 + 2 * 4 * KP * 4;
-  dim3 grid((R + 63) / 64);
-#define LDG(TG, TX)                                                                                              \
-  do {                                                                                                           \
-    set_smem_once((const void*)ln_linear_bwd_kernel<TG, TX>);                                                    \
-    hipLaunchKernelGGL((ln_linear_bwd_kernel<TG, TX>), grid, dim3(256), smem, st, (const TG*)G, g_rs, N, W, Kin, \
-                       (const TX*)X, x_rs, mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, dlnw, dlnb, dW, db, R); \
-  } while (0)
+  const int nch = pick_nch(Kin);  // Kin ≤ 160 → ≤ 5
+#define LDG(TG, TX)                                                                                           \
+  ln_linear_bwd_n<TG, TX>(nch, G, g_rs, N, W, Kin, X, x_rs, mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, \
+                          dlnw, dlnb, dW, db, R, st)
   if (g_bf16 && x_bf16) LDG(uint16_t, uint16_t);
   else if (g_bf16) LDG(uint16_t, float);
   else if (x_bf16) LDG(float, uint16_t);

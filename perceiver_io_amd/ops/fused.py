@@ -251,7 +251,7 @@ class _LayerFn(torch.autograd.Function):
             dx_kv = dx_kv.view(B, M, -1) if ctx.kv_grad else None
         else:
             qkv3 = qx.view(B, Nq, 3 * C)
-            dqkv = torch.zeros((B, Nq, 3 * C), **f32)  # dQ third is accumulated with atomics
+            dqkv = torch.empty((B, Nq, 3 * C), **f32)  # every column block is written by attn_bwd
             K.attn_bwd(qkv3[:, :, :C], qkv3[:, :, C:2 * C], qkv3[:, :, 2 * C:], kmask, o, do.view(B, Nq, C), lse,
                        delta3, H, D, scale, ctx.p_attn, ctx.seed, dqkv[:, :, :C], dqkv[:, :, C:2 * C],
                        dqkv[:, :, 2 * C:])

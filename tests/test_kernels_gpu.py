@@ -94,6 +94,15 @@ def test_attention_fwd_bwd(B, Bq, Nq, Nk, H, D, ns):
     g2 = _emu().attn_bwd(q, k, v, km, o1, do, l1, None, H, D, scale, 0.0, 0, None, None, None)
     for a, b, n in zip(g1, g2, ("dq", "dk", "dv")):
         close(a, b, 3e-2, n)
+    # packed, uninitialised output buffer (the kernel must overwrite / clear dQ itself)
+    if Bq == B:
+        E = H * D
+        pk = torch.full((B, Nq, 3 * E), float("nan"), device=DEV)
+        dkv = torch.full((B, Nk, 2 * E), float("nan"), device=DEV)
+        _ext().attn_bwd(q, k, v, km, o1, do, l1, None, H, D, scale, 0.0, 0, pk[:, :, :E], dkv[:, :, :E], dkv[:, :, E:])
+        close(pk[:, :, :E], g2[0], 3e-2, "dq packed")
+        close(dkv[:, :, :E], g2[1], 3e-2, "dk packed")
+        close(dkv[:, :, E:], g2[2], 3e-2, "dv packed")
 
 
 def test_attention_dropout_statistics():
