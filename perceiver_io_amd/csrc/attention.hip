@@ -192,7 +192,7 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(AttnArgs a, uint16_t
         s[kh][i] = v;
         mt = fmaxf(mt, v);
       }
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    mt = xor32_max(mt);
     const float m_new = fmaxf(m_run, mt);
     const float alpha = exp2f(m_run - m_new);
     m_run = m_new;
@@ -227,7 +227,7 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(AttnArgs a, uint16_t
       }
   }
 
-  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float l_tot = xor32_sum(l_run);
   if (qi >= a.Nq) return;
   const int HD = a.H * D;
   if (nsplit == 1) {

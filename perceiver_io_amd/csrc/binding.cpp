@@ -19,7 +19,7 @@ struct AttnArgs {
   float drop_scale;
   uint32_t seed;
 };
-struct PostAttnGrads { float *dWo, *dbo, *dg2, *dbe2, *dW1, *db1, *dW2, *db2; };
+struct PostAttnGrads { float *dWo, *dbo, *dg2, *dbe2, *dW1, *db1, *dW2, *db2; int vrs; };
 
 void attn_fwd_launch(const AttnArgs&, int, uint16_t*, float*, float*, float*, int, hipStream_t);
 void attn_bwd_launch(const AttnArgs&, int, const uint16_t*, const uint16_t*, const float*, float*, float*, long long,
@@ -28,28 +28,30 @@ void ln_linear_fwd_launch(const void*, bool, int, int, int, const float*, const 
                           const float*, int, int, const float*, int, void*, bool, int, float*, float*, hipStream_t);
 void post_attn_fwd_launch(int, const uint16_t*, const float*, const uint16_t*, const float*, const float*,
                           const float*, float, const uint16_t*, const float*, const uint16_t*, const float*, float*,
-                          float*, float*, float*, uint16_t*, int, hipStream_t);
+                          float*, float*, float*, uint16_t*, int, int, hipStream_t);
 void post_attn_bwd_launch(int, const float*, const float*, const float*, const float*, const uint16_t*,
                           const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*, const float*,
                           const float*, float*, uint16_t*, float*, int, const PostAttnGrads&, int, hipStream_t);
 void ln_linear_bwd_launch(const void*, bool, int, int, const uint16_t*, int, const void*, bool, int, const float*,
                           const float*, const float*, const float*, const float*, int, float*, int, float*, float*,
-                          float*, float*, int, hipStream_t);
+                          float*, float*, int, int, hipStream_t);
 void wgrad_launch(const void*, bool, int, int, const void*, bool, int, int, int, const float*, const float*,
                   const float*, const float*, int, int, float*, float*, hipStream_t);
 void ce_fwd_launch(int, const uint16_t*, const int64_t*, const uint16_t*, const float*, int, int, float*, float*,
                    float*, float*, int, hipStream_t);
 int ce_num_splits(int, int);
 void ce_bwd_launch(int, const uint16_t*, const int64_t*, const uint16_t*, const float*, const float*, const float*,
-                   int, int, float*, float*, float*, int, hipStream_t);
+                   int, int, float*, const int64_t*, float*, float*, int, hipStream_t);
 void embed_fwd_launch(const int64_t*, const float*, const float*, float*, long long, int, int, float, hipStream_t);
 void embed_bwd_launch(const int64_t*, const float*, float*, float*, int, int, int, float, hipStream_t);
+void embed_bwd_sorted_launch(const int64_t*, const int64_t*, const float*, float*, long long, int, float, hipStream_t);
 void text_mask_launch(const int64_t*, const bool*, const float*, const int64_t*, int64_t*, int64_t*, long long, int,
                       int, float, hipStream_t);
 void sumsq_launch(const float*, long long, float*, hipStream_t);
 void adamw_launch(float*, const float*, float*, float*, uint16_t*, long long, const float*, float, float, float, float,
                   hipStream_t);
 void cast_bf16_launch(const float*, uint16_t*, long long, hipStream_t);
+void reduce_probe_launch(const float*, float*, hipStream_t);
 }  // namespace pio
 
 using torch::Tensor;
@@ -189,7 +191,8 @@ std::vector<Tensor> ln_linear_fwd(Tensor x, OptT lnw, OptT lnb, double eps, Tens
 std::vector<Tensor> post_attn_fwd(Tensor o, Tensor x, Tensor wo, Tensor bo, Tensor g2, Tensor be2, double eps,
                                   Tensor w1, Tensor b1, Tensor w2, Tensor b2) {
   TORCH_CHECK(o.is_contiguous() && x.is_contiguous(), "o/x must be contiguous (R, C)");
-  const int R = (int)o.size(0), C = (int)o.size(1);
+  const int R = (int)o.size(0), C = (int)o.size(1), Rx = (int)x.size(0);
+  TORCH_CHECK(x.size(1) == C && Rx > 0 && R % Rx == 0, "x must be (R / k, C): row r adds x[r % rows(x)]");
   TORCH_CHECK(C == 32 || C == 64 || C == 128, "post_attn supports C in {32, 64, 128}");
   auto f32 = x.options().dtype(torch::kFloat32);
   Tensor z = torch::empty({R, C}, f32), y = torch::empty({R, C}, f32);
@@ -197,7 +200,7 @@ std::vector<Tensor> post_attn_fwd(Tensor o, Tensor x, Tensor wo, Tensor bo, Tens
   Tensor u = torch::empty({R, C}, x.options().dtype(torch::kBFloat16));
   pio::post_attn_fwd_launch(C, bfp(o), f32p(x), bfp(wo), f32p(bo), f32p(g2), f32p(be2), (float)eps, bfp(w1), f32p(b1),
                             bfp(w2), f32p(b2), z.data_ptr<float>(), y.data_ptr<float>(), m.data_ptr<float>(),
-                            r.data_ptr<float>(), bfp_mut(u), R, stream());
+                            r.data_ptr<float>(), bfp_mut(u), R, Rx, stream());
   return {z, y, m, r, u};
 }
 
@@ -208,6 +211,22 @@ namespace {
 float* grad_target(Tensor& t, int64_t numel, const char* what) {
   TORCH_CHECK(t.is_contiguous() && t.numel() == numel, "bad gradient target ", what);
   CHECK_DT(t, torch::kFloat32);
+  return t.data_ptr<float>();
+}
+constexpr int kGradReplicas = 8;
+// vector gradient target: (K,) contiguous, or (8, K) replicas with unit inner stride whose row
+// stride is shared by every vector target of the call (workgroup i adds into row i % 8)
+float* vec_target(Tensor& t, int64_t K, const char* what, int& vrs) {
+  CHECK_DT(t, torch::kFloat32);
+  if (t.dim() == 2) {
+    TORCH_CHECK(t.size(0) == kGradReplicas && t.size(1) == K && t.stride(1) == 1, "bad replicated target ", what);
+    TORCH_CHECK(vrs < 0 || vrs == (int)t.stride(0), "replicated targets must share one row stride");
+    vrs = (int)t.stride(0);
+  } else {
+    TORCH_CHECK(t.is_contiguous() && t.numel() == K, "bad gradient target ", what);
+    TORCH_CHECK(vrs <= 0, "mixing replicated and plain vector targets");
+    vrs = 0;
+  }
   return t.data_ptr<float>();
 }
 }  // namespace
@@ -222,10 +241,12 @@ std::vector<Tensor> post_attn_bwd(Tensor dz, Tensor y, Tensor m2, Tensor r2, Ten
   TORCH_CHECK(H > 0 && C % H == 0, "heads must divide C");
   TORCH_CHECK(grads.size() == 8, "post_attn_bwd needs 8 gradient targets");
   const int64_t CC = (int64_t)C * C;
-  pio::PostAttnGrads pg{grad_target(grads[0], CC, "dWo"), grad_target(grads[1], C, "dbo"),
-                        grad_target(grads[2], C, "dg2"), grad_target(grads[3], C, "dbe2"),
-                        grad_target(grads[4], CC, "dW1"), grad_target(grads[5], C, "db1"),
-                        grad_target(grads[6], CC, "dW2"), grad_target(grads[7], C, "db2")};
+  int vrs = -1;
+  pio::PostAttnGrads pg{grad_target(grads[0], CC, "dWo"), vec_target(grads[1], C, "dbo", vrs),
+                        vec_target(grads[2], C, "dg2", vrs), vec_target(grads[3], C, "dbe2", vrs),
+                        grad_target(grads[4], CC, "dW1"), vec_target(grads[5], C, "db1", vrs),
+                        grad_target(grads[6], CC, "dW2"), vec_target(grads[7], C, "db2", vrs), 0};
+  pg.vrs = vrs < 0 ? 0 : vrs;
   auto f32 = dz.options().dtype(torch::kFloat32);
   Tensor dy = torch::empty({R, C}, f32);
   Tensor dO = torch::empty({R, C}, dz.options().dtype(torch::kBFloat16));
@@ -248,20 +269,21 @@ OptT ln_linear_bwd(Tensor g, Tensor w, Tensor x, OptT mean, OptT rstd, OptT lnw,
   auto f32 = g.options().dtype(torch::kFloat32);
   Tensor dx;
   float *dxp = nullptr, *dgp = nullptr, *dbp = nullptr, *dwp = nullptr, *dbiasp = nullptr;
+  int vrs = -1;
   if (need_dx) { dx = torch::empty({R, Kin}, f32); dxp = dx.data_ptr<float>(); }
   if (lnw.has_value()) {
     TORCH_CHECK(lnb.has_value() && mean.has_value() && rstd.has_value(), "LN weight needs bias and row stats");
     TORCH_CHECK(dlnw.has_value() && dlnb.has_value(), "LN grad targets required");
-    dgp = grad_target(*dlnw, Kin, "dlnw");
-    dbp = grad_target(*dlnb, Kin, "dlnb");
+    dgp = vec_target(*dlnw, Kin, "dlnw", vrs);
+    dbp = vec_target(*dlnb, Kin, "dlnb", vrs);
   }
   if (dW.has_value()) dwp = grad_target(*dW, (int64_t)N * Kin, "dW");
-  if (db.has_value()) { TORCH_CHECK(dW.has_value(), "db needs dW"); dbiasp = grad_target(*db, N, "db"); }
+  if (db.has_value()) { TORCH_CHECK(dW.has_value(), "db needs dW"); dbiasp = vec_target(*db, N, "db", vrs); }
   const float* dr = nullptr; int drs = 0;
   if (dres.has_value()) { dr = f32p(*dres); drs = (int)dres->stride(0); TORCH_CHECK(dres->stride(1) == 1); }
   pio::ln_linear_bwd_launch(g.data_ptr(), is_bf16(g), (int)g.stride(0), N, bfp(w), Kin, x.data_ptr(), is_bf16(x),
                             (int)x.stride(0), f32o(mean), f32o(rstd), f32o(lnw), f32o(lnb), dr, drs, dxp, Kin, dgp, dbp,
-                            dwp, dbiasp, R, stream());
+                            dwp, dbiasp, vrs < 0 ? 0 : vrs, R, stream());
   if (need_dx) return dx;
   return c10::nullopt;
 }
@@ -294,12 +316,23 @@ std::vector<Tensor> ce_fwd(Tensor h, Tensor labels, Tensor w, Tensor bias) {
   return {loss, lse};
 }
 
+// dH (+)= rows: row r of the compacted batch lands in dH[rowmap[r]] when rowmap is given
+// (dH then has the full (positions, C) shape), else in dH[r]; dW / db accumulate or overwrite
 void ce_bwd(Tensor h, Tensor labels, Tensor w, Tensor bias, Tensor lse, Tensor gscale, Tensor dH, Tensor dW, Tensor db,
-            bool accumulate) {
+            bool accumulate, OptT rowmap) {
   const int M = (int)h.size(0), C = (int)h.size(1), V = (int)w.size(0);
   TORCH_CHECK(dH.is_contiguous() && dW.is_contiguous() && db.is_contiguous());
+  TORCH_CHECK(dH.dim() == 2 && dH.size(1) == C, "dH must be (rows, C)");
+  const int64_t* rm = nullptr;
+  if (rowmap.has_value()) {
+    CHECK_DT(*rowmap, torch::kInt64);
+    TORCH_CHECK(rowmap->is_contiguous() && rowmap->numel() == M, "rowmap must hold one row index per row");
+    rm = rowmap->data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(dH.size(0) == M, "dH must be (M, C) without a rowmap");
+  }
   pio::ce_bwd_launch(C, bfp(h), labels.data_ptr<int64_t>(), bfp(w), f32p(bias), f32p(lse), f32p(gscale), M, V,
-                     dH.data_ptr<float>(), dW.data_ptr<float>(), db.data_ptr<float>(), accumulate ? 1 : 0, stream());
+                     dH.data_ptr<float>(), rm, dW.data_ptr<float>(), db.data_ptr<float>(), accumulate ? 1 : 0, stream());
 }
 
 Tensor embed_fwd(Tensor ids, Tensor E, Tensor P, double scale) {
@@ -316,8 +349,18 @@ Tensor embed_fwd(Tensor ids, Tensor E, Tensor P, double scale) {
 void embed_bwd(Tensor ids, Tensor g, OptT dE, OptT dP, double scale) {
   TORCH_CHECK(g.is_contiguous() && ids.is_contiguous());
   const int B = (int)ids.size(0), L = (int)ids.size(1), C = (int)g.size(2);
-  pio::embed_bwd_launch(ids.data_ptr<int64_t>(), f32p(g), dE.has_value() ? dE->data_ptr<float>() : nullptr,
-                        dP.has_value() ? dP->data_ptr<float>() : nullptr, B, L, C, (float)scale, stream());
+  if (dE.has_value()) {  // token-embedding rows: sort positions by id, fold equal-id runs, then add
+    TORCH_CHECK(dE->is_contiguous() && dE->size(1) == C, "dE must be (V, C) contiguous");
+    const bool small = dE->size(0) <= 32767;  // int16 keys: a 2-pass radix sort instead of 8
+    Tensor keys = small ? ids.reshape({-1}).to(torch::kInt16) : ids.reshape({-1});
+    auto sorted = keys.sort();
+    Tensor sid = std::get<0>(sorted).to(torch::kInt64).contiguous(), perm = std::get<1>(sorted).contiguous();
+    pio::embed_bwd_sorted_launch(sid.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), f32p(g), dE->data_ptr<float>(),
+                                 ids.numel(), C, (float)scale, stream());
+  }
+  if (dP.has_value())
+    pio::embed_bwd_launch(ids.data_ptr<int64_t>(), f32p(g), nullptr, dP->data_ptr<float>(), B, L, C, (float)scale,
+                          stream());
 }
 
 std::vector<Tensor> text_mask(Tensor x, OptT pad, Tensor u, Tensor rid, int64_t unk, int64_t mask, double p) {
@@ -344,6 +387,15 @@ void adamw(Tensor p, Tensor g, Tensor m, Tensor v, OptT shadow, Tensor hyper, do
                     (float)eps, (float)wd, (float)clip, (float)gscale, stream());
 }
 
+// self-test of the device cross-lane reductions: (6, 64) = wave_sum, wave_max, half_sum,
+// half_max, xor16_sum, xor32_sum of a 64-element fp32 vector
+Tensor reduce_probe(Tensor x) {
+  TORCH_CHECK(x.is_contiguous() && x.numel() == 64, "reduce_probe takes 64 floats");
+  Tensor out = torch::empty({6, 64}, x.options().dtype(torch::kFloat32));
+  pio::reduce_probe_launch(f32p(x), out.data_ptr<float>(), stream());
+  return out;
+}
+
 void cast_bf16(Tensor x, Tensor y) {
   TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && x.numel() == y.numel());
   pio::cast_bf16_launch(f32p(x), reinterpret_cast<uint16_t*>(y.data_ptr()), x.numel(), stream());
@@ -366,5 +418,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sumsq", &sumsq);
   m.def("adamw", &adamw);
   m.def("cast_bf16", &cast_bf16);
+  m.def("reduce_probe", &reduce_probe);
   m.attr("arch") = "gfx950";
 }

@@ -91,6 +91,10 @@ def build(force: bool = False, jobs: int = 0, debug: bool = False, verbose: bool
         _run(link)
         if verbose:
             print(f"[perceiver_io_amd] linked {out.relative_to(PKG.parent)}")
+    keep = {p.name for p in objs + [bobj]}
+    for stale in BUILD.glob("*.o"):  # objects of superseded sources (the cache holds the current ones)
+        if stale.name not in keep:
+            stale.unlink()
     return out
 
 

@@ -64,16 +64,65 @@ __device__ __forceinline__ bf16x8 frag_ks(const uint16_t* lds, int ld, int i0, i
   return r;
 }
 
-// ---- reductions ---------------------------------------------------------------------
+// ---- reductions (VALU only: DPP within 16-lane rows, gfx950 lane swaps across rows) --
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+// v_permlane16_swap exchanges the odd 16-lane rows of its first operand with the even rows of
+// its second, v_permlane32_swap the upper half of the first with the lower half of the second;
+// with both operands = v the two registers end up holding v[l] and v[l ^ 16] (resp. v[l ^ 32])
+// in some order.  Inline asm with two in/out operands: the instruction rewrites BOTH registers
+// (with identical inputs the builtin lets the compiler merge them into one register, which
+// swaps a register with itself).  s_nop 1 = the 2 wait states a VALU write of either operand
+// needs before the swap reads it.
+__device__ __forceinline__ void xor16_pair(float v, float& a, float& b) {
+  a = v;
+  b = v;
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+__device__ __forceinline__ void xor32_pair(float v, float& a, float& b) {
+  a = v;
+  b = v;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+__device__ __forceinline__ float xor16_sum(float v) { float a, b; xor16_pair(v, a, b); return a + b; }
+__device__ __forceinline__ float xor32_sum(float v) { float a, b; xor32_pair(v, a, b); return a + b; }
+__device__ __forceinline__ float xor32_max(float v) { float a, b; xor32_pair(v, a, b); return fmaxf(a, b); }
+
+// reductions over each 32-lane half (lanes l and l ^ 1..16)
+__device__ __forceinline__ float half_sum(float v) {
+  v += dpp<0xB1>(v);
+  v += dpp<0x4E>(v);
+  v += dpp<0x124>(v);
+  v += dpp<0x128>(v);
+  return xor16_sum(v);
+}
+__device__ __forceinline__ float half_max(float v) {
+  v = fmaxf(v, dpp<0xB1>(v));
+  v = fmaxf(v, dpp<0x4E>(v));
+  v = fmaxf(v, dpp<0x124>(v));
+  v = fmaxf(v, dpp<0x128>(v));
+  float a, b;
+  xor16_pair(v, a, b);
+  return fmaxf(a, b);
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp<0x124>(v);  // row_ror:4
+  v += dpp<0x128>(v);  // row_ror:8
+  return xor32_sum(xor16_sum(v));
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  v = fmaxf(v, dpp<0xB1>(v));
+  v = fmaxf(v, dpp<0x4E>(v));
+  v = fmaxf(v, dpp<0x124>(v));
+  v = fmaxf(v, dpp<0x128>(v));
+  float a, b;
+  xor16_pair(v, a, b);
+  xor32_pair(fmaxf(a, b), a, b);
+  return fmaxf(a, b);
 }
 
 // ---- GELU (erf form, nn.GELU default) ------------------------------------------------

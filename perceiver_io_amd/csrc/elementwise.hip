@@ -31,20 +31,60 @@ __global__ void embed_fwd_kernel(const int64_t* __restrict__ ids, const float* _
   }
 }
 
-// dE[ids[r]] += g[r] * scale (atomics), dP[l] += Σ_b g[b, l] (per-column sums over the batch)
+// dE[ids[r]] += g[r] * scale, dP[l] += Σ_b g[b, l]  (both fp32 atomics)
+// grid (L, ceil(B / EB)): block (l, j) handles batch rows j·EB .. j·EB+EB-1 of position l, one
+// thread per channel; the EB loads per thread are issued together, then the EB scatter-adds
+constexpr int EB = 16;
 __global__ void embed_bwd_kernel(const int64_t* __restrict__ ids, const float* __restrict__ g, float* __restrict__ dE,
                                  float* __restrict__ dP, int B, int L, int C, float scale) {
-  // one block per position l: sums the batch for dP exactly (no atomics), scatters dE rows
-  const int l = blockIdx.x;
+  const int l = blockIdx.x, b0 = blockIdx.y * EB;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float acc = 0.f;
-    for (int b = 0; b < B; ++b) {
-      const long long r = (long long)b * L + l;
-      const float v = g[r * C + c];
-      acc += v;
-      if (dE) atomicAdd(dE + ids[r] * C + c, v * scale);
+    float v[EB];
+    int64_t id[EB];
+#pragma unroll
+    for (int j = 0; j < EB; ++j) {
+      const long long r = (long long)(b0 + j) * L + l;
+      const bool ok = b0 + j < B;
+      v[j] = ok ? g[r * C + c] : 0.f;
+      id[j] = ok ? ids[r] : -1;
     }
-    if (dP) dP[(long long)l * C + c] += acc;
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < EB; ++j) {
+      acc += v[j];
+      if (dE && id[j] >= 0) atomicAdd(dE + id[j] * C + c, v[j] * scale);
+    }
+    if (dP) atomicAdd(dP + (long long)l * C + c, acc);
+  }
+}
+
+// dE[id] += scale · Σ g rows with that id, over token positions SORTED by id (perm = the
+// sort permutation): each 64-position chunk folds its runs of equal ids in registers and adds
+// one row per run, so a frequent id ([MASK] is ~12 % of an MLM batch, [PAD] of a padded one)
+// costs a few atomics per chunk instead of one per occurrence.  One thread per channel.
+constexpr int ES = 64;
+__global__ void embed_bwd_sorted_kernel(const int64_t* __restrict__ sorted_ids, const int64_t* __restrict__ perm,
+                                        const float* __restrict__ g, float* __restrict__ dE, long long n, int C,
+                                        float scale) {
+  const long long j0 = (long long)blockIdx.x * ES;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float v[ES];
+#pragma unroll
+    for (int j = 0; j < ES; ++j) v[j] = j0 + j < n ? g[perm[j0 + j] * C + c] : 0.f;
+    int64_t cur = sorted_ids[j0];
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < ES; ++j) {
+      if (j0 + j >= n) break;
+      const int64_t id = sorted_ids[j0 + j];
+      if (id != cur) {
+        atomicAdd(dE + cur * C + c, acc * scale);
+        cur = id;
+        acc = 0.f;
+      }
+      acc += v[j];
+    }
+    atomicAdd(dE + cur * C + c, acc * scale);
   }
 }
 
@@ -131,7 +171,13 @@ void embed_fwd_launch(const int64_t* ids, const float* E, const float* P, float*
 }
 void embed_bwd_launch(const int64_t* ids, const float* g, float* dE, float* dP, int B, int L, int C, float scale,
                       hipStream_t st) {
-  hipLaunchKernelGGL(embed_bwd_kernel, dim3(L), dim3(64), 0, st, ids, g, dE, dP, B, L, C, scale);
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3(L, (B + EB - 1) / EB), dim3(C < 256 ? C : 256), 0, st, ids, g, dE, dP, B, L,
+                     C, scale);
+}
+void embed_bwd_sorted_launch(const int64_t* sorted_ids, const int64_t* perm, const float* g, float* dE, long long n,
+                             int C, float scale, hipStream_t st) {
+  hipLaunchKernelGGL(embed_bwd_sorted_kernel, dim3((unsigned)((n + ES - 1) / ES)), dim3(C < 256 ? C : 256), 0, st,
+                     sorted_ids, perm, g, dE, n, C, scale);
 }
 void text_mask_launch(const int64_t* x, const bool* pad, const float* u, const int64_t* rid, int64_t* xm,
                       int64_t* labels, long long n, int unk_id, int mask_id, float p, hipStream_t st) {
@@ -144,6 +190,22 @@ void adamw_launch(float* p, const float* g, float* m, float* v, uint16_t* shadow
                   float eps, float wd, float clip, float gscale, hipStream_t st) {
   hipLaunchKernelGGL(adamw_kernel, grid_for(n), dim3(256), 0, st, p, g, m, v, shadow, n, hyper, eps, wd, clip, gscale);
 }
+// one wave: the cross-lane reduction helpers of common.h on x[0..63] (numerics self-test)
+__global__ void reduce_probe_kernel(const float* __restrict__ x, float* __restrict__ out) {
+  const int l = threadIdx.x;
+  const float v = x[l];
+  out[l] = wave_sum(v);
+  out[64 + l] = wave_max(v);
+  out[128 + l] = half_sum(v);
+  out[192 + l] = half_max(v);
+  out[256 + l] = xor16_sum(v);
+  out[320 + l] = xor32_sum(v);
+}
+
+void reduce_probe_launch(const float* x, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(reduce_probe_kernel, dim3(1), dim3(64), 0, st, x, out);
+}
+
 void cast_bf16_launch(const float* x, uint16_t* y, long long n, hipStream_t st) {
   hipLaunchKernelGGL(cast_bf16_kernel, grid_for(n), dim3(256), 0, st, x, y, n);
 }

@@ -8,7 +8,8 @@
 //          per-lane (max, sum-exp) with a deferred-rescale online logsumexp, label logit
 //          picked in passing; a combine kernel merges splits → per-row loss and LSE.
 //   bwd-a: dH  = (softmax − onehot)·g · W   (rows × vocab split, fp32 atomics into dH)
-//   bwd-b: dW  = (softmax − onehot)ᵀ·g · H, db = Σ rows   (one vocab chunk per workgroup)
+//   bwd-b: dW  = (softmax − onehot)ᵀ·g · H, db = Σ rows   (vocab chunk × row split, fp32 atomics)
+// Streamed operands (W chunks, H tiles) are register-prefetched one tile ahead.
 // Only the ~15 % masked positions are ever passed in (rows compacted on device).
 #include "common.h"
 
@@ -39,6 +40,28 @@ __device__ __forceinline__ void stage_rows(uint16_t* s, int ld, const uint16_t* 
   }
 }
 
+// register-staged variant: rows [r0, r0+64) × C of a bf16 row-major matrix → NI = C/32
+// 16-byte chunks per thread (issued early, written to LDS after the next barrier)
+template <int C>
+__device__ __forceinline__ void fetch_rows(bf16x8 (&v)[C / 32], const uint16_t* g, int r0, int R) {
+  constexpr int CH = C / 8;
+#pragma unroll
+  for (int i = 0; i < C / 32; ++i) {
+    const int e = threadIdx.x + 256 * i, rr = e / CH, c = (e % CH) * 8;
+    v[i] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (r0 + rr < R) v[i] = *reinterpret_cast<const bf16x8*>(g + (long long)(r0 + rr) * C + c);
+  }
+}
+template <int C>
+__device__ __forceinline__ void store_rows(const bf16x8 (&v)[C / 32], uint16_t* s, int ld) {
+  constexpr int CH = C / 8;
+#pragma unroll
+  for (int i = 0; i < C / 32; ++i) {
+    const int e = threadIdx.x + 256 * i, rr = e / CH, c = (e % CH) * 8;
+    *reinterpret_cast<bf16x8*>(s + rr * ld + c) = v[i];
+  }
+}
+
 template <int C>
 __global__ __launch_bounds__(256) void ce_fwd_kernel(const uint16_t* __restrict__ Hm, const int64_t* __restrict__ labels,
                                                      const uint16_t* __restrict__ W, const float* __restrict__ bias,
@@ -62,15 +85,18 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const uint16_t* __restrict_
     m[i] = -1e30f;
     s[i] = 0.f;
   }
+  bf16x8 wr[C / 32];
+  if (c_begin < c_end) fetch_rows<C>(wr, W, c_begin * VB, V);
   for (int c = c_begin; c < c_end; ++c) {
     const int v0 = c * VB;
     __syncthreads();
-    stage_rows<C>(sW, LD, W, v0, V);
+    store_rows<C>(wr, sW, LD);
     __syncthreads();
-    const f32x16 acc = logits_tile<C>(sH, sW, LD);
+    if (c + 1 < c_end) fetch_rows<C>(wr, W, v0 + VB, V);
     const int col = v0 + 32 * (w & 1) + (l & 31);
     const bool valid = col < V;
     const float bv = valid ? bias[col] : 0.f;
+    const f32x16 acc = logits_tile<C>(sH, sW, LD);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       if (valid) {
@@ -84,12 +110,8 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const uint16_t* __restrict_
   // combine over the 32 lanes of each half (same rows), then the two waves sharing rows
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    float mm = m[i];
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) mm = fmaxf(mm, __shfl_xor(mm, o, 64));
-    float ss = s[i] * __expf(m[i] - mm);
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) ss += __shfl_xor(ss, o, 64);
+    const float mm = half_max(m[i]);
+    const float ss = half_sum(s[i] * __expf(m[i] - mm));
     if ((l & 31) == 0) {
       const int rr = 32 * (w >> 1) + acc_row(i, hh);
       sMS[w & 1][rr][0] = mm;
@@ -135,17 +157,23 @@ __global__ __launch_bounds__(256) void ce_bwd_dh_kernel(const uint16_t* __restri
                                                         const int64_t* __restrict__ labels,
                                                         const uint16_t* __restrict__ W, const float* __restrict__ bias,
                                                         const float* __restrict__ lse, const float* __restrict__ gscale,
-                                                        int M, int V, int chunks_per_split, float* __restrict__ dH) {
+                                                        int M, int V, int chunks_per_split, float* __restrict__ dH,
+                                                        const int64_t* __restrict__ rowmap) {
   constexpr int LD = C + 8, LDL = VB + 8, NT = C / 32;
   __shared__ __attribute__((aligned(16))) uint16_t sH[HB * LD];
   __shared__ __attribute__((aligned(16))) uint16_t sW[VB * LD];
   __shared__ __attribute__((aligned(16))) uint16_t sL[HB * LDL];
+  __shared__ long long sDst[HB];  // dH row of each tile row (−1: ignored row)
   const int w = wave_id(), l = lane_id(), hh = l >> 5;
   const int m0 = blockIdx.x * HB, split = blockIdx.y;
   const int nchunks = (V + VB - 1) / VB;
   const int c_begin = split * chunks_per_split, c_end = min(nchunks, c_begin + chunks_per_split);
   const float g = gscale[0];
   stage_rows<C>(sH, LD, Hm, m0, M);
+  if (threadIdx.x < HB) {
+    const int gr = m0 + threadIdx.x;
+    sDst[threadIdx.x] = (gr < M && labels[gr] >= 0) ? (rowmap ? rowmap[gr] : gr) : -1;
+  }
   int lab[16];
   float ls[16];
 #pragma unroll
@@ -159,16 +187,19 @@ __global__ __launch_bounds__(256) void ce_bwd_dh_kernel(const uint16_t* __restri
   f32x16 acc_o[MAXT];
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc_o[t] = f32x16{};
+  bf16x8 wr[C / 32];
+  if (c_begin < c_end) fetch_rows<C>(wr, W, c_begin * VB, V);
   for (int c = c_begin; c < c_end; ++c) {
     const int v0 = c * VB;
     __syncthreads();
-    stage_rows<C>(sW, LD, W, v0, V);
+    store_rows<C>(wr, sW, LD);
     __syncthreads();
-    const f32x16 acc = logits_tile<C>(sH, sW, LD);
+    if (c + 1 < c_end) fetch_rows<C>(wr, W, v0 + VB, V);
     const int coll = 32 * (w & 1) + (l & 31);
     const int col = v0 + coll;
     const bool valid = col < V;
     const float bv = valid ? bias[col] : 0.f;
+    const f32x16 acc = logits_tile<C>(sH, sW, LD);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const float d = valid ? dlogit(acc[i] + bv, ls[i], col, lab[i], g) : 0.f;
@@ -193,28 +224,35 @@ __global__ __launch_bounds__(256) void ce_bwd_dh_kernel(const uint16_t* __restri
       const int r0 = 32 * (tg / NT), n0 = 32 * (tg % NT);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int gr = m0 + r0 + acc_row(i, hh);
-        if (gr < M) atomicAdd(dH + (long long)gr * C + n0 + (l & 31), acc_o[t][i]);
+        // dH row: the compacted row's source position (rowmap) or the row itself; ignored rows
+        // (label −100, incl. compaction padding) carry no gradient
+        const long long dst = sDst[r0 + acc_row(i, hh)];
+        if (dst >= 0) atomicAdd(dH + dst * C + n0 + (l & 31), acc_o[t][i]);
       }
     }
   }
 }
 
-// bwd-b: dW[v][c] = Σ_r dl[r][v] H[r][c], db[v] = Σ_r dl[r][v]; one 64-entry vocab chunk per block
+// bwd-b: dW[v][c] += Σ_r dl[r][v] H[r][c], db[v] += Σ_r dl[r][v]; grid (vocab chunk, row split),
+// H tiles (+ their LSE / labels) register-prefetched one tile ahead, partials added atomically
 template <int C>
 __global__ __launch_bounds__(256) void ce_bwd_dw_kernel(const uint16_t* __restrict__ Hm,
                                                         const int64_t* __restrict__ labels,
                                                         const uint16_t* __restrict__ W, const float* __restrict__ bias,
                                                         const float* __restrict__ lse, const float* __restrict__ gscale,
-                                                        int M, int V, float* __restrict__ dW, float* __restrict__ db,
-                                                        int accumulate) {
+                                                        int M, int V, int tiles_per_split, float* __restrict__ dW,
+                                                        float* __restrict__ db) {
   constexpr int LD = C + 8, LDL = VB + 8, NT = C / 32;
   __shared__ __attribute__((aligned(16))) uint16_t sH[HB * LD];
   __shared__ __attribute__((aligned(16))) uint16_t sW[VB * LD];
   __shared__ __attribute__((aligned(16))) uint16_t sL[HB * LDL];
+  __shared__ float sLse[HB];
+  __shared__ int sLab[HB];
   __shared__ float sB[2][64];
   const int w = wave_id(), l = lane_id(), hh = l >> 5;
   const int v0 = blockIdx.x * VB;
+  const int mt_begin = blockIdx.y * tiles_per_split;
+  const int mt_end = min((M + HB - 1) / HB, mt_begin + tiles_per_split);
   const float g = gscale[0];
   stage_rows<C>(sW, LD, W, v0, V);
   const int coll = 32 * (w & 1) + (l & 31);
@@ -226,18 +264,31 @@ __global__ __launch_bounds__(256) void ce_bwd_dw_kernel(const uint16_t* __restri
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc_o[t] = f32x16{};
   float bsum = 0.f;
-  for (int m0 = 0; m0 < M; m0 += HB) {
+  bf16x8 hr[C / 32];
+  float aux = 0.f;  // threads [0,64): LSE of row tid, [64,128): label of row tid-64
+  auto fetch = [&](int mt) {
+    fetch_rows<C>(hr, Hm, mt * HB, M);
+    const int t = threadIdx.x & 63, gr = mt * HB + t;
+    if (threadIdx.x < 64) aux = gr < M ? lse[gr] : 0.f;
+    else if (threadIdx.x < 128) aux = __int_as_float(gr < M ? (int)labels[gr] : -100);
+  };
+  if (mt_begin < mt_end) fetch(mt_begin);
+  for (int mt = mt_begin; mt < mt_end; ++mt) {
+    const int m0 = mt * HB;
     __syncthreads();
-    stage_rows<C>(sH, LD, Hm, m0, M);
+    store_rows<C>(hr, sH, LD);
+    if (threadIdx.x < 64) sLse[threadIdx.x] = aux;
+    else if (threadIdx.x < 128) sLab[threadIdx.x - 64] = __float_as_int(aux);
     __syncthreads();
+    if (mt + 1 < mt_end) fetch(mt + 1);
     const f32x16 acc = logits_tile<C>(sH, sW, LD);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int gr = m0 + 32 * (w >> 1) + acc_row(i, hh);
+      const int rr = 32 * (w >> 1) + acc_row(i, hh);
       float d = 0.f;
-      if (gr < M && valid) d = dlogit(acc[i] + bv, lse[gr], col, (int)labels[gr], g);
+      if (m0 + rr < M && valid) d = dlogit(acc[i] + bv, sLse[rr], col, sLab[rr], g);
       bsum += d;
-      sL[(32 * (w >> 1) + acc_row(i, hh)) * LDL + coll] = f2bf(d);
+      sL[rr * LDL + coll] = f2bf(d);
     }
     __syncthreads();
     // dW chunk (64 vocab × C) += dlᵀ · H : A = dl stored [r][v] (k=r strided), B = H [r][c] (k strided)
@@ -252,13 +303,10 @@ __global__ __launch_bounds__(256) void ce_bwd_dw_kernel(const uint16_t* __restri
     }
   }
   // bias: reduce bsum over the two lane halves and the two waves sharing a column set
-  bsum += __shfl_xor(bsum, 32, 64);
+  bsum = xor32_sum(bsum);
   if (hh == 0) sB[w >> 1][coll] = bsum;
   __syncthreads();
-  if (threadIdx.x < 64 && v0 + threadIdx.x < V) {
-    const float v = sB[0][threadIdx.x] + sB[1][threadIdx.x];
-    db[v0 + threadIdx.x] = accumulate ? db[v0 + threadIdx.x] + v : v;
-  }
+  if (threadIdx.x < 64 && v0 + threadIdx.x < V) atomicAdd(db + v0 + threadIdx.x, sB[0][threadIdx.x] + sB[1][threadIdx.x]);
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) {
     const int tg = w + 4 * t;
@@ -267,18 +315,16 @@ __global__ __launch_bounds__(256) void ce_bwd_dw_kernel(const uint16_t* __restri
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int vv = v0 + r0 + acc_row(i, hh);
-        if (vv < V) {
-          float* p = dW + (long long)vv * C + n0 + (l & 31);
-          *p = accumulate ? *p + acc_o[t][i] : acc_o[t][i];
-        }
+        if (vv < V) atomicAdd(dW + (long long)vv * C + n0 + (l & 31), acc_o[t][i]);
       }
     }
   }
 }
 
-static int pick_split(int M, int nchunks) {
+// vocab splits so that a launch has ≈ target workgroups (several per CU hide the W-chunk latency)
+static int pick_split(int M, int nchunks, int target) {
   const int mt = (M + HB - 1) / HB;
-  int s = (512 + mt - 1) / mt;  // aim for ≈512 workgroups
+  int s = (target + mt - 1) / mt;
   s = s < 1 ? 1 : s;
   return s > nchunks ? nchunks : s;
 }
@@ -295,18 +341,28 @@ void ce_fwd_launch(int C, const uint16_t* Hm, const int64_t* labels, const uint1
                      loss_rows, lse);
 }
 
-int ce_num_splits(int M, int V) { return pick_split(M, (V + VB - 1) / VB); }
+int ce_num_splits(int M, int V) { return pick_split(M, (V + VB - 1) / VB, 2048); }
 
 void ce_bwd_launch(int C, const uint16_t* Hm, const int64_t* labels, const uint16_t* W, const float* bias,
-                   const float* lse, const float* gscale, int M, int V, float* dH, float* dW, float* db, int accumulate,
-                   hipStream_t st) {
+                   const float* lse, const float* gscale, int M, int V, float* dH, const int64_t* rowmap, float* dW,
+                   float* db, int accumulate, hipStream_t st) {
   const int nchunks = (V + VB - 1) / VB;
-  const int nsplit = pick_split(M, nchunks);
+  const int nsplit = pick_split(M, nchunks, 512);  // dH partials are added atomically: few splits
   const int cps = (nchunks + nsplit - 1) / nsplit;
-  dim3 ga((M + HB - 1) / HB, nsplit), gb(nchunks);
+  // dW: (vocab chunk × row split) workgroups, ≈ 4 per CU; dW / db partials added atomically
+  const int mtiles = (M + HB - 1) / HB;
+  int rsplit = (1024 + nchunks - 1) / nchunks;
+  rsplit = rsplit < 1 ? 1 : (rsplit > mtiles ? mtiles : rsplit);
+  const int tps = (mtiles + rsplit - 1) / rsplit;
+  rsplit = (mtiles + tps - 1) / tps;
+  if (!accumulate) {
+    (void)hipMemsetAsync(dW, 0, sizeof(float) * (size_t)V * C, st);
+    (void)hipMemsetAsync(db, 0, sizeof(float) * (size_t)V, st);
+  }
+  dim3 ga((M + HB - 1) / HB, nsplit), gb(nchunks, rsplit);
 #define CEB(CC)                                                                                                  \
-  hipLaunchKernelGGL(ce_bwd_dh_kernel<CC>, ga, dim3(256), 0, st, Hm, labels, W, bias, lse, gscale, M, V, cps, dH); \
-  hipLaunchKernelGGL(ce_bwd_dw_kernel<CC>, gb, dim3(256), 0, st, Hm, labels, W, bias, lse, gscale, M, V, dW, db, accumulate)
+  hipLaunchKernelGGL(ce_bwd_dh_kernel<CC>, ga, dim3(256), 0, st, Hm, labels, W, bias, lse, gscale, M, V, cps, dH, rowmap); \
+  hipLaunchKernelGGL(ce_bwd_dw_kernel<CC>, gb, dim3(256), 0, st, Hm, labels, W, bias, lse, gscale, M, V, tps, dW, db)
   if (C == 64) { CEB(64); }
   else if (C == 128) { CEB(128); }
   else if (C == 32) { CEB(32); }

@@ -107,10 +107,18 @@ __device__ __forceinline__ void stage(uint16_t* s, int ld, const T* g, long long
   }
 }
 
-// fp32 gradient targets of the post-attention block (views of the flat gradient buffer)
+// fp32 gradient targets of the post-attention block (views of the flat gradient buffer).
+// Vector targets (biases, LN affine) may be replicated: workgroup i adds into replica
+// i % kGradReplicas at vrs floats per replica (vrs = 0: one copy), so that no address takes
+// more than grid/8 atomic adds; the replicas are folded once per step (ops/optim.py).
+constexpr int kGradReplicas = 8;
 struct PostAttnGrads {
   float *dWo, *dbo, *dg2, *dbe2, *dW1, *db1, *dW2, *db2;
+  int vrs;
 };
+__device__ __forceinline__ float* rep(float* p, int vrs) {
+  return p + (blockIdx.x & (kGradReplicas - 1)) * vrs;
+}
 
 __host__ __device__ __forceinline__ int round_up(int x, int m) { return (x + m - 1) / m * m; }
 
@@ -124,10 +132,6 @@ __host__ __device__ __forceinline__ int round_up(int x, int m) { return (x + m -
 // a phase is issued before its first use, so a kernel pays the memory latency once per
 // phase instead of once per row.
 // ------------------------------------------------------------------------------------
-template <int CTRL>
-__device__ __forceinline__ float dpp(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
-}
 __device__ __forceinline__ float quad_sum(float v) {  // over lanes 4r .. 4r+3
   v += dpp<0xB1>(v);                                    // quad_perm [1,0,3,2]
   v += dpp<0x4E>(v);                                    // quad_perm [2,3,0,1]
@@ -136,9 +140,7 @@ __device__ __forceinline__ float quad_sum(float v) {  // over lanes 4r .. 4r+3
 __device__ __forceinline__ float rows16_sum(float v) {  // over lanes ≡ l (mod 4)
   v += dpp<0x124>(v);                                     // row_ror:4
   v += dpp<0x128>(v);                                     // row_ror:8
-  v += __shfl_xor(v, 16, 64);
-  v += __shfl_xor(v, 32, 64);
-  return v;
+  return xor32_sum(xor16_sum(v));
 }
 __device__ __forceinline__ int rp_row() { return threadIdx.x >> 2; }
 __device__ __forceinline__ int rp_col(int j) { return 8 * ((threadIdx.x & 3) + 4 * j); }
@@ -406,7 +408,8 @@ __global__ __launch_bounds__(256) void post_attn_fwd_kernel(
     const float* __restrict__ bo, const float* __restrict__ g2, const float* __restrict__ be2, float eps,
     const uint16_t* __restrict__ W1, const float* __restrict__ b1, const uint16_t* __restrict__ W2,
     const float* __restrict__ b2, float* __restrict__ Z, float* __restrict__ Ysave, float* __restrict__ mean2,
-    float* __restrict__ rstd2, uint16_t* __restrict__ Usave, int R) {
+    float* __restrict__ rstd2, uint16_t* __restrict__ Usave, int R, int Rx) {
+  // X has Rx rows, row r of the tile adds X[r % Rx] (Rx < R: batch-broadcast residual)
   constexpr int LD = C + 8, LDF = C + 4, MAXT = (2 * C / 32 + 3) / 4, NCH = C / 32;
   constexpr int NWB = C <= 64 ? 3 : 1, NIW = (C * C / 8 + 255) / 256;
   __shared__ __attribute__((aligned(16))) uint16_t sA[64 * LD];   // O → LN2(Y) → GELU(U)
@@ -426,7 +429,7 @@ __global__ __launch_bounds__(256) void post_attn_fwd_kernel(
     tile_fetch<NIW>(wr[2], W2, C, 0, C, C, C, C, av);
   }
   float yv[NCH][8];
-  row_load<NCH>(yv, X, C, gr, R, C, av);
+  row_load<NCH>(yv, X, C, gr < R ? gr % Rx : Rx, Rx, C, av);
   for (int k = threadIdx.x; k < C; k += blockDim.x) {
     sP[0][k] = bo[k]; sP[1][k] = b1[k]; sP[2][k] = b2[k]; sP[3][k] = g2[k]; sP[4][k] = be2[k];
   }
@@ -664,15 +667,15 @@ __global__ __launch_bounds__(256) void post_attn_bwd_kernel(
           sF[m * LDF + n] = du;
           cs += du;
         }
-        cs += __shfl_xor(cs, 32, 64);
+        cs = xor32_sum(cs);
         if (l < 32) sDb1[mt][n0 + l] = cs;
       }
     }
   }
   __syncthreads();
   for (int k = threadIdx.x; k < C; k += blockDim.x) {
-    atomicAdd(gr_out.db1 + k, sDb1[0][k] + sDb1[1][k]);
-    atomicAdd(gr_out.db2 + k, sPart[0][k] + sPart[0][C + k] + sPart[0][2 * C + k] + sPart[0][3 * C + k]);
+    atomicAdd(rep(gr_out.db1, gr_out.vrs) + k, sDb1[0][k] + sDb1[1][k]);
+    atomicAdd(rep(gr_out.db2, gr_out.vrs) + k, sPart[0][k] + sPart[0][C + k] + sPart[0][2 * C + k] + sPart[0][3 * C + k]);
   }
   if constexpr (NWB == 1) tile_store<NIW>(wr[0], sW[0], LD, C, C);
   {
@@ -732,9 +735,9 @@ __global__ __launch_bounds__(256) void post_attn_bwd_kernel(
   }
   __syncthreads();
   for (int k = threadIdx.x; k < C; k += blockDim.x) {
-    atomicAdd(gr_out.dg2 + k, sPart[1][k] + sPart[1][C + k] + sPart[1][2 * C + k] + sPart[1][3 * C + k]);
-    atomicAdd(gr_out.dbe2 + k, sPart[2][k] + sPart[2][C + k] + sPart[2][2 * C + k] + sPart[2][3 * C + k]);
-    atomicAdd(gr_out.dbo + k, sPart[3][k] + sPart[3][C + k] + sPart[3][2 * C + k] + sPart[3][3 * C + k]);
+    atomicAdd(rep(gr_out.dg2, gr_out.vrs) + k, sPart[1][k] + sPart[1][C + k] + sPart[1][2 * C + k] + sPart[1][3 * C + k]);
+    atomicAdd(rep(gr_out.dbe2, gr_out.vrs) + k, sPart[2][k] + sPart[2][C + k] + sPart[2][2 * C + k] + sPart[2][3 * C + k]);
+    atomicAdd(rep(gr_out.dbo, gr_out.vrs) + k, sPart[3][k] + sPart[3][C + k] + sPart[3][2 * C + k] + sPart[3][3 * C + k]);
   }
 
   // ---- out-projection
@@ -775,7 +778,8 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
     const TG* __restrict__ G, int g_rs, int N, const uint16_t* __restrict__ W, int Kin, const TX* __restrict__ X,
     int x_rs, const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ lnw,
     const float* __restrict__ lnb, const float* __restrict__ dres, int dres_rs, float* __restrict__ dX, int dx_rs,
-    float* __restrict__ dlnw, float* __restrict__ dlnb, float* __restrict__ dW, float* __restrict__ db, int R) {
+    float* __restrict__ dlnw, float* __restrict__ dlnb, float* __restrict__ dW, float* __restrict__ db, int vrs,
+    int R) {
   constexpr int KP = 32 * NCH, LD = KP + 8, LDG = 64 + 8, LDF = KP + 4;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* sG = smem;                                   // [64][LDG]  G chunk
@@ -839,9 +843,7 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
       if (db) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          float s = cs[e] + dpp<0x128>(cs[e]);  // lanes i, i ± 8 share a column group
-          s += __shfl_xor(s, 16, 64);
-          s += __shfl_xor(s, 32, 64);
+          const float s = xor32_sum(xor16_sum(cs[e] + dpp<0x128>(cs[e])));  // lanes ≡ l (mod 8)
           if (l < 8) sPb[w * 64 + 8 * l + e] = s;
         }
       }
@@ -849,7 +851,7 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
     __syncthreads();
     if (dW && db && threadIdx.x < 64 && nc + (int)threadIdx.x < N) {
       const int t = threadIdx.x;
-      atomicAdd(db + nc + t, sPb[t] + sPb[64 + t] + sPb[128 + t] + sPb[192 + t]);
+      atomicAdd(rep(db, vrs) + nc + t, sPb[t] + sPb[64 + t] + sPb[128 + t] + sPb[192 + t]);
     }
   }
   for_acc<MAXT>(64, KP, [&](int t, int m, int n, int i) { sF[m * LDF + n] = acc[t][i]; });
@@ -907,8 +909,8 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
   }
   if (lnw && dlnw) {
     __syncthreads();
-    colsum_flush(sPart, KP, dlnw, Kin);
-    colsum_flush(sPart + 4 * KP, KP, dlnb, Kin);
+    colsum_flush(sPart, KP, rep(dlnw, vrs), Kin);
+    colsum_flush(sPart + 4 * KP, KP, rep(dlnb, vrs), Kin);
   }
 }
 
@@ -1015,11 +1017,11 @@ void ln_linear_fwd_launch(const void* X, bool x_bf16, int x_rs, int R, int Kin, 
 void post_attn_fwd_launch(int C, const uint16_t* O, const float* X, const uint16_t* Wo, const float* bo,
                           const float* g2, const float* be2, float eps, const uint16_t* W1, const float* b1,
                           const uint16_t* W2, const float* b2, float* Z, float* Ysave, float* mean2, float* rstd2,
-                          uint16_t* Usave, int R, hipStream_t st) {
+                          uint16_t* Usave, int R, int Rx, hipStream_t st) {
   dim3 grid((R + 63) / 64);
 #define PAF(CC)                                                                                                     \
   hipLaunchKernelGGL(post_attn_fwd_kernel<CC>, grid, dim3(256), 0, st, O, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, \
-                     Z, Ysave, mean2, rstd2, Usave, R)
+                     Z, Ysave, mean2, rstd2, Usave, R, Rx)
   if (C == 64) PAF(64);
   else if (C == 128) PAF(128);
   else if (C == 32) PAF(32);
@@ -1043,24 +1045,24 @@ void post_attn_bwd_launch(int C, const float* dZ, const float* Ysave, const floa
 template <typename TG, typename TX, int NCH>
 static void ln_linear_bwd_t(const void* G, int g_rs, int N, const uint16_t* W, int Kin, const void* X, int x_rs,
                             const float* mean, const float* rstd, const float* lnw, const float* lnb, const float* dres,
-                            int dres_rs, float* dX, int dx_rs, float* dlnw, float* dlnb, float* dW, float* db, int R,
-                            hipStream_t st) {
+                            int dres_rs, float* dX, int dx_rs, float* dlnw, float* dlnb, float* dW, float* db, int vrs,
+                            int R, hipStream_t st) {
   constexpr int KP = 32 * NCH;
   const size_t smem = 64 * 72 * 2 + 2 * 64 * (KP + 8) * 2 + 64 * (KP + 4) * 4 + 8 * KP * 4 + 4 * 64 * 4;
   auto fn = ln_linear_bwd_kernel<TG, TX, NCH>;
   set_smem_once((const void*)fn);
   hipLaunchKernelGGL(fn, dim3((R + 63) / 64), dim3(256), smem, st, (const TG*)G, g_rs, N, W, Kin, (const TX*)X, x_rs,
-                     mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, dlnw, dlnb, dW, db, R);
+                     mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, dlnw, dlnb, dW, db, vrs, R);
 }
 
 template <typename TG, typename TX>
 static void ln_linear_bwd_n(int nch, const void* G, int g_rs, int N, const uint16_t* W, int Kin, const void* X,
                             int x_rs, const float* mean, const float* rstd, const float* lnw, const float* lnb,
                             const float* dres, int dres_rs, float* dX, int dx_rs, float* dlnw, float* dlnb, float* dW,
-                            float* db, int R, hipStream_t st) {
+                            float* db, int vrs, int R, hipStream_t st) {
 #define LNB(K)                                                                                                    \
   ln_linear_bwd_t<TG, TX, K>(G, g_rs, N, W, Kin, X, x_rs, mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, dlnw, \
-                             dlnb, dW, db, R, st)
+                             dlnb, dW, db, vrs, R, st)
   switch (nch) {
     case 1: LNB(1); break;
     case 2: LNB(2); break;
@@ -1073,11 +1075,11 @@ static void ln_linear_bwd_n(int nch, const void* G, int g_rs, int N, const uint1
 void ln_linear_bwd_launch(const void* G, bool g_bf16, int g_rs, int N, const uint16_t* W, int Kin, const void* X,
                           bool x_bf16, int x_rs, const float* mean, const float* rstd, const float* lnw,
                           const float* lnb, const float* dres, int dres_rs, float* dX, int dx_rs, float* dlnw,
-                          float* dlnb, float* dW, float* db, int R, hipStream_t st) {
+                          float* dlnb, float* dW, float* db, int vrs, int R, hipStream_t st) {
   const int nch = pick_nch(Kin);  // Kin ≤ 160 → ≤ 5
 #define LDG(TG, TX)                                                                                           \
   ln_linear_bwd_n<TG, TX>(nch, G, g_rs, N, W, Kin, X, x_rs, mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, \
-                          dlnw, dlnb, dW, db, R, st)
+                          dlnw, dlnb, dW, db, vrs, R, st)
   if (g_bf16 && x_bf16) LDG(uint16_t, uint16_t);
   else if (g_bf16) LDG(uint16_t, float);
   else if (x_bf16) LDG(float, uint16_t);

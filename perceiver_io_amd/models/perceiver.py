@@ -200,6 +200,4 @@ class PerceiverMLM(nn.Module):
             # reference compute: all K queries decoded, full (B, V, L) logits, CE with ignore_index
             logits = self.decoder(x_latent)[:, :l, :]
             return torch.nn.functional.cross_entropy(logits.transpose(1, 2), labels, ignore_index=-100)
-        h = self.decoder.hidden(x_latent, num_queries=l)
-        lin = self.decoder.output_adapter.linear
-        return ops.mlm_head.masked_lm_loss(h, labels, lin.weight, lin.bias)
+        return ops.mlm_head.masked_decode_loss(self.decoder, x_latent, labels)

@@ -110,6 +110,9 @@ def attn_bwd(q, k, v, kmask, o, dO, lse, delta_in, H, D, scale, dropout_p, seed,
 
 
 def post_attn_fwd(o, x, wo, bo, g2, be2, eps, w1, b1, w2, b2):
+    """x may have R / k rows (batch-broadcast residual): row r adds x[r % rows(x)]."""
+    if x.shape[0] != o.shape[0]:
+        x = x.repeat(o.shape[0] // x.shape[0], 1)
     y = x + _bf(o.float()) @ _bf(wo.float()).t() + bo
     xn, m, r = _ln(y, g2, be2, eps)
     u = _bf(xn) @ _bf(w1.float()).t() + b1
@@ -201,13 +204,18 @@ def ce_fwd(h, labels, w, bias):
     return loss, lse
 
 
-def ce_bwd(h, labels, w, bias, lse, gscale, dH, dW, db, accumulate):
+def ce_bwd(h, labels, w, bias, lse, gscale, dH, dW, db, accumulate, rowmap=None):
     logits = _bf(h.float()) @ _bf(w.float()).t() + bias
     p = torch.exp(logits - lse[:, None])
     valid = (labels >= 0).float()[:, None]
     onehot = F.one_hot(labels.clamp(min=0), w.shape[0]).float()
     dl = (p - onehot) * valid * gscale
-    dH.add_(_bf(dl) @ _bf(w.float()))
+    rows = _bf(dl) @ _bf(w.float())
+    if rowmap is None:
+        dH.add_(rows)
+    else:
+        keep = labels >= 0
+        dH.index_add_(0, rowmap[keep], rows[keep])
     gw = _bf(dl).t() @ _bf(h.float())
     gb = dl.sum(0)
     if accumulate:

@@ -169,8 +169,8 @@ class _LayerFn(torch.autograd.Function):
         nsplit = pick_splits(B, H, Nq, k3.shape[1])
         o, lse = K.attn_fwd(q3, k3, v3, kmask, H, D, scale, p_attn, seed, nsplit)
         o2 = o.view(B * Nq, C)
-        xres = xq2 if Bq == B else x_q.expand(B, Nq, C).reshape(B * Nq, C).contiguous()
-        z, y, m2, r2, u = K.post_attn_fwd(o2, xres, wo, bo, g2, be2, EPS, w1, b1, w2, b2)
+        # a batch-broadcast query stream (Bq = 1) is added as the residual without expanding it
+        z, y, m2, r2, u = K.post_attn_fwd(o2, xq2, wo, bo, g2, be2, EPS, w1, b1, w2, b2)
         ctx.spec, ctx.bw, ctx.seed, ctx.p_attn = spec, bw, seed, p_attn
         ctx.dims = (B, Bq, Nq, C, H, D, scale)
         ctx.kv_grad = x_kv is not None and ctx.needs_input_grad[5]

@@ -34,14 +34,20 @@ def capacity(n_positions: int, p: float = 0.15) -> int:
 
 
 class _MaskedCE(torch.autograd.Function):
+    """Mean CE over rows ``idx`` of ``h`` (``idx=None``: every row, ``h`` already compacted)."""
+
     @staticmethod
     def forward(ctx, h, weight, bias, idx, labels_c, count):
         c = h.shape[-1]
-        hs = h.reshape(-1, c).index_select(0, idx).to(torch.bfloat16).contiguous()
-        wb = weight.to(torch.bfloat16).contiguous()
+        h2 = h.reshape(-1, c)
+        hs = (h2 if idx is None else h2.index_select(0, idx)).to(torch.bfloat16).contiguous()
+        from .fused import weight_cache
+
+        wb = weight_cache.get(weight)  # bf16 shadow written by the fused optimizer
         loss_rows, lse = ext.ce_fwd(hs, labels_c, wb, bias.contiguous())
         denom = count.clamp(min=1).to(torch.float32)
-        ctx.save_for_backward(hs, wb, bias, lse, idx, labels_c, denom)
+        ctx.save_for_backward(hs, wb, bias, lse, idx if idx is not None else torch.empty(0, dtype=torch.int64),
+                              labels_c, denom)
         ctx.hshape = h.shape
         ctx.weight, ctx.bias_p = weight, bias
         return loss_rows.sum() / denom
@@ -51,15 +57,15 @@ class _MaskedCE(torch.autograd.Function):
         hs, wb, bias, lse, idx, labels_c, denom = ctx.saved_tensors
         weight = ctx.weight
         gscale = (g.to(torch.float32) / denom).reshape(1).contiguous()
-        d_rows = torch.zeros(hs.shape, device=hs.device, dtype=torch.float32)
-        # vocab-head parameter gradients are accumulated in place into .grad (flat buffer views)
+        # vocab-head parameter gradients are accumulated in place into .grad (flat buffer views);
+        # the hidden-state gradient rows land straight at their source positions (rowmap)
         for p in (weight, ctx.bias_p):
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
-        ext.ce_bwd(hs, labels_c, wb, bias.contiguous(), lse, gscale, d_rows, weight.grad, ctx.bias_p.grad, True)
         shp = ctx.hshape
         dh = torch.zeros((shp[0] * shp[1], shp[2]), device=hs.device, dtype=torch.float32)
-        dh.index_add_(0, idx, d_rows)
+        ext.ce_bwd(hs, labels_c, wb, bias.contiguous(), lse, gscale, dh, weight.grad, ctx.bias_p.grad, True,
+                   idx if idx.numel() else None)
         return dh.view(shp), None, None, None, None, None
 
 
@@ -95,3 +101,68 @@ def masked_lm_loss(h: torch.Tensor, labels: torch.Tensor, weight: torch.Tensor, 
     if hs.shape[0] == 0:
         return logits.sum() * 0.0
     return F.cross_entropy(logits.float(), labels.reshape(-1)[sel])
+
+
+# ------------------------------------------------------------------------------------------
+# training-time decode of the selected positions only
+# ------------------------------------------------------------------------------------------
+def row_capacity(length: int, p: float = 0.15) -> int:
+    """Per-sequence slots for selected positions: expected + 8σ + 16, a multiple of 32, ≤ L
+    (L = 512: 160 slots for ~77 selected; overflow probability < 1e-15 per sequence)."""
+    mu = length * p
+    cap = int(math.ceil(mu + 8.0 * math.sqrt(max(mu * (1 - p), 1.0)) + 16))
+    cap = (cap + 31) // 32 * 32
+    return max(1, min(length, cap))
+
+
+def compact_per_row(labels: torch.Tensor, cap: int):
+    """Sync-free per-sequence compaction of ``labels != -100``: positions ``(B, cap)``, their
+    labels (-100 in unused slots) and the total count."""
+    global _overflow
+    B, L = labels.shape
+    sel = labels != -100
+    pos = torch.cumsum(sel.to(torch.int32), 1) - 1
+    target = torch.where(sel & (pos < cap), pos, torch.full_like(pos, cap)).to(torch.int64)
+    # unused slots point at distinct positions (slot mod L): their zero gradients then do not
+    # pile onto one output-query row in the gather's backward
+    buf = (torch.arange(cap + 1, device=labels.device, dtype=torch.int64) % L).repeat(B, 1)
+    buf.scatter_(1, target, torch.arange(L, device=labels.device, dtype=torch.int64).expand(B, L).contiguous())
+    idx = buf[:, :cap].contiguous()
+    cnt = sel.sum(1, keepdim=True)
+    valid = torch.arange(cap, device=labels.device) < cnt
+    labels_c = torch.where(valid, labels.gather(1, idx), torch.full_like(idx, -100))
+    _overflow = (cnt > cap).any()
+    return idx, labels_c, sel.sum()
+
+
+def compact_lm_loss(h: torch.Tensor, labels_c: torch.Tensor, count: torch.Tensor, weight: torch.Tensor,
+                    bias: torch.Tensor, positions: int):
+    """Mean CE over the rows of a per-sequence-compacted ``(B, cap, C)`` batch whose label is
+    not -100.  The HIP path compacts those rows once more over the whole batch (capacity for
+    ``positions`` tokens at the masking rate), so the vocab GEMMs see only real rows."""
+    from . import use_hip
+
+    if use_hip(h) and h.shape[-1] in (32, 64, 128):
+        idx, lab, cnt = compact_rows(labels_c, capacity(positions))
+        return _MaskedCE.apply(h, weight, bias, idx, lab, cnt)
+    lab = labels_c.reshape(-1)
+    logits = F.linear(h.reshape(-1, h.shape[-1]), weight, bias)
+    return F.cross_entropy(logits.float(), lab, ignore_index=-100, reduction="sum") / count.clamp(min=1)
+
+
+def masked_decode_loss(decoder, x_latent: torch.Tensor, labels: torch.Tensor):
+    """MLM loss decoding only the selected positions.
+
+    Decoder queries never interact (reference ``perceiver/model.py:236``: one cross-attention
+    from the K output queries to the latents), so decoding the ~15 % selected positions of each
+    sequence — gathered into ``row_capacity(L)`` slots — gives the same loss and gradients as
+    decoding all ``L`` at a third of the decoder cost.  The output-query
+    gradient flows back through the gather (index_select → index_add).
+    """
+    B, L = labels.shape
+    decoder.check_latent(x_latent)
+    idx, labels_c, count = compact_per_row(labels, row_capacity(L))
+    q = decoder.output.index_select(0, idx.reshape(-1)).view(B, idx.shape[1], -1)
+    h = decoder.cross_attention(q, x_latent)
+    lin = decoder.output_adapter.linear
+    return compact_lm_loss(h, labels_c, count, lin.weight, lin.bias, B * L)

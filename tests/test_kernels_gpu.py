@@ -42,6 +42,20 @@ def bf(x):
     return x.to(torch.bfloat16)
 
 
+def test_cross_lane_reductions():
+    x = torch.randn(64, device=DEV)
+    out = _ext().reduce_probe(x).cpu()
+    xc = x.cpu()
+    idx = torch.arange(64)
+    halves = xc.view(2, 32)
+    torch.testing.assert_close(out[0], xc.sum().expand(64), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(out[1], xc.max().expand(64))
+    torch.testing.assert_close(out[2], halves.sum(1).repeat_interleave(32), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(out[3], halves.max(1).values.repeat_interleave(32))
+    torch.testing.assert_close(out[4], xc + xc[idx ^ 16])
+    torch.testing.assert_close(out[5], xc + xc[idx ^ 32])
+
+
 @pytest.mark.parametrize("R,Kin,N,xbf", [(200, 64, 192, False), (130, 131, 128, False), (64, 64, 64, True)])
 def test_ln_linear_fwd(R, Kin, N, xbf):
     torch.manual_seed(0)
@@ -131,6 +145,11 @@ def test_post_attn(C, H):
     b = _emu().post_attn_fwd(o, x, ws[0], bo, g2, be2, 1e-5, ws[1], b1, ws[2], b2)
     for t1, t2, n in zip(a, b, ("z", "y", "mean", "rstd", "u")):
         close(t1, t2, 2e-2, n)
+    # batch-broadcast residual: x has R / 3 rows, row r adds x[r % (R / 3)]
+    xs = x[: R // 3].contiguous()
+    a3 = _ext().post_attn_fwd(o[: 3 * (R // 3)].contiguous(), xs, ws[0], bo, g2, be2, 1e-5, ws[1], b1, ws[2], b2)
+    b3 = _emu().post_attn_fwd(o[: 3 * (R // 3)].contiguous(), xs, ws[0], bo, g2, be2, 1e-5, ws[1], b1, ws[2], b2)
+    close(a3[0], b3[0], 2e-2, "z (broadcast x)")
     z, y, m, r, u = b
     dz = torch.randn(R, C, device=DEV)
     outs = []
@@ -193,14 +212,18 @@ def test_fused_cross_entropy(M, V, C):
     close(l1, l2, 1e-2, "loss")
     close(s1, s2, 1e-3, "lse")
     gs = torch.tensor([0.37], device=DEV)
+    rowmap = torch.randperm(3 * M, device=DEV)[:M]  # scatter rows into a larger (3M, C) gradient
     outs = []
     for K in (_ext(), _emu()):
         dH = torch.zeros(M, C, device=DEV)
-        dW = torch.zeros(V, C, device=DEV)
+        dW = torch.full((V, C), 7.0, device=DEV)  # overwritten (accumulate=False)
         db = torch.zeros(V, device=DEV)
-        K.ce_bwd(h, lab, w, bias, s2, gs, dH, dW, db, False)
-        outs.append((dH, dW, db))
-    for a, b, n in zip(outs[0], outs[1], ("dH", "dW", "db")):
+        K.ce_bwd(h, lab, w, bias, s2, gs, dH, dW, db, False, None)
+        dHs = torch.zeros(3 * M, C, device=DEV)
+        dW2, db2 = dW.clone(), db.clone()
+        K.ce_bwd(h, lab, w, bias, s2, gs, dHs, dW2, db2, True, rowmap)
+        outs.append((dH, dW, db, dHs, dW2, db2))
+    for a, b, n in zip(outs[0], outs[1], ("dH", "dW", "db", "dH rowmap", "dW acc", "db acc")):
         close(a, b, 3e-2, n)
 
 
@@ -208,6 +231,7 @@ def test_embed_mask_adamw():
     torch.manual_seed(6)
     B, L, V, C = 4, 50, 300, 64
     ids = torch.randint(0, V, (B, L), device=DEV)
+    ids[:, ::3] = 2  # a very frequent id (like [MASK]): long equal-id runs after sorting
     E, P = torch.randn(V, C, device=DEV), torch.randn(64, C, device=DEV)
     close(_ext().embed_fwd(ids, E, P[:L].contiguous(), 8.0), _emu().embed_fwd(ids, E, P[:L].contiguous(), 8.0), 1e-6, "emb")
     g = torch.randn(B, L, C, device=DEV)

@@ -29,6 +29,7 @@ for step in "$@"; do
     ref32)    run bench_ref32 600 python bench.py --backend reference --dtype fp32 --steps 5 --warmup 2 ;;
     eager)    run bench_eager 600 python bench.py --no-graph --steps 10 --warmup 3 ;;
     bench)    run bench 600 python bench.py --steps 20 --warmup 5 ;;
+    micro)    run micro 300 python tools/microbench.py ;;
     prof)     run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 3 ;;
     dbg0)     run dbg0 300 env AMD_SERIALIZE_KERNEL=3 python tools/debug_engine.py 0 ;;
     dbg1)     run dbg1 300 python tools/debug_engine.py 1 ;;

@@ -1,0 +1,84 @@
+"""Kernel microbenchmarks at the headline (MLM-256) self-attention layer shapes.
+
+    python tools/microbench.py            (GPU)
+
+Times each HIP entry point with CUDA events over many launches (one stream, warm L2) and
+prints µs per call; variants isolate costs (e.g. the weight-gradient atomics).
+"""
+import math
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from perceiver_io_amd.ops import ext  # noqa: E402
+
+
+def timeit(fn, iters=200, warmup=20):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters * 1e3
+
+
+def main():
+    K = ext.require()
+    dev = "cuda"
+    B, N, C, H = 64, 256, 64, 4
+    R = B * N
+    D = C // H
+    bf = torch.bfloat16
+    x = torch.randn(R, C, device=dev)
+    g1, b1 = torch.randn(C, device=dev), torch.randn(C, device=dev)
+    wqkv = (torch.randn(3 * C, C, device=dev) / 8).to(bf)
+    bqkv = torch.randn(3 * C, device=dev)
+    res = {}
+    res["ln_linear_fwd qkv"] = timeit(lambda: K.ln_linear_fwd(x, g1, b1, 1e-5, wqkv, bqkv, 0, None, True, True))
+    qkv, mean, rstd = K.ln_linear_fwd(x, g1, b1, 1e-5, wqkv, bqkv, 0, None, True, True)
+    q3 = qkv.view(B, N, 3 * C)
+    q, k, v = q3[:, :, :C], q3[:, :, C:2 * C], q3[:, :, 2 * C:]
+    res["attn_fwd self"] = timeit(lambda: K.attn_fwd(q, k, v, None, H, D, 1 / math.sqrt(D), 0.0, 0, 1))
+    o, lse = K.attn_fwd(q, k, v, None, H, D, 1 / math.sqrt(D), 0.0, 0, 1)
+    ws = [(torch.randn(C, C, device=dev) / 8).to(bf) for _ in range(3)]
+    bs = [torch.randn(C, device=dev) for _ in range(3)]
+    g2, be2 = torch.randn(C, device=dev), torch.randn(C, device=dev)
+    o2 = o.view(R, C)
+    res["post_attn_fwd"] = timeit(lambda: K.post_attn_fwd(o2, x, ws[0], bs[0], g2, be2, 1e-5, ws[1], bs[1], ws[2], bs[2]))
+    z, y, m2, r2, u = K.post_attn_fwd(o2, x, ws[0], bs[0], g2, be2, 1e-5, ws[1], bs[1], ws[2], bs[2])
+    dz = torch.randn(R, C, device=dev)
+    grads = [torch.zeros((C, C) if i in (0, 4, 6) else (C,), device=dev) for i in range(8)]
+    res["post_attn_bwd"] = timeit(lambda: K.post_attn_bwd(dz, y, m2, r2, u, o2, ws[0], ws[1], ws[2], g2, be2, H, grads))
+    dy, do, delta = K.post_attn_bwd(dz, y, m2, r2, u, o2, ws[0], ws[1], ws[2], g2, be2, H, grads)
+    dqkv = torch.empty(B, N, 3 * C, device=dev)
+    res["attn_bwd self"] = timeit(lambda: K.attn_bwd(q, k, v, None, o, do.view(B, N, C), lse, delta.view(B, N, H), H, D,
+                                                     1 / math.sqrt(D), 0.0, 0, dqkv[:, :, :C], dqkv[:, :, C:2 * C],
+                                                     dqkv[:, :, 2 * C:]))
+    dg, db_ = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    dW, dbias = torch.zeros(3 * C, C, device=dev), torch.zeros(3 * C, device=dev)
+    g = dqkv.view(R, 3 * C)
+    res["ln_linear_bwd qkv (+dW)"] = timeit(lambda: K.ln_linear_bwd(g, wqkv, x, mean, rstd, g1, b1, dy, True, dg, db_, dW, dbias))
+    res["ln_linear_bwd qkv (no dW)"] = timeit(lambda: K.ln_linear_bwd(g, wqkv, x, mean, rstd, g1, b1, dy, True, dg, db_, None, None))
+    res["ln_linear_bwd qkv (no dW, no LN)"] = timeit(
+        lambda: K.ln_linear_bwd(g, wqkv, x, None, None, None, None, dy, True, None, None, None, None))
+    res["wgrad standalone qkv"] = timeit(lambda: K.wgrad(g, x, 1, mean, rstd, g1, b1, 256, dW, dbias))
+    # vector grads (biases / LN affine) spread over 8 replicas: ≤ grid/8 adders per address
+    repbuf = torch.zeros(8, 8 * C + 3 * C, device=dev)
+    rv = [repbuf[:, i * C:(i + 1) * C] for i in range(8)]
+    rq = repbuf[:, 8 * C:]
+    gr = [grads[0], rv[0], rv[1], rv[2], grads[4], rv[3], grads[6], rv[4]]
+    res["post_attn_bwd (replicated vec grads)"] = timeit(
+        lambda: K.post_attn_bwd(dz, y, m2, r2, u, o2, ws[0], ws[1], ws[2], g2, be2, H, gr))
+    res["ln_linear_bwd qkv (+dW, replicated vec)"] = timeit(
+        lambda: K.ln_linear_bwd(g, wqkv, x, mean, rstd, g1, b1, dy, True, rv[5], rv[6], dW, rq))
+    for k_, v_ in res.items():
+        print(f"{k_:45s} {v_:8.2f} us")
+
+
+if __name__ == "__main__":
+    main()
