@@ -40,6 +40,8 @@ void wgrad_launch(const void*, bool, int, int, const void*, bool, int, int, int,
 void ce_fwd_launch(int, const uint16_t*, const int64_t*, const uint16_t*, const float*, int, int, float*, float*,
                    float*, float*, int, hipStream_t);
 int ce_num_splits(int, int);
+void mlm_select_launch(const int64_t*, int, int, int, int, int64_t*, int64_t*, int*, int64_t*, int64_t*, float*, bool*,
+                       hipStream_t);
 void ce_bwd_launch(int, const uint16_t*, const int64_t*, const uint16_t*, const float*, const float*, const float*,
                    int, int, float*, const int64_t*, float*, float*, int, hipStream_t);
 void embed_fwd_launch(const int64_t*, const float*, const float*, float*, long long, int, int, float, hipStream_t);
@@ -302,6 +304,24 @@ void wgrad(Tensor g, Tensor a, int64_t amode, OptT mean, OptT rstd, OptT lnw, Op
                     (int)amode, f32o(mean), f32o(rstd), f32o(lnw), f32o(lnb), R, (int)rows_per_wg, dwp, dbp, stream());
 }
 
+// labels (B, L) → [idx_b (B, cap), labels_b (B, cap), gidx (gcap), glabels (gcap), total (1) fp32,
+// overflow (1) bool]: per-sequence slots of the selected positions and their global compaction
+std::vector<Tensor> mlm_select(Tensor labels, int64_t cap, int64_t gcap) {
+  CHECK_DT(labels, torch::kInt64);
+  TORCH_CHECK(labels.dim() == 2 && labels.is_contiguous(), "labels must be (B, L) contiguous");
+  const int B = (int)labels.size(0), L = (int)labels.size(1);
+  TORCH_CHECK(cap > 0 && cap <= L && gcap > 0, "bad capacities");
+  auto i64 = labels.options();
+  Tensor idx_b = torch::empty({B, cap}, i64), lab_b = torch::empty({B, cap}, i64);
+  Tensor count = torch::empty({B}, i64.dtype(torch::kInt32));
+  Tensor gidx = torch::empty({gcap}, i64), glab = torch::empty({gcap}, i64);
+  Tensor total = torch::empty({1}, i64.dtype(torch::kFloat32)), ovf = torch::empty({1}, i64.dtype(torch::kBool));
+  pio::mlm_select_launch(labels.data_ptr<int64_t>(), B, L, (int)cap, (int)gcap, idx_b.data_ptr<int64_t>(),
+                         lab_b.data_ptr<int64_t>(), count.data_ptr<int>(), gidx.data_ptr<int64_t>(),
+                         glab.data_ptr<int64_t>(), total.data_ptr<float>(), ovf.data_ptr<bool>(), stream());
+  return {idx_b, lab_b, gidx, glab, total, ovf};
+}
+
 std::vector<Tensor> ce_fwd(Tensor h, Tensor labels, Tensor w, Tensor bias) {
   TORCH_CHECK(h.is_contiguous() && w.is_contiguous() && labels.is_contiguous());
   CHECK_DT(labels, torch::kInt64);
@@ -410,6 +430,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("post_attn_bwd", &post_attn_bwd);
   m.def("ln_linear_bwd", &ln_linear_bwd);
   m.def("wgrad", &wgrad);
+  m.def("mlm_select", &mlm_select);
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);
   m.def("embed_fwd", &embed_fwd);

@@ -321,6 +321,88 @@ __global__ __launch_bounds__(256) void ce_bwd_dw_kernel(const uint16_t* __restri
   }
 }
 
+// ------------------------------------------------------------------------------------
+// selected-position bookkeeping for the MLM loss (replaces ~15 small framework kernels)
+//   rows  : per sequence b, slots [0, cap): positions of labels != -100 in order (unused
+//           slots → slot mod L, label −100), count[b]
+//   global: the valid slots of all sequences compacted into gcap rows for the vocab GEMMs
+//           (unused → slot 0 with label −100), total = Σ count (the mean's denominator)
+// ------------------------------------------------------------------------------------
+__global__ void select_rows_kernel(const int64_t* __restrict__ labels, int L, int cap, int64_t* __restrict__ idx_b,
+                                   int64_t* __restrict__ lab_b, int* __restrict__ count) {
+  __shared__ int sW[4], sOff;
+  const int b = blockIdx.x, w = wave_id(), l = lane_id();
+  if (threadIdx.x == 0) sOff = 0;
+  __syncthreads();
+  for (int c0 = 0; c0 < L; c0 += 256) {
+    const int i = c0 + threadIdx.x;
+    const int64_t lab = i < L ? labels[(long long)b * L + i] : -100;
+    const bool sel = lab != -100;
+    const uint64_t m = __ballot(sel);
+    const int pre = __popcll(m & ((1ull << l) - 1ull));
+    if (l == 0) sW[w] = __popcll(m);
+    __syncthreads();
+    int woff = 0;
+    for (int k = 0; k < w; ++k) woff += sW[k];
+    const int pos = sOff + woff + pre;
+    if (sel && pos < cap) {
+      idx_b[(long long)b * cap + pos] = i;
+      lab_b[(long long)b * cap + pos] = lab;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) sOff += sW[0] + sW[1] + sW[2] + sW[3];
+    __syncthreads();
+  }
+  const int cnt = sOff;
+  for (int j = (cnt < cap ? cnt : cap) + threadIdx.x; j < cap; j += blockDim.x) {
+    idx_b[(long long)b * cap + j] = j % L;
+    lab_b[(long long)b * cap + j] = -100;
+  }
+  if (threadIdx.x == 0) count[b] = cnt;
+}
+
+__global__ void select_global_kernel(const int* __restrict__ count, int B, int cap, const int64_t* __restrict__ lab_b,
+                                     int gcap, int64_t* __restrict__ gidx, int64_t* __restrict__ glab,
+                                     float* __restrict__ total, bool* __restrict__ overflow) {
+  extern __shared__ int sOffs[];  // [B + 1] exclusive prefix of min(count, cap)
+  if (threadIdx.x == 0) {
+    int acc = 0, all = 0;
+    bool ovf = false;
+    for (int b = 0; b < B; ++b) {
+      const int n = count[b] < cap ? count[b] : cap;
+      ovf |= count[b] > cap;
+      sOffs[b] = acc;
+      acc += n;
+      all += count[b];
+    }
+    sOffs[B] = acc;
+    total[0] = (float)all;
+    overflow[0] = ovf || acc > gcap;
+  }
+  __syncthreads();
+  const int used = sOffs[B] < gcap ? sOffs[B] : gcap;
+  for (long long s = threadIdx.x; s < (long long)B * cap; s += blockDim.x) {
+    const int b = (int)(s / cap), j = (int)(s - (long long)b * cap);
+    const int n = sOffs[b + 1] - sOffs[b];
+    const int g = sOffs[b] + j;
+    if (j < n && g < gcap) {
+      gidx[g] = s;
+      glab[g] = lab_b[s];
+    }
+  }
+  for (int g = used + threadIdx.x; g < gcap; g += blockDim.x) {
+    gidx[g] = 0;
+    glab[g] = -100;
+  }
+}
+
+void mlm_select_launch(const int64_t* labels, int B, int L, int cap, int gcap, int64_t* idx_b, int64_t* lab_b,
+                       int* count, int64_t* gidx, int64_t* glab, float* total, bool* overflow, hipStream_t st) {
+  hipLaunchKernelGGL(select_rows_kernel, dim3(B), dim3(256), 0, st, labels, L, cap, idx_b, lab_b, count);
+  hipLaunchKernelGGL(select_global_kernel, dim3(1), dim3(1024), (B + 1) * sizeof(int), st, count, B, cap, lab_b, gcap,
+                     gidx, glab, total, overflow);
+}
+
 // vocab splits so that a launch has ≈ target workgroups (several per CU hide the W-chunk latency)
 static int pick_split(int M, int nchunks, int target) {
   const int mt = (M + HB - 1) / HB;

@@ -195,6 +195,31 @@ def wgrad(g, a, amode, mean, rstd, lnw, lnb, rows_per_wg, dW, db=None):
         db += g.float().sum(0).view(db.shape)
 
 
+def mlm_select(labels, cap, gcap):
+    B, L = labels.shape
+    sel = labels != -100
+    pos = torch.cumsum(sel.to(torch.int64), 1) - 1
+    idx_b = (torch.arange(cap, device=labels.device) % L).repeat(B, 1)
+    lab_b = torch.full((B, cap), -100, dtype=torch.int64, device=labels.device)
+    keep = sel & (pos < cap)
+    rows = torch.arange(B, device=labels.device)[:, None].expand(B, L)
+    cols = torch.arange(L, device=labels.device).expand(B, L)
+    idx_b[rows[keep], pos[keep]] = cols[keep]
+    lab_b[rows[keep], pos[keep]] = labels[keep]
+    count = sel.sum(1)
+    n = count.clamp(max=cap)
+    slot_ok = torch.arange(cap, device=labels.device)[None, :] < n[:, None]
+    flat = torch.nonzero(slot_ok.reshape(-1)).reshape(-1)
+    gidx = torch.zeros(gcap, dtype=torch.int64, device=labels.device)
+    glab = torch.full((gcap,), -100, dtype=torch.int64, device=labels.device)
+    m = min(gcap, flat.numel())
+    gidx[:m] = flat[:m]
+    glab[:m] = lab_b.reshape(-1)[flat[:m]]
+    total = count.sum().float().reshape(1)
+    ovf = ((count > cap).any() | (n.sum() > gcap)).reshape(1)
+    return idx_b, lab_b, gidx, glab, total, ovf
+
+
 def ce_fwd(h, labels, w, bias):
     logits = _bf(h.float()) @ _bf(w.float()).t() + bias
     lse = torch.logsumexp(logits, -1)

@@ -159,10 +159,19 @@ def masked_decode_loss(decoder, x_latent: torch.Tensor, labels: torch.Tensor):
     decoding all ``L`` at a third of the decoder cost.  The output-query
     gradient flows back through the gather (index_select → index_add).
     """
+    global _overflow
+    from . import use_hip
+
     B, L = labels.shape
     decoder.check_latent(x_latent)
-    idx, labels_c, count = compact_per_row(labels, row_capacity(L))
-    q = decoder.output.index_select(0, idx.reshape(-1)).view(B, idx.shape[1], -1)
-    h = decoder.cross_attention(q, x_latent)
     lin = decoder.output_adapter.linear
+    cap = row_capacity(L)
+    if use_hip(x_latent) and lin.weight.shape[1] in (32, 64, 128):
+        idx, _, gidx, glab, total, _overflow = ext.require().mlm_select(labels.contiguous(), cap, capacity(B * L))
+        q = decoder.output.index_select(0, idx.reshape(-1)).view(B, cap, -1)
+        h = decoder.cross_attention(q, x_latent)
+        return _MaskedCE.apply(h, lin.weight, lin.bias, gidx, glab, total)
+    idx, labels_c, count = compact_per_row(labels, cap)
+    q = decoder.output.index_select(0, idx.reshape(-1)).view(B, cap, -1)
+    h = decoder.cross_attention(q, x_latent)
     return compact_lm_loss(h, labels_c, count, lin.weight, lin.bias, B * L)

@@ -199,6 +199,17 @@ def test_ln_linear_bwd_and_wgrad(R, N, Kin, gbf):
         close(outs[0][1], outs[1][1], 1e-4, f"db mode {mode}")
 
 
+@pytest.mark.parametrize("B,L,cap,gcap,p", [(6, 300, 96, 400, 0.15), (3, 40, 8, 12, 0.4), (64, 512, 160, 5632, 0.15)])
+def test_mlm_select(B, L, cap, gcap, p):
+    torch.manual_seed(8)
+    lab = torch.randint(3, 1000, (B, L), device=DEV)
+    lab[torch.rand(B, L, device=DEV) > p] = -100
+    a = _ext().mlm_select(lab, cap, gcap)
+    b = _emu().mlm_select(lab, cap, gcap)
+    for x, y, n in zip(a, b, ("idx_b", "lab_b", "gidx", "glab", "total", "overflow")):
+        assert torch.equal(x.cpu(), y.cpu()), n
+
+
 @pytest.mark.parametrize("M,V,C", [(300, 1000, 64), (77, 10003, 64), (64, 257, 128)])
 def test_fused_cross_entropy(M, V, C):
     torch.manual_seed(5)
