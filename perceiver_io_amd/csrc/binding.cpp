@@ -54,6 +54,7 @@ void adamw_launch(float*, const float*, float*, float*, uint16_t*, long long, co
                   hipStream_t);
 void cast_bf16_launch(const float*, uint16_t*, long long, hipStream_t);
 void reduce_probe_launch(const float*, float*, hipStream_t);
+void fold_replicas_launch(float*, float*, long long, int, hipStream_t);
 }  // namespace pio
 
 using torch::Tensor;
@@ -216,12 +217,13 @@ float* grad_target(Tensor& t, int64_t numel, const char* what) {
   return t.data_ptr<float>();
 }
 constexpr int kGradReplicas = 8;
-// vector gradient target: (K,) contiguous, or (8, K) replicas with unit inner stride whose row
-// stride is shared by every vector target of the call (workgroup i adds into row i % 8)
+// gradient target: K contiguous floats (any shape), or an (8, K) replica view with unit inner
+// stride whose row stride is shared by every target of the call (workgroup i adds into row
+// i % 8).  A 2-D target counts as replicated only when it is (8, K) with K == its numel / 8.
 float* vec_target(Tensor& t, int64_t K, const char* what, int& vrs) {
   CHECK_DT(t, torch::kFloat32);
-  if (t.dim() == 2) {
-    TORCH_CHECK(t.size(0) == kGradReplicas && t.size(1) == K && t.stride(1) == 1, "bad replicated target ", what);
+  if (t.dim() == 2 && t.size(0) == kGradReplicas && t.size(1) == K) {
+    TORCH_CHECK(t.stride(1) == 1, "bad replicated target ", what);
     TORCH_CHECK(vrs < 0 || vrs == (int)t.stride(0), "replicated targets must share one row stride");
     vrs = (int)t.stride(0);
   } else {
@@ -244,10 +246,10 @@ std::vector<Tensor> post_attn_bwd(Tensor dz, Tensor y, Tensor m2, Tensor r2, Ten
   TORCH_CHECK(grads.size() == 8, "post_attn_bwd needs 8 gradient targets");
   const int64_t CC = (int64_t)C * C;
   int vrs = -1;
-  pio::PostAttnGrads pg{grad_target(grads[0], CC, "dWo"), vec_target(grads[1], C, "dbo", vrs),
+  pio::PostAttnGrads pg{vec_target(grads[0], CC, "dWo", vrs), vec_target(grads[1], C, "dbo", vrs),
                         vec_target(grads[2], C, "dg2", vrs), vec_target(grads[3], C, "dbe2", vrs),
-                        grad_target(grads[4], CC, "dW1"), vec_target(grads[5], C, "db1", vrs),
-                        grad_target(grads[6], CC, "dW2"), vec_target(grads[7], C, "db2", vrs), 0};
+                        vec_target(grads[4], CC, "dW1", vrs), vec_target(grads[5], C, "db1", vrs),
+                        vec_target(grads[6], CC, "dW2", vrs), vec_target(grads[7], C, "db2", vrs), 0};
   pg.vrs = vrs < 0 ? 0 : vrs;
   auto f32 = dz.options().dtype(torch::kFloat32);
   Tensor dy = torch::empty({R, C}, f32);
@@ -279,7 +281,7 @@ OptT ln_linear_bwd(Tensor g, Tensor w, Tensor x, OptT mean, OptT rstd, OptT lnw,
     dgp = vec_target(*dlnw, Kin, "dlnw", vrs);
     dbp = vec_target(*dlnb, Kin, "dlnb", vrs);
   }
-  if (dW.has_value()) dwp = grad_target(*dW, (int64_t)N * Kin, "dW");
+  if (dW.has_value()) dwp = vec_target(*dW, (int64_t)N * Kin, "dW", vrs);
   if (db.has_value()) { TORCH_CHECK(dW.has_value(), "db needs dW"); dbiasp = vec_target(*db, N, "db", vrs); }
   const float* dr = nullptr; int drs = 0;
   if (dres.has_value()) { dr = f32p(*dres); drs = (int)dres->stride(0); TORCH_CHECK(dres->stride(1) == 1); }
@@ -416,6 +418,15 @@ Tensor reduce_probe(Tensor x) {
   return out;
 }
 
+// grad[:n] += Σ_r rep[r], rep ← 0   (rep: (R, n) contiguous fp32)
+void fold_replicas(Tensor grad, Tensor rep) {
+  CHECK_DT(grad, torch::kFloat32); CHECK_DT(rep, torch::kFloat32);
+  TORCH_CHECK(rep.dim() == 2 && rep.is_contiguous() && grad.is_contiguous() && grad.numel() >= rep.size(1),
+              "fold_replicas: rep must be (R, n) contiguous, grad at least n long");
+  if (rep.size(1) == 0) return;
+  pio::fold_replicas_launch(grad.data_ptr<float>(), rep.data_ptr<float>(), rep.size(1), (int)rep.size(0), stream());
+}
+
 void cast_bf16(Tensor x, Tensor y) {
   TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && x.numel() == y.numel());
   pio::cast_bf16_launch(f32p(x), reinterpret_cast<uint16_t*>(y.data_ptr()), x.numel(), stream());
@@ -440,5 +451,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adamw", &adamw);
   m.def("cast_bf16", &cast_bf16);
   m.def("reduce_probe", &reduce_probe);
+  m.def("fold_replicas", &fold_replicas);
   m.attr("arch") = "gfx950";
 }

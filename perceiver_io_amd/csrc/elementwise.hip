@@ -190,6 +190,30 @@ void adamw_launch(float* p, const float* g, float* m, float* v, uint16_t* shadow
                   float eps, float wd, float clip, float gscale, hipStream_t st) {
   hipLaunchKernelGGL(adamw_kernel, grid_for(n), dim3(256), 0, st, p, g, m, v, shadow, n, hyper, eps, wd, clip, gscale);
 }
+// grad[i] += Σ_r rep[r][i], rep[r][i] ← 0 (replicated gradient accumulators, see ops/optim.py)
+__global__ void fold_replicas_kernel(float* __restrict__ grad, float* __restrict__ rep, long long n, int nrep) {
+  const long long n4 = n >> 2;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    float4 acc = reinterpret_cast<float4*>(grad)[i];
+    for (int r = 0; r < nrep; ++r) {
+      float4* p = reinterpret_cast<float4*>(rep + r * n) + i;
+      const float4 v = *p;
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      *p = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    reinterpret_cast<float4*>(grad)[i] = acc;
+  }
+  for (long long i = (n4 << 2) + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    float acc = grad[i];
+    for (int r = 0; r < nrep; ++r) { acc += rep[r * n + i]; rep[r * n + i] = 0.f; }
+    grad[i] = acc;
+  }
+}
+void fold_replicas_launch(float* grad, float* rep, long long n, int nrep, hipStream_t st) {
+  hipLaunchKernelGGL(fold_replicas_kernel, grid_for((n + 3) / 4), dim3(256), 0, st, grad, rep, n, nrep);
+}
+
 // one wave: the cross-lane reduction helpers of common.h on x[0..63] (numerics self-test)
 __global__ void reduce_probe_kernel(const float* __restrict__ x, float* __restrict__ out) {
   const int l = threadIdx.x;

@@ -108,9 +108,9 @@ __device__ __forceinline__ void stage(uint16_t* s, int ld, const T* g, long long
 }
 
 // fp32 gradient targets of the post-attention block (views of the flat gradient buffer).
-// Vector targets (biases, LN affine) may be replicated: workgroup i adds into replica
-// i % kGradReplicas at vrs floats per replica (vrs = 0: one copy), so that no address takes
-// more than grid/8 atomic adds; the replicas are folded once per step (ops/optim.py).
+// Targets may be replicated: workgroup i adds into replica i % kGradReplicas, vrs floats
+// apart (vrs = 0: one copy), so that no address takes more than grid/8 atomic adds (same-
+// address float atomics serialise at the memory side); replicas are folded once per step.
 constexpr int kGradReplicas = 8;
 struct PostAttnGrads {
   float *dWo, *dbo, *dg2, *dbe2, *dW1, *db1, *dW2, *db2;
@@ -651,7 +651,7 @@ __global__ __launch_bounds__(256) void post_attn_bwd_kernel(
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
   tile_gemm<MAXT, true, false>(sG, LD, sW[0], LD, 64, C, C, acc);  // dH = dZ · W2
-  wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, gr_out.dW2, C);
+  wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, rep(gr_out.dW2, gr_out.vrs), C);
   {
     constexpr int NTN = C / 32;
 #pragma unroll
@@ -698,7 +698,7 @@ __global__ __launch_bounds__(256) void post_attn_bwd_kernel(
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
   tile_gemm<MAXT, true, false>(sG, LD, sW[NWB == 3 ? 1 : 0], LD, 64, C, C, acc);  // dXn2 = dU · W1
-  wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, gr_out.dW1, C);
+  wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, rep(gr_out.dW1, gr_out.vrs), C);
   for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) { sF[m * LDF + n] = acc[t][i]; });
   __syncthreads();
   if constexpr (NWB == 1) tile_store<NIW>(wr[0], sW[0], LD, C, C);
@@ -744,7 +744,7 @@ __global__ __launch_bounds__(256) void post_attn_bwd_kernel(
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
   tile_gemm<MAXT, true, false>(sG, LD, sW[NWB == 3 ? 2 : 0], LD, 64, C, C, acc);  // dO = dY · Wo
-  wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, gr_out.dWo, C);
+  wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, rep(gr_out.dWo, gr_out.vrs), C);
   for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) { sF[m * LDF + n] = bf2f(f2bf(acc[t][i])); });
   __syncthreads();
   {
@@ -839,7 +839,7 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
     }
     tile_gemm<MAXT, true, false>(sG, LDG, sW, LD, 64, KP, 64, acc);
     if (dW) {
-      wgrad_tile<MAXT>(sG, LDG, sXn, LD, 64, KP, N - nc, Kin, dW + (long long)nc * Kin, Kin);
+      wgrad_tile<MAXT>(sG, LDG, sXn, LD, 64, KP, N - nc, Kin, rep(dW, vrs) + (long long)nc * Kin, Kin);
       if (db) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {

@@ -174,7 +174,16 @@ class SelfAttention(nn.Module):
 
 
 class _FusedLayer(Sequential):
-    """Residual(attention) → Residual(mlp) pair that can run as one fused node."""
+    """Residual(attention) → Residual(mlp) pair that can run as one fused node.
+
+    Its parameters are flagged ``_pio_replicate``: a flat parameter space gives them 8-way
+    replicated gradient accumulators, because every row tile of the fused backward adds its
+    weight-gradient partial to them (ops/optim.py)."""
+
+    def __init__(self, *modules):
+        super().__init__(*modules)
+        for p in self.parameters():
+            p._pio_replicate = True
 
     @property
     def attn(self):

@@ -47,6 +47,15 @@ def ln_linear_fwd(x, lnw, lnb, eps, w, bias, act, res, out_bf16, save_stats):
     return out
 
 
+def _acc(t, v):
+    """t += v for a gradient target: plain (any shape with v's numel) or an (8, numel)
+    replicated accumulator (the emulation adds into replica 0)."""
+    if t.dim() == 2 and t.shape[0] == 8 and t.shape[1] == v.numel():
+        t[0] += v.reshape(-1)
+    else:
+        t += v.reshape(t.shape)
+
+
 def _heads(x, H):
     b, n, _ = x.shape
     return x[:, :, : x.shape[2]].reshape(b, n, H, -1).permute(0, 2, 1, 3)
@@ -141,23 +150,23 @@ def post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, be2, H, grads):
     dWo, dbo, dg2, dbe2, dW1, db1, dW2, db2 = grads
     uf = u.float()
     dh = _bf(dz) @ _bf(w2.float())
-    dW2 += (_bf(dz).t() @ _bf(F.gelu(uf))).view(dW2.shape)
-    db2 += dz.sum(0).view(db2.shape)
+    _acc(dW2, _bf(dz).t() @ _bf(F.gelu(uf)))
+    _acc(db2, dz.sum(0))
     du = dh * _gelu_grad(uf)
     dxn = _bf(du) @ _bf(w1.float())
     xn = (y - m2[:, None]) * r2[:, None] * g2 + be2
-    dW1 += (_bf(du).t() @ _bf(xn)).view(dW1.shape)
-    db1 += du.sum(0).view(db1.shape)
+    _acc(dW1, _bf(du).t() @ _bf(xn))
+    _acc(db1, du.sum(0))
     dln, xh = _ln_bwd(dxn, y, m2, r2, g2)
     dy = dz + dln
     do = (_bf(dy) @ _bf(wo.float())).to(torch.bfloat16)
-    dWo += (_bf(dy).t() @ _bf(o.float())).view(dWo.shape)
-    dbo += dy.sum(0).view(dbo.shape)
+    _acc(dWo, _bf(dy).t() @ _bf(o.float()))
+    _acc(dbo, dy.sum(0))
     R, C = dz.shape
     D = C // H
     delta = (do.float().view(R, H, D) * o.float().view(R, H, D)).sum(-1)
-    dg2 += (dxn * xh).sum(0).view(dg2.shape)
-    dbe2 += dxn.sum(0).view(dbe2.shape)
+    _acc(dg2, (dxn * xh).sum(0))
+    _acc(dbe2, dxn.sum(0))
     return dy, do, delta
 
 
@@ -169,13 +178,13 @@ def ln_linear_bwd(g, w, x, mean, rstd, lnw, lnb, dres, need_dx, dlnw=None, dlnb=
     xf = x.float()
     if dW is not None:
         xn = (xf - mean[:, None]) * rstd[:, None] * lnw + lnb if lnw is not None else xf
-        dW += (_bf(gf).t() @ _bf(xn)).view(dW.shape)
+        _acc(dW, _bf(gf).t() @ _bf(xn))
         if db is not None:
-            db += gf.sum(0).view(db.shape)
+            _acc(db, gf.sum(0))
     if lnw is not None:
         d, xh = _ln_bwd(dxn, xf, mean, rstd, lnw)
-        dlnw += (dxn * xh).sum(0).view(dlnw.shape)
-        dlnb += dxn.sum(0).view(dlnb.shape)
+        _acc(dlnw, (dxn * xh).sum(0))
+        _acc(dlnb, dxn.sum(0))
     else:
         d = dxn
     if need_dx:
@@ -295,6 +304,12 @@ def adamw(p, g, m, v, shadow, hyper, eps, wd, clip, gscale):
     p.addcdiv_(m, denom, value=-lr / bc1)
     if shadow is not None:
         shadow.copy_(p.to(shadow.dtype))
+
+
+def fold_replicas(grad, rep):
+    n = rep.shape[1]
+    grad[:n] += rep.sum(0)
+    rep.zero_()
 
 
 def cast_bf16(x, y):

@@ -207,17 +207,27 @@ class _LayerFn(torch.autograd.Function):
         f32 = dict(device=dz.device, dtype=torch.float32)
         scratch = {}
 
+        # gradient targets: the parameter's replicated accumulator (8, numel) when the flat
+        # parameter space gave it one (ops/optim.py), else its .grad; frozen parameters get a
+        # throw-away buffer of the same kind.  All targets of one kernel call share the kind.
+        rep_mode = any(getattr(p, "_pio_grad_rep", None) is not None for p in ps if p.requires_grad)
+
         def gb(p):
-            """Gradient target of parameter p (its .grad, normally a view of the flat buffer);
-            kernels accumulate into it directly.  Frozen parameters get a throw-away buffer."""
             if not p.requires_grad:
                 t = scratch.get(id(p))
                 if t is None:
-                    t = scratch[id(p)] = torch.zeros(p.shape, **f32)
+                    shape = (8, p.numel()) if rep_mode else p.shape
+                    t = scratch[id(p)] = torch.zeros(shape, **f32)
                 return t
+            if rep_mode:
+                return p._pio_grad_rep
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
             return p.grad
+
+        def rows(t, a, b, width):
+            """rows [a, b) of an (N, width) gradient target (plain or replicated)."""
+            return t[:, a * width:b * width] if rep_mode else t[a:b]
 
         dy, do, delta = K.post_attn_bwd(dz2, y, m2, r2, u, o2, wo, w1, w2, g2, be2, H,
                                         [gb(Wo), gb(bo), gb(g2), gb(be2), gb(W1), gb(b1), gb(W2), gb(b2)])
@@ -233,20 +243,21 @@ class _LayerFn(torch.autograd.Function):
             if Bq == 1 and B > 1:
                 dq2, dres = dq.sum(0), dy.view(B, Nq, C).sum(0)
             gbias = gb(bin_)
+            Ckv = xkv2.shape[1]
             if spec.packed:
                 gin = gb(ps[4])
-                gwq, gwkv = gin[:C], gin[C:]
+                gwq, gwkv = rows(gin, 0, C, C), rows(gin, C, 3 * C, C)
             else:
                 gwq = gb(ps[4])
-                gwkv = torch.zeros((2 * C, xkv2.shape[1]), **f32)
+                gwkv = torch.zeros((8, 2 * C * Ckv) if rep_mode else (2 * C, Ckv), **f32)
             dx_q = K.ln_linear_bwd(dq2, wq, xq2, mean_q, rstd_q, g_q, b_q, dres, True, gb(g_q), gb(b_q), gwq,
-                                   gbias[:C])
+                                   rows(gbias, 0, C, 1))
             dkv2 = dkv.view(B * M, 2 * C)
             dx_kv = K.ln_linear_bwd(dkv2, wkv, xkv2, mean_kv, rstd_kv, g_kv, b_kv, None, ctx.kv_grad, gb(g_kv),
-                                    gb(b_kv), gwkv, gbias[C:])
+                                    gb(b_kv), gwkv, rows(gbias, C, 3 * C, 1))
             if not spec.packed:
-                gb(ps[5]).add_(gwkv[:C])
-                gb(ps[6]).add_(gwkv[C:])
+                gb(ps[5]).add_(rows(gwkv, 0, C, Ckv))
+                gb(ps[6]).add_(rows(gwkv, C, 2 * C, Ckv))
             dx_q = dx_q.view(Bq, Nq, C)
             dx_kv = dx_kv.view(B, M, -1) if ctx.kv_grad else None
         else:

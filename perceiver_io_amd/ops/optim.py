@@ -7,7 +7,13 @@ kernels).  Consequences on MI355X:
     buffer instead of ~190 per-tensor collectives (``parallel/reducer.py``);
   * the optimizer is a single kernel launch over the flat buffers that also refreshes the
     bf16 shadow (no per-step weight casts);
-  * zeroing gradients is one memset.
+  * zeroing gradients is one memset;
+  * parameters flagged ``_pio_replicate`` (the fused attention/MLP layers) are placed first
+    and get an 8-way replicated gradient accumulator ``grad_rep`` (8, n_rep): the fused
+    backward kernels add their per-row-tile weight-gradient partials into replica
+    (tile mod 8), so no address takes more than 1/8 of the tiles' float atomics (same-address
+    atomics serialise at the memory side); ``fold()`` adds the replicas into ``grad`` (and
+    clears them) once per step, before the all-reduce / optimizer.
 
 ``FusedAdamW`` is a ``torch.optim.Optimizer`` (so ``torch.optim.lr_scheduler`` schedulers
 such as ``OneCycleLR`` drive it through ``param_groups``) with torch.optim.AdamW semantics
@@ -27,21 +33,35 @@ from . import emulation, ext
 ALIGN = 64  # elements; keeps every parameter view 256-byte aligned
 
 
+GRAD_REPLICAS = 8  # matches kGradReplicas in csrc/rowgemm.hip
+
+
 class FlatParameterSpace:
-    def __init__(self, params: Iterable[torch.nn.Parameter], with_shadow: Optional[bool] = None):
-        self.params: List[torch.nn.Parameter] = [p for p in params if p.requires_grad]
-        if not self.params:
+    def __init__(self, params: Iterable[torch.nn.Parameter], with_shadow: Optional[bool] = None,
+                 replicate: Optional[bool] = None):
+        params = [p for p in params if p.requires_grad]
+        if not params:
             raise ValueError("no trainable parameters")
-        dev = self.params[0].device
+        dev = params[0].device
         self.device = dev
+        if replicate is None:
+            replicate = dev.type == "cuda"
+        rep = [p for p in params if replicate and getattr(p, "_pio_replicate", False)]
+        rep_ids = {id(p) for p in rep}
+        # replicated parameters first (one contiguous region), then the rest in module order
+        self.params: List[torch.nn.Parameter] = rep + [p for p in params if id(p) not in rep_ids]
         self.offsets = []
         off = 0
         for p in self.params:
             self.offsets.append(off)
             off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
         self.numel = off
+        self.n_rep = self.offsets[len(rep)] if len(rep) < len(self.params) else off
+        if not rep:
+            self.n_rep = 0
         self.data = torch.zeros(off, dtype=torch.float32, device=dev)
         self.grad = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.grad_rep = torch.zeros(GRAD_REPLICAS, self.n_rep, dtype=torch.float32, device=dev) if rep else None
         if with_shadow is None:
             with_shadow = dev.type == "cuda"
         self.shadow = torch.zeros(off, dtype=torch.bfloat16, device=dev) if with_shadow else None
@@ -51,17 +71,32 @@ class FlatParameterSpace:
                 self.data[o:o + n].copy_(p.detach().reshape(-1).float())
                 p.data = self.data[o:o + n].view_as(p)
                 p.grad = self.grad[o:o + n].view_as(p)
+                if self.grad_rep is not None and o < self.n_rep:
+                    p._pio_grad_rep = self.grad_rep[:, o:o + n]  # (8, numel) replica view
         if self.shadow is not None:
             from .fused import weight_cache
 
             for p, o in zip(self.params, self.offsets):
                 weight_cache.bind(p, self.shadow[o:o + p.numel()].view(p.shape))
 
+    def fold(self):
+        """grad[:n_rep] += Σ replicas; replicas ← 0 (no-op without replicated parameters)."""
+        if self.grad_rep is None:
+            return
+        K = ext.require() if self.device.type == "cuda" else emulation
+        K.fold_replicas(self.grad, self.grad_rep)
+
     def views(self, buf: torch.Tensor):
         return [buf[o:o + p.numel()].view(p.shape) for p, o in zip(self.params, self.offsets)]
 
-    def zero_grad(self):
+    def zero_grad_buffers(self):
+        """Zero the gradient buffer and its replicas (capturable; no Python-side view fixes)."""
         self.grad.zero_()
+        if self.grad_rep is not None:
+            self.grad_rep.zero_()
+
+    def zero_grad(self):
+        self.zero_grad_buffers()
         # re-attach views autograd may have replaced (e.g. a grad that was set to None)
         for p, o in zip(self.params, self.offsets):
             g = p.grad
@@ -150,6 +185,7 @@ class FusedAdamW(torch.optim.Optimizer):
         """The capturable part: (grad-norm) + fused AdamW kernel over the flat buffers."""
         K = ext.require() if self.flat.device.type == "cuda" else emulation
         g = self.param_groups[0]
+        self.flat.fold()
         if self.max_grad_norm > 0:
             self.hyper[2:3].zero_()
             K.sumsq(self.flat.grad, self.hyper[2:3])

@@ -74,6 +74,7 @@ class FlatGradReducer:
         """All remaining buckets, then join the side stream."""
         if not self.enabled:
             return
+        self.flat.fold()  # replicated fused-layer gradients → grad before they are reduced
         for i in range(len(self.buckets)):
             self.ready(i)
         if self._side is not None:

@@ -114,14 +114,14 @@ class StepEngine:
         self._static_batch = _clone_to(batch, self.device)
         # warmup on the capture stream (allocator + lazy init); no optimizer update → nothing to undo
         for _ in range(2):
-            opt.flat.grad.zero_()
+            opt.flat.zero_grad_buffers()
             loss = self.loss_fn(self._static_batch)
             loss.backward()
             del loss
-        opt.flat.grad.zero_()
+        opt.flat.zero_grad_buffers()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=self.stream):
-            opt.flat.grad.zero_()
+            opt.flat.zero_grad_buffers()
             loss = self.loss_fn(self._static_batch)
             loss.backward()
             if self._opt_in_graph:

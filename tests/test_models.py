@@ -190,3 +190,35 @@ def test_fused_executor_matches_eager_via_emulation(kind):
     for n, p in enc.named_parameters():
         if n in g_ref:
             assert (p.grad - g_ref[n]).abs().max() < 0.03 * gmax, n
+
+
+def test_fused_executor_replicated_gradients_fold_to_eager():
+    """Flat parameter space with 8-way replicated gradient accumulators for the fused layers:
+    after fold() the gradients equal the eager ones, and non-layer parameters are untouched
+    by the replica mechanism."""
+    from perceiver_io_amd.ops.optim import FlatParameterSpace
+
+    torch.manual_seed(4)
+    m = mlm_model()
+    x = torch.randint(3, 300, (3, 64))
+    pad = torch.zeros(3, 64, dtype=torch.bool)
+    pad[1, 40:] = True
+    enc = m.encoder
+    ref = enc(x, pad)[0]
+    w = torch.randn_like(ref)
+    (ref * w).sum().backward()
+    g_ref = {n: p.grad.clone() for n, p in enc.named_parameters() if p.grad is not None}
+    flat = FlatParameterSpace(enc.parameters(), with_shadow=False, replicate=True)
+    assert flat.grad_rep is not None and flat.n_rep > 0
+    rep_params = [p for p in flat.params if getattr(p, "_pio_grad_rep", None) is not None]
+    assert rep_params and all(getattr(p, "_pio_replicate", False) for p in rep_params)
+    flat.zero_grad()
+    fused = ops.fused.encoder_forward(enc, x, pad)
+    (fused * w).sum().backward()
+    assert flat.grad_rep.abs().sum() > 0  # layer kernels accumulated into the replicas
+    flat.fold()
+    assert flat.grad_rep.abs().sum() == 0
+    gmax = max(g.abs().max() for g in g_ref.values())
+    for n, p in enc.named_parameters():
+        if n in g_ref:
+            assert (p.grad - g_ref[n]).abs().max() < 0.03 * gmax, n

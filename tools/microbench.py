@@ -67,15 +67,20 @@ def main():
     res["ln_linear_bwd qkv (no dW, no LN)"] = timeit(
         lambda: K.ln_linear_bwd(g, wqkv, x, None, None, None, None, dy, True, None, None, None, None))
     res["wgrad standalone qkv"] = timeit(lambda: K.wgrad(g, x, 1, mean, rstd, g1, b1, 256, dW, dbias))
-    # vector grads (biases / LN affine) spread over 8 replicas: ≤ grid/8 adders per address
-    repbuf = torch.zeros(8, 8 * C + 3 * C, device=dev)
-    rv = [repbuf[:, i * C:(i + 1) * C] for i in range(8)]
-    rq = repbuf[:, 8 * C:]
-    gr = [grads[0], rv[0], rv[1], rv[2], grads[4], rv[3], grads[6], rv[4]]
-    res["post_attn_bwd (replicated vec grads)"] = timeit(
-        lambda: K.post_attn_bwd(dz, y, m2, r2, u, o2, ws[0], ws[1], ws[2], g2, be2, H, gr))
-    res["ln_linear_bwd qkv (+dW, replicated vec)"] = timeit(
-        lambda: K.ln_linear_bwd(g, wqkv, x, mean, rstd, g1, b1, dy, True, rv[5], rv[6], dW, rq))
+    # every target replicated (weights too)
+    big = torch.zeros(8, 3 * C * C + 5 * C + 3 * C * C + 3 * C + 2 * C, device=dev)
+    off = [0]
+
+    def take(n):
+        t = big[:, off[0]:off[0] + n]
+        off[0] += n
+        return t
+    ga = [take(C * C), take(C), take(C), take(C), take(C * C), take(C), take(C * C), take(C)]
+    res["post_attn_bwd (all targets replicated)"] = timeit(
+        lambda: K.post_attn_bwd(dz, y, m2, r2, u, o2, ws[0], ws[1], ws[2], g2, be2, H, ga))
+    wq_r, bq_r, g_r, b_r = take(3 * C * C), take(3 * C), take(C), take(C)
+    res["ln_linear_bwd qkv (all targets replicated)"] = timeit(
+        lambda: K.ln_linear_bwd(g, wqkv, x, mean, rstd, g1, b1, dy, True, g_r, b_r, wq_r, bq_r))
     for k_, v_ in res.items():
         print(f"{k_:45s} {v_:8.2f} us")
 
