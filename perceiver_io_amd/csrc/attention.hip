@@ -81,10 +81,15 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(AttnArgs a, uint16_t
   constexpr int NT = (D < 32) ? 1 : D / 32;   // O^T tiles of 32 rows (head-dim)
   constexpr int KS = D / 16;                  // k-steps for QK^T
   constexpr int CH = D / 8;                   // 16-byte chunks per K/V row
-  constexpr int NTH = 64 * NWV, NI = (KT * CH + NTH - 1) / NTH;
-  constexpr bool PF = NI <= 4;  // next K/V tile prefetched into registers during this tile's math
-  __shared__ __attribute__((aligned(16))) uint16_t sK[KT * LDK];
-  __shared__ __attribute__((aligned(16))) uint16_t sV[KT * LDV + 64];
+  constexpr int NTH = 64 * NWV;
+  // keys are staged in rounds of NST 64-key tiles (≤ 4 16-byte chunks per thread per tensor),
+  // the next round register-prefetched while this round's tiles are processed
+  constexpr int NST0 = 4 * NTH / (KT * CH);
+  constexpr int NST = NST0 >= 4 ? 4 : (NST0 >= 1 ? NST0 : 1);
+  constexpr int NI = (NST * KT * CH + NTH - 1) / NTH;
+  constexpr bool PF = NI <= 4;
+  __shared__ __attribute__((aligned(16))) uint16_t sK[NST * KT * LDK];
+  __shared__ __attribute__((aligned(16))) uint16_t sV[NST * KT * LDV + 64];
 
   const int w = wave_id(), l = lane_id(), r = l & 31, hh = l >> 5;
   const int h = blockIdx.y;
@@ -101,8 +106,8 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(AttnArgs a, uint16_t
     for (int s = 0; s < KS; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qp + 16 * s);
   }
 
-  if (D < 32) {  // zero the unused head-dim columns 16..31 of the V tile once
-    for (int i = threadIdx.x; i < KT; i += NTH)
+  if (D < 32) {  // zero the unused head-dim columns 16..31 of the V tiles once
+    for (int i = threadIdx.x; i < NST * KT; i += NTH)
       *reinterpret_cast<bf16x8*>(sV + i * LDV + 16) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0},
       *reinterpret_cast<bf16x8*>(sV + i * LDV + 24) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
   }
@@ -115,116 +120,137 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(AttnArgs a, uint16_t
   const int ntiles = (a.Nk + KT - 1) / KT;
   const int t_begin = split * tiles_per_split;
   const int t_end = min(ntiles, t_begin + tiles_per_split);
+  const int k_end = min(a.Nk, t_end * KT);  // keys of this split
   const uint16_t* kb = a.k + (long long)b * a.k_bs + h * D;
   const uint16_t* vb = a.v + (long long)b * a.v_bs + h * D;
 
-  // K/V tile staging: items c = tid + NTH·i of the tile's KT × CH 16-byte chunks
+  // staging: items c = tid + NTH·i of the round's NST·KT × CH 16-byte chunks
   bf16x8 kreg[PF ? NI : 1], vreg[PF ? NI : 1];
-  bool pad_next = true;
-  auto fetch = [&](int t) {
-    const int key0 = t * KT;
+  bool pad_next[NST];
+  auto fetch_pad = [&](int key0) {
+#pragma unroll
+    for (int j = 0; j < NST; ++j) {
+      const int key = key0 + j * KT + l;
+      pad_next[j] = key >= k_end;
+      if (!pad_next[j] && a.kmask) pad_next[j] = a.kmask[(long long)b * a.Nk + key] != 0;
+    }
+  };
+  auto fetch = [&](int key0) {
 #pragma unroll
     for (int i = 0; i < (PF ? NI : 1); ++i) {
       const int c = threadIdx.x + NTH * i, key = key0 + c / CH, col = (c % CH) * 8;
       kreg[i] = vreg[i] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (c < KT * CH && key < a.Nk) {
+      if (c < NST * KT * CH && key < k_end) {
         kreg[i] = *reinterpret_cast<const bf16x8*>(kb + (long long)key * a.k_rs + col);
         vreg[i] = *reinterpret_cast<const bf16x8*>(vb + (long long)key * a.v_rs + col);
       }
     }
-    const int key = key0 + l;
-    pad_next = key >= a.Nk;
-    if (!pad_next && a.kmask) pad_next = a.kmask[(long long)b * a.Nk + key] != 0;
+    fetch_pad(key0);
   };
-  auto store = [&]() {
-#pragma unroll
-    for (int i = 0; i < (PF ? NI : 1); ++i) {
-      const int c = threadIdx.x + NTH * i, kr = c / CH, col = (c % CH) * 8;
-      if (c < KT * CH) {
-        *reinterpret_cast<bf16x8*>(sK + kr * LDK + col) = kreg[i];
-        *reinterpret_cast<bf16x8*>(sV + kr * LDV + col) = vreg[i];
-      }
-    }
-  };
-  if (PF && t_begin < t_end) fetch(t_begin);
+  if (PF && t_begin < t_end) fetch(t_begin * KT);
 
-  for (int t = t_begin; t < t_end; ++t) {
-    const int key0 = t * KT;
+  for (int t0 = t_begin; t0 < t_end; t0 += NST) {
+    const int rkey0 = t0 * KT;
     __syncthreads();
     if constexpr (PF) {
-      store();
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int c = threadIdx.x + NTH * i, kr = c / CH, col = (c % CH) * 8;
+        if (c < NST * KT * CH) {
+          *reinterpret_cast<bf16x8*>(sK + kr * LDK + col) = kreg[i];
+          *reinterpret_cast<bf16x8*>(sV + kr * LDV + col) = vreg[i];
+        }
+      }
     } else {
-      for (int c = threadIdx.x; c < KT * CH; c += NTH) {
-        const int kr = c / CH, col = (c % CH) * 8, key = key0 + kr;
+      for (int c = threadIdx.x; c < NST * KT * CH; c += NTH) {
+        const int kr = c / CH, col = (c % CH) * 8, key = rkey0 + kr;
         bf16x8 kv = bf16x8{0, 0, 0, 0, 0, 0, 0, 0}, vv = kv;
-        if (key < a.Nk) {
+        if (key < k_end) {
           kv = *reinterpret_cast<const bf16x8*>(kb + (long long)key * a.k_rs + col);
           vv = *reinterpret_cast<const bf16x8*>(vb + (long long)key * a.v_rs + col);
         }
         *reinterpret_cast<bf16x8*>(sK + kr * LDK + col) = kv;
         *reinterpret_cast<bf16x8*>(sV + kr * LDV + col) = vv;
       }
-      const int key = key0 + l;
-      pad_next = key >= a.Nk;
-      if (!pad_next && a.kmask) pad_next = a.kmask[(long long)b * a.Nk + key] != 0;
+      fetch_pad(rkey0);
     }
-    // key-padding bits for this tile (bit i = key0+i is padding or out of range)
-    const uint64_t padbits = __ballot(pad_next);
+    // key-padding bits per tile of the round (bit i = key is padding or outside the split)
+    uint64_t padbits[NST];
+#pragma unroll
+    for (int j = 0; j < NST; ++j) padbits[j] = __ballot(pad_next[j]);
     __syncthreads();
-    if (PF && t + 1 < t_end) fetch(t + 1);
+    if (PF && t0 + NST < t_end) fetch((t0 + NST) * KT);
 
-    f32x16 s[2];
 #pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
-      s[kh] = f32x16{};
+    for (int j = 0; j < NST; ++j) {
+      if (t0 + j >= t_end) break;
+      const int key0 = (t0 + j) * KT;
+      const uint16_t* tK = sK + j * KT * LDK;
+      const uint16_t* tV = sV + j * KT * LDV;
+      f32x16 s[2];
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) s[kh] = mfma32(frag_kc(sK, LDK, 32 * kh, 16 * ks), qf[ks], s[kh]);
-    }
-    // scale, mask, tile max
-    float mt = -INFINITY;
+      for (int kh = 0; kh < 2; ++kh) {
+        s[kh] = f32x16{};
 #pragma unroll
-    for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int kr = 32 * kh + acc_row(i, hh);
-        float v = s[kh][i] * a.scale_log2;
-        v = ((padbits >> kr) & 1ull) ? -INFINITY : v;
-        s[kh][i] = v;
-        mt = fmaxf(mt, v);
+        for (int ks = 0; ks < KS; ++ks) s[kh] = mfma32(frag_kc(tK, LDK, 32 * kh, 16 * ks), qf[ks], s[kh]);
       }
-    mt = xor32_max(mt);
-    const float m_new = fmaxf(m_run, mt);
-    const float alpha = exp2f(m_run - m_new);
-    m_run = m_new;
-    float ls = 0.f;
+      // scale, mask (only tiles that hold padding keys), tile max
+      float mt = -INFINITY;
+      if (padbits[j] == 0ull) {
 #pragma unroll
-    for (int kh = 0; kh < 2; ++kh)
+        for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float p = exp2f(s[kh][i] - m_new);
-        ls += p;
-        if (a.drop_thresh) {
-          const int key = key0 + 32 * kh + acc_row(i, hh);
-          const uint32_t idx = (uint32_t)qi * (uint32_t)a.Nk + (uint32_t)key;
-          p = keep_elem(a.seed, (uint32_t)(b * a.H + h), idx, a.drop_thresh) ? p * a.drop_scale : 0.f;
+          for (int i = 0; i < 16; ++i) {
+            s[kh][i] *= a.scale_log2;
+            mt = fmaxf(mt, s[kh][i]);
+          }
+      } else {
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+          // bits of this lane-half's 16 accumulator rows: row = 32kh + (i&3) + 8(i>>2) + 4hh
+          const uint32_t word = (uint32_t)(padbits[j] >> (32 * kh)) >> (4 * hh);
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const float v = ((word >> ((i & 3) + 8 * (i >> 2))) & 1u) ? -INFINITY : s[kh][i] * a.scale_log2;
+            s[kh][i] = v;
+            mt = fmaxf(mt, v);
+          }
         }
-        s[kh][i] = p;
       }
-    l_run = l_run * alpha + ls;
+      mt = xor32_max(mt);
+      const float m_new = fmaxf(m_run, mt);
+      const float alpha = fast_exp2(m_run - m_new);
+      m_run = m_new;
+      float ls = 0.f;
 #pragma unroll
-    for (int t2 = 0; t2 < NT; ++t2)
+      for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) o[t2][i] *= alpha;
-    // O^T += V^T · P^T
+        for (int i = 0; i < 16; ++i) {
+          float p = fast_exp2(s[kh][i] - m_new);
+          ls += p;
+          if (a.drop_thresh) {
+            const int key = key0 + 32 * kh + acc_row(i, hh);
+            const uint32_t idx = (uint32_t)qi * (uint32_t)a.Nk + (uint32_t)key;
+            p = keep_elem(a.seed, (uint32_t)(b * a.H + h), idx, a.drop_thresh) ? p * a.drop_scale : 0.f;
+          }
+          s[kh][i] = p;
+        }
+      l_run = l_run * alpha + ls;
 #pragma unroll
-    for (int kh = 0; kh < 2; ++kh)
+      for (int t2 = 0; t2 < NT; ++t2)
 #pragma unroll
-      for (int ss = 0; ss < 2; ++ss) {
-        const bf16x8 pb = pack_acc(s[kh], ss);
+        for (int i = 0; i < 16; ++i) o[t2][i] *= alpha;
+      // O^T += V^T · P^T
 #pragma unroll
-        for (int t2 = 0; t2 < NT; ++t2)
-          o[t2] = mfma32(frag_ks_perm(sV, LDV, 32 * t2, 32 * kh + 16 * ss), pb, o[t2]);
-      }
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const bf16x8 pb = pack_acc(s[kh], ss);
+#pragma unroll
+          for (int t2 = 0; t2 < NT; ++t2)
+            o[t2] = mfma32(frag_ks_perm(tV, LDV, 32 * t2, 32 * kh + 16 * ss), pb, o[t2]);
+        }
+    }
   }
 
   const float l_tot = xor32_sum(l_run);
@@ -316,16 +342,21 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
   constexpr int LD = (D < 32 ? 32 : D) + 8;  // Q / dO / K tiles [row][d] (D=16 zero-padded to 32 cols)
   constexpr int NT = (D < 32) ? 1 : D / 32;
   constexpr int KS = D / 16;
-  constexpr int LDS_ = 40;                   // dS tile [key][q] (32 q + pad)
+  constexpr int LDS_ = 40;                   // dS tiles [key][q] (32 q + pad)
   constexpr int KB = 32 * NW;                // keys per workgroup
   constexpr int NTH = 64 * NW, CH = D / 8;
-  constexpr int NI = (2 * 32 * CH + NTH - 1) / NTH;  // Q + dO tile 16-B items per thread
-  __shared__ __attribute__((aligned(16))) uint16_t sQ[2][32 * LD + 64];
-  __shared__ __attribute__((aligned(16))) uint16_t sdO[2][32 * LD + 64];
+  // queries in rounds of NQS 32-query tiles (≤ 4 16-byte chunks of Q + dO per thread), the
+  // next round register-prefetched.  Every wave writes its dS slab of each tile into LDS;
+  // after one barrier wave j (< NQS) forms tile j's dQ over all KB keys of the block with
+  // MFMAs (no cross-wave reduction, no atomics inside the block).
+  constexpr int NQS0 = 4 * NTH / (64 * CH);
+  constexpr int NQS = NQS0 >= 4 ? 4 : (NQS0 >= 1 ? NQS0 : 1);
+  constexpr int NI = (NQS * 64 * CH + NTH - 1) / NTH;
+  __shared__ __attribute__((aligned(16))) uint16_t sQ[NQS * 32 * LD + 64];
+  __shared__ __attribute__((aligned(16))) uint16_t sdO[NQS * 32 * LD + 64];
   __shared__ __attribute__((aligned(16))) uint16_t sK[KB * LD + 64];
-  __shared__ __attribute__((aligned(16))) uint16_t sdS[NW * 32 * LDS_];
-  __shared__ float sL[2][32], sDl[2][32];
-  __shared__ float sdQ[NW][32 * (D + 1)];
+  __shared__ __attribute__((aligned(16))) uint16_t sdS[NQS * KB * LDS_];
+  __shared__ float sL[NQS * 32], sDl[NQS * 32];
 
   const int w = wave_id(), l = lane_id(), r = l & 31, hh = l >> 5;
   const int h = blockIdx.y, b = blockIdx.z;
@@ -342,35 +373,26 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
   const uint16_t* dobp = dO + (long long)b * a.Nq * HD + h * D;
   const int nqt = (a.Nq + 31) / 32;
 
-  // per-tile register staging: items c < 32·CH are Q chunks, the next 32·CH dO chunks;
-  // threads [0, 32) also carry the tile's LSE, [32, 64) its delta
+  // round staging: chunk c < NQS·32·CH is Q, the next NQS·32·CH are dO; threads [0, NQS·32)
+  // carry the round's LSE, [NQS·32, NQS·64) its delta
   bf16x8 qreg[NI];
   float lreg = 0.f;
-  auto fetch = [&](int qt) {
-    const int q0 = qt * 32;
+  auto fetch = [&](int qt0) {
+    const int q00 = qt0 * 32;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int c = threadIdx.x + NTH * i, isdo = c >= 32 * CH, cc = isdo ? c - 32 * CH : c;
-      const int qq = q0 + cc / CH, col = (cc % CH) * 8;
+      const int c = threadIdx.x + NTH * i, isdo = c >= NQS * 32 * CH, cc = isdo ? c - NQS * 32 * CH : c;
+      const int qq = q00 + cc / CH, col = (cc % CH) * 8;
       qreg[i] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (c < 64 * CH && qq < a.Nq)
+      if (c < NQS * 64 * CH && qq < a.Nq)
         qreg[i] = isdo ? *reinterpret_cast<const bf16x8*>(dobp + (long long)qq * HD + col)
                        : *reinterpret_cast<const bf16x8*>(qbp + (long long)qq * a.q_rs + col);
     }
-    if (threadIdx.x < 64) {
-      const int qq = q0 + (threadIdx.x & 31);
+    if (threadIdx.x < NQS * 64) {
+      const int isd = threadIdx.x >= NQS * 32, qq = q00 + (isd ? threadIdx.x - NQS * 32 : threadIdx.x);
       const long long idx = ((long long)b * a.Nq + qq) * a.H + h;
-      lreg = threadIdx.x < 32 ? (qq < a.Nq ? LSE[idx] : INFINITY) : (qq < a.Nq ? delta[idx] : 0.f);
+      lreg = isd ? (qq < a.Nq ? delta[idx] : 0.f) : (qq < a.Nq ? LSE[idx] : INFINITY);
     }
-  };
-  auto store = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int c = threadIdx.x + NTH * i, isdo = c >= 32 * CH, cc = isdo ? c - 32 * CH : c;
-      if (c < 64 * CH) *reinterpret_cast<bf16x8*>((isdo ? sdO[buf] : sQ[buf]) + (cc / CH) * LD + (cc % CH) * 8) = qreg[i];
-    }
-    if (threadIdx.x < 32) sL[buf][threadIdx.x] = lreg;
-    else if (threadIdx.x < 64) sDl[buf][threadIdx.x - 32] = lreg;
   };
   if (nqt > 0) fetch(0);
 
@@ -387,12 +409,11 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
       *reinterpret_cast<bf16x8*>(sK + i * LD + 16) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
       *reinterpret_cast<bf16x8*>(sK + i * LD + 24) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
     }
-    for (int i = threadIdx.x; i < 64; i += NTH) {
-      const int bb = i >> 5, rr = i & 31;
-      *reinterpret_cast<bf16x8*>(sQ[bb] + rr * LD + 16) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      *reinterpret_cast<bf16x8*>(sQ[bb] + rr * LD + 24) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      *reinterpret_cast<bf16x8*>(sdO[bb] + rr * LD + 16) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      *reinterpret_cast<bf16x8*>(sdO[bb] + rr * LD + 24) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = threadIdx.x; i < NQS * 32; i += NTH) {
+      *reinterpret_cast<bf16x8*>(sQ + i * LD + 16) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      *reinterpret_cast<bf16x8*>(sQ + i * LD + 24) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      *reinterpret_cast<bf16x8*>(sdO + i * LD + 16) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      *reinterpret_cast<bf16x8*>(sdO + i * LD + 24) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
     }
   }
   // K^T / V^T operand fragments for this wave's 32 keys (B operand: B[k=d][col=key])
@@ -405,83 +426,89 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
   f32x16 dK[NT], dV[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) dK[t] = dV[t] = f32x16{};
-  uint16_t* mydS = sdS + w * 32 * LDS_;
+  const int kvalid = min(KB, a.Nk - kbase);  // keys of this block (rows of the dS tiles in use)
 
-  for (int qt = 0; qt < nqt; ++qt) {
-    const int q0 = qt * 32, buf = qt & 1;
-    store(buf);
-    __syncthreads();  // tile qt visible; last iteration's dQ reduction finished
-    if (qt + 1 < nqt) fetch(qt + 1);
-    const uint16_t* tQ = sQ[buf];
-    const uint16_t* tdO = sdO[buf];
+  for (int qt0 = 0; qt0 < nqt; qt0 += NQS) {
+    __syncthreads();  // the previous round's tiles and dS slabs are consumed
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int c = threadIdx.x + NTH * i, isdo = c >= NQS * 32 * CH, cc = isdo ? c - NQS * 32 * CH : c;
+      if (c < NQS * 64 * CH) *reinterpret_cast<bf16x8*>((isdo ? sdO : sQ) + (cc / CH) * LD + (cc % CH) * 8) = qreg[i];
+    }
+    if (threadIdx.x < NQS * 32) sL[threadIdx.x] = lreg;
+    else if (threadIdx.x < NQS * 64) sDl[threadIdx.x - NQS * 32] = lreg;
+    __syncthreads();
+    if (qt0 + NQS < nqt) fetch(qt0 + NQS);
 
-    // S = Q K^T and dP = dO V^T  (rows: queries; lane: key)
-    f32x16 S = f32x16{}, dP = f32x16{};
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      S = mfma32(frag_kc(tQ, LD, 0, 16 * s), kf[s], S);
-      dP = mfma32(frag_kc(tdO, LD, 0, 16 * s), vf[s], dP);
-    }
-    f32x16 P, dS;
+    for (int j = 0; j < NQS; ++j) {
+      if (qt0 + j >= nqt) break;
+      const int q0 = (qt0 + j) * 32;
+      const uint16_t* tQ = sQ + j * 32 * LD;
+      const uint16_t* tdO = sdO + j * 32 * LD;
+      // S = Q K^T and dP = dO V^T  (rows: queries; lane: key)
+      f32x16 S = f32x16{}, dP = f32x16{};
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int qr = acc_row(i, hh);
-      float p = kpad ? 0.f : exp2f(S[i] * a.scale_log2 - sL[buf][qr]);
-      float dp = dP[i];
-      float pd = p;
-      if (a.drop_thresh) {
-        const uint32_t idx = (uint32_t)(q0 + qr) * (uint32_t)a.Nk + (uint32_t)key;
-        const bool keep = keep_elem(a.seed, (uint32_t)(b * a.H + h), idx, a.drop_thresh);
-        pd = keep ? p * a.drop_scale : 0.f;
-        dp = keep ? dp * a.drop_scale : 0.f;
+      for (int s = 0; s < KS; ++s) {
+        S = mfma32(frag_kc(tQ, LD, 0, 16 * s), kf[s], S);
+        dP = mfma32(frag_kc(tdO, LD, 0, 16 * s), vf[s], dP);
       }
-      P[i] = pd;
-      dS[i] = p * (dp - sDl[buf][qr]);
-    }
-    // dV += P^T dO ; dK += dS^T Q   (accumulator as A operand: X^T · B)
-#pragma unroll
-    for (int ss = 0; ss < 2; ++ss) {
-      const bf16x8 pa = pack_acc(P, ss), sa = pack_acc(dS, ss);
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        dV[t] = mfma32(pa, frag_ks_perm(tdO, LD, 32 * t, 16 * ss), dV[t]);
-        dK[t] = mfma32(sa, frag_ks_perm(tQ, LD, 32 * t, 16 * ss), dK[t]);
-      }
-    }
-    // this wave's dQ partial = dS (32 q × its 32 keys) · K (32 keys × d): dS goes through the
-    // wave's own LDS slab (no barrier needed), the partial into sdQ[w]
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      uint2 pk;
-      pk.x = pack2(dS[4 * g], dS[4 * g + 1]);
-      pk.y = pack2(dS[4 * g + 2], dS[4 * g + 3]);
-      *reinterpret_cast<uint2*>(mydS + r * LDS_ + 8 * g + 4 * hh) = pk;
-    }
-    asm volatile("" ::: "memory");  // keep the slab reads behind the writes (one wave: LDS is in order)
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      f32x16 dq_acc = f32x16{};
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss)
-        dq_acc = mfma32(frag_ks(mydS, LDS_, 0, 16 * ss), frag_ks(sK + (32 * w) * LD, LD, 32 * t, 16 * ss), dq_acc);
+      f32x16 P, dS;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int dd = 32 * t + r;
-        if (dd < D) sdQ[w][acc_row(i, hh) * (D + 1) + dd] = dq_acc[i];
+        const int qr = acc_row(i, hh);
+        float p = kpad ? 0.f : fast_exp2(S[i] * a.scale_log2 - sL[j * 32 + qr]);
+        float dp = dP[i];
+        float pd = p;
+        if (a.drop_thresh) {
+          const uint32_t idx = (uint32_t)(q0 + qr) * (uint32_t)a.Nk + (uint32_t)key;
+          const bool keep = keep_elem(a.seed, (uint32_t)(b * a.H + h), idx, a.drop_thresh);
+          pd = keep ? p * a.drop_scale : 0.f;
+          dp = keep ? dp * a.drop_scale : 0.f;
+        }
+        P[i] = pd;
+        dS[i] = p * (dp - sDl[j * 32 + qr]);
+      }
+      // dV += P^T dO ; dK += dS^T Q   (accumulator as A operand: X^T · B)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const bf16x8 pa = pack_acc(P, ss), sa = pack_acc(dS, ss);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          dV[t] = mfma32(pa, frag_ks_perm(tdO, LD, 32 * t, 16 * ss), dV[t]);
+          dK[t] = mfma32(sa, frag_ks_perm(tQ, LD, 32 * t, 16 * ss), dK[t]);
+        }
+      }
+      // dS slab of (this wave's 32 keys) × (tile j's 32 queries) as [key][q]
+      uint16_t* slab = sdS + (j * KB + 32 * w) * LDS_;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint2 pk;
+        pk.x = pack2(dS[4 * g], dS[4 * g + 1]);
+        pk.y = pack2(dS[4 * g + 2], dS[4 * g + 3]);
+        *reinterpret_cast<uint2*>(slab + r * LDS_ + 8 * g + 4 * hh) = pk;
       }
     }
     __syncthreads();
-    // Σ over the waves' key slices; a single key block owns dQ outright (plain store)
-    for (int e = threadIdx.x; e < 32 * D; e += NTH) {
-      const int qr = e / D, dd = e % D;
-      const int qq = q0 + qr;
-      if (qq < a.Nq) {
-        float v = 0.f;
+    // dQ of tile j = w: Σ over the block's keys of dS[key][q] · K[key][d]
+    if (w < NQS && qt0 + w < nqt) {
+      const uint16_t* tS = sdS + w * KB * LDS_;
 #pragma unroll
-        for (int ww = 0; ww < NW; ++ww) v += sdQ[ww][qr * (D + 1) + dd];
-        float* dst = dq + (long long)b * dq_bs + (long long)qq * dq_rs + h * D + dd;
-        if (dq_atomic) atomicAdd(dst, v * a.scale);
-        else *dst = v * a.scale;
+      for (int t = 0; t < NT; ++t) {
+        f32x16 dq_acc = f32x16{};
+        for (int k0 = 0; k0 < kvalid; k0 += 16)
+          dq_acc = mfma32(frag_ks(tS, LDS_, 0, k0), frag_ks(sK, LD, 32 * t, k0), dq_acc);
+        // accumulator: col = lane&31 = d, row = acc_row = query within the tile
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int dd = 32 * t + r, qq = (qt0 + w) * 32 + acc_row(i, hh);
+          if (dd < D && qq < a.Nq) {
+            float* dst = dq + (long long)b * dq_bs + (long long)qq * dq_rs + h * D + dd;
+            const float v = dq_acc[i] * a.scale;
+            if (dq_atomic) atomicAdd(dst, v);
+            else *dst = v;
+          }
+        }
       }
     }
   }

@@ -125,6 +125,9 @@ __device__ __forceinline__ float wave_max(float v) {
   return fmaxf(a, b);
 }
 
+// 2^x as one v_exp_f32 (no denormal-range fixup: results below 2^-126 flush to 0, -inf → 0)
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 // ---- GELU (erf form, nn.GELU default) ------------------------------------------------
 __device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float gelu_grad(float x) {
