@@ -1,17 +1,24 @@
 #!/usr/bin/env python
-"""Headline benchmark: IMDB masked-language-model training throughput (samples/s, whole job).
+"""Training-throughput benchmark (samples/s, whole job) for the BASELINE.json configs.
 
-Config (BASELINE.json config 2 / metric): Perceiver IO MLM, seq_len 512, vocab 10003,
-256 latents × 64 channels, 3 encoder layers × (1 cross + 6 self-attention), 4/4/4 heads,
-dropout 0, batch 64 per GPU (reference README MLM command), AdamW + OneCycleLR, bf16 compute.
-Synthetic token ids of that shape, random-init weights (no network on the GPU box).
+Default (the headline, BASELINE.json metric / config 2): Perceiver IO MLM, seq_len 512,
+vocab 10003, 256 latents × 64 channels, 3 encoder layers × (1 cross + 6 self-attention),
+4/4/4 heads, dropout 0, batch 64 per GPU (reference README MLM command), AdamW + OneCycleLR,
+bf16 compute.  Synthetic token ids of that shape, random-init weights (no network on the GPU box).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, RCCL)
+    python bench.py --config {mlm256,seq_clf,imagenet,long_mlm,mnist} ...
 
-Prints ONE JSON line on rank 0.  ``--backend reference`` measures the reference's own
-compute (nn.MultiheadAttention math, full-logit CE, torch AdamW) eagerly on the same
-device — the bar recorded in BASELINE.md.
+Other configs (BASELINE.json configs 1, 3-5): ``seq_clf`` = IMDB text classifier with a frozen
+encoder (decoder-only training, batch 128/GPU, README seq_clf command); ``imagenet`` =
+224×224×3 image classifier with Fourier position encoding (50,176 inputs × 133 channels,
+32×128 latents, 3×(1+3) layers, 1000 classes); ``long_mlm`` = MLM at seq_len 8192 with 512
+latents; ``mnist`` = the 28×28 classifier of the README (batch 128).
+
+Prints ONE JSON line on rank 0.  ``--backend reference`` measures the reference's own compute
+(nn.MultiheadAttention math, full-logit CE, torch AdamW) eagerly under bf16 autocast on the same
+device — the bar recorded in BASELINE.md and bench/baseline_measured.json.
 """
 from __future__ import annotations
 
@@ -25,41 +32,123 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 BASELINE_FILE = os.path.join(ROOT, "bench", "baseline_measured.json")
+HEADLINE_METRIC = "samples/sec (whole node) IMDB MLM seq_len=512 at 1/2/4/8 MI355X"
+
+# config name → defaults (batch per GPU, sequence length / inputs) and the metric string
+CONFIGS = {
+    "mlm256": dict(batch=64, seq_len=512, latents=256, channels=64, metric=HEADLINE_METRIC),
+    "seq_clf": dict(batch=128, seq_len=512, latents=64, channels=64,
+                    metric="samples/sec (whole node) IMDB seq_clf frozen encoder seq_len=512"),
+    "imagenet": dict(batch=32, seq_len=224 * 224, latents=32, channels=128,
+                     metric="samples/sec (whole node) ImageNet-shape 224x224x3 img_clf Fourier PE"),
+    "long_mlm": dict(batch=8, seq_len=8192, latents=512, channels=64,
+                     metric="samples/sec (whole node) IMDB MLM seq_len=8192 512 latents"),
+    "mnist": dict(batch=128, seq_len=28 * 28, latents=32, channels=128,
+                  metric="samples/sec (whole node) MNIST img_clf 32x128 latents"),
+}
 
 
 def parse(argv=None):
-    ap = argparse.ArgumentParser(description="Perceiver IO MLM training throughput")
+    ap = argparse.ArgumentParser(description="Perceiver IO training throughput")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=64, help="per-GPU batch (reference README: 64)")
-    ap.add_argument("--seq-len", type=int, default=512)
-    ap.add_argument("--latents", type=int, default=256)
-    ap.add_argument("--channels", type=int, default=64)
+    ap.add_argument("--config", default="mlm256", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the config's)")
+    ap.add_argument("--seq-len", type=int, default=None)
+    ap.add_argument("--latents", type=int, default=None)
+    ap.add_argument("--channels", type=int, default=None)
     ap.add_argument("--vocab", type=int, default=10003)
     ap.add_argument("--backend", default="hip", choices=["hip", "torch", "reference"])
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture of the step")
     ap.add_argument("--profile-steps", type=int, default=0)
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    cfg = CONFIGS[a.config]
+    for k in ("batch", "seq_len", "latents", "channels"):
+        if getattr(a, k) is None:
+            setattr(a, k, cfg[k])
+    return a
+
+
+def _opt(lr=3e-3, wd=0.0):
+    return {"class_path": "torch.optim.AdamW", "init_args": {"lr": lr, "weight_decay": wd}}
+
+
+def _sched(lr=3e-3):
+    return {"class_path": "torch.optim.lr_scheduler.OneCycleLR",
+            "init_args": {"max_lr": lr, "total_steps": 50000, "pct_start": 0.1, "cycle_momentum": False}}
 
 
 def build(args, device):
+    """→ (lit module, loss_fn(batch), make_batch(generator), model description, lr, weight decay)."""
     import torch
 
-    from perceiver_io_amd.tasks import LitMaskedLanguageModel
+    from perceiver_io_amd.tasks import LitImageClassifier, LitMaskedLanguageModel, LitTextClassifier
 
-    lit = LitMaskedLanguageModel(
-        vocab_size=args.vocab, max_seq_len=args.seq_len,
-        optimizer_init={"class_path": "torch.optim.AdamW", "init_args": {"lr": 3e-3, "weight_decay": 0.0}},
-        scheduler_init={"class_path": "torch.optim.lr_scheduler.OneCycleLR",
-                        "init_args": {"max_lr": 3e-3, "total_steps": 50000, "pct_start": 0.1, "cycle_momentum": False}},
-        num_latents=args.latents, num_latent_channels=args.channels, num_encoder_layers=3,
+    B, L = args.batch, args.seq_len
+    if args.config in ("mlm256", "long_mlm"):
+        lit = LitMaskedLanguageModel(
+            vocab_size=args.vocab, max_seq_len=L, optimizer_init=_opt(), scheduler_init=_sched(),
+            num_latents=args.latents, num_latent_channels=args.channels, num_encoder_layers=3,
+            num_encoder_cross_attention_heads=4, num_encoder_self_attention_heads=4,
+            num_encoder_self_attention_layers_per_block=6, num_decoder_cross_attention_heads=4, dropout=0.0,
+            masked_samples=None)
+        model = lit.model
+
+        def loss_fn(batch):
+            _, ids, pad = batch
+            return model.loss(ids, pad)
+
+        def make_batch(g):
+            ids = torch.randint(3, args.vocab, (B, L), generator=g)
+            return (torch.zeros(B, dtype=torch.long), ids, torch.zeros(B, L, dtype=torch.bool))
+
+        desc = f"perceiver-io-mlm latents={args.latents}x{args.channels} layers=3x(1+6) vocab={args.vocab}"
+        return lit, loss_fn, make_batch, desc, 3e-3, 0.0
+    if args.config == "seq_clf":
+        lit = LitTextClassifier(
+            num_classes=2, vocab_size=args.vocab, max_seq_len=L, freeze_encoder=True,
+            optimizer_init=_opt(1e-3, 0.01), scheduler_init=None, num_latents=args.latents,
+            num_latent_channels=args.channels, num_encoder_layers=3, num_encoder_cross_attention_heads=4,
+            num_encoder_self_attention_heads=4, num_encoder_self_attention_layers_per_block=6,
+            num_decoder_cross_attention_heads=1, dropout=0.0)
+        model = lit.model
+
+        def loss_fn(batch):
+            y, ids, pad = batch
+            return torch.nn.functional.cross_entropy(model(ids, pad).float(), y)
+
+        def make_batch(g):
+            ids = torch.randint(3, args.vocab, (B, L), generator=g)
+            return (torch.randint(0, 2, (B,), generator=g), ids, torch.zeros(B, L, dtype=torch.bool))
+
+        desc = (f"perceiver-io-seq-clf frozen-encoder latents={args.latents}x{args.channels} layers=3x(1+6) "
+                f"vocab={args.vocab}")
+        return lit, loss_fn, make_batch, desc, 1e-3, 0.01
+    # image classifiers
+    if args.config == "imagenet":
+        side = int(round(args.seq_len ** 0.5))
+        shape, classes, sa, bands = (side, side, 3), 1000, 3, 32
+    else:
+        shape, classes, sa, bands = (28, 28, 1), 10, 3, 32
+    lit = LitImageClassifier(
+        image_shape=shape, num_classes=classes, num_frequency_bands=bands, optimizer_init=_opt(1e-3, 0.01),
+        scheduler_init=None, num_latents=args.latents, num_latent_channels=args.channels, num_encoder_layers=3,
         num_encoder_cross_attention_heads=4, num_encoder_self_attention_heads=4,
-        num_encoder_self_attention_layers_per_block=6, num_decoder_cross_attention_heads=4, dropout=0.0,
-        masked_samples=None)
-    lit.to(device)
-    return lit
+        num_encoder_self_attention_layers_per_block=sa, num_decoder_cross_attention_heads=1, dropout=0.0)
+    model = lit.model
+
+    def loss_fn(batch):
+        x, y = batch
+        return torch.nn.functional.cross_entropy(model(x).float(), y)
+
+    def make_batch(g):
+        return (torch.randn((B,) + shape, generator=g), torch.randint(0, classes, (B,), generator=g))
+
+    desc = (f"perceiver-io-img-clf {shape[0]}x{shape[1]}x{shape[2]} fourier-bands={bands} "
+            f"latents={args.latents}x{args.channels} layers=3x(1+{sa}) classes={classes}")
+    return lit, loss_fn, make_batch, desc, 1e-3, 0.01
 
 
 def main(argv=None):
@@ -79,44 +168,42 @@ def main(argv=None):
     ops.set_backend("auto" if args.backend == "hip" else args.backend)
     torch.manual_seed(1234 + info.rank)
 
-    lit = build(args, device)
+    lit, loss_inner, make_batch, desc, lr, wd = build(args, device)
+    lit.to(device)
     model = lit.model
-    B, L = args.batch, args.seq_len
+    params = [p for p in model.parameters() if p.requires_grad]
     fused = args.backend == "hip" and cuda
     if fused:
         from perceiver_io_amd.ops.optim import FusedAdamW
 
-        opt = FusedAdamW(model.parameters(), lr=3e-3, weight_decay=0.0)
+        opt = FusedAdamW(params, lr=lr, weight_decay=wd)
     else:
-        opt = torch.optim.AdamW(model.parameters(), lr=3e-3, weight_decay=0.0)
-    sched = torch.optim.lr_scheduler.OneCycleLR(opt, max_lr=3e-3, total_steps=50000, pct_start=0.1,
+        opt = torch.optim.AdamW(params, lr=lr, weight_decay=wd)
+    sched = torch.optim.lr_scheduler.OneCycleLR(opt, max_lr=lr, total_steps=50000, pct_start=0.1,
                                                 cycle_momentum=False)
     reducer = None
     if world > 1:
         from perceiver_io_amd.ops.optim import FlatParameterSpace
 
-        flat = opt.flat if fused else FlatParameterSpace(model.parameters(), with_shadow=False)
+        flat = opt.flat if fused else FlatParameterSpace(params, with_shadow=False, replicate=False)
         reducer = FlatGradReducer(flat, bucket_bytes=64 << 20)
         reducer.broadcast_parameters(model)
 
     autocast = (not fused) and args.dtype == "bf16" and cuda
 
     def loss_fn(batch):
-        _, ids, pad = batch
         if autocast:
             with torch.autocast("cuda", dtype=torch.bfloat16):
-                return model.loss(ids, pad)
-        return model.loss(ids, pad)
+                return loss_inner(batch)
+        return loss_inner(batch)
 
     engine = StepEngine(loss_fn, opt, sched, reducer=reducer, device=device, graph=fused and not args.no_graph)
     g = torch.Generator(device="cpu").manual_seed(99 + info.rank)
 
-    def batch():
-        ids = torch.randint(3, args.vocab, (B, L), generator=g)
-        pad = torch.zeros(B, L, dtype=torch.bool)
-        return (torch.zeros(B, dtype=torch.long), ids.to(device), pad.to(device))
+    def to_dev(b):
+        return tuple(t.to(device) for t in b)
 
-    data = [batch() for _ in range(4)]
+    data = [to_dev(make_batch(g)) for _ in range(4)]
     for i in range(args.warmup):
         loss = engine.step(data[i % 4])
     if cuda:
@@ -144,6 +231,7 @@ def main(argv=None):
             torch.cuda.synchronize()
         if info.is_main:
             print(prof.key_averages().table(sort_by="cuda_time_total", row_limit=40), file=sys.stderr)
+    B = args.batch
     ms = dt / args.steps * 1e3
     value = B * world * args.steps / dt
     # bar: the reference's own compute measured eagerly on one MI355X (bench/baseline_measured.json,
@@ -151,20 +239,22 @@ def main(argv=None):
     vs = None
     if os.path.exists(BASELINE_FILE):
         try:
-            ref = float(json.load(open(BASELINE_FILE))["mlm256_reference_samples_per_s_per_gpu"])
-            vs = value / (ref * world)
+            key = "mlm256" if args.config == "mlm256" else args.config
+            ref = json.load(open(BASELINE_FILE)).get(f"{key}_reference_samples_per_s_per_gpu")
+            vs = value / (float(ref) * world) if ref else None
         except Exception:
             vs = None
     if info.is_main:
         out = {
-            "metric": "samples/sec (whole node) IMDB MLM seq_len=512 at 1/2/4/8 MI355X",
+            "metric": CONFIGS[args.config]["metric"],
             "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": round(vs, 3) if vs else None,
-            "dtype": args.dtype if not fused else "bf16", "data": "synthetic (random token ids, random-init weights)",
-            "config": {"model": f"perceiver-io-mlm latents={args.latents}x{args.channels} layers=3x(1+6) vocab={args.vocab}",
-                       "global_batch": B * world, "seq_len": L, "parallelism": f"dp{world}",
-                       "backend": args.backend, "graph": bool(fused and not args.no_graph)},
+            "dtype": args.dtype if not fused else "bf16",
+            "data": "synthetic (random inputs of the config's shape, random-init weights)",
+            "config": {"model": desc, "global_batch": B * world, "seq_len": args.seq_len,
+                       "parallelism": f"dp{world}", "backend": args.backend,
+                       "graph": bool(fused and not args.no_graph), "name": args.config},
             "final_loss": round(final_loss, 4),
         }
         print(json.dumps(out), flush=True)

@@ -34,7 +34,7 @@ void post_attn_bwd_launch(int, const float*, const float*, const float*, const f
                           const float*, float*, uint16_t*, float*, int, const PostAttnGrads&, int, hipStream_t);
 void ln_linear_bwd_launch(const void*, bool, int, int, const uint16_t*, int, const void*, bool, int, const float*,
                           const float*, const float*, const float*, const float*, int, float*, int, float*, float*,
-                          float*, float*, int, int, hipStream_t);
+                          float*, float*, int, int, int, hipStream_t);
 void wgrad_launch(const void*, bool, int, int, const void*, bool, int, int, int, const float*, const float*,
                   const float*, const float*, int, int, float*, float*, hipStream_t);
 void ce_fwd_launch(int, const uint16_t*, const int64_t*, const uint16_t*, const float*, int, int, float*, float*,
@@ -281,13 +281,14 @@ OptT ln_linear_bwd(Tensor g, Tensor w, Tensor x, OptT mean, OptT rstd, OptT lnw,
     dgp = vec_target(*dlnw, Kin, "dlnw", vrs);
     dbp = vec_target(*dlnb, Kin, "dlnb", vrs);
   }
-  if (dW.has_value()) dwp = vec_target(*dW, (int64_t)N * Kin, "dW", vrs);
+  int wrs = -1;  // the weight target's replica stride may differ from the vectors'
+  if (dW.has_value()) dwp = vec_target(*dW, (int64_t)N * Kin, "dW", wrs);
   if (db.has_value()) { TORCH_CHECK(dW.has_value(), "db needs dW"); dbiasp = vec_target(*db, N, "db", vrs); }
   const float* dr = nullptr; int drs = 0;
   if (dres.has_value()) { dr = f32p(*dres); drs = (int)dres->stride(0); TORCH_CHECK(dres->stride(1) == 1); }
   pio::ln_linear_bwd_launch(g.data_ptr(), is_bf16(g), (int)g.stride(0), N, bfp(w), Kin, x.data_ptr(), is_bf16(x),
                             (int)x.stride(0), f32o(mean), f32o(rstd), f32o(lnw), f32o(lnb), dr, drs, dxp, Kin, dgp, dbp,
-                            dwp, dbiasp, vrs < 0 ? 0 : vrs, R, stream());
+                            dwp, dbiasp, vrs < 0 ? 0 : vrs, wrs < 0 ? 0 : wrs, R, stream());
   if (need_dx) return dx;
   return c10::nullopt;
 }

@@ -779,7 +779,7 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
     int x_rs, const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ lnw,
     const float* __restrict__ lnb, const float* __restrict__ dres, int dres_rs, float* __restrict__ dX, int dx_rs,
     float* __restrict__ dlnw, float* __restrict__ dlnb, float* __restrict__ dW, float* __restrict__ db, int vrs,
-    int R) {
+    int wrs, int R) {
   constexpr int KP = 32 * NCH, LD = KP + 8, LDG = 64 + 8, LDF = KP + 4;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* sG = smem;                                   // [64][LDG]  G chunk
@@ -839,7 +839,7 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
     }
     tile_gemm<MAXT, true, false>(sG, LDG, sW, LD, 64, KP, 64, acc);
     if (dW) {
-      wgrad_tile<MAXT>(sG, LDG, sXn, LD, 64, KP, N - nc, Kin, rep(dW, vrs) + (long long)nc * Kin, Kin);
+      wgrad_tile<MAXT>(sG, LDG, sXn, LD, 64, KP, N - nc, Kin, rep(dW, wrs) + (long long)nc * Kin, Kin);
       if (db) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -1046,23 +1046,23 @@ template <typename TG, typename TX, int NCH>
 static void ln_linear_bwd_t(const void* G, int g_rs, int N, const uint16_t* W, int Kin, const void* X, int x_rs,
                             const float* mean, const float* rstd, const float* lnw, const float* lnb, const float* dres,
                             int dres_rs, float* dX, int dx_rs, float* dlnw, float* dlnb, float* dW, float* db, int vrs,
-                            int R, hipStream_t st) {
+                            int wrs, int R, hipStream_t st) {
   constexpr int KP = 32 * NCH;
   const size_t smem = 64 * 72 * 2 + 2 * 64 * (KP + 8) * 2 + 64 * (KP + 4) * 4 + 8 * KP * 4 + 4 * 64 * 4;
   auto fn = ln_linear_bwd_kernel<TG, TX, NCH>;
   set_smem_once((const void*)fn);
   hipLaunchKernelGGL(fn, dim3((R + 63) / 64), dim3(256), smem, st, (const TG*)G, g_rs, N, W, Kin, (const TX*)X, x_rs,
-                     mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, dlnw, dlnb, dW, db, vrs, R);
+                     mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, dlnw, dlnb, dW, db, vrs, wrs, R);
 }
 
 template <typename TG, typename TX>
 static void ln_linear_bwd_n(int nch, const void* G, int g_rs, int N, const uint16_t* W, int Kin, const void* X,
                             int x_rs, const float* mean, const float* rstd, const float* lnw, const float* lnb,
                             const float* dres, int dres_rs, float* dX, int dx_rs, float* dlnw, float* dlnb, float* dW,
-                            float* db, int vrs, int R, hipStream_t st) {
+                            float* db, int vrs, int wrs, int R, hipStream_t st) {
 #define LNB(K)                                                                                                    \
   ln_linear_bwd_t<TG, TX, K>(G, g_rs, N, W, Kin, X, x_rs, mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, dlnw, \
-                             dlnb, dW, db, vrs, R, st)
+                             dlnb, dW, db, vrs, wrs, R, st)
   switch (nch) {
     case 1: LNB(1); break;
     case 2: LNB(2); break;
@@ -1075,11 +1075,11 @@ static void ln_linear_bwd_n(int nch, const void* G, int g_rs, int N, const uint1
 void ln_linear_bwd_launch(const void* G, bool g_bf16, int g_rs, int N, const uint16_t* W, int Kin, const void* X,
                           bool x_bf16, int x_rs, const float* mean, const float* rstd, const float* lnw,
                           const float* lnb, const float* dres, int dres_rs, float* dX, int dx_rs, float* dlnw,
-                          float* dlnb, float* dW, float* db, int vrs, int R, hipStream_t st) {
+                          float* dlnb, float* dW, float* db, int vrs, int wrs, int R, hipStream_t st) {
   const int nch = pick_nch(Kin);  // Kin ≤ 160 → ≤ 5
 #define LDG(TG, TX)                                                                                           \
   ln_linear_bwd_n<TG, TX>(nch, G, g_rs, N, W, Kin, X, x_rs, mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, \
-                          dlnw, dlnb, dW, db, vrs, R, st)
+                          dlnw, dlnb, dW, db, vrs, wrs, R, st)
   if (g_bf16 && x_bf16) LDG(uint16_t, uint16_t);
   else if (g_bf16) LDG(uint16_t, float);
   else if (x_bf16) LDG(float, uint16_t);

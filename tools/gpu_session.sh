@@ -32,6 +32,12 @@ for step in "$@"; do
     micro)    run micro 300 python tools/microbench.py ;;
     attn)     run attn 300 python tools/attn_scaling.py ;;
     pmc_attn) run pmc_attn 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_INSTS_LDS --output-format csv -d gpurun_out/pmc -o attn -- python tools/attn_scaling.py 64 ;;
+    configs)  for c in seq_clf imagenet long_mlm mnist; do
+                run "cfg_${c}" 600 python bench.py --config $c --steps 10 --warmup 3
+              done ;;
+    configs_ref) for c in mlm256 seq_clf imagenet long_mlm mnist; do
+                run "cfgref_${c}" 900 python bench.py --config $c --backend reference --steps 5 --warmup 2
+              done ;;
     prof)     run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 3 ;;
     dbg0)     run dbg0 300 env AMD_SERIALIZE_KERNEL=3 python tools/debug_engine.py 0 ;;
     dbg1)     run dbg1 300 python tools/debug_engine.py 1 ;;
