@@ -338,7 +338,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
                                                            const float* __restrict__ delta, float* __restrict__ dq,
                                                            long long dq_bs, int dq_rs, float* __restrict__ dk,
                                                            long long dk_bs, int dk_rs, float* __restrict__ dv,
-                                                           long long dv_bs, int dv_rs, int dq_atomic) {
+                                                           long long dv_bs, int dv_rs, int dq_atomic, int kv_acc) {
   constexpr int LD = (D < 32 ? 32 : D) + 8;  // Q / dO / K tiles [row][d] (D=16 zero-padded to 32 cols)
   constexpr int NT = (D < 32) ? 1 : D / 32;
   constexpr int KS = D / 16;
@@ -521,8 +521,11 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
       const int kk = kbase + 32 * w + acc_row(i, hh);
       const int dd = 32 * t + r;
       if (kk < a.Nk && dd < D) {
-        dk[(long long)b * dk_bs + (long long)kk * dk_rs + h * D + dd] = dK[t][i] * a.scale;
-        dv[(long long)b * dv_bs + (long long)kk * dv_rs + h * D + dd] = dV[t][i];
+        // kv_acc: add onto earlier contributions (K/V shared by several applications, K-06)
+        float* pk = dk + (long long)b * dk_bs + (long long)kk * dk_rs + h * D + dd;
+        float* pv = dv + (long long)b * dv_bs + (long long)kk * dv_rs + h * D + dd;
+        *pk = kv_acc ? *pk + dK[t][i] * a.scale : dK[t][i] * a.scale;
+        *pv = kv_acc ? *pv + dV[t][i] : dV[t][i];
       }
     }
 }
@@ -577,7 +580,7 @@ void attn_fwd_launch(const AttnArgs& a, int D, uint16_t* O, float* LSE, float* O
 template <int D, int NW>
 static void bwd_launch_t(const AttnArgs& a, const uint16_t* dO, const float* LSE, float* delta, float* dq,
                          long long dq_bs, int dq_rs, float* dk, long long dk_bs, int dk_rs, float* dv, long long dv_bs,
-                         int dv_rs, hipStream_t st) {
+                         int dv_rs, int kv_acc, hipStream_t st) {
   const int nkb = (a.Nk + 32 * NW - 1) / (32 * NW);
   if (nkb > 1) {  // several key blocks accumulate into dQ
     const long long total = (long long)a.B * a.Nq * a.H * D;
@@ -586,12 +589,12 @@ static void bwd_launch_t(const AttnArgs& a, const uint16_t* dO, const float* LSE
   }
   dim3 grid(nkb, a.H, a.B);
   hipLaunchKernelGGL((attn_bwd_kernel<D, NW>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs, dk,
-                     dk_bs, dk_rs, dv, dv_bs, dv_rs, nkb > 1 ? 1 : 0);
+                     dk_bs, dk_rs, dv, dv_bs, dv_rs, nkb > 1 ? 1 : 0, kv_acc);
 }
 
 void attn_bwd_launch(const AttnArgs& a, int D, const uint16_t* O, const uint16_t* dO, const float* LSE, float* delta,
                      float* dq, long long dq_bs, int dq_rs, float* dk, long long dk_bs, int dk_rs, float* dv,
-                     long long dv_bs, int dv_rs, bool compute_delta, hipStream_t st) {
+                     long long dv_bs, int dv_rs, bool compute_delta, bool kv_acc, hipStream_t st) {
   // delta = rowsum(dO∘O) is normally produced by the post-attention backward kernel;
   // compute it here otherwise.  dQ needs no zero fill from the caller.
   const int rows = a.B * a.Nq;
@@ -599,10 +602,10 @@ void attn_bwd_launch(const AttnArgs& a, int D, const uint16_t* O, const uint16_t
     hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, dO, O, delta, (float*)nullptr,
                        rows, a.H, D, dq_rs);
   switch (D) {  // waves per workgroup: 8 for d ≤ 32, 4 above (keys per block = 32 × waves)
-    case 16: bwd_launch_t<16, 8>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, st); break;
-    case 32: bwd_launch_t<32, 8>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, st); break;
-    case 64: bwd_launch_t<64, 4>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, st); break;
-    case 128: bwd_launch_t<128, 4>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, st); break;
+    case 16: bwd_launch_t<16, 8>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, st); break;
+    case 32: bwd_launch_t<32, 8>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, st); break;
+    case 64: bwd_launch_t<64, 4>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, st); break;
+    case 128: bwd_launch_t<128, 4>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, st); break;
     default: break;
   }
 }

@@ -23,9 +23,10 @@ struct PostAttnGrads { float *dWo, *dbo, *dg2, *dbe2, *dW1, *db1, *dW2, *db2; in
 
 void attn_fwd_launch(const AttnArgs&, int, uint16_t*, float*, float*, float*, int, hipStream_t);
 void attn_bwd_launch(const AttnArgs&, int, const uint16_t*, const uint16_t*, const float*, float*, float*, long long,
-                     int, float*, long long, int, float*, long long, int, bool, hipStream_t);
+                     int, float*, long long, int, float*, long long, int, bool, bool, hipStream_t);
 void ln_linear_fwd_launch(const void*, bool, int, int, int, const float*, const float*, float, const uint16_t*,
-                          const float*, int, int, const float*, int, void*, bool, int, float*, float*, hipStream_t);
+                          const float*, int, int, const float*, int, void*, bool, int, float*, float*, const float*, int,
+                          int, int, hipStream_t);
 void post_attn_fwd_launch(int, const uint16_t*, const float*, const uint16_t*, const float*, const float*,
                           const float*, float, const uint16_t*, const float*, const uint16_t*, const float*, float*,
                           float*, float*, float*, uint16_t*, int, int, hipStream_t);
@@ -34,7 +35,7 @@ void post_attn_bwd_launch(int, const float*, const float*, const float*, const f
                           const float*, float*, uint16_t*, float*, int, const PostAttnGrads&, int, hipStream_t);
 void ln_linear_bwd_launch(const void*, bool, int, int, const uint16_t*, int, const void*, bool, int, const float*,
                           const float*, const float*, const float*, const float*, int, float*, int, float*, float*,
-                          float*, float*, int, int, int, hipStream_t);
+                          float*, float*, int, int, int, const float*, int, int, int, hipStream_t);
 void wgrad_launch(const void*, bool, int, int, const void*, bool, int, int, int, const float*, const float*,
                   const float*, const float*, int, int, float*, float*, hipStream_t);
 void ce_fwd_launch(int, const uint16_t*, const int64_t*, const uint16_t*, const float*, int, int, float*, float*,
@@ -142,7 +143,7 @@ std::vector<Tensor> attn_fwd(Tensor q, Tensor k, Tensor v, OptT kmask, int64_t H
 // skips the delta pass.
 std::vector<Tensor> attn_bwd(Tensor q, Tensor k, Tensor v, OptT kmask, Tensor o, Tensor dO, Tensor lse, OptT delta_in,
                              int64_t H, int64_t D, double scale, double dropout_p, int64_t seed, OptT dq_out,
-                             OptT dk_out, OptT dv_out) {
+                             OptT dk_out, OptT dv_out, bool kv_accumulate) {
   auto a = make_args(q, k, v, kmask, (int)H, (int)D, scale, dropout_p, seed);
   TORCH_CHECK(dO.is_contiguous() && o.is_contiguous(), "O / dO must be contiguous (B, Nq, H*D)");
   auto f32 = q.options().dtype(torch::kFloat32);
@@ -162,17 +163,38 @@ std::vector<Tensor> attn_bwd(Tensor q, Tensor k, Tensor v, OptT kmask, Tensor o,
   }
   pio::attn_bwd_launch(a, (int)D, bfp(o), bfp(dO), f32p(lse), delta.data_ptr<float>(), dq.data_ptr<float>(),
                        dq.stride(0), (int)dq.stride(1), dk.data_ptr<float>(), dk.stride(0), (int)dk.stride(1),
-                       dv.data_ptr<float>(), dv.stride(0), (int)dv.stride(1), !delta_in.has_value(), stream());
+                       dv.data_ptr<float>(), dv.stride(0), (int)dv.stride(1), !delta_in.has_value(), kv_accumulate,
+                       stream());
   return {dq, dk, dv};
 }
 
+// pe (optional, SURVEY K-03): x holds only the npix pixel channels of each row and row r's
+// input is pe[r mod rows(pe)] with the pixels added into its npix leading (zero) columns;
+// pe is (M, pe_rs) fp32 contiguous with pe_rs a multiple of 8, ≥ Kin = w.size(1)
+namespace {
+void pe_args(const OptT& pe, const Tensor& x, int R, int Kin, const float*& pp, int& prs, int& prows, int& npix) {
+  pp = nullptr; prs = 0; prows = 1; npix = 0;
+  if (!pe.has_value()) return;
+  CHECK_DT(*pe, torch::kFloat32);
+  TORCH_CHECK(pe->dim() == 2 && pe->is_contiguous() && pe->size(1) % 8 == 0 && pe->size(1) >= Kin,
+              "pe must be (M, pe_rs) contiguous fp32, pe_rs a multiple of 8 and >= Kin");
+  TORCH_CHECK(R % pe->size(0) == 0, "rows must be a multiple of the PE rows");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(pe->data_ptr()) % 16 == 0, "pe must be 16-byte aligned");
+  pp = pe->data_ptr<float>(); prs = (int)pe->size(1); prows = (int)pe->size(0); npix = (int)x.size(1);
+  TORCH_CHECK(npix <= Kin, "more pixel channels than inputs");
+}
+}  // namespace
+
 std::vector<Tensor> ln_linear_fwd(Tensor x, OptT lnw, OptT lnb, double eps, Tensor w, OptT bias, int64_t act, OptT res,
-                                  bool out_bf16, bool save_stats) {
+                                  bool out_bf16, bool save_stats, OptT pe) {
   CHECK_CUDA(x); CHECK_CUDA(w);
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be 2-D rows");
-  TORCH_CHECK(w.dim() == 2 && w.is_contiguous() && w.size(1) == x.size(1), "w must be (N, Kin) contiguous");
-  const int R = (int)x.size(0), Kin = (int)x.size(1), N = (int)w.size(0);
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous() && (pe.has_value() || w.size(1) == x.size(1)),
+              "w must be (N, Kin) contiguous");
+  const int R = (int)x.size(0), Kin = (int)w.size(1), N = (int)w.size(0);
   TORCH_CHECK(Kin <= 256, "Kin > 256 unsupported");
+  const float* pp; int prs, prows, npix;
+  pe_args(pe, x, R, Kin, pp, prs, prows, npix);
   auto opts = x.options();
   Tensor y = torch::empty({R, N}, opts.dtype(out_bf16 ? torch::kBFloat16 : torch::kFloat32));
   Tensor mean, rstd;
@@ -185,7 +207,8 @@ std::vector<Tensor> ln_linear_fwd(Tensor x, OptT lnw, OptT lnb, double eps, Tens
   const float* rptr = nullptr; int res_rs = 0;
   if (res.has_value()) { rptr = f32p(*res); res_rs = (int)res->stride(0); TORCH_CHECK(res->stride(1) == 1); }
   pio::ln_linear_fwd_launch(x.data_ptr(), is_bf16(x), (int)x.stride(0), R, Kin, f32o(lnw), f32o(lnb), (float)eps, bfp(w),
-                            f32o(bias), N, (int)act, rptr, res_rs, y.data_ptr(), out_bf16, N, mp, rp, stream());
+                            f32o(bias), N, (int)act, rptr, res_rs, y.data_ptr(), out_bf16, N, mp, rp, pp, prs, prows,
+                            npix, stream());
   std::vector<Tensor> out{y};
   if (mp) { out.push_back(mean); out.push_back(rstd); }
   return out;
@@ -264,11 +287,14 @@ std::vector<Tensor> post_attn_bwd(Tensor dz, Tensor y, Tensor m2, Tensor r2, Ten
 // dX = LN_bwd(g·w) (+ dres); accumulates dγ/dβ (dlnw/dlnb, needed when lnw is given) and, when
 // dW is given, dW += gᵀ·LN(x) and db += Σ_rows g.  Returns dX when need_dx.
 OptT ln_linear_bwd(Tensor g, Tensor w, Tensor x, OptT mean, OptT rstd, OptT lnw, OptT lnb, OptT dres, bool need_dx,
-                   OptT dlnw, OptT dlnb, OptT dW, OptT db) {
+                   OptT dlnw, OptT dlnb, OptT dW, OptT db, OptT pe) {
   TORCH_CHECK(g.dim() == 2 && g.stride(1) == 1 && x.dim() == 2 && x.stride(1) == 1, "g / x must be 2-D rows");
   const int R = (int)g.size(0), N = (int)g.size(1), Kin = (int)w.size(1);
   TORCH_CHECK(w.size(0) == N && w.is_contiguous(), "w must be (N, Kin) contiguous, N = g columns");
-  TORCH_CHECK(x.size(0) == R && x.size(1) == Kin, "x must be (R, Kin)");
+  TORCH_CHECK(x.size(0) == R && (pe.has_value() || x.size(1) == Kin), "x must be (R, Kin)");
+  TORCH_CHECK(!(pe.has_value() && need_dx), "no input gradient for a split (pixels + PE) input");
+  const float* pp; int prs, prows, npix;
+  pe_args(pe, x, R, Kin, pp, prs, prows, npix);
   TORCH_CHECK(Kin <= 160, "ln_linear_bwd supports Kin <= 160");
   auto f32 = g.options().dtype(torch::kFloat32);
   Tensor dx;
@@ -288,7 +314,7 @@ OptT ln_linear_bwd(Tensor g, Tensor w, Tensor x, OptT mean, OptT rstd, OptT lnw,
   if (dres.has_value()) { dr = f32p(*dres); drs = (int)dres->stride(0); TORCH_CHECK(dres->stride(1) == 1); }
   pio::ln_linear_bwd_launch(g.data_ptr(), is_bf16(g), (int)g.stride(0), N, bfp(w), Kin, x.data_ptr(), is_bf16(x),
                             (int)x.stride(0), f32o(mean), f32o(rstd), f32o(lnw), f32o(lnb), dr, drs, dxp, Kin, dgp, dbp,
-                            dwp, dbiasp, vrs < 0 ? 0 : vrs, wrs < 0 ? 0 : wrs, R, stream());
+                            dwp, dbiasp, vrs < 0 ? 0 : vrs, wrs < 0 ? 0 : wrs, R, pp, prs, prows, npix, stream());
   if (need_dx) return dx;
   return c10::nullopt;
 }
@@ -436,11 +462,17 @@ void cast_bf16(Tensor x, Tensor y) {
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "Perceiver IO CDNA4 (gfx950) kernels";
   m.def("attn_fwd", &attn_fwd);
-  m.def("attn_bwd", &attn_bwd);
-  m.def("ln_linear_fwd", &ln_linear_fwd);
+  m.def("attn_bwd", &attn_bwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("kmask"), py::arg("o"), py::arg("dO"),
+        py::arg("lse"), py::arg("delta_in"), py::arg("H"), py::arg("D"), py::arg("scale"), py::arg("dropout_p"),
+        py::arg("seed"), py::arg("dq_out"), py::arg("dk_out"), py::arg("dv_out"), py::arg("kv_accumulate") = false);
+  m.def("ln_linear_fwd", &ln_linear_fwd, py::arg("x"), py::arg("lnw"), py::arg("lnb"), py::arg("eps"), py::arg("w"),
+        py::arg("bias"), py::arg("act"), py::arg("res"), py::arg("out_bf16"), py::arg("save_stats"),
+        py::arg("pe") = py::none());
   m.def("post_attn_fwd", &post_attn_fwd);
   m.def("post_attn_bwd", &post_attn_bwd);
-  m.def("ln_linear_bwd", &ln_linear_bwd);
+  m.def("ln_linear_bwd", &ln_linear_bwd, py::arg("g"), py::arg("w"), py::arg("x"), py::arg("mean"), py::arg("rstd"),
+        py::arg("lnw"), py::arg("lnb"), py::arg("dres"), py::arg("need_dx"), py::arg("dlnw"), py::arg("dlnb"),
+        py::arg("dW"), py::arg("db"), py::arg("pe") = py::none());
   m.def("wgrad", &wgrad);
   m.def("mlm_select", &mlm_select);
   m.def("ce_fwd", &ce_fwd);

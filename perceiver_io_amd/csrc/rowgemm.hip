@@ -171,6 +171,36 @@ __device__ __forceinline__ void row_load(float (&v)[NCH][8], const T* __restrict
   }
 }
 
+// Fourier-PE split input (SURVEY K-03): logical row r = pe[r mod M] (row stride pe_rs, a
+// multiple of 8, with npix leading zero columns and zero padding past Kin) + the npix pixel
+// values of row r in those leading columns.  The (B, M, npix + C_pe) concatenation is never
+// materialised; the PE table stays L2/MALL-resident across the batch.
+struct PeSplit {
+  const float* pe;
+  int pe_rs, M, npix;
+};
+
+template <int NCH, typename T>
+__device__ __forceinline__ void row_load_x(float (&v)[NCH][8], const T* __restrict__ X, long long x_rs, int gr, int R,
+                                           int Kin, bool vec, const PeSplit& ps) {
+  if (ps.pe == nullptr) {
+    row_load<NCH>(v, X, x_rs, gr, R, Kin, vec);
+    return;
+  }
+  row_load<NCH>(v, ps.pe, ps.pe_rs, gr < R ? gr % ps.M : 0, gr < R ? ps.M : 0, ps.pe_rs, true);
+  if (gr < R) {
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const int c = rp_col(j);
+      if (c < ps.npix) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (c + e < ps.npix) v[j][e] += ldf(X + (long long)gr * x_rs + c + e);
+      }
+    }
+  }
+}
+
 template <int NCH, typename T>
 __device__ __forceinline__ void row_store(const float (&v)[NCH][8], T* __restrict__ base, long long rs, int gr, int R,
                                           int K, bool vec) {
@@ -326,7 +356,7 @@ __global__ __launch_bounds__(256) void ln_linear_fwd_kernel(const TIn* __restric
                                                             const float* __restrict__ bias, int N, int act,
                                                             const float* __restrict__ res, int res_rs,
                                                             TOut* __restrict__ Y, int y_rs, float* __restrict__ mean_out,
-                                                            float* __restrict__ rstd_out) {
+                                                            float* __restrict__ rstd_out, PeSplit ps) {
   constexpr int KP = 32 * NCH, LD = KP + 8, LDO = 64 + 4;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* sA = smem;                                  // [64][LD]  LN(X), bf16
@@ -337,7 +367,7 @@ __global__ __launch_bounds__(256) void ln_linear_fwd_kernel(const TIn* __restric
   const bool yvec = (N & 7) == 0 && (y_rs & 7) == 0 && aligned16(Y);
 
   float xv[NCH][8];
-  row_load<NCH>(xv, X, x_rs, gr, R, Kin, (Kin & 7) == 0 && (x_rs & 7) == 0 && aligned16(X));
+  row_load_x<NCH>(xv, X, x_rs, gr, R, Kin, (Kin & 7) == 0 && (x_rs & 7) == 0 && aligned16(X), ps);
   bf16x8 wb[NCH];
   tile_fetch<NCH>(wb, W, Kin, 0, N, 64, Kin, KP, wvec);
   if (lnw) {
@@ -779,7 +809,7 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
     int x_rs, const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ lnw,
     const float* __restrict__ lnb, const float* __restrict__ dres, int dres_rs, float* __restrict__ dX, int dx_rs,
     float* __restrict__ dlnw, float* __restrict__ dlnb, float* __restrict__ dW, float* __restrict__ db, int vrs,
-    int wrs, int R) {
+    int wrs, int R, PeSplit ps) {
   constexpr int KP = 32 * NCH, LD = KP + 8, LDG = 64 + 8, LDF = KP + 4;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* sG = smem;                                   // [64][LDG]  G chunk
@@ -795,7 +825,7 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
 
   // ---- phase 0
   float xv[NCH][8], gw[NCH][8];
-  row_load<NCH>(xv, X, x_rs, gr, R, Kin, kvec && (x_rs & 7) == 0 && aligned16(X));
+  row_load_x<NCH>(xv, X, x_rs, gr, R, Kin, kvec && (x_rs & 7) == 0 && aligned16(X), ps);
   float mu = 0.f, rs = 1.f;
   if (lnw) {
     row_load<NCH>(gw, lnw, 0, 0, 1, Kin, kvec && aligned16(lnw));
@@ -977,20 +1007,22 @@ static int pick_nch(int K) {
 template <typename TI, typename TO, int NCH>
 static void ln_linear_fwd_t(const void* X, int x_rs, int R, int Kin, const float* lnw, const float* lnb, float eps,
                             const uint16_t* W, const float* bias, int N, int act, const float* res, int res_rs,
-                            void* Y, int y_rs, float* mean, float* rstd, hipStream_t st) {
+                            void* Y, int y_rs, float* mean, float* rstd, const PeSplit& ps, hipStream_t st) {
   constexpr int KP = 32 * NCH;
   const size_t smem = 2 * 64 * (KP + 8) * sizeof(uint16_t) + 64 * 68 * sizeof(float);
   auto fn = ln_linear_fwd_kernel<TI, TO, NCH>;
   set_smem_once((const void*)fn);
   hipLaunchKernelGGL(fn, dim3((R + 63) / 64), dim3(256), smem, st, (const TI*)X, x_rs, R, Kin, lnw, lnb, eps, W, bias,
-                     N, act, res, res_rs, (TO*)Y, y_rs, mean, rstd);
+                     N, act, res, res_rs, (TO*)Y, y_rs, mean, rstd, ps);
 }
 
 template <typename TI, typename TO>
 static void ln_linear_fwd_n(int nch, const void* X, int x_rs, int R, int Kin, const float* lnw, const float* lnb,
                             float eps, const uint16_t* W, const float* bias, int N, int act, const float* res,
-                            int res_rs, void* Y, int y_rs, float* mean, float* rstd, hipStream_t st) {
-#define LNF(K) ln_linear_fwd_t<TI, TO, K>(X, x_rs, R, Kin, lnw, lnb, eps, W, bias, N, act, res, res_rs, Y, y_rs, mean, rstd, st)
+                            int res_rs, void* Y, int y_rs, float* mean, float* rstd, const PeSplit& ps,
+                            hipStream_t st) {
+#define LNF(K) \
+  ln_linear_fwd_t<TI, TO, K>(X, x_rs, R, Kin, lnw, lnb, eps, W, bias, N, act, res, res_rs, Y, y_rs, mean, rstd, ps, st)
   switch (nch) {
     case 1: LNF(1); break;
     case 2: LNF(2); break;
@@ -1003,10 +1035,12 @@ static void ln_linear_fwd_n(int nch, const void* X, int x_rs, int R, int Kin, co
 
 void ln_linear_fwd_launch(const void* X, bool x_bf16, int x_rs, int R, int Kin, const float* lnw, const float* lnb,
                           float eps, const uint16_t* W, const float* bias, int N, int act, const float* res,
-                          int res_rs, void* Y, bool y_bf16, int y_rs, float* mean, float* rstd, hipStream_t st) {
+                          int res_rs, void* Y, bool y_bf16, int y_rs, float* mean, float* rstd, const float* pe, int pe_rs,
+                          int pe_rows, int npix, hipStream_t st) {
   const int nch = pick_nch(Kin);
+  const PeSplit ps{pe, pe_rs, pe_rows, npix};
 #define LNL(TI, TO) \
-  ln_linear_fwd_n<TI, TO>(nch, X, x_rs, R, Kin, lnw, lnb, eps, W, bias, N, act, res, res_rs, Y, y_rs, mean, rstd, st)
+  ln_linear_fwd_n<TI, TO>(nch, X, x_rs, R, Kin, lnw, lnb, eps, W, bias, N, act, res, res_rs, Y, y_rs, mean, rstd, ps, st)
   if (x_bf16 && y_bf16) LNL(uint16_t, uint16_t);
   else if (x_bf16) LNL(uint16_t, float);
   else if (y_bf16) LNL(float, uint16_t);
@@ -1046,23 +1080,23 @@ template <typename TG, typename TX, int NCH>
 static void ln_linear_bwd_t(const void* G, int g_rs, int N, const uint16_t* W, int Kin, const void* X, int x_rs,
                             const float* mean, const float* rstd, const float* lnw, const float* lnb, const float* dres,
                             int dres_rs, float* dX, int dx_rs, float* dlnw, float* dlnb, float* dW, float* db, int vrs,
-                            int wrs, int R, hipStream_t st) {
+                            int wrs, int R, const PeSplit& ps, hipStream_t st) {
   constexpr int KP = 32 * NCH;
   const size_t smem = 64 * 72 * 2 + 2 * 64 * (KP + 8) * 2 + 64 * (KP + 4) * 4 + 8 * KP * 4 + 4 * 64 * 4;
   auto fn = ln_linear_bwd_kernel<TG, TX, NCH>;
   set_smem_once((const void*)fn);
   hipLaunchKernelGGL(fn, dim3((R + 63) / 64), dim3(256), smem, st, (const TG*)G, g_rs, N, W, Kin, (const TX*)X, x_rs,
-                     mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, dlnw, dlnb, dW, db, vrs, wrs, R);
+                     mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, dlnw, dlnb, dW, db, vrs, wrs, R, ps);
 }
 
 template <typename TG, typename TX>
 static void ln_linear_bwd_n(int nch, const void* G, int g_rs, int N, const uint16_t* W, int Kin, const void* X,
                             int x_rs, const float* mean, const float* rstd, const float* lnw, const float* lnb,
                             const float* dres, int dres_rs, float* dX, int dx_rs, float* dlnw, float* dlnb, float* dW,
-                            float* db, int vrs, int wrs, int R, hipStream_t st) {
+                            float* db, int vrs, int wrs, int R, const PeSplit& ps, hipStream_t st) {
 #define LNB(K)                                                                                                    \
   ln_linear_bwd_t<TG, TX, K>(G, g_rs, N, W, Kin, X, x_rs, mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, dlnw, \
-                             dlnb, dW, db, vrs, wrs, R, st)
+                             dlnb, dW, db, vrs, wrs, R, ps, st)
   switch (nch) {
     case 1: LNB(1); break;
     case 2: LNB(2); break;
@@ -1075,11 +1109,13 @@ static void ln_linear_bwd_n(int nch, const void* G, int g_rs, int N, const uint1
 void ln_linear_bwd_launch(const void* G, bool g_bf16, int g_rs, int N, const uint16_t* W, int Kin, const void* X,
                           bool x_bf16, int x_rs, const float* mean, const float* rstd, const float* lnw,
                           const float* lnb, const float* dres, int dres_rs, float* dX, int dx_rs, float* dlnw,
-                          float* dlnb, float* dW, float* db, int vrs, int wrs, int R, hipStream_t st) {
+                          float* dlnb, float* dW, float* db, int vrs, int wrs, int R, const float* pe, int pe_rs,
+                          int pe_rows, int npix, hipStream_t st) {
   const int nch = pick_nch(Kin);  // Kin ≤ 160 → ≤ 5
+  const PeSplit ps{pe, pe_rs, pe_rows, npix};
 #define LDG(TG, TX)                                                                                           \
   ln_linear_bwd_n<TG, TX>(nch, G, g_rs, N, W, Kin, X, x_rs, mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, \
-                          dlnw, dlnb, dW, db, vrs, wrs, R, st)
+                          dlnw, dlnb, dW, db, vrs, wrs, R, ps, st)
   if (g_bf16 && x_bf16) LDG(uint16_t, uint16_t);
   else if (g_bf16) LDG(uint16_t, float);
   else if (x_bf16) LDG(float, uint16_t);

@@ -92,6 +92,22 @@ class ImageInputAdapter(InputAdapter):
         if tuple(d) != self.image_shape:
             raise ValueError(f"Input image shape {tuple(d)} different from required shape {self.image_shape}")
 
+    def padded_position_encoding(self) -> torch.Tensor:
+        """``(M, round_up(C_img + C_pe, 8))`` fp32: ``C_img`` zero columns, the position encoding,
+        zero padding — the table the fused K/V projection reads instead of the materialised
+        ``[pixels ‖ PE]`` input (SURVEY K-03).  Cached; rebuilt if the buffer changes."""
+        pe = self.position_encoding
+        key = (pe.data_ptr(), pe._version, pe.device)
+        cache = getattr(self, "_pe_pad", None)
+        if cache is not None and cache[0] == key:
+            return cache[1]
+        ci = self.num_image_channels
+        width = (ci + pe.shape[1] + 7) // 8 * 8
+        pad = torch.zeros(pe.shape[0], width, dtype=torch.float32, device=pe.device)
+        pad[:, ci:ci + pe.shape[1]] = pe.float()
+        self._pe_pad = (key, pad)
+        return pad
+
     def forward(self, x):
         self.check_shape(x)
         b = x.shape[0]

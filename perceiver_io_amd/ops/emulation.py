@@ -26,8 +26,19 @@ def _ln(x, w, b, eps):
     return (x - mean[:, None]) * rstd[:, None] * w + b, mean, rstd
 
 
-def ln_linear_fwd(x, lnw, lnb, eps, w, bias, act, res, out_bf16, save_stats):
-    xf = x.float()
+def _split_x(x, pe, kin):
+    """Logical input rows: x itself, or pe[r mod M] (first kin columns) with x's pixel
+    channels added into the leading columns (SURVEY K-03 split input)."""
+    if pe is None:
+        return x.float()
+    r, m = x.shape[0], pe.shape[0]
+    full = pe.repeat(r // m, 1)[:, :kin].clone()
+    full[:, : x.shape[1]] += x.float()
+    return full
+
+
+def ln_linear_fwd(x, lnw, lnb, eps, w, bias, act, res, out_bf16, save_stats, pe=None):
+    xf = _split_x(x, pe, w.shape[1])
     mean = rstd = None
     if lnw is not None:
         xn, mean, rstd = _ln(xf, lnw, lnb, eps)
@@ -90,7 +101,8 @@ def attn_fwd(q, k, v, kmask, H, D, scale, dropout_p, seed, nsplit):
     return o, lse2.permute(0, 2, 1).contiguous()
 
 
-def attn_bwd(q, k, v, kmask, o, dO, lse, delta_in, H, D, scale, dropout_p, seed, dq_out, dk_out, dv_out):
+def attn_bwd(q, k, v, kmask, o, dO, lse, delta_in, H, D, scale, dropout_p, seed, dq_out, dk_out, dv_out,
+             kv_accumulate=False):
     B, qf, kf, vf = _qkv(q, k, v, H, D)
     s = _scores(qf, kf, kmask, scale)
     l2 = lse.permute(0, 2, 1)  # (B, H, Nq)
@@ -109,10 +121,13 @@ def attn_bwd(q, k, v, kmask, o, dO, lse, delta_in, H, D, scale, dropout_p, seed,
         return t.permute(0, 2, 1, 3).reshape(B, t.shape[2], H * D)
 
     res = []
-    for t, out in ((dq, dq_out), (dk, dk_out), (dv, dv_out)):
+    for i, (t, out) in enumerate(((dq, dq_out), (dk, dk_out), (dv, dv_out))):
         t = merge(t)
         if out is not None:
-            out[:, :, : H * D].copy_(t)
+            if kv_accumulate and i > 0:
+                out[:, :, : H * D] += t
+            else:
+                out[:, :, : H * D].copy_(t)
             t = out
         res.append(t)
     return res
@@ -170,12 +185,12 @@ def post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, be2, H, grads):
     return dy, do, delta
 
 
-def ln_linear_bwd(g, w, x, mean, rstd, lnw, lnb, dres, need_dx, dlnw=None, dlnb=None, dW=None, db=None):
+def ln_linear_bwd(g, w, x, mean, rstd, lnw, lnb, dres, need_dx, dlnw=None, dlnb=None, dW=None, db=None, pe=None):
     """Returns dX (or None); LN grads accumulate into dlnw / dlnb and, when given,
     dW += gᵀ·LN(x), db += Σ_rows g."""
     gf = g.float()
     dxn = _bf(gf) @ _bf(w.float())
-    xf = x.float()
+    xf = _split_x(x, pe, w.shape[1])
     if dW is not None:
         xn = (xf - mean[:, None]) * rstd[:, None] * lnw + lnb if lnw is not None else xf
         _acc(dW, _bf(gf).t() @ _bf(xn))

@@ -131,9 +131,43 @@ def _bf16_weights(spec: LayerSpec, ps):
     return wq, wkv, wc.get(rest[1]), wc.get(rest[5]), wc.get(rest[7])
 
 
+class KVSource:
+    """The key/value input of the encoder's cross-attention layers for one forward pass.
+
+    * K-06 (reference ``model.py:186-187`` applies the same ``layer_n`` to the same input
+      ``num_layers - 1`` times): the LayerNorm + K/V projection of a cross layer runs once per
+      forward; later applications reuse the K/V, their dK/dV are accumulated into one buffer
+      (attention backward in accumulate mode) and the projection's backward runs once — in the
+      backward of the first application, which autograd schedules after the later ones (their
+      queries depend on its output).
+    * K-03 (``adapter.py:99-109`` materialises ``[pixels ‖ Fourier PE]``): with ``pe`` given, ``x``
+      holds only the pixels ``(B, M, C_img)`` and the projection kernels add them into the
+      zero leading columns of the padded PE table ``pe`` ``(M, round_up(Kin, 8))``.
+    """
+
+    def __init__(self, x: torch.Tensor, pe: Optional[torch.Tensor] = None, kin: Optional[int] = None):
+        self.x = x
+        self.pe = pe
+        self.kin = kin if kin is not None else x.shape[-1]
+        self.entries = {}
+
+    @property
+    def channels(self) -> int:
+        return self.kin
+
+    def materialize(self) -> torch.Tensor:
+        """The (B, M, Kin) input the unfused path consumes."""
+        if self.pe is None:
+            return self.x
+        b, m = self.x.shape[0], self.x.shape[1]
+        full = self.pe[:, : self.kin].unsqueeze(0).repeat(b, 1, 1)
+        full[:, :, : self.x.shape[2]] += self.x
+        return full
+
+
 class _LayerFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, spec: LayerSpec, bw, seed, p_attn, x_q, x_kv, kmask, *ps):
+    def forward(ctx, spec: LayerSpec, bw, seed, p_attn, src, x_q, x_kv, kmask, *ps):
         K = kernels(x_q)
         C, H = spec.C, spec.heads
         D = C // H
@@ -151,10 +185,21 @@ class _LayerFn(torch.autograd.Function):
         if not xq2.is_contiguous():
             xq2 = xq2.contiguous()
         if spec.cross:
-            B, M, Ckv = x_kv.shape
-            xkv2 = x_kv.reshape(B * M, Ckv)
+            B, M = x_kv.shape[0], x_kv.shape[1]
+            xkv2 = x_kv.reshape(B * M, x_kv.shape[2])
             q, mean_q, rstd_q = K.ln_linear_fwd(xq2, g_q, b_q, EPS, wq, bin_[:C], 0, None, True, True)
-            kv, mean_kv, rstd_kv = K.ln_linear_fwd(xkv2, g_kv, b_kv, EPS, wkv, bin_[C:], 0, None, True, True)
+            key = id(ps[0])
+            ent = src.entries.get(key) if src is not None else None
+            ctx.kv_owner = ent is None
+            if ent is None:  # first application of this layer: project K/V (LN over [pixels ‖ PE] if split)
+                kv, mean_kv, rstd_kv = K.ln_linear_fwd(xkv2, g_kv, b_kv, EPS, wkv, bin_[C:], 0, None, True, True,
+                                                       src.pe if src is not None else None)
+                ent = {"kv": kv, "mean": mean_kv, "rstd": rstd_kv, "dkv": None}
+                if src is not None:
+                    src.entries[key] = ent
+            kv, mean_kv, rstd_kv = ent["kv"], ent["mean"], ent["rstd"]
+            ctx.kv_entry = ent
+            ctx.kv_pe = src.pe if src is not None else None
             q3 = q.view(Bq, Nq, C)
             kv3 = kv.view(B, M, 2 * C)
             k3, v3 = kv3[:, :, :C], kv3[:, :, C:]
@@ -173,7 +218,7 @@ class _LayerFn(torch.autograd.Function):
         z, y, m2, r2, u = K.post_attn_fwd(o2, xq2, wo, bo, g2, be2, EPS, w1, b1, w2, b2)
         ctx.spec, ctx.bw, ctx.seed, ctx.p_attn = spec, bw, seed, p_attn
         ctx.dims = (B, Bq, Nq, C, H, D, scale)
-        ctx.kv_grad = x_kv is not None and ctx.needs_input_grad[5]
+        ctx.kv_grad = x_kv is not None and ctx.needs_input_grad[6]
         ctx.has_mask = kmask is not None
         ctx.save_for_backward(xq2, xkv2 if xkv2 is not None else torch.empty(0), q3 if spec.cross else qkv,
                               kv if kv is not None else torch.empty(0), o, lse, y, m2, r2, u, mean_q, rstd_q,
@@ -236,14 +281,20 @@ class _LayerFn(torch.autograd.Function):
         if spec.cross:
             M = kv.shape[0] // B
             kv3 = kv.view(B, M, 2 * C)
-            dkv = torch.empty((B, M, 2 * C), **f32)
+            ent = ctx.kv_entry
+            # dK/dV of every application of this layer land in one buffer (K-06); the first
+            # writer stores, later ones accumulate
+            acc = ent["dkv"] is not None
+            if not acc:
+                ent["dkv"] = torch.empty((B, M, 2 * C), **f32)
+            dkv = ent["dkv"]
             dq, _, _ = K.attn_bwd(qx, kv3[:, :, :C], kv3[:, :, C:], kmask, o, do.view(B, Nq, C), lse, delta3, H, D,
-                                  scale, ctx.p_attn, ctx.seed, None, dkv[:, :, :C], dkv[:, :, C:])
+                                  scale, ctx.p_attn, ctx.seed, None, dkv[:, :, :C], dkv[:, :, C:], acc)
             dq2, dres = dq.reshape(B * Nq, C), dy
             if Bq == 1 and B > 1:
                 dq2, dres = dq.sum(0), dy.view(B, Nq, C).sum(0)
             gbias = gb(bin_)
-            Ckv = xkv2.shape[1]
+            Ckv = wkv.shape[1]
             if spec.packed:
                 gin = gb(ps[4])
                 gwq, gwkv = rows(gin, 0, C, C), rows(gin, C, 3 * C, C)
@@ -252,14 +303,17 @@ class _LayerFn(torch.autograd.Function):
                 gwkv = torch.zeros((8, 2 * C * Ckv) if rep_mode else (2 * C, Ckv), **f32)
             dx_q = K.ln_linear_bwd(dq2, wq, xq2, mean_q, rstd_q, g_q, b_q, dres, True, gb(g_q), gb(b_q), gwq,
                                    rows(gbias, 0, C, 1))
-            dkv2 = dkv.view(B * M, 2 * C)
-            dx_kv = K.ln_linear_bwd(dkv2, wkv, xkv2, mean_kv, rstd_kv, g_kv, b_kv, None, ctx.kv_grad, gb(g_kv),
-                                    gb(b_kv), gwkv, rows(gbias, C, 3 * C, 1))
-            if not spec.packed:
-                gb(ps[5]).add_(rows(gwkv, 0, C, Ckv))
-                gb(ps[6]).add_(rows(gwkv, C, 2 * C, Ckv))
+            dx_kv = None
+            if ctx.kv_owner:  # the projection's backward, once, over the summed dK/dV
+                dkv2 = dkv.view(B * M, 2 * C)
+                dx_kv = K.ln_linear_bwd(dkv2, wkv, xkv2, mean_kv, rstd_kv, g_kv, b_kv, None, ctx.kv_grad, gb(g_kv),
+                                        gb(b_kv), gwkv, rows(gbias, C, 3 * C, 1), ctx.kv_pe)
+                ent["dkv"] = None
+                if not spec.packed:
+                    gb(ps[5]).add_(rows(gwkv, 0, C, Ckv))
+                    gb(ps[6]).add_(rows(gwkv, C, 2 * C, Ckv))
             dx_q = dx_q.view(Bq, Nq, C)
-            dx_kv = dx_kv.view(B, M, -1) if ctx.kv_grad else None
+            dx_kv = dx_kv.view(B, M, -1) if (ctx.kv_grad and dx_kv is not None) else None
         else:
             qkv3 = qx.view(B, Nq, 3 * C)
             dqkv = torch.empty((B, Nq, 3 * C), **f32)  # every column block is written by attn_bwd
@@ -271,7 +325,7 @@ class _LayerFn(torch.autograd.Function):
             dx_q = dx_q.view(B, Nq, C)
             dx_kv = None
         # parameter gradients were accumulated in place (no autograd AccumulateGrad pass)
-        return (None, None, None, None, dx_q, dx_kv, None) + (None,) * len(ps)
+        return (None, None, None, None, None, dx_q, dx_kv, None) + (None,) * len(ps)
 
 
 def _seed(spec: LayerSpec, training: bool) -> int:
@@ -280,7 +334,7 @@ def _seed(spec: LayerSpec, training: bool) -> int:
     return 0
 
 
-def _run_layer(layer, x_q, x_kv=None, pad_mask=None):
+def _run_layer(layer, x_q, x_kv=None, pad_mask=None, src: Optional[KVSource] = None):
     spec, ps = layer_spec_and_params(layer)
     if spec.dropout > 0.0 and layer.training:
         raise NotImplementedError("fused path: dropout > 0 handled by the eager path")
@@ -291,7 +345,7 @@ def _run_layer(layer, x_q, x_kv=None, pad_mask=None):
         x_q = x_q.float()
     if x_kv is not None and x_kv.dtype != torch.float32:
         x_kv = x_kv.float()
-    return _LayerFn.apply(spec, bw, _seed(spec, layer.training), p_attn, x_q, x_kv, kmask, *ps)
+    return _LayerFn.apply(spec, bw, _seed(spec, layer.training), p_attn, src, x_q, x_kv, kmask, *ps)
 
 
 def _fusable(layer, x=None) -> bool:
@@ -301,7 +355,8 @@ def _fusable(layer, x=None) -> bool:
 
 
 def can_fuse(layer, x_kv=None) -> bool:
-    return _fusable(layer) and (x_kv is None or x_kv.shape[-1] <= 160)
+    ch = x_kv.channels if isinstance(x_kv, KVSource) else (x_kv.shape[-1] if x_kv is not None else 0)
+    return _fusable(layer) and ch <= 160
 
 
 def self_attention_layer(layer, x):
@@ -311,11 +366,15 @@ def self_attention_layer(layer, x):
 
 
 def cross_attention_layer(layer, x_q, x_kv, pad_mask=None):
+    """``x_kv`` is a tensor or a :class:`KVSource` (shared K/V projection, split PE input)."""
+    src = x_kv if isinstance(x_kv, KVSource) else None
     if not can_fuse(layer, x_kv):
+        if src is not None:
+            x_kv = src.materialize()
         return layer.eager_forward(x_q, x_kv, pad_mask)
     if x_q.dim() == 3 and x_q.shape[0] > 1 and x_q.stride(0) == 0:
         x_q = x_q[:1]  # batch-broadcast queries (decoder output array): project once
-    return _run_layer(layer, x_q, x_kv, pad_mask)
+    return _run_layer(layer, x_q, src.x if src is not None else x_kv, pad_mask, src)
 
 
 # ------------------------------------------------------------------------------------------
@@ -353,20 +412,24 @@ def text_embed(adapter, ids):
 # encoder
 # ------------------------------------------------------------------------------------------
 def encoder_forward(encoder, x, pad_mask=None):
-    from ..models.adapters import TextInputAdapter
+    from ..models.adapters import ImageInputAdapter, TextInputAdapter
 
     ad = encoder.input_adapter
     if isinstance(ad, TextInputAdapter):
-        xin = text_embed(ad, x)
+        src = KVSource(text_embed(ad, x))
+    elif isinstance(ad, ImageInputAdapter) and not x.requires_grad:
+        ad.check_shape(x)
+        pix = x.reshape(x.shape[0], -1, ad.num_image_channels).float().contiguous()
+        src = KVSource(pix, pe=ad.padded_position_encoding(), kin=ad.num_input_channels)
     else:
-        xin = ad(x)
+        src = KVSource(ad(x))
     lat = encoder.latent.unsqueeze(0)  # (1, N, C): projected once, broadcast inside the kernels
-    b = xin.shape[0]
+    b = src.x.shape[0]
     for layer in encoder.layers():
         cross, block = layer[0], layer[1]
-        if lat.shape[0] == 1 and not can_fuse(cross, xin):
+        if lat.shape[0] == 1 and not can_fuse(cross, src):
             lat = lat.expand(b, -1, -1)
-        lat = cross_attention_layer(cross, lat, xin, pad_mask)
+        lat = cross_attention_layer(cross, lat, src, pad_mask)
         if lat.shape[0] == 1 and b > 1:
             lat = lat.expand(b, -1, -1)
         for sa in block:

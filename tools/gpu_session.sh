@@ -38,6 +38,8 @@ for step in "$@"; do
     configs_ref) for c in mlm256 seq_clf imagenet long_mlm mnist; do
                 run "cfgref_${c}" 900 python bench.py --config $c --backend reference --steps 5 --warmup 2
               done ;;
+    prof_img) run prof_img 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_img -o run --output-format csv -- python bench.py --config imagenet --steps 3 --warmup 2 ;;
+    prof_mnist) run prof_mnist 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_mnist -o run --output-format csv -- python bench.py --config mnist --steps 3 --warmup 2 ;;
     prof)     run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 3 ;;
     dbg0)     run dbg0 300 env AMD_SERIALIZE_KERNEL=3 python tools/debug_engine.py 0 ;;
     dbg1)     run dbg1 300 python tools/debug_engine.py 1 ;;
