@@ -24,7 +24,7 @@ struct PostAttnGrads { float *dWo, *dbo, *dg2, *dbe2, *dW1, *db1, *dW2, *db2; in
 void attn_fwd_launch(const AttnArgs&, int, uint16_t*, float*, float*, float*, int, hipStream_t);
 void attn_bwd_launch(const AttnArgs&, int, const uint16_t*, const uint16_t*, const float*, float*, float*, long long,
                      int, float*, long long, int, float*, long long, int, bool, bool, hipStream_t);
-void ln_linear_fwd_launch(const void*, bool, int, int, int, const float*, const float*, float, const uint16_t*,
+void ln_linear_fwd_launch(const void*, bool, int, int, int, const float*, const float*, float, const uint16_t*, int,
                           const float*, int, int, const float*, int, void*, bool, int, float*, float*, const float*, int,
                           int, int, hipStream_t);
 void post_attn_fwd_launch(int, const uint16_t*, const float*, const uint16_t*, const float*, const float*,
@@ -33,11 +33,12 @@ void post_attn_fwd_launch(int, const uint16_t*, const float*, const uint16_t*, c
 void post_attn_bwd_launch(int, const float*, const float*, const float*, const float*, const uint16_t*,
                           const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*, const float*,
                           const float*, float*, uint16_t*, float*, int, const PostAttnGrads&, int, hipStream_t);
-void ln_linear_bwd_launch(const void*, bool, int, int, const uint16_t*, int, const void*, bool, int, const float*,
+void ln_linear_bwd_launch(const void*, bool, int, int, const uint16_t*, int, int, const void*, bool, int, const float*,
                           const float*, const float*, const float*, const float*, int, float*, int, float*, float*,
                           float*, float*, int, int, int, const float*, int, int, int, hipStream_t);
 void wgrad_launch(const void*, bool, int, int, const void*, bool, int, int, int, const float*, const float*,
-                  const float*, const float*, int, int, float*, float*, hipStream_t);
+                  const float*, const float*, int, int, float*, float*, int, int, const float*, int, int, int,
+                  hipStream_t);
 void ce_fwd_launch(int, const uint16_t*, const int64_t*, const uint16_t*, const float*, int, int, float*, float*,
                    float*, float*, int, hipStream_t);
 int ce_num_splits(int, int);
@@ -185,13 +186,15 @@ void pe_args(const OptT& pe, const Tensor& x, int R, int Kin, const float*& pp, 
 }
 }  // namespace
 
+// kin (optional): the logical input width when w's rows are zero padded past it (w (N, ≥ kin))
 std::vector<Tensor> ln_linear_fwd(Tensor x, OptT lnw, OptT lnb, double eps, Tensor w, OptT bias, int64_t act, OptT res,
-                                  bool out_bf16, bool save_stats, OptT pe) {
+                                  bool out_bf16, bool save_stats, OptT pe, int64_t kin) {
   CHECK_CUDA(x); CHECK_CUDA(w);
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be 2-D rows");
-  TORCH_CHECK(w.dim() == 2 && w.is_contiguous() && (pe.has_value() || w.size(1) == x.size(1)),
-              "w must be (N, Kin) contiguous");
-  const int R = (int)x.size(0), Kin = (int)w.size(1), N = (int)w.size(0);
+  const int R = (int)x.size(0), N = (int)w.size(0);
+  const int Kin = kin >= 0 ? (int)kin : (int)w.size(1);
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous() && w.size(1) >= Kin, "w must be (N, >= Kin) contiguous");
+  TORCH_CHECK(pe.has_value() || x.size(1) == Kin, "x must be (R, Kin)");
   TORCH_CHECK(Kin <= 256, "Kin > 256 unsupported");
   const float* pp; int prs, prows, npix;
   pe_args(pe, x, R, Kin, pp, prs, prows, npix);
@@ -207,7 +210,7 @@ std::vector<Tensor> ln_linear_fwd(Tensor x, OptT lnw, OptT lnb, double eps, Tens
   const float* rptr = nullptr; int res_rs = 0;
   if (res.has_value()) { rptr = f32p(*res); res_rs = (int)res->stride(0); TORCH_CHECK(res->stride(1) == 1); }
   pio::ln_linear_fwd_launch(x.data_ptr(), is_bf16(x), (int)x.stride(0), R, Kin, f32o(lnw), f32o(lnb), (float)eps, bfp(w),
-                            f32o(bias), N, (int)act, rptr, res_rs, y.data_ptr(), out_bf16, N, mp, rp, pp, prs, prows,
+                            (int)w.size(1), f32o(bias), N, (int)act, rptr, res_rs, y.data_ptr(), out_bf16, N, mp, rp, pp, prs, prows,
                             npix, stream());
   std::vector<Tensor> out{y};
   if (mp) { out.push_back(mean); out.push_back(rstd); }
@@ -286,11 +289,14 @@ std::vector<Tensor> post_attn_bwd(Tensor dz, Tensor y, Tensor m2, Tensor r2, Ten
 
 // dX = LN_bwd(g·w) (+ dres); accumulates dγ/dβ (dlnw/dlnb, needed when lnw is given) and, when
 // dW is given, dW += gᵀ·LN(x) and db += Σ_rows g.  Returns dX when need_dx.
+constexpr int kTallRows = 1 << 17;
+
 OptT ln_linear_bwd(Tensor g, Tensor w, Tensor x, OptT mean, OptT rstd, OptT lnw, OptT lnb, OptT dres, bool need_dx,
-                   OptT dlnw, OptT dlnb, OptT dW, OptT db, OptT pe) {
+                   OptT dlnw, OptT dlnb, OptT dW, OptT db, OptT pe, int64_t kin) {
   TORCH_CHECK(g.dim() == 2 && g.stride(1) == 1 && x.dim() == 2 && x.stride(1) == 1, "g / x must be 2-D rows");
-  const int R = (int)g.size(0), N = (int)g.size(1), Kin = (int)w.size(1);
-  TORCH_CHECK(w.size(0) == N && w.is_contiguous(), "w must be (N, Kin) contiguous, N = g columns");
+  const int R = (int)g.size(0), N = (int)g.size(1);
+  const int Kin = kin >= 0 ? (int)kin : (int)w.size(1);
+  TORCH_CHECK(w.size(0) == N && w.is_contiguous() && w.size(1) >= Kin, "w must be (N, >= Kin) contiguous, N = g columns");
   TORCH_CHECK(x.size(0) == R && (pe.has_value() || x.size(1) == Kin), "x must be (R, Kin)");
   TORCH_CHECK(!(pe.has_value() && need_dx), "no input gradient for a split (pixels + PE) input");
   const float* pp; int prs, prows, npix;
@@ -312,25 +318,40 @@ OptT ln_linear_bwd(Tensor g, Tensor w, Tensor x, OptT mean, OptT rstd, OptT lnw,
   if (db.has_value()) { TORCH_CHECK(dW.has_value(), "db needs dW"); dbiasp = vec_target(*db, N, "db", vrs); }
   const float* dr = nullptr; int drs = 0;
   if (dres.has_value()) { dr = f32p(*dres); drs = (int)dres->stride(0); TORCH_CHECK(dres->stride(1) == 1); }
-  pio::ln_linear_bwd_launch(g.data_ptr(), is_bf16(g), (int)g.stride(0), N, bfp(w), Kin, x.data_ptr(), is_bf16(x),
-                            (int)x.stride(0), f32o(mean), f32o(rstd), f32o(lnw), f32o(lnb), dr, drs, dxp, Kin, dgp, dbp,
-                            dwp, dbiasp, vrs < 0 ? 0 : vrs, wrs < 0 ? 0 : wrs, R, pp, prs, prows, npix, stream());
+  // very tall inputs (image K/V projections): the weight gradient leaves the row-tile kernel
+  // for the streaming tall-wgrad kernel (one partial per ~R/128 rows instead of per 64)
+  const bool tall = dwp != nullptr && R >= kTallRows;
+  pio::ln_linear_bwd_launch(g.data_ptr(), is_bf16(g), (int)g.stride(0), N, bfp(w), (int)w.size(1), Kin, x.data_ptr(),
+                            is_bf16(x), (int)x.stride(0), f32o(mean), f32o(rstd), f32o(lnw), f32o(lnb), dr, drs, dxp,
+                            Kin, dgp, dbp, tall ? nullptr : dwp, tall ? nullptr : dbiasp, vrs < 0 ? 0 : vrs,
+                            wrs < 0 ? 0 : wrs, R, pp, prs, prows, npix, stream());
+  if (tall)
+    pio::wgrad_launch(g.data_ptr(), is_bf16(g), (int)g.stride(0), N, x.data_ptr(), is_bf16(x), (int)x.stride(0), Kin,
+                      lnw.has_value() ? 1 : 0, f32o(mean), f32o(rstd), f32o(lnw), f32o(lnb), R, 0, dwp, dbiasp,
+                      vrs < 0 ? 0 : vrs, wrs < 0 ? 0 : wrs, pp, prs, prows, npix, stream());
   if (need_dx) return dx;
   return c10::nullopt;
 }
 
+// dW (+)= gᵀ·A', db (+)= Σ rows g  (A' = a | LN(a) | GELU(a); a may be pixels with a PE table)
 void wgrad(Tensor g, Tensor a, int64_t amode, OptT mean, OptT rstd, OptT lnw, OptT lnb, int64_t rows_per_wg, Tensor dW,
-           OptT db) {
+           OptT db, OptT pe, int64_t kin) {
   TORCH_CHECK(g.dim() == 2 && a.dim() == 2 && g.stride(1) == 1 && a.stride(1) == 1, "2-D row tensors expected");
-  const int R = (int)g.size(0), N = (int)g.size(1), Kin = (int)a.size(1);
+  const int R = (int)g.size(0), N = (int)g.size(1);
+  const int Kin = kin >= 0 ? (int)kin : (int)a.size(1);
   TORCH_CHECK(a.size(0) == R, "row mismatch");
+  TORCH_CHECK(pe.has_value() || a.size(1) == Kin, "a must be (R, Kin)");
   TORCH_CHECK(Kin <= 160, "wgrad supports Kin <= 160");
   TORCH_CHECK(amode != 1 || (mean.has_value() && rstd.has_value() && lnw.has_value() && lnb.has_value()),
               "LN mode needs stats and affine");
-  float* dwp = grad_target(dW, (int64_t)N * Kin, "dW");
-  float* dbp = db.has_value() ? grad_target(*db, N, "db") : nullptr;
+  const float* pp; int prs, prows, npix;
+  pe_args(pe, a, R, Kin, pp, prs, prows, npix);
+  int wrs = -1, vrs = -1;
+  float* dwp = vec_target(dW, (int64_t)N * Kin, "dW", wrs);
+  float* dbp = db.has_value() ? vec_target(*db, N, "db", vrs) : nullptr;
   pio::wgrad_launch(g.data_ptr(), is_bf16(g), (int)g.stride(0), N, a.data_ptr(), is_bf16(a), (int)a.stride(0), Kin,
-                    (int)amode, f32o(mean), f32o(rstd), f32o(lnw), f32o(lnb), R, (int)rows_per_wg, dwp, dbp, stream());
+                    (int)amode, f32o(mean), f32o(rstd), f32o(lnw), f32o(lnb), R, (int)rows_per_wg, dwp, dbp,
+                    vrs < 0 ? 0 : vrs, wrs < 0 ? 0 : wrs, pp, prs, prows, npix, stream());
 }
 
 // labels (B, L) → [idx_b (B, cap), labels_b (B, cap), gidx (gcap), glabels (gcap), total (1) fp32,
@@ -467,13 +488,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("seed"), py::arg("dq_out"), py::arg("dk_out"), py::arg("dv_out"), py::arg("kv_accumulate") = false);
   m.def("ln_linear_fwd", &ln_linear_fwd, py::arg("x"), py::arg("lnw"), py::arg("lnb"), py::arg("eps"), py::arg("w"),
         py::arg("bias"), py::arg("act"), py::arg("res"), py::arg("out_bf16"), py::arg("save_stats"),
-        py::arg("pe") = py::none());
+        py::arg("pe") = py::none(), py::arg("kin") = -1);
   m.def("post_attn_fwd", &post_attn_fwd);
   m.def("post_attn_bwd", &post_attn_bwd);
   m.def("ln_linear_bwd", &ln_linear_bwd, py::arg("g"), py::arg("w"), py::arg("x"), py::arg("mean"), py::arg("rstd"),
         py::arg("lnw"), py::arg("lnb"), py::arg("dres"), py::arg("need_dx"), py::arg("dlnw"), py::arg("dlnb"),
-        py::arg("dW"), py::arg("db"), py::arg("pe") = py::none());
-  m.def("wgrad", &wgrad);
+        py::arg("dW"), py::arg("db"), py::arg("pe") = py::none(), py::arg("kin") = -1);
+  m.def("wgrad", &wgrad, py::arg("g"), py::arg("a"), py::arg("amode"), py::arg("mean"), py::arg("rstd"), py::arg("lnw"),
+        py::arg("lnb"), py::arg("rows_per_wg"), py::arg("dW"), py::arg("db"), py::arg("pe") = py::none(),
+        py::arg("kin") = -1);
   m.def("mlm_select", &mlm_select);
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);

@@ -352,7 +352,7 @@ __device__ __forceinline__ void g_store(const float (&v)[2][8], uint16_t* sG, in
 template <typename TIn, typename TOut, int NCH>
 __global__ __launch_bounds__(256) void ln_linear_fwd_kernel(const TIn* __restrict__ X, int x_rs, int R, int Kin,
                                                             const float* __restrict__ lnw, const float* __restrict__ lnb,
-                                                            float eps, const uint16_t* __restrict__ W,
+                                                            float eps, const uint16_t* __restrict__ W, int w_rs,
                                                             const float* __restrict__ bias, int N, int act,
                                                             const float* __restrict__ res, int res_rs,
                                                             TOut* __restrict__ Y, int y_rs, float* __restrict__ mean_out,
@@ -363,13 +363,15 @@ __global__ __launch_bounds__(256) void ln_linear_fwd_kernel(const TIn* __restric
   uint16_t* sW = sA + 64 * LD;                          // [64][LD]  W chunk
   float* sO = reinterpret_cast<float*>(sW + 64 * LD);   // [64][LDO] output chunk
   const int m0 = blockIdx.x * 64, gr = m0 + rp_row(), w = wave_id(), l = lane_id();
-  const bool wvec = (Kin & 7) == 0 && aligned16(W);
+  // W rows are w_rs apart (≥ Kin, zero padded): a multiple of 8 keeps the staging vectorised
+  const bool wvec = (w_rs & 7) == 0 && aligned16(W);
+  const int wk = w_rs > Kin ? w_rs : Kin;
   const bool yvec = (N & 7) == 0 && (y_rs & 7) == 0 && aligned16(Y);
 
   float xv[NCH][8];
   row_load_x<NCH>(xv, X, x_rs, gr, R, Kin, (Kin & 7) == 0 && (x_rs & 7) == 0 && aligned16(X), ps);
   bf16x8 wb[NCH];
-  tile_fetch<NCH>(wb, W, Kin, 0, N, 64, Kin, KP, wvec);
+  tile_fetch<NCH>(wb, W, w_rs, 0, N, 64, wk, KP, wvec);
   if (lnw) {
     float gw[NCH][8], gb[NCH][8];
     const bool pvec = (Kin & 7) == 0 && aligned16(lnw) && aligned16(lnb);
@@ -401,7 +403,7 @@ __global__ __launch_bounds__(256) void ln_linear_fwd_kernel(const TIn* __restric
   for (int n0 = 0; n0 < N; n0 += 64) {
     tile_store<NCH>(wb, sW, LD, 64, KP);
     __syncthreads();
-    if (n0 + 64 < N) tile_fetch<NCH>(wb, W, Kin, n0 + 64, N, 64, Kin, KP, wvec);
+    if (n0 + 64 < N) tile_fetch<NCH>(wb, W, w_rs, n0 + 64, N, 64, wk, KP, wvec);
     const int bc = n0 + 32 * (w & 1) + (l & 31);
     const float bv = (bias && bc < N) ? bias[bc] : 0.f;
     f32x16 acc[1] = {f32x16{}};
@@ -805,7 +807,8 @@ __global__ __launch_bounds__(256) void post_attn_bwd_kernel(
 // ------------------------------------------------------------------------------------
 template <typename TG, typename TX, int NCH>
 __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
-    const TG* __restrict__ G, int g_rs, int N, const uint16_t* __restrict__ W, int Kin, const TX* __restrict__ X,
+    const TG* __restrict__ G, int g_rs, int N, const uint16_t* __restrict__ W, int w_rs, int Kin,
+    const TX* __restrict__ X,
     int x_rs, const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ lnw,
     const float* __restrict__ lnb, const float* __restrict__ dres, int dres_rs, float* __restrict__ dX, int dx_rs,
     float* __restrict__ dlnw, float* __restrict__ dlnb, float* __restrict__ dW, float* __restrict__ db, int vrs,
@@ -820,7 +823,8 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
   float* sPb = sPart + 8 * KP;                           // [4][64]
   const int m0 = blockIdx.x * 64, gr = m0 + rp_row(), w = wave_id(), l = lane_id();
   const bool gvec = (N & 7) == 0 && (g_rs & 7) == 0 && aligned16(G);
-  const bool wvec = (Kin & 7) == 0 && aligned16(W);
+  const bool wvec = (w_rs & 7) == 0 && aligned16(W);
+  const int wk = w_rs > Kin ? w_rs : Kin;  // W rows zero padded to w_rs
   const bool kvec = (Kin & 7) == 0;
 
   // ---- phase 0
@@ -834,7 +838,7 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
   float gv[2][8];
   g_fetch<TG>(gv, G, g_rs, m0, R, 0, N, gvec);
   bf16x8 wb[NCH];
-  tile_fetch<NCH>(wb, W, Kin, 0, N, 64, Kin, KP, wvec);
+  tile_fetch<NCH>(wb, W, w_rs, 0, N, 64, wk, KP, wvec);
   if (dW) {  // LN(X), the forward GEMM's A operand, for the weight gradient
     float xn[NCH][8];
     if (lnw) {
@@ -865,7 +869,7 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
     __syncthreads();
     if (nc + 64 < N) {
       g_fetch<TG>(gv, G, g_rs, m0, R, nc + 64, N, gvec);
-      tile_fetch<NCH>(wb, W, Kin, nc + 64, N, 64, Kin, KP, wvec);
+      tile_fetch<NCH>(wb, W, w_rs, nc + 64, N, 64, wk, KP, wvec);
     }
     tile_gemm<MAXT, true, false>(sG, LDG, sW, LD, 64, KP, 64, acc);
     if (dW) {
@@ -945,41 +949,85 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
 }
 
 // ------------------------------------------------------------------------------------
-// standalone weight gradient (for projections without a fused backward producer):
-// dW[n][k] += Σ_rows G[r][n] · A'[r][k], db[n] += Σ_rows G[r][n], A' = A | LN(A) | GELU(A)
-// grid (N/64, row splits); partials flushed with atomics
+// tall weight gradient: dW[n][k] += Σ_rows G[r][n] · A'[r][k], db[n] += Σ_rows G[r][n]
+// A' = A | LN(A) | GELU(A) recomputed on load (A may be a Fourier-PE split input).
+// grid (N / 64, row splits); each workgroup streams its row range in 64-row tiles with the
+// next tile register-prefetched, accumulates in MFMA registers and adds its partial once —
+// the form for row counts (≥ 10⁵: image K/V projections) where per-tile atomics would cost
+// more than the GEMM.
 // ------------------------------------------------------------------------------------
-template <typename TG, typename TA>
+template <typename TG, typename TA, int NCH>
 __global__ __launch_bounds__(256) void wgrad_kernel(const TG* __restrict__ G, int g_rs, int N, const TA* __restrict__ A,
                                                     int a_rs, int Kin, int amode, const float* __restrict__ mean,
                                                     const float* __restrict__ rstd, const float* __restrict__ lnw,
                                                     const float* __restrict__ lnb, int R, int rows_per_split,
-                                                    float* __restrict__ dW, float* __restrict__ db) {
+                                                    float* __restrict__ dW, float* __restrict__ db, int vrs, int wrs,
+                                                    PeSplit ps) {
+  constexpr int KP = 32 * NCH, LDA = KP + 8, LDG = 64 + 8, MAXT = 3;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  const int KP = round_up(Kin, 32), lda = KP + 8, ldg = 64 + 8;
-  uint16_t* sG = smem;           // [64 rows][64 n]
-  uint16_t* sA = sG + 64 * ldg;  // [64 rows][KP]
-  const int n0 = blockIdx.x * 64, s = blockIdx.y;
+  uint16_t* sG = smem;                                // [64 rows][64 n]
+  uint16_t* sA = sG + 64 * LDG;                       // [64 rows][KP]
+  float* sAff = reinterpret_cast<float*>(sA + 64 * LDA);  // [2][KP] LN affine
+  float* sPb = sAff + 2 * KP;                         // [4][64] bias partials
+  const int n0 = blockIdx.x * 64, s = blockIdx.y, l = lane_id(), w = wave_id();
   const int r_begin = s * rows_per_split, r_end = min(R, r_begin + rows_per_split);
-  constexpr int MAXT = 3;
+  const bool gvec = (N & 7) == 0 && (g_rs & 7) == 0 && aligned16(G);
+  const bool avec = (Kin & 7) == 0 && (a_rs & 7) == 0 && aligned16(A);
+  for (int k = threadIdx.x; k < KP; k += blockDim.x) {
+    sAff[k] = (amode == 1 && k < Kin) ? lnw[k] : 0.f;
+    sAff[KP + k] = (amode == 1 && k < Kin) ? lnb[k] : 0.f;
+  }
   f32x16 acc[MAXT];
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
-  float bsum = 0.f;  // thread n = threadIdx.x (< 64)
+  float cs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) cs[e] = 0.f;
+  float gv[2][8], av[NCH][8], mu = 0.f, rs = 1.f;
+  auto fetch = [&](int r0) {
+    g_fetch<TG>(gv, G, g_rs, r0, r_end, n0, N, gvec);
+    const int gr = r0 + rp_row();
+    row_load_x<NCH>(av, A, a_rs, gr, r_end, Kin, avec, ps);
+    if (amode == 1 && gr < r_end) { mu = mean[gr]; rs = rstd[gr]; }
+  };
+  if (r_begin < r_end) fetch(r_begin);
   for (int r0 = r_begin; r0 < r_end; r0 += 64) {
+    __syncthreads();  // previous tile's MFMAs done with sG / sA
+    g_store(gv, sG, LDG);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cs[e] += gv[0][e] + gv[1][e];
+#pragma unroll
+    for (int j = 0; j < NCH; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = rp_col(j) + e;
+        float v = av[j][e];
+        if (amode == 1) v = c < Kin ? (v - mu) * rs * sAff[c] + sAff[KP + c] : 0.f;
+        else if (amode == 2) v = gelu_f(v);
+        av[j][e] = v;
+      }
+    lds_row_write_bf16<NCH>(sA, LDA, av);
     __syncthreads();
-    stage(sG, ldg, G, g_rs, r0, r_end, n0, N, 64, 64);
-    stage_act(sA, lda, A, a_rs, r0, r_end, Kin, KP, amode, mean, rstd, lnw, lnb);
-    __syncthreads();
-    if (threadIdx.x < 64 && n0 + threadIdx.x < N)
-      for (int rr = r0; rr < min(r_end, r0 + 64); ++rr) bsum += ldf(G + (long long)rr * g_rs + n0 + threadIdx.x);
-    tile_gemm<MAXT, false, false>(sG, ldg, sA, lda, 64, KP, 64, acc);
+    if (r0 + 64 < r_end) fetch(r0 + 64);
+    tile_gemm<MAXT, false, false>(sG, LDG, sA, LDA, 64, KP, 64, acc);
   }
+  float* dWr = rep(dW, wrs);
   for_acc<MAXT>(64, KP, [&](int t, int m, int n, int i) {
     const int gn = n0 + m;
-    if (gn < N && n < Kin) atomicAdd(dW + (long long)gn * Kin + n, acc[t][i]);
+    if (gn < N && n < Kin) atomicAdd(dWr + (long long)gn * Kin + n, acc[t][i]);
   });
-  if (db && threadIdx.x < 64 && n0 + threadIdx.x < N) atomicAdd(db + n0 + threadIdx.x, bsum);
+  if (db) {  // column sums: lanes ≡ l (mod 8) share a column group
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float v = xor32_sum(xor16_sum(cs[e] + dpp<0x128>(cs[e])));
+      if (l < 8) sPb[w * 64 + 8 * l + e] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64 && n0 + (int)threadIdx.x < N) {
+      const int t = threadIdx.x;
+      atomicAdd(rep(db, vrs) + n0 + t, sPb[t] + sPb[64 + t] + sPb[128 + t] + sPb[192 + t]);
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -1006,23 +1054,23 @@ static int pick_nch(int K) {
 
 template <typename TI, typename TO, int NCH>
 static void ln_linear_fwd_t(const void* X, int x_rs, int R, int Kin, const float* lnw, const float* lnb, float eps,
-                            const uint16_t* W, const float* bias, int N, int act, const float* res, int res_rs,
+                            const uint16_t* W, int w_rs, const float* bias, int N, int act, const float* res, int res_rs,
                             void* Y, int y_rs, float* mean, float* rstd, const PeSplit& ps, hipStream_t st) {
   constexpr int KP = 32 * NCH;
   const size_t smem = 2 * 64 * (KP + 8) * sizeof(uint16_t) + 64 * 68 * sizeof(float);
   auto fn = ln_linear_fwd_kernel<TI, TO, NCH>;
   set_smem_once((const void*)fn);
-  hipLaunchKernelGGL(fn, dim3((R + 63) / 64), dim3(256), smem, st, (const TI*)X, x_rs, R, Kin, lnw, lnb, eps, W, bias,
+  hipLaunchKernelGGL(fn, dim3((R + 63) / 64), dim3(256), smem, st, (const TI*)X, x_rs, R, Kin, lnw, lnb, eps, W, w_rs, bias,
                      N, act, res, res_rs, (TO*)Y, y_rs, mean, rstd, ps);
 }
 
 template <typename TI, typename TO>
 static void ln_linear_fwd_n(int nch, const void* X, int x_rs, int R, int Kin, const float* lnw, const float* lnb,
-                            float eps, const uint16_t* W, const float* bias, int N, int act, const float* res,
+                            float eps, const uint16_t* W, int w_rs, const float* bias, int N, int act, const float* res,
                             int res_rs, void* Y, int y_rs, float* mean, float* rstd, const PeSplit& ps,
                             hipStream_t st) {
 #define LNF(K) \
-  ln_linear_fwd_t<TI, TO, K>(X, x_rs, R, Kin, lnw, lnb, eps, W, bias, N, act, res, res_rs, Y, y_rs, mean, rstd, ps, st)
+  ln_linear_fwd_t<TI, TO, K>(X, x_rs, R, Kin, lnw, lnb, eps, W, w_rs, bias, N, act, res, res_rs, Y, y_rs, mean, rstd, ps, st)
   switch (nch) {
     case 1: LNF(1); break;
     case 2: LNF(2); break;
@@ -1034,13 +1082,13 @@ static void ln_linear_fwd_n(int nch, const void* X, int x_rs, int R, int Kin, co
 }
 
 void ln_linear_fwd_launch(const void* X, bool x_bf16, int x_rs, int R, int Kin, const float* lnw, const float* lnb,
-                          float eps, const uint16_t* W, const float* bias, int N, int act, const float* res,
+                          float eps, const uint16_t* W, int w_rs, const float* bias, int N, int act, const float* res,
                           int res_rs, void* Y, bool y_bf16, int y_rs, float* mean, float* rstd, const float* pe, int pe_rs,
                           int pe_rows, int npix, hipStream_t st) {
   const int nch = pick_nch(Kin);
   const PeSplit ps{pe, pe_rs, pe_rows, npix};
 #define LNL(TI, TO) \
-  ln_linear_fwd_n<TI, TO>(nch, X, x_rs, R, Kin, lnw, lnb, eps, W, bias, N, act, res, res_rs, Y, y_rs, mean, rstd, ps, st)
+  ln_linear_fwd_n<TI, TO>(nch, X, x_rs, R, Kin, lnw, lnb, eps, W, w_rs, bias, N, act, res, res_rs, Y, y_rs, mean, rstd, ps, st)
   if (x_bf16 && y_bf16) LNL(uint16_t, uint16_t);
   else if (x_bf16) LNL(uint16_t, float);
   else if (y_bf16) LNL(float, uint16_t);
@@ -1077,7 +1125,7 @@ void post_attn_bwd_launch(int C, const float* dZ, const float* Ysave, const floa
 }
 
 template <typename TG, typename TX, int NCH>
-static void ln_linear_bwd_t(const void* G, int g_rs, int N, const uint16_t* W, int Kin, const void* X, int x_rs,
+static void ln_linear_bwd_t(const void* G, int g_rs, int N, const uint16_t* W, int w_rs, int Kin, const void* X, int x_rs,
                             const float* mean, const float* rstd, const float* lnw, const float* lnb, const float* dres,
                             int dres_rs, float* dX, int dx_rs, float* dlnw, float* dlnb, float* dW, float* db, int vrs,
                             int wrs, int R, const PeSplit& ps, hipStream_t st) {
@@ -1085,17 +1133,17 @@ static void ln_linear_bwd_t(const void* G, int g_rs, int N, const uint16_t* W, i
   const size_t smem = 64 * 72 * 2 + 2 * 64 * (KP + 8) * 2 + 64 * (KP + 4) * 4 + 8 * KP * 4 + 4 * 64 * 4;
   auto fn = ln_linear_bwd_kernel<TG, TX, NCH>;
   set_smem_once((const void*)fn);
-  hipLaunchKernelGGL(fn, dim3((R + 63) / 64), dim3(256), smem, st, (const TG*)G, g_rs, N, W, Kin, (const TX*)X, x_rs,
+  hipLaunchKernelGGL(fn, dim3((R + 63) / 64), dim3(256), smem, st, (const TG*)G, g_rs, N, W, w_rs, Kin, (const TX*)X, x_rs,
                      mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, dlnw, dlnb, dW, db, vrs, wrs, R, ps);
 }
 
 template <typename TG, typename TX>
-static void ln_linear_bwd_n(int nch, const void* G, int g_rs, int N, const uint16_t* W, int Kin, const void* X,
+static void ln_linear_bwd_n(int nch, const void* G, int g_rs, int N, const uint16_t* W, int w_rs, int Kin, const void* X,
                             int x_rs, const float* mean, const float* rstd, const float* lnw, const float* lnb,
                             const float* dres, int dres_rs, float* dX, int dx_rs, float* dlnw, float* dlnb, float* dW,
                             float* db, int vrs, int wrs, int R, const PeSplit& ps, hipStream_t st) {
 #define LNB(K)                                                                                                    \
-  ln_linear_bwd_t<TG, TX, K>(G, g_rs, N, W, Kin, X, x_rs, mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, dlnw, \
+  ln_linear_bwd_t<TG, TX, K>(G, g_rs, N, W, w_rs, Kin, X, x_rs, mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, dlnw, \
                              dlnb, dW, db, vrs, wrs, R, ps, st)
   switch (nch) {
     case 1: LNB(1); break;
@@ -1106,7 +1154,7 @@ static void ln_linear_bwd_n(int nch, const void* G, int g_rs, int N, const uint1
 #undef LNB
 }
 
-void ln_linear_bwd_launch(const void* G, bool g_bf16, int g_rs, int N, const uint16_t* W, int Kin, const void* X,
+void ln_linear_bwd_launch(const void* G, bool g_bf16, int g_rs, int N, const uint16_t* W, int w_rs, int Kin, const void* X,
                           bool x_bf16, int x_rs, const float* mean, const float* rstd, const float* lnw,
                           const float* lnb, const float* dres, int dres_rs, float* dX, int dx_rs, float* dlnw,
                           float* dlnb, float* dW, float* db, int vrs, int wrs, int R, const float* pe, int pe_rs,
@@ -1114,7 +1162,7 @@ void ln_linear_bwd_launch(const void* G, bool g_bf16, int g_rs, int N, const uin
   const int nch = pick_nch(Kin);  // Kin ≤ 160 → ≤ 5
   const PeSplit ps{pe, pe_rs, pe_rows, npix};
 #define LDG(TG, TX)                                                                                           \
-  ln_linear_bwd_n<TG, TX>(nch, G, g_rs, N, W, Kin, X, x_rs, mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, \
+  ln_linear_bwd_n<TG, TX>(nch, G, g_rs, N, W, w_rs, Kin, X, x_rs, mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, \
                           dlnw, dlnb, dW, db, vrs, wrs, R, ps, st)
   if (g_bf16 && x_bf16) LDG(uint16_t, uint16_t);
   else if (g_bf16) LDG(uint16_t, float);
@@ -1123,16 +1171,48 @@ void ln_linear_bwd_launch(const void* G, bool g_bf16, int g_rs, int N, const uin
 #undef LDG
 }
 
+template <typename TG, typename TA, int NCH>
+static void wgrad_t(const void* G, int g_rs, int N, const void* A, int a_rs, int Kin, int amode, const float* mean,
+                    const float* rstd, const float* lnw, const float* lnb, int R, int rps, float* dW, float* db,
+                    int vrs, int wrs, const PeSplit& ps, hipStream_t st) {
+  constexpr int KP = 32 * NCH;
+  const size_t smem = (64 * (64 + 8) + 64 * (KP + 8)) * 2 + 2 * KP * 4 + 4 * 64 * 4;
+  auto fn = wgrad_kernel<TG, TA, NCH>;
+  set_smem_once((const void*)fn);
+  dim3 grid((N + 63) / 64, (R + rps - 1) / rps);
+  hipLaunchKernelGGL(fn, grid, dim3(256), smem, st, (const TG*)G, g_rs, N, (const TA*)A, a_rs, Kin, amode, mean, rstd,
+                     lnw, lnb, R, rps, dW, db, vrs, wrs, ps);
+}
+
+template <typename TG, typename TA>
+static void wgrad_n(int nch, const void* G, int g_rs, int N, const void* A, int a_rs, int Kin, int amode,
+                    const float* mean, const float* rstd, const float* lnw, const float* lnb, int R, int rps, float* dW,
+                    float* db, int vrs, int wrs, const PeSplit& ps, hipStream_t st) {
+#define WGN(K) wgrad_t<TG, TA, K>(G, g_rs, N, A, a_rs, Kin, amode, mean, rstd, lnw, lnb, R, rps, dW, db, vrs, wrs, ps, st)
+  switch (nch) {
+    case 1: WGN(1); break;
+    case 2: WGN(2); break;
+    case 4: WGN(4); break;
+    default: WGN(5); break;
+  }
+#undef WGN
+}
+
+// rows_per_wg ≤ 0: pick the split so that the launch has ≈ 512 workgroups
 void wgrad_launch(const void* G, bool g_bf16, int g_rs, int N, const void* A, bool a_bf16, int a_rs, int Kin,
                   int amode, const float* mean, const float* rstd, const float* lnw, const float* lnb, int R,
-                  int rows_per_wg, float* dW, float* db, hipStream_t st) {
-  const int KP = round_up(Kin, 32);
-  const size_t smem = (64 * (64 + 8) + 64 * (KP + 8)) * 2;
-  const int rps = round_up(rows_per_wg > 0 ? rows_per_wg : 256, 64);
-  dim3 grid((N + 63) / 64, (R + rps - 1) / rps);
-#define WG(TG, TA)                                                                                                 \
-  hipLaunchKernelGGL((wgrad_kernel<TG, TA>), grid, dim3(256), smem, st, (const TG*)G, g_rs, N, (const TA*)A, a_rs, \
-                     Kin, amode, mean, rstd, lnw, lnb, R, rps, dW, db)
+                  int rows_per_wg, float* dW, float* db, int vrs, int wrs, const float* pe, int pe_rs, int pe_rows,
+                  int npix, hipStream_t st) {
+  const int nblk = (N + 63) / 64;
+  int rps = rows_per_wg;
+  if (rps <= 0) {
+    const int splits = (512 + nblk - 1) / nblk;
+    rps = (R + splits - 1) / splits;
+  }
+  rps = round_up(rps < 64 ? 64 : rps, 64);
+  const PeSplit ps{pe, pe_rs, pe_rows, npix};
+  const int nch = pick_nch(Kin);
+#define WG(TG, TA) wgrad_n<TG, TA>(nch, G, g_rs, N, A, a_rs, Kin, amode, mean, rstd, lnw, lnb, R, rps, dW, db, vrs, wrs, ps, st)
   if (g_bf16 && a_bf16) WG(uint16_t, uint16_t);
   else if (g_bf16) WG(uint16_t, float);
   else if (a_bf16) WG(float, uint16_t);

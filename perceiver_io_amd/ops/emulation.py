@@ -37,7 +37,9 @@ def _split_x(x, pe, kin):
     return full
 
 
-def ln_linear_fwd(x, lnw, lnb, eps, w, bias, act, res, out_bf16, save_stats, pe=None):
+def ln_linear_fwd(x, lnw, lnb, eps, w, bias, act, res, out_bf16, save_stats, pe=None, kin=-1):
+    if kin >= 0:
+        w = w[:, :kin]
     xf = _split_x(x, pe, w.shape[1])
     mean = rstd = None
     if lnw is not None:
@@ -185,9 +187,12 @@ def post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, be2, H, grads):
     return dy, do, delta
 
 
-def ln_linear_bwd(g, w, x, mean, rstd, lnw, lnb, dres, need_dx, dlnw=None, dlnb=None, dW=None, db=None, pe=None):
+def ln_linear_bwd(g, w, x, mean, rstd, lnw, lnb, dres, need_dx, dlnw=None, dlnb=None, dW=None, db=None, pe=None,
+                  kin=-1):
     """Returns dX (or None); LN grads accumulate into dlnw / dlnb and, when given,
     dW += gᵀ·LN(x), db += Σ_rows g."""
+    if kin >= 0:
+        w = w[:, :kin]
     gf = g.float()
     dxn = _bf(gf) @ _bf(w.float())
     xf = _split_x(x, pe, w.shape[1])
@@ -207,16 +212,16 @@ def ln_linear_bwd(g, w, x, mean, rstd, lnw, lnb, dres, need_dx, dlnw=None, dlnb=
     return None
 
 
-def wgrad(g, a, amode, mean, rstd, lnw, lnb, rows_per_wg, dW, db=None):
+def wgrad(g, a, amode, mean, rstd, lnw, lnb, rows_per_wg, dW, db=None, pe=None, kin=-1):
     """dW += Gᵀ·A(transformed), db += Σ_rows G (accumulated in place)."""
-    af = a.float()
+    af = _split_x(a, pe, kin if kin >= 0 else a.shape[1])
     if amode == 1:
         af = (af - mean[:, None]) * rstd[:, None] * lnw + lnb
     elif amode == 2:
         af = F.gelu(af)
-    dW += (_bf(g.float()).t() @ _bf(af)).view(dW.shape)
+    _acc(dW, _bf(g.float()).t() @ _bf(af))
     if db is not None:
-        db += g.float().sum(0).view(db.shape)
+        _acc(db, g.float().sum(0))
 
 
 def mlm_select(labels, cap, gcap):

@@ -122,7 +122,12 @@ def _bf16_weights(spec: LayerSpec, ps):
             rest = ps[5:]
         else:
             wq = wc.get(ps[4])
-            wkv = torch.cat([wc.get(ps[5]), wc.get(ps[6])], 0)
+            wk, wv = wc.get(ps[5]), wc.get(ps[6])
+            kin = wk.shape[1]
+            # rows zero padded to a multiple of 8 columns: vectorised weight staging in the kernels
+            wkv = torch.zeros((2 * spec.C, (kin + 7) // 8 * 8), dtype=wk.dtype, device=wk.device)
+            wkv[: spec.C, :kin] = wk
+            wkv[spec.C:, :kin] = wv
             rest = ps[7:]
     else:
         wq, wkv = wc.get(ps[2]), None
@@ -193,7 +198,7 @@ class _LayerFn(torch.autograd.Function):
             ctx.kv_owner = ent is None
             if ent is None:  # first application of this layer: project K/V (LN over [pixels ‖ PE] if split)
                 kv, mean_kv, rstd_kv = K.ln_linear_fwd(xkv2, g_kv, b_kv, EPS, wkv, bin_[C:], 0, None, True, True,
-                                                       src.pe if src is not None else None)
+                                                       src.pe if src is not None else None, g_kv.shape[0])
                 ent = {"kv": kv, "mean": mean_kv, "rstd": rstd_kv, "dkv": None}
                 if src is not None:
                     src.entries[key] = ent
@@ -294,7 +299,7 @@ class _LayerFn(torch.autograd.Function):
             if Bq == 1 and B > 1:
                 dq2, dres = dq.sum(0), dy.view(B, Nq, C).sum(0)
             gbias = gb(bin_)
-            Ckv = wkv.shape[1]
+            Ckv = g_kv.shape[0]
             if spec.packed:
                 gin = gb(ps[4])
                 gwq, gwkv = rows(gin, 0, C, C), rows(gin, C, 3 * C, C)
@@ -307,7 +312,7 @@ class _LayerFn(torch.autograd.Function):
             if ctx.kv_owner:  # the projection's backward, once, over the summed dK/dV
                 dkv2 = dkv.view(B * M, 2 * C)
                 dx_kv = K.ln_linear_bwd(dkv2, wkv, xkv2, mean_kv, rstd_kv, g_kv, b_kv, None, ctx.kv_grad, gb(g_kv),
-                                        gb(b_kv), gwkv, rows(gbias, C, 3 * C, 1), ctx.kv_pe)
+                                        gb(b_kv), gwkv, rows(gbias, C, 3 * C, 1), ctx.kv_pe, Ckv)
                 ent["dkv"] = None
                 if not spec.packed:
                     gb(ps[5]).add_(rows(gwkv, 0, C, Ckv))

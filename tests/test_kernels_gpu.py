@@ -210,6 +210,36 @@ def test_mlm_select(B, L, cap, gcap, p):
         assert torch.equal(x.cpu(), y.cpu()), n
 
 
+@pytest.mark.parametrize("R,M,npix,kin,tall", [(6 * 100, 100, 3, 133, False), (2 * 70000, 70000, 1, 131, True)])
+def test_split_pe_input_projection(R, M, npix, kin, tall):
+    """Fourier-PE split input (pixels + padded PE table) for the LN+projection forward, its
+    backward (incl. the tall-R weight-gradient path) and the standalone weight gradient."""
+    torch.manual_seed(9)
+    N = 64 if tall else 256
+    pe = torch.zeros(M, (kin + 7) // 8 * 8, device=DEV)
+    pe[:, npix:kin] = torch.randn(M, kin - npix, device=DEV)
+    pix = torch.randn(R, npix, device=DEV)
+    wp = torch.zeros(N, (kin + 7) // 8 * 8, device=DEV)
+    wp[:, :kin] = torch.randn(N, kin, device=DEV) / math.sqrt(kin)
+    w = bf(wp)
+    lw, lb, bias = torch.randn(kin, device=DEV), torch.randn(kin, device=DEV), torch.randn(N, device=DEV)
+    outs = [K.ln_linear_fwd(pix, lw, lb, 1e-5, w, bias, 0, None, True, True, pe, kin) for K in (_ext(), _emu())]
+    for a, b, n in zip(outs[0], outs[1], ("y", "mean", "rstd")):
+        close(a, b, 2e-2 if n == "y" else 1e-3, n)
+    y, mean, rstd = outs[1]
+    g = torch.randn(R, N, device=DEV)
+    res = []
+    for K in (_ext(), _emu()):
+        dg, dbn = torch.zeros(kin, device=DEV), torch.zeros(kin, device=DEV)
+        dW, dbias = torch.zeros(N, kin, device=DEV), torch.zeros(N, device=DEV)
+        K.ln_linear_bwd(g, w, pix, mean, rstd, lw, lb, None, False, dg, dbn, dW, dbias, pe, kin)
+        dW2, db2 = torch.ones(N, kin, device=DEV), torch.ones(N, device=DEV)
+        K.wgrad(g, pix, 1, mean, rstd, lw, lb, 0, dW2, db2, pe, kin)
+        res.append((dg, dbn, dW, dbias, dW2, db2))
+    for a, b, n in zip(res[0], res[1], ("dgamma", "dbeta", "dW", "dbias", "wgrad dW", "wgrad db")):
+        close(a, b, 3e-2, n)
+
+
 @pytest.mark.parametrize("M,V,C", [(300, 1000, 64), (77, 10003, 64), (64, 257, 128)])
 def test_fused_cross_entropy(M, V, C):
     torch.manual_seed(5)
