@@ -64,6 +64,37 @@ class _Timer:
         return "\n".join(["action                          calls      total      mean"] + rows)
 
 
+class _TorchProfiler:
+    """``--trainer.profiler=pytorch``: torch.profiler (ROCm activity tracing) over training steps
+    ``wait``..``wait+active``; writes a Chrome trace and a per-kernel table into
+    ``<log_dir>/profiler/``.  ``advanced`` also records shapes and stacks."""
+
+    def __init__(self, out_dir: str, advanced: bool = False, wait: int = 3, active: int = 5):
+        from torch.profiler import ProfilerActivity, profile, schedule
+
+        acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if torch.cuda.is_available() else [])
+        self.out_dir = out_dir
+        self.prof = profile(activities=acts, schedule=schedule(wait=wait, warmup=1, active=active, repeat=1),
+                            record_shapes=advanced, with_stack=advanced, on_trace_ready=self._ready)
+        self.prof.__enter__()
+        self.done = False
+
+    def _ready(self, prof):
+        os.makedirs(self.out_dir, exist_ok=True)
+        prof.export_chrome_trace(os.path.join(self.out_dir, "trace.json"))
+        key = "cuda_time_total" if torch.cuda.is_available() else "cpu_time_total"
+        with open(os.path.join(self.out_dir, "kernels.txt"), "w") as f:
+            f.write(prof.key_averages().table(sort_by=key, row_limit=60))
+        self.done = True
+
+    def step(self):
+        if not self.done:
+            self.prof.step()
+
+    def close(self):
+        self.prof.__exit__(None, None, None)
+
+
 class Trainer:
     def __init__(self, logger: Any = True, checkpoint_callback: Optional[bool] = None, enable_checkpointing: bool = True,
                  callbacks: Optional[List[Callback]] = None, default_root_dir: Optional[str] = None,
@@ -361,6 +392,10 @@ class Trainer:
             max(1, int(n_train * vci)) if isinstance(vci, float) else int(vci))
         max_epochs = self.max_epochs if self.max_epochs is not None else (1000 if self.max_steps < 0 else 10 ** 9)
         t_last, steps_last = time.perf_counter(), self.global_step
+        tprof = None
+        if self.profiler_name in ("pytorch", "advanced") and self.is_global_zero:
+            base = self.logger.log_dir if self.logger is not None else (self.default_root_dir or ".")
+            tprof = _TorchProfiler(os.path.join(base, "profiler"), advanced=self.profiler_name == "advanced")
         while self.current_epoch < max_epochs and not self.should_stop:
             model.train()
             sampler = getattr(train_dl, "sampler", None)
@@ -384,6 +419,8 @@ class Trainer:
                 acc_buf = []
                 self._in_train = False
                 self.global_step += 1
+                if tprof is not None:
+                    tprof.step()
                 for cb in self.callbacks:
                     cb.on_train_batch_end(self, model)
                 if self.global_step % self.log_every_n_steps == 0 or self.fast_dev_run:
@@ -409,6 +446,8 @@ class Trainer:
             for cb in self.callbacks:
                 cb.on_train_epoch_end(self, model)
             self.current_epoch += 1
+        if tprof is not None:
+            tprof.close()
 
     def _eager_clip_step(self, batches):
         opt = self.optimizers[0]

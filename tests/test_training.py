@@ -148,3 +148,13 @@ def test_fused_adamw_matches_torch_adamw():
     ob2 = FusedAdamW(torch.nn.Linear(7, 5).parameters(), lr=1.0)
     ob2.load_state_dict(sd)
     assert ob2._step == 5 and torch.allclose(ob2.exp_avg, ob.exp_avg)
+
+
+def test_pytorch_profiler_flag_writes_trace(tmp_path):
+    cli = run_cli("img_clf", tmp_path, "fit", "--data=MNISTDataModule", "--data.synthetic=true",
+                  "--data.synthetic_size=120", "--data.batch_size=8", "--data.num_workers=0", "--data.val_split=16",
+                  "--trainer.max_epochs=1", "--trainer.limit_train_batches=10", "--trainer.limit_val_batches=1",
+                  "--trainer.profiler=pytorch", "--model.num_encoder_layers=1",
+                  "--model.num_encoder_self_attention_layers_per_block=1")
+    out = os.path.join(cli.trainer.logger.log_dir, "profiler")
+    assert os.path.exists(os.path.join(out, "trace.json")) and os.path.exists(os.path.join(out, "kernels.txt"))
