@@ -54,8 +54,8 @@ def init(backend: str | None = None, timeout_s: float = 1800.0, device_type: str
         return _INFO
     if device_type is None:
         device_type = "cuda" if torch.cuda.is_available() else "cpu"
-    if backend is None:
-        backend = "nccl" if device_type == "cuda" else "gloo"
+    if backend is None:  # PERCEIVER_DIST_BACKEND=gloo: rehearse GPU ranks over gloo (e.g. several on one GPU)
+        backend = os.environ.get("PERCEIVER_DIST_BACKEND") or ("nccl" if device_type == "cuda" else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29511")
     # the host driver only supports dmabuf IPC (RCCL / CUDA-tensor sharing across processes)
