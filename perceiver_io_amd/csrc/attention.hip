@@ -92,9 +92,10 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(AttnArgs a, uint16_t
   __shared__ __attribute__((aligned(16))) uint16_t sV[NST * KT * LDV + 64];
 
   const int w = wave_id(), l = lane_id(), r = l & 31, hh = l >> 5;
-  const int h = blockIdx.y;
-  const int b = blockIdx.z / nsplit, split = blockIdx.z % nsplit;
-  const int q0 = (blockIdx.x * NWV + w) * 32;
+  const Blk3 blk = xcd_block3();  // the heads / q-blocks / splits of one batch element share an L2
+  const int h = blk.y;
+  const int b = blk.z / nsplit, split = blk.z % nsplit;
+  const int q0 = (blk.x * NWV + w) * 32;
   const int qi = q0 + r;
   const int qc = qi < a.Nq ? qi : a.Nq - 1;
 
@@ -226,15 +227,19 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(AttnArgs a, uint16_t
       for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          float p = fast_exp2(s[kh][i] - m_new);
-          ls += p;
-          if (a.drop_thresh) {
+          s[kh][i] = fast_exp2(s[kh][i] - m_new);
+          ls += s[kh][i];
+        }
+      if (a.drop_thresh) {  // uniform: the element loop above stays branch-free
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
             const int key = key0 + 32 * kh + acc_row(i, hh);
             const uint32_t idx = (uint32_t)qi * (uint32_t)a.Nk + (uint32_t)key;
-            p = keep_elem(a.seed, (uint32_t)(b * a.H + h), idx, a.drop_thresh) ? p * a.drop_scale : 0.f;
+            s[kh][i] = keep_elem(a.seed, (uint32_t)(b * a.H + h), idx, a.drop_thresh) ? s[kh][i] * a.drop_scale : 0.f;
           }
-          s[kh][i] = p;
-        }
+      }
       l_run = l_run * alpha + ls;
 #pragma unroll
       for (int t2 = 0; t2 < NT; ++t2)
@@ -356,17 +361,24 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
   __shared__ __attribute__((aligned(16))) uint16_t sdO[NQS * 32 * LD + 64];
   __shared__ __attribute__((aligned(16))) uint16_t sK[KB * LD + 64];
   __shared__ __attribute__((aligned(16))) uint16_t sdS[NQS * KB * LDS_];
-  __shared__ float sL[NQS * 32], sDl[NQS * 32];
+  __shared__ __attribute__((aligned(16))) float sL[NQS * 32];
+  __shared__ __attribute__((aligned(16))) float sDl[NQS * 32];
 
+  PIO_WG_BEGIN();
+  PIO_TS(0);
   const int w = wave_id(), l = lane_id(), r = l & 31, hh = l >> 5;
-  const int h = blockIdx.y, b = blockIdx.z;
-  const int kbase = blockIdx.x * KB;
+  const Blk3 blk = xcd_block3();  // the heads / key blocks of one batch element share an L2
+  const int h = blk.y, b = blk.z;
+  const int kbase = blk.x * KB;
   const int key = kbase + 32 * w + r;  // this lane's key (column of S / dP)
   const int kc = key < a.Nk ? key : a.Nk - 1;
   bool kpad = key >= a.Nk;
   if (!kpad && a.kmask) kpad = a.kmask[(long long)b * a.Nk + key] != 0;
 
   const int HD = a.H * D;
+  // 16-byte output rows possible (fp32 dQ / dK / dV views 16-byte aligned)
+  const bool vec_out = ((((uintptr_t)dq | (uintptr_t)dk | (uintptr_t)dv) & 15) == 0) &&
+                       (((dq_bs | dk_bs | dv_bs) & 3) == 0) && (((dq_rs | dk_rs | dv_rs) & 3) == 0);
   const uint16_t* kbp = a.k + (long long)b * a.k_bs + h * D;
   const uint16_t* vbp = a.v + (long long)b * a.v_bs + h * D;
   const uint16_t* qbp = a.q + (long long)b * a.q_bs + h * D;
@@ -394,17 +406,24 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
       lreg = isd ? (qq < a.Nq ? delta[idx] : 0.f) : (qq < a.Nq ? LSE[idx] : INFINITY);
     }
   };
-  if (nqt > 0) fetch(0);
-
-  // stage the block's K tile (for dQ) and zero padded columns
-  for (int c = threadIdx.x; c < KB * CH; c += NTH) {
-    const int kr = c / CH, col = (c % CH) * 8;
-    const int kk = kbase + kr;
-    bf16x8 kv = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    if (kk < a.Nk) kv = *reinterpret_cast<const bf16x8*>(kbp + (long long)kk * a.k_rs + col);
-    *reinterpret_cast<bf16x8*>(sK + kr * LD + col) = kv;
+  // every prologue load is issued before the first wait: this wave's K^T / V^T operand
+  // fragments (B[k=d][col=key]), the block's K tile (for dQ), the first query round
+  bf16x8 kf[KS], vf[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    kf[s] = *reinterpret_cast<const bf16x8*>(kbp + (long long)kc * a.k_rs + 16 * s + 8 * hh);
+    vf[s] = *reinterpret_cast<const bf16x8*>(vbp + (long long)kc * a.v_rs + 16 * s + 8 * hh);
   }
-  if (D < 32) {
+  constexpr int KSI = KB * CH / NTH;  // K-tile chunks per thread (= CH / 2)
+  bf16x8 kst[KSI];
+#pragma unroll
+  for (int i = 0; i < KSI; ++i) {
+    const int c = threadIdx.x + NTH * i, kk = kbase + c / CH, col = (c % CH) * 8;
+    kst[i] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (kk < a.Nk) kst[i] = *reinterpret_cast<const bf16x8*>(kbp + (long long)kk * a.k_rs + col);
+  }
+  if (nqt > 0) fetch(0);
+  if (D < 32) {  // zero the padded head-dim columns 16..31
     for (int i = threadIdx.x; i < KB; i += NTH) {
       *reinterpret_cast<bf16x8*>(sK + i * LD + 16) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
       *reinterpret_cast<bf16x8*>(sK + i * LD + 24) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
@@ -416,17 +435,15 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
       *reinterpret_cast<bf16x8*>(sdO + i * LD + 24) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
     }
   }
-  // K^T / V^T operand fragments for this wave's 32 keys (B operand: B[k=d][col=key])
-  bf16x8 kf[KS], vf[KS];
 #pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    kf[s] = *reinterpret_cast<const bf16x8*>(kbp + (long long)kc * a.k_rs + 16 * s + 8 * hh);
-    vf[s] = *reinterpret_cast<const bf16x8*>(vbp + (long long)kc * a.v_rs + 16 * s + 8 * hh);
+  for (int i = 0; i < KSI; ++i) {
+    const int c = threadIdx.x + NTH * i;
+    *reinterpret_cast<bf16x8*>(sK + (c / CH) * LD + (c % CH) * 8) = kst[i];
   }
   f32x16 dK[NT], dV[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) dK[t] = dV[t] = f32x16{};
-  const int kvalid = min(KB, a.Nk - kbase);  // keys of this block (rows of the dS tiles in use)
+  PIO_TS(1);
 
   for (int qt0 = 0; qt0 < nqt; qt0 += NQS) {
     __syncthreads();  // the previous round's tiles and dS slabs are consumed
@@ -438,6 +455,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
     if (threadIdx.x < NQS * 32) sL[threadIdx.x] = lreg;
     else if (threadIdx.x < NQS * 64) sDl[threadIdx.x - NQS * 32] = lreg;
     __syncthreads();
+    PIO_TS(2 + 4 * (qt0 / NQS));
     if (qt0 + NQS < nqt) fetch(qt0 + NQS);
 
 #pragma unroll
@@ -453,21 +471,32 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
         S = mfma32(frag_kc(tQ, LD, 0, 16 * s), kf[s], S);
         dP = mfma32(frag_kc(tdO, LD, 0, 16 * s), vf[s], dP);
       }
-      f32x16 P, dS;
+      // LSE / delta of this lane's accumulator rows (registers 4g..4g+3 = tile rows
+      // 8g + 4hh + 0..3): 8 vector LDS reads, then a branch-free element loop (a per-element
+      // condition around an LDS read serialises the loop on LDS latency)
+      f32x4 lrow[4], drow[4];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int qr = acc_row(i, hh);
-        float p = kpad ? 0.f : fast_exp2(S[i] * a.scale_log2 - sL[j * 32 + qr]);
-        float dp = dP[i];
-        float pd = p;
-        if (a.drop_thresh) {
-          const uint32_t idx = (uint32_t)(q0 + qr) * (uint32_t)a.Nk + (uint32_t)key;
-          const bool keep = keep_elem(a.seed, (uint32_t)(b * a.H + h), idx, a.drop_thresh);
-          pd = keep ? p * a.drop_scale : 0.f;
-          dp = keep ? dp * a.drop_scale : 0.f;
+      for (int g = 0; g < 4; ++g) {
+        lrow[g] = *reinterpret_cast<const f32x4*>(sL + j * 32 + 8 * g + 4 * hh);
+        drow[g] = *reinterpret_cast<const f32x4*>(sDl + j * 32 + 8 * g + 4 * hh);
+      }
+      f32x16 P, dS;
+      if (!a.drop_thresh) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float p = fast_exp2(kpad ? -INFINITY : S[i] * a.scale_log2 - lrow[i >> 2][i & 3]);
+          P[i] = p;
+          dS[i] = p * (dP[i] - drow[i >> 2][i & 3]);
         }
-        P[i] = pd;
-        dS[i] = p * (dp - sDl[j * 32 + qr]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float p = fast_exp2(kpad ? -INFINITY : S[i] * a.scale_log2 - lrow[i >> 2][i & 3]);
+          const uint32_t idx = (uint32_t)(q0 + acc_row(i, hh)) * (uint32_t)a.Nk + (uint32_t)key;
+          const bool keep = keep_elem(a.seed, (uint32_t)(b * a.H + h), idx, a.drop_thresh);
+          P[i] = keep ? p * a.drop_scale : 0.f;
+          dS[i] = p * ((keep ? dP[i] * a.drop_scale : 0.f) - drow[i >> 2][i & 3]);
+        }
       }
       // dV += P^T dO ; dK += dS^T Q   (accumulator as A operand: X^T · B)
 #pragma unroll
@@ -489,31 +518,92 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
         *reinterpret_cast<uint2*>(slab + r * LDS_ + 8 * g + 4 * hh) = pk;
       }
     }
+    PIO_TS(3 + 4 * (qt0 / NQS));
     __syncthreads();
+    PIO_TS(4 + 4 * (qt0 / NQS));
     // dQ of tile j = w: Σ over the block's keys of dS[key][q] · K[key][d]
     if (w < NQS && qt0 + w < nqt) {
       const uint16_t* tS = sdS + w * KB * LDS_;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        f32x16 dq_acc = f32x16{};
-        for (int k0 = 0; k0 < kvalid; k0 += 16)
-          dq_acc = mfma32(frag_ks(tS, LDS_, 0, k0), frag_ks(sK, LD, 32 * t, k0), dq_acc);
-        // accumulator: col = lane&31 = d, row = acc_row = query within the tile
+        // all KB keys (slab rows / K rows past the block's keys are zero): unrolled, two
+        // independent accumulation chains
+        f32x16 dq_acc = f32x16{}, dq_acc2 = f32x16{};
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int dd = 32 * t + r, qq = (qt0 + w) * 32 + acc_row(i, hh);
-          if (dd < D && qq < a.Nq) {
-            float* dst = dq + (long long)b * dq_bs + (long long)qq * dq_rs + h * D + dd;
-            const float v = dq_acc[i] * a.scale;
-            if (dq_atomic) atomicAdd(dst, v);
-            else *dst = v;
+        for (int k0 = 0; k0 < KB; k0 += 32) {
+          dq_acc = mfma32(frag_ks(tS, LDS_, 0, k0), frag_ks(sK, LD, 32 * t, k0), dq_acc);
+          dq_acc2 = mfma32(frag_ks(tS, LDS_, 0, k0 + 16), frag_ks(sK, LD, 32 * t, k0 + 16), dq_acc2);
+        }
+        dq_acc += dq_acc2;
+        // accumulator: col = lane&31 = d, row = acc_row = query within the tile
+        if (dq_atomic || !vec_out || D > 32) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int dd = 32 * t + r, qq = (qt0 + w) * 32 + acc_row(i, hh);
+            if (dd < D && qq < a.Nq) {
+              float* dst = dq + (long long)b * dq_bs + (long long)qq * dq_rs + h * D + dd;
+              const float v = dq_acc[i] * a.scale;
+              if (dq_atomic) atomicAdd(dst, v);
+              else *dst = v;
+            }
+          }
+        } else {
+          // single key block: transpose through this wave's own (consumed) dS slab, then
+          // 16-byte row stores
+          float* sE = reinterpret_cast<float*>(sdS + w * KB * LDS_);
+          constexpr int LDE = D + 4;
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (r < D) sE[acc_row(i, hh) * LDE + r] = dq_acc[i] * a.scale;
+          constexpr int CPR = D / 4;
+#pragma unroll
+          for (int c = l; c < 32 * CPR; c += 64) {
+            const int qq = (qt0 + w) * 32 + c / CPR, col = (c % CPR) * 4;
+            if (qq < a.Nq)
+              *reinterpret_cast<float4*>(dq + (long long)b * dq_bs + (long long)qq * dq_rs + h * D + col) =
+                  *reinterpret_cast<const float4*>(sE + (c / CPR) * LDE + col);
           }
         }
       }
     }
+    PIO_TS(5 + 4 * (qt0 / NQS));
   }
+  PIO_TS(40);
   // write dK (scaled) and dV: rows = keys (registers), lane = head-dim column
   // accumulator: col = lane&31 = d, row = acc_row(reg) = key within the wave's 32
+  if constexpr (D <= 32) {
+    if (vec_out) {  // transpose through LDS (the dS slabs are consumed), 16-byte row stores
+      constexpr int LDE = D + 4, CPR = D / 4;
+      float* sE = reinterpret_cast<float*>(sdS);  // [dK | dV][KB keys][LDE]
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (r < D) {
+          const int kl = 32 * w + acc_row(i, hh);
+          sE[kl * LDE + r] = dK[0][i] * a.scale;
+          sE[(KB + kl) * LDE + r] = dV[0][i];
+        }
+      __syncthreads();
+#pragma unroll
+      for (int c = threadIdx.x; c < 2 * KB * CPR; c += NTH) {
+        const int isv = c >= KB * CPR, cc = isv ? c - KB * CPR : c;
+        const int kl = cc / CPR, col = (cc % CPR) * 4, kk = kbase + kl;
+        if (kk < a.Nk) {
+          float4 v = *reinterpret_cast<const float4*>(sE + ((isv ? KB : 0) + kl) * LDE + col);
+          float* dst = (isv ? dv + (long long)b * dv_bs + (long long)kk * dv_rs
+                            : dk + (long long)b * dk_bs + (long long)kk * dk_rs) + h * D + col;
+          if (kv_acc) {
+            const float4 o = *reinterpret_cast<const float4*>(dst);
+            v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+          }
+          *reinterpret_cast<float4*>(dst) = v;
+        }
+      }
+      PIO_TS(41);
+      PIO_WG_END();
+      return;
+    }
+  }
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -528,6 +618,8 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
         *pv = kv_acc ? *pv + dV[t][i] : dV[t][i];
       }
     }
+  PIO_TS(41);
+  PIO_WG_END();
 }
 
 // zero rows of a strided fp32 (B, N, W) view (dQ accumulator when several key blocks add into it)

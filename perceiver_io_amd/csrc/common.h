@@ -128,6 +128,52 @@ __device__ __forceinline__ float wave_max(float v) {
 // 2^x as one v_exp_f32 (no denormal-range fixup: results below 2^-126 flush to 0, -inf → 0)
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// ---- XCD-aware workgroup order --------------------------------------------------------
+// Workgroups are dealt round-robin over the 8 XCDs (observed placement; speed only, never
+// correctness).  xcd_remap turns the dispatch-order id into a logical id such that
+// consecutive logical ids share an XCD (and its L2) — bijective for any grid size.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+// logical 3-D block index (x fastest) after the remap: the (x, y) blocks of one z are
+// consecutive, i.e. all heads / key blocks of one batch element read their rows through one L2
+struct Blk3 { int x, y, z; };
+__device__ __forceinline__ Blk3 xcd_block3() {
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int nwg = gx * gy * gridDim.z;
+  const int m = xcd_remap(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), nwg);
+  return Blk3{m % gx, (m / gx) % gy, m / (gx * gy)};
+}
+
+// ---- phase timestamps (tools/trace only; compiled out unless PIO_TRACE is defined) ----
+// PIO_TS(slot): lane 0 of every wave of workgroup (trace_bx, trace_by, trace_bz) records the
+// shader clock into trace_buf[wave * 64 + slot]; slot 63 of every workgroup's wave 0 goes to
+// trace_wg[2 * wg + {0, 1}] via PIO_WG_BEGIN / PIO_WG_END (dispatch timeline).
+#ifdef PIO_TRACE
+__device__ long long* trace_buf;
+__device__ long long* trace_wg;
+__device__ int trace_bx, trace_by, trace_bz;
+#define PIO_TS(slot)                                                                                 \
+  do {                                                                                               \
+    if (blockIdx.x == (unsigned)trace_bx && blockIdx.y == (unsigned)trace_by &&                      \
+        blockIdx.z == (unsigned)trace_bz && (threadIdx.x & 63) == 0)                                 \
+      trace_buf[(threadIdx.x >> 6) * 64 + (slot)] = __builtin_amdgcn_s_memtime();                    \
+  } while (0)
+#define PIO_WG_MARK(which)                                                                           \
+  do {                                                                                               \
+    if (threadIdx.x == 0 && trace_wg)                                                                \
+      trace_wg[2 * ((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) + (which)] =     \
+          __builtin_amdgcn_s_memtime();                                                              \
+  } while (0)
+#define PIO_WG_BEGIN() PIO_WG_MARK(0)
+#define PIO_WG_END() PIO_WG_MARK(1)
+#else
+#define PIO_TS(slot) do {} while (0)
+#define PIO_WG_BEGIN() do {} while (0)
+#define PIO_WG_END() do {} while (0)
+#endif
+
 // ---- GELU (erf form, nn.GELU default) ------------------------------------------------
 __device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float gelu_grad(float x) {

@@ -117,6 +117,11 @@ def test_attention_fwd_bwd(B, Bq, Nq, Nk, H, D, ns):
         close(pk[:, :, :E], g2[0], 3e-2, "dq packed")
         close(dkv[:, :, :E], g2[1], 3e-2, "dk packed")
         close(dkv[:, :, E:], g2[2], 3e-2, "dv packed")
+        # K/V shared by several layers: the second application adds onto the first
+        _ext().attn_bwd(q, k, v, km, o1, do, l1, None, H, D, scale, 0.0, 0, pk[:, :, :E], dkv[:, :, :E], dkv[:, :, E:],
+                        True)
+        close(dkv[:, :, :E], 2 * g2[1], 3e-2, "dk accumulated")
+        close(dkv[:, :, E:], 2 * g2[2], 3e-2, "dv accumulated")
 
 
 def test_attention_dropout_statistics():
