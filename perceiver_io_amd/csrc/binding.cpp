@@ -19,7 +19,16 @@ struct AttnArgs {
   float drop_scale;
   uint32_t seed;
 };
-struct PostAttnGrads { float *dWo, *dbo, *dg2, *dbe2, *dW1, *db1, *dW2, *db2; int vrs; };
+struct PostAttnGrads { float *dWo, *dbo, *dg2, *dbe2, *dW1, *db1, *dW2, *db2; int vrs; int slab; };
+constexpr int kMaxSlabSegs = 8, kSlabRowsPerBlock = 32;  // common.h
+struct SlabJob {
+  const float* slab;
+  int S, P, nbx, nblk;
+  int n;
+  float* dst[kMaxSlabSegs];
+  int off[kMaxSlabSegs];
+  int len[kMaxSlabSegs];
+};
 
 void attn_fwd_launch(const AttnArgs&, int, uint16_t*, float*, float*, float*, int, hipStream_t);
 void attn_bwd_launch(const AttnArgs&, int, const uint16_t*, const uint16_t*, const float*, float*, float*, long long,
@@ -32,10 +41,11 @@ void post_attn_fwd_launch(int, const uint16_t*, const float*, const uint16_t*, c
                           float*, float*, float*, uint16_t*, int, int, hipStream_t);
 void post_attn_bwd_launch(int, const float*, const float*, const float*, const float*, const uint16_t*,
                           const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*, const float*,
-                          const float*, float*, uint16_t*, float*, int, const PostAttnGrads&, int, hipStream_t);
+                          const float*, float*, uint16_t*, float*, int, const PostAttnGrads&, int, const SlabJob&,
+                          hipStream_t);
 void ln_linear_bwd_launch(const void*, bool, int, int, const uint16_t*, int, int, const void*, bool, int, const float*,
                           const float*, const float*, const float*, const float*, int, float*, int, float*, float*,
-                          float*, float*, int, int, int, const float*, int, int, int, hipStream_t);
+                          float*, float*, int, int, int, int, const float*, int, int, int, const SlabJob&, hipStream_t);
 void wgrad_launch(const void*, bool, int, int, const void*, bool, int, int, int, const float*, const float*,
                   const float*, const float*, int, int, float*, float*, int, int, const float*, int, int, int,
                   hipStream_t);
@@ -57,6 +67,7 @@ void adamw_launch(float*, const float*, float*, float*, uint16_t*, long long, co
 void cast_bf16_launch(const float*, uint16_t*, long long, hipStream_t);
 void reduce_probe_launch(const float*, float*, hipStream_t);
 void fold_replicas_launch(float*, float*, long long, int, hipStream_t);
+void slab_reduce_launch(const SlabJob&, hipStream_t);
 }  // namespace pio
 
 using torch::Tensor;
@@ -246,9 +257,16 @@ constexpr int kGradReplicas = 8;
 // gradient target: K contiguous floats (any shape), or an (8, K) replica view with unit inner
 // stride whose row stride is shared by every target of the call (workgroup i adds into row
 // i % 8).  A 2-D target counts as replicated only when it is (8, K) with K == its numel / 8.
-float* vec_target(Tensor& t, int64_t K, const char* what, int& vrs) {
+// Slab mode (slab_rows > 0): every target is an (slab_rows, K) view of ONE (tiles, P) slab —
+// workgroup i stores its partial into row i (no atomics; ops/fused.py reduces the slab).
+float* vec_target(Tensor& t, int64_t K, const char* what, int& vrs, int64_t slab_rows = 0) {
   CHECK_DT(t, torch::kFloat32);
-  if (t.dim() == 2 && t.size(0) == kGradReplicas && t.size(1) == K) {
+  if (slab_rows > 0) {
+    TORCH_CHECK(t.dim() == 2 && t.size(0) == slab_rows && t.size(1) == K && t.stride(1) == 1,
+                "slab target ", what, " must be a (tiles, K) view");
+    TORCH_CHECK(vrs < 0 || vrs == (int)t.stride(0), "slab targets must share one row stride");
+    vrs = (int)t.stride(0);
+  } else if (t.dim() == 2 && t.size(0) == kGradReplicas && t.size(1) == K) {
     TORCH_CHECK(t.stride(1) == 1, "bad replicated target ", what);
     TORCH_CHECK(vrs < 0 || vrs == (int)t.stride(0), "replicated targets must share one row stride");
     vrs = (int)t.stride(0);
@@ -259,11 +277,39 @@ float* vec_target(Tensor& t, int64_t K, const char* what, int& vrs) {
   }
   return t.data_ptr<float>();
 }
+// a slab reduction job: dsts[j] += Σ_rows slab[:, offs[j] : offs[j] + dsts[j].numel()]
+// (slab (S, P) contiguous fp32, P and every offset multiples of 4, ≤ 8 segments)
+pio::SlabJob make_job(const OptT& slab, std::vector<Tensor>& dsts, const std::vector<int64_t>& offs) {
+  pio::SlabJob j{};
+  if (!slab.has_value()) return j;
+  const Tensor& t = *slab;
+  CHECK_DT(t, torch::kFloat32);
+  TORCH_CHECK(t.dim() == 2 && t.is_contiguous() && t.size(1) % 4 == 0, "slab must be (S, P), P % 4 == 0");
+  TORCH_CHECK(dsts.size() == offs.size() && dsts.size() <= (size_t)pio::kMaxSlabSegs, "slab job: ≤ 8 segments");
+  const int P = (int)t.size(1);
+  for (size_t q = 0; q < dsts.size(); ++q) {
+    Tensor& d = dsts[q];
+    CHECK_DT(d, torch::kFloat32);
+    TORCH_CHECK(d.is_contiguous() && d.device() == t.device(), "slab job: destinations must be contiguous");
+    TORCH_CHECK(offs[q] % 4 == 0 && offs[q] >= 0 && offs[q] + d.numel() <= P, "slab job: bad segment");
+    if (d.numel() == 0) continue;
+    j.dst[j.n] = d.data_ptr<float>(); j.off[j.n] = (int)offs[q]; j.len[j.n] = (int)d.numel(); ++j.n;
+  }
+  if (j.n == 0 || t.size(0) == 0) return j;
+  j.slab = t.data_ptr<float>();
+  j.S = (int)t.size(0);
+  j.P = P;
+  j.nbx = (P + 255) / 256;
+  j.nblk = j.nbx * ((j.S + pio::kSlabRowsPerBlock - 1) / pio::kSlabRowsPerBlock);
+  return j;
+}
 }  // namespace
 
 // grads = [dWo, dbo, dg2, dbe2, dW1, db1, dW2, db2]; returns (dy, dO, delta)
+// slab: targets are (ceil(R/64), ·) views of one slab (see vec_target), reduced by slab_reduce
 std::vector<Tensor> post_attn_bwd(Tensor dz, Tensor y, Tensor m2, Tensor r2, Tensor u, Tensor o, Tensor wo, Tensor w1,
-                                  Tensor w2, Tensor g2, Tensor be2, int64_t H, std::vector<Tensor> grads) {
+                                  Tensor w2, Tensor g2, Tensor be2, int64_t H, std::vector<Tensor> grads, bool slab,
+                                  OptT job_slab, std::vector<Tensor> job_dsts, std::vector<int64_t> job_offs) {
   TORCH_CHECK(dz.is_contiguous() && y.is_contiguous() && u.is_contiguous() && o.is_contiguous(),
               "post_attn_bwd operands must be contiguous (R, C)");
   const int R = (int)dz.size(0), C = (int)dz.size(1);
@@ -272,18 +318,20 @@ std::vector<Tensor> post_attn_bwd(Tensor dz, Tensor y, Tensor m2, Tensor r2, Ten
   TORCH_CHECK(grads.size() == 8, "post_attn_bwd needs 8 gradient targets");
   const int64_t CC = (int64_t)C * C;
   int vrs = -1;
-  pio::PostAttnGrads pg{vec_target(grads[0], CC, "dWo", vrs), vec_target(grads[1], C, "dbo", vrs),
-                        vec_target(grads[2], C, "dg2", vrs), vec_target(grads[3], C, "dbe2", vrs),
-                        vec_target(grads[4], CC, "dW1", vrs), vec_target(grads[5], C, "db1", vrs),
-                        vec_target(grads[6], CC, "dW2", vrs), vec_target(grads[7], C, "db2", vrs), 0};
+  const int64_t sr = slab ? (R + 63) / 64 : 0;
+  pio::PostAttnGrads pg{vec_target(grads[0], CC, "dWo", vrs, sr), vec_target(grads[1], C, "dbo", vrs, sr),
+                        vec_target(grads[2], C, "dg2", vrs, sr), vec_target(grads[3], C, "dbe2", vrs, sr),
+                        vec_target(grads[4], CC, "dW1", vrs, sr), vec_target(grads[5], C, "db1", vrs, sr),
+                        vec_target(grads[6], CC, "dW2", vrs, sr), vec_target(grads[7], C, "db2", vrs, sr), 0, 0};
   pg.vrs = vrs < 0 ? 0 : vrs;
+  pg.slab = slab ? 1 : 0;
   auto f32 = dz.options().dtype(torch::kFloat32);
   Tensor dy = torch::empty({R, C}, f32);
   Tensor dO = torch::empty({R, C}, dz.options().dtype(torch::kBFloat16));
   Tensor delta = torch::empty({R, H}, f32);
   pio::post_attn_bwd_launch(C, f32p(dz), f32p(y), f32p(m2), f32p(r2), bfp(u), bfp(o), bfp(wo), bfp(w1), bfp(w2),
                             f32p(g2), f32p(be2), dy.data_ptr<float>(), bfp_mut(dO), delta.data_ptr<float>(), (int)H,
-                            pg, R, stream());
+                            pg, R, make_job(job_slab, job_dsts, job_offs), stream());
   return {dy, dO, delta};
 }
 
@@ -292,9 +340,12 @@ std::vector<Tensor> post_attn_bwd(Tensor dz, Tensor y, Tensor m2, Tensor r2, Ten
 constexpr int kTallRows = 1 << 17;
 
 OptT ln_linear_bwd(Tensor g, Tensor w, Tensor x, OptT mean, OptT rstd, OptT lnw, OptT lnb, OptT dres, bool need_dx,
-                   OptT dlnw, OptT dlnb, OptT dW, OptT db, OptT pe, int64_t kin) {
+                   OptT dlnw, OptT dlnb, OptT dW, OptT db, OptT pe, int64_t kin, bool slab, OptT job_slab,
+                   std::vector<Tensor> job_dsts, std::vector<int64_t> job_offs) {
   TORCH_CHECK(g.dim() == 2 && g.stride(1) == 1 && x.dim() == 2 && x.stride(1) == 1, "g / x must be 2-D rows");
   const int R = (int)g.size(0), N = (int)g.size(1);
+  TORCH_CHECK(!(slab && R >= kTallRows), "slab gradients are for R < ", kTallRows, " rows");
+  const int64_t sr = slab ? (R + 63) / 64 : 0;
   const int Kin = kin >= 0 ? (int)kin : (int)w.size(1);
   TORCH_CHECK(w.size(0) == N && w.is_contiguous() && w.size(1) >= Kin, "w must be (N, >= Kin) contiguous, N = g columns");
   TORCH_CHECK(x.size(0) == R && (pe.has_value() || x.size(1) == Kin), "x must be (R, Kin)");
@@ -310,12 +361,13 @@ OptT ln_linear_bwd(Tensor g, Tensor w, Tensor x, OptT mean, OptT rstd, OptT lnw,
   if (lnw.has_value()) {
     TORCH_CHECK(lnb.has_value() && mean.has_value() && rstd.has_value(), "LN weight needs bias and row stats");
     TORCH_CHECK(dlnw.has_value() && dlnb.has_value(), "LN grad targets required");
-    dgp = vec_target(*dlnw, Kin, "dlnw", vrs);
-    dbp = vec_target(*dlnb, Kin, "dlnb", vrs);
+    dgp = vec_target(*dlnw, Kin, "dlnw", vrs, sr);
+    dbp = vec_target(*dlnb, Kin, "dlnb", vrs, sr);
   }
   int wrs = -1;  // the weight target's replica stride may differ from the vectors'
-  if (dW.has_value()) dwp = vec_target(*dW, (int64_t)N * Kin, "dW", wrs);
-  if (db.has_value()) { TORCH_CHECK(dW.has_value(), "db needs dW"); dbiasp = vec_target(*db, N, "db", vrs); }
+  if (dW.has_value()) dwp = vec_target(*dW, (int64_t)N * Kin, "dW", wrs, sr);
+  if (db.has_value()) { TORCH_CHECK(dW.has_value(), "db needs dW"); dbiasp = vec_target(*db, N, "db", vrs, sr); }
+  TORCH_CHECK(!slab || vrs < 0 || wrs < 0 || vrs == wrs, "slab targets must share one slab");
   const float* dr = nullptr; int drs = 0;
   if (dres.has_value()) { dr = f32p(*dres); drs = (int)dres->stride(0); TORCH_CHECK(dres->stride(1) == 1); }
   // very tall inputs (image K/V projections): the weight gradient leaves the row-tile kernel
@@ -324,7 +376,8 @@ OptT ln_linear_bwd(Tensor g, Tensor w, Tensor x, OptT mean, OptT rstd, OptT lnw,
   pio::ln_linear_bwd_launch(g.data_ptr(), is_bf16(g), (int)g.stride(0), N, bfp(w), (int)w.size(1), Kin, x.data_ptr(),
                             is_bf16(x), (int)x.stride(0), f32o(mean), f32o(rstd), f32o(lnw), f32o(lnb), dr, drs, dxp,
                             Kin, dgp, dbp, tall ? nullptr : dwp, tall ? nullptr : dbiasp, vrs < 0 ? 0 : vrs,
-                            wrs < 0 ? 0 : wrs, R, pp, prs, prows, npix, stream());
+                            wrs < 0 ? 0 : wrs, slab ? 1 : 0, R, pp, prs, prows, npix,
+                            make_job(job_slab, job_dsts, job_offs), stream());
   if (tall)
     pio::wgrad_launch(g.data_ptr(), is_bf16(g), (int)g.stride(0), N, x.data_ptr(), is_bf16(x), (int)x.stride(0), Kin,
                       lnw.has_value() ? 1 : 0, f32o(mean), f32o(rstd), f32o(lnw), f32o(lnb), R, 0, dwp, dbiasp,
@@ -475,6 +528,11 @@ void fold_replicas(Tensor grad, Tensor rep) {
   pio::fold_replicas_launch(grad.data_ptr<float>(), rep.data_ptr<float>(), rep.size(1), (int)rep.size(0), stream());
 }
 
+// standalone slab job (see make_job)
+void slab_reduce(Tensor slab, std::vector<Tensor> dsts, std::vector<int64_t> offs) {
+  pio::slab_reduce_launch(make_job(slab, dsts, offs), stream());
+}
+
 void cast_bf16(Tensor x, Tensor y) {
   TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && x.numel() == y.numel());
   pio::cast_bf16_launch(f32p(x), reinterpret_cast<uint16_t*>(y.data_ptr()), x.numel(), stream());
@@ -490,10 +548,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bias"), py::arg("act"), py::arg("res"), py::arg("out_bf16"), py::arg("save_stats"),
         py::arg("pe") = py::none(), py::arg("kin") = -1);
   m.def("post_attn_fwd", &post_attn_fwd);
-  m.def("post_attn_bwd", &post_attn_bwd);
+  m.def("post_attn_bwd", &post_attn_bwd, py::arg("dz"), py::arg("y"), py::arg("m2"), py::arg("r2"), py::arg("u"),
+        py::arg("o"), py::arg("wo"), py::arg("w1"), py::arg("w2"), py::arg("g2"), py::arg("be2"), py::arg("H"),
+        py::arg("grads"), py::arg("slab") = false, py::arg("job_slab") = py::none(),
+        py::arg("job_dsts") = std::vector<Tensor>(), py::arg("job_offs") = std::vector<int64_t>());
   m.def("ln_linear_bwd", &ln_linear_bwd, py::arg("g"), py::arg("w"), py::arg("x"), py::arg("mean"), py::arg("rstd"),
         py::arg("lnw"), py::arg("lnb"), py::arg("dres"), py::arg("need_dx"), py::arg("dlnw"), py::arg("dlnb"),
-        py::arg("dW"), py::arg("db"), py::arg("pe") = py::none(), py::arg("kin") = -1);
+        py::arg("dW"), py::arg("db"), py::arg("pe") = py::none(), py::arg("kin") = -1, py::arg("slab") = false,
+        py::arg("job_slab") = py::none(), py::arg("job_dsts") = std::vector<Tensor>(),
+        py::arg("job_offs") = std::vector<int64_t>());
   m.def("wgrad", &wgrad, py::arg("g"), py::arg("a"), py::arg("amode"), py::arg("mean"), py::arg("rstd"), py::arg("lnw"),
         py::arg("lnb"), py::arg("rows_per_wg"), py::arg("dW"), py::arg("db"), py::arg("pe") = py::none(),
         py::arg("kin") = -1);
@@ -508,5 +571,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cast_bf16", &cast_bf16);
   m.def("reduce_probe", &reduce_probe);
   m.def("fold_replicas", &fold_replicas);
+  m.def("slab_reduce", &slab_reduce);
   m.attr("arch") = "gfx950";
 }

@@ -174,6 +174,58 @@ __device__ int trace_bx, trace_by, trace_bz;
 #define PIO_WG_END() do {} while (0)
 #endif
 
+// ---- parameter-gradient slab reduction ----------------------------------------------
+// A backward kernel in "slab" mode stores workgroup i's parameter-gradient partials into row
+// i of an (S, P) fp32 slab (rowgemm.hip); a SlabJob sums the rows into the gradients:
+// dst_j[k] += Σ_s slab[s][off_j + k] (P and every off_j multiples of 4).  The job runs as
+// extra workgroups appended to the NEXT kernel of the backward chain (horizontal fusion: the
+// latency-bound chain kernels leave most CU slots idle, and a separate node — or a side-stream
+// branch, whose cross-queue hand-off costs 10–15 µs per fork in a replayed hipGraph — would sit
+// on the critical path), or as a standalone launch at the end of the backward pass.
+// Reduction block (x, y): 256 columns × slab rows [32y, 32y + 32); wave w sums rows w, w+4, …
+// (all loads in flight), LDS combine, then wave w adds columns 64w..64w+63 with one
+// contiguous 256-B no-return atomic instruction: S/32 adds per element in all.
+constexpr int kMaxSlabSegs = 8;
+constexpr int kSlabRowsPerBlock = 32;
+struct SlabJob {
+  const float* slab;  // nullptr: no job
+  int S, P, nbx, nblk;
+  int n;
+  float* dst[kMaxSlabSegs];
+  int off[kMaxSlabSegs];
+  int len[kMaxSlabSegs];
+};
+// part: ≥ 4 KiB of 16-B aligned LDS
+__device__ __forceinline__ void slab_reduce_block(const SlabJob& j, int b, float4* part) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int bx = b % j.nbx, by = b / j.nbx;
+  const int cb = bx * 256, c = cb + 4 * l, P = j.P;
+  const int s0 = by * kSlabRowsPerBlock, s1 = min(j.S, s0 + kSlabRowsPerBlock);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c < P) {
+    float4 v[kSlabRowsPerBlock / 4];
+#pragma unroll
+    for (int i = 0; i < kSlabRowsPerBlock / 4; ++i) {
+      const int s = s0 + w + 4 * i;
+      v[i] = s < s1 ? *reinterpret_cast<const float4*>(j.slab + (long long)s * P + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < kSlabRowsPerBlock / 4; ++i) {
+      acc.x += v[i].x; acc.y += v[i].y; acc.z += v[i].z; acc.w += v[i].w;
+    }
+  }
+  part[w * 64 + l] = acc;
+  __syncthreads();
+  const float* pf = reinterpret_cast<const float*>(part);
+  const int k = 64 * w + l, col = cb + k;
+  if (col >= P) return;
+  const float sum = pf[k] + pf[256 + k] + pf[512 + k] + pf[768 + k];
+  for (int q = 0; q < j.n; ++q) {
+    const int lo = j.off[q];
+    if (col >= lo && col < lo + j.len[q]) atomicAdd(j.dst[q] + (col - lo), sum);
+  }
+}
+
 // ---- GELU (erf form, nn.GELU default) ------------------------------------------------
 __device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float gelu_grad(float x) {

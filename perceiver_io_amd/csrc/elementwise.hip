@@ -214,6 +214,17 @@ void fold_replicas_launch(float* grad, float* rep, long long n, int nrep, hipStr
   hipLaunchKernelGGL(fold_replicas_kernel, grid_for((n + 3) / 4), dim3(256), 0, st, grad, rep, n, nrep);
 }
 
+// standalone form of a SlabJob (common.h): the reductions still pending at the end of a
+// backward pass
+__global__ __launch_bounds__(256) void slab_reduce_kernel(SlabJob job) {
+  __shared__ float4 part[256];
+  slab_reduce_block(job, blockIdx.x, part);
+}
+void slab_reduce_launch(const SlabJob& job, hipStream_t st) {
+  if (job.slab == nullptr || job.nblk == 0) return;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(job.nblk), dim3(256), 0, st, job);
+}
+
 // one wave: the cross-lane reduction helpers of common.h on x[0..63] (numerics self-test)
 __global__ void reduce_probe_kernel(const float* __restrict__ x, float* __restrict__ out) {
   const int l = threadIdx.x;

@@ -108,16 +108,26 @@ __device__ __forceinline__ void stage(uint16_t* s, int ld, const T* g, long long
 }
 
 // fp32 gradient targets of the post-attention block (views of the flat gradient buffer).
-// Targets may be replicated: workgroup i adds into replica i % kGradReplicas, vrs floats
-// apart (vrs = 0: one copy), so that no address takes more than grid/8 atomic adds (same-
-// address float atomics serialise at the memory side); replicas are folded once per step.
+// Two sinks for a workgroup's parameter-gradient partials:
+//  * atomic (slab = 0): targets may be replicated: workgroup i adds into replica
+//    i % kGradReplicas, vrs floats apart (vrs = 0: one copy), folded once per step;
+//  * slab (slab = 1): workgroup i STORES its partials into row i of a (tiles, P) fp32 slab
+//    (vrs = P floats per row).  Float atomics execute at the memory side at ≈1.3 TB/s
+//    chip-wide, so 256 tiles × 50 KB of partials per kernel cost ≈10 µs of a ≈25 µs kernel;
+//    plain stores cost ≈0.3 µs per CU, and slab_reduce (elementwise.hip) sums the rows on a
+//    side stream, overlapped with the rest of the backward chain.
 constexpr int kGradReplicas = 8;
 struct PostAttnGrads {
   float *dWo, *dbo, *dg2, *dbe2, *dW1, *db1, *dW2, *db2;
   int vrs;
+  int slab;
 };
-__device__ __forceinline__ float* rep(float* p, int vrs) {
-  return p + (blockIdx.x & (kGradReplicas - 1)) * vrs;
+__device__ __forceinline__ float* rep(float* p, int vrs, int slab) {
+  return p + (long long)(slab ? blockIdx.x : (blockIdx.x & (kGradReplicas - 1))) * vrs;
+}
+__device__ __forceinline__ void gadd(float* p, float v, int slab) {
+  if (slab) *p = v;
+  else atomicAdd(p, v);
 }
 
 __host__ __device__ __forceinline__ int round_up(int x, int m) { return (x + m - 1) / m * m; }
@@ -272,9 +282,9 @@ __device__ __forceinline__ void colsum_partial(const float (&v)[NCH][8], float* 
       if (l < 4) sPart[w * KP + rp_col(j) + e] = s;
     }
 }
-__device__ __forceinline__ void colsum_flush(const float* sPart, int KP, float* __restrict__ dst, int K) {
+__device__ __forceinline__ void colsum_flush(const float* sPart, int KP, float* __restrict__ dst, int K, int slab) {
   for (int k = threadIdx.x; k < K; k += blockDim.x)
-    atomicAdd(dst + k, sPart[k] + sPart[KP + k] + sPart[2 * KP + k] + sPart[3 * KP + k]);
+    gadd(dst + k, sPart[k] + sPart[KP + k] + sPart[2 * KP + k] + sPart[3 * KP + k], slab);
 }
 
 // rows [r0, r0 + rows) × cols [0, KP) of a bf16 row-major matrix → registers (zero beyond
@@ -602,13 +612,13 @@ __device__ __forceinline__ void stage_act(uint16_t* s, int ld, const T* A, long 
 // operands).  Each wave instruction adds two 128-byte row segments: the full-rate atomic shape.
 template <int MAXW>
 __device__ __forceinline__ void wgrad_tile(const uint16_t* sG, int ldg, const uint16_t* sX, int ldx, int NG, int KX,
-                                           int Nvalid, int Kvalid, float* __restrict__ dW, int dw_rs) {
+                                           int Nvalid, int Kvalid, float* __restrict__ dW, int dw_rs, int slab) {
   f32x16 acc[MAXW];
 #pragma unroll
   for (int t = 0; t < MAXW; ++t) acc[t] = f32x16{};
   tile_gemm<MAXW, false, false>(sG, ldg, sX, ldx, NG, KX, 64, acc);
   for_acc<MAXW>(NG, KX, [&](int t, int m, int n, int i) {
-    if (m < Nvalid && n < Kvalid) atomicAdd(dW + (long long)m * dw_rs + n, acc[t][i]);
+    if (m < Nvalid && n < Kvalid) gadd(dW + (long long)m * dw_rs + n, acc[t][i], slab);
   });
 }
 
@@ -629,7 +639,7 @@ __global__ __launch_bounds__(256) void post_attn_bwd_kernel(
     const float* __restrict__ rstd2, const uint16_t* __restrict__ U, const uint16_t* __restrict__ O,
     const uint16_t* __restrict__ Wo, const uint16_t* __restrict__ W1, const uint16_t* __restrict__ W2,
     const float* __restrict__ g2, const float* __restrict__ be2, float* __restrict__ dY, uint16_t* __restrict__ dO,
-    float* __restrict__ delta, int H, PostAttnGrads gr_out, int R) {
+    float* __restrict__ delta, int H, PostAttnGrads gr_out, int R, SlabJob job) {
   constexpr int LD = C + 8, LDF = C + 4, MAXT = (2 * C / 32 + 3) / 4, MAXW = ((C / 32) * (C / 32) + 3) / 4;
   constexpr int NCH = C / 32, NWB = C <= 64 ? 3 : 1, NIW = (C * C / 8 + 255) / 256;
   __shared__ __attribute__((aligned(16))) uint16_t sG[64 * LD];  // dZ → dU → dY
@@ -639,6 +649,10 @@ __global__ __launch_bounds__(256) void post_attn_bwd_kernel(
   __shared__ __attribute__((aligned(16))) float sPart[4][4 * C];  // wave partials: Σ dZ, dγ2, dβ2, Σ dY
   __shared__ float sDb1[2][C];
   __shared__ float sP[2][C];  // γ2, β2
+  if ((int)blockIdx.x >= (R + 63) / 64) {  // appended workgroups: the previous kernel's slab job
+    slab_reduce_block(job, blockIdx.x - (R + 63) / 64, reinterpret_cast<float4*>(sF));
+    return;
+  }
   const int m0 = blockIdx.x * 64, gr = m0 + rp_row(), w = wave_id(), l = lane_id();
   const bool av = aligned16(dZ) && aligned16(Ysave) && aligned16(U) && aligned16(O) && aligned16(dY) &&
                   aligned16(dO) && aligned16(Wo) && aligned16(W1) && aligned16(W2);
@@ -683,7 +697,7 @@ __global__ __launch_bounds__(256) void post_attn_bwd_kernel(
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
   tile_gemm<MAXT, true, false>(sG, LD, sW[0], LD, 64, C, C, acc);  // dH = dZ · W2
-  wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, rep(gr_out.dW2, gr_out.vrs), C);
+  wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, rep(gr_out.dW2, gr_out.vrs, gr_out.slab), C, gr_out.slab);
   {
     constexpr int NTN = C / 32;
 #pragma unroll
@@ -706,8 +720,10 @@ __global__ __launch_bounds__(256) void post_attn_bwd_kernel(
   }
   __syncthreads();
   for (int k = threadIdx.x; k < C; k += blockDim.x) {
-    atomicAdd(rep(gr_out.db1, gr_out.vrs) + k, sDb1[0][k] + sDb1[1][k]);
-    atomicAdd(rep(gr_out.db2, gr_out.vrs) + k, sPart[0][k] + sPart[0][C + k] + sPart[0][2 * C + k] + sPart[0][3 * C + k]);
+    gadd(rep(gr_out.db1, gr_out.vrs, gr_out.slab) + k,
+         sDb1[0][k] + sDb1[1][k], gr_out.slab);
+    gadd(rep(gr_out.db2, gr_out.vrs, gr_out.slab) + k,
+         sPart[0][k] + sPart[0][C + k] + sPart[0][2 * C + k] + sPart[0][3 * C + k], gr_out.slab);
   }
   if constexpr (NWB == 1) tile_store<NIW>(wr[0], sW[0], LD, C, C);
   {
@@ -730,7 +746,7 @@ __global__ __launch_bounds__(256) void post_attn_bwd_kernel(
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
   tile_gemm<MAXT, true, false>(sG, LD, sW[NWB == 3 ? 1 : 0], LD, 64, C, C, acc);  // dXn2 = dU · W1
-  wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, rep(gr_out.dW1, gr_out.vrs), C);
+  wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, rep(gr_out.dW1, gr_out.vrs, gr_out.slab), C, gr_out.slab);
   for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) { sF[m * LDF + n] = acc[t][i]; });
   __syncthreads();
   if constexpr (NWB == 1) tile_store<NIW>(wr[0], sW[0], LD, C, C);
@@ -767,16 +783,19 @@ __global__ __launch_bounds__(256) void post_attn_bwd_kernel(
   }
   __syncthreads();
   for (int k = threadIdx.x; k < C; k += blockDim.x) {
-    atomicAdd(rep(gr_out.dg2, gr_out.vrs) + k, sPart[1][k] + sPart[1][C + k] + sPart[1][2 * C + k] + sPart[1][3 * C + k]);
-    atomicAdd(rep(gr_out.dbe2, gr_out.vrs) + k, sPart[2][k] + sPart[2][C + k] + sPart[2][2 * C + k] + sPart[2][3 * C + k]);
-    atomicAdd(rep(gr_out.dbo, gr_out.vrs) + k, sPart[3][k] + sPart[3][C + k] + sPart[3][2 * C + k] + sPart[3][3 * C + k]);
+    gadd(rep(gr_out.dg2, gr_out.vrs, gr_out.slab) + k,
+         sPart[1][k] + sPart[1][C + k] + sPart[1][2 * C + k] + sPart[1][3 * C + k], gr_out.slab);
+    gadd(rep(gr_out.dbe2, gr_out.vrs, gr_out.slab) + k,
+         sPart[2][k] + sPart[2][C + k] + sPart[2][2 * C + k] + sPart[2][3 * C + k], gr_out.slab);
+    gadd(rep(gr_out.dbo, gr_out.vrs, gr_out.slab) + k,
+         sPart[3][k] + sPart[3][C + k] + sPart[3][2 * C + k] + sPart[3][3 * C + k], gr_out.slab);
   }
 
   // ---- out-projection
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
   tile_gemm<MAXT, true, false>(sG, LD, sW[NWB == 3 ? 2 : 0], LD, 64, C, C, acc);  // dO = dY · Wo
-  wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, rep(gr_out.dWo, gr_out.vrs), C);
+  wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, rep(gr_out.dWo, gr_out.vrs, gr_out.slab), C, gr_out.slab);
   for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) { sF[m * LDF + n] = bf2f(f2bf(acc[t][i])); });
   __syncthreads();
   {
@@ -812,9 +831,13 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
     int x_rs, const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ lnw,
     const float* __restrict__ lnb, const float* __restrict__ dres, int dres_rs, float* __restrict__ dX, int dx_rs,
     float* __restrict__ dlnw, float* __restrict__ dlnb, float* __restrict__ dW, float* __restrict__ db, int vrs,
-    int wrs, int R, PeSplit ps) {
+    int wrs, int slab, int R, PeSplit ps, SlabJob job) {
   constexpr int KP = 32 * NCH, LD = KP + 8, LDG = 64 + 8, LDF = KP + 4;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  if ((int)blockIdx.x >= (R + 63) / 64) {  // appended workgroups: the previous kernel's slab job
+    slab_reduce_block(job, blockIdx.x - (R + 63) / 64, reinterpret_cast<float4*>(smem));
+    return;
+  }
   uint16_t* sG = smem;                                   // [64][LDG]  G chunk
   uint16_t* sW = sG + 64 * LDG;                          // [64][LD]   W chunk
   uint16_t* sXn = sW + 64 * LD;                          // [64][LD]   LN(X)
@@ -873,7 +896,7 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
     }
     tile_gemm<MAXT, true, false>(sG, LDG, sW, LD, 64, KP, 64, acc);
     if (dW) {
-      wgrad_tile<MAXT>(sG, LDG, sXn, LD, 64, KP, N - nc, Kin, rep(dW, wrs) + (long long)nc * Kin, Kin);
+      wgrad_tile<MAXT>(sG, LDG, sXn, LD, 64, KP, N - nc, Kin, rep(dW, wrs, slab) + (long long)nc * Kin, Kin, slab);
       if (db) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -885,7 +908,7 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
     __syncthreads();
     if (dW && db && threadIdx.x < 64 && nc + (int)threadIdx.x < N) {
       const int t = threadIdx.x;
-      atomicAdd(rep(db, vrs) + nc + t, sPb[t] + sPb[64 + t] + sPb[128 + t] + sPb[192 + t]);
+      gadd(rep(db, vrs, slab) + nc + t, sPb[t] + sPb[64 + t] + sPb[128 + t] + sPb[192 + t], slab);
     }
   }
   for_acc<MAXT>(64, KP, [&](int t, int m, int n, int i) { sF[m * LDF + n] = acc[t][i]; });
@@ -943,8 +966,8 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
   }
   if (lnw && dlnw) {
     __syncthreads();
-    colsum_flush(sPart, KP, rep(dlnw, vrs), Kin);
-    colsum_flush(sPart + 4 * KP, KP, rep(dlnb, vrs), Kin);
+    colsum_flush(sPart, KP, rep(dlnw, vrs, slab), Kin, slab);
+    colsum_flush(sPart + 4 * KP, KP, rep(dlnb, vrs, slab), Kin, slab);
   }
 }
 
@@ -1011,7 +1034,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const TG* __restrict__ G, in
     if (r0 + 64 < r_end) fetch(r0 + 64);
     tile_gemm<MAXT, false, false>(sG, LDG, sA, LDA, 64, KP, 64, acc);
   }
-  float* dWr = rep(dW, wrs);
+  float* dWr = rep(dW, wrs, 0);
   for_acc<MAXT>(64, KP, [&](int t, int m, int n, int i) {
     const int gn = n0 + m;
     if (gn < N && n < Kin) atomicAdd(dWr + (long long)gn * Kin + n, acc[t][i]);
@@ -1025,7 +1048,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const TG* __restrict__ G, in
     __syncthreads();
     if (threadIdx.x < 64 && n0 + (int)threadIdx.x < N) {
       const int t = threadIdx.x;
-      atomicAdd(rep(db, vrs) + n0 + t, sPb[t] + sPb[64 + t] + sPb[128 + t] + sPb[192 + t]);
+      atomicAdd(rep(db, vrs, 0) + n0 + t, sPb[t] + sPb[64 + t] + sPb[128 + t] + sPb[192 + t]);
     }
   }
 }
@@ -1113,11 +1136,11 @@ void post_attn_fwd_launch(int C, const uint16_t* O, const float* X, const uint16
 void post_attn_bwd_launch(int C, const float* dZ, const float* Ysave, const float* mean2, const float* rstd2,
                           const uint16_t* U, const uint16_t* O, const uint16_t* Wo, const uint16_t* W1,
                           const uint16_t* W2, const float* g2, const float* be2, float* dY, uint16_t* dO,
-                          float* delta, int H, const PostAttnGrads& grads, int R, hipStream_t st) {
-  dim3 grid((R + 63) / 64);
+                          float* delta, int H, const PostAttnGrads& grads, int R, const SlabJob& job, hipStream_t st) {
+  dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0));
 #define PAB(CC)                                                                                                  \
   hipLaunchKernelGGL(post_attn_bwd_kernel<CC>, grid, dim3(256), 0, st, dZ, Ysave, mean2, rstd2, U, O, Wo, W1, W2, \
-                     g2, be2, dY, dO, delta, H, grads, R)
+                     g2, be2, dY, dO, delta, H, grads, R, job)
   if (C == 64) PAB(64);
   else if (C == 128) PAB(128);
   else if (C == 32) PAB(32);
@@ -1128,23 +1151,25 @@ template <typename TG, typename TX, int NCH>
 static void ln_linear_bwd_t(const void* G, int g_rs, int N, const uint16_t* W, int w_rs, int Kin, const void* X, int x_rs,
                             const float* mean, const float* rstd, const float* lnw, const float* lnb, const float* dres,
                             int dres_rs, float* dX, int dx_rs, float* dlnw, float* dlnb, float* dW, float* db, int vrs,
-                            int wrs, int R, const PeSplit& ps, hipStream_t st) {
+                            int wrs, int slab, int R, const PeSplit& ps, const SlabJob& job, hipStream_t st) {
   constexpr int KP = 32 * NCH;
   const size_t smem = 64 * 72 * 2 + 2 * 64 * (KP + 8) * 2 + 64 * (KP + 4) * 4 + 8 * KP * 4 + 4 * 64 * 4;
   auto fn = ln_linear_bwd_kernel<TG, TX, NCH>;
   set_smem_once((const void*)fn);
-  hipLaunchKernelGGL(fn, dim3((R + 63) / 64), dim3(256), smem, st, (const TG*)G, g_rs, N, W, w_rs, Kin, (const TX*)X, x_rs,
-                     mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, dlnw, dlnb, dW, db, vrs, wrs, R, ps);
+  const dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0));  // + the appended slab-job workgroups
+  hipLaunchKernelGGL(fn, grid, dim3(256), smem, st, (const TG*)G, g_rs, N, W, w_rs, Kin, (const TX*)X, x_rs,
+                     mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, dlnw, dlnb, dW, db, vrs, wrs, slab, R, ps, job);
 }
 
 template <typename TG, typename TX>
 static void ln_linear_bwd_n(int nch, const void* G, int g_rs, int N, const uint16_t* W, int w_rs, int Kin, const void* X,
                             int x_rs, const float* mean, const float* rstd, const float* lnw, const float* lnb,
                             const float* dres, int dres_rs, float* dX, int dx_rs, float* dlnw, float* dlnb, float* dW,
-                            float* db, int vrs, int wrs, int R, const PeSplit& ps, hipStream_t st) {
+                            float* db, int vrs, int wrs, int slab, int R, const PeSplit& ps, const SlabJob& job,
+                            hipStream_t st) {
 #define LNB(K)                                                                                                    \
   ln_linear_bwd_t<TG, TX, K>(G, g_rs, N, W, w_rs, Kin, X, x_rs, mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, dlnw, \
-                             dlnb, dW, db, vrs, wrs, R, ps, st)
+                             dlnb, dW, db, vrs, wrs, slab, R, ps, job, st)
   switch (nch) {
     case 1: LNB(1); break;
     case 2: LNB(2); break;
@@ -1157,13 +1182,13 @@ static void ln_linear_bwd_n(int nch, const void* G, int g_rs, int N, const uint1
 void ln_linear_bwd_launch(const void* G, bool g_bf16, int g_rs, int N, const uint16_t* W, int w_rs, int Kin, const void* X,
                           bool x_bf16, int x_rs, const float* mean, const float* rstd, const float* lnw,
                           const float* lnb, const float* dres, int dres_rs, float* dX, int dx_rs, float* dlnw,
-                          float* dlnb, float* dW, float* db, int vrs, int wrs, int R, const float* pe, int pe_rs,
-                          int pe_rows, int npix, hipStream_t st) {
+                          float* dlnb, float* dW, float* db, int vrs, int wrs, int slab, int R, const float* pe,
+                          int pe_rs, int pe_rows, int npix, const SlabJob& job, hipStream_t st) {
   const int nch = pick_nch(Kin);  // Kin ≤ 160 → ≤ 5
   const PeSplit ps{pe, pe_rs, pe_rows, npix};
 #define LDG(TG, TX)                                                                                           \
   ln_linear_bwd_n<TG, TX>(nch, G, g_rs, N, W, w_rs, Kin, X, x_rs, mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, \
-                          dlnw, dlnb, dW, db, vrs, wrs, R, ps, st)
+                          dlnw, dlnb, dW, db, vrs, wrs, slab, R, ps, job, st)
   if (g_bf16 && x_bf16) LDG(uint16_t, uint16_t);
   else if (g_bf16) LDG(uint16_t, float);
   else if (x_bf16) LDG(float, uint16_t);

@@ -60,10 +60,18 @@ def ln_linear_fwd(x, lnw, lnb, eps, w, bias, act, res, out_bf16, save_stats, pe=
     return out
 
 
+_SLAB = [False]
+
+
 def _acc(t, v):
     """t += v for a gradient target: plain (any shape with v's numel) or an (8, numel)
-    replicated accumulator (the emulation adds into replica 0)."""
-    if t.dim() == 2 and t.shape[0] == 8 and t.shape[1] == v.numel():
+    replicated accumulator (the emulation adds into replica 0).  In slab mode the target is a
+    (tiles, numel) slab view: the emulation stores the whole sum into row 0, zeros elsewhere
+    (the HIP kernels store one partial per 64-row tile; slab_reduce sums either form)."""
+    if _SLAB[0]:
+        t[0] = v.reshape(-1)
+        t[1:] = 0
+    elif t.dim() == 2 and t.shape[0] == 8 and t.shape[1] == v.numel():
         t[0] += v.reshape(-1)
     else:
         t += v.reshape(t.shape)
@@ -161,9 +169,25 @@ def _ln_bwd(dxn, x, mean, rstd, w):
     return rstd[:, None] * (g - s1 - xh * s2), xh
 
 
-def post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, be2, H, grads):
+def _run_job(job_slab, job_dsts, job_offs):
+    """the slab-reduction job a HIP backward kernel runs in its appended workgroups"""
+    if job_slab is not None:
+        slab_reduce(job_slab, job_dsts, job_offs)
+
+
+def post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, be2, H, grads, slab=False, job_slab=None, job_dsts=(),
+                  job_offs=()):
     """Returns (dy, dO, delta); parameter grads are ACCUMULATED into
-    grads = [dWo, dbo, dg2, dbe2, dW1, db1, dW2, db2]."""
+    grads = [dWo, dbo, dg2, dbe2, dW1, db1, dW2, db2] (or stored into slab views)."""
+    _run_job(job_slab, job_dsts, job_offs)
+    _SLAB[0] = slab
+    try:
+        return _post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, be2, H, grads)
+    finally:
+        _SLAB[0] = False
+
+
+def _post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, be2, H, grads):
     dWo, dbo, dg2, dbe2, dW1, db1, dW2, db2 = grads
     uf = u.float()
     dh = _bf(dz) @ _bf(w2.float())
@@ -188,9 +212,18 @@ def post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, be2, H, grads):
 
 
 def ln_linear_bwd(g, w, x, mean, rstd, lnw, lnb, dres, need_dx, dlnw=None, dlnb=None, dW=None, db=None, pe=None,
-                  kin=-1):
+                  kin=-1, slab=False, job_slab=None, job_dsts=(), job_offs=()):
     """Returns dX (or None); LN grads accumulate into dlnw / dlnb and, when given,
-    dW += gᵀ·LN(x), db += Σ_rows g."""
+    dW += gᵀ·LN(x), db += Σ_rows g (slab: stored into (tiles, ·) slab views)."""
+    _run_job(job_slab, job_dsts, job_offs)
+    _SLAB[0] = slab
+    try:
+        return _ln_linear_bwd(g, w, x, mean, rstd, lnw, lnb, dres, need_dx, dlnw, dlnb, dW, db, pe, kin)
+    finally:
+        _SLAB[0] = False
+
+
+def _ln_linear_bwd(g, w, x, mean, rstd, lnw, lnb, dres, need_dx, dlnw, dlnb, dW, db, pe, kin):
     if kin >= 0:
         w = w[:, :kin]
     gf = g.float()
@@ -330,6 +363,13 @@ def fold_replicas(grad, rep):
     n = rep.shape[1]
     grad[:n] += rep.sum(0)
     rep.zero_()
+
+
+def slab_reduce(slab, dsts, offs):
+    for d, o in zip(dsts, offs):
+        n = d.numel()
+        if n:
+            d += slab[:, o:o + n].sum(0).view(d.shape)
 
 
 def cast_bf16(x, y):

@@ -26,6 +26,7 @@ PyTorch), so the executor's bookkeeping is testable on CPU.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -34,6 +35,10 @@ import torch
 from . import emulation, ext
 
 EPS = 1e-5
+# per-tile weight-gradient partials go to a slab reduced on a side stream (see _GradSlab);
+# PERCEIVER_WGRAD_SLAB=0 restores in-kernel float atomics into the replicated accumulators
+WGRAD_SLAB = os.environ.get("PERCEIVER_WGRAD_SLAB", "1") != "0"
+TALL_ROWS = 1 << 17  # kTallRows in csrc/binding.cpp: taller projections stream their dW (wgrad kernel)
 
 
 def kernels(t: torch.Tensor):
@@ -77,6 +82,87 @@ class WeightCache:
 
 
 weight_cache = WeightCache()
+
+
+# ------------------------------------------------------------------------------------------
+# weight-gradient slabs
+# ------------------------------------------------------------------------------------------
+_pending = []          # deferred slab reductions: (K, slab, dsts, offsets, stream)
+_flush_queued = [False]
+
+
+def _flush_pending():
+    """Run every deferred slab reduction as a standalone launch (end of a backward pass)."""
+    _flush_queued[0] = False
+    while _pending:
+        K, t, ds, os_, st = _pending.pop(0)
+        if st is None:
+            K.slab_reduce(t, ds, os_)
+        else:
+            with torch.cuda.stream(st):
+                K.slab_reduce(t, ds, os_)
+
+
+def _take_job() -> dict:
+    """kwargs handing the oldest deferred slab reduction to the next backward kernel, which
+    runs it in extra workgroups appended to its own grid (csrc/common.h SlabJob)."""
+    if not _pending:
+        return {}
+    _, t, ds, os_, _ = _pending.pop(0)
+    return dict(job_slab=t, job_dsts=ds, job_offs=os_)
+
+
+class _GradSlab:
+    """(tiles, P) fp32 slab holding one backward kernel's per-64-row-tile parameter-gradient
+    partials (one row per workgroup, segments 4-float aligned).  The kernel stores its partials
+    with plain stores instead of float atomics (which run at ≈1.3 TB/s chip-wide: ≈10 µs of a
+    ≈25 µs post-attention / QKV backward at the headline shape).  ``defer`` queues the
+    reduction of the slab into the parameter gradients; the next backward kernel of the chain
+    runs it in appended workgroups, overlapped with its own latency-bound tiles, on the same
+    stream (a side-stream branch costs 10–15 µs of cross-queue hand-off per fork in a
+    replayed hipGraph).  Reductions still pending when the backward pass ends are launched by
+    an autograd final callback, so gradients are complete when ``backward()`` returns."""
+
+    def __init__(self, R: int, sizes, like: torch.Tensor):
+        self.offs, P = [], 0
+        for n in sizes:
+            self.offs.append(P)
+            P += (n + 3) // 4 * 4
+        self.sizes = list(sizes)
+        self.t = torch.empty(((R + 63) // 64, P), dtype=torch.float32, device=like.device)
+
+    def targets(self):
+        return [self.t[:, o:o + n] for o, n in zip(self.offs, self.sizes)]
+
+    def defer(self, K, dsts):
+        """dsts[i]: None (frozen: dropped), a contiguous tensor of sizes[i] elements, or a list
+        of (tensor, offset within segment i) pieces."""
+        ds, os_ = [], []
+        for i, d in enumerate(dsts):
+            if d is None:
+                continue
+            for t, extra in (d if isinstance(d, list) else [(d, 0)]):
+                ds.append(t.view(-1))
+                os_.append(self.offs[i] + extra)
+        if not ds:
+            return
+        st = torch.cuda.current_stream(self.t.device) if self.t.is_cuda else None
+        _pending.append((K, self.t, ds, os_, st))
+        if not _flush_queued[0]:
+            try:
+                torch.autograd.Variable._execution_engine.queue_callback(_flush_pending)
+                _flush_queued[0] = True
+            except RuntimeError:  # not inside a backward pass
+                _flush_pending()
+
+
+def _grad_of(p: torch.Tensor):
+    """p's fp32 gradient tensor (created if absent); None for frozen parameters."""
+    if not p.requires_grad:
+        return None
+    if p.grad is None:
+        p.grad = torch.zeros_like(p)
+    return p.grad
 
 
 # ------------------------------------------------------------------------------------------
@@ -279,8 +365,19 @@ class _LayerFn(torch.autograd.Function):
             """rows [a, b) of an (N, width) gradient target (plain or replicated)."""
             return t[:, a * width:b * width] if rep_mode else t[a:b]
 
-        dy, do, delta = K.post_attn_bwd(dz2, y, m2, r2, u, o2, wo, w1, w2, g2, be2, H,
-                                        [gb(Wo), gb(bo), gb(g2), gb(be2), gb(W1), gb(b1), gb(W2), gb(b2)])
+        def flat(p, a=None, b=None):
+            """final gradient destination p.grad (flattened [a:b]); None if p is frozen."""
+            g = _grad_of(p)
+            return None if g is None else g.view(-1)[a:b]
+
+        if WGRAD_SLAB and R < TALL_ROWS:
+            sl = _GradSlab(R, [C * C, C, C, C, C * C, C, C * C, C], dz2)
+            dy, do, delta = K.post_attn_bwd(dz2, y, m2, r2, u, o2, wo, w1, w2, g2, be2, H, sl.targets(), slab=True,
+                                            **_take_job())
+            sl.defer(K, [flat(p) for p in (Wo, bo, g2, be2, W1, b1, W2, b2)])
+        else:
+            dy, do, delta = K.post_attn_bwd(dz2, y, m2, r2, u, o2, wo, w1, w2, g2, be2, H,
+                                            [gb(Wo), gb(bo), gb(g2), gb(be2), gb(W1), gb(b1), gb(W2), gb(b2)])
         delta3 = delta.view(B, Nq, H)
         # --- attention backward + input-side projections (weight grads fused into ln_linear_bwd) ----
         if spec.cross:
@@ -298,25 +395,43 @@ class _LayerFn(torch.autograd.Function):
             dq2, dres = dq.reshape(B * Nq, C), dy
             if Bq == 1 and B > 1:
                 dq2, dres = dq.sum(0), dy.view(B, Nq, C).sum(0)
-            gbias = gb(bin_)
             Ckv = g_kv.shape[0]
-            if spec.packed:
-                gin = gb(ps[4])
-                gwq, gwkv = rows(gin, 0, C, C), rows(gin, C, 3 * C, C)
+            Rq = dq2.shape[0]
+            if WGRAD_SLAB and Rq < TALL_ROWS:
+                sl = _GradSlab(Rq, [C, C, C * C, C], dz2)
+                dx_q = K.ln_linear_bwd(dq2, wq, xq2, mean_q, rstd_q, g_q, b_q, dres, True, *sl.targets(), slab=True,
+                                       **_take_job())
+                sl.defer(K, [flat(g_q), flat(b_q), flat(ps[4], 0, C * C), flat(bin_, 0, C)])
             else:
-                gwq = gb(ps[4])
-                gwkv = torch.zeros((8, 2 * C * Ckv) if rep_mode else (2 * C, Ckv), **f32)
-            dx_q = K.ln_linear_bwd(dq2, wq, xq2, mean_q, rstd_q, g_q, b_q, dres, True, gb(g_q), gb(b_q), gwq,
-                                   rows(gbias, 0, C, 1))
+                gwq = rows(gb(ps[4]), 0, C, C) if spec.packed else gb(ps[4])
+                dx_q = K.ln_linear_bwd(dq2, wq, xq2, mean_q, rstd_q, g_q, b_q, dres, True, gb(g_q), gb(b_q), gwq,
+                                       rows(gb(bin_), 0, C, 1))
             dx_kv = None
             if ctx.kv_owner:  # the projection's backward, once, over the summed dK/dV
                 dkv2 = dkv.view(B * M, 2 * C)
-                dx_kv = K.ln_linear_bwd(dkv2, wkv, xkv2, mean_kv, rstd_kv, g_kv, b_kv, None, ctx.kv_grad, gb(g_kv),
-                                        gb(b_kv), gwkv, rows(gbias, C, 3 * C, 1), ctx.kv_pe, Ckv)
+                Rkv = dkv2.shape[0]
+                if WGRAD_SLAB and Rkv < TALL_ROWS:
+                    sl = _GradSlab(Rkv, [Ckv, Ckv, 2 * C * Ckv, 2 * C], dz2)
+                    dx_kv = K.ln_linear_bwd(dkv2, wkv, xkv2, mean_kv, rstd_kv, g_kv, b_kv, None, ctx.kv_grad,
+                                            *sl.targets(), ctx.kv_pe, Ckv, slab=True, **_take_job())
+                    if spec.packed:
+                        dwkv = flat(ps[4], C * C, 3 * C * C)
+                    else:
+                        gk, gv = flat(ps[5]), flat(ps[6])
+                        dwkv = [(t, o) for t, o in ((gk, 0), (gv, C * Ckv)) if t is not None] or None
+                    sl.defer(K, [flat(g_kv), flat(b_kv), dwkv, flat(bin_, C, 3 * C)])
+                else:
+                    gbias = gb(bin_)
+                    if spec.packed:
+                        gwkv = rows(gb(ps[4]), C, 3 * C, C)
+                    else:
+                        gwkv = torch.zeros((8, 2 * C * Ckv) if rep_mode else (2 * C, Ckv), **f32)
+                    dx_kv = K.ln_linear_bwd(dkv2, wkv, xkv2, mean_kv, rstd_kv, g_kv, b_kv, None, ctx.kv_grad,
+                                            gb(g_kv), gb(b_kv), gwkv, rows(gbias, C, 3 * C, 1), ctx.kv_pe, Ckv)
+                    if not spec.packed:
+                        gb(ps[5]).add_(rows(gwkv, 0, C, Ckv))
+                        gb(ps[6]).add_(rows(gwkv, C, 2 * C, Ckv))
                 ent["dkv"] = None
-                if not spec.packed:
-                    gb(ps[5]).add_(rows(gwkv, 0, C, Ckv))
-                    gb(ps[6]).add_(rows(gwkv, C, 2 * C, Ckv))
             dx_q = dx_q.view(Bq, Nq, C)
             dx_kv = dx_kv.view(B, M, -1) if (ctx.kv_grad and dx_kv is not None) else None
         else:
@@ -325,8 +440,14 @@ class _LayerFn(torch.autograd.Function):
             K.attn_bwd(qkv3[:, :, :C], qkv3[:, :, C:2 * C], qkv3[:, :, 2 * C:], kmask, o, do.view(B, Nq, C), lse,
                        delta3, H, D, scale, ctx.p_attn, ctx.seed, dqkv[:, :, :C], dqkv[:, :, C:2 * C],
                        dqkv[:, :, 2 * C:])
-            dx_q = K.ln_linear_bwd(dqkv.view(R, 3 * C), wq, xq2, mean_q, rstd_q, g_q, b_q, dy, True, gb(g_q), gb(b_q),
-                                   gb(ps[2]), gb(ps[3]))
+            if WGRAD_SLAB and R < TALL_ROWS:
+                sl = _GradSlab(R, [C, C, 3 * C * C, 3 * C], dz2)
+                dx_q = K.ln_linear_bwd(dqkv.view(R, 3 * C), wq, xq2, mean_q, rstd_q, g_q, b_q, dy, True, *sl.targets(),
+                                       slab=True, **_take_job())
+                sl.defer(K, [flat(g_q), flat(b_q), flat(ps[2]), flat(ps[3])])
+            else:
+                dx_q = K.ln_linear_bwd(dqkv.view(R, 3 * C), wq, xq2, mean_q, rstd_q, g_q, b_q, dy, True, gb(g_q),
+                                       gb(b_q), gb(ps[2]), gb(ps[3]))
             dx_q = dx_q.view(B, Nq, C)
             dx_kv = None
         # parameter gradients were accumulated in place (no autograd AccumulateGrad pass)

@@ -165,6 +165,27 @@ def test_post_attn(C, H):
     ga, gb = outs
     for i, n in enumerate(("dy", "dO", "delta") + names):
         close(ga[i], gb[i], 3e-2, n)
+    # slab sink: one partial row per 64-row tile (plain stores, NaN-initialised slab), then
+    # slab_reduce onto the same 0.5-initialised destinations
+    sizes = [C * C if n.startswith("dW") else C for n in names]
+    offs = [sum(sizes[:i]) for i in range(8)]
+    slab = torch.full(((R + 63) // 64, sum(sizes)), float("nan"), device=DEV)
+    views = [slab[:, o:o + n] for o, n in zip(offs, sizes)]
+    outs_s = _ext().post_attn_bwd(dz, y, m, r, u, o, ws[0], ws[1], ws[2], g2, be2, H, views, slab=True)
+    assert torch.isfinite(slab).all()  # every tile wrote every element of its row
+    dst = [torch.full((C, C) if n.startswith("dW") else (C,), 0.5, device=DEV) for n in names]
+    _ext().slab_reduce(slab, dst, offs)
+    for i, n in enumerate(("dy", "dO", "delta")):
+        close(outs_s[i], gb[i], 3e-2, n + " (slab)")
+    for i, n in enumerate(names):
+        close(dst[i], gb[3 + i], 3e-2, n + " (slab)")
+    # the same reduction as a job run by the appended workgroups of the next backward kernel
+    dst2 = [torch.full((C, C) if n.startswith("dW") else (C,), 0.5, device=DEV) for n in names]
+    scratch = [torch.zeros_like(t) for t in dst2]
+    _ext().post_attn_bwd(dz, y, m, r, u, o, ws[0], ws[1], ws[2], g2, be2, H, scratch, job_slab=slab,
+                         job_dsts=[t.view(-1) for t in dst2], job_offs=offs)
+    for i, n in enumerate(names):
+        close(dst2[i], gb[3 + i], 3e-2, n + " (slab job)")
 
 
 @pytest.mark.parametrize("R,N,Kin,gbf", [(300, 192, 64, False), (200, 128, 131, False), (129, 64, 64, True)])
@@ -187,6 +208,29 @@ def test_ln_linear_bwd_and_wgrad(R, N, Kin, gbf):
         res.append((dx, dg, db, dW, dbias))
     for i, n in enumerate(("dx", "dgamma", "dbeta", "dW", "dbias")):
         close(res[0][i], res[1][i], 3e-2 if i < 4 else 1e-4, n)
+    # slab sink (segments 4-aligned, odd Kin included) + slab_reduce
+    sizes = [Kin, Kin, N * Kin, N]
+    offs, P = [], 0
+    for n_ in sizes:
+        offs.append(P)
+        P += (n_ + 3) // 4 * 4
+    slab = torch.full(((R + 63) // 64, P), float("nan"), device=DEV)
+    views = [slab[:, o:o + n_] for o, n_ in zip(offs, sizes)]
+    dx_s = _ext().ln_linear_bwd(g, w, x, mean, rstd, lw, lb, dres, True, *views, slab=True)
+    dst = [torch.zeros(Kin, device=DEV), torch.zeros(Kin, device=DEV), torch.ones(N, Kin, device=DEV),
+           torch.ones(N, device=DEV)]
+    _ext().slab_reduce(slab, dst, offs)
+    close(dx_s, res[1][0], 3e-2, "dx (slab)")
+    for i, n in enumerate(("dgamma", "dbeta", "dW", "dbias")):
+        close(dst[i], res[1][i + 1], 3e-2 if i < 3 else 1e-4, n + " (slab)")
+    dst2 = [torch.zeros(Kin, device=DEV), torch.zeros(Kin, device=DEV), torch.ones(N, Kin, device=DEV),
+            torch.ones(N, device=DEV)]
+    dx_j = _ext().ln_linear_bwd(g, w, x, mean, rstd, lw, lb, dres, True, torch.zeros(Kin, device=DEV),
+                                torch.zeros(Kin, device=DEV), None, None, job_slab=slab,
+                                job_dsts=[t.view(-1) for t in dst2], job_offs=offs)
+    close(dx_j, res[1][0], 3e-2, "dx (with job)")
+    for i, n in enumerate(("dgamma", "dbeta", "dW", "dbias")):
+        close(dst2[i], res[1][i + 1], 3e-2 if i < 3 else 1e-4, n + " (slab job)")
     # no-dx / no-LN variants
     for K in (_ext(), _emu()):
         assert K.ln_linear_bwd(g, w, x, None, None, None, None, None, False, None, None, None, None) is None

@@ -164,8 +164,10 @@ def test_reference_backend_matches_nn_multihead_attention():
         assert torch.allclose(mha(q, kv, pad), want, atol=1e-6)
 
 
+@pytest.mark.parametrize("slab", [True, False])
 @pytest.mark.parametrize("kind", ["mlm", "image"])
-def test_fused_executor_matches_eager_via_emulation(kind):
+def test_fused_executor_matches_eager_via_emulation(kind, slab, monkeypatch):
+    monkeypatch.setattr(ops.fused, "WGRAD_SLAB", slab)
     torch.manual_seed(3)
     if kind == "mlm":
         m = mlm_model()
@@ -192,12 +194,15 @@ def test_fused_executor_matches_eager_via_emulation(kind):
             assert (p.grad - g_ref[n]).abs().max() < 0.03 * gmax, n
 
 
-def test_fused_executor_replicated_gradients_fold_to_eager():
+@pytest.mark.parametrize("slab", [False, True])
+def test_fused_executor_replicated_gradients_fold_to_eager(slab, monkeypatch):
     """Flat parameter space with 8-way replicated gradient accumulators for the fused layers:
     after fold() the gradients equal the eager ones, and non-layer parameters are untouched
-    by the replica mechanism."""
+    by the replica mechanism.  With per-tile slabs (slab=True) the layer gradients bypass the
+    replicas and land in the flat gradient through slab_reduce."""
     from perceiver_io_amd.ops.optim import FlatParameterSpace
 
+    monkeypatch.setattr(ops.fused, "WGRAD_SLAB", slab)
     torch.manual_seed(4)
     m = mlm_model()
     x = torch.randint(3, 300, (3, 64))
@@ -215,7 +220,10 @@ def test_fused_executor_replicated_gradients_fold_to_eager():
     flat.zero_grad()
     fused = ops.fused.encoder_forward(enc, x, pad)
     (fused * w).sum().backward()
-    assert flat.grad_rep.abs().sum() > 0  # layer kernels accumulated into the replicas
+    if not slab:
+        assert flat.grad_rep.abs().sum() > 0  # layer kernels accumulated into the replicas
+    else:
+        assert flat.grad_rep.abs().sum() == 0 and flat.grad.abs().sum() > 0
     flat.fold()
     assert flat.grad_rep.abs().sum() == 0
     gmax = max(g.abs().max() for g in g_ref.values())

@@ -43,6 +43,8 @@ for step in "$@"; do
     ddp2)     run ddp2 600 env PERCEIVER_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 3 ;;
     trace)    for t in tools/trace/*_trace; do run "trace_$(basename $t)" 120 $t; done ;;
     pmc_trace) run pmc_trace 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES --output-format csv -d gpurun_out/pmc_trace -o pmc -- tools/trace/attn_bwd_trace ;;
+    bench_noslab) run bench_noslab 600 env PERCEIVER_WGRAD_SLAB=0 python bench.py --steps 20 --warmup 5 ;;
+    prof_noslab) run prof_noslab 600 env PERCEIVER_WGRAD_SLAB=0 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_noslab -o run --output-format csv -- python bench.py --steps 5 --warmup 3 ;;
     prof)     run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 3 ;;
     dbg0)     run dbg0 300 env AMD_SERIALIZE_KERNEL=3 python tools/debug_engine.py 0 ;;
     dbg1)     run dbg1 300 python tools/debug_engine.py 1 ;;

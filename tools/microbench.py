@@ -81,6 +81,30 @@ def main():
     wq_r, bq_r, g_r, b_r = take(3 * C * C), take(3 * C), take(C), take(C)
     res["ln_linear_bwd qkv (all targets replicated)"] = timeit(
         lambda: K.ln_linear_bwd(g, wqkv, x, mean, rstd, g1, b1, dy, True, g_r, b_r, wq_r, bq_r))
+    # per-tile slab sinks (plain stores) + the side-stream reduction, timed separately
+    nt = (R + 63) // 64
+    pa_sizes = [C * C, C, C, C, C * C, C, C * C, C]
+    pa_offs = [sum(pa_sizes[:i]) for i in range(8)]
+    pa_slab = torch.empty(nt, sum(pa_sizes), device=dev)
+    pa_views = [pa_slab[:, o:o + n] for o, n in zip(pa_offs, pa_sizes)]
+    res["post_attn_bwd (slab)"] = timeit(
+        lambda: K.post_attn_bwd(dz, y, m2, r2, u, o2, ws[0], ws[1], ws[2], g2, be2, H, pa_views, slab=True))
+    res["slab_reduce post_attn"] = timeit(lambda: K.slab_reduce(pa_slab, [g.view(-1) for g in grads], pa_offs))
+    ll_sizes = [C, C, 3 * C * C, 3 * C]
+    ll_offs = [sum(ll_sizes[:i]) for i in range(4)]
+    ll_slab = torch.empty(nt, sum(ll_sizes), device=dev)
+    ll_views = [ll_slab[:, o:o + n] for o, n in zip(ll_offs, ll_sizes)]
+    res["ln_linear_bwd qkv (slab)"] = timeit(
+        lambda: K.ln_linear_bwd(g, wqkv, x, mean, rstd, g1, b1, dy, True, *ll_views, slab=True))
+    res["slab_reduce qkv"] = timeit(lambda: K.slab_reduce(ll_slab, [dg, db_, dW.view(-1), dbias], ll_offs))
+    pa_dsts = [t.view(-1) for t in grads]
+    res["ln_linear_bwd qkv (slab) + post_attn job"] = timeit(
+        lambda: K.ln_linear_bwd(g, wqkv, x, mean, rstd, g1, b1, dy, True, *ll_views, slab=True, job_slab=pa_slab,
+                                job_dsts=pa_dsts, job_offs=pa_offs))
+    ll_dsts = [dg, db_, dW.view(-1), dbias]
+    res["post_attn_bwd (slab) + qkv job"] = timeit(
+        lambda: K.post_attn_bwd(dz, y, m2, r2, u, o2, ws[0], ws[1], ws[2], g2, be2, H, pa_views, slab=True,
+                                job_slab=ll_slab, job_dsts=ll_dsts, job_offs=ll_offs))
     for k_, v_ in res.items():
         print(f"{k_:45s} {v_:8.2f} us")
 
