@@ -52,10 +52,11 @@ void wgrad_launch(const void*, bool, int, int, const void*, bool, int, int, int,
 void ce_fwd_launch(int, const uint16_t*, const int64_t*, const uint16_t*, const float*, int, int, float*, float*,
                    float*, float*, int, hipStream_t);
 int ce_num_splits(int, int);
+int ce_dw_splits(int, int);
 void mlm_select_launch(const int64_t*, int, int, int, int, int64_t*, int64_t*, int*, int64_t*, int64_t*, float*, bool*,
                        hipStream_t);
 void ce_bwd_launch(int, const uint16_t*, const int64_t*, const uint16_t*, const float*, const float*, const float*,
-                   int, int, float*, const int64_t*, float*, float*, int, hipStream_t);
+                   int, int, float*, const int64_t*, float*, float*, int, float*, hipStream_t);
 void embed_fwd_launch(const int64_t*, const float*, const float*, float*, long long, int, int, float, hipStream_t);
 void embed_bwd_launch(const int64_t*, const float*, float*, float*, int, int, int, float, hipStream_t);
 void embed_bwd_sorted_launch(const int64_t*, const int64_t*, const float*, float*, long long, int, float, hipStream_t);
@@ -440,9 +441,11 @@ std::vector<Tensor> ce_fwd(Tensor h, Tensor labels, Tensor w, Tensor bias) {
 }
 
 // dH (+)= rows: row r of the compacted batch lands in dH[rowmap[r]] when rowmap is given
-// (dH then has the full (positions, C) shape), else in dH[r]; dW / db accumulate or overwrite
-void ce_bwd(Tensor h, Tensor labels, Tensor w, Tensor bias, Tensor lse, Tensor gscale, Tensor dH, Tensor dW, Tensor db,
-            bool accumulate, OptT rowmap) {
+// (dH then has the full (positions, C) shape), else in dH[r]; dW / db accumulate or overwrite.
+// slab: the dW kernel stores its row-split partials into a returned (splits, V·C + V₄) slab
+// instead of adding them (the caller sums it into dW | db with a slab job, offsets 0 and V·C).
+OptT ce_bwd(Tensor h, Tensor labels, Tensor w, Tensor bias, Tensor lse, Tensor gscale, Tensor dH, Tensor dW, Tensor db,
+            bool accumulate, OptT rowmap, bool slab) {
   const int M = (int)h.size(0), C = (int)h.size(1), V = (int)w.size(0);
   TORCH_CHECK(dH.is_contiguous() && dW.is_contiguous() && db.is_contiguous());
   TORCH_CHECK(dH.dim() == 2 && dH.size(1) == C, "dH must be (rows, C)");
@@ -454,8 +457,13 @@ void ce_bwd(Tensor h, Tensor labels, Tensor w, Tensor bias, Tensor lse, Tensor g
   } else {
     TORCH_CHECK(dH.size(0) == M, "dH must be (M, C) without a rowmap");
   }
+  Tensor sl;
+  if (slab) sl = torch::empty({pio::ce_dw_splits(M, V), (int64_t)V * C + ((V + 3) & ~3)}, dW.options());
   pio::ce_bwd_launch(C, bfp(h), labels.data_ptr<int64_t>(), bfp(w), f32p(bias), f32p(lse), f32p(gscale), M, V,
-                     dH.data_ptr<float>(), rm, dW.data_ptr<float>(), db.data_ptr<float>(), accumulate ? 1 : 0, stream());
+                     dH.data_ptr<float>(), rm, dW.data_ptr<float>(), db.data_ptr<float>(), accumulate ? 1 : 0,
+                     slab ? sl.data_ptr<float>() : nullptr, stream());
+  if (slab) return sl;
+  return c10::nullopt;
 }
 
 Tensor embed_fwd(Tensor ids, Tensor E, Tensor P, double scale) {
@@ -562,7 +570,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("kin") = -1);
   m.def("mlm_select", &mlm_select);
   m.def("ce_fwd", &ce_fwd);
-  m.def("ce_bwd", &ce_bwd);
+  m.def("ce_bwd", &ce_bwd, py::arg("h"), py::arg("labels"), py::arg("w"), py::arg("bias"), py::arg("lse"),
+        py::arg("gscale"), py::arg("dH"), py::arg("dW"), py::arg("db"), py::arg("accumulate"),
+        py::arg("rowmap") = py::none(), py::arg("slab") = false);
   m.def("embed_fwd", &embed_fwd);
   m.def("embed_bwd", &embed_bwd);
   m.def("text_mask", &text_mask);

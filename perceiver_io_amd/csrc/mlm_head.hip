@@ -4,9 +4,9 @@
 // rearrange + nn.CrossEntropyLoss(ignore_index=-100) (perceiver/lightning.py:223-226), which
 // materialises (B, V, L) fp32 logits (20.5 MB/sample at L=512) plus a contiguous copy.
 // Here logits exist only as MFMA accumulator tiles:
-//   fwd  : per (64-row tile, vocab split): logits = H·Wᵀ + b tile by tile, running
-//          per-lane (max, sum-exp) with a deferred-rescale online logsumexp, label logit
-//          picked in passing; a combine kernel merges splits → per-row loss and LSE.
+//   fwd  : per (64-row tile, vocab split): transposed logit tiles (W·Hᵀ: one row per lane),
+//          running per-lane (max, sum-exp2) online logsumexp, label logit picked in passing;
+//          a combine kernel merges splits → per-row loss and LSE.
 //   bwd-a: dH  = (softmax − onehot)·g · W   (rows × vocab split, fp32 atomics into dH)
 //   bwd-b: dW  = (softmax − onehot)ᵀ·g · H, db = Σ rows   (vocab chunk × row split, fp32 atomics)
 // Streamed operands (W chunks, H tiles) are register-prefetched one tile ahead.
@@ -18,15 +18,48 @@ namespace pio {
 constexpr int HB = 64;  // rows per tile
 constexpr int VB = 64;  // vocab entries per tile
 
-// logits tile for rows [m0, m0+64) × vocab [v0, v0+64): 4 sub-tiles, one per wave
-// A = H tile [r][c] (k-contiguous), B = W chunk [v][c] (k-contiguous)
+// Transposed logits tile (vocab on the accumulator rows, the query row on the lane):
+// wave w covers vocab [v0 + 32(w & 1), +32) × rows [m0 + 32(w >> 1), +32) of a 64 × 64 tile;
+// lane l holds row 32(w >> 1) + (l & 31) and the 16 vocab entries 32(w & 1) + acc_row(i, l >> 5).
+// With every value of a lane belonging to ONE row, the softmax statistics need no cross-lane
+// work inside the vocab loop: one max over 16 registers, one rescale exp per tile, and one
+// v_exp_f32 per logit (log2 domain) — ≈4 VALU instructions per logit instead of ≈20.
+// A = W chunk [v][c], B = H tile [r][c] (both k-contiguous).
+constexpr float kL2E = 1.4426950408889634f;
+constexpr float kLN2 = 0.6931471805599453f;
 template <int C>
-__device__ __forceinline__ f32x16 logits_tile(const uint16_t* sH, const uint16_t* sW, int ld) {
+__device__ __forceinline__ f32x16 logits_tile_t(const uint16_t* sH, const uint16_t* sW, int ld) {
   const int w = wave_id();
   f32x16 acc = f32x16{};
 #pragma unroll
-  for (int k0 = 0; k0 < C; k0 += 16) acc = mfma32(frag_kc(sH, ld, 32 * (w >> 1), k0), frag_kc(sW, ld, 32 * (w & 1), k0), acc);
+  for (int k0 = 0; k0 < C; k0 += 16) acc = mfma32(frag_kc(sW, ld, 32 * (w & 1), k0), frag_kc(sH, ld, 32 * (w >> 1), k0), acc);
   return acc;
+}
+// the 16 per-register values of a 64-entry LDS vector (vocab-indexed) for this lane:
+// register i <-> entry 32(w & 1) + 4h + (i & 3) + 8(i >> 2): four 16-byte reads
+__device__ __forceinline__ void vocab_regs(const float* sv, float (&out)[16]) {
+  const float* p = sv + 32 * (wave_id() & 1) + 4 * (lane_id() >> 5);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 v = *reinterpret_cast<const float4*>(p + 8 * q);
+    out[4 * q] = v.x; out[4 * q + 1] = v.y; out[4 * q + 2] = v.z; out[4 * q + 3] = v.w;
+  }
+}
+// register of this lane holding entry j of the wave's 32-entry vocab block, or -1
+__device__ __forceinline__ int vocab_reg(int j) {
+  if (j < 0 || j >= 32 || ((j >> 2) & 1) != (lane_id() >> 5)) return -1;
+  return (j & 3) + 4 * (j >> 3);
+}
+// this lane's row of a dl tile -> LDS [row][vocab] bf16, four 8-byte writes
+__device__ __forceinline__ void store_dl_row(uint16_t* sL, int ldl, int row, const float (&d)[16]) {
+  uint16_t* p = sL + row * ldl + 32 * (wave_id() & 1) + 4 * (lane_id() >> 5);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint2 pk;
+    pk.x = pack2(d[4 * q], d[4 * q + 1]);
+    pk.y = pack2(d[4 * q + 2], d[4 * q + 3]);
+    *reinterpret_cast<uint2*>(p + 8 * q) = pk;
+  }
 }
 
 template <int C>
@@ -70,63 +103,73 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const uint16_t* __restrict_
   constexpr int LD = C + 8;
   __shared__ __attribute__((aligned(16))) uint16_t sH[HB * LD];
   __shared__ __attribute__((aligned(16))) uint16_t sW[VB * LD];
+  __shared__ __attribute__((aligned(16))) float sB[VB];  // bias * log2e of the chunk (-inf past V)
   __shared__ float sMS[2][64][2];
-  const int w = wave_id(), l = lane_id(), hh = l >> 5;
+  const int w = wave_id(), l = lane_id();
   const int m0 = blockIdx.x * HB, split = blockIdx.y;
   const int nchunks = (V + VB - 1) / VB;
   const int c_begin = split * chunks_per_split, c_end = min(nchunks, c_begin + chunks_per_split);
   stage_rows<C>(sH, LD, Hm, m0, M);
-  int lab[16];
-  float m[16], s[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int gr = m0 + 32 * (w >> 1) + acc_row(i, hh);
-    lab[i] = gr < M ? (int)labels[gr] : -100;
-    m[i] = -1e30f;
-    s[i] = 0.f;
-  }
+  const int rl = 32 * (w >> 1) + (l & 31), gr = m0 + rl;
+  const int lab = gr < M ? (int)labels[gr] : -100;
+  float m = -1e30f, s = 0.f;  // log2-domain running max / sum of 2^(t - m) over this lane's logits
   bf16x8 wr[C / 32];
-  if (c_begin < c_end) fetch_rows<C>(wr, W, c_begin * VB, V);
+  float bnext = 0.f;
+  auto fetch = [&](int c) {
+    fetch_rows<C>(wr, W, c * VB, V);
+    const int v = c * VB + threadIdx.x;
+    if (threadIdx.x < VB) bnext = v < V ? bias[v] * kL2E : -__builtin_inff();
+  };
+  if (c_begin < c_end) fetch(c_begin);
   for (int c = c_begin; c < c_end; ++c) {
     const int v0 = c * VB;
     __syncthreads();
     store_rows<C>(wr, sW, LD);
+    if (threadIdx.x < VB) sB[threadIdx.x] = bnext;
     __syncthreads();
-    if (c + 1 < c_end) fetch_rows<C>(wr, W, v0 + VB, V);
-    const int col = v0 + 32 * (w & 1) + (l & 31);
-    const bool valid = col < V;
-    const float bv = valid ? bias[col] : 0.f;
-    const f32x16 acc = logits_tile<C>(sH, sW, LD);
+    if (c + 1 < c_end) fetch(c + 1);
+    const f32x16 acc = logits_tile_t<C>(sH, sW, LD);
+    float t[16];
+    vocab_regs(sB, t);
+    float mt = -__builtin_inff();
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      if (valid) {
-        const float v = acc[i] + bv;
-        if (v > m[i]) { s[i] *= __expf(m[i] - v); m[i] = v; }
-        s[i] += __expf(v - m[i]);
-        if (col == lab[i]) picked[m0 + 32 * (w >> 1) + acc_row(i, hh)] = v;
-      }
+      t[i] = fmaf(acc[i], kL2E, t[i]);
+      mt = fmaxf(mt, t[i]);
+    }
+    const float mn = fmaxf(m, mt);
+    float acc_s = s * fast_exp2(m - mn);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc_s += fast_exp2(t[i] - mn);
+    s = acc_s;
+    m = mn;
+    const int ri = vocab_reg(lab - v0 - 32 * (w & 1));
+    if (ri >= 0) {  // this lane holds the label's logit (stored in natural units)
+      float pv = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) pv = i == ri ? t[i] : pv;
+      picked[gr] = pv * kLN2;
     }
   }
-  // combine over the 32 lanes of each half (same rows), then the two waves sharing rows
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const float mm = half_max(m[i]);
-    const float ss = half_sum(s[i] * __expf(m[i] - mm));
-    if ((l & 31) == 0) {
-      const int rr = 32 * (w >> 1) + acc_row(i, hh);
-      sMS[w & 1][rr][0] = mm;
-      sMS[w & 1][rr][1] = ss;
-    }
+  // merge the two lanes of each row (l, l ^ 32), then the two waves sharing the rows
+  float ma, mb, sa, sb;
+  xor32_pair(m, ma, mb);
+  xor32_pair(s, sa, sb);
+  const float mm = fmaxf(ma, mb);
+  const float ss = sa * fast_exp2(ma - mm) + sb * fast_exp2(mb - mm);
+  if (l < 32) {
+    sMS[w & 1][rl][0] = mm;
+    sMS[w & 1][rl][1] = ss;
   }
   __syncthreads();
   if (threadIdx.x < 64) {
-    const int rr = threadIdx.x, gr = m0 + rr;
-    if (gr < M) {
+    const int rr = threadIdx.x, g = m0 + rr;
+    if (g < M) {
       const float m1 = sMS[0][rr][0], m2 = sMS[1][rr][0];
-      const float mm = fmaxf(m1, m2);
-      const float ss = sMS[0][rr][1] * __expf(m1 - mm) + sMS[1][rr][1] * __expf(m2 - mm);
-      part_ms[((long long)split * M + gr) * 2] = mm;
-      part_ms[((long long)split * M + gr) * 2 + 1] = ss;
+      const float mx = fmaxf(m1, m2);
+      const float sx = sMS[0][rr][1] * fast_exp2(m1 - mx) + sMS[1][rr][1] * fast_exp2(m2 - mx);
+      part_ms[((long long)split * M + g) * 2] = mx * kLN2;  // natural-log units for the combine
+      part_ms[((long long)split * M + g) * 2 + 1] = sx;
     }
   }
 }
@@ -146,12 +189,20 @@ __global__ void ce_combine_kernel(const float* __restrict__ part_ms, const float
   loss_rows[r] = labels[r] >= 0 ? L - picked[r] : 0.f;
 }
 
-// dlogit for one accumulator element
-__device__ __forceinline__ float dlogit(float v, float lse, int col, int lab, float g) {
-  return lab < 0 ? 0.f : (__expf(v - lse) - (col == lab ? 1.f : 0.f)) * g;
+// dl = (softmax - onehot) * g for the 16 logits of this lane's row (transposed tile):
+// d_i = 2^(acc_i * log2e + b_i - lse * log2e) * g, minus g at the label's entry.  g = 0 for
+// ignored rows (label -100: unselected positions and compaction padding).
+__device__ __forceinline__ void dl_regs(const f32x16& acc, const float (&b)[16], float lse_l2, float g, int lab_reg,
+                                        float (&d)[16]) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) d[i] = fast_exp2(fmaf(acc[i], kL2E, b[i] - lse_l2)) * g;
+  if (lab_reg >= 0) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) d[i] -= i == lab_reg ? g : 0.f;
+  }
 }
 
-// bwd-a: dH[r][c] += Σ_v dl[r][v] W[v][c]  over this split's vocab chunks (fp32 atomics)
+// bwd-a: dH[r][c] += sum_v dl[r][v] W[v][c]  over this split's vocab chunks (fp32 atomics)
 template <int C>
 __global__ __launch_bounds__(256) void ce_bwd_dh_kernel(const uint16_t* __restrict__ Hm,
                                                         const int64_t* __restrict__ labels,
@@ -163,50 +214,48 @@ __global__ __launch_bounds__(256) void ce_bwd_dh_kernel(const uint16_t* __restri
   __shared__ __attribute__((aligned(16))) uint16_t sH[HB * LD];
   __shared__ __attribute__((aligned(16))) uint16_t sW[VB * LD];
   __shared__ __attribute__((aligned(16))) uint16_t sL[HB * LDL];
-  __shared__ long long sDst[HB];  // dH row of each tile row (−1: ignored row)
+  __shared__ __attribute__((aligned(16))) float sB[VB];
+  __shared__ long long sDst[HB];  // dH row of each tile row (-1: ignored row)
   const int w = wave_id(), l = lane_id(), hh = l >> 5;
   const int m0 = blockIdx.x * HB, split = blockIdx.y;
   const int nchunks = (V + VB - 1) / VB;
   const int c_begin = split * chunks_per_split, c_end = min(nchunks, c_begin + chunks_per_split);
-  const float g = gscale[0];
   stage_rows<C>(sH, LD, Hm, m0, M);
   if (threadIdx.x < HB) {
     const int gr = m0 + threadIdx.x;
     sDst[threadIdx.x] = (gr < M && labels[gr] >= 0) ? (rowmap ? rowmap[gr] : gr) : -1;
   }
-  int lab[16];
-  float ls[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int gr = m0 + 32 * (w >> 1) + acc_row(i, hh);
-    lab[i] = gr < M ? (int)labels[gr] : -100;
-    ls[i] = gr < M ? lse[gr] : 0.f;
-  }
-  // output dH tile 64 × C: sub-tiles (2 × NT), wave w owns tiles w, w+4
+  const int rl = 32 * (w >> 1) + (l & 31), gr = m0 + rl;
+  const int lab = gr < M ? (int)labels[gr] : -100;
+  const float lse_l2 = gr < M ? lse[gr] * kL2E : 0.f;
+  const float g = lab >= 0 ? gscale[0] : 0.f;
+  // output dH tile 64 x C: sub-tiles (2 x NT), wave w owns tiles w, w+4
   constexpr int MAXT = (2 * NT + 3) / 4;
   f32x16 acc_o[MAXT];
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc_o[t] = f32x16{};
   bf16x8 wr[C / 32];
-  if (c_begin < c_end) fetch_rows<C>(wr, W, c_begin * VB, V);
+  float bnext = 0.f;
+  auto fetch = [&](int c) {
+    fetch_rows<C>(wr, W, c * VB, V);
+    const int v = c * VB + threadIdx.x;
+    if (threadIdx.x < VB) bnext = v < V ? bias[v] * kL2E : -__builtin_inff();
+  };
+  if (c_begin < c_end) fetch(c_begin);
   for (int c = c_begin; c < c_end; ++c) {
     const int v0 = c * VB;
     __syncthreads();
     store_rows<C>(wr, sW, LD);
+    if (threadIdx.x < VB) sB[threadIdx.x] = bnext;
     __syncthreads();
-    if (c + 1 < c_end) fetch_rows<C>(wr, W, v0 + VB, V);
-    const int coll = 32 * (w & 1) + (l & 31);
-    const int col = v0 + coll;
-    const bool valid = col < V;
-    const float bv = valid ? bias[col] : 0.f;
-    const f32x16 acc = logits_tile<C>(sH, sW, LD);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float d = valid ? dlogit(acc[i] + bv, ls[i], col, lab[i], g) : 0.f;
-      sL[(32 * (w >> 1) + acc_row(i, hh)) * LDL + coll] = f2bf(d);
-    }
+    if (c + 1 < c_end) fetch(c + 1);
+    const f32x16 acc = logits_tile_t<C>(sH, sW, LD);
+    float b[16], d[16];
+    vocab_regs(sB, b);
+    dl_regs(acc, b, lse_l2, g, vocab_reg(lab - v0 - 32 * (w & 1)), d);
+    store_dl_row(sL, LDL, rl, d);
     __syncthreads();
-    // dH += dl (64 × 64 vocab) · Wchunk (64 vocab × C): A k-contiguous, B = W[v][c] k-strided
+    // dH += dl (64 x 64 vocab) . Wchunk (64 vocab x C): A k-contiguous, B = W[v][c] k-strided
 #pragma unroll
     for (int t = 0; t < MAXT; ++t) {
       const int tg = w + 4 * t;
@@ -225,7 +274,7 @@ __global__ __launch_bounds__(256) void ce_bwd_dh_kernel(const uint16_t* __restri
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         // dH row: the compacted row's source position (rowmap) or the row itself; ignored rows
-        // (label −100, incl. compaction padding) carry no gradient
+        // (label -100, incl. compaction padding) carry no gradient
         const long long dst = sDst[r0 + acc_row(i, hh)];
         if (dst >= 0) atomicAdd(dH + dst * C + n0 + (l & 31), acc_o[t][i]);
       }
@@ -233,7 +282,7 @@ __global__ __launch_bounds__(256) void ce_bwd_dh_kernel(const uint16_t* __restri
   }
 }
 
-// bwd-b: dW[v][c] += Σ_r dl[r][v] H[r][c], db[v] += Σ_r dl[r][v]; grid (vocab chunk, row split),
+// bwd-b: dW[v][c] += sum_r dl[r][v] H[r][c], db[v] += sum_r dl[r][v]; grid (vocab chunk, row split),
 // H tiles (+ their LSE / labels) register-prefetched one tile ahead, partials added atomically
 template <int C>
 __global__ __launch_bounds__(256) void ce_bwd_dw_kernel(const uint16_t* __restrict__ Hm,
@@ -241,57 +290,58 @@ __global__ __launch_bounds__(256) void ce_bwd_dw_kernel(const uint16_t* __restri
                                                         const uint16_t* __restrict__ W, const float* __restrict__ bias,
                                                         const float* __restrict__ lse, const float* __restrict__ gscale,
                                                         int M, int V, int tiles_per_split, float* __restrict__ dW,
-                                                        float* __restrict__ db) {
+                                                        float* __restrict__ db, float* __restrict__ slab) {
   constexpr int LD = C + 8, LDL = VB + 8, NT = C / 32;
   __shared__ __attribute__((aligned(16))) uint16_t sH[HB * LD];
   __shared__ __attribute__((aligned(16))) uint16_t sW[VB * LD];
   __shared__ __attribute__((aligned(16))) uint16_t sL[HB * LDL];
+  __shared__ __attribute__((aligned(16))) float sB[VB];
   __shared__ float sLse[HB];
   __shared__ int sLab[HB];
-  __shared__ float sB[2][64];
+  __shared__ float sBs[2][64];
   const int w = wave_id(), l = lane_id(), hh = l >> 5;
   const int v0 = blockIdx.x * VB;
   const int mt_begin = blockIdx.y * tiles_per_split;
   const int mt_end = min((M + HB - 1) / HB, mt_begin + tiles_per_split);
-  const float g = gscale[0];
+  const float gs = gscale[0];
   stage_rows<C>(sW, LD, W, v0, V);
-  const int coll = 32 * (w & 1) + (l & 31);
-  const int col = v0 + coll;
-  const bool valid = col < V;
-  const float bv = valid ? bias[col] : 0.f;
+  if (threadIdx.x < VB) sB[threadIdx.x] = v0 + (int)threadIdx.x < V ? bias[v0 + threadIdx.x] * kL2E : -__builtin_inff();
+  const int rl = 32 * (w >> 1) + (l & 31);
   constexpr int MAXT = (2 * NT + 3) / 4;
   f32x16 acc_o[MAXT];
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc_o[t] = f32x16{};
-  float bsum = 0.f;
+  float bsum[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) bsum[i] = 0.f;
   bf16x8 hr[C / 32];
-  float aux = 0.f;  // threads [0,64): LSE of row tid, [64,128): label of row tid-64
+  float aux = 0.f;  // threads [0,64): LSE * log2e of row tid, [64,128): label of row tid-64
   auto fetch = [&](int mt) {
     fetch_rows<C>(hr, Hm, mt * HB, M);
     const int t = threadIdx.x & 63, gr = mt * HB + t;
-    if (threadIdx.x < 64) aux = gr < M ? lse[gr] : 0.f;
+    if (threadIdx.x < 64) aux = gr < M ? lse[gr] * kL2E : 0.f;
     else if (threadIdx.x < 128) aux = __int_as_float(gr < M ? (int)labels[gr] : -100);
   };
   if (mt_begin < mt_end) fetch(mt_begin);
+  __syncthreads();
+  float b[16];
+  vocab_regs(sB, b);
   for (int mt = mt_begin; mt < mt_end; ++mt) {
-    const int m0 = mt * HB;
     __syncthreads();
     store_rows<C>(hr, sH, LD);
     if (threadIdx.x < 64) sLse[threadIdx.x] = aux;
     else if (threadIdx.x < 128) sLab[threadIdx.x - 64] = __float_as_int(aux);
     __syncthreads();
     if (mt + 1 < mt_end) fetch(mt + 1);
-    const f32x16 acc = logits_tile<C>(sH, sW, LD);
+    const f32x16 acc = logits_tile_t<C>(sH, sW, LD);
+    const int lab = sLab[rl];
+    float d[16];
+    dl_regs(acc, b, sLse[rl], lab >= 0 ? gs : 0.f, vocab_reg(lab - v0 - 32 * (w & 1)), d);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int rr = 32 * (w >> 1) + acc_row(i, hh);
-      float d = 0.f;
-      if (m0 + rr < M && valid) d = dlogit(acc[i] + bv, sLse[rr], col, sLab[rr], g);
-      bsum += d;
-      sL[rr * LDL + coll] = f2bf(d);
-    }
+    for (int i = 0; i < 16; ++i) bsum[i] += d[i];
+    store_dl_row(sL, LDL, rl, d);
     __syncthreads();
-    // dW chunk (64 vocab × C) += dlᵀ · H : A = dl stored [r][v] (k=r strided), B = H [r][c] (k strided)
+    // dW chunk (64 vocab x C) += dl^T . H : A = dl stored [r][v] (k=r strided), B = H [r][c] (k strided)
 #pragma unroll
     for (int t = 0; t < MAXT; ++t) {
       const int tg = w + 4 * t;
@@ -302,11 +352,27 @@ __global__ __launch_bounds__(256) void ce_bwd_dw_kernel(const uint16_t* __restri
       }
     }
   }
-  // bias: reduce bsum over the two lane halves and the two waves sharing a column set
-  bsum = xor32_sum(bsum);
-  if (hh == 0) sB[w >> 1][coll] = bsum;
+  // bias: register i of lane l <-> vocab entry 32(w & 1) + acc_row(i, hh): sum over the 32 lanes
+  // of the half (their rows), then over the two waves sharing the vocab block
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const float v = half_sum(bsum[i]);
+    if ((l & 31) == 0) sBs[w >> 1][32 * (w & 1) + acc_row(i, hh)] = v;
+  }
   __syncthreads();
-  if (threadIdx.x < 64 && v0 + threadIdx.x < V) atomicAdd(db + v0 + threadIdx.x, sB[0][threadIdx.x] + sB[1][threadIdx.x]);
+  // partials: atomics into dW / db, or (slab) plain stores into row blockIdx.y of a
+  // (row splits, V·C + V₄) slab that a SlabJob later sums into dW | db (common.h)
+  float* dWp = dW;
+  float* dbp = db;
+  if (slab) {
+    dWp = slab + (long long)blockIdx.y * ((long long)V * C + ((V + 3) & ~3));
+    dbp = dWp + (long long)V * C;
+  }
+  if (threadIdx.x < 64 && v0 + threadIdx.x < V) {
+    const float v = sBs[0][threadIdx.x] + sBs[1][threadIdx.x];
+    if (slab) dbp[v0 + threadIdx.x] = v;
+    else atomicAdd(dbp + v0 + threadIdx.x, v);
+  }
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) {
     const int tg = w + 4 * t;
@@ -315,7 +381,11 @@ __global__ __launch_bounds__(256) void ce_bwd_dw_kernel(const uint16_t* __restri
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int vv = v0 + r0 + acc_row(i, hh);
-        if (vv < V) atomicAdd(dW + (long long)vv * C + n0 + (l & 31), acc_o[t][i]);
+        float* p = dWp + (long long)vv * C + n0 + (l & 31);
+        if (vv < V) {
+          if (slab) *p = acc_o[t][i];
+          else atomicAdd(p, acc_o[t][i]);
+        }
       }
     }
   }
@@ -425,18 +495,26 @@ void ce_fwd_launch(int C, const uint16_t* Hm, const int64_t* labels, const uint1
 
 int ce_num_splits(int M, int V) { return pick_split(M, (V + VB - 1) / VB, 2048); }
 
+// row splits of the dW kernel (≈ 4 workgroups per CU): the slab height in slab mode
+int ce_dw_splits(int M, int V) {
+  const int nchunks = (V + VB - 1) / VB, mtiles = (M + HB - 1) / HB;
+  int rsplit = (1024 + nchunks - 1) / nchunks;
+  rsplit = rsplit < 1 ? 1 : (rsplit > mtiles ? mtiles : rsplit);
+  const int tps = (mtiles + rsplit - 1) / rsplit;
+  return (mtiles + tps - 1) / tps;
+}
+
 void ce_bwd_launch(int C, const uint16_t* Hm, const int64_t* labels, const uint16_t* W, const float* bias,
                    const float* lse, const float* gscale, int M, int V, float* dH, const int64_t* rowmap, float* dW,
-                   float* db, int accumulate, hipStream_t st) {
+                   float* db, int accumulate, float* slab, hipStream_t st) {
   const int nchunks = (V + VB - 1) / VB;
   const int nsplit = pick_split(M, nchunks, 512);  // dH partials are added atomically: few splits
   const int cps = (nchunks + nsplit - 1) / nsplit;
   // dW: (vocab chunk × row split) workgroups, ≈ 4 per CU; dW / db partials added atomically
+  // or stored into the slab
   const int mtiles = (M + HB - 1) / HB;
-  int rsplit = (1024 + nchunks - 1) / nchunks;
-  rsplit = rsplit < 1 ? 1 : (rsplit > mtiles ? mtiles : rsplit);
+  const int rsplit = ce_dw_splits(M, V);
   const int tps = (mtiles + rsplit - 1) / rsplit;
-  rsplit = (mtiles + tps - 1) / tps;
   if (!accumulate) {
     (void)hipMemsetAsync(dW, 0, sizeof(float) * (size_t)V * C, st);
     (void)hipMemsetAsync(db, 0, sizeof(float) * (size_t)V, st);
@@ -444,7 +522,8 @@ void ce_bwd_launch(int C, const uint16_t* Hm, const int64_t* labels, const uint1
   dim3 ga((M + HB - 1) / HB, nsplit), gb(nchunks, rsplit);
 #define CEB(CC)                                                                                                  \
   hipLaunchKernelGGL(ce_bwd_dh_kernel<CC>, ga, dim3(256), 0, st, Hm, labels, W, bias, lse, gscale, M, V, cps, dH, rowmap); \
-  hipLaunchKernelGGL(ce_bwd_dw_kernel<CC>, gb, dim3(256), 0, st, Hm, labels, W, bias, lse, gscale, M, V, tps, dW, db)
+  hipLaunchKernelGGL(ce_bwd_dw_kernel<CC>, gb, dim3(256), 0, st, Hm, labels, W, bias, lse, gscale, M, V, tps, dW, db, \
+                     slab)
   if (C == 64) { CEB(64); }
   else if (C == 128) { CEB(128); }
   else if (C == 32) { CEB(32); }

@@ -103,6 +103,21 @@ def _flush_pending():
                 K.slab_reduce(t, ds, os_)
 
 
+def defer_slab(K, t: torch.Tensor, dsts, offs):
+    """Queue ``dsts[j] += Σ_rows t[:, offs[j]:offs[j] + dsts[j].numel()]`` (a slab job) for the
+    next backward kernel of the chain, or the end-of-backward flush."""
+    if not dsts:
+        return
+    st = torch.cuda.current_stream(t.device) if t.is_cuda else None
+    _pending.append((K, t, list(dsts), list(offs), st))
+    if not _flush_queued[0]:
+        try:
+            torch.autograd.Variable._execution_engine.queue_callback(_flush_pending)
+            _flush_queued[0] = True
+        except RuntimeError:  # not inside a backward pass
+            _flush_pending()
+
+
 def _take_job() -> dict:
     """kwargs handing the oldest deferred slab reduction to the next backward kernel, which
     runs it in extra workgroups appended to its own grid (csrc/common.h SlabJob)."""
@@ -144,16 +159,7 @@ class _GradSlab:
             for t, extra in (d if isinstance(d, list) else [(d, 0)]):
                 ds.append(t.view(-1))
                 os_.append(self.offs[i] + extra)
-        if not ds:
-            return
-        st = torch.cuda.current_stream(self.t.device) if self.t.is_cuda else None
-        _pending.append((K, self.t, ds, os_, st))
-        if not _flush_queued[0]:
-            try:
-                torch.autograd.Variable._execution_engine.queue_callback(_flush_pending)
-                _flush_queued[0] = True
-            except RuntimeError:  # not inside a backward pass
-                _flush_pending()
+        defer_slab(K, self.t, ds, os_)
 
 
 def _grad_of(p: torch.Tensor):

@@ -64,8 +64,12 @@ class _MaskedCE(torch.autograd.Function):
                 p.grad = torch.zeros_like(p)
         shp = ctx.hshape
         dh = torch.zeros((shp[0] * shp[1], shp[2]), device=hs.device, dtype=torch.float32)
-        ext.ce_bwd(hs, labels_c, wb, bias.contiguous(), lse, gscale, dh, weight.grad, ctx.bias_p.grad, True,
-                   idx if idx.numel() else None)
+        from . import fused
+
+        slab = ext.ce_bwd(hs, labels_c, wb, bias.contiguous(), lse, gscale, dh, weight.grad, ctx.bias_p.grad, True,
+                          idx if idx.numel() else None, slab=fused.WGRAD_SLAB)
+        if slab is not None:  # dW / db row-split partials: reduced by the next backward kernel
+            fused.defer_slab(ext, slab, [weight.grad.view(-1), ctx.bias_p.grad.view(-1)], [0, weight.numel()])
         return dh.view(shp), None, None, None, None, None
 
 

@@ -30,6 +30,9 @@ for step in "$@"; do
     eager)    run bench_eager 600 python bench.py --no-graph --steps 10 --warmup 3 ;;
     bench)    run bench 600 python bench.py --steps 20 --warmup 5 ;;
     micro)    run micro 300 python tools/microbench.py ;;
+    tiles)    run tiles 300 python tools/tile_latency.py ;;
+    pmc_layer) run pmc_layer 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS --output-format csv -d gpurun_out/pmc_layer -o pmc -- python tools/tile_latency.py pmc ;;
+    pmc_layer2) run pmc_layer2 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_MFMA SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM SQ_ACTIVE_INST_MISC --output-format csv -d gpurun_out/pmc_layer2 -o pmc -- python tools/tile_latency.py pmc ;;
     attn)     run attn 300 python tools/attn_scaling.py ;;
     pmc_attn) run pmc_attn 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_INSTS_LDS --output-format csv -d gpurun_out/pmc -o attn -- python tools/attn_scaling.py 64 ;;
     configs)  for c in seq_clf imagenet long_mlm mnist; do
