@@ -20,7 +20,7 @@ struct AttnArgs {
   uint32_t seed;
 };
 struct PostAttnGrads { float *dWo, *dbo, *dg2, *dbe2, *dW1, *db1, *dW2, *db2; int vrs; int slab; };
-constexpr int kMaxSlabSegs = 8, kSlabRowsPerBlock = 32;  // common.h
+constexpr int kMaxSlabSegs = 16, kSlabRowsPerBlock = 32;  // common.h
 struct SlabJob {
   const float* slab;
   int S, P, nbx, nblk;
@@ -39,6 +39,16 @@ void ln_linear_fwd_launch(const void*, bool, int, int, int, const float*, const 
 void post_attn_fwd_launch(int, const uint16_t*, const float*, const uint16_t*, const float*, const float*,
                           const float*, float, const uint16_t*, const float*, const uint16_t*, const float*, float*,
                           float*, float*, float*, uint16_t*, int, int, hipStream_t);
+void post_attn_ln_linear_fwd_launch(int, const uint16_t*, const float*, const uint16_t*, const float*, const float*,
+                                    const float*, float, const uint16_t*, const float*, const uint16_t*, const float*,
+                                    float*, float*, float*, float*, uint16_t*, int, const float*, const float*,
+                                    const uint16_t*, const float*, uint16_t*, float*, float*, hipStream_t);
+void ln_linear_post_attn_bwd_launch(int, const float*, const uint16_t*, const float*, const float*, const float*,
+                                    const float*, const float*, const float*, float*, float*, float*, float*,
+                                    const float*, const float*, const float*, const uint16_t*, const uint16_t*,
+                                    const uint16_t*, const uint16_t*, const uint16_t*, const float*, const float*,
+                                    float*, uint16_t*, float*, int, const PostAttnGrads&, int, const SlabJob&,
+                                    hipStream_t);
 void post_attn_bwd_launch(int, const float*, const float*, const float*, const float*, const uint16_t*,
                           const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*, const float*,
                           const float*, float*, uint16_t*, float*, int, const PostAttnGrads&, int, const SlabJob&,
@@ -245,6 +255,31 @@ std::vector<Tensor> post_attn_fwd(Tensor o, Tensor x, Tensor wo, Tensor bo, Tens
   return {z, y, m, r, u};
 }
 
+// self-attention layer boundary l → l+1: post-attention block of layer l, then LN1 + packed QKV
+// projection of layer l+1 from the same tile.  Returns (z, y, mean2, rstd2, u, qkv, mean1, rstd1).
+std::vector<Tensor> post_attn_ln_linear_fwd(Tensor o, Tensor x, Tensor wo, Tensor bo, Tensor g2, Tensor be2, double eps,
+                                            Tensor w1, Tensor b1, Tensor w2, Tensor b2, Tensor lnw, Tensor lnb,
+                                            Tensor wq, Tensor bq) {
+  TORCH_CHECK(o.is_contiguous() && x.is_contiguous(), "o/x must be contiguous (R, C)");
+  const int R = (int)o.size(0), C = (int)o.size(1);
+  TORCH_CHECK(x.size(0) == R && x.size(1) == C, "x must be (R, C)");
+  TORCH_CHECK(C == 32 || C == 64 || C == 128, "post_attn supports C in {32, 64, 128}");
+  TORCH_CHECK(wq.is_contiguous() && wq.size(0) == 3 * C && wq.size(1) == C && bq.numel() == 3 * C,
+              "wq must be the packed (3C, C) in-projection");
+  TORCH_CHECK(lnw.numel() == C && lnb.numel() == C, "LN1 affine must have C entries");
+  auto f32 = x.options().dtype(torch::kFloat32);
+  auto b16 = x.options().dtype(torch::kBFloat16);
+  Tensor z = torch::empty({R, C}, f32), y = torch::empty({R, C}, f32);
+  Tensor m = torch::empty({R}, f32), r = torch::empty({R}, f32), u = torch::empty({R, C}, b16);
+  Tensor qkv = torch::empty({R, 3 * C}, b16), m1 = torch::empty({R}, f32), r1 = torch::empty({R}, f32);
+  pio::post_attn_ln_linear_fwd_launch(C, bfp(o), f32p(x), bfp(wo), f32p(bo), f32p(g2), f32p(be2), (float)eps, bfp(w1),
+                                      f32p(b1), bfp(w2), f32p(b2), z.data_ptr<float>(), y.data_ptr<float>(),
+                                      m.data_ptr<float>(), r.data_ptr<float>(), bfp_mut(u), R, f32p(lnw), f32p(lnb),
+                                      bfp(wq), f32p(bq), bfp_mut(qkv), m1.data_ptr<float>(), r1.data_ptr<float>(),
+                                      stream());
+  return {z, y, m, r, u, qkv, m1, r1};
+}
+
 // the backward entry points below ACCUMULATE parameter gradients into caller-provided fp32
 // tensors (normally views of the flat gradient buffer) with device atomics: no partial slabs,
 // no reduction pass, no autograd AccumulateGrad adds
@@ -286,7 +321,7 @@ pio::SlabJob make_job(const OptT& slab, std::vector<Tensor>& dsts, const std::ve
   const Tensor& t = *slab;
   CHECK_DT(t, torch::kFloat32);
   TORCH_CHECK(t.dim() == 2 && t.is_contiguous() && t.size(1) % 4 == 0, "slab must be (S, P), P % 4 == 0");
-  TORCH_CHECK(dsts.size() == offs.size() && dsts.size() <= (size_t)pio::kMaxSlabSegs, "slab job: ≤ 8 segments");
+  TORCH_CHECK(dsts.size() == offs.size() && dsts.size() <= (size_t)pio::kMaxSlabSegs, "slab job: ≤ 16 segments");
   const int P = (int)t.size(1);
   for (size_t q = 0; q < dsts.size(); ++q) {
     Tensor& d = dsts[q];
@@ -333,6 +368,49 @@ std::vector<Tensor> post_attn_bwd(Tensor dz, Tensor y, Tensor m2, Tensor r2, Ten
   pio::post_attn_bwd_launch(C, f32p(dz), f32p(y), f32p(m2), f32p(r2), bfp(u), bfp(o), bfp(wo), bfp(w1), bfp(w2),
                             f32p(g2), f32p(be2), dy.data_ptr<float>(), bfp_mut(dO), delta.data_ptr<float>(), (int)H,
                             pg, R, make_job(job_slab, job_dsts, job_offs), stream());
+  return {dy, dO, delta};
+}
+
+// self-attention layer boundary l+1 → l, backward, slab mode only: the LN1+QKV backward of
+// layer l+1 (g = dQKV (R, 3C) fp32, dres = dY_{l+1}) produces dZ_l in registers, the
+// post-attention backward of layer l consumes it.  ll_grads = slab views for (dγ1, dβ1, dWqkv,
+// dbqkv) of layer l+1, pa_grads = the 8 post-attention slab views of layer l — all of ONE slab.
+// Returns (dy, dO, delta) of layer l.
+std::vector<Tensor> ln_linear_post_attn_bwd(Tensor g, Tensor wq, Tensor x, Tensor mean1, Tensor rstd1, Tensor lnw,
+                                            Tensor lnb, Tensor dres, std::vector<Tensor> ll_grads, Tensor y, Tensor m2,
+                                            Tensor r2, Tensor u, Tensor o, Tensor wo, Tensor w1, Tensor w2, Tensor g2,
+                                            Tensor be2, int64_t H, std::vector<Tensor> pa_grads, OptT job_slab,
+                                            std::vector<Tensor> job_dsts, std::vector<int64_t> job_offs) {
+  TORCH_CHECK(y.is_contiguous() && u.is_contiguous() && o.is_contiguous() && x.is_contiguous() && dres.is_contiguous(),
+              "operands must be contiguous (R, C)");
+  const int R = (int)y.size(0), C = (int)y.size(1);
+  TORCH_CHECK(C == 32 || C == 64, "the fused self-attention backward supports C in {32, 64}");
+  TORCH_CHECK(H > 0 && C % H == 0, "heads must divide C");
+  TORCH_CHECK(g.is_contiguous() && g.size(0) == R && g.size(1) == 3 * C, "g must be (R, 3C) contiguous");
+  CHECK_DT(g, torch::kFloat32);
+  TORCH_CHECK(wq.is_contiguous() && wq.size(0) == 3 * C && wq.size(1) == C, "wq must be (3C, C)");
+  TORCH_CHECK(x.size(0) == R && x.size(1) == C && dres.size(0) == R && dres.size(1) == C, "x / dres must be (R, C)");
+  TORCH_CHECK(ll_grads.size() == 4 && pa_grads.size() == 8, "4 + 8 slab targets expected");
+  const int64_t sr = (R + 63) / 64, CC = (int64_t)C * C;
+  int vrs = -1;
+  float* dg1 = vec_target(ll_grads[0], C, "dlnw", vrs, sr);
+  float* db1 = vec_target(ll_grads[1], C, "dlnb", vrs, sr);
+  float* dwq = vec_target(ll_grads[2], 3 * CC, "dWqkv", vrs, sr);
+  float* dbq = vec_target(ll_grads[3], 3 * C, "dbqkv", vrs, sr);
+  pio::PostAttnGrads pg{vec_target(pa_grads[0], CC, "dWo", vrs, sr), vec_target(pa_grads[1], C, "dbo", vrs, sr),
+                        vec_target(pa_grads[2], C, "dg2", vrs, sr), vec_target(pa_grads[3], C, "dbe2", vrs, sr),
+                        vec_target(pa_grads[4], CC, "dW1", vrs, sr), vec_target(pa_grads[5], C, "db1", vrs, sr),
+                        vec_target(pa_grads[6], CC, "dW2", vrs, sr), vec_target(pa_grads[7], C, "db2", vrs, sr),
+                        vrs, 1};
+  auto f32 = y.options().dtype(torch::kFloat32);
+  Tensor dy = torch::empty({R, C}, f32);
+  Tensor dO = torch::empty({R, C}, y.options().dtype(torch::kBFloat16));
+  Tensor delta = torch::empty({R, H}, f32);
+  pio::ln_linear_post_attn_bwd_launch(C, f32p(g), bfp(wq), f32p(x), f32p(mean1), f32p(rstd1), f32p(lnw), f32p(lnb),
+                                      f32p(dres), dg1, db1, dwq, dbq, f32p(y), f32p(m2), f32p(r2), bfp(u), bfp(o),
+                                      bfp(wo), bfp(w1), bfp(w2), f32p(g2), f32p(be2), dy.data_ptr<float>(),
+                                      bfp_mut(dO), delta.data_ptr<float>(), (int)H, pg, R,
+                                      make_job(job_slab, job_dsts, job_offs), stream());
   return {dy, dO, delta};
 }
 
@@ -556,6 +634,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bias"), py::arg("act"), py::arg("res"), py::arg("out_bf16"), py::arg("save_stats"),
         py::arg("pe") = py::none(), py::arg("kin") = -1);
   m.def("post_attn_fwd", &post_attn_fwd);
+  m.def("post_attn_ln_linear_fwd", &post_attn_ln_linear_fwd);
+  m.def("ln_linear_post_attn_bwd", &ln_linear_post_attn_bwd, py::arg("g"), py::arg("wq"), py::arg("x"),
+        py::arg("mean1"), py::arg("rstd1"), py::arg("lnw"), py::arg("lnb"), py::arg("dres"), py::arg("ll_grads"),
+        py::arg("y"), py::arg("m2"), py::arg("r2"), py::arg("u"), py::arg("o"), py::arg("wo"), py::arg("w1"),
+        py::arg("w2"), py::arg("g2"), py::arg("be2"), py::arg("H"), py::arg("pa_grads"),
+        py::arg("job_slab") = py::none(), py::arg("job_dsts") = std::vector<Tensor>(),
+        py::arg("job_offs") = std::vector<int64_t>());
   m.def("post_attn_bwd", &post_attn_bwd, py::arg("dz"), py::arg("y"), py::arg("m2"), py::arg("r2"), py::arg("u"),
         py::arg("o"), py::arg("wo"), py::arg("w1"), py::arg("w2"), py::arg("g2"), py::arg("be2"), py::arg("H"),
         py::arg("grads"), py::arg("slab") = false, py::arg("job_slab") = py::none(),

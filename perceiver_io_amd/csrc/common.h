@@ -185,7 +185,7 @@ __device__ int trace_bx, trace_by, trace_bz;
 // Reduction block (x, y): 256 columns × slab rows [32y, 32y + 32); wave w sums rows w, w+4, …
 // (all loads in flight), LDS combine, then wave w adds columns 64w..64w+63 with one
 // contiguous 256-B no-return atomic instruction: S/32 adds per element in all.
-constexpr int kMaxSlabSegs = 8;
+constexpr int kMaxSlabSegs = 16;
 constexpr int kSlabRowsPerBlock = 32;
 struct SlabJob {
   const float* slab;  // nullptr: no job

@@ -359,34 +359,30 @@ __device__ __forceinline__ void g_store(const float (&v)[2][8], uint16_t* sG, in
 // registers (row-pass layout) into a resident bf16 tile; W chunks are double-buffered
 // through registers; each 64-column output chunk leaves through LDS as 16-byte row stores.
 // ------------------------------------------------------------------------------------
-template <typename TIn, typename TOut, int NCH>
-__global__ __launch_bounds__(256) void ln_linear_fwd_kernel(const TIn* __restrict__ X, int x_rs, int R, int Kin,
-                                                            const float* __restrict__ lnw, const float* __restrict__ lnb,
-                                                            float eps, const uint16_t* __restrict__ W, int w_rs,
-                                                            const float* __restrict__ bias, int N, int act,
-                                                            const float* __restrict__ res, int res_rs,
-                                                            TOut* __restrict__ Y, int y_rs, float* __restrict__ mean_out,
-                                                            float* __restrict__ rstd_out, PeSplit ps) {
+// LN-Linear shared-memory footprint for NCH chunks: LN(X) tile, W chunk, fp32 output chunk
+template <int NCH>
+constexpr int ln_linear_fwd_smem() { return 2 * 64 * (32 * NCH + 8) * 2 + 64 * 68 * 4; }
+
+// the LN + GEMM part of one 64-row tile: xv = this thread's rows (row-pass layout), wb = the
+// prefetched first W chunk, gw/gb = LN affine (read when has_ln); smem ≥ ln_linear_fwd_smem
+template <typename TOut, int NCH>
+__device__ __forceinline__ void ln_linear_fwd_tile(float (&xv)[NCH][8], bf16x8 (&wb)[NCH], const float (&gw)[NCH][8],
+                                                   const float (&gb)[NCH][8], bool has_ln, int m0, int R, int Kin,
+                                                   float eps, const uint16_t* __restrict__ W, int w_rs,
+                                                   const float* __restrict__ bias, int N, int act,
+                                                   const float* __restrict__ res, int res_rs, TOut* __restrict__ Y,
+                                                   int y_rs, float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                   uint16_t* smem) {
   constexpr int KP = 32 * NCH, LD = KP + 8, LDO = 64 + 4;
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* sA = smem;                                  // [64][LD]  LN(X), bf16
   uint16_t* sW = sA + 64 * LD;                          // [64][LD]  W chunk
   float* sO = reinterpret_cast<float*>(sW + 64 * LD);   // [64][LDO] output chunk
-  const int m0 = blockIdx.x * 64, gr = m0 + rp_row(), w = wave_id(), l = lane_id();
+  const int gr = m0 + rp_row(), w = wave_id(), l = lane_id();
   // W rows are w_rs apart (≥ Kin, zero padded): a multiple of 8 keeps the staging vectorised
   const bool wvec = (w_rs & 7) == 0 && aligned16(W);
   const int wk = w_rs > Kin ? w_rs : Kin;
   const bool yvec = (N & 7) == 0 && (y_rs & 7) == 0 && aligned16(Y);
-
-  float xv[NCH][8];
-  row_load_x<NCH>(xv, X, x_rs, gr, R, Kin, (Kin & 7) == 0 && (x_rs & 7) == 0 && aligned16(X), ps);
-  bf16x8 wb[NCH];
-  tile_fetch<NCH>(wb, W, w_rs, 0, N, 64, wk, KP, wvec);
-  if (lnw) {
-    float gw[NCH][8], gb[NCH][8];
-    const bool pvec = (Kin & 7) == 0 && aligned16(lnw) && aligned16(lnb);
-    row_load<NCH>(gw, lnw, 0, 0, 1, Kin, pvec);
-    row_load<NCH>(gb, lnb, 0, 0, 1, Kin, pvec);
+  if (has_ln) {
     float s = 0.f;
 #pragma unroll
     for (int j = 0; j < NCH; ++j)
@@ -438,19 +434,46 @@ __global__ __launch_bounds__(256) void ln_linear_fwd_kernel(const TIn* __restric
   }
 }
 
+template <typename TIn, typename TOut, int NCH>
+__global__ __launch_bounds__(256) void ln_linear_fwd_kernel(const TIn* __restrict__ X, int x_rs, int R, int Kin,
+                                                            const float* __restrict__ lnw, const float* __restrict__ lnb,
+                                                            float eps, const uint16_t* __restrict__ W, int w_rs,
+                                                            const float* __restrict__ bias, int N, int act,
+                                                            const float* __restrict__ res, int res_rs,
+                                                            TOut* __restrict__ Y, int y_rs, float* __restrict__ mean_out,
+                                                            float* __restrict__ rstd_out, PeSplit ps) {
+  constexpr int KP = 32 * NCH;
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int m0 = blockIdx.x * 64, gr = m0 + rp_row();
+  // phase 0: X rows, the first W chunk and the LN affine in flight together
+  float xv[NCH][8];
+  row_load_x<NCH>(xv, X, x_rs, gr, R, Kin, (Kin & 7) == 0 && (x_rs & 7) == 0 && aligned16(X), ps);
+  bf16x8 wb[NCH];
+  tile_fetch<NCH>(wb, W, w_rs, 0, N, 64, w_rs > Kin ? w_rs : Kin, KP, (w_rs & 7) == 0 && aligned16(W));
+  float gw[NCH][8], gb[NCH][8];
+  if (lnw) {
+    const bool pvec = (Kin & 7) == 0 && aligned16(lnw) && aligned16(lnb);
+    row_load<NCH>(gw, lnw, 0, 0, 1, Kin, pvec);
+    row_load<NCH>(gb, lnb, 0, 0, 1, Kin, pvec);
+  }
+  ln_linear_fwd_tile<TOut, NCH>(xv, wb, gw, gb, lnw != nullptr, m0, R, Kin, eps, W, w_rs, bias, N, act, res, res_rs, Y,
+                                y_rs, mean_out, rstd_out, smem);
+}
+
 // ------------------------------------------------------------------------------------
 // post-attention block forward: Z = Y + W2·gelu(W1·LN2(Y) + b1) + b2, Y = X + Wo·O + bo
 // Phase 0 fetches the O tile, the X rows and (C ≤ 64) all three weights; the three GEMMs
 // then run back to back on LDS with row-pass epilogues (LN2 in registers, 16-byte stores).
 // For C = 128 the weights share one LDS buffer, each fetched during the previous GEMM.
 // ------------------------------------------------------------------------------------
+// one 64-row tile; Z is also left in z (row-pass registers) for a fused epilogue
 template <int C>
-__global__ __launch_bounds__(256) void post_attn_fwd_kernel(
+__device__ __forceinline__ void post_attn_fwd_body(
     const uint16_t* __restrict__ O, const float* __restrict__ X, const uint16_t* __restrict__ Wo,
     const float* __restrict__ bo, const float* __restrict__ g2, const float* __restrict__ be2, float eps,
     const uint16_t* __restrict__ W1, const float* __restrict__ b1, const uint16_t* __restrict__ W2,
     const float* __restrict__ b2, float* __restrict__ Z, float* __restrict__ Ysave, float* __restrict__ mean2,
-    float* __restrict__ rstd2, uint16_t* __restrict__ Usave, int R, int Rx) {
+    float* __restrict__ rstd2, uint16_t* __restrict__ Usave, int R, int Rx, float (&z)[C / 32][8]) {
   // X has Rx rows, row r of the tile adds X[r % Rx] (Rx < R: batch-broadcast residual)
   constexpr int LD = C + 8, LDF = C + 4, MAXT = (2 * C / 32 + 3) / 4, NCH = C / 32;
   constexpr int NWB = C <= 64 ? 3 : 1, NIW = (C * C / 8 + 255) / 256;
@@ -538,15 +561,52 @@ __global__ __launch_bounds__(256) void post_attn_fwd_kernel(
   tile_gemm<MAXT, true, true>(sA, LD, sW[NWB == 3 ? 2 : 0], LD, 64, C, C, acc);
   for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) { sF[m * LDF + n] = acc[t][i] + sP[2][n]; });
   __syncthreads();
-  {
-    float z[NCH][8];
-    lds_row_read<NCH>(z, sF, LDF);
+  lds_row_read<NCH>(z, sF, LDF);
 #pragma unroll
-    for (int j = 0; j < NCH; ++j)
+  for (int j = 0; j < NCH; ++j)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) z[j][e] += yv[j][e];
-    row_store<NCH>(z, Z, C, gr, R, C, av);
-  }
+    for (int e = 0; e < 8; ++e) z[j][e] += yv[j][e];
+  row_store<NCH>(z, Z, C, gr, R, C, av);
+}
+
+template <int C>
+__global__ __launch_bounds__(256) void post_attn_fwd_kernel(
+    const uint16_t* __restrict__ O, const float* __restrict__ X, const uint16_t* __restrict__ Wo,
+    const float* __restrict__ bo, const float* __restrict__ g2, const float* __restrict__ be2, float eps,
+    const uint16_t* __restrict__ W1, const float* __restrict__ b1, const uint16_t* __restrict__ W2,
+    const float* __restrict__ b2, float* __restrict__ Z, float* __restrict__ Ysave, float* __restrict__ mean2,
+    float* __restrict__ rstd2, uint16_t* __restrict__ Usave, int R, int Rx) {
+  float z[C / 32][8];
+  post_attn_fwd_body<C>(O, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, Rx, z);
+}
+
+// ------------------------------------------------------------------------------------
+// cross-layer fusion inside a self-attention block (layer l → l+1, both row-local):
+// post-attention block of layer l, then LayerNorm1 + packed QKV projection of layer l+1 on the
+// same 64-row tile straight from the Z registers — one launch and one phase-0 latency fewer
+// per layer boundary, and Z is never re-read.  The QKV chunk-0 weights and the LN1 affine are
+// fetched in phase 0 with everything else.
+// ------------------------------------------------------------------------------------
+template <int C>
+__global__ __launch_bounds__(256) void post_attn_ln_linear_fwd_kernel(
+    const uint16_t* __restrict__ O, const float* __restrict__ X, const uint16_t* __restrict__ Wo,
+    const float* __restrict__ bo, const float* __restrict__ g2, const float* __restrict__ be2, float eps,
+    const uint16_t* __restrict__ W1, const float* __restrict__ b1, const uint16_t* __restrict__ W2,
+    const float* __restrict__ b2, float* __restrict__ Z, float* __restrict__ Ysave, float* __restrict__ mean2,
+    float* __restrict__ rstd2, uint16_t* __restrict__ Usave, int R, const float* __restrict__ lnw,
+    const float* __restrict__ lnb, const uint16_t* __restrict__ Wq, const float* __restrict__ bq,
+    uint16_t* __restrict__ QKV, float* __restrict__ mean1, float* __restrict__ rstd1) {
+  constexpr int NCH = C / 32, KP = 32 * NCH;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[ln_linear_fwd_smem<NCH>() / 2];  // LN1+QKV half
+  bf16x8 wb[NCH];
+  tile_fetch<NCH>(wb, Wq, C, 0, 3 * C, 64, C, KP, aligned16(Wq));
+  float gw[NCH][8], gb[NCH][8];
+  row_load<NCH>(gw, lnw, 0, 0, 1, C, aligned16(lnw) && aligned16(lnb));
+  row_load<NCH>(gb, lnb, 0, 0, 1, C, aligned16(lnw) && aligned16(lnb));
+  float z[NCH][8];
+  post_attn_fwd_body<C>(O, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, R, z);
+  ln_linear_fwd_tile<uint16_t, NCH>(z, wb, gw, gb, true, blockIdx.x * 64, R, C, eps, Wq, C, bq, 3 * C, 0, nullptr, 0,
+                                    QKV, 3 * C, mean1, rstd1, smem);
 }
 
 // ------------------------------------------------------------------------------------
@@ -633,33 +693,36 @@ __device__ __forceinline__ void wgrad_tile(const uint16_t* sG, int ldg, const ui
 // U, O and (C ≤ 64) all weights at once; the rest of the kernel touches global memory only
 // to store results and to add parameter gradients.
 // ------------------------------------------------------------------------------------
+// LDS bytes of post_attn_bwd_body: sG, sX, sW[NWB], sF, sPart, sDb1, sP
 template <int C>
-__global__ __launch_bounds__(256) void post_attn_bwd_kernel(
-    const float* __restrict__ dZ, const float* __restrict__ Ysave, const float* __restrict__ mean2,
+constexpr int post_attn_bwd_smem() {
+  return 2 * (2 * 64 * (C + 8) + (C <= 64 ? 3 : 1) * C * (C + 8)) + 4 * (64 * (C + 4) + 16 * C + 2 * C + 2 * C);
+}
+
+// dz: this thread's rows of dZ (row-pass layout), loaded by the caller or produced by a fused
+// prologue (ln_linear_post_attn_bwd_kernel); smem ≥ post_attn_bwd_smem<C>() bytes, 16-B aligned
+template <int C>
+__device__ __forceinline__ void post_attn_bwd_body(
+    float (&dz)[C / 32][8], const float* __restrict__ Ysave, const float* __restrict__ mean2,
     const float* __restrict__ rstd2, const uint16_t* __restrict__ U, const uint16_t* __restrict__ O,
     const uint16_t* __restrict__ Wo, const uint16_t* __restrict__ W1, const uint16_t* __restrict__ W2,
     const float* __restrict__ g2, const float* __restrict__ be2, float* __restrict__ dY, uint16_t* __restrict__ dO,
-    float* __restrict__ delta, int H, PostAttnGrads gr_out, int R, SlabJob job) {
+    float* __restrict__ delta, int H, PostAttnGrads gr_out, int R, unsigned char* smem) {
   constexpr int LD = C + 8, LDF = C + 4, MAXT = (2 * C / 32 + 3) / 4, MAXW = ((C / 32) * (C / 32) + 3) / 4;
   constexpr int NCH = C / 32, NWB = C <= 64 ? 3 : 1, NIW = (C * C / 8 + 255) / 256;
-  __shared__ __attribute__((aligned(16))) uint16_t sG[64 * LD];  // dZ → dU → dY
-  __shared__ __attribute__((aligned(16))) uint16_t sX[64 * LD];  // GELU(U) → LN2(Y) → O
-  __shared__ __attribute__((aligned(16))) uint16_t sW[NWB][C * LD];  // W2, W1, Wo
-  __shared__ __attribute__((aligned(16))) float sF[64 * LDF];    // GELU'(U) → dU → dXn2 → dO
-  __shared__ __attribute__((aligned(16))) float sPart[4][4 * C];  // wave partials: Σ dZ, dγ2, dβ2, Σ dY
-  __shared__ float sDb1[2][C];
-  __shared__ float sP[2][C];  // γ2, β2
-  if ((int)blockIdx.x >= (R + 63) / 64) {  // appended workgroups: the previous kernel's slab job
-    slab_reduce_block(job, blockIdx.x - (R + 63) / 64, reinterpret_cast<float4*>(sF));
-    return;
-  }
+  uint16_t* sG = reinterpret_cast<uint16_t*>(smem);  // [64][LD] dZ → dU → dY
+  uint16_t* sX = sG + 64 * LD;                        // [64][LD] GELU(U) → LN2(Y) → O
+  uint16_t(*sW)[C * LD] = reinterpret_cast<uint16_t(*)[C * LD]>(sX + 64 * LD);  // W2, W1, Wo
+  float* sF = reinterpret_cast<float*>(sX + 64 * LD + NWB * C * LD);           // [64][LDF] GELU'(U) → dU → dXn2 → dO
+  float(*sPart)[4 * C] = reinterpret_cast<float(*)[4 * C]>(sF + 64 * LDF);     // wave partials: Σ dZ, dγ2, dβ2, Σ dY
+  float(*sDb1)[C] = reinterpret_cast<float(*)[C]>(sF + 64 * LDF + 16 * C);
+  float(*sP)[C] = reinterpret_cast<float(*)[C]>(sF + 64 * LDF + 18 * C);       // γ2, β2
   const int m0 = blockIdx.x * 64, gr = m0 + rp_row(), w = wave_id(), l = lane_id();
-  const bool av = aligned16(dZ) && aligned16(Ysave) && aligned16(U) && aligned16(O) && aligned16(dY) &&
-                  aligned16(dO) && aligned16(Wo) && aligned16(W1) && aligned16(W2);
+  const bool av = aligned16(Ysave) && aligned16(U) && aligned16(O) && aligned16(dY) && aligned16(dO) &&
+                  aligned16(Wo) && aligned16(W1) && aligned16(W2);
 
   // ---- phase 0: every input of the tile in flight at once
-  float dz[NCH][8], yv[NCH][8], t0[NCH][8];
-  row_load<NCH>(dz, dZ, C, gr, R, C, av);
+  float yv[NCH][8], t0[NCH][8];
   row_load<NCH>(yv, Ysave, C, gr, R, C, av);
   row_load<NCH>(t0, U, C, gr, R, C, av);
   bf16x8 ob[NCH];
@@ -819,25 +882,43 @@ __global__ __launch_bounds__(256) void post_attn_bwd_kernel(
   }
 }
 
+template <int C>
+__global__ __launch_bounds__(256) void post_attn_bwd_kernel(
+    const float* __restrict__ dZ, const float* __restrict__ Ysave, const float* __restrict__ mean2,
+    const float* __restrict__ rstd2, const uint16_t* __restrict__ U, const uint16_t* __restrict__ O,
+    const uint16_t* __restrict__ Wo, const uint16_t* __restrict__ W1, const uint16_t* __restrict__ W2,
+    const float* __restrict__ g2, const float* __restrict__ be2, float* __restrict__ dY, uint16_t* __restrict__ dO,
+    float* __restrict__ delta, int H, PostAttnGrads gr_out, int R, SlabJob job) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[post_attn_bwd_smem<C>()];
+  if ((int)blockIdx.x >= (R + 63) / 64) {  // appended workgroups: the previous kernel's slab job
+    slab_reduce_block(job, blockIdx.x - (R + 63) / 64, reinterpret_cast<float4*>(smem));
+    return;
+  }
+  float dz[C / 32][8];
+  row_load<C / 32>(dz, dZ, C, blockIdx.x * 64 + rp_row(), R, C, aligned16(dZ));
+  post_attn_bwd_body<C>(dz, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO, delta, H, gr_out, R, smem);
+}
+
 // ------------------------------------------------------------------------------------
 // LayerNorm(+)Linear backward, one 64-row tile:
 //   dXn = G·W (N streamed in 64-column chunks, double-buffered through registers),
 //   dW += Gᵀ·LN(X), db += Σ G (per chunk, atomics), dX = LN_bwd(dXn) (+ dres), dγ/dβ.
 // ------------------------------------------------------------------------------------
+template <int NCH>
+constexpr int ln_linear_bwd_smem() {
+  return 64 * 72 * 2 + 2 * 64 * (32 * NCH + 8) * 2 + 64 * (32 * NCH + 4) * 4 + 8 * 32 * NCH * 4 + 4 * 64 * 4;
+}
+
+// one 64-row tile; dX (incl. dres) is also left in dxo (row-pass registers) for a fused epilogue
 template <typename TG, typename TX, int NCH>
-__global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
+__device__ __forceinline__ void ln_linear_bwd_body(
     const TG* __restrict__ G, int g_rs, int N, const uint16_t* __restrict__ W, int w_rs, int Kin,
     const TX* __restrict__ X,
     int x_rs, const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ lnw,
     const float* __restrict__ lnb, const float* __restrict__ dres, int dres_rs, float* __restrict__ dX, int dx_rs,
     float* __restrict__ dlnw, float* __restrict__ dlnb, float* __restrict__ dW, float* __restrict__ db, int vrs,
-    int wrs, int slab, int R, PeSplit ps, SlabJob job) {
+    int wrs, int slab, int R, PeSplit ps, uint16_t* smem, float (&dxo)[NCH][8]) {
   constexpr int KP = 32 * NCH, LD = KP + 8, LDG = 64 + 8, LDF = KP + 4;
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  if ((int)blockIdx.x >= (R + 63) / 64) {  // appended workgroups: the previous kernel's slab job
-    slab_reduce_block(job, blockIdx.x - (R + 63) / 64, reinterpret_cast<float4*>(smem));
-    return;
-  }
   uint16_t* sG = smem;                                   // [64][LDG]  G chunk
   uint16_t* sW = sG + 64 * LDG;                          // [64][LD]   W chunk
   uint16_t* sXn = sW + 64 * LD;                          // [64][LD]   LN(X)
@@ -955,20 +1036,76 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
 #pragma unroll
       for (int e = 0; e < 8; ++e) gw[j][e] = dxn[j][e];
   }
-  if (dX) {
-    if (dres) {
+  if (dres) {
 #pragma unroll
-      for (int j = 0; j < NCH; ++j)
+    for (int j = 0; j < NCH; ++j)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) gw[j][e] += dr[j][e];
-    }
-    row_store<NCH>(gw, dX, dx_rs, gr, R, Kin, kvec && (dx_rs & 7) == 0 && aligned16(dX));
+      for (int e = 0; e < 8; ++e) gw[j][e] += dr[j][e];
   }
+  if (dX) row_store<NCH>(gw, dX, dx_rs, gr, R, Kin, kvec && (dx_rs & 7) == 0 && aligned16(dX));
+#pragma unroll
+  for (int j = 0; j < NCH; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dxo[j][e] = gw[j][e];
   if (lnw && dlnw) {
     __syncthreads();
     colsum_flush(sPart, KP, rep(dlnw, vrs, slab), Kin, slab);
     colsum_flush(sPart + 4 * KP, KP, rep(dlnb, vrs, slab), Kin, slab);
   }
+}
+
+template <typename TG, typename TX, int NCH>
+__global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
+    const TG* __restrict__ G, int g_rs, int N, const uint16_t* __restrict__ W, int w_rs, int Kin,
+    const TX* __restrict__ X,
+    int x_rs, const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ lnw,
+    const float* __restrict__ lnb, const float* __restrict__ dres, int dres_rs, float* __restrict__ dX, int dx_rs,
+    float* __restrict__ dlnw, float* __restrict__ dlnb, float* __restrict__ dW, float* __restrict__ db, int vrs,
+    int wrs, int slab, int R, PeSplit ps, SlabJob job) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  if ((int)blockIdx.x >= (R + 63) / 64) {  // appended workgroups: the previous kernel's slab job
+    slab_reduce_block(job, blockIdx.x - (R + 63) / 64, reinterpret_cast<float4*>(smem));
+    return;
+  }
+  float dxo[NCH][8];
+  ln_linear_bwd_body<TG, TX, NCH>(G, g_rs, N, W, w_rs, Kin, X, x_rs, mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs,
+                                  dlnw, dlnb, dW, db, vrs, wrs, slab, R, ps, smem, dxo);
+}
+
+// ------------------------------------------------------------------------------------
+// cross-layer fusion inside a self-attention block, backward (layer l+1 → l, both row-local):
+// LN1+QKV backward of layer l+1 (dX_{l+1} = LN1_bwd(dQKV·W) + dY_{l+1}) is dZ_l, which the
+// post-attention backward of layer l consumes from registers on the same tile: dZ never
+// touches memory, one launch and one phase-0 latency fewer per boundary.  Both halves store
+// their parameter-gradient partials into ONE slab row per tile (12 segments).  C ≤ 64 (the
+// two halves' LDS must coexist: ≈117 KB at C = 64).
+// ------------------------------------------------------------------------------------
+template <int C>
+__global__ __launch_bounds__(256) void ln_linear_post_attn_bwd_kernel(
+    const float* __restrict__ G, const uint16_t* __restrict__ Wq, const float* __restrict__ X,
+    const float* __restrict__ mean1, const float* __restrict__ rstd1, const float* __restrict__ lnw,
+    const float* __restrict__ lnb, const float* __restrict__ dres, float* __restrict__ dlnw, float* __restrict__ dlnb,
+    float* __restrict__ dWq, float* __restrict__ dbq, const float* __restrict__ Ysave, const float* __restrict__ mean2,
+    const float* __restrict__ rstd2, const uint16_t* __restrict__ U, const uint16_t* __restrict__ O,
+    const uint16_t* __restrict__ Wo, const uint16_t* __restrict__ W1, const uint16_t* __restrict__ W2,
+    const float* __restrict__ g2, const float* __restrict__ be2, float* __restrict__ dY, uint16_t* __restrict__ dO,
+    float* __restrict__ delta, int H, PostAttnGrads gr_out, int R, SlabJob job) {
+  constexpr int NCH = C / 32;
+  constexpr int SM = ln_linear_bwd_smem<NCH>() > post_attn_bwd_smem<C>() ? ln_linear_bwd_smem<NCH>()
+                                                                          : post_attn_bwd_smem<C>();
+  // ONE buffer for both halves (used one after the other): ≈69 KB at C = 64, two workgroups per
+  // CU, so the appended slab-job workgroups run beside the tiles instead of after them
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SM];
+  if ((int)blockIdx.x >= (R + 63) / 64) {  // appended workgroups: the previous kernel's slab job
+    slab_reduce_block(job, blockIdx.x - (R + 63) / 64, reinterpret_cast<float4*>(smem));
+    return;
+  }
+  float dz[NCH][8];
+  ln_linear_bwd_body<float, float, NCH>(G, 3 * C, 3 * C, Wq, C, C, X, C, mean1, rstd1, lnw, lnb, dres, C, nullptr, C,
+                                        dlnw, dlnb, dWq, dbq, gr_out.vrs, gr_out.vrs, gr_out.slab, R, PeSplit{},
+                                        reinterpret_cast<uint16_t*>(smem), dz);
+  __syncthreads();  // the ln_linear half's LDS traffic is done before the post-attention half reuses it
+  post_attn_bwd_body<C>(dz, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO, delta, H, gr_out, R, smem);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1080,7 +1217,7 @@ static void ln_linear_fwd_t(const void* X, int x_rs, int R, int Kin, const float
                             const uint16_t* W, int w_rs, const float* bias, int N, int act, const float* res, int res_rs,
                             void* Y, int y_rs, float* mean, float* rstd, const PeSplit& ps, hipStream_t st) {
   constexpr int KP = 32 * NCH;
-  const size_t smem = 2 * 64 * (KP + 8) * sizeof(uint16_t) + 64 * 68 * sizeof(float);
+  const size_t smem = ln_linear_fwd_smem<NCH>();
   auto fn = ln_linear_fwd_kernel<TI, TO, NCH>;
   set_smem_once((const void*)fn);
   hipLaunchKernelGGL(fn, dim3((R + 63) / 64), dim3(256), smem, st, (const TI*)X, x_rs, R, Kin, lnw, lnb, eps, W, w_rs, bias,
@@ -1133,6 +1270,22 @@ void post_attn_fwd_launch(int C, const uint16_t* O, const float* X, const uint16
 #undef PAF
 }
 
+void post_attn_ln_linear_fwd_launch(int C, const uint16_t* O, const float* X, const uint16_t* Wo, const float* bo,
+                                    const float* g2, const float* be2, float eps, const uint16_t* W1, const float* b1,
+                                    const uint16_t* W2, const float* b2, float* Z, float* Ysave, float* mean2,
+                                    float* rstd2, uint16_t* Usave, int R, const float* lnw, const float* lnb,
+                                    const uint16_t* Wq, const float* bq, uint16_t* QKV, float* mean1, float* rstd1,
+                                    hipStream_t st) {
+  dim3 grid((R + 63) / 64);
+#define PLF(CC)                                                                                                  \
+  hipLaunchKernelGGL(post_attn_ln_linear_fwd_kernel<CC>, grid, dim3(256), 0, st, O, X, Wo, bo, g2, be2, eps, W1, b1, \
+                     W2, b2, Z, Ysave, mean2, rstd2, Usave, R, lnw, lnb, Wq, bq, QKV, mean1, rstd1)
+  if (C == 64) PLF(64);
+  else if (C == 128) PLF(128);
+  else if (C == 32) PLF(32);
+#undef PLF
+}
+
 void post_attn_bwd_launch(int C, const float* dZ, const float* Ysave, const float* mean2, const float* rstd2,
                           const uint16_t* U, const uint16_t* O, const uint16_t* Wo, const uint16_t* W1,
                           const uint16_t* W2, const float* g2, const float* be2, float* dY, uint16_t* dO,
@@ -1147,13 +1300,30 @@ void post_attn_bwd_launch(int C, const float* dZ, const float* Ysave, const floa
 #undef PAB
 }
 
+void ln_linear_post_attn_bwd_launch(int C, const float* G, const uint16_t* Wq, const float* X, const float* mean1,
+                                    const float* rstd1, const float* lnw, const float* lnb, const float* dres,
+                                    float* dlnw, float* dlnb, float* dWq, float* dbq, const float* Ysave,
+                                    const float* mean2, const float* rstd2, const uint16_t* U, const uint16_t* O,
+                                    const uint16_t* Wo, const uint16_t* W1, const uint16_t* W2, const float* g2,
+                                    const float* be2, float* dY, uint16_t* dO, float* delta, int H,
+                                    const PostAttnGrads& grads, int R, const SlabJob& job, hipStream_t st) {
+  dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0));
+#define LPB(CC)                                                                                                   \
+  hipLaunchKernelGGL(ln_linear_post_attn_bwd_kernel<CC>, grid, dim3(256), 0, st, G, Wq, X, mean1, rstd1, lnw, lnb, \
+                     dres, dlnw, dlnb, dWq, dbq, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO, delta, H,  \
+                     grads, R, job)
+  if (C == 64) LPB(64);
+  else if (C == 32) LPB(32);
+#undef LPB
+}
+
 template <typename TG, typename TX, int NCH>
 static void ln_linear_bwd_t(const void* G, int g_rs, int N, const uint16_t* W, int w_rs, int Kin, const void* X, int x_rs,
                             const float* mean, const float* rstd, const float* lnw, const float* lnb, const float* dres,
                             int dres_rs, float* dX, int dx_rs, float* dlnw, float* dlnb, float* dW, float* db, int vrs,
                             int wrs, int slab, int R, const PeSplit& ps, const SlabJob& job, hipStream_t st) {
   constexpr int KP = 32 * NCH;
-  const size_t smem = 64 * 72 * 2 + 2 * 64 * (KP + 8) * 2 + 64 * (KP + 4) * 4 + 8 * KP * 4 + 4 * 64 * 4;
+  const size_t smem = ln_linear_bwd_smem<NCH>();
   auto fn = ln_linear_bwd_kernel<TG, TX, NCH>;
   set_smem_once((const void*)fn);
   const dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0));  // + the appended slab-job workgroups

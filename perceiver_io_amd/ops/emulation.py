@@ -77,6 +77,22 @@ def _acc(t, v):
         t += v.reshape(t.shape)
 
 
+def post_attn_ln_linear_fwd(o, x, wo, bo, g2, be2, eps, w1, b1, w2, b2, lnw, lnb, wq, bq):
+    """post_attn_fwd of layer l, then ln_linear_fwd (LN1 + packed QKV) of layer l+1."""
+    z, y, m2, r2, u = post_attn_fwd(o, x, wo, bo, g2, be2, eps, w1, b1, w2, b2)
+    qkv, mean1, rstd1 = ln_linear_fwd(z, lnw, lnb, eps, wq, bq, 0, None, True, True)
+    return z, y, m2, r2, u, qkv, mean1, rstd1
+
+
+def ln_linear_post_attn_bwd(g, wq, x, mean1, rstd1, lnw, lnb, dres, ll_grads, y, m2, r2, u, o, wo, w1, w2, g2, be2,
+                            H, pa_grads, job_slab=None, job_dsts=(), job_offs=()):
+    """ln_linear_bwd of layer l+1 (dX = dZ of layer l, incl. dres) → post_attn_bwd of layer l,
+    both into slab targets."""
+    _run_job(job_slab, job_dsts, job_offs)
+    dz = ln_linear_bwd(g, wq, x, mean1, rstd1, lnw, lnb, dres, True, *ll_grads, slab=True)
+    return post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, be2, H, pa_grads, slab=True)
+
+
 def _heads(x, H):
     b, n, _ = x.shape
     return x[:, :, : x.shape[2]].reshape(b, n, H, -1).permute(0, 2, 1, 3)

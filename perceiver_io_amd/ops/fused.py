@@ -460,6 +460,143 @@ class _LayerFn(torch.autograd.Function):
         return (None, None, None, None, None, dx_q, dx_kv, None) + (None,) * len(ps)
 
 
+PA_SIZES = lambda C: [C * C, C, C, C, C * C, C, C * C, C]  # noqa: E731  (Wo bo γ2 β2 W1 b1 W2 b2)
+LL_SIZES = lambda C: [C, C, 3 * C * C, 3 * C]                 # noqa: E731  (γ1 β1 Wqkv bqkv)
+SA_NP = 12  # parameters per self-attention layer (layer_spec_and_params order)
+
+
+class _SABlockFn(torch.autograd.Function):
+    """A whole self-attention block (reference ``model.py:43-44``: ``num_layers`` self-attention
+    layers) as ONE autograd node, so that the row-local kernels of adjacent layers fuse across
+    the layer boundary:
+
+        forward : ln_linear(0) → [attn(l) → post_attn(l)+ln_linear(l+1)]… → attn(L-1) → post_attn(L-1)
+        backward: post_attn_bwd(L-1) → [attn_bwd(l) → ln_linear_bwd(l)+post_attn_bwd(l-1)]… → attn_bwd(0)
+                  → ln_linear_bwd(0)
+
+    i.e. 2L+1 launches each way instead of 3L; the residual stream between layers never
+    leaves registers at a boundary.  Weight gradients go through per-tile slabs (slab jobs)."""
+
+    @staticmethod
+    def forward(ctx, specs, bws, x, *ps):
+        K = kernels(x)
+        L = len(specs)
+        spec = specs[0]
+        C, H = spec.C, spec.heads
+        D = C // H
+        scale = 1.0 / math.sqrt(D)
+        B, N = x.shape[0], x.shape[1]
+        R = B * N
+        from .attention import pick_splits
+
+        nsplit = pick_splits(B, H, N, N)
+        P = [ps[SA_NP * i:SA_NP * (i + 1)] for i in range(L)]
+        xl = x.reshape(R, C)
+        if not xl.is_contiguous():
+            xl = xl.contiguous()
+        qkv, mean1, rstd1 = K.ln_linear_fwd(xl, P[0][0], P[0][1], EPS, bws[0][0], P[0][3], 0, None, True, True)
+        saved = []
+        for i in range(L):
+            p = P[i]
+            _, _, wo, w1, w2 = bws[i]
+            bo, g2, be2, b1, b2 = p[5], p[6], p[7], p[9], p[11]
+            qkv3 = qkv.view(B, N, 3 * C)
+            o, lse = K.attn_fwd(qkv3[:, :, :C], qkv3[:, :, C:2 * C], qkv3[:, :, 2 * C:], None, H, D, scale, 0.0, 0,
+                                nsplit)
+            o2 = o.view(R, C)
+            if i + 1 < L:
+                pn = P[i + 1]
+                z, y, m2, r2, u, qkv_n, mean_n, rstd_n = K.post_attn_ln_linear_fwd(
+                    o2, xl, wo, bo, g2, be2, EPS, w1, b1, w2, b2, pn[0], pn[1], bws[i + 1][0], pn[3])
+            else:
+                z, y, m2, r2, u = K.post_attn_fwd(o2, xl, wo, bo, g2, be2, EPS, w1, b1, w2, b2)
+                qkv_n = mean_n = rstd_n = None
+            saved += [xl, qkv, mean1, rstd1, o, lse, y, m2, r2, u]
+            xl, qkv, mean1, rstd1 = z, qkv_n, mean_n, rstd_n
+        ctx.specs, ctx.bws, ctx.dims = specs, bws, (B, N, C, H, D, scale)
+        ctx.save_for_backward(*saved, *ps)
+        return xl.view(B, N, C)
+
+    @staticmethod
+    def backward(ctx, dz):
+        K = kernels(dz)
+        B, N, C, H, D, scale = ctx.dims
+        R = B * N
+        L = len(ctx.specs)
+        bws = ctx.bws
+        t = ctx.saved_tensors
+        S = [t[10 * i:10 * (i + 1)] for i in range(L)]
+        ps = t[10 * L:]
+        P = [ps[SA_NP * i:SA_NP * (i + 1)] for i in range(L)]
+        f32 = dict(device=dz.device, dtype=torch.float32)
+
+        def flat(p):
+            g = _grad_of(p)
+            return None if g is None else g.view(-1)
+
+        def pa_dsts(p):  # Wo bo γ2 β2 W1 b1 W2 b2
+            return [flat(p[4]), flat(p[5]), flat(p[6]), flat(p[7]), flat(p[8]), flat(p[9]), flat(p[10]), flat(p[11])]
+
+        def ll_dsts(p):  # γ1 β1 Wqkv bqkv
+            return [flat(p[0]), flat(p[1]), flat(p[2]), flat(p[3])]
+
+        def pa_args(i):
+            xl, qkv, mean1, rstd1, o, lse, y, m2, r2, u = S[i]
+            _, _, wo, w1, w2 = bws[i]
+            return (y, m2, r2, u, o.view(R, C), wo, w1, w2, P[i][6], P[i][7])
+
+        dz2 = dz.reshape(R, C)
+        if not dz2.is_contiguous():
+            dz2 = dz2.contiguous()
+        sl = _GradSlab(R, PA_SIZES(C), dz2)
+        dy, do, delta = K.post_attn_bwd(dz2, *pa_args(L - 1), H, sl.targets(), slab=True, **_take_job())
+        sl.defer(K, pa_dsts(P[L - 1]))
+        dx = None
+        for i in range(L - 1, -1, -1):
+            xl, qkv, mean1, rstd1, o, lse, y, m2, r2, u = S[i]
+            qkv3 = qkv.view(B, N, 3 * C)
+            dqkv = torch.empty((B, N, 3 * C), **f32)  # every column block is written by attn_bwd
+            K.attn_bwd(qkv3[:, :, :C], qkv3[:, :, C:2 * C], qkv3[:, :, 2 * C:], None, o, do.view(B, N, C), lse,
+                       delta.view(B, N, H), H, D, scale, 0.0, 0, dqkv[:, :, :C], dqkv[:, :, C:2 * C],
+                       dqkv[:, :, 2 * C:])
+            if i > 0:
+                sl = _GradSlab(R, LL_SIZES(C) + PA_SIZES(C), dz2)
+                tg = sl.targets()
+                dy, do, delta = K.ln_linear_post_attn_bwd(dqkv.view(R, 3 * C), bws[i][0], xl, mean1, rstd1, P[i][0],
+                                                          P[i][1], dy, tg[:4], *pa_args(i - 1), H, tg[4:],
+                                                          **_take_job())
+                sl.defer(K, ll_dsts(P[i]) + pa_dsts(P[i - 1]))
+            else:
+                sl = _GradSlab(R, LL_SIZES(C), dz2)
+                dx = K.ln_linear_bwd(dqkv.view(R, 3 * C), bws[0][0], xl, mean1, rstd1, P[0][0], P[0][1], dy, True,
+                                     *sl.targets(), slab=True, **_take_job())
+                sl.defer(K, ll_dsts(P[0]))
+        return (None, None, dx.view(B, N, C)) + (None,) * len(ps)
+
+
+def self_attention_block(block, x):
+    """All layers of a self-attention block; one fused autograd node when every layer is
+    fusable at C ≤ 64 (slab gradients on), else layer by layer."""
+    layers = list(block)
+    specs, pss = [], []
+    for layer in layers:
+        spec, ps = layer_spec_and_params(layer)
+        specs.append(spec)
+        pss.append(ps)
+    ok = (WGRAD_SLAB and len(layers) > 1 and all(_fusable(lay) for lay in layers)
+          and all(sp == specs[0] for sp in specs) and specs[0].C in (32, 64) and not specs[0].cross
+          and x.dim() == 3 and x.shape[1] * x.shape[0] < TALL_ROWS)
+    if not ok:
+        for layer in layers:
+            x = self_attention_layer(layer, x)
+        return x
+    if x.dtype != torch.float32:
+        x = x.float()
+    bws = tuple(_bf16_weights(sp, ps) for sp, ps in zip(specs, pss))
+    flat_ps = [p for ps in pss for p in ps]
+    return _SABlockFn.apply(tuple(specs), bws, x, *flat_ps)
+
+
 def _seed(spec: LayerSpec, training: bool) -> int:
     if spec.dropout > 0.0 and training:
         return int(torch.randint(0, 2**31 - 1, (1,)).item())
@@ -564,6 +701,5 @@ def encoder_forward(encoder, x, pad_mask=None):
         lat = cross_attention_layer(cross, lat, src, pad_mask)
         if lat.shape[0] == 1 and b > 1:
             lat = lat.expand(b, -1, -1)
-        for sa in block:
-            lat = self_attention_layer(sa, lat)
+        lat = self_attention_block(block, lat)
     return lat
