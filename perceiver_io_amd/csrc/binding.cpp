@@ -70,6 +70,7 @@ void ce_bwd_launch(int, const uint16_t*, const int64_t*, const uint16_t*, const 
 void embed_fwd_launch(const int64_t*, const float*, const float*, float*, long long, int, int, float, hipStream_t);
 void embed_bwd_launch(const int64_t*, const float*, float*, float*, int, int, int, float, hipStream_t);
 void embed_bwd_sorted_launch(const int64_t*, const int64_t*, const float*, float*, long long, int, float, hipStream_t);
+bool embed_bwd_local_launch(const int64_t*, const float*, float*, float*, int, int, int, float, hipStream_t);
 void text_mask_launch(const int64_t*, const bool*, const float*, const int64_t*, int64_t*, int64_t*, long long, int,
                       int, float, hipStream_t);
 void sumsq_launch(const float*, long long, float*, hipStream_t);
@@ -558,6 +559,13 @@ Tensor embed_fwd(Tensor ids, Tensor E, Tensor P, double scale) {
 void embed_bwd(Tensor ids, Tensor g, OptT dE, OptT dP, double scale) {
   TORCH_CHECK(g.is_contiguous() && ids.is_contiguous());
   const int B = (int)ids.size(0), L = (int)ids.size(1), C = (int)g.size(2);
+  if (dE.has_value()) TORCH_CHECK(dE->is_contiguous() && dE->size(1) == C, "dE must be (V, C) contiguous");
+  if (dP.has_value()) TORCH_CHECK(dP->is_contiguous() && dP->size(1) == C && dP->size(0) >= L, "dP must be (>= L, C)");
+  // one launch: block-local sort + run folding for dE, batch sums for dP (C ∈ {64, 128, 256}, ids < 2^24)
+  if ((!dE.has_value() || dE->size(0) < (1 << 24)) &&
+      pio::embed_bwd_local_launch(ids.data_ptr<int64_t>(), f32p(g), dE.has_value() ? dE->data_ptr<float>() : nullptr,
+                                  dP.has_value() ? dP->data_ptr<float>() : nullptr, B, L, C, (float)scale, stream()))
+    return;
   if (dE.has_value()) {  // token-embedding rows: sort positions by id, fold equal-id runs, then add
     TORCH_CHECK(dE->is_contiguous() && dE->size(1) == C, "dE must be (V, C) contiguous");
     const bool small = dE->size(0) <= 32767;  // int16 keys: a 2-pass radix sort instead of 8

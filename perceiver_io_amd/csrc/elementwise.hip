@@ -88,6 +88,87 @@ __global__ void embed_bwd_sorted_kernel(const int64_t* __restrict__ sorted_ids, 
   }
 }
 
+// dE[id] += scale · Σ g rows with that id, with NO global sort: each workgroup takes 256
+// consecutive token positions, bitonic-sorts their (id, slot) keys in LDS, and every wave walks
+// a quarter of the sorted keys with its g rows' loads all in flight (lane = channel), adding
+// one contiguous 256-B row per run of equal ids.  A hot id ([MASK] ≈ 12 % of an MLM batch,
+// [PAD], frequent words) then costs ≤ 4 row atomics per 256 tokens instead of one per
+// occurrence — the property the earlier sort-by-id pipeline (≈10 launches) paid for.
+// Workgroups past the token blocks do the position-table gradient dP (batch sums per
+// position, embed_bwd_kernel's layout): one launch for the whole text-embedding backward.
+constexpr int ET = 256;
+template <int C>
+__global__ __launch_bounds__(256) void embed_bwd_local_kernel(const int64_t* __restrict__ ids,
+                                                              const float* __restrict__ g, float* __restrict__ dE,
+                                                              float* __restrict__ dP, long long n, int nblk_e, int B,
+                                                              int L, float scale) {
+  __shared__ uint32_t sKey[ET];
+  const int t = threadIdx.x;
+  if ((int)blockIdx.x >= nblk_e) {  // position-table gradient: block (l, batch group)
+    const int pb = blockIdx.x - nblk_e, l = pb % L, b0 = (pb / L) * EB;
+    for (int c = t; c < C; c += blockDim.x) {
+      float v[EB];
+#pragma unroll
+      for (int j = 0; j < EB; ++j) v[j] = b0 + j < B ? g[((long long)(b0 + j) * L + l) * C + c] : 0.f;
+      float acc = 0.f;
+#pragma unroll
+      for (int j = 0; j < EB; ++j) acc += v[j];
+      atomicAdd(dP + (long long)l * C + c, acc);
+    }
+    return;
+  }
+  const long long j0 = (long long)blockIdx.x * ET;
+  sKey[t] = j0 + t < n ? ((uint32_t)ids[j0 + t] << 8) | (uint32_t)t : 0xFFFFFFFFu;  // ids < 2^24
+  __syncthreads();
+  for (int k = 2; k <= ET; k <<= 1) {
+    for (int jj = k >> 1; jj > 0; jj >>= 1) {
+      const int ix = t ^ jj;
+      if (ix > t) {
+        const uint32_t a = sKey[t], b = sKey[ix];
+        if ((a > b) == ((t & k) == 0)) { sKey[t] = b; sKey[ix] = a; }
+      }
+      __syncthreads();
+    }
+  }
+  if (dE == nullptr) return;
+  constexpr int NC = C / 64;  // channels per lane (lane l: l, l + 64, ...)
+  const int w = wave_id(), l = lane_id();
+  const int e0 = 64 * w;
+  for (int h = 0; h < 64; h += 32) {  // 32 sorted entries at a time: their loads all in flight
+    float v[32][NC];
+#pragma unroll
+    for (int e = 0; e < 32; ++e) {
+      const uint32_t key = sKey[e0 + h + e];
+      const long long row = j0 + (key & 255u);
+#pragma unroll
+      for (int q = 0; q < NC; ++q) v[e][q] = key != 0xFFFFFFFFu ? g[row * C + l + 64 * q] : 0.f;
+    }
+    uint32_t cur = sKey[e0 + h] >> 8;
+    float acc[NC];
+#pragma unroll
+    for (int q = 0; q < NC; ++q) acc[q] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 32; ++e) {
+      const uint32_t key = sKey[e0 + h + e];
+      if (key == 0xFFFFFFFFu) break;  // padding past n sorts last (wave-uniform)
+      if ((key >> 8) != cur) {
+#pragma unroll
+        for (int q = 0; q < NC; ++q) {
+          atomicAdd(dE + (long long)cur * C + l + 64 * q, acc[q] * scale);
+          acc[q] = 0.f;
+        }
+        cur = key >> 8;
+      }
+#pragma unroll
+      for (int q = 0; q < NC; ++q) acc[q] += v[e][q];
+    }
+    if (cur != (0xFFFFFFFFu >> 8)) {
+#pragma unroll
+      for (int q = 0; q < NC; ++q) atomicAdd(dE + (long long)cur * C + l + 64 * q, acc[q] * scale);
+    }
+  }
+}
+
 // BERT masking from three uniform draws per token (torch.rand, graph-safe RNG):
 //   sel = ~special & u0 < p ; msk = sel & u1 < 0.9 ; rnd = msk & u2 < 1/9
 //   x' = rnd ? rid : (msk ? MASK : x) ; label = sel ? x : -100
@@ -173,6 +254,22 @@ void embed_bwd_launch(const int64_t* ids, const float* g, float* dE, float* dP, 
                       hipStream_t st) {
   hipLaunchKernelGGL(embed_bwd_kernel, dim3(L, (B + EB - 1) / EB), dim3(C < 256 ? C : 256), 0, st, ids, g, dE, dP, B, L,
                      C, scale);
+}
+// C a multiple of 64 (≤ 256); dE and/or dP
+bool embed_bwd_local_launch(const int64_t* ids, const float* g, float* dE, float* dP, int B, int L, int C, float scale,
+                            hipStream_t st) {
+  const long long n = (long long)B * L;
+  const int nblk_e = dE ? (int)((n + ET - 1) / ET) : 0;
+  const int nblk_p = dP ? L * ((B + EB - 1) / EB) : 0;
+  const dim3 grid(nblk_e + nblk_p);
+  if (nblk_e + nblk_p == 0) return true;
+  switch (C) {
+    case 64: hipLaunchKernelGGL(embed_bwd_local_kernel<64>, grid, dim3(256), 0, st, ids, g, dE, dP, n, nblk_e, B, L, scale); break;
+    case 128: hipLaunchKernelGGL(embed_bwd_local_kernel<128>, grid, dim3(256), 0, st, ids, g, dE, dP, n, nblk_e, B, L, scale); break;
+    case 256: hipLaunchKernelGGL(embed_bwd_local_kernel<256>, grid, dim3(256), 0, st, ids, g, dE, dP, n, nblk_e, B, L, scale); break;
+    default: return false;
+  }
+  return true;
 }
 void embed_bwd_sorted_launch(const int64_t* sorted_ids, const int64_t* perm, const float* g, float* dE, long long n,
                              int C, float scale, hipStream_t st) {

@@ -324,14 +324,20 @@ def test_embed_mask_adamw():
     ids[:, ::3] = 2  # a very frequent id (like [MASK]): long equal-id runs after sorting
     E, P = torch.randn(V, C, device=DEV), torch.randn(64, C, device=DEV)
     close(_ext().embed_fwd(ids, E, P[:L].contiguous(), 8.0), _emu().embed_fwd(ids, E, P[:L].contiguous(), 8.0), 1e-6, "emb")
-    g = torch.randn(B, L, C, device=DEV)
-    r = []
-    for K in (_ext(), _emu()):
-        dE, dP = torch.zeros(V, C, device=DEV), torch.zeros(64, C, device=DEV)
-        K.embed_bwd(ids, g, dE, dP, 8.0)
-        r.append((dE, dP))
-    close(r[0][0], r[1][0], 1e-5, "dE")
-    close(r[0][1], r[1][1], 1e-5, "dP")
+    # embedding backward: small ragged batch, and multi-block batches (block-local sort + run
+    # folding across 256-token blocks, partial last block), C = 64 and 128
+    for (Bb, Lb, Cb) in ((B, L, C), (8, 512, 64), (3, 333, 128)):
+        idb = torch.randint(0, V, (Bb, Lb), device=DEV)
+        idb[:, ::3] = 2
+        idb[:, 1::7] = 0
+        g = torch.randn(Bb, Lb, Cb, device=DEV)
+        r = []
+        for K in (_ext(), _emu()):
+            dE, dP = torch.ones(V, Cb, device=DEV), torch.zeros(Lb, Cb, device=DEV)
+            K.embed_bwd(idb, g, dE, dP, 8.0)
+            r.append((dE, dP))
+        close(r[0][0], r[1][0], 1e-5, f"dE {Bb}x{Lb}x{Cb}")
+        close(r[0][1], r[1][1], 1e-5, f"dP {Bb}x{Lb}x{Cb}")
     x = torch.randint(0, V, (B, L), device=DEV)
     pad = torch.rand(B, L, device=DEV) < 0.2
     u = torch.rand(3, B, L, device=DEV)
