@@ -45,7 +45,11 @@ class FlatParameterSpace:
         dev = params[0].device
         self.device = dev
         if replicate is None:
-            replicate = dev.type == "cuda"
+            # the replicas only serve the in-kernel float-atomic gradient path; with per-tile
+            # weight-gradient slabs (ops.fused.WGRAD_SLAB) they would stay zero
+            from .fused import WGRAD_SLAB
+
+            replicate = dev.type == "cuda" and not WGRAD_SLAB
         rep = [p for p in params if replicate and getattr(p, "_pio_replicate", False)]
         rep_ids = {id(p) for p in rep}
         # replicated parameters first (one contiguous region), then the rest in module order
