@@ -154,6 +154,28 @@ def compact_lm_loss(h: torch.Tensor, labels_c: torch.Tensor, count: torch.Tensor
     return F.cross_entropy(logits.float(), lab, ignore_index=-100, reduction="sum") / count.clamp(min=1)
 
 
+class _GatherQueries(torch.autograd.Function):
+    """``param.index_select(0, idx)`` whose backward index-adds straight into ``param.grad``
+    (one kernel; autograd's version is zeros + index_add + AccumulateGrad add)."""
+
+    @staticmethod
+    def forward(ctx, param, idx):
+        ctx.save_for_backward(idx)
+        ctx.param = param
+        return param.index_select(0, idx)
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        p = ctx.param
+        if not ctx.needs_input_grad[0]:
+            return None, None
+        if p.grad is None:
+            p.grad = torch.zeros_like(p)
+        p.grad.index_add_(0, idx, g.to(p.grad.dtype))
+        return None, None
+
+
 def masked_decode_loss(decoder, x_latent: torch.Tensor, labels: torch.Tensor):
     """MLM loss decoding only the selected positions.
 
@@ -172,10 +194,10 @@ def masked_decode_loss(decoder, x_latent: torch.Tensor, labels: torch.Tensor):
     cap = row_capacity(L)
     if use_hip(x_latent) and lin.weight.shape[1] in (32, 64, 128):
         idx, _, gidx, glab, total, _overflow = ext.require().mlm_select(labels.contiguous(), cap, capacity(B * L))
-        q = decoder.output.index_select(0, idx.reshape(-1)).view(B, cap, -1)
+        q = _GatherQueries.apply(decoder.output, idx.reshape(-1)).view(B, cap, -1)
         h = decoder.cross_attention(q, x_latent)
         return _MaskedCE.apply(h, lin.weight, lin.bias, gidx, glab, total)
     idx, labels_c, count = compact_per_row(labels, cap)
-    q = decoder.output.index_select(0, idx.reshape(-1)).view(B, cap, -1)
+    q = _GatherQueries.apply(decoder.output, idx.reshape(-1)).view(B, cap, -1)
     h = decoder.cross_attention(q, x_latent)
     return compact_lm_loss(h, labels_c, count, lin.weight, lin.bias, B * L)

@@ -157,3 +157,18 @@ def test_self_attention_block_node_matches_layerwise():
     assert torch.allclose(outs[0], outs[1], atol=1e-5)
     for a, b in zip(*grads):
         assert torch.allclose(a, b, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.gpu
+def test_lartpc_run_gpu(tmp_path):
+    """run.py on the MI355X through the HIP path: Fourier-PE image input with the zero-pixel
+    key-padding mask, a one-query-per-pixel decoder, weighted CE, grad clipping."""
+    import run
+    from perceiver_io_amd.ops import ext
+
+    ext.require()
+    ck = tmp_path / "ckpt"
+    run.main(["--epochs", "1", "--events", "4", "--val-events", "2", "--size", "128", "--batch-size", "2",
+              "--max-steps", "2", "--log-dir", str(tmp_path / "runs"), "--ckpt-dir", str(ck), "--device", "cuda"])
+    state = torch.load(ck / "model_0.ckpt", weights_only=True)
+    assert all(torch.isfinite(v).all() for v in state["model_state_dict"].values() if v.is_floating_point())

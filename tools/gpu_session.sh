@@ -49,6 +49,8 @@ for step in "$@"; do
     bench_noslab) run bench_noslab 600 env PERCEIVER_WGRAD_SLAB=0 python bench.py --steps 20 --warmup 5 ;;
     prof_noslab) run prof_noslab 600 env PERCEIVER_WGRAD_SLAB=0 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_noslab -o run --output-format csv -- python bench.py --steps 5 --warmup 3 ;;
     prof)     run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 3 ;;
+    lartpc)   run lartpc 600 python run.py --epochs 1 --events 8 --val-events 4 --size 512 --batch-size 4 --max-steps 2 --log-dir /tmp/lartpc_runs --ckpt-dir /tmp/lartpc_ckpt ;;
+    lartpc_test) run lartpc_test 300 python -u -m pytest tests/test_components.py -m gpu -x -v --timeout 240 --timeout-method thread -p no:cacheprovider ;;
     dbg0)     run dbg0 300 env AMD_SERIALIZE_KERNEL=3 python tools/debug_engine.py 0 ;;
     dbg1)     run dbg1 300 python tools/debug_engine.py 1 ;;
     *) echo "unknown step $step" ;;
