@@ -23,7 +23,7 @@ run build 900 python -m perceiver_io_amd.csrc.build
 for step in "$@"; do
   case "$step" in
     smoke)    run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    kernels)  run kernels 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    kernels)  run kernels 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     kernels_all) run kernels_all 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     ref)      run bench_ref 600 python bench.py --backend reference --steps 5 --warmup 2 ;;
     ref32)    run bench_ref32 600 python bench.py --backend reference --dtype fp32 --steps 5 --warmup 2 ;;
