@@ -63,6 +63,8 @@ def parse(argv=None):
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture of the step")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--profile-stacks", type=int, default=0,
+                    help="with --profile-steps: group copy/fill ops by N Python stack frames (finds stray copies)")
     a = ap.parse_args(argv)
     cfg = CONFIGS[a.config]
     for k in ("batch", "seq_len", "latents", "channels"):
@@ -225,12 +227,21 @@ def main(argv=None):
     if args.profile_steps and cuda:
         from torch.profiler import ProfilerActivity, profile
 
-        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA],
+                     with_stack=args.profile_stacks > 0) as prof:
             for i in range(args.profile_steps):
                 engine.step(data[i % 4])
             torch.cuda.synchronize()
         if info.is_main:
             print(prof.key_averages().table(sort_by="cuda_time_total", row_limit=40), file=sys.stderr)
+            if args.profile_stacks:
+                keep = ("aten::copy_", "aten::fill_", "aten::zero_", "aten::sum", "aten::clone")
+                rows = [e for e in prof.key_averages(group_by_stack_n=args.profile_stacks) if e.key in keep]
+                rows.sort(key=lambda e: -e.count)
+                for e in rows[:40]:
+                    print(f"{e.key} x{e.count} dev_us={e.device_time_total:.0f}", file=sys.stderr)
+                    for fr in e.stack[:args.profile_stacks]:
+                        print(f"    {fr}", file=sys.stderr)
     B = args.batch
     ms = dt / args.steps * 1e3
     value = B * world * args.steps / dt
