@@ -80,6 +80,11 @@ void cast_bf16_launch(const float*, uint16_t*, long long, hipStream_t);
 void reduce_probe_launch(const float*, float*, hipStream_t);
 void fold_replicas_launch(float*, float*, long long, int, hipStream_t);
 void slab_reduce_launch(const SlabJob&, hipStream_t);
+void pe_proj_fwd_launch(const float*, int, const float*, const float*, const float*, const float*, const float*,
+                        const float*, long long, int, int, int, float, uint16_t*, float*, float*, hipStream_t);
+int pe_proj_bwd_blocks(int);
+void pe_proj_bwd_launch(const float*, const float*, int, const float*, const float*, int, int, int, float*, float*,
+                        hipStream_t);
 }  // namespace pio
 
 using torch::Tensor;
@@ -632,6 +637,50 @@ void cast_bf16(Tensor x, Tensor y) {
   pio::cast_bf16_launch(f32p(x), reinterpret_cast<uint16_t*>(y.data_ptr()), x.numel(), stream());
 }
 
+// factored LN + K/V projection over [pixels ‖ PE] (pe_proj.hip).  pix (R, nc) with R = B·M,
+// P (M, O) = (E⊙γ_e)·W_eᵀ, pes/pesq (M), wpg (nc, O), gw/bw (O) → y bf16 (R, O), mean/rstd (R)
+std::vector<Tensor> pe_proj_fwd(Tensor pix, Tensor P, Tensor pes, Tensor pesq, Tensor wpg, Tensor gw, Tensor bw,
+                                int64_t kin, double eps) {
+  for (const Tensor* t : {&pix, &P, &pes, &pesq, &wpg, &gw, &bw}) {
+    CHECK_CUDA(*t); CHECK_DT(*t, torch::kFloat32);
+    TORCH_CHECK(t->is_contiguous(), "pe_proj_fwd: operands must be contiguous");
+  }
+  TORCH_CHECK(pix.dim() == 2 && P.dim() == 2, "pe_proj_fwd: pix (R, nc), P (M, O)");
+  const long long R = pix.size(0);
+  const int nc = (int)pix.size(1), M = (int)P.size(0), O = (int)P.size(1);
+  TORCH_CHECK(nc >= 1 && nc <= 4 && O % 4 == 0 && O <= 512 && M > 0 && R % M == 0 && kin > nc,
+              "pe_proj_fwd: need 1 <= nc <= 4, O % 4 == 0, O <= 512, R a multiple of M");
+  TORCH_CHECK(pes.numel() == M && pesq.numel() == M && wpg.size(0) == nc && wpg.size(1) == O && gw.numel() == O &&
+                  bw.numel() == O, "pe_proj_fwd: operand shapes");
+  auto y = torch::empty({R, O}, pix.options().dtype(torch::kBFloat16));
+  auto mean = torch::empty({R}, pix.options());
+  auto rstd = torch::empty({R}, pix.options());
+  if (R > 0)
+    pio::pe_proj_fwd_launch(f32p(pix), nc, f32p(P), f32p(pes), f32p(pesq), f32p(wpg), f32p(gw), f32p(bw), R, M, O,
+                            (int)kin, (float)eps, bfp_mut(y), mean.data_ptr<float>(), rstd.data_ptr<float>(), stream());
+  return {y, mean, rstd};
+}
+
+// backward pass over dY (R, O): D (M, O) and per-block partials (nblk, (2 + nc)·O) of
+// [Σ dY | Σ dY·μ·rσ | Σ dY·x̂_c (c < nc)]
+std::vector<Tensor> pe_proj_bwd(Tensor dy, Tensor pix, Tensor mean, Tensor rstd, int64_t M) {
+  for (const Tensor* t : {&dy, &pix, &mean, &rstd}) {
+    CHECK_CUDA(*t); CHECK_DT(*t, torch::kFloat32);
+    TORCH_CHECK(t->is_contiguous(), "pe_proj_bwd: operands must be contiguous");
+  }
+  TORCH_CHECK(dy.dim() == 2 && pix.dim() == 2 && dy.size(0) == pix.size(0), "pe_proj_bwd: dy (R, O), pix (R, nc)");
+  const long long R = dy.size(0);
+  const int nc = (int)pix.size(1), O = (int)dy.size(1);
+  TORCH_CHECK(M > 0 && R % M == 0 && R / M <= INT32_MAX && nc >= 1 && nc <= 4 && O % 4 == 0 && O <= 512 &&
+                  mean.numel() == R && rstd.numel() == R, "pe_proj_bwd: shapes");
+  const int nblk = pio::pe_proj_bwd_blocks((int)M);
+  auto D = torch::empty({M, O}, dy.options());
+  auto part = torch::empty({nblk, (2 + nc) * O}, dy.options());
+  pio::pe_proj_bwd_launch(f32p(dy), f32p(pix), nc, f32p(mean), f32p(rstd), (int)(R / M), (int)M, O,
+                          D.data_ptr<float>(), part.data_ptr<float>(), stream());
+  return {D, part};
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "Perceiver IO CDNA4 (gfx950) kernels";
   m.def("attn_fwd", &attn_fwd);
@@ -675,5 +724,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("reduce_probe", &reduce_probe);
   m.def("fold_replicas", &fold_replicas);
   m.def("slab_reduce", &slab_reduce);
+  m.def("pe_proj_fwd", &pe_proj_fwd);
+  m.def("pe_proj_bwd", &pe_proj_bwd);
   m.attr("arch") = "gfx950";
 }

@@ -60,6 +60,29 @@ def ln_linear_fwd(x, lnw, lnb, eps, w, bias, act, res, out_bf16, save_stats, pe=
     return out
 
 
+def pe_proj_fwd(pix, P, pes, pesq, wpg, gw, bw, kin, eps):
+    """csrc/pe_proj.hip forward: factored LN + K/V projection over [pixels ‖ PE]."""
+    M = P.shape[0]
+    R = pix.shape[0]
+    m = torch.arange(R, device=pix.device) % M
+    s = pes[m] + pix.sum(1)
+    sq = pesq[m] + (pix * pix).sum(1)
+    mu = s / kin
+    rs = torch.rsqrt((sq / kin - mu * mu).clamp(min=0) + eps)
+    y = (P[m] + pix @ wpg) * rs[:, None] - (mu * rs)[:, None] * gw + bw
+    return [y.to(torch.bfloat16), mu, rs]
+
+
+def pe_proj_bwd(dy, pix, mean, rstd, M):
+    """csrc/pe_proj.hip backward: D = Σ_b dY·rσ and one 'partial' row [ΣdY | ΣdY·μ·rσ | ΣdY·x̂_c]."""
+    R, O = dy.shape
+    B = R // M
+    D = (dy * rstd[:, None]).view(B, M, O).sum(0)
+    xh = (pix - mean[:, None]) * rstd[:, None]
+    part = torch.cat([dy.sum(0), (dy * (mean * rstd)[:, None]).sum(0), (xh.t() @ dy).reshape(-1)])
+    return [D, part[None]]
+
+
 _SLAB = [False]
 
 

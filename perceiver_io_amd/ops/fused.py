@@ -262,6 +262,38 @@ class KVSource:
         return full
 
 
+# K/V projection over [pixels ‖ Fourier PE] in factored form (csrc/pe_proj.hip): the PE part of
+# LN(x)·Wᵀ is batch-independent, so it is one (M × Kin)·(Kin × O) GEMM per step and each sample
+# only pays a bandwidth-bound epilogue.  PERCEIVER_PE_FACTORED=0 restores the fused ln_linear path.
+PE_FACTORED = os.environ.get("PERCEIVER_PE_FACTORED", "1") != "0"
+
+
+def _pe_proj_fwd(K, pix, pe, g, b, W, bias):
+    """pix (B·M, nc) pixel channels, pe (M, ≥Kin) padded PE table with zero pixel columns,
+    g/b (Kin) kv_norm affine, W (O, Kin) fp32 K‖V weights, bias (O) → bf16 (B·M, O), mean, rstd."""
+    nc, kin = pix.shape[1], g.shape[0]
+    pe_e = pe[:, nc:kin]
+    P = torch.mm(pe_e * g[nc:], W[:, nc:].t()).contiguous()
+    wpg = (W[:, :nc] * g[:nc]).t().contiguous()
+    gw = torch.mv(W, g).contiguous()
+    bw = (torch.mv(W, b) + bias).contiguous()
+    return K.pe_proj_fwd(pix, P, pe_e.sum(1).contiguous(), (pe_e * pe_e).sum(1).contiguous(), wpg, gw, bw, kin, EPS)
+
+
+def _pe_proj_bwd(K, dy, pix, mean, rstd, pe, g, b, W, M):
+    """Gradients of _pe_proj_fwd w.r.t. W, bias, g, b from one streaming pass over dy (B·M, O):
+    G[o,c] = Σ dY_o·x̂_c (pixel channels from the kernel, PE channels = E_cᵀ·D − e),
+    dW = G⊙γ + S⊗β, db = S, dγ = Σ_o W⊙G, dβ = Wᵀ·S."""
+    nc, kin, O = pix.shape[1], g.shape[0], dy.shape[1]
+    D, part = K.pe_proj_bwd(dy, pix, mean, rstd, M)
+    tot = part.sum(0)
+    S, e, Gp = tot[:O], tot[O:2 * O], tot[2 * O:].view(nc, O)
+    Ge = torch.mm(pe[:, nc:kin].t(), D) - e[None, :]
+    G = torch.cat([Gp, Ge], 0).t()  # (O, Kin)
+    dW = G * g[None, :] + S[:, None] * b[None, :]
+    return dW, S, (W * G).sum(0), torch.mv(W.t(), S)
+
+
 class _LayerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, spec: LayerSpec, bw, seed, p_attn, src, x_q, x_kv, kmask, *ps):
@@ -289,9 +321,15 @@ class _LayerFn(torch.autograd.Function):
             ent = src.entries.get(key) if src is not None else None
             ctx.kv_owner = ent is None
             if ent is None:  # first application of this layer: project K/V (LN over [pixels ‖ PE] if split)
-                kv, mean_kv, rstd_kv = K.ln_linear_fwd(xkv2, g_kv, b_kv, EPS, wkv, bin_[C:], 0, None, True, True,
-                                                       src.pe if src is not None else None, g_kv.shape[0])
-                ent = {"kv": kv, "mean": mean_kv, "rstd": rstd_kv, "dkv": None}
+                factored = (PE_FACTORED and src is not None and src.pe is not None and not spec.packed
+                            and not ctx.needs_input_grad[6] and 1 <= xkv2.shape[1] <= 4 and 2 * C <= 512)
+                if factored:
+                    kv, mean_kv, rstd_kv = _pe_proj_fwd(K, xkv2, src.pe, g_kv, b_kv,
+                                                        torch.cat([ps[5], ps[6]], 0), bin_[C:])
+                else:
+                    kv, mean_kv, rstd_kv = K.ln_linear_fwd(xkv2, g_kv, b_kv, EPS, wkv, bin_[C:], 0, None, True, True,
+                                                           src.pe if src is not None else None, g_kv.shape[0])
+                ent = {"kv": kv, "mean": mean_kv, "rstd": rstd_kv, "dkv": None, "factored": factored}
                 if src is not None:
                     src.entries[key] = ent
             kv, mean_kv, rstd_kv = ent["kv"], ent["mean"], ent["rstd"]
@@ -416,7 +454,20 @@ class _LayerFn(torch.autograd.Function):
             if ctx.kv_owner:  # the projection's backward, once, over the summed dK/dV
                 dkv2 = dkv.view(B * M, 2 * C)
                 Rkv = dkv2.shape[0]
-                if WGRAD_SLAB and Rkv < TALL_ROWS:
+                if ent.get("factored"):
+                    dW, db, dg, dbeta = _pe_proj_bwd(K, dkv2, xkv2, mean_kv, rstd_kv, ctx.kv_pe, g_kv, b_kv,
+                                                     torch.cat([ps[5], ps[6]], 0), M)
+
+                    def add(t, v):
+                        (t[0] if rep_mode else t).view(-1).add_(v.reshape(-1))
+
+                    add(gb(g_kv), dg)
+                    add(gb(b_kv), dbeta)
+                    add(gb(ps[5]), dW[:C])
+                    add(gb(ps[6]), dW[C:])
+                    gbias = gb(bin_)
+                    (gbias[0, C:3 * C] if rep_mode else gbias[C:3 * C]).add_(db)
+                elif WGRAD_SLAB and Rkv < TALL_ROWS:
                     sl = _GradSlab(Rkv, [Ckv, Ckv, 2 * C * Ckv, 2 * C], dz2)
                     dx_kv = K.ln_linear_bwd(dkv2, wkv, xkv2, mean_kv, rstd_kv, g_kv, b_kv, None, ctx.kv_grad,
                                             *sl.targets(), ctx.kv_pe, Ckv, slab=True, **_take_job())

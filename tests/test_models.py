@@ -230,3 +230,40 @@ def test_fused_executor_replicated_gradients_fold_to_eager(slab, monkeypatch):
     for n, p in enc.named_parameters():
         if n in g_ref:
             assert (p.grad - g_ref[n]).abs().max() < 0.03 * gmax, n
+
+
+def check_factored_pe_projection(K, device, channels, B=3, M=120, O=64, tol=2e-3):
+    """ops/fused.py _pe_proj_fwd/_pe_proj_bwd (csrc/pe_proj.hip: per-step PE GEMM + per-sample
+    epilogue + one streaming backward pass) against fp32 autograd of LayerNorm + Linear over the
+    materialised [pixels ‖ PE] rows (reference adapter.py:106-109, model.py:89-99)."""
+    import torch.nn.functional as F
+
+    g = torch.Generator().manual_seed(channels)
+    kin = channels + 40
+    pe = torch.zeros(M, (kin + 7) // 8 * 8)
+    pe[:, channels:kin] = torch.rand(M, kin - channels, generator=g) * 2 - 1
+    pix = torch.randn(B * M, channels, generator=g)
+    lnw = 1 + 0.3 * torch.randn(kin, generator=g)
+    lnb = 0.3 * torch.randn(kin, generator=g)
+    W = torch.randn(O, kin, generator=g) / kin ** 0.5
+    bias = 0.3 * torch.randn(O, generator=g)
+    dy = torch.randn(B * M, O, generator=g)
+    t = [v.double().requires_grad_() for v in (lnw, lnb, W, bias)]
+    full = pe[:, :kin].repeat(B, 1).double()
+    full[:, :channels] += pix.double()
+    y = F.linear(F.layer_norm(full, (kin,), t[0], t[1], 1e-5), t[2], t[3])
+    y.backward(dy.double())
+    dev = [v.to(device) for v in (pix, pe, lnw, lnb, W, bias, dy)]
+    yk, mean, rstd = ops.fused._pe_proj_fwd(K, *dev[:6])
+    assert (yk.float().cpu().double() - y.detach()).abs().max() < 1e-2 * y.abs().max()
+    got = ops.fused._pe_proj_bwd(K, dev[6], dev[0], mean, rstd, dev[1], dev[2], dev[3], dev[4], M)
+    for name, a, ref in zip(("dW", "db", "dln_w", "dln_b"), got, (t[2].grad, t[3].grad, t[0].grad, t[1].grad)):
+        err = (a.cpu().double() - ref).abs().max() / ref.abs().max()
+        assert err < tol, (name, err.item())
+
+
+@pytest.mark.parametrize("channels", [1, 3, 4])
+def test_factored_pe_projection_matches_autograd(channels):
+    from perceiver_io_amd.ops import emulation
+
+    check_factored_pe_projection(emulation, "cpu", channels)
