@@ -22,51 +22,73 @@
 
 namespace pio {
 
-// one wave per input row r = b·M + m; lanes stride the O outputs four at a time
+// one wave per pixel m: P'[m] (≤ 512 outputs) is read once into registers and reused for the
+// B rows r = b·M + m of that pixel (a row-per-wave mapping would re-read it B times)
 __global__ __launch_bounds__(256) void pe_proj_fwd_kernel(
     const float* __restrict__ pix, int nc, const float* __restrict__ P, const float* __restrict__ pes,
     const float* __restrict__ pesq, const float* __restrict__ wpg, const float* __restrict__ gw,
-    const float* __restrict__ bw, long long R, int M, int O, float inv_k, float eps, uint16_t* __restrict__ y,
-    float* __restrict__ mean, float* __restrict__ rstd) {
+    const float* __restrict__ bw, int B, int bchunk, int M, int O, float inv_k, float eps,
+    uint16_t* __restrict__ y, float* __restrict__ mean, float* __restrict__ rstd) {
   const int lane = threadIdx.x & 63;
-  const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+  const int b0 = blockIdx.y * bchunk, b1 = b0 + bchunk < B ? b0 + bchunk : B;  // this block's batch slice
+  const int nw = (gridDim.x * blockDim.x) >> 6;
   const int O4 = O >> 2;
-  for (long long r = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < R; r += nw) {
-    const int m = (int)(r % M);
-    float px[4] = {0.f, 0.f, 0.f, 0.f};
-    float s = pes[m], sq = pesq[m];
+  float4 wc[4][2], g[2], bb[2];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      if (c < nc) {
-        const float v = pix[r * nc + c];
-        px[c] = v;
-        s += v;
-        sq += v * v;
-      }
+  for (int j = 0; j < 2; ++j) {
+    const int o4 = lane + 64 * j;
+    const bool ok = o4 < O4;
+    g[j] = ok ? reinterpret_cast<const float4*>(gw)[o4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    bb[j] = ok ? reinterpret_cast<const float4*>(bw)[o4] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      wc[c][j] = (ok && c < nc) ? reinterpret_cast<const float4*>(wpg + (long long)c * O)[o4]
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  for (int m = ((int)(blockIdx.x * blockDim.x + threadIdx.x)) >> 6; m < M; m += nw) {
+    float4 pm[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int o4 = lane + 64 * j;
+      pm[j] = o4 < O4 ? reinterpret_cast<const float4*>(P + (long long)m * O)[o4] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    const float mu = s * inv_k;
-    const float var = fmaxf(sq * inv_k - mu * mu, 0.f);
-    const float rs = rsqrtf(var + eps);
-    const float mrs = mu * rs;
-    if (lane == 0) {
-      mean[r] = mu;
-      rstd[r] = rs;
-    }
-    const float4* Pm = reinterpret_cast<const float4*>(P + (long long)m * O);
-    uint2* yr = reinterpret_cast<uint2*>(y + r * O);
-    for (int o4 = lane; o4 < O4; o4 += 64) {
-      float4 a = Pm[o4];
+    const float pes_m = pes[m], pesq_m = pesq[m];
+#pragma unroll 2
+    for (int b = b0; b < b1; ++b) {
+      const long long r = (long long)b * M + m;
+      float px[4] = {0.f, 0.f, 0.f, 0.f};
+      float s = pes_m, sq = pesq_m;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         if (c < nc) {
-          const float4 w = reinterpret_cast<const float4*>(wpg + (long long)c * O)[o4];
-          a.x += px[c] * w.x; a.y += px[c] * w.y; a.z += px[c] * w.z; a.w += px[c] * w.w;
+          const float v = pix[r * nc + c];
+          px[c] = v;
+          s += v;
+          sq += v * v;
         }
       }
-      const float4 g = reinterpret_cast<const float4*>(gw)[o4];
-      const float4 b = reinterpret_cast<const float4*>(bw)[o4];
-      yr[o4] = make_uint2(pack2(a.x * rs - mrs * g.x + b.x, a.y * rs - mrs * g.y + b.y),
-                          pack2(a.z * rs - mrs * g.z + b.z, a.w * rs - mrs * g.w + b.w));
+      const float mu = s * inv_k;
+      const float var = fmaxf(sq * inv_k - mu * mu, 0.f);
+      const float rs = rsqrtf(var + eps);
+      const float mrs = mu * rs;
+      if (lane == 0) {
+        mean[r] = mu;
+        rstd[r] = rs;
+      }
+      uint2* yr = reinterpret_cast<uint2*>(y + r * O);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int o4 = lane + 64 * j;
+        if (o4 < O4) {
+          float4 a = pm[j];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            a.x += px[c] * wc[c][j].x; a.y += px[c] * wc[c][j].y; a.z += px[c] * wc[c][j].z; a.w += px[c] * wc[c][j].w;
+          }
+          yr[o4] = make_uint2(pack2(a.x * rs - mrs * g[j].x + bb[j].x, a.y * rs - mrs * g[j].y + bb[j].y),
+                              pack2(a.z * rs - mrs * g[j].z + bb[j].z, a.w * rs - mrs * g[j].w + bb[j].w));
+        }
+      }
     }
   }
 }
@@ -137,10 +159,15 @@ __global__ __launch_bounds__(256) void pe_proj_bwd_kernel(
 void pe_proj_fwd_launch(const float* pix, int nc, const float* P, const float* pes, const float* pesq,
                         const float* wpg, const float* gw, const float* bw, long long R, int M, int O, int kin,
                         float eps, uint16_t* y, float* mean, float* rstd, hipStream_t st) {
-  long long blocks = (R + 3) / 4;
-  if (blocks > 65536) blocks = 65536;
-  hipLaunchKernelGGL(pe_proj_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, st, pix, nc, P, pes, pesq, wpg, gw,
-                     bw, R, M, O, 1.f / (float)kin, eps, y, mean, rstd);
+  // one wave per pixel looping over a batch slice; small images split the batch over
+  // blockIdx.y so the grid still holds ≥ 16k waves
+  const int B = (int)(R / M);
+  int splits = (16384 + M - 1) / M;
+  splits = splits < 1 ? 1 : (splits > B ? B : splits);
+  const int bchunk = (B + splits - 1) / splits;
+  const dim3 grid((unsigned)((M + 3) / 4), (unsigned)((B + bchunk - 1) / bchunk));
+  hipLaunchKernelGGL(pe_proj_fwd_kernel, grid, dim3(256), 0, st, pix, nc, P, pes, pesq, wpg, gw, bw, B, bchunk, M, O,
+                     1.f / (float)kin, eps, y, mean, rstd);
 }
 
 int pe_proj_bwd_blocks(int M) {

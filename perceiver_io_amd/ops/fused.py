@@ -273,7 +273,14 @@ def _pe_proj_fwd(K, pix, pe, g, b, W, bias):
     g/b (Kin) kv_norm affine, W (O, Kin) fp32 K‖V weights, bias (O) → bf16 (B·M, O), mean, rstd."""
     nc, kin = pix.shape[1], g.shape[0]
     pe_e = pe[:, nc:kin]
-    P = torch.mm(pe_e * g[nc:], W[:, nc:].t()).contiguous()
+    # P' over the whole padded table (pixel and pad columns of pe are zero): an 8-aligned
+    # contraction keeps the library GEMM on its fast path
+    kp = pe.shape[1]
+    ge = torch.zeros(kp, device=g.device, dtype=g.dtype)
+    ge[nc:kin] = g[nc:]
+    wp = torch.zeros((W.shape[0], kp), device=W.device, dtype=W.dtype)
+    wp[:, :kin] = W
+    P = torch.mm(pe * ge, wp.t())
     wpg = (W[:, :nc] * g[:nc]).t().contiguous()
     gw = torch.mv(W, g).contiguous()
     bw = (torch.mv(W, b) + bias).contiguous()
@@ -288,7 +295,7 @@ def _pe_proj_bwd(K, dy, pix, mean, rstd, pe, g, b, W, M):
     D, part = K.pe_proj_bwd(dy, pix, mean, rstd, M)
     tot = part.sum(0)
     S, e, Gp = tot[:O], tot[O:2 * O], tot[2 * O:].view(nc, O)
-    Ge = torch.mm(pe[:, nc:kin].t(), D) - e[None, :]
+    Ge = torch.mm(pe.t(), D)[nc:kin] - e[None, :]
     G = torch.cat([Gp, Ge], 0).t()  # (O, Kin)
     dW = G * g[None, :] + S[:, None] * b[None, :]
     return dW, S, (W * G).sum(0), torch.mv(W.t(), S)

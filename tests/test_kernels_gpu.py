@@ -93,6 +93,11 @@ def _attn_inputs(B, Bq, Nq, Nk, H, D, packed=True, mask=True):
     (2, 2, 32, 1000, 4, 32, 4),
     (2, 2, 96, 64, 2, 64, 1),
     (2, 2, 33, 80, 1, 128, 2),
+    # ≥ 4 key blocks per (batch, head) adding into dQ
+    (2, 2, 40, 3000, 4, 16, 4),
+    (2, 1, 40, 1200, 4, 16, 2),
+    (2, 2, 64, 2000, 2, 64, 4),
+    (2, 2, 33, 800, 1, 128, 2),
 ])
 def test_attention_fwd_bwd(B, Bq, Nq, Nk, H, D, ns):
     torch.manual_seed(1)
