@@ -172,7 +172,7 @@ void pe_proj_fwd_launch(const float* pix, int nc, const float* P, const float* p
 
 int pe_proj_bwd_blocks(int M) {
   int blocks = (M + 3) / 4;
-  return blocks > 2048 ? 2048 : blocks;
+  return blocks > 8192 ? 8192 : blocks;
 }
 
 void pe_proj_bwd_launch(const float* dy, const float* pix, int nc, const float* mean, const float* rstd, int B, int M,
