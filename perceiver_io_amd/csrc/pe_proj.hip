@@ -52,29 +52,34 @@ __global__ __launch_bounds__(256) void pe_proj_fwd_kernel(
       const int o4 = lane + 64 * j;
       pm[j] = o4 < O4 ? reinterpret_cast<const float4*>(P + (long long)m * O)[o4] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    const float pes_m = pes[m], pesq_m = pesq[m];
-#pragma unroll 2
-    for (int b = b0; b < b1; ++b) {
-      const long long r = (long long)b * M + m;
-      float px[4] = {0.f, 0.f, 0.f, 0.f};
-      float s = pes_m, sq = pesq_m;
+    // row statistics lane-parallel (lane i ↔ sample b0 + i, bchunk ≤ 64), then broadcast with
+    // cross-lane reads inside the loop: no dependent global load per output row
+    float my_mu = 0.f, my_rs = 0.f, my_px[4] = {0.f, 0.f, 0.f, 0.f};
+    if (b0 + lane < b1) {
+      const long long r = (long long)(b0 + lane) * M + m;
+      float s = pes[m], sq = pesq[m];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         if (c < nc) {
           const float v = pix[r * nc + c];
-          px[c] = v;
+          my_px[c] = v;
           s += v;
           sq += v * v;
         }
       }
-      const float mu = s * inv_k;
-      const float var = fmaxf(sq * inv_k - mu * mu, 0.f);
-      const float rs = rsqrtf(var + eps);
+      my_mu = s * inv_k;
+      my_rs = rsqrtf(fmaxf(sq * inv_k - my_mu * my_mu, 0.f) + eps);
+      mean[r] = my_mu;
+      rstd[r] = my_rs;
+    }
+#pragma unroll 4
+    for (int b = b0; b < b1; ++b) {
+      const long long r = (long long)b * M + m;
+      const float mu = __shfl(my_mu, b - b0), rs = __shfl(my_rs, b - b0);
+      float px[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) px[c] = __shfl(my_px[c], b - b0);
       const float mrs = mu * rs;
-      if (lane == 0) {
-        mean[r] = mu;
-        rstd[r] = rs;
-      }
       uint2* yr = reinterpret_cast<uint2*>(y + r * O);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -110,25 +115,39 @@ __global__ __launch_bounds__(256) void pe_proj_bwd_kernel(
   }
   for (int m = blockIdx.x * 4 + wid; m < M; m += gridDim.x * 4) {
     float4 d[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+    for (int bb = 0; bb < B; bb += 64) {
+      // per-row factors lane-parallel (lane i ↔ sample bb + i), broadcast in the loop
+      float my_rs = 0.f, my_mrs = 0.f, my_xh[4] = {0.f, 0.f, 0.f, 0.f};
+      if (bb + lane < B) {
+        const long long r = (long long)(bb + lane) * M + m;
+        my_rs = rstd[r];
+        const float mu = mean[r];
+        my_mrs = mu * my_rs;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (c < nc) my_xh[c] = (pix[r * nc + c] - mu) * my_rs;
+      }
+      const int be = B - bb < 64 ? B - bb : 64;
 #pragma unroll 4
-    for (int b = 0; b < B; ++b) {
-      const long long r = (long long)b * M + m;
-      const float rs = rstd[r], mu = mean[r], mrs = mu * rs;
-      float xh[4];
+      for (int i = 0; i < be; ++i) {
+        const long long r = (long long)(bb + i) * M + m;
+        const float rs = __shfl(my_rs, i), mrs = __shfl(my_mrs, i);
+        float xh[4];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) xh[c] = c < nc ? (pix[r * nc + c] - mu) * rs : 0.f;
-      const float4* dyr = reinterpret_cast<const float4*>(dy + r * O);
+        for (int c = 0; c < 4; ++c) xh[c] = __shfl(my_xh[c], i);
+        const float4* dyr = reinterpret_cast<const float4*>(dy + r * O);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int o4 = lane + 64 * j;
-        if (o4 < O4) {
-          const float4 v = dyr[o4];
-          d[j].x += v.x * rs; d[j].y += v.y * rs; d[j].z += v.z * rs; d[j].w += v.w * rs;
-          S[j].x += v.x; S[j].y += v.y; S[j].z += v.z; S[j].w += v.w;
-          E[j].x += v.x * mrs; E[j].y += v.y * mrs; E[j].z += v.z * mrs; E[j].w += v.w * mrs;
+        for (int j = 0; j < 2; ++j) {
+          const int o4 = lane + 64 * j;
+          if (o4 < O4) {
+            const float4 v = dyr[o4];
+            d[j].x += v.x * rs; d[j].y += v.y * rs; d[j].z += v.z * rs; d[j].w += v.w * rs;
+            S[j].x += v.x; S[j].y += v.y; S[j].z += v.z; S[j].w += v.w;
+            E[j].x += v.x * mrs; E[j].y += v.y * mrs; E[j].z += v.z * mrs; E[j].w += v.w * mrs;
 #pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            G[c][j].x += v.x * xh[c]; G[c][j].y += v.y * xh[c]; G[c][j].z += v.z * xh[c]; G[c][j].w += v.w * xh[c];
+            for (int c = 0; c < 4; ++c) {
+              G[c][j].x += v.x * xh[c]; G[c][j].y += v.y * xh[c]; G[c][j].z += v.z * xh[c]; G[c][j].w += v.w * xh[c];
+            }
           }
         }
       }
@@ -164,6 +183,7 @@ void pe_proj_fwd_launch(const float* pix, int nc, const float* P, const float* p
   const int B = (int)(R / M);
   int splits = (16384 + M - 1) / M;
   splits = splits < 1 ? 1 : (splits > B ? B : splits);
+  if ((B + splits - 1) / splits > 64) splits = (B + 63) / 64;  // a batch slice fits one wave's lanes
   const int bchunk = (B + splits - 1) / splits;
   const dim3 grid((unsigned)((M + 3) / 4), (unsigned)((B + bchunk - 1) / bchunk));
   hipLaunchKernelGGL(pe_proj_fwd_kernel, grid, dim3(256), 0, st, pix, nc, P, pes, pesq, wpg, gw, bw, B, bchunk, M, O,

@@ -365,7 +365,8 @@ def test_embed_mask_adamw():
         close(a_, b_, 1e-5, nme)
 
 
-@pytest.mark.parametrize("channels,B,M,O", [(3, 2, 50176, 256), (1, 4, 784, 256), (4, 3, 1000, 512), (2, 5, 333, 128)])
+@pytest.mark.parametrize("channels,B,M,O", [(3, 2, 50176, 256), (1, 4, 784, 256), (4, 3, 1000, 512), (2, 5, 333, 128),
+                                              (2, 130, 40, 128)])
 def test_factored_pe_projection_kernels(channels, B, M, O):
     """csrc/pe_proj.hip forward epilogue + streaming backward vs fp64 autograd of LayerNorm +
     Linear over the materialised [pixels ‖ PE] rows (ImageNet shape first: M = 224·224)."""
