@@ -27,6 +27,8 @@
 // Both directions stage the next K/V (forward) or Q/dO (backward) tile in registers while
 // the current tile's MFMAs run, so global latency is paid once per kernel, not per tile.
 // Fully-masked query rows produce O = 0 and zero gradients (defect D10 defined).
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace pio {
@@ -337,7 +339,9 @@ __global__ void attn_bwd_prep_kernel(const uint16_t* __restrict__ dO, const uint
     for (int j = l; j < HD; j += 64) dq[(long long)row * dq_rs + j] = 0.f;
 }
 
-template <int D, int NW>
+// QR > 0 fixes the query tiles per round (QR = 1 for ≤ 32 queries: a quarter of the LDS, so
+// several workgroups share a CU on the few-query / many-key encoder cross-attention)
+template <int D, int NW, int QR = 0>
 __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uint16_t* __restrict__ dO,
                                                            const float* __restrict__ LSE,
                                                            const float* __restrict__ delta, float* __restrict__ dq,
@@ -355,7 +359,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
   // after one barrier wave j (< NQS) forms tile j's dQ over all KB keys of the block with
   // MFMAs (no cross-wave reduction, no atomics inside the block).
   constexpr int NQS0 = 4 * NTH / (64 * CH);
-  constexpr int NQS = NQS0 >= 4 ? 4 : (NQS0 >= 1 ? NQS0 : 1);
+  constexpr int NQS = QR > 0 ? QR : (NQS0 >= 4 ? 4 : (NQS0 >= 1 ? NQS0 : 1));
   constexpr int NI = (NQS * 64 * CH + NTH - 1) / NTH;
   __shared__ __attribute__((aligned(16))) uint16_t sQ[NQS * 32 * LD + 64];
   __shared__ __attribute__((aligned(16))) uint16_t sdO[NQS * 32 * LD + 64];
@@ -571,7 +575,8 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
   PIO_TS(40);
   // write dK (scaled) and dV: rows = keys (registers), lane = head-dim column
   // accumulator: col = lane&31 = d, row = acc_row(reg) = key within the wave's 32
-  if constexpr (D <= 32) {
+  // (needs the dS slabs to hold both [KB][D + 4] fp32 tiles: not in the QR = 1 variant)
+  if constexpr (D <= 32 && 2 * KB * (D + 4) * 4 <= NQS * KB * LDS_ * 2) {
     if (vec_out) {  // transpose through LDS (the dS slabs are consumed), 16-byte row stores
       constexpr int LDE = D + 4, CPR = D / 4;
       float* sE = reinterpret_cast<float*>(sdS);  // [dK | dV][KB keys][LDE]
@@ -669,6 +674,15 @@ void attn_fwd_launch(const AttnArgs& a, int D, uint16_t* O, float* LSE, float* O
   }
 }
 
+static bool getenv_flag(const char* name) {
+  static int cached = -1;  // one knob; read once
+  if (cached < 0) {
+    const char* v = getenv(name);
+    cached = (v && v[0] && v[0] != '0') ? 1 : 0;
+  }
+  return cached == 1;
+}
+
 template <int D, int NW>
 static void bwd_launch_t(const AttnArgs& a, const uint16_t* dO, const float* LSE, float* delta, float* dq,
                          long long dq_bs, int dq_rs, float* dk, long long dk_bs, int dk_rs, float* dv, long long dv_bs,
@@ -680,8 +694,12 @@ static void bwd_launch_t(const AttnArgs& a, const uint16_t* dO, const float* LSE
                        st, dq, dq_bs, dq_rs, a.Nq, a.H * D, total);
   }
   dim3 grid(nkb, a.H, a.B);
-  hipLaunchKernelGGL((attn_bwd_kernel<D, NW>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs, dk,
-                     dk_bs, dk_rs, dv, dv_bs, dv_rs, nkb > 1 ? 1 : 0, kv_acc);
+  if (a.Nq <= 32 && !getenv_flag("PIO_ATTN_BWD_FULL_LDS"))
+    hipLaunchKernelGGL((attn_bwd_kernel<D, NW, 1>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs,
+                       dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, nkb > 1 ? 1 : 0, kv_acc);
+  else
+    hipLaunchKernelGGL((attn_bwd_kernel<D, NW>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs, dk,
+                       dk_bs, dk_rs, dv, dv_bs, dv_rs, nkb > 1 ? 1 : 0, kv_acc);
 }
 
 void attn_bwd_launch(const AttnArgs& a, int D, const uint16_t* O, const uint16_t* dO, const float* LSE, float* delta,
