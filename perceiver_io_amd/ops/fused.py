@@ -280,11 +280,23 @@ def _pe_proj_fwd(K, pix, pe, g, b, W, bias):
     ge[nc:kin] = g[nc:]
     wp = torch.zeros((W.shape[0], kp), device=W.device, dtype=W.dtype)
     wp[:, :kin] = W
-    P = torch.mm(pe * ge, wp.t())
+    # bf16 operands, fp32 accumulation: the same product precision as the MFMA projection it
+    # replaces (its output feeds a bf16 K/V), at a fraction of an fp32 library GEMM's time
+    P = torch.mm((pe * ge).to(torch.bfloat16), wp.to(torch.bfloat16).t()).float()
     wpg = (W[:, :nc] * g[:nc]).t().contiguous()
     gw = torch.mv(W, g).contiguous()
     bw = (torch.mv(W, b) + bias).contiguous()
     return K.pe_proj_fwd(pix, P, pe_e.sum(1).contiguous(), (pe_e * pe_e).sum(1).contiguous(), wpg, gw, bw, kin, EPS)
+
+
+def _mm_tn_split(a, b):
+    """aᵀ·b for tall a (M, K1), b (M, K2): the long contraction is split into batches of a
+    bmm (split-K) so the small (K1 × K2) output still spreads over the whole GPU."""
+    M = a.shape[0]
+    s = max((d for d in range(1, 65) if M % d == 0 and M // d >= 256), default=1)
+    if s == 1:
+        return torch.mm(a.t(), b)
+    return torch.bmm(a.reshape(s, M // s, a.shape[1]).transpose(1, 2), b.reshape(s, M // s, b.shape[1])).sum(0)
 
 
 def _pe_proj_bwd(K, dy, pix, mean, rstd, pe, g, b, W, M):
@@ -295,7 +307,7 @@ def _pe_proj_bwd(K, dy, pix, mean, rstd, pe, g, b, W, M):
     D, part = K.pe_proj_bwd(dy, pix, mean, rstd, M)
     tot = part.sum(0)
     S, e, Gp = tot[:O], tot[O:2 * O], tot[2 * O:].view(nc, O)
-    Ge = torch.mm(pe.t(), D)[nc:kin] - e[None, :]
+    Ge = _mm_tn_split(pe, D)[nc:kin] - e[None, :]
     G = torch.cat([Gp, Ge], 0).t()  # (O, Kin)
     dW = G * g[None, :] + S[:, None] * b[None, :]
     return dW, S, (W * G).sum(0), torch.mv(W.t(), S)
