@@ -339,8 +339,9 @@ __global__ void attn_bwd_prep_kernel(const uint16_t* __restrict__ dO, const uint
     for (int j = l; j < HD; j += 64) dq[(long long)row * dq_rs + j] = 0.f;
 }
 
-// QR > 0 fixes the query tiles per round (QR = 1 for ≤ 32 queries: a quarter of the LDS, so
-// several workgroups share a CU on the few-query / many-key encoder cross-attention)
+// QR > 0 fixes the query tiles per round (QR = 1 for ≤ 32 queries, 2 for ≤ 64: a quarter / half
+// of the LDS, so several workgroups share a CU on the few-query / many-key cross-attention;
+// PIO_ATTN_BWD_FULL_LDS=1 restores the 4-tile rounds)
 template <int D, int NW, int QR = 0>
 __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uint16_t* __restrict__ dO,
                                                            const float* __restrict__ LSE,
@@ -694,8 +695,12 @@ static void bwd_launch_t(const AttnArgs& a, const uint16_t* dO, const float* LSE
                        st, dq, dq_bs, dq_rs, a.Nq, a.H * D, total);
   }
   dim3 grid(nkb, a.H, a.B);
-  if (a.Nq <= 32 && !getenv_flag("PIO_ATTN_BWD_FULL_LDS"))
+  const bool small_lds = !getenv_flag("PIO_ATTN_BWD_FULL_LDS");
+  if (a.Nq <= 32 && small_lds)
     hipLaunchKernelGGL((attn_bwd_kernel<D, NW, 1>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs,
+                       dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, nkb > 1 ? 1 : 0, kv_acc);
+  else if (a.Nq <= 64 && small_lds)
+    hipLaunchKernelGGL((attn_bwd_kernel<D, NW, 2>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs,
                        dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, nkb > 1 ? 1 : 0, kv_acc);
   else
     hipLaunchKernelGGL((attn_bwd_kernel<D, NW>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs, dk,
