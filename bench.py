@@ -188,7 +188,8 @@ def main(argv=None):
         from perceiver_io_amd.ops.optim import FlatParameterSpace
 
         flat = opt.flat if fused else FlatParameterSpace(params, with_shadow=False, replicate=False)
-        reducer = FlatGradReducer(flat, bucket_bytes=64 << 20)
+        reducer = FlatGradReducer(flat)
+        reducer.set_early_params(model.decoder.parameters())  # all-reduced during the encoder backward
         reducer.broadcast_parameters(model)
 
     autocast = (not fused) and args.dtype == "bf16" and cuda

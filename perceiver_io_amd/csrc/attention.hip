@@ -67,7 +67,8 @@ struct AttnArgs {
   float scale;           // softmax scale (backward)
   uint32_t drop_thresh;  // dropout probability * 2^32 (0 = off)
   float drop_scale;      // 1 / (1 - p)
-  uint32_t seed;
+  const int64_t* seedp;  // device seed of the call (common.h DropCfg); read only when drop_thresh
+  uint32_t site;
 };
 
 // ------------------------------------------------------------------------------------
@@ -99,6 +100,7 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(AttnArgs a, uint16_t
   const int b = blk.z / nsplit, split = blk.z % nsplit;
   const int q0 = (blk.x * NWV + w) * 32;
   const int qi = q0 + r;
+  const uint32_t dkey = a.drop_thresh ? drop_key(a.seedp, a.site, 2u) : 0u;
   const int qc = qi < a.Nq ? qi : a.Nq - 1;
 
   // this wave's Q^T operand fragments (B operand: B[k=d][col=query])
@@ -239,7 +241,7 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(AttnArgs a, uint16_t
           for (int i = 0; i < 16; ++i) {
             const int key = key0 + 32 * kh + acc_row(i, hh);
             const uint32_t idx = (uint32_t)qi * (uint32_t)a.Nk + (uint32_t)key;
-            s[kh][i] = keep_elem(a.seed, (uint32_t)(b * a.H + h), idx, a.drop_thresh) ? s[kh][i] * a.drop_scale : 0.f;
+            s[kh][i] = keep_elem(dkey, (uint32_t)(b * a.H + h), idx, a.drop_thresh) ? s[kh][i] * a.drop_scale : 0.f;
           }
       }
       l_run = l_run * alpha + ls;
@@ -377,6 +379,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
   const int kbase = blk.x * KB;
   const int key = kbase + 32 * w + r;  // this lane's key (column of S / dP)
   const int kc = key < a.Nk ? key : a.Nk - 1;
+  const uint32_t dkey = a.drop_thresh ? drop_key(a.seedp, a.site, 2u) : 0u;
   bool kpad = key >= a.Nk;
   if (!kpad && a.kmask) kpad = a.kmask[(long long)b * a.Nk + key] != 0;
 
@@ -498,7 +501,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
         for (int i = 0; i < 16; ++i) {
           const float p = fast_exp2(kpad ? -INFINITY : S[i] * a.scale_log2 - lrow[i >> 2][i & 3]);
           const uint32_t idx = (uint32_t)(q0 + acc_row(i, hh)) * (uint32_t)a.Nk + (uint32_t)key;
-          const bool keep = keep_elem(a.seed, (uint32_t)(b * a.H + h), idx, a.drop_thresh);
+          const bool keep = keep_elem(dkey, (uint32_t)(b * a.H + h), idx, a.drop_thresh);
           P[i] = keep ? p * a.drop_scale : 0.f;
           dS[i] = p * ((keep ? dP[i] * a.drop_scale : 0.f) - drow[i >> 2][i & 3]);
         }

@@ -17,7 +17,14 @@ struct AttnArgs {
   float scale_log2, scale;
   uint32_t drop_thresh;
   float drop_scale;
-  uint32_t seed;
+  const int64_t* seedp;
+  uint32_t site;
+};
+struct DropCfg {  // common.h
+  const int64_t* seed;
+  uint32_t site;
+  uint32_t thresh;
+  float scale;
 };
 struct PostAttnGrads { float *dWo, *dbo, *dg2, *dbe2, *dW1, *db1, *dW2, *db2; int vrs; int slab; };
 constexpr int kMaxSlabSegs = 16, kSlabRowsPerBlock = 32;  // common.h
@@ -38,21 +45,22 @@ void ln_linear_fwd_launch(const void*, bool, int, int, int, const float*, const 
                           int, int, hipStream_t);
 void post_attn_fwd_launch(int, const uint16_t*, const float*, const uint16_t*, const float*, const float*,
                           const float*, float, const uint16_t*, const float*, const uint16_t*, const float*, float*,
-                          float*, float*, float*, uint16_t*, int, int, hipStream_t);
+                          float*, float*, float*, uint16_t*, int, int, const DropCfg&, hipStream_t);
 void post_attn_ln_linear_fwd_launch(int, const uint16_t*, const float*, const uint16_t*, const float*, const float*,
                                     const float*, float, const uint16_t*, const float*, const uint16_t*, const float*,
                                     float*, float*, float*, float*, uint16_t*, int, const float*, const float*,
-                                    const uint16_t*, const float*, uint16_t*, float*, float*, hipStream_t);
+                                    const uint16_t*, const float*, uint16_t*, float*, float*, const DropCfg&,
+                                    hipStream_t);
 void ln_linear_post_attn_bwd_launch(int, const float*, const uint16_t*, const float*, const float*, const float*,
                                     const float*, const float*, const float*, float*, float*, float*, float*,
                                     const float*, const float*, const float*, const uint16_t*, const uint16_t*,
                                     const uint16_t*, const uint16_t*, const uint16_t*, const float*, const float*,
                                     float*, uint16_t*, float*, int, const PostAttnGrads&, int, const SlabJob&,
-                                    hipStream_t);
+                                    const DropCfg&, hipStream_t);
 void post_attn_bwd_launch(int, const float*, const float*, const float*, const float*, const uint16_t*,
                           const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*, const float*,
                           const float*, float*, uint16_t*, float*, int, const PostAttnGrads&, int, const SlabJob&,
-                          hipStream_t);
+                          const DropCfg&, hipStream_t);
 void ln_linear_bwd_launch(const void*, bool, int, int, const uint16_t*, int, int, const void*, bool, int, const float*,
                           const float*, const float*, const float*, const float*, int, float*, int, float*, float*,
                           float*, float*, int, int, int, int, const float*, int, int, int, const SlabJob&, hipStream_t);
@@ -115,8 +123,27 @@ void strides3(const Tensor& t, int B, long long& bs, int& rs) {
               "attention operands need 16-byte aligned rows");
 }
 
+// device dropout seed: a 1-element int64 GPU tensor (drawn per forward call, see common.h DropCfg)
+const int64_t* seed_ptr(const OptT& seed, double p) {
+  if (!(p > 0)) return nullptr;
+  TORCH_CHECK(seed.has_value(), "dropout > 0 needs a device seed tensor");
+  TORCH_CHECK(seed->is_cuda() && seed->scalar_type() == torch::kInt64 && seed->numel() >= 1,
+              "dropout seed must be an int64 GPU tensor");
+  return seed->data_ptr<int64_t>();
+}
+
+pio::DropCfg make_drop(const OptT& seed, int64_t site, double p) {
+  TORCH_CHECK(p >= 0 && p < 1, "dropout probability must be in [0, 1)");
+  pio::DropCfg d{};
+  d.seed = seed_ptr(seed, p);
+  d.site = (uint32_t)site;
+  d.thresh = p > 0 ? (uint32_t)std::min(4294967295.0, p * 4294967296.0) : 0u;
+  d.scale = p > 0 ? (float)(1.0 / (1.0 - p)) : 1.f;
+  return d;
+}
+
 pio::AttnArgs make_args(const Tensor& q, const Tensor& k, const Tensor& v, const OptT& kmask, int H, int D,
-                        double scale, double dropout_p, int64_t seed) {
+                        double scale, double dropout_p, const OptT& seed, int64_t site) {
   CHECK_CUDA(q); CHECK_CUDA(k); CHECK_CUDA(v);
   pio::AttnArgs a{};
   a.B = (int)std::max(q.size(0), k.size(0));
@@ -141,16 +168,18 @@ pio::AttnArgs make_args(const Tensor& q, const Tensor& k, const Tensor& v, const
   }
   a.scale = (float)scale;
   a.scale_log2 = (float)(scale * 1.4426950408889634);
-  a.drop_thresh = dropout_p > 0 ? (uint32_t)std::min(4294967295.0, dropout_p * 4294967296.0) : 0u;
-  a.drop_scale = dropout_p > 0 ? (float)(1.0 / (1.0 - dropout_p)) : 1.f;
-  a.seed = (uint32_t)seed;
+  const pio::DropCfg d = make_drop(seed, site, dropout_p);
+  a.drop_thresh = d.thresh;
+  a.drop_scale = d.scale;
+  a.seedp = d.seed;
+  a.site = d.site;
   return a;
 }
 }  // namespace
 
 std::vector<Tensor> attn_fwd(Tensor q, Tensor k, Tensor v, OptT kmask, int64_t H, int64_t D, double scale,
-                             double dropout_p, int64_t seed, int64_t nsplit) {
-  auto a = make_args(q, k, v, kmask, (int)H, (int)D, scale, dropout_p, seed);
+                             double dropout_p, OptT seed, int64_t nsplit, int64_t site) {
+  auto a = make_args(q, k, v, kmask, (int)H, (int)D, scale, dropout_p, seed, site);
   auto opts = q.options();
   Tensor O = torch::empty({a.B, a.Nq, H * D}, opts.dtype(torch::kBFloat16));
   Tensor L = torch::empty({a.B, a.Nq, H}, opts.dtype(torch::kFloat32));
@@ -171,9 +200,9 @@ std::vector<Tensor> attn_fwd(Tensor q, Tensor k, Tensor v, OptT kmask, int64_t H
 // (the launcher clears it itself when several key blocks accumulate into it).  delta_in ((B, Nq, H) fp32 rowsum(dO∘O), e.g. from post_attn_bwd)
 // skips the delta pass.
 std::vector<Tensor> attn_bwd(Tensor q, Tensor k, Tensor v, OptT kmask, Tensor o, Tensor dO, Tensor lse, OptT delta_in,
-                             int64_t H, int64_t D, double scale, double dropout_p, int64_t seed, OptT dq_out,
-                             OptT dk_out, OptT dv_out, bool kv_accumulate) {
-  auto a = make_args(q, k, v, kmask, (int)H, (int)D, scale, dropout_p, seed);
+                             int64_t H, int64_t D, double scale, double dropout_p, OptT seed, OptT dq_out,
+                             OptT dk_out, OptT dv_out, bool kv_accumulate, int64_t site) {
+  auto a = make_args(q, k, v, kmask, (int)H, (int)D, scale, dropout_p, seed, site);
   TORCH_CHECK(dO.is_contiguous() && o.is_contiguous(), "O / dO must be contiguous (B, Nq, H*D)");
   auto f32 = q.options().dtype(torch::kFloat32);
   Tensor dq = dq_out.has_value() ? *dq_out : torch::empty({a.B, a.Nq, H * D}, f32);
@@ -246,7 +275,7 @@ std::vector<Tensor> ln_linear_fwd(Tensor x, OptT lnw, OptT lnb, double eps, Tens
 }
 
 std::vector<Tensor> post_attn_fwd(Tensor o, Tensor x, Tensor wo, Tensor bo, Tensor g2, Tensor be2, double eps,
-                                  Tensor w1, Tensor b1, Tensor w2, Tensor b2) {
+                                  Tensor w1, Tensor b1, Tensor w2, Tensor b2, OptT seed, int64_t site, double p) {
   TORCH_CHECK(o.is_contiguous() && x.is_contiguous(), "o/x must be contiguous (R, C)");
   const int R = (int)o.size(0), C = (int)o.size(1), Rx = (int)x.size(0);
   TORCH_CHECK(x.size(1) == C && Rx > 0 && R % Rx == 0, "x must be (R / k, C): row r adds x[r % rows(x)]");
@@ -257,7 +286,7 @@ std::vector<Tensor> post_attn_fwd(Tensor o, Tensor x, Tensor wo, Tensor bo, Tens
   Tensor u = torch::empty({R, C}, x.options().dtype(torch::kBFloat16));
   pio::post_attn_fwd_launch(C, bfp(o), f32p(x), bfp(wo), f32p(bo), f32p(g2), f32p(be2), (float)eps, bfp(w1), f32p(b1),
                             bfp(w2), f32p(b2), z.data_ptr<float>(), y.data_ptr<float>(), m.data_ptr<float>(),
-                            r.data_ptr<float>(), bfp_mut(u), R, Rx, stream());
+                            r.data_ptr<float>(), bfp_mut(u), R, Rx, make_drop(seed, site, p), stream());
   return {z, y, m, r, u};
 }
 
@@ -265,7 +294,7 @@ std::vector<Tensor> post_attn_fwd(Tensor o, Tensor x, Tensor wo, Tensor bo, Tens
 // projection of layer l+1 from the same tile.  Returns (z, y, mean2, rstd2, u, qkv, mean1, rstd1).
 std::vector<Tensor> post_attn_ln_linear_fwd(Tensor o, Tensor x, Tensor wo, Tensor bo, Tensor g2, Tensor be2, double eps,
                                             Tensor w1, Tensor b1, Tensor w2, Tensor b2, Tensor lnw, Tensor lnb,
-                                            Tensor wq, Tensor bq) {
+                                            Tensor wq, Tensor bq, OptT seed, int64_t site, double p) {
   TORCH_CHECK(o.is_contiguous() && x.is_contiguous(), "o/x must be contiguous (R, C)");
   const int R = (int)o.size(0), C = (int)o.size(1);
   TORCH_CHECK(x.size(0) == R && x.size(1) == C, "x must be (R, C)");
@@ -282,7 +311,7 @@ std::vector<Tensor> post_attn_ln_linear_fwd(Tensor o, Tensor x, Tensor wo, Tenso
                                       f32p(b1), bfp(w2), f32p(b2), z.data_ptr<float>(), y.data_ptr<float>(),
                                       m.data_ptr<float>(), r.data_ptr<float>(), bfp_mut(u), R, f32p(lnw), f32p(lnb),
                                       bfp(wq), f32p(bq), bfp_mut(qkv), m1.data_ptr<float>(), r1.data_ptr<float>(),
-                                      stream());
+                                      make_drop(seed, site, p), stream());
   return {z, y, m, r, u, qkv, m1, r1};
 }
 
@@ -351,7 +380,8 @@ pio::SlabJob make_job(const OptT& slab, std::vector<Tensor>& dsts, const std::ve
 // slab: targets are (ceil(R/64), ·) views of one slab (see vec_target), reduced by slab_reduce
 std::vector<Tensor> post_attn_bwd(Tensor dz, Tensor y, Tensor m2, Tensor r2, Tensor u, Tensor o, Tensor wo, Tensor w1,
                                   Tensor w2, Tensor g2, Tensor be2, int64_t H, std::vector<Tensor> grads, bool slab,
-                                  OptT job_slab, std::vector<Tensor> job_dsts, std::vector<int64_t> job_offs) {
+                                  OptT job_slab, std::vector<Tensor> job_dsts, std::vector<int64_t> job_offs,
+                                  OptT seed, int64_t site, double p) {
   TORCH_CHECK(dz.is_contiguous() && y.is_contiguous() && u.is_contiguous() && o.is_contiguous(),
               "post_attn_bwd operands must be contiguous (R, C)");
   const int R = (int)dz.size(0), C = (int)dz.size(1);
@@ -373,7 +403,7 @@ std::vector<Tensor> post_attn_bwd(Tensor dz, Tensor y, Tensor m2, Tensor r2, Ten
   Tensor delta = torch::empty({R, H}, f32);
   pio::post_attn_bwd_launch(C, f32p(dz), f32p(y), f32p(m2), f32p(r2), bfp(u), bfp(o), bfp(wo), bfp(w1), bfp(w2),
                             f32p(g2), f32p(be2), dy.data_ptr<float>(), bfp_mut(dO), delta.data_ptr<float>(), (int)H,
-                            pg, R, make_job(job_slab, job_dsts, job_offs), stream());
+                            pg, R, make_job(job_slab, job_dsts, job_offs), make_drop(seed, site, p), stream());
   return {dy, dO, delta};
 }
 
@@ -386,7 +416,8 @@ std::vector<Tensor> ln_linear_post_attn_bwd(Tensor g, Tensor wq, Tensor x, Tenso
                                             Tensor lnb, Tensor dres, std::vector<Tensor> ll_grads, Tensor y, Tensor m2,
                                             Tensor r2, Tensor u, Tensor o, Tensor wo, Tensor w1, Tensor w2, Tensor g2,
                                             Tensor be2, int64_t H, std::vector<Tensor> pa_grads, OptT job_slab,
-                                            std::vector<Tensor> job_dsts, std::vector<int64_t> job_offs) {
+                                            std::vector<Tensor> job_dsts, std::vector<int64_t> job_offs, OptT seed,
+                                            int64_t site, double p) {
   TORCH_CHECK(y.is_contiguous() && u.is_contiguous() && o.is_contiguous() && x.is_contiguous() && dres.is_contiguous(),
               "operands must be contiguous (R, C)");
   const int R = (int)y.size(0), C = (int)y.size(1);
@@ -416,7 +447,7 @@ std::vector<Tensor> ln_linear_post_attn_bwd(Tensor g, Tensor wq, Tensor x, Tenso
                                       f32p(dres), dg1, db1, dwq, dbq, f32p(y), f32p(m2), f32p(r2), bfp(u), bfp(o),
                                       bfp(wo), bfp(w1), bfp(w2), f32p(g2), f32p(be2), dy.data_ptr<float>(),
                                       bfp_mut(dO), delta.data_ptr<float>(), (int)H, pg, R,
-                                      make_job(job_slab, job_dsts, job_offs), stream());
+                                      make_job(job_slab, job_dsts, job_offs), make_drop(seed, site, p), stream());
   return {dy, dO, delta};
 }
 
@@ -683,25 +714,34 @@ std::vector<Tensor> pe_proj_bwd(Tensor dy, Tensor pix, Tensor mean, Tensor rstd,
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "Perceiver IO CDNA4 (gfx950) kernels";
-  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("kmask"), py::arg("H"), py::arg("D"),
+        py::arg("scale"), py::arg("dropout_p"), py::arg("seed"), py::arg("nsplit"), py::arg("site") = 0);
   m.def("attn_bwd", &attn_bwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("kmask"), py::arg("o"), py::arg("dO"),
         py::arg("lse"), py::arg("delta_in"), py::arg("H"), py::arg("D"), py::arg("scale"), py::arg("dropout_p"),
-        py::arg("seed"), py::arg("dq_out"), py::arg("dk_out"), py::arg("dv_out"), py::arg("kv_accumulate") = false);
+        py::arg("seed"), py::arg("dq_out"), py::arg("dk_out"), py::arg("dv_out"), py::arg("kv_accumulate") = false,
+        py::arg("site") = 0);
   m.def("ln_linear_fwd", &ln_linear_fwd, py::arg("x"), py::arg("lnw"), py::arg("lnb"), py::arg("eps"), py::arg("w"),
         py::arg("bias"), py::arg("act"), py::arg("res"), py::arg("out_bf16"), py::arg("save_stats"),
         py::arg("pe") = py::none(), py::arg("kin") = -1);
-  m.def("post_attn_fwd", &post_attn_fwd);
-  m.def("post_attn_ln_linear_fwd", &post_attn_ln_linear_fwd);
+  m.def("post_attn_fwd", &post_attn_fwd, py::arg("o"), py::arg("x"), py::arg("wo"), py::arg("bo"), py::arg("g2"),
+        py::arg("be2"), py::arg("eps"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("b2"),
+        py::arg("seed") = py::none(), py::arg("site") = 0, py::arg("p") = 0.0);
+  m.def("post_attn_ln_linear_fwd", &post_attn_ln_linear_fwd, py::arg("o"), py::arg("x"), py::arg("wo"), py::arg("bo"),
+        py::arg("g2"), py::arg("be2"), py::arg("eps"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("b2"),
+        py::arg("lnw"), py::arg("lnb"), py::arg("wq"), py::arg("bq"), py::arg("seed") = py::none(),
+        py::arg("site") = 0, py::arg("p") = 0.0);
   m.def("ln_linear_post_attn_bwd", &ln_linear_post_attn_bwd, py::arg("g"), py::arg("wq"), py::arg("x"),
         py::arg("mean1"), py::arg("rstd1"), py::arg("lnw"), py::arg("lnb"), py::arg("dres"), py::arg("ll_grads"),
         py::arg("y"), py::arg("m2"), py::arg("r2"), py::arg("u"), py::arg("o"), py::arg("wo"), py::arg("w1"),
         py::arg("w2"), py::arg("g2"), py::arg("be2"), py::arg("H"), py::arg("pa_grads"),
         py::arg("job_slab") = py::none(), py::arg("job_dsts") = std::vector<Tensor>(),
-        py::arg("job_offs") = std::vector<int64_t>());
+        py::arg("job_offs") = std::vector<int64_t>(), py::arg("seed") = py::none(), py::arg("site") = 0,
+        py::arg("p") = 0.0);
   m.def("post_attn_bwd", &post_attn_bwd, py::arg("dz"), py::arg("y"), py::arg("m2"), py::arg("r2"), py::arg("u"),
         py::arg("o"), py::arg("wo"), py::arg("w1"), py::arg("w2"), py::arg("g2"), py::arg("be2"), py::arg("H"),
         py::arg("grads"), py::arg("slab") = false, py::arg("job_slab") = py::none(),
-        py::arg("job_dsts") = std::vector<Tensor>(), py::arg("job_offs") = std::vector<int64_t>());
+        py::arg("job_dsts") = std::vector<Tensor>(), py::arg("job_offs") = std::vector<int64_t>(),
+        py::arg("seed") = py::none(), py::arg("site") = 0, py::arg("p") = 0.0);
   m.def("ln_linear_bwd", &ln_linear_bwd, py::arg("g"), py::arg("w"), py::arg("x"), py::arg("mean"), py::arg("rstd"),
         py::arg("lnw"), py::arg("lnb"), py::arg("dres"), py::arg("need_dx"), py::arg("dlnw"), py::arg("dlnb"),
         py::arg("dW"), py::arg("db"), py::arg("pe") = py::none(), py::arg("kin") = -1, py::arg("slab") = false,

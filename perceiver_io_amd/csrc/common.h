@@ -249,4 +249,34 @@ __device__ __forceinline__ bool keep_elem(uint32_t seed, uint32_t stream, uint32
   return hash3(seed, stream, idx) >= thresh;
 }
 
+// Dropout configuration of one fused call.  The 64-bit seed lives in DEVICE memory: it is
+// drawn per forward call by torch's graph-safe generator (a 1-element randint on the step's
+// stream), so a replayed hipGraph reads a fresh seed every step instead of a value frozen at
+// capture time, and the backward regenerates the forward's masks from the same tensor.
+// ``site`` separates the masks of one call: sub-stream 0 = residual after attention,
+// 1 = residual after the MLP, 2 = attention probabilities (reference model.py:47-56, 66-71).
+struct DropCfg {
+  const int64_t* seed;  // nullptr or thresh == 0: dropout off
+  uint32_t site;
+  uint32_t thresh;      // p · 2^32
+  float scale;          // 1 / (1 - p)
+};
+__device__ __forceinline__ uint32_t drop_key(const int64_t* seed, uint32_t site, uint32_t sub) {
+  const uint64_t s = (uint64_t)*seed;
+  return hash3((uint32_t)s, (uint32_t)(s >> 32), site * 4u + sub);
+}
+// this thread's row-pass elements (row gr, columns rp_col(j) + e of a C-wide row) × mask·scale
+template <int NCH>
+__device__ __forceinline__ void drop_rows(float (&v)[NCH][8], const DropCfg& d, uint32_t sub, int gr, int C) {
+  if (d.thresh == 0u) return;
+  const uint32_t key = drop_key(d.seed, d.site, sub);
+#pragma unroll
+  for (int j = 0; j < NCH; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const uint32_t idx = (uint32_t)gr * (uint32_t)C + (uint32_t)(8 * ((threadIdx.x & 3) + 4 * j) + e);
+      v[j][e] = keep_elem(key, 0u, idx, d.thresh) ? v[j][e] * d.scale : 0.f;
+    }
+}
+
 }  // namespace pio

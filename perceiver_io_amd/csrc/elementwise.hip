@@ -212,9 +212,11 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
                              const float* __restrict__ hyper, float eps, float wd, float clip, float gscale) {
   const float lr = hyper[0], step = hyper[1], beta1 = hyper[3], beta2 = hyper[4];
   const float bc1 = 1.f - powf(beta1, step), bc2 = 1.f - powf(beta2, step);
+  // g holds the all-reduced SUM over ranks (gscale = 1 / world makes it the mean): the clip
+  // threshold applies to the norm of the MEAN gradient, as in single-process training
   float gs = gscale;
   if (clip > 0.f) {
-    const float norm = sqrtf(hyper[2]);
+    const float norm = sqrtf(hyper[2]) * gscale;
     const float f = clip / (norm + 1e-6f);
     if (f < 1.f) gs *= f;
   }

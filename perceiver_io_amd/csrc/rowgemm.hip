@@ -473,8 +473,10 @@ __device__ __forceinline__ void post_attn_fwd_body(
     const float* __restrict__ bo, const float* __restrict__ g2, const float* __restrict__ be2, float eps,
     const uint16_t* __restrict__ W1, const float* __restrict__ b1, const uint16_t* __restrict__ W2,
     const float* __restrict__ b2, float* __restrict__ Z, float* __restrict__ Ysave, float* __restrict__ mean2,
-    float* __restrict__ rstd2, uint16_t* __restrict__ Usave, int R, int Rx, float (&z)[C / 32][8]) {
-  // X has Rx rows, row r of the tile adds X[r % Rx] (Rx < R: batch-broadcast residual)
+    float* __restrict__ rstd2, uint16_t* __restrict__ Usave, int R, int Rx, const DropCfg& dr, float (&z)[C / 32][8]) {
+  // X has Rx rows, row r of the tile adds X[r % Rx] (Rx < R: batch-broadcast residual).
+  // Residual dropout (dr.thresh > 0): Y = X + drop₀(attn-out), Z = Y + drop₁(MLP(Y)), masks
+  // hashed from (device seed, site, row·C + col) and regenerated by the backward.
   constexpr int LD = C + 8, LDF = C + 4, MAXT = (2 * C / 32 + 3) / 4, NCH = C / 32;
   constexpr int NWB = C <= 64 ? 3 : 1, NIW = (C * C / 8 + 255) / 256;
   __shared__ __attribute__((aligned(16))) uint16_t sA[64 * LD];   // O → LN2(Y) → GELU(U)
@@ -514,6 +516,7 @@ __device__ __forceinline__ void post_attn_fwd_body(
   {
     float t[NCH][8];
     lds_row_read<NCH>(t, sF, LDF);
+    drop_rows<NCH>(t, dr, 0u, gr, C);
     float s = 0.f;
 #pragma unroll
     for (int j = 0; j < NCH; ++j)
@@ -562,6 +565,7 @@ __device__ __forceinline__ void post_attn_fwd_body(
   for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) { sF[m * LDF + n] = acc[t][i] + sP[2][n]; });
   __syncthreads();
   lds_row_read<NCH>(z, sF, LDF);
+  drop_rows<NCH>(z, dr, 1u, gr, C);
 #pragma unroll
   for (int j = 0; j < NCH; ++j)
 #pragma unroll
@@ -575,9 +579,9 @@ __global__ __launch_bounds__(256) void post_attn_fwd_kernel(
     const float* __restrict__ bo, const float* __restrict__ g2, const float* __restrict__ be2, float eps,
     const uint16_t* __restrict__ W1, const float* __restrict__ b1, const uint16_t* __restrict__ W2,
     const float* __restrict__ b2, float* __restrict__ Z, float* __restrict__ Ysave, float* __restrict__ mean2,
-    float* __restrict__ rstd2, uint16_t* __restrict__ Usave, int R, int Rx) {
+    float* __restrict__ rstd2, uint16_t* __restrict__ Usave, int R, int Rx, DropCfg dr) {
   float z[C / 32][8];
-  post_attn_fwd_body<C>(O, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, Rx, z);
+  post_attn_fwd_body<C>(O, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, Rx, dr, z);
 }
 
 // ------------------------------------------------------------------------------------
@@ -595,7 +599,7 @@ __global__ __launch_bounds__(256) void post_attn_ln_linear_fwd_kernel(
     const float* __restrict__ b2, float* __restrict__ Z, float* __restrict__ Ysave, float* __restrict__ mean2,
     float* __restrict__ rstd2, uint16_t* __restrict__ Usave, int R, const float* __restrict__ lnw,
     const float* __restrict__ lnb, const uint16_t* __restrict__ Wq, const float* __restrict__ bq,
-    uint16_t* __restrict__ QKV, float* __restrict__ mean1, float* __restrict__ rstd1) {
+    uint16_t* __restrict__ QKV, float* __restrict__ mean1, float* __restrict__ rstd1, DropCfg dr) {
   constexpr int NCH = C / 32, KP = 32 * NCH;
   __shared__ __attribute__((aligned(16))) uint16_t smem[ln_linear_fwd_smem<NCH>() / 2];  // LN1+QKV half
   bf16x8 wb[NCH];
@@ -604,7 +608,7 @@ __global__ __launch_bounds__(256) void post_attn_ln_linear_fwd_kernel(
   row_load<NCH>(gw, lnw, 0, 0, 1, C, aligned16(lnw) && aligned16(lnb));
   row_load<NCH>(gb, lnb, 0, 0, 1, C, aligned16(lnw) && aligned16(lnb));
   float z[NCH][8];
-  post_attn_fwd_body<C>(O, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, R, z);
+  post_attn_fwd_body<C>(O, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, R, dr, z);
   ln_linear_fwd_tile<uint16_t, NCH>(z, wb, gw, gb, true, blockIdx.x * 64, R, C, eps, Wq, C, bq, 3 * C, 0, nullptr, 0,
                                     QKV, 3 * C, mean1, rstd1, smem);
 }
@@ -707,7 +711,9 @@ __device__ __forceinline__ void post_attn_bwd_body(
     const float* __restrict__ rstd2, const uint16_t* __restrict__ U, const uint16_t* __restrict__ O,
     const uint16_t* __restrict__ Wo, const uint16_t* __restrict__ W1, const uint16_t* __restrict__ W2,
     const float* __restrict__ g2, const float* __restrict__ be2, float* __restrict__ dY, uint16_t* __restrict__ dO,
-    float* __restrict__ delta, int H, PostAttnGrads gr_out, int R, unsigned char* smem) {
+    float* __restrict__ delta, int H, PostAttnGrads gr_out, int R, const DropCfg& dr, unsigned char* smem) {
+  // residual dropout: the MLP output layer sees dZ∘m₁, the out-projection dY∘m₀; the residual
+  // gradients (dZ into dY, dY out of the kernel) stay unmasked
   constexpr int LD = C + 8, LDF = C + 4, MAXT = (2 * C / 32 + 3) / 4, MAXW = ((C / 32) * (C / 32) + 3) / 4;
   constexpr int NCH = C / 32, NWB = C <= 64 ? 3 : 1, NIW = (C * C / 8 + 255) / 256;
   uint16_t* sG = reinterpret_cast<uint16_t*>(smem);  // [64][LD] dZ → dU → dY
@@ -739,7 +745,13 @@ __device__ __forceinline__ void post_attn_bwd_body(
     tile_fetch<NIW>(wr[2], Wo, C, 0, C, C, C, C, av);
   }
   for (int k = threadIdx.x; k < C; k += blockDim.x) { sP[0][k] = g2[k]; sP[1][k] = be2[k]; }
-  lds_row_write_bf16<NCH>(sG, LD, dz);
+  float dzm[NCH][8];  // dZ∘m₁: the MLP output layer's gradient
+#pragma unroll
+  for (int j = 0; j < NCH; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dzm[j][e] = dz[j][e];
+  drop_rows<NCH>(dzm, dr, 1u, gr, C);
+  lds_row_write_bf16<NCH>(sG, LD, dzm);
   {
     float gp[NCH][8];
 #pragma unroll
@@ -751,7 +763,7 @@ __device__ __forceinline__ void post_attn_bwd_body(
   }
 #pragma unroll
   for (int b = 0; b < NWB; ++b) tile_store<NIW>(wr[b], sW[b], LD, C, C);
-  colsum_partial<NCH>(dz, sPart[0], C);
+  colsum_partial<NCH>(dzm, sPart[0], C);
   __syncthreads();
   if constexpr (NWB == 1) tile_fetch<NIW>(wr[0], W1, C, 0, C, C, C, C, av);
 
@@ -838,8 +850,9 @@ __device__ __forceinline__ void post_attn_bwd_body(
       }
     colsum_partial<NCH>(yv, sPart[1], C);
     colsum_partial<NCH>(dxn, sPart[2], C);
-    colsum_partial<NCH>(dz, sPart[3], C);
     row_store<NCH>(dz, dY, C, gr, R, C, av);
+    drop_rows<NCH>(dz, dr, 0u, gr, C);  // dY∘m₀: the out-projection's gradient
+    colsum_partial<NCH>(dz, sPart[3], C);
     lds_row_write_bf16<NCH>(sG, LD, dz);
 #pragma unroll
     for (int j = 0; j < NCH; ++j) *reinterpret_cast<bf16x8*>(sX + rp_row() * LD + rp_col(j)) = ob[j];
@@ -888,7 +901,7 @@ __global__ __launch_bounds__(256) void post_attn_bwd_kernel(
     const float* __restrict__ rstd2, const uint16_t* __restrict__ U, const uint16_t* __restrict__ O,
     const uint16_t* __restrict__ Wo, const uint16_t* __restrict__ W1, const uint16_t* __restrict__ W2,
     const float* __restrict__ g2, const float* __restrict__ be2, float* __restrict__ dY, uint16_t* __restrict__ dO,
-    float* __restrict__ delta, int H, PostAttnGrads gr_out, int R, SlabJob job) {
+    float* __restrict__ delta, int H, PostAttnGrads gr_out, int R, SlabJob job, DropCfg dr) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[post_attn_bwd_smem<C>()];
   if ((int)blockIdx.x >= (R + 63) / 64) {  // appended workgroups: the previous kernel's slab job
     slab_reduce_block(job, blockIdx.x - (R + 63) / 64, reinterpret_cast<float4*>(smem));
@@ -896,7 +909,7 @@ __global__ __launch_bounds__(256) void post_attn_bwd_kernel(
   }
   float dz[C / 32][8];
   row_load<C / 32>(dz, dZ, C, blockIdx.x * 64 + rp_row(), R, C, aligned16(dZ));
-  post_attn_bwd_body<C>(dz, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO, delta, H, gr_out, R, smem);
+  post_attn_bwd_body<C>(dz, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO, delta, H, gr_out, R, dr, smem);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1089,7 +1102,7 @@ __global__ __launch_bounds__(256) void ln_linear_post_attn_bwd_kernel(
     const float* __restrict__ rstd2, const uint16_t* __restrict__ U, const uint16_t* __restrict__ O,
     const uint16_t* __restrict__ Wo, const uint16_t* __restrict__ W1, const uint16_t* __restrict__ W2,
     const float* __restrict__ g2, const float* __restrict__ be2, float* __restrict__ dY, uint16_t* __restrict__ dO,
-    float* __restrict__ delta, int H, PostAttnGrads gr_out, int R, SlabJob job) {
+    float* __restrict__ delta, int H, PostAttnGrads gr_out, int R, SlabJob job, DropCfg dr) {
   constexpr int NCH = C / 32;
   constexpr int SM = ln_linear_bwd_smem<NCH>() > post_attn_bwd_smem<C>() ? ln_linear_bwd_smem<NCH>()
                                                                           : post_attn_bwd_smem<C>();
@@ -1105,7 +1118,7 @@ __global__ __launch_bounds__(256) void ln_linear_post_attn_bwd_kernel(
                                         dlnw, dlnb, dWq, dbq, gr_out.vrs, gr_out.vrs, gr_out.slab, R, PeSplit{},
                                         reinterpret_cast<uint16_t*>(smem), dz);
   __syncthreads();  // the ln_linear half's LDS traffic is done before the post-attention half reuses it
-  post_attn_bwd_body<C>(dz, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO, delta, H, gr_out, R, smem);
+  post_attn_bwd_body<C>(dz, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO, delta, H, gr_out, R, dr, smem);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1259,11 +1272,11 @@ void ln_linear_fwd_launch(const void* X, bool x_bf16, int x_rs, int R, int Kin, 
 void post_attn_fwd_launch(int C, const uint16_t* O, const float* X, const uint16_t* Wo, const float* bo,
                           const float* g2, const float* be2, float eps, const uint16_t* W1, const float* b1,
                           const uint16_t* W2, const float* b2, float* Z, float* Ysave, float* mean2, float* rstd2,
-                          uint16_t* Usave, int R, int Rx, hipStream_t st) {
+                          uint16_t* Usave, int R, int Rx, const DropCfg& dr, hipStream_t st) {
   dim3 grid((R + 63) / 64);
 #define PAF(CC)                                                                                                     \
   hipLaunchKernelGGL(post_attn_fwd_kernel<CC>, grid, dim3(256), 0, st, O, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, \
-                     Z, Ysave, mean2, rstd2, Usave, R, Rx)
+                     Z, Ysave, mean2, rstd2, Usave, R, Rx, dr)
   if (C == 64) PAF(64);
   else if (C == 128) PAF(128);
   else if (C == 32) PAF(32);
@@ -1275,11 +1288,11 @@ void post_attn_ln_linear_fwd_launch(int C, const uint16_t* O, const float* X, co
                                     const uint16_t* W2, const float* b2, float* Z, float* Ysave, float* mean2,
                                     float* rstd2, uint16_t* Usave, int R, const float* lnw, const float* lnb,
                                     const uint16_t* Wq, const float* bq, uint16_t* QKV, float* mean1, float* rstd1,
-                                    hipStream_t st) {
+                                    const DropCfg& dr, hipStream_t st) {
   dim3 grid((R + 63) / 64);
 #define PLF(CC)                                                                                                  \
   hipLaunchKernelGGL(post_attn_ln_linear_fwd_kernel<CC>, grid, dim3(256), 0, st, O, X, Wo, bo, g2, be2, eps, W1, b1, \
-                     W2, b2, Z, Ysave, mean2, rstd2, Usave, R, lnw, lnb, Wq, bq, QKV, mean1, rstd1)
+                     W2, b2, Z, Ysave, mean2, rstd2, Usave, R, lnw, lnb, Wq, bq, QKV, mean1, rstd1, dr)
   if (C == 64) PLF(64);
   else if (C == 128) PLF(128);
   else if (C == 32) PLF(32);
@@ -1289,11 +1302,12 @@ void post_attn_ln_linear_fwd_launch(int C, const uint16_t* O, const float* X, co
 void post_attn_bwd_launch(int C, const float* dZ, const float* Ysave, const float* mean2, const float* rstd2,
                           const uint16_t* U, const uint16_t* O, const uint16_t* Wo, const uint16_t* W1,
                           const uint16_t* W2, const float* g2, const float* be2, float* dY, uint16_t* dO,
-                          float* delta, int H, const PostAttnGrads& grads, int R, const SlabJob& job, hipStream_t st) {
+                          float* delta, int H, const PostAttnGrads& grads, int R, const SlabJob& job, const DropCfg& dr,
+                          hipStream_t st) {
   dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0));
 #define PAB(CC)                                                                                                  \
   hipLaunchKernelGGL(post_attn_bwd_kernel<CC>, grid, dim3(256), 0, st, dZ, Ysave, mean2, rstd2, U, O, Wo, W1, W2, \
-                     g2, be2, dY, dO, delta, H, grads, R, job)
+                     g2, be2, dY, dO, delta, H, grads, R, job, dr)
   if (C == 64) PAB(64);
   else if (C == 128) PAB(128);
   else if (C == 32) PAB(32);
@@ -1306,12 +1320,13 @@ void ln_linear_post_attn_bwd_launch(int C, const float* G, const uint16_t* Wq, c
                                     const float* mean2, const float* rstd2, const uint16_t* U, const uint16_t* O,
                                     const uint16_t* Wo, const uint16_t* W1, const uint16_t* W2, const float* g2,
                                     const float* be2, float* dY, uint16_t* dO, float* delta, int H,
-                                    const PostAttnGrads& grads, int R, const SlabJob& job, hipStream_t st) {
+                                    const PostAttnGrads& grads, int R, const SlabJob& job, const DropCfg& dr,
+                                    hipStream_t st) {
   dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0));
 #define LPB(CC)                                                                                                   \
   hipLaunchKernelGGL(ln_linear_post_attn_bwd_kernel<CC>, grid, dim3(256), 0, st, G, Wq, X, mean1, rstd1, lnw, lnb, \
                      dres, dlnw, dlnb, dWq, dbq, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO, delta, H,  \
-                     grads, R, job)
+                     grads, R, job, dr)
   if (C == 64) LPB(64);
   else if (C == 32) LPB(32);
 #undef LPB

@@ -31,6 +31,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
+from ..parallel.reducer import bucket_ready_point
 from ..utils.tokenizer import MASK_TOKEN, SPECIAL_TOKENS, UNK_TOKEN
 from .adapters import InputAdapter, OutputAdapter
 from .blocks import Sequential, cross_attention_layer, init_latent_, self_attention_block
@@ -106,6 +107,7 @@ class PerceiverDecoder(nn.Module):
     def hidden(self, x, num_queries: Optional[int] = None):
         """Decoder output before the adapter, ``(B, K, C_out)``; optionally only the
         first ``num_queries`` queries (queries are independent of each other)."""
+        x = bucket_ready_point(x)  # DDP: decoder grads final here → early bucket (parallel/reducer.py)
         self.check_latent(x)
         q = self.output if num_queries is None else self.output[:num_queries]
         return self.cross_attention(q.unsqueeze(0).expand(x.shape[0], -1, -1), x)
@@ -200,4 +202,4 @@ class PerceiverMLM(nn.Module):
             # reference compute: all K queries decoded, full (B, V, L) logits, CE with ignore_index
             logits = self.decoder(x_latent)[:, :l, :]
             return torch.nn.functional.cross_entropy(logits.transpose(1, 2), labels, ignore_index=-100)
-        return ops.mlm_head.masked_decode_loss(self.decoder, x_latent, labels)
+        return ops.mlm_head.masked_decode_loss(self.decoder, x_latent, labels, p=self.masking.mask_p)

@@ -90,11 +90,14 @@ class _FlashAttention(torch.autograd.Function):
 
 
 def flash_attention(q, k, v, num_heads: int, key_padding_mask: Optional[torch.Tensor] = None,
-                    dropout_p: float = 0.0, seed: Optional[int] = None):
-    """HIP flash attention on ``(B|1, Nq, E)`` queries and ``(B, Nk, E)`` keys/values."""
+                    dropout_p: float = 0.0, seed: Optional[torch.Tensor] = None):
+    """HIP flash attention on ``(B|1, Nq, E)`` queries and ``(B, Nk, E)`` keys/values.
+
+    ``seed``: 1-element int64 device tensor for the dropout masks; drawn here on the device
+    (graph-safe: a fresh draw on every replay of a captured step) when not given."""
     ext.require()
-    if seed is None:
-        seed = int(torch.randint(0, 2**31 - 1, (1,)).item()) if dropout_p > 0 else 0
+    if seed is None and dropout_p > 0:
+        seed = torch.randint(-(2**62), 2**62, (1,), device=q.device, dtype=torch.int64)
     km = None
     if key_padding_mask is not None:
         km = key_padding_mask.to(torch.bool).contiguous()

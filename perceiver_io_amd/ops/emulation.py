@@ -19,6 +19,53 @@ def _bf(x):
     return x.to(torch.bfloat16).to(torch.float32)
 
 
+# ---- the kernels' counter-based dropout RNG (csrc/common.h hash3 / drop_key), bit-exact --------
+M32 = 0xFFFFFFFF
+
+
+def _u32(x):
+    return x & M32
+
+
+def hash3(a, b, c):
+    """uint32 murmur-style mixer over int64 tensors / ints holding uint32 values."""
+    h = _u32(_u32(a * 0x9E3779B1) ^ _u32(b + 0x7F4A7C15))
+    h = h ^ _u32(c * 0x85EBCA77)
+    h = _u32((h ^ (h >> 15)) * 0x2C1B3C6D)
+    h = _u32((h ^ (h >> 12)) * 0x297A2D39)
+    return h ^ (h >> 15)
+
+
+def drop_key(seed, site: int, sub: int) -> int:
+    s = int(seed.reshape(-1)[0].item()) & 0xFFFFFFFFFFFFFFFF
+    return int(hash3(torch.tensor(s & M32), torch.tensor(s >> 32), torch.tensor(_u32(site * 4 + sub))).item())
+
+
+def drop_thresh(p: float) -> int:
+    return min(M32, int(p * 4294967296.0)) if p > 0 else 0
+
+
+def keep_mask(key: int, stream, idx, p: float):
+    """bool keep mask: hash3(key, stream, idx) >= p·2^32 (stream / idx int64 tensors)."""
+    return hash3(torch.as_tensor(key, dtype=torch.int64), stream, idx) >= drop_thresh(p)
+
+
+def row_drop_mask(seed, site: int, sub: int, R: int, C: int, p: float, device=None):
+    """(R, C) float mask·1/(1-p) of a fused post-attention kernel's residual dropout."""
+    idx = torch.arange(R * C, dtype=torch.int64, device=device).view(R, C)
+    keep = keep_mask(drop_key(seed, site, sub), torch.zeros((), dtype=torch.int64), idx, p)
+    return keep.float() / (1.0 - p)
+
+
+def attn_drop_mask(seed, site: int, B: int, H: int, Nq: int, Nk: int, p: float, device=None):
+    """(B, H, Nq, Nk) float mask·1/(1-p) of the attention kernels' probability dropout."""
+    stream = torch.arange(B * H, dtype=torch.int64, device=device).view(B, H, 1, 1)
+    idx = (torch.arange(Nq, dtype=torch.int64, device=device).view(Nq, 1) * Nk
+           + torch.arange(Nk, dtype=torch.int64, device=device).view(1, Nk))
+    keep = keep_mask(drop_key(seed, site, 2), stream, _u32(idx), p)
+    return keep.float() / (1.0 - p)
+
+
 def _ln(x, w, b, eps):
     mean = x.mean(-1)
     var = x.var(-1, unbiased=False)
@@ -100,20 +147,20 @@ def _acc(t, v):
         t += v.reshape(t.shape)
 
 
-def post_attn_ln_linear_fwd(o, x, wo, bo, g2, be2, eps, w1, b1, w2, b2, lnw, lnb, wq, bq):
+def post_attn_ln_linear_fwd(o, x, wo, bo, g2, be2, eps, w1, b1, w2, b2, lnw, lnb, wq, bq, seed=None, site=0, p=0.0):
     """post_attn_fwd of layer l, then ln_linear_fwd (LN1 + packed QKV) of layer l+1."""
-    z, y, m2, r2, u = post_attn_fwd(o, x, wo, bo, g2, be2, eps, w1, b1, w2, b2)
+    z, y, m2, r2, u = post_attn_fwd(o, x, wo, bo, g2, be2, eps, w1, b1, w2, b2, seed, site, p)
     qkv, mean1, rstd1 = ln_linear_fwd(z, lnw, lnb, eps, wq, bq, 0, None, True, True)
     return z, y, m2, r2, u, qkv, mean1, rstd1
 
 
 def ln_linear_post_attn_bwd(g, wq, x, mean1, rstd1, lnw, lnb, dres, ll_grads, y, m2, r2, u, o, wo, w1, w2, g2, be2,
-                            H, pa_grads, job_slab=None, job_dsts=(), job_offs=()):
+                            H, pa_grads, job_slab=None, job_dsts=(), job_offs=(), seed=None, site=0, p=0.0):
     """ln_linear_bwd of layer l+1 (dX = dZ of layer l, incl. dres) → post_attn_bwd of layer l,
     both into slab targets."""
     _run_job(job_slab, job_dsts, job_offs)
     dz = ln_linear_bwd(g, wq, x, mean1, rstd1, lnw, lnb, dres, True, *ll_grads, slab=True)
-    return post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, be2, H, pa_grads, slab=True)
+    return post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, be2, H, pa_grads, slab=True, seed=seed, site=site, p=p)
 
 
 def _heads(x, H):
@@ -136,14 +183,14 @@ def _scores(qf, kf, kmask, scale):
     return s
 
 
-def attn_fwd(q, k, v, kmask, H, D, scale, dropout_p, seed, nsplit):
-    if dropout_p > 0:
-        raise NotImplementedError("emulation: attention dropout uses the kernel's hash RNG (GPU only)")
+def attn_fwd(q, k, v, kmask, H, D, scale, dropout_p, seed, nsplit, site=0):
     B, qf, kf, vf = _qkv(q, k, v, H, D)
     s = _scores(qf, kf, kmask, scale)
     lse = torch.logsumexp(s, -1)  # (B, H, Nq), -inf for dead rows
     p = torch.exp(s - lse[..., None])
     p = torch.nan_to_num(p, nan=0.0)
+    if dropout_p > 0:
+        p = p * attn_drop_mask(seed, site, B, H, q.shape[1], k.shape[1], dropout_p, q.device)
     o = torch.matmul(_bf(p), vf)
     lse2 = torch.where(torch.isfinite(lse), lse * LOG2E, torch.full_like(lse, float("inf")))
     o = o.permute(0, 2, 1, 3).reshape(B, q.shape[1], H * D).to(torch.bfloat16)
@@ -151,7 +198,7 @@ def attn_fwd(q, k, v, kmask, H, D, scale, dropout_p, seed, nsplit):
 
 
 def attn_bwd(q, k, v, kmask, o, dO, lse, delta_in, H, D, scale, dropout_p, seed, dq_out, dk_out, dv_out,
-             kv_accumulate=False):
+             kv_accumulate=False, site=0):
     B, qf, kf, vf = _qkv(q, k, v, H, D)
     s = _scores(qf, kf, kmask, scale)
     l2 = lse.permute(0, 2, 1)  # (B, H, Nq)
@@ -161,10 +208,16 @@ def attn_bwd(q, k, v, kmask, o, dO, lse, delta_in, H, D, scale, dropout_p, seed,
     of = o.float().reshape(B, -1, H, D).permute(0, 2, 1, 3)
     delta = (dof * of).sum(-1, keepdim=True)
     dp = torch.matmul(dof, vf.transpose(-1, -2))
-    ds = p * (dp - delta)
+    if dropout_p > 0:
+        m = attn_drop_mask(seed, site, B, H, q.shape[1], k.shape[1], dropout_p, q.device)
+        ds = p * (dp * m - delta)
+        pd = p * m
+    else:
+        ds = p * (dp - delta)
+        pd = p
     dq = torch.matmul(ds, kf) * scale
     dk = torch.matmul(ds.transpose(-1, -2), qf) * scale
-    dv = torch.matmul(p.transpose(-1, -2), dof)
+    dv = torch.matmul(pd.transpose(-1, -2), dof)
 
     def merge(t):
         return t.permute(0, 2, 1, 3).reshape(B, t.shape[2], H * D)
@@ -182,15 +235,23 @@ def attn_bwd(q, k, v, kmask, o, dO, lse, delta_in, H, D, scale, dropout_p, seed,
     return res
 
 
-def post_attn_fwd(o, x, wo, bo, g2, be2, eps, w1, b1, w2, b2):
-    """x may have R / k rows (batch-broadcast residual): row r adds x[r % rows(x)]."""
+def post_attn_fwd(o, x, wo, bo, g2, be2, eps, w1, b1, w2, b2, seed=None, site=0, p=0.0):
+    """x may have R / k rows (batch-broadcast residual): row r adds x[r % rows(x)].
+    p > 0: residual dropout with the kernels' hashed masks (sub-streams 0 / 1)."""
     if x.shape[0] != o.shape[0]:
         x = x.repeat(o.shape[0] // x.shape[0], 1)
-    y = x + _bf(o.float()) @ _bf(wo.float()).t() + bo
+    R, C = o.shape
+    a = _bf(o.float()) @ _bf(wo.float()).t() + bo
+    if p > 0:
+        a = a * row_drop_mask(seed, site, 0, R, C, p, o.device)
+    y = x + a
     xn, m, r = _ln(y, g2, be2, eps)
     u = _bf(xn) @ _bf(w1.float()).t() + b1
     h = F.gelu(u)
-    z = y + _bf(h) @ _bf(w2.float()).t() + b2
+    f = _bf(h) @ _bf(w2.float()).t() + b2
+    if p > 0:
+        f = f * row_drop_mask(seed, site, 1, R, C, p, o.device)
+    z = y + f
     return z, y, m, r, u.to(torch.bfloat16)
 
 
@@ -215,23 +276,25 @@ def _run_job(job_slab, job_dsts, job_offs):
 
 
 def post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, be2, H, grads, slab=False, job_slab=None, job_dsts=(),
-                  job_offs=()):
+                  job_offs=(), seed=None, site=0, p=0.0):
     """Returns (dy, dO, delta); parameter grads are ACCUMULATED into
     grads = [dWo, dbo, dg2, dbe2, dW1, db1, dW2, db2] (or stored into slab views)."""
     _run_job(job_slab, job_dsts, job_offs)
     _SLAB[0] = slab
     try:
-        return _post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, be2, H, grads)
+        return _post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, be2, H, grads, seed, site, p)
     finally:
         _SLAB[0] = False
 
 
-def _post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, be2, H, grads):
+def _post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, be2, H, grads, seed=None, site=0, p=0.0):
     dWo, dbo, dg2, dbe2, dW1, db1, dW2, db2 = grads
+    R, C = dz.shape
     uf = u.float()
-    dh = _bf(dz) @ _bf(w2.float())
-    _acc(dW2, _bf(dz).t() @ _bf(F.gelu(uf)))
-    _acc(db2, dz.sum(0))
+    dzm = dz * row_drop_mask(seed, site, 1, R, C, p, dz.device) if p > 0 else dz
+    dh = _bf(dzm) @ _bf(w2.float())
+    _acc(dW2, _bf(dzm).t() @ _bf(F.gelu(uf)))
+    _acc(db2, dzm.sum(0))
     du = dh * _gelu_grad(uf)
     dxn = _bf(du) @ _bf(w1.float())
     xn = (y - m2[:, None]) * r2[:, None] * g2 + be2
@@ -239,10 +302,10 @@ def _post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, be2, H, grads):
     _acc(db1, du.sum(0))
     dln, xh = _ln_bwd(dxn, y, m2, r2, g2)
     dy = dz + dln
-    do = (_bf(dy) @ _bf(wo.float())).to(torch.bfloat16)
-    _acc(dWo, _bf(dy).t() @ _bf(o.float()))
-    _acc(dbo, dy.sum(0))
-    R, C = dz.shape
+    dym = dy * row_drop_mask(seed, site, 0, R, C, p, dz.device) if p > 0 else dy
+    do = (_bf(dym) @ _bf(wo.float())).to(torch.bfloat16)
+    _acc(dWo, _bf(dym).t() @ _bf(o.float()))
+    _acc(dbo, dym.sum(0))
     D = C // H
     delta = (do.float().view(R, H, D) * o.float().view(R, H, D)).sum(-1)
     _acc(dg2, (dxn * xh).sum(0))
@@ -330,7 +393,16 @@ def ce_fwd(h, labels, w, bias):
     return loss, lse
 
 
-def ce_bwd(h, labels, w, bias, lse, gscale, dH, dW, db, accumulate, rowmap=None):
+def ce_bwd(h, labels, w, bias, lse, gscale, dH, dW, db, accumulate, rowmap=None, slab=False):
+    """slab=True: dW | db are returned as a one-row (1, V·C + V₄) slab instead of being added."""
+    if slab:
+        gw, gb = torch.zeros_like(dW), torch.zeros_like(db)
+        ce_bwd(h, labels, w, bias, lse, gscale, dH, gw, gb, False, rowmap)
+        V = w.shape[0]
+        out = torch.zeros(1, dW.numel() + (V + 3) // 4 * 4, dtype=dW.dtype, device=dW.device)
+        out[0, :dW.numel()] = gw.reshape(-1)
+        out[0, dW.numel():dW.numel() + V] = gb
+        return out
     logits = _bf(h.float()) @ _bf(w.float()).t() + bias
     p = torch.exp(logits - lse[:, None])
     valid = (labels >= 0).float()[:, None]
@@ -350,6 +422,7 @@ def ce_bwd(h, labels, w, bias, lse, gscale, dH, dW, db, accumulate, rowmap=None)
     else:
         dW.copy_(gw)
         db.copy_(gb)
+    return None
 
 
 def embed_fwd(ids, E, P, scale):
@@ -383,7 +456,7 @@ def adamw(p, g, m, v, shadow, hyper, eps, wd, clip, gscale):
     lr, step, b1, b2 = float(hyper[0]), float(hyper[1]), float(hyper[3]), float(hyper[4])
     gs = gscale
     if clip > 0:
-        norm = math.sqrt(float(hyper[2]))
+        norm = math.sqrt(float(hyper[2])) * gscale  # norm of the mean (all-reduced sum × 1/world)
         f = clip / (norm + 1e-6)
         if f < 1:
             gs *= f

@@ -103,6 +103,12 @@ def _flush_pending():
                 K.slab_reduce(t, ds, os_)
 
 
+def flush_pending():
+    """Launch every deferred slab reduction now (e.g. before a gradient bucket that depends on
+    them is all-reduced mid-backward, parallel/reducer.py)."""
+    _flush_pending()
+
+
 def defer_slab(K, t: torch.Tensor, dsts, offs):
     """Queue ``dsts[j] += Σ_rows t[:, offs[j]:offs[j] + dsts[j].numel()]`` (a slab job) for the
     next backward kernel of the chain, or the end-of-backward flush."""
@@ -369,8 +375,9 @@ class _LayerFn(torch.autograd.Function):
         nsplit = pick_splits(B, H, Nq, k3.shape[1])
         o, lse = K.attn_fwd(q3, k3, v3, kmask, H, D, scale, p_attn, seed, nsplit)
         o2 = o.view(B * Nq, C)
-        # a batch-broadcast query stream (Bq = 1) is added as the residual without expanding it
-        z, y, m2, r2, u = K.post_attn_fwd(o2, xq2, wo, bo, g2, be2, EPS, w1, b1, w2, b2)
+        # a batch-broadcast query stream (Bq = 1) is added as the residual without expanding it;
+        # residual dropout (p_attn: the layer's one dropout rate) in the kernel epilogues
+        z, y, m2, r2, u = K.post_attn_fwd(o2, xq2, wo, bo, g2, be2, EPS, w1, b1, w2, b2, seed=seed, p=p_attn)
         ctx.spec, ctx.bw, ctx.seed, ctx.p_attn = spec, bw, seed, p_attn
         ctx.dims = (B, Bq, Nq, C, H, D, scale)
         ctx.kv_grad = x_kv is not None and ctx.needs_input_grad[6]
@@ -434,14 +441,15 @@ class _LayerFn(torch.autograd.Function):
             g = _grad_of(p)
             return None if g is None else g.view(-1)[a:b]
 
+        drop = dict(seed=ctx.seed, p=ctx.p_attn)
         if WGRAD_SLAB and R < TALL_ROWS:
             sl = _GradSlab(R, [C * C, C, C, C, C * C, C, C * C, C], dz2)
             dy, do, delta = K.post_attn_bwd(dz2, y, m2, r2, u, o2, wo, w1, w2, g2, be2, H, sl.targets(), slab=True,
-                                            **_take_job())
+                                            **_take_job(), **drop)
             sl.defer(K, [flat(p) for p in (Wo, bo, g2, be2, W1, b1, W2, b2)])
         else:
             dy, do, delta = K.post_attn_bwd(dz2, y, m2, r2, u, o2, wo, w1, w2, g2, be2, H,
-                                            [gb(Wo), gb(bo), gb(g2), gb(be2), gb(W1), gb(b1), gb(W2), gb(b2)])
+                                            [gb(Wo), gb(bo), gb(g2), gb(be2), gb(W1), gb(b1), gb(W2), gb(b2)], **drop)
         delta3 = delta.view(B, Nq, H)
         # --- attention backward + input-side projections (weight grads fused into ln_linear_bwd) ----
         if spec.cross:
@@ -549,7 +557,7 @@ class _SABlockFn(torch.autograd.Function):
     leaves registers at a boundary.  Weight gradients go through per-tile slabs (slab jobs)."""
 
     @staticmethod
-    def forward(ctx, specs, bws, x, *ps):
+    def forward(ctx, specs, bws, seed, pdrop, x, *ps):
         K = kernels(x)
         L = len(specs)
         spec = specs[0]
@@ -572,19 +580,22 @@ class _SABlockFn(torch.autograd.Function):
             _, _, wo, w1, w2 = bws[i]
             bo, g2, be2, b1, b2 = p[5], p[6], p[7], p[9], p[11]
             qkv3 = qkv.view(B, N, 3 * C)
-            o, lse = K.attn_fwd(qkv3[:, :, :C], qkv3[:, :, C:2 * C], qkv3[:, :, 2 * C:], None, H, D, scale, 0.0, 0,
-                                nsplit)
+            # layer i of the block draws its masks from site i of the block's device seed
+            o, lse = K.attn_fwd(qkv3[:, :, :C], qkv3[:, :, C:2 * C], qkv3[:, :, 2 * C:], None, H, D, scale, pdrop, seed,
+                                nsplit, site=i)
             o2 = o.view(R, C)
             if i + 1 < L:
                 pn = P[i + 1]
                 z, y, m2, r2, u, qkv_n, mean_n, rstd_n = K.post_attn_ln_linear_fwd(
-                    o2, xl, wo, bo, g2, be2, EPS, w1, b1, w2, b2, pn[0], pn[1], bws[i + 1][0], pn[3])
+                    o2, xl, wo, bo, g2, be2, EPS, w1, b1, w2, b2, pn[0], pn[1], bws[i + 1][0], pn[3],
+                    seed=seed, site=i, p=pdrop)
             else:
-                z, y, m2, r2, u = K.post_attn_fwd(o2, xl, wo, bo, g2, be2, EPS, w1, b1, w2, b2)
+                z, y, m2, r2, u = K.post_attn_fwd(o2, xl, wo, bo, g2, be2, EPS, w1, b1, w2, b2, seed=seed, site=i, p=pdrop)
                 qkv_n = mean_n = rstd_n = None
             saved += [xl, qkv, mean1, rstd1, o, lse, y, m2, r2, u]
             xl, qkv, mean1, rstd1 = z, qkv_n, mean_n, rstd_n
         ctx.specs, ctx.bws, ctx.dims = specs, bws, (B, N, C, H, D, scale)
+        ctx.seed, ctx.p = seed, pdrop
         ctx.save_for_backward(*saved, *ps)
         return xl.view(B, N, C)
 
@@ -616,11 +627,14 @@ class _SABlockFn(torch.autograd.Function):
             _, _, wo, w1, w2 = bws[i]
             return (y, m2, r2, u, o.view(R, C), wo, w1, w2, P[i][6], P[i][7])
 
+        def drop(i):
+            return dict(seed=ctx.seed, site=i, p=ctx.p)
+
         dz2 = dz.reshape(R, C)
         if not dz2.is_contiguous():
             dz2 = dz2.contiguous()
         sl = _GradSlab(R, PA_SIZES(C), dz2)
-        dy, do, delta = K.post_attn_bwd(dz2, *pa_args(L - 1), H, sl.targets(), slab=True, **_take_job())
+        dy, do, delta = K.post_attn_bwd(dz2, *pa_args(L - 1), H, sl.targets(), slab=True, **_take_job(), **drop(L - 1))
         sl.defer(K, pa_dsts(P[L - 1]))
         dx = None
         for i in range(L - 1, -1, -1):
@@ -628,21 +642,21 @@ class _SABlockFn(torch.autograd.Function):
             qkv3 = qkv.view(B, N, 3 * C)
             dqkv = torch.empty((B, N, 3 * C), **f32)  # every column block is written by attn_bwd
             K.attn_bwd(qkv3[:, :, :C], qkv3[:, :, C:2 * C], qkv3[:, :, 2 * C:], None, o, do.view(B, N, C), lse,
-                       delta.view(B, N, H), H, D, scale, 0.0, 0, dqkv[:, :, :C], dqkv[:, :, C:2 * C],
-                       dqkv[:, :, 2 * C:])
+                       delta.view(B, N, H), H, D, scale, ctx.p, ctx.seed, dqkv[:, :, :C], dqkv[:, :, C:2 * C],
+                       dqkv[:, :, 2 * C:], site=i)
             if i > 0:
                 sl = _GradSlab(R, LL_SIZES(C) + PA_SIZES(C), dz2)
                 tg = sl.targets()
                 dy, do, delta = K.ln_linear_post_attn_bwd(dqkv.view(R, 3 * C), bws[i][0], xl, mean1, rstd1, P[i][0],
                                                           P[i][1], dy, tg[:4], *pa_args(i - 1), H, tg[4:],
-                                                          **_take_job())
+                                                          **_take_job(), **drop(i - 1))
                 sl.defer(K, ll_dsts(P[i]) + pa_dsts(P[i - 1]))
             else:
                 sl = _GradSlab(R, LL_SIZES(C), dz2)
                 dx = K.ln_linear_bwd(dqkv.view(R, 3 * C), bws[0][0], xl, mean1, rstd1, P[0][0], P[0][1], dy, True,
                                      *sl.targets(), slab=True, **_take_job())
                 sl.defer(K, ll_dsts(P[0]))
-        return (None, None, dx.view(B, N, C)) + (None,) * len(ps)
+        return (None, None, None, None, dx.view(B, N, C)) + (None,) * len(ps)
 
 
 def self_attention_block(block, x):
@@ -665,19 +679,24 @@ def self_attention_block(block, x):
         x = x.float()
     bws = tuple(_bf16_weights(sp, ps) for sp, ps in zip(specs, pss))
     flat_ps = [p for ps in pss for p in ps]
-    return _SABlockFn.apply(tuple(specs), bws, x, *flat_ps)
+    p = specs[0].dropout if layers[0].training else 0.0
+    return _SABlockFn.apply(tuple(specs), bws, _seed(p, x.device), p, x, *flat_ps)
 
 
-def _seed(spec: LayerSpec, training: bool) -> int:
-    if spec.dropout > 0.0 and training:
-        return int(torch.randint(0, 2**31 - 1, (1,)).item())
-    return 0
+def _seed(p: float, device) -> Optional[torch.Tensor]:
+    """Device seed of one fused call's dropout masks (None when p == 0).
+
+    Drawn ON THE DEVICE by torch's generator: under hipGraph capture the draw is a graph node
+    whose Philox offset torch advances on every replay, so each replayed step gets fresh masks
+    (a host integer would be frozen into the graph).  The backward reads the same tensor, so
+    masks are regenerated, never stored."""
+    if p <= 0.0:
+        return None
+    return torch.randint(-(2**62), 2**62, (1,), device=device, dtype=torch.int64)
 
 
 def _run_layer(layer, x_q, x_kv=None, pad_mask=None, src: Optional[KVSource] = None):
     spec, ps = layer_spec_and_params(layer)
-    if spec.dropout > 0.0 and layer.training:
-        raise NotImplementedError("fused path: dropout > 0 handled by the eager path")
     kmask = pad_mask.to(torch.bool).contiguous() if pad_mask is not None else None
     bw = _bf16_weights(spec, ps)
     p_attn = spec.dropout if layer.training else 0.0
@@ -685,13 +704,13 @@ def _run_layer(layer, x_q, x_kv=None, pad_mask=None, src: Optional[KVSource] = N
         x_q = x_q.float()
     if x_kv is not None and x_kv.dtype != torch.float32:
         x_kv = x_kv.float()
-    return _LayerFn.apply(spec, bw, _seed(spec, layer.training), p_attn, src, x_q, x_kv, kmask, *ps)
+    return _LayerFn.apply(spec, bw, _seed(p_attn, x_q.device), p_attn, src, x_q, x_kv, kmask, *ps)
 
 
 def _fusable(layer, x=None) -> bool:
     spec, _ = layer_spec_and_params(layer)
     d = spec.C // spec.heads
-    return (spec.C in (32, 64, 128) and d in (16, 32, 64, 128) and not (spec.dropout > 0.0 and layer.training))
+    return spec.C in (32, 64, 128) and d in (16, 32, 64, 128)
 
 
 def can_fuse(layer, x_kv=None) -> bool:

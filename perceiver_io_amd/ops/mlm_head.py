@@ -6,9 +6,13 @@ interact, evaluating the head only where ``label != -100`` gives the identical m
 and gradients at ~15 % of the cost.
 
 HIP path: rows are compacted on device into a fixed-capacity index list (no host sync,
-graph-capturable; capacity = expected count + 8σ + 64, overflow probability < 1e-15 and
-reported through :func:`last_overflow`), then one fused kernel pair computes logits tile
+graph-capturable; capacity = expected count + 8σ + 64 at the masking rate ``p`` of the model's
+``TextMasking``, overflow probability < 1e-15), then one fused kernel pair computes logits tile
 by tile in registers (``csrc/mlm_head.hip``) — the logits are never written to memory.
+
+Overflow is never silent: every call ORs its device overflow bit into a persistent per-device
+flag (an in-place op, so replayed hipGraphs update it too); the trainer reads it at log steps
+(:func:`check_overflow`) and raises.
 """
 from __future__ import annotations
 
@@ -20,14 +24,44 @@ import torch.nn.functional as F
 from . import ext
 
 _overflow = None
+_flags = {}
 
 
 def last_overflow():
-    """Device bool of the most recent HIP call: True if selected rows exceeded capacity."""
+    """Device bool of the most recent call: True if selected rows exceeded capacity."""
     return _overflow
 
 
+def overflow_flag(device) -> torch.Tensor:
+    """Persistent device bool: set once any call on ``device`` overflowed its capacity."""
+    device = torch.device(device)
+    f = _flags.get(device)
+    if f is None:
+        f = _flags[device] = torch.zeros((), dtype=torch.bool, device=device)
+    return f
+
+
+def _record(ovf: torch.Tensor):
+    global _overflow
+    _overflow = ovf
+    overflow_flag(ovf.device).logical_or_(ovf.reshape(()))
+
+
+def check_overflow(reset: bool = False) -> bool:
+    """Host check (one sync) of every device's overflow flag; raises if any is set."""
+    hit = [d for d, f in _flags.items() if bool(f.item())]
+    if reset:
+        for f in _flags.values():
+            f.zero_()
+    if hit:
+        raise RuntimeError(f"masked-LM selected positions exceeded the fixed row capacity on {hit}: "
+                           "labels fell out of the loss.  The capacity follows TextMasking.mask_p — "
+                           "check that the masking rate passed to the loss matches the model's")
+    return False
+
+
 def capacity(n_positions: int, p: float = 0.15) -> int:
+    p = min(max(float(p), 1e-6), 1.0)
     mu = n_positions * p
     cap = int(math.ceil(mu + 8.0 * math.sqrt(max(mu * (1 - p), 1.0)) + 64))
     return max(1, min(n_positions, cap))
@@ -87,16 +121,18 @@ def compact_rows(labels: torch.Tensor, cap: int):
     idx = buf[:cap]
     valid = torch.arange(cap, device=labels.device) < count
     labels_c = torch.where(valid, flat.index_select(0, idx), torch.full_like(idx, -100)).contiguous()
-    _overflow = count > cap
+    _record(count > cap)
     return idx, labels_c, count
 
 
-def masked_lm_loss(h: torch.Tensor, labels: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor):
-    """Mean CE over positions with ``label != -100``; ``h`` is ``(B, L, C)``."""
+def masked_lm_loss(h: torch.Tensor, labels: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor,
+                   p: float = 0.15):
+    """Mean CE over positions with ``label != -100``; ``h`` is ``(B, L, C)``; ``p`` the
+    masking rate (sizes the row capacity)."""
     from . import use_hip
 
     if use_hip(h) and h.shape[-1] in (32, 64, 128):
-        cap = capacity(labels.numel())
+        cap = capacity(labels.numel(), p)
         idx, labels_c, count = compact_rows(labels, cap)
         return _MaskedCE.apply(h, weight, bias, idx, labels_c, count)
     sel = labels.reshape(-1) != -100
@@ -112,7 +148,8 @@ def masked_lm_loss(h: torch.Tensor, labels: torch.Tensor, weight: torch.Tensor, 
 # ------------------------------------------------------------------------------------------
 def row_capacity(length: int, p: float = 0.15) -> int:
     """Per-sequence slots for selected positions: expected + 8σ + 16, a multiple of 32, ≤ L
-    (L = 512: 160 slots for ~77 selected; overflow probability < 1e-15 per sequence)."""
+    (L = 512, p = 0.15: 160 slots for ~77 selected; overflow probability < 1e-15 per sequence)."""
+    p = min(max(float(p), 1e-6), 1.0)
     mu = length * p
     cap = int(math.ceil(mu + 8.0 * math.sqrt(max(mu * (1 - p), 1.0)) + 16))
     cap = (cap + 31) // 32 * 32
@@ -135,19 +172,19 @@ def compact_per_row(labels: torch.Tensor, cap: int):
     cnt = sel.sum(1, keepdim=True)
     valid = torch.arange(cap, device=labels.device) < cnt
     labels_c = torch.where(valid, labels.gather(1, idx), torch.full_like(idx, -100))
-    _overflow = (cnt > cap).any()
+    _record((cnt > cap).any())
     return idx, labels_c, sel.sum()
 
 
 def compact_lm_loss(h: torch.Tensor, labels_c: torch.Tensor, count: torch.Tensor, weight: torch.Tensor,
-                    bias: torch.Tensor, positions: int):
+                    bias: torch.Tensor, positions: int, p: float = 0.15):
     """Mean CE over the rows of a per-sequence-compacted ``(B, cap, C)`` batch whose label is
     not -100.  The HIP path compacts those rows once more over the whole batch (capacity for
     ``positions`` tokens at the masking rate), so the vocab GEMMs see only real rows."""
     from . import use_hip
 
     if use_hip(h) and h.shape[-1] in (32, 64, 128):
-        idx, lab, cnt = compact_rows(labels_c, capacity(positions))
+        idx, lab, cnt = compact_rows(labels_c, capacity(positions, p))
         return _MaskedCE.apply(h, weight, bias, idx, lab, cnt)
     lab = labels_c.reshape(-1)
     logits = F.linear(h.reshape(-1, h.shape[-1]), weight, bias)
@@ -176,28 +213,31 @@ class _GatherQueries(torch.autograd.Function):
         return None, None
 
 
-def masked_decode_loss(decoder, x_latent: torch.Tensor, labels: torch.Tensor):
+def masked_decode_loss(decoder, x_latent: torch.Tensor, labels: torch.Tensor, p: float = 0.15):
     """MLM loss decoding only the selected positions.
 
     Decoder queries never interact (reference ``perceiver/model.py:236``: one cross-attention
     from the K output queries to the latents), so decoding the ~15 % selected positions of each
-    sequence — gathered into ``row_capacity(L)`` slots — gives the same loss and gradients as
+    sequence — gathered into ``row_capacity(L, p)`` slots — gives the same loss and gradients as
     decoding all ``L`` at a third of the decoder cost.  The output-query
-    gradient flows back through the gather (index_select → index_add).
+    gradient flows back through the gather (index_select → index_add).  ``p`` is the masking
+    rate (``TextMasking.mask_p``): it sizes both capacities.
     """
-    global _overflow
+    from ..parallel.reducer import bucket_ready_point
     from . import use_hip
 
+    x_latent = bucket_ready_point(x_latent)  # before any decoder op (DDP early bucket)
     B, L = labels.shape
     decoder.check_latent(x_latent)
     lin = decoder.output_adapter.linear
-    cap = row_capacity(L)
+    cap = row_capacity(L, p)
     if use_hip(x_latent) and lin.weight.shape[1] in (32, 64, 128):
-        idx, _, gidx, glab, total, _overflow = ext.require().mlm_select(labels.contiguous(), cap, capacity(B * L))
+        idx, _, gidx, glab, total, ovf = ext.require().mlm_select(labels.contiguous(), cap, capacity(B * L, p))
+        _record(ovf)
         q = _GatherQueries.apply(decoder.output, idx.reshape(-1)).view(B, cap, -1)
         h = decoder.cross_attention(q, x_latent)
         return _MaskedCE.apply(h, lin.weight, lin.bias, gidx, glab, total)
     idx, labels_c, count = compact_per_row(labels, cap)
     q = _GatherQueries.apply(decoder.output, idx.reshape(-1)).view(B, cap, -1)
     h = decoder.cross_attention(q, x_latent)
-    return compact_lm_loss(h, labels_c, count, lin.weight, lin.bias, B * L)
+    return compact_lm_loss(h, labels_c, count, lin.weight, lin.bias, B * L, p)

@@ -111,20 +111,21 @@ class FlatParameterSpace:
         return all(p.grad is not None and p.grad.data_ptr() == self.grad[o:o + 1].data_ptr()
                    for p, o in zip(self.params, self.offsets))
 
-    def bucket_ranges(self, bucket_bytes: int):
-        """Split [0, numel) into contiguous ranges of ≤ bucket_bytes in reverse parameter
-        order (gradients of late parameters are produced first in backward)."""
+    def bucket_ranges(self, bucket_bytes: int, hi: Optional[int] = None):
+        """Split [0, hi) (default: the whole buffer) into contiguous ranges of about
+        ``bucket_bytes`` at parameter boundaries, in reverse parameter order (gradients of late
+        parameters are produced first in backward)."""
         cap = max(ALIGN, bucket_bytes // 4)
-        ends = self.offsets[1:] + [self.numel]
+        hi = self.numel if hi is None else hi
         ranges = []
-        hi = self.numel
         for o in reversed(self.offsets):
+            if o >= hi:
+                continue
             if hi - o >= cap:
                 ranges.append((o, hi))
                 hi = o
         if hi > 0:
             ranges.append((0, hi))
-        del ends
         return ranges
 
 

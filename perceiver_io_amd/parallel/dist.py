@@ -71,6 +71,53 @@ def init(backend: str | None = None, timeout_s: float = 1800.0, device_type: str
     return _INFO
 
 
+_GRAPH_COLL = {}
+
+
+def graph_collectives_ok(device) -> bool:
+    """Can RCCL collectives be captured in a hipGraph on this node?  Probed once per device:
+    every rank captures a tiny all-reduce on a side stream, the ranks agree (eager all-reduce of
+    the capture status) before anyone replays, the replay's result is checked, and the ranks
+    agree again.  ``PERCEIVER_GRAPH_COLLECTIVES=0/1`` forces the answer.  Never true for gloo."""
+    env = os.environ.get("PERCEIVER_GRAPH_COLLECTIVES")
+    if _INFO.backend != "nccl" or not (dist.is_available() and dist.is_initialized()):
+        return False
+    if env is not None:
+        return env not in ("0", "", "false")
+    device = torch.device(device)
+    if device in _GRAPH_COLL:
+        return _GRAPH_COLL[device]
+    ws = _INFO.world_size
+    t = torch.ones(64, device=device)
+    side = torch.cuda.Stream(device=device)
+    g = None
+    captured = 1.0
+    try:
+        side.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(side):
+            dist.all_reduce(t)  # warm the communicator outside the capture
+        torch.cuda.synchronize(device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=side):
+            dist.all_reduce(t)
+    except Exception:  # noqa: BLE001 - any capture failure means "not capturable"
+        captured, g = 0.0, None
+    flag = torch.tensor([captured], device=device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    ok = bool(flag.item() > 0.5)
+    if ok:
+        t.fill_(1.0)
+        torch.cuda.synchronize(device)
+        g.replay()
+        torch.cuda.synchronize(device)
+        good = float(torch.allclose(t, torch.full_like(t, float(ws))))
+        flag = torch.tensor([good], device=device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        ok = bool(flag.item() > 0.5)
+    _GRAPH_COLL[device] = ok
+    return ok
+
+
 def barrier():
     if dist.is_available() and dist.is_initialized():
         if _INFO.backend == "nccl":

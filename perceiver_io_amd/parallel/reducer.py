@@ -3,36 +3,112 @@
 Replaces the DDP Reducer the reference gets from Lightning (``trainer.yaml:47``):
   * parameters and buffers are broadcast once from rank 0 as flat tensors (C-01); the
     deterministic Fourier position-encoding buffer is *not* re-broadcast every step (C-02);
-  * gradients live in ONE contiguous fp32 buffer (``ops.optim.FlatParameterSpace``), reduced
-    by a few large RCCL all-reduces instead of per-parameter buckets.  Per-step gradient
-    volume is 4–11 MB, so on xGMI the collective is latency-bound: 1–2 buckets is optimal
-    and more, smaller buckets only add ring-hop latency;
+  * gradients live in ONE contiguous fp32 buffer (``ops.optim.FlatParameterSpace``), reduced by
+    a few large RCCL all-reduces instead of per-parameter buckets.  Per-step gradient volume is
+    4–11 MB, so on xGMI (point-to-point links, ring all-reduce bound by one link per hop) the
+    collective is latency-bound: 2–3 buckets, not DDP's 25 MB-bucket machinery;
   * the average (÷ world) is folded into the fused optimizer's gradient scale (no extra pass);
-  * optional overlap: ``ready(range)`` launches a bucket's all-reduce on a side HIP stream
-    as soon as the backward has produced it (the decoder/head grads are produced first);
-    ``finish()`` makes the main stream wait on the side stream.
+  * overlap with the backward: the decoder / output head runs first in backward and is the tail
+    of the flat buffer (module order: encoder, then decoder).  ``bucket_ready_point(x)`` marks the
+    decoder's input; when autograd reaches it every decoder-side gradient is final (see
+    ``_ReadyFn``), and the tail bucket's all-reduce is launched on a side HIP stream while the
+    encoder backward runs.  ``finish()`` reduces the remaining buckets and joins the side stream;
+  * the whole step — backward-driven bucket launches, the join and the fused AdamW — is captured
+    in the step's hipGraph when RCCL collectives are capturable on this node
+    (``dist.graph_collectives_ok``, probed once: capture + replay of a tiny all-reduce agreed by
+    every rank); otherwise the collectives run eagerly after the replayed forward/backward.
 """
 from __future__ import annotations
 
-from typing import List, Optional, Tuple
+from typing import Iterable, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
 
+_ACTIVE: List["FlatGradReducer"] = []
+
+
+class _ReadyFn(torch.autograd.Function):
+    """Identity whose backward launches the early bucket.
+
+    Applied to the decoder's input *before* any decoder op is recorded.  The autograd engine
+    runs ready nodes in decreasing sequence number, and every decoder/head node (the output-query
+    gather or expand, the fused layers, the vocab head, their AccumulateGrad leaves) was created
+    after this one — so when this backward runs, every gradient of the decoder's parameters has
+    been produced (the fused kernels' deferred weight-gradient slab reductions are flushed
+    first)."""
+
+    @staticmethod
+    def forward(ctx, x, red):
+        ctx.red = red
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        ctx.red.early_ready()
+        return g, None
+
+
+def bucket_ready_point(x: torch.Tensor) -> torch.Tensor:
+    """Mark ``x`` (the decoder's input) as the early-bucket ready point of the active reducer."""
+    if not _ACTIVE or not torch.is_grad_enabled() or not x.requires_grad:
+        return x
+    red = _ACTIVE[-1]
+    if not red.overlap_ready():
+        return x
+    return _ReadyFn.apply(x, red)
+
 
 class FlatGradReducer:
-    def __init__(self, flat, bucket_bytes: int = 32 << 20, overlap: bool = False, wire_dtype: Optional[torch.dtype] = None):
+    def __init__(self, flat, bucket_bytes: int = 4 << 20, overlap: bool = True, in_graph: Optional[bool] = None,
+                 wire_dtype: Optional[torch.dtype] = None):
         self.flat = flat
         self.world = dist.get_world_size() if (dist.is_available() and dist.is_initialized()) else 1
+        self.bucket_bytes = bucket_bytes
         self.buckets: List[Tuple[int, int]] = flat.bucket_ranges(bucket_bytes)
-        self.overlap = overlap and flat.device.type == "cuda"
+        self.early: Optional[Tuple[int, int]] = None
+        # overlap needs every parameter gradient to land in flat.grad directly (no 8-way replicas
+        # that a later fold() would still add into the early bucket's range)
+        self.overlap = bool(overlap) and getattr(flat, "grad_rep", None) is None
         self.wire_dtype = wire_dtype
-        self._side = torch.cuda.Stream() if self.overlap else None
+        self.on_gpu = flat.device.type == "cuda"
+        self._side = torch.cuda.Stream(device=flat.device) if (self.on_gpu and self.overlap) else None
         self._launched = set()
+        self.early_launches = 0  # early-bucket launches driven by backward (tests / diagnostics)
+        if in_graph is None:
+            from .dist import graph_collectives_ok
+
+            in_graph = self.enabled and self.on_gpu and graph_collectives_ok(flat.device)
+        self.in_graph = bool(in_graph)
+        if self.enabled:
+            _ACTIVE.append(self)
 
     @property
     def enabled(self) -> bool:
         return self.world > 1
+
+    def close(self):
+        if self in _ACTIVE:
+            _ACTIVE.remove(self)
+
+    # -- buckets -------------------------------------------------------------------------
+    def set_early_params(self, params: Iterable[torch.nn.Parameter]):
+        """Declare the parameters final at the ready point (the decoder + head).  They must be a
+        contiguous tail ``[lo, numel)`` of the flat buffer; bucket 0 becomes that tail."""
+        ids = {id(p) for p in params}
+        offs = [o for p, o in zip(self.flat.params, self.flat.offsets) if id(p) in ids]
+        if not offs:
+            return
+        lo = min(offs)
+        tail = [p for p, o in zip(self.flat.params, self.flat.offsets) if o >= lo]
+        if any(id(p) not in ids for p in tail):
+            return  # not a contiguous tail: no early bucket (everything reduced in finish())
+        self.early = (lo, self.flat.numel)
+        rest = [r for r in self.flat.bucket_ranges(self.bucket_bytes, hi=lo)]
+        self.buckets = [self.early] + rest
+
+    def overlap_ready(self) -> bool:
+        return self.enabled and self.overlap and self.early is not None
 
     def broadcast_parameters(self, module: torch.nn.Module, src: int = 0):
         """C-01: one broadcast of the flat parameter buffer + remaining buffers."""
@@ -58,17 +134,27 @@ class FlatGradReducer:
             dist.all_reduce(g)
 
     def ready(self, bucket: int):
-        """Launch one bucket's all-reduce (side stream when overlapping)."""
+        """Launch one bucket's all-reduce (on the side stream when overlapping on a GPU)."""
         if not self.enabled or bucket in self._launched:
             return
         self._launched.add(bucket)
         lo, hi = self.buckets[bucket]
         if self._side is not None:
-            self._side.wait_stream(torch.cuda.current_stream())
+            self._side.wait_stream(torch.cuda.current_stream(self.flat.device))
             with torch.cuda.stream(self._side):
                 self._reduce(lo, hi)
         else:
             self._reduce(lo, hi)
+
+    def early_ready(self):
+        """Backward reached the decoder input: the tail bucket is final → launch it."""
+        if not self.overlap_ready() or 0 in self._launched:
+            return
+        from ..ops.fused import flush_pending
+
+        flush_pending()  # deferred weight-gradient slab reductions of the decoder/head kernels
+        self.early_launches += 1
+        self.ready(0)
 
     def finish(self):
         """All remaining buckets, then join the side stream."""
@@ -78,7 +164,7 @@ class FlatGradReducer:
         for i in range(len(self.buckets)):
             self.ready(i)
         if self._side is not None:
-            torch.cuda.current_stream().wait_stream(self._side)
+            torch.cuda.current_stream(self.flat.device).wait_stream(self._side)
         self._launched.clear()
 
     def grad_scale(self) -> float:

@@ -29,7 +29,31 @@ from .models import (ClassificationOutputAdapter, ImageInputAdapter, PerceiverDe
                      PerceiverMLM, TextInputAdapter, TextMasking, TextOutputAdapter)
 from .train.module import LitModuleBase, instantiate_class
 from .utils.misc import freeze, predict_masked_samples
-from .utils.tokenizer import MASK_TOKEN_ID, SPECIAL_TOKENS, UNK_TOKEN_ID
+from .utils.tokenizer import MASK_TOKEN_ID, PAD_TOKEN_ID, SPECIAL_TOKENS, UNK_TOKEN_ID
+
+# text batches are padded to a multiple of this many tokens before a graph-captured step
+LENGTH_BUCKET = 64
+
+
+def bucket_text_batch(batch, max_seq_len: int, multiple: int = LENGTH_BUCKET):
+    """``(labels, ids, pad_mask)`` padded along the sequence to ``round_up(L, multiple)``
+    (capped at ``max_seq_len``) with PAD ids and ``True`` (= padding) mask entries.
+
+    The reference collator pads each batch to its longest sequence (``data/imdb.py:52-63``), so
+    an epoch sees hundreds of lengths; captured step graphs are cached per shape, and this
+    bounds the distinct shapes to ``max_seq_len / multiple``.  Semantics are unchanged: padded
+    keys are masked out of every cross-attention (K-08), masking never selects PAD positions,
+    and the MLM loss / classifier read no padded position."""
+    y, x, m = batch
+    L = x.shape[1]
+    Lp = min(-(-L // multiple) * multiple, max(L, int(max_seq_len)))
+    if Lp == L:
+        return batch
+    if m is None:
+        m = torch.zeros(x.shape, dtype=torch.bool, device=x.device)
+    x = torch.nn.functional.pad(x, (0, Lp - L), value=PAD_TOKEN_ID)
+    m = torch.nn.functional.pad(m, (0, Lp - L), value=True)
+    return y, x, m
 
 
 class LitModel(LitModuleBase):
@@ -146,6 +170,9 @@ class LitTextClassifier(LitClassifier):
         y, x, x_mask = batch
         return self.model(x, x_mask), y
 
+    def graph_batch(self, batch):
+        return bucket_text_batch(batch, self.hparams.max_seq_len)
+
 
 def _stale_ckpt_overrides(clf_ckpt: str) -> dict:
     """D8: the clf checkpoint's hparams may carry an mlm_ckpt path that no longer exists."""
@@ -195,6 +222,9 @@ class LitMaskedLanguageModel(LitModel):
     def step(self, batch):
         _, x, x_mask = batch
         return self.model.loss(x, x_mask)
+
+    def graph_batch(self, batch):
+        return bucket_text_batch(batch, self.hparams.max_seq_len)
 
     def training_step(self, batch, batch_idx):
         loss = self.step(batch)

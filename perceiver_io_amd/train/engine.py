@@ -11,9 +11,18 @@ generator, optimizer hyper-parameters read from device memory (staged before rep
 
 Gradient accumulation: ``accumulate`` micro-batches per optimizer step (the all-reduce and
 update run only on the last one, as in Lightning's ``accumulate_grad_batches``).
+
+Variable batch shapes (the reference's IMDB collator pads to the longest sequence of each
+batch, ``data/imdb.py:52-63``, and its loaders keep the partial last batch): captured graphs
+are cached per batch *shape signature* (tensor shapes + dtypes), at most ``max_graphs`` of
+them (least recently used evicted, each with its own private memory pool so an evicted
+graph's memory is really released).  Task modules bucket text lengths before the step
+(``LitModuleBase.graph_batch``: pad to a multiple of 64, pad keys masked — identical
+semantics), so an epoch of pad-to-longest batches needs a handful of graphs, not hundreds.
 """
 from __future__ import annotations
 
+from collections import OrderedDict
 from typing import Callable, Dict, Optional
 
 import torch
@@ -40,6 +49,26 @@ def _clone_to(obj, device):
     return obj
 
 
+def shape_key(obj):
+    """Hashable signature of a (nested) batch: tensor shapes/dtypes, other leaves by value."""
+    if isinstance(obj, torch.Tensor):
+        return ("T", tuple(obj.shape), obj.dtype)
+    if isinstance(obj, (list, tuple)):
+        return (type(obj).__name__,) + tuple(shape_key(o) for o in obj)
+    if isinstance(obj, dict):
+        return ("D",) + tuple((k, shape_key(obj[k])) for k in sorted(obj))
+    return ("V", obj)
+
+
+class _Captured:
+    """One captured step: the graph, its static input batch and its static outputs."""
+
+    __slots__ = ("graph", "batch", "loss", "state")
+
+    def __init__(self, graph, batch, loss, state):
+        self.graph, self.batch, self.loss, self.state = graph, batch, loss, state
+
+
 def _to(obj, device):
     if isinstance(obj, torch.Tensor):
         return obj.to(device, non_blocking=True)
@@ -58,7 +87,8 @@ class StepEngine:
     """
 
     def __init__(self, loss_fn: Callable, optimizer, scheduler=None, reducer=None, device=None,
-                 graph: bool = False, accumulate: int = 1, warmup_eager: int = 2):
+                 graph: bool = False, accumulate: int = 1, warmup_eager: int = 2, max_graphs: int = 12,
+                 state_hooks=None):
         from ..ops.optim import FusedAdamW
 
         self.loss_fn = loss_fn
@@ -70,9 +100,13 @@ class StepEngine:
         self.graph_enabled = bool(graph) and self.fused and self.device.type == "cuda"
         self.accumulate = max(1, int(accumulate))
         self.warmup_eager = warmup_eager
-        self._graph: Optional[torch.cuda.CUDAGraph] = None
-        self._static_batch = None
-        self._static_loss = None
+        self.max_graphs = max(1, int(max_graphs))
+        # state_hooks = (save, restore): side state produced while capturing (e.g. the
+        # trainer's logged metric tensors, which are static outputs of that graph) is saved per
+        # graph and restored before each replay of it
+        self.state_hooks = state_hooks
+        self._graphs: "OrderedDict[tuple, _Captured]" = OrderedDict()
+        self.captures = 0  # graphs captured so far (evictions included)
         self._eager_steps = 0
         self._micro = 0
         # every step (eager warmups, capture, replays) runs on ONE dedicated stream: autograd's
@@ -109,27 +143,48 @@ class StepEngine:
             self.opt.zero_grad()
 
     # -- graph -----------------------------------------------------------------------------
-    def _capture(self, batch):
+    def _capture(self, batch) -> _Captured:
         opt = self.opt
-        self._static_batch = _clone_to(batch, self.device)
+        static = _clone_to(batch, self.device)
         # warmup on the capture stream (allocator + lazy init); no optimizer update → nothing to undo
         for _ in range(2):
             opt.flat.zero_grad_buffers()
-            loss = self.loss_fn(self._static_batch)
+            loss = self.loss_fn(static)
             loss.backward()
             del loss
         opt.flat.zero_grad_buffers()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=self.stream):
             opt.flat.zero_grad_buffers()
-            loss = self.loss_fn(self._static_batch)
+            loss = self.loss_fn(static)
             loss.backward()
             if self._opt_in_graph:
                 if self.reducer is not None and self.reducer.enabled:
                     self.reducer.finish()
                 opt.device_update()
-        self._graph = g
-        self._static_loss = loss
+        state = self.state_hooks[0]() if self.state_hooks is not None else None
+        self.captures += 1
+        return _Captured(g, static, loss, state)
+
+    def _graph_for(self, batch) -> _Captured:
+        """The captured step for this batch's shape (captured on first sight, LRU-cached)."""
+        key = shape_key(batch)
+        ent = self._graphs.get(key)
+        if ent is not None:
+            self._graphs.move_to_end(key)
+            if self.state_hooks is not None:
+                self.state_hooks[1](ent.state)
+            return ent
+        while len(self._graphs) >= self.max_graphs:
+            _, old = self._graphs.popitem(last=False)
+            del old  # its private pool is released with the graph
+        ent = self._capture(batch)
+        self._graphs[key] = ent
+        return ent
+
+    @property
+    def num_graphs(self) -> int:
+        return len(self._graphs)
 
     @property
     def _opt_in_graph(self) -> bool:
@@ -156,20 +211,19 @@ class StepEngine:
                 loss = self._eager_micro(_to(b, self.device), True)
                 self._optimizer_step()
                 return loss.detach()
-            if self._graph is None:
-                self._capture(b)
-            _copy_into(self._static_batch, b)
+            ent = self._graph_for(b)
+            _copy_into(ent.batch, b)
             if self._opt_in_graph:
                 self.opt.stage_hyper()
-                self._graph.replay()
+                ent.graph.replay()
                 self.opt._step += 1
             else:  # forward+backward replayed; RCCL all-reduce + update eager (3 launches)
-                self._graph.replay()
+                ent.graph.replay()
                 self.reducer.finish()
                 self.opt.step()
             if self.sched is not None:
                 self.sched.step()
-            return self._static_loss.detach().clone()
+            return ent.loss.detach().clone()
         loss = None
         for i, b in enumerate(batches):
             loss = self._eager_micro(_to(b, self.device), i == len(batches) - 1)
@@ -177,7 +231,5 @@ class StepEngine:
         return loss.detach()
 
     def invalidate(self):
-        """Drop the captured graph (e.g. after shapes or parameters were re-bound)."""
-        self._graph = None
-        self._static_batch = None
-        self._static_loss = None
+        """Drop every captured graph (e.g. after parameters were re-bound)."""
+        self._graphs.clear()

@@ -123,6 +123,11 @@ class LitModuleBase(nn.Module):
     def on_validation_epoch_end(self) -> None:
         pass
 
+    def graph_batch(self, batch):
+        """Canonicalise a training batch before a hipGraph-captured step (graphs are cached
+        per batch shape, train/engine.py).  Identity here; text modules bucket lengths."""
+        return batch
+
     # -- checkpoints ----------------------------------------------------------------------
     @classmethod
     def load_from_checkpoint(cls, checkpoint_path: str, map_location=None, strict: bool = True, **overrides):

@@ -323,6 +323,9 @@ class Trainer:
                 flat = getattr(opt, "flat", None) or FlatParameterSpace(
                     [p for p in model.parameters() if p.requires_grad], with_shadow=False)
                 reducer = FlatGradReducer(flat)
+                dec = getattr(getattr(model, "model", None), "decoder", None)
+                if dec is not None:  # decoder + head gradients are final first: the early bucket
+                    reducer.set_early_params(dec.parameters())
                 reducer.broadcast_parameters(model)
             if not self.fused and self.gradient_clip_val:
                 warnings.warn("gradient clipping on the eager path uses torch.nn.utils.clip_grad_norm_")
@@ -330,8 +333,12 @@ class Trainer:
             if ckpt_path:
                 self._restore(ckpt_path)
             use_graph = self.graph_capture if self.graph_capture is not None else self.fused
+            # the metric tensors a captured step logs are static outputs of THAT graph: saved per
+            # graph, restored before its replays
+            hooks = (lambda: dict(self._step_logs), self._restore_step_logs)
             self._engine = StepEngine(self._training_loss, opt, sched, reducer=reducer, device=self.device,
-                                      graph=bool(use_graph) and self.accumulate == 1, accumulate=self.accumulate)
+                                      graph=bool(use_graph) and self.accumulate == 1, accumulate=self.accumulate,
+                                      state_hooks=hooks)
             if self.logger is not None and self.is_global_zero:
                 self.logger.log_hyperparams(dict(model.hparams))
             for cb in self.callbacks:
@@ -377,6 +384,12 @@ class Trainer:
     _in_train = False
     _cur_bs = 1
 
+    def _restore_step_logs(self, logs):
+        self._step_logs = dict(logs)
+        for k in self.progress_bar_metrics:
+            if k in logs:
+                self.progress_bar_metrics[k] = logs[k]
+
     def _training_loss(self, batch):
         out = self.model.training_step(batch, self._batch_idx)
         return out["loss"] if isinstance(out, dict) else out
@@ -408,6 +421,8 @@ class Trainer:
                 self._batch_idx = bi
                 self._in_train = True
                 batch = _to(batch, self.device)
+                if self._engine.graph_enabled:
+                    batch = model.graph_batch(batch)  # bounded set of shapes → bounded set of graphs
                 acc_buf.append(batch)
                 if len(acc_buf) < self.accumulate:
                     continue
@@ -432,6 +447,7 @@ class Trainer:
                     vals["steps_per_sec"] = sps
                     self.callback_metrics.update(vals)
                     self.log_scalars(vals)
+                    ops.mlm_head.check_overflow()  # fixed-capacity MLM rows: fail loudly, never truncate
                     if self.terminate_on_nan and not all(math.isfinite(v) for v in vals.values()):
                         raise ValueError(f"non-finite metric at step {self.global_step}: {vals}")
                     if self.enable_progress_bar and self.is_global_zero:
@@ -454,8 +470,13 @@ class Trainer:
         for b in batches:
             loss = self._training_loss(b)
             (loss / len(batches)).backward()
-        if self._engine.reducer is not None:
-            self._engine.reducer.finish()
+        red = self._engine.reducer
+        if red is not None:
+            red.finish()
+            if red.enabled:  # all-reduced SUM → mean before clipping (clip the mean's norm)
+                for p in self.model.parameters():
+                    if p.grad is not None:
+                        p.grad.mul_(red.grad_scale())
         torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.gradient_clip_val)
         opt.step()
         for s in self.lr_schedulers:

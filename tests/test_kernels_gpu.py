@@ -103,14 +103,14 @@ def test_attention_fwd_bwd(B, Bq, Nq, Nk, H, D, ns):
     torch.manual_seed(1)
     q, k, v, km = _attn_inputs(B, Bq, Nq, Nk, H, D)
     scale = 1.0 / math.sqrt(D)
-    o1, l1 = _ext().attn_fwd(q, k, v, km, H, D, scale, 0.0, 0, ns)
-    o2, l2 = _emu().attn_fwd(q, k, v, km, H, D, scale, 0.0, 0, ns)
+    o1, l1 = _ext().attn_fwd(q, k, v, km, H, D, scale, 0.0, None, ns)
+    o2, l2 = _emu().attn_fwd(q, k, v, km, H, D, scale, 0.0, None, ns)
     close(o1, o2, name="O")
     close(l1, l2, 1e-3, "lse")
     assert o1[0].abs().max().item() == 0.0  # fully masked rows → 0
     do = bf(torch.randn(B, Nq, H * D, device=DEV))
-    g1 = _ext().attn_bwd(q, k, v, km, o1, do, l1, None, H, D, scale, 0.0, 0, None, None, None)
-    g2 = _emu().attn_bwd(q, k, v, km, o1, do, l1, None, H, D, scale, 0.0, 0, None, None, None)
+    g1 = _ext().attn_bwd(q, k, v, km, o1, do, l1, None, H, D, scale, 0.0, None, None, None, None)
+    g2 = _emu().attn_bwd(q, k, v, km, o1, do, l1, None, H, D, scale, 0.0, None, None, None, None)
     for a, b, n in zip(g1, g2, ("dq", "dk", "dv")):
         close(a, b, 3e-2, n)
     # packed, uninitialised output buffer (the kernel must overwrite / clear dQ itself)
@@ -118,15 +118,19 @@ def test_attention_fwd_bwd(B, Bq, Nq, Nk, H, D, ns):
         E = H * D
         pk = torch.full((B, Nq, 3 * E), float("nan"), device=DEV)
         dkv = torch.full((B, Nk, 2 * E), float("nan"), device=DEV)
-        _ext().attn_bwd(q, k, v, km, o1, do, l1, None, H, D, scale, 0.0, 0, pk[:, :, :E], dkv[:, :, :E], dkv[:, :, E:])
+        _ext().attn_bwd(q, k, v, km, o1, do, l1, None, H, D, scale, 0.0, None, pk[:, :, :E], dkv[:, :, :E], dkv[:, :, E:])
         close(pk[:, :, :E], g2[0], 3e-2, "dq packed")
         close(dkv[:, :, :E], g2[1], 3e-2, "dk packed")
         close(dkv[:, :, E:], g2[2], 3e-2, "dv packed")
         # K/V shared by several layers: the second application adds onto the first
-        _ext().attn_bwd(q, k, v, km, o1, do, l1, None, H, D, scale, 0.0, 0, pk[:, :, :E], dkv[:, :, :E], dkv[:, :, E:],
+        _ext().attn_bwd(q, k, v, km, o1, do, l1, None, H, D, scale, 0.0, None, pk[:, :, :E], dkv[:, :, :E], dkv[:, :, E:],
                         True)
         close(dkv[:, :, :E], 2 * g2[1], 3e-2, "dk accumulated")
         close(dkv[:, :, E:], 2 * g2[2], 3e-2, "dv accumulated")
+
+
+def _seed(v):
+    return torch.tensor([v], dtype=torch.int64, device=DEV)
 
 
 def test_attention_dropout_statistics():
@@ -134,12 +138,75 @@ def test_attention_dropout_statistics():
     B, Nq, Nk, H, D = 2, 64, 256, 4, 16
     q, k, v, _ = _attn_inputs(B, B, Nq, Nk, H, D, mask=False)
     v = torch.ones_like(v)
-    o, _ = _ext().attn_fwd(q, k, v, None, H, D, 0.25, 0.25, 123, 1)
+    o, _ = _ext().attn_fwd(q, k, v, None, H, D, 0.25, 0.25, _seed(123), 1)
     # E[dropout(P)·1] = 1 per row; rows average close to 1
     m = o.float().mean().item()
     assert abs(m - 1.0) < 0.05, m
-    o2, _ = _ext().attn_fwd(q, k, v, None, H, D, 0.25, 0.25, 123, 1)
-    assert torch.equal(o, o2)  # deterministic for a given seed
+    o2, _ = _ext().attn_fwd(q, k, v, None, H, D, 0.25, 0.25, _seed(123), 1)
+    assert torch.equal(o, o2)  # deterministic for a given device seed
+    o3, _ = _ext().attn_fwd(q, k, v, None, H, D, 0.25, 0.25, _seed(124), 1)
+    assert not torch.equal(o, o3)  # a new seed draws new masks
+    o4, _ = _ext().attn_fwd(q, k, v, None, H, D, 0.25, 0.25, _seed(123), 1, site=1)
+    assert not torch.equal(o, o4)  # so does another call site
+
+
+@pytest.mark.parametrize("B,Bq,Nq,Nk,H,D,ns,p", [
+    (3, 3, 70, 200, 4, 16, 1, 0.1),
+    (2, 1, 32, 900, 4, 32, 3, 0.3),
+    (2, 2, 96, 64, 1, 64, 1, 0.5),
+])
+def test_attention_dropout_matches_emulation(B, Bq, Nq, Nk, H, D, ns, p):
+    """The kernels' hashed masks are reproduced bit-exactly by the emulation, so fwd AND bwd
+    with dropout compare against the fp32 oracle like the p = 0 path."""
+    torch.manual_seed(5)
+    q, k, v, km = _attn_inputs(B, Bq, Nq, Nk, H, D)
+    scale = 1.0 / math.sqrt(D)
+    sd = _seed(987654321987)
+    o1, l1 = _ext().attn_fwd(q, k, v, km, H, D, scale, p, sd, ns, site=3)
+    o2, l2 = _emu().attn_fwd(q, k, v, km, H, D, scale, p, sd, ns, site=3)
+    close(o1, o2, name="O (dropout)")
+    close(l1, l2, 1e-3, "lse (dropout)")
+    do = bf(torch.randn(B, Nq, H * D, device=DEV))
+    g1 = _ext().attn_bwd(q, k, v, km, o1, do, l1, None, H, D, scale, p, sd, None, None, None, site=3)
+    g2 = _emu().attn_bwd(q, k, v, km, o1, do, l1, None, H, D, scale, p, sd, None, None, None, site=3)
+    for a, b, n in zip(g1, g2, ("dq", "dk", "dv")):
+        close(a, b, 3e-2, n + " (dropout)")
+
+
+@pytest.mark.parametrize("C,H", [(64, 4), (128, 4), (32, 1)])
+def test_post_attn_residual_dropout(C, H):
+    """Residual dropout in the post-attention epilogues: fwd + bwd vs the emulation with the
+    same hashed masks; p = 0 through the dropout arguments is bit-identical to no dropout."""
+    torch.manual_seed(6)
+    R, p = 200, 0.2
+    o = bf(torch.randn(R, C, device=DEV))
+    x = torch.randn(R, C, device=DEV)
+    ws = [bf(torch.randn(C, C, device=DEV) / math.sqrt(C)) for _ in range(3)]
+    bo, b1, b2 = (torch.randn(C, device=DEV) * 0.1 for _ in range(3))
+    g2, be2 = torch.randn(C, device=DEV), torch.randn(C, device=DEV)
+    sd = _seed(42)
+    a = _ext().post_attn_fwd(o, x, ws[0], bo, g2, be2, 1e-5, ws[1], b1, ws[2], b2, seed=sd, site=5, p=p)
+    b = _emu().post_attn_fwd(o, x, ws[0], bo, g2, be2, 1e-5, ws[1], b1, ws[2], b2, seed=sd, site=5, p=p)
+    for t1, t2, n in zip(a, b, ("z", "y", "mean", "rstd", "u")):
+        close(t1, t2, 2e-2, n + " (dropout)")
+    a0 = _ext().post_attn_fwd(o, x, ws[0], bo, g2, be2, 1e-5, ws[1], b1, ws[2], b2, seed=sd, site=5, p=0.0)
+    r0 = _ext().post_attn_fwd(o, x, ws[0], bo, g2, be2, 1e-5, ws[1], b1, ws[2], b2)
+    for t1, t2 in zip(a0, r0):
+        assert torch.equal(t1, t2)
+    # the attention-output residual branch really drops ≈ p of its elements
+    att = (a[1] - x).abs() < 1e-6
+    frac = att.float().mean().item()
+    assert abs(frac - p) < 0.04, frac
+    z, y, m, r, u = b
+    dz = torch.randn(R, C, device=DEV)
+    names = ("dWo", "dbo", "dg2", "dbe2", "dW1", "db1", "dW2", "db2")
+    outs = []
+    for K in (_ext(), _emu()):
+        grads = [torch.zeros((C, C) if n.startswith("dW") else (C,), device=DEV) for n in names]
+        outs.append(tuple(K.post_attn_bwd(dz, y, m, r, u, o, ws[0], ws[1], ws[2], g2, be2, H, grads, seed=sd, site=5,
+                                          p=p)) + tuple(grads))
+    for i, n in enumerate(("dy", "dO", "delta") + names):
+        close(outs[0][i], outs[1][i], 3e-2, n + " (dropout)")
 
 
 @pytest.mark.parametrize("C,H", [(64, 4), (128, 4), (32, 1)])

@@ -19,6 +19,74 @@ def _grads(m):
     return {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
 
 
+def _rel(a, b):
+    """per-tensor relative Frobenius error ‖a − b‖ / ‖b‖"""
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def _check_grads(g_hip, g_ref, tol=2e-2, floor=None):
+    """every gradient tensor within ``tol`` of ITS OWN norm (small-gradient tensors — LN
+    biases, latents, biases — are checked as strictly as the large ones).  ``floor``: per-tensor
+    bf16 rounding floor (the kernel emulation's own error vs fp32), added twice to ``tol`` —
+    a few tensors are ill-conditioned in bf16 (e.g. the decoder query-LN affine: its gradient
+    is a sum of dQ = dS·(K − K̄) over near-identical keys, where bf16 keys lose most bits)."""
+    bad = {}
+    for n, g in g_ref.items():
+        assert n in g_hip, n
+        if g.norm() == 0:
+            assert g_hip[n].norm() == 0, n
+            continue
+        e = _rel(g_hip[n], g)
+        t = tol + (2 * floor[n] if floor is not None else 0.0)
+        if e > t:
+            bad[n] = (e, t)
+    assert not bad, bad
+
+
+class _emulated:
+    """Run the fused executor on ops.emulation (fp32 maths, the kernels' bf16 rounding points
+    and dropout hash) instead of the HIP extension, on the same GPU tensors."""
+
+    def __enter__(self):
+        from perceiver_io_amd import ops
+        from perceiver_io_amd.ops import emulation, ext
+
+        self.saved = (ext._mod, ops.fused.kernels)
+        ext._mod = emulation
+        ops.fused.kernels = lambda t: emulation
+        return self
+
+    def __exit__(self, *exc):
+        from perceiver_io_amd import ops
+        from perceiver_io_amd.ops import ext
+
+        ext._mod, ops.fused.kernels = self.saved
+
+
+def _three_way(mod, run, loss_tol=1e-2, tol=2e-2):
+    """``run()`` → loss (backward inside) on: eager fp32 (reference maths), HIP kernels, and the
+    kernels' emulation.  Checks HIP vs emulation per tensor at ``tol`` (kernel correctness) and
+    HIP vs fp32 per tensor at ``tol`` + 2 × the emulation's own bf16 error (precision)."""
+    from perceiver_io_amd import ops
+
+    res = {}
+    for name in ("torch", "hip", "emu"):
+        mod.zero_grad()
+        if name == "emu":
+            with ops.backend("hip"), _emulated():
+                loss = run()
+        else:
+            with ops.backend(name):
+                loss = run()
+        res[name] = (loss.item(), _grads(mod))
+    (l0, g0), (l1, g1), (l2, g2) = res["torch"], res["hip"], res["emu"]
+    assert abs(l1 - l0) < loss_tol * abs(l0), (l0, l1)
+    assert abs(l1 - l2) < 1e-3 * abs(l2), (l1, l2)
+    floor = {n: _rel(g2[n], g) for n, g in g0.items()}
+    _check_grads(g1, g2, tol=tol, floor=floor)
+    _check_grads(g1, g0, tol=tol, floor=floor)
+
+
 def test_mlm_fused_matches_eager():
     from perceiver_io_amd import ops
 
@@ -38,12 +106,18 @@ def test_mlm_fused_matches_eager():
         l_hip = m.loss(ids, pad, labels=lab, x_masked=xm)
         l_hip.backward()
     g_hip = _grads(m)
-    assert abs(l_hip.item() - l_ref.item()) < 2e-2 * abs(l_ref.item())
-    gmax = max(g.abs().max().item() for g in g_ref.values())
-    for n, g in g_ref.items():
-        assert n in g_hip, n
-        err = (g_hip[n] - g).abs().max().item()
-        assert err < 3e-2 * gmax, (n, err, gmax)
+    m.zero_grad()
+    with ops.backend("hip"), _emulated():
+        l_emu = m.loss(ids, pad, labels=lab, x_masked=xm)
+        l_emu.backward()
+    g_emu = _grads(m)
+    assert abs(l_hip.item() - l_ref.item()) < 1e-2 * abs(l_ref.item())
+    assert abs(l_hip.item() - l_emu.item()) < 1e-3 * abs(l_emu.item())
+    # per-tensor bf16 noise floor: how far an independent bf16 implementation (the emulation)
+    # lands from fp32; the kernels must be as close to fp32 AND to the emulation
+    floor = {n: _rel(g_emu[n], g) for n, g in g_ref.items()}
+    _check_grads(g_hip, g_emu, floor=floor)
+    _check_grads(g_hip, g_ref, floor=floor)
 
 
 def test_image_classifier_fused_matches_eager():
@@ -57,18 +131,13 @@ def test_image_classifier_fused_matches_eager():
                              num_encoder_self_attention_layers_per_block=2, num_decoder_cross_attention_heads=1).cuda()
     x = torch.randn(4, 28, 28, 1, device="cuda")
     y = torch.randint(0, 10, (4,), device="cuda")
-    outs = []
-    for be in ("torch", "hip"):
-        lit.zero_grad()
-        with ops.backend(be):
-            loss, _ = lit.step((x, y))
-            loss.backward()
-        outs.append((loss.item(), _grads(lit)))
-    (l0, g0), (l1, g1) = outs
-    assert abs(l0 - l1) < 2e-2 * abs(l0)
-    gmax = max(g.abs().max().item() for g in g0.values())
-    for n, g in g0.items():
-        assert (g1[n] - g).abs().max().item() < 3e-2 * gmax, n
+
+    def run():
+        loss, _ = lit.step((x, y))
+        loss.backward()
+        return loss
+
+    _three_way(lit, run)
 
 
 def test_image_classifier_replicated_flat_grads_match_eager():
@@ -88,6 +157,12 @@ def test_image_classifier_replicated_flat_grads_match_eager():
         loss, _ = lit.step((x, y))
         loss.backward()
     g0 = _grads(lit)
+    lit.zero_grad()
+    with ops.backend("hip"), _emulated():
+        loss, _ = lit.step((x, y))
+        loss.backward()
+    floor = {n: _rel(g, g0[n]) for n, g in _grads(lit).items()}
+    lit.zero_grad()
     flat = FlatParameterSpace(lit.parameters(), replicate=True)
     assert flat.grad_rep is not None
     flat.zero_grad()
@@ -96,30 +171,141 @@ def test_image_classifier_replicated_flat_grads_match_eager():
         loss.backward()
     flat.fold()
     g1 = _grads(lit)
-    gmax = max(g.abs().max().item() for g in g0.values())
-    for n, g in g0.items():
-        assert (g1[n] - g).abs().max().item() < 3e-2 * gmax, n
+    _check_grads(g1, g0, floor=floor)
 
 
-def test_graph_engine_matches_eager_steps():
+def _fixed_mask_engine(lit, graph, ids, pad, lr=1e-3, warmup=1):
+    """StepEngine whose loss replays ONE precomputed masking (no RNG inside the step)."""
     from perceiver_io_amd.ops.optim import FusedAdamW
     from perceiver_io_amd.train.engine import StepEngine
 
+    m = lit.model
+    with torch.no_grad():
+        xm, lab = m.masking(ids, pad)
+    opt = FusedAdamW(m.parameters(), lr=lr)
+    return StepEngine(lambda b: m.loss(b[1], b[2], labels=lab, x_masked=xm), opt, device="cuda", graph=graph,
+                      warmup_eager=warmup)
+
+
+def test_graph_engine_matches_eager_steps():
+    """Replayed hipGraph steps vs eager steps from the same initial state with identical
+    inputs and masks: losses and parameters agree to fp32-atomic reordering noise."""
     torch.manual_seed(2)
     ids = torch.randint(3, 500, (4, 96), device="cuda")
     pad = torch.zeros(4, 96, dtype=torch.bool, device="cuda")
+    pad[1, 70:] = True
     states = []
     for graph in (False, True):
         torch.manual_seed(3)
         lit = _mlm()
-        opt = FusedAdamW(lit.model.parameters(), lr=1e-3)
-        gen_state = torch.cuda.get_rng_state()
-        eng = StepEngine(lambda b: lit.model.loss(b[1], b[2]), opt, device="cuda", graph=graph, warmup_eager=1)
-        torch.manual_seed(4)
-        losses = [eng.step((None, ids, pad)).item() for _ in range(4)]
+        eng = _fixed_mask_engine(lit, graph, ids, pad)
+        losses = [eng.step((None, ids, pad)).item() for _ in range(5)]
         states.append((losses, [p.detach().clone() for p in lit.model.parameters()]))
-        del gen_state
+        if graph:
+            assert eng.num_graphs == 1
     (la, pa), (lb, pb) = states
-    # masking RNG streams differ between eager and replay, so compare trajectories loosely
-    assert all(abs(a - b) < 0.5 for a, b in zip(la, lb)), (la, lb)
-    assert all(torch.isfinite(p).all() for p in pb)
+    # identical up to fp32-atomic summation order (which Adam's sign-like first steps amplify
+    # for near-zero gradient elements); the deterministic mode test pins bitwise equality
+    for a, b in zip(la, lb):
+        assert abs(a - b) <= 5e-3 * abs(a), (la, lb)
+    # per element, Adam turns pure-rounding-noise gradients (true value ≈ 0) into ±lr steps, so
+    # the parameters are compared as a whole here; bitwise per-element equality is pinned by
+    # the deterministic-mode test
+    assert _rel(torch.cat([t.reshape(-1) for t in pb]), torch.cat([t.reshape(-1) for t in pa])) < 1e-2
+
+
+def test_graph_engine_variable_shapes():
+    """One captured graph per batch shape (LRU), each replayed with its own static buffers."""
+    torch.manual_seed(5)
+    lit = _mlm(L=128)
+    from perceiver_io_amd.ops.optim import FusedAdamW
+    from perceiver_io_amd.train.engine import StepEngine
+
+    opt = FusedAdamW(lit.model.parameters(), lr=1e-3)
+    eng = StepEngine(lambda b: lit.model.loss(b[1], b[2]), opt, device="cuda", graph=True, warmup_eager=0,
+                     max_graphs=2)
+    shapes = [(4, 64), (4, 128), (4, 64), (3, 64), (4, 128)]
+    for b, L in shapes:
+        ids = torch.randint(3, 500, (b, L), device="cuda")
+        pad = torch.zeros(b, L, dtype=torch.bool, device="cuda")
+        loss = eng.step((None, ids, pad))
+        assert torch.isfinite(loss)
+    assert eng.captures == 4 and eng.num_graphs == 2  # (4,128) was evicted by (3,64) and recaptured
+
+
+def test_graph_replays_draw_fresh_dropout_masks():
+    """Dropout under graph capture: with lr = 0 the parameters never change, so consecutive
+    replays of one graph differ ONLY through the dropout masks — they must differ (device
+    seed drawn inside the graph) — while at p = 0 they are bit-identical."""
+    ids = torch.randint(3, 500, (4, 96), device="cuda")
+    pad = torch.zeros(4, 96, dtype=torch.bool, device="cuda")
+    for p in (0.0, 0.2):
+        torch.manual_seed(6)
+        lit = _mlm_dropout(p)
+        eng = _fixed_mask_engine(lit, True, ids, pad, lr=0.0, warmup=0)
+        losses = [eng.step((None, ids, pad)).item() for _ in range(4)]
+        if p == 0.0:
+            assert len(set(losses)) == 1, losses
+        else:
+            assert len(set(losses)) == 4, losses
+
+
+def _mlm_dropout(p, **kw):
+    from perceiver_io_amd.tasks import LitMaskedLanguageModel
+
+    return LitMaskedLanguageModel(vocab_size=500, max_seq_len=96,
+                                  optimizer_init={"class_path": "torch.optim.AdamW", "init_args": {"lr": 1e-3}},
+                                  num_latents=64, num_latent_channels=64, num_encoder_layers=2,
+                                  num_encoder_self_attention_layers_per_block=2, dropout=p, **kw).cuda()
+
+
+def test_dropout_fused_matches_masked_emulation_end_to_end(monkeypatch):
+    """Whole MLM encoder with dropout 0.1 on the HIP kernels vs the same executor on the
+    kernel emulation (bit-identical hashed masks, fp32 oracle maths)."""
+    from perceiver_io_amd import ops
+
+    seed = torch.tensor([123456789], dtype=torch.int64, device="cuda")
+    monkeypatch.setattr(ops.fused, "_seed", lambda p, device: seed if p > 0 else None)
+    torch.manual_seed(7)
+    lit = _mlm_dropout(0.1)
+    enc = lit.model.encoder.train()
+    ids = torch.randint(3, 500, (4, 96), device="cuda")
+    pad = torch.zeros(4, 96, dtype=torch.bool, device="cuda")
+    pad[2, 50:] = True
+    outs = []
+    for K in ("hip", "emu"):
+        enc.zero_grad()
+        if K == "emu":
+            monkeypatch.setattr(ops.fused, "kernels", lambda t: ops.emulation)
+        z = ops.fused.encoder_forward(enc, ids, pad)
+        w = torch.randn(z.shape, generator=torch.Generator(device="cuda").manual_seed(1), device="cuda")
+        (z * w).sum().backward()
+        outs.append((z.detach().clone(), _grads(enc)))
+    (z1, g1), (z2, g2) = outs
+    assert _rel(z1, z2) < 1e-2
+    _check_grads(g1, g2, tol=3e-2)
+
+
+def test_headline_shape_fused_matches_eager_fp32():
+    """The benchmark configuration itself (B = 64, L = 512, 256 × 64 latents, 3 × (1 + 6)
+    layers, vocab 10003): fused bf16 loss + gradients vs the eager fp32 path."""
+    from perceiver_io_amd import ops
+    from perceiver_io_amd.tasks import LitMaskedLanguageModel
+
+    torch.manual_seed(8)
+    lit = LitMaskedLanguageModel(vocab_size=10003, max_seq_len=512,
+                                 optimizer_init={"class_path": "torch.optim.AdamW", "init_args": {"lr": 1e-3}},
+                                 num_latents=256, num_latent_channels=64, num_encoder_layers=3,
+                                 num_encoder_self_attention_layers_per_block=6).cuda()
+    m = lit.model
+    ids = torch.randint(3, 10003, (64, 512), device="cuda")
+    pad = torch.zeros(64, 512, dtype=torch.bool, device="cuda")
+    pad[::3, 400:] = True
+    xm, lab = m.masking(ids, pad)
+
+    def run():
+        loss = m.loss(ids, pad, labels=lab, x_masked=xm)
+        loss.backward()
+        return loss
+
+    _three_way(m, run, loss_tol=5e-3)

@@ -148,6 +148,40 @@ def test_mlm_loss_matches_full_logit_reference():
     assert torch.allclose(fast, ref, atol=1e-5) and torch.allclose(fast, full, atol=1e-5)
 
 
+@pytest.mark.parametrize("mask_p", [0.5, 0.9])
+def test_mlm_loss_capacity_follows_mask_p(mask_p):
+    """Capacities derive from TextMasking.mask_p: at high masking rates every selected position
+    still reaches the loss (no silent truncation), and the persistent overflow flag stays clear."""
+    from perceiver_io_amd.ops import mlm_head
+
+    torch.manual_seed(5)
+    m = mlm_model()
+    m.masking.mask_p = mask_p
+    x = torch.randint(3, 300, (4, 64))
+    pad = torch.zeros(4, 64, dtype=torch.bool)
+    pad[2, 50:] = True
+    xm, lab = m.masking(x, pad)
+    assert (lab != -100).float().mean() > 0.6 * mask_p
+    mlm_head.check_overflow(reset=True)
+    fast = m.loss(x, pad, labels=lab, x_masked=xm)
+    logits, _ = m(xm, pad, masking=False)
+    full = torch.nn.functional.cross_entropy(logits.transpose(1, 2), lab, ignore_index=-100)
+    assert torch.allclose(fast, full, atol=1e-5)
+    assert mlm_head.check_overflow() is False
+
+
+def test_mlm_capacity_overflow_fails_loudly():
+    from perceiver_io_amd.ops import mlm_head
+
+    mlm_head.check_overflow(reset=True)
+    labels = torch.full((2, 32), -100, dtype=torch.long)
+    labels[:, :20] = 7  # 40 selected positions
+    mlm_head.compact_rows(labels, 16)
+    with pytest.raises(RuntimeError, match="capacity"):
+        mlm_head.check_overflow(reset=True)
+    assert mlm_head.check_overflow() is False  # reset cleared it
+
+
 def test_reference_backend_matches_nn_multihead_attention():
     torch.manual_seed(2)
     from perceiver_io_amd.models.blocks import MultiHeadAttention

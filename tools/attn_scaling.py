@@ -18,12 +18,12 @@ def main():
         qkv = torch.randn(B, N, 3 * C, device="cuda").to(torch.bfloat16)
         q, k, v = qkv[:, :, :C], qkv[:, :, C:2 * C], qkv[:, :, 2 * C:]
         sc = 1 / math.sqrt(D)
-        tf = timeit(lambda: K.attn_fwd(q, k, v, None, H, D, sc, 0.0, 0, 1), iters=100)
-        o, lse = K.attn_fwd(q, k, v, None, H, D, sc, 0.0, 0, 1)
+        tf = timeit(lambda: K.attn_fwd(q, k, v, None, H, D, sc, 0.0, None, 1), iters=100)
+        o, lse = K.attn_fwd(q, k, v, None, H, D, sc, 0.0, None, 1)
         do = torch.randn(B, N, C, device="cuda").to(torch.bfloat16)
         delta = (do.float() * o.float()).view(B, N, H, D).sum(-1).contiguous()
         d = torch.empty(B, N, 3 * C, device="cuda")
-        tb = timeit(lambda: K.attn_bwd(q, k, v, None, o, do, lse, delta, H, D, sc, 0.0, 0, d[:, :, :C], d[:, :, C:2 * C],
+        tb = timeit(lambda: K.attn_bwd(q, k, v, None, o, do, lse, delta, H, D, sc, 0.0, None, d[:, :, :C], d[:, :, C:2 * C],
                                        d[:, :, 2 * C:]), iters=100)
         print(f"B={B:4d}  fwd {tf:8.2f} us   bwd {tb:8.2f} us")
 

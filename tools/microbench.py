@@ -43,8 +43,8 @@ def main():
     qkv, mean, rstd = K.ln_linear_fwd(x, g1, b1, 1e-5, wqkv, bqkv, 0, None, True, True)
     q3 = qkv.view(B, N, 3 * C)
     q, k, v = q3[:, :, :C], q3[:, :, C:2 * C], q3[:, :, 2 * C:]
-    res["attn_fwd self"] = timeit(lambda: K.attn_fwd(q, k, v, None, H, D, 1 / math.sqrt(D), 0.0, 0, 1))
-    o, lse = K.attn_fwd(q, k, v, None, H, D, 1 / math.sqrt(D), 0.0, 0, 1)
+    res["attn_fwd self"] = timeit(lambda: K.attn_fwd(q, k, v, None, H, D, 1 / math.sqrt(D), 0.0, None, 1))
+    o, lse = K.attn_fwd(q, k, v, None, H, D, 1 / math.sqrt(D), 0.0, None, 1)
     ws = [(torch.randn(C, C, device=dev) / 8).to(bf) for _ in range(3)]
     bs = [torch.randn(C, device=dev) for _ in range(3)]
     g2, be2 = torch.randn(C, device=dev), torch.randn(C, device=dev)
@@ -57,7 +57,7 @@ def main():
     dy, do, delta = K.post_attn_bwd(dz, y, m2, r2, u, o2, ws[0], ws[1], ws[2], g2, be2, H, grads)
     dqkv = torch.empty(B, N, 3 * C, device=dev)
     res["attn_bwd self"] = timeit(lambda: K.attn_bwd(q, k, v, None, o, do.view(B, N, C), lse, delta.view(B, N, H), H, D,
-                                                     1 / math.sqrt(D), 0.0, 0, dqkv[:, :, :C], dqkv[:, :, C:2 * C],
+                                                     1 / math.sqrt(D), 0.0, None, dqkv[:, :, :C], dqkv[:, :, C:2 * C],
                                                      dqkv[:, :, 2 * C:]))
     dg, db_ = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
     dW, dbias = torch.zeros(3 * C, C, device=dev), torch.zeros(3 * C, device=dev)

@@ -42,8 +42,8 @@ def main():
         qkv, mean, rstd = K.ln_linear_fwd(x, g1, b1, 1e-5, wqkv, bqkv, 0, None, True, True)
         q3 = qkv.view(B, N, 3 * C)
         q, k, v = q3[:, :, :C], q3[:, :, C:2 * C], q3[:, :, 2 * C:]
-        rows.setdefault("attn_fwd", []).append(timeit(lambda: K.attn_fwd(q, k, v, None, H, D, 1 / math.sqrt(D), 0.0, 0, 1)))
-        o, lse = K.attn_fwd(q, k, v, None, H, D, 1 / math.sqrt(D), 0.0, 0, 1)
+        rows.setdefault("attn_fwd", []).append(timeit(lambda: K.attn_fwd(q, k, v, None, H, D, 1 / math.sqrt(D), 0.0, None, 1)))
+        o, lse = K.attn_fwd(q, k, v, None, H, D, 1 / math.sqrt(D), 0.0, None, 1)
         ws = [(torch.randn(C, C, device=dev) / 8).to(bf) for _ in range(3)]
         bs = [torch.randn(C, device=dev) for _ in range(3)]
         g2, be2 = torch.randn(C, device=dev), torch.randn(C, device=dev)
@@ -63,7 +63,7 @@ def main():
         dqkv = torch.empty(B, N, 3 * C, device=dev)
         rows.setdefault("attn_bwd", []).append(
             timeit(lambda: K.attn_bwd(q, k, v, None, o, do.view(B, N, C), lse, delta.view(B, N, H), H, D,
-                                      1 / math.sqrt(D), 0.0, 0, dqkv[:, :, :C], dqkv[:, :, C:2 * C], dqkv[:, :, 2 * C:])))
+                                      1 / math.sqrt(D), 0.0, None, dqkv[:, :, :C], dqkv[:, :, C:2 * C], dqkv[:, :, 2 * C:])))
         ll_sizes = [C, C, 3 * C * C, 3 * C]
         ll_offs = [sum(ll_sizes[:i]) for i in range(4)]
         ll_slab = torch.empty(nt, sum(ll_sizes), device=dev)
