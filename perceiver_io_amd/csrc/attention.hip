@@ -35,28 +35,6 @@ namespace pio {
 
 constexpr int KT = 64;  // keys per forward tile
 
-// A-operand read of V^T / dO^T / Q^T from an LDS tile stored [k][i] with the k order
-// permuted to match an accumulator used as the other operand (see common.h).
-__device__ __forceinline__ bf16x8 frag_ks_perm(const uint16_t* lds, int ld, int i0, int k0) {
-  const int l = lane_id();
-  const int g = l >> 4, i = l & 15, q = i >> 2, p = i & 3;
-  const uint16_t* base = lds + (k0 + 4 * (g >> 1) + q) * ld + i0 + 16 * (g & 1) + 4 * p;
-  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(base));
-  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(base + 8 * ld));
-  bf16x8 r;
-  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
-  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
-  return r;
-}
-
-// pack accumulator registers 8s..8s+7 to a bf16 operand fragment
-__device__ __forceinline__ bf16x8 pack_acc(const f32x16& a, int s) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (short)f2bf(a[8 * s + j]);
-  return r;
-}
-
 struct AttnArgs {
   const uint16_t* q; long long q_bs; int q_rs;
   const uint16_t* k; long long k_bs; int k_rs;

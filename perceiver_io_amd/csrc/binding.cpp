@@ -91,6 +91,23 @@ void slab_reduce_launch(const SlabJob&, hipStream_t);
 void pe_proj_fwd_launch(const float*, int, const float*, const float*, const float*, const float*, const float*,
                         const float*, long long, int, int, int, float, uint16_t*, float*, float*, hipStream_t);
 int pe_proj_bwd_blocks(int);
+struct PeBwdArgs {  // attention_pe.hip
+  const uint16_t* q; long long q_bs; int q_rs;
+  const uint16_t* kv; int kv_rs;
+  const uint16_t* dO;
+  const float* lse;
+  const float* delta;
+  const float* mean; const float* rstd;
+  const float* pix;
+  float* dq;
+  float* D;
+  float* part;
+  int B, H, Nq, M, C, nc, bper;
+  float scale, scale_log2;
+  int accumulate;
+  int d_atomic;
+};
+void attn_bwd_pe_launch(const PeBwdArgs&, int, int, hipStream_t);
 void pe_proj_bwd_launch(const float*, const float*, int, const float*, const float*, int, int, int, float*, float*,
                         hipStream_t);
 }  // namespace pio
@@ -712,6 +729,55 @@ std::vector<Tensor> pe_proj_bwd(Tensor dy, Tensor pix, Tensor mean, Tensor rstd,
   return {D, part};
 }
 
+// encoder cross-attention backward fused with the factored K/V-projection reductions
+// (attention_pe.hip): queries (1 | B, Nq ≤ 32, ·), head dim 32, no key mask, no dropout.
+// Writes dq (zeroed here) — (Nq, C) summed over the batch for broadcast queries, else (B, Nq, C)
+// — and D (M, 2C), part (nkb·bsplit, (2 + nc)·2C), both added onto when accumulate.
+void attn_bwd_pe(Tensor q, Tensor kv, Tensor dO, Tensor lse, Tensor delta, Tensor mean, Tensor rstd, Tensor pix,
+                 Tensor dq, Tensor D, Tensor part, int64_t H, double scale, bool accumulate, int64_t bsplit) {
+  for (const Tensor* t : {&q, &kv, &dO, &lse, &delta, &mean, &rstd, &pix, &dq, &D, &part}) CHECK_CUDA(*t);
+  const int C = (int)(H * 32);
+  TORCH_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.size(2) >= C, "q must be (B|1, Nq, >= C) with unit inner stride");
+  const int Nq = (int)q.size(1);
+  TORCH_CHECK(Nq >= 1 && Nq <= 32, "attn_bwd_pe: at most 32 queries");
+  TORCH_CHECK(dO.dim() == 3 && dO.is_contiguous() && dO.size(1) == Nq && dO.size(2) == C, "dO must be (B, Nq, C)");
+  const int B = (int)dO.size(0);
+  TORCH_CHECK(q.size(0) == 1 || q.size(0) == B, "q batch must be 1 (broadcast) or B");
+  const bool qb = q.size(0) == B && B > 1;
+  TORCH_CHECK(kv.dim() == 2 && kv.stride(1) == 1 && kv.size(1) >= 2 * C && kv.size(0) % B == 0,
+              "kv must be (B*M, >= 2C) rows");
+  const int M = (int)(kv.size(0) / B);
+  TORCH_CHECK(kv.stride(0) % 8 == 0 && q.stride(1) % 8 == 0 && (!qb || q.stride(0) % 8 == 0) &&
+                  reinterpret_cast<uintptr_t>(kv.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(q.data_ptr()) % 16 == 0,
+              "attn_bwd_pe: 16-byte aligned rows");
+  TORCH_CHECK(pix.dim() == 2 && pix.is_contiguous() && pix.size(0) == (int64_t)B * M && pix.size(1) >= 1 && pix.size(1) <= 4,
+              "pix must be (B*M, nc <= 4)");
+  const int nc = (int)pix.size(1);
+  TORCH_CHECK(mean.numel() == (int64_t)B * M && rstd.numel() == (int64_t)B * M && mean.is_contiguous() && rstd.is_contiguous(),
+              "row statistics must be (B*M)");
+  TORCH_CHECK(lse.is_contiguous() && delta.is_contiguous() && lse.numel() == (int64_t)B * Nq * H && delta.numel() == lse.numel(),
+              "lse / delta must be (B, Nq, H)");
+  TORCH_CHECK(dq.is_contiguous() && dq.numel() == (int64_t)(qb ? B : 1) * Nq * C,
+              "dq must be (Nq, C) for broadcast queries (Σ over the batch), else (B, Nq, C)");
+  TORCH_CHECK(D.is_contiguous() && D.size(0) == M && D.size(1) == 2 * C, "D must be (M, 2C) contiguous");
+  const int nkb = (M + 255) / 256;
+  TORCH_CHECK(bsplit >= 1 && bsplit <= B, "bsplit in [1, B]");
+  TORCH_CHECK(part.is_contiguous() && part.size(0) == (int64_t)nkb * bsplit && part.size(1) == (int64_t)(2 + nc) * 2 * C,
+              "part must be (ceil(M/256)*bsplit, (2+nc)*2C)");
+  for (const Tensor* t : {&lse, &delta, &mean, &rstd, &pix, &dq, &D, &part}) CHECK_DT(*t, torch::kFloat32);
+  dq.zero_();
+  pio::PeBwdArgs a{};
+  a.q = bfp(q); a.q_bs = qb ? q.stride(0) : 0; a.q_rs = (int)q.stride(1);
+  a.kv = bfp(kv); a.kv_rs = (int)kv.stride(0);
+  a.dO = bfp(dO); a.lse = f32p(lse); a.delta = f32p(delta); a.mean = f32p(mean); a.rstd = f32p(rstd); a.pix = f32p(pix);
+  a.dq = dq.data_ptr<float>(); a.D = D.data_ptr<float>(); a.part = part.data_ptr<float>();
+  a.B = B; a.H = (int)H; a.Nq = Nq; a.M = M; a.C = C; a.nc = nc;
+  a.scale = (float)scale; a.scale_log2 = (float)(scale * 1.4426950408889634);
+  a.accumulate = accumulate ? 1 : 0;
+  if (bsplit > 1 && !accumulate) D.zero_();  // atomics add onto it
+  pio::attn_bwd_pe_launch(a, nkb, (int)bsplit, stream());
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "Perceiver IO CDNA4 (gfx950) kernels";
   m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("kmask"), py::arg("H"), py::arg("D"),
@@ -766,5 +832,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("slab_reduce", &slab_reduce);
   m.def("pe_proj_fwd", &pe_proj_fwd);
   m.def("pe_proj_bwd", &pe_proj_bwd);
+  m.def("attn_bwd_pe", &attn_bwd_pe, py::arg("q"), py::arg("kv"), py::arg("dO"), py::arg("lse"), py::arg("delta"),
+        py::arg("mean"), py::arg("rstd"), py::arg("pix"), py::arg("dq"), py::arg("D"), py::arg("part"), py::arg("H"),
+        py::arg("scale"), py::arg("accumulate"), py::arg("bsplit"));
   m.attr("arch") = "gfx950";
 }

@@ -130,6 +130,30 @@ def pe_proj_bwd(dy, pix, mean, rstd, M):
     return [D, part[None]]
 
 
+def attn_bwd_pe(q, kv, dO, lse, delta, mean, rstd, pix, dq, D, part, H, scale, accumulate, bsplit):
+    """csrc/attention_pe.hip: encoder cross-attention backward whose dK/dV are folded into the
+    factored projection's reductions D = Σ_b dY·rσ and [Σ dY | Σ dY·μ·rσ | Σ dY·x̂_c] (one
+    partial row here; the kernel writes one per (key block, batch group)).  q is batch-broadcast
+    (1, Nq, C) and dq (Nq, C) receives the gradient summed over the batch."""
+    C = H * 32
+    B = dO.shape[0]
+    M = kv.shape[0] // B
+    kv3 = kv.view(B, M, -1)
+    g = attn_bwd(q, kv3[:, :, :C], kv3[:, :, C:2 * C], None, None, dO, lse, delta, H, 32, scale, 0.0, None, None,
+                 None, None)
+    dq.copy_((g[0].sum(0) if q.shape[0] == 1 else g[0]).reshape(dq.shape))
+    dy = torch.cat([g[1], g[2]], -1).reshape(B * M, 2 * C)
+    Dn, pn = pe_proj_bwd(dy, pix, mean, rstd, M)
+    full = torch.zeros_like(part)
+    full[0] = pn[0]
+    if accumulate:
+        D += Dn
+        part += full
+    else:
+        D.copy_(Dn)
+        part.copy_(full)
+
+
 _SLAB = [False]
 
 
@@ -205,8 +229,11 @@ def attn_bwd(q, k, v, kmask, o, dO, lse, delta_in, H, D, scale, dropout_p, seed,
     p = torch.exp2(s * LOG2E - l2[..., None])
     p = torch.nan_to_num(p, nan=0.0)
     dof = dO.float().reshape(B, -1, H, D).permute(0, 2, 1, 3)
-    of = o.float().reshape(B, -1, H, D).permute(0, 2, 1, 3)
-    delta = (dof * of).sum(-1, keepdim=True)
+    if delta_in is not None:  # rowsum(dO∘O) from the post-attention backward
+        delta = delta_in.float().reshape(B, -1, H).permute(0, 2, 1)[..., None]
+    else:
+        of = o.float().reshape(B, -1, H, D).permute(0, 2, 1, 3)
+        delta = (dof * of).sum(-1, keepdim=True)
     dp = torch.matmul(dof, vf.transpose(-1, -2))
     if dropout_p > 0:
         m = attn_drop_mask(seed, site, B, H, q.shape[1], k.shape[1], dropout_p, q.device)

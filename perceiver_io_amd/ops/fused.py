@@ -306,11 +306,29 @@ def _mm_tn_split(a, b):
 
 
 def _pe_proj_bwd(K, dy, pix, mean, rstd, pe, g, b, W, M):
-    """Gradients of _pe_proj_fwd w.r.t. W, bias, g, b from one streaming pass over dy (B·M, O):
-    G[o,c] = Σ dY_o·x̂_c (pixel channels from the kernel, PE channels = E_cᵀ·D − e),
-    dW = G⊙γ + S⊗β, db = S, dγ = Σ_o W⊙G, dβ = Wᵀ·S."""
-    nc, kin, O = pix.shape[1], g.shape[0], dy.shape[1]
+    """Gradients of _pe_proj_fwd w.r.t. W, bias, g, b from one streaming pass over dy (B·M, O)."""
     D, part = K.pe_proj_bwd(dy, pix, mean, rstd, M)
+    return _pe_proj_grads(D, part, pix.shape[1], pe, g, b, W)
+
+
+# the encoder cross-attention backward folds dK/dV straight into the factored projection's
+# reductions (csrc/attention_pe.hip): no fp32 (B·M, 2C) dK/dV tensor.  PERCEIVER_PE_ATTN_FUSED=0
+# restores attn_bwd + pe_proj_bwd.
+PE_ATTN_FUSED = os.environ.get("PERCEIVER_PE_ATTN_FUSED", "1") != "0"
+
+
+def pe_attn_bsplit(B: int, M: int, H: int) -> int:
+    """Batch groups of the fused PE attention backward: ≥ 512 workgroups when the image is small."""
+    nkb = (M + 255) // 256
+    return max(1, min(B, -(-512 // (nkb * H))))
+
+
+def _pe_proj_grads(D, part, nc, pe, g, b, W):
+    """W, bias, g, b gradients of the factored projection from its reductions
+    D[m,o] = Σ_b dY·rσ and part rows [Σ dY | Σ dY·μ·rσ | Σ dY·x̂_c]:
+    G[o,c] = Σ dY_o·x̂_c (pixel channels from the partials, PE channels = E_cᵀ·D − e),
+    dW = G⊙γ + S⊗β, db = S, dγ = Σ_o W⊙G, dβ = Wᵀ·S."""
+    kin, O = g.shape[0], D.shape[1]
     tot = part.sum(0)
     S, e, Gp = tot[:O], tot[O:2 * O], tot[2 * O:].view(nc, O)
     Ge = _mm_tn_split(pe, D)[nc:kin] - e[None, :]
@@ -456,17 +474,34 @@ class _LayerFn(torch.autograd.Function):
             M = kv.shape[0] // B
             kv3 = kv.view(B, M, 2 * C)
             ent = ctx.kv_entry
-            # dK/dV of every application of this layer land in one buffer (K-06); the first
-            # writer stores, later ones accumulate
-            acc = ent["dkv"] is not None
-            if not acc:
-                ent["dkv"] = torch.empty((B, M, 2 * C), **f32)
-            dkv = ent["dkv"]
-            dq, _, _ = K.attn_bwd(qx, kv3[:, :, :C], kv3[:, :, C:], kmask, o, do.view(B, Nq, C), lse, delta3, H, D,
-                                  scale, ctx.p_attn, ctx.seed, None, dkv[:, :, :C], dkv[:, :, C:], acc)
-            dq2, dres = dq.reshape(B * Nq, C), dy
+            pe_fused = (ent.get("factored") and PE_ATTN_FUSED and D == 32 and Nq <= 32 and kmask is None
+                        and ctx.p_attn == 0.0 and xkv2.shape[1] <= 4)
+            if pe_fused:
+                # dK/dV folded into the factored projection's reductions (D, partials), which every
+                # application of this layer accumulates (attention_pe.hip): no dK/dV tensor
+                acc = ent.get("pe_D") is not None
+                if not acc:
+                    bs = pe_attn_bsplit(B, M, H)
+                    ent["pe_D"] = torch.empty((M, 2 * C), **f32)
+                    ent["pe_part"] = torch.empty((((M + 255) // 256) * bs, (2 + xkv2.shape[1]) * 2 * C), **f32)
+                    ent["pe_bsplit"] = bs
+                # broadcast latent queries (layer_1): dq comes back summed over the batch
+                dq = torch.empty((Bq, Nq, C), **f32)
+                K.attn_bwd_pe(qx, kv, do.view(B, Nq, C), lse, delta3, mean_kv, rstd_kv, xkv2, dq, ent["pe_D"],
+                              ent["pe_part"], H, scale, acc, ent["pe_bsplit"])
+            else:
+                # dK/dV of every application of this layer land in one buffer (K-06); the first
+                # writer stores, later ones accumulate
+                acc = ent["dkv"] is not None
+                if not acc:
+                    ent["dkv"] = torch.empty((B, M, 2 * C), **f32)
+                dkv = ent["dkv"]
+                dq, _, _ = K.attn_bwd(qx, kv3[:, :, :C], kv3[:, :, C:], kmask, o, do.view(B, Nq, C), lse, delta3, H,
+                                      D, scale, ctx.p_attn, ctx.seed, None, dkv[:, :, :C], dkv[:, :, C:], acc)
             if Bq == 1 and B > 1:
                 dq2, dres = dq.sum(0), dy.view(B, Nq, C).sum(0)
+            else:
+                dq2, dres = dq.reshape(B * Nq, C), dy
             Ckv = g_kv.shape[0]
             Rq = dq2.shape[0]
             if WGRAD_SLAB and Rq < TALL_ROWS:
@@ -480,11 +515,18 @@ class _LayerFn(torch.autograd.Function):
                                        rows(gb(bin_), 0, C, 1))
             dx_kv = None
             if ctx.kv_owner:  # the projection's backward, once, over the summed dK/dV
-                dkv2 = dkv.view(B * M, 2 * C)
-                Rkv = dkv2.shape[0]
+                if ent.get("pe_D") is not None:
+                    dkv2, Rkv = None, B * M
+                else:
+                    dkv2 = dkv.view(B * M, 2 * C)
+                    Rkv = dkv2.shape[0]
                 if ent.get("factored"):
-                    dW, db, dg, dbeta = _pe_proj_bwd(K, dkv2, xkv2, mean_kv, rstd_kv, ctx.kv_pe, g_kv, b_kv,
-                                                     torch.cat([ps[5], ps[6]], 0), M)
+                    Wkv = torch.cat([ps[5], ps[6]], 0)
+                    if ent.get("pe_D") is not None:
+                        dW, db, dg, dbeta = _pe_proj_grads(ent["pe_D"], ent["pe_part"], xkv2.shape[1], ctx.kv_pe,
+                                                           g_kv, b_kv, Wkv)
+                    else:
+                        dW, db, dg, dbeta = _pe_proj_bwd(K, dkv2, xkv2, mean_kv, rstd_kv, ctx.kv_pe, g_kv, b_kv, Wkv, M)
 
                     def add(t, v):
                         (t[0] if rep_mode else t).view(-1).add_(v.reshape(-1))
@@ -516,7 +558,7 @@ class _LayerFn(torch.autograd.Function):
                     if not spec.packed:
                         gb(ps[5]).add_(rows(gwkv, 0, C, Ckv))
                         gb(ps[6]).add_(rows(gwkv, C, 2 * C, Ckv))
-                ent["dkv"] = None
+                ent["dkv"] = ent["pe_D"] = ent["pe_part"] = None
             dx_q = dx_q.view(Bq, Nq, C)
             dx_kv = dx_kv.view(B, M, -1) if (ctx.kv_grad and dx_kv is not None) else None
         else:

@@ -440,3 +440,42 @@ def test_factored_pe_projection_kernels(channels, B, M, O):
     from test_models import check_factored_pe_projection
 
     check_factored_pe_projection(_ext(), "cuda", channels, B=B, M=M, O=O)
+
+
+@pytest.mark.parametrize("B,Bq,Nq,M,H,nc,bsplit", [
+    (3, 1, 32, 600, 4, 3, 1),
+    (4, 1, 17, 300, 4, 1, 2),
+    (2, 1, 32, 50176, 4, 3, 1),
+    (8, 1, 32, 784, 2, 4, 8),
+    (3, 3, 32, 600, 4, 3, 1),
+    (2, 2, 32, 50176, 4, 3, 1),
+    (8, 8, 20, 784, 4, 1, 4),
+])
+def test_attention_bwd_pe_fused(B, Bq, Nq, M, H, nc, bsplit):
+    """Cross-attention backward folded into the factored projection's reductions
+    (attention_pe.hip) vs the emulation (attn_bwd → pe_proj_bwd), incl. a second accumulating
+    application (weight-shared layer_n) and batch groups (atomics on D)."""
+    torch.manual_seed(9)
+    C = 32 * H
+    q = bf(torch.randn(Bq, Nq, 3 * C, device=DEV))[:, :, :C]
+    kv = bf(torch.randn(B * M, 2 * C, device=DEV))
+    dO = bf(torch.randn(B, Nq, C, device=DEV))
+    scale = 1 / math.sqrt(32)
+    kv3 = kv.view(B, M, 2 * C)
+    o, lse = _emu().attn_fwd(q, kv3[:, :, :C], kv3[:, :, C:], None, H, 32, scale, 0.0, None, 1)
+    delta = (dO.float().view(B, Nq, H, 32) * o.float().view(B, Nq, H, 32)).sum(-1).contiguous()
+    pix = torch.randn(B * M, nc, device=DEV)
+    mean = torch.randn(B * M, device=DEV) * 0.1
+    rstd = torch.rand(B * M, device=DEV) + 0.5
+    nkb = (M + 255) // 256
+    res = []
+    for K in (_ext(), _emu()):
+        dq = torch.empty(Bq, Nq, C, device=DEV)
+        D = torch.empty(M, 2 * C, device=DEV)
+        part = torch.empty(nkb * bsplit, (2 + nc) * 2 * C, device=DEV)
+        K.attn_bwd_pe(q, kv, dO, lse, delta, mean, rstd, pix, dq, D, part, H, scale, False, bsplit)
+        dq1 = dq.clone()
+        K.attn_bwd_pe(q, kv, dO, lse, delta, mean, rstd, pix, dq, D, part, H, scale, True, bsplit)
+        res.append((dq1, dq, D, part.sum(0)))
+    for a, b, n in zip(res[0], res[1], ("dq", "dq (2nd)", "D (2 applications)", "partials")):
+        close(a, b, 2e-2, n)

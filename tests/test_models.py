@@ -199,7 +199,7 @@ def test_reference_backend_matches_nn_multihead_attention():
 
 
 @pytest.mark.parametrize("slab", [True, False])
-@pytest.mark.parametrize("kind", ["mlm", "image"])
+@pytest.mark.parametrize("kind", ["mlm", "image", "image128"])
 def test_fused_executor_matches_eager_via_emulation(kind, slab, monkeypatch):
     monkeypatch.setattr(ops.fused, "WGRAD_SLAB", slab)
     torch.manual_seed(3)
@@ -208,6 +208,11 @@ def test_fused_executor_matches_eager_via_emulation(kind, slab, monkeypatch):
         x = torch.randint(3, 300, (3, 64))
         pad = torch.zeros(3, 64, dtype=torch.bool)
         pad[2, 30:] = True
+        enc = m.encoder
+    elif kind == "image128":  # head dim 32: cross-attention bwd fused into the PE reductions
+        m = mnist_model(latents=16, c=128, layers=3, sa=1)
+        x = torch.randn(2, 28, 28, 1)
+        pad = None
         enc = m.encoder
     else:
         m = mnist_model(latents=16, c=64, layers=2, sa=1)
