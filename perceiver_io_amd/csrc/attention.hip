@@ -328,7 +328,8 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
                                                            const float* __restrict__ delta, float* __restrict__ dq,
                                                            long long dq_bs, int dq_rs, float* __restrict__ dk,
                                                            long long dk_bs, int dk_rs, float* __restrict__ dv,
-                                                           long long dv_bs, int dv_rs, int dq_atomic, int kv_acc) {
+                                                           long long dv_bs, int dv_rs, int dq_atomic, int kv_acc,
+                                                           long long dq_kbs) {
   constexpr int LD = (D < 32 ? 32 : D) + 8;  // Q / dO / K tiles [row][d] (D=16 zero-padded to 32 cols)
   constexpr int NT = (D < 32) ? 1 : D / 32;
   constexpr int KS = D / 16;
@@ -355,6 +356,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
   const Blk3 blk = xcd_block3();  // the heads / key blocks of one batch element share an L2
   const int h = blk.y, b = blk.z;
   const int kbase = blk.x * KB;
+  dq += (long long)blk.x * dq_kbs;  // deterministic mode: one dQ partial slice per key block
   const int key = kbase + 32 * w + r;  // this lane's key (column of S / dP)
   const int kc = key < a.Nk ? key : a.Nk - 1;
   const uint32_t dkey = a.drop_thresh ? drop_key(a.seedp, a.site, 2u) : 0u;
@@ -668,9 +670,12 @@ static bool getenv_flag(const char* name) {
 template <int D, int NW>
 static void bwd_launch_t(const AttnArgs& a, const uint16_t* dO, const float* LSE, float* delta, float* dq,
                          long long dq_bs, int dq_rs, float* dk, long long dk_bs, int dk_rs, float* dv, long long dv_bs,
-                         int dv_rs, int kv_acc, hipStream_t st) {
+                         int dv_rs, int kv_acc, long long dq_kbs, hipStream_t st) {
   const int nkb = (a.Nk + 32 * NW - 1) / (32 * NW);
-  if (nkb > 1) {  // several key blocks accumulate into dQ
+  // several key blocks add into dQ (fp32 atomics), unless each stores its own partial slice
+  // (deterministic mode: dq_kbs > 0, summed by the caller)
+  const int atomic = nkb > 1 && dq_kbs == 0;
+  if (atomic) {
     const long long total = (long long)a.B * a.Nq * a.H * D;
     hipLaunchKernelGGL(zero_rows_kernel, dim3((unsigned)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096)), dim3(256), 0,
                        st, dq, dq_bs, dq_rs, a.Nq, a.H * D, total);
@@ -679,18 +684,24 @@ static void bwd_launch_t(const AttnArgs& a, const uint16_t* dO, const float* LSE
   const bool small_lds = !getenv_flag("PIO_ATTN_BWD_FULL_LDS");
   if (a.Nq <= 32 && small_lds)
     hipLaunchKernelGGL((attn_bwd_kernel<D, NW, 1>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs,
-                       dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, nkb > 1 ? 1 : 0, kv_acc);
+                       dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs);
   else if (a.Nq <= 64 && small_lds)
     hipLaunchKernelGGL((attn_bwd_kernel<D, NW, 2>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs,
-                       dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, nkb > 1 ? 1 : 0, kv_acc);
+                       dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs);
   else
     hipLaunchKernelGGL((attn_bwd_kernel<D, NW>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs, dk,
-                       dk_bs, dk_rs, dv, dv_bs, dv_rs, nkb > 1 ? 1 : 0, kv_acc);
+                       dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs);
+}
+
+// key blocks of the backward grid (dQ partial slices in deterministic mode)
+int attn_bwd_key_blocks(int Nk, int D) {
+  const int nw = D <= 32 ? 8 : 4;
+  return (Nk + 32 * nw - 1) / (32 * nw);
 }
 
 void attn_bwd_launch(const AttnArgs& a, int D, const uint16_t* O, const uint16_t* dO, const float* LSE, float* delta,
                      float* dq, long long dq_bs, int dq_rs, float* dk, long long dk_bs, int dk_rs, float* dv,
-                     long long dv_bs, int dv_rs, bool compute_delta, bool kv_acc, hipStream_t st) {
+                     long long dv_bs, int dv_rs, bool compute_delta, bool kv_acc, long long dq_kbs, hipStream_t st) {
   // delta = rowsum(dO∘O) is normally produced by the post-attention backward kernel;
   // compute it here otherwise.  dQ needs no zero fill from the caller.
   const int rows = a.B * a.Nq;
@@ -698,10 +709,10 @@ void attn_bwd_launch(const AttnArgs& a, int D, const uint16_t* O, const uint16_t
     hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, dO, O, delta, (float*)nullptr,
                        rows, a.H, D, dq_rs);
   switch (D) {  // waves per workgroup: 8 for d ≤ 32, 4 above (keys per block = 32 × waves)
-    case 16: bwd_launch_t<16, 8>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, st); break;
-    case 32: bwd_launch_t<32, 8>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, st); break;
-    case 64: bwd_launch_t<64, 4>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, st); break;
-    case 128: bwd_launch_t<128, 4>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, st); break;
+    case 16: bwd_launch_t<16, 8>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, st); break;
+    case 32: bwd_launch_t<32, 8>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, st); break;
+    case 64: bwd_launch_t<64, 4>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, st); break;
+    case 128: bwd_launch_t<128, 4>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, st); break;
     default: break;
   }
 }

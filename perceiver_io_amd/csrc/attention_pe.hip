@@ -49,6 +49,7 @@ struct PeBwdArgs {
   float scale, scale_log2;
   int accumulate;  // add onto D / part (a later application of the weight-shared layer)
   int d_atomic;    // batch split over several workgroups: D by atomics
+  long long dq_kbs;  // deterministic mode: dq slice per key block (plain stores, summed by the caller)
 };
 
 constexpr int PD = 32;          // head dim
@@ -266,10 +267,14 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
         f32x4 v = *reinterpret_cast<const f32x4*>(&sDQb[0][dd * 36 + q0]);
 #pragma unroll
         for (int ww = 1; ww < NW; ++ww) v += *reinterpret_cast<const f32x4*>(&sDQb[ww][dd * 36 + q0]);
-        float* dst = a.dq + ((long long)b * a.Nq) * C + h * PD + dd;
+        float* dst = a.dq + (long long)kb * a.dq_kbs + ((long long)b * a.Nq) * C + h * PD + dd;
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (q0 + e < a.Nq) atomicAdd(dst + (long long)(q0 + e) * C, v[e] * a.scale);
+        for (int e = 0; e < 4; ++e) {
+          if (q0 + e < a.Nq) {
+            if (a.dq_kbs) dst[(long long)(q0 + e) * C] = v[e] * a.scale;
+            else atomicAdd(dst + (long long)(q0 + e) * C, v[e] * a.scale);
+          }
+        }
       }
     } else {
       accQ = mfma32(frag_ks(tS, PLD, 0, 0), frag_ks(tKV, KVLD, 0, 0), accQ);
@@ -314,7 +319,11 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
     float v = 0.f;
 #pragma unroll
     for (int ww = 0; ww < NW; ++ww) v += sDQ[ww][qq * 33 + dd];
-    if (qq < a.Nq) atomicAdd(a.dq + (long long)qq * C + h * PD + dd, v * a.scale);
+    if (qq < a.Nq) {
+      float* dst = a.dq + (long long)kb * a.dq_kbs + (long long)qq * C + h * PD + dd;
+      if (a.dq_kbs) *dst = v * a.scale;
+      else atomicAdd(dst, v * a.scale);
+    }
   }
   const long long prow = (long long)blockIdx.x * gridDim.z + blockIdx.z;
   const int nseg = 2 + nc;

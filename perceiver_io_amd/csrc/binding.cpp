@@ -31,6 +31,7 @@ constexpr int kMaxSlabSegs = 16, kSlabRowsPerBlock = 32;  // common.h
 struct SlabJob {
   const float* slab;
   int S, P, nbx, nblk;
+  int det;
   int n;
   float* dst[kMaxSlabSegs];
   int off[kMaxSlabSegs];
@@ -39,7 +40,8 @@ struct SlabJob {
 
 void attn_fwd_launch(const AttnArgs&, int, uint16_t*, float*, float*, float*, int, hipStream_t);
 void attn_bwd_launch(const AttnArgs&, int, const uint16_t*, const uint16_t*, const float*, float*, float*, long long,
-                     int, float*, long long, int, float*, long long, int, bool, bool, hipStream_t);
+                     int, float*, long long, int, float*, long long, int, bool, bool, long long, hipStream_t);
+int attn_bwd_key_blocks(int, int);
 void ln_linear_fwd_launch(const void*, bool, int, int, int, const float*, const float*, float, const uint16_t*, int,
                           const float*, int, int, const float*, int, void*, bool, int, float*, float*, const float*, int,
                           int, int, hipStream_t);
@@ -74,7 +76,7 @@ int ce_dw_splits(int, int);
 void mlm_select_launch(const int64_t*, int, int, int, int, int64_t*, int64_t*, int*, int64_t*, int64_t*, float*, bool*,
                        hipStream_t);
 void ce_bwd_launch(int, const uint16_t*, const int64_t*, const uint16_t*, const float*, const float*, const float*,
-                   int, int, float*, const int64_t*, float*, float*, int, float*, hipStream_t);
+                   int, int, float*, const int64_t*, float*, float*, int, float*, int, hipStream_t);
 void embed_fwd_launch(const int64_t*, const float*, const float*, float*, long long, int, int, float, hipStream_t);
 void embed_bwd_launch(const int64_t*, const float*, float*, float*, int, int, int, float, hipStream_t);
 void embed_bwd_sorted_launch(const int64_t*, const int64_t*, const float*, float*, long long, int, float, hipStream_t);
@@ -106,6 +108,7 @@ struct PeBwdArgs {  // attention_pe.hip
   float scale, scale_log2;
   int accumulate;
   int d_atomic;
+  long long dq_kbs;
 };
 void attn_bwd_pe_launch(const PeBwdArgs&, int, int, hipStream_t);
 void pe_proj_bwd_launch(const float*, const float*, int, const float*, const float*, int, int, int, float*, float*,
@@ -117,6 +120,10 @@ using OptT = c10::optional<Tensor>;
 
 namespace {
 hipStream_t stream() { return at::hip::getCurrentHIPStream(); }
+
+// deterministic mode (trainer flag ``deterministic``): every reduction that would
+// use fp32 atomics with several writers per address runs as a fixed-order split reduction
+bool g_det = false;
 
 #define CHECK_CUDA(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
 #define CHECK_DT(t, dt) TORCH_CHECK((t).scalar_type() == (dt), #t " has wrong dtype ", (t).scalar_type())
@@ -236,9 +243,19 @@ std::vector<Tensor> attn_bwd(Tensor q, Tensor k, Tensor v, OptT kmask, Tensor o,
   } else {
     delta = torch::empty({a.B, a.Nq, H}, f32);
   }
+  const int nkb = pio::attn_bwd_key_blocks(a.Nk, (int)D);
+  if (g_det && nkb > 1) {  // one dQ partial slice per key block, summed in a fixed order
+    Tensor part = torch::empty({nkb, a.B, a.Nq, H * D}, f32);
+    pio::attn_bwd_launch(a, (int)D, bfp(o), bfp(dO), f32p(lse), delta.data_ptr<float>(), part.data_ptr<float>(),
+                         (long long)a.Nq * H * D, (int)(H * D), dk.data_ptr<float>(), dk.stride(0), (int)dk.stride(1),
+                         dv.data_ptr<float>(), dv.stride(0), (int)dv.stride(1), !delta_in.has_value(), kv_accumulate,
+                         (long long)a.B * a.Nq * H * D, stream());
+    dq.narrow(2, 0, H * D).copy_(part.sum(0));
+    return {dq, dk, dv};
+  }
   pio::attn_bwd_launch(a, (int)D, bfp(o), bfp(dO), f32p(lse), delta.data_ptr<float>(), dq.data_ptr<float>(),
                        dq.stride(0), (int)dq.stride(1), dk.data_ptr<float>(), dk.stride(0), (int)dk.stride(1),
-                       dv.data_ptr<float>(), dv.stride(0), (int)dv.stride(1), !delta_in.has_value(), kv_accumulate,
+                       dv.data_ptr<float>(), dv.stride(0), (int)dv.stride(1), !delta_in.has_value(), kv_accumulate, 0,
                        stream());
   return {dq, dk, dv};
 }
@@ -388,7 +405,8 @@ pio::SlabJob make_job(const OptT& slab, std::vector<Tensor>& dsts, const std::ve
   j.S = (int)t.size(0);
   j.P = P;
   j.nbx = (P + 255) / 256;
-  j.nblk = j.nbx * ((j.S + pio::kSlabRowsPerBlock - 1) / pio::kSlabRowsPerBlock);
+  j.det = g_det ? 1 : 0;
+  j.nblk = g_det ? j.nbx : j.nbx * ((j.S + pio::kSlabRowsPerBlock - 1) / pio::kSlabRowsPerBlock);
   return j;
 }
 }  // namespace
@@ -405,6 +423,7 @@ std::vector<Tensor> post_attn_bwd(Tensor dz, Tensor y, Tensor m2, Tensor r2, Ten
   TORCH_CHECK(C == 32 || C == 64 || C == 128, "post_attn supports C in {32, 64, 128}");
   TORCH_CHECK(H > 0 && C % H == 0, "heads must divide C");
   TORCH_CHECK(grads.size() == 8, "post_attn_bwd needs 8 gradient targets");
+  TORCH_CHECK(!g_det || slab, "deterministic mode: post_attn_bwd parameter gradients need slab mode (R < 2^17 rows)");
   const int64_t CC = (int64_t)C * C;
   int vrs = -1;
   const int64_t sr = slab ? (R + 63) / 64 : 0;
@@ -478,6 +497,8 @@ OptT ln_linear_bwd(Tensor g, Tensor w, Tensor x, OptT mean, OptT rstd, OptT lnw,
   TORCH_CHECK(g.dim() == 2 && g.stride(1) == 1 && x.dim() == 2 && x.stride(1) == 1, "g / x must be 2-D rows");
   const int R = (int)g.size(0), N = (int)g.size(1);
   TORCH_CHECK(!(slab && R >= kTallRows), "slab gradients are for R < ", kTallRows, " rows");
+  TORCH_CHECK(!g_det || slab || (!dW.has_value() && !lnw.has_value()),
+              "deterministic mode: ln_linear_bwd parameter gradients need slab mode (R < 2^17 rows)");
   const int64_t sr = slab ? (R + 63) / 64 : 0;
   const int Kin = kin >= 0 ? (int)kin : (int)w.size(1);
   TORCH_CHECK(w.size(0) == N && w.is_contiguous() && w.size(1) >= Kin, "w must be (N, >= Kin) contiguous, N = g columns");
@@ -528,6 +549,7 @@ void wgrad(Tensor g, Tensor a, int64_t amode, OptT mean, OptT rstd, OptT lnw, Op
   TORCH_CHECK(a.size(0) == R, "row mismatch");
   TORCH_CHECK(pe.has_value() || a.size(1) == Kin, "a must be (R, Kin)");
   TORCH_CHECK(Kin <= 160, "wgrad supports Kin <= 160");
+  TORCH_CHECK(!g_det, "deterministic mode: the streaming wgrad kernel adds partials with atomics");
   TORCH_CHECK(amode != 1 || (mean.has_value() && rstd.has_value() && lnw.has_value() && lnb.has_value()),
               "LN mode needs stats and affine");
   const float* pp; int prs, prows, npix;
@@ -593,7 +615,7 @@ OptT ce_bwd(Tensor h, Tensor labels, Tensor w, Tensor bias, Tensor lse, Tensor g
   if (slab) sl = torch::empty({pio::ce_dw_splits(M, V), (int64_t)V * C + ((V + 3) & ~3)}, dW.options());
   pio::ce_bwd_launch(C, bfp(h), labels.data_ptr<int64_t>(), bfp(w), f32p(bias), f32p(lse), f32p(gscale), M, V,
                      dH.data_ptr<float>(), rm, dW.data_ptr<float>(), db.data_ptr<float>(), accumulate ? 1 : 0,
-                     slab ? sl.data_ptr<float>() : nullptr, stream());
+                     slab ? sl.data_ptr<float>() : nullptr, g_det ? 1 : 0, stream());
   if (slab) return sl;
   return c10::nullopt;
 }
@@ -765,20 +787,31 @@ void attn_bwd_pe(Tensor q, Tensor kv, Tensor dO, Tensor lse, Tensor delta, Tenso
   TORCH_CHECK(part.is_contiguous() && part.size(0) == (int64_t)nkb * bsplit && part.size(1) == (int64_t)(2 + nc) * 2 * C,
               "part must be (ceil(M/256)*bsplit, (2+nc)*2C)");
   for (const Tensor* t : {&lse, &delta, &mean, &rstd, &pix, &dq, &D, &part}) CHECK_DT(*t, torch::kFloat32);
-  dq.zero_();
+  TORCH_CHECK(!(g_det && bsplit > 1), "deterministic mode: attn_bwd_pe needs bsplit = 1");
+  Tensor dq_part;
+  if (g_det) dq_part = torch::empty({nkb, dq.numel()}, dq.options());
+  else dq.zero_();
   pio::PeBwdArgs a{};
   a.q = bfp(q); a.q_bs = qb ? q.stride(0) : 0; a.q_rs = (int)q.stride(1);
   a.kv = bfp(kv); a.kv_rs = (int)kv.stride(0);
   a.dO = bfp(dO); a.lse = f32p(lse); a.delta = f32p(delta); a.mean = f32p(mean); a.rstd = f32p(rstd); a.pix = f32p(pix);
-  a.dq = dq.data_ptr<float>(); a.D = D.data_ptr<float>(); a.part = part.data_ptr<float>();
+  a.dq = g_det ? dq_part.data_ptr<float>() : dq.data_ptr<float>();
+  a.dq_kbs = g_det ? dq.numel() : 0;
+  a.D = D.data_ptr<float>(); a.part = part.data_ptr<float>();
   a.B = B; a.H = (int)H; a.Nq = Nq; a.M = M; a.C = C; a.nc = nc;
   a.scale = (float)scale; a.scale_log2 = (float)(scale * 1.4426950408889634);
   a.accumulate = accumulate ? 1 : 0;
   if (bsplit > 1 && !accumulate) D.zero_();  // atomics add onto it
   pio::attn_bwd_pe_launch(a, nkb, (int)bsplit, stream());
+  if (g_det) dq.view({-1}).copy_(dq_part.sum(0));
 }
 
+void set_deterministic(bool on) { g_det = on; }
+bool get_deterministic() { return g_det; }
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("set_deterministic", &set_deterministic);
+  m.def("get_deterministic", &get_deterministic);
   m.doc() = "Perceiver IO CDNA4 (gfx950) kernels";
   m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("kmask"), py::arg("H"), py::arg("D"),
         py::arg("scale"), py::arg("dropout_p"), py::arg("seed"), py::arg("nsplit"), py::arg("site") = 0);

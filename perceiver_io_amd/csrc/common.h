@@ -212,6 +212,7 @@ constexpr int kSlabRowsPerBlock = 32;
 struct SlabJob {
   const float* slab;  // nullptr: no job
   int S, P, nbx, nblk;
+  int det;            // deterministic mode: one block per column range sums ALL rows, plain add
   int n;
   float* dst[kMaxSlabSegs];
   int off[kMaxSlabSegs];
@@ -224,6 +225,24 @@ __device__ __forceinline__ void slab_reduce_block(const SlabJob& j, int b, float
   const int cb = bx * 256, c = cb + 4 * l, P = j.P;
   const int s0 = by * kSlabRowsPerBlock, s1 = min(j.S, s0 + kSlabRowsPerBlock);
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (j.det) {  // fixed summation order, a single writer per element: bitwise reproducible
+    if (c < P)
+      for (int s = w; s < j.S; s += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(j.slab + (long long)s * P + c);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+    part[w * 64 + l] = acc;
+    __syncthreads();
+    const float* pf = reinterpret_cast<const float*>(part);
+    const int k = 64 * w + l, col = cb + k;
+    if (col >= P) return;
+    const float sum = ((pf[k] + pf[256 + k]) + pf[512 + k]) + pf[768 + k];
+    for (int q = 0; q < j.n; ++q) {
+      const int lo = j.off[q];
+      if (col >= lo && col < lo + j.len[q]) j.dst[q][col - lo] += sum;
+    }
+    return;
+  }
   if (c < P) {
     float4 v[kSlabRowsPerBlock / 4];
 #pragma unroll

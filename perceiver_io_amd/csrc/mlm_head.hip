@@ -506,9 +506,11 @@ int ce_dw_splits(int M, int V) {
 
 void ce_bwd_launch(int C, const uint16_t* Hm, const int64_t* labels, const uint16_t* W, const float* bias,
                    const float* lse, const float* gscale, int M, int V, float* dH, const int64_t* rowmap, float* dW,
-                   float* db, int accumulate, float* slab, hipStream_t st) {
+                   float* db, int accumulate, float* slab, int det, hipStream_t st) {
   const int nchunks = (V + VB - 1) / VB;
-  const int nsplit = pick_split(M, nchunks, 512);  // dH partials are added atomically: few splits
+  // dH partials are added atomically: few splits; deterministic mode: one (a single writer per
+  // dH element — every compacted row maps to its own source position)
+  const int nsplit = det ? 1 : pick_split(M, nchunks, 512);
   const int cps = (nchunks + nsplit - 1) / nsplit;
   // dW: (vocab chunk × row split) workgroups, ≈ 4 per CU; dW / db partials added atomically
   // or stored into the slab

@@ -44,6 +44,22 @@ def backend(name: str):
         set_backend(prev)
 
 
+_DETERMINISTIC = [False]
+
+
+def set_deterministic(flag: bool) -> None:
+    """Deterministic mode (trainer ``deterministic=True``): every kernel reduction
+    that would use fp32 atomics with several writers per address runs as a fixed-order split
+    reduction, so identical runs give bitwise-identical parameters."""
+    _DETERMINISTIC[0] = bool(flag)
+    if ext.available():
+        ext.require().set_deterministic(bool(flag))
+
+
+def deterministic() -> bool:
+    return _DETERMINISTIC[0]
+
+
 def use_hip(t: torch.Tensor) -> bool:
     """True when ``t`` should be processed by the HIP kernels."""
     if _BACKEND in ("torch", "reference") or not t.is_cuda:

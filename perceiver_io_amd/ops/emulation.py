@@ -511,5 +511,13 @@ def slab_reduce(slab, dsts, offs):
             d += slab[:, o:o + n].sum(0).view(d.shape)
 
 
+def set_deterministic(flag):
+    """the emulation has no atomics: nothing to switch"""
+
+
+def get_deterministic():
+    return False
+
+
 def cast_bf16(x, y):
     y.copy_(x.to(torch.bfloat16).view(y.shape))

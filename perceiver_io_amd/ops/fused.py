@@ -319,6 +319,10 @@ PE_ATTN_FUSED = os.environ.get("PERCEIVER_PE_ATTN_FUSED", "1") != "0"
 
 def pe_attn_bsplit(B: int, M: int, H: int) -> int:
     """Batch groups of the fused PE attention backward: ≥ 512 workgroups when the image is small."""
+    from . import deterministic
+
+    if deterministic():  # batch groups would add into D with atomics
+        return 1
     nkb = (M + 255) // 256
     return max(1, min(B, -(-512 // (nkb * H))))
 
@@ -800,6 +804,15 @@ class _TextEmbedFn(torch.autograd.Function):
             if need and p.grad is None:
                 p.grad = torch.zeros_like(p)
             targets.append(p.grad if need else None)
+        from . import deterministic
+
+        if deterministic() and g.is_cuda:  # sorted segment sums instead of fp32 atomics
+            C = g.shape[-1]
+            if targets[0] is not None:
+                targets[0].index_put_((ids.reshape(-1),), g.reshape(-1, C) * ctx.scale, accumulate=True)
+            if targets[1] is not None:
+                targets[1][: ids.shape[1]] += g.sum(0)
+            return None, None, None, None
         # scatter-add straight into the (flat-buffer) gradients
         K.embed_bwd(ids, g.contiguous(), targets[0], targets[1], ctx.scale)
         return None, None, None, None

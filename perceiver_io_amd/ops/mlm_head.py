@@ -209,7 +209,12 @@ class _GatherQueries(torch.autograd.Function):
             return None, None
         if p.grad is None:
             p.grad = torch.zeros_like(p)
-        p.grad.index_add_(0, idx, g.to(p.grad.dtype))
+        from . import deterministic
+
+        if deterministic():
+            p.grad.index_put_((idx,), g.to(p.grad.dtype), accumulate=True)
+        else:
+            p.grad.index_add_(0, idx, g.to(p.grad.dtype))
         return None, None
 
 

@@ -192,8 +192,13 @@ class FusedAdamW(torch.optim.Optimizer):
         g = self.param_groups[0]
         self.flat.fold()
         if self.max_grad_norm > 0:
-            self.hyper[2:3].zero_()
-            K.sumsq(self.flat.grad, self.hyper[2:3])
+            from . import deterministic
+
+            if deterministic():  # torch's tree reduction instead of per-block atomics
+                torch.sum(self.flat.grad * self.flat.grad, dim=0, keepdim=True, out=self.hyper[2:3])
+            else:
+                self.hyper[2:3].zero_()
+                K.sumsq(self.flat.grad, self.hyper[2:3])
         K.adamw(self.flat.data, self.flat.grad, self.exp_avg, self.exp_avg_sq, self.flat.shadow, self.hyper,
                 g["eps"], g["weight_decay"], self.max_grad_norm, self.grad_scale)
 

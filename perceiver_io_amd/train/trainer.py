@@ -297,8 +297,9 @@ class Trainer:
     def fit(self, model, datamodule=None, train_dataloaders=None, val_dataloaders=None, ckpt_path=None):
         if self.seed is not None:
             torch.manual_seed(self.seed + self.dist.rank)
-        if self.deterministic:
+        if self.deterministic:  # atomics-free kernel reductions + torch's deterministic algorithms
             torch.use_deterministic_algorithms(True, warn_only=True)
+            ops.set_deterministic(True)
         torch.autograd.set_detect_anomaly(self.detect_anomaly)
         if datamodule is not None:
             if self.dist.local_rank == 0:

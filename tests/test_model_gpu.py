@@ -309,3 +309,59 @@ def test_headline_shape_fused_matches_eager_fp32():
         return loss
 
     _three_way(m, run, loss_tol=5e-3)
+
+
+def _det_run(graph, steps=4, image=False):
+    from perceiver_io_amd.ops.optim import FusedAdamW
+    from perceiver_io_amd.train.engine import StepEngine
+
+    torch.manual_seed(11)
+    if image:
+        from perceiver_io_amd.tasks import LitImageClassifier
+
+        lit = LitImageClassifier(image_shape=(28, 28, 1), num_classes=10,
+                                 optimizer_init={"class_path": "torch.optim.AdamW", "init_args": {"lr": 1e-3}},
+                                 num_latents=32, num_latent_channels=128, num_encoder_layers=3,
+                                 num_encoder_self_attention_layers_per_block=2,
+                                 num_decoder_cross_attention_heads=1).cuda()
+        x = torch.randn(16, 28, 28, 1, device="cuda")
+        y = torch.randint(0, 10, (16,), device="cuda")
+        opt = FusedAdamW(lit.parameters(), lr=1e-3, max_grad_norm=0.5)
+        eng = StepEngine(lambda b: lit.step(b)[0], opt, device="cuda", graph=graph, warmup_eager=1)
+        batch = (x, y)
+    else:
+        lit = _mlm(L=96)
+        ids = torch.randint(3, 500, (8, 96), device="cuda")
+        pad = torch.zeros(8, 96, dtype=torch.bool, device="cuda")
+        pad[3, 40:] = True
+        m = lit.model
+        with torch.no_grad():
+            xm, lab = m.masking(ids, pad)
+        opt = FusedAdamW(m.parameters(), lr=1e-3, max_grad_norm=0.5)
+        eng = StepEngine(lambda b: m.loss(b[1], b[2], labels=lab, x_masked=xm), opt, device="cuda", graph=graph,
+                         warmup_eager=1)
+        batch = (None, ids, pad)
+    losses = [eng.step(batch).item() for _ in range(steps)]
+    return losses, [p.detach().clone() for p in lit.parameters()]
+
+
+@pytest.mark.parametrize("image", [False, True])
+def test_deterministic_mode_bitwise(image):
+    """``--trainer.deterministic=true`` (reference trainer.yaml:57): with the
+    atomics-free reductions two identical runs give bitwise-identical parameters, and a replayed
+    hipGraph step equals the eager step bit for bit."""
+    from perceiver_io_amd import ops
+
+    ops.set_deterministic(True)
+    torch.use_deterministic_algorithms(True, warn_only=True)
+    try:
+        la, pa = _det_run(True, image=image)
+        lb, pb = _det_run(True, image=image)
+        lc, pc = _det_run(False, image=image)
+    finally:
+        ops.set_deterministic(False)
+        torch.use_deterministic_algorithms(False)
+    assert la == lb, (la, lb)
+    assert all(torch.equal(a, b) for a, b in zip(pa, pb))
+    assert la == lc, (la, lc)
+    assert all(torch.equal(a, c) for a, c in zip(pa, pc))
