@@ -76,7 +76,7 @@ int ce_dw_splits(int, int);
 void mlm_select_launch(const int64_t*, int, int, int, int, int64_t*, int64_t*, int*, int64_t*, int64_t*, float*, bool*,
                        hipStream_t);
 void ce_bwd_launch(int, const uint16_t*, const int64_t*, const uint16_t*, const float*, const float*, const float*,
-                   int, int, float*, const int64_t*, float*, float*, int, float*, int, hipStream_t);
+                   int, int, float*, long long, const int64_t*, float*, float*, int, float*, int, hipStream_t);
 void embed_fwd_launch(const int64_t*, const float*, const float*, float*, long long, int, int, float, hipStream_t);
 void embed_bwd_launch(const int64_t*, const float*, float*, float*, int, int, int, float, hipStream_t);
 void embed_bwd_sorted_launch(const int64_t*, const int64_t*, const float*, float*, long long, int, float, hipStream_t);
@@ -614,7 +614,7 @@ OptT ce_bwd(Tensor h, Tensor labels, Tensor w, Tensor bias, Tensor lse, Tensor g
   Tensor sl;
   if (slab) sl = torch::empty({pio::ce_dw_splits(M, V), (int64_t)V * C + ((V + 3) & ~3)}, dW.options());
   pio::ce_bwd_launch(C, bfp(h), labels.data_ptr<int64_t>(), bfp(w), f32p(bias), f32p(lse), f32p(gscale), M, V,
-                     dH.data_ptr<float>(), rm, dW.data_ptr<float>(), db.data_ptr<float>(), accumulate ? 1 : 0,
+                     dH.data_ptr<float>(), dH.size(0), rm, dW.data_ptr<float>(), db.data_ptr<float>(), accumulate ? 1 : 0,
                      slab ? sl.data_ptr<float>() : nullptr, g_det ? 1 : 0, stream());
   if (slab) return sl;
   return c10::nullopt;

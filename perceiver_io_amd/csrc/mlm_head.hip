@@ -209,7 +209,7 @@ __global__ __launch_bounds__(256) void ce_bwd_dh_kernel(const uint16_t* __restri
                                                         const uint16_t* __restrict__ W, const float* __restrict__ bias,
                                                         const float* __restrict__ lse, const float* __restrict__ gscale,
                                                         int M, int V, int chunks_per_split, float* __restrict__ dH,
-                                                        const int64_t* __restrict__ rowmap) {
+                                                        const int64_t* __restrict__ rowmap, long long dh_rows) {
   constexpr int LD = C + 8, LDL = VB + 8, NT = C / 32;
   __shared__ __attribute__((aligned(16))) uint16_t sH[HB * LD];
   __shared__ __attribute__((aligned(16))) uint16_t sW[VB * LD];
@@ -223,7 +223,8 @@ __global__ __launch_bounds__(256) void ce_bwd_dh_kernel(const uint16_t* __restri
   stage_rows<C>(sH, LD, Hm, m0, M);
   if (threadIdx.x < HB) {
     const int gr = m0 + threadIdx.x;
-    sDst[threadIdx.x] = (gr < M && labels[gr] >= 0) ? (rowmap ? rowmap[gr] : gr) : -1;
+    const long long r = (gr < M && labels[gr] >= 0) ? (rowmap ? rowmap[gr] : gr) : -1;
+    sDst[threadIdx.x] = r < dh_rows ? r : -1;  // a row outside dH is dropped, never written
   }
   const int rl = 32 * (w >> 1) + (l & 31), gr = m0 + rl;
   const int lab = gr < M ? (int)labels[gr] : -100;
@@ -266,6 +267,7 @@ __global__ __launch_bounds__(256) void ce_bwd_dh_kernel(const uint16_t* __restri
       }
     }
   }
+  __syncthreads();  // sDst is read across waves (no in-loop barrier has run for an empty split)
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) {
     const int tg = w + 4 * t;
@@ -473,12 +475,14 @@ void mlm_select_launch(const int64_t* labels, int B, int L, int cap, int gcap, i
                      gidx, glab, total, overflow);
 }
 
-// vocab splits so that a launch has ≈ target workgroups (several per CU hide the W-chunk latency)
+// vocab splits so that a launch has ≈ target workgroups (several per CU hide the W-chunk latency);
+// rounded so that every split owns at least one chunk (ceil(nchunks / ceil(nchunks / s)) splits)
 static int pick_split(int M, int nchunks, int target) {
   const int mt = (M + HB - 1) / HB;
   int s = (target + mt - 1) / mt;
-  s = s < 1 ? 1 : s;
-  return s > nchunks ? nchunks : s;
+  s = s < 1 ? 1 : (s > nchunks ? nchunks : s);
+  const int cps = (nchunks + s - 1) / s;
+  return (nchunks + cps - 1) / cps;
 }
 
 void ce_fwd_launch(int C, const uint16_t* Hm, const int64_t* labels, const uint16_t* W, const float* bias, int M,
@@ -505,7 +509,7 @@ int ce_dw_splits(int M, int V) {
 }
 
 void ce_bwd_launch(int C, const uint16_t* Hm, const int64_t* labels, const uint16_t* W, const float* bias,
-                   const float* lse, const float* gscale, int M, int V, float* dH, const int64_t* rowmap, float* dW,
+                   const float* lse, const float* gscale, int M, int V, float* dH, long long dh_rows, const int64_t* rowmap, float* dW,
                    float* db, int accumulate, float* slab, int det, hipStream_t st) {
   const int nchunks = (V + VB - 1) / VB;
   // dH partials are added atomically: few splits; deterministic mode: one (a single writer per
@@ -523,7 +527,7 @@ void ce_bwd_launch(int C, const uint16_t* Hm, const int64_t* labels, const uint1
   }
   dim3 ga((M + HB - 1) / HB, nsplit), gb(nchunks, rsplit);
 #define CEB(CC)                                                                                                  \
-  hipLaunchKernelGGL(ce_bwd_dh_kernel<CC>, ga, dim3(256), 0, st, Hm, labels, W, bias, lse, gscale, M, V, cps, dH, rowmap); \
+  hipLaunchKernelGGL(ce_bwd_dh_kernel<CC>, ga, dim3(256), 0, st, Hm, labels, W, bias, lse, gscale, M, V, cps, dH, rowmap, dh_rows); \
   hipLaunchKernelGGL(ce_bwd_dw_kernel<CC>, gb, dim3(256), 0, st, Hm, labels, W, bias, lse, gscale, M, V, tps, dW, db, \
                      slab)
   if (C == 64) { CEB(64); }

@@ -7,7 +7,9 @@ saved to ``<data_dir>/imdb-tokenizer-<vocab>.json`` when missing (``Replace('<br
 + NFD/Lowercase/StripAccents, like the reference).  Validation uses the IMDB *test* split.
 
 ``synthetic=True`` generates token sequences of the same shape (and a matching tokenizer)
-so every task runs without the dataset.  ``pad_to_max=True`` pads every batch to
+so every task runs without the dataset: ``synthetic_structure="topic"`` (default) mixes Zipf,
+per-document topic and Markov-successor tokens (label = topic parity, so both MLM and
+classifier have something to learn); ``"markov"`` / ``"unigram"`` are simpler variants.  ``pad_to_max=True`` pads every batch to
 ``max_seq_len`` instead of the longest sequence: padded positions are masked (keys) or never
 selected (MLM), so results are identical, and static shapes let the step be graph-captured.
 """
@@ -73,10 +75,11 @@ class Collator:
 class IMDBDataModule:
     def __init__(self, data_dir: str = ".cache", vocab_size: int = 10003, max_seq_len: int = 512, batch_size: int = 64,
                  num_workers: int = 3, pin_memory: bool = False, synthetic: bool = False, synthetic_size: int = 25000,
-                 pad_to_max: bool = False, seed: int = 0):
+                 pad_to_max: bool = False, seed: int = 0, synthetic_structure: str = "topic"):
         self.hparams = dict(data_dir=data_dir, vocab_size=vocab_size, max_seq_len=max_seq_len, batch_size=batch_size,
                             num_workers=num_workers, pin_memory=pin_memory, synthetic=synthetic,
-                            synthetic_size=synthetic_size, pad_to_max=pad_to_max, seed=seed)
+                            synthetic_size=synthetic_size, pad_to_max=pad_to_max, seed=seed,
+                            synthetic_structure=synthetic_structure)
         self.data_dir = data_dir
         self.vocab_size = vocab_size
         self.max_seq_len = max_seq_len
@@ -87,6 +90,7 @@ class IMDBDataModule:
         self.synthetic_size = synthetic_size
         self.pad_to_max = pad_to_max
         self.seed = seed
+        self.synthetic_structure = synthetic_structure
         tag = "synthetic-" if synthetic else ""
         self.tokenizer_path = os.path.join(data_dir, f"imdb-{tag}tokenizer-{vocab_size}.json")
         self.tokenizer = None
@@ -96,7 +100,7 @@ class IMDBDataModule:
     def _synthetic(self, split: str):
         n = self.synthetic_size if split == "train" else max(64, self.synthetic_size // 10)
         return SyntheticText(n, self.vocab_size, max(8, self.max_seq_len // 4), self.max_seq_len,
-                             seed=self.seed + (0 if split == "train" else 1))
+                             seed=self.seed + (0 if split == "train" else 1), structure=self.synthetic_structure)
 
     def prepare_data(self):
         if not self.synthetic and not os.path.isdir(os.path.join(self.data_dir, "IMDB", "aclImdb")):
