@@ -6,6 +6,12 @@ neg=0 / pos=1) — the torchtext download the reference performs is not availabl
 saved to ``<data_dir>/imdb-tokenizer-<vocab>.json`` when missing (``Replace('<br />', ' ')``
 + NFD/Lowercase/StripAccents, like the reference).  Validation uses the IMDB *test* split.
 
+Tokenizer: the reference ships its trained WordPiece tokenizer as
+``.cache/imdb-tokenizer-10003.json`` (vocab 10003, [PAD]/[UNK]/[MASK] = 0/1/2).  Copy that file
+to ``<data_dir>/imdb-tokenizer-<vocab>.json`` (the default ``data_dir`` is ``.cache``, so the
+reference's location works as is) or pass ``tokenizer_path=``: an existing file is loaded as is
+and never retrained, so token ids match checkpoints trained by the reference.
+
 ``synthetic=True`` generates token sequences of the same shape (and a matching tokenizer)
 so every task runs without the dataset: ``synthetic_structure="topic"`` (default) mixes Zipf,
 per-document topic and Markov-successor tokens (label = topic parity, so both MLM and
@@ -75,11 +81,12 @@ class Collator:
 class IMDBDataModule:
     def __init__(self, data_dir: str = ".cache", vocab_size: int = 10003, max_seq_len: int = 512, batch_size: int = 64,
                  num_workers: int = 3, pin_memory: bool = False, synthetic: bool = False, synthetic_size: int = 25000,
-                 pad_to_max: bool = False, seed: int = 0, synthetic_structure: str = "topic"):
+                 pad_to_max: bool = False, seed: int = 0, synthetic_structure: str = "topic",
+                 tokenizer_path: Optional[str] = None):
         self.hparams = dict(data_dir=data_dir, vocab_size=vocab_size, max_seq_len=max_seq_len, batch_size=batch_size,
                             num_workers=num_workers, pin_memory=pin_memory, synthetic=synthetic,
                             synthetic_size=synthetic_size, pad_to_max=pad_to_max, seed=seed,
-                            synthetic_structure=synthetic_structure)
+                            synthetic_structure=synthetic_structure, tokenizer_path=tokenizer_path)
         self.data_dir = data_dir
         self.vocab_size = vocab_size
         self.max_seq_len = max_seq_len
@@ -92,7 +99,8 @@ class IMDBDataModule:
         self.seed = seed
         self.synthetic_structure = synthetic_structure
         tag = "synthetic-" if synthetic else ""
-        self.tokenizer_path = os.path.join(data_dir, f"imdb-{tag}tokenizer-{vocab_size}.json")
+        self.user_tokenizer = tokenizer_path is not None
+        self.tokenizer_path = tokenizer_path or os.path.join(data_dir, f"imdb-{tag}tokenizer-{vocab_size}.json")
         self.tokenizer = None
         self.collator = None
         self.ds_train = self.ds_valid = None
@@ -107,6 +115,8 @@ class IMDBDataModule:
             raise FileNotFoundError(
                 f"IMDB not found under {self.data_dir}/IMDB/aclImdb (no network access to download it); "
                 "place the extracted aclImdb directory there or use --data.synthetic=true")
+        if self.user_tokenizer and not os.path.exists(self.tokenizer_path):
+            raise FileNotFoundError(f"tokenizer_path={self.tokenizer_path} does not exist")
         if not os.path.exists(self.tokenizer_path):
             os.makedirs(self.data_dir, exist_ok=True)
             if self.synthetic:
@@ -123,6 +133,9 @@ class IMDBDataModule:
 
     def setup(self, stage: Optional[str] = None):
         self.tokenizer = load_tokenizer(self.tokenizer_path)
+        if self.tokenizer.get_vocab_size() > self.vocab_size:  # ids past the embedding table
+            raise ValueError(f"{self.tokenizer_path} has {self.tokenizer.get_vocab_size()} tokens, more than "
+                             f"vocab_size={self.vocab_size}")
         self.collator = Collator(self.tokenizer, self.max_seq_len, pad_to_max=self.pad_to_max)
         if self.synthetic:
             self.ds_train, self.ds_valid = self._synthetic("train"), self._synthetic("test")

@@ -14,21 +14,20 @@ def freeze(module: torch.nn.Module):
 
 @torch.no_grad()
 def predict_masked_samples(masked_samples, encode_fn, tokenizer, model, num_predictions: int = 5, device=None):
-    n = len(masked_samples)
-    xs, ms = encode_fn(masked_samples)
-    xs, ms = xs.to(device), ms.to(device)
-    was_training = model.training
+    """For each sample, ``num_predictions`` decoded strings: the i-th fills every ``[MASK]``
+    with its i-th most likely token.  All variants are built as one ``(k, n, L)`` tensor and
+    decoded with one ``decode_batch`` call."""
+    ids, pad = (t.to(device) for t in encode_fn(masked_samples))
+    mode = model.training
     model.eval()
     try:
-        logits, _ = model(xs, ms, masking=False)
+        logits, _ = model(ids, pad, masking=False)
     finally:
-        model.train(was_training)
-    pred_mask = xs == tokenizer.token_to_id(MASK_TOKEN)
-    _, pred = torch.topk(logits[pred_mask].float(), k=num_predictions, dim=-1)
-    out = xs.clone()
-    dec = [[] for _ in range(n)]
-    for i in range(num_predictions):
-        out[pred_mask] = pred[:, i]
-        for j in range(n):
-            dec[j].append(tokenizer.decode(out[j].tolist(), skip_special_tokens=True))
-    return dec
+        model.train(mode)
+    at_mask = ids == tokenizer.token_to_id(MASK_TOKEN)                      # (n, L)
+    top = logits[at_mask].float().topk(num_predictions, dim=-1).indices     # (masks, k)
+    filled = ids.unsqueeze(0).repeat(num_predictions, 1, 1)                 # (k, n, L)
+    filled[:, at_mask] = top.t().to(filled.dtype)
+    n = ids.shape[0]
+    texts = tokenizer.decode_batch(filled.reshape(num_predictions * n, -1).tolist(), skip_special_tokens=True)
+    return [[texts[i * n + j] for i in range(num_predictions)] for j in range(n)]

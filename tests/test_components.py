@@ -103,6 +103,54 @@ def test_predict_masked_samples_topk_fill_ins():
                                  num_predictions=3)
     assert len(out) == 2 and all(len(o) == 3 for o in out)
     assert all(isinstance(s, str) and "[MASK]" not in s for o in out for s in o)
+    # the i-th variant fills every [MASK] with its i-th most likely token
+    x, pad = encode(["i have watched this [MASK] and it was awesome", "a [MASK]"])
+    model.eval()
+    logits, _ = model(x, pad, masking=False)
+    at = x == tok.token_to_id("[MASK]")
+    for i in range(3):
+        y = x.clone()
+        y[at] = logits[at].topk(3, dim=-1).indices[:, i]
+        assert [out[j][i] for j in range(2)] == [tok.decode(r.tolist(), skip_special_tokens=True) for r in y]
+
+
+def _fake_imdb(root, n=3):
+    for split in ("train", "test"):
+        for lab in ("neg", "pos"):
+            d = root / "IMDB" / "aclImdb" / split / lab
+            d.mkdir(parents=True)
+            for i in range(n):
+                (d / f"{i}_1.txt").write_text(f"this movie was {'bad' if lab == 'neg' else 'great'}<br />film {i}")
+
+
+@pytest.mark.skipif(not os.path.exists(REF_TOKENIZER), reason="reference tokenizer not mounted")
+@pytest.mark.parametrize("explicit", [False, True])
+def test_imdb_uses_shipped_tokenizer(tmp_path, explicit):
+    """The reference's shipped tokenizer (``.cache/imdb-tokenizer-10003.json``) is loaded as is —
+    at ``<data_dir>/imdb-tokenizer-10003.json`` or via ``tokenizer_path`` — and never retrained."""
+    import shutil
+
+    from perceiver_io_amd.data.imdb import IMDBDataModule
+
+    _fake_imdb(tmp_path)
+    if explicit:
+        tok_path = tmp_path / "user-tok.json"
+        shutil.copy(REF_TOKENIZER, tok_path)
+        dm = IMDBDataModule(data_dir=str(tmp_path), batch_size=2, num_workers=0, tokenizer_path=str(tok_path))
+    else:
+        tok_path = tmp_path / "imdb-tokenizer-10003.json"
+        shutil.copy(REF_TOKENIZER, tok_path)
+        dm = IMDBDataModule(data_dir=str(tmp_path), batch_size=2, num_workers=0)
+    before = tok_path.read_bytes()
+    dm.prepare_data()
+    dm.setup()
+    assert tok_path.read_bytes() == before  # not retrained
+    assert dm.tokenizer.get_vocab_size() == 10003
+    assert [dm.tokenizer.token_to_id(t) for t in ("[PAD]", "[UNK]", "[MASK]")] == [0, 1, 2]
+    y, ids, pad = next(iter(dm.train_dataloader()))
+    assert ids.shape[0] == 2 and int(ids.max()) < 10003 and pad.dtype == torch.bool
+    with pytest.raises(FileNotFoundError):
+        IMDBDataModule(data_dir=str(tmp_path), tokenizer_path=str(tmp_path / "missing.json")).prepare_data()
 
 
 class _DeferInBackward(torch.autograd.Function):
