@@ -8,13 +8,16 @@ bf16 compute.  Synthetic token ids of that shape, random-init weights (no networ
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, RCCL)
-    python bench.py --config {mlm256,seq_clf,imagenet,long_mlm,mnist} ...
+    python bench.py --config {mlm256,seq_clf,imagenet,long_mlm,mnist,lartpc} ...
 
 Other configs (BASELINE.json configs 1, 3-5): ``seq_clf`` = IMDB text classifier with a frozen
 encoder (decoder-only training, batch 128/GPU, README seq_clf command); ``imagenet`` =
 224×224×3 image classifier with Fourier position encoding (50,176 inputs × 133 channels,
 32×128 latents, 3×(1+3) layers, 1000 classes); ``long_mlm`` = MLM at seq_len 8192 with 512
-latents; ``mnist`` = the 28×28 classifier of the README (batch 128).
+latents; ``mnist`` = the 28×28 classifier of the README (batch 128); ``lartpc`` = the LArTPC
+segmentation experiment of ``run.py`` (512×512 synthetic events, batch 4, Adam + clip 10; the
+HIP backend runs it sparse — loss and gradients equal to the dense model's, see
+``models/lartpc.py`` — and ``--backend reference`` densely, as the reference does).
 
 Prints ONE JSON line on rank 0.  ``--backend reference`` measures the reference's own compute
 (nn.MultiheadAttention math, full-logit CE, torch AdamW) eagerly under bf16 autocast on the same
@@ -45,6 +48,8 @@ CONFIGS = {
                      metric="samples/sec (whole node) IMDB MLM seq_len=8192 512 latents"),
     "mnist": dict(batch=128, seq_len=28 * 28, latents=32, channels=128,
                   metric="samples/sec (whole node) MNIST img_clf 32x128 latents"),
+    "lartpc": dict(batch=4, seq_len=512 * 512, latents=32, channels=64,
+                   metric="samples/sec (whole node) LArTPC 512x512 per-pixel segmentation (run.py)"),
 }
 
 
@@ -62,6 +67,7 @@ def parse(argv=None):
     ap.add_argument("--backend", default="hip", choices=["hip", "torch", "reference"])
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture of the step")
+    ap.add_argument("--dense", action="store_true", help="lartpc: evaluate all pixels (the reference's cost)")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--profile-stacks", type=int, default=0,
                     help="with --profile-steps: group copy/fill ops by N Python stack frames (finds stray copies)")
@@ -89,6 +95,8 @@ def build(args, device):
     from perceiver_io_amd.tasks import LitImageClassifier, LitMaskedLanguageModel, LitTextClassifier
 
     B, L = args.batch, args.seq_len
+    if args.config == "lartpc":
+        return _build_lartpc(args)
     if args.config in ("mlm256", "long_mlm"):
         lit = LitMaskedLanguageModel(
             vocab_size=args.vocab, max_seq_len=L, optimizer_init=_opt(), scheduler_init=_sched(),
@@ -153,6 +161,62 @@ def build(args, device):
     return lit, loss_fn, make_batch, desc, 1e-3, 0.01
 
 
+class _LArHolder:
+    """``lit``-like holder: ``.model`` (with ``.decoder``), moved by ``.to``."""
+
+    def __init__(self, model):
+        self.model = model
+
+    def to(self, device):
+        self.model.to(device)
+        return self
+
+
+def _build_lartpc(args):
+    import torch
+    import torch.nn.functional as F
+
+    from perceiver_io_amd.data.lartpc import sparse_collate
+    from perceiver_io_amd.data.synthetic import lartpc_event
+    from perceiver_io_amd.models.lartpc import LArPerceiver, class_weights
+
+    side = int(round(args.seq_len ** 0.5))
+    model = LArPerceiver(side, latents=(args.latents, args.channels))
+    B = args.batch
+    dense = args.backend == "reference" or args.dense
+    state = {}
+
+    def loss_fn(batch):
+        w = state.get("w")
+        if w is None or w.device != batch[0].device:
+            w = state["w"] = class_weights(batch[0].device)
+        if dense:
+            img, lab = batch
+            return F.cross_entropy(model(img).float(), lab, weight=w)
+        return model.sparse_loss(batch, w)[0]
+
+    pool = []
+
+    def make_batch(g):
+        # the 4 benchmark batches share one capacity bucket (one captured graph)
+        if not pool:
+            seeds = torch.randint(0, 2**31 - 1, (4 * B,), generator=g).tolist()
+            ev = [lartpc_event(s, side) for s in seeds]
+            if dense:
+                for i in range(4):
+                    chunk = ev[i * B:(i + 1) * B]
+                    pool.append((torch.stack([e[0] for e in chunk]), torch.stack([e[1] for e in chunk])))
+            else:
+                allb = sparse_collate(ev, bucket=2048)
+                for i in range(4):
+                    pool.append(tuple(t[i * B:(i + 1) * B] for t in allb))
+        return pool.pop(0)
+
+    desc = (f"perceiver-io-lartpc {side}x{side}x1 fourier-bands=32 latents={args.latents}x{args.channels} "
+            f"layers=3x(1+3) queries={side * side} {'dense' if dense else 'sparse'}")
+    return _LArHolder(model), loss_fn, make_batch, desc, 1e-3, 1e-4
+
+
 def main(argv=None):
     args = parse(argv)
     import torch
@@ -173,16 +237,18 @@ def main(argv=None):
     lit, loss_inner, make_batch, desc, lr, wd = build(args, device)
     lit.to(device)
     model = lit.model
-    params = [p for p in model.parameters() if p.requires_grad]
+    lar = args.config == "lartpc"  # Adam (L2 decay) + clip 10 over the trained parameters (run.py)
+    params = model.trained_parameters() if lar else [p for p in model.parameters() if p.requires_grad]
     fused = args.backend == "hip" and cuda
     if fused:
-        from perceiver_io_amd.ops.optim import FusedAdamW
+        from perceiver_io_amd.ops.optim import FusedAdam, FusedAdamW
 
-        opt = FusedAdamW(params, lr=lr, weight_decay=wd)
+        opt = (FusedAdam(params, lr=lr, weight_decay=wd, max_grad_norm=10.0) if lar
+               else FusedAdamW(params, lr=lr, weight_decay=wd))
     else:
-        opt = torch.optim.AdamW(params, lr=lr, weight_decay=wd)
-    sched = torch.optim.lr_scheduler.OneCycleLR(opt, max_lr=lr, total_steps=50000, pct_start=0.1,
-                                                cycle_momentum=False)
+        opt = (torch.optim.Adam if lar else torch.optim.AdamW)(params, lr=lr, weight_decay=wd)
+    sched = None if lar else torch.optim.lr_scheduler.OneCycleLR(opt, max_lr=lr, total_steps=50000, pct_start=0.1,
+                                                                 cycle_momentum=False)
     reducer = None
     if world > 1:
         from perceiver_io_amd.ops.optim import FlatParameterSpace

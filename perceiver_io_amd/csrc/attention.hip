@@ -329,7 +329,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
                                                            long long dq_bs, int dq_rs, float* __restrict__ dk,
                                                            long long dk_bs, int dk_rs, float* __restrict__ dv,
                                                            long long dv_bs, int dv_rs, int dq_atomic, int kv_acc,
-                                                           long long dq_kbs) {
+                                                           long long dq_kbs, int nqs, int q_tiles_per_split) {
   constexpr int LD = (D < 32 ? 32 : D) + 8;  // Q / dO / K tiles [row][d] (D=16 zero-padded to 32 cols)
   constexpr int NT = (D < 32) ? 1 : D / 32;
   constexpr int KS = D / 16;
@@ -355,8 +355,12 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
   const int w = wave_id(), l = lane_id(), r = l & 31, hh = l >> 5;
   const Blk3 blk = xcd_block3();  // the heads / key blocks of one batch element share an L2
   const int h = blk.y, b = blk.z;
-  const int kbase = blk.x * KB;
-  dq += (long long)blk.x * dq_kbs;  // deterministic mode: one dQ partial slice per key block
+  // blk.x = key block × nqs + query split: many-query / few-key shapes (a decoder's pixel or
+  // token queries over a few dozen latents) split the query range across workgroups, whose
+  // dK / dV partials are added atomically (the host zeroes dK / dV first unless accumulating)
+  const int kblk = blk.x / nqs, qsplit = blk.x - kblk * nqs;
+  const int kbase = kblk * KB;
+  dq += (long long)kblk * dq_kbs;  // deterministic mode: one dQ partial slice per key block
   const int key = kbase + 32 * w + r;  // this lane's key (column of S / dP)
   const int kc = key < a.Nk ? key : a.Nk - 1;
   const uint32_t dkey = a.drop_thresh ? drop_key(a.seedp, a.site, 2u) : 0u;
@@ -371,7 +375,9 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
   const uint16_t* vbp = a.v + (long long)b * a.v_bs + h * D;
   const uint16_t* qbp = a.q + (long long)b * a.q_bs + h * D;
   const uint16_t* dobp = dO + (long long)b * a.Nq * HD + h * D;
-  const int nqt = (a.Nq + 31) / 32;
+  const int nqt_all = (a.Nq + 31) / 32;
+  const int qt_begin = qsplit * q_tiles_per_split;
+  const int nqt = min(nqt_all, qt_begin + q_tiles_per_split);  // end of this split's query tiles
 
   // round staging: chunk c < NQS·32·CH is Q, the next NQS·32·CH are dO; threads [0, NQS·32)
   // carry the round's LSE, [NQS·32, NQS·64) its delta
@@ -410,7 +416,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
     kst[i] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
     if (kk < a.Nk) kst[i] = *reinterpret_cast<const bf16x8*>(kbp + (long long)kk * a.k_rs + col);
   }
-  if (nqt > 0) fetch(0);
+  if (qt_begin < nqt) fetch(qt_begin);
   if (D < 32) {  // zero the padded head-dim columns 16..31
     for (int i = threadIdx.x; i < KB; i += NTH) {
       *reinterpret_cast<bf16x8*>(sK + i * LD + 16) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
@@ -433,7 +439,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
   for (int t = 0; t < NT; ++t) dK[t] = dV[t] = f32x16{};
   PIO_TS(1);
 
-  for (int qt0 = 0; qt0 < nqt; qt0 += NQS) {
+  for (int qt0 = qt_begin; qt0 < nqt; qt0 += NQS) {
     __syncthreads();  // the previous round's tiles and dS slabs are consumed
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
@@ -443,7 +449,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
     if (threadIdx.x < NQS * 32) sL[threadIdx.x] = lreg;
     else if (threadIdx.x < NQS * 64) sDl[threadIdx.x - NQS * 32] = lreg;
     __syncthreads();
-    PIO_TS(2 + 4 * (qt0 / NQS));
+    PIO_TS(2 + 4 * ((qt0 - qt_begin) / NQS));
     if (qt0 + NQS < nqt) fetch(qt0 + NQS);
 
 #pragma unroll
@@ -506,9 +512,9 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
         *reinterpret_cast<uint2*>(slab + r * LDS_ + 8 * g + 4 * hh) = pk;
       }
     }
-    PIO_TS(3 + 4 * (qt0 / NQS));
+    PIO_TS(3 + 4 * ((qt0 - qt_begin) / NQS));
     __syncthreads();
-    PIO_TS(4 + 4 * (qt0 / NQS));
+    PIO_TS(4 + 4 * ((qt0 - qt_begin) / NQS));
     // dQ of tile j = w: Σ over the block's keys of dS[key][q] · K[key][d]
     if (w < NQS && qt0 + w < nqt) {
       const uint16_t* tS = sdS + w * KB * LDS_;
@@ -554,14 +560,14 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
         }
       }
     }
-    PIO_TS(5 + 4 * (qt0 / NQS));
+    PIO_TS(5 + 4 * ((qt0 - qt_begin) / NQS));
   }
   PIO_TS(40);
   // write dK (scaled) and dV: rows = keys (registers), lane = head-dim column
   // accumulator: col = lane&31 = d, row = acc_row(reg) = key within the wave's 32
   // (needs the dS slabs to hold both [KB][D + 4] fp32 tiles: not in the QR = 1 variant)
   if constexpr (D <= 32 && 2 * KB * (D + 4) * 4 <= NQS * KB * LDS_ * 2) {
-    if (vec_out) {  // transpose through LDS (the dS slabs are consumed), 16-byte row stores
+    if (vec_out && nqs == 1) {  // transpose through LDS (the dS slabs are consumed), 16-byte row stores
       constexpr int LDE = D + 4, CPR = D / 4;
       float* sE = reinterpret_cast<float*>(sdS);  // [dK | dV][KB keys][LDE]
       __syncthreads();
@@ -603,8 +609,13 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
         // kv_acc: add onto earlier contributions (K/V shared by several applications, K-06)
         float* pk = dk + (long long)b * dk_bs + (long long)kk * dk_rs + h * D + dd;
         float* pv = dv + (long long)b * dv_bs + (long long)kk * dv_rs + h * D + dd;
-        *pk = kv_acc ? *pk + dK[t][i] * a.scale : dK[t][i] * a.scale;
-        *pv = kv_acc ? *pv + dV[t][i] : dV[t][i];
+        if (nqs > 1) {
+          atomicAdd(pk, dK[t][i] * a.scale);
+          atomicAdd(pv, dV[t][i]);
+        } else {
+          *pk = kv_acc ? *pk + dK[t][i] * a.scale : dK[t][i] * a.scale;
+          *pv = kv_acc ? *pv + dV[t][i] : dV[t][i];
+        }
       }
     }
   PIO_TS(41);
@@ -670,8 +681,24 @@ static bool getenv_flag(const char* name) {
 template <int D, int NW>
 static void bwd_launch_t(const AttnArgs& a, const uint16_t* dO, const float* LSE, float* delta, float* dq,
                          long long dq_bs, int dq_rs, float* dk, long long dk_bs, int dk_rs, float* dv, long long dv_bs,
-                         int dv_rs, int kv_acc, long long dq_kbs, hipStream_t st) {
+                         int dv_rs, int kv_acc, long long dq_kbs, int qsplit_ok, hipStream_t st) {
   const int nkb = (a.Nk + 32 * NW - 1) / (32 * NW);
+  // query splits when key blocks × heads × batch leave the GPU idle (≥ 4 query tiles each)
+  const int nqt = (a.Nq + 31) / 32, base = nkb * a.H * a.B;
+  int nqs = 1;
+  if (qsplit_ok && base < 256 && nqt >= 8) {
+    nqs = (512 + base - 1) / base;
+    const int cap = (nqt + 3) / 4;
+    nqs = nqs < cap ? nqs : cap;
+  }
+  const int tps = (nqt + nqs - 1) / nqs;
+  nqs = (nqt + tps - 1) / tps;  // no empty split
+  if (nqs > 1 && !kv_acc) {     // the splits add into dK / dV
+    const long long total = (long long)a.B * a.Nk * a.H * D;
+    const unsigned zb = (unsigned)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+    hipLaunchKernelGGL(zero_rows_kernel, dim3(zb), dim3(256), 0, st, dk, dk_bs, dk_rs, a.Nk, a.H * D, total);
+    hipLaunchKernelGGL(zero_rows_kernel, dim3(zb), dim3(256), 0, st, dv, dv_bs, dv_rs, a.Nk, a.H * D, total);
+  }
   // several key blocks add into dQ (fp32 atomics), unless each stores its own partial slice
   // (deterministic mode: dq_kbs > 0, summed by the caller)
   const int atomic = nkb > 1 && dq_kbs == 0;
@@ -680,17 +707,17 @@ static void bwd_launch_t(const AttnArgs& a, const uint16_t* dO, const float* LSE
     hipLaunchKernelGGL(zero_rows_kernel, dim3((unsigned)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096)), dim3(256), 0,
                        st, dq, dq_bs, dq_rs, a.Nq, a.H * D, total);
   }
-  dim3 grid(nkb, a.H, a.B);
+  dim3 grid(nkb * nqs, a.H, a.B);
   const bool small_lds = !getenv_flag("PIO_ATTN_BWD_FULL_LDS");
   if (a.Nq <= 32 && small_lds)
     hipLaunchKernelGGL((attn_bwd_kernel<D, NW, 1>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs,
-                       dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs);
+                       dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs, nqs, tps);
   else if (a.Nq <= 64 && small_lds)
     hipLaunchKernelGGL((attn_bwd_kernel<D, NW, 2>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs,
-                       dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs);
+                       dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs, nqs, tps);
   else
     hipLaunchKernelGGL((attn_bwd_kernel<D, NW>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs, dk,
-                       dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs);
+                       dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs, nqs, tps);
 }
 
 // key blocks of the backward grid (dQ partial slices in deterministic mode)
@@ -701,7 +728,8 @@ int attn_bwd_key_blocks(int Nk, int D) {
 
 void attn_bwd_launch(const AttnArgs& a, int D, const uint16_t* O, const uint16_t* dO, const float* LSE, float* delta,
                      float* dq, long long dq_bs, int dq_rs, float* dk, long long dk_bs, int dk_rs, float* dv,
-                     long long dv_bs, int dv_rs, bool compute_delta, bool kv_acc, long long dq_kbs, hipStream_t st) {
+                     long long dv_bs, int dv_rs, bool compute_delta, bool kv_acc, long long dq_kbs, int qsplit_ok,
+                     hipStream_t st) {
   // delta = rowsum(dO∘O) is normally produced by the post-attention backward kernel;
   // compute it here otherwise.  dQ needs no zero fill from the caller.
   const int rows = a.B * a.Nq;
@@ -709,10 +737,10 @@ void attn_bwd_launch(const AttnArgs& a, int D, const uint16_t* O, const uint16_t
     hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, dO, O, delta, (float*)nullptr,
                        rows, a.H, D, dq_rs);
   switch (D) {  // waves per workgroup: 8 for d ≤ 32, 4 above (keys per block = 32 × waves)
-    case 16: bwd_launch_t<16, 8>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, st); break;
-    case 32: bwd_launch_t<32, 8>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, st); break;
-    case 64: bwd_launch_t<64, 4>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, st); break;
-    case 128: bwd_launch_t<128, 4>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, st); break;
+    case 16: bwd_launch_t<16, 8>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, qsplit_ok, st); break;
+    case 32: bwd_launch_t<32, 8>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, qsplit_ok, st); break;
+    case 64: bwd_launch_t<64, 4>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, qsplit_ok, st); break;
+    case 128: bwd_launch_t<128, 4>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, qsplit_ok, st); break;
     default: break;
   }
 }

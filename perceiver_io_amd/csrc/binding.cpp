@@ -40,7 +40,7 @@ struct SlabJob {
 
 void attn_fwd_launch(const AttnArgs&, int, uint16_t*, float*, float*, float*, int, hipStream_t);
 void attn_bwd_launch(const AttnArgs&, int, const uint16_t*, const uint16_t*, const float*, float*, float*, long long,
-                     int, float*, long long, int, float*, long long, int, bool, bool, long long, hipStream_t);
+                     int, float*, long long, int, float*, long long, int, bool, bool, long long, int, hipStream_t);
 int attn_bwd_key_blocks(int, int);
 void ln_linear_fwd_launch(const void*, bool, int, int, int, const float*, const float*, float, const uint16_t*, int,
                           const float*, int, int, const float*, int, void*, bool, int, float*, float*, const float*, int,
@@ -84,8 +84,14 @@ bool embed_bwd_local_launch(const int64_t*, const float*, float*, float*, int, i
 void text_mask_launch(const int64_t*, const bool*, const float*, const int64_t*, int64_t*, int64_t*, long long, int,
                       int, float, hipStream_t);
 void sumsq_launch(const float*, long long, float*, hipStream_t);
+void index_add_rows_launch(float*, long long, const int64_t*, const float*, long long, int, hipStream_t);
+int pixel_ce_blocks(long long);
+void pixel_ce_fwd_launch(int, int, const float*, const float*, const float*, const int64_t*, const float*, long long,
+                         float*, float*, float*, hipStream_t);
+void pixel_ce_bwd_launch(int, int, const float*, const float*, const float*, const int64_t*, const float*,
+                         const float*, const float*, long long, float*, float*, float*, float*, hipStream_t);
 void adamw_launch(float*, const float*, float*, float*, uint16_t*, long long, const float*, float, float, float, float,
-                  hipStream_t);
+                  int, hipStream_t);
 void cast_bf16_launch(const float*, uint16_t*, long long, hipStream_t);
 void reduce_probe_launch(const float*, float*, hipStream_t);
 void fold_replicas_launch(float*, float*, long long, int, hipStream_t);
@@ -249,14 +255,14 @@ std::vector<Tensor> attn_bwd(Tensor q, Tensor k, Tensor v, OptT kmask, Tensor o,
     pio::attn_bwd_launch(a, (int)D, bfp(o), bfp(dO), f32p(lse), delta.data_ptr<float>(), part.data_ptr<float>(),
                          (long long)a.Nq * H * D, (int)(H * D), dk.data_ptr<float>(), dk.stride(0), (int)dk.stride(1),
                          dv.data_ptr<float>(), dv.stride(0), (int)dv.stride(1), !delta_in.has_value(), kv_accumulate,
-                         (long long)a.B * a.Nq * H * D, stream());
+                         (long long)a.B * a.Nq * H * D, 0, stream());
     dq.narrow(2, 0, H * D).copy_(part.sum(0));
     return {dq, dk, dv};
   }
   pio::attn_bwd_launch(a, (int)D, bfp(o), bfp(dO), f32p(lse), delta.data_ptr<float>(), dq.data_ptr<float>(),
                        dq.stride(0), (int)dq.stride(1), dk.data_ptr<float>(), dk.stride(0), (int)dk.stride(1),
                        dv.data_ptr<float>(), dv.stride(0), (int)dv.stride(1), !delta_in.has_value(), kv_accumulate, 0,
-                       stream());
+                       g_det ? 0 : 1, stream());
   return {dq, dk, dv};
 }
 
@@ -669,14 +675,73 @@ std::vector<Tensor> text_mask(Tensor x, OptT pad, Tensor u, Tensor rid, int64_t 
 
 void sumsq(Tensor g, Tensor out) { pio::sumsq_launch(f32p(g), g.numel(), out.data_ptr<float>(), stream()); }
 
+// dst (N, C) fp32 += src (R, C) fp32 scattered to rows idx (R) — the backward of a row gather
+void index_add_rows(Tensor dst, Tensor idx, Tensor src) {
+  CHECK_DT(dst, torch::kFloat32); CHECK_DT(src, torch::kFloat32); CHECK_DT(idx, torch::kInt64);
+  TORCH_CHECK(dst.dim() == 2 && dst.is_contiguous() && src.dim() == 2 && src.is_contiguous() && idx.is_contiguous(),
+              "index_add_rows: contiguous dst (N, C), src (R, C), idx (R)");
+  TORCH_CHECK(src.size(1) == dst.size(1) && idx.numel() == src.size(0) && dst.size(1) % 4 == 0,
+              "index_add_rows: shapes (C % 4 == 0)");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(dst.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0,
+              "index_add_rows: 16-byte aligned rows");
+  if (src.size(0) == 0) return;
+  pio::index_add_rows_launch(dst.data_ptr<float>(), dst.size(0), idx.data_ptr<int64_t>(), f32p(src), src.size(0),
+                             (int)src.size(1), stream());
+}
+
+namespace {
+void check_pixel_head(const Tensor& h, const Tensor& w, const Tensor& b, const Tensor& labels, const Tensor& wts) {
+  CHECK_DT(h, torch::kFloat32); CHECK_DT(w, torch::kFloat32); CHECK_DT(b, torch::kFloat32);
+  CHECK_DT(labels, torch::kInt64); CHECK_DT(wts, torch::kFloat32);
+  TORCH_CHECK(h.dim() == 2 && h.is_contiguous() && w.dim() == 2 && w.is_contiguous() && b.is_contiguous() &&
+                  labels.is_contiguous() && wts.is_contiguous(), "pixel head: contiguous h (R, C), w (K, C)");
+  const int C = (int)h.size(1), K = (int)w.size(0);
+  TORCH_CHECK((C == 32 || C == 64 || C == 128) && K >= 2 && K <= 4 && w.size(1) == C && b.numel() == K &&
+                  wts.numel() == K && labels.numel() == h.size(0), "pixel head: C in {32, 64, 128}, 2 <= K <= 4");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(h.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
+              "pixel head: 16-byte aligned rows");
+}
+}  // namespace
+
+// → [stats (4 + 2K sums: Σ w·ce, Σ w, n(lab>0), hit(lab>0), (n_k, hit_k)… | acc, acc_1 … acc_{K-1}),
+//    loss = Σ w·ce / Σ w (0-dim)]
+std::vector<Tensor> pixel_ce_fwd(Tensor h, Tensor w, Tensor b, Tensor labels, Tensor wts) {
+  check_pixel_head(h, w, b, labels, wts);
+  const long long R = h.size(0);
+  const int K = (int)w.size(0);
+  Tensor part = torch::zeros({pio::pixel_ce_blocks(R), 4 + 2 * K}, h.options());
+  Tensor stats = torch::empty({4 + 2 * K + K}, h.options()), loss = torch::empty({}, h.options());
+  pio::pixel_ce_fwd_launch((int)h.size(1), K, f32p(h), f32p(w), f32p(b), labels.data_ptr<int64_t>(), f32p(wts), R,
+                           part.data_ptr<float>(), stats.data_ptr<float>(), loss.data_ptr<float>(), stream());
+  return {stats, loss};
+}
+
+// dH (R, C) written; dW (K, C) / db (K) += the head's weight gradients (fixed-order sums)
+void pixel_ce_bwd(Tensor h, Tensor w, Tensor b, Tensor labels, Tensor wts, Tensor gout, Tensor stats, Tensor dH,
+                  Tensor dW, Tensor db) {
+  check_pixel_head(h, w, b, labels, wts);
+  CHECK_DT(gout, torch::kFloat32); CHECK_DT(stats, torch::kFloat32); CHECK_DT(dH, torch::kFloat32);
+  CHECK_DT(dW, torch::kFloat32); CHECK_DT(db, torch::kFloat32);
+  TORCH_CHECK(dH.is_contiguous() && dH.sizes() == h.sizes() && gout.numel() == 1 && stats.numel() >= 2,
+              "pixel head bwd: dH like h, scalar loss gradient");
+  TORCH_CHECK(dW.is_contiguous() && dW.numel() == w.numel() && db.is_contiguous() && db.numel() == b.numel(),
+              "pixel head bwd: dW / db like w / b");
+  const long long R = h.size(0);
+  const int K = (int)w.size(0), C = (int)h.size(1);
+  Tensor part = torch::zeros({pio::pixel_ce_blocks(R), (int64_t)K * C + K}, h.options());
+  pio::pixel_ce_bwd_launch(C, K, f32p(h), f32p(w), f32p(b), labels.data_ptr<int64_t>(), f32p(wts), f32p(gout),
+                           f32p(stats), R, dH.data_ptr<float>(), part.data_ptr<float>(), dW.data_ptr<float>(),
+                           db.data_ptr<float>(), stream());
+}
+
 void adamw(Tensor p, Tensor g, Tensor m, Tensor v, OptT shadow, Tensor hyper, double eps, double wd, double clip,
-           double gscale) {
+           double gscale, bool l2) {
   TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && m.is_contiguous() && v.is_contiguous());
   TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel());
   uint16_t* sp = nullptr;
   if (shadow.has_value()) { TORCH_CHECK(shadow->numel() == p.numel()); sp = reinterpret_cast<uint16_t*>(shadow->data_ptr()); }
   pio::adamw_launch(p.data_ptr<float>(), f32p(g), m.data_ptr<float>(), v.data_ptr<float>(), sp, p.numel(), f32p(hyper),
-                    (float)eps, (float)wd, (float)clip, (float)gscale, stream());
+                    (float)eps, (float)wd, (float)clip, (float)gscale, l2 ? 1 : 0, stream());
 }
 
 // self-test of the device cross-lane reductions: (6, 64) = wave_sum, wave_max, half_sum,
@@ -850,6 +915,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("lnb"), py::arg("rows_per_wg"), py::arg("dW"), py::arg("db"), py::arg("pe") = py::none(),
         py::arg("kin") = -1);
   m.def("mlm_select", &mlm_select);
+  m.def("index_add_rows", &index_add_rows);
+  m.def("pixel_ce_fwd", &pixel_ce_fwd);
+  m.def("pixel_ce_bwd", &pixel_ce_bwd);
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd, py::arg("h"), py::arg("labels"), py::arg("w"), py::arg("bias"), py::arg("lse"),
         py::arg("gscale"), py::arg("dH"), py::arg("dW"), py::arg("db"), py::arg("accumulate"),
@@ -858,7 +926,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embed_bwd", &embed_bwd);
   m.def("text_mask", &text_mask);
   m.def("sumsq", &sumsq);
-  m.def("adamw", &adamw);
+  m.def("adamw", &adamw, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("shadow"), py::arg("hyper"),
+        py::arg("eps"), py::arg("wd"), py::arg("clip"), py::arg("gscale"), py::arg("l2") = false);
   m.def("cast_bf16", &cast_bf16);
   m.def("reduce_probe", &reduce_probe);
   m.def("fold_replicas", &fold_replicas);

@@ -187,13 +187,27 @@ __global__ void text_mask_kernel(const int64_t* __restrict__ x, const bool* __re
 }
 
 // sum of squares of the flat gradient (for clip_grad_norm) → atomic into out[0]
+// 16-byte loads, four independent accumulation chains, ≈4 workgroups per CU
 __global__ void sumsq_kernel(const float* __restrict__ g, long long n, float* __restrict__ out) {
-  float s = 0.f;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    const float v = g[i];
-    s += v * v;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  const long long n4 = ((reinterpret_cast<uintptr_t>(g) & 15) == 0) ? n >> 2 : 0;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + stride < n4; i += 2 * stride) {
+    const float4 a = g4[i], b = g4[i + stride];
+    s0 = fmaf(a.x, a.x, s0); s1 = fmaf(a.y, a.y, s1); s2 = fmaf(a.z, a.z, s2); s3 = fmaf(a.w, a.w, s3);
+    s0 = fmaf(b.x, b.x, s0); s1 = fmaf(b.y, b.y, s1); s2 = fmaf(b.z, b.z, s2); s3 = fmaf(b.w, b.w, s3);
   }
-  s = wave_sum(s);
+  for (; i < n4; i += stride) {
+    const float4 a = g4[i];
+    s0 = fmaf(a.x, a.x, s0); s1 = fmaf(a.y, a.y, s1); s2 = fmaf(a.z, a.z, s2); s3 = fmaf(a.w, a.w, s3);
+  }
+  for (long long j = (n4 << 2) + (long long)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
+    const float v = g[j];
+    s0 = fmaf(v, v, s0);
+  }
+  float s = wave_sum((s0 + s1) + (s2 + s3));
   __shared__ float red[16];
   if (lane_id() == 0) red[wave_id()] = s;
   __syncthreads();
@@ -209,7 +223,8 @@ __global__ void sumsq_kernel(const float* __restrict__ g, long long n, float* __
 // replays of a captured step.
 __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                              float* __restrict__ v, uint16_t* __restrict__ shadow, long long n,
-                             const float* __restrict__ hyper, float eps, float wd, float clip, float gscale) {
+                             const float* __restrict__ hyper, float eps, float wd, float clip, float gscale,
+                             int l2) {
   const float lr = hyper[0], step = hyper[1], beta1 = hyper[3], beta2 = hyper[4];
   const float bc1 = 1.f - powf(beta1, step), bc2 = 1.f - powf(beta2, step);
   // g holds the all-reduced SUM over ranks (gscale = 1 / world makes it the mean): the clip
@@ -223,9 +238,11 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
   const float step_size = lr / bc1;
   const float bc2s = sqrtf(bc2);
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    const float gi = g[i] * gs;
     float pi = p[i];
-    pi *= 1.f - lr * wd;
+    // l2 (torch.optim.Adam weight_decay): the decay joins the (clipped) gradient; else AdamW's
+    // decoupled decay of the weights
+    const float gi = l2 ? fmaf(wd, pi, g[i] * gs) : g[i] * gs;
+    if (!l2) pi *= 1.f - lr * wd;
     const float mi = beta1 * m[i] + (1.f - beta1) * gi;
     const float vi = beta2 * v[i] + (1.f - beta2) * gi * gi;
     m[i] = mi;
@@ -283,11 +300,41 @@ void text_mask_launch(const int64_t* x, const bool* pad, const float* u, const i
   hipLaunchKernelGGL(text_mask_kernel, grid_for(n), dim3(256), 0, st, x, pad, u, rid, xm, labels, n, unk_id, mask_id, p);
 }
 void sumsq_launch(const float* g, long long n, float* out, hipStream_t st) {
-  hipLaunchKernelGGL(sumsq_kernel, grid_for(n, 1024), dim3(256), 0, st, g, n, out);
+  long long b = (n + 4095) / 4096;
+  b = b > 1024 ? 1024 : (b < 1 ? 1 : b);
+  hipLaunchKernelGGL(sumsq_kernel, dim3((unsigned)b), dim3(256), 0, st, g, n, out);
+}
+
+// dst[idx[r]][:] += src[r][:] — the backward of a row gather (rows of idx may repeat: fp32
+// atomics; an index outside dst is skipped).  One thread per 4 columns.
+__global__ void index_add_rows_kernel(float* __restrict__ dst, long long nrows, const int64_t* __restrict__ idx,
+                                      const float* __restrict__ src, long long R, int C) {
+  const int c4 = C >> 2;
+  const long long total = R * c4;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / c4;
+    const int c = (int)(i - r * c4) * 4;
+    const long long d = idx[r];
+    const float4 v = *reinterpret_cast<const float4*>(src + r * C + c);
+    // all-zero quads (padding rows of a fixed-capacity gather) skip their atomics: padding
+    // slots often share one destination row, whose serialised atomics would dominate
+    const bool nz = v.x != 0.f || v.y != 0.f || v.z != 0.f || v.w != 0.f;
+    if (nz && d >= 0 && d < nrows) {
+      float* p = dst + d * C + c;
+      atomicAdd(p, v.x);
+      atomicAdd(p + 1, v.y);
+      atomicAdd(p + 2, v.z);
+      atomicAdd(p + 3, v.w);
+    }
+  }
+}
+void index_add_rows_launch(float* dst, long long nrows, const int64_t* idx, const float* src, long long R, int C,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(index_add_rows_kernel, grid_for(R * (C / 4)), dim3(256), 0, st, dst, nrows, idx, src, R, C);
 }
 void adamw_launch(float* p, const float* g, float* m, float* v, uint16_t* shadow, long long n, const float* hyper,
-                  float eps, float wd, float clip, float gscale, hipStream_t st) {
-  hipLaunchKernelGGL(adamw_kernel, grid_for(n), dim3(256), 0, st, p, g, m, v, shadow, n, hyper, eps, wd, clip, gscale);
+                  float eps, float wd, float clip, float gscale, int l2, hipStream_t st) {
+  hipLaunchKernelGGL(adamw_kernel, grid_for(n), dim3(256), 0, st, p, g, m, v, shadow, n, hyper, eps, wd, clip, gscale, l2);
 }
 // grad[i] += Σ_r rep[r][i], rep[r][i] ← 0 (replicated gradient accumulators, see ops/optim.py)
 __global__ void fold_replicas_kernel(float* __restrict__ grad, float* __restrict__ rep, long long n, int nrep) {

@@ -74,11 +74,17 @@ class PerceiverEncoder(nn.Module):
         b = x.shape[0]
         if attn_mask is None and ops.use_hip(self.latent):
             return ops.fused.encoder_forward(self, x, pad_mask), pad_mask
-        x = self.input_adapter(x)
-        x_latent = self.latent.unsqueeze(0).expand(b, -1, -1)
+        return self.forward_inputs(self.input_adapter(x), pad_mask, attn_mask), pad_mask
+
+    def forward_inputs(self, x_in, pad_mask=None, attn_mask=None):
+        """Latents for already adapted inputs ``x_in`` (B, M, Kin), bypassing the input adapter
+        (used for sparse image inputs: the adapter's rows gathered at the non-zero pixels)."""
+        if attn_mask is None and ops.use_hip(self.latent):
+            return ops.fused.encode_inputs(self, x_in, pad_mask)
+        x_latent = self.latent.unsqueeze(0).expand(x_in.shape[0], -1, -1)
         for layer in self.layers():
-            x_latent = layer(x_latent, x, pad_mask, attn_mask)
-        return x_latent, pad_mask
+            x_latent = layer(x_latent, x_in, pad_mask, attn_mask)
+        return x_latent
 
 
 class PerceiverDecoder(nn.Module):
@@ -111,6 +117,17 @@ class PerceiverDecoder(nn.Module):
         self.check_latent(x)
         q = self.output if num_queries is None else self.output[:num_queries]
         return self.cross_attention(q.unsqueeze(0).expand(x.shape[0], -1, -1), x)
+
+    def hidden_at(self, x, idx):
+        """Decoder output at output-query rows ``idx`` (B, K') only, ``(B, K', C_out)``: queries
+        never interact, so this equals ``hidden(x)`` gathered at ``idx``.  The gather's backward
+        adds straight into the query parameter's gradient rows."""
+        from ..ops.mlm_head import _GatherQueries
+
+        x = bucket_ready_point(x)
+        self.check_latent(x)
+        q = _GatherQueries.apply(self.output, idx.reshape(-1)).view(idx.shape[0], idx.shape[1], -1)
+        return self.cross_attention(q, x)
 
     def forward(self, x, pad_mask=None):
         return self.output_adapter(self.hidden(x))

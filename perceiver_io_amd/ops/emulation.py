@@ -479,7 +479,7 @@ def sumsq(g, out):
     out += (g.float() ** 2).sum()
 
 
-def adamw(p, g, m, v, shadow, hyper, eps, wd, clip, gscale):
+def adamw(p, g, m, v, shadow, hyper, eps, wd, clip, gscale, l2=False):
     lr, step, b1, b2 = float(hyper[0]), float(hyper[1]), float(hyper[3]), float(hyper[4])
     gs = gscale
     if clip > 0:
@@ -488,7 +488,10 @@ def adamw(p, g, m, v, shadow, hyper, eps, wd, clip, gscale):
         if f < 1:
             gs *= f
     gg = g * gs
-    p.mul_(1 - lr * wd)
+    if l2:  # torch.optim.Adam: coupled L2 decay added to the (clipped) gradient
+        gg = gg + wd * p
+    else:
+        p.mul_(1 - lr * wd)
     m.mul_(b1).add_(gg, alpha=1 - b1)
     v.mul_(b2).addcmul_(gg, gg, value=1 - b2)
     bc1, bc2 = 1 - b1 ** step, 1 - b2 ** step
@@ -521,3 +524,52 @@ def get_deterministic():
 
 def cast_bf16(x, y):
     y.copy_(x.to(torch.bfloat16).view(y.shape))
+
+
+def index_add_rows(dst, idx, src):
+    dst.index_add_(0, idx, src.to(dst.dtype))
+
+
+def _pixel_logits(h, w, b):
+    return h.float() @ w.float().t() + b.float()
+
+
+def pixel_ce_fwd(h, w, b, labels, wts):
+    """(stats, loss): stats = [Σ w·ce, Σ w, n(lab>0), hit(lab>0), (n_k, hit_k)… | acc, acc_1…]
+    (pixel_head.hip), loss = Σ w·ce / Σ w."""
+    part = _pixel_ce_sums(h, w, b, labels, wts)
+    K = w.shape[0]
+
+    def ratio(hit, n):
+        return torch.where(n > 0, hit / n.clamp(min=1), torch.zeros_like(n))
+
+    accs = [ratio(part[3], part[2])] + [ratio(part[5 + 2 * k], part[4 + 2 * k]) for k in range(1, K)]
+    return torch.cat([part, torch.stack(accs)]), part[0] / part[1]
+
+
+def _pixel_ce_sums(h, w, b, labels, wts):
+    K = w.shape[0]
+    z = _pixel_logits(h, w, b)
+    valid = (labels >= 0) & (labels < K)
+    lab = labels.clamp(0, K - 1)
+    ce = torch.logsumexp(z, -1) - z.gather(1, lab[:, None])[:, 0]
+    wl = torch.where(valid, wts[lab], torch.zeros_like(ce))
+    hit = (z.argmax(-1) == lab) & valid
+    out = [(wl * ce).sum(), wl.sum(), (valid & (lab > 0)).sum().float(), (hit & (lab > 0)).sum().float()]
+    for k in range(K):
+        out += [(valid & (lab == k)).sum().float(), (hit & (lab == k)).sum().float()]
+    return torch.stack(out)
+
+
+def pixel_ce_bwd(h, w, b, labels, wts, gout, stats, dH, dW, db):
+    gscale = gout.reshape(1).float() / stats[1]
+    K, C = w.shape
+    z = _pixel_logits(h, w, b)
+    valid = (labels >= 0) & (labels < K)
+    lab = labels.clamp(0, K - 1)
+    p = torch.softmax(z, -1)
+    coef = p - torch.nn.functional.one_hot(lab, K).float()
+    coef = coef * (torch.where(valid, wts[lab], torch.zeros_like(p[:, 0])) * gscale.float())[:, None]
+    dH.copy_(coef @ w.float())
+    dW += (coef.t() @ h.float()).view_as(dW)
+    db += coef.sum(0)

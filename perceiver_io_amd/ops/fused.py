@@ -210,8 +210,22 @@ def layer_spec_and_params(layer):
     return spec, ps
 
 
+def _kv_weight(spec: LayerSpec, ps):
+    """bf16 K‖V projection weight of a cross layer with kdim ≠ embed_dim, rows zero padded to a
+    multiple of 8 columns (vectorised weight staging in the kernels).  Built only where the K/V
+    projection runs (once per forward for a weight-shared layer)."""
+    wc = weight_cache
+    wk, wv = wc.get(ps[5]), wc.get(ps[6])
+    kin = wk.shape[1]
+    wkv = torch.zeros((2 * spec.C, (kin + 7) // 8 * 8), dtype=wk.dtype, device=wk.device)
+    wkv[: spec.C, :kin] = wk
+    wkv[spec.C:, :kin] = wv
+    return wkv
+
+
 def _bf16_weights(spec: LayerSpec, ps):
-    """bf16 GEMM operands: (w_q_or_qkv, w_kv or None, w_o, w_1, w_2)."""
+    """bf16 GEMM operands: (w_q_or_qkv, w_kv (packed layers; None otherwise, see _kv_weight),
+    w_o, w_1, w_2)."""
     wc = weight_cache
     if spec.cross:
         if spec.packed:
@@ -219,13 +233,7 @@ def _bf16_weights(spec: LayerSpec, ps):
             wq, wkv = win[: spec.C], win[spec.C:]
             rest = ps[5:]
         else:
-            wq = wc.get(ps[4])
-            wk, wv = wc.get(ps[5]), wc.get(ps[6])
-            kin = wk.shape[1]
-            # rows zero padded to a multiple of 8 columns: vectorised weight staging in the kernels
-            wkv = torch.zeros((2 * spec.C, (kin + 7) // 8 * 8), dtype=wk.dtype, device=wk.device)
-            wkv[: spec.C, :kin] = wk
-            wkv[spec.C:, :kin] = wv
+            wq, wkv = wc.get(ps[4]), None
             rest = ps[7:]
     else:
         wq, wkv = wc.get(ps[2]), None
@@ -375,9 +383,11 @@ class _LayerFn(torch.autograd.Function):
                     kv, mean_kv, rstd_kv = _pe_proj_fwd(K, xkv2, src.pe, g_kv, b_kv,
                                                         torch.cat([ps[5], ps[6]], 0), bin_[C:])
                 else:
+                    if wkv is None:
+                        wkv = _kv_weight(spec, ps)
                     kv, mean_kv, rstd_kv = K.ln_linear_fwd(xkv2, g_kv, b_kv, EPS, wkv, bin_[C:], 0, None, True, True,
                                                            src.pe if src is not None else None, g_kv.shape[0])
-                ent = {"kv": kv, "mean": mean_kv, "rstd": rstd_kv, "dkv": None, "factored": factored}
+                ent = {"kv": kv, "mean": mean_kv, "rstd": rstd_kv, "dkv": None, "factored": factored, "wkv": wkv}
                 if src is not None:
                     src.entries[key] = ent
             kv, mean_kv, rstd_kv = ent["kv"], ent["mean"], ent["rstd"]
@@ -423,6 +433,8 @@ class _LayerFn(torch.autograd.Function):
             g_q, b_q, g_kv, b_kv = ps[0:4]
             rest = ps[5:] if spec.packed else ps[7:]
             ibias = 5 if spec.packed else 7
+            if wkv is None:
+                wkv = ctx.kv_entry.get("wkv")
         else:
             g_q, b_q = ps[0:2]
             rest = ps[3:]
@@ -837,6 +849,16 @@ def encoder_forward(encoder, x, pad_mask=None):
         src = KVSource(pix, pe=ad.padded_position_encoding(), kin=ad.num_input_channels)
     else:
         src = KVSource(ad(x))
+    return _encode(encoder, src, pad_mask)
+
+
+def encode_inputs(encoder, x_in, pad_mask=None):
+    """The encoder body over already adapted inputs ``x_in`` (B, M, Kin) — e.g. the gathered
+    ``[pixel ‖ PE]`` rows of a sparse image (``models/lartpc.py``)."""
+    return _encode(encoder, KVSource(x_in.float().contiguous()), pad_mask)
+
+
+def _encode(encoder, src: KVSource, pad_mask):
     lat = encoder.latent.unsqueeze(0)  # (1, N, C): projected once, broadcast inside the kernels
     b = src.x.shape[0]
     for layer in encoder.layers():

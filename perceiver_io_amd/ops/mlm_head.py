@@ -209,10 +209,15 @@ class _GatherQueries(torch.autograd.Function):
             return None, None
         if p.grad is None:
             p.grad = torch.zeros_like(p)
-        from . import deterministic
+        from . import deterministic, use_hip
 
         if deterministic():
             p.grad.index_put_((idx,), g.to(p.grad.dtype), accumulate=True)
+        elif use_hip(g) and p.grad.dim() == 2 and p.grad.is_contiguous() and p.grad.shape[1] % 4 == 0:
+            from .fused import kernels
+
+            src = g.reshape(-1, p.grad.shape[1]).to(p.grad.dtype).contiguous()
+            kernels(g).index_add_rows(p.grad, idx.contiguous(), src)
         else:
             p.grad.index_add_(0, idx, g.to(p.grad.dtype))
         return None, None

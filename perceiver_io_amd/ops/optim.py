@@ -171,6 +171,7 @@ class FusedAdamW(torch.optim.Optimizer):
         self.exp_avg_sq = torch.zeros(self.flat.numel, dtype=torch.float32, device=dev)
         self.hyper = torch.zeros(8, dtype=torch.float32, device=dev)
         self.max_grad_norm = float(max_grad_norm)
+        self.l2 = False  # decoupled decay (AdamW); FusedAdam sets the coupled L2 form
         self._step = 0
         self._ring = _HostRing(8, 8, dev) if dev.type == "cuda" else None
         self.grad_scale = 1.0
@@ -200,7 +201,7 @@ class FusedAdamW(torch.optim.Optimizer):
                 self.hyper[2:3].zero_()
                 K.sumsq(self.flat.grad, self.hyper[2:3])
         K.adamw(self.flat.data, self.flat.grad, self.exp_avg, self.exp_avg_sq, self.flat.shadow, self.hyper,
-                g["eps"], g["weight_decay"], self.max_grad_norm, self.grad_scale)
+                g["eps"], g["weight_decay"], self.max_grad_norm, self.grad_scale, l2=self.l2)
 
     @torch.no_grad()
     def step(self, closure=None, staged: bool = False):
@@ -240,3 +241,18 @@ class FusedAdamW(torch.optim.Optimizer):
                 es[i].copy_(st["exp_avg_sq"])
             step = int(float(st.get("step", 0)))
         self._step = step
+
+
+class FusedAdam(FusedAdamW):
+    """``torch.optim.Adam`` semantics (coupled L2: ``weight_decay · p`` joins the gradient after
+    clipping) in the same single fused kernel — the optimizer of the LArTPC experiment
+    (reference ``run.py:134``: ``Adam(lr=1e-3, weight_decay=1e-4)`` + ``clip_grad_norm_(10)``).
+    Parameters whose gradient is identically zero still decay, exactly as torch.optim.Adam does
+    for parameters that took part in the backward; leave parameters that never receive a
+    gradient (torch skips ``grad is None``) out of ``params``."""
+
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
+                 amsgrad: bool = False, max_grad_norm: float = 0.0, flat: Optional[FlatParameterSpace] = None):
+        super().__init__(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=amsgrad,
+                         max_grad_norm=max_grad_norm, flat=flat)
+        self.l2 = True

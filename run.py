@@ -1,20 +1,36 @@
 #!/usr/bin/env python
 """LArTPC per-pixel semantic segmentation with Perceiver IO (reference ``run.py``).
 
-512×512 single-plane wire images → 3 classes per pixel.  Perceiver IO with a Fourier-encoded
-image input (262,144 inputs, key-padding mask on zero pixels = sparse attention), 32×64
-latents, 3 layers × (1 cross + 3 self-attention), and a decoder with 262,144 output queries
-(one per pixel) → 3-way classifier.  A U-ResNet is constructed alongside (unused in forward,
-as in the reference).  Weighted cross-entropy (background weight 0), Adam (lr 1e-3, wd 1e-4),
-ReduceLROnPlateau stepped on the loss before backward, grad-norm clip 10, batch 4, per-class
-accuracies, validation each epoch, checkpoint ``{'epoch','model_state_dict','optimizer_state_dict'}``.
+512×512 single-plane wire images → 3 classes per pixel (background / track / shower).  The
+model is the reference's (``perceiver_io_amd/models/lartpc.py``): Fourier-encoded image input,
+32×64 latents, 3 layers × (1 cross + 3 self-attention), one decoder query per pixel, a 3-way
+classifier, and a U-ResNet built alongside (unused, as in the reference).  Training follows
+the reference: weighted cross-entropy with background weight 0, Adam (lr 1e-3, L2 weight decay
+1e-4), grad-norm clip 10, ReduceLROnPlateau(patience 5000, factor 0.1) stepped on the training
+loss, batch 4, per-class accuracies, validation each epoch, and a checkpoint
+``{'epoch', 'model_state_dict', 'optimizer_state_dict'}``.
 
-Differences (documented): the larcv/ROOT reader is replaced by a synthetic track/shower
-generator (``perceiver_io_amd.data.synthetic.lartpc_event``; larcv/ROOT are not available);
-logits are permuted to (B, 3, H·W) instead of the reference's ``reshape(B, 3, -1)`` which
-interleaves pixels and classes (defect D6); metrics go to JSONL/tfevents.
+On a GPU the default is the MI355X path:
 
-    python run.py [--epochs 10] [--events 64] [--size 512] [--batch-size 4]
+* **sparse execution** (``models/lartpc.py``).  The encoder sees only the non-zero pixels and
+  the decoder only the weighted pixels.  Loss and gradients are the same as the dense model's.
+  Pass ``--dense`` to run all 262,144 keys and queries, the reference's cost.
+* **fused kernels + hipGraph step** (``StepEngine``).  One graph is captured per capacity bucket.
+  ``FusedAdam`` does the coupled-L2 Adam update and the clip in one kernel pass.
+  ReduceLROnPlateau reads the previous step's loss, so the host never waits on the step in
+  flight.  The reference steps it on the current loss; with patience 5000 the one-step lag
+  changes nothing in practice.
+
+``--engine eager`` (the default on CPU) runs the reference sequence exactly: zero_grad,
+forward, ``scheduler.step(loss)``, backward, ``clip_grad_norm_``, ``Adam.step``.
+
+Documented differences: a synthetic track/shower generator stands in for the larcv/ROOT
+reader (``data/synthetic.py:lartpc_event``), because larcv and ROOT are not available.
+Logits are permuted to (B, 3, H·W) instead of reshaped (defect D6).  Metrics go to
+tfevents/JSONL.  With the fused optimizer, ``optimizer_state_dict`` covers the trained (Perceiver)
+parameters.  The unused U-ResNet never has a gradient, and torch's Adam skips it too.
+
+    python run.py [--epochs 10] [--events 64] [--size 512] [--batch-size 4] [--dense] [--engine eager]
 """
 from __future__ import annotations
 
@@ -28,40 +44,33 @@ import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+from perceiver_io_amd.data.lartpc import SparseCollator  # noqa: E402
 from perceiver_io_amd.data.synthetic import SyntheticLArTPC  # noqa: E402
-from perceiver_io_amd.models import (ClassificationOutputAdapter, ImageInputAdapter, PerceiverDecoder,  # noqa: E402
-                                     PerceiverEncoder, PerceiverIO)
-from perceiver_io_amd.models.uresnet import UResNet  # noqa: E402
+from perceiver_io_amd.models.lartpc import LArPerceiver, accuracies, class_weights  # noqa: E402
 from perceiver_io_amd.train.loggers import TensorBoardLogger  # noqa: E402
 
-
-class LArPerceiver(torch.nn.Module):
-    def __init__(self, size: int = 512, latents=(32, 64), bands: int = 32):
-        super().__init__()
-        n, c = latents
-        enc = PerceiverEncoder(ImageInputAdapter((size, size, 1), bands), (n, c), num_layers=3,
-                               num_cross_attention_heads=4, num_self_attention_heads=4,
-                               num_self_attention_layers_per_block=3, dropout=0.0)
-        dec = PerceiverDecoder(ClassificationOutputAdapter(num_classes=3, num_outputs=size * size, num_output_channels=c),
-                               (n, c), num_cross_attention_heads=1, dropout=0.0)
-        self.size = size
-        self.perceiver = PerceiverIO(enc, dec)
-        self.uresnet = UResNet(num_classes=3, input_channels=c, inplanes=16)
-
-    def forward(self, img):
-        b = img.shape[0]
-        x = img.reshape(b, self.size, self.size, 1)
-        mask = (x == 0).reshape(b, -1)  # zero pixels are padding keys (sparse attention)
-        logits = self.perceiver(x, mask)  # (B, H*W, 3)
-        return logits.permute(0, 2, 1)  # (B, 3, H*W)
+__all__ = ["LArPerceiver", "accuracies", "main"]
 
 
-def accuracies(pred, lab):
-    out = {}
-    for name, sel in (("acc", lab > 0), ("acc1", lab == 1), ("acc2", lab == 2)):
-        n = sel.sum()
-        out[name] = ((pred[sel] == lab[sel]).float().mean().item() if n > 0 else 0.0)
-    return out
+def _to(batch, dev):
+    return tuple(t.to(dev, non_blocking=True) for t in batch)
+
+
+def make_step_fn(model, weights, sparse: bool, metrics: dict):
+    """loss_fn(batch) → loss; per-class accuracies of the batch land in ``metrics`` (device)."""
+
+    def loss_fn(batch):
+        if sparse:
+            loss, acc = model.sparse_loss(batch, weights)
+        else:
+            img, lab = batch
+            out = model(img)
+            loss = F.cross_entropy(out, lab, weight=weights)
+            acc = accuracies(out.argmax(1).detach(), lab)
+        metrics.update(acc)
+        return loss
+
+    return loss_fn
 
 
 def main(argv=None):
@@ -76,52 +85,92 @@ def main(argv=None):
     ap.add_argument("--log-dir", default="runs")
     ap.add_argument("--ckpt-dir", default="ckpt")
     ap.add_argument("--device", default="cuda" if torch.cuda.is_available() else "cpu")
+    ap.add_argument("--engine", choices=["auto", "graph", "eager"], default="auto",
+                    help="graph: fused kernels + hipGraph step (GPU default); eager: the reference sequence")
+    ap.add_argument("--dense", action="store_true", help="evaluate all pixels (the reference's cost)")
+    ap.add_argument("--bucket", type=int, default=2048, help="sparse capacity rounding (keys / queries)")
+    ap.add_argument("--log-every", type=int, default=1)
+    ap.add_argument("--workers", type=int, default=1)
     a = ap.parse_args(argv)
     dev = torch.device(a.device)
     torch.manual_seed(0)
     model = LArPerceiver(a.size).to(dev)
+    weights = class_weights(dev)
+    sparse = not a.dense
+    collate = SparseCollator(a.bucket) if sparse else None
+    kw = dict(num_workers=a.workers, persistent_workers=a.workers > 0, collate_fn=collate)
     train = torch.utils.data.DataLoader(SyntheticLArTPC(a.events, a.size, seed=0), batch_size=a.batch_size,
-                                        shuffle=True, drop_last=True, num_workers=1)
+                                        shuffle=True, drop_last=True, **kw)
     val = torch.utils.data.DataLoader(SyntheticLArTPC(a.val_events, a.size, seed=1), batch_size=a.batch_size,
-                                      drop_last=True)
-    opt = torch.optim.Adam(model.parameters(), lr=a.lr, weight_decay=1e-4)
+                                      drop_last=True, collate_fn=collate)
+    fused = dev.type == "cuda" and a.engine != "eager"
+    if fused:
+        from perceiver_io_amd.ops.optim import FusedAdam
+        from perceiver_io_amd.train.engine import StepEngine
+
+        opt = FusedAdam(model.trained_parameters(), lr=a.lr, weight_decay=1e-4, max_grad_norm=10.0)
+    else:
+        opt = torch.optim.Adam(model.parameters(), lr=a.lr, weight_decay=1e-4)
     sched = torch.optim.lr_scheduler.ReduceLROnPlateau(opt, patience=5000, factor=0.1)
-    weights = torch.tensor([0.0, 1.0, 1.0], device=dev)
+    metrics: dict = {}
+    loss_fn = make_step_fn(model, weights, sparse, metrics)
+    engine = None
+    if fused:
+        engine = StepEngine(loss_fn, opt, None, device=dev, graph=True,
+                            state_hooks=(lambda: dict(metrics), lambda s: metrics.update(s)))
     log = TensorBoardLogger(a.log_dir, name="lartpc")
-    step = 0
-    epoch = 0
+    step, epoch, prev = 0, 0, None
+    t_start, n_timed = None, 0
     for epoch in range(a.epochs):
         model.train()
-        for img, lab in train:
+        for batch in train:
+            batch = _to(batch, dev)
             t0 = time.perf_counter()
-            img, lab = img.to(dev), lab.to(dev)
-            opt.zero_grad()
-            out = model(img)
-            loss = F.cross_entropy(out, lab, weight=weights)
-            sched.step(loss.item())  # stepped before backward, like the reference
-            loss.backward()
-            torch.nn.utils.clip_grad_norm_(model.parameters(), 10)
-            opt.step()
-            acc = accuracies(out.argmax(1), lab)
-            log.log_metrics({"loss": loss.item(), "lr": opt.param_groups[0]["lr"],
-                             **{f"train_{k}": v for k, v in acc.items()}}, step)
-            print(f"epoch {epoch} step {step} loss {loss.item():.4f} {time.perf_counter() - t0:.3f}s", flush=True)
+            if fused:
+                loss = engine.step(batch)
+                if prev is not None:
+                    sched.step(float(prev))  # the previous step's loss: no wait on this one
+                prev = loss
+            else:
+                opt.zero_grad()
+                loss = loss_fn(batch)
+                sched.step(loss.item())  # stepped before backward, like the reference
+                loss.backward()
+                torch.nn.utils.clip_grad_norm_(model.parameters(), 10)
+                opt.step()
+            if step == 2:  # throughput after graph capture / allocator warm-up
+                if dev.type == "cuda":
+                    torch.cuda.synchronize()
+                t_start, n_timed = time.perf_counter(), 0
+            elif t_start is not None:
+                n_timed += a.batch_size
+            if step % a.log_every == 0:
+                vals = {k: float(v) for k, v in metrics.items()}
+                log.log_metrics({"loss": float(loss), "lr": opt.param_groups[0]["lr"],
+                                 **{f"train_{k}": v for k, v in vals.items()}}, step)
+                print(f"epoch {epoch} step {step} loss {float(loss):.4f} acc {vals.get('acc', 0):.3f} "
+                      f"{time.perf_counter() - t0:.3f}s", flush=True)
             step += 1
             if 0 < a.max_steps <= step:
                 break
         model.eval()
         vl, va = [], []
         with torch.no_grad():
-            for img, lab in val:
-                img, lab = img.to(dev), lab.to(dev)
-                out = model(img)
-                vl.append(F.cross_entropy(out, lab, weight=weights).item())
-                va.append(accuracies(out.argmax(1), lab)["acc"])
+            for batch in val:
+                batch = _to(batch, dev)
+                vm: dict = {}
+                vl.append(float(make_step_fn(model, weights, sparse, vm)(batch)))
+                va.append(float(vm["acc"]))
         if vl:
             log.log_metrics({"validation_loss": sum(vl) / len(vl), "val_acc": sum(va) / len(va)}, step)
             print(f"validation loss: {sum(vl) / len(vl):.4f}", flush=True)
         if 0 < a.max_steps <= step:
             break
+    if t_start is not None and n_timed:
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        print(f"throughput: {n_timed / (time.perf_counter() - t_start):.1f} samples/s "
+              f"({'sparse' if sparse else 'dense'}, {'fused graph' if fused else 'eager'})", flush=True)
     os.makedirs(a.ckpt_dir, exist_ok=True)
     torch.save({"epoch": epoch, "model_state_dict": model.state_dict(), "optimizer_state_dict": opt.state_dict()},
                os.path.join(a.ckpt_dir, f"model_{epoch}.ckpt"))

@@ -98,6 +98,11 @@ def _attn_inputs(B, Bq, Nq, Nk, H, D, packed=True, mask=True):
     (2, 1, 40, 1200, 4, 16, 2),
     (2, 2, 64, 2000, 2, 64, 4),
     (2, 2, 33, 800, 1, 128, 2),
+    # many queries over a few keys (decoder pixel / token queries over the latents): the query
+    # range is split across workgroups, dK / dV partials added atomically
+    (4, 4, 4000, 32, 1, 64, 1),
+    (2, 2, 3000, 40, 4, 16, 1),
+    (2, 2, 2500, 64, 2, 32, 1),
 ])
 def test_attention_fwd_bwd(B, Bq, Nq, Nk, H, D, ns):
     torch.manual_seed(1)
@@ -154,6 +159,7 @@ def test_attention_dropout_statistics():
     (3, 3, 70, 200, 4, 16, 1, 0.1),
     (2, 1, 32, 900, 4, 32, 3, 0.3),
     (2, 2, 96, 64, 1, 64, 1, 0.5),
+    (2, 2, 1500, 32, 1, 64, 1, 0.2),
 ])
 def test_attention_dropout_matches_emulation(B, Bq, Nq, Nk, H, D, ns, p):
     """The kernels' hashed masks are reproduced bit-exactly by the emulation, so fwd AND bwd
@@ -482,3 +488,51 @@ def test_attention_bwd_pe_fused(B, Bq, Nq, M, H, nc, bsplit):
         res.append((dq1, dq, D, part.sum(0)))
     for a, b, n in zip(res[0], res[1], ("dq", "dq (2nd)", "D (2 applications)", "partials")):
         close(a, b, 2e-2, n)
+
+
+def test_index_add_rows_and_sumsq():
+    torch.manual_seed(11)
+    dst = torch.randn(1000, 64, device=DEV)
+    idx = torch.randint(0, 1000, (5000,), device=DEV)  # repeated rows
+    src = torch.randn(5000, 64, device=DEV)
+    ref = dst.clone().index_add_(0, idx, src)
+    _ext().index_add_rows(dst, idx, src)
+    close(dst, ref, 1e-5, "index_add_rows")
+    for n in (1, 1000, 17 * 1024 * 1024 + 3):
+        g = torch.randn(n, device=DEV)
+        out = torch.zeros(1, device=DEV)
+        _ext().sumsq(g, out)
+        ref = (g.double() ** 2).sum().float()
+        assert abs(out.item() - ref.item()) <= 1e-4 * ref.item(), (n, out.item(), ref.item())
+    g = torch.randn(4097, device=DEV)[1:]  # 4-byte aligned, not 16: scalar path
+    out = torch.zeros(1, device=DEV)
+    _ext().sumsq(g, out)
+    assert abs(out.item() - (g.double() ** 2).sum().item()) <= 1e-4 * out.item()
+
+
+@pytest.mark.parametrize("R,C,K", [(5000, 64, 3), (333, 32, 2), (1000, 128, 4), (17, 64, 3)])
+def test_pixel_ce_kernels(R, C, K):
+    """Fused per-pixel head + weighted CE (pixel_head.hip) vs the fp32 emulation."""
+    torch.manual_seed(12)
+    h = torch.randn(R, C, device=DEV)
+    W = torch.randn(K, C, device=DEV) * 0.3
+    b = torch.randn(K, device=DEV) * 0.1
+    lab = torch.randint(0, K, (R,), device=DEV)
+    lab[::5] = -100
+    wts = torch.rand(K, device=DEV) + 0.5
+    wts[0] = 0.0
+    (t1, l1), (t2, l2) = _ext().pixel_ce_fwd(h, W, b, lab, wts), _emu().pixel_ce_fwd(h, W, b, lab, wts)
+    close(t1[:2], t2[:2], 1e-4, "loss sums")
+    close(l1, l2, 1e-4, "loss")
+    ns = 4 + 2 * K
+    assert torch.equal(t1[2:ns], t2[2:ns]), (t1[2:ns], t2[2:ns])  # counts / hits exact
+    close(t1[ns:], t2[ns:], 1e-6, "accuracies")
+    gout = torch.tensor([0.7], device=DEV)
+    res = []
+    for Kx in (_ext(), _emu()):
+        d = torch.empty_like(h)
+        dW, db = torch.ones(K, C, device=DEV), torch.ones(K, device=DEV)  # accumulated onto
+        Kx.pixel_ce_bwd(h, W, b, lab, wts, gout, t2, d, dW, db)
+        res.append((d, dW, db))
+    for a, c, n in zip(res[0], res[1], ("dH", "dW", "db")):
+        close(a, c, 1e-4, n)
