@@ -134,7 +134,7 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(AttnArgs a, uint16_t
 
   for (int t0 = t_begin; t0 < t_end; t0 += NST) {
     const int rkey0 = t0 * KT;
-    __syncthreads();
+    lds_sync();
     if constexpr (PF) {
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
@@ -161,7 +161,7 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(AttnArgs a, uint16_t
     uint64_t padbits[NST];
 #pragma unroll
     for (int j = 0; j < NST; ++j) padbits[j] = __ballot(pad_next[j]);
-    __syncthreads();
+    lds_sync();
     if (PF && t0 + NST < t_end) fetch((t0 + NST) * KT);
 
 #pragma unroll
@@ -440,7 +440,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
   PIO_TS(1);
 
   for (int qt0 = qt_begin; qt0 < nqt; qt0 += NQS) {
-    __syncthreads();  // the previous round's tiles and dS slabs are consumed
+    lds_sync();  // the previous round's tiles and dS slabs are consumed
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int c = threadIdx.x + NTH * i, isdo = c >= NQS * 32 * CH, cc = isdo ? c - NQS * 32 * CH : c;
@@ -448,7 +448,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
     }
     if (threadIdx.x < NQS * 32) sL[threadIdx.x] = lreg;
     else if (threadIdx.x < NQS * 64) sDl[threadIdx.x - NQS * 32] = lreg;
-    __syncthreads();
+    lds_sync();
     PIO_TS(2 + 4 * ((qt0 - qt_begin) / NQS));
     if (qt0 + NQS < nqt) fetch(qt0 + NQS);
 
@@ -513,7 +513,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
       }
     }
     PIO_TS(3 + 4 * ((qt0 - qt_begin) / NQS));
-    __syncthreads();
+    lds_sync();
     PIO_TS(4 + 4 * ((qt0 - qt_begin) / NQS));
     // dQ of tile j = w: Σ over the block's keys of dS[key][q] · K[key][d]
     if (w < NQS && qt0 + w < nqt) {
@@ -570,7 +570,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
     if (vec_out && nqs == 1) {  // transpose through LDS (the dS slabs are consumed), 16-byte row stores
       constexpr int LDE = D + 4, CPR = D / 4;
       float* sE = reinterpret_cast<float*>(sdS);  // [dK | dV][KB keys][LDE]
-      __syncthreads();
+      lds_sync();
 #pragma unroll
       for (int i = 0; i < 16; ++i)
         if (r < D) {
@@ -578,7 +578,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
           sE[kl * LDE + r] = dK[0][i] * a.scale;
           sE[(KB + kl) * LDE + r] = dV[0][i];
         }
-      __syncthreads();
+      lds_sync();
 #pragma unroll
       for (int c = threadIdx.x; c < 2 * KB * CPR; c += NTH) {
         const int isv = c >= KB * CPR, cc = isv ? c - KB * CPR : c;
@@ -693,7 +693,7 @@ static void bwd_launch_t(const AttnArgs& a, const uint16_t* dO, const float* LSE
   }
   const int tps = (nqt + nqs - 1) / nqs;
   nqs = (nqt + tps - 1) / tps;  // no empty split
-  if (nqs > 1 && !kv_acc) {     // the splits add into dK / dV
+  if (nqs > 1 && !kv_acc) {      // the splits add into dK / dV
     const long long total = (long long)a.B * a.Nk * a.H * D;
     const unsigned zb = (unsigned)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
     hipLaunchKernelGGL(zero_rows_kernel, dim3(zb), dim3(256), 0, st, dk, dk_bs, dk_rs, a.Nk, a.H * D, total);
@@ -709,6 +709,8 @@ static void bwd_launch_t(const AttnArgs& a, const uint16_t* dO, const float* LSE
   }
   dim3 grid(nkb * nqs, a.H, a.B);
   const bool small_lds = !getenv_flag("PIO_ATTN_BWD_FULL_LDS");
+  // ≤ 64 queries (few-query cross-attention): the small-LDS variants let several workgroups
+  // share a CU
   if (a.Nq <= 32 && small_lds)
     hipLaunchKernelGGL((attn_bwd_kernel<D, NW, 1>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs,
                        dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs, nqs, tps);

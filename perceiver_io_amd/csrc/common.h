@@ -209,6 +209,18 @@ __device__ int trace_bx, trace_by, trace_bz;
 // contiguous 256-B no-return atomic instruction: S/32 adds per element in all.
 constexpr int kMaxSlabSegs = 16;
 constexpr int kSlabRowsPerBlock = 32;
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() is a workgroup-scope fence and
+// waits for every outstanding global load AND store of the thread (s_waitcnt vmcnt(0)), so a
+// register prefetch issued before it, or a row store just before it, puts a full memory
+// latency on the critical path at every LDS hand-off.  This barrier waits for LDS traffic only;
+// global loads stay in flight until their registers are used (the compiler's own waits).
+// Never use it where another thread of the workgroup reads global memory this thread wrote.
+__device__ __forceinline__ void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 struct SlabJob {
   const float* slab;  // nullptr: no job
   int S, P, nbx, nblk;

@@ -123,10 +123,10 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const uint16_t* __restrict_
   if (c_begin < c_end) fetch(c_begin);
   for (int c = c_begin; c < c_end; ++c) {
     const int v0 = c * VB;
-    __syncthreads();
+    lds_sync();
     store_rows<C>(wr, sW, LD);
     if (threadIdx.x < VB) sB[threadIdx.x] = bnext;
-    __syncthreads();
+    lds_sync();
     if (c + 1 < c_end) fetch(c + 1);
     const f32x16 acc = logits_tile_t<C>(sH, sW, LD);
     float t[16];
@@ -161,7 +161,7 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const uint16_t* __restrict_
     sMS[w & 1][rl][0] = mm;
     sMS[w & 1][rl][1] = ss;
   }
-  __syncthreads();
+  lds_sync();
   if (threadIdx.x < 64) {
     const int rr = threadIdx.x, g = m0 + rr;
     if (g < M) {
@@ -245,17 +245,17 @@ __global__ __launch_bounds__(256) void ce_bwd_dh_kernel(const uint16_t* __restri
   if (c_begin < c_end) fetch(c_begin);
   for (int c = c_begin; c < c_end; ++c) {
     const int v0 = c * VB;
-    __syncthreads();
+    lds_sync();
     store_rows<C>(wr, sW, LD);
     if (threadIdx.x < VB) sB[threadIdx.x] = bnext;
-    __syncthreads();
+    lds_sync();
     if (c + 1 < c_end) fetch(c + 1);
     const f32x16 acc = logits_tile_t<C>(sH, sW, LD);
     float b[16], d[16];
     vocab_regs(sB, b);
     dl_regs(acc, b, lse_l2, g, vocab_reg(lab - v0 - 32 * (w & 1)), d);
     store_dl_row(sL, LDL, rl, d);
-    __syncthreads();
+    lds_sync();
     // dH += dl (64 x 64 vocab) . Wchunk (64 vocab x C): A k-contiguous, B = W[v][c] k-strided
 #pragma unroll
     for (int t = 0; t < MAXT; ++t) {
@@ -267,7 +267,7 @@ __global__ __launch_bounds__(256) void ce_bwd_dh_kernel(const uint16_t* __restri
       }
     }
   }
-  __syncthreads();  // sDst is read across waves (no in-loop barrier has run for an empty split)
+  lds_sync();  // sDst is read across waves (no in-loop barrier has run for an empty split)
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) {
     const int tg = w + 4 * t;
@@ -325,15 +325,15 @@ __global__ __launch_bounds__(256) void ce_bwd_dw_kernel(const uint16_t* __restri
     else if (threadIdx.x < 128) aux = __int_as_float(gr < M ? (int)labels[gr] : -100);
   };
   if (mt_begin < mt_end) fetch(mt_begin);
-  __syncthreads();
+  lds_sync();
   float b[16];
   vocab_regs(sB, b);
   for (int mt = mt_begin; mt < mt_end; ++mt) {
-    __syncthreads();
+    lds_sync();
     store_rows<C>(hr, sH, LD);
     if (threadIdx.x < 64) sLse[threadIdx.x] = aux;
     else if (threadIdx.x < 128) sLab[threadIdx.x - 64] = __float_as_int(aux);
-    __syncthreads();
+    lds_sync();
     if (mt + 1 < mt_end) fetch(mt + 1);
     const f32x16 acc = logits_tile_t<C>(sH, sW, LD);
     const int lab = sLab[rl];
@@ -342,7 +342,7 @@ __global__ __launch_bounds__(256) void ce_bwd_dw_kernel(const uint16_t* __restri
 #pragma unroll
     for (int i = 0; i < 16; ++i) bsum[i] += d[i];
     store_dl_row(sL, LDL, rl, d);
-    __syncthreads();
+    lds_sync();
     // dW chunk (64 vocab x C) += dl^T . H : A = dl stored [r][v] (k=r strided), B = H [r][c] (k strided)
 #pragma unroll
     for (int t = 0; t < MAXT; ++t) {
@@ -361,7 +361,7 @@ __global__ __launch_bounds__(256) void ce_bwd_dw_kernel(const uint16_t* __restri
     const float v = half_sum(bsum[i]);
     if ((l & 31) == 0) sBs[w >> 1][32 * (w & 1) + acc_row(i, hh)] = v;
   }
-  __syncthreads();
+  lds_sync();
   // partials: atomics into dW / db, or (slab) plain stores into row blockIdx.y of a
   // (row splits, V·C + V₄) slab that a SlabJob later sums into dW | db (common.h)
   float* dWp = dW;
@@ -405,7 +405,7 @@ __global__ void select_rows_kernel(const int64_t* __restrict__ labels, int L, in
   __shared__ int sW[4], sOff;
   const int b = blockIdx.x, w = wave_id(), l = lane_id();
   if (threadIdx.x == 0) sOff = 0;
-  __syncthreads();
+  lds_sync();
   for (int c0 = 0; c0 < L; c0 += 256) {
     const int i = c0 + threadIdx.x;
     const int64_t lab = i < L ? labels[(long long)b * L + i] : -100;
@@ -413,7 +413,7 @@ __global__ void select_rows_kernel(const int64_t* __restrict__ labels, int L, in
     const uint64_t m = __ballot(sel);
     const int pre = __popcll(m & ((1ull << l) - 1ull));
     if (l == 0) sW[w] = __popcll(m);
-    __syncthreads();
+    lds_sync();
     int woff = 0;
     for (int k = 0; k < w; ++k) woff += sW[k];
     const int pos = sOff + woff + pre;
@@ -421,9 +421,9 @@ __global__ void select_rows_kernel(const int64_t* __restrict__ labels, int L, in
       idx_b[(long long)b * cap + pos] = i;
       lab_b[(long long)b * cap + pos] = lab;
     }
-    __syncthreads();
+    lds_sync();
     if (threadIdx.x == 0) sOff += sW[0] + sW[1] + sW[2] + sW[3];
-    __syncthreads();
+    lds_sync();
   }
   const int cnt = sOff;
   for (int j = (cnt < cap ? cnt : cap) + threadIdx.x; j < cap; j += blockDim.x) {
@@ -451,7 +451,7 @@ __global__ void select_global_kernel(const int* __restrict__ count, int B, int c
     total[0] = (float)all;
     overflow[0] = ovf || acc > gcap;
   }
-  __syncthreads();
+  lds_sync();
   const int used = sOffs[B] < gcap ? sOffs[B] : gcap;
   for (long long s = threadIdx.x; s < (long long)B * cap; s += blockDim.x) {
     const int b = (int)(s / cap), j = (int)(s - (long long)b * cap);

@@ -156,10 +156,35 @@ __device__ __forceinline__ int rp_row() { return threadIdx.x >> 2; }
 __device__ __forceinline__ int rp_col(int j) { return 8 * ((threadIdx.x & 3) + 4 * j); }
 __device__ __forceinline__ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// 32 bytes of zeros in global memory: the source of every out-of-range element of the fetches
+// below.  A load whose predicate is false reads here instead (an address select), so a
+// phase's loads are straight-line code.  hipcc waits for a load at the first branch, phi copy
+// or arithmetic that touches its result: a conditional load inside a fetch loop costs one full
+// memory latency per load instead of one per phase.
+__device__ __attribute__((aligned(16))) const float kZero32B[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+
 // row gr (< R) of a row-major [.. × K] matrix, this thread's chunks; zero outside
 template <int NCH, typename T>
 __device__ __forceinline__ void row_load(float (&v)[NCH][8], const T* __restrict__ base, long long rs, int gr, int R,
                                          int K, bool vec) {
+  if (vec) {  // branch-free (vec ⇒ 16-B aligned base, rs and K multiples of 8): zeros outside
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const int c = rp_col(j);
+      const bool ok = gr < R && c < K;
+      const T* src = ok ? base + (long long)gr * rs + c : reinterpret_cast<const T*>(kZero32B);
+      if constexpr (sizeof(T) == 2) {
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(src);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[j][e] = bf2f(b[e]);
+      } else {
+        const float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
+        v[j][0] = a.x; v[j][1] = a.y; v[j][2] = a.z; v[j][3] = a.w;
+        v[j][4] = b.x; v[j][5] = b.y; v[j][6] = b.z; v[j][7] = b.w;
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < NCH; ++j) {
     const int c = rp_col(j);
@@ -293,6 +318,16 @@ template <int NI>
 __device__ __forceinline__ void tile_fetch(bf16x8 (&b)[NI], const uint16_t* __restrict__ src, long long rs, int r0,
                                            int Rmax, int rows, int K, int KP, bool vec) {
   const int cpr = KP >> 3;
+  if (vec) {  // branch-free (vec ⇒ 16-B aligned src, rs and K multiples of 8): zeros outside
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int e = threadIdx.x + 256 * i, rr = e / cpr, cc = (e - rr * cpr) * 8, gr = r0 + rr;
+      const bool ok = rr < rows && gr < Rmax && cc < K;
+      const uint16_t* p = ok ? src + (long long)gr * rs + cc : reinterpret_cast<const uint16_t*>(kZero32B);
+      b[i] = *reinterpret_cast<const bf16x8*>(p);
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     const int e = threadIdx.x + 256 * i, rr = e / cpr, cc = (e - rr * cpr) * 8, gr = r0 + rr;
@@ -323,6 +358,23 @@ __device__ __forceinline__ void tile_store(const bf16x8 (&b)[NI], uint16_t* s, i
 template <typename TG>
 __device__ __forceinline__ void g_fetch(float (&v)[2][8], const TG* __restrict__ G, int g_rs, int m0, int R, int nc,
                                         int N, bool vec) {
+  if (vec) {  // branch-free (vec ⇒ 16-B aligned G, g_rs and N multiples of 8): zeros outside
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int rr = (threadIdx.x >> 3) + 32 * i, cc = (threadIdx.x & 7) * 8, gr = m0 + rr, gc = nc + cc;
+      const TG* p = (gr < R && gc < N) ? G + (long long)gr * g_rs + gc : reinterpret_cast<const TG*>(kZero32B);
+      if constexpr (sizeof(TG) == 2) {
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[i][e] = bf2f(b[e]);
+      } else {
+        const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+        v[i][0] = a.x; v[i][1] = a.y; v[i][2] = a.z; v[i][3] = a.w;
+        v[i][4] = b.x; v[i][5] = b.y; v[i][6] = b.z; v[i][7] = b.w;
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int rr = (threadIdx.x >> 3) + 32 * i, cc = (threadIdx.x & 7) * 8, gr = m0 + rr, gc = nc + cc;
@@ -365,7 +417,9 @@ constexpr int ln_linear_fwd_smem() { return 2 * 64 * (32 * NCH + 8) * 2 + 64 * 6
 
 // the LN + GEMM part of one 64-row tile: xv = this thread's rows (row-pass layout), wb = the
 // prefetched first W chunk, gw/gb = LN affine (read when has_ln); smem ≥ ln_linear_fwd_smem
-template <typename TOut, int NCH>
+// AV: every operand meets the vector-load preconditions (checked on the host) — the loads are
+// then straight-line code with no runtime layout branches (see kZero32B)
+template <typename TOut, int NCH, bool AV>
 __device__ __forceinline__ void ln_linear_fwd_tile(float (&xv)[NCH][8], bf16x8 (&wb)[NCH], const float (&gw)[NCH][8],
                                                    const float (&gb)[NCH][8], bool has_ln, int m0, int R, int Kin,
                                                    float eps, const uint16_t* __restrict__ W, int w_rs,
@@ -379,7 +433,7 @@ __device__ __forceinline__ void ln_linear_fwd_tile(float (&xv)[NCH][8], bf16x8 (
   float* sO = reinterpret_cast<float*>(sW + 64 * LD);   // [64][LDO] output chunk
   const int gr = m0 + rp_row(), w = wave_id(), l = lane_id();
   // W rows are w_rs apart (≥ Kin, zero padded): a multiple of 8 keeps the staging vectorised
-  const bool wvec = (w_rs & 7) == 0 && aligned16(W);
+  constexpr bool wvec = AV;
   const int wk = w_rs > Kin ? w_rs : Kin;
   const bool yvec = (N & 7) == 0 && (y_rs & 7) == 0 && aligned16(Y);
   if (has_ln) {
@@ -408,7 +462,7 @@ __device__ __forceinline__ void ln_linear_fwd_tile(float (&xv)[NCH][8], bf16x8 (
 
   for (int n0 = 0; n0 < N; n0 += 64) {
     tile_store<NCH>(wb, sW, LD, 64, KP);
-    __syncthreads();
+    lds_sync();
     if (n0 + 64 < N) tile_fetch<NCH>(wb, W, w_rs, n0 + 64, N, 64, wk, KP, wvec);
     const int bc = n0 + 32 * (w & 1) + (l & 31);
     const float bv = (bias && bc < N) ? bias[bc] : 0.f;
@@ -419,7 +473,7 @@ __device__ __forceinline__ void ln_linear_fwd_tile(float (&xv)[NCH][8], bf16x8 (
       if (act == 1) v = gelu_f(v);
       sO[m * LDO + n] = v;
     });
-    __syncthreads();
+    lds_sync();
     float ov[2][8];
     lds_row_read<2>(ov, sO, LDO);
     if (res) {
@@ -434,7 +488,7 @@ __device__ __forceinline__ void ln_linear_fwd_tile(float (&xv)[NCH][8], bf16x8 (
   }
 }
 
-template <typename TIn, typename TOut, int NCH>
+template <typename TIn, typename TOut, int NCH, bool AV>
 __global__ __launch_bounds__(256) void ln_linear_fwd_kernel(const TIn* __restrict__ X, int x_rs, int R, int Kin,
                                                             const float* __restrict__ lnw, const float* __restrict__ lnb,
                                                             float eps, const uint16_t* __restrict__ W, int w_rs,
@@ -447,16 +501,15 @@ __global__ __launch_bounds__(256) void ln_linear_fwd_kernel(const TIn* __restric
   const int m0 = blockIdx.x * 64, gr = m0 + rp_row();
   // phase 0: X rows, the first W chunk and the LN affine in flight together
   float xv[NCH][8];
-  row_load_x<NCH>(xv, X, x_rs, gr, R, Kin, (Kin & 7) == 0 && (x_rs & 7) == 0 && aligned16(X), ps);
+  row_load_x<NCH>(xv, X, x_rs, gr, R, Kin, AV, ps);
   bf16x8 wb[NCH];
-  tile_fetch<NCH>(wb, W, w_rs, 0, N, 64, w_rs > Kin ? w_rs : Kin, KP, (w_rs & 7) == 0 && aligned16(W));
+  tile_fetch<NCH>(wb, W, w_rs, 0, N, 64, w_rs > Kin ? w_rs : Kin, KP, AV);
   float gw[NCH][8], gb[NCH][8];
   if (lnw) {
-    const bool pvec = (Kin & 7) == 0 && aligned16(lnw) && aligned16(lnb);
-    row_load<NCH>(gw, lnw, 0, 0, 1, Kin, pvec);
-    row_load<NCH>(gb, lnb, 0, 0, 1, Kin, pvec);
+    row_load<NCH>(gw, lnw, 0, 0, 1, Kin, AV);
+    row_load<NCH>(gb, lnb, 0, 0, 1, Kin, AV);
   }
-  ln_linear_fwd_tile<TOut, NCH>(xv, wb, gw, gb, lnw != nullptr, m0, R, Kin, eps, W, w_rs, bias, N, act, res, res_rs, Y,
+  ln_linear_fwd_tile<TOut, NCH, AV>(xv, wb, gw, gb, lnw != nullptr, m0, R, Kin, eps, W, w_rs, bias, N, act, res, res_rs, Y,
                                 y_rs, mean_out, rstd_out, smem);
 }
 
@@ -467,7 +520,7 @@ __global__ __launch_bounds__(256) void ln_linear_fwd_kernel(const TIn* __restric
 // For C = 128 the weights share one LDS buffer, each fetched during the previous GEMM.
 // ------------------------------------------------------------------------------------
 // one 64-row tile; Z is also left in z (row-pass registers) for a fused epilogue
-template <int C>
+template <int C, bool AV>
 __device__ __forceinline__ void post_attn_fwd_body(
     const uint16_t* __restrict__ O, const float* __restrict__ X, const uint16_t* __restrict__ Wo,
     const float* __restrict__ bo, const float* __restrict__ g2, const float* __restrict__ be2, float eps,
@@ -484,8 +537,7 @@ __device__ __forceinline__ void post_attn_fwd_body(
   __shared__ __attribute__((aligned(16))) float sF[64 * LDF];
   __shared__ float sP[5][C];  // bo, b1, b2, γ2, β2
   const int m0 = blockIdx.x * 64, gr = m0 + rp_row();
-  const bool av = aligned16(O) && aligned16(X) && aligned16(Z) && aligned16(Ysave) && aligned16(Usave) &&
-                  aligned16(Wo) && aligned16(W1) && aligned16(W2);
+  constexpr bool av = AV;  // O, X, Z, Ysave, Usave, Wo, W1, W2 16-B aligned (host-checked)
 
   bf16x8 ob[NCH];
   tile_fetch<NCH>(ob, O, C, m0, R, 64, C, C, av);
@@ -503,14 +555,14 @@ __device__ __forceinline__ void post_attn_fwd_body(
   tile_store<NCH>(ob, sA, LD, 64, C);
 #pragma unroll
   for (int b = 0; b < NWB; ++b) tile_store<NIW>(wr[b], sW[b], LD, C, C);
-  __syncthreads();
+  lds_sync();
   if constexpr (NWB == 1) tile_fetch<NIW>(wr[0], W1, C, 0, C, C, C, C, av);
   f32x16 acc[MAXT];
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
   tile_gemm<MAXT, true, true>(sA, LD, sW[0], LD, 64, C, C, acc);
   for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) { sF[m * LDF + n] = acc[t][i] + sP[0][n]; });
-  __syncthreads();
+  lds_sync();
   if constexpr (NWB == 1) tile_store<NIW>(wr[0], sW[0], LD, C, C);
   // Y = X + attn-out; LN2 → sA
   {
@@ -540,13 +592,13 @@ __device__ __forceinline__ void post_attn_fwd_body(
       }
     lds_row_write_bf16<NCH>(sA, LD, t);
   }
-  __syncthreads();
+  lds_sync();
   if constexpr (NWB == 1) tile_fetch<NIW>(wr[0], W2, C, 0, C, C, C, C, av);
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
   tile_gemm<MAXT, true, true>(sA, LD, sW[NWB == 3 ? 1 : 0], LD, 64, C, C, acc);
   for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) { sF[m * LDF + n] = acc[t][i] + sP[1][n]; });
-  __syncthreads();
+  lds_sync();
   if constexpr (NWB == 1) tile_store<NIW>(wr[0], sW[0], LD, C, C);
   {
     float u[NCH][8];
@@ -558,12 +610,12 @@ __device__ __forceinline__ void post_attn_fwd_body(
       for (int e = 0; e < 8; ++e) u[j][e] = gelu_f(u[j][e]);
     lds_row_write_bf16<NCH>(sA, LD, u);
   }
-  __syncthreads();
+  lds_sync();
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
   tile_gemm<MAXT, true, true>(sA, LD, sW[NWB == 3 ? 2 : 0], LD, 64, C, C, acc);
   for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) { sF[m * LDF + n] = acc[t][i] + sP[2][n]; });
-  __syncthreads();
+  lds_sync();
   lds_row_read<NCH>(z, sF, LDF);
   drop_rows<NCH>(z, dr, 1u, gr, C);
 #pragma unroll
@@ -573,7 +625,7 @@ __device__ __forceinline__ void post_attn_fwd_body(
   row_store<NCH>(z, Z, C, gr, R, C, av);
 }
 
-template <int C>
+template <int C, bool AV>
 __global__ __launch_bounds__(256) void post_attn_fwd_kernel(
     const uint16_t* __restrict__ O, const float* __restrict__ X, const uint16_t* __restrict__ Wo,
     const float* __restrict__ bo, const float* __restrict__ g2, const float* __restrict__ be2, float eps,
@@ -581,7 +633,7 @@ __global__ __launch_bounds__(256) void post_attn_fwd_kernel(
     const float* __restrict__ b2, float* __restrict__ Z, float* __restrict__ Ysave, float* __restrict__ mean2,
     float* __restrict__ rstd2, uint16_t* __restrict__ Usave, int R, int Rx, DropCfg dr) {
   float z[C / 32][8];
-  post_attn_fwd_body<C>(O, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, Rx, dr, z);
+  post_attn_fwd_body<C, AV>(O, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, Rx, dr, z);
 }
 
 // ------------------------------------------------------------------------------------
@@ -591,7 +643,7 @@ __global__ __launch_bounds__(256) void post_attn_fwd_kernel(
 // per layer boundary, and Z is never re-read.  The QKV chunk-0 weights and the LN1 affine are
 // fetched in phase 0 with everything else.
 // ------------------------------------------------------------------------------------
-template <int C>
+template <int C, bool AV>
 __global__ __launch_bounds__(256) void post_attn_ln_linear_fwd_kernel(
     const uint16_t* __restrict__ O, const float* __restrict__ X, const uint16_t* __restrict__ Wo,
     const float* __restrict__ bo, const float* __restrict__ g2, const float* __restrict__ be2, float eps,
@@ -603,13 +655,13 @@ __global__ __launch_bounds__(256) void post_attn_ln_linear_fwd_kernel(
   constexpr int NCH = C / 32, KP = 32 * NCH;
   __shared__ __attribute__((aligned(16))) uint16_t smem[ln_linear_fwd_smem<NCH>() / 2];  // LN1+QKV half
   bf16x8 wb[NCH];
-  tile_fetch<NCH>(wb, Wq, C, 0, 3 * C, 64, C, KP, aligned16(Wq));
+  tile_fetch<NCH>(wb, Wq, C, 0, 3 * C, 64, C, KP, AV);
   float gw[NCH][8], gb[NCH][8];
-  row_load<NCH>(gw, lnw, 0, 0, 1, C, aligned16(lnw) && aligned16(lnb));
-  row_load<NCH>(gb, lnb, 0, 0, 1, C, aligned16(lnw) && aligned16(lnb));
+  row_load<NCH>(gw, lnw, 0, 0, 1, C, AV);
+  row_load<NCH>(gb, lnb, 0, 0, 1, C, AV);
   float z[NCH][8];
-  post_attn_fwd_body<C>(O, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, R, dr, z);
-  ln_linear_fwd_tile<uint16_t, NCH>(z, wb, gw, gb, true, blockIdx.x * 64, R, C, eps, Wq, C, bq, 3 * C, 0, nullptr, 0,
+  post_attn_fwd_body<C, AV>(O, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, R, dr, z);
+  ln_linear_fwd_tile<uint16_t, NCH, AV>(z, wb, gw, gb, true, blockIdx.x * 64, R, C, eps, Wq, C, bq, 3 * C, 0, nullptr, 0,
                                     QKV, 3 * C, mean1, rstd1, smem);
 }
 
@@ -705,7 +757,7 @@ constexpr int post_attn_bwd_smem() {
 
 // dz: this thread's rows of dZ (row-pass layout), loaded by the caller or produced by a fused
 // prologue (ln_linear_post_attn_bwd_kernel); smem ≥ post_attn_bwd_smem<C>() bytes, 16-B aligned
-template <int C>
+template <int C, bool AV>
 __device__ __forceinline__ void post_attn_bwd_body(
     float (&dz)[C / 32][8], const float* __restrict__ Ysave, const float* __restrict__ mean2,
     const float* __restrict__ rstd2, const uint16_t* __restrict__ U, const uint16_t* __restrict__ O,
@@ -724,8 +776,7 @@ __device__ __forceinline__ void post_attn_bwd_body(
   float(*sDb1)[C] = reinterpret_cast<float(*)[C]>(sF + 64 * LDF + 16 * C);
   float(*sP)[C] = reinterpret_cast<float(*)[C]>(sF + 64 * LDF + 18 * C);       // γ2, β2
   const int m0 = blockIdx.x * 64, gr = m0 + rp_row(), w = wave_id(), l = lane_id();
-  const bool av = aligned16(Ysave) && aligned16(U) && aligned16(O) && aligned16(dY) && aligned16(dO) &&
-                  aligned16(Wo) && aligned16(W1) && aligned16(W2);
+  constexpr bool av = AV;  // Ysave, U, O, dY, dO, Wo, W1, W2 16-B aligned (host-checked)
 
   // ---- phase 0: every input of the tile in flight at once
   float yv[NCH][8], t0[NCH][8];
@@ -734,10 +785,10 @@ __device__ __forceinline__ void post_attn_bwd_body(
   bf16x8 ob[NCH];
 #pragma unroll
   for (int j = 0; j < NCH; ++j) {
-    ob[j] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    if (gr < R) ob[j] = *reinterpret_cast<const bf16x8*>(O + (long long)gr * C + rp_col(j));
+    const uint16_t* p = gr < R ? O + (long long)gr * C + rp_col(j) : reinterpret_cast<const uint16_t*>(kZero32B);
+    ob[j] = *reinterpret_cast<const bf16x8*>(p);
   }
-  const float mu = gr < R ? mean2[gr] : 0.f, rs = gr < R ? rstd2[gr] : 0.f;
+  const float mu = *(gr < R ? mean2 + gr : kZero32B), rs = *(gr < R ? rstd2 + gr : kZero32B);
   bf16x8 wr[NWB][NIW];
   tile_fetch<NIW>(wr[0], W2, C, 0, C, C, C, C, av);
   if constexpr (NWB == 3) {
@@ -764,7 +815,7 @@ __device__ __forceinline__ void post_attn_bwd_body(
 #pragma unroll
   for (int b = 0; b < NWB; ++b) tile_store<NIW>(wr[b], sW[b], LD, C, C);
   colsum_partial<NCH>(dzm, sPart[0], C);
-  __syncthreads();
+  lds_sync();
   if constexpr (NWB == 1) tile_fetch<NIW>(wr[0], W1, C, 0, C, C, C, C, av);
 
   // ---- MLP output layer
@@ -793,7 +844,7 @@ __device__ __forceinline__ void post_attn_bwd_body(
       }
     }
   }
-  __syncthreads();
+  lds_sync();
   for (int k = threadIdx.x; k < C; k += blockDim.x) {
     gadd(rep(gr_out.db1, gr_out.vrs, gr_out.slab) + k,
          sDb1[0][k] + sDb1[1][k], gr_out.slab);
@@ -814,7 +865,7 @@ __device__ __forceinline__ void post_attn_bwd_body(
       }
     lds_row_write_bf16<NCH>(sX, LD, t0);
   }
-  __syncthreads();
+  lds_sync();
   if constexpr (NWB == 1) tile_fetch<NIW>(wr[0], Wo, C, 0, C, C, C, C, av);
 
   // ---- MLP hidden layer
@@ -823,7 +874,7 @@ __device__ __forceinline__ void post_attn_bwd_body(
   tile_gemm<MAXT, true, false>(sG, LD, sW[NWB == 3 ? 1 : 0], LD, 64, C, C, acc);  // dXn2 = dU · W1
   wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, rep(gr_out.dW1, gr_out.vrs, gr_out.slab), C, gr_out.slab);
   for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) { sF[m * LDF + n] = acc[t][i]; });
-  __syncthreads();
+  lds_sync();
   if constexpr (NWB == 1) tile_store<NIW>(wr[0], sW[0], LD, C, C);
   // ---- LN2 backward → dY = dZ + LN_bwd(dXn2); the O tile replaces LN2(Y) in sX
   {
@@ -857,7 +908,7 @@ __device__ __forceinline__ void post_attn_bwd_body(
 #pragma unroll
     for (int j = 0; j < NCH; ++j) *reinterpret_cast<bf16x8*>(sX + rp_row() * LD + rp_col(j)) = ob[j];
   }
-  __syncthreads();
+  lds_sync();
   for (int k = threadIdx.x; k < C; k += blockDim.x) {
     gadd(rep(gr_out.dg2, gr_out.vrs, gr_out.slab) + k,
          sPart[1][k] + sPart[1][C + k] + sPart[1][2 * C + k] + sPart[1][3 * C + k], gr_out.slab);
@@ -873,7 +924,7 @@ __device__ __forceinline__ void post_attn_bwd_body(
   tile_gemm<MAXT, true, false>(sG, LD, sW[NWB == 3 ? 2 : 0], LD, 64, C, C, acc);  // dO = dY · Wo
   wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, rep(gr_out.dWo, gr_out.vrs, gr_out.slab), C, gr_out.slab);
   for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) { sF[m * LDF + n] = bf2f(f2bf(acc[t][i])); });
-  __syncthreads();
+  lds_sync();
   {
     float dov[NCH][8];
     lds_row_read<NCH>(dov, sF, LDF);
@@ -895,7 +946,7 @@ __device__ __forceinline__ void post_attn_bwd_body(
   }
 }
 
-template <int C>
+template <int C, bool AV>
 __global__ __launch_bounds__(256) void post_attn_bwd_kernel(
     const float* __restrict__ dZ, const float* __restrict__ Ysave, const float* __restrict__ mean2,
     const float* __restrict__ rstd2, const uint16_t* __restrict__ U, const uint16_t* __restrict__ O,
@@ -908,8 +959,8 @@ __global__ __launch_bounds__(256) void post_attn_bwd_kernel(
     return;
   }
   float dz[C / 32][8];
-  row_load<C / 32>(dz, dZ, C, blockIdx.x * 64 + rp_row(), R, C, aligned16(dZ));
-  post_attn_bwd_body<C>(dz, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO, delta, H, gr_out, R, dr, smem);
+  row_load<C / 32>(dz, dZ, C, blockIdx.x * 64 + rp_row(), R, C, AV);
+  post_attn_bwd_body<C, AV>(dz, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO, delta, H, gr_out, R, dr, smem);
 }
 
 // ------------------------------------------------------------------------------------
@@ -923,7 +974,7 @@ constexpr int ln_linear_bwd_smem() {
 }
 
 // one 64-row tile; dX (incl. dres) is also left in dxo (row-pass registers) for a fused epilogue
-template <typename TG, typename TX, int NCH>
+template <typename TG, typename TX, int NCH, bool AV>
 __device__ __forceinline__ void ln_linear_bwd_body(
     const TG* __restrict__ G, int g_rs, int N, const uint16_t* __restrict__ W, int w_rs, int Kin,
     const TX* __restrict__ X,
@@ -939,18 +990,19 @@ __device__ __forceinline__ void ln_linear_bwd_body(
   float* sPart = sF + 64 * LDF;                          // [2][4][KP]
   float* sPb = sPart + 8 * KP;                           // [4][64]
   const int m0 = blockIdx.x * 64, gr = m0 + rp_row(), w = wave_id(), l = lane_id();
-  const bool gvec = (N & 7) == 0 && (g_rs & 7) == 0 && aligned16(G);
-  const bool wvec = (w_rs & 7) == 0 && aligned16(W);
+  // AV: G, W, X, the LN affine and dres meet the vector-load preconditions (host-checked)
+  constexpr bool gvec = AV, wvec = AV;
   const int wk = w_rs > Kin ? w_rs : Kin;  // W rows zero padded to w_rs
   const bool kvec = (Kin & 7) == 0;
 
   // ---- phase 0
   float xv[NCH][8], gw[NCH][8];
-  row_load_x<NCH>(xv, X, x_rs, gr, R, Kin, kvec && (x_rs & 7) == 0 && aligned16(X), ps);
+  row_load_x<NCH>(xv, X, x_rs, gr, R, Kin, AV, ps);
   float mu = 0.f, rs = 1.f;
   if (lnw) {
-    row_load<NCH>(gw, lnw, 0, 0, 1, Kin, kvec && aligned16(lnw));
-    if (gr < R) { mu = mean[gr]; rs = rstd[gr]; }
+    row_load<NCH>(gw, lnw, 0, 0, 1, Kin, AV);
+    mu = *(gr < R ? mean + gr : kZero32B);  // address selects: no conditional loads
+    rs = *(gr < R ? rstd + gr : kZero32B);
   }
   float gv[2][8];
   g_fetch<TG>(gv, G, g_rs, m0, R, 0, N, gvec);
@@ -959,7 +1011,7 @@ __device__ __forceinline__ void ln_linear_bwd_body(
   if (dW) {  // LN(X), the forward GEMM's A operand, for the weight gradient
     float xn[NCH][8];
     if (lnw) {
-      row_load<NCH>(xn, lnb, 0, 0, 1, Kin, kvec && aligned16(lnb));
+      row_load<NCH>(xn, lnb, 0, 0, 1, Kin, AV);
 #pragma unroll
       for (int j = 0; j < NCH; ++j)
 #pragma unroll
@@ -983,7 +1035,7 @@ __device__ __forceinline__ void ln_linear_bwd_body(
     float cs[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) cs[e] = gv[0][e] + gv[1][e];
-    __syncthreads();
+    lds_sync();
     if (nc + 64 < N) {
       g_fetch<TG>(gv, G, g_rs, m0, R, nc + 64, N, gvec);
       tile_fetch<NCH>(wb, W, w_rs, nc + 64, N, 64, wk, KP, wvec);
@@ -999,18 +1051,18 @@ __device__ __forceinline__ void ln_linear_bwd_body(
         }
       }
     }
-    __syncthreads();
+    lds_sync();
     if (dW && db && threadIdx.x < 64 && nc + (int)threadIdx.x < N) {
       const int t = threadIdx.x;
       gadd(rep(db, vrs, slab) + nc + t, sPb[t] + sPb[64 + t] + sPb[128 + t] + sPb[192 + t], slab);
     }
   }
   for_acc<MAXT>(64, KP, [&](int t, int m, int n, int i) { sF[m * LDF + n] = acc[t][i]; });
-  __syncthreads();
+  lds_sync();
 
   // ---- row pass: LN backward, residual gradient, LN parameter gradients
   float dr[NCH][8];
-  if (dres) row_load<NCH>(dr, dres, dres_rs, gr, R, Kin, kvec && (dres_rs & 7) == 0 && aligned16(dres));
+  if (dres) row_load<NCH>(dr, dres, dres_rs, gr, R, Kin, AV);
   float dxn[NCH][8];
   lds_row_read<NCH>(dxn, sF, LDF);
   if (lnw) {
@@ -1061,13 +1113,13 @@ __device__ __forceinline__ void ln_linear_bwd_body(
 #pragma unroll
     for (int e = 0; e < 8; ++e) dxo[j][e] = gw[j][e];
   if (lnw && dlnw) {
-    __syncthreads();
+    lds_sync();
     colsum_flush(sPart, KP, rep(dlnw, vrs, slab), Kin, slab);
     colsum_flush(sPart + 4 * KP, KP, rep(dlnb, vrs, slab), Kin, slab);
   }
 }
 
-template <typename TG, typename TX, int NCH>
+template <typename TG, typename TX, int NCH, bool AV>
 __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
     const TG* __restrict__ G, int g_rs, int N, const uint16_t* __restrict__ W, int w_rs, int Kin,
     const TX* __restrict__ X,
@@ -1081,7 +1133,7 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
     return;
   }
   float dxo[NCH][8];
-  ln_linear_bwd_body<TG, TX, NCH>(G, g_rs, N, W, w_rs, Kin, X, x_rs, mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs,
+  ln_linear_bwd_body<TG, TX, NCH, AV>(G, g_rs, N, W, w_rs, Kin, X, x_rs, mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs,
                                   dlnw, dlnb, dW, db, vrs, wrs, slab, R, ps, smem, dxo);
 }
 
@@ -1093,7 +1145,7 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
 // their parameter-gradient partials into ONE slab row per tile (12 segments).  C ≤ 64 (the
 // two halves' LDS must coexist: ≈117 KB at C = 64).
 // ------------------------------------------------------------------------------------
-template <int C>
+template <int C, bool AV>
 __global__ __launch_bounds__(256) void ln_linear_post_attn_bwd_kernel(
     const float* __restrict__ G, const uint16_t* __restrict__ Wq, const float* __restrict__ X,
     const float* __restrict__ mean1, const float* __restrict__ rstd1, const float* __restrict__ lnw,
@@ -1114,11 +1166,11 @@ __global__ __launch_bounds__(256) void ln_linear_post_attn_bwd_kernel(
     return;
   }
   float dz[NCH][8];
-  ln_linear_bwd_body<float, float, NCH>(G, 3 * C, 3 * C, Wq, C, C, X, C, mean1, rstd1, lnw, lnb, dres, C, nullptr, C,
+  ln_linear_bwd_body<float, float, NCH, AV>(G, 3 * C, 3 * C, Wq, C, C, X, C, mean1, rstd1, lnw, lnb, dres, C, nullptr, C,
                                         dlnw, dlnb, dWq, dbq, gr_out.vrs, gr_out.vrs, gr_out.slab, R, PeSplit{},
                                         reinterpret_cast<uint16_t*>(smem), dz);
-  __syncthreads();  // the ln_linear half's LDS traffic is done before the post-attention half reuses it
-  post_attn_bwd_body<C>(dz, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO, delta, H, gr_out, R, dr, smem);
+  lds_sync();  // the ln_linear half's LDS traffic is done before the post-attention half reuses it
+  post_attn_bwd_body<C, AV>(dz, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO, delta, H, gr_out, R, dr, smem);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1165,7 +1217,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const TG* __restrict__ G, in
   };
   if (r_begin < r_end) fetch(r_begin);
   for (int r0 = r_begin; r0 < r_end; r0 += 64) {
-    __syncthreads();  // previous tile's MFMAs done with sG / sA
+    lds_sync();  // previous tile's MFMAs done with sG / sA
     g_store(gv, sG, LDG);
 #pragma unroll
     for (int e = 0; e < 8; ++e) cs[e] += gv[0][e] + gv[1][e];
@@ -1180,7 +1232,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const TG* __restrict__ G, in
         av[j][e] = v;
       }
     lds_row_write_bf16<NCH>(sA, LDA, av);
-    __syncthreads();
+    lds_sync();
     if (r0 + 64 < r_end) fetch(r0 + 64);
     tile_gemm<MAXT, false, false>(sG, LDG, sA, LDA, 64, KP, 64, acc);
   }
@@ -1195,7 +1247,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const TG* __restrict__ G, in
       const float v = xor32_sum(xor16_sum(cs[e] + dpp<0x128>(cs[e])));
       if (l < 8) sPb[w * 64 + 8 * l + e] = v;
     }
-    __syncthreads();
+    lds_sync();
     if (threadIdx.x < 64 && n0 + (int)threadIdx.x < N) {
       const int t = threadIdx.x;
       atomicAdd(rep(db, vrs, 0) + n0 + t, sPb[t] + sPb[64 + t] + sPb[128 + t] + sPb[192 + t]);
@@ -1208,7 +1260,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const TG* __restrict__ G, in
 // ------------------------------------------------------------------------------------
 // kernels whose dynamic LDS can exceed 64 KiB: raise the per-function limit once (gfx950: 160 KiB/CU)
 static void set_smem_once(const void* fn) {
-  static const void* done[64] = {nullptr};
+  static const void* done[256] = {nullptr};
   for (auto& d : done) {
     if (d == fn) return;
     if (d == nullptr) {
@@ -1220,6 +1272,17 @@ static void set_smem_once(const void* fn) {
 }
 
 // row-pass chunk count for a K-wide row: K ≤ 32·NCH, NCH ∈ {1, 2, 4, 5, 8}
+// host side of the AV template flag: every pointer 16-B aligned (nullptr allowed), every row
+// stride / width a multiple of 8 elements
+static bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+static bool av_ok(std::initializer_list<const void*> ptrs, std::initializer_list<long long> widths) {
+  for (const void* p : ptrs)
+    if (!al16(p)) return false;
+  for (long long w : widths)
+    if (w & 7) return false;
+  return true;
+}
+
 static int pick_nch(int K) {
   const int n = (K + 31) / 32;
   return n <= 2 ? n : n <= 4 ? 4 : n <= 5 ? 5 : 8;
@@ -1231,7 +1294,8 @@ static void ln_linear_fwd_t(const void* X, int x_rs, int R, int Kin, const float
                             void* Y, int y_rs, float* mean, float* rstd, const PeSplit& ps, hipStream_t st) {
   constexpr int KP = 32 * NCH;
   const size_t smem = ln_linear_fwd_smem<NCH>();
-  auto fn = ln_linear_fwd_kernel<TI, TO, NCH>;
+  const bool av = av_ok({X, W, lnw, lnb}, {Kin, x_rs, w_rs});
+  auto fn = av ? ln_linear_fwd_kernel<TI, TO, NCH, true> : ln_linear_fwd_kernel<TI, TO, NCH, false>;
   set_smem_once((const void*)fn);
   hipLaunchKernelGGL(fn, dim3((R + 63) / 64), dim3(256), smem, st, (const TI*)X, x_rs, R, Kin, lnw, lnb, eps, W, w_rs, bias,
                      N, act, res, res_rs, (TO*)Y, y_rs, mean, rstd, ps);
@@ -1273,10 +1337,13 @@ void post_attn_fwd_launch(int C, const uint16_t* O, const float* X, const uint16
                           const float* g2, const float* be2, float eps, const uint16_t* W1, const float* b1,
                           const uint16_t* W2, const float* b2, float* Z, float* Ysave, float* mean2, float* rstd2,
                           uint16_t* Usave, int R, int Rx, const DropCfg& dr, hipStream_t st) {
+  const bool av = av_ok({O, X, Wo, W1, W2, Z, Ysave, Usave}, {});
   dim3 grid((R + 63) / 64);
 #define PAF(CC)                                                                                                     \
-  hipLaunchKernelGGL(post_attn_fwd_kernel<CC>, grid, dim3(256), 0, st, O, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, \
-                     Z, Ysave, mean2, rstd2, Usave, R, Rx, dr)
+  if (av) hipLaunchKernelGGL((post_attn_fwd_kernel<CC, true>), grid, dim3(256), 0, st, O, X, Wo, bo, g2, be2, eps, \
+                             W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, Rx, dr);                         \
+  else hipLaunchKernelGGL((post_attn_fwd_kernel<CC, false>), grid, dim3(256), 0, st, O, X, Wo, bo, g2, be2, eps,   \
+                          W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, Rx, dr)
   if (C == 64) PAF(64);
   else if (C == 128) PAF(128);
   else if (C == 32) PAF(32);
@@ -1289,10 +1356,15 @@ void post_attn_ln_linear_fwd_launch(int C, const uint16_t* O, const float* X, co
                                     float* rstd2, uint16_t* Usave, int R, const float* lnw, const float* lnb,
                                     const uint16_t* Wq, const float* bq, uint16_t* QKV, float* mean1, float* rstd1,
                                     const DropCfg& dr, hipStream_t st) {
+  const bool av = av_ok({O, X, Wo, W1, W2, Z, Ysave, Usave, Wq, lnw, lnb, QKV}, {});
   dim3 grid((R + 63) / 64);
 #define PLF(CC)                                                                                                  \
-  hipLaunchKernelGGL(post_attn_ln_linear_fwd_kernel<CC>, grid, dim3(256), 0, st, O, X, Wo, bo, g2, be2, eps, W1, b1, \
-                     W2, b2, Z, Ysave, mean2, rstd2, Usave, R, lnw, lnb, Wq, bq, QKV, mean1, rstd1, dr)
+  if (av) hipLaunchKernelGGL((post_attn_ln_linear_fwd_kernel<CC, true>), grid, dim3(256), 0, st, O, X, Wo, bo, g2, \
+                             be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, lnw, lnb, Wq, bq, QKV,      \
+                             mean1, rstd1, dr);                                                                    \
+  else hipLaunchKernelGGL((post_attn_ln_linear_fwd_kernel<CC, false>), grid, dim3(256), 0, st, O, X, Wo, bo, g2,     \
+                          be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, lnw, lnb, Wq, bq, QKV, mean1,  \
+                          rstd1, dr)
   if (C == 64) PLF(64);
   else if (C == 128) PLF(128);
   else if (C == 32) PLF(32);
@@ -1305,9 +1377,12 @@ void post_attn_bwd_launch(int C, const float* dZ, const float* Ysave, const floa
                           float* delta, int H, const PostAttnGrads& grads, int R, const SlabJob& job, const DropCfg& dr,
                           hipStream_t st) {
   dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0));
+  const bool av = av_ok({dZ, Ysave, U, O, Wo, W1, W2, dY, dO}, {});
 #define PAB(CC)                                                                                                  \
-  hipLaunchKernelGGL(post_attn_bwd_kernel<CC>, grid, dim3(256), 0, st, dZ, Ysave, mean2, rstd2, U, O, Wo, W1, W2, \
-                     g2, be2, dY, dO, delta, H, grads, R, job, dr)
+  if (av) hipLaunchKernelGGL((post_attn_bwd_kernel<CC, true>), grid, dim3(256), 0, st, dZ, Ysave, mean2, rstd2, U, \
+                             O, Wo, W1, W2, g2, be2, dY, dO, delta, H, grads, R, job, dr);                        \
+  else hipLaunchKernelGGL((post_attn_bwd_kernel<CC, false>), grid, dim3(256), 0, st, dZ, Ysave, mean2, rstd2, U, O,  \
+                          Wo, W1, W2, g2, be2, dY, dO, delta, H, grads, R, job, dr)
   if (C == 64) PAB(64);
   else if (C == 128) PAB(128);
   else if (C == 32) PAB(32);
@@ -1323,10 +1398,14 @@ void ln_linear_post_attn_bwd_launch(int C, const float* G, const uint16_t* Wq, c
                                     const PostAttnGrads& grads, int R, const SlabJob& job, const DropCfg& dr,
                                     hipStream_t st) {
   dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0));
+  const bool av = av_ok({G, Wq, X, lnw, lnb, dres, Ysave, U, O, Wo, W1, W2, dY, dO}, {});
 #define LPB(CC)                                                                                                   \
-  hipLaunchKernelGGL(ln_linear_post_attn_bwd_kernel<CC>, grid, dim3(256), 0, st, G, Wq, X, mean1, rstd1, lnw, lnb, \
-                     dres, dlnw, dlnb, dWq, dbq, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO, delta, H,  \
-                     grads, R, job, dr)
+  if (av) hipLaunchKernelGGL((ln_linear_post_attn_bwd_kernel<CC, true>), grid, dim3(256), 0, st, G, Wq, X, mean1,   \
+                             rstd1, lnw, lnb, dres, dlnw, dlnb, dWq, dbq, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, \
+                             be2, dY, dO, delta, H, grads, R, job, dr);                                            \
+  else hipLaunchKernelGGL((ln_linear_post_attn_bwd_kernel<CC, false>), grid, dim3(256), 0, st, G, Wq, X, mean1,      \
+                          rstd1, lnw, lnb, dres, dlnw, dlnb, dWq, dbq, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2,    \
+                          be2, dY, dO, delta, H, grads, R, job, dr)
   if (C == 64) LPB(64);
   else if (C == 32) LPB(32);
 #undef LPB
@@ -1339,7 +1418,8 @@ static void ln_linear_bwd_t(const void* G, int g_rs, int N, const uint16_t* W, i
                             int wrs, int slab, int R, const PeSplit& ps, const SlabJob& job, hipStream_t st) {
   constexpr int KP = 32 * NCH;
   const size_t smem = ln_linear_bwd_smem<NCH>();
-  auto fn = ln_linear_bwd_kernel<TG, TX, NCH>;
+  const bool av = av_ok({G, W, X, lnw, lnb, dres}, {N, g_rs, w_rs, Kin, x_rs, dres ? dres_rs : 0});
+  auto fn = av ? ln_linear_bwd_kernel<TG, TX, NCH, true> : ln_linear_bwd_kernel<TG, TX, NCH, false>;
   set_smem_once((const void*)fn);
   const dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0));  // + the appended slab-job workgroups
   hipLaunchKernelGGL(fn, grid, dim3(256), smem, st, (const TG*)G, g_rs, N, W, w_rs, Kin, (const TX*)X, x_rs,
