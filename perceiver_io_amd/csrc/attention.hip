@@ -110,23 +110,33 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(AttnArgs a, uint16_t
   // staging: items c = tid + NTH·i of the round's NST·KT × CH 16-byte chunks
   bf16x8 kreg[PF ? NI : 1], vreg[PF ? NI : 1];
   bool pad_next[NST];
+  // branch-free fetches (see kZero32B): out-of-range keys read zeros, the mask byte of a
+  // key outside the split / without a mask reads a zero byte and is then overridden
+  const unsigned char* zb = reinterpret_cast<const unsigned char*>(kZero32B);
+  const unsigned char* kmb = a.kmask ? a.kmask + (long long)b * a.Nk : nullptr;
   auto fetch_pad = [&](int key0) {
+    if (kmb == nullptr) {  // wave-uniform: no mask, no loads
+#pragma unroll
+      for (int j = 0; j < NST; ++j) pad_next[j] = key0 + j * KT + l >= k_end;
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < NST; ++j) {
       const int key = key0 + j * KT + l;
-      pad_next[j] = key >= k_end;
-      if (!pad_next[j] && a.kmask) pad_next[j] = a.kmask[(long long)b * a.Nk + key] != 0;
+      const bool in = key < k_end;
+      const unsigned char mv = *(in ? kmb + key : zb);  // unconditional load (address select)
+      pad_next[j] = (mv != 0) | !in;                      // bitwise: no short-circuit branch
     }
   };
   auto fetch = [&](int key0) {
 #pragma unroll
     for (int i = 0; i < (PF ? NI : 1); ++i) {
       const int c = threadIdx.x + NTH * i, key = key0 + c / CH, col = (c % CH) * 8;
-      kreg[i] = vreg[i] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (c < NST * KT * CH && key < k_end) {
-        kreg[i] = *reinterpret_cast<const bf16x8*>(kb + (long long)key * a.k_rs + col);
-        vreg[i] = *reinterpret_cast<const bf16x8*>(vb + (long long)key * a.v_rs + col);
-      }
+      const bool ok = c < NST * KT * CH && key < k_end;
+      const uint16_t* kp = ok ? kb + (long long)key * a.k_rs + col : reinterpret_cast<const uint16_t*>(kZero32B);
+      const uint16_t* vp = ok ? vb + (long long)key * a.v_rs + col : reinterpret_cast<const uint16_t*>(kZero32B);
+      kreg[i] = *reinterpret_cast<const bf16x8*>(kp);
+      vreg[i] = *reinterpret_cast<const bf16x8*>(vp);
     }
     fetch_pad(key0);
   };
@@ -364,8 +374,11 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
   const int key = kbase + 32 * w + r;  // this lane's key (column of S / dP)
   const int kc = key < a.Nk ? key : a.Nk - 1;
   const uint32_t dkey = a.drop_thresh ? drop_key(a.seedp, a.site, 2u) : 0u;
-  bool kpad = key >= a.Nk;
-  if (!kpad && a.kmask) kpad = a.kmask[(long long)b * a.Nk + key] != 0;
+  const bool kin = key < a.Nk;
+  const unsigned char* kmp = (a.kmask && kin) ? a.kmask + (long long)b * a.Nk + key
+                                              : reinterpret_cast<const unsigned char*>(kZero32B);
+  const unsigned char kmv = *kmp;  // unconditional load (address select)
+  const bool kpad = (kmv != 0) | !kin;
 
   const int HD = a.H * D;
   // 16-byte output rows possible (fp32 dQ / dK / dV views 16-byte aligned)
@@ -383,21 +396,27 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
   // carry the round's LSE, [NQS·32, NQS·64) its delta
   bf16x8 qreg[NI];
   float lreg = 0.f;
+  bool lq_out = false;
+  // branch-free fetches (see kZero32B): out-of-range rows read zeros; the LSE of a query past
+  // Nq is forced to +inf after the (unconditional) load
   auto fetch = [&](int qt0) {
     const int q00 = qt0 * 32;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int c = threadIdx.x + NTH * i, isdo = c >= NQS * 32 * CH, cc = isdo ? c - NQS * 32 * CH : c;
       const int qq = q00 + cc / CH, col = (cc % CH) * 8;
-      qreg[i] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (c < NQS * 64 * CH && qq < a.Nq)
-        qreg[i] = isdo ? *reinterpret_cast<const bf16x8*>(dobp + (long long)qq * HD + col)
-                       : *reinterpret_cast<const bf16x8*>(qbp + (long long)qq * a.q_rs + col);
+      const bool ok = c < NQS * 64 * CH && qq < a.Nq;
+      const uint16_t* p = !ok ? reinterpret_cast<const uint16_t*>(kZero32B)
+                              : (isdo ? dobp + (long long)qq * HD + col : qbp + (long long)qq * a.q_rs + col);
+      qreg[i] = *reinterpret_cast<const bf16x8*>(p);
     }
-    if (threadIdx.x < NQS * 64) {
-      const int isd = threadIdx.x >= NQS * 32, qq = q00 + (isd ? threadIdx.x - NQS * 32 : threadIdx.x);
+    {
+      const int t = threadIdx.x < NQS * 64 ? threadIdx.x : 0;
+      const int isd = t >= NQS * 32, qq = q00 + (isd ? t - NQS * 32 : t);
       const long long idx = ((long long)b * a.Nq + qq) * a.H + h;
-      lreg = isd ? (qq < a.Nq ? delta[idx] : 0.f) : (qq < a.Nq ? LSE[idx] : INFINITY);
+      const bool ok = qq < a.Nq;
+      lreg = *(!ok ? kZero32B : (isd ? delta + idx : LSE + idx));
+      lq_out = !ok && !isd;  // LSE of a missing query: +inf (set when the value is stored)
     }
   };
   // every prologue load is issued before the first wait: this wave's K^T / V^T operand
@@ -413,8 +432,8 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
 #pragma unroll
   for (int i = 0; i < KSI; ++i) {
     const int c = threadIdx.x + NTH * i, kk = kbase + c / CH, col = (c % CH) * 8;
-    kst[i] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    if (kk < a.Nk) kst[i] = *reinterpret_cast<const bf16x8*>(kbp + (long long)kk * a.k_rs + col);
+    const uint16_t* p = kk < a.Nk ? kbp + (long long)kk * a.k_rs + col : reinterpret_cast<const uint16_t*>(kZero32B);
+    kst[i] = *reinterpret_cast<const bf16x8*>(p);
   }
   if (qt_begin < nqt) fetch(qt_begin);
   if (D < 32) {  // zero the padded head-dim columns 16..31
@@ -446,7 +465,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
       const int c = threadIdx.x + NTH * i, isdo = c >= NQS * 32 * CH, cc = isdo ? c - NQS * 32 * CH : c;
       if (c < NQS * 64 * CH) *reinterpret_cast<bf16x8*>((isdo ? sdO : sQ) + (cc / CH) * LD + (cc % CH) * 8) = qreg[i];
     }
-    if (threadIdx.x < NQS * 32) sL[threadIdx.x] = lreg;
+    if (threadIdx.x < NQS * 32) sL[threadIdx.x] = lq_out ? INFINITY : lreg;
     else if (threadIdx.x < NQS * 64) sDl[threadIdx.x - NQS * 32] = lreg;
     lds_sync();
     PIO_TS(2 + 4 * ((qt0 - qt_begin) / NQS));

@@ -209,6 +209,17 @@ __device__ int trace_bx, trace_by, trace_bz;
 // contiguous 256-B no-return atomic instruction: S/32 adds per element in all.
 constexpr int kMaxSlabSegs = 16;
 constexpr int kSlabRowsPerBlock = 32;
+// 32 bytes of zeros in global memory: the source of every out-of-range element of a fetch.  A
+// load whose predicate is false reads here instead (an address select), so a phase's loads
+// are straight-line code.  hipcc waits for a load at the first branch, phi copy or arithmetic
+// that touches its result, and after a conditional load (even one skipped at run time) it can
+// no longer count outstanding loads, so it falls back to vmcnt(0): one conditional load in a
+// prefetch loop serialises the whole prefetch with the compute it was meant to overlap.
+// (A writable __device__ array: a const one lands in the constant address space, and a select
+// between it and a global pointer becomes a flat load, which also counts against lgkmcnt and
+// so stalls every LDS wait behind the global loads.)  Never written.
+static __device__ __attribute__((aligned(16))) float kZero32B[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() is a workgroup-scope fence and
 // waits for every outstanding global load AND store of the thread (s_waitcnt vmcnt(0)), so a
 // register prefetch issued before it, or a row store just before it, puts a full memory

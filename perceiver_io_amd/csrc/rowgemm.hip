@@ -156,13 +156,6 @@ __device__ __forceinline__ int rp_row() { return threadIdx.x >> 2; }
 __device__ __forceinline__ int rp_col(int j) { return 8 * ((threadIdx.x & 3) + 4 * j); }
 __device__ __forceinline__ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-// 32 bytes of zeros in global memory: the source of every out-of-range element of the fetches
-// below.  A load whose predicate is false reads here instead (an address select), so a
-// phase's loads are straight-line code.  hipcc waits for a load at the first branch, phi copy
-// or arithmetic that touches its result: a conditional load inside a fetch loop costs one full
-// memory latency per load instead of one per phase.
-__device__ __attribute__((aligned(16))) const float kZero32B[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-
 // row gr (< R) of a row-major [.. × K] matrix, this thread's chunks; zero outside
 template <int NCH, typename T>
 __device__ __forceinline__ void row_load(float (&v)[NCH][8], const T* __restrict__ base, long long rs, int gr, int R,
