@@ -772,6 +772,7 @@ __device__ __forceinline__ void post_attn_bwd_body(
   constexpr bool av = AV;  // Ysave, U, O, dY, dO, Wo, W1, W2 16-B aligned (host-checked)
 
   // ---- phase 0: every input of the tile in flight at once
+  PIO_TS(0);
   float yv[NCH][8], t0[NCH][8];
   row_load<NCH>(yv, Ysave, C, gr, R, C, av);
   row_load<NCH>(t0, U, C, gr, R, C, av);
@@ -789,6 +790,7 @@ __device__ __forceinline__ void post_attn_bwd_body(
     tile_fetch<NIW>(wr[2], Wo, C, 0, C, C, C, C, av);
   }
   for (int k = threadIdx.x; k < C; k += blockDim.x) { sP[0][k] = g2[k]; sP[1][k] = be2[k]; }
+  PIO_TS(1);
   float dzm[NCH][8];  // dZ∘m₁: the MLP output layer's gradient
 #pragma unroll
   for (int j = 0; j < NCH; ++j)
@@ -808,7 +810,9 @@ __device__ __forceinline__ void post_attn_bwd_body(
 #pragma unroll
   for (int b = 0; b < NWB; ++b) tile_store<NIW>(wr[b], sW[b], LD, C, C);
   colsum_partial<NCH>(dzm, sPart[0], C);
+  PIO_TS(2);
   lds_sync();
+  PIO_TS(3);
   if constexpr (NWB == 1) tile_fetch<NIW>(wr[0], W1, C, 0, C, C, C, C, av);
 
   // ---- MLP output layer
@@ -816,7 +820,9 @@ __device__ __forceinline__ void post_attn_bwd_body(
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
   tile_gemm<MAXT, true, false>(sG, LD, sW[0], LD, 64, C, C, acc);  // dH = dZ · W2
+  PIO_TS(4);
   wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, rep(gr_out.dW2, gr_out.vrs, gr_out.slab), C, gr_out.slab);
+  PIO_TS(5);
   {
     constexpr int NTN = C / 32;
 #pragma unroll
@@ -837,7 +843,9 @@ __device__ __forceinline__ void post_attn_bwd_body(
       }
     }
   }
+  PIO_TS(6);
   lds_sync();
+  PIO_TS(7);
   for (int k = threadIdx.x; k < C; k += blockDim.x) {
     gadd(rep(gr_out.db1, gr_out.vrs, gr_out.slab) + k,
          sDb1[0][k] + sDb1[1][k], gr_out.slab);
@@ -858,7 +866,9 @@ __device__ __forceinline__ void post_attn_bwd_body(
       }
     lds_row_write_bf16<NCH>(sX, LD, t0);
   }
+  PIO_TS(8);
   lds_sync();
+  PIO_TS(9);
   if constexpr (NWB == 1) tile_fetch<NIW>(wr[0], Wo, C, 0, C, C, C, C, av);
 
   // ---- MLP hidden layer
@@ -867,7 +877,9 @@ __device__ __forceinline__ void post_attn_bwd_body(
   tile_gemm<MAXT, true, false>(sG, LD, sW[NWB == 3 ? 1 : 0], LD, 64, C, C, acc);  // dXn2 = dU · W1
   wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, rep(gr_out.dW1, gr_out.vrs, gr_out.slab), C, gr_out.slab);
   for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) { sF[m * LDF + n] = acc[t][i]; });
+  PIO_TS(10);
   lds_sync();
+  PIO_TS(11);
   if constexpr (NWB == 1) tile_store<NIW>(wr[0], sW[0], LD, C, C);
   // ---- LN2 backward → dY = dZ + LN_bwd(dXn2); the O tile replaces LN2(Y) in sX
   {
@@ -901,7 +913,9 @@ __device__ __forceinline__ void post_attn_bwd_body(
 #pragma unroll
     for (int j = 0; j < NCH; ++j) *reinterpret_cast<bf16x8*>(sX + rp_row() * LD + rp_col(j)) = ob[j];
   }
+  PIO_TS(12);
   lds_sync();
+  PIO_TS(13);
   for (int k = threadIdx.x; k < C; k += blockDim.x) {
     gadd(rep(gr_out.dg2, gr_out.vrs, gr_out.slab) + k,
          sPart[1][k] + sPart[1][C + k] + sPart[1][2 * C + k] + sPart[1][3 * C + k], gr_out.slab);
@@ -916,8 +930,10 @@ __device__ __forceinline__ void post_attn_bwd_body(
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
   tile_gemm<MAXT, true, false>(sG, LD, sW[NWB == 3 ? 2 : 0], LD, 64, C, C, acc);  // dO = dY · Wo
   wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, rep(gr_out.dWo, gr_out.vrs, gr_out.slab), C, gr_out.slab);
+  PIO_TS(14);
   for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) { sF[m * LDF + n] = bf2f(f2bf(acc[t][i])); });
   lds_sync();
+  PIO_TS(15);
   {
     float dov[NCH][8];
     lds_row_read<NCH>(dov, sF, LDF);
@@ -937,6 +953,7 @@ __device__ __forceinline__ void post_attn_bwd_body(
       if ((threadIdx.x & 3) == 0 && gr < R) delta[(long long)gr * H + h] = s;
     }
   }
+  PIO_TS(16);
 }
 
 template <int C, bool AV>
