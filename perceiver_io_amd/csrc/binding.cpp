@@ -5,6 +5,7 @@
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
 
+#include <unordered_map>
 #include <vector>
 
 namespace pio {
@@ -69,22 +70,25 @@ void ln_linear_bwd_launch(const void*, bool, int, int, const uint16_t*, int, int
 void wgrad_launch(const void*, bool, int, int, const void*, bool, int, int, int, const float*, const float*,
                   const float*, const float*, int, int, float*, float*, int, int, const float*, int, int, int,
                   hipStream_t);
-void ce_fwd_launch(int, const uint16_t*, const int64_t*, const uint16_t*, const float*, int, int, float*, float*,
-                   float*, float*, int, hipStream_t);
+void ce_fwd_launch(int, const float*, const int64_t*, const int64_t*, const uint16_t*, const float*, int, int, float*,
+                   float*, float*, const float*, float*, float*, unsigned*, int, hipStream_t);
+int ce_combine_blocks(int);
 int ce_num_splits(int, int);
 int ce_dw_splits(int, int);
-void mlm_select_launch(const int64_t*, int, int, int, int, int64_t*, int64_t*, int*, int64_t*, int64_t*, float*, bool*,
+void mlm_select_launch(const int64_t*, int, int, int, int, int64_t*, int64_t*, int*, int64_t*, int64_t*, float*, bool*, bool*,
                        hipStream_t);
-void ce_bwd_launch(int, const uint16_t*, const int64_t*, const uint16_t*, const float*, const float*, const float*,
-                   int, int, float*, long long, const int64_t*, float*, float*, int, float*, int, hipStream_t);
+void ce_bwd_launch(int, const float*, const int64_t*, const int64_t*, const uint16_t*, const float*, const float*,
+                   const float*, const float*, int, int, float*, long long, const int64_t*, float*, float*, int, float*, int,
+                   hipStream_t);
 void embed_fwd_launch(const int64_t*, const float*, const float*, float*, long long, int, int, float, hipStream_t);
 void embed_bwd_launch(const int64_t*, const float*, float*, float*, int, int, int, float, hipStream_t);
 void embed_bwd_sorted_launch(const int64_t*, const int64_t*, const float*, float*, long long, int, float, hipStream_t);
 bool embed_bwd_local_launch(const int64_t*, const float*, float*, float*, int, int, int, float, hipStream_t);
-void text_mask_launch(const int64_t*, const bool*, const float*, const int64_t*, int64_t*, int64_t*, long long, int,
-                      int, float, hipStream_t);
+void text_mask_launch(const int64_t*, const bool*, int64_t*, int64_t*, int64_t*, long long, int, int, float, int,
+                      uint32_t, int, hipStream_t);
 void sumsq_launch(const float*, long long, float*, hipStream_t);
 void index_add_rows_launch(float*, long long, const int64_t*, const float*, long long, int, hipStream_t);
+void batch_sum2_launch(const float*, const float*, float*, float*, int, long long, hipStream_t);
 int pixel_ce_blocks(long long);
 void pixel_ce_fwd_launch(int, int, const float*, const float*, const float*, const int64_t*, const float*, long long,
                          float*, float*, float*, hipStream_t);
@@ -569,8 +573,9 @@ void wgrad(Tensor g, Tensor a, int64_t amode, OptT mean, OptT rstd, OptT lnw, Op
 }
 
 // labels (B, L) → [idx_b (B, cap), labels_b (B, cap), gidx (gcap), glabels (gcap), total (1) fp32,
-// overflow (1) bool]: per-sequence slots of the selected positions and their global compaction
-std::vector<Tensor> mlm_select(Tensor labels, int64_t cap, int64_t gcap) {
+// overflow (1) bool]: per-sequence slots of the selected positions and their global compaction.
+// sticky: optional persistent bool the kernel sets when this call overflows (never clears)
+std::vector<Tensor> mlm_select(Tensor labels, int64_t cap, int64_t gcap, OptT sticky) {
   CHECK_DT(labels, torch::kInt64);
   TORCH_CHECK(labels.dim() == 2 && labels.is_contiguous(), "labels must be (B, L) contiguous");
   const int B = (int)labels.size(0), L = (int)labels.size(1);
@@ -582,33 +587,66 @@ std::vector<Tensor> mlm_select(Tensor labels, int64_t cap, int64_t gcap) {
   Tensor total = torch::empty({1}, i64.dtype(torch::kFloat32)), ovf = torch::empty({1}, i64.dtype(torch::kBool));
   pio::mlm_select_launch(labels.data_ptr<int64_t>(), B, L, (int)cap, (int)gcap, idx_b.data_ptr<int64_t>(),
                          lab_b.data_ptr<int64_t>(), count.data_ptr<int>(), gidx.data_ptr<int64_t>(),
-                         glab.data_ptr<int64_t>(), total.data_ptr<float>(), ovf.data_ptr<bool>(), stream());
+                         glab.data_ptr<int64_t>(), total.data_ptr<float>(), ovf.data_ptr<bool>(),
+                         sticky.has_value() ? sticky->data_ptr<bool>() : nullptr, stream());
   return {idx_b, lab_b, gidx, glab, total, ovf};
 }
 
-std::vector<Tensor> ce_fwd(Tensor h, Tensor labels, Tensor w, Tensor bias) {
-  TORCH_CHECK(h.is_contiguous() && w.is_contiguous() && labels.is_contiguous());
+// one ticket per device for the CE loss finalisation (ce_combine_kernel): zero between
+// launches (the last workgroup resets it); CE calls on a device are stream-ordered
+static Tensor& ce_ticket(const Tensor& like) {
+  static std::unordered_map<int, Tensor> tickets;
+  const int d = like.get_device();
+  auto it = tickets.find(d);
+  if (it == tickets.end()) it = tickets.emplace(d, torch::zeros({4}, like.options().dtype(torch::kInt32))).first;
+  return it->second;
+}
+
+static const int64_t* opt_idx(const OptT& idx, int64_t n) {
+  if (!idx.has_value()) return nullptr;
+  CHECK_DT(*idx, torch::kInt64);
+  TORCH_CHECK(idx->is_contiguous() && idx->numel() == n, "ce: idx must hold one source row per row");
+  return idx->data_ptr<int64_t>();
+}
+
+// mean CE over the rows of h (fp32 (N, C); row r = h[idx[r]] when idx is given, else h[r]) with
+// label ≥ 0: → {loss (0-dim) = Σ rows / max(count, 1), per-row lse (M,)}.  count: fp32 (1,).
+std::vector<Tensor> ce_fwd(Tensor h, OptT idx, Tensor labels, Tensor w, Tensor bias, Tensor count) {
+  TORCH_CHECK(h.is_contiguous() && w.is_contiguous() && labels.is_contiguous() && bias.is_contiguous());
   CHECK_DT(labels, torch::kInt64);
-  const int M = (int)h.size(0), C = (int)h.size(1), V = (int)w.size(0);
+  CHECK_DT(h, torch::kFloat32);
+  CHECK_DT(count, torch::kFloat32);
+  const int M = (int)labels.numel(), C = (int)h.size(1), V = (int)w.size(0);
   TORCH_CHECK(w.size(1) == C && (C == 32 || C == 64 || C == 128), "bad vocab head shape");
+  TORCH_CHECK(idx.has_value() || h.size(0) == M, "ce_fwd: h must have one row per label without idx");
+  const int64_t* ip = opt_idx(idx, M);
   auto f32 = h.options().dtype(torch::kFloat32);
   const int ns = pio::ce_num_splits(M, V);
-  Tensor part = torch::empty({ns, M, 2}, f32), picked = torch::zeros({M}, f32);
-  Tensor loss = torch::empty({M}, f32), lse = torch::empty({M}, f32);
-  pio::ce_fwd_launch(C, bfp(h), labels.data_ptr<int64_t>(), bfp(w), f32p(bias), M, V, part.data_ptr<float>(),
-                     picked.data_ptr<float>(), loss.data_ptr<float>(), lse.data_ptr<float>(), ns, stream());
+  Tensor part = torch::empty({ns, M, 2}, f32), picked = torch::empty({M}, f32);
+  Tensor lse = torch::empty({M}, f32), loss = torch::empty({}, f32);
+  Tensor blk = torch::empty({pio::ce_combine_blocks(M)}, f32);
+  Tensor& tk = ce_ticket(h);
+  pio::ce_fwd_launch(C, h.data_ptr<float>(), ip, labels.data_ptr<int64_t>(), bfp(w), f32p(bias), M, V,
+                     part.data_ptr<float>(), picked.data_ptr<float>(), lse.data_ptr<float>(), f32p(count),
+                     loss.data_ptr<float>(), blk.data_ptr<float>(), reinterpret_cast<unsigned*>(tk.data_ptr<int>()), ns,
+                     stream());
   return {loss, lse};
 }
 
-// dH (+)= rows: row r of the compacted batch lands in dH[rowmap[r]] when rowmap is given
-// (dH then has the full (positions, C) shape), else in dH[r]; dW / db accumulate or overwrite.
+// dH (+)= rows: row r lands in dH[rowmap[r]] when rowmap is given (dH then has the full
+// (positions, C) shape), else in dH[r]; dW / db accumulate or overwrite.  The row-loss gradient
+// is gout / max(count, 1) (gout: the 0-dim gradient of the mean loss).
 // slab: the dW kernel stores its row-split partials into a returned (splits, V·C + V₄) slab
 // instead of adding them (the caller sums it into dW | db with a slab job, offsets 0 and V·C).
-OptT ce_bwd(Tensor h, Tensor labels, Tensor w, Tensor bias, Tensor lse, Tensor gscale, Tensor dH, Tensor dW, Tensor db,
-            bool accumulate, OptT rowmap, bool slab) {
-  const int M = (int)h.size(0), C = (int)h.size(1), V = (int)w.size(0);
-  TORCH_CHECK(dH.is_contiguous() && dW.is_contiguous() && db.is_contiguous());
+OptT ce_bwd(Tensor h, OptT idx, Tensor labels, Tensor w, Tensor bias, Tensor lse, Tensor gout, Tensor count, Tensor dH,
+            Tensor dW, Tensor db, bool accumulate, OptT rowmap, bool slab) {
+  const int M = (int)labels.numel(), C = (int)h.size(1), V = (int)w.size(0);
+  CHECK_DT(h, torch::kFloat32);
+  CHECK_DT(gout, torch::kFloat32);
+  CHECK_DT(count, torch::kFloat32);
+  TORCH_CHECK(h.is_contiguous() && dH.is_contiguous() && dW.is_contiguous() && db.is_contiguous());
   TORCH_CHECK(dH.dim() == 2 && dH.size(1) == C, "dH must be (rows, C)");
+  const int64_t* ip = opt_idx(idx, M);
   const int64_t* rm = nullptr;
   if (rowmap.has_value()) {
     CHECK_DT(*rowmap, torch::kInt64);
@@ -619,9 +657,9 @@ OptT ce_bwd(Tensor h, Tensor labels, Tensor w, Tensor bias, Tensor lse, Tensor g
   }
   Tensor sl;
   if (slab) sl = torch::empty({pio::ce_dw_splits(M, V), (int64_t)V * C + ((V + 3) & ~3)}, dW.options());
-  pio::ce_bwd_launch(C, bfp(h), labels.data_ptr<int64_t>(), bfp(w), f32p(bias), f32p(lse), f32p(gscale), M, V,
-                     dH.data_ptr<float>(), dH.size(0), rm, dW.data_ptr<float>(), db.data_ptr<float>(), accumulate ? 1 : 0,
-                     slab ? sl.data_ptr<float>() : nullptr, g_det ? 1 : 0, stream());
+  pio::ce_bwd_launch(C, h.data_ptr<float>(), ip, labels.data_ptr<int64_t>(), bfp(w), f32p(bias), f32p(lse), f32p(gout),
+                     f32p(count), M, V, dH.data_ptr<float>(), dH.size(0), rm, dW.data_ptr<float>(), db.data_ptr<float>(),
+                     accumulate ? 1 : 0, slab ? sl.data_ptr<float>() : nullptr, g_det ? 1 : 0, stream());
   if (slab) return sl;
   return c10::nullopt;
 }
@@ -661,19 +699,44 @@ void embed_bwd(Tensor ids, Tensor g, OptT dE, OptT dP, double scale) {
                           stream());
 }
 
-std::vector<Tensor> text_mask(Tensor x, OptT pad, Tensor u, Tensor rid, int64_t unk, int64_t mask, double p) {
-  TORCH_CHECK(x.is_contiguous() && u.is_contiguous() && rid.is_contiguous());
+// state: int64 (3,) {seed, counter, ticket} on the device (see text_mask_kernel); advance: the
+// launch increments the counter (fresh masks on every call / graph replay)
+std::vector<Tensor> text_mask(Tensor x, OptT pad, Tensor state, int64_t unk, int64_t mask, double p, int64_t lo,
+                              int64_t hi, bool advance) {
+  TORCH_CHECK(x.is_contiguous() && state.is_contiguous() && state.numel() == 3, "text_mask: bad x / state");
+  CHECK_DT(x, torch::kInt64);
+  CHECK_DT(state, torch::kInt64);
+  TORCH_CHECK(hi > lo && hi - lo < (1LL << 32), "text_mask: bad random-id range");
   const long long n = x.numel();
-  TORCH_CHECK(u.numel() == 3 * n && rid.numel() == n);
+  TORCH_CHECK(n < (1LL << 32), "text_mask: too many tokens");
   Tensor xm = torch::empty_like(x), lab = torch::empty_like(x);
   const bool* pp = nullptr;
-  if (pad.has_value()) { CHECK_DT(*pad, torch::kBool); pp = pad->data_ptr<bool>(); }
-  pio::text_mask_launch(x.data_ptr<int64_t>(), pp, f32p(u), rid.data_ptr<int64_t>(), xm.data_ptr<int64_t>(),
-                        lab.data_ptr<int64_t>(), n, (int)unk, (int)mask, (float)p, stream());
+  if (pad.has_value()) {
+    CHECK_DT(*pad, torch::kBool);
+    TORCH_CHECK(pad->is_contiguous() && pad->numel() == n, "text_mask: pad mask must match x");
+    pp = pad->data_ptr<bool>();
+  }
+  pio::text_mask_launch(x.data_ptr<int64_t>(), pp, state.data_ptr<int64_t>(), xm.data_ptr<int64_t>(),
+                        lab.data_ptr<int64_t>(), n, (int)unk, (int)mask, (float)p, (int)lo, (uint32_t)(hi - lo),
+                        advance ? 1 : 0, stream());
   return {xm, lab};
 }
 
 void sumsq(Tensor g, Tensor out) { pio::sumsq_launch(f32p(g), g.numel(), out.data_ptr<float>(), stream()); }
+
+// a, b: (B, ...) fp32 contiguous, equal shapes → (Σ_b a[b], Σ_b b[b]) in one launch
+std::vector<Tensor> batch_sum2(Tensor a, Tensor b) {
+  CHECK_DT(a, torch::kFloat32); CHECK_DT(b, torch::kFloat32);
+  TORCH_CHECK(a.is_contiguous() && b.is_contiguous() && a.sizes() == b.sizes() && a.dim() >= 2, "batch_sum2: shapes");
+  const long long n = a.numel() / a.size(0);
+  TORCH_CHECK(n % 4 == 0 && reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 &&
+              reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0, "batch_sum2: 16-byte rows");
+  std::vector<int64_t> shp(a.sizes().begin() + 1, a.sizes().end());
+  Tensor oa = torch::empty(shp, a.options()), ob = torch::empty(shp, a.options());
+  pio::batch_sum2_launch(a.data_ptr<float>(), b.data_ptr<float>(), oa.data_ptr<float>(), ob.data_ptr<float>(),
+                         (int)a.size(0), n, stream());
+  return {oa, ob};
+}
 
 // dst (N, C) fp32 += src (R, C) fp32 scattered to rows idx (R) — the backward of a row gather
 void index_add_rows(Tensor dst, Tensor idx, Tensor src) {
@@ -914,17 +977,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad", &wgrad, py::arg("g"), py::arg("a"), py::arg("amode"), py::arg("mean"), py::arg("rstd"), py::arg("lnw"),
         py::arg("lnb"), py::arg("rows_per_wg"), py::arg("dW"), py::arg("db"), py::arg("pe") = py::none(),
         py::arg("kin") = -1);
-  m.def("mlm_select", &mlm_select);
+  m.def("mlm_select", &mlm_select, py::arg("labels"), py::arg("cap"), py::arg("gcap"), py::arg("sticky") = py::none());
   m.def("index_add_rows", &index_add_rows);
+  m.def("batch_sum2", &batch_sum2);
   m.def("pixel_ce_fwd", &pixel_ce_fwd);
   m.def("pixel_ce_bwd", &pixel_ce_bwd);
   m.def("ce_fwd", &ce_fwd);
-  m.def("ce_bwd", &ce_bwd, py::arg("h"), py::arg("labels"), py::arg("w"), py::arg("bias"), py::arg("lse"),
-        py::arg("gscale"), py::arg("dH"), py::arg("dW"), py::arg("db"), py::arg("accumulate"),
-        py::arg("rowmap") = py::none(), py::arg("slab") = false);
+  m.def("ce_bwd", &ce_bwd, py::arg("h"), py::arg("idx"), py::arg("labels"), py::arg("w"), py::arg("bias"),
+        py::arg("lse"), py::arg("gout"), py::arg("count"), py::arg("dH"), py::arg("dW"), py::arg("db"),
+        py::arg("accumulate"), py::arg("rowmap") = py::none(), py::arg("slab") = false);
   m.def("embed_fwd", &embed_fwd);
   m.def("embed_bwd", &embed_bwd);
-  m.def("text_mask", &text_mask);
+  m.def("text_mask", &text_mask, py::arg("x"), py::arg("pad"), py::arg("state"), py::arg("unk"), py::arg("mask"),
+        py::arg("p"), py::arg("lo"), py::arg("hi"), py::arg("advance") = true);
   m.def("sumsq", &sumsq);
   m.def("adamw", &adamw, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("shadow"), py::arg("hyper"),
         py::arg("eps"), py::arg("wd"), py::arg("clip"), py::arg("gscale"), py::arg("l2") = false);

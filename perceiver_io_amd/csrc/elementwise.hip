@@ -169,20 +169,42 @@ __global__ __launch_bounds__(256) void embed_bwd_local_kernel(const int64_t* __r
   }
 }
 
-// BERT masking from three uniform draws per token (torch.rand, graph-safe RNG):
+// BERT masking with in-kernel counter-based randomness (no torch RNG kernels, no generator
+// bookkeeping in a replayed graph).  Per token i, with key = hash3(seed, counter):
+//   u_k = (hash3(key, k, i) >> 8) · 2^-24 (k = 0, 1, 2), rid = lo + mulhi(hash3(key, 3, i), range)
 //   sel = ~special & u0 < p ; msk = sel & u1 < 0.9 ; rnd = msk & u2 < 1/9
 //   x' = rnd ? rid : (msk ? MASK : x) ; label = sel ? x : -100
-__global__ void text_mask_kernel(const int64_t* __restrict__ x, const bool* __restrict__ pad,
-                                 const float* __restrict__ u, const int64_t* __restrict__ rid, int64_t* __restrict__ xm,
-                                 int64_t* __restrict__ labels, long long n, int unk_id, int mask_id, float p) {
+// state = {seed, counter, ticket}: with advance != 0 the last workgroup to finish (ticket
+// count) increments the counter, so every launch — every replay of a captured step — draws
+// fresh masks; every workgroup has read the counter before it takes its ticket.
+__device__ __forceinline__ float unit24(uint32_t h) { return (float)(h >> 8) * (1.0f / 16777216.0f); }
+
+__global__ void text_mask_kernel(const int64_t* __restrict__ x, const bool* __restrict__ pad, int64_t* __restrict__ state,
+                                 int64_t* __restrict__ xm, int64_t* __restrict__ labels, long long n, int unk_id,
+                                 int mask_id, float p, int lo, uint32_t range, int advance) {
+  const uint64_t seed = (uint64_t)state[0];
+  const int64_t ctr = state[1];
+  const uint32_t key = hash3((uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)ctr);
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const uint32_t ii = (uint32_t)i;
     const int64_t t = x[i];
-    const bool special = (t == unk_id) || (pad && pad[i]);
-    const bool sel = !special && (u[i] < p);
-    const bool msk = sel && (u[n + i] < 0.9f);
-    const bool rnd = msk && (u[2 * n + i] < (1.0f / 9.0f));
-    xm[i] = rnd ? rid[i] : (msk ? (int64_t)mask_id : t);
+    const bool special = (t == unk_id) | (pad != nullptr && pad[i]);
+    const bool sel = !special & (unit24(hash3(key, 0u, ii)) < p);
+    const bool msk = sel & (unit24(hash3(key, 1u, ii)) < 0.9f);
+    const bool rnd = msk & (unit24(hash3(key, 2u, ii)) < (1.0f / 9.0f));
+    const int64_t rid = (int64_t)lo + (int64_t)__umulhi(hash3(key, 3u, ii), range);
+    xm[i] = rnd ? rid : (msk ? (int64_t)mask_id : t);
     labels[i] = sel ? t : (int64_t)-100;
+  }
+  if (advance) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned* ticket = reinterpret_cast<unsigned*>(state + 2);
+      if (atomicAdd(ticket, 1u) == gridDim.x - 1) {
+        state[1] = ctr + 1;
+        *ticket = 0u;
+      }
+    }
   }
 }
 
@@ -295,9 +317,10 @@ void embed_bwd_sorted_launch(const int64_t* sorted_ids, const int64_t* perm, con
   hipLaunchKernelGGL(embed_bwd_sorted_kernel, dim3((unsigned)((n + ES - 1) / ES)), dim3(C < 256 ? C : 256), 0, st,
                      sorted_ids, perm, g, dE, n, C, scale);
 }
-void text_mask_launch(const int64_t* x, const bool* pad, const float* u, const int64_t* rid, int64_t* xm,
-                      int64_t* labels, long long n, int unk_id, int mask_id, float p, hipStream_t st) {
-  hipLaunchKernelGGL(text_mask_kernel, grid_for(n), dim3(256), 0, st, x, pad, u, rid, xm, labels, n, unk_id, mask_id, p);
+void text_mask_launch(const int64_t* x, const bool* pad, int64_t* state, int64_t* xm, int64_t* labels, long long n,
+                      int unk_id, int mask_id, float p, int lo, uint32_t range, int advance, hipStream_t st) {
+  hipLaunchKernelGGL(text_mask_kernel, grid_for(n), dim3(256), 0, st, x, pad, state, xm, labels, n, unk_id, mask_id, p, lo,
+                     range, advance);
 }
 void sumsq_launch(const float* g, long long n, float* out, hipStream_t st) {
   long long b = (n + 4095) / 4096;
@@ -331,6 +354,43 @@ __global__ void index_add_rows_kernel(float* __restrict__ dst, long long nrows, 
 void index_add_rows_launch(float* dst, long long nrows, const int64_t* idx, const float* src, long long R, int C,
                            hipStream_t st) {
   hipLaunchKernelGGL(index_add_rows_kernel, grid_for(R * (C / 4)), dim3(256), 0, st, dst, nrows, idx, src, R, C);
+}
+// Σ over the batch of two (B, n) fp32 tensors in one launch: oa = Σ_b a[b], ob = Σ_b b[b] (the
+// gradients of a batch-broadcast query stream: dQ and the residual dY of the first cross-attention
+// over the shared latent array).  Block = 64 float4 columns × 4 batch groups, fixed summation
+// order (deterministic).  n a multiple of 4, 16-byte aligned rows.
+__global__ __launch_bounds__(256) void batch_sum2_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                         float* __restrict__ oa, float* __restrict__ ob, int B,
+                                                         long long n4) {
+  __shared__ float4 part[4][64];
+  const int l = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const long long c = (long long)blockIdx.x * 64 + l;  // float4 column of [a | b]
+  const bool second = c >= n4;
+  const long long cc = second ? c - n4 : c;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c < 2 * n4) {
+    const float4* src = reinterpret_cast<const float4*>(second ? b : a) + cc;
+#pragma unroll 8
+    for (int bb = g; bb < B; bb += 4) {
+      const float4 v = src[(long long)bb * n4];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  part[g][l] = acc;
+  __syncthreads();
+  if (g == 0 && c < 2 * n4) {
+    float4 r = part[0][l];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      const float4 v = part[k][l];
+      r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
+    }
+    reinterpret_cast<float4*>(second ? ob : oa)[cc] = r;
+  }
+}
+void batch_sum2_launch(const float* a, const float* b, float* oa, float* ob, int B, long long n, hipStream_t st) {
+  const long long n4 = n / 4;
+  hipLaunchKernelGGL(batch_sum2_kernel, dim3((unsigned)((2 * n4 + 63) / 64)), dim3(256), 0, st, a, b, oa, ob, B, n4);
 }
 void adamw_launch(float* p, const float* g, float* m, float* v, uint16_t* shadow, long long n, const float* hyper,
                   float eps, float wd, float clip, float gscale, int l2, hipStream_t st) {

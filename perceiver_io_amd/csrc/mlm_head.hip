@@ -62,6 +62,32 @@ __device__ __forceinline__ void store_dl_row(uint16_t* sL, int ldl, int row, con
   }
 }
 
+// Row r of the head input is H[idx[r]] (idx == nullptr: H[r]) of the fp32 decoder output: the
+// compaction gather and the bf16 cast happen on load, no gathered copy is ever written.
+template <int C>
+__device__ __forceinline__ bf16x8 hrow8(const float* __restrict__ H, const int64_t* __restrict__ idx, int r, int c) {
+  const long long row = idx ? idx[r] : (long long)r;
+  const float4 a = *reinterpret_cast<const float4*>(H + row * C + c);
+  const float4 b = *reinterpret_cast<const float4*>(H + row * C + c + 4);
+  bf16x8 v;
+  v[0] = (short)f2bf(a.x); v[1] = (short)f2bf(a.y); v[2] = (short)f2bf(a.z); v[3] = (short)f2bf(a.w);
+  v[4] = (short)f2bf(b.x); v[5] = (short)f2bf(b.y); v[6] = (short)f2bf(b.z); v[7] = (short)f2bf(b.w);
+  return v;
+}
+
+// rows [r0, r0+64) of H (gathered) → LDS bf16 [64][ld]
+template <int C>
+__device__ __forceinline__ void stage_hrows(uint16_t* s, int ld, const float* H, const int64_t* idx, int r0, int R) {
+  constexpr int CH = C / 8;
+  for (int e = threadIdx.x; e < 64 * CH; e += blockDim.x) {
+    const int rr = e / CH, c = (e % CH) * 8;
+    bf16x8 v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (r0 + rr < R) v = hrow8<C>(H, idx, r0 + rr, c);
+    *reinterpret_cast<bf16x8*>(s + rr * ld + c) = v;
+  }
+}
+
+// rows [r0, r0+64) × C of a bf16 row-major matrix → LDS
 template <int C>
 __device__ __forceinline__ void stage_rows(uint16_t* s, int ld, const uint16_t* g, int r0, int R) {
   constexpr int CH = C / 8;
@@ -85,6 +111,17 @@ __device__ __forceinline__ void fetch_rows(bf16x8 (&v)[C / 32], const uint16_t* 
     if (r0 + rr < R) v[i] = *reinterpret_cast<const bf16x8*>(g + (long long)(r0 + rr) * C + c);
   }
 }
+// the same for gathered fp32 H rows
+template <int C>
+__device__ __forceinline__ void fetch_hrows(bf16x8 (&v)[C / 32], const float* H, const int64_t* idx, int r0, int R) {
+  constexpr int CH = C / 8;
+#pragma unroll
+  for (int i = 0; i < C / 32; ++i) {
+    const int e = threadIdx.x + 256 * i, rr = e / CH, c = (e % CH) * 8;
+    v[i] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (r0 + rr < R) v[i] = hrow8<C>(H, idx, r0 + rr, c);
+  }
+}
 template <int C>
 __device__ __forceinline__ void store_rows(const bf16x8 (&v)[C / 32], uint16_t* s, int ld) {
   constexpr int CH = C / 8;
@@ -96,7 +133,8 @@ __device__ __forceinline__ void store_rows(const bf16x8 (&v)[C / 32], uint16_t* 
 }
 
 template <int C>
-__global__ __launch_bounds__(256) void ce_fwd_kernel(const uint16_t* __restrict__ Hm, const int64_t* __restrict__ labels,
+__global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ Hm, const int64_t* __restrict__ hidx,
+                                                     const int64_t* __restrict__ labels,
                                                      const uint16_t* __restrict__ W, const float* __restrict__ bias,
                                                      int M, int V, int chunks_per_split, float* __restrict__ part_ms,
                                                      float* __restrict__ picked) {
@@ -109,7 +147,7 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const uint16_t* __restrict_
   const int m0 = blockIdx.x * HB, split = blockIdx.y;
   const int nchunks = (V + VB - 1) / VB;
   const int c_begin = split * chunks_per_split, c_end = min(nchunks, c_begin + chunks_per_split);
-  stage_rows<C>(sH, LD, Hm, m0, M);
+  stage_hrows<C>(sH, LD, Hm, hidx, m0, M);
   const int rl = 32 * (w >> 1) + (l & 31), gr = m0 + rl;
   const int lab = gr < M ? (int)labels[gr] : -100;
   float m = -1e30f, s = 0.f;  // log2-domain running max / sum of 2^(t - m) over this lane's logits
@@ -174,19 +212,51 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const uint16_t* __restrict_
   }
 }
 
-// per-row loss = lse − picked (0 for ignored rows); lse kept for backward
-__global__ void ce_combine_kernel(const float* __restrict__ part_ms, const float* __restrict__ picked,
-                                  const int64_t* __restrict__ labels, int M, int nsplit, float* __restrict__ loss_rows,
-                                  float* __restrict__ lse) {
+// per-row lse (kept for backward) and loss = lse − picked (0 for ignored rows); the mean loss
+// Σ rows / max(count, 1) is finalised in-kernel: each workgroup stores its partial sum, and the
+// last one to take a ticket adds the partials in a fixed order (deterministic) and resets the
+// ticket.  (picked[r] is written by the forward for every row with a label, so it needs no
+// zero fill.)
+__global__ __launch_bounds__(256) void ce_combine_kernel(const float* __restrict__ part_ms,
+                                                         const float* __restrict__ picked,
+                                                         const int64_t* __restrict__ labels, int M, int nsplit,
+                                                         float* __restrict__ lse, const float* __restrict__ count,
+                                                         float* __restrict__ loss, float* __restrict__ blk,
+                                                         unsigned* __restrict__ ticket) {
+  __shared__ float red[4];
+  __shared__ int last;
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= M) return;
-  float mm = -1e30f;
-  for (int s = 0; s < nsplit; ++s) mm = fmaxf(mm, part_ms[((long long)s * M + r) * 2]);
-  float ss = 0.f;
-  for (int s = 0; s < nsplit; ++s) ss += part_ms[((long long)s * M + r) * 2 + 1] * __expf(part_ms[((long long)s * M + r) * 2] - mm);
-  const float L = mm + __logf(ss);
-  lse[r] = L;
-  loss_rows[r] = labels[r] >= 0 ? L - picked[r] : 0.f;
+  float lr = 0.f;
+  if (r < M) {
+    float mm = -1e30f;
+    for (int s = 0; s < nsplit; ++s) mm = fmaxf(mm, part_ms[((long long)s * M + r) * 2]);
+    float ss = 0.f;
+    for (int s = 0; s < nsplit; ++s) ss += part_ms[((long long)s * M + r) * 2 + 1] * __expf(part_ms[((long long)s * M + r) * 2] - mm);
+    const float L = mm + __logf(ss);
+    lse[r] = L;
+    lr = labels[r] >= 0 ? L - picked[r] : 0.f;
+  }
+  lr = wave_sum(lr);
+  if (lane_id() == 0) red[wave_id()] = lr;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    blk[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+    __threadfence();
+    last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  float t = 0.f;
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x) t += *(volatile const float*)(blk + i);
+  t = wave_sum(t);
+  __syncthreads();
+  if (lane_id() == 0) red[wave_id()] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    loss[0] = ((red[0] + red[1]) + (red[2] + red[3])) / fmaxf(count[0], 1.f);
+    *ticket = 0u;
+  }
 }
 
 // dl = (softmax - onehot) * g for the 16 logits of this lane's row (transposed tile):
@@ -204,11 +274,13 @@ __device__ __forceinline__ void dl_regs(const f32x16& acc, const float (&b)[16],
 
 // bwd-a: dH[r][c] += sum_v dl[r][v] W[v][c]  over this split's vocab chunks (fp32 atomics)
 template <int C>
-__global__ __launch_bounds__(256) void ce_bwd_dh_kernel(const uint16_t* __restrict__ Hm,
+__global__ __launch_bounds__(256) void ce_bwd_dh_kernel(const float* __restrict__ Hm,
+                                                        const int64_t* __restrict__ hidx,
                                                         const int64_t* __restrict__ labels,
                                                         const uint16_t* __restrict__ W, const float* __restrict__ bias,
-                                                        const float* __restrict__ lse, const float* __restrict__ gscale,
-                                                        int M, int V, int chunks_per_split, float* __restrict__ dH,
+                                                        const float* __restrict__ lse, const float* __restrict__ gout,
+                                                        const float* __restrict__ count, int M, int V,
+                                                        int chunks_per_split, float* __restrict__ dH,
                                                         const int64_t* __restrict__ rowmap, long long dh_rows) {
   constexpr int LD = C + 8, LDL = VB + 8, NT = C / 32;
   __shared__ __attribute__((aligned(16))) uint16_t sH[HB * LD];
@@ -220,7 +292,7 @@ __global__ __launch_bounds__(256) void ce_bwd_dh_kernel(const uint16_t* __restri
   const int m0 = blockIdx.x * HB, split = blockIdx.y;
   const int nchunks = (V + VB - 1) / VB;
   const int c_begin = split * chunks_per_split, c_end = min(nchunks, c_begin + chunks_per_split);
-  stage_rows<C>(sH, LD, Hm, m0, M);
+  stage_hrows<C>(sH, LD, Hm, hidx, m0, M);
   if (threadIdx.x < HB) {
     const int gr = m0 + threadIdx.x;
     const long long r = (gr < M && labels[gr] >= 0) ? (rowmap ? rowmap[gr] : gr) : -1;
@@ -229,7 +301,7 @@ __global__ __launch_bounds__(256) void ce_bwd_dh_kernel(const uint16_t* __restri
   const int rl = 32 * (w >> 1) + (l & 31), gr = m0 + rl;
   const int lab = gr < M ? (int)labels[gr] : -100;
   const float lse_l2 = gr < M ? lse[gr] * kL2E : 0.f;
-  const float g = lab >= 0 ? gscale[0] : 0.f;
+  const float g = lab >= 0 ? gout[0] / fmaxf(count[0], 1.f) : 0.f;  // d(mean loss) / d(row loss)
   // output dH tile 64 x C: sub-tiles (2 x NT), wave w owns tiles w, w+4
   constexpr int MAXT = (2 * NT + 3) / 4;
   f32x16 acc_o[MAXT];
@@ -287,11 +359,13 @@ __global__ __launch_bounds__(256) void ce_bwd_dh_kernel(const uint16_t* __restri
 // bwd-b: dW[v][c] += sum_r dl[r][v] H[r][c], db[v] += sum_r dl[r][v]; grid (vocab chunk, row split),
 // H tiles (+ their LSE / labels) register-prefetched one tile ahead, partials added atomically
 template <int C>
-__global__ __launch_bounds__(256) void ce_bwd_dw_kernel(const uint16_t* __restrict__ Hm,
+__global__ __launch_bounds__(256) void ce_bwd_dw_kernel(const float* __restrict__ Hm,
+                                                        const int64_t* __restrict__ hidx,
                                                         const int64_t* __restrict__ labels,
                                                         const uint16_t* __restrict__ W, const float* __restrict__ bias,
-                                                        const float* __restrict__ lse, const float* __restrict__ gscale,
-                                                        int M, int V, int tiles_per_split, float* __restrict__ dW,
+                                                        const float* __restrict__ lse, const float* __restrict__ gout,
+                                                        const float* __restrict__ count, int M, int V,
+                                                        int tiles_per_split, float* __restrict__ dW,
                                                         float* __restrict__ db, float* __restrict__ slab) {
   constexpr int LD = C + 8, LDL = VB + 8, NT = C / 32;
   __shared__ __attribute__((aligned(16))) uint16_t sH[HB * LD];
@@ -305,7 +379,7 @@ __global__ __launch_bounds__(256) void ce_bwd_dw_kernel(const uint16_t* __restri
   const int v0 = blockIdx.x * VB;
   const int mt_begin = blockIdx.y * tiles_per_split;
   const int mt_end = min((M + HB - 1) / HB, mt_begin + tiles_per_split);
-  const float gs = gscale[0];
+  const float gs = gout[0] / fmaxf(count[0], 1.f);
   stage_rows<C>(sW, LD, W, v0, V);
   if (threadIdx.x < VB) sB[threadIdx.x] = v0 + (int)threadIdx.x < V ? bias[v0 + threadIdx.x] * kL2E : -__builtin_inff();
   const int rl = 32 * (w >> 1) + (l & 31);
@@ -319,7 +393,7 @@ __global__ __launch_bounds__(256) void ce_bwd_dw_kernel(const uint16_t* __restri
   bf16x8 hr[C / 32];
   float aux = 0.f;  // threads [0,64): LSE * log2e of row tid, [64,128): label of row tid-64
   auto fetch = [&](int mt) {
-    fetch_rows<C>(hr, Hm, mt * HB, M);
+    fetch_hrows<C>(hr, Hm, hidx, mt * HB, M);
     const int t = threadIdx.x & 63, gr = mt * HB + t;
     if (threadIdx.x < 64) aux = gr < M ? lse[gr] * kL2E : 0.f;
     else if (threadIdx.x < 128) aux = __int_as_float(gr < M ? (int)labels[gr] : -100);
@@ -435,7 +509,8 @@ __global__ void select_rows_kernel(const int64_t* __restrict__ labels, int L, in
 
 __global__ void select_global_kernel(const int* __restrict__ count, int B, int cap, const int64_t* __restrict__ lab_b,
                                      int gcap, int64_t* __restrict__ gidx, int64_t* __restrict__ glab,
-                                     float* __restrict__ total, bool* __restrict__ overflow) {
+                                     float* __restrict__ total, bool* __restrict__ overflow,
+                                     bool* __restrict__ sticky) {
   extern __shared__ int sOffs[];  // [B + 1] exclusive prefix of min(count, cap)
   if (threadIdx.x == 0) {
     int acc = 0, all = 0;
@@ -449,7 +524,9 @@ __global__ void select_global_kernel(const int* __restrict__ count, int B, int c
     }
     sOffs[B] = acc;
     total[0] = (float)all;
-    overflow[0] = ovf || acc > gcap;
+    ovf = ovf || acc > gcap;
+    overflow[0] = ovf;
+    if (sticky != nullptr && ovf) sticky[0] = true;  // the persistent per-device flag (never cleared here)
   }
   lds_sync();
   const int used = sOffs[B] < gcap ? sOffs[B] : gcap;
@@ -469,10 +546,11 @@ __global__ void select_global_kernel(const int* __restrict__ count, int B, int c
 }
 
 void mlm_select_launch(const int64_t* labels, int B, int L, int cap, int gcap, int64_t* idx_b, int64_t* lab_b,
-                       int* count, int64_t* gidx, int64_t* glab, float* total, bool* overflow, hipStream_t st) {
+                       int* count, int64_t* gidx, int64_t* glab, float* total, bool* overflow, bool* sticky,
+                       hipStream_t st) {
   hipLaunchKernelGGL(select_rows_kernel, dim3(B), dim3(256), 0, st, labels, L, cap, idx_b, lab_b, count);
   hipLaunchKernelGGL(select_global_kernel, dim3(1), dim3(1024), (B + 1) * sizeof(int), st, count, B, cap, lab_b, gcap,
-                     gidx, glab, total, overflow);
+                     gidx, glab, total, overflow, sticky);
 }
 
 // vocab splits so that a launch has ≈ target workgroups (several per CU hide the W-chunk latency);
@@ -485,17 +563,22 @@ static int pick_split(int M, int nchunks, int target) {
   return (nchunks + cps - 1) / cps;
 }
 
-void ce_fwd_launch(int C, const uint16_t* Hm, const int64_t* labels, const uint16_t* W, const float* bias, int M,
-                   int V, float* part_ms, float* picked, float* loss_rows, float* lse, int nsplit, hipStream_t st) {
+int ce_combine_blocks(int M);
+
+void ce_fwd_launch(int C, const float* Hm, const int64_t* hidx, const int64_t* labels, const uint16_t* W,
+                   const float* bias, int M, int V, float* part_ms, float* picked, float* lse, const float* count,
+                   float* loss, float* blk, unsigned* ticket, int nsplit, hipStream_t st) {
   const int nchunks = (V + VB - 1) / VB;
   const int cps = (nchunks + nsplit - 1) / nsplit;
   dim3 grid((M + HB - 1) / HB, nsplit);
-  if (C == 64) hipLaunchKernelGGL(ce_fwd_kernel<64>, grid, dim3(256), 0, st, Hm, labels, W, bias, M, V, cps, part_ms, picked);
-  else if (C == 128) hipLaunchKernelGGL(ce_fwd_kernel<128>, grid, dim3(256), 0, st, Hm, labels, W, bias, M, V, cps, part_ms, picked);
-  else if (C == 32) hipLaunchKernelGGL(ce_fwd_kernel<32>, grid, dim3(256), 0, st, Hm, labels, W, bias, M, V, cps, part_ms, picked);
-  hipLaunchKernelGGL(ce_combine_kernel, dim3((M + 255) / 256), dim3(256), 0, st, part_ms, picked, labels, M, nsplit,
-                     loss_rows, lse);
+  if (C == 64) hipLaunchKernelGGL(ce_fwd_kernel<64>, grid, dim3(256), 0, st, Hm, hidx, labels, W, bias, M, V, cps, part_ms, picked);
+  else if (C == 128) hipLaunchKernelGGL(ce_fwd_kernel<128>, grid, dim3(256), 0, st, Hm, hidx, labels, W, bias, M, V, cps, part_ms, picked);
+  else if (C == 32) hipLaunchKernelGGL(ce_fwd_kernel<32>, grid, dim3(256), 0, st, Hm, hidx, labels, W, bias, M, V, cps, part_ms, picked);
+  hipLaunchKernelGGL(ce_combine_kernel, dim3(ce_combine_blocks(M)), dim3(256), 0, st, part_ms, picked, labels, M, nsplit,
+                     lse, count, loss, blk, ticket);
 }
+
+int ce_combine_blocks(int M) { return (M + 255) / 256; }
 
 int ce_num_splits(int M, int V) { return pick_split(M, (V + VB - 1) / VB, 2048); }
 
@@ -508,8 +591,8 @@ int ce_dw_splits(int M, int V) {
   return (mtiles + tps - 1) / tps;
 }
 
-void ce_bwd_launch(int C, const uint16_t* Hm, const int64_t* labels, const uint16_t* W, const float* bias,
-                   const float* lse, const float* gscale, int M, int V, float* dH, long long dh_rows, const int64_t* rowmap, float* dW,
+void ce_bwd_launch(int C, const float* Hm, const int64_t* hidx, const int64_t* labels, const uint16_t* W,
+                   const float* bias, const float* lse, const float* gout, const float* count, int M, int V, float* dH, long long dh_rows, const int64_t* rowmap, float* dW,
                    float* db, int accumulate, float* slab, int det, hipStream_t st) {
   const int nchunks = (V + VB - 1) / VB;
   // dH partials are added atomically: few splits; deterministic mode: one (a single writer per
@@ -527,8 +610,10 @@ void ce_bwd_launch(int C, const uint16_t* Hm, const int64_t* labels, const uint1
   }
   dim3 ga((M + HB - 1) / HB, nsplit), gb(nchunks, rsplit);
 #define CEB(CC)                                                                                                  \
-  hipLaunchKernelGGL(ce_bwd_dh_kernel<CC>, ga, dim3(256), 0, st, Hm, labels, W, bias, lse, gscale, M, V, cps, dH, rowmap, dh_rows); \
-  hipLaunchKernelGGL(ce_bwd_dw_kernel<CC>, gb, dim3(256), 0, st, Hm, labels, W, bias, lse, gscale, M, V, tps, dW, db, \
+  hipLaunchKernelGGL(ce_bwd_dh_kernel<CC>, ga, dim3(256), 0, st, Hm, hidx, labels, W, bias, lse, gout, count, M, V, cps, dH, \
+                     rowmap, dh_rows);                                                                           \
+  hipLaunchKernelGGL(ce_bwd_dw_kernel<CC>, gb, dim3(256), 0, st, Hm, hidx, labels, W, bias, lse, gout, count, M, V, tps, \
+                     dW, db,                                                                                     \
                      slab)
   if (C == 64) { CEB(64); }
   else if (C == 128) { CEB(128); }

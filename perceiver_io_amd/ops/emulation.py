@@ -386,7 +386,7 @@ def wgrad(g, a, amode, mean, rstd, lnw, lnb, rows_per_wg, dW, db=None, pe=None, 
         _acc(db, g.float().sum(0))
 
 
-def mlm_select(labels, cap, gcap):
+def mlm_select(labels, cap, gcap, sticky=None):
     B, L = labels.shape
     sel = labels != -100
     pos = torch.cumsum(sel.to(torch.int64), 1) - 1
@@ -408,28 +408,38 @@ def mlm_select(labels, cap, gcap):
     glab[:m] = lab_b.reshape(-1)[flat[:m]]
     total = count.sum().float().reshape(1)
     ovf = ((count > cap).any() | (n.sum() > gcap)).reshape(1)
+    if sticky is not None:
+        sticky.logical_or_(ovf.reshape(sticky.shape))
     return idx_b, lab_b, gidx, glab, total, ovf
 
 
-def ce_fwd(h, labels, w, bias):
-    logits = _bf(h.float()) @ _bf(w.float()).t() + bias
+def _ce_rows(h, idx):
+    return h if idx is None else h.index_select(0, idx)
+
+
+def ce_fwd(h, idx, labels, w, bias, count):
+    """→ (mean loss Σ rows / max(count, 1) as a 0-dim tensor, per-row lse); rows of ``h`` are
+    gathered through ``idx`` when given."""
+    logits = _bf(_ce_rows(h, idx).float()) @ _bf(w.float()).t() + bias
     lse = torch.logsumexp(logits, -1)
     valid = labels >= 0
     picked = logits.gather(1, labels.clamp(min=0)[:, None])[:, 0]
     loss = torch.where(valid, lse - picked, torch.zeros_like(lse))
-    return loss, lse
+    return loss.sum() / count.reshape(()).clamp(min=1), lse
 
 
-def ce_bwd(h, labels, w, bias, lse, gscale, dH, dW, db, accumulate, rowmap=None, slab=False):
+def ce_bwd(h, idx, labels, w, bias, lse, gout, count, dH, dW, db, accumulate, rowmap=None, slab=False):
     """slab=True: dW | db are returned as a one-row (1, V·C + V₄) slab instead of being added."""
     if slab:
         gw, gb = torch.zeros_like(dW), torch.zeros_like(db)
-        ce_bwd(h, labels, w, bias, lse, gscale, dH, gw, gb, False, rowmap)
+        ce_bwd(h, idx, labels, w, bias, lse, gout, count, dH, gw, gb, False, rowmap)
         V = w.shape[0]
         out = torch.zeros(1, dW.numel() + (V + 3) // 4 * 4, dtype=dW.dtype, device=dW.device)
         out[0, :dW.numel()] = gw.reshape(-1)
         out[0, dW.numel():dW.numel() + V] = gb
         return out
+    h = _ce_rows(h, idx)
+    gscale = gout.reshape(()) / count.reshape(()).clamp(min=1)
     logits = _bf(h.float()) @ _bf(w.float()).t() + bias
     p = torch.exp(logits - lse[:, None])
     valid = (labels >= 0).float()[:, None]
@@ -464,14 +474,32 @@ def embed_bwd(ids, g, dE, dP, scale):
         dP[: ids.shape[1]] += g.sum(0)
 
 
-def text_mask(x, pad, u, rid, unk, mask, p):
+def _unit24(h):
+    return (h >> 8).to(torch.float32) * (1.0 / 16777216.0)
+
+
+def _mulhi32(a, b: int):
+    """floor(a · b / 2^32) for uint32 a (int64 tensor) and b < 2^32, exact in int64."""
+    return ((a >> 16) * b + (((a & 0xFFFF) * b) >> 16)) >> 16
+
+
+def text_mask(x, pad, state, unk, mask, p, lo, hi, advance=True):
+    """Counter-hash BERT masking, bit-exact with ``text_mask_kernel`` (elementwise.hip)."""
+    seed = int(state[0].item()) & 0xFFFFFFFFFFFFFFFF
+    ctr = int(state[1].item())
+    key = hash3(torch.tensor(seed & M32), torch.tensor(seed >> 32), torch.tensor(ctr & M32))
+    i = torch.arange(x.numel(), device=x.device, dtype=torch.int64).view(x.shape)
+    h = [hash3(key.to(x.device), torch.tensor(k, device=x.device), i) for k in range(4)]
     special = x == unk
     if pad is not None:
         special = special | pad
-    sel = ~special & (u[0] < p)
-    msk = sel & (u[1] < 0.9)
-    rnd = msk & (u[2] < 1.0 / 9.0)
+    sel = ~special & (_unit24(h[0]) < p)
+    msk = sel & (_unit24(h[1]) < 0.9)
+    rnd = msk & (_unit24(h[2]) < 1.0 / 9.0)
+    rid = lo + _mulhi32(h[3], hi - lo)
     xm = torch.where(rnd, rid, torch.where(msk, torch.full_like(x, mask), x))
+    if advance:
+        state[1] += 1
     return xm, torch.where(sel, x, torch.full_like(x, -100))
 
 
@@ -524,6 +552,10 @@ def get_deterministic():
 
 def cast_bf16(x, y):
     y.copy_(x.to(torch.bfloat16).view(y.shape))
+
+
+def batch_sum2(a, b):
+    return a.sum(0), b.sum(0)
 
 
 def index_add_rows(dst, idx, src):

@@ -261,6 +261,11 @@ class KVSource:
         self.pe = pe
         self.kin = kin if kin is not None else x.shape[-1]
         self.entries = {}
+        # input-gradient hand-off between the projections of different layers (layer_1 and
+        # layer_n both project this input): each backward adds the previous one's dX as the
+        # residual of its ln_linear_bwd, and only the last returns the total to autograd
+        self.pending_dx = None
+        self.owners_left = None
 
     @property
     def channels(self) -> int:
@@ -411,6 +416,7 @@ class _LayerFn(torch.autograd.Function):
         # residual dropout (p_attn: the layer's one dropout rate) in the kernel epilogues
         z, y, m2, r2, u = K.post_attn_fwd(o2, xq2, wo, bo, g2, be2, EPS, w1, b1, w2, b2, seed=seed, p=p_attn)
         ctx.spec, ctx.bw, ctx.seed, ctx.p_attn = spec, bw, seed, p_attn
+        ctx.src = src if spec.cross else None
         ctx.dims = (B, Bq, Nq, C, H, D, scale)
         ctx.kv_grad = x_kv is not None and ctx.needs_input_grad[6]
         ctx.has_mask = kmask is not None
@@ -514,8 +520,11 @@ class _LayerFn(torch.autograd.Function):
                 dkv = ent["dkv"]
                 dq, _, _ = K.attn_bwd(qx, kv3[:, :, :C], kv3[:, :, C:], kmask, o, do.view(B, Nq, C), lse, delta3, H,
                                       D, scale, ctx.p_attn, ctx.seed, None, dkv[:, :, :C], dkv[:, :, C:], acc)
-            if Bq == 1 and B > 1:
-                dq2, dres = dq.sum(0), dy.view(B, Nq, C).sum(0)
+            if Bq == 1 and B > 1 and dq.shape[0] == B:
+                # broadcast latent queries: both batch sums in one deterministic kernel
+                dq2, dres = K.batch_sum2(dq.contiguous(), dy.view(B, Nq, C))
+            elif Bq == 1 and B > 1:  # dq already summed (fused pe path)
+                dq2, dres = dq.reshape(Nq, C), dy.view(B, Nq, C).sum(0)
             else:
                 dq2, dres = dq.reshape(B * Nq, C), dy
             Ckv = g_kv.shape[0]
@@ -555,8 +564,19 @@ class _LayerFn(torch.autograd.Function):
                     (gbias[0, C:3 * C] if rep_mode else gbias[C:3 * C]).add_(db)
                 elif WGRAD_SLAB and Rkv < TALL_ROWS:
                     sl = _GradSlab(Rkv, [Ckv, Ckv, 2 * C * Ckv, 2 * C], dz2)
-                    dx_kv = K.ln_linear_bwd(dkv2, wkv, xkv2, mean_kv, rstd_kv, g_kv, b_kv, None, ctx.kv_grad,
+                    src = ctx.src
+                    chain = src is not None and ctx.kv_grad and ctx.kv_pe is None
+                    if chain and src.owners_left is None:
+                        src.owners_left = len(src.entries)
+                    dx_kv = K.ln_linear_bwd(dkv2, wkv, xkv2, mean_kv, rstd_kv, g_kv, b_kv,
+                                            src.pending_dx if chain else None, ctx.kv_grad,
                                             *sl.targets(), ctx.kv_pe, Ckv, slab=True, **_take_job())
+                    if chain:  # hand the partial input gradient on; the last projection returns it
+                        src.owners_left -= 1
+                        if src.owners_left > 0:
+                            src.pending_dx, dx_kv = dx_kv, None
+                        else:
+                            src.pending_dx = src.owners_left = None
                     if spec.packed:
                         dwkv = flat(ps[4], C * C, 3 * C * C)
                     else:

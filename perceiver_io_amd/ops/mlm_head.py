@@ -68,40 +68,50 @@ def capacity(n_positions: int, p: float = 0.15) -> int:
 
 
 class _MaskedCE(torch.autograd.Function):
-    """Mean CE over rows ``idx`` of ``h`` (``idx=None``: every row, ``h`` already compacted)."""
+    """Mean CE over rows ``idx`` of ``h`` (``idx=None``: every row, ``h`` already compacted).
+
+    The kernels read the fp32 rows of ``h`` through ``idx`` (no gathered / bf16 copy), finalise
+    the mean ``Σ rows / max(count, 1)`` in the combine kernel and form the row-loss gradient
+    ``g / max(count, 1)`` on the device: no framework kernels around the head."""
 
     @staticmethod
     def forward(ctx, h, weight, bias, idx, labels_c, count):
         c = h.shape[-1]
         h2 = h.reshape(-1, c)
-        hs = (h2 if idx is None else h2.index_select(0, idx)).to(torch.bfloat16).contiguous()
+        if h2.dtype != torch.float32 or not h2.is_contiguous():
+            h2 = h2.float().contiguous()
+        cnt = count.reshape(1)
+        if cnt.dtype != torch.float32:
+            cnt = cnt.to(torch.float32)
         from .fused import weight_cache
 
         wb = weight_cache.get(weight)  # bf16 shadow written by the fused optimizer
-        loss_rows, lse = ext.ce_fwd(hs, labels_c, wb, bias.contiguous())
-        denom = count.clamp(min=1).to(torch.float32)
-        ctx.save_for_backward(hs, wb, bias, lse, idx if idx is not None else torch.empty(0, dtype=torch.int64),
-                              labels_c, denom)
+        loss, lse = ext.ce_fwd(h2, idx, labels_c, wb, bias.contiguous(), cnt)
+        ctx.save_for_backward(h2, wb, bias, lse, idx if idx is not None else torch.empty(0, dtype=torch.int64),
+                              labels_c, cnt)
         ctx.hshape = h.shape
         ctx.weight, ctx.bias_p = weight, bias
-        return loss_rows.sum() / denom
+        return loss
 
     @staticmethod
     def backward(ctx, g):
-        hs, wb, bias, lse, idx, labels_c, denom = ctx.saved_tensors
+        h2, wb, bias, lse, idx, labels_c, cnt = ctx.saved_tensors
         weight = ctx.weight
-        gscale = (g.to(torch.float32) / denom).reshape(1).contiguous()
+        gout = g.reshape(1)
+        if gout.dtype != torch.float32:
+            gout = gout.to(torch.float32)
         # vocab-head parameter gradients are accumulated in place into .grad (flat buffer views);
         # the hidden-state gradient rows land straight at their source positions (rowmap)
         for p in (weight, ctx.bias_p):
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
         shp = ctx.hshape
-        dh = torch.zeros((shp[0] * shp[1], shp[2]), device=hs.device, dtype=torch.float32)
+        dh = torch.zeros((h2.shape[0], shp[-1]), device=h2.device, dtype=torch.float32)
         from . import fused
 
-        slab = ext.ce_bwd(hs, labels_c, wb, bias.contiguous(), lse, gscale, dh, weight.grad, ctx.bias_p.grad, True,
-                          idx if idx.numel() else None, slab=fused.WGRAD_SLAB)
+        ix = idx if idx.numel() else None
+        slab = ext.ce_bwd(h2, ix, labels_c, wb, bias.contiguous(), lse, gout.contiguous(), cnt, dh, weight.grad,
+                          ctx.bias_p.grad, True, ix, slab=fused.WGRAD_SLAB)
         if slab is not None:  # dW / db row-split partials: reduced by the next backward kernel
             fused.defer_slab(ext, slab, [weight.grad.view(-1), ctx.bias_p.grad.view(-1)], [0, weight.numel()])
         return dh.view(shp), None, None, None, None, None
@@ -242,8 +252,11 @@ def masked_decode_loss(decoder, x_latent: torch.Tensor, labels: torch.Tensor, p:
     lin = decoder.output_adapter.linear
     cap = row_capacity(L, p)
     if use_hip(x_latent) and lin.weight.shape[1] in (32, 64, 128):
-        idx, _, gidx, glab, total, ovf = ext.require().mlm_select(labels.contiguous(), cap, capacity(B * L, p))
-        _record(ovf)
+        # the kernel ORs the overflow into the persistent per-device flag itself
+        idx, _, gidx, glab, total, ovf = ext.require().mlm_select(labels.contiguous(), cap, capacity(B * L, p),
+                                                                  overflow_flag(labels.device).view(1))
+        global _overflow
+        _overflow = ovf
         q = _GatherQueries.apply(decoder.output, idx.reshape(-1)).view(B, cap, -1)
         h = decoder.cross_attention(q, x_latent)
         return _MaskedCE.apply(h, lin.weight, lin.bias, gidx, glab, total)

@@ -63,10 +63,11 @@ def shape_key(obj):
 class _Captured:
     """One captured step: the graph, its static input batch and its static outputs."""
 
-    __slots__ = ("graph", "batch", "loss", "state")
+    __slots__ = ("graph", "batch", "loss", "state", "seed_grad")
 
-    def __init__(self, graph, batch, loss, state):
+    def __init__(self, graph, batch, loss, state, seed_grad=None):
         self.graph, self.batch, self.loss, self.state = graph, batch, loss, state
+        self.seed_grad = seed_grad  # read by the captured backward: kept alive with the graph
 
 
 def _to(obj, device):
@@ -153,18 +154,21 @@ class StepEngine:
             loss.backward()
             del loss
         opt.flat.zero_grad_buffers()
+        # the backward seed lives outside the graph (autograd would fill a fresh ones tensor
+        # inside it on every replay)
+        one = torch.ones((), device=self.device)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=self.stream):
             opt.flat.zero_grad_buffers()
             loss = self.loss_fn(static)
-            loss.backward()
+            loss.backward(one if loss.dim() == 0 and loss.dtype == one.dtype else None)
             if self._opt_in_graph:
                 if self.reducer is not None and self.reducer.enabled:
                     self.reducer.finish()
                 opt.device_update()
         state = self.state_hooks[0]() if self.state_hooks is not None else None
         self.captures += 1
-        return _Captured(g, static, loss, state)
+        return _Captured(g, static, loss, state, one)
 
     def _graph_for(self, batch) -> _Captured:
         """The captured step for this batch's shape (captured on first sight, LRU-cached)."""

@@ -378,21 +378,31 @@ def test_fused_cross_entropy(M, V, C):
     bias = torch.randn(V, device=DEV) * 0.1
     lab = torch.randint(0, V, (M,), device=DEV)
     lab[::7] = -100
-    l1, s1 = _ext().ce_fwd(h, lab, w, bias)
-    l2, s2 = _emu().ce_fwd(h, lab, w, bias)
-    close(l1, l2, 1e-2, "loss")
-    close(s1, s2, 1e-3, "lse")
-    gs = torch.tensor([0.37], device=DEV)
+    hf = h.float()  # bf16-exact fp32 rows (the kernels cast on load)
+    cnt = torch.tensor([float((lab >= 0).sum())], device=DEV)
+    l2, s2 = _emu().ce_fwd(hf, None, lab, w, bias, cnt)
+    for _ in range(3):  # the loss finalisation's ticket is reset by every launch
+        l1, s1 = _ext().ce_fwd(hf, None, lab, w, bias, cnt)
+        close(l1, l2, 1e-3, "loss")
+        close(s1, s2, 1e-3, "lse")
+    # gathered rows: row r of the head input is hbig[idx[r]]
+    idx = torch.randperm(2 * M, device=DEV)[:M]
+    hbig = torch.zeros(2 * M, C, device=DEV)
+    hbig[idx] = hf
+    lg, sg = _ext().ce_fwd(hbig, idx, lab, w, bias, cnt)
+    close(lg, l2, 1e-3, "loss gathered")
+    close(sg, s2, 1e-3, "lse gathered")
+    gout = torch.tensor([0.37], device=DEV)
     rowmap = torch.randperm(3 * M, device=DEV)[:M]  # scatter rows into a larger (3M, C) gradient
     outs = []
     for K in (_ext(), _emu()):
         dH = torch.zeros(M, C, device=DEV)
         dW = torch.full((V, C), 7.0, device=DEV)  # overwritten (accumulate=False)
         db = torch.zeros(V, device=DEV)
-        K.ce_bwd(h, lab, w, bias, s2, gs, dH, dW, db, False, None)
+        K.ce_bwd(hf, None, lab, w, bias, s2, gout, cnt, dH, dW, db, False, None)
         dHs = torch.zeros(3 * M, C, device=DEV)
         dW2, db2 = dW.clone(), db.clone()
-        K.ce_bwd(h, lab, w, bias, s2, gs, dHs, dW2, db2, True, rowmap)
+        K.ce_bwd(hbig, idx, lab, w, bias, s2, gout, cnt, dHs, dW2, db2, True, rowmap)
         outs.append((dH, dW, db, dHs, dW2, db2))
     for a, b, n in zip(outs[0], outs[1], ("dH", "dW", "db", "dH rowmap", "dW acc", "db acc")):
         close(a, b, 3e-2, n)
@@ -421,11 +431,18 @@ def test_embed_mask_adamw():
         close(r[0][1], r[1][1], 1e-5, f"dP {Bb}x{Lb}x{Cb}")
     x = torch.randint(0, V, (B, L), device=DEV)
     pad = torch.rand(B, L, device=DEV) < 0.2
-    u = torch.rand(3, B, L, device=DEV)
-    rid = torch.randint(3, V, (B, L), device=DEV)
-    a = _ext().text_mask(x, pad, u, rid, 1, 2, 0.15)
-    b = _emu().text_mask(x, pad, u, rid, 1, 2, 0.15)
-    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    # counter-hash masking: bit-exact with the emulation, and the kernel advances the counter
+    # (ticket reset) so consecutive launches draw different masks
+    st_k = torch.tensor([0x123456789AB, 5, 0], device=DEV)
+    st_e = st_k.clone()
+    for _ in range(3):
+        a = _ext().text_mask(x, pad, st_k, 1, 2, 0.15, 3, V, True)
+        b = _emu().text_mask(x, pad, st_e, 1, 2, 0.15, 3, V, True)
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+        assert torch.equal(st_k, st_e) and int(st_k[2]) == 0
+    assert int(st_k[1]) == 8
+    c = _ext().text_mask(x, pad, st_k, 1, 2, 0.15, 3, V, False)
+    assert not torch.equal(c[1], a[1]) and int(st_k[1]) == 8
     n = 10000
     res = []
     for K in (_ext(), _emu()):

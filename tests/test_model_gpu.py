@@ -180,8 +180,8 @@ def _fixed_mask_engine(lit, graph, ids, pad, lr=1e-3, warmup=1):
     from perceiver_io_amd.train.engine import StepEngine
 
     m = lit.model
-    with torch.no_grad():
-        xm, lab = m.masking(ids, pad)
+    with torch.no_grad():  # a fixed generator: every engine of a test sees the same masking
+        xm, lab = m.masking(ids, pad, generator=torch.Generator(device="cuda").manual_seed(7))
     opt = FusedAdamW(m.parameters(), lr=lr)
     return StepEngine(lambda b: m.loss(b[1], b[2], labels=lab, x_masked=xm), opt, device="cuda", graph=graph,
                       warmup_eager=warmup)
@@ -336,7 +336,7 @@ def _det_run(graph, steps=4, image=False):
         pad[3, 40:] = True
         m = lit.model
         with torch.no_grad():
-            xm, lab = m.masking(ids, pad)
+            xm, lab = m.masking(ids, pad, generator=torch.Generator(device="cuda").manual_seed(7))
         opt = FusedAdamW(m.parameters(), lr=1e-3, max_grad_norm=0.5)
         eng = StepEngine(lambda b: m.loss(b[1], b[2], labels=lab, x_masked=xm), opt, device="cuda", graph=graph,
                          warmup_eager=1)

@@ -102,7 +102,36 @@ def test_text_adapter_and_masking_semantics():
     assert abs(masked.float().sum().item() / sel.float().sum().item() - 0.8) < 0.03
     assert torch.equal(lab[sel], x[sel]) and torch.equal(xm[~sel], x[~sel])
     rnd = sel & (xm != 2) & (xm != x)
-    assert rnd.any() and (xm[rnd] >= 3).all()
+    assert rnd.any() and (xm[rnd] >= 3).all() and (xm[rnd] < 1000).all()
+    kept = sel & (xm == x)  # the 10 % left unchanged
+    assert abs(kept.float().sum().item() / sel.float().sum().item() - 0.1) < 0.02
+
+
+def test_masking_counter_state_and_generator():
+    """The device-resident counter advances per call (fresh masks, as on every replay of a
+    captured step); an explicit generator reproduces a masking and leaves the state alone."""
+    from perceiver_io_amd.ops import masking
+
+    masking.reset_mask_state()
+    torch.manual_seed(11)
+    mk = TextMasking(500)
+    x = torch.randint(3, 500, (8, 256))
+    st = masking.mask_state(x.device)
+    c0 = int(st[1])
+    _, l1 = mk(x)
+    _, l2 = mk(x)
+    assert int(st[1]) == c0 + 2 and not torch.equal(l1, l2)
+    masking.reset_mask_state()
+    torch.manual_seed(11)
+    torch.randint(3, 500, (8, 256))  # the same generator draws as before the first state
+    _, l1b = mk(x)
+    assert torch.equal(l1, l1b)  # torch.manual_seed reproduces the state's seed
+    g1, g2 = torch.Generator().manual_seed(3), torch.Generator().manual_seed(3)
+    c1 = int(masking.mask_state(x.device)[1])
+    a = mk(x, generator=g1)
+    b = mk(x, generator=g2)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    assert int(masking.mask_state(x.device)[1]) == c1
 
 
 def test_encoder_weight_sharing():

@@ -19,9 +19,10 @@ run() {  # run <name> <timeout-s> <cmd...>
   fi
   return 0
 }
-run build 900 python -m perceiver_io_amd.csrc.build
+# the in-tree .so (built on the CPU host) travels with the snapshot; "build" re-links it on the box
 for step in "$@"; do
   case "$step" in
+    build)    run build 900 python -m perceiver_io_amd.csrc.build ;;
     smoke)    run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     kernels)  run kernels 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     kernels_all) run kernels_all 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
