@@ -89,6 +89,13 @@ void text_mask_launch(const int64_t*, const bool*, int64_t*, int64_t*, int64_t*,
 void sumsq_launch(const float*, long long, float*, hipStream_t);
 void index_add_rows_launch(float*, long long, const int64_t*, const float*, long long, int, hipStream_t);
 void batch_sum2_launch(const float*, const float*, float*, float*, int, long long, hipStream_t);
+void pe_gemm_launch(const uint16_t*, const uint16_t*, float*, int, int, int, hipStream_t);
+struct PeGradTargets { float *dWa, *dWb, *db, *dg, *dbeta; };
+int pe_grad_splits(int);
+void pe_grads_launch(const uint16_t*, const float*, int, int, int, const float*, int, float*, float*, float*,
+                     const float*, const float*, const float*, const float*, int, int, int, PeGradTargets, hipStream_t);
+void pe_weight_prep_launch(const float*, const float*, const float*, const float*, int, int, int, int, uint16_t*, float*,
+                           float*, float*, hipStream_t);
 int pixel_ce_blocks(long long);
 void pixel_ce_fwd_launch(int, int, const float*, const float*, const float*, const int64_t*, const float*, long long,
                          float*, float*, float*, hipStream_t);
@@ -859,6 +866,72 @@ std::vector<Tensor> pe_proj_fwd(Tensor pix, Tensor P, Tensor pes, Tensor pesq, T
   return {y, mean, rstd};
 }
 
+// C (M, N) fp32 = A (M, K) bf16 · B (N, K) bf16ᵀ — the factored projection's per-step PE GEMM
+Tensor pe_gemm(Tensor A, Tensor B) {
+  CHECK_CUDA(A); CHECK_DT(A, torch::kBFloat16); CHECK_DT(B, torch::kBFloat16);
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.is_contiguous() && B.is_contiguous() && A.size(1) == B.size(1),
+              "pe_gemm: A (M, K), B (N, K) contiguous");
+  const int M = (int)A.size(0), N = (int)B.size(0), K = (int)A.size(1);
+  TORCH_CHECK(K % 32 == 0 && N % 128 == 0 && K > 0, "pe_gemm: K a multiple of 32, N a multiple of 128");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(B.data_ptr()) % 16 == 0,
+              "pe_gemm: 16-byte aligned operands");
+  Tensor C = torch::empty({M, N}, A.options().dtype(torch::kFloat32));
+  if (M > 0) pio::pe_gemm_launch(bfp(A), bfp(B), C.data_ptr<float>(), M, N, K, stream());
+  return C;
+}
+
+// weight / LayerNorm gradients of the factored projection, ADDED into the given targets (each
+// optional, fp32 contiguous): D (M, O) = Σ_b dY·rσ, part (nblk, (2 + nc)·O) = [ΣdY | ΣdY·μ·rσ |
+// ΣdY·x̂_c] partial rows, E (M, Kp) the bf16 PE table, W = [Wa; Wb] (O, kin) as two row blocks
+void pe_grads(Tensor D, Tensor part, Tensor E, Tensor Wa, Tensor Wb, Tensor g, Tensor b, int64_t nc, OptT dWa, OptT dWb,
+              OptT db, OptT dg, OptT dbeta) {
+  for (const Tensor* t : {&D, &part, &Wa, &Wb, &g, &b}) {
+    CHECK_CUDA(*t); CHECK_DT(*t, torch::kFloat32);
+    TORCH_CHECK(t->is_contiguous(), "pe_grads: contiguous operands");
+  }
+  CHECK_DT(E, torch::kBFloat16);
+  TORCH_CHECK(E.is_contiguous() && E.dim() == 2 && D.dim() == 2 && E.size(0) == D.size(0), "pe_grads: E (M, Kp), D (M, O)");
+  const int M = (int)D.size(0), O = (int)D.size(1), Kp = (int)E.size(1), kin = (int)g.numel(), Ch = (int)Wa.size(0);
+  const int on = O % 128 == 0 ? 128 : O;  // output columns per workgroup (pe_grads_launch)
+  TORCH_CHECK(Kp % 32 == 0 && Kp <= 384 && O % 32 == 0 && on <= 256 && (Kp / 32) * (on / 32) <= 36 && kin <= Kp,
+              "pe_grads: Kp a multiple of 32 (≤ 384), O a multiple of 128 or ≤ 256, ≤ 36 output tiles per group");
+  TORCH_CHECK(Wa.size(1) == kin && Wb.size(1) == kin && Ch + Wb.size(0) == O && b.numel() == kin, "pe_grads: W shapes");
+  TORCH_CHECK(part.size(1) == (2 + nc) * O, "pe_grads: part width");
+  auto tgt = [](const OptT& t, int64_t n, const char* name) -> float* {
+    if (!t.has_value()) return nullptr;
+    CHECK_DT(*t, torch::kFloat32);
+    TORCH_CHECK(t->is_contiguous() && t->numel() == n, "pe_grads: target ", name);
+    return t->data_ptr<float>();
+  };
+  pio::PeGradTargets tg{tgt(dWa, (int64_t)Ch * kin, "dWa"), tgt(dWb, (int64_t)(O - Ch) * kin, "dWb"), tgt(db, O, "db"),
+                        tgt(dg, kin, "dg"), tgt(dbeta, kin, "dbeta")};
+  const int S = pio::pe_grad_splits(M);
+  auto f32 = D.options();
+  Tensor slab = torch::empty({S, Kp, O}, f32), graw = torch::empty({Kp, O}, f32), tot = torch::empty({(2 + nc) * O}, f32);
+  pio::pe_grads_launch(bfp(E), D.data_ptr<float>(), M, Kp, O, part.data_ptr<float>(), (int)part.size(0),
+                       slab.data_ptr<float>(), graw.data_ptr<float>(), tot.data_ptr<float>(), Wa.data_ptr<float>(),
+                       Wb.data_ptr<float>(), g.data_ptr<float>(), b.data_ptr<float>(), Ch, kin, (int)nc, tg, stream());
+}
+
+// W (O, kin) fp32, γ/β (kin), bias (O) → [Wg (O, Kp) bf16 = W⊙γ on columns [nc, kin) else 0,
+// wpg (nc, O) = (W⊙γ)[:, :nc]ᵀ, gw (O) = W·γ, bw (O) = W·β + bias]
+std::vector<Tensor> pe_weight_prep(Tensor W, Tensor g, Tensor b, Tensor bias, int64_t nc, int64_t Kp) {
+  for (const Tensor* t : {&W, &g, &b, &bias}) {
+    CHECK_CUDA(*t); CHECK_DT(*t, torch::kFloat32);
+    TORCH_CHECK(t->is_contiguous(), "pe_weight_prep: contiguous operands");
+  }
+  const int O = (int)W.size(0), kin = (int)W.size(1);
+  TORCH_CHECK(g.numel() == kin && b.numel() == kin && bias.numel() == O && nc >= 1 && nc < kin && Kp >= kin,
+              "pe_weight_prep: shapes");
+  auto f32 = W.options();
+  Tensor Wg = torch::empty({O, Kp}, f32.dtype(torch::kBFloat16));
+  Tensor wpg = torch::empty({nc, O}, f32), gw = torch::empty({O}, f32), bw = torch::empty({O}, f32);
+  pio::pe_weight_prep_launch(W.data_ptr<float>(), g.data_ptr<float>(), b.data_ptr<float>(), bias.data_ptr<float>(), O,
+                             (int)nc, kin, (int)Kp, bfp_mut(Wg), wpg.data_ptr<float>(), gw.data_ptr<float>(),
+                             bw.data_ptr<float>(), stream());
+  return {Wg, wpg, gw, bw};
+}
+
 // backward pass over dY (R, O): D (M, O) and per-block partials (nblk, (2 + nc)·O) of
 // [Σ dY | Σ dY·μ·rσ | Σ dY·x̂_c (c < nc)]
 std::vector<Tensor> pe_proj_bwd(Tensor dy, Tensor pix, Tensor mean, Tensor rstd, int64_t M) {
@@ -998,6 +1071,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fold_replicas", &fold_replicas);
   m.def("slab_reduce", &slab_reduce);
   m.def("pe_proj_fwd", &pe_proj_fwd);
+  m.def("pe_gemm", &pe_gemm);
+  m.def("pe_weight_prep", &pe_weight_prep);
+  m.def("pe_grads", &pe_grads);
   m.def("pe_proj_bwd", &pe_proj_bwd);
   m.def("attn_bwd_pe", &attn_bwd_pe, py::arg("q"), py::arg("kv"), py::arg("dO"), py::arg("lse"), py::arg("delta"),
         py::arg("mean"), py::arg("rstd"), py::arg("pix"), py::arg("dq"), py::arg("D"), py::arg("part"), py::arg("H"),

@@ -175,6 +175,320 @@ __global__ __launch_bounds__(256) void pe_proj_bwd_kernel(
     part[(long long)blockIdx.x * W + k] = red[k] + red[W + k] + red[2 * W + k] + red[3 * W + k];
 }
 
+// ------------------------------------------------------------------------------------
+// The per-step PE GEMM P'[m, o] = Σ_k Ebf[m, k]·Wg[o, k] (replaces a library GEMM plus the
+// per-step pad / scale / cast kernels around it).  Ebf is the bf16 PE table, zero outside the
+// PE columns [nc, kin) and padded to Kp (a multiple of 32): a constant cached across steps.
+// Wg = (W ⊙ γ) with the same column layout is built each step by pe_weight_prep_kernel, which
+// also emits the per-sample epilogue vectors wpg, gw, bw.
+// Tiles: 128 × 128 outputs per workgroup (2 × 2 waves of 64 × 64, v_mfma_f32_32x32x16_bf16),
+// K in 32-wide chunks staged through double-buffered LDS (k-contiguous rows), the next chunk
+// register-prefetched while the current one is multiplied.  fp32 output (pe_proj_fwd input).
+// ------------------------------------------------------------------------------------
+constexpr int GT = 128, GKC = 32, GLD = GKC + 8;
+
+__global__ __launch_bounds__(256) void pe_gemm_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bw,
+                                                      float* __restrict__ C, int M, int N, int K) {
+  __shared__ __attribute__((aligned(16))) uint16_t sA[2][GT * GLD];
+  __shared__ __attribute__((aligned(16))) uint16_t sB[2][GT * GLD];
+  const int w = wave_id(), l = lane_id(), hh = l >> 5;
+  const int wm = w >> 1, wn = w & 1;
+  const int m0 = blockIdx.x * GT, n0 = blockIdx.y * GT;
+  // chunk staging: 128 rows × 32 k = 512 16-byte pieces per operand, 2 per thread
+  bf16x8 ra[2], rb[2];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = threadIdx.x + 256 * i, row = c >> 2, kk = k0 + (c & 3) * 8;
+      const int gm = m0 + row;
+      const uint16_t* pa = gm < M ? A + (long long)gm * K + kk : reinterpret_cast<const uint16_t*>(kZero32B);
+      ra[i] = *reinterpret_cast<const bf16x8*>(pa);
+      rb[i] = *reinterpret_cast<const bf16x8*>(Bw + (long long)(n0 + row) * K + kk);
+    }
+  };
+  auto stash = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = threadIdx.x + 256 * i, row = c >> 2, kk = (c & 3) * 8;
+      *reinterpret_cast<bf16x8*>(&sA[buf][row * GLD + kk]) = ra[i];
+      *reinterpret_cast<bf16x8*>(&sB[buf][row * GLD + kk]) = rb[i];
+    }
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+  const int nk = K / GKC;
+  fetch(0);
+  for (int kc = 0; kc < nk; ++kc) {
+    const int buf = kc & 1;
+    stash(buf);  // the other buffer is still being read by the previous chunk's MFMAs: double buffer
+    lds_sync();
+    if (kc + 1 < nk) fetch((kc + 1) * GKC);
+#pragma unroll
+    for (int ks = 0; ks < GKC; ks += 16) {
+      bf16x8 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        fa[i] = frag_kc(sA[buf], GLD, 64 * wm + 32 * i, ks);
+        fb[i] = frag_kc(sB[buf], GLD, 64 * wn + 32 * i, ks);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(fa[i], fb[j], acc[i][j]);
+    }
+  }
+  // accumulator: col = lane & 31 (n), row = acc_row (m)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + 64 * wn + 32 * j + (l & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + 64 * wm + 32 * i + acc_row(r, hh);
+        if (m < M) C[(long long)m * N + n] = acc[i][j][r];
+      }
+    }
+}
+
+// one workgroup per output row o of the factored projection (O ≤ 65535 rows, blockDim 256):
+//   Wg[o, k] = W[o, k]·γ[k] for k in [nc, kin), 0 elsewhere (k < Kp), bf16
+//   wpg[c, o] = W[o, c]·γ[c] (c < nc), gw[o] = Σ_k W[o, k]γ[k], bw[o] = Σ_k W[o, k]β[k] + bias[o]
+__global__ __launch_bounds__(256) void pe_weight_prep_kernel(const float* __restrict__ W, const float* __restrict__ g,
+                                                             const float* __restrict__ b, const float* __restrict__ bias,
+                                                             int O, int nc, int kin, int Kp, uint16_t* __restrict__ Wg,
+                                                             float* __restrict__ wpg, float* __restrict__ gw,
+                                                             float* __restrict__ bw) {
+  __shared__ float red[2][4];
+  const int o = blockIdx.x;
+  float sg = 0.f, sb = 0.f;
+  for (int k = threadIdx.x; k < Kp; k += blockDim.x) {
+    float wgk = 0.f;
+    if (k < kin) {
+      const float wv = W[(long long)o * kin + k];
+      wgk = wv * g[k];
+      sg += wgk;
+      sb += wv * b[k];
+      if (k < nc) wpg[(long long)k * O + o] = wgk;
+    }
+    Wg[(long long)o * Kp + k] = f2bf(k >= nc && k < kin ? wgk : 0.f);
+  }
+  sg = wave_sum(sg);
+  sb = wave_sum(sb);
+  if (lane_id() == 0) { red[0][wave_id()] = sg; red[1][wave_id()] = sb; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    gw[o] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    bw[o] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]) + bias[o];
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Backward of the factored projection's weights (replaces a split-K library GEMM, its batch
+// sum and ~20 small framework kernels per call):
+//   A  pe_gemm_tn : slab[s] = Ebf[rows of split s]ᵀ · bf16(D[rows of split s])   (Kp × O fp32)
+//   B  pe_grad_reduce : Graw = Σ_s slab[s],  tot = Σ_blocks part  (= [S | e | Gp])
+//   C  pe_grad_finalize : per input column k,  G[o] = Gp[k][o] (pixel k < nc) or Graw[k][o] − e[o],
+//      dW[o][k] += G·γ_k + S_o·β_k,  dγ_k += Σ_o W[o][k]·G[o],  dβ_k += Σ_o W[o][k]·S_o,  db += S
+// W / dW are split in two row blocks (the separate K and V projection weights, rows [0, Ch) and
+// [Ch, O)).  Every gradient element has exactly one writer: deterministic.
+// ------------------------------------------------------------------------------------
+constexpr int TN_MAXT = 9;  // ≤ 4 × 9 = 36 output 32 × 32 tiles per workgroup (Kp ≤ 288 with 128 columns)
+
+// grid (row splits, column groups): workgroup (s, c) accumulates output columns [c·on, c·on + on)
+// over rows [s·rps, (s+1)·rps) in 32-row chunks (register prefetch one chunk ahead, double-
+// buffered LDS), and stores its (Kp × on) partial into slab[s]
+__global__ __launch_bounds__(256) void pe_gemm_tn_kernel(const uint16_t* __restrict__ E, const float* __restrict__ D,
+                                                         float* __restrict__ slab, int M, int Kp, int O, int on,
+                                                         int rows_per_split) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t tsm[];
+  const int LDE = Kp + 8, LDD = on + 8;
+  uint16_t* sE[2] = {tsm, tsm + 32 * LDE};
+  uint16_t* sD[2] = {tsm + 64 * LDE, tsm + 64 * LDE + 32 * LDD};
+  const int w = wave_id(), l = lane_id(), hh = l >> 5;
+  const int r_begin = blockIdx.x * rows_per_split, r_end = min(M, r_begin + rows_per_split);
+  const int c0 = blockIdx.y * on;
+  const int ntj = on / 32, ntiles = (Kp / 32) * ntj;
+  const int ce = Kp / 8, cd = on / 4;  // 16-byte pieces per E row, float4 per D row slice
+  bf16x8 re[6];  // 32 × Kp/8 ≤ 1536 pieces (Kp ≤ 384)
+  float4 rd[8];  // 32 × on/4 ≤ 2048 (on ≤ 256)
+  // branch-free: rows past the split (or the matrix) read zeros, so the prefetch of the chunk
+  // after the last one is harmless and every fetch is straight-line code (see kZero32B)
+  auto fetch = [&](int r0) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const int c = threadIdx.x + 256 * i, row = c / ce, col = (c % ce) * 8;
+      const bool ok = (c < 32 * ce) & (r0 + row < r_end);
+      const uint16_t* p = ok ? E + (long long)(r0 + row) * Kp + col : reinterpret_cast<const uint16_t*>(kZero32B);
+      re[i] = *reinterpret_cast<const bf16x8*>(p);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = threadIdx.x + 256 * i, row = c / cd, col = (c % cd) * 4;
+      const bool ok = (c < 32 * cd) & (r0 + row < r_end);
+      const float* p = ok ? D + (long long)(r0 + row) * O + c0 + col : kZero32B;
+      rd[i] = *reinterpret_cast<const float4*>(p);
+    }
+  };
+  auto stash = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const int c = threadIdx.x + 256 * i, row = c / ce, col = (c % ce) * 8;
+      if (c < 32 * ce) *reinterpret_cast<bf16x8*>(sE[buf] + row * LDE + col) = re[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = threadIdx.x + 256 * i, row = c / cd, col = (c % cd) * 4;
+      if (c < 32 * cd) {
+        uint2 pk;
+        pk.x = pack2(rd[i].x, rd[i].y);
+        pk.y = pack2(rd[i].z, rd[i].w);
+        *reinterpret_cast<uint2*>(sD[buf] + row * LDD + col) = pk;
+      }
+    }
+  };
+  f32x16 acc[TN_MAXT];
+#pragma unroll
+  for (int t = 0; t < TN_MAXT; ++t) acc[t] = f32x16{};
+  fetch(r_begin);
+  int buf = 0;
+  for (int r0 = r_begin; r0 < r_end; r0 += 32, buf ^= 1) {
+    stash(buf);
+    lds_sync();
+    fetch(r0 + 32);
+#pragma unroll
+    for (int t = 0; t < TN_MAXT; ++t) {
+      const int tile = w + 4 * t;
+      if (tile < ntiles) {  // wave-uniform
+        const int ti = tile / ntj, tj = tile % ntj;
+#pragma unroll
+        for (int ks = 0; ks < 32; ks += 16)
+          acc[t] = mfma32(frag_ks(sE[buf], LDE, 32 * ti, ks), frag_ks(sD[buf], LDD, 32 * tj, ks), acc[t]);
+      }
+    }
+  }
+  // accumulator: col = lane & 31 → o, row = acc_row → k
+  float* out = slab + (long long)blockIdx.x * Kp * O + c0;
+#pragma unroll
+  for (int t = 0; t < TN_MAXT; ++t) {
+    const int tile = w + 4 * t;
+    if (tile < ntiles) {
+      const int ti = tile / ntj, tj = tile % ntj;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) out[(long long)(32 * ti + acc_row(i, hh)) * O + 32 * tj + (l & 31)] = acc[t][i];
+    }
+  }
+}
+
+// Graw = Σ_s slab[s] (Kp·O floats) and tot = Σ_b part[b] ((2 + nc)·O floats) in one launch: a
+// block sums 64 float4 columns with 4 row groups (loads 8 deep), fixed combination order
+__global__ __launch_bounds__(256) void pe_grad_reduce_kernel(const float* __restrict__ slab, int S, long long KO4,
+                                                             const float* __restrict__ part, int nblk, long long W4,
+                                                             float* __restrict__ Graw, float* __restrict__ tot) {
+  __shared__ float4 red[4][64];
+  const int l = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const long long c = (long long)blockIdx.x * 64 + l;  // float4 column of [slab | part]
+  const bool second = c >= KO4;
+  const long long cc = second ? c - KO4 : c;
+  const long long stride = second ? W4 : KO4;
+  const int rows = second ? nblk : S;
+  const float4* src = reinterpret_cast<const float4*>(second ? part : slab) + cc;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c < KO4 + W4) {
+#pragma unroll 8
+    for (int r = g; r < rows; r += 4) {
+      const float4 v = src[(long long)r * stride];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  red[g][l] = acc;
+  __syncthreads();
+  if (g == 0 && c < KO4 + W4) {
+    float4 r = red[0][l];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      const float4 v = red[k][l];
+      r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
+    }
+    reinterpret_cast<float4*>(second ? tot : Graw)[cc] = r;
+  }
+}
+
+struct PeGradTargets {
+  float *dWa, *dWb, *db, *dg, *dbeta;  // dW rows [0, Ch) / [Ch, O) (kin columns each); any may be null
+};
+
+// one block per input column k (< kin), threads over the outputs o
+__global__ __launch_bounds__(256) void pe_grad_finalize_kernel(const float* __restrict__ Graw, const float* __restrict__ tot,
+                                                               const float* __restrict__ Wa, const float* __restrict__ Wb,
+                                                               const float* __restrict__ g, const float* __restrict__ b,
+                                                               int O, int Ch, int kin, int nc, PeGradTargets t) {
+  __shared__ float red[2][4];
+  const int k = blockIdx.x;
+  float sg = 0.f, sb = 0.f;
+  for (int o = threadIdx.x; o < O; o += blockDim.x) {
+    const float S = tot[o];
+    const float G = k < nc ? tot[(long long)(2 + k) * O + o] : Graw[(long long)k * O + o] - tot[O + o];
+    const bool lo = o < Ch;
+    const int oo = lo ? o : o - Ch;
+    const float wv = (lo ? Wa : Wb)[(long long)oo * kin + k];
+    sg += wv * G;
+    sb += wv * S;
+    float* dW = lo ? t.dWa : t.dWb;
+    if (dW) dW[(long long)oo * kin + k] += G * g[k] + S * b[k];
+    if (k == 0 && t.db) t.db[o] += S;
+  }
+  sg = wave_sum(sg);
+  sb = wave_sum(sb);
+  if (lane_id() == 0) { red[0][wave_id()] = sg; red[1][wave_id()] = sb; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (t.dg) t.dg[k] += (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    if (t.dbeta) t.dbeta[k] += (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+  }
+}
+
+int pe_grad_splits(int M) {
+  const int s = (M + 511) / 512;  // ≈ 512 rows (16 chunks) per workgroup, ≤ 96 slab rows
+  return s < 1 ? 1 : (s > 96 ? 96 : s);
+}
+
+void pe_grads_launch(const uint16_t* E, const float* D, int M, int Kp, int O, const float* part, int nblk, float* slab,
+                     float* Graw, float* tot, const float* Wa, const float* Wb, const float* g, const float* b, int Ch,
+                     int kin, int nc, PeGradTargets t, hipStream_t st) {
+  const int S0 = pe_grad_splits(M);
+  const int rps = ((M + S0 - 1) / S0 + 31) / 32 * 32;
+  const int S = (M + rps - 1) / rps;
+  const int on = O % 128 == 0 ? 128 : O;  // output columns per workgroup
+  const size_t lds = (size_t)2 * 32 * ((Kp + 8) + (on + 8)) * sizeof(uint16_t);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pe_gemm_tn_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(pe_gemm_tn_kernel, dim3((unsigned)S, (unsigned)(O / on)), dim3(256), lds, st, E, D, slab, M, Kp, O,
+                     on, rps);
+  const long long KO4 = (long long)Kp * O / 4, W4 = (long long)(2 + nc) * O / 4;
+  hipLaunchKernelGGL(pe_grad_reduce_kernel, dim3((unsigned)((KO4 + W4 + 63) / 64)), dim3(256), 0, st, slab, S, KO4, part,
+                     nblk, W4, Graw, tot);
+  hipLaunchKernelGGL(pe_grad_finalize_kernel, dim3((unsigned)kin), dim3(256), 0, st, Graw, tot, Wa, Wb, g, b, O, Ch, kin,
+                     nc, t);
+}
+
+void pe_gemm_launch(const uint16_t* A, const uint16_t* Bw, float* C, int M, int N, int K, hipStream_t st) {
+  hipLaunchKernelGGL(pe_gemm_kernel, dim3((unsigned)((M + GT - 1) / GT), (unsigned)(N / GT)), dim3(256), 0, st, A, Bw, C,
+                     M, N, K);
+}
+void pe_weight_prep_launch(const float* W, const float* g, const float* b, const float* bias, int O, int nc, int kin,
+                           int Kp, uint16_t* Wg, float* wpg, float* gw, float* bw, hipStream_t st) {
+  hipLaunchKernelGGL(pe_weight_prep_kernel, dim3((unsigned)O), dim3(256), 0, st, W, g, b, bias, O, nc, kin, Kp, Wg, wpg,
+                     gw, bw);
+}
+
 void pe_proj_fwd_launch(const float* pix, int nc, const float* P, const float* pes, const float* pesq,
                         const float* wpg, const float* gw, const float* bw, long long R, int M, int O, int kin,
                         float eps, uint16_t* y, float* mean, float* rstd, hipStream_t st) {

@@ -107,6 +107,34 @@ def ln_linear_fwd(x, lnw, lnb, eps, w, bias, act, res, out_bf16, save_stats, pe=
     return out
 
 
+def pe_gemm(A, B):
+    """bf16 operands, fp32 accumulation and output (csrc/pe_proj.hip pe_gemm_kernel)."""
+    return A.float() @ B.float().t()
+
+
+def pe_weight_prep(W, g, b, bias, nc, Kp):
+    O, kin = W.shape
+    wg = W * g[None, :]
+    Wg = torch.zeros((O, Kp), device=W.device, dtype=torch.float32)
+    Wg[:, nc:kin] = wg[:, nc:]
+    return [Wg.to(torch.bfloat16), wg[:, :nc].t().contiguous(), wg.sum(1), W @ b + bias]
+
+
+def pe_grads(D, part, E, Wa, Wb, g, b, nc, dWa=None, dWb=None, db=None, dg=None, dbeta=None):
+    """csrc/pe_proj.hip pe_grads: factored-projection weight / LN gradients added into targets
+    (the PE GEMM with bf16 operands, fp32 accumulation)."""
+    O, kin, Ch = D.shape[1], g.shape[0], Wa.shape[0]
+    graw = E.float().t() @ D.to(torch.bfloat16).float()
+    tot = part.sum(0)
+    S, e, Gp = tot[:O], tot[O:2 * O], tot[2 * O:].view(nc, O)
+    G = torch.cat([Gp, graw[nc:kin] - e[None, :]], 0).t()  # (O, kin)
+    W = torch.cat([Wa, Wb], 0)
+    dW = G * g[None, :] + S[:, None] * b[None, :]
+    for t, v in ((dWa, dW[:Ch]), (dWb, dW[Ch:]), (db, S), (dg, (W * G).sum(0)), (dbeta, W.t() @ S)):
+        if t is not None:
+            t.view(-1).add_(v.reshape(-1))
+
+
 def pe_proj_fwd(pix, P, pes, pesq, wpg, gw, bw, kin, eps):
     """csrc/pe_proj.hip forward: factored LN + K/V projection over [pixels ‖ PE]."""
     M = P.shape[0]

@@ -287,25 +287,44 @@ class KVSource:
 PE_FACTORED = os.environ.get("PERCEIVER_PE_FACTORED", "1") != "0"
 
 
+_pe_tables = {}
+
+
+def _pe_table(pe, nc: int, kin: int):
+    """Step-invariant PE operands, cached per PE table (refreshed if it is modified): the bf16
+    table Ebf (M, Kp) with only the PE columns [nc, kin) kept (Kp = kin rounded up to 32) and
+    the row sums Σe, Σe² over those columns."""
+    key = (pe.data_ptr(), pe.shape[0], nc, kin)
+    ent = _pe_tables.get(key)
+    if ent is not None and ent[0] is pe and ent[1] == pe._version:
+        return ent[2]
+    kp = -(-kin // 32) * 32
+    pe_e = pe[:, nc:kin]
+    ebf = torch.zeros((pe.shape[0], kp), device=pe.device, dtype=torch.bfloat16)
+    ebf[:, nc:kin] = pe_e.to(torch.bfloat16)
+    tab = (ebf, pe_e.sum(1).contiguous(), (pe_e * pe_e).sum(1).contiguous())
+    _pe_tables[key] = (pe, pe._version, tab)
+    return tab
+
+
 def _pe_proj_fwd(K, pix, pe, g, b, W, bias):
     """pix (B·M, nc) pixel channels, pe (M, ≥Kin) padded PE table with zero pixel columns,
-    g/b (Kin) kv_norm affine, W (O, Kin) fp32 K‖V weights, bias (O) → bf16 (B·M, O), mean, rstd."""
+    g/b (Kin) kv_norm affine, W (O, Kin) fp32 K‖V weights, bias (O) → bf16 (B·M, O), mean, rstd.
+
+    Per step: one weight-prep kernel (W⊙γ in bf16 + the epilogue vectors) and the in-tree MFMA
+    GEMM P' = Ebf·(W⊙γ)ᵀ over the cached bf16 PE table (bf16 operands, fp32 accumulation: the
+    precision of the bf16 K/V it feeds); then the per-sample epilogue (pe_proj_fwd)."""
     nc, kin = pix.shape[1], g.shape[0]
-    pe_e = pe[:, nc:kin]
-    # P' over the whole padded table (pixel and pad columns of pe are zero): an 8-aligned
-    # contraction keeps the library GEMM on its fast path
-    kp = pe.shape[1]
-    ge = torch.zeros(kp, device=g.device, dtype=g.dtype)
-    ge[nc:kin] = g[nc:]
-    wp = torch.zeros((W.shape[0], kp), device=W.device, dtype=W.dtype)
-    wp[:, :kin] = W
-    # bf16 operands, fp32 accumulation: the same product precision as the MFMA projection it
-    # replaces (its output feeds a bf16 K/V), at a fraction of an fp32 library GEMM's time
-    P = torch.mm((pe * ge).to(torch.bfloat16), wp.to(torch.bfloat16).t()).float()
-    wpg = (W[:, :nc] * g[:nc]).t().contiguous()
-    gw = torch.mv(W, g).contiguous()
-    bw = (torch.mv(W, b) + bias).contiguous()
-    return K.pe_proj_fwd(pix, P, pe_e.sum(1).contiguous(), (pe_e * pe_e).sum(1).contiguous(), wpg, gw, bw, kin, EPS)
+    ebf, pes, pesq = _pe_table(pe, nc, kin)
+    O = W.shape[0]
+    if O % 128 == 0 and hasattr(K, "pe_gemm"):
+        wg, wpg, gw, bw = K.pe_weight_prep(W.contiguous(), g.contiguous(), b.contiguous(), bias.contiguous(), nc,
+                                           ebf.shape[1])
+        P = K.pe_gemm(ebf, wg)
+    else:
+        wg, wpg, gw, bw = emulation.pe_weight_prep(W, g, b, bias, nc, ebf.shape[1])
+        P = torch.mm(ebf, wg.t()).float()
+    return K.pe_proj_fwd(pix, P, pes, pesq, wpg, gw, bw, kin, EPS)
 
 
 def _mm_tn_split(a, b):
@@ -546,22 +565,23 @@ class _LayerFn(torch.autograd.Function):
                     dkv2 = dkv.view(B * M, 2 * C)
                     Rkv = dkv2.shape[0]
                 if ent.get("factored"):
-                    Wkv = torch.cat([ps[5], ps[6]], 0)
+                    # (D, partials) from the fused attention backward or a pe_proj_bwd pass, then
+                    # the weight / LN gradients in three kernels, added straight into the targets
                     if ent.get("pe_D") is not None:
-                        dW, db, dg, dbeta = _pe_proj_grads(ent["pe_D"], ent["pe_part"], xkv2.shape[1], ctx.kv_pe,
-                                                           g_kv, b_kv, Wkv)
+                        Dm, part = ent["pe_D"], ent["pe_part"]
                     else:
-                        dW, db, dg, dbeta = _pe_proj_bwd(K, dkv2, xkv2, mean_kv, rstd_kv, ctx.kv_pe, g_kv, b_kv, Wkv, M)
+                        Dm, part = K.pe_proj_bwd(dkv2, xkv2, mean_kv, rstd_kv, M)
+                    nc = xkv2.shape[1]
+                    ebf = _pe_table(ctx.kv_pe, nc, g_kv.shape[0])[0]
 
-                    def add(t, v):
-                        (t[0] if rep_mode else t).view(-1).add_(v.reshape(-1))
+                    def tg(p):
+                        t = gb(p)
+                        return t[0] if rep_mode else t
 
-                    add(gb(g_kv), dg)
-                    add(gb(b_kv), dbeta)
-                    add(gb(ps[5]), dW[:C])
-                    add(gb(ps[6]), dW[C:])
                     gbias = gb(bin_)
-                    (gbias[0, C:3 * C] if rep_mode else gbias[C:3 * C]).add_(db)
+                    K.pe_grads(Dm, part, ebf, ps[5].detach(), ps[6].detach(), g_kv.detach(), b_kv.detach(), nc,
+                               tg(ps[5]), tg(ps[6]), gbias[0, C:3 * C] if rep_mode else gbias[C:3 * C], tg(g_kv),
+                               tg(b_kv))
                 elif WGRAD_SLAB and Rkv < TALL_ROWS:
                     sl = _GradSlab(Rkv, [Ckv, Ckv, 2 * C * Ckv, 2 * C], dz2)
                     src = ctx.src

@@ -553,3 +553,48 @@ def test_pixel_ce_kernels(R, C, K):
         res.append((d, dW, db))
     for a, c, n in zip(res[0], res[1], ("dH", "dW", "db")):
         close(a, c, 1e-4, n)
+
+
+@pytest.mark.parametrize("M,N,K", [(50176, 256, 288), (1000, 128, 32), (333, 384, 96)])
+def test_pe_gemm_and_weight_prep(M, N, K):
+    """In-tree PE GEMM (bf16 operands, fp32 accumulate / output) and the per-step weight prep of
+    the factored K/V projection, against fp32 torch references."""
+    torch.manual_seed(9)
+    A = bf(torch.rand(M, K, device=DEV) * 2 - 1)
+    A[:, :3] = 0
+    B = bf(torch.randn(N, K, device=DEV) * 0.1)
+    c1 = _ext().pe_gemm(A, B)
+    c2 = A.float() @ B.float().t()
+    close(c1, c2, 1e-4, "pe_gemm")
+    kin, nc = K - 5, 3
+    W = torch.randn(N, kin, device=DEV)
+    g, b = torch.randn(kin, device=DEV), torch.randn(kin, device=DEV)
+    bias = torch.randn(N, device=DEV)
+    r1 = _ext().pe_weight_prep(W, g, b, bias, nc, K)
+    r2 = _emu().pe_weight_prep(W, g, b, bias, nc, K)
+    for x, y, n in zip(r1, r2, ("Wg", "wpg", "gw", "bw")):
+        close(x, y, 1e-5, n)
+
+
+@pytest.mark.parametrize("M,O,Kp,kin,nc,nblk", [(50176, 256, 288, 261, 3, 37), (784, 256, 160, 131, 1, 5),
+                                               (1000, 64, 96, 70, 2, 3)])
+def test_pe_grads(M, O, Kp, kin, nc, nblk):
+    """Factored-projection weight / LN gradients (pe_gemm_tn → reduce → finalize), added into
+    pre-filled targets, against the emulation."""
+    torch.manual_seed(10)
+    D = torch.randn(M, O, device=DEV)
+    part = torch.randn(nblk, (2 + nc) * O, device=DEV)
+    E = torch.zeros(M, Kp, device=DEV)
+    E[:, nc:kin] = torch.rand(M, kin - nc, device=DEV) * 2 - 1
+    E = bf(E)
+    Ch = O // 2
+    Wa, Wb = torch.randn(Ch, kin, device=DEV), torch.randn(O - Ch, kin, device=DEV)
+    g, b = torch.randn(kin, device=DEV), torch.randn(kin, device=DEV)
+    outs = []
+    for K in (_ext(), _emu()):
+        t = [torch.full((Ch, kin), 0.5, device=DEV), torch.full((O - Ch, kin), 0.5, device=DEV),
+             torch.ones(O, device=DEV), torch.ones(kin, device=DEV), torch.ones(kin, device=DEV)]
+        K.pe_grads(D, part, E, Wa, Wb, g, b, nc, *t)
+        outs.append(t)
+    for a, c, n in zip(outs[0], outs[1], ("dWa", "dWb", "db", "dgamma", "dbeta")):
+        close(a, c, 2e-3, n)
