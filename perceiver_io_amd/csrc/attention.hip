@@ -187,16 +187,14 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(AttnArgs a, uint16_t
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) s[kh] = mfma32(frag_kc(tK, LDK, 32 * kh, 16 * ks), qf[ks], s[kh]);
       }
-      // scale, mask (only tiles that hold padding keys), tile max
+      // mask (only tiles that hold padding keys) and tile max on the RAW scores (the scale is
+      // positive), then one fma + exp2 per score: p = 2^(s·scale·log2e − m)
       float mt = -INFINITY;
       if (padbits[j] == 0ull) {
 #pragma unroll
         for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            s[kh][i] *= a.scale_log2;
-            mt = fmaxf(mt, s[kh][i]);
-          }
+          for (int i = 0; i < 16; ++i) mt = fmaxf(mt, s[kh][i]);
       } else {
 #pragma unroll
         for (int kh = 0; kh < 2; ++kh) {
@@ -204,14 +202,14 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(AttnArgs a, uint16_t
           const uint32_t word = (uint32_t)(padbits[j] >> (32 * kh)) >> (4 * hh);
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
-            const float v = ((word >> ((i & 3) + 8 * (i >> 2))) & 1u) ? -INFINITY : s[kh][i] * a.scale_log2;
+            const float v = ((word >> ((i & 3) + 8 * (i >> 2))) & 1u) ? -INFINITY : s[kh][i];
             s[kh][i] = v;
             mt = fmaxf(mt, v);
           }
         }
       }
       mt = xor32_max(mt);
-      const float m_new = fmaxf(m_run, mt);
+      const float m_new = fmaxf(m_run, mt * a.scale_log2);
       const float alpha = fast_exp2(m_run - m_new);
       m_run = m_new;
       float ls = 0.f;
@@ -219,7 +217,7 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(AttnArgs a, uint16_t
       for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          s[kh][i] = fast_exp2(s[kh][i] - m_new);
+          s[kh][i] = fast_exp2(fmaf(s[kh][i], a.scale_log2, -m_new));
           ls += s[kh][i];
         }
       if (a.drop_thresh) {  // uniform: the element loop above stays branch-free

@@ -61,6 +61,8 @@ def pick_splits(batch: int, heads: int, nq: int, nk: int) -> int:
     waves = max(1, min(4, (nq + 31) // 32))
     blocks = ((nq + 32 * waves - 1) // (32 * waves)) * heads * batch
     tiles = (nk + 63) // 64
+    if blocks >= 512:  # ≥ 2 workgroups per CU already: a split only adds the combine launch
+        return 1
     want = max(1, 1024 // max(blocks, 1))
     return int(max(1, min(want, tiles // 4 if tiles >= 8 else 1)))
 
