@@ -101,8 +101,8 @@ void pixel_ce_fwd_launch(int, int, const float*, const float*, const float*, con
                          float*, float*, float*, hipStream_t);
 void pixel_ce_bwd_launch(int, int, const float*, const float*, const float*, const int64_t*, const float*,
                          const float*, const float*, long long, float*, float*, float*, float*, hipStream_t);
-void adamw_launch(float*, const float*, float*, float*, uint16_t*, long long, const float*, float, float, float, float,
-                  int, hipStream_t);
+void adamw_launch(float*, float*, float*, float*, uint16_t*, long long, const float*, float, float, float, float,
+                  int, int, hipStream_t);
 void cast_bf16_launch(const float*, uint16_t*, long long, hipStream_t);
 void reduce_probe_launch(const float*, float*, hipStream_t);
 void fold_replicas_launch(float*, float*, long long, int, hipStream_t);
@@ -805,13 +805,14 @@ void pixel_ce_bwd(Tensor h, Tensor w, Tensor b, Tensor labels, Tensor wts, Tenso
 }
 
 void adamw(Tensor p, Tensor g, Tensor m, Tensor v, OptT shadow, Tensor hyper, double eps, double wd, double clip,
-           double gscale, bool l2) {
+           double gscale, bool l2, bool zero_grad) {
   TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && m.is_contiguous() && v.is_contiguous());
   TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel());
   uint16_t* sp = nullptr;
   if (shadow.has_value()) { TORCH_CHECK(shadow->numel() == p.numel()); sp = reinterpret_cast<uint16_t*>(shadow->data_ptr()); }
-  pio::adamw_launch(p.data_ptr<float>(), f32p(g), m.data_ptr<float>(), v.data_ptr<float>(), sp, p.numel(), f32p(hyper),
-                    (float)eps, (float)wd, (float)clip, (float)gscale, l2 ? 1 : 0, stream());
+  pio::adamw_launch(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), sp, p.numel(),
+                    f32p(hyper), (float)eps, (float)wd, (float)clip, (float)gscale, l2 ? 1 : 0, zero_grad ? 1 : 0,
+                    stream());
 }
 
 // self-test of the device cross-lane reductions: (6, 64) = wave_sum, wave_max, half_sum,
@@ -1065,7 +1066,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("p"), py::arg("lo"), py::arg("hi"), py::arg("advance") = true);
   m.def("sumsq", &sumsq);
   m.def("adamw", &adamw, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("shadow"), py::arg("hyper"),
-        py::arg("eps"), py::arg("wd"), py::arg("clip"), py::arg("gscale"), py::arg("l2") = false);
+        py::arg("eps"), py::arg("wd"), py::arg("clip"), py::arg("gscale"), py::arg("l2") = false,
+        py::arg("zero_grad") = false);
   m.def("cast_bf16", &cast_bf16);
   m.def("reduce_probe", &reduce_probe);
   m.def("fold_replicas", &fold_replicas);

@@ -243,10 +243,12 @@ __global__ void sumsq_kernel(const float* __restrict__ g, long long n, float* __
 // hyper[0] = lr, [1] = step (already incremented), [2] = grad sum of squares (if clip > 0),
 // [3] = beta1, [4] = beta2 — read from device memory so schedulers can change them between
 // replays of a captured step.
-__global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+// zero_g: the gradient is cleared as it is consumed (a replayed step then needs no separate
+// zero fill of the flat gradient buffer before its backward)
+__global__ void adamw_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                              float* __restrict__ v, uint16_t* __restrict__ shadow, long long n,
                              const float* __restrict__ hyper, float eps, float wd, float clip, float gscale,
-                             int l2) {
+                             int l2, int zero_g) {
   const float lr = hyper[0], step = hyper[1], beta1 = hyper[3], beta2 = hyper[4];
   const float bc1 = 1.f - powf(beta1, step), bc2 = 1.f - powf(beta2, step);
   // g holds the all-reduced SUM over ranks (gscale = 1 / world makes it the mean): the clip
@@ -263,7 +265,9 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
     float pi = p[i];
     // l2 (torch.optim.Adam weight_decay): the decay joins the (clipped) gradient; else AdamW's
     // decoupled decay of the weights
-    const float gi = l2 ? fmaf(wd, pi, g[i] * gs) : g[i] * gs;
+    const float g0 = g[i];
+    if (zero_g) g[i] = 0.f;
+    const float gi = l2 ? fmaf(wd, pi, g0 * gs) : g0 * gs;
     if (!l2) pi *= 1.f - lr * wd;
     const float mi = beta1 * m[i] + (1.f - beta1) * gi;
     const float vi = beta2 * v[i] + (1.f - beta2) * gi * gi;
@@ -392,9 +396,10 @@ void batch_sum2_launch(const float* a, const float* b, float* oa, float* ob, int
   const long long n4 = n / 4;
   hipLaunchKernelGGL(batch_sum2_kernel, dim3((unsigned)((2 * n4 + 63) / 64)), dim3(256), 0, st, a, b, oa, ob, B, n4);
 }
-void adamw_launch(float* p, const float* g, float* m, float* v, uint16_t* shadow, long long n, const float* hyper,
-                  float eps, float wd, float clip, float gscale, int l2, hipStream_t st) {
-  hipLaunchKernelGGL(adamw_kernel, grid_for(n), dim3(256), 0, st, p, g, m, v, shadow, n, hyper, eps, wd, clip, gscale, l2);
+void adamw_launch(float* p, float* g, float* m, float* v, uint16_t* shadow, long long n, const float* hyper,
+                  float eps, float wd, float clip, float gscale, int l2, int zero_g, hipStream_t st) {
+  hipLaunchKernelGGL(adamw_kernel, grid_for(n), dim3(256), 0, st, p, g, m, v, shadow, n, hyper, eps, wd, clip, gscale, l2,
+                     zero_g);
 }
 // grad[i] += Σ_r rep[r][i], rep[r][i] ← 0 (replicated gradient accumulators, see ops/optim.py)
 __global__ void fold_replicas_kernel(float* __restrict__ grad, float* __restrict__ rep, long long n, int nrep) {

@@ -535,7 +535,7 @@ def sumsq(g, out):
     out += (g.float() ** 2).sum()
 
 
-def adamw(p, g, m, v, shadow, hyper, eps, wd, clip, gscale, l2=False):
+def adamw(p, g, m, v, shadow, hyper, eps, wd, clip, gscale, l2=False, zero_grad=False):
     lr, step, b1, b2 = float(hyper[0]), float(hyper[1]), float(hyper[3]), float(hyper[4])
     gs = gscale
     if clip > 0:
@@ -544,6 +544,8 @@ def adamw(p, g, m, v, shadow, hyper, eps, wd, clip, gscale, l2=False):
         if f < 1:
             gs *= f
     gg = g * gs
+    if zero_grad:
+        g.zero_()
     if l2:  # torch.optim.Adam: coupled L2 decay added to the (clipped) gradient
         gg = gg + wd * p
     else:

@@ -187,8 +187,10 @@ class FusedAdamW(torch.optim.Optimizer):
         else:
             self.hyper.copy_(torch.tensor(vals))
 
-    def device_update(self):
-        """The capturable part: (grad-norm) + fused AdamW kernel over the flat buffers."""
+    def device_update(self, zero_grad: bool = False):
+        """The capturable part: (grad-norm) + fused AdamW kernel over the flat buffers.
+        ``zero_grad``: the kernel clears the gradient as it consumes it (flat buffers without
+        replicas only; the step engine's captured step then skips its leading zero fill)."""
         K = ext.require() if self.flat.device.type == "cuda" else emulation
         g = self.param_groups[0]
         self.flat.fold()
@@ -201,7 +203,8 @@ class FusedAdamW(torch.optim.Optimizer):
                 self.hyper[2:3].zero_()
                 K.sumsq(self.flat.grad, self.hyper[2:3])
         K.adamw(self.flat.data, self.flat.grad, self.exp_avg, self.exp_avg_sq, self.flat.shadow, self.hyper,
-                g["eps"], g["weight_decay"], self.max_grad_norm, self.grad_scale, l2=self.l2)
+                g["eps"], g["weight_decay"], self.max_grad_norm, self.grad_scale, l2=self.l2,
+                zero_grad=zero_grad and self.flat.grad_rep is None)
 
     @torch.no_grad()
     def step(self, closure=None, staged: bool = False):

@@ -158,14 +158,19 @@ class StepEngine:
         # inside it on every replay)
         one = torch.ones((), device=self.device)
         g = torch.cuda.CUDAGraph()
+        # with the optimizer in the graph, the AdamW kernel clears the gradient it consumes, so the
+        # replay needs no leading zero fill (gradients are zero between steps on every path: the
+        # fill above, eager steps' zero_grad, and the previous replay's update)
+        self_zeroing = self._opt_in_graph and opt.flat.grad_rep is None
         with torch.cuda.graph(g, stream=self.stream):
-            opt.flat.zero_grad_buffers()
+            if not self_zeroing:
+                opt.flat.zero_grad_buffers()
             loss = self.loss_fn(static)
             loss.backward(one if loss.dim() == 0 and loss.dtype == one.dtype else None)
             if self._opt_in_graph:
                 if self.reducer is not None and self.reducer.enabled:
                     self.reducer.finish()
-                opt.device_update()
+                opt.device_update(zero_grad=self_zeroing)
         state = self.state_hooks[0]() if self.state_hooks is not None else None
         self.captures += 1
         return _Captured(g, static, loss, state, one)
