@@ -54,6 +54,10 @@ void post_attn_ln_linear_fwd_launch(int, const uint16_t*, const float*, const ui
                                     float*, float*, float*, float*, uint16_t*, int, const float*, const float*,
                                     const uint16_t*, const float*, uint16_t*, float*, float*, const DropCfg&,
                                     hipStream_t);
+void sa_layer_fwd_launch(const uint16_t*, int, float, uint16_t*, float*, const float*, const uint16_t*, const float*,
+                         const float*, const float*, float, const uint16_t*, const float*, const uint16_t*, const float*,
+                         float*, float*, float*, float*, uint16_t*, int, const float*, const float*, const uint16_t*,
+                         const float*, uint16_t*, float*, float*, const DropCfg&, hipStream_t);
 void ln_linear_post_attn_bwd_launch(int, const float*, const uint16_t*, const float*, const float*, const float*,
                                     const float*, const float*, const float*, float*, float*, float*, float*,
                                     const float*, const float*, const float*, const uint16_t*, const uint16_t*,
@@ -71,15 +75,14 @@ void wgrad_launch(const void*, bool, int, int, const void*, bool, int, int, int,
                   const float*, const float*, int, int, float*, float*, int, int, const float*, int, int, int,
                   hipStream_t);
 void ce_fwd_launch(int, const float*, const int64_t*, const int64_t*, const uint16_t*, const float*, int, int, float*,
-                   float*, float*, const float*, float*, float*, unsigned*, int, hipStream_t);
+                   float*, float*, const float*, float*, float*, unsigned*, uint16_t*, int, hipStream_t);
 int ce_combine_blocks(int);
 int ce_num_splits(int, int);
 int ce_dw_splits(int, int);
 void mlm_select_launch(const int64_t*, int, int, int, int, int64_t*, int64_t*, int*, int64_t*, int64_t*, float*, bool*, bool*,
                        hipStream_t);
-void ce_bwd_launch(int, const float*, const int64_t*, const int64_t*, const uint16_t*, const float*, const float*,
-                   const float*, const float*, int, int, float*, long long, const int64_t*, float*, float*, int, float*, int,
-                   hipStream_t);
+void ce_bwd_launch(int, const uint16_t*, const int64_t*, const uint16_t*, const float*, const float*, const float*,
+                   const float*, int, int, float*, long long, const int64_t*, float*, float*, int, float*, int, hipStream_t);
 void embed_fwd_launch(const int64_t*, const float*, const float*, float*, long long, int, int, float, hipStream_t);
 void embed_bwd_launch(const int64_t*, const float*, float*, float*, int, int, int, float, hipStream_t);
 void embed_bwd_sorted_launch(const int64_t*, const int64_t*, const float*, float*, long long, int, float, hipStream_t);
@@ -366,6 +369,40 @@ std::vector<Tensor> post_attn_ln_linear_fwd(Tensor o, Tensor x, Tensor wo, Tenso
   return {z, y, m, r, u, qkv, m1, r1};
 }
 
+// fused latent self-attention layer forward (C = 64, H = 4, N ≤ 256, N % 64 == 0, no attention
+// dropout; residual dropout allowed): qkv (R, 3C) bf16 of this layer, x (R, C) fp32 its input →
+// [o, lse, z, y, m2, r2, u] (+ [qkv, mean1, rstd1] of the next layer when lnw/lnb/wq/bq given)
+std::vector<Tensor> sa_layer_fwd(Tensor qkv, Tensor x, int64_t N, double scale, Tensor wo, Tensor bo, Tensor g2,
+                                 Tensor be2, double eps, Tensor w1, Tensor b1, Tensor w2, Tensor b2, OptT lnw, OptT lnb,
+                                 OptT wq, OptT bq, OptT seed, int64_t site, double p) {
+  const int C = 64, H = 4;
+  TORCH_CHECK(qkv.is_contiguous() && x.is_contiguous(), "qkv/x must be contiguous");
+  const int R = (int)x.size(0);
+  TORCH_CHECK(x.size(1) == C && qkv.size(0) == R && qkv.size(1) == 3 * C, "sa_layer_fwd: C = 64, qkv (R, 192)");
+  TORCH_CHECK(N > 0 && N <= 256 && N % 64 == 0 && R % N == 0, "sa_layer_fwd: N <= 256, N % 64 == 0, R = B·N");
+  const bool next = wq.has_value();
+  if (next)
+    TORCH_CHECK(lnw.has_value() && lnb.has_value() && bq.has_value() && wq->is_contiguous() && wq->size(0) == 3 * C &&
+                    wq->size(1) == C && bq->numel() == 3 * C && lnw->numel() == C && lnb->numel() == C,
+                "sa_layer_fwd: next-layer LN1 / packed in-projection");
+  auto f32 = x.options().dtype(torch::kFloat32);
+  auto b16 = x.options().dtype(torch::kBFloat16);
+  Tensor o = torch::empty({R / N, N, C}, b16), lse = torch::empty({R / N, N, H}, f32);
+  Tensor z = torch::empty({R, C}, f32), y = torch::empty({R, C}, f32);
+  Tensor m = torch::empty({R}, f32), r = torch::empty({R}, f32), u = torch::empty({R, C}, b16);
+  Tensor qn, m1, r1;
+  if (next) { qn = torch::empty({R, 3 * C}, b16); m1 = torch::empty({R}, f32); r1 = torch::empty({R}, f32); }
+  pio::sa_layer_fwd_launch(bfp(qkv), (int)N, (float)(scale * 1.4426950408889634), bfp_mut(o), lse.data_ptr<float>(),
+                           f32p(x), bfp(wo), f32p(bo), f32p(g2), f32p(be2), (float)eps, bfp(w1), f32p(b1), bfp(w2),
+                           f32p(b2), z.data_ptr<float>(), y.data_ptr<float>(), m.data_ptr<float>(), r.data_ptr<float>(),
+                           bfp_mut(u), R, next ? f32p(*lnw) : nullptr, next ? f32p(*lnb) : nullptr,
+                           next ? bfp(*wq) : nullptr, next ? f32p(*bq) : nullptr, next ? bfp_mut(qn) : nullptr,
+                           next ? m1.data_ptr<float>() : nullptr, next ? r1.data_ptr<float>() : nullptr,
+                           make_drop(seed, site, p), stream());
+  if (next) return {o, lse, z, y, m, r, u, qn, m1, r1};
+  return {o, lse, z, y, m, r, u};
+}
+
 // the backward entry points below ACCUMULATE parameter gradients into caller-provided fp32
 // tensors (normally views of the flat gradient buffer) with device atomics: no partial slabs,
 // no reduction pass, no autograd AccumulateGrad adds
@@ -617,7 +654,8 @@ static const int64_t* opt_idx(const OptT& idx, int64_t n) {
 }
 
 // mean CE over the rows of h (fp32 (N, C); row r = h[idx[r]] when idx is given, else h[r]) with
-// label ≥ 0: → {loss (0-dim) = Σ rows / max(count, 1), per-row lse (M,)}.  count: fp32 (1,).
+// label ≥ 0: → {loss (0-dim) = Σ rows / max(count, 1), per-row lse (M,), the compact bf16 rows
+// hs (M, C) the backward kernels read}.  count: fp32 (1,).
 std::vector<Tensor> ce_fwd(Tensor h, OptT idx, Tensor labels, Tensor w, Tensor bias, Tensor count) {
   TORCH_CHECK(h.is_contiguous() && w.is_contiguous() && labels.is_contiguous() && bias.is_contiguous());
   CHECK_DT(labels, torch::kInt64);
@@ -632,28 +670,30 @@ std::vector<Tensor> ce_fwd(Tensor h, OptT idx, Tensor labels, Tensor w, Tensor b
   Tensor part = torch::empty({ns, M, 2}, f32), picked = torch::empty({M}, f32);
   Tensor lse = torch::empty({M}, f32), loss = torch::empty({}, f32);
   Tensor blk = torch::empty({pio::ce_combine_blocks(M)}, f32);
+  Tensor hs = torch::empty({M, C}, h.options().dtype(torch::kBFloat16));
   Tensor& tk = ce_ticket(h);
   pio::ce_fwd_launch(C, h.data_ptr<float>(), ip, labels.data_ptr<int64_t>(), bfp(w), f32p(bias), M, V,
                      part.data_ptr<float>(), picked.data_ptr<float>(), lse.data_ptr<float>(), f32p(count),
-                     loss.data_ptr<float>(), blk.data_ptr<float>(), reinterpret_cast<unsigned*>(tk.data_ptr<int>()), ns,
-                     stream());
-  return {loss, lse};
+                     loss.data_ptr<float>(), blk.data_ptr<float>(), reinterpret_cast<unsigned*>(tk.data_ptr<int>()),
+                     bfp_mut(hs), ns, stream());
+  return {loss, lse, hs};
 }
 
-// dH (+)= rows: row r lands in dH[rowmap[r]] when rowmap is given (dH then has the full
-// (positions, C) shape), else in dH[r]; dW / db accumulate or overwrite.  The row-loss gradient
+// h: the compact bf16 rows from ce_fwd.  dH (+)= rows: row r lands in dH[rowmap[r]] when rowmap
+// is given (dH then has the full (positions, C) shape), else in dH[r]; dW / db accumulate or
+// overwrite.  The row-loss gradient
 // is gout / max(count, 1) (gout: the 0-dim gradient of the mean loss).
 // slab: the dW kernel stores its row-split partials into a returned (splits, V·C + V₄) slab
 // instead of adding them (the caller sums it into dW | db with a slab job, offsets 0 and V·C).
-OptT ce_bwd(Tensor h, OptT idx, Tensor labels, Tensor w, Tensor bias, Tensor lse, Tensor gout, Tensor count, Tensor dH,
+OptT ce_bwd(Tensor h, Tensor labels, Tensor w, Tensor bias, Tensor lse, Tensor gout, Tensor count, Tensor dH,
             Tensor dW, Tensor db, bool accumulate, OptT rowmap, bool slab) {
   const int M = (int)labels.numel(), C = (int)h.size(1), V = (int)w.size(0);
-  CHECK_DT(h, torch::kFloat32);
+  CHECK_DT(h, torch::kBFloat16);
+  TORCH_CHECK(h.size(0) == M, "ce_bwd: h must be the compact (M, C) bf16 rows of ce_fwd");
   CHECK_DT(gout, torch::kFloat32);
   CHECK_DT(count, torch::kFloat32);
   TORCH_CHECK(h.is_contiguous() && dH.is_contiguous() && dW.is_contiguous() && db.is_contiguous());
   TORCH_CHECK(dH.dim() == 2 && dH.size(1) == C, "dH must be (rows, C)");
-  const int64_t* ip = opt_idx(idx, M);
   const int64_t* rm = nullptr;
   if (rowmap.has_value()) {
     CHECK_DT(*rowmap, torch::kInt64);
@@ -664,7 +704,7 @@ OptT ce_bwd(Tensor h, OptT idx, Tensor labels, Tensor w, Tensor bias, Tensor lse
   }
   Tensor sl;
   if (slab) sl = torch::empty({pio::ce_dw_splits(M, V), (int64_t)V * C + ((V + 3) & ~3)}, dW.options());
-  pio::ce_bwd_launch(C, h.data_ptr<float>(), ip, labels.data_ptr<int64_t>(), bfp(w), f32p(bias), f32p(lse), f32p(gout),
+  pio::ce_bwd_launch(C, bfp(h), labels.data_ptr<int64_t>(), bfp(w), f32p(bias), f32p(lse), f32p(gout),
                      f32p(count), M, V, dH.data_ptr<float>(), dH.size(0), rm, dW.data_ptr<float>(), db.data_ptr<float>(),
                      accumulate ? 1 : 0, slab ? sl.data_ptr<float>() : nullptr, g_det ? 1 : 0, stream());
   if (slab) return sl;
@@ -1027,6 +1067,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("post_attn_fwd", &post_attn_fwd, py::arg("o"), py::arg("x"), py::arg("wo"), py::arg("bo"), py::arg("g2"),
         py::arg("be2"), py::arg("eps"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("b2"),
         py::arg("seed") = py::none(), py::arg("site") = 0, py::arg("p") = 0.0);
+  m.def("sa_layer_fwd", &sa_layer_fwd, py::arg("qkv"), py::arg("x"), py::arg("N"), py::arg("scale"), py::arg("wo"),
+        py::arg("bo"), py::arg("g2"), py::arg("be2"), py::arg("eps"), py::arg("w1"), py::arg("b1"), py::arg("w2"),
+        py::arg("b2"), py::arg("lnw") = py::none(), py::arg("lnb") = py::none(), py::arg("wq") = py::none(),
+        py::arg("bq") = py::none(), py::arg("seed") = py::none(), py::arg("site") = 0, py::arg("p") = 0.0);
   m.def("post_attn_ln_linear_fwd", &post_attn_ln_linear_fwd, py::arg("o"), py::arg("x"), py::arg("wo"), py::arg("bo"),
         py::arg("g2"), py::arg("be2"), py::arg("eps"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("b2"),
         py::arg("lnw"), py::arg("lnb"), py::arg("wq"), py::arg("bq"), py::arg("seed") = py::none(),
@@ -1057,7 +1101,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pixel_ce_fwd", &pixel_ce_fwd);
   m.def("pixel_ce_bwd", &pixel_ce_bwd);
   m.def("ce_fwd", &ce_fwd);
-  m.def("ce_bwd", &ce_bwd, py::arg("h"), py::arg("idx"), py::arg("labels"), py::arg("w"), py::arg("bias"),
+  m.def("ce_bwd", &ce_bwd, py::arg("h"), py::arg("labels"), py::arg("w"), py::arg("bias"),
         py::arg("lse"), py::arg("gout"), py::arg("count"), py::arg("dH"), py::arg("dW"), py::arg("db"),
         py::arg("accumulate"), py::arg("rowmap") = py::none(), py::arg("slab") = false);
   m.def("embed_fwd", &embed_fwd);

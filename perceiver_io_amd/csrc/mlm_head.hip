@@ -111,17 +111,6 @@ __device__ __forceinline__ void fetch_rows(bf16x8 (&v)[C / 32], const uint16_t* 
     if (r0 + rr < R) v[i] = *reinterpret_cast<const bf16x8*>(g + (long long)(r0 + rr) * C + c);
   }
 }
-// the same for gathered fp32 H rows
-template <int C>
-__device__ __forceinline__ void fetch_hrows(bf16x8 (&v)[C / 32], const float* H, const int64_t* idx, int r0, int R) {
-  constexpr int CH = C / 8;
-#pragma unroll
-  for (int i = 0; i < C / 32; ++i) {
-    const int e = threadIdx.x + 256 * i, rr = e / CH, c = (e % CH) * 8;
-    v[i] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    if (r0 + rr < R) v[i] = hrow8<C>(H, idx, r0 + rr, c);
-  }
-}
 template <int C>
 __device__ __forceinline__ void store_rows(const bf16x8 (&v)[C / 32], uint16_t* s, int ld) {
   constexpr int CH = C / 8;
@@ -137,7 +126,7 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ H
                                                      const int64_t* __restrict__ labels,
                                                      const uint16_t* __restrict__ W, const float* __restrict__ bias,
                                                      int M, int V, int chunks_per_split, float* __restrict__ part_ms,
-                                                     float* __restrict__ picked) {
+                                                     float* __restrict__ picked, uint16_t* __restrict__ hs_out) {
   constexpr int LD = C + 8;
   __shared__ __attribute__((aligned(16))) uint16_t sH[HB * LD];
   __shared__ __attribute__((aligned(16))) uint16_t sW[VB * LD];
@@ -148,6 +137,15 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ H
   const int nchunks = (V + VB - 1) / VB;
   const int c_begin = split * chunks_per_split, c_end = min(nchunks, c_begin + chunks_per_split);
   stage_hrows<C>(sH, LD, Hm, hidx, m0, M);
+  if (split == 0 && hs_out != nullptr) {  // the compact bf16 rows for the backward kernels
+    lds_sync();
+    constexpr int CH = C / 8;
+    for (int e = threadIdx.x; e < 64 * CH; e += blockDim.x) {
+      const int rr = e / CH, c = (e % CH) * 8;
+      if (m0 + rr < M)
+        *reinterpret_cast<bf16x8*>(hs_out + (long long)(m0 + rr) * C + c) = *reinterpret_cast<const bf16x8*>(sH + rr * LD + c);
+    }
+  }
   const int rl = 32 * (w >> 1) + (l & 31), gr = m0 + rl;
   const int lab = gr < M ? (int)labels[gr] : -100;
   float m = -1e30f, s = 0.f;  // log2-domain running max / sum of 2^(t - m) over this lane's logits
@@ -274,8 +272,7 @@ __device__ __forceinline__ void dl_regs(const f32x16& acc, const float (&b)[16],
 
 // bwd-a: dH[r][c] += sum_v dl[r][v] W[v][c]  over this split's vocab chunks (fp32 atomics)
 template <int C>
-__global__ __launch_bounds__(256) void ce_bwd_dh_kernel(const float* __restrict__ Hm,
-                                                        const int64_t* __restrict__ hidx,
+__global__ __launch_bounds__(256) void ce_bwd_dh_kernel(const uint16_t* __restrict__ Hm,
                                                         const int64_t* __restrict__ labels,
                                                         const uint16_t* __restrict__ W, const float* __restrict__ bias,
                                                         const float* __restrict__ lse, const float* __restrict__ gout,
@@ -292,7 +289,7 @@ __global__ __launch_bounds__(256) void ce_bwd_dh_kernel(const float* __restrict_
   const int m0 = blockIdx.x * HB, split = blockIdx.y;
   const int nchunks = (V + VB - 1) / VB;
   const int c_begin = split * chunks_per_split, c_end = min(nchunks, c_begin + chunks_per_split);
-  stage_hrows<C>(sH, LD, Hm, hidx, m0, M);
+  stage_rows<C>(sH, LD, Hm, m0, M);
   if (threadIdx.x < HB) {
     const int gr = m0 + threadIdx.x;
     const long long r = (gr < M && labels[gr] >= 0) ? (rowmap ? rowmap[gr] : gr) : -1;
@@ -359,8 +356,7 @@ __global__ __launch_bounds__(256) void ce_bwd_dh_kernel(const float* __restrict_
 // bwd-b: dW[v][c] += sum_r dl[r][v] H[r][c], db[v] += sum_r dl[r][v]; grid (vocab chunk, row split),
 // H tiles (+ their LSE / labels) register-prefetched one tile ahead, partials added atomically
 template <int C>
-__global__ __launch_bounds__(256) void ce_bwd_dw_kernel(const float* __restrict__ Hm,
-                                                        const int64_t* __restrict__ hidx,
+__global__ __launch_bounds__(256) void ce_bwd_dw_kernel(const uint16_t* __restrict__ Hm,
                                                         const int64_t* __restrict__ labels,
                                                         const uint16_t* __restrict__ W, const float* __restrict__ bias,
                                                         const float* __restrict__ lse, const float* __restrict__ gout,
@@ -393,7 +389,7 @@ __global__ __launch_bounds__(256) void ce_bwd_dw_kernel(const float* __restrict_
   bf16x8 hr[C / 32];
   float aux = 0.f;  // threads [0,64): LSE * log2e of row tid, [64,128): label of row tid-64
   auto fetch = [&](int mt) {
-    fetch_hrows<C>(hr, Hm, hidx, mt * HB, M);
+    fetch_rows<C>(hr, Hm, mt * HB, M);
     const int t = threadIdx.x & 63, gr = mt * HB + t;
     if (threadIdx.x < 64) aux = gr < M ? lse[gr] * kL2E : 0.f;
     else if (threadIdx.x < 128) aux = __int_as_float(gr < M ? (int)labels[gr] : -100);
@@ -567,13 +563,13 @@ int ce_combine_blocks(int M);
 
 void ce_fwd_launch(int C, const float* Hm, const int64_t* hidx, const int64_t* labels, const uint16_t* W,
                    const float* bias, int M, int V, float* part_ms, float* picked, float* lse, const float* count,
-                   float* loss, float* blk, unsigned* ticket, int nsplit, hipStream_t st) {
+                   float* loss, float* blk, unsigned* ticket, uint16_t* hs_out, int nsplit, hipStream_t st) {
   const int nchunks = (V + VB - 1) / VB;
   const int cps = (nchunks + nsplit - 1) / nsplit;
   dim3 grid((M + HB - 1) / HB, nsplit);
-  if (C == 64) hipLaunchKernelGGL(ce_fwd_kernel<64>, grid, dim3(256), 0, st, Hm, hidx, labels, W, bias, M, V, cps, part_ms, picked);
-  else if (C == 128) hipLaunchKernelGGL(ce_fwd_kernel<128>, grid, dim3(256), 0, st, Hm, hidx, labels, W, bias, M, V, cps, part_ms, picked);
-  else if (C == 32) hipLaunchKernelGGL(ce_fwd_kernel<32>, grid, dim3(256), 0, st, Hm, hidx, labels, W, bias, M, V, cps, part_ms, picked);
+  if (C == 64) hipLaunchKernelGGL(ce_fwd_kernel<64>, grid, dim3(256), 0, st, Hm, hidx, labels, W, bias, M, V, cps, part_ms, picked, hs_out);
+  else if (C == 128) hipLaunchKernelGGL(ce_fwd_kernel<128>, grid, dim3(256), 0, st, Hm, hidx, labels, W, bias, M, V, cps, part_ms, picked, hs_out);
+  else if (C == 32) hipLaunchKernelGGL(ce_fwd_kernel<32>, grid, dim3(256), 0, st, Hm, hidx, labels, W, bias, M, V, cps, part_ms, picked, hs_out);
   hipLaunchKernelGGL(ce_combine_kernel, dim3(ce_combine_blocks(M)), dim3(256), 0, st, part_ms, picked, labels, M, nsplit,
                      lse, count, loss, blk, ticket);
 }
@@ -591,7 +587,7 @@ int ce_dw_splits(int M, int V) {
   return (mtiles + tps - 1) / tps;
 }
 
-void ce_bwd_launch(int C, const float* Hm, const int64_t* hidx, const int64_t* labels, const uint16_t* W,
+void ce_bwd_launch(int C, const uint16_t* Hm, const int64_t* labels, const uint16_t* W,
                    const float* bias, const float* lse, const float* gout, const float* count, int M, int V, float* dH, long long dh_rows, const int64_t* rowmap, float* dW,
                    float* db, int accumulate, float* slab, int det, hipStream_t st) {
   const int nchunks = (V + VB - 1) / VB;
@@ -610,9 +606,9 @@ void ce_bwd_launch(int C, const float* Hm, const int64_t* hidx, const int64_t* l
   }
   dim3 ga((M + HB - 1) / HB, nsplit), gb(nchunks, rsplit);
 #define CEB(CC)                                                                                                  \
-  hipLaunchKernelGGL(ce_bwd_dh_kernel<CC>, ga, dim3(256), 0, st, Hm, hidx, labels, W, bias, lse, gout, count, M, V, cps, dH, \
+  hipLaunchKernelGGL(ce_bwd_dh_kernel<CC>, ga, dim3(256), 0, st, Hm, labels, W, bias, lse, gout, count, M, V, cps, dH, \
                      rowmap, dh_rows);                                                                           \
-  hipLaunchKernelGGL(ce_bwd_dw_kernel<CC>, gb, dim3(256), 0, st, Hm, hidx, labels, W, bias, lse, gout, count, M, V, tps, \
+  hipLaunchKernelGGL(ce_bwd_dw_kernel<CC>, gb, dim3(256), 0, st, Hm, labels, W, bias, lse, gout, count, M, V, tps, \
                      dW, db,                                                                                     \
                      slab)
   if (C == 64) { CEB(64); }

@@ -512,14 +512,47 @@ __global__ __launch_bounds__(256) void ln_linear_fwd_kernel(const TIn* __restric
 // then run back to back on LDS with row-pass epilogues (LN2 in registers, 16-byte stores).
 // For C = 128 the weights share one LDS buffer, each fetched during the previous GEMM.
 // ------------------------------------------------------------------------------------
-// one 64-row tile; Z is also left in z (row-pass registers) for a fused epilogue
+// phase-0 operands of the post-attention block that do not depend on the attention output:
+// the weights (C ≤ 64: all three), the residual rows and the bias / LN2 vectors (thread k < C
+// holds entry k) — issued before the attention in the fused self-attention layer kernel
+template <int C>
+struct PaPre {
+  static constexpr int NCH = C / 32, NWB = C <= 64 ? 3 : 1, NIW = (C * C / 8 + 255) / 256;
+  bf16x8 wr[NWB][NIW];
+  float yv[NCH][8];
+  float pp[5];
+};
 template <int C, bool AV>
+__device__ __forceinline__ void post_attn_fwd_prefetch(PaPre<C>& pre, const float* __restrict__ X,
+                                                       const uint16_t* __restrict__ Wo, const float* __restrict__ bo,
+                                                       const float* __restrict__ g2, const float* __restrict__ be2,
+                                                       const uint16_t* __restrict__ W1, const float* __restrict__ b1,
+                                                       const uint16_t* __restrict__ W2, const float* __restrict__ b2,
+                                                       int R, int Rx) {
+  using P = PaPre<C>;
+  const int gr = blockIdx.x * 64 + rp_row();
+  tile_fetch<P::NIW>(pre.wr[0], Wo, C, 0, C, C, C, C, AV);
+  if constexpr (P::NWB == 3) {
+    tile_fetch<P::NIW>(pre.wr[1], W1, C, 0, C, C, C, C, AV);
+    tile_fetch<P::NIW>(pre.wr[2], W2, C, 0, C, C, C, C, AV);
+  }
+  row_load<P::NCH>(pre.yv, X, C, gr < R ? gr % Rx : Rx, Rx, C, AV);
+  // bias / LN2 vectors: address select (thread ≥ C reads a zero), no branch around the loads
+  const int k = threadIdx.x < C ? (int)threadIdx.x : 0;
+  pre.pp[0] = bo[k]; pre.pp[1] = b1[k]; pre.pp[2] = b2[k]; pre.pp[3] = g2[k]; pre.pp[4] = be2[k];
+}
+
+// one 64-row tile; Z is also left in z (row-pass registers) for a fused epilogue.  OLDS: the
+// attention output tile is already in LDS (sO, [64][C + 8] bf16, written by the caller before a
+// barrier); else it is fetched from O.
+template <int C, bool AV, bool OLDS = false>
 __device__ __forceinline__ void post_attn_fwd_body(
     const uint16_t* __restrict__ O, const float* __restrict__ X, const uint16_t* __restrict__ Wo,
     const float* __restrict__ bo, const float* __restrict__ g2, const float* __restrict__ be2, float eps,
     const uint16_t* __restrict__ W1, const float* __restrict__ b1, const uint16_t* __restrict__ W2,
     const float* __restrict__ b2, float* __restrict__ Z, float* __restrict__ Ysave, float* __restrict__ mean2,
-    float* __restrict__ rstd2, uint16_t* __restrict__ Usave, int R, int Rx, const DropCfg& dr, float (&z)[C / 32][8]) {
+    float* __restrict__ rstd2, uint16_t* __restrict__ Usave, int R, int Rx, const DropCfg& dr, float (&z)[C / 32][8],
+    PaPre<C>& pre, const uint16_t* sO = nullptr) {
   // X has Rx rows, row r of the tile adds X[r % Rx] (Rx < R: batch-broadcast residual).
   // Residual dropout (dr.thresh > 0): Y = X + drop₀(attn-out), Z = Y + drop₁(MLP(Y)), masks
   // hashed from (device seed, site, row·C + col) and regenerated by the backward.
@@ -532,20 +565,17 @@ __device__ __forceinline__ void post_attn_fwd_body(
   const int m0 = blockIdx.x * 64, gr = m0 + rp_row();
   constexpr bool av = AV;  // O, X, Z, Ysave, Usave, Wo, W1, W2 16-B aligned (host-checked)
 
-  bf16x8 ob[NCH];
-  tile_fetch<NCH>(ob, O, C, m0, R, 64, C, C, av);
-  bf16x8 wr[NWB][NIW];
-  tile_fetch<NIW>(wr[0], Wo, C, 0, C, C, C, C, av);
-  if constexpr (NWB == 3) {
-    tile_fetch<NIW>(wr[1], W1, C, 0, C, C, C, C, av);
-    tile_fetch<NIW>(wr[2], W2, C, 0, C, C, C, C, av);
+  bf16x8 (&wr)[NWB][NIW] = pre.wr;
+  float (&yv)[NCH][8] = pre.yv;
+  if constexpr (!OLDS) {
+    bf16x8 ob[NCH];
+    tile_fetch<NCH>(ob, O, C, m0, R, 64, C, C, av);
+    tile_store<NCH>(ob, sA, LD, 64, C);
   }
-  float yv[NCH][8];
-  row_load<NCH>(yv, X, C, gr < R ? gr % Rx : Rx, Rx, C, av);
-  for (int k = threadIdx.x; k < C; k += blockDim.x) {
-    sP[0][k] = bo[k]; sP[1][k] = b1[k]; sP[2][k] = b2[k]; sP[3][k] = g2[k]; sP[4][k] = be2[k];
+  if (threadIdx.x < C) {
+    const int k = threadIdx.x;
+    sP[0][k] = pre.pp[0]; sP[1][k] = pre.pp[1]; sP[2][k] = pre.pp[2]; sP[3][k] = pre.pp[3]; sP[4][k] = pre.pp[4];
   }
-  tile_store<NCH>(ob, sA, LD, 64, C);
 #pragma unroll
   for (int b = 0; b < NWB; ++b) tile_store<NIW>(wr[b], sW[b], LD, C, C);
   lds_sync();
@@ -553,7 +583,7 @@ __device__ __forceinline__ void post_attn_fwd_body(
   f32x16 acc[MAXT];
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
-  tile_gemm<MAXT, true, true>(sA, LD, sW[0], LD, 64, C, C, acc);
+  tile_gemm<MAXT, true, true>(OLDS ? sO : sA, LD, sW[0], LD, 64, C, C, acc);
   for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) { sF[m * LDF + n] = acc[t][i] + sP[0][n]; });
   lds_sync();
   if constexpr (NWB == 1) tile_store<NIW>(wr[0], sW[0], LD, C, C);
@@ -626,7 +656,10 @@ __global__ __launch_bounds__(256) void post_attn_fwd_kernel(
     const float* __restrict__ b2, float* __restrict__ Z, float* __restrict__ Ysave, float* __restrict__ mean2,
     float* __restrict__ rstd2, uint16_t* __restrict__ Usave, int R, int Rx, DropCfg dr) {
   float z[C / 32][8];
-  post_attn_fwd_body<C, AV>(O, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, Rx, dr, z);
+  PaPre<C> pre;
+  post_attn_fwd_prefetch<C, AV>(pre, X, Wo, bo, g2, be2, W1, b1, W2, b2, R, Rx);
+  post_attn_fwd_body<C, AV>(O, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, Rx, dr, z,
+                            pre);
 }
 
 // ------------------------------------------------------------------------------------
@@ -653,9 +686,140 @@ __global__ __launch_bounds__(256) void post_attn_ln_linear_fwd_kernel(
   row_load<NCH>(gw, lnw, 0, 0, 1, C, AV);
   row_load<NCH>(gb, lnb, 0, 0, 1, C, AV);
   float z[NCH][8];
-  post_attn_fwd_body<C, AV>(O, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, R, dr, z);
+  PaPre<C> pre;
+  post_attn_fwd_prefetch<C, AV>(pre, X, Wo, bo, g2, be2, W1, b1, W2, b2, R, R);
+  post_attn_fwd_body<C, AV>(O, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, R, dr, z, pre);
   ln_linear_fwd_tile<uint16_t, NCH, AV>(z, wb, gw, gb, true, blockIdx.x * 64, R, C, eps, Wq, C, bq, 3 * C, 0, nullptr, 0,
                                     QKV, 3 * C, mean1, rstd1, smem);
+}
+
+// ------------------------------------------------------------------------------------
+// Fused latent self-attention layer forward (C = 64, H = 4, D = 16, N ≤ 256 latents with
+// N % 64 == 0, no attention dropout): ONE launch per layer instead of attn_fwd +
+// post_attn(_ln_linear)_fwd.  A workgroup owns a 64-row tile (64 queries of one batch element):
+//   phase 0  every operand load in flight together — K fragments straight from global (the
+//            A operand of Sᵀ = K·Qᵀ is one 16-byte row piece per lane), Q fragments, the batch
+//            element's V rows (→ LDS), the post-attention weights / residual / bias vectors and
+//            the next layer's LN1 affine and first QKV weight chunk;
+//   attention wave h = head h: per 32-query block all N keys at once (N/32 MFMAs, one max, one
+//            fma + exp2 per score, no online rescaling), Oᵀ += Vᵀ·Pᵀ straight from the
+//            accumulators (Vᵀ by transposed LDS reads of the all-head V tile; the rows past the
+//            head's 16 columns are never used), O → LDS tile (and to global for the backward),
+//            LSE (log2 units);
+//   then the post-attention block on the LDS O tile and (NEXT) LN1 + QKV of the next layer —
+// the attention output never makes a global round trip before its consumer.
+// ------------------------------------------------------------------------------------
+template <bool NEXT, bool AV>
+__global__ __launch_bounds__(256) void sa_layer_fwd_kernel(
+    const uint16_t* __restrict__ QKV, int N, float scale_log2, uint16_t* __restrict__ Oout, float* __restrict__ LSE,
+    const float* __restrict__ X, const uint16_t* __restrict__ Wo, const float* __restrict__ bo,
+    const float* __restrict__ g2, const float* __restrict__ be2, float eps, const uint16_t* __restrict__ W1,
+    const float* __restrict__ b1, const uint16_t* __restrict__ W2, const float* __restrict__ b2, float* __restrict__ Z,
+    float* __restrict__ Ysave, float* __restrict__ mean2, float* __restrict__ rstd2, uint16_t* __restrict__ Usave, int R,
+    const float* __restrict__ lnw, const float* __restrict__ lnb, const uint16_t* __restrict__ Wq,
+    const float* __restrict__ bq, uint16_t* __restrict__ QKVn, float* __restrict__ mean1, float* __restrict__ rstd1,
+    DropCfg dr) {
+  constexpr int C = 64, H = 4, D = 16, NCH = 2, KP = 64, LD = C + 8, LDV = C + 8, C3 = 3 * C, MAXKT = 8;
+  __shared__ __attribute__((aligned(16))) uint16_t sV[256 * LDV + 64];  // V rows of the batch element (+ overrun)
+  __shared__ __attribute__((aligned(16))) uint16_t sO[64 * LD];
+  __shared__ __attribute__((aligned(16))) uint16_t smem[NEXT ? ln_linear_fwd_smem<NCH>() / 2 : 8];
+  const int w = wave_id(), l = lane_id(), hh = l >> 5, r = l & 31;
+  const int m0 = blockIdx.x * 64;
+  const int b = m0 / N;
+  const long long rb = (long long)b * N;  // first row of the batch element
+  const int nkt = N / 32;
+  const int h = w;
+  const uint16_t* zp = reinterpret_cast<const uint16_t*>(kZero32B);
+
+  // ---- phase 0: every load issued, branch-free (address selects) ----
+  bf16x8 kf[MAXKT], qf[2], vr[8];
+#pragma unroll
+  for (int kt = 0; kt < MAXKT; ++kt)
+    kf[kt] = *reinterpret_cast<const bf16x8*>(kt < nkt ? QKV + (rb + 32 * kt + r) * C3 + C + h * D + 8 * hh : zp);
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+    qf[qb] = *reinterpret_cast<const bf16x8*>(QKV + (long long)(m0 + 32 * qb + r) * C3 + h * D + 8 * hh);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {  // 256 keys × 8 pieces of 16 bytes: key c >> 3, columns (c & 7)·8
+    const int c = threadIdx.x + 256 * i, key = c >> 3, col = (c & 7) * 8;
+    vr[i] = *reinterpret_cast<const bf16x8*>(key < N ? QKV + (rb + key) * C3 + 2 * C + col : zp);
+  }
+  PaPre<C> pre;
+  post_attn_fwd_prefetch<C, AV>(pre, X, Wo, bo, g2, be2, W1, b1, W2, b2, R, R);
+  bf16x8 wb[NCH];
+  float gw[NCH][8], gb[NCH][8];
+  if constexpr (NEXT) {
+    tile_fetch<NCH>(wb, Wq, C, 0, 3 * C, 64, C, KP, AV);
+    row_load<NCH>(gw, lnw, 0, 0, 1, C, AV);
+    row_load<NCH>(gb, lnb, 0, 0, 1, C, AV);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = threadIdx.x + 256 * i, key = c >> 3, col = (c & 7) * 8;
+    *reinterpret_cast<bf16x8*>(sV + key * LDV + col) = vr[i];
+  }
+  lds_sync();
+
+  // ---- attention: wave h, two 32-query blocks ----
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    f32x16 s[MAXKT];
+    float mt = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < MAXKT; ++kt) {
+      s[kt] = f32x16{};
+      if (kt < nkt) {  // wave-uniform
+        s[kt] = mfma32(kf[kt], qf[qb], s[kt]);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) mt = fmaxf(mt, s[kt][i]);
+      }
+    }
+    const float m = xor32_max(mt) * scale_log2;
+    float ls = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < MAXKT; ++kt)
+      if (kt < nkt) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          s[kt][i] = fast_exp2(fmaf(s[kt][i], scale_log2, -m));
+          ls += s[kt][i];
+        }
+      }
+    ls = xor32_sum(ls);
+    f32x16 o = f32x16{};
+#pragma unroll
+    for (int kt = 0; kt < MAXKT; ++kt)
+      if (kt < nkt) {
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss)
+          o = mfma32(frag_ks_perm(sV, LDV, h * D, 32 * kt + 16 * ss), pack_acc(s[kt], ss), o);
+      }
+    // Oᵀ: column = query (lane), rows = head dims acc_row(i, hh) (< 16 for i < 8)
+    const float inv = 1.f / ls;
+    const int row = 32 * qb + r;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      uint2 pk;
+      pk.x = pack2(o[4 * g] * inv, o[4 * g + 1] * inv);
+      pk.y = pack2(o[4 * g + 2] * inv, o[4 * g + 3] * inv);
+      *reinterpret_cast<uint2*>(sO + row * LD + h * D + 8 * g + 4 * hh) = pk;
+    }
+    if (hh == 0) LSE[(long long)(m0 + row) * H + h] = m + __log2f(ls);
+  }
+  lds_sync();
+  // the O tile for the backward: 64 rows × 128 bytes, 16-byte row stores
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = threadIdx.x + 256 * i, row = c >> 3, col = (c & 7) * 8;
+    *reinterpret_cast<bf16x8*>(Oout + (long long)(m0 + row) * C + col) =
+        *reinterpret_cast<const bf16x8*>(sO + row * LD + col);
+  }
+  float z[NCH][8];
+  post_attn_fwd_body<C, AV, true>(nullptr, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, R,
+                                  dr, z, pre, sO);
+  if constexpr (NEXT)
+    ln_linear_fwd_tile<uint16_t, NCH, AV>(z, wb, gw, gb, true, m0, R, C, eps, Wq, C, bq, 3 * C, 0, nullptr, 0, QKVn,
+                                          3 * C, mean1, rstd1, smem);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1379,6 +1543,27 @@ void post_attn_ln_linear_fwd_launch(int C, const uint16_t* O, const float* X, co
   else if (C == 128) PLF(128);
   else if (C == 32) PLF(32);
 #undef PLF
+}
+
+// fused self-attention layer forward (C = 64, H = 4): see sa_layer_fwd_kernel; NEXT = Wq != nullptr
+void sa_layer_fwd_launch(const uint16_t* QKV, int N, float scale_log2, uint16_t* O, float* LSE, const float* X,
+                         const uint16_t* Wo, const float* bo, const float* g2, const float* be2, float eps,
+                         const uint16_t* W1, const float* b1, const uint16_t* W2, const float* b2, float* Z,
+                         float* Ysave, float* mean2, float* rstd2, uint16_t* Usave, int R, const float* lnw,
+                         const float* lnb, const uint16_t* Wq, const float* bq, uint16_t* QKVn, float* mean1,
+                         float* rstd1, const DropCfg& dr, hipStream_t st) {
+  const bool next = Wq != nullptr;
+  const bool av = av_ok({QKV, O, X, Wo, W1, W2, Z, Ysave, Usave, Wq, lnw, lnb, QKVn}, {});
+  dim3 grid(R / 64);
+#define SAL(NX, A)                                                                                                 \
+  hipLaunchKernelGGL((sa_layer_fwd_kernel<NX, A>), grid, dim3(256), 0, st, QKV, N, scale_log2, O, LSE, X, Wo, bo, g2, \
+                     be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, lnw, lnb, Wq, bq, QKVn, mean1, rstd1, dr)
+  if (next) {
+    if (av) SAL(true, true); else SAL(true, false);
+  } else {
+    if (av) SAL(false, true); else SAL(false, false);
+  }
+#undef SAL
 }
 
 void post_attn_bwd_launch(int C, const float* dZ, const float* Ysave, const float* mean2, const float* rstd2,

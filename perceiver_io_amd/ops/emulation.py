@@ -199,6 +199,22 @@ def _acc(t, v):
         t += v.reshape(t.shape)
 
 
+def sa_layer_fwd(qkv, x, N, scale, wo, bo, g2, be2, eps, w1, b1, w2, b2, lnw=None, lnb=None, wq=None, bq=None,
+                 seed=None, site=0, p=0.0):
+    """The fused self-attention layer forward (rowgemm.hip sa_layer_fwd_kernel): attention of the
+    packed qkv (C = 64, H = 4, no attention dropout), then the post-attention block and, when the
+    next layer's LN1 / in-projection are given, its QKV."""
+    C, H = 64, 4
+    R = x.shape[0]
+    q3 = qkv.view(R // N, N, 3 * C)
+    o, lse = attn_fwd(q3[:, :, :C], q3[:, :, C:2 * C], q3[:, :, 2 * C:], None, H, C // H, scale, 0.0, None, 1)
+    o2 = o.reshape(R, C)
+    if wq is None:
+        return [o, lse] + list(post_attn_fwd(o2, x, wo, bo, g2, be2, eps, w1, b1, w2, b2, seed, site, p))
+    return [o, lse] + list(post_attn_ln_linear_fwd(o2, x, wo, bo, g2, be2, eps, w1, b1, w2, b2, lnw, lnb, wq, bq, seed,
+                                                    site, p))
+
+
 def post_attn_ln_linear_fwd(o, x, wo, bo, g2, be2, eps, w1, b1, w2, b2, lnw, lnb, wq, bq, seed=None, site=0, p=0.0):
     """post_attn_fwd of layer l, then ln_linear_fwd (LN1 + packed QKV) of layer l+1."""
     z, y, m2, r2, u = post_attn_fwd(o, x, wo, bo, g2, be2, eps, w1, b1, w2, b2, seed, site, p)
@@ -453,20 +469,20 @@ def ce_fwd(h, idx, labels, w, bias, count):
     valid = labels >= 0
     picked = logits.gather(1, labels.clamp(min=0)[:, None])[:, 0]
     loss = torch.where(valid, lse - picked, torch.zeros_like(lse))
-    return loss.sum() / count.reshape(()).clamp(min=1), lse
+    return loss.sum() / count.reshape(()).clamp(min=1), lse, _ce_rows(h, idx).to(torch.bfloat16).contiguous()
 
 
-def ce_bwd(h, idx, labels, w, bias, lse, gout, count, dH, dW, db, accumulate, rowmap=None, slab=False):
-    """slab=True: dW | db are returned as a one-row (1, V·C + V₄) slab instead of being added."""
+def ce_bwd(h, labels, w, bias, lse, gout, count, dH, dW, db, accumulate, rowmap=None, slab=False):
+    """h: the compact bf16 rows returned by ce_fwd.  slab=True: dW | db are returned as a one-row
+    (1, V·C + V₄) slab instead of being added."""
     if slab:
         gw, gb = torch.zeros_like(dW), torch.zeros_like(db)
-        ce_bwd(h, idx, labels, w, bias, lse, gout, count, dH, gw, gb, False, rowmap)
+        ce_bwd(h, labels, w, bias, lse, gout, count, dH, gw, gb, False, rowmap)
         V = w.shape[0]
         out = torch.zeros(1, dW.numel() + (V + 3) // 4 * 4, dtype=dW.dtype, device=dW.device)
         out[0, :dW.numel()] = gw.reshape(-1)
         out[0, dW.numel():dW.numel() + V] = gb
         return out
-    h = _ce_rows(h, idx)
     gscale = gout.reshape(()) / count.reshape(()).clamp(min=1)
     logits = _bf(h.float()) @ _bf(w.float()).t() + bias
     p = torch.exp(logits - lse[:, None])

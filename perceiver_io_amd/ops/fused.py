@@ -637,6 +637,9 @@ class _LayerFn(torch.autograd.Function):
         return (None, None, None, None, None, dx_q, dx_kv, None) + (None,) * len(ps)
 
 
+# the fused latent self-attention layer forward (rowgemm.hip sa_layer_fwd_kernel);
+# PERCEIVER_SA_LAYER_FUSED=0 restores attn_fwd + post_attn(_ln_linear)_fwd
+SA_LAYER_FUSED = os.environ.get("PERCEIVER_SA_LAYER_FUSED", "1") != "0"
 PA_SIZES = lambda C: [C * C, C, C, C, C * C, C, C * C, C]  # noqa: E731  (Wo bo γ2 β2 W1 b1 W2 b2)
 LL_SIZES = lambda C: [C, C, 3 * C * C, 3 * C]                 # noqa: E731  (γ1 β1 Wqkv bqkv)
 SA_NP = 12  # parameters per self-attention layer (layer_spec_and_params order)
@@ -673,10 +676,26 @@ class _SABlockFn(torch.autograd.Function):
             xl = xl.contiguous()
         qkv, mean1, rstd1 = K.ln_linear_fwd(xl, P[0][0], P[0][1], EPS, bws[0][0], P[0][3], 0, None, True, True)
         saved = []
+        # one fused launch per layer (attention + post-attention + next LN1/QKV) for the
+        # C = 64, H = 4 latent stacks without attention dropout (sa_layer_fwd_kernel)
+        fused_layer = SA_LAYER_FUSED and C == 64 and H == 4 and N <= 256 and N % 64 == 0 and pdrop == 0.0
         for i in range(L):
             p = P[i]
             _, _, wo, w1, w2 = bws[i]
             bo, g2, be2, b1, b2 = p[5], p[6], p[7], p[9], p[11]
+            if fused_layer:
+                if i + 1 < L:
+                    pn = P[i + 1]
+                    o, lse, z, y, m2, r2, u, qkv_n, mean_n, rstd_n = K.sa_layer_fwd(
+                        qkv, xl, N, scale, wo, bo, g2, be2, EPS, w1, b1, w2, b2, pn[0], pn[1], bws[i + 1][0], pn[3],
+                        seed=seed, site=i, p=pdrop)
+                else:
+                    o, lse, z, y, m2, r2, u = K.sa_layer_fwd(qkv, xl, N, scale, wo, bo, g2, be2, EPS, w1, b1, w2, b2,
+                                                             seed=seed, site=i, p=pdrop)
+                    qkv_n = mean_n = rstd_n = None
+                saved += [xl, qkv, mean1, rstd1, o, lse, y, m2, r2, u]
+                xl, qkv, mean1, rstd1 = z, qkv_n, mean_n, rstd_n
+                continue
             qkv3 = qkv.view(B, N, 3 * C)
             # layer i of the block draws its masks from site i of the block's device seed
             o, lse = K.attn_fwd(qkv3[:, :, :C], qkv3[:, :, C:2 * C], qkv3[:, :, 2 * C:], None, H, D, scale, pdrop, seed,

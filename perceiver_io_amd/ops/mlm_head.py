@@ -70,7 +70,8 @@ def capacity(n_positions: int, p: float = 0.15) -> int:
 class _MaskedCE(torch.autograd.Function):
     """Mean CE over rows ``idx`` of ``h`` (``idx=None``: every row, ``h`` already compacted).
 
-    The kernels read the fp32 rows of ``h`` through ``idx`` (no gathered / bf16 copy), finalise
+    The forward reads the fp32 rows of ``h`` through ``idx`` and leaves their compact bf16 copy
+    for the backward (no separate gather / cast kernels), finalises
     the mean ``Σ rows / max(count, 1)`` in the combine kernel and form the row-loss gradient
     ``g / max(count, 1)`` on the device: no framework kernels around the head."""
 
@@ -86,16 +87,17 @@ class _MaskedCE(torch.autograd.Function):
         from .fused import weight_cache
 
         wb = weight_cache.get(weight)  # bf16 shadow written by the fused optimizer
-        loss, lse = ext.ce_fwd(h2, idx, labels_c, wb, bias.contiguous(), cnt)
-        ctx.save_for_backward(h2, wb, bias, lse, idx if idx is not None else torch.empty(0, dtype=torch.int64),
+        loss, lse, hs = ext.ce_fwd(h2, idx, labels_c, wb, bias.contiguous(), cnt)
+        ctx.save_for_backward(hs, wb, bias, lse, idx if idx is not None else torch.empty(0, dtype=torch.int64),
                               labels_c, cnt)
         ctx.hshape = h.shape
+        ctx.hrows = h2.shape[0]
         ctx.weight, ctx.bias_p = weight, bias
         return loss
 
     @staticmethod
     def backward(ctx, g):
-        h2, wb, bias, lse, idx, labels_c, cnt = ctx.saved_tensors
+        hs, wb, bias, lse, idx, labels_c, cnt = ctx.saved_tensors
         weight = ctx.weight
         gout = g.reshape(1)
         if gout.dtype != torch.float32:
@@ -106,11 +108,11 @@ class _MaskedCE(torch.autograd.Function):
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
         shp = ctx.hshape
-        dh = torch.zeros((h2.shape[0], shp[-1]), device=h2.device, dtype=torch.float32)
+        dh = torch.zeros((ctx.hrows, shp[-1]), device=hs.device, dtype=torch.float32)
         from . import fused
 
         ix = idx if idx.numel() else None
-        slab = ext.ce_bwd(h2, ix, labels_c, wb, bias.contiguous(), lse, gout.contiguous(), cnt, dh, weight.grad,
+        slab = ext.ce_bwd(hs, labels_c, wb, bias.contiguous(), lse, gout.contiguous(), cnt, dh, weight.grad,
                           ctx.bias_p.grad, True, ix, slab=fused.WGRAD_SLAB)
         if slab is not None:  # dW / db row-split partials: reduced by the next backward kernel
             fused.defer_slab(ext, slab, [weight.grad.view(-1), ctx.bias_p.grad.view(-1)], [0, weight.numel()])

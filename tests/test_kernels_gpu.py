@@ -380,18 +380,20 @@ def test_fused_cross_entropy(M, V, C):
     lab[::7] = -100
     hf = h.float()  # bf16-exact fp32 rows (the kernels cast on load)
     cnt = torch.tensor([float((lab >= 0).sum())], device=DEV)
-    l2, s2 = _emu().ce_fwd(hf, None, lab, w, bias, cnt)
+    l2, s2, hs2 = _emu().ce_fwd(hf, None, lab, w, bias, cnt)
     for _ in range(3):  # the loss finalisation's ticket is reset by every launch
-        l1, s1 = _ext().ce_fwd(hf, None, lab, w, bias, cnt)
+        l1, s1, hs1 = _ext().ce_fwd(hf, None, lab, w, bias, cnt)
         close(l1, l2, 1e-3, "loss")
         close(s1, s2, 1e-3, "lse")
+        assert torch.equal(hs1, hs2)
     # gathered rows: row r of the head input is hbig[idx[r]]
     idx = torch.randperm(2 * M, device=DEV)[:M]
     hbig = torch.zeros(2 * M, C, device=DEV)
     hbig[idx] = hf
-    lg, sg = _ext().ce_fwd(hbig, idx, lab, w, bias, cnt)
+    lg, sg, hsg = _ext().ce_fwd(hbig, idx, lab, w, bias, cnt)
     close(lg, l2, 1e-3, "loss gathered")
     close(sg, s2, 1e-3, "lse gathered")
+    assert torch.equal(hsg, hs2)  # the compact rows: gathered and cast on load
     gout = torch.tensor([0.37], device=DEV)
     rowmap = torch.randperm(3 * M, device=DEV)[:M]  # scatter rows into a larger (3M, C) gradient
     outs = []
@@ -399,10 +401,10 @@ def test_fused_cross_entropy(M, V, C):
         dH = torch.zeros(M, C, device=DEV)
         dW = torch.full((V, C), 7.0, device=DEV)  # overwritten (accumulate=False)
         db = torch.zeros(V, device=DEV)
-        K.ce_bwd(hf, None, lab, w, bias, s2, gout, cnt, dH, dW, db, False, None)
+        K.ce_bwd(hs2, lab, w, bias, s2, gout, cnt, dH, dW, db, False, None)
         dHs = torch.zeros(3 * M, C, device=DEV)
         dW2, db2 = dW.clone(), db.clone()
-        K.ce_bwd(hbig, idx, lab, w, bias, s2, gout, cnt, dHs, dW2, db2, True, rowmap)
+        K.ce_bwd(hs2, lab, w, bias, s2, gout, cnt, dHs, dW2, db2, True, rowmap)
         outs.append((dH, dW, db, dHs, dW2, db2))
     for a, b, n in zip(outs[0], outs[1], ("dH", "dW", "db", "dH rowmap", "dW acc", "db acc")):
         close(a, b, 3e-2, n)
@@ -598,3 +600,31 @@ def test_pe_grads(M, O, Kp, kin, nc, nblk):
         outs.append(t)
     for a, c, n in zip(outs[0], outs[1], ("dWa", "dWb", "db", "dgamma", "dbeta")):
         close(a, c, 2e-3, n)
+
+
+@pytest.mark.parametrize("B,N,nxt", [(4, 256, True), (3, 128, False), (2, 64, True)])
+def test_sa_layer_fwd_fused(B, N, nxt):
+    """Fused self-attention layer forward (attention + post-attention block + next LN1/QKV in one
+    launch) against the emulation's composition of the separate ops."""
+    torch.manual_seed(12)
+    C, R = 64, B * N
+    qkv = bf(torch.randn(R, 3 * C, device=DEV))
+    x = torch.randn(R, C, device=DEV)
+
+    def w(*s, sc=0.15):
+        return bf(torch.randn(*s, device=DEV) * sc)
+
+    wo, w1, w2 = w(C, C), w(C, C), w(C, C)
+    bo, b1, b2 = (torch.randn(C, device=DEV) * 0.1 for _ in range(3))
+    g2, be2 = 1 + 0.1 * torch.randn(C, device=DEV), 0.1 * torch.randn(C, device=DEV)
+    extra = {}
+    if nxt:
+        extra = dict(lnw=1 + 0.1 * torch.randn(C, device=DEV), lnb=0.1 * torch.randn(C, device=DEV), wq=w(3 * C, C),
+                     bq=0.1 * torch.randn(3 * C, device=DEV))
+    a = _ext().sa_layer_fwd(qkv, x, N, 0.25, wo, bo, g2, be2, 1e-5, w1, b1, w2, b2, **extra)
+    e = _emu().sa_layer_fwd(qkv, x, N, 0.25, wo, bo, g2, be2, 1e-5, w1, b1, w2, b2, **extra)
+    names = ["o", "lse", "z", "y", "mean2", "rstd2", "u"] + (["qkv_next", "mean1", "rstd1"] if nxt else [])
+    assert len(a) == len(e) == len(names)
+    for u, v, n in zip(a, e, names):
+        # the next layer's LN1 statistics come from z, after the bf16 GEMM chain: 1 %
+        close(u, v, 1e-3 if n in ("lse", "mean2", "rstd2") else 1e-2 if n in ("mean1", "rstd1") else 2e-2, n)
