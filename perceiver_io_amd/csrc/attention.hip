@@ -140,7 +140,9 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(AttnArgs a, uint16_t
     }
     fetch_pad(key0);
   };
-  if (PF && t_begin < t_end) fetch(t_begin * KT);
+  // unconditional prefetches (rows past the split read zeros): a load inside a branch makes the
+  // compiler drain every outstanding load (vmcnt(0)) before it, serialising the prologue
+  if constexpr (PF) fetch(t_begin * KT);
 
   for (int t0 = t_begin; t0 < t_end; t0 += NST) {
     const int rkey0 = t0 * KT;
@@ -172,7 +174,7 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(AttnArgs a, uint16_t
 #pragma unroll
     for (int j = 0; j < NST; ++j) padbits[j] = __ballot(pad_next[j]);
     lds_sync();
-    if (PF && t0 + NST < t_end) fetch((t0 + NST) * KT);
+    if constexpr (PF) fetch((t0 + NST) * KT);  // past the last round: zeros, never used
 
 #pragma unroll
     for (int j = 0; j < NST; ++j) {
@@ -418,22 +420,15 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
     }
   };
   // every prologue load is issued before the first wait: this wave's K^T / V^T operand
-  // fragments (B[k=d][col=key]), the block's K tile (for dQ), the first query round
+  // fragments (B[k=d][col=key]; the K ones also fill the block's LDS K tile for dQ), the
+  // first query round
   bf16x8 kf[KS], vf[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     kf[s] = *reinterpret_cast<const bf16x8*>(kbp + (long long)kc * a.k_rs + 16 * s + 8 * hh);
     vf[s] = *reinterpret_cast<const bf16x8*>(vbp + (long long)kc * a.v_rs + 16 * s + 8 * hh);
   }
-  constexpr int KSI = KB * CH / NTH;  // K-tile chunks per thread (= CH / 2)
-  bf16x8 kst[KSI];
-#pragma unroll
-  for (int i = 0; i < KSI; ++i) {
-    const int c = threadIdx.x + NTH * i, kk = kbase + c / CH, col = (c % CH) * 8;
-    const uint16_t* p = kk < a.Nk ? kbp + (long long)kk * a.k_rs + col : reinterpret_cast<const uint16_t*>(kZero32B);
-    kst[i] = *reinterpret_cast<const bf16x8*>(p);
-  }
-  if (qt_begin < nqt) fetch(qt_begin);
+  fetch(qt_begin);  // unconditional (see the forward): out-of-range query rows read zeros
   if (D < 32) {  // zero the padded head-dim columns 16..31
     for (int i = threadIdx.x; i < KB; i += NTH) {
       *reinterpret_cast<bf16x8*>(sK + i * LD + 16) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
@@ -446,11 +441,11 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
       *reinterpret_cast<bf16x8*>(sdO + i * LD + 24) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
     }
   }
+  // the block's K tile (for dQ) from this wave's own K fragments: no second global read of K
+  // (keys past Nk hold the clamped last key — finite, and their dS is zero)
 #pragma unroll
-  for (int i = 0; i < KSI; ++i) {
-    const int c = threadIdx.x + NTH * i;
-    *reinterpret_cast<bf16x8*>(sK + (c / CH) * LD + (c % CH) * 8) = kst[i];
-  }
+  for (int s2 = 0; s2 < KS; ++s2)
+    *reinterpret_cast<bf16x8*>(sK + (32 * w + r) * LD + 16 * s2 + 8 * hh) = kf[s2];
   f32x16 dK[NT], dV[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) dK[t] = dV[t] = f32x16{};
@@ -467,7 +462,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
     else if (threadIdx.x < NQS * 64) sDl[threadIdx.x - NQS * 32] = lreg;
     lds_sync();
     PIO_TS(2 + 4 * ((qt0 - qt_begin) / NQS));
-    if (qt0 + NQS < nqt) fetch(qt0 + NQS);
+    fetch(qt0 + NQS);  // past the last round: zeros, never used
 
 #pragma unroll
     for (int j = 0; j < NQS; ++j) {

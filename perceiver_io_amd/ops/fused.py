@@ -287,23 +287,20 @@ class KVSource:
 PE_FACTORED = os.environ.get("PERCEIVER_PE_FACTORED", "1") != "0"
 
 
-_pe_tables = {}
-
-
 def _pe_table(pe, nc: int, kin: int):
-    """Step-invariant PE operands, cached per PE table (refreshed if it is modified): the bf16
-    table Ebf (M, Kp) with only the PE columns [nc, kin) kept (Kp = kin rounded up to 32) and
-    the row sums Σe, Σe² over those columns."""
-    key = (pe.data_ptr(), pe.shape[0], nc, kin)
-    ent = _pe_tables.get(key)
-    if ent is not None and ent[0] is pe and ent[1] == pe._version:
-        return ent[2]
+    """Step-invariant PE operands, cached ON the PE table tensor (so they live exactly as long as
+    it does; refreshed if it is modified): the bf16 table Ebf (M, Kp) with only the PE columns
+    [nc, kin) kept (Kp = kin rounded up to 32) and the row sums Σe, Σe² over those columns."""
+    key = (pe._version, nc, kin)
+    ent = getattr(pe, "_pio_pe_table", None)
+    if ent is not None and ent[0] == key:
+        return ent[1]
     kp = -(-kin // 32) * 32
     pe_e = pe[:, nc:kin]
     ebf = torch.zeros((pe.shape[0], kp), device=pe.device, dtype=torch.bfloat16)
     ebf[:, nc:kin] = pe_e.to(torch.bfloat16)
     tab = (ebf, pe_e.sum(1).contiguous(), (pe_e * pe_e).sum(1).contiguous())
-    _pe_tables[key] = (pe, pe._version, tab)
+    pe._pio_pe_table = (key, tab)
     return tab
 
 
