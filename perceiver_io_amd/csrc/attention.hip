@@ -453,13 +453,16 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
 
   for (int qt0 = qt_begin; qt0 < nqt; qt0 += NQS) {
     lds_sync();  // the previous round's tiles and dS slabs are consumed
+    if (qt0 == qt_begin) PIO_TS(30);
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int c = threadIdx.x + NTH * i, isdo = c >= NQS * 32 * CH, cc = isdo ? c - NQS * 32 * CH : c;
       if (c < NQS * 64 * CH) *reinterpret_cast<bf16x8*>((isdo ? sdO : sQ) + (cc / CH) * LD + (cc % CH) * 8) = qreg[i];
     }
+    if (qt0 == qt_begin) PIO_TS(31);
     if (threadIdx.x < NQS * 32) sL[threadIdx.x] = lq_out ? INFINITY : lreg;
     else if (threadIdx.x < NQS * 64) sDl[threadIdx.x - NQS * 32] = lreg;
+    if (qt0 == qt_begin) PIO_TS(32);
     lds_sync();
     PIO_TS(2 + 4 * ((qt0 - qt_begin) / NQS));
     fetch(qt0 + NQS);  // past the last round: zeros, never used
@@ -495,10 +498,14 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
           dS[i] = p * (dP[i] - drow[i >> 2][i & 3]);
         }
       } else {
+        // Nk made opaque inside the dropout branch: the per-element index products cannot be
+        // hoisted into the prologue of the dropout-free path
+        uint32_t nk = (uint32_t)a.Nk;
+        asm volatile("" : "+s"(nk));
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const float p = fast_exp2(kpad ? -INFINITY : S[i] * a.scale_log2 - lrow[i >> 2][i & 3]);
-          const uint32_t idx = (uint32_t)(q0 + acc_row(i, hh)) * (uint32_t)a.Nk + (uint32_t)key;
+          const uint32_t idx = (uint32_t)(q0 + acc_row(i, hh)) * nk + (uint32_t)key;
           const bool keep = keep_elem(dkey, (uint32_t)(b * a.H + h), idx, a.drop_thresh);
           P[i] = keep ? p * a.drop_scale : 0.f;
           dS[i] = p * ((keep ? dP[i] * a.drop_scale : 0.f) - drow[i >> 2][i & 3]);

@@ -308,8 +308,12 @@ __device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
   h ^= h >> 15;
   return h;
 }
-// keep with probability (1-p): threshold = p * 2^32
+// keep with probability (1-p): threshold = p * 2^32.  The empty asm makes idx opaque at the call
+// site: every caller sits inside a dropout-enabled branch, and without it the compiler hoists
+// the hash's per-element multiplies (hundreds of quarter-rate v_mul_lo_u32) out of the loops
+// and the branch into the kernel prologue, where they run even with dropout off.
 __device__ __forceinline__ bool keep_elem(uint32_t seed, uint32_t stream, uint32_t idx, uint32_t thresh) {
+  asm volatile("" : "+v"(idx));
   return hash3(seed, stream, idx) >= thresh;
 }
 

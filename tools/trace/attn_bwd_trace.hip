@@ -116,6 +116,10 @@ int main(int argc, char** argv) {
     }
     printf("  total %.2f\n", us(prev - t[wv * 64]));
   }
+  printf("wave start skew vs wave 0 (us):");
+  for (int wv = 0; wv < 8; ++wv)
+    if (t[wv * 64]) printf(" %.2f", us(t[wv * 64] - t[0]));
+  printf("\n");
   std::vector<double> st, du;
   for (int i = 0; i < nwg; ++i) { st.push_back(us(w[2 * i] - g0)); du.push_back(us(w[2 * i + 1] - w[2 * i])); }
   std::sort(st.begin(), st.end());
