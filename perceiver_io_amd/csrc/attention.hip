@@ -700,7 +700,7 @@ static bool getenv_flag(const char* name) {
 template <int D, int NW>
 static void bwd_launch_t(const AttnArgs& a, const uint16_t* dO, const float* LSE, float* delta, float* dq,
                          long long dq_bs, int dq_rs, float* dk, long long dk_bs, int dk_rs, float* dv, long long dv_bs,
-                         int dv_rs, int kv_acc, long long dq_kbs, int qsplit_ok, hipStream_t st) {
+                         int dv_rs, int kv_acc, long long dq_kbs, int qsplit_ok, int dq_zeroed, hipStream_t st) {
   const int nkb = (a.Nk + 32 * NW - 1) / (32 * NW);
   // query splits when key blocks × heads × batch leave the GPU idle (≥ 4 query tiles each)
   const int nqt = (a.Nq + 31) / 32, base = nkb * a.H * a.B;
@@ -721,7 +721,7 @@ static void bwd_launch_t(const AttnArgs& a, const uint16_t* dO, const float* LSE
   // several key blocks add into dQ (fp32 atomics), unless each stores its own partial slice
   // (deterministic mode: dq_kbs > 0, summed by the caller)
   const int atomic = nkb > 1 && dq_kbs == 0;
-  if (atomic) {
+  if (atomic && !dq_zeroed) {
     const long long total = (long long)a.B * a.Nq * a.H * D;
     hipLaunchKernelGGL(zero_rows_kernel, dim3((unsigned)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096)), dim3(256), 0,
                        st, dq, dq_bs, dq_rs, a.Nq, a.H * D, total);
@@ -750,7 +750,7 @@ int attn_bwd_key_blocks(int Nk, int D) {
 void attn_bwd_launch(const AttnArgs& a, int D, const uint16_t* O, const uint16_t* dO, const float* LSE, float* delta,
                      float* dq, long long dq_bs, int dq_rs, float* dk, long long dk_bs, int dk_rs, float* dv,
                      long long dv_bs, int dv_rs, bool compute_delta, bool kv_acc, long long dq_kbs, int qsplit_ok,
-                     hipStream_t st) {
+                     int dq_zeroed, hipStream_t st) {
   // delta = rowsum(dO∘O) is normally produced by the post-attention backward kernel;
   // compute it here otherwise.  dQ needs no zero fill from the caller.
   const int rows = a.B * a.Nq;
@@ -758,10 +758,10 @@ void attn_bwd_launch(const AttnArgs& a, int D, const uint16_t* O, const uint16_t
     hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, dO, O, delta, (float*)nullptr,
                        rows, a.H, D, dq_rs);
   switch (D) {  // waves per workgroup: 8 for d ≤ 32, 4 above (keys per block = 32 × waves)
-    case 16: bwd_launch_t<16, 8>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, qsplit_ok, st); break;
-    case 32: bwd_launch_t<32, 8>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, qsplit_ok, st); break;
-    case 64: bwd_launch_t<64, 4>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, qsplit_ok, st); break;
-    case 128: bwd_launch_t<128, 4>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, qsplit_ok, st); break;
+    case 16: bwd_launch_t<16, 8>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, qsplit_ok, dq_zeroed, st); break;
+    case 32: bwd_launch_t<32, 8>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, qsplit_ok, dq_zeroed, st); break;
+    case 64: bwd_launch_t<64, 4>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, qsplit_ok, dq_zeroed, st); break;
+    case 128: bwd_launch_t<128, 4>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, qsplit_ok, dq_zeroed, st); break;
     default: break;
   }
 }

@@ -37,11 +37,13 @@ struct SlabJob {
   float* dst[kMaxSlabSegs];
   int off[kMaxSlabSegs];
   int len[kMaxSlabSegs];
+  float* zero_p;  // (mirror of csrc/common.h)
+  long long zero_n4;
 };
 
 void attn_fwd_launch(const AttnArgs&, int, uint16_t*, float*, float*, float*, int, hipStream_t);
 void attn_bwd_launch(const AttnArgs&, int, const uint16_t*, const uint16_t*, const float*, float*, float*, long long,
-                     int, float*, long long, int, float*, long long, int, bool, bool, long long, int, hipStream_t);
+                     int, float*, long long, int, float*, long long, int, bool, bool, long long, int, int, hipStream_t);
 int attn_bwd_key_blocks(int, int);
 void ln_linear_fwd_launch(const void*, bool, int, int, int, const float*, const float*, float, const uint16_t*, int,
                           const float*, int, int, const float*, int, void*, bool, int, float*, float*, const float*, int,
@@ -75,12 +77,12 @@ void wgrad_launch(const void*, bool, int, int, const void*, bool, int, int, int,
                   const float*, const float*, int, int, float*, float*, int, int, const float*, int, int, int,
                   hipStream_t);
 void ce_fwd_launch(int, const float*, const int64_t*, const int64_t*, const uint16_t*, const float*, int, int, float*,
-                   float*, float*, const float*, float*, float*, unsigned*, uint16_t*, int, hipStream_t);
+                   float*, float*, const float*, float*, float*, unsigned*, uint16_t*, int, float*, long long, hipStream_t);
 int ce_combine_blocks(int);
 int ce_num_splits(int, int);
 int ce_dw_splits(int, int);
 void mlm_select_launch(const int64_t*, int, int, int, int, int64_t*, int64_t*, int*, int64_t*, int64_t*, float*, bool*, bool*,
-                       hipStream_t);
+                       const float*, int, float*, unsigned*, hipStream_t);
 void ce_bwd_launch(int, const uint16_t*, const int64_t*, const uint16_t*, const float*, const float*, const float*,
                    const float*, int, int, float*, long long, const int64_t*, float*, float*, int, float*, int, hipStream_t);
 void embed_fwd_launch(const int64_t*, const float*, const float*, float*, long long, int, int, float, hipStream_t);
@@ -89,6 +91,7 @@ void embed_bwd_sorted_launch(const int64_t*, const int64_t*, const float*, float
 bool embed_bwd_local_launch(const int64_t*, const float*, float*, float*, int, int, int, float, hipStream_t);
 void text_mask_launch(const int64_t*, const bool*, int64_t*, int64_t*, int64_t*, long long, int, int, float, int,
                       uint32_t, int, hipStream_t);
+int stage_step_launch(void* const*, const void* const*, const long long*, int, float*, const float*, int, hipStream_t);
 void sumsq_launch(const float*, long long, float*, hipStream_t);
 void index_add_rows_launch(float*, long long, const int64_t*, const float*, long long, int, hipStream_t);
 void batch_sum2_launch(const float*, const float*, float*, float*, int, long long, hipStream_t);
@@ -245,7 +248,7 @@ std::vector<Tensor> attn_fwd(Tensor q, Tensor k, Tensor v, OptT kmask, int64_t H
 // skips the delta pass.
 std::vector<Tensor> attn_bwd(Tensor q, Tensor k, Tensor v, OptT kmask, Tensor o, Tensor dO, Tensor lse, OptT delta_in,
                              int64_t H, int64_t D, double scale, double dropout_p, OptT seed, OptT dq_out,
-                             OptT dk_out, OptT dv_out, bool kv_accumulate, int64_t site) {
+                             OptT dk_out, OptT dv_out, bool kv_accumulate, int64_t site, bool dq_zeroed) {
   auto a = make_args(q, k, v, kmask, (int)H, (int)D, scale, dropout_p, seed, site);
   TORCH_CHECK(dO.is_contiguous() && o.is_contiguous(), "O / dO must be contiguous (B, Nq, H*D)");
   auto f32 = q.options().dtype(torch::kFloat32);
@@ -269,14 +272,14 @@ std::vector<Tensor> attn_bwd(Tensor q, Tensor k, Tensor v, OptT kmask, Tensor o,
     pio::attn_bwd_launch(a, (int)D, bfp(o), bfp(dO), f32p(lse), delta.data_ptr<float>(), part.data_ptr<float>(),
                          (long long)a.Nq * H * D, (int)(H * D), dk.data_ptr<float>(), dk.stride(0), (int)dk.stride(1),
                          dv.data_ptr<float>(), dv.stride(0), (int)dv.stride(1), !delta_in.has_value(), kv_accumulate,
-                         (long long)a.B * a.Nq * H * D, 0, stream());
+                         (long long)a.B * a.Nq * H * D, 0, 0, stream());
     dq.narrow(2, 0, H * D).copy_(part.sum(0));
     return {dq, dk, dv};
   }
   pio::attn_bwd_launch(a, (int)D, bfp(o), bfp(dO), f32p(lse), delta.data_ptr<float>(), dq.data_ptr<float>(),
                        dq.stride(0), (int)dq.stride(1), dk.data_ptr<float>(), dk.stride(0), (int)dk.stride(1),
                        dv.data_ptr<float>(), dv.stride(0), (int)dv.stride(1), !delta_in.has_value(), kv_accumulate, 0,
-                       g_det ? 0 : 1, stream());
+                       g_det ? 0 : 1, dq_zeroed ? 1 : 0, stream());
   return {dq, dk, dv};
 }
 
@@ -470,7 +473,7 @@ pio::SlabJob make_job(const OptT& slab, std::vector<Tensor>& dsts, const std::ve
 std::vector<Tensor> post_attn_bwd(Tensor dz, Tensor y, Tensor m2, Tensor r2, Tensor u, Tensor o, Tensor wo, Tensor w1,
                                   Tensor w2, Tensor g2, Tensor be2, int64_t H, std::vector<Tensor> grads, bool slab,
                                   OptT job_slab, std::vector<Tensor> job_dsts, std::vector<int64_t> job_offs,
-                                  OptT seed, int64_t site, double p) {
+                                  OptT seed, int64_t site, double p, OptT zero_out) {
   TORCH_CHECK(dz.is_contiguous() && y.is_contiguous() && u.is_contiguous() && o.is_contiguous(),
               "post_attn_bwd operands must be contiguous (R, C)");
   const int R = (int)dz.size(0), C = (int)dz.size(1);
@@ -491,9 +494,18 @@ std::vector<Tensor> post_attn_bwd(Tensor dz, Tensor y, Tensor m2, Tensor r2, Ten
   Tensor dy = torch::empty({R, C}, f32);
   Tensor dO = torch::empty({R, C}, dz.options().dtype(torch::kBFloat16));
   Tensor delta = torch::empty({R, H}, f32);
+  pio::SlabJob job = make_job(job_slab, job_dsts, job_offs);
+  if (zero_out.has_value()) {  // cleared by this kernel's workgroups on the way (the next kernel's accumulator)
+    CHECK_DT(*zero_out, torch::kFloat32);
+    TORCH_CHECK(zero_out->is_contiguous() && zero_out->numel() % 4 == 0 && zero_out->get_device() == dz.get_device() &&
+                    reinterpret_cast<uintptr_t>(zero_out->data_ptr()) % 16 == 0,
+                "post_attn_bwd: zero_out must be a contiguous, 16-byte aligned fp32 buffer of 4k elements");
+    job.zero_p = zero_out->data_ptr<float>();
+    job.zero_n4 = zero_out->numel() / 4;
+  }
   pio::post_attn_bwd_launch(C, f32p(dz), f32p(y), f32p(m2), f32p(r2), bfp(u), bfp(o), bfp(wo), bfp(w1), bfp(w2),
                             f32p(g2), f32p(be2), dy.data_ptr<float>(), bfp_mut(dO), delta.data_ptr<float>(), (int)H,
-                            pg, R, make_job(job_slab, job_dsts, job_offs), make_drop(seed, site, p), stream());
+                            pg, R, job, make_drop(seed, site, p), stream());
   return {dy, dO, delta};
 }
 
@@ -616,34 +628,56 @@ void wgrad(Tensor g, Tensor a, int64_t amode, OptT mean, OptT rstd, OptT lnw, Op
                     vrs < 0 ? 0 : vrs, wrs < 0 ? 0 : wrs, pp, prs, prows, npix, stream());
 }
 
+// per-device counters shared by the MLM head kernels: [0, kCeTickets - 1) ce_fwd_kernel's
+// per-tile + global tickets, kCeTickets - 1 the selection kernel's.  Zero between launches (each
+// counter is reset by its last taker); calls on a device are stream-ordered.  Fixed size,
+// allocated once, so captured graphs never see it move.
+constexpr int64_t kCeTickets = 1 << 16;
+static Tensor& ce_ticket(const Tensor& like) {
+  static std::unordered_map<int, Tensor> tickets;
+  const int d = like.get_device();
+  auto it = tickets.find(d);
+  if (it == tickets.end()) it = tickets.emplace(d, torch::zeros({kCeTickets}, like.options().dtype(torch::kInt32))).first;
+  return it->second;
+}
+
 // labels (B, L) → [idx_b (B, cap), labels_b (B, cap), gidx (gcap), glabels (gcap), total (1) fp32,
-// overflow (1) bool]: per-sequence slots of the selected positions and their global compaction.
+// overflow (1) bool (+ q (B, cap, C) = queries[idx_b] when the output-query array is given)]:
+// per-sequence slots of the selected positions and their global compaction, one launch.
 // sticky: optional persistent bool the kernel sets when this call overflows (never clears)
-std::vector<Tensor> mlm_select(Tensor labels, int64_t cap, int64_t gcap, OptT sticky) {
+std::vector<Tensor> mlm_select(Tensor labels, int64_t cap, int64_t gcap, OptT sticky, OptT queries) {
   CHECK_DT(labels, torch::kInt64);
   TORCH_CHECK(labels.dim() == 2 && labels.is_contiguous(), "labels must be (B, L) contiguous");
   const int B = (int)labels.size(0), L = (int)labels.size(1);
-  TORCH_CHECK(cap > 0 && cap <= L && gcap > 0, "bad capacities");
+  TORCH_CHECK(cap > 0 && cap <= L && gcap > 0 && B > 0, "bad capacities");
   auto i64 = labels.options();
   Tensor idx_b = torch::empty({B, cap}, i64), lab_b = torch::empty({B, cap}, i64);
   Tensor count = torch::empty({B}, i64.dtype(torch::kInt32));
   Tensor gidx = torch::empty({gcap}, i64), glab = torch::empty({gcap}, i64);
   Tensor total = torch::empty({1}, i64.dtype(torch::kFloat32)), ovf = torch::empty({1}, i64.dtype(torch::kBool));
+  const float* P = nullptr;
+  float* qp = nullptr;
+  int C = 0;
+  Tensor q;
+  if (queries.has_value()) {
+    CHECK_DT(*queries, torch::kFloat32);
+    TORCH_CHECK(queries->dim() == 2 && queries->is_contiguous() && queries->size(0) >= L && queries->size(1) % 4 == 0 &&
+                    queries->get_device() == labels.get_device(),
+                "mlm_select: queries must be a contiguous fp32 (>= L, C) array, C % 4 == 0, on the labels' device");
+    C = (int)queries->size(1);
+    P = queries->data_ptr<float>();
+    q = torch::empty({B, cap, C}, queries->options());
+    qp = q.data_ptr<float>();
+  }
+  Tensor& tk = ce_ticket(labels);
   pio::mlm_select_launch(labels.data_ptr<int64_t>(), B, L, (int)cap, (int)gcap, idx_b.data_ptr<int64_t>(),
                          lab_b.data_ptr<int64_t>(), count.data_ptr<int>(), gidx.data_ptr<int64_t>(),
                          glab.data_ptr<int64_t>(), total.data_ptr<float>(), ovf.data_ptr<bool>(),
-                         sticky.has_value() ? sticky->data_ptr<bool>() : nullptr, stream());
-  return {idx_b, lab_b, gidx, glab, total, ovf};
-}
-
-// one ticket per device for the CE loss finalisation (ce_combine_kernel): zero between
-// launches (the last workgroup resets it); CE calls on a device are stream-ordered
-static Tensor& ce_ticket(const Tensor& like) {
-  static std::unordered_map<int, Tensor> tickets;
-  const int d = like.get_device();
-  auto it = tickets.find(d);
-  if (it == tickets.end()) it = tickets.emplace(d, torch::zeros({4}, like.options().dtype(torch::kInt32))).first;
-  return it->second;
+                         sticky.has_value() ? sticky->data_ptr<bool>() : nullptr, P, C, qp,
+                         reinterpret_cast<unsigned*>(tk.data_ptr<int>()) + (kCeTickets - 1), stream());
+  std::vector<Tensor> out{idx_b, lab_b, gidx, glab, total, ovf};
+  if (queries.has_value()) out.push_back(q);
+  return out;
 }
 
 static const int64_t* opt_idx(const OptT& idx, int64_t n) {
@@ -656,7 +690,8 @@ static const int64_t* opt_idx(const OptT& idx, int64_t n) {
 // mean CE over the rows of h (fp32 (N, C); row r = h[idx[r]] when idx is given, else h[r]) with
 // label ≥ 0: → {loss (0-dim) = Σ rows / max(count, 1), per-row lse (M,), the compact bf16 rows
 // hs (M, C) the backward kernels read}.  count: fp32 (1,).
-std::vector<Tensor> ce_fwd(Tensor h, OptT idx, Tensor labels, Tensor w, Tensor bias, Tensor count) {
+// zero_out: an optional fp32 buffer the kernel clears on the way (the backward's dH accumulator)
+std::vector<Tensor> ce_fwd(Tensor h, OptT idx, Tensor labels, Tensor w, Tensor bias, Tensor count, OptT zero_out) {
   TORCH_CHECK(h.is_contiguous() && w.is_contiguous() && labels.is_contiguous() && bias.is_contiguous());
   CHECK_DT(labels, torch::kInt64);
   CHECK_DT(h, torch::kFloat32);
@@ -672,10 +707,21 @@ std::vector<Tensor> ce_fwd(Tensor h, OptT idx, Tensor labels, Tensor w, Tensor b
   Tensor blk = torch::empty({pio::ce_combine_blocks(M)}, f32);
   Tensor hs = torch::empty({M, C}, h.options().dtype(torch::kBFloat16));
   Tensor& tk = ce_ticket(h);
+  TORCH_CHECK(pio::ce_combine_blocks(M) + 1 < kCeTickets - 1, "ce_fwd: too many rows");
+  float* zp = nullptr;
+  int64_t zn = 0;
+  if (zero_out.has_value()) {
+    CHECK_DT(*zero_out, torch::kFloat32);
+    TORCH_CHECK(zero_out->is_contiguous() && zero_out->numel() % 4 == 0 && zero_out->get_device() == h.get_device() &&
+                    reinterpret_cast<uintptr_t>(zero_out->data_ptr()) % 16 == 0,
+                "ce_fwd: zero_out must be a contiguous, 16-byte aligned fp32 buffer of 4k elements");
+    zp = zero_out->data_ptr<float>();
+    zn = zero_out->numel();
+  }
   pio::ce_fwd_launch(C, h.data_ptr<float>(), ip, labels.data_ptr<int64_t>(), bfp(w), f32p(bias), M, V,
                      part.data_ptr<float>(), picked.data_ptr<float>(), lse.data_ptr<float>(), f32p(count),
                      loss.data_ptr<float>(), blk.data_ptr<float>(), reinterpret_cast<unsigned*>(tk.data_ptr<int>()),
-                     bfp_mut(hs), ns, stream());
+                     bfp_mut(hs), ns, zp, zn, stream());
   return {loss, lse, hs};
 }
 
@@ -767,6 +813,33 @@ std::vector<Tensor> text_mask(Tensor x, OptT pad, Tensor state, int64_t unk, int
                         lab.data_ptr<int64_t>(), n, (int)unk, (int)mask, (float)p, (int)lo, (uint32_t)(hi - lo),
                         advance ? 1 : 0, stream());
   return {xm, lab};
+}
+
+// one launch per replayed step: dsts[i] <- srcs[i] (same device, dtype-agnostic byte copies of
+// contiguous tensors of equal size) and hyper_dst[:len(hyper)] <- hyper (values by kernel argument)
+void stage_step(std::vector<Tensor> dsts, std::vector<Tensor> srcs, OptT hyper_dst, std::vector<double> hyper) {
+  TORCH_CHECK(dsts.size() == srcs.size() && dsts.size() <= 8 && hyper.size() <= 8, "stage_step: at most 8 tensors / 8 values");
+  std::vector<void*> d;
+  std::vector<const void*> x;
+  std::vector<long long> n;
+  for (size_t i = 0; i < dsts.size(); ++i) {
+    const Tensor& a = dsts[i];
+    const Tensor& b = srcs[i];
+    TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.get_device() == b.get_device() && a.is_contiguous() && b.is_contiguous() &&
+                    a.scalar_type() == b.scalar_type() && a.numel() == b.numel(),
+                "stage_step: pairs must be contiguous same-device tensors of equal dtype and size");
+    d.push_back(a.data_ptr());
+    x.push_back(b.data_ptr());
+    n.push_back((long long)(a.numel() * a.element_size()));
+  }
+  float* hp = nullptr;
+  std::vector<float> hv(hyper.begin(), hyper.end());
+  if (hyper_dst.has_value()) {
+    CHECK_DT(*hyper_dst, torch::kFloat32);
+    TORCH_CHECK(hyper_dst->is_contiguous() && hyper_dst->numel() >= (int64_t)hv.size(), "stage_step: hyper_dst too small");
+    hp = hyper_dst->data_ptr<float>();
+  }
+  TORCH_CHECK(pio::stage_step_launch(d.data(), x.data(), n.data(), (int)d.size(), hp, hv.data(), (int)hv.size(), stream()) == 0);
 }
 
 void sumsq(Tensor g, Tensor out) { pio::sumsq_launch(f32p(g), g.numel(), out.data_ptr<float>(), stream()); }
@@ -1060,7 +1133,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_bwd", &attn_bwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("kmask"), py::arg("o"), py::arg("dO"),
         py::arg("lse"), py::arg("delta_in"), py::arg("H"), py::arg("D"), py::arg("scale"), py::arg("dropout_p"),
         py::arg("seed"), py::arg("dq_out"), py::arg("dk_out"), py::arg("dv_out"), py::arg("kv_accumulate") = false,
-        py::arg("site") = 0);
+        py::arg("site") = 0, py::arg("dq_zeroed") = false);
   m.def("ln_linear_fwd", &ln_linear_fwd, py::arg("x"), py::arg("lnw"), py::arg("lnb"), py::arg("eps"), py::arg("w"),
         py::arg("bias"), py::arg("act"), py::arg("res"), py::arg("out_bf16"), py::arg("save_stats"),
         py::arg("pe") = py::none(), py::arg("kin") = -1);
@@ -1086,7 +1159,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("o"), py::arg("wo"), py::arg("w1"), py::arg("w2"), py::arg("g2"), py::arg("be2"), py::arg("H"),
         py::arg("grads"), py::arg("slab") = false, py::arg("job_slab") = py::none(),
         py::arg("job_dsts") = std::vector<Tensor>(), py::arg("job_offs") = std::vector<int64_t>(),
-        py::arg("seed") = py::none(), py::arg("site") = 0, py::arg("p") = 0.0);
+        py::arg("seed") = py::none(), py::arg("site") = 0, py::arg("p") = 0.0, py::arg("zero_out") = py::none());
   m.def("ln_linear_bwd", &ln_linear_bwd, py::arg("g"), py::arg("w"), py::arg("x"), py::arg("mean"), py::arg("rstd"),
         py::arg("lnw"), py::arg("lnb"), py::arg("dres"), py::arg("need_dx"), py::arg("dlnw"), py::arg("dlnb"),
         py::arg("dW"), py::arg("db"), py::arg("pe") = py::none(), py::arg("kin") = -1, py::arg("slab") = false,
@@ -1095,12 +1168,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad", &wgrad, py::arg("g"), py::arg("a"), py::arg("amode"), py::arg("mean"), py::arg("rstd"), py::arg("lnw"),
         py::arg("lnb"), py::arg("rows_per_wg"), py::arg("dW"), py::arg("db"), py::arg("pe") = py::none(),
         py::arg("kin") = -1);
-  m.def("mlm_select", &mlm_select, py::arg("labels"), py::arg("cap"), py::arg("gcap"), py::arg("sticky") = py::none());
+  m.def("mlm_select", &mlm_select, py::arg("labels"), py::arg("cap"), py::arg("gcap"), py::arg("sticky") = py::none(),
+        py::arg("queries") = py::none());
   m.def("index_add_rows", &index_add_rows);
   m.def("batch_sum2", &batch_sum2);
   m.def("pixel_ce_fwd", &pixel_ce_fwd);
   m.def("pixel_ce_bwd", &pixel_ce_bwd);
-  m.def("ce_fwd", &ce_fwd);
+  m.def("stage_step", &stage_step, py::arg("dsts"), py::arg("srcs"), py::arg("hyper_dst") = py::none(),
+        py::arg("hyper") = std::vector<double>{});
+  m.def("ce_fwd", &ce_fwd, py::arg("h"), py::arg("idx"), py::arg("labels"), py::arg("w"), py::arg("bias"),
+        py::arg("count"), py::arg("zero_out") = py::none());
   m.def("ce_bwd", &ce_bwd, py::arg("h"), py::arg("labels"), py::arg("w"), py::arg("bias"),
         py::arg("lse"), py::arg("gout"), py::arg("count"), py::arg("dH"), py::arg("dW"), py::arg("db"),
         py::arg("accumulate"), py::arg("rowmap") = py::none(), py::arg("slab") = false);

@@ -240,7 +240,20 @@ struct SlabJob {
   float* dst[kMaxSlabSegs];
   int off[kMaxSlabSegs];
   int len[kMaxSlabSegs];
+  // side job of the kernel that carries this struct: clear zero_n4 float4s at zero_p (the
+  // accumulator of the NEXT kernel, e.g. the attention backward's atomic dQ), one slice per
+  // workgroup — no separate fill launch on the chain
+  float* zero_p;
+  long long zero_n4;
 };
+// this workgroup's slice of a SlabJob zero span
+__device__ __forceinline__ void zero_span_block(const SlabJob& j) {
+  if (j.zero_p == nullptr) return;
+  const long long nwg = gridDim.x, per = (j.zero_n4 + nwg - 1) / nwg;
+  const long long z0 = (long long)blockIdx.x * per, z1 = z0 + per < j.zero_n4 ? z0 + per : j.zero_n4;
+  for (long long i = z0 + threadIdx.x; i < z1; i += blockDim.x)
+    reinterpret_cast<float4*>(j.zero_p)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
 // part: ≥ 4 KiB of 16-B aligned LDS
 __device__ __forceinline__ void slab_reduce_block(const SlabJob& j, int b, float4* part) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;

@@ -457,3 +457,65 @@ void cast_bf16_launch(const float* x, uint16_t* y, long long n, hipStream_t st) 
 }
 
 }  // namespace pio
+
+// ------------------------------------------------------------------------------------------
+// Per-step staging for a replayed hipGraph in ONE launch: the new batch's tensors are copied
+// into the graph's static input buffers and the optimizer's per-step hyper-parameters (lr,
+// step, betas, ...) arrive as kernel arguments (captured by value at launch, so no pinned
+// staging ring and no host→device copy).  Replaces one copyBuffer per input tensor + one for
+// the hyper-parameters.  Segments whose pointers and size are 16-byte multiples are copied in
+// 16-byte units, the others byte-wise.
+// ------------------------------------------------------------------------------------------
+namespace pio {
+constexpr int kStageSegs = 8, kStageHyper = 8;
+struct StageArgs {
+  void* dst[kStageSegs];
+  const void* src[kStageSegs];
+  long long bytes[kStageSegs];
+  int vec[kStageSegs];
+  int nseg;
+  float* hyper_dst;
+  float hyper[kStageHyper];
+  int nhyper;
+};
+
+__global__ __launch_bounds__(256) void stage_step_kernel(StageArgs a) {
+  const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x, nt = (long long)gridDim.x * blockDim.x;
+  if (blockIdx.x == 0 && threadIdx.x < a.nhyper && a.hyper_dst != nullptr) a.hyper_dst[threadIdx.x] = a.hyper[threadIdx.x];
+  for (int s = 0; s < a.nseg; ++s) {
+    if (a.vec[s]) {
+      const long long n = a.bytes[s] >> 4;
+      uint4* d = reinterpret_cast<uint4*>(a.dst[s]);
+      const uint4* x = reinterpret_cast<const uint4*>(a.src[s]);
+      for (long long i = tid; i < n; i += nt) d[i] = x[i];
+    } else {
+      uint8_t* d = reinterpret_cast<uint8_t*>(a.dst[s]);
+      const uint8_t* x = reinterpret_cast<const uint8_t*>(a.src[s]);
+      for (long long i = tid; i < a.bytes[s]; i += nt) d[i] = x[i];
+    }
+  }
+}
+
+int stage_step_launch(void* const* dst, const void* const* src, const long long* bytes, int nseg, float* hyper_dst,
+                      const float* hyper, int nhyper, hipStream_t st) {
+  if (nseg > kStageSegs || nhyper > kStageHyper) return -1;
+  StageArgs a{};
+  long long units = 0;
+  for (int s = 0; s < nseg; ++s) {
+    a.dst[s] = dst[s];
+    a.src[s] = src[s];
+    a.bytes[s] = bytes[s];
+    a.vec[s] = ((reinterpret_cast<uintptr_t>(dst[s]) | reinterpret_cast<uintptr_t>(src[s]) | (uintptr_t)bytes[s]) & 15) == 0;
+    const long long u = a.vec[s] ? bytes[s] >> 4 : bytes[s];
+    units = u > units ? u : units;
+  }
+  a.nseg = nseg;
+  a.hyper_dst = hyper_dst;
+  for (int i = 0; i < nhyper; ++i) a.hyper[i] = hyper[i];
+  a.nhyper = hyper_dst ? nhyper : 0;
+  long long blocks = (units + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > 1024 ? 1024 : blocks);
+  hipLaunchKernelGGL(stage_step_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  return 0;
+}
+}  // namespace pio

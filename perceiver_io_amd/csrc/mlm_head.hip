@@ -11,6 +11,8 @@
 //   bwd-b: dW  = (softmax − onehot)ᵀ·g · H, db = Σ rows   (vocab chunk × row split, fp32 atomics)
 // Streamed operands (W chunks, H tiles) are register-prefetched one tile ahead.
 // Only the ~15 % masked positions are ever passed in (rows compacted on device).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace pio {
@@ -126,7 +128,8 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ H
                                                      const int64_t* __restrict__ labels,
                                                      const uint16_t* __restrict__ W, const float* __restrict__ bias,
                                                      int M, int V, int chunks_per_split, float* __restrict__ part_ms,
-                                                     float* __restrict__ picked, uint16_t* __restrict__ hs_out) {
+                                                     float* __restrict__ picked, uint16_t* __restrict__ hs_out,
+                                                     float* __restrict__ zero_out, long long zero_n4) {
   constexpr int LD = C + 8;
   __shared__ __attribute__((aligned(16))) uint16_t sH[HB * LD];
   __shared__ __attribute__((aligned(16))) uint16_t sW[VB * LD];
@@ -208,28 +211,52 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ H
       part_ms[((long long)split * M + g) * 2 + 1] = sx;
     }
   }
+  // the backward's atomically accumulated dH rows are cleared here (no separate fill launch)
+  if (zero_out != nullptr) {
+    const long long nwg = (long long)gridDim.x * gridDim.y, wg = (long long)split * gridDim.x + blockIdx.x;
+    const long long per = (zero_n4 + nwg - 1) / nwg, z1 = min(zero_n4, (wg + 1) * per);
+    for (long long i = wg * per + threadIdx.x; i < z1; i += blockDim.x)
+      reinterpret_cast<float4*>(zero_out)[i] = float4{0.f, 0.f, 0.f, 0.f};
+  }
 }
 
-// per-row lse (kept for backward) and loss = lse − picked (0 for ignored rows); the mean loss
-// Σ rows / max(count, 1) is finalised in-kernel: each workgroup stores its partial sum, and the
-// last one to take a ticket adds the partials in a fixed order (deterministic) and resets the
-// ticket.  (picked[r] is written by the forward for every row with a label, so it needs no
-// zero fill.)
-__global__ __launch_bounds__(256) void ce_combine_kernel(const float* __restrict__ part_ms,
-                                                         const float* __restrict__ picked,
-                                                         const int64_t* __restrict__ labels, int M, int nsplit,
-                                                         float* __restrict__ lse, const float* __restrict__ count,
-                                                         float* __restrict__ loss, float* __restrict__ blk,
-                                                         unsigned* __restrict__ ticket) {
-  __shared__ float red[4];
+// per-row lse (kept for backward) and loss = lse − picked (0 for ignored rows), four threads per
+// row (splits q, q + 4, … merged online, then across the four); the mean loss Σ rows /
+// max(count, 1) is finalised in-kernel: each workgroup stores its partial sum, and the last one
+// to take a ticket adds the partials in a fixed order (deterministic) and resets the ticket.
+// (picked[r] is written by the forward for every row with a label, so it needs no zero fill.)
+constexpr int kCombineRows = 256;
+__global__ __launch_bounds__(1024) void ce_combine_kernel(const float* __restrict__ part_ms,
+                                                          const float* __restrict__ picked,
+                                                          const int64_t* __restrict__ labels, int M, int nsplit,
+                                                          float* __restrict__ lse, const float* __restrict__ count,
+                                                          float* __restrict__ loss, float* __restrict__ blk,
+                                                          unsigned* __restrict__ ticket) {
+  __shared__ float sM[4][kCombineRows], sS[4][kCombineRows], red[16];
   __shared__ int last;
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  float lr = 0.f;
+  const int rr = threadIdx.x % kCombineRows, q = threadIdx.x / kCombineRows;
+  const int r = blockIdx.x * kCombineRows + rr;
+  float mx = -1e30f, sx = 0.f;
   if (r < M) {
-    float mm = -1e30f;
-    for (int s = 0; s < nsplit; ++s) mm = fmaxf(mm, part_ms[((long long)s * M + r) * 2]);
+#pragma unroll 2
+    for (int s = q; s < nsplit; s += 4) {
+      const float m = part_ms[((long long)s * M + r) * 2], e = part_ms[((long long)s * M + r) * 2 + 1];
+      const float mn = fmaxf(mx, m);
+      sx = sx * __expf(mx - mn) + e * __expf(m - mn);
+      mx = mn;
+    }
+  }
+  sM[q][rr] = mx;
+  sS[q][rr] = sx;
+  __syncthreads();
+  float lr = 0.f;
+  if (q == 0 && r < M) {
+    float mm = sM[0][rr];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) mm = fmaxf(mm, sM[k][rr]);
     float ss = 0.f;
-    for (int s = 0; s < nsplit; ++s) ss += part_ms[((long long)s * M + r) * 2 + 1] * __expf(part_ms[((long long)s * M + r) * 2] - mm);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ss += sS[k][rr] * __expf(sM[k][rr] - mm);
     const float L = mm + __logf(ss);
     lse[r] = L;
     lr = labels[r] >= 0 ? L - picked[r] : 0.f;
@@ -238,7 +265,9 @@ __global__ __launch_bounds__(256) void ce_combine_kernel(const float* __restrict
   if (lane_id() == 0) red[wave_id()] = lr;
   __syncthreads();
   if (threadIdx.x == 0) {
-    blk[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+    float t = 0.f;
+    for (int k = 0; k < 4; ++k) t += red[k];  // waves 4..15 hold q > 0 threads: zero
+    blk[blockIdx.x] = t;
     __threadfence();
     last = atomicAdd(ticket, 1u) == gridDim.x - 1;
   }
@@ -252,7 +281,9 @@ __global__ __launch_bounds__(256) void ce_combine_kernel(const float* __restrict
   if (lane_id() == 0) red[wave_id()] = t;
   __syncthreads();
   if (threadIdx.x == 0) {
-    loss[0] = ((red[0] + red[1]) + (red[2] + red[3])) / fmaxf(count[0], 1.f);
+    float tt = 0.f;
+    for (int k = 0; k < 16; ++k) tt += red[k];
+    loss[0] = tt / fmaxf(count[0], 1.f);
     *ticket = 0u;
   }
 }
@@ -470,8 +501,15 @@ __global__ __launch_bounds__(256) void ce_bwd_dw_kernel(const uint16_t* __restri
 //   global: the valid slots of all sequences compacted into gcap rows for the vocab GEMMs
 //           (unused → slot 0 with label −100), total = Σ count (the mean's denominator)
 // ------------------------------------------------------------------------------------
-__global__ void select_rows_kernel(const int64_t* __restrict__ labels, int L, int cap, int64_t* __restrict__ idx_b,
-                                   int64_t* __restrict__ lab_b, int* __restrict__ count) {
+// select_rows: workgroup b compacts sequence b (slot → position also kept in LDS) and, when
+// given, copies the output-query rows q[b, j] = P[idx_b[b, j]] the decoder cross-attention reads
+// (the gather of the query array).  select_global (one workgroup): block-wide scan of the
+// per-sequence counts, then one wave per sequence writes its valid slots into the global rows.
+__global__ __launch_bounds__(256) void select_rows_kernel(const int64_t* __restrict__ labels, int L, int cap,
+                                                          int64_t* __restrict__ idx_b, int64_t* __restrict__ lab_b,
+                                                          int* __restrict__ count, const float* __restrict__ P, int C,
+                                                          float* __restrict__ q) {
+  extern __shared__ int sIdx[];  // [cap]
   __shared__ int sW[4], sOff;
   const int b = blockIdx.x, w = wave_id(), l = lane_id();
   if (threadIdx.x == 0) sOff = 0;
@@ -490,6 +528,7 @@ __global__ void select_rows_kernel(const int64_t* __restrict__ labels, int L, in
     if (sel && pos < cap) {
       idx_b[(long long)b * cap + pos] = i;
       lab_b[(long long)b * cap + pos] = lab;
+      sIdx[pos] = i;
     }
     lds_sync();
     if (threadIdx.x == 0) sOff += sW[0] + sW[1] + sW[2] + sW[3];
@@ -499,42 +538,85 @@ __global__ void select_rows_kernel(const int64_t* __restrict__ labels, int L, in
   for (int j = (cnt < cap ? cnt : cap) + threadIdx.x; j < cap; j += blockDim.x) {
     idx_b[(long long)b * cap + j] = j % L;
     lab_b[(long long)b * cap + j] = -100;
+    sIdx[j] = j % L;
   }
   if (threadIdx.x == 0) count[b] = cnt;
+  if (q == nullptr) return;
+  lds_sync();
+  const int C4 = C >> 2;
+  const float4* P4 = reinterpret_cast<const float4*>(P);
+  float4* q4 = reinterpret_cast<float4*>(q) + (long long)b * cap * C4;
+  const int n4 = cap * C4;
+  for (int e0 = 0; e0 < n4; e0 += 4 * 256) {  // four independent row loads in flight per thread
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * 256 + threadIdx.x;
+      if (e < n4) {
+        const int j = e / C4;
+        v[u] = P4[(long long)sIdx[j] * C4 + (e - j * C4)];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * 256 + threadIdx.x;
+      if (e < n4) q4[e] = v[u];
+    }
+  }
 }
 
-__global__ void select_global_kernel(const int* __restrict__ count, int B, int cap, const int64_t* __restrict__ lab_b,
-                                     int gcap, int64_t* __restrict__ gidx, int64_t* __restrict__ glab,
-                                     float* __restrict__ total, bool* __restrict__ overflow,
-                                     bool* __restrict__ sticky) {
+__global__ __launch_bounds__(1024) void select_global_kernel(const int* __restrict__ count, int B, int cap,
+                                                             const int64_t* __restrict__ lab_b, int gcap,
+                                                             int64_t* __restrict__ gidx, int64_t* __restrict__ glab,
+                                                             float* __restrict__ total, bool* __restrict__ overflow,
+                                                             bool* __restrict__ sticky) {
   extern __shared__ int sOffs[];  // [B + 1] exclusive prefix of min(count, cap)
+  __shared__ int sW[16], sAll, sOvf;
+  const int w = wave_id(), l = lane_id(), nw = blockDim.x >> 6;
+  if (threadIdx.x == 0) { sAll = 0; sOvf = 0; }
+  __syncthreads();
+  int carry = 0, all = 0, ovf = 0;
+  for (int b0 = 0; b0 < B; b0 += blockDim.x) {  // block-wide exclusive scan
+    const int bb = b0 + threadIdx.x;
+    const int c = bb < B ? count[bb] : 0, n = c < cap ? c : cap;
+    all += c;
+    ovf |= c > cap;
+    int v = n;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int u = __shfl_up(v, d, 64);
+      if (l >= d) v += u;
+    }
+    if (l == 63) sW[w] = v;
+    __syncthreads();
+    int woff = carry;
+    for (int k = 0; k < w; ++k) woff += sW[k];
+    if (bb < B) sOffs[bb] = woff + v - n;
+    for (int k = 0; k < nw; ++k) carry += sW[k];
+    __syncthreads();
+  }
+  if (all) atomicAdd(&sAll, all);
+  if (ovf) sOvf = 1;
+  if (threadIdx.x == 0) sOffs[B] = carry;
+  __syncthreads();
   if (threadIdx.x == 0) {
-    int acc = 0, all = 0;
-    bool ovf = false;
-    for (int b = 0; b < B; ++b) {
-      const int n = count[b] < cap ? count[b] : cap;
-      ovf |= count[b] > cap;
-      sOffs[b] = acc;
-      acc += n;
-      all += count[b];
-    }
-    sOffs[B] = acc;
-    total[0] = (float)all;
-    ovf = ovf || acc > gcap;
-    overflow[0] = ovf;
-    if (sticky != nullptr && ovf) sticky[0] = true;  // the persistent per-device flag (never cleared here)
+    const bool o = sOvf || carry > gcap;
+    total[0] = (float)sAll;
+    overflow[0] = o;
+    if (sticky != nullptr && o) sticky[0] = true;  // the persistent per-device flag (never cleared here)
   }
-  lds_sync();
+  for (int bb = w; bb < B; bb += nw) {  // one wave per sequence: its valid slots → global rows
+    const int off = sOffs[bb], n = sOffs[bb + 1] - off;
+    for (int j = l; j < n; j += 64) {
+      const int g = off + j;
+      if (g < gcap) {
+        const long long s = (long long)bb * cap + j;
+        gidx[g] = s;
+        glab[g] = lab_b[s];
+      }
+    }
+  }
   const int used = sOffs[B] < gcap ? sOffs[B] : gcap;
-  for (long long s = threadIdx.x; s < (long long)B * cap; s += blockDim.x) {
-    const int b = (int)(s / cap), j = (int)(s - (long long)b * cap);
-    const int n = sOffs[b + 1] - sOffs[b];
-    const int g = sOffs[b] + j;
-    if (j < n && g < gcap) {
-      gidx[g] = s;
-      glab[g] = lab_b[s];
-    }
-  }
   for (int g = used + threadIdx.x; g < gcap; g += blockDim.x) {
     gidx[g] = 0;
     glab[g] = -100;
@@ -543,8 +625,10 @@ __global__ void select_global_kernel(const int* __restrict__ count, int B, int c
 
 void mlm_select_launch(const int64_t* labels, int B, int L, int cap, int gcap, int64_t* idx_b, int64_t* lab_b,
                        int* count, int64_t* gidx, int64_t* glab, float* total, bool* overflow, bool* sticky,
-                       hipStream_t st) {
-  hipLaunchKernelGGL(select_rows_kernel, dim3(B), dim3(256), 0, st, labels, L, cap, idx_b, lab_b, count);
+                       const float* P, int C, float* q, unsigned* ticket, hipStream_t st) {
+  (void)ticket;
+  hipLaunchKernelGGL(select_rows_kernel, dim3(B), dim3(256), cap * sizeof(int), st, labels, L, cap, idx_b, lab_b, count,
+                     P, C, q);
   hipLaunchKernelGGL(select_global_kernel, dim3(1), dim3(1024), (B + 1) * sizeof(int), st, count, B, cap, lab_b, gcap,
                      gidx, glab, total, overflow, sticky);
 }
@@ -561,27 +645,40 @@ static int pick_split(int M, int nchunks, int target) {
 
 int ce_combine_blocks(int M);
 
+// workgroup targets of the three CE launches (PIO_CE_{FWD,DH,DW}_WGS override, for tuning sweeps)
+static int ce_target(const char* name, int dflt) {
+  const char* v = getenv(name);
+  const int t = v ? atoi(v) : 0;
+  return t > 0 ? t : dflt;
+}
+
+// tickets: one zeroed counter (the combine kernel's)
 void ce_fwd_launch(int C, const float* Hm, const int64_t* hidx, const int64_t* labels, const uint16_t* W,
                    const float* bias, int M, int V, float* part_ms, float* picked, float* lse, const float* count,
-                   float* loss, float* blk, unsigned* ticket, uint16_t* hs_out, int nsplit, hipStream_t st) {
+                   float* loss, float* blk, unsigned* tickets, uint16_t* hs_out, int nsplit, float* zero_out,
+                   long long zero_n, hipStream_t st) {
   const int nchunks = (V + VB - 1) / VB;
   const int cps = (nchunks + nsplit - 1) / nsplit;
   dim3 grid((M + HB - 1) / HB, nsplit);
-  if (C == 64) hipLaunchKernelGGL(ce_fwd_kernel<64>, grid, dim3(256), 0, st, Hm, hidx, labels, W, bias, M, V, cps, part_ms, picked, hs_out);
-  else if (C == 128) hipLaunchKernelGGL(ce_fwd_kernel<128>, grid, dim3(256), 0, st, Hm, hidx, labels, W, bias, M, V, cps, part_ms, picked, hs_out);
-  else if (C == 32) hipLaunchKernelGGL(ce_fwd_kernel<32>, grid, dim3(256), 0, st, Hm, hidx, labels, W, bias, M, V, cps, part_ms, picked, hs_out);
-  hipLaunchKernelGGL(ce_combine_kernel, dim3(ce_combine_blocks(M)), dim3(256), 0, st, part_ms, picked, labels, M, nsplit,
-                     lse, count, loss, blk, ticket);
+#define CEF(CC)                                                                                                 \
+  hipLaunchKernelGGL(ce_fwd_kernel<CC>, grid, dim3(256), 0, st, Hm, hidx, labels, W, bias, M, V, cps, part_ms, picked, \
+                     hs_out, zero_out, zero_n / 4)
+  if (C == 64) { CEF(64); }
+  else if (C == 128) { CEF(128); }
+  else if (C == 32) { CEF(32); }
+#undef CEF
+  hipLaunchKernelGGL(ce_combine_kernel, dim3(ce_combine_blocks(M)), dim3(1024), 0, st, part_ms, picked, labels, M, nsplit,
+                     lse, count, loss, blk, tickets);
 }
 
-int ce_combine_blocks(int M) { return (M + 255) / 256; }
+int ce_combine_blocks(int M) { return (M + kCombineRows - 1) / kCombineRows; }
 
-int ce_num_splits(int M, int V) { return pick_split(M, (V + VB - 1) / VB, 2048); }
+int ce_num_splits(int M, int V) { return pick_split(M, (V + VB - 1) / VB, ce_target("PIO_CE_FWD_WGS", 2048)); }
 
 // row splits of the dW kernel (≈ 4 workgroups per CU): the slab height in slab mode
 int ce_dw_splits(int M, int V) {
   const int nchunks = (V + VB - 1) / VB, mtiles = (M + HB - 1) / HB;
-  int rsplit = (1024 + nchunks - 1) / nchunks;
+  int rsplit = (ce_target("PIO_CE_DW_WGS", 1024) + nchunks - 1) / nchunks;
   rsplit = rsplit < 1 ? 1 : (rsplit > mtiles ? mtiles : rsplit);
   const int tps = (mtiles + rsplit - 1) / rsplit;
   return (mtiles + tps - 1) / tps;
@@ -593,7 +690,7 @@ void ce_bwd_launch(int C, const uint16_t* Hm, const int64_t* labels, const uint1
   const int nchunks = (V + VB - 1) / VB;
   // dH partials are added atomically: few splits; deterministic mode: one (a single writer per
   // dH element — every compacted row maps to its own source position)
-  const int nsplit = det ? 1 : pick_split(M, nchunks, 512);
+  const int nsplit = det ? 1 : pick_split(M, nchunks, ce_target("PIO_CE_DH_WGS", 1024));
   const int cps = (nchunks + nsplit - 1) / nsplit;
   // dW: (vocab chunk × row split) workgroups, ≈ 4 per CU; dW / db partials added atomically
   // or stored into the slab

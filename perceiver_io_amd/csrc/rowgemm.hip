@@ -1128,6 +1128,7 @@ __global__ __launch_bounds__(256) void post_attn_bwd_kernel(
     const float* __restrict__ g2, const float* __restrict__ be2, float* __restrict__ dY, uint16_t* __restrict__ dO,
     float* __restrict__ delta, int H, PostAttnGrads gr_out, int R, SlabJob job, DropCfg dr) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[post_attn_bwd_smem<C>()];
+  zero_span_block(job);
   if ((int)blockIdx.x >= (R + 63) / 64) {  // appended workgroups: the previous kernel's slab job
     slab_reduce_block(job, blockIdx.x - (R + 63) / 64, reinterpret_cast<float4*>(smem));
     return;

@@ -266,7 +266,7 @@ def attn_fwd(q, k, v, kmask, H, D, scale, dropout_p, seed, nsplit, site=0):
 
 
 def attn_bwd(q, k, v, kmask, o, dO, lse, delta_in, H, D, scale, dropout_p, seed, dq_out, dk_out, dv_out,
-             kv_accumulate=False, site=0):
+             kv_accumulate=False, site=0, dq_zeroed=False):
     B, qf, kf, vf = _qkv(q, k, v, H, D)
     s = _scores(qf, kf, kmask, scale)
     l2 = lse.permute(0, 2, 1)  # (B, H, Nq)
@@ -347,7 +347,7 @@ def _run_job(job_slab, job_dsts, job_offs):
 
 
 def post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, be2, H, grads, slab=False, job_slab=None, job_dsts=(),
-                  job_offs=(), seed=None, site=0, p=0.0):
+                  job_offs=(), seed=None, site=0, p=0.0, zero_out=None):
     """Returns (dy, dO, delta); parameter grads are ACCUMULATED into
     grads = [dWo, dbo, dg2, dbe2, dW1, db1, dW2, db2] (or stored into slab views)."""
     _run_job(job_slab, job_dsts, job_offs)
@@ -430,7 +430,7 @@ def wgrad(g, a, amode, mean, rstd, lnw, lnb, rows_per_wg, dW, db=None, pe=None, 
         _acc(db, g.float().sum(0))
 
 
-def mlm_select(labels, cap, gcap, sticky=None):
+def mlm_select(labels, cap, gcap, sticky=None, queries=None):
     B, L = labels.shape
     sel = labels != -100
     pos = torch.cumsum(sel.to(torch.int64), 1) - 1
@@ -454,6 +454,8 @@ def mlm_select(labels, cap, gcap, sticky=None):
     ovf = ((count > cap).any() | (n.sum() > gcap)).reshape(1)
     if sticky is not None:
         sticky.logical_or_(ovf.reshape(sticky.shape))
+    if queries is not None:
+        return idx_b, lab_b, gidx, glab, total, ovf, queries.index_select(0, idx_b.reshape(-1)).view(B, cap, -1)
     return idx_b, lab_b, gidx, glab, total, ovf
 
 
@@ -461,9 +463,11 @@ def _ce_rows(h, idx):
     return h if idx is None else h.index_select(0, idx)
 
 
-def ce_fwd(h, idx, labels, w, bias, count):
+def ce_fwd(h, idx, labels, w, bias, count, zero_out=None):
     """→ (mean loss Σ rows / max(count, 1) as a 0-dim tensor, per-row lse); rows of ``h`` are
-    gathered through ``idx`` when given."""
+    gathered through ``idx`` when given; ``zero_out`` (the backward's dH accumulator) is cleared."""
+    if zero_out is not None:
+        zero_out.zero_()
     logits = _bf(_ce_rows(h, idx).float()) @ _bf(w.float()).t() + bias
     lse = torch.logsumexp(logits, -1)
     valid = labels >= 0

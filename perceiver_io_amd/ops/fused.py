@@ -498,6 +498,16 @@ class _LayerFn(torch.autograd.Function):
             return None if g is None else g.view(-1)[a:b]
 
         drop = dict(seed=ctx.seed, p=ctx.p_attn)
+        # the cross-attention backward's dQ accumulator (atomic key-block partials) is cleared by
+        # the post-attention backward kernel on the way (no fill launch on the chain)
+        from . import deterministic
+
+        pe_fused = spec.cross and bool(ctx.kv_entry.get("factored") and PE_ATTN_FUSED and D == 32 and Nq <= 32
+                                       and kmask is None and ctx.p_attn == 0.0 and xkv2.shape[1] <= 4)
+        dq_pre = None
+        if spec.cross and not pe_fused and not deterministic():
+            dq_pre = torch.empty((B, Nq, C), **f32)
+            drop["zero_out"] = dq_pre
         if WGRAD_SLAB and R < TALL_ROWS:
             sl = _GradSlab(R, [C * C, C, C, C, C * C, C, C * C, C], dz2)
             dy, do, delta = K.post_attn_bwd(dz2, y, m2, r2, u, o2, wo, w1, w2, g2, be2, H, sl.targets(), slab=True,
@@ -512,8 +522,6 @@ class _LayerFn(torch.autograd.Function):
             M = kv.shape[0] // B
             kv3 = kv.view(B, M, 2 * C)
             ent = ctx.kv_entry
-            pe_fused = (ent.get("factored") and PE_ATTN_FUSED and D == 32 and Nq <= 32 and kmask is None
-                        and ctx.p_attn == 0.0 and xkv2.shape[1] <= 4)
             if pe_fused:
                 # dK/dV folded into the factored projection's reductions (D, partials), which every
                 # application of this layer accumulates (attention_pe.hip): no dK/dV tensor
@@ -535,7 +543,8 @@ class _LayerFn(torch.autograd.Function):
                     ent["dkv"] = torch.empty((B, M, 2 * C), **f32)
                 dkv = ent["dkv"]
                 dq, _, _ = K.attn_bwd(qx, kv3[:, :, :C], kv3[:, :, C:], kmask, o, do.view(B, Nq, C), lse, delta3, H,
-                                      D, scale, ctx.p_attn, ctx.seed, None, dkv[:, :, :C], dkv[:, :, C:], acc)
+                                      D, scale, ctx.p_attn, ctx.seed, dq_pre, dkv[:, :, :C], dkv[:, :, C:], acc,
+                                      dq_zeroed=dq_pre is not None)
             if Bq == 1 and B > 1 and dq.shape[0] == B:
                 # broadcast latent queries: both batch sums in one deterministic kernel
                 dq2, dres = K.batch_sum2(dq.contiguous(), dy.view(B, Nq, C))

@@ -87,7 +87,10 @@ class _MaskedCE(torch.autograd.Function):
         from .fused import weight_cache
 
         wb = weight_cache.get(weight)  # bf16 shadow written by the fused optimizer
-        loss, lse, hs = ext.ce_fwd(h2, idx, labels_c, wb, bias.contiguous(), cnt)
+        # the backward's dH accumulator (atomic partials) is cleared by the forward kernel
+        dh = torch.empty((h2.shape[0], c), device=h2.device, dtype=torch.float32)
+        loss, lse, hs = ext.ce_fwd(h2, idx, labels_c, wb, bias.contiguous(), cnt, dh)
+        ctx.dh = dh
         ctx.save_for_backward(hs, wb, bias, lse, idx if idx is not None else torch.empty(0, dtype=torch.int64),
                               labels_c, cnt)
         ctx.hshape = h.shape
@@ -108,7 +111,7 @@ class _MaskedCE(torch.autograd.Function):
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
         shp = ctx.hshape
-        dh = torch.zeros((ctx.hrows, shp[-1]), device=hs.device, dtype=torch.float32)
+        dh, ctx.dh = ctx.dh, None
         from . import fused
 
         ix = idx if idx.numel() else None
@@ -203,9 +206,26 @@ def compact_lm_loss(h: torch.Tensor, labels_c: torch.Tensor, count: torch.Tensor
     return F.cross_entropy(logits.float(), lab, ignore_index=-100, reduction="sum") / count.clamp(min=1)
 
 
+def _index_add_grad(p: torch.nn.Parameter, idx: torch.Tensor, g: torch.Tensor):
+    """``p.grad[idx] += g`` straight into the (flat-buffer) gradient: one kernel, no autograd
+    zeros + index_add + AccumulateGrad."""
+    if p.grad is None:
+        p.grad = torch.zeros_like(p)
+    from . import deterministic, use_hip
+
+    if deterministic():
+        p.grad.index_put_((idx,), g.reshape(-1, p.grad.shape[1]).to(p.grad.dtype), accumulate=True)
+    elif use_hip(g) and p.grad.dim() == 2 and p.grad.is_contiguous() and p.grad.shape[1] % 4 == 0:
+        from .fused import kernels
+
+        src = g.reshape(-1, p.grad.shape[1]).to(p.grad.dtype).contiguous()
+        kernels(g).index_add_rows(p.grad, idx.contiguous(), src)
+    else:
+        p.grad.index_add_(0, idx, g.reshape(-1, p.grad.shape[1]).to(p.grad.dtype))
+
+
 class _GatherQueries(torch.autograd.Function):
-    """``param.index_select(0, idx)`` whose backward index-adds straight into ``param.grad``
-    (one kernel; autograd's version is zeros + index_add + AccumulateGrad add)."""
+    """``param.index_select(0, idx)`` whose backward index-adds straight into ``param.grad``."""
 
     @staticmethod
     def forward(ctx, param, idx):
@@ -216,23 +236,32 @@ class _GatherQueries(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         (idx,) = ctx.saved_tensors
-        p = ctx.param
-        if not ctx.needs_input_grad[0]:
-            return None, None
-        if p.grad is None:
-            p.grad = torch.zeros_like(p)
-        from . import deterministic, use_hip
-
-        if deterministic():
-            p.grad.index_put_((idx,), g.to(p.grad.dtype), accumulate=True)
-        elif use_hip(g) and p.grad.dim() == 2 and p.grad.is_contiguous() and p.grad.shape[1] % 4 == 0:
-            from .fused import kernels
-
-            src = g.reshape(-1, p.grad.shape[1]).to(p.grad.dtype).contiguous()
-            kernels(g).index_add_rows(p.grad, idx.contiguous(), src)
-        else:
-            p.grad.index_add_(0, idx, g.to(p.grad.dtype))
+        if ctx.needs_input_grad[0]:
+            _index_add_grad(ctx.param, idx, g)
         return None, None
+
+
+class _SelectQueries(torch.autograd.Function):
+    """HIP path: one kernel selects the masked positions (per-sequence slots + global
+    compaction) and gathers their output queries ``q = param[idx]`` (B, cap, C); the backward
+    index-adds dq into ``param.grad``.  → q, idx (B, cap), gidx, glab, total, overflow."""
+
+    @staticmethod
+    def forward(ctx, param, labels, cap, gcap, sticky):
+        idx, _, gidx, glab, total, ovf, q = ext.require().mlm_select(labels.contiguous(), cap, gcap, sticky,
+                                                                     param.detach().contiguous())
+        ctx.save_for_backward(idx)
+        ctx.param = param
+        ctx.mark_non_differentiable(idx, gidx, glab, total, ovf)
+        ctx.set_materialize_grads(False)  # no zero-filled gradients for the index outputs
+        return q, idx, gidx, glab, total, ovf
+
+    @staticmethod
+    def backward(ctx, g, *_):
+        (idx,) = ctx.saved_tensors
+        if g is not None and ctx.needs_input_grad[0]:
+            _index_add_grad(ctx.param, idx.reshape(-1), g)
+        return None, None, None, None, None
 
 
 def masked_decode_loss(decoder, x_latent: torch.Tensor, labels: torch.Tensor, p: float = 0.15):
@@ -255,11 +284,10 @@ def masked_decode_loss(decoder, x_latent: torch.Tensor, labels: torch.Tensor, p:
     cap = row_capacity(L, p)
     if use_hip(x_latent) and lin.weight.shape[1] in (32, 64, 128):
         # the kernel ORs the overflow into the persistent per-device flag itself
-        idx, _, gidx, glab, total, ovf = ext.require().mlm_select(labels.contiguous(), cap, capacity(B * L, p),
-                                                                  overflow_flag(labels.device).view(1))
+        q, idx, gidx, glab, total, ovf = _SelectQueries.apply(decoder.output, labels, cap, capacity(B * L, p),
+                                                              overflow_flag(labels.device).view(1))
         global _overflow
         _overflow = ovf
-        q = _GatherQueries.apply(decoder.output, idx.reshape(-1)).view(B, cap, -1)
         h = decoder.cross_attention(q, x_latent)
         return _MaskedCE.apply(h, lin.weight, lin.bias, gidx, glab, total)
     idx, labels_c, count = compact_per_row(labels, cap)

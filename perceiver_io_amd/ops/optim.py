@@ -177,11 +177,15 @@ class FusedAdamW(torch.optim.Optimizer):
         self.grad_scale = 1.0
 
     # -- the update ---------------------------------------------------------------------
-    def stage_hyper(self):
-        """Write lr / step / betas for the NEXT update into device memory (outside any graph)."""
+    def hyper_values(self):
+        """lr / step / betas of the NEXT update, in ``self.hyper``'s layout."""
         g = self.param_groups[0]
         b1, b2 = g["betas"]
-        vals = [g["lr"], self._step + 1, 0.0, b1, b2, 0.0, 0.0, 0.0]
+        return [float(g["lr"]), float(self._step + 1), 0.0, float(b1), float(b2), 0.0, 0.0, 0.0]
+
+    def stage_hyper(self):
+        """Write lr / step / betas for the NEXT update into device memory (outside any graph)."""
+        vals = self.hyper_values()
         if self._ring is not None:
             self._ring.push(vals, self.hyper)
         else:
