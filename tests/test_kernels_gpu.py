@@ -335,6 +335,76 @@ def test_mlm_select(B, L, cap, gcap, p):
     b = _emu().mlm_select(lab, cap, gcap)
     for x, y, n in zip(a, b, ("idx_b", "lab_b", "gidx", "glab", "total", "overflow")):
         assert torch.equal(x.cpu(), y.cpu()), n
+    # with the output-query gather folded in: q = queries[idx_b] (exact copy), same selection
+    queries = torch.randn(L + 3, 64, device=DEV)
+    aq = _ext().mlm_select(lab, cap, gcap, None, queries)
+    bq = _emu().mlm_select(lab, cap, gcap, None, queries)
+    for x, y, n in zip(aq, bq, ("idx_b", "lab_b", "gidx", "glab", "total", "overflow", "q")):
+        assert torch.equal(x.cpu(), y.cpu()), n + " (with queries)"
+
+
+def test_stage_step_copies_and_hyper():
+    """One launch copies every (dst, src) pair — 16-byte and odd sizes / offsets — and writes the
+    hyper-parameter values given as kernel arguments."""
+    torch.manual_seed(9)
+    base = torch.randint(0, 1 << 30, (1001,), device=DEV)
+    srcs = [torch.randint(0, 9000, (64, 512), device=DEV), torch.rand(64, 512, device=DEV) > 0.5,
+            torch.randn(33, device=DEV), base[3:700], torch.rand(7, device=DEV) > 0.3]
+    dsts = [torch.empty_like(t) for t in srcs]
+    hyper = torch.full((8,), -1.0, device=DEV)
+    vals = [3e-3, 17.0, 0.0, 0.9, 0.999, 0.0, 0.0, 0.0]
+    _ext().stage_step(dsts, srcs, hyper, vals)
+    for d, t in zip(dsts, srcs):
+        assert torch.equal(d, t)
+    assert torch.equal(hyper.cpu(), torch.tensor(vals, dtype=torch.float32))
+    _ext().stage_step([], [], hyper, [1.0, 2.0])  # hyper only
+    assert hyper[:2].tolist() == [1.0, 2.0] and hyper[2].item() == 0.0
+
+
+def test_side_zero_spans():
+    """ce_fwd and post_attn_bwd clear the NEXT kernel's accumulator on the way (zero_out);
+    attn_bwd with dq_zeroed then matches its own-fill path."""
+    torch.manual_seed(10)
+    M, V, C = 300, 1000, 64
+    h = torch.randn(M, C, device=DEV)
+    w = bf(torch.randn(V, C, device=DEV) * 0.05)
+    bias = torch.randn(V, device=DEV) * 0.01
+    lab = torch.randint(0, V, (M,), device=DEV)
+    cnt = torch.tensor([float(M)], device=DEV)
+    z = torch.full((4 * M + 12, C), float("nan"), device=DEV)
+    ref = _ext().ce_fwd(h, None, lab, w, bias, cnt)
+    out = _ext().ce_fwd(h, None, lab, w, bias, cnt, z)
+    assert torch.equal(z, torch.zeros_like(z))
+    for x, y in zip(out, ref):
+        assert torch.equal(x, y)
+    # post_attn_bwd clears the cross-attention dQ buffer; attn_bwd adds into it without a fill
+    B, Nq, Nk, H, D = 4, 64, 600, 4, 16
+    R = B * Nq
+    E = H * D
+    q, k, v, km = _attn_inputs(B, B, Nq, Nk, H, D)
+    scale = 1.0 / math.sqrt(D)
+    o1, l1 = _ext().attn_fwd(q, k, v, km, H, D, scale, 0.0, None, 1)
+    do = bf(torch.randn(B, Nq, E, device=DEV))
+    g_ref = _ext().attn_bwd(q, k, v, km, o1, do, l1, None, H, D, scale, 0.0, None, None, None, None)
+    ws = [bf(torch.randn(E, E, device=DEV) / 8) for _ in range(3)]
+    y = torch.randn(R, E, device=DEV)
+    m, r = torch.randn(R, device=DEV), torch.rand(R, device=DEV) + 0.5
+    u = bf(torch.randn(R, E, device=DEV))
+    g2, be2 = torch.randn(E, device=DEV), torch.randn(E, device=DEV)
+    dz = torch.randn(R, E, device=DEV)
+    names = ("dWo", "dbo", "dg2", "dbe2", "dW1", "db1", "dW2", "db2")
+    outs = []
+    dq = torch.full((B, Nq, E), float("nan"), device=DEV)
+    for zo in (None, dq):
+        grads = [torch.zeros((E, E) if n.startswith("dW") else (E,), device=DEV) for n in names]
+        outs.append(_ext().post_attn_bwd(dz, y, m, r, u, o1.view(R, E), ws[0], ws[1], ws[2], g2, be2, H, grads,
+                                         zero_out=zo))
+    assert torch.equal(dq, torch.zeros_like(dq))
+    for a_, b_ in zip(*outs):
+        assert torch.equal(a_, b_)
+    g_pre = _ext().attn_bwd(q, k, v, km, o1, do, l1, None, H, D, scale, 0.0, None, dq, None, None, dq_zeroed=True)
+    for a_, b_, n in zip(g_pre, g_ref, ("dq", "dk", "dv")):
+        close(a_, b_, 1e-5, n + " (pre-zeroed dq)")
 
 
 @pytest.mark.parametrize("R,M,npix,kin,tall", [(6 * 100, 100, 3, 133, False), (2 * 70000, 70000, 1, 131, True)])
