@@ -28,9 +28,14 @@ Gradients (Megatron-style conjugate pairs, one per cross-attention):
 Fully masked rows (every key of every shard PAD) give 0, as in the single-GPU kernels
 (defect D10).
 
-This path runs the attention math in PyTorch ops on each shard (RCCL ``all_reduce`` over
-xGMI between them); dropout must be 0 (replicated computations would otherwise draw
-different masks per rank).
+On a GPU the shard-local attention runs on the flash-attention kernels (``csrc/attention.hip``,
+no score matrix in memory): the forward kernel returns the shard's normalised output and its
+log-sum-exp; the ranks merge them with one all-reduce MAX of the LSE and one all-reduce SUM of
+``[w_r·O_r ‖ w_r]`` (``w_r = 2^(lse_r − max)``), which also gives the global LSE.  The backward
+kernel, fed the GLOBAL output and LSE, yields this shard's exact dK/dV and a partial dQ (summed
+by the replicated-input identity).  ``impl="torch"`` (the CPU default) keeps the plain fp32
+PyTorch math.  Dropout must be 0 (replicated computations would otherwise draw different masks
+per rank).
 """
 from __future__ import annotations
 
@@ -104,9 +109,67 @@ class _ShardGradScale(torch.autograd.Function):
         return g * ctx.world, None
 
 
-def cp_cross_attention(attn, x_q: torch.Tensor, x_kv: torch.Tensor, pad_mask: Optional[torch.Tensor], group=None):
+class _ShardFlashAttention(torch.autograd.Function):
+    """Shard-local flash attention merged over ``group`` (module doc): q (B, N, E) replicated,
+    k / v (B, M_local, E) this rank's keys → the exact full-sequence output (B, N, E) fp32."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, kmask, H, D, scale, group):
+        from ..ops.fused import kernels
+
+        K = kernels(q)
+        B, N, E = q.shape
+        qb, kb, vb = (t.to(torch.bfloat16).contiguous() for t in (q, k, v))
+        km = kmask.to(torch.bool).contiguous() if kmask is not None else None
+        if k.shape[1] > 0:
+            o_r, l2 = K.attn_fwd(qb, kb, vb, km, H, D, scale, 0.0, None, 1)  # lse in log2 units, +inf: no key
+            l2 = torch.where(torch.isfinite(l2), l2, torch.full_like(l2, float("-inf")))
+            o_r = o_r.float().view(B, N, H, D)
+        else:  # an empty shard contributes nothing
+            l2 = torch.full((B, N, H), float("-inf"), device=q.device)
+            o_r = torch.zeros((B, N, H, D), device=q.device)
+        m = l2.clone()
+        if _group_size(group) > 1:
+            dist.all_reduce(m, op=dist.ReduceOp.MAX, group=group)
+        m = torch.where(torch.isfinite(m), m, torch.zeros_like(m))
+        w = torch.exp2(l2 - m)  # (B, N, H); 0 for a shard without live keys
+        packed = torch.cat([o_r * w[..., None], w[..., None]], dim=-1)
+        if _group_size(group) > 1:
+            dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
+        S = packed[..., D]
+        o = torch.where(S[..., None] > 0, packed[..., :D] / S.clamp_min(1e-30)[..., None], torch.zeros_like(o_r))
+        lse = torch.where(S > 0, m + torch.log2(S.clamp_min(1e-30)), torch.full_like(S, float("inf")))
+        o = o.reshape(B, N, E)
+        ob = o.to(torch.bfloat16).contiguous()
+        ctx.save_for_backward(qb, kb, vb, ob, lse.contiguous(), km if km is not None else torch.empty(0))
+        ctx.cfg = (H, D, scale, km is not None)
+        return o
+
+    @staticmethod
+    def backward(ctx, g):
+        from ..ops.fused import kernels
+
+        qb, kb, vb, ob, lse, km = ctx.saved_tensors
+        H, D, scale, has_mask = ctx.cfg
+        if kb.shape[1] == 0:
+            return torch.zeros_like(g), torch.zeros(kb.shape, device=g.device), torch.zeros(vb.shape, device=g.device), \
+                None, None, None, None, None
+        dq, dk, dv = kernels(g).attn_bwd(qb, kb, vb, km if has_mask else None, ob, g.to(torch.bfloat16).contiguous(), lse,
+                                         None, H, D, scale, 0.0, None, None, None, None)
+        return dq, dk, dv, None, None, None, None, None
+
+
+def _default_impl(t: torch.Tensor) -> str:
+    from .. import ops
+
+    return "kernel" if ops.use_hip(t) else "torch"
+
+
+def cp_cross_attention(attn, x_q: torch.Tensor, x_kv: torch.Tensor, pad_mask: Optional[torch.Tensor], group=None,
+                       impl: Optional[str] = None):
     """``CrossAttention`` (q_norm / kv_norm / MHA, ``perceiver/model.py:77-99``) over this
-    rank's K/V shard, combined over ``group`` into the exact full-sequence output."""
+    rank's K/V shard, combined over ``group`` into the exact full-sequence output.
+    ``impl``: "kernel" (flash-attention kernels; the default on a GPU) or "torch"."""
     a = attn.attention.attention  # MHAParams (nn.MultiheadAttention layout)
     e, h = a.embed_dim, a.num_heads
     d = e // h
@@ -114,6 +177,10 @@ def cp_cross_attention(attn, x_q: torch.Tensor, x_kv: torch.Tensor, pad_mask: Op
     q = _ReplicatedIn.apply(F.linear(attn.q_norm(x_q), a.q_weight(), a.in_proj_bias[:e]), group)
     kv = _ShardGradScale.apply(F.linear(attn.kv_norm(x_kv), a.kv_weight(), a.in_proj_bias[e:]), world)
     k, v = kv.split(e, dim=-1)
+    if (impl or _default_impl(x_q)) == "kernel" and d in (16, 32, 64, 128):
+        qc = q.contiguous() if q.stride(-1) == 1 and q.shape[0] == k.shape[0] else q.expand(k.shape[0], -1, -1).contiguous()
+        o = _ShardFlashAttention.apply(qc, k, v, pad_mask, h, d, 1.0 / math.sqrt(d), group)
+        return F.linear(o.to(x_q.dtype), a.out_proj.weight, a.out_proj.bias)
     B, N, _ = q.shape
     M = k.shape[1]
     q = q.view(B, N, h, d).transpose(1, 2) * (1.0 / math.sqrt(d))
@@ -136,10 +203,10 @@ def cp_cross_attention(attn, x_q: torch.Tensor, x_kv: torch.Tensor, pad_mask: Op
     return F.linear(o, a.out_proj.weight, a.out_proj.bias)
 
 
-def cp_cross_attention_layer(layer, x_q, x_kv, pad_mask, group=None):
+def cp_cross_attention_layer(layer, x_q, x_kv, pad_mask, group=None, impl=None):
     """``Residual(CrossAttention)`` then ``Residual(mlp)`` (``perceiver/model.py:29-33``)."""
     att_res, mlp_res = layer[0], layer[1]
-    y = att_res.dropout(cp_cross_attention(att_res.module, x_q, x_kv, pad_mask, group)) + x_q
+    y = att_res.dropout(cp_cross_attention(att_res.module, x_q, x_kv, pad_mask, group, impl)) + x_q
     return mlp_res.dropout(mlp_res.module(y)) + y
 
 
@@ -164,10 +231,11 @@ class ContextParallelEncoder(nn.Module):
     ``group`` (default: the whole world).  Same parameters (it wraps, not copies, the encoder),
     same return value ``(x_latent, pad_mask)`` — the latent output is replicated on every rank."""
 
-    def __init__(self, encoder, group=None):
+    def __init__(self, encoder, group=None, impl: Optional[str] = None):
         super().__init__()
         self.encoder = encoder
         self.group = group
+        self.impl = impl  # "kernel" / "torch" / None (kernel on a GPU)
 
     def shard(self, m: int) -> Tuple[int, int]:
         return shard_range(m, _group_rank(self.group), _group_size(self.group))
@@ -184,7 +252,7 @@ class ContextParallelEncoder(nn.Module):
         x_latent = enc.latent.unsqueeze(0).expand(b, -1, -1)
         for layer in enc.layers():
             cross, block = layer[0], layer[1]
-            x_latent = cp_cross_attention_layer(cross, x_latent, x_kv, pm, self.group)
+            x_latent = cp_cross_attention_layer(cross, x_latent, x_kv, pm, self.group, self.impl)
             x_latent = block(x_latent)
         return x_latent, pad_mask
 

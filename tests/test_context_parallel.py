@@ -41,7 +41,7 @@ def _inputs(kind):
     return torch.randn(3, 6, 5, 2, generator=g), None
 
 
-def _worker(rank, world, port, kind, out):
+def _worker(rank, world, port, kind, out, impl="torch"):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
 
@@ -59,7 +59,7 @@ def _worker(rank, world, port, kind, out):
     ref_grads = {n: p.grad.clone() for n, p in enc.named_parameters() if p.grad is not None}
     enc.zero_grad(set_to_none=True)
     # context parallel: this rank's input shard, then the data-parallel gradient average
-    lat, _ = ContextParallelEncoder(enc)(x, pad)
+    lat, _ = ContextParallelEncoder(enc, impl=impl)(x, pad)
     (lat * w).sum().backward()
     err_g = 0.0
     for n, p in enc.named_parameters():
@@ -81,6 +81,19 @@ def test_context_parallel_encoder_matches_full(kind, world):
         err_out, err_g, _, same_params = out[r]
         assert err_out < 1e-5, (r, err_out)
         assert err_g < 1e-4, (r, err_g)
+        assert same_params
+
+
+@pytest.mark.parametrize("kind,world", [("text", 3), ("image", 2)])
+def test_context_parallel_flash_merge_matches_full(kind, world):
+    """The kernel implementation (shard-local flash attention + LSE merge; the CPU runs the
+    kernels' emulation, bf16 operands) against the fp32 single-process encoder."""
+    out = mp.Manager().dict()
+    mp.spawn(_worker, args=(world, _port(), kind, out, "kernel"), nprocs=world, join=True)
+    for r in range(world):
+        err_out, err_g, dead, same_params = out[r]
+        assert err_out < 3e-2, (r, err_out)
+        assert err_g < 5e-2, (r, err_g)
         assert same_params
 
 
@@ -108,12 +121,23 @@ def _worker_gpu(rank, world, port, out):
     x, pad = (t.to(dev) for t in _inputs("text"))
     w = torch.randn(3, 8, 32, generator=torch.Generator().manual_seed(9)).to(dev)
     ref, _ = enc(x, pad)  # fused HIP encoder on the full input
-    lat, _ = ContextParallelEncoder(enc)(x, pad)  # CP cross-attention + fused HIP self-attention blocks
+    (ref * w).sum().backward()
+    def flat_grads():
+        return torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1).clone()
+                          for p in enc.parameters()])
+
+    ref_g = flat_grads()
+    enc.zero_grad(set_to_none=False)
+    # CP cross-attention on the flash kernels (shard-local attention + LSE merge) + fused HIP
+    # self-attention blocks
+    lat, _ = ContextParallelEncoder(enc)(x, pad)
     (lat * w).sum().backward()
-    g = torch.cat([p.grad.reshape(-1) for p in enc.parameters() if p.grad is not None])
+    g = flat_grads()
     dist.all_reduce(g)
+    g /= 2
     torch.cuda.synchronize()
-    out[rank] = ((lat - ref).abs().max().item() / ref.abs().max().item(), bool(torch.isfinite(g).all().item()))
+    out[rank] = ((lat - ref).abs().max().item() / ref.abs().max().item(), bool(torch.isfinite(g).all().item()),
+                 ((g - ref_g).norm() / ref_g.norm()).item())
     dist.destroy_process_group()
 
 
@@ -122,5 +146,6 @@ def test_context_parallel_encoder_gpu_two_ranks():
     out = mp.Manager().dict()
     mp.spawn(_worker_gpu, args=(2, _port(), out), nprocs=2, join=True)
     for r in range(2):
-        rel, finite = out[r]
+        rel, finite, grel = out[r]
         assert rel < 3e-2 and finite, (r, rel)
+        assert grel < 3e-2, (r, grel)
