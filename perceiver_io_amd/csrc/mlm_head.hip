@@ -494,6 +494,227 @@ __global__ __launch_bounds__(256) void ce_bwd_dw_kernel(const uint16_t* __restri
   }
 }
 
+
+// ---- register-operand variants (default): the dl tile never goes through LDS -------------
+// The logits tile's accumulator is used directly as an MFMA operand (pack_acc: the 16 values of
+// a lane in the accumulator's permuted row order, matched by a frag_ks_perm read of the other
+// operand), so a chunk costs two workgroup barriers instead of three and no dl store / reload.
+// Each wave owns a (32-row, 32-vocab) quarter of the 64 × 64 tile; the two waves that share an
+// output block add their partials once, through LDS, at the end.
+__device__ __forceinline__ bf16x8 pack_regs(const float (&d)[16], int s) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (short)f2bf(d[8 * s + j]);
+  return r;
+}
+// owner wave parity of output tile t when two waves hold partials of it
+template <int NT>
+__device__ __forceinline__ int tile_owner(int t) { return NT == 1 ? 0 : (t & 1); }
+
+// bwd-a: dH[r][c] += Σ_v dl[r][v] W[v][c]; wave w: rows 32(w >> 1) + [0, 32), vocab 32(w & 1) + [0, 32)
+// of each chunk (the transposed logits tile: a lane holds one row), partial over its vocab half
+template <int C>
+__global__ __launch_bounds__(256) void ce_bwd_dh_reg_kernel(const uint16_t* __restrict__ Hm,
+                                                            const int64_t* __restrict__ labels,
+                                                            const uint16_t* __restrict__ W, const float* __restrict__ bias,
+                                                            const float* __restrict__ lse, const float* __restrict__ gout,
+                                                            const float* __restrict__ count, int M, int V,
+                                                            int chunks_per_split, float* __restrict__ dH,
+                                                            const int64_t* __restrict__ rowmap, long long dh_rows) {
+  constexpr int LD = C + 8, NT = C / 32;
+  __shared__ __attribute__((aligned(16))) uint16_t sH[HB * LD];
+  __shared__ __attribute__((aligned(16))) uint16_t sW[VB * LD];
+  __shared__ __attribute__((aligned(16))) float sB[VB];
+  __shared__ __attribute__((aligned(16))) float sX[2][NT][16 * 64];
+  __shared__ long long sDst[HB];  // dH row of each tile row (-1: ignored row)
+  const int w = wave_id(), l = lane_id(), hh = l >> 5;
+  const int m0 = blockIdx.x * HB, split = blockIdx.y;
+  const int nchunks = (V + VB - 1) / VB;
+  const int c_begin = split * chunks_per_split, c_end = min(nchunks, c_begin + chunks_per_split);
+  stage_rows<C>(sH, LD, Hm, m0, M);
+  if (threadIdx.x < HB) {
+    const int gr = m0 + threadIdx.x;
+    const long long r = (gr < M && labels[gr] >= 0) ? (rowmap ? rowmap[gr] : gr) : -1;
+    sDst[threadIdx.x] = r < dh_rows ? r : -1;  // a row outside dH is dropped, never written
+  }
+  const int rl = 32 * (w >> 1) + (l & 31), gr = m0 + rl;
+  const int lab = gr < M ? (int)labels[gr] : -100;
+  const float lse_l2 = gr < M ? lse[gr] * kL2E : 0.f;
+  const float g = lab >= 0 ? gout[0] / fmaxf(count[0], 1.f) : 0.f;  // d(mean loss) / d(row loss)
+  f32x16 acc_o[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc_o[t] = f32x16{};
+  bf16x8 wr[C / 32];
+  float bnext = 0.f;
+  auto fetch = [&](int c) {
+    fetch_rows<C>(wr, W, c * VB, V);
+    const int v = c * VB + threadIdx.x;
+    if (threadIdx.x < VB) bnext = v < V ? bias[v] * kL2E : -__builtin_inff();
+  };
+  if (c_begin < c_end) fetch(c_begin);
+  for (int c = c_begin; c < c_end; ++c) {
+    const int v0 = c * VB;
+    lds_sync();
+    store_rows<C>(wr, sW, LD);
+    if (threadIdx.x < VB) sB[threadIdx.x] = bnext;
+    lds_sync();
+    if (c + 1 < c_end) fetch(c + 1);
+    const f32x16 acc = logits_tile_t<C>(sH, sW, LD);
+    float b[16], d[16];
+    vocab_regs(sB, b);
+    dl_regs(acc, b, lse_l2, g, vocab_reg(lab - v0 - 32 * (w & 1)), d);
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      const bf16x8 pa = pack_regs(d, ss);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc_o[t] = mfma32(pa, frag_ks_perm(sW, LD, 32 * t, 32 * (w & 1) + 16 * ss), acc_o[t]);
+    }
+  }
+  // the two vocab halves of each row block: the non-owner hands its partial over
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+    if ((w & 1) != tile_owner<NT>(t)) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sX[w >> 1][t][i * 64 + l] = acc_o[t][i];
+    }
+  lds_sync();  // also publishes sDst (no in-loop barrier has run for an empty split)
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    if ((w & 1) != tile_owner<NT>(t)) continue;
+    const int r0 = 32 * (w >> 1), n0 = 32 * t;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      // dH row: the compacted row's source position (rowmap) or the row itself; ignored rows
+      // (label -100, incl. compaction padding) carry no gradient
+      const long long dst = sDst[r0 + acc_row(i, hh)];
+      if (dst >= 0) atomicAdd(dH + dst * C + n0 + (l & 31), acc_o[t][i] + sX[w >> 1][t][i * 64 + l]);
+    }
+  }
+}
+
+// bwd-b: dW[v][c] += Σ_r dl[r][v] H[r][c], db[v] += Σ_r dl[r][v]; grid (vocab chunk, row split).
+// The logits tile is NOT transposed here (a lane holds one vocab entry), so dl feeds the dW
+// product as its A operand directly; wave w: rows 32(w >> 1), vocab 32(w & 1), partial over its
+// row half.  H tiles (+ their LSE / labels) are register-prefetched one tile ahead.
+template <int C>
+__global__ __launch_bounds__(256) void ce_bwd_dw_reg_kernel(const uint16_t* __restrict__ Hm,
+                                                            const int64_t* __restrict__ labels,
+                                                            const uint16_t* __restrict__ W, const float* __restrict__ bias,
+                                                            const float* __restrict__ lse, const float* __restrict__ gout,
+                                                            const float* __restrict__ count, int M, int V,
+                                                            int tiles_per_split, float* __restrict__ dW,
+                                                            float* __restrict__ db, float* __restrict__ slab) {
+  constexpr int LD = C + 8, NT = C / 32;
+  __shared__ __attribute__((aligned(16))) uint16_t sH[HB * LD];
+  __shared__ __attribute__((aligned(16))) uint16_t sW[VB * LD];
+  __shared__ __attribute__((aligned(16))) float sLse[HB];
+  __shared__ __attribute__((aligned(16))) float sG[HB];    // row-loss gradient (0: ignored row)
+  __shared__ __attribute__((aligned(16))) int sLab[HB];
+  __shared__ __attribute__((aligned(16))) float sX[2][NT][16 * 64];
+  __shared__ float sBs[2][64];
+  const int w = wave_id(), l = lane_id(), hh = l >> 5;
+  const int v0 = blockIdx.x * VB;
+  const int mt_begin = blockIdx.y * tiles_per_split;
+  const int mt_end = min((M + HB - 1) / HB, mt_begin + tiles_per_split);
+  const float gs = gout[0] / fmaxf(count[0], 1.f);
+  stage_rows<C>(sW, LD, W, v0, V);
+  const int vl = 32 * (w & 1) + (l & 31), vg = v0 + vl;  // this lane's vocab entry
+  const float bl2 = vg < V ? bias[vg] * kL2E : -__builtin_inff();
+  const int r0 = 32 * (w >> 1);
+  f32x16 acc_o[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc_o[t] = f32x16{};
+  float bsum = 0.f;
+  bf16x8 hr[C / 32];
+  float aux = 0.f;  // threads [0,64): LSE * log2e of row tid, [64,128): label of row tid-64
+  auto fetch = [&](int mt) {
+    fetch_rows<C>(hr, Hm, mt * HB, M);
+    const int t = threadIdx.x & 63, gr = mt * HB + t;
+    if (threadIdx.x < 64) aux = gr < M ? lse[gr] * kL2E : 0.f;
+    else if (threadIdx.x < 128) aux = __int_as_float(gr < M ? (int)labels[gr] : -100);
+  };
+  if (mt_begin < mt_end) fetch(mt_begin);
+  for (int mt = mt_begin; mt < mt_end; ++mt) {
+    lds_sync();
+    store_rows<C>(hr, sH, LD);
+    if (threadIdx.x < 64) {
+      sLse[threadIdx.x] = aux;
+    } else if (threadIdx.x < 128) {
+      const int lb = __float_as_int(aux);
+      sLab[threadIdx.x - 64] = lb;
+      sG[threadIdx.x - 64] = lb >= 0 ? gs : 0.f;
+    }
+    lds_sync();
+    if (mt + 1 < mt_end) fetch(mt + 1);
+    f32x16 acc = f32x16{};
+#pragma unroll
+    for (int k0 = 0; k0 < C; k0 += 16) acc = mfma32(frag_kc(sH, LD, r0, k0), frag_kc(sW, LD, 32 * (w & 1), k0), acc);
+    float d[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // rows r0 + 4hh + 8q + (0..3): four consecutive LDS entries
+      const int rr = r0 + 4 * hh + 8 * q;
+      const float4 ls = *reinterpret_cast<const float4*>(sLse + rr);
+      const float4 gg = *reinterpret_cast<const float4*>(sG + rr);
+      const int4 lb = *reinterpret_cast<const int4*>(sLab + rr);
+      const float lsv[4] = {ls.x, ls.y, ls.z, ls.w}, ggv[4] = {gg.x, gg.y, gg.z, gg.w};
+      const int lbv[4] = {lb.x, lb.y, lb.z, lb.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = 4 * q + j;
+        const float p = fast_exp2(fmaf(acc[i], kL2E, bl2 - lsv[j])) * ggv[j];
+        d[i] = lbv[j] == vg ? p - ggv[j] : p;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) bsum += d[i];
+    // dW (vocab 32(w & 1) + [0, 32) × C) += dlᵀ · H over this wave's 32 rows
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      const bf16x8 pa = pack_regs(d, ss);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc_o[t] = mfma32(pa, frag_ks_perm(sH, LD, 32 * t, r0 + 16 * ss), acc_o[t]);
+    }
+  }
+  // bias: the lane's vocab entry summed over its 16 rows, then the other lane half, then the
+  // other row-half wave
+  bsum = xor32_sum(bsum);
+  if (l < 32) sBs[w >> 1][vl] = bsum;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+    if ((w >> 1) != tile_owner<NT>(t)) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sX[w & 1][t][i * 64 + l] = acc_o[t][i];
+    }
+  lds_sync();
+  // partials: atomics into dW / db, or (slab) plain stores into row blockIdx.y of a
+  // (row splits, V·C + V₄) slab that a SlabJob later sums into dW | db (common.h)
+  float* dWp = dW;
+  float* dbp = db;
+  if (slab) {
+    dWp = slab + (long long)blockIdx.y * ((long long)V * C + ((V + 3) & ~3));
+    dbp = dWp + (long long)V * C;
+  }
+  if (threadIdx.x < 64 && v0 + threadIdx.x < V) {
+    const float v = sBs[0][threadIdx.x] + sBs[1][threadIdx.x];
+    if (slab) dbp[v0 + threadIdx.x] = v;
+    else atomicAdd(dbp + v0 + threadIdx.x, v);
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    if ((w >> 1) != tile_owner<NT>(t)) continue;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int vv = v0 + 32 * (w & 1) + acc_row(i, hh);
+      float* p = dWp + (long long)vv * C + 32 * t + (l & 31);
+      const float x = acc_o[t][i] + sX[w & 1][t][i * 64 + l];
+      if (vv < V) {
+        if (slab) *p = x;
+        else atomicAdd(p, x);
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // selected-position bookkeeping for the MLM loss (replaces ~15 small framework kernels)
 //   rows  : per sequence b, slots [0, cap): positions of labels != -100 in order (unused
@@ -702,12 +923,20 @@ void ce_bwd_launch(int C, const uint16_t* Hm, const int64_t* labels, const uint1
     (void)hipMemsetAsync(db, 0, sizeof(float) * (size_t)V, st);
   }
   dim3 ga((M + HB - 1) / HB, nsplit), gb(nchunks, rsplit);
+  // PIO_CE_BWD_LDS=1: the variants that pass the dl tile through LDS (A/B reference)
+  static const bool lds_dl = [] { const char* v = getenv("PIO_CE_BWD_LDS"); return v && v[0] == '1'; }();
 #define CEB(CC)                                                                                                  \
-  hipLaunchKernelGGL(ce_bwd_dh_kernel<CC>, ga, dim3(256), 0, st, Hm, labels, W, bias, lse, gout, count, M, V, cps, dH, \
-                     rowmap, dh_rows);                                                                           \
-  hipLaunchKernelGGL(ce_bwd_dw_kernel<CC>, gb, dim3(256), 0, st, Hm, labels, W, bias, lse, gout, count, M, V, tps, \
-                     dW, db,                                                                                     \
-                     slab)
+  if (lds_dl) {                                                                                                  \
+    hipLaunchKernelGGL(ce_bwd_dh_kernel<CC>, ga, dim3(256), 0, st, Hm, labels, W, bias, lse, gout, count, M, V, cps, \
+                       dH, rowmap, dh_rows);                                                                     \
+    hipLaunchKernelGGL(ce_bwd_dw_kernel<CC>, gb, dim3(256), 0, st, Hm, labels, W, bias, lse, gout, count, M, V, tps, \
+                       dW, db, slab);                                                                            \
+  } else {                                                                                                       \
+    hipLaunchKernelGGL(ce_bwd_dh_reg_kernel<CC>, ga, dim3(256), 0, st, Hm, labels, W, bias, lse, gout, count, M, V, \
+                       cps, dH, rowmap, dh_rows);                                                                \
+    hipLaunchKernelGGL(ce_bwd_dw_reg_kernel<CC>, gb, dim3(256), 0, st, Hm, labels, W, bias, lse, gout, count, M, V, \
+                       tps, dW, db, slab);                                                                       \
+  }
   if (C == 64) { CEB(64); }
   else if (C == 128) { CEB(128); }
   else if (C == 32) { CEB(32); }
