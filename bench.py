@@ -332,7 +332,10 @@ def main(argv=None):
             "data": "synthetic (random inputs of the config's shape, random-init weights)",
             "config": {"model": desc, "global_batch": B * world, "seq_len": args.seq_len,
                        "parallelism": f"dp{world}", "backend": args.backend,
-                       "graph": bool(fused and not args.no_graph), "name": args.config},
+                       "graph": bool(fused and not args.no_graph), "name": args.config,
+                       "dist_backend": info.backend if world > 1 else None,
+                       "allreduce_in_graph": bool(reducer is not None and getattr(reducer, "in_graph", False)),
+                       "allreduce_overlap": bool(reducer is not None and reducer.overlap_ready())},
             "final_loss": round(final_loss, 4),
         }
         print(json.dumps(out), flush=True)
