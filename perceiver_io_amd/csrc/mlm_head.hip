@@ -220,26 +220,24 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ H
   }
 }
 
-// per-row lse (kept for backward) and loss = lse − picked (0 for ignored rows), four threads per
-// row (splits q, q + 4, … merged online, then across the four); the mean loss Σ rows /
-// max(count, 1) is finalised in-kernel: each workgroup stores its partial sum, and the last one
-// to take a ticket adds the partials in a fixed order (deterministic) and resets the ticket.
-// (picked[r] is written by the forward for every row with a label, so it needs no zero fill.)
-constexpr int kCombineRows = 256;
-__global__ __launch_bounds__(1024) void ce_combine_kernel(const float* __restrict__ part_ms,
-                                                          const float* __restrict__ picked,
-                                                          const int64_t* __restrict__ labels, int M, int nsplit,
-                                                          float* __restrict__ lse, const float* __restrict__ count,
-                                                          float* __restrict__ loss, float* __restrict__ blk,
-                                                          unsigned* __restrict__ ticket) {
-  __shared__ float sM[4][kCombineRows], sS[4][kCombineRows], red[16];
+// per-row lse (kept for backward) and loss = lse − picked (0 for ignored rows), kCombineQ threads
+// per row (splits q, q + kCombineQ, … merged online, then across the group in LDS); the mean loss
+// Σ rows / max(count, 1) is finalised in-kernel: each workgroup stores its partial sum, and the
+// last one to take a ticket adds the partials in a fixed order (deterministic) and resets the
+// ticket.  (picked[r] is written by the forward for every row with a label, so it needs no zero
+// fill.)
+constexpr int kCombineRows = 64, kCombineQ = 16;
+__global__ __launch_bounds__(kCombineRows * kCombineQ) void ce_combine_kernel(
+    const float* __restrict__ part_ms, const float* __restrict__ picked, const int64_t* __restrict__ labels, int M,
+    int nsplit, float* __restrict__ lse, const float* __restrict__ count, float* __restrict__ loss,
+    float* __restrict__ blk, unsigned* __restrict__ ticket) {
+  __shared__ float sM[kCombineQ][kCombineRows], sS[kCombineQ][kCombineRows], red[16];
   __shared__ int last;
   const int rr = threadIdx.x % kCombineRows, q = threadIdx.x / kCombineRows;
   const int r = blockIdx.x * kCombineRows + rr;
   float mx = -1e30f, sx = 0.f;
   if (r < M) {
-#pragma unroll 2
-    for (int s = q; s < nsplit; s += 4) {
+    for (int s = q; s < nsplit; s += kCombineQ) {
       const float m = part_ms[((long long)s * M + r) * 2], e = part_ms[((long long)s * M + r) * 2 + 1];
       const float mn = fmaxf(mx, m);
       sx = sx * __expf(mx - mn) + e * __expf(m - mn);
@@ -253,21 +251,17 @@ __global__ __launch_bounds__(1024) void ce_combine_kernel(const float* __restric
   if (q == 0 && r < M) {
     float mm = sM[0][rr];
 #pragma unroll
-    for (int k = 1; k < 4; ++k) mm = fmaxf(mm, sM[k][rr]);
+    for (int k = 1; k < kCombineQ; ++k) mm = fmaxf(mm, sM[k][rr]);
     float ss = 0.f;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) ss += sS[k][rr] * __expf(sM[k][rr] - mm);
+    for (int k = 0; k < kCombineQ; ++k) ss += sS[k][rr] * __expf(sM[k][rr] - mm);
     const float L = mm + __logf(ss);
     lse[r] = L;
     lr = labels[r] >= 0 ? L - picked[r] : 0.f;
   }
-  lr = wave_sum(lr);
-  if (lane_id() == 0) red[wave_id()] = lr;
-  __syncthreads();
+  lr = wave_sum(lr);  // rows of q == 0 live in wave 0
   if (threadIdx.x == 0) {
-    float t = 0.f;
-    for (int k = 0; k < 4; ++k) t += red[k];  // waves 4..15 hold q > 0 threads: zero
-    blk[blockIdx.x] = t;
+    blk[blockIdx.x] = lr;
     __threadfence();
     last = atomicAdd(ticket, 1u) == gridDim.x - 1;
   }
@@ -277,12 +271,11 @@ __global__ __launch_bounds__(1024) void ce_combine_kernel(const float* __restric
   float t = 0.f;
   for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x) t += *(volatile const float*)(blk + i);
   t = wave_sum(t);
-  __syncthreads();
   if (lane_id() == 0) red[wave_id()] = t;
   __syncthreads();
   if (threadIdx.x == 0) {
     float tt = 0.f;
-    for (int k = 0; k < 16; ++k) tt += red[k];
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) tt += red[k];
     loss[0] = tt / fmaxf(count[0], 1.f);
     *ticket = 0u;
   }
@@ -724,18 +717,21 @@ __global__ __launch_bounds__(256) void ce_bwd_dw_reg_kernel(const uint16_t* __re
 // ------------------------------------------------------------------------------------
 // select_rows: workgroup b compacts sequence b (slot → position also kept in LDS) and, when
 // given, copies the output-query rows q[b, j] = P[idx_b[b, j]] the decoder cross-attention reads
-// (the gather of the query array).  select_global (one workgroup): block-wide scan of the
-// per-sequence counts, then one wave per sequence writes its valid slots into the global rows.
-__global__ __launch_bounds__(256) void select_rows_kernel(const int64_t* __restrict__ labels, int L, int cap,
-                                                          int64_t* __restrict__ idx_b, int64_t* __restrict__ lab_b,
-                                                          int* __restrict__ count, const float* __restrict__ P, int C,
-                                                          float* __restrict__ q) {
+// (the gather of the query array).  select_global: workgroup b finds its sequence's offset in
+// the global rows from all the per-sequence counts (each workgroup scans them itself: no
+// grid-wide hand-off) and writes its valid slots; workgroup 0 also writes the totals, the last
+// one the unused tail.
+constexpr int kSelThreads = 1024;
+__global__ __launch_bounds__(kSelThreads) void select_rows_kernel(const int64_t* __restrict__ labels, int L, int cap,
+                                                                  int64_t* __restrict__ idx_b, int64_t* __restrict__ lab_b,
+                                                                  int* __restrict__ count, const float* __restrict__ P,
+                                                                  int C, float* __restrict__ q) {
   extern __shared__ int sIdx[];  // [cap]
-  __shared__ int sW[4], sOff;
-  const int b = blockIdx.x, w = wave_id(), l = lane_id();
+  __shared__ int sW[kSelThreads / 64], sOff;
+  const int b = blockIdx.x, w = wave_id(), l = lane_id(), nw = blockDim.x >> 6;
   if (threadIdx.x == 0) sOff = 0;
   lds_sync();
-  for (int c0 = 0; c0 < L; c0 += 256) {
+  for (int c0 = 0; c0 < L; c0 += blockDim.x) {
     const int i = c0 + threadIdx.x;
     const int64_t lab = i < L ? labels[(long long)b * L + i] : -100;
     const bool sel = lab != -100;
@@ -743,8 +739,11 @@ __global__ __launch_bounds__(256) void select_rows_kernel(const int64_t* __restr
     const int pre = __popcll(m & ((1ull << l) - 1ull));
     if (l == 0) sW[w] = __popcll(m);
     lds_sync();
-    int woff = 0;
-    for (int k = 0; k < w; ++k) woff += sW[k];
+    int woff = 0, tot = 0;
+    for (int k = 0; k < nw; ++k) {
+      woff += k < w ? sW[k] : 0;
+      tot += sW[k];
+    }
     const int pos = sOff + woff + pre;
     if (sel && pos < cap) {
       idx_b[(long long)b * cap + pos] = i;
@@ -752,7 +751,7 @@ __global__ __launch_bounds__(256) void select_rows_kernel(const int64_t* __restr
       sIdx[pos] = i;
     }
     lds_sync();
-    if (threadIdx.x == 0) sOff += sW[0] + sW[1] + sW[2] + sW[3];
+    if (threadIdx.x == 0) sOff += tot;
     lds_sync();
   }
   const int cnt = sOff;
@@ -768,11 +767,11 @@ __global__ __launch_bounds__(256) void select_rows_kernel(const int64_t* __restr
   const float4* P4 = reinterpret_cast<const float4*>(P);
   float4* q4 = reinterpret_cast<float4*>(q) + (long long)b * cap * C4;
   const int n4 = cap * C4;
-  for (int e0 = 0; e0 < n4; e0 += 4 * 256) {  // four independent row loads in flight per thread
+  for (int e0 = 0; e0 < n4; e0 += 4 * kSelThreads) {  // four independent row loads in flight per thread
     float4 v[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int e = e0 + u * 256 + threadIdx.x;
+      const int e = e0 + u * kSelThreads + threadIdx.x;
       if (e < n4) {
         const int j = e / C4;
         v[u] = P4[(long long)sIdx[j] * C4 + (e - j * C4)];
@@ -780,67 +779,57 @@ __global__ __launch_bounds__(256) void select_rows_kernel(const int64_t* __restr
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int e = e0 + u * 256 + threadIdx.x;
+      const int e = e0 + u * kSelThreads + threadIdx.x;
       if (e < n4) q4[e] = v[u];
     }
   }
 }
 
-__global__ __launch_bounds__(1024) void select_global_kernel(const int* __restrict__ count, int B, int cap,
-                                                             const int64_t* __restrict__ lab_b, int gcap,
-                                                             int64_t* __restrict__ gidx, int64_t* __restrict__ glab,
-                                                             float* __restrict__ total, bool* __restrict__ overflow,
-                                                             bool* __restrict__ sticky) {
-  extern __shared__ int sOffs[];  // [B + 1] exclusive prefix of min(count, cap)
-  __shared__ int sW[16], sAll, sOvf;
-  const int w = wave_id(), l = lane_id(), nw = blockDim.x >> 6;
-  if (threadIdx.x == 0) { sAll = 0; sOvf = 0; }
-  __syncthreads();
-  int carry = 0, all = 0, ovf = 0;
-  for (int b0 = 0; b0 < B; b0 += blockDim.x) {  // block-wide exclusive scan
-    const int bb = b0 + threadIdx.x;
-    const int c = bb < B ? count[bb] : 0, n = c < cap ? c : cap;
-    all += c;
-    ovf |= c > cap;
-    int v = n;
+__device__ __forceinline__ int wave_isum(int v) {
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int u = __shfl_up(v, d, 64);
-      if (l >= d) v += u;
-    }
-    if (l == 63) sW[w] = v;
-    __syncthreads();
-    int woff = carry;
-    for (int k = 0; k < w; ++k) woff += sW[k];
-    if (bb < B) sOffs[bb] = woff + v - n;
-    for (int k = 0; k < nw; ++k) carry += sW[k];
-    __syncthreads();
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(256) void select_global_kernel(const int* __restrict__ count, int B, int cap,
+                                                            const int64_t* __restrict__ lab_b, int gcap,
+                                                            int64_t* __restrict__ gidx, int64_t* __restrict__ glab,
+                                                            float* __restrict__ total, bool* __restrict__ overflow,
+                                                            bool* __restrict__ sticky) {
+  __shared__ int sRed[4][4];
+  const int b = blockIdx.x, w = wave_id(), l = lane_id();
+  int pre = 0, used = 0, all = 0, ovf = 0;
+  for (int i = threadIdx.x; i < B; i += blockDim.x) {
+    const int c = count[i], n = c < cap ? c : cap;
+    pre += i < b ? n : 0;
+    used += n;
+    all += c;
+    ovf += c > cap ? 1 : 0;
   }
-  if (all) atomicAdd(&sAll, all);
-  if (ovf) sOvf = 1;
-  if (threadIdx.x == 0) sOffs[B] = carry;
+  pre = wave_isum(pre); used = wave_isum(used); all = wave_isum(all); ovf = wave_isum(ovf);
+  if (l == 0) { sRed[0][w] = pre; sRed[1][w] = used; sRed[2][w] = all; sRed[3][w] = ovf; }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const bool o = sOvf || carry > gcap;
-    total[0] = (float)sAll;
+  pre = sRed[0][0] + sRed[0][1] + sRed[0][2] + sRed[0][3];
+  used = sRed[1][0] + sRed[1][1] + sRed[1][2] + sRed[1][3];
+  const int c = count[b], n = c < cap ? c : cap;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) {
+    const int g = pre + j;
+    if (g < gcap) {
+      const long long s = (long long)b * cap + j;
+      gidx[g] = s;
+      glab[g] = lab_b[s];
+    }
+  }
+  if (b == B - 1)
+    for (int g = (used < gcap ? used : gcap) + threadIdx.x; g < gcap; g += blockDim.x) {
+      gidx[g] = 0;
+      glab[g] = -100;
+    }
+  if (b == 0 && threadIdx.x == 0) {
+    const bool o = (sRed[3][0] + sRed[3][1] + sRed[3][2] + sRed[3][3]) > 0 || used > gcap;
+    total[0] = (float)(sRed[2][0] + sRed[2][1] + sRed[2][2] + sRed[2][3]);
     overflow[0] = o;
     if (sticky != nullptr && o) sticky[0] = true;  // the persistent per-device flag (never cleared here)
-  }
-  for (int bb = w; bb < B; bb += nw) {  // one wave per sequence: its valid slots → global rows
-    const int off = sOffs[bb], n = sOffs[bb + 1] - off;
-    for (int j = l; j < n; j += 64) {
-      const int g = off + j;
-      if (g < gcap) {
-        const long long s = (long long)bb * cap + j;
-        gidx[g] = s;
-        glab[g] = lab_b[s];
-      }
-    }
-  }
-  const int used = sOffs[B] < gcap ? sOffs[B] : gcap;
-  for (int g = used + threadIdx.x; g < gcap; g += blockDim.x) {
-    gidx[g] = 0;
-    glab[g] = -100;
   }
 }
 
@@ -848,10 +837,10 @@ void mlm_select_launch(const int64_t* labels, int B, int L, int cap, int gcap, i
                        int* count, int64_t* gidx, int64_t* glab, float* total, bool* overflow, bool* sticky,
                        const float* P, int C, float* q, unsigned* ticket, hipStream_t st) {
   (void)ticket;
-  hipLaunchKernelGGL(select_rows_kernel, dim3(B), dim3(256), cap * sizeof(int), st, labels, L, cap, idx_b, lab_b, count,
-                     P, C, q);
-  hipLaunchKernelGGL(select_global_kernel, dim3(1), dim3(1024), (B + 1) * sizeof(int), st, count, B, cap, lab_b, gcap,
-                     gidx, glab, total, overflow, sticky);
+  hipLaunchKernelGGL(select_rows_kernel, dim3(B), dim3(kSelThreads), cap * sizeof(int), st, labels, L, cap, idx_b, lab_b,
+                     count, P, C, q);
+  hipLaunchKernelGGL(select_global_kernel, dim3(B), dim3(256), 0, st, count, B, cap, lab_b, gcap, gidx, glab, total,
+                     overflow, sticky);
 }
 
 // vocab splits so that a launch has ≈ target workgroups (several per CU hide the W-chunk latency);
@@ -888,7 +877,8 @@ void ce_fwd_launch(int C, const float* Hm, const int64_t* hidx, const int64_t* l
   else if (C == 128) { CEF(128); }
   else if (C == 32) { CEF(32); }
 #undef CEF
-  hipLaunchKernelGGL(ce_combine_kernel, dim3(ce_combine_blocks(M)), dim3(1024), 0, st, part_ms, picked, labels, M, nsplit,
+  hipLaunchKernelGGL(ce_combine_kernel, dim3(ce_combine_blocks(M)), dim3(kCombineRows * kCombineQ), 0, st, part_ms, picked,
+                     labels, M, nsplit,
                      lse, count, loss, blk, tickets);
 }
 
