@@ -53,7 +53,7 @@ void post_attn_fwd_launch(int, const uint16_t*, const float*, const uint16_t*, c
                           float*, float*, float*, uint16_t*, int, int, const DropCfg&, hipStream_t);
 void post_attn_ln_linear_fwd_launch(int, const uint16_t*, const float*, const uint16_t*, const float*, const float*,
                                     const float*, float, const uint16_t*, const float*, const uint16_t*, const float*,
-                                    float*, float*, float*, float*, uint16_t*, int, const float*, const float*,
+                                    float*, float*, float*, float*, uint16_t*, int, int, const float*, const float*,
                                     const uint16_t*, const float*, uint16_t*, float*, float*, const DropCfg&,
                                     hipStream_t);
 void sa_layer_fwd_launch(const uint16_t*, int, float, uint16_t*, float*, const float*, const uint16_t*, const float*,
@@ -354,7 +354,8 @@ std::vector<Tensor> post_attn_ln_linear_fwd(Tensor o, Tensor x, Tensor wo, Tenso
                                             Tensor wq, Tensor bq, OptT seed, int64_t site, double p) {
   TORCH_CHECK(o.is_contiguous() && x.is_contiguous(), "o/x must be contiguous (R, C)");
   const int R = (int)o.size(0), C = (int)o.size(1);
-  TORCH_CHECK(x.size(0) == R && x.size(1) == C, "x must be (R, C)");
+  const int Rx = (int)x.size(0);
+  TORCH_CHECK(x.size(1) == C && Rx > 0 && R % Rx == 0, "x must be (R / k, C): row r adds x[r % rows(x)]");
   TORCH_CHECK(C == 32 || C == 64 || C == 128, "post_attn supports C in {32, 64, 128}");
   TORCH_CHECK(wq.is_contiguous() && wq.size(0) == 3 * C && wq.size(1) == C && bq.numel() == 3 * C,
               "wq must be the packed (3C, C) in-projection");
@@ -366,7 +367,7 @@ std::vector<Tensor> post_attn_ln_linear_fwd(Tensor o, Tensor x, Tensor wo, Tenso
   Tensor qkv = torch::empty({R, 3 * C}, b16), m1 = torch::empty({R}, f32), r1 = torch::empty({R}, f32);
   pio::post_attn_ln_linear_fwd_launch(C, bfp(o), f32p(x), bfp(wo), f32p(bo), f32p(g2), f32p(be2), (float)eps, bfp(w1),
                                       f32p(b1), bfp(w2), f32p(b2), z.data_ptr<float>(), y.data_ptr<float>(),
-                                      m.data_ptr<float>(), r.data_ptr<float>(), bfp_mut(u), R, f32p(lnw), f32p(lnb),
+                                      m.data_ptr<float>(), r.data_ptr<float>(), bfp_mut(u), R, Rx, f32p(lnw), f32p(lnb),
                                       bfp(wq), f32p(bq), bfp_mut(qkv), m1.data_ptr<float>(), r1.data_ptr<float>(),
                                       make_drop(seed, site, p), stream());
   return {z, y, m, r, u, qkv, m1, r1};

@@ -675,7 +675,7 @@ __global__ __launch_bounds__(256) void post_attn_ln_linear_fwd_kernel(
     const float* __restrict__ bo, const float* __restrict__ g2, const float* __restrict__ be2, float eps,
     const uint16_t* __restrict__ W1, const float* __restrict__ b1, const uint16_t* __restrict__ W2,
     const float* __restrict__ b2, float* __restrict__ Z, float* __restrict__ Ysave, float* __restrict__ mean2,
-    float* __restrict__ rstd2, uint16_t* __restrict__ Usave, int R, const float* __restrict__ lnw,
+    float* __restrict__ rstd2, uint16_t* __restrict__ Usave, int R, int Rx, const float* __restrict__ lnw,
     const float* __restrict__ lnb, const uint16_t* __restrict__ Wq, const float* __restrict__ bq,
     uint16_t* __restrict__ QKV, float* __restrict__ mean1, float* __restrict__ rstd1, DropCfg dr) {
   constexpr int NCH = C / 32, KP = 32 * NCH;
@@ -687,8 +687,8 @@ __global__ __launch_bounds__(256) void post_attn_ln_linear_fwd_kernel(
   row_load<NCH>(gb, lnb, 0, 0, 1, C, AV);
   float z[NCH][8];
   PaPre<C> pre;
-  post_attn_fwd_prefetch<C, AV>(pre, X, Wo, bo, g2, be2, W1, b1, W2, b2, R, R);
-  post_attn_fwd_body<C, AV>(O, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, R, dr, z, pre);
+  post_attn_fwd_prefetch<C, AV>(pre, X, Wo, bo, g2, be2, W1, b1, W2, b2, R, Rx);
+  post_attn_fwd_body<C, AV>(O, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, Rx, dr, z, pre);
   ln_linear_fwd_tile<uint16_t, NCH, AV>(z, wb, gw, gb, true, blockIdx.x * 64, R, C, eps, Wq, C, bq, 3 * C, 0, nullptr, 0,
                                     QKV, 3 * C, mean1, rstd1, smem);
 }
@@ -1528,18 +1528,18 @@ void post_attn_fwd_launch(int C, const uint16_t* O, const float* X, const uint16
 void post_attn_ln_linear_fwd_launch(int C, const uint16_t* O, const float* X, const uint16_t* Wo, const float* bo,
                                     const float* g2, const float* be2, float eps, const uint16_t* W1, const float* b1,
                                     const uint16_t* W2, const float* b2, float* Z, float* Ysave, float* mean2,
-                                    float* rstd2, uint16_t* Usave, int R, const float* lnw, const float* lnb,
+                                    float* rstd2, uint16_t* Usave, int R, int Rx, const float* lnw, const float* lnb,
                                     const uint16_t* Wq, const float* bq, uint16_t* QKV, float* mean1, float* rstd1,
                                     const DropCfg& dr, hipStream_t st) {
   const bool av = av_ok({O, X, Wo, W1, W2, Z, Ysave, Usave, Wq, lnw, lnb, QKV}, {});
   dim3 grid((R + 63) / 64);
 #define PLF(CC)                                                                                                  \
   if (av) hipLaunchKernelGGL((post_attn_ln_linear_fwd_kernel<CC, true>), grid, dim3(256), 0, st, O, X, Wo, bo, g2, \
-                             be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, lnw, lnb, Wq, bq, QKV,      \
+                             be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, Rx, lnw, lnb, Wq, bq, QKV,  \
                              mean1, rstd1, dr);                                                                    \
   else hipLaunchKernelGGL((post_attn_ln_linear_fwd_kernel<CC, false>), grid, dim3(256), 0, st, O, X, Wo, bo, g2,     \
-                          be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, lnw, lnb, Wq, bq, QKV, mean1,  \
-                          rstd1, dr)
+                          be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, Rx, lnw, lnb, Wq, bq, QKV,     \
+                          mean1, rstd1, dr)
   if (C == 64) PLF(64);
   else if (C == 128) PLF(128);
   else if (C == 32) PLF(32);

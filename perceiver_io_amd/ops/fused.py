@@ -430,7 +430,15 @@ class _LayerFn(torch.autograd.Function):
         o2 = o.view(B * Nq, C)
         # a batch-broadcast query stream (Bq = 1) is added as the residual without expanding it;
         # residual dropout (p_attn: the layer's one dropout rate) in the kernel epilogues
-        z, y, m2, r2, u = K.post_attn_fwd(o2, xq2, wo, bo, g2, be2, EPS, w1, b1, w2, b2, seed=seed, p=p_attn)
+        nxt, _LOOKAHEAD["want"] = _LOOKAHEAD["want"], None
+        if nxt is not None and spec.cross:
+            # the following self-attention block's LN1 + QKV projection in the same launch (its
+            # forward picks the result up instead of launching ln_linear_fwd)
+            z, y, m2, r2, u, qkv_n, mean_n, rstd_n = K.post_attn_ln_linear_fwd(
+                o2, xq2, wo, bo, g2, be2, EPS, w1, b1, w2, b2, nxt[0], nxt[1], nxt[2], nxt[3], seed=seed, p=p_attn)
+            _LOOKAHEAD["have"] = (z, qkv_n, mean_n, rstd_n, nxt[0])
+        else:
+            z, y, m2, r2, u = K.post_attn_fwd(o2, xq2, wo, bo, g2, be2, EPS, w1, b1, w2, b2, seed=seed, p=p_attn)
         ctx.spec, ctx.bw, ctx.seed, ctx.p_attn = spec, bw, seed, p_attn
         ctx.src = src if spec.cross else None
         ctx.dims = (B, Bq, Nq, C, H, D, scale)
@@ -680,7 +688,12 @@ class _SABlockFn(torch.autograd.Function):
         xl = x.reshape(R, C)
         if not xl.is_contiguous():
             xl = xl.contiguous()
-        qkv, mean1, rstd1 = K.ln_linear_fwd(xl, P[0][0], P[0][1], EPS, bws[0][0], P[0][3], 0, None, True, True)
+        have, _LOOKAHEAD["have"] = _LOOKAHEAD["have"], None
+        if (have is not None and have[4] is P[0][0] and have[0].data_ptr() == xl.data_ptr()
+                and have[0].numel() == xl.numel()):
+            qkv, mean1, rstd1 = have[1:4]  # computed by the preceding cross-attention layer's kernel
+        else:
+            qkv, mean1, rstd1 = K.ln_linear_fwd(xl, P[0][0], P[0][1], EPS, bws[0][0], P[0][3], 0, None, True, True)
         saved = []
         # one fused launch per layer (attention + post-attention + next LN1/QKV) for the
         # C = 64, H = 4 latent stacks without attention dropout (sa_layer_fwd_kernel)
@@ -782,9 +795,15 @@ class _SABlockFn(torch.autograd.Function):
         return (None, None, None, None, dx.view(B, N, C)) + (None,) * len(ps)
 
 
-def self_attention_block(block, x):
-    """All layers of a self-attention block; one fused autograd node when every layer is
-    fusable at C ≤ 64 (slab gradients on), else layer by layer."""
+# cross-layer hand-off between a fused cross-attention layer and the self-attention block that
+# follows it (_encode): "want" = the block's first-layer (γ1, β1, Wqkv bf16, bqkv), consumed by the
+# cross layer's forward, which then runs post_attn + LN1/QKV in one launch and leaves
+# "have" = (z, qkv, mean1, rstd1, γ1) for the block's forward
+_LOOKAHEAD = {"want": None, "have": None}
+
+
+def _sa_block_plan(block, rows: int):
+    """(layers, specs, param lists, fused?) of a self-attention block applied to ``rows`` rows."""
     layers = list(block)
     specs, pss = [], []
     for layer in layers:
@@ -793,7 +812,25 @@ def self_attention_block(block, x):
         pss.append(ps)
     ok = (WGRAD_SLAB and len(layers) > 1 and all(_fusable(lay) for lay in layers)
           and all(sp == specs[0] for sp in specs) and specs[0].C in (32, 64) and not specs[0].cross
-          and x.dim() == 3 and x.shape[1] * x.shape[0] < TALL_ROWS)
+          and rows < TALL_ROWS)
+    return layers, specs, pss, ok
+
+
+def sa_block_lookahead(block, rows: int):
+    """The (γ1, β1, Wqkv bf16, bqkv) a preceding cross-attention layer can fuse into its
+    post-attention kernel, or None when the block will not run fused."""
+    _, specs, pss, ok = _sa_block_plan(block, rows)
+    if not ok:
+        return None
+    ps = pss[0]
+    return (ps[0], ps[1], _bf16_weights(specs[0], ps)[0], ps[3])
+
+
+def self_attention_block(block, x):
+    """All layers of a self-attention block; one fused autograd node when every layer is
+    fusable at C ≤ 64 (slab gradients on), else layer by layer."""
+    layers, specs, pss, ok = _sa_block_plan(block, x.shape[1] * x.shape[0] if x.dim() == 3 else TALL_ROWS)
+    ok = ok and x.dim() == 3
     if not ok:
         for layer in layers:
             x = self_attention_layer(layer, x)
@@ -926,12 +963,21 @@ def encode_inputs(encoder, x_in, pad_mask=None):
 def _encode(encoder, src: KVSource, pad_mask):
     lat = encoder.latent.unsqueeze(0)  # (1, N, C): projected once, broadcast inside the kernels
     b = src.x.shape[0]
+    n = lat.shape[1]
     for layer in encoder.layers():
         cross, block = layer[0], layer[1]
         if lat.shape[0] == 1 and not can_fuse(cross, src):
             lat = lat.expand(b, -1, -1)
-        lat = cross_attention_layer(cross, lat, src, pad_mask)
+        # the block's first LN1 + QKV projection rides on the cross layer's post-attention kernel
+        _LOOKAHEAD["want"] = sa_block_lookahead(block, b * n) if can_fuse(cross, src) else None
+        try:
+            lat = cross_attention_layer(cross, lat, src, pad_mask)
+        finally:
+            _LOOKAHEAD["want"] = None
         if lat.shape[0] == 1 and b > 1:
             lat = lat.expand(b, -1, -1)
-        lat = self_attention_block(block, lat)
+        try:
+            lat = self_attention_block(block, lat)
+        finally:
+            _LOOKAHEAD["have"] = None
     return lat
