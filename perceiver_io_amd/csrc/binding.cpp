@@ -467,6 +467,20 @@ pio::SlabJob make_job(const OptT& slab, std::vector<Tensor>& dsts, const std::ve
   j.nblk = g_det ? j.nbx : j.nbx * ((j.S + pio::kSlabRowsPerBlock - 1) / pio::kSlabRowsPerBlock);
   return j;
 }
+
+// zero_out (optional): an fp32 buffer the kernel carrying this job clears on the way (the NEXT
+// kernel's atomic accumulator, e.g. the cross-attention dQ) — no separate fill launch
+pio::SlabJob with_zero_span(pio::SlabJob job, const OptT& zero_out, const Tensor& like) {
+  if (zero_out.has_value()) {
+    CHECK_DT(*zero_out, torch::kFloat32);
+    TORCH_CHECK(zero_out->is_contiguous() && zero_out->numel() % 4 == 0 && zero_out->get_device() == like.get_device() &&
+                    reinterpret_cast<uintptr_t>(zero_out->data_ptr()) % 16 == 0,
+                "zero_out must be a contiguous, 16-byte aligned fp32 buffer of 4k elements");
+    job.zero_p = zero_out->data_ptr<float>();
+    job.zero_n4 = zero_out->numel() / 4;
+  }
+  return job;
+}
 }  // namespace
 
 // grads = [dWo, dbo, dg2, dbe2, dW1, db1, dW2, db2]; returns (dy, dO, delta)
@@ -495,15 +509,7 @@ std::vector<Tensor> post_attn_bwd(Tensor dz, Tensor y, Tensor m2, Tensor r2, Ten
   Tensor dy = torch::empty({R, C}, f32);
   Tensor dO = torch::empty({R, C}, dz.options().dtype(torch::kBFloat16));
   Tensor delta = torch::empty({R, H}, f32);
-  pio::SlabJob job = make_job(job_slab, job_dsts, job_offs);
-  if (zero_out.has_value()) {  // cleared by this kernel's workgroups on the way (the next kernel's accumulator)
-    CHECK_DT(*zero_out, torch::kFloat32);
-    TORCH_CHECK(zero_out->is_contiguous() && zero_out->numel() % 4 == 0 && zero_out->get_device() == dz.get_device() &&
-                    reinterpret_cast<uintptr_t>(zero_out->data_ptr()) % 16 == 0,
-                "post_attn_bwd: zero_out must be a contiguous, 16-byte aligned fp32 buffer of 4k elements");
-    job.zero_p = zero_out->data_ptr<float>();
-    job.zero_n4 = zero_out->numel() / 4;
-  }
+  pio::SlabJob job = with_zero_span(make_job(job_slab, job_dsts, job_offs), zero_out, dz);
   pio::post_attn_bwd_launch(C, f32p(dz), f32p(y), f32p(m2), f32p(r2), bfp(u), bfp(o), bfp(wo), bfp(w1), bfp(w2),
                             f32p(g2), f32p(be2), dy.data_ptr<float>(), bfp_mut(dO), delta.data_ptr<float>(), (int)H,
                             pg, R, job, make_drop(seed, site, p), stream());
@@ -520,7 +526,7 @@ std::vector<Tensor> ln_linear_post_attn_bwd(Tensor g, Tensor wq, Tensor x, Tenso
                                             Tensor r2, Tensor u, Tensor o, Tensor wo, Tensor w1, Tensor w2, Tensor g2,
                                             Tensor be2, int64_t H, std::vector<Tensor> pa_grads, OptT job_slab,
                                             std::vector<Tensor> job_dsts, std::vector<int64_t> job_offs, OptT seed,
-                                            int64_t site, double p) {
+                                            int64_t site, double p, OptT zero_out) {
   TORCH_CHECK(y.is_contiguous() && u.is_contiguous() && o.is_contiguous() && x.is_contiguous() && dres.is_contiguous(),
               "operands must be contiguous (R, C)");
   const int R = (int)y.size(0), C = (int)y.size(1);
@@ -550,7 +556,8 @@ std::vector<Tensor> ln_linear_post_attn_bwd(Tensor g, Tensor wq, Tensor x, Tenso
                                       f32p(dres), dg1, db1, dwq, dbq, f32p(y), f32p(m2), f32p(r2), bfp(u), bfp(o),
                                       bfp(wo), bfp(w1), bfp(w2), f32p(g2), f32p(be2), dy.data_ptr<float>(),
                                       bfp_mut(dO), delta.data_ptr<float>(), (int)H, pg, R,
-                                      make_job(job_slab, job_dsts, job_offs), make_drop(seed, site, p), stream());
+                                      with_zero_span(make_job(job_slab, job_dsts, job_offs), zero_out, y),
+                                      make_drop(seed, site, p), stream());
   return {dy, dO, delta};
 }
 
@@ -1155,7 +1162,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("w2"), py::arg("g2"), py::arg("be2"), py::arg("H"), py::arg("pa_grads"),
         py::arg("job_slab") = py::none(), py::arg("job_dsts") = std::vector<Tensor>(),
         py::arg("job_offs") = std::vector<int64_t>(), py::arg("seed") = py::none(), py::arg("site") = 0,
-        py::arg("p") = 0.0);
+        py::arg("p") = 0.0, py::arg("zero_out") = py::none());
   m.def("post_attn_bwd", &post_attn_bwd, py::arg("dz"), py::arg("y"), py::arg("m2"), py::arg("r2"), py::arg("u"),
         py::arg("o"), py::arg("wo"), py::arg("w1"), py::arg("w2"), py::arg("g2"), py::arg("be2"), py::arg("H"),
         py::arg("grads"), py::arg("slab") = false, py::arg("job_slab") = py::none(),

@@ -1336,6 +1336,7 @@ __global__ __launch_bounds__(256) void ln_linear_post_attn_bwd_kernel(
   // ONE buffer for both halves (used one after the other): ≈69 KB at C = 64, two workgroups per
   // CU, so the appended slab-job workgroups run beside the tiles instead of after them
   __shared__ __attribute__((aligned(16))) unsigned char smem[SM];
+  zero_span_block(job);
   if ((int)blockIdx.x >= (R + 63) / 64) {  // appended workgroups: the previous kernel's slab job
     slab_reduce_block(job, blockIdx.x - (R + 63) / 64, reinterpret_cast<float4*>(smem));
     return;

@@ -223,7 +223,8 @@ def post_attn_ln_linear_fwd(o, x, wo, bo, g2, be2, eps, w1, b1, w2, b2, lnw, lnb
 
 
 def ln_linear_post_attn_bwd(g, wq, x, mean1, rstd1, lnw, lnb, dres, ll_grads, y, m2, r2, u, o, wo, w1, w2, g2, be2,
-                            H, pa_grads, job_slab=None, job_dsts=(), job_offs=(), seed=None, site=0, p=0.0):
+                            H, pa_grads, job_slab=None, job_dsts=(), job_offs=(), seed=None, site=0, p=0.0,
+                            zero_out=None):
     """ln_linear_bwd of layer l+1 (dX = dZ of layer l, incl. dres) → post_attn_bwd of layer l,
     both into slab targets."""
     _run_job(job_slab, job_dsts, job_offs)

@@ -437,6 +437,7 @@ class _LayerFn(torch.autograd.Function):
             z, y, m2, r2, u, qkv_n, mean_n, rstd_n = K.post_attn_ln_linear_fwd(
                 o2, xq2, wo, bo, g2, be2, EPS, w1, b1, w2, b2, nxt[0], nxt[1], nxt[2], nxt[3], seed=seed, p=p_attn)
             _LOOKAHEAD["have"] = (z, qkv_n, mean_n, rstd_n, nxt[0])
+            ctx.lookahead_z = z.data_ptr()  # the block's backward hands its LN1/QKV backward back here
         else:
             z, y, m2, r2, u = K.post_attn_fwd(o2, xq2, wo, bo, g2, be2, EPS, w1, b1, w2, b2, seed=seed, p=p_attn)
         ctx.spec, ctx.bw, ctx.seed, ctx.p_attn = spec, bw, seed, p_attn
@@ -516,7 +517,20 @@ class _LayerFn(torch.autograd.Function):
         if spec.cross and not pe_fused and not deterministic():
             dq_pre = torch.empty((B, Nq, C), **f32)
             drop["zero_out"] = dq_pre
-        if WGRAD_SLAB and R < TALL_ROWS:
+        ho, _LOOKAHEAD["bwd"] = _LOOKAHEAD["bwd"], None
+        if ho is not None and ho["key"] != getattr(ctx, "lookahead_z", None):
+            raise RuntimeError("fused encoder: a self-attention block handed its LN1/QKV backward to the wrong "
+                               "cross-attention layer")
+        if ho is not None:
+            # the following block's first LN1/QKV backward (its dX = this layer's dZ) and this
+            # layer's post-attention backward in one launch; both weight-gradient sets in one slab
+            sl = _GradSlab(R, LL_SIZES(C) + PA_SIZES(C), dz2)
+            tg = sl.targets()
+            dy, do, delta = K.ln_linear_post_attn_bwd(ho["g"], ho["wq"], ho["x"], ho["mean1"], ho["rstd1"], ho["lnw"],
+                                                      ho["lnb"], ho["dres"], tg[:4], y, m2, r2, u, o2, wo, w1, w2, g2,
+                                                      be2, H, tg[4:], **_take_job(), **drop)
+            sl.defer(K, ho["ll_dsts"] + [flat(p) for p in (Wo, bo, g2, be2, W1, b1, W2, b2)])
+        elif WGRAD_SLAB and R < TALL_ROWS:
             sl = _GradSlab(R, [C * C, C, C, C, C * C, C, C * C, C], dz2)
             dy, do, delta = K.post_attn_bwd(dz2, y, m2, r2, u, o2, wo, w1, w2, g2, be2, H, sl.targets(), slab=True,
                                             **_take_job(), **drop)
@@ -692,6 +706,7 @@ class _SABlockFn(torch.autograd.Function):
         if (have is not None and have[4] is P[0][0] and have[0].data_ptr() == xl.data_ptr()
                 and have[0].numel() == xl.numel()):
             qkv, mean1, rstd1 = have[1:4]  # computed by the preceding cross-attention layer's kernel
+            ctx.handoff = xl.data_ptr()
         else:
             qkv, mean1, rstd1 = K.ln_linear_fwd(xl, P[0][0], P[0][1], EPS, bws[0][0], P[0][3], 0, None, True, True)
         saved = []
@@ -787,6 +802,13 @@ class _SABlockFn(torch.autograd.Function):
                                                           P[i][1], dy, tg[:4], *pa_args(i - 1), H, tg[4:],
                                                           **_take_job(), **drop(i - 1))
                 sl.defer(K, ll_dsts(P[i]) + pa_dsts(P[i - 1]))
+            elif getattr(ctx, "handoff", None) is not None:
+                # the producing cross-attention layer runs this LN1/QKV backward fused with its
+                # post-attention backward (ln_linear_post_attn_bwd); it ignores the gradient
+                # returned here (dy stands in as a correctly shaped tensor: no fill launch)
+                _LOOKAHEAD["bwd"] = dict(key=ctx.handoff, g=dqkv.view(R, 3 * C), wq=bws[0][0], x=xl, mean1=mean1,
+                                         rstd1=rstd1, lnw=P[0][0], lnb=P[0][1], dres=dy, ll_dsts=ll_dsts(P[0]))
+                dx = dy
             else:
                 sl = _GradSlab(R, LL_SIZES(C), dz2)
                 dx = K.ln_linear_bwd(dqkv.view(R, 3 * C), bws[0][0], xl, mean1, rstd1, P[0][0], P[0][1], dy, True,
@@ -798,8 +820,9 @@ class _SABlockFn(torch.autograd.Function):
 # cross-layer hand-off between a fused cross-attention layer and the self-attention block that
 # follows it (_encode): "want" = the block's first-layer (γ1, β1, Wqkv bf16, bqkv), consumed by the
 # cross layer's forward, which then runs post_attn + LN1/QKV in one launch and leaves
-# "have" = (z, qkv, mean1, rstd1, γ1) for the block's forward
-_LOOKAHEAD = {"want": None, "have": None}
+# "have" = (z, qkv, mean1, rstd1, γ1) for the block's forward.  Backward, the block hands its first
+# LN1/QKV backward back ("bwd"), which the cross layer runs fused with its post-attention backward.
+_LOOKAHEAD = {"want": None, "have": None, "bwd": None}
 
 
 def _sa_block_plan(block, rows: int):
