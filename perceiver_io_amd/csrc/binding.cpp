@@ -59,13 +59,13 @@ void post_attn_ln_linear_fwd_launch(int, const uint16_t*, const float*, const ui
 void sa_layer_fwd_launch(const uint16_t*, int, float, uint16_t*, float*, const float*, const uint16_t*, const float*,
                          const float*, const float*, float, const uint16_t*, const float*, const uint16_t*, const float*,
                          float*, float*, float*, float*, uint16_t*, int, const float*, const float*, const uint16_t*,
-                         const float*, uint16_t*, float*, float*, const DropCfg&, hipStream_t);
+                         const float*, uint16_t*, float*, float*, const DropCfg&, int, hipStream_t);
 void ln_linear_post_attn_bwd_launch(int, const float*, const uint16_t*, const float*, const float*, const float*,
                                     const float*, const float*, const float*, float*, float*, float*, float*,
                                     const float*, const float*, const float*, const uint16_t*, const uint16_t*,
                                     const uint16_t*, const uint16_t*, const uint16_t*, const float*, const float*,
                                     float*, uint16_t*, float*, int, const PostAttnGrads&, int, const SlabJob&,
-                                    const DropCfg&, hipStream_t);
+                                    const DropCfg&, int, hipStream_t);
 void post_attn_bwd_launch(int, const float*, const float*, const float*, const float*, const uint16_t*,
                           const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*, const float*,
                           const float*, float*, uint16_t*, float*, int, const PostAttnGrads&, int, const SlabJob&,
@@ -386,23 +386,25 @@ std::vector<Tensor> sa_layer_fwd(Tensor qkv, Tensor x, int64_t N, double scale, 
   TORCH_CHECK(N > 0 && N <= 256 && N % 64 == 0 && R % N == 0, "sa_layer_fwd: N <= 256, N % 64 == 0, R = B·N");
   const bool next = wq.has_value();
   if (next)
-    TORCH_CHECK(lnw.has_value() && lnb.has_value() && bq.has_value() && wq->is_contiguous() && wq->size(0) == 3 * C &&
-                    wq->size(1) == C && bq->numel() == 3 * C && lnw->numel() == C && lnb->numel() == C,
-                "sa_layer_fwd: next-layer LN1 / packed in-projection");
+    TORCH_CHECK(lnw.has_value() && lnb.has_value() && bq.has_value() && wq->is_contiguous() &&
+                    (wq->size(0) == 3 * C || wq->size(0) == C) && wq->size(1) == C && bq->numel() == wq->size(0) &&
+                    lnw->numel() == C && lnb->numel() == C,
+                "sa_layer_fwd: next LN + projection (packed QKV (3C, C) or a query projection (C, C))");
+  const int nq = next ? (int)wq->size(0) : 3 * C;
   auto f32 = x.options().dtype(torch::kFloat32);
   auto b16 = x.options().dtype(torch::kBFloat16);
   Tensor o = torch::empty({R / N, N, C}, b16), lse = torch::empty({R / N, N, H}, f32);
   Tensor z = torch::empty({R, C}, f32), y = torch::empty({R, C}, f32);
   Tensor m = torch::empty({R}, f32), r = torch::empty({R}, f32), u = torch::empty({R, C}, b16);
   Tensor qn, m1, r1;
-  if (next) { qn = torch::empty({R, 3 * C}, b16); m1 = torch::empty({R}, f32); r1 = torch::empty({R}, f32); }
+  if (next) { qn = torch::empty({R, nq}, b16); m1 = torch::empty({R}, f32); r1 = torch::empty({R}, f32); }
   pio::sa_layer_fwd_launch(bfp(qkv), (int)N, (float)(scale * 1.4426950408889634), bfp_mut(o), lse.data_ptr<float>(),
                            f32p(x), bfp(wo), f32p(bo), f32p(g2), f32p(be2), (float)eps, bfp(w1), f32p(b1), bfp(w2),
                            f32p(b2), z.data_ptr<float>(), y.data_ptr<float>(), m.data_ptr<float>(), r.data_ptr<float>(),
                            bfp_mut(u), R, next ? f32p(*lnw) : nullptr, next ? f32p(*lnb) : nullptr,
                            next ? bfp(*wq) : nullptr, next ? f32p(*bq) : nullptr, next ? bfp_mut(qn) : nullptr,
                            next ? m1.data_ptr<float>() : nullptr, next ? r1.data_ptr<float>() : nullptr,
-                           make_drop(seed, site, p), stream());
+                           make_drop(seed, site, p), nq, stream());
   if (next) return {o, lse, z, y, m, r, u, qn, m1, r1};
   return {o, lse, z, y, m, r, u};
 }
@@ -532,17 +534,18 @@ std::vector<Tensor> ln_linear_post_attn_bwd(Tensor g, Tensor wq, Tensor x, Tenso
   const int R = (int)y.size(0), C = (int)y.size(1);
   TORCH_CHECK(C == 32 || C == 64, "the fused self-attention backward supports C in {32, 64}");
   TORCH_CHECK(H > 0 && C % H == 0, "heads must divide C");
-  TORCH_CHECK(g.is_contiguous() && g.size(0) == R && g.size(1) == 3 * C, "g must be (R, 3C) contiguous");
+  const int nq = (int)wq.size(0);  // 3C: packed QKV of a self-attention layer; C: a cross-attention query projection
+  TORCH_CHECK(wq.is_contiguous() && (nq == 3 * C || nq == C) && wq.size(1) == C, "wq must be (3C, C) or (C, C)");
+  TORCH_CHECK(g.is_contiguous() && g.size(0) == R && g.size(1) == nq, "g must be (R, rows(wq)) contiguous");
   CHECK_DT(g, torch::kFloat32);
-  TORCH_CHECK(wq.is_contiguous() && wq.size(0) == 3 * C && wq.size(1) == C, "wq must be (3C, C)");
   TORCH_CHECK(x.size(0) == R && x.size(1) == C && dres.size(0) == R && dres.size(1) == C, "x / dres must be (R, C)");
   TORCH_CHECK(ll_grads.size() == 4 && pa_grads.size() == 8, "4 + 8 slab targets expected");
   const int64_t sr = (R + 63) / 64, CC = (int64_t)C * C;
   int vrs = -1;
   float* dg1 = vec_target(ll_grads[0], C, "dlnw", vrs, sr);
   float* db1 = vec_target(ll_grads[1], C, "dlnb", vrs, sr);
-  float* dwq = vec_target(ll_grads[2], 3 * CC, "dWqkv", vrs, sr);
-  float* dbq = vec_target(ll_grads[3], 3 * C, "dbqkv", vrs, sr);
+  float* dwq = vec_target(ll_grads[2], (int64_t)nq * C, "dWqkv", vrs, sr);
+  float* dbq = vec_target(ll_grads[3], nq, "dbqkv", vrs, sr);
   pio::PostAttnGrads pg{vec_target(pa_grads[0], CC, "dWo", vrs, sr), vec_target(pa_grads[1], C, "dbo", vrs, sr),
                         vec_target(pa_grads[2], C, "dg2", vrs, sr), vec_target(pa_grads[3], C, "dbe2", vrs, sr),
                         vec_target(pa_grads[4], CC, "dW1", vrs, sr), vec_target(pa_grads[5], C, "db1", vrs, sr),
@@ -557,7 +560,7 @@ std::vector<Tensor> ln_linear_post_attn_bwd(Tensor g, Tensor wq, Tensor x, Tenso
                                       bfp(wo), bfp(w1), bfp(w2), f32p(g2), f32p(be2), dy.data_ptr<float>(),
                                       bfp_mut(dO), delta.data_ptr<float>(), (int)H, pg, R,
                                       with_zero_span(make_job(job_slab, job_dsts, job_offs), zero_out, y),
-                                      make_drop(seed, site, p), stream());
+                                      make_drop(seed, site, p), nq, stream());
   return {dy, dO, delta};
 }
 

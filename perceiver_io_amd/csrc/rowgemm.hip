@@ -709,7 +709,7 @@ __global__ __launch_bounds__(256) void post_attn_ln_linear_fwd_kernel(
 //   then the post-attention block on the LDS O tile and (NEXT) LN1 + QKV of the next layer —
 // the attention output never makes a global round trip before its consumer.
 // ------------------------------------------------------------------------------------
-template <bool NEXT, bool AV>
+template <bool NEXT, bool AV, int NQ = 3>
 __global__ __launch_bounds__(256) void sa_layer_fwd_kernel(
     const uint16_t* __restrict__ QKV, int N, float scale_log2, uint16_t* __restrict__ Oout, float* __restrict__ LSE,
     const float* __restrict__ X, const uint16_t* __restrict__ Wo, const float* __restrict__ bo,
@@ -719,7 +719,10 @@ __global__ __launch_bounds__(256) void sa_layer_fwd_kernel(
     const float* __restrict__ lnw, const float* __restrict__ lnb, const uint16_t* __restrict__ Wq,
     const float* __restrict__ bq, uint16_t* __restrict__ QKVn, float* __restrict__ mean1, float* __restrict__ rstd1,
     DropCfg dr) {
+  // NQ·C: width of the next projection (3C: the next self-attention layer's packed QKV; C: the
+  // query projection of a following cross-attention layer)
   constexpr int C = 64, H = 4, D = 16, NCH = 2, KP = 64, LD = C + 8, LDV = C + 8, C3 = 3 * C, MAXKT = 8;
+  constexpr int nq = NQ * C;
   __shared__ __attribute__((aligned(16))) uint16_t sV[256 * LDV + 64];  // V rows of the batch element (+ overrun)
   __shared__ __attribute__((aligned(16))) uint16_t sO[64 * LD];
   __shared__ __attribute__((aligned(16))) uint16_t smem[NEXT ? ln_linear_fwd_smem<NCH>() / 2 : 8];
@@ -749,7 +752,7 @@ __global__ __launch_bounds__(256) void sa_layer_fwd_kernel(
   bf16x8 wb[NCH];
   float gw[NCH][8], gb[NCH][8];
   if constexpr (NEXT) {
-    tile_fetch<NCH>(wb, Wq, C, 0, 3 * C, 64, C, KP, AV);
+    tile_fetch<NCH>(wb, Wq, C, 0, nq, 64, C, KP, AV);
     row_load<NCH>(gw, lnw, 0, 0, 1, C, AV);
     row_load<NCH>(gb, lnb, 0, 0, 1, C, AV);
   }
@@ -818,8 +821,8 @@ __global__ __launch_bounds__(256) void sa_layer_fwd_kernel(
   post_attn_fwd_body<C, AV, true>(nullptr, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, R,
                                   dr, z, pre, sO);
   if constexpr (NEXT)
-    ln_linear_fwd_tile<uint16_t, NCH, AV>(z, wb, gw, gb, true, m0, R, C, eps, Wq, C, bq, 3 * C, 0, nullptr, 0, QKVn,
-                                          3 * C, mean1, rstd1, smem);
+    ln_linear_fwd_tile<uint16_t, NCH, AV>(z, wb, gw, gb, true, m0, R, C, eps, Wq, C, bq, nq, 0, nullptr, 0, QKVn, nq,
+                                          mean1, rstd1, smem);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1320,7 +1323,7 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
 // their parameter-gradient partials into ONE slab row per tile (12 segments).  C ≤ 64 (the
 // two halves' LDS must coexist: ≈117 KB at C = 64).
 // ------------------------------------------------------------------------------------
-template <int C, bool AV>
+template <int C, bool AV, int NQ = 3>
 __global__ __launch_bounds__(256) void ln_linear_post_attn_bwd_kernel(
     const float* __restrict__ G, const uint16_t* __restrict__ Wq, const float* __restrict__ X,
     const float* __restrict__ mean1, const float* __restrict__ rstd1, const float* __restrict__ lnw,
@@ -1330,7 +1333,7 @@ __global__ __launch_bounds__(256) void ln_linear_post_attn_bwd_kernel(
     const uint16_t* __restrict__ Wo, const uint16_t* __restrict__ W1, const uint16_t* __restrict__ W2,
     const float* __restrict__ g2, const float* __restrict__ be2, float* __restrict__ dY, uint16_t* __restrict__ dO,
     float* __restrict__ delta, int H, PostAttnGrads gr_out, int R, SlabJob job, DropCfg dr) {
-  constexpr int NCH = C / 32;
+  constexpr int NCH = C / 32, nq = NQ * C;  // NQ·C: rows of Wq (3C packed QKV, C a query projection)
   constexpr int SM = ln_linear_bwd_smem<NCH>() > post_attn_bwd_smem<C>() ? ln_linear_bwd_smem<NCH>()
                                                                           : post_attn_bwd_smem<C>();
   // ONE buffer for both halves (used one after the other): ≈69 KB at C = 64, two workgroups per
@@ -1342,7 +1345,7 @@ __global__ __launch_bounds__(256) void ln_linear_post_attn_bwd_kernel(
     return;
   }
   float dz[NCH][8];
-  ln_linear_bwd_body<float, float, NCH, AV>(G, 3 * C, 3 * C, Wq, C, C, X, C, mean1, rstd1, lnw, lnb, dres, C, nullptr, C,
+  ln_linear_bwd_body<float, float, NCH, AV>(G, nq, nq, Wq, C, C, X, C, mean1, rstd1, lnw, lnb, dres, C, nullptr, C,
                                         dlnw, dlnb, dWq, dbq, gr_out.vrs, gr_out.vrs, gr_out.slab, R, PeSplit{},
                                         reinterpret_cast<uint16_t*>(smem), dz);
   lds_sync();  // the ln_linear half's LDS traffic is done before the post-attention half reuses it
@@ -1553,13 +1556,17 @@ void sa_layer_fwd_launch(const uint16_t* QKV, int N, float scale_log2, uint16_t*
                          const uint16_t* W1, const float* b1, const uint16_t* W2, const float* b2, float* Z,
                          float* Ysave, float* mean2, float* rstd2, uint16_t* Usave, int R, const float* lnw,
                          const float* lnb, const uint16_t* Wq, const float* bq, uint16_t* QKVn, float* mean1,
-                         float* rstd1, const DropCfg& dr, hipStream_t st) {
+                         float* rstd1, const DropCfg& dr, int nq, hipStream_t st) {
   const bool next = Wq != nullptr;
   const bool av = av_ok({QKV, O, X, Wo, W1, W2, Z, Ysave, Usave, Wq, lnw, lnb, QKVn}, {});
   dim3 grid(R / 64);
 #define SAL(NX, A)                                                                                                 \
-  hipLaunchKernelGGL((sa_layer_fwd_kernel<NX, A>), grid, dim3(256), 0, st, QKV, N, scale_log2, O, LSE, X, Wo, bo, g2, \
-                     be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, lnw, lnb, Wq, bq, QKVn, mean1, rstd1, dr)
+  if (nq == 64) hipLaunchKernelGGL((sa_layer_fwd_kernel<NX, A, 1>), grid, dim3(256), 0, st, QKV, N, scale_log2, O, LSE, X, \
+                                   Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, lnw, lnb, Wq, bq, \
+                                   QKVn, mean1, rstd1, dr);                                                            \
+  else hipLaunchKernelGGL((sa_layer_fwd_kernel<NX, A>), grid, dim3(256), 0, st, QKV, N, scale_log2, O, LSE, X, Wo, bo,   \
+                          g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, lnw, lnb, Wq, bq, QKVn, mean1,  \
+                          rstd1, dr)
   if (next) {
     if (av) SAL(true, true); else SAL(true, false);
   } else {
@@ -1593,18 +1600,20 @@ void ln_linear_post_attn_bwd_launch(int C, const float* G, const uint16_t* Wq, c
                                     const uint16_t* Wo, const uint16_t* W1, const uint16_t* W2, const float* g2,
                                     const float* be2, float* dY, uint16_t* dO, float* delta, int H,
                                     const PostAttnGrads& grads, int R, const SlabJob& job, const DropCfg& dr,
-                                    hipStream_t st) {
+                                    int nq, hipStream_t st) {
   dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0));
   const bool av = av_ok({G, Wq, X, lnw, lnb, dres, Ysave, U, O, Wo, W1, W2, dY, dO}, {});
-#define LPB(CC)                                                                                                   \
-  if (av) hipLaunchKernelGGL((ln_linear_post_attn_bwd_kernel<CC, true>), grid, dim3(256), 0, st, G, Wq, X, mean1,   \
+#define LPB(CC, NQ)                                                                                               \
+  if (av) hipLaunchKernelGGL((ln_linear_post_attn_bwd_kernel<CC, true, NQ>), grid, dim3(256), 0, st, G, Wq, X, mean1, \
                              rstd1, lnw, lnb, dres, dlnw, dlnb, dWq, dbq, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, \
                              be2, dY, dO, delta, H, grads, R, job, dr);                                            \
-  else hipLaunchKernelGGL((ln_linear_post_attn_bwd_kernel<CC, false>), grid, dim3(256), 0, st, G, Wq, X, mean1,      \
+  else hipLaunchKernelGGL((ln_linear_post_attn_bwd_kernel<CC, false, NQ>), grid, dim3(256), 0, st, G, Wq, X, mean1,  \
                           rstd1, lnw, lnb, dres, dlnw, dlnb, dWq, dbq, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2,    \
                           be2, dY, dO, delta, H, grads, R, job, dr)
-  if (C == 64) LPB(64);
-  else if (C == 32) LPB(32);
+  if (C == 64 && nq == 3 * C) { LPB(64, 3); }
+  else if (C == 64) { LPB(64, 1); }
+  else if (nq == 3 * C) { LPB(32, 3); }
+  else { LPB(32, 1); }
 #undef LPB
 }
 

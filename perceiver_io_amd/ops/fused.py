@@ -392,7 +392,13 @@ class _LayerFn(torch.autograd.Function):
         if spec.cross:
             B, M = x_kv.shape[0], x_kv.shape[1]
             xkv2 = x_kv.reshape(B * M, x_kv.shape[2])
-            q, mean_q, rstd_q = K.ln_linear_fwd(xq2, g_q, b_q, EPS, wq, bin_[:C], 0, None, True, True)
+            hq, _LOOKAHEAD["have_q"] = _LOOKAHEAD["have_q"], None
+            if hq is not None and hq[4] is g_q and hq[0].data_ptr() == xq2.data_ptr() and hq[0].numel() == xq2.numel():
+                # LN + query projection computed by the producing self-attention block's last kernel
+                q, mean_q, rstd_q = hq[1:4]
+                ctx.q_handoff = True
+            else:
+                q, mean_q, rstd_q = K.ln_linear_fwd(xq2, g_q, b_q, EPS, wq, bin_[:C], 0, None, True, True)
             key = id(ps[0])
             ent = src.entries.get(key) if src is not None else None
             ctx.kv_owner = ent is None
@@ -576,7 +582,15 @@ class _LayerFn(torch.autograd.Function):
                 dq2, dres = dq.reshape(B * Nq, C), dy
             Ckv = g_kv.shape[0]
             Rq = dq2.shape[0]
-            if WGRAD_SLAB and Rq < TALL_ROWS:
+            if getattr(ctx, "q_handoff", False):
+                # the producing self-attention block runs this LN + query-projection backward
+                # fused with its last post-attention backward; dres stands in for dx_q (same
+                # shape, no fill launch) and is ignored by that block
+                _LOOKAHEAD["bwd_q"] = dict(key=xq2.data_ptr(), g=dq2.contiguous(), wq=wq, x=xq2, mean1=mean_q,
+                                           rstd1=rstd_q, lnw=g_q, lnb=b_q, dres=dres.contiguous(),
+                                           ll_dsts=[flat(g_q), flat(b_q), flat(ps[4], 0, C * C), flat(bin_, 0, C)])
+                dx_q = dres
+            elif WGRAD_SLAB and Rq < TALL_ROWS:
                 sl = _GradSlab(Rq, [C, C, C * C, C], dz2)
                 dx_q = K.ln_linear_bwd(dq2, wq, xq2, mean_q, rstd_q, g_q, b_q, dres, True, *sl.targets(), slab=True,
                                        **_take_job())
@@ -724,8 +738,16 @@ class _SABlockFn(torch.autograd.Function):
                         qkv, xl, N, scale, wo, bo, g2, be2, EPS, w1, b1, w2, b2, pn[0], pn[1], bws[i + 1][0], pn[3],
                         seed=seed, site=i, p=pdrop)
                 else:
-                    o, lse, z, y, m2, r2, u = K.sa_layer_fwd(qkv, xl, N, scale, wo, bo, g2, be2, EPS, w1, b1, w2, b2,
-                                                             seed=seed, site=i, p=pdrop)
+                    wantq, _LOOKAHEAD["want_q"] = _LOOKAHEAD["want_q"], None
+                    if wantq is not None:  # the following cross-attention layer's LN + query projection
+                        o, lse, z, y, m2, r2, u, qn, mq, rq = K.sa_layer_fwd(
+                            qkv, xl, N, scale, wo, bo, g2, be2, EPS, w1, b1, w2, b2, wantq[0], wantq[1], wantq[2],
+                            wantq[3], seed=seed, site=i, p=pdrop)
+                        _LOOKAHEAD["have_q"] = (z, qn, mq, rq, wantq[0])
+                        ctx.out_ptr = z.data_ptr()
+                    else:
+                        o, lse, z, y, m2, r2, u = K.sa_layer_fwd(qkv, xl, N, scale, wo, bo, g2, be2, EPS, w1, b1, w2,
+                                                                 b2, seed=seed, site=i, p=pdrop)
                     qkv_n = mean_n = rstd_n = None
                 saved += [xl, qkv, mean1, rstd1, o, lse, y, m2, r2, u]
                 xl, qkv, mean1, rstd1 = z, qkv_n, mean_n, rstd_n
@@ -784,9 +806,24 @@ class _SABlockFn(torch.autograd.Function):
         dz2 = dz.reshape(R, C)
         if not dz2.is_contiguous():
             dz2 = dz2.contiguous()
-        sl = _GradSlab(R, PA_SIZES(C), dz2)
-        dy, do, delta = K.post_attn_bwd(dz2, *pa_args(L - 1), H, sl.targets(), slab=True, **_take_job(), **drop(L - 1))
-        sl.defer(K, pa_dsts(P[L - 1]))
+        ho, _LOOKAHEAD["bwd_q"] = _LOOKAHEAD["bwd_q"], None
+        if ho is not None and ho["key"] != getattr(ctx, "out_ptr", None):
+            raise RuntimeError("fused encoder: a cross-attention layer handed its query-path backward to the wrong "
+                               "self-attention block")
+        if ho is not None:
+            # the next cross-attention layer's LN + query-projection backward (dX = this block's
+            # dZ) fused with the last layer's post-attention backward
+            sl = _GradSlab(R, [C, C, C * C, C] + PA_SIZES(C), dz2)
+            tg = sl.targets()
+            dy, do, delta = K.ln_linear_post_attn_bwd(ho["g"], ho["wq"], ho["x"], ho["mean1"], ho["rstd1"], ho["lnw"],
+                                                      ho["lnb"], ho["dres"], tg[:4], *pa_args(L - 1), H, tg[4:],
+                                                      **_take_job(), **drop(L - 1))
+            sl.defer(K, ho["ll_dsts"] + pa_dsts(P[L - 1]))
+        else:
+            sl = _GradSlab(R, PA_SIZES(C), dz2)
+            dy, do, delta = K.post_attn_bwd(dz2, *pa_args(L - 1), H, sl.targets(), slab=True, **_take_job(),
+                                            **drop(L - 1))
+            sl.defer(K, pa_dsts(P[L - 1]))
         dx = None
         for i in range(L - 1, -1, -1):
             xl, qkv, mean1, rstd1, o, lse, y, m2, r2, u = S[i]
@@ -822,7 +859,10 @@ class _SABlockFn(torch.autograd.Function):
 # cross layer's forward, which then runs post_attn + LN1/QKV in one launch and leaves
 # "have" = (z, qkv, mean1, rstd1, γ1) for the block's forward.  Backward, the block hands its first
 # LN1/QKV backward back ("bwd"), which the cross layer runs fused with its post-attention backward.
-_LOOKAHEAD = {"want": None, "have": None, "bwd": None}
+# The same in the other direction ("want_q" / "have_q" / "bwd_q"): a block's last fused layer
+# computes the next cross-attention layer's LN + query projection, and that layer hands the
+# backward of it back to the block.
+_LOOKAHEAD = {"want": None, "have": None, "bwd": None, "want_q": None, "have_q": None, "bwd_q": None}
 
 
 def _sa_block_plan(block, rows: int):
@@ -987,7 +1027,8 @@ def _encode(encoder, src: KVSource, pad_mask):
     lat = encoder.latent.unsqueeze(0)  # (1, N, C): projected once, broadcast inside the kernels
     b = src.x.shape[0]
     n = lat.shape[1]
-    for layer in encoder.layers():
+    layers = list(encoder.layers())
+    for li, layer in enumerate(layers):
         cross, block = layer[0], layer[1]
         if lat.shape[0] == 1 and not can_fuse(cross, src):
             lat = lat.expand(b, -1, -1)
@@ -999,8 +1040,23 @@ def _encode(encoder, src: KVSource, pad_mask):
             _LOOKAHEAD["want"] = None
         if lat.shape[0] == 1 and b > 1:
             lat = lat.expand(b, -1, -1)
+        nxt_cross = layers[li + 1][0] if li + 1 < len(layers) else None
+        if nxt_cross is not None and can_fuse(nxt_cross, src):
+            _LOOKAHEAD["want_q"] = cross_q_lookahead(nxt_cross, src)
         try:
             lat = self_attention_block(block, lat)
         finally:
-            _LOOKAHEAD["have"] = None
+            _LOOKAHEAD["have"] = _LOOKAHEAD["want_q"] = None
+    _LOOKAHEAD["have_q"] = None
     return lat
+
+
+def cross_q_lookahead(cross, src):
+    """(γq, βq, Wq bf16 (C, C), bq) of a cross-attention layer's query path, for the preceding
+    self-attention block's last kernel (C = 64, H = 4: the fused layer kernel's shape)."""
+    spec, ps = layer_spec_and_params(cross)
+    if not spec.cross or spec.C != 64 or spec.heads != 4:
+        return None
+    bw = _bf16_weights(spec, ps)
+    bin_ = ps[5] if spec.packed else ps[7]
+    return (ps[0], ps[1], bw[0], bin_[:spec.C])

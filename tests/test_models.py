@@ -262,52 +262,49 @@ def test_fused_executor_matches_eager_via_emulation(kind, slab, monkeypatch):
             assert (p.grad - g_ref[n]).abs().max() < 0.03 * gmax, n
 
 
-def test_cross_to_self_attention_boundary_fusion(monkeypatch):
-    """The cross-attention layer runs the next self-attention block's LN1/QKV forward in its
-    post-attention kernel, and that block hands its LN1/QKV backward back to the cross layer
-    (ln_linear_post_attn_bwd): same outputs / gradients as the unfused boundary."""
+@pytest.mark.parametrize("latents", [16, 64])
+def test_cross_self_attention_boundary_fusion(latents, monkeypatch):
+    """Layer-boundary fusion between the encoder's cross-attention layers and self-attention
+    blocks, both ways: a cross layer runs the next block's LN1/QKV in its post-attention kernel
+    and that block hands the LN1/QKV backward back to it; with 64 latents (the fused layer
+    kernel's shape) a block's last kernel also computes the next cross layer's LN + query
+    projection, whose backward comes back to the block.  Same outputs / gradients as unfused."""
     monkeypatch.setattr(ops.fused, "WGRAD_SLAB", True)
     torch.manual_seed(4)
-    m = mlm_model(layers=3, sa=2)
+    m = mlm_model(n=latents, layers=3, sa=2)
     enc = m.encoder
     x = torch.randint(3, 300, (3, 64))
     pad = torch.zeros(3, 64, dtype=torch.bool)
     pad[1, 40:] = True
+    emu = ops.emulation
+    calls = {}
+
+    class Counting:  # the executor's kernel calls (not the emulation's internal compositions)
+        def __getattr__(self, name):
+            calls[name] = calls.get(name, 0) + 1
+            return getattr(emu, name)
+
     w = None
     res = []
-    calls = {"fwd": 0, "bwd": 0}
-    emu = ops.emulation
-    f0, b0 = emu.post_attn_ln_linear_fwd, emu.ln_linear_post_attn_bwd
-
-    def fwd(*a, **k):
-        calls["fwd"] += 1
-        return f0(*a, **k)
-
-    def bwd(*a, **k):
-        calls["bwd"] += 1
-        return b0(*a, **k)
-
-    monkeypatch.setattr(emu, "post_attn_ln_linear_fwd", fwd)
-    monkeypatch.setattr(emu, "ln_linear_post_attn_bwd", bwd)
     for fuse in (False, True):
-        if not fuse:
-            monkeypatch.setattr(ops.fused, "sa_block_lookahead", lambda block, rows: None)
-        else:
-            monkeypatch.undo()
-            monkeypatch.setattr(ops.fused, "WGRAD_SLAB", True)
-            monkeypatch.setattr(emu, "post_attn_ln_linear_fwd", fwd)
-            monkeypatch.setattr(emu, "ln_linear_post_attn_bwd", bwd)
-        calls.update(fwd=0, bwd=0)
-        enc.zero_grad(set_to_none=True)
-        out = ops.fused.encoder_forward(enc, x, pad)
-        if w is None:
-            w = torch.randn_like(out)
-        (out * w).sum().backward()
-        res.append((out.detach(), {n: p.grad.clone() for n, p in enc.named_parameters() if p.grad is not None},
-                    dict(calls)))
+        with monkeypatch.context() as mp:
+            mp.setattr(ops.fused, "kernels", lambda t: Counting())
+            if not fuse:
+                mp.setattr(ops.fused, "sa_block_lookahead", lambda block, rows: None)
+                mp.setattr(ops.fused, "cross_q_lookahead", lambda cross, src: None)
+            calls.clear()
+            enc.zero_grad(set_to_none=True)
+            out = ops.fused.encoder_forward(enc, x, pad)
+            if w is None:
+                w = torch.randn_like(out)
+            (out * w).sum().backward()
+            res.append((out.detach(), {n: p.grad.clone() for n, p in enc.named_parameters() if p.grad is not None},
+                        dict(calls)))
     (o0, g0, c0), (o1, g1, c1) = res
-    # 3 layers: each cross layer fuses the block's first LN1/QKV (forward and backward)
-    assert c1["fwd"] - c0["fwd"] == 3 and c1["bwd"] - c0["bwd"] == 3, (c0, c1)
+    # 3 cross → block boundaries (+ 2 block → cross boundaries with the fused layer kernel)
+    k = 3 + (2 if latents == 64 else 0)
+    assert c0["ln_linear_fwd"] - c1["ln_linear_fwd"] == k, (c0, c1)
+    assert c1["ln_linear_post_attn_bwd"] - c0.get("ln_linear_post_attn_bwd", 0) == k, (c0, c1)
     torch.testing.assert_close(o1, o0, rtol=1e-5, atol=1e-5)
     assert set(g0) == set(g1)
     for n in g0:
