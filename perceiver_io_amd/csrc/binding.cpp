@@ -532,7 +532,7 @@ std::vector<Tensor> ln_linear_post_attn_bwd(Tensor g, Tensor wq, Tensor x, Tenso
   TORCH_CHECK(y.is_contiguous() && u.is_contiguous() && o.is_contiguous() && x.is_contiguous() && dres.is_contiguous(),
               "operands must be contiguous (R, C)");
   const int R = (int)y.size(0), C = (int)y.size(1);
-  TORCH_CHECK(C == 32 || C == 64, "the fused self-attention backward supports C in {32, 64}");
+  TORCH_CHECK(C == 32 || C == 64 || C == 128, "the fused self-attention backward supports C in {32, 64, 128}");
   TORCH_CHECK(H > 0 && C % H == 0, "heads must divide C");
   const int nq = (int)wq.size(0);  // 3C: packed QKV of a self-attention layer; C: a cross-attention query projection
   TORCH_CHECK(wq.is_contiguous() && (nq == 3 * C || nq == C) && wq.size(1) == C, "wq must be (3C, C) or (C, C)");

@@ -1612,6 +1612,8 @@ void ln_linear_post_attn_bwd_launch(int C, const float* G, const uint16_t* Wq, c
                           be2, dY, dO, delta, H, grads, R, job, dr)
   if (C == 64 && nq == 3 * C) { LPB(64, 3); }
   else if (C == 64) { LPB(64, 1); }
+  else if (C == 128 && nq == 3 * C) { LPB(128, 3); }
+  else if (C == 128) { LPB(128, 1); }
   else if (nq == 3 * C) { LPB(32, 3); }
   else { LPB(32, 1); }
 #undef LPB

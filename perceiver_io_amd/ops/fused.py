@@ -685,6 +685,9 @@ SA_LAYER_FUSED = os.environ.get("PERCEIVER_SA_LAYER_FUSED", "1") != "0"
 PA_SIZES = lambda C: [C * C, C, C, C, C * C, C, C * C, C]  # noqa: E731  (Wo bo γ2 β2 W1 b1 W2 b2)
 LL_SIZES = lambda C: [C, C, 3 * C * C, 3 * C]                 # noqa: E731  (γ1 β1 Wqkv bqkv)
 SA_NP = 12  # parameters per self-attention layer (layer_spec_and_params order)
+# channel widths run as one fused self-attention block node (PERCEIVER_SA_BLOCK_C128=0 keeps C = 128
+# stacks layer by layer)
+SA_BLOCK_CHANNELS = (32, 64, 128) if os.environ.get("PERCEIVER_SA_BLOCK_C128", "1") != "0" else (32, 64)
 
 
 class _SABlockFn(torch.autograd.Function):
@@ -874,7 +877,7 @@ def _sa_block_plan(block, rows: int):
         specs.append(spec)
         pss.append(ps)
     ok = (WGRAD_SLAB and len(layers) > 1 and all(_fusable(lay) for lay in layers)
-          and all(sp == specs[0] for sp in specs) and specs[0].C in (32, 64) and not specs[0].cross
+          and all(sp == specs[0] for sp in specs) and specs[0].C in SA_BLOCK_CHANNELS and not specs[0].cross
           and rows < TALL_ROWS)
     return layers, specs, pss, ok
 
