@@ -115,8 +115,18 @@ class PerceiverDecoder(nn.Module):
         first ``num_queries`` queries (queries are independent of each other)."""
         x = bucket_ready_point(x)  # DDP: decoder grads final here → early bucket (parallel/reducer.py)
         self.check_latent(x)
-        q = self.output if num_queries is None else self.output[:num_queries]
-        return self.cross_attention(q.unsqueeze(0).expand(x.shape[0], -1, -1), x)
+        q = (self.output if num_queries is None else self.output[:num_queries]).unsqueeze(0)
+        ca = self.cross_attention
+        if ca._fusable(x, None) and ops.fused.can_fuse(ca, x):
+            # one query stream broadcast over the batch inside the fused kernels: the query
+            # gradient comes back summed over the batch (no expand / slice backward glue)
+            return ca(q, x)
+        return ca(q.expand(x.shape[0], -1, -1), x)
+
+    def loss(self, x_latent, labels):
+        """Mean cross-entropy of the output adapter's logits against ``labels`` (classification
+        adapters); on the GPU through the fused vocab-projection + CE kernels (no logits tensor)."""
+        return ops.mlm_head.classification_loss(self, x_latent, labels)
 
     def hidden_at(self, x, idx):
         """Decoder output at output-query rows ``idx`` (B, K') only, ``(B, K', C_out)``: queries
@@ -136,6 +146,12 @@ class PerceiverDecoder(nn.Module):
 class PerceiverIO(Sequential):
     def __init__(self, encoder: PerceiverEncoder, decoder: PerceiverDecoder):
         super().__init__(encoder, decoder)
+
+    def loss(self, x, labels, pad_mask=None):
+        """Training loss of a classifier: ``cross_entropy(self(x, pad_mask), labels)`` computed
+        through the decoder's fused head (same value and gradients)."""
+        x_latent, _ = self.encoder(x, pad_mask)
+        return self.decoder.loss(x_latent, labels)
 
     @property
     def encoder(self) -> PerceiverEncoder:

@@ -294,3 +294,23 @@ def masked_decode_loss(decoder, x_latent: torch.Tensor, labels: torch.Tensor, p:
     q = _GatherQueries.apply(decoder.output, idx.reshape(-1)).view(B, cap, -1)
     h = decoder.cross_attention(q, x_latent)
     return compact_lm_loss(h, labels_c, count, lin.weight, lin.bias, B * L, p)
+
+
+def classification_loss(decoder, x_latent: torch.Tensor, labels: torch.Tensor):
+    """``cross_entropy(decoder(x_latent), labels)`` for a one-query classification decoder
+    (``ClassificationOutputAdapter``, reference ``perceiver/adapter.py:138-143`` +
+    ``lightning.py:61-66``).  HIP path: the class projection and the softmax cross-entropy run
+    in the fused CE kernels over the decoder's (B, C) output rows — no logits tensor and no
+    framework GEMM / reduction kernels; mean over the labels that are not ``-100``."""
+    from . import use_hip
+
+    h = decoder.hidden(x_latent)
+    ad = decoder.output_adapter
+    lin = getattr(ad, "linear", None)
+    if (lin is not None and use_hip(h) and h.dim() == 3 and h.shape[1] == 1 and h.shape[-1] in (32, 64, 128)
+            and labels.dim() == 1 and labels.shape[0] == h.shape[0]):
+        lab = labels.to(torch.int64).contiguous()
+        cnt = (lab >= 0).sum(dtype=torch.float32).reshape(1)
+        return _MaskedCE.apply(h, lin.weight, lin.bias, None, lab, cnt)
+    return F.cross_entropy(ad(h).float(), labels)
+

@@ -150,6 +150,52 @@ def test_image_classifier_fused_matches_eager():
     _three_way(lit, run, jitter_run=lambda: run(xj))
 
 
+@pytest.mark.parametrize("kind", ["image", "text"])
+def test_classifier_fused_head_loss(kind):
+    """PerceiverIO.loss through the fused CE head (ce_fwd / ce_bwd over the decoder rows, the
+    query stream broadcast inside the fused decoder layer) vs the same loss in fp32 eager maths
+    (= cross_entropy of the logits) and vs the kernels' emulation: loss and every gradient."""
+    import torch.nn.functional as F
+
+    from perceiver_io_amd import ops
+    from perceiver_io_amd.tasks import LitImageClassifier, LitTextClassifier
+
+    torch.manual_seed(2)
+    opt = {"class_path": "torch.optim.AdamW", "init_args": {"lr": 1e-3}}
+    if kind == "image":
+        lit = LitImageClassifier(image_shape=(28, 28, 1), num_classes=10, optimizer_init=opt, num_latents=32,
+                                 num_latent_channels=128, num_encoder_layers=2,
+                                 num_encoder_self_attention_layers_per_block=2,
+                                 num_decoder_cross_attention_heads=1).cuda()
+        args = (torch.randn(6, 28, 28, 1, device="cuda"),)
+        y = torch.randint(0, 10, (6,), device="cuda")
+    else:
+        lit = LitTextClassifier(num_classes=2, vocab_size=300, max_seq_len=64, optimizer_init=opt, num_latents=64,
+                                num_latent_channels=64, num_encoder_layers=2,
+                                num_encoder_self_attention_layers_per_block=2,
+                                num_decoder_cross_attention_heads=1).cuda()
+        ids = torch.randint(3, 300, (6, 64), device="cuda")
+        pad = torch.zeros(6, 64, dtype=torch.bool, device="cuda")
+        pad[2, 40:] = True
+        args = (ids, pad)
+        y = torch.randint(0, 2, (6,), device="cuda")
+    m = lit.model
+    with ops.backend("torch"):  # the fused head's value = cross_entropy of the logits
+        ref = F.cross_entropy(m(*args).float(), y).item()
+    assert abs(m.loss(args[0], y, *args[1:]).item() - ref) < 1e-2 * max(1.0, abs(ref))
+
+    def run(a0=args[0]):
+        loss = m.loss(a0, y, *args[1:])
+        loss.backward()
+        return loss
+
+    jit = None
+    if kind == "image":  # conditioning floor of the decoder query-LN affine (see _three_way)
+        xj = args[0] * (1 + 1e-6 * torch.randn_like(args[0]))
+        jit = lambda: run(xj)  # noqa: E731
+    _three_way(m, run, jitter_run=jit)
+
+
 def test_image_classifier_replicated_flat_grads_match_eager():
     """Separate q/k/v projections (Cin ≠ C) with the flat space's replicated accumulators."""
     from perceiver_io_amd import ops

@@ -384,3 +384,28 @@ def test_factored_pe_projection_matches_autograd(channels):
     from perceiver_io_amd.ops import emulation
 
     check_factored_pe_projection(emulation, "cpu", channels)
+
+
+def test_classifier_loss_matches_logits_cross_entropy():
+    """PerceiverIO.loss (the fused-head entry point) equals cross_entropy of the logits, value and
+    gradients, for image and text classifiers (CPU: the eager path; GPU coverage in
+    tests/test_model_gpu.py)."""
+    import torch.nn.functional as F
+
+    from perceiver_io_amd.models import ClassificationOutputAdapter
+
+    torch.manual_seed(6)
+    m = mnist_model(latents=8, c=64, layers=2, sa=2)
+    x = torch.randn(3, 28, 28, 1)
+    y = torch.tensor([1, 7, 3])
+    ref = F.cross_entropy(m(x).float(), y)
+    ref.backward()
+    g = {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+    m.zero_grad()
+    out = m.loss(x, y)
+    out.backward()
+    torch.testing.assert_close(out, ref)
+    for n, p in m.named_parameters():
+        if n in g:
+            torch.testing.assert_close(p.grad, g[n], msg=n)
+    assert isinstance(m.decoder.output_adapter, ClassificationOutputAdapter)
