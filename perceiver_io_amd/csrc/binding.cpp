@@ -85,7 +85,10 @@ void mlm_select_launch(const int64_t*, int, int, int, int, int64_t*, int64_t*, i
                        const float*, int, float*, unsigned*, hipStream_t);
 void ce_bwd_launch(int, const uint16_t*, const int64_t*, const uint16_t*, const float*, const float*, const float*,
                    const float*, int, int, float*, long long, const int64_t*, float*, float*, int, float*, int, hipStream_t);
-void embed_fwd_launch(const int64_t*, const float*, const float*, float*, long long, int, int, float, hipStream_t);
+void embed_fwd_launch(const int64_t*, const float*, const float*, float*, long long, int, int, float, long long,
+                      hipStream_t);
+unsigned check_errors_elementwise(bool);
+unsigned check_errors_mlm_head(bool);
 void embed_bwd_launch(const int64_t*, const float*, float*, float*, int, int, int, float, hipStream_t);
 void embed_bwd_sorted_launch(const int64_t*, const int64_t*, const float*, float*, long long, int, float, hipStream_t);
 bool embed_bwd_local_launch(const int64_t*, const float*, float*, float*, int, int, int, float, hipStream_t);
@@ -143,6 +146,29 @@ using OptT = c10::optional<Tensor>;
 
 namespace {
 hipStream_t stream() { return at::hip::getCurrentHIPStream(); }
+
+#ifndef PIO_CHECKS
+#define PIO_CHECKS 0
+#endif
+// checked builds: the device error words of every checked translation unit (bit 1: a token id
+// outside the embedding table, 2: a gather row outside its destination, 4: a class label
+// outside [0, V) ∪ {-100}); reset clears them
+int64_t check_errors(bool reset) {
+  return (int64_t)(pio::check_errors_elementwise(reset) | pio::check_errors_mlm_head(reset));
+}
+bool checked_build() { return PIO_CHECKS != 0; }
+// checked builds, outside graph capture: wait for the kernel just launched and raise on any
+// device-side index violation (the kernel itself clamped / skipped the access)
+void checked_sync(const char* what) {
+  if (!PIO_CHECKS) return;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing(stream(), &cs);
+  if (cs != hipStreamCaptureStatusNone) return;
+  (void)hipStreamSynchronize(stream());
+  const int64_t e = check_errors(true);
+  TORCH_CHECK(e == 0, "checked build: ", what, " saw out-of-range indices (error bits ", e,
+              ": 1 token id >= vocab, 2 gather row out of range, 4 label outside [0, V) and != -100)");
+}
 
 // deterministic mode (trainer flag ``deterministic``): every reduction that would
 // use fp32 atomics with several writers per address runs as a fixed-order split reduction
@@ -733,6 +759,7 @@ std::vector<Tensor> ce_fwd(Tensor h, OptT idx, Tensor labels, Tensor w, Tensor b
                      part.data_ptr<float>(), picked.data_ptr<float>(), lse.data_ptr<float>(), f32p(count),
                      loss.data_ptr<float>(), blk.data_ptr<float>(), reinterpret_cast<unsigned*>(tk.data_ptr<int>()),
                      bfp_mut(hs), ns, zp, zn, stream());
+  checked_sync("ce_fwd");
   return {loss, lse, hs};
 }
 
@@ -775,7 +802,9 @@ Tensor embed_fwd(Tensor ids, Tensor E, Tensor P, double scale) {
   const int L = (int)ids.size(1), C = (int)E.size(1);
   TORCH_CHECK(C % 4 == 0, "embedding width must be a multiple of 4");
   Tensor out = torch::empty({ids.size(0), L, C}, E.options());
-  pio::embed_fwd_launch(ids.data_ptr<int64_t>(), f32p(E), f32p(P), out.data_ptr<float>(), rows, L, C, (float)scale, stream());
+  pio::embed_fwd_launch(ids.data_ptr<int64_t>(), f32p(E), f32p(P), out.data_ptr<float>(), rows, L, C, (float)scale,
+                        E.size(0), stream());
+  checked_sync("embed_fwd");
   return out;
 }
 
@@ -881,6 +910,7 @@ void index_add_rows(Tensor dst, Tensor idx, Tensor src) {
   if (src.size(0) == 0) return;
   pio::index_add_rows_launch(dst.data_ptr<float>(), dst.size(0), idx.data_ptr<int64_t>(), f32p(src), src.size(0),
                              (int)src.size(1), stream());
+  checked_sync("index_add_rows");
 }
 
 namespace {
@@ -1137,6 +1167,8 @@ bool get_deterministic() { return g_det; }
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_deterministic", &set_deterministic);
+  m.def("check_errors", &check_errors, py::arg("reset") = true);
+  m.def("checked_build", &checked_build);
   m.def("get_deterministic", &get_deterministic);
   m.doc() = "Perceiver IO CDNA4 (gfx950) kernels";
   m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("kmask"), py::arg("H"), py::arg("D"),

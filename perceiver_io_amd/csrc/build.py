@@ -48,32 +48,39 @@ def _digest(paths, flags):
     return h.hexdigest()[:16]
 
 
-def ext_path() -> Path:
+def ext_path(name: str = "_C") -> Path:
     suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
-    return PKG / f"_C{suffix}"
+    return PKG / f"{name}{suffix}"
 
 
-def build(force: bool = False, jobs: int = 0, debug: bool = False, verbose: bool = True) -> Path:
-    BUILD.mkdir(parents=True, exist_ok=True)
+def build(force: bool = False, jobs: int = 0, debug: bool = False, verbose: bool = True, check: bool = False) -> Path:
+    """check=True: the checked variant ``_C_check`` (device-side index validation with clamping and
+    error words, PIO_CHECKS=1; host binding under UBSan), loaded instead of ``_C`` when
+    ``PERCEIVER_CHECKED=1``."""
+    bdir = BUILD / "check" if check else BUILD  # separate object caches per variant
+    bdir.mkdir(parents=True, exist_ok=True)
     headers = sorted(HERE.glob("*.h"))
     hip_srcs = sorted(HERE.glob("*.hip"))
     opt = ["-O0", "-g"] if debug else ["-O3"]
     hip_flags = [f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-ffp-contract=fast", "-munsafe-fp-atomics",
-                 "-Wno-unused-result"] + opt
+                 "-Wno-unused-result"] + opt + (["-DPIO_CHECKS=1"] if check else [])
     objs = []
     todo = []
     for src in hip_srcs:
-        obj = BUILD / f"{src.stem}.{_digest([src] + headers, hip_flags)}.o"
+        obj = bdir / f"{src.stem}.{_digest([src] + headers, hip_flags)}.o"
         objs.append(obj)
         if force or not obj.exists():
             todo.append([HIPCC, *hip_flags, "-I", str(HERE), "-c", str(src), "-o", str(obj)])
     inc, libdir = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
+    name = "_C_check" if check else "_C"
+    san = ["-DPIO_CHECKS=1", "-fsanitize=undefined", "-fno-omit-frame-pointer"] if check else []
     cxx_flags = ["-O2", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
-                 "-DTORCH_API_INCLUDE_EXTENSION_H", "-DTORCH_EXTENSION_NAME=_C", "-D_GLIBCXX_USE_CXX11_ABI=1",
+                 "-DTORCH_API_INCLUDE_EXTENSION_H", f"-DTORCH_EXTENSION_NAME={name}", "-D_GLIBCXX_USE_CXX11_ABI=1",
+                 *san,
                  "-isystem", "/opt/rocm/include", "-isystem", py_inc] + sum((["-isystem", p] for p in inc), [])
     bsrc = HERE / "binding.cpp"
-    bobj = BUILD / f"binding.{_digest([bsrc], cxx_flags)}.o"
+    bobj = bdir / f"binding.{_digest([bsrc], cxx_flags)}.o"
     if force or not bobj.exists():
         todo.append(["g++", *cxx_flags, "-c", str(bsrc), "-o", str(bobj)])
     if todo:
@@ -82,8 +89,9 @@ def build(force: bool = False, jobs: int = 0, debug: bool = False, verbose: bool
             print(f"[perceiver_io_amd] compiling {len(todo)} translation unit(s) for {ARCH} with {n} job(s)")
         with ThreadPoolExecutor(max_workers=n) as ex:
             list(ex.map(_run, todo))
-    out = ext_path()
-    link = ["g++", "-shared", "-o", str(out), str(bobj), *map(str, objs), f"-L{libdir}", "-L/opt/rocm/lib",
+    out = ext_path(name)
+    link = ["g++", "-shared", *(["-fsanitize=undefined"] if check else []), "-o", str(out), str(bobj),
+            *map(str, objs), f"-L{libdir}", "-L/opt/rocm/lib",
             "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lamdhip64", "-lc10_hip", "-ltorch_hip",
             f"-Wl,-rpath,{libdir}", "-Wl,-rpath,/opt/rocm/lib"]
     newest = max(p.stat().st_mtime for p in objs + [bobj])
@@ -92,7 +100,7 @@ def build(force: bool = False, jobs: int = 0, debug: bool = False, verbose: bool
         if verbose:
             print(f"[perceiver_io_amd] linked {out.relative_to(PKG.parent)}")
     keep = {p.name for p in objs + [bobj]}
-    for stale in BUILD.glob("*.o"):  # objects of superseded sources (the cache holds the current ones)
+    for stale in bdir.glob("*.o"):  # objects of superseded sources (the cache holds the current ones)
         if stale.name not in keep:
             stale.unlink()
     return out
@@ -103,8 +111,9 @@ def main(argv=None):
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--jobs", type=int, default=0)
     ap.add_argument("--debug", action="store_true")
+    ap.add_argument("--check", action="store_true", help="build the checked variant _C_check")
     a = ap.parse_args(argv)
-    build(force=a.force, jobs=a.jobs, debug=a.debug)
+    build(force=a.force, jobs=a.jobs, debug=a.debug, check=a.check)
 
 
 if __name__ == "__main__":

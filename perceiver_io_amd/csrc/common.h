@@ -15,6 +15,34 @@
 
 namespace pio {
 
+// ---- checked builds (python -m perceiver_io_amd.csrc.build --check → _C_check) ------------
+// Index operands that come from user data (token ids, class labels, gather rows) are validated
+// on the device: a violation sets a bit in this translation unit's error word (read and cleared
+// by ext.check_errors()) and the access is clamped / skipped instead of faulting.  Release
+// builds compile the checks out.
+#ifndef PIO_CHECKS
+#define PIO_CHECKS 0
+#endif
+enum : unsigned { kErrEmbedId = 1u, kErrGatherRow = 2u, kErrLabel = 4u };
+static __device__ unsigned pio_errors;
+__device__ __forceinline__ void pio_flag(unsigned bit) {
+#if PIO_CHECKS
+  atomicOr(&pio_errors, bit);
+#else
+  (void)bit;
+#endif
+}
+// this TU's error word (host side), optionally cleared
+static inline unsigned pio_read_errors(bool reset) {
+  unsigned h = 0;
+  (void)hipMemcpyFromSymbol(&h, HIP_SYMBOL(pio_errors), sizeof(h), 0, hipMemcpyDeviceToHost);
+  if (reset) {
+    const unsigned z = 0;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(pio_errors), &z, sizeof(z), 0, hipMemcpyHostToDevice);
+  }
+  return h;
+}
+
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef short bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));

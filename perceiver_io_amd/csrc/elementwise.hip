@@ -17,13 +17,21 @@ namespace pio {
 // out[r, c] = E[ids[r], c] * scale + P[r % L, c]     (fp32), float4 vectorised over c
 __global__ void embed_fwd_kernel(const int64_t* __restrict__ ids, const float* __restrict__ E,
                                  const float* __restrict__ P, float* __restrict__ out, long long rows, int L, int C,
-                                 float scale) {
+                                 float scale, long long V) {
   const int c4 = C / 4;
   const long long n = rows * c4;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     const long long r = i / c4;
     const int c = (int)(i % c4) * 4;
-    const int64_t id = ids[r];
+    int64_t id = ids[r];
+#if PIO_CHECKS
+    if (id < 0 || id >= V) {
+      pio_flag(kErrEmbedId);
+      id = id < 0 ? 0 : V - 1;
+    }
+#else
+    (void)V;
+#endif
     const float4 e = *reinterpret_cast<const float4*>(E + id * C + c);
     const float4 p = *reinterpret_cast<const float4*>(P + (r % L) * C + c);
     *reinterpret_cast<float4*>(out + r * C + c) =
@@ -292,8 +300,8 @@ static dim3 grid_for(long long n, int per = 256) {
 }
 
 void embed_fwd_launch(const int64_t* ids, const float* E, const float* P, float* out, long long rows, int L, int C,
-                      float scale, hipStream_t st) {
-  hipLaunchKernelGGL(embed_fwd_kernel, grid_for(rows * C / 4), dim3(256), 0, st, ids, E, P, out, rows, L, C, scale);
+                      float scale, long long V, hipStream_t st) {
+  hipLaunchKernelGGL(embed_fwd_kernel, grid_for(rows * C / 4), dim3(256), 0, st, ids, E, P, out, rows, L, C, scale, V);
 }
 void embed_bwd_launch(const int64_t* ids, const float* g, float* dE, float* dP, int B, int L, int C, float scale,
                       hipStream_t st) {
@@ -342,6 +350,9 @@ __global__ void index_add_rows_kernel(float* __restrict__ dst, long long nrows, 
     const long long r = i / c4;
     const int c = (int)(i - r * c4) * 4;
     const long long d = idx[r];
+#if PIO_CHECKS
+    if (d < 0 || d >= nrows) pio_flag(kErrGatherRow);
+#endif
     const float4 v = *reinterpret_cast<const float4*>(src + r * C + c);
     // all-zero quads (padding rows of a fixed-capacity gather) skip their atomics: padding
     // slots often share one destination row, whose serialised atomics would dominate
@@ -519,3 +530,8 @@ int stage_step_launch(void* const* dst, const void* const* src, const long long*
   return 0;
 }
 }  // namespace pio
+
+namespace pio {
+unsigned check_errors_elementwise(bool reset) { return pio_read_errors(reset); }
+}  // namespace pio
+

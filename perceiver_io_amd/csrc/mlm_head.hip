@@ -151,6 +151,9 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ H
   }
   const int rl = 32 * (w >> 1) + (l & 31), gr = m0 + rl;
   const int lab = gr < M ? (int)labels[gr] : -100;
+#if PIO_CHECKS
+  if (split == 0 && (w & 1) == 0 && (lab >= V || (lab < 0 && lab != -100))) pio_flag(kErrLabel);
+#endif
   float m = -1e30f, s = 0.f;  // log2-domain running max / sum of 2^(t - m) over this lane's logits
   bf16x8 wr[C / 32];
   float bnext = 0.f;
@@ -934,3 +937,8 @@ void ce_bwd_launch(int C, const uint16_t* Hm, const int64_t* labels, const uint1
 }
 
 }  // namespace pio
+
+namespace pio {
+unsigned check_errors_mlm_head(bool reset) { return pio_read_errors(reset); }
+}  // namespace pio
+

@@ -8,6 +8,7 @@ tensor reaches a fused op: a missing extension is an error.
 from __future__ import annotations
 
 import importlib
+import os
 
 _mod = None
 _err: Exception | None = None
@@ -18,7 +19,10 @@ def _load():
     if _mod is not None or _err is not None:
         return _mod
     try:
-        _mod = importlib.import_module("perceiver_io_amd._C")
+        # PERCEIVER_CHECKED=1: the checked build (device-side index validation, see csrc/build.py)
+        name = "perceiver_io_amd._C_check" if os.environ.get("PERCEIVER_CHECKED", "0") not in ("", "0") \
+            else "perceiver_io_amd._C"
+        _mod = importlib.import_module(name)
     except Exception as e:  # pragma: no cover - depends on build state
         _err = e
     return _mod

@@ -220,3 +220,18 @@ def test_lartpc_run_gpu(tmp_path):
               "--max-steps", "2", "--log-dir", str(tmp_path / "runs"), "--ckpt-dir", str(ck), "--device", "cuda"])
     state = torch.load(ck / "model_0.ckpt", weights_only=True)
     assert all(torch.isfinite(v).all() for v in state["model_state_dict"].values() if v.is_floating_point())
+
+
+def test_checked_variant_is_built_and_flagged():
+    """build.py --check produces _C_check (PIO_CHECKS=1, host binding under UBSan) next to the
+    release _C; each reports which it is (the loader picks _C_check with PERCEIVER_CHECKED=1)."""
+    import importlib
+
+    import pytest
+
+    try:
+        rel = importlib.import_module("perceiver_io_amd._C")
+        chk = importlib.import_module("perceiver_io_amd._C_check")
+    except ImportError as e:  # pragma: no cover - depends on the build state
+        pytest.skip(f"extension not built: {e}")
+    assert not rel.checked_build() and chk.checked_build()

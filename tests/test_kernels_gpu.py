@@ -698,3 +698,48 @@ def test_sa_layer_fwd_fused(B, N, nxt):
     for u, v, n in zip(a, e, names):
         # the next layer's LN1 statistics come from z, after the bf16 GEMM chain: 1 %
         close(u, v, 1e-3 if n in ("lse", "mean2", "rstd2") else 1e-2 if n in ("mean1", "rstd1") else 2e-2, n)
+
+
+_CHECKED_PROBE = r"""
+import torch
+from perceiver_io_amd.ops import ext
+K = ext.require()
+assert K.checked_build() and K.__name__.endswith("_C_check"), K.__name__
+dev = "cuda"
+E, P = torch.randn(50, 64, device=dev), torch.randn(8, 64, device=dev)
+ok = K.embed_fwd(torch.randint(0, 50, (2, 8), device=dev), E, P, 1.0)
+assert K.check_errors(True) == 0
+out = []
+for name, fn in (
+        ("embed", lambda: K.embed_fwd(torch.tensor([[3, 50, 1, 2, 0, 0, 0, 0]], device=dev), E, P, 1.0)),
+        ("label", lambda: K.ce_fwd(torch.randn(4, 64, device=dev), None, torch.tensor([1, 2, 1000, -100], device=dev),
+                                   torch.randn(100, 64, device=dev).to(torch.bfloat16), torch.zeros(100, device=dev),
+                                   torch.tensor([3.0], device=dev))),
+        ("gather", lambda: K.index_add_rows(torch.zeros(10, 64, device=dev), torch.tensor([1, 12], device=dev),
+                                            torch.ones(2, 64, device=dev)))):
+    try:
+        fn()
+        out.append((name, "no error"))
+    except RuntimeError as e:
+        out.append((name, "checked build" in str(e)))
+torch.cuda.synchronize()
+print(out)
+assert all(r is True for _, r in out), out
+assert K.check_errors(True) == 0
+print("CHECKED_OK")
+"""
+
+
+def test_checked_build_flags_out_of_range_indices():
+    """The checked variant (build.py --check → _C_check, PERCEIVER_CHECKED=1) validates token ids,
+    class labels and gather rows on the device: the access is clamped / skipped and the call
+    raises; valid inputs pass.  Runs in a child process (the loaded variant is process-wide)."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PERCEIVER_CHECKED="1", PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-c", _CHECKED_PROBE], env=env, capture_output=True, text=True, timeout=240,
+                       cwd=root)
+    assert r.returncode == 0 and "CHECKED_OK" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
