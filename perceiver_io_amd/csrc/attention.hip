@@ -697,13 +697,10 @@ static bool getenv_flag(const char* name) {
   return cached == 1;
 }
 
-template <int D, int NW>
-static void bwd_launch_t(const AttnArgs& a, const uint16_t* dO, const float* LSE, float* delta, float* dq,
-                         long long dq_bs, int dq_rs, float* dk, long long dk_bs, int dk_rs, float* dv, long long dv_bs,
-                         int dv_rs, int kv_acc, long long dq_kbs, int qsplit_ok, int dq_zeroed, hipStream_t st) {
-  const int nkb = (a.Nk + 32 * NW - 1) / (32 * NW);
-  // query splits when key blocks × heads × batch leave the GPU idle (≥ 4 query tiles each)
-  const int nqt = (a.Nq + 31) / 32, base = nkb * a.H * a.B;
+// query splits of the backward grid when key blocks × heads × batch leave the GPU idle (≥ 4
+// query tiles each; no empty split)
+static int bwd_query_splits(int nkb, int H, int B, int Nq, int qsplit_ok) {
+  const int nqt = (Nq + 31) / 32, base = nkb * H * B;
   int nqs = 1;
   if (qsplit_ok && base < 256 && nqt >= 8) {
     nqs = (512 + base - 1) / base;
@@ -711,8 +708,28 @@ static void bwd_launch_t(const AttnArgs& a, const uint16_t* dO, const float* LSE
     nqs = nqs < cap ? nqs : cap;
   }
   const int tps = (nqt + nqs - 1) / nqs;
-  nqs = (nqt + tps - 1) / tps;  // no empty split
-  if (nqs > 1 && !kv_acc) {      // the splits add into dK / dV
+  return (nqt + tps - 1) / tps;
+}
+
+// which accumulators a (non-deterministic, non-accumulating) backward launch clears itself:
+// bit 0 dQ (several key blocks add into it), bit 1 dK / dV (query splits add into them) — a
+// caller that clears them on the way (a SlabJob zero span of the previous kernel) passes the
+// same bits back as dq_zeroed
+int attn_bwd_zero_plan(int B, int H, int Nq, int Nk, int D) {
+  const int nw = D <= 32 ? 8 : 4;
+  const int nkb = (Nk + 32 * nw - 1) / (32 * nw);
+  return (nkb > 1 ? 1 : 0) | (bwd_query_splits(nkb, H, B, Nq, 1) > 1 ? 2 : 0);
+}
+
+template <int D, int NW>
+static void bwd_launch_t(const AttnArgs& a, const uint16_t* dO, const float* LSE, float* delta, float* dq,
+                         long long dq_bs, int dq_rs, float* dk, long long dk_bs, int dk_rs, float* dv, long long dv_bs,
+                         int dv_rs, int kv_acc, long long dq_kbs, int qsplit_ok, int dq_zeroed, hipStream_t st) {
+  const int nkb = (a.Nk + 32 * NW - 1) / (32 * NW);
+  const int nqt = (a.Nq + 31) / 32;
+  const int nqs = bwd_query_splits(nkb, a.H, a.B, a.Nq, qsplit_ok);
+  const int tps = (nqt + nqs - 1) / nqs;
+  if (nqs > 1 && !kv_acc && !(dq_zeroed & 2)) {  // the splits add into dK / dV (bit 1: cleared by the caller)
     const long long total = (long long)a.B * a.Nk * a.H * D;
     const unsigned zb = (unsigned)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
     hipLaunchKernelGGL(zero_rows_kernel, dim3(zb), dim3(256), 0, st, dk, dk_bs, dk_rs, a.Nk, a.H * D, total);
@@ -721,7 +738,7 @@ static void bwd_launch_t(const AttnArgs& a, const uint16_t* dO, const float* LSE
   // several key blocks add into dQ (fp32 atomics), unless each stores its own partial slice
   // (deterministic mode: dq_kbs > 0, summed by the caller)
   const int atomic = nkb > 1 && dq_kbs == 0;
-  if (atomic && !dq_zeroed) {
+  if (atomic && !(dq_zeroed & 1)) {
     const long long total = (long long)a.B * a.Nq * a.H * D;
     hipLaunchKernelGGL(zero_rows_kernel, dim3((unsigned)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096)), dim3(256), 0,
                        st, dq, dq_bs, dq_rs, a.Nq, a.H * D, total);

@@ -45,6 +45,7 @@ void attn_fwd_launch(const AttnArgs&, int, uint16_t*, float*, float*, float*, in
 void attn_bwd_launch(const AttnArgs&, int, const uint16_t*, const uint16_t*, const float*, float*, float*, long long,
                      int, float*, long long, int, float*, long long, int, bool, bool, long long, int, int, hipStream_t);
 int attn_bwd_key_blocks(int, int);
+int attn_bwd_zero_plan(int, int, int, int, int);
 void ln_linear_fwd_launch(const void*, bool, int, int, int, const float*, const float*, float, const uint16_t*, int,
                           const float*, int, int, const float*, int, void*, bool, int, float*, float*, const float*, int,
                           int, int, hipStream_t);
@@ -274,7 +275,8 @@ std::vector<Tensor> attn_fwd(Tensor q, Tensor k, Tensor v, OptT kmask, int64_t H
 // skips the delta pass.
 std::vector<Tensor> attn_bwd(Tensor q, Tensor k, Tensor v, OptT kmask, Tensor o, Tensor dO, Tensor lse, OptT delta_in,
                              int64_t H, int64_t D, double scale, double dropout_p, OptT seed, OptT dq_out,
-                             OptT dk_out, OptT dv_out, bool kv_accumulate, int64_t site, bool dq_zeroed) {
+                             OptT dk_out, OptT dv_out, bool kv_accumulate, int64_t site, bool dq_zeroed,
+                             bool kv_zeroed) {
   auto a = make_args(q, k, v, kmask, (int)H, (int)D, scale, dropout_p, seed, site);
   TORCH_CHECK(dO.is_contiguous() && o.is_contiguous(), "O / dO must be contiguous (B, Nq, H*D)");
   auto f32 = q.options().dtype(torch::kFloat32);
@@ -305,7 +307,7 @@ std::vector<Tensor> attn_bwd(Tensor q, Tensor k, Tensor v, OptT kmask, Tensor o,
   pio::attn_bwd_launch(a, (int)D, bfp(o), bfp(dO), f32p(lse), delta.data_ptr<float>(), dq.data_ptr<float>(),
                        dq.stride(0), (int)dq.stride(1), dk.data_ptr<float>(), dk.stride(0), (int)dk.stride(1),
                        dv.data_ptr<float>(), dv.stride(0), (int)dv.stride(1), !delta_in.has_value(), kv_accumulate, 0,
-                       g_det ? 0 : 1, dq_zeroed ? 1 : 0, stream());
+                       g_det ? 0 : 1, (dq_zeroed ? 1 : 0) | (kv_zeroed ? 2 : 0), stream());
   return {dq, dk, dv};
 }
 
@@ -1176,7 +1178,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_bwd", &attn_bwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("kmask"), py::arg("o"), py::arg("dO"),
         py::arg("lse"), py::arg("delta_in"), py::arg("H"), py::arg("D"), py::arg("scale"), py::arg("dropout_p"),
         py::arg("seed"), py::arg("dq_out"), py::arg("dk_out"), py::arg("dv_out"), py::arg("kv_accumulate") = false,
-        py::arg("site") = 0, py::arg("dq_zeroed") = false);
+        py::arg("site") = 0, py::arg("dq_zeroed") = false, py::arg("kv_zeroed") = false);
+  m.def("attn_bwd_zero_plan", &pio::attn_bwd_zero_plan, py::arg("B"), py::arg("H"), py::arg("Nq"), py::arg("Nk"),
+        py::arg("D"));
   m.def("ln_linear_fwd", &ln_linear_fwd, py::arg("x"), py::arg("lnw"), py::arg("lnb"), py::arg("eps"), py::arg("w"),
         py::arg("bias"), py::arg("act"), py::arg("res"), py::arg("out_bf16"), py::arg("save_stats"),
         py::arg("pe") = py::none(), py::arg("kin") = -1);

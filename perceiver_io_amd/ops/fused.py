@@ -809,6 +809,15 @@ class _SABlockFn(torch.autograd.Function):
         dz2 = dz.reshape(R, C)
         if not dz2.is_contiguous():
             dz2 = dz2.contiguous()
+        # attention-backward accumulators the launcher would clear itself (several key blocks /
+        # query splits adding up, e.g. 512 latents): cleared instead by the kernel before it
+        zp = _zero_plan(K, B, H, N, N, D)
+
+        def new_dqkv():  # every column block is written (or accumulated onto a cleared buffer) by attn_bwd
+            t_ = torch.empty((B, N, 3 * C), **f32)
+            return t_, (dict(zero_out=t_) if zp else {})
+
+        dqkv_next, zkw = new_dqkv()
         ho, _LOOKAHEAD["bwd_q"] = _LOOKAHEAD["bwd_q"], None
         if ho is not None and ho["key"] != getattr(ctx, "out_ptr", None):
             raise RuntimeError("fused encoder: a cross-attention layer handed its query-path backward to the wrong "
@@ -820,27 +829,28 @@ class _SABlockFn(torch.autograd.Function):
             tg = sl.targets()
             dy, do, delta = K.ln_linear_post_attn_bwd(ho["g"], ho["wq"], ho["x"], ho["mean1"], ho["rstd1"], ho["lnw"],
                                                       ho["lnb"], ho["dres"], tg[:4], *pa_args(L - 1), H, tg[4:],
-                                                      **_take_job(), **drop(L - 1))
+                                                      **_take_job(), **drop(L - 1), **zkw)
             sl.defer(K, ho["ll_dsts"] + pa_dsts(P[L - 1]))
         else:
             sl = _GradSlab(R, PA_SIZES(C), dz2)
             dy, do, delta = K.post_attn_bwd(dz2, *pa_args(L - 1), H, sl.targets(), slab=True, **_take_job(),
-                                            **drop(L - 1))
+                                            **drop(L - 1), **zkw)
             sl.defer(K, pa_dsts(P[L - 1]))
         dx = None
         for i in range(L - 1, -1, -1):
             xl, qkv, mean1, rstd1, o, lse, y, m2, r2, u = S[i]
             qkv3 = qkv.view(B, N, 3 * C)
-            dqkv = torch.empty((B, N, 3 * C), **f32)  # every column block is written by attn_bwd
+            dqkv = dqkv_next
             K.attn_bwd(qkv3[:, :, :C], qkv3[:, :, C:2 * C], qkv3[:, :, 2 * C:], None, o, do.view(B, N, C), lse,
                        delta.view(B, N, H), H, D, scale, ctx.p, ctx.seed, dqkv[:, :, :C], dqkv[:, :, C:2 * C],
-                       dqkv[:, :, 2 * C:], site=i)
+                       dqkv[:, :, 2 * C:], site=i, dq_zeroed=bool(zp & 1), kv_zeroed=bool(zp & 2))
             if i > 0:
+                dqkv_next, zkw = new_dqkv()
                 sl = _GradSlab(R, LL_SIZES(C) + PA_SIZES(C), dz2)
                 tg = sl.targets()
                 dy, do, delta = K.ln_linear_post_attn_bwd(dqkv.view(R, 3 * C), bws[i][0], xl, mean1, rstd1, P[i][0],
                                                           P[i][1], dy, tg[:4], *pa_args(i - 1), H, tg[4:],
-                                                          **_take_job(), **drop(i - 1))
+                                                          **_take_job(), **drop(i - 1), **zkw)
                 sl.defer(K, ll_dsts(P[i]) + pa_dsts(P[i - 1]))
             elif getattr(ctx, "handoff", None) is not None:
                 # the producing cross-attention layer runs this LN1/QKV backward fused with its
@@ -890,6 +900,16 @@ def sa_block_lookahead(block, rows: int):
         return None
     ps = pss[0]
     return (ps[0], ps[1], _bf16_weights(specs[0], ps)[0], ps[3])
+
+
+def _zero_plan(K, B, H, Nq, Nk, D) -> int:
+    """Bits of the attention-backward accumulators the launcher would clear (1: dQ, 2: dK/dV),
+    0 in deterministic mode (partial slices, no atomics) or on the emulation."""
+    from . import deterministic
+
+    if deterministic() or not hasattr(K, "attn_bwd_zero_plan"):
+        return 0
+    return int(K.attn_bwd_zero_plan(B, H, Nq, Nk, D))
 
 
 def self_attention_block(block, x):

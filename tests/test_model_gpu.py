@@ -96,11 +96,14 @@ def _three_way(mod, run, loss_tol=1e-2, tol=2e-2, jitter_run=None):
     _check_grads(g1, g0, tol=tol, floor=floor)
 
 
-def test_mlm_fused_matches_eager():
+@pytest.mark.parametrize("latents", [64, 512])
+def test_mlm_fused_matches_eager(latents):
+    """(512 latents: the self-attention backward has 2 key blocks and query splits, whose
+    accumulators the preceding kernel clears — csrc attn_bwd_zero_plan)"""
     from perceiver_io_amd import ops
 
     torch.manual_seed(0)
-    lit = _mlm()
+    lit = _mlm(latents=latents)
     m = lit.model
     ids = torch.randint(3, 500, (6, 96), device="cuda")
     pad = torch.zeros(6, 96, dtype=torch.bool, device="cuda")
