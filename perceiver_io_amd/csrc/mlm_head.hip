@@ -718,18 +718,17 @@ __global__ __launch_bounds__(256) void ce_bwd_dw_reg_kernel(const uint16_t* __re
 //   global: the valid slots of all sequences compacted into gcap rows for the vocab GEMMs
 //           (unused → slot 0 with label −100), total = Σ count (the mean's denominator)
 // ------------------------------------------------------------------------------------
-// select_rows: workgroup b compacts sequence b (slot → position also kept in LDS) and, when
-// given, copies the output-query rows q[b, j] = P[idx_b[b, j]] the decoder cross-attention reads
-// (the gather of the query array).  select_global: workgroup b finds its sequence's offset in
-// the global rows from all the per-sequence counts (each workgroup scans them itself: no
-// grid-wide hand-off) and writes its valid slots; workgroup 0 also writes the totals, the last
-// one the unused tail.
+// select_rows: workgroup b compacts sequence b.  select_global, workgroup (b, 0): finds sequence
+// b's offset in the global rows from all the per-sequence counts (each workgroup scans them
+// itself: no grid-wide hand-off) and writes its valid slots; workgroup (0, 0) also writes the
+// totals, the last one the unused tail.  Every workgroup (b, y) also copies the output-query rows
+// q[b, j] = P[idx_b[b, j]] of its kSelSlots slots (the gather of the decoder's query array,
+// spread over the whole grid).
 constexpr int kSelThreads = 1024;
+constexpr int kSelSlots = 128;  // query-gather slots per select_global workgroup
 __global__ __launch_bounds__(kSelThreads) void select_rows_kernel(const int64_t* __restrict__ labels, int L, int cap,
                                                                   int64_t* __restrict__ idx_b, int64_t* __restrict__ lab_b,
-                                                                  int* __restrict__ count, const float* __restrict__ P,
-                                                                  int C, float* __restrict__ q) {
-  extern __shared__ int sIdx[];  // [cap]
+                                                                  int* __restrict__ count) {
   __shared__ int sW[kSelThreads / 64], sOff;
   const int b = blockIdx.x, w = wave_id(), l = lane_id(), nw = blockDim.x >> 6;
   if (threadIdx.x == 0) sOff = 0;
@@ -751,7 +750,6 @@ __global__ __launch_bounds__(kSelThreads) void select_rows_kernel(const int64_t*
     if (sel && pos < cap) {
       idx_b[(long long)b * cap + pos] = i;
       lab_b[(long long)b * cap + pos] = lab;
-      sIdx[pos] = i;
     }
     lds_sync();
     if (threadIdx.x == 0) sOff += tot;
@@ -761,31 +759,8 @@ __global__ __launch_bounds__(kSelThreads) void select_rows_kernel(const int64_t*
   for (int j = (cnt < cap ? cnt : cap) + threadIdx.x; j < cap; j += blockDim.x) {
     idx_b[(long long)b * cap + j] = j % L;
     lab_b[(long long)b * cap + j] = -100;
-    sIdx[j] = j % L;
   }
   if (threadIdx.x == 0) count[b] = cnt;
-  if (q == nullptr) return;
-  lds_sync();
-  const int C4 = C >> 2;
-  const float4* P4 = reinterpret_cast<const float4*>(P);
-  float4* q4 = reinterpret_cast<float4*>(q) + (long long)b * cap * C4;
-  const int n4 = cap * C4;
-  for (int e0 = 0; e0 < n4; e0 += 4 * kSelThreads) {  // four independent row loads in flight per thread
-    float4 v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = e0 + u * kSelThreads + threadIdx.x;
-      if (e < n4) {
-        const int j = e / C4;
-        v[u] = P4[(long long)sIdx[j] * C4 + (e - j * C4)];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = e0 + u * kSelThreads + threadIdx.x;
-      if (e < n4) q4[e] = v[u];
-    }
-  }
 }
 
 __device__ __forceinline__ int wave_isum(int v) {
@@ -798,9 +773,33 @@ __global__ __launch_bounds__(256) void select_global_kernel(const int* __restric
                                                             const int64_t* __restrict__ lab_b, int gcap,
                                                             int64_t* __restrict__ gidx, int64_t* __restrict__ glab,
                                                             float* __restrict__ total, bool* __restrict__ overflow,
-                                                            bool* __restrict__ sticky) {
+                                                            bool* __restrict__ sticky, const int64_t* __restrict__ idx_b,
+                                                            const float* __restrict__ P, int C, float* __restrict__ q) {
   __shared__ int sRed[4][4];
   const int b = blockIdx.x, w = wave_id(), l = lane_id();
+  if (q != nullptr) {  // slots [kSelSlots·y, +kSelSlots) of sequence b: q[b, j] = P[idx_b[b, j]]
+    const int C4 = C >> 2, j0 = blockIdx.y * kSelSlots, nj = min(cap - j0, kSelSlots);
+    const float4* P4 = reinterpret_cast<const float4*>(P);
+    float4* q4 = reinterpret_cast<float4*>(q) + ((long long)b * cap + j0) * C4;
+    const int64_t* ib = idx_b + (long long)b * cap + j0;
+    for (int e0 = 0; e0 < nj * C4; e0 += 4 * 256) {  // four independent row loads in flight per thread
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = e0 + u * 256 + threadIdx.x;
+        if (e < nj * C4) {
+          const int j = e / C4;
+          v[u] = P4[ib[j] * C4 + (e - j * C4)];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = e0 + u * 256 + threadIdx.x;
+        if (e < nj * C4) q4[e] = v[u];
+      }
+    }
+  }
+  if (blockIdx.y != 0) return;
   int pre = 0, used = 0, all = 0, ovf = 0;
   for (int i = threadIdx.x; i < B; i += blockDim.x) {
     const int c = count[i], n = c < cap ? c : cap;
@@ -840,10 +839,10 @@ void mlm_select_launch(const int64_t* labels, int B, int L, int cap, int gcap, i
                        int* count, int64_t* gidx, int64_t* glab, float* total, bool* overflow, bool* sticky,
                        const float* P, int C, float* q, unsigned* ticket, hipStream_t st) {
   (void)ticket;
-  hipLaunchKernelGGL(select_rows_kernel, dim3(B), dim3(kSelThreads), cap * sizeof(int), st, labels, L, cap, idx_b, lab_b,
-                     count, P, C, q);
-  hipLaunchKernelGGL(select_global_kernel, dim3(B), dim3(256), 0, st, count, B, cap, lab_b, gcap, gidx, glab, total,
-                     overflow, sticky);
+  hipLaunchKernelGGL(select_rows_kernel, dim3(B), dim3(kSelThreads), 0, st, labels, L, cap, idx_b, lab_b, count);
+  const int gy = q ? (cap + kSelSlots - 1) / kSelSlots : 1;
+  hipLaunchKernelGGL(select_global_kernel, dim3(B, gy), dim3(256), 0, st, count, B, cap, lab_b, gcap, gidx, glab, total,
+                     overflow, sticky, idx_b, P, C, q);
 }
 
 // vocab splits so that a launch has ≈ target workgroups (several per CU hide the W-chunk latency);
