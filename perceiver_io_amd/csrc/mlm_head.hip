@@ -776,24 +776,26 @@ __global__ __launch_bounds__(256) void select_global_kernel(const int* __restric
                                                             bool* __restrict__ sticky, const int64_t* __restrict__ idx_b,
                                                             const float* __restrict__ P, int C, float* __restrict__ q) {
   __shared__ int sRed[4][4];
+  __shared__ long long sI[kSelSlots];
   const int b = blockIdx.x, w = wave_id(), l = lane_id();
   if (q != nullptr) {  // slots [kSelSlots·y, +kSelSlots) of sequence b: q[b, j] = P[idx_b[b, j]]
     const int C4 = C >> 2, j0 = blockIdx.y * kSelSlots, nj = min(cap - j0, kSelSlots);
     const float4* P4 = reinterpret_cast<const float4*>(P);
     float4* q4 = reinterpret_cast<float4*>(q) + ((long long)b * cap + j0) * C4;
-    const int64_t* ib = idx_b + (long long)b * cap + j0;
-    for (int e0 = 0; e0 < nj * C4; e0 += 4 * 256) {  // four independent row loads in flight per thread
-      float4 v[4];
+    for (int j = threadIdx.x; j < nj; j += blockDim.x) sI[j] = idx_b[(long long)b * cap + j0 + j];
+    __syncthreads();
+    for (int e0 = 0; e0 < nj * C4; e0 += 8 * 256) {  // eight independent row loads in flight per thread
+      float4 v[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; ++u) {
         const int e = e0 + u * 256 + threadIdx.x;
         if (e < nj * C4) {
           const int j = e / C4;
-          v[u] = P4[ib[j] * C4 + (e - j * C4)];
+          v[u] = P4[sI[j] * C4 + (e - j * C4)];
         }
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; ++u) {
         const int e = e0 + u * 256 + threadIdx.x;
         if (e < nj * C4) q4[e] = v[u];
       }
