@@ -83,7 +83,7 @@ int ce_combine_blocks(int);
 int ce_num_splits(int, int);
 int ce_dw_splits(int, int);
 void mlm_select_launch(const int64_t*, int, int, int, int, int64_t*, int64_t*, int*, int64_t*, int64_t*, float*, bool*, bool*,
-                       const float*, int, float*, unsigned*, hipStream_t);
+                       const float*, int, float*, hipStream_t);
 void ce_bwd_launch(int, const uint16_t*, const int64_t*, const uint16_t*, const float*, const float*, const float*,
                    const float*, int, int, float*, long long, const int64_t*, float*, float*, int, float*, int, hipStream_t);
 void embed_fwd_launch(const int64_t*, const float*, const float*, float*, long long, int, int, float, long long,
@@ -667,11 +667,10 @@ void wgrad(Tensor g, Tensor a, int64_t amode, OptT mean, OptT rstd, OptT lnw, Op
                     vrs < 0 ? 0 : vrs, wrs < 0 ? 0 : wrs, pp, prs, prows, npix, stream());
 }
 
-// per-device counters shared by the MLM head kernels: [0, kCeTickets - 1) ce_fwd_kernel's
-// per-tile + global tickets, kCeTickets - 1 the selection kernel's.  Zero between launches (each
-// counter is reset by its last taker); calls on a device are stream-ordered.  Fixed size,
-// allocated once, so captured graphs never see it move.
-constexpr int64_t kCeTickets = 1 << 16;
+// per-device ticket of the CE combine kernel (its last workgroup sums the per-block partials):
+// zero between launches (reset by its last taker); calls on a device are stream-ordered.
+// Allocated once, so captured graphs never see it move.
+constexpr int64_t kCeTickets = 4;
 static Tensor& ce_ticket(const Tensor& like) {
   static std::unordered_map<int, Tensor> tickets;
   const int d = like.get_device();
@@ -708,12 +707,10 @@ std::vector<Tensor> mlm_select(Tensor labels, int64_t cap, int64_t gcap, OptT st
     q = torch::empty({B, cap, C}, queries->options());
     qp = q.data_ptr<float>();
   }
-  Tensor& tk = ce_ticket(labels);
   pio::mlm_select_launch(labels.data_ptr<int64_t>(), B, L, (int)cap, (int)gcap, idx_b.data_ptr<int64_t>(),
                          lab_b.data_ptr<int64_t>(), count.data_ptr<int>(), gidx.data_ptr<int64_t>(),
                          glab.data_ptr<int64_t>(), total.data_ptr<float>(), ovf.data_ptr<bool>(),
-                         sticky.has_value() ? sticky->data_ptr<bool>() : nullptr, P, C, qp,
-                         reinterpret_cast<unsigned*>(tk.data_ptr<int>()) + (kCeTickets - 1), stream());
+                         sticky.has_value() ? sticky->data_ptr<bool>() : nullptr, P, C, qp, stream());
   std::vector<Tensor> out{idx_b, lab_b, gidx, glab, total, ovf};
   if (queries.has_value()) out.push_back(q);
   return out;
@@ -746,7 +743,6 @@ std::vector<Tensor> ce_fwd(Tensor h, OptT idx, Tensor labels, Tensor w, Tensor b
   Tensor blk = torch::empty({pio::ce_combine_blocks(M)}, f32);
   Tensor hs = torch::empty({M, C}, h.options().dtype(torch::kBFloat16));
   Tensor& tk = ce_ticket(h);
-  TORCH_CHECK(pio::ce_combine_blocks(M) + 1 < kCeTickets - 1, "ce_fwd: too many rows");
   float* zp = nullptr;
   int64_t zn = 0;
   if (zero_out.has_value()) {

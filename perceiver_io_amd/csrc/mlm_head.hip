@@ -839,8 +839,7 @@ __global__ __launch_bounds__(256) void select_global_kernel(const int* __restric
 
 void mlm_select_launch(const int64_t* labels, int B, int L, int cap, int gcap, int64_t* idx_b, int64_t* lab_b,
                        int* count, int64_t* gidx, int64_t* glab, float* total, bool* overflow, bool* sticky,
-                       const float* P, int C, float* q, unsigned* ticket, hipStream_t st) {
-  (void)ticket;
+                       const float* P, int C, float* q, hipStream_t st) {
   hipLaunchKernelGGL(select_rows_kernel, dim3(B), dim3(kSelThreads), 0, st, labels, L, cap, idx_b, lab_b, count);
   const int gy = q ? (cap + kSelSlots - 1) / kSelSlots : 1;
   hipLaunchKernelGGL(select_global_kernel, dim3(B, gy), dim3(256), 0, st, count, B, cap, lab_b, gcap, gidx, glab, total,

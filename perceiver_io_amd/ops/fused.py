@@ -404,8 +404,7 @@ class _LayerFn(torch.autograd.Function):
             ctx.kv_owner = ent is None
             if ent is None:  # first application of this layer: project K/V (LN over [pixels ‖ PE] if split)
                 factored = (PE_FACTORED and src is not None and src.pe is not None and not spec.packed
-                            and not ctx.needs_input_grad[6] and 1 <= xkv2.shape[1] <= 4 and 2 * C <= 512
-                            and C % 2 == 0)
+                            and not ctx.needs_input_grad[6] and 1 <= xkv2.shape[1] <= 4 and 2 * C <= 512)
                 if factored:
                     kv, mean_kv, rstd_kv = _pe_proj_fwd(K, xkv2, src.pe, g_kv, b_kv,
                                                         torch.cat([ps[5], ps[6]], 0), bin_[C:])
