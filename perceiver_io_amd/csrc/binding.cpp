@@ -415,9 +415,10 @@ std::vector<Tensor> sa_layer_fwd(Tensor qkv, Tensor x, int64_t N, double scale, 
   const bool next = wq.has_value();
   if (next)
     TORCH_CHECK(lnw.has_value() && lnb.has_value() && bq.has_value() && wq->is_contiguous() &&
-                    (wq->size(0) == 3 * C || wq->size(0) == C) && wq->size(1) == C && bq->numel() == wq->size(0) &&
+                    (wq->size(0) == 3 * C || wq->size(0) == 2 * C || wq->size(0) == C) && wq->size(1) == C &&
+                    bq->numel() == wq->size(0) &&
                     lnw->numel() == C && lnb->numel() == C,
-                "sa_layer_fwd: next LN + projection (packed QKV (3C, C) or a query projection (C, C))");
+                "sa_layer_fwd: next LN + projection (packed QKV (3C, C), K/V (2C, C) or a query projection (C, C))");
   const int nq = next ? (int)wq->size(0) : 3 * C;
   auto f32 = x.options().dtype(torch::kFloat32);
   auto b16 = x.options().dtype(torch::kBFloat16);

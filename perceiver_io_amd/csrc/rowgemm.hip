@@ -720,7 +720,8 @@ __global__ __launch_bounds__(256) void sa_layer_fwd_kernel(
     const float* __restrict__ bq, uint16_t* __restrict__ QKVn, float* __restrict__ mean1, float* __restrict__ rstd1,
     DropCfg dr) {
   // NQ·C: width of the next projection (3C: the next self-attention layer's packed QKV; C: the
-  // query projection of a following cross-attention layer)
+  // query projection of a following cross-attention layer; 2C: the K/V projection of a decoder
+  // cross-attention over this block's output)
   constexpr int C = 64, H = 4, D = 16, NCH = 2, KP = 64, LD = C + 8, LDV = C + 8, C3 = 3 * C, MAXKT = 8;
   constexpr int nq = NQ * C;
   __shared__ __attribute__((aligned(16))) uint16_t sV[256 * LDV + 64];  // V rows of the batch element (+ overrun)
@@ -1564,6 +1565,9 @@ void sa_layer_fwd_launch(const uint16_t* QKV, int N, float scale_log2, uint16_t*
   if (nq == 64) hipLaunchKernelGGL((sa_layer_fwd_kernel<NX, A, 1>), grid, dim3(256), 0, st, QKV, N, scale_log2, O, LSE, X, \
                                    Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, lnw, lnb, Wq, bq, \
                                    QKVn, mean1, rstd1, dr);                                                            \
+  else if (nq == 128) hipLaunchKernelGGL((sa_layer_fwd_kernel<NX, A, 2>), grid, dim3(256), 0, st, QKV, N, scale_log2, O,  \
+                                         LSE, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R,  \
+                                         lnw, lnb, Wq, bq, QKVn, mean1, rstd1, dr);                                    \
   else hipLaunchKernelGGL((sa_layer_fwd_kernel<NX, A>), grid, dim3(256), 0, st, QKV, N, scale_log2, O, LSE, X, Wo, bo,   \
                           g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, lnw, lnb, Wq, bq, QKVn, mean1,  \
                           rstd1, dr)

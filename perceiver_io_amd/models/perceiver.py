@@ -230,9 +230,17 @@ class PerceiverMLM(nn.Module):
         l = x_input.shape[1]
         if labels is None:
             x_masked, labels = self.masking(x_input, pad_mask)
-        x_latent, _ = self.encoder(x_masked, pad_mask)
         if ops.get_backend() == "reference":
+            x_latent, _ = self.encoder(x_masked, pad_mask)
             # reference compute: all K queries decoded, full (B, V, L) logits, CE with ignore_index
             logits = self.decoder(x_latent)[:, :l, :]
             return torch.nn.functional.cross_entropy(logits.transpose(1, 2), labels, ignore_index=-100)
-        return ops.mlm_head.masked_decode_loss(self.decoder, x_latent, labels, p=self.masking.mask_p)
+        look = ops.fused._LOOKAHEAD
+        # on the fused path the encoder's last kernel also projects the decoder's K/V
+        look["want_kv"] = (ops.fused.decoder_kv_lookahead(self.decoder.cross_attention)
+                           if ops.use_hip(x_masked) else None)
+        try:
+            x_latent, _ = self.encoder(x_masked, pad_mask)
+            return ops.mlm_head.masked_decode_loss(self.decoder, x_latent, labels, p=self.masking.mask_p)
+        finally:
+            look["want_kv"] = look["have_q"] = None

@@ -392,10 +392,11 @@ class _LayerFn(torch.autograd.Function):
         if spec.cross:
             B, M = x_kv.shape[0], x_kv.shape[1]
             xkv2 = x_kv.reshape(B * M, x_kv.shape[2])
-            hq, _LOOKAHEAD["have_q"] = _LOOKAHEAD["have_q"], None
+            hq = _LOOKAHEAD["have_q"]
             if hq is not None and hq[4] is g_q and hq[0].data_ptr() == xq2.data_ptr() and hq[0].numel() == xq2.numel():
                 # LN + query projection computed by the producing self-attention block's last kernel
                 q, mean_q, rstd_q = hq[1:4]
+                _LOOKAHEAD["have_q"] = None
                 ctx.q_handoff = True
             else:
                 q, mean_q, rstd_q = K.ln_linear_fwd(xq2, g_q, b_q, EPS, wq, bin_[:C], 0, None, True, True)
@@ -411,8 +412,17 @@ class _LayerFn(torch.autograd.Function):
                 else:
                     if wkv is None:
                         wkv = _kv_weight(spec, ps)
-                    kv, mean_kv, rstd_kv = K.ln_linear_fwd(xkv2, g_kv, b_kv, EPS, wkv, bin_[C:], 0, None, True, True,
-                                                           src.pe if src is not None else None, g_kv.shape[0])
+                    hk = _LOOKAHEAD["have_q"]
+                    if (src is None and hk is not None and hk[4] is g_kv and hk[0].data_ptr() == xkv2.data_ptr()
+                            and hk[0].numel() == xkv2.numel()):
+                        # K/V of a decoder over the encoder output: computed by the encoder's last
+                        # self-attention kernel (its backward stays here: plain ln_linear_bwd)
+                        kv, mean_kv, rstd_kv = hk[1:4]
+                        _LOOKAHEAD["have_q"] = None
+                    else:
+                        kv, mean_kv, rstd_kv = K.ln_linear_fwd(xkv2, g_kv, b_kv, EPS, wkv, bin_[C:], 0, None, True,
+                                                               True, src.pe if src is not None else None,
+                                                               g_kv.shape[0])
                 ent = {"kv": kv, "mean": mean_kv, "rstd": rstd_kv, "dkv": None, "factored": factored, "wkv": wkv}
                 if src is not None:
                     src.entries[key] = ent
@@ -874,7 +884,8 @@ class _SABlockFn(torch.autograd.Function):
 # The same in the other direction ("want_q" / "have_q" / "bwd_q"): a block's last fused layer
 # computes the next cross-attention layer's LN + query projection, and that layer hands the
 # backward of it back to the block.
-_LOOKAHEAD = {"want": None, "have": None, "bwd": None, "want_q": None, "have_q": None, "bwd_q": None}
+_LOOKAHEAD = {"want": None, "have": None, "bwd": None, "want_q": None, "have_q": None, "bwd_q": None,
+              "want_kv": None}
 
 
 def _sa_block_plan(block, rows: int):
@@ -1065,12 +1076,32 @@ def _encode(encoder, src: KVSource, pad_mask):
         nxt_cross = layers[li + 1][0] if li + 1 < len(layers) else None
         if nxt_cross is not None and can_fuse(nxt_cross, src):
             _LOOKAHEAD["want_q"] = cross_q_lookahead(nxt_cross, src)
+        elif nxt_cross is None:  # a decoder's K/V over the encoder output, when its caller asked for it
+            _LOOKAHEAD["want_q"] = _LOOKAHEAD["want_kv"]
         try:
             lat = self_attention_block(block, lat)
         finally:
             _LOOKAHEAD["have"] = _LOOKAHEAD["want_q"] = None
-    _LOOKAHEAD["have_q"] = None
+    if _LOOKAHEAD["want_kv"] is None:
+        _LOOKAHEAD["have_q"] = None
     return lat
+
+
+def decoder_kv_lookahead(cross):
+    """(γkv, βkv, Wkv bf16 (2C, C), bkv) of a decoder cross-attention over the encoder's latents, for
+    the encoder's last self-attention kernel (C = 64, H = 4 latents: the fused layer kernel's
+    shape), or None.  Set by the caller for the duration of one encoder + decoder call only
+    (PerceiverMLM.loss), so the stashed K/V never outlives it."""
+    spec, ps = layer_spec_and_params(cross)
+    if not spec.cross or spec.C != 64 or ps[2].shape[0] != 64:
+        return None
+    wkv = _bf16_weights(spec, ps)[1]
+    if wkv is None:
+        wkv = _kv_weight(spec, ps)
+    bin_ = ps[5] if spec.packed else ps[7]
+    if not wkv.is_contiguous() or tuple(wkv.shape) != (2 * spec.C, 64):
+        return None
+    return (ps[2], ps[3], wkv, bin_[spec.C:])
 
 
 def cross_q_lookahead(cross, src):
