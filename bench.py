@@ -217,8 +217,28 @@ def _build_lartpc(args):
     return _LArHolder(model), loss_fn, make_batch, desc, 1e-3, 1e-4
 
 
+def _spawn_self(args, argv) -> int:
+    """``--gpus N`` without a torchrun environment: start N ranks of this script (one per GPU,
+    RCCL) and return the worst exit code.  The parent only counts devices — it never initialises
+    the GPU.  With no GPU at all it is a CPU dry run over gloo; with fewer than N GPUs it fails."""
+    import torch
+
+    from perceiver_io_amd.parallel.launch import spawn
+
+    n = torch.cuda.device_count()
+    if 0 < n < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but only {n} GPU(s) visible", file=sys.stderr)
+        return 2
+    if n == 0:
+        print(f"bench.py: no GPU visible: CPU dry run with {args.gpus} gloo ranks", file=sys.stderr)
+    argv = list(sys.argv[1:] if argv is None else argv)
+    return spawn(args.gpus, [sys.executable, os.path.abspath(__file__)] + argv)
+
+
 def main(argv=None):
     args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_spawn_self(args, argv))
     import torch
 
     from perceiver_io_amd import ops
@@ -227,8 +247,8 @@ def main(argv=None):
 
     info = pdist.init()
     world = info.world_size
-    if world != args.gpus and pdist.env_world_size() > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}")
     cuda = torch.cuda.is_available()
     device = torch.device("cuda", torch.cuda.current_device()) if cuda else torch.device("cpu")
     ops.set_backend("auto" if args.backend == "hip" else args.backend)
@@ -255,7 +275,7 @@ def main(argv=None):
 
         flat = opt.flat if fused else FlatParameterSpace(params, with_shadow=False, replicate=False)
         reducer = FlatGradReducer(flat)
-        reducer.set_early_params(model.decoder.parameters())  # all-reduced during the encoder backward
+        reducer.plan(model)  # ready points: decoder + head, layer_n — all-reduced during the backward
         reducer.broadcast_parameters(model)
 
     autocast = (not fused) and args.dtype == "bf16" and cuda
@@ -291,6 +311,10 @@ def main(argv=None):
     dt = time.perf_counter() - t0
     dt = pdist.all_reduce_max(dt)
     final_loss = float(loss.float().item())
+    # data parallelism must leave every rank with bitwise the same parameters
+    from perceiver_io_amd.parallel.reducer import params_in_sync
+
+    sync_diff = params_in_sync(reducer.flat if reducer is not None else params) if world > 1 else 0.0
     if args.profile_steps and cuda:
         from torch.profiler import ProfilerActivity, profile
 
@@ -328,17 +352,21 @@ def main(argv=None):
             "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": round(vs, 3) if vs else None,
-            "dtype": args.dtype if not fused else "bf16",
+            "dtype": ("bf16" if fused else args.dtype) if cuda else "fp32",
             "data": "synthetic (random inputs of the config's shape, random-init weights)",
             "config": {"model": desc, "global_batch": B * world, "seq_len": args.seq_len,
                        "parallelism": f"dp{world}", "backend": args.backend,
                        "graph": bool(fused and not args.no_graph), "name": args.config,
                        "dist_backend": info.backend if world > 1 else None,
                        "allreduce_in_graph": bool(reducer is not None and getattr(reducer, "in_graph", False)),
-                       "allreduce_overlap": bool(reducer is not None and reducer.overlap_ready())},
+                       "allreduce_overlap": sorted(reducer.points) if reducer is not None else []},
             "final_loss": round(final_loss, 4),
+            "dist_backend": info.backend if world > 1 else None,
+            "params_in_sync": sync_diff == 0.0, "params_max_abs_diff": sync_diff,
         }
         print(json.dumps(out), flush=True)
+    if reducer is not None:
+        reducer.close()
     pdist.shutdown()
 
 

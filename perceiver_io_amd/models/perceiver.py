@@ -82,7 +82,9 @@ class PerceiverEncoder(nn.Module):
         if attn_mask is None and ops.use_hip(self.latent):
             return ops.fused.encode_inputs(self, x_in, pad_mask)
         x_latent = self.latent.unsqueeze(0).expand(x_in.shape[0], -1, -1)
-        for layer in self.layers():
+        for i, layer in enumerate(self.layers()):
+            if i == 1:  # DDP: layer_n's gradients are final here (parallel/reducer.py)
+                x_latent = bucket_ready_point(x_latent, self, "layer_n")
             x_latent = layer(x_latent, x_in, pad_mask, attn_mask)
         return x_latent
 
@@ -113,7 +115,7 @@ class PerceiverDecoder(nn.Module):
     def hidden(self, x, num_queries: Optional[int] = None):
         """Decoder output before the adapter, ``(B, K, C_out)``; optionally only the
         first ``num_queries`` queries (queries are independent of each other)."""
-        x = bucket_ready_point(x)  # DDP: decoder grads final here → early bucket (parallel/reducer.py)
+        x = bucket_ready_point(x, self, "decoder")  # DDP: decoder grads final here (parallel/reducer.py)
         self.check_latent(x)
         q = (self.output if num_queries is None else self.output[:num_queries]).unsqueeze(0)
         ca = self.cross_attention
@@ -134,7 +136,7 @@ class PerceiverDecoder(nn.Module):
         adds straight into the query parameter's gradient rows."""
         from ..ops.mlm_head import _GatherQueries
 
-        x = bucket_ready_point(x)
+        x = bucket_ready_point(x, self, "decoder")
         self.check_latent(x)
         q = _GatherQueries.apply(self.output, idx.reshape(-1)).view(idx.shape[0], idx.shape[1], -1)
         return self.cross_attention(q, x)

@@ -33,6 +33,7 @@ from typing import List, Optional
 import torch
 
 from . import emulation, ext
+from ..parallel.reducer import bucket_ready_point
 
 EPS = 1e-5
 # per-tile weight-gradient partials go to a slab reduced on a side stream (see _GradSlab);
@@ -1063,6 +1064,8 @@ def _encode(encoder, src: KVSource, pad_mask):
     layers = list(encoder.layers())
     for li, layer in enumerate(layers):
         cross, block = layer[0], layer[1]
+        if li == 1:  # DDP: every layer_n gradient but its query path is final here (parallel/reducer.py)
+            lat = bucket_ready_point(lat, encoder, "layer_n")
         if lat.shape[0] == 1 and not can_fuse(cross, src):
             lat = lat.expand(b, -1, -1)
         # the block's first LN1 + QKV projection rides on the cross layer's post-attention kernel

@@ -277,7 +277,7 @@ def masked_decode_loss(decoder, x_latent: torch.Tensor, labels: torch.Tensor, p:
     from ..parallel.reducer import bucket_ready_point
     from . import use_hip
 
-    x_latent = bucket_ready_point(x_latent)  # before any decoder op (DDP early bucket)
+    x_latent = bucket_ready_point(x_latent, decoder, "decoder")  # before any decoder op (DDP)
     B, L = labels.shape
     decoder.check_latent(x_latent)
     lin = decoder.output_adapter.linear

@@ -165,7 +165,10 @@ class FusedAdamW(torch.optim.Optimizer):
         super().__init__(params, defaults)
         if len(self.param_groups) != 1:
             raise ValueError("FusedAdamW supports a single parameter group")
-        self.flat = flat if flat is not None else FlatParameterSpace(self.param_groups[0]["params"])
+        # always with the bf16 shadow the fused executor reads its GEMM operands from (also for the
+        # CPU emulation: re-homed parameters do not share the flat buffer's version counter, so a
+        # version-keyed weight cache would never see the in-place update)
+        self.flat = flat if flat is not None else FlatParameterSpace(self.param_groups[0]["params"], with_shadow=True)
         dev = self.flat.device
         self.exp_avg = torch.zeros(self.flat.numel, dtype=torch.float32, device=dev)
         self.exp_avg_sq = torch.zeros(self.flat.numel, dtype=torch.float32, device=dev)

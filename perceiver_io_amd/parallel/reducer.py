@@ -1,26 +1,41 @@
 """Data-parallel gradient reducer over the flat gradient buffer (SURVEY C-01..C-03, §5.8).
 
-Replaces the DDP Reducer the reference gets from Lightning (``trainer.yaml:47``):
+Replaces the DDP Reducer the reference gets from Lightning (``trainer.yaml:47``: every gradient
+averaged over the ranks on every step):
   * parameters and buffers are broadcast once from rank 0 as flat tensors (C-01); the
     deterministic Fourier position-encoding buffer is *not* re-broadcast every step (C-02);
   * gradients live in ONE contiguous fp32 buffer (``ops.optim.FlatParameterSpace``), reduced by
     a few large RCCL all-reduces instead of per-parameter buckets.  Per-step gradient volume is
     4–11 MB, so on xGMI (point-to-point links, ring all-reduce bound by one link per hop) the
-    collective is latency-bound: 2–3 buckets, not DDP's 25 MB-bucket machinery;
+    collective is latency-bound: 3–4 buckets, not DDP's 25 MB-bucket machinery;
   * the average (÷ world) is folded into the fused optimizer's gradient scale (no extra pass);
-  * overlap with the backward: the decoder / output head runs first in backward and is the tail
-    of the flat buffer (module order: encoder, then decoder).  ``bucket_ready_point(x)`` marks the
-    decoder's input; when autograd reaches it every decoder-side gradient is final (see
-    ``_ReadyFn``), and the tail bucket's all-reduce is launched on a side HIP stream while the
-    encoder backward runs.  ``finish()`` reduces the remaining buckets and joins the side stream;
-  * the whole step — backward-driven bucket launches, the join and the fused AdamW — is captured
-    in the step's hipGraph when RCCL collectives are capturable on this node
-    (``dist.graph_collectives_ok``, probed once: capture + replay of a tiny all-reduce agreed by
-    every rank); otherwise the collectives run eagerly after the replayed forward/backward.
+  * overlap with the backward through READY POINTS: identity autograd nodes placed on a tensor
+    whose gradient arrives only after a known flat range of parameter gradients is final
+    (``bucket_ready_point``).  Their backward launches that range's all-reduce on a side HIP
+    stream while the rest of the backward runs:
+      - ``"decoder"`` on the decoder's input: the decoder + output head (the flat buffer's tail);
+      - ``"layer_n"`` on the input of the weight-shared ``layer_n``'s first application: all of
+        ``layer_n`` except its cross-attention query path (the fused executor runs that
+        LN + Q-projection backward inside ``layer_1``'s self-attention block backward,
+        ``ops/fused.py`` ``_LOOKAHEAD["bwd_q"]``), i.e. from the K/V part of its in-projection
+        bias to its last parameter.
+    ``finish()`` reduces the remaining buckets (embedding, ``layer_1``, latents, the layer_n
+    query path) and joins the side stream.
+
+Step protocol (enforced, so a stale launch can never leak into a later step or a graph):
+    arm()      before the forward of the LAST micro-batch of an optimizer step — ready points
+               fire only while armed (with gradient accumulation the earlier micro-batches'
+               backwards launch nothing: their gradients are not final yet);
+    backward   ready points launch their buckets (each at most once; a second hit is an error);
+    finish()   launches every bucket not launched yet, joins, disarms.
+While a hipGraph capture is in progress, ``arm()`` only arms when the collectives are captured
+into the graph (``in_graph``: RCCL capturable on this node, probed once by
+``dist.graph_collectives_ok``); otherwise the captured backward launches nothing and
+``finish()`` runs eagerly after each replay.
 """
 from __future__ import annotations
 
-from typing import Iterable, List, Optional, Tuple
+from typing import Dict, Iterable, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -29,52 +44,62 @@ _ACTIVE: List["FlatGradReducer"] = []
 
 
 class _ReadyFn(torch.autograd.Function):
-    """Identity whose backward launches the early bucket.
+    """Identity whose backward launches the bucket of one ready point.
 
-    Applied to the decoder's input *before* any decoder op is recorded.  The autograd engine
-    runs ready nodes in decreasing sequence number, and every decoder/head node (the output-query
-    gather or expand, the fused layers, the vocab head, their AccumulateGrad leaves) was created
-    after this one — so when this backward runs, every gradient of the decoder's parameters has
-    been produced (the fused kernels' deferred weight-gradient slab reductions are flushed
-    first)."""
+    Applied to a tensor *before* any op of the covered parameters is recorded.  The autograd
+    engine runs this node only once the gradient of its output is complete, i.e. after every
+    node that consumed the output; the covered parameters' AccumulateGrad nodes run as soon as
+    their inputs are ready (highest priority), and the fused kernels' deferred weight-gradient
+    slab reductions are flushed first (``ops.fused.flush_pending``)."""
 
     @staticmethod
-    def forward(ctx, x, red):
-        ctx.red = red
+    def forward(ctx, x, red, name):
+        ctx.red, ctx.name = red, name
         return x.view_as(x)
 
     @staticmethod
     def backward(ctx, g):
-        ctx.red.early_ready()
-        return g, None
+        ctx.red.point_reached(ctx.name)
+        return g, None, None
 
 
-def bucket_ready_point(x: torch.Tensor) -> torch.Tensor:
-    """Mark ``x`` (the decoder's input) as the early-bucket ready point of the active reducer."""
+def bucket_ready_point(x: torch.Tensor, module: torch.nn.Module, name: str) -> torch.Tensor:
+    """Mark ``x`` as ready point ``name`` of the armed reducer that planned ``module``."""
     if not _ACTIVE or not torch.is_grad_enabled() or not x.requires_grad:
         return x
-    red = _ACTIVE[-1]
-    if not red.overlap_ready():
-        return x
-    return _ReadyFn.apply(x, red)
+    for red in reversed(_ACTIVE):
+        if red.owns_point(module, name):
+            if not red.armed:
+                return x
+            return _ReadyFn.apply(x, red, name)
+    return x
+
+
+def _capturing(device) -> bool:
+    return device.type == "cuda" and torch.cuda.is_current_stream_capturing()
 
 
 class FlatGradReducer:
     def __init__(self, flat, bucket_bytes: int = 4 << 20, overlap: bool = True, in_graph: Optional[bool] = None,
-                 wire_dtype: Optional[torch.dtype] = None):
+                 wire_dtype: Optional[torch.dtype] = None, force: bool = False):
         self.flat = flat
         self.world = dist.get_world_size() if (dist.is_available() and dist.is_initialized()) else 1
+        # force: run the collectives even for a 1-rank group (tests of the capture mechanics on one GPU)
+        self.force = bool(force) and dist.is_available() and dist.is_initialized()
         self.bucket_bytes = bucket_bytes
         self.buckets: List[Tuple[int, int]] = flat.bucket_ranges(bucket_bytes)
-        self.early: Optional[Tuple[int, int]] = None
+        self.points: Dict[str, int] = {}          # ready point → bucket index
+        self._point_modules: Dict[str, int] = {}  # ready point → id() of the module it was planned on
         # overlap needs every parameter gradient to land in flat.grad directly (no 8-way replicas
-        # that a later fold() would still add into the early bucket's range)
+        # that a later fold() would still add into an early bucket's range)
         self.overlap = bool(overlap) and getattr(flat, "grad_rep", None) is None
         self.wire_dtype = wire_dtype
         self.on_gpu = flat.device.type == "cuda"
         self._side = torch.cuda.Stream(device=flat.device) if (self.on_gpu and self.overlap) else None
-        self._launched = set()
-        self.early_launches = 0  # early-bucket launches driven by backward (tests / diagnostics)
+        self._counts = [0] * len(self.buckets)
+        self._armed = False
+        self.early_launches = 0  # buckets launched from a backward (tests / diagnostics)
+        self.launch_log: List[str] = []  # names of the ready points that fired, in order (tests)
         if in_graph is None:
             from .dist import graph_collectives_ok
 
@@ -85,30 +110,129 @@ class FlatGradReducer:
 
     @property
     def enabled(self) -> bool:
-        return self.world > 1
+        return self.world > 1 or self.force
+
+    @property
+    def armed(self) -> bool:
+        return self._armed
 
     def close(self):
+        """Unregister (end of a fit / bench): a stale reducer must never be the target of a later
+        model's ready points."""
         if self in _ACTIVE:
             _ACTIVE.remove(self)
 
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
     # -- buckets -------------------------------------------------------------------------
-    def set_early_params(self, params: Iterable[torch.nn.Parameter]):
-        """Declare the parameters final at the ready point (the decoder + head).  They must be a
-        contiguous tail ``[lo, numel)`` of the flat buffer; bucket 0 becomes that tail."""
+    def _param_range(self, params, lo_param=None, lo_extra: int = 0) -> Optional[Tuple[int, int]]:
+        """Flat range [lo, hi) covering exactly ``params`` (contiguous in the buffer), optionally
+        starting ``lo_extra`` elements into ``lo_param``; None if they are not contiguous."""
         ids = {id(p) for p in params}
-        offs = [o for p, o in zip(self.flat.params, self.flat.offsets) if id(p) in ids]
-        if not offs:
+        idx = [i for i, p in enumerate(self.flat.params) if id(p) in ids]
+        if not idx or idx != list(range(idx[0], idx[-1] + 1)):
+            return None
+        offs = self.flat.offsets
+        last = idx[-1]
+        hi = offs[last + 1] if last + 1 < len(offs) else self.flat.numel
+        lo = offs[idx[0]]
+        if lo_param is not None:
+            j = next((i for i in idx if self.flat.params[i] is lo_param), None)
+            if j is None:
+                return None
+            lo = offs[j] + lo_extra
+        return (lo, hi) if hi > lo else None
+
+    def set_ready_ranges(self, ranges: Dict[str, Tuple[Tuple[int, int], torch.nn.Module]]):
+        """Ready points ``name → ((lo, hi), module)``: disjoint flat ranges reduced when the
+        backward reaches the point; the complement is split into ``bucket_bytes`` buckets that
+        ``finish()`` reduces."""
+        items = sorted(((r, n, m) for n, (r, m) in ranges.items()), key=lambda t: -t[0][0])
+        for (a, _, _), (b, _, _) in zip(items, items[1:]):
+            if b[1] > a[0]:
+                raise ValueError("ready-point ranges overlap")
+        self.buckets, self.points, self._point_modules = [], {}, {}
+        for (lo, hi), name, mod in items:
+            self.points[name] = len(self.buckets)
+            self._point_modules[name] = id(mod)
+            self.buckets.append((lo, hi))
+        # the complement, highest offsets first (late parameters' gradients are produced first)
+        hi = self.flat.numel
+        gaps = []
+        for (lo_r, hi_r), _, _ in items:
+            if hi_r < hi:
+                gaps.append((hi_r, hi))
+            hi = lo_r
+        if hi > 0:
+            gaps.append((0, hi))
+        cap = max(64, self.bucket_bytes // 4)
+        for lo, hi in gaps:
+            while hi - lo > cap:
+                self.buckets.append((hi - cap, hi))
+                hi -= cap
+            self.buckets.append((lo, hi))
+        self._counts = [0] * len(self.buckets)
+
+    def plan(self, model) -> Dict[str, Tuple[int, int]]:
+        """Ready points for a Perceiver model (anything with ``.decoder`` and/or ``.encoder``):
+        ``"decoder"`` and, for a weight-shared encoder (``layer_n``), ``"layer_n"``.  Returns the
+        planned flat ranges (empty when nothing can overlap, e.g. a frozen encoder's decoder-only
+        training keeps one bucket)."""
+        ranges = {}
+        dec = getattr(model, "decoder", None)
+        if isinstance(dec, torch.nn.Module):
+            r = self._param_range([p for p in dec.parameters() if p.requires_grad])
+            if r is not None:
+                ranges["decoder"] = (r, dec)
+        enc = getattr(model, "encoder", None)
+        lay = getattr(enc, "layer_n", None) if isinstance(enc, torch.nn.Module) else None
+        if lay is not None:
+            ps = [p for p in lay.parameters() if p.requires_grad]
+            try:
+                mha = lay[0].attn.attention.attention
+                bias, c = mha.in_proj_bias, mha.embed_dim
+            except (AttributeError, IndexError, TypeError):
+                bias = None
+            if ps and bias is not None and bias.requires_grad:
+                # everything of layer_n from the K/V part of its in-projection bias on (the query
+                # path before it finishes inside layer_1's backward on the fused path)
+                r = self._param_range(ps, lo_param=bias, lo_extra=c)
+                if r is not None:
+                    ranges["layer_n"] = (r, enc)
+        if not self.overlap:
+            # overlap off: same bucket layout (so results stay bit-comparable), no ready points
+            self.set_ready_ranges(ranges)
+            self.points, self._point_modules = {}, {}
+            return {}
+        self.set_ready_ranges(ranges)
+        return {k: v[0] for k, v in ranges.items()}
+
+    def set_early_params(self, params: Iterable[torch.nn.Parameter], module: Optional[torch.nn.Module] = None):
+        """Compatibility: one ``"decoder"`` ready point over ``params`` (a contiguous range)."""
+        params = list(params)
+        r = self._param_range([p for p in params if p.requires_grad])
+        if r is None:
             return
-        lo = min(offs)
-        tail = [p for p, o in zip(self.flat.params, self.flat.offsets) if o >= lo]
-        if any(id(p) not in ids for p in tail):
-            return  # not a contiguous tail: no early bucket (everything reduced in finish())
-        self.early = (lo, self.flat.numel)
-        rest = [r for r in self.flat.bucket_ranges(self.bucket_bytes, hi=lo)]
-        self.buckets = [self.early] + rest
+        if module is None:
+            raise ValueError("set_early_params needs the module whose forward places the ready point")
+        self.set_ready_ranges({"decoder": (r, module)})
+        if not self.overlap:
+            self.points, self._point_modules = {}, {}
+
+    @property
+    def early(self) -> Optional[Tuple[int, int]]:
+        i = self.points.get("decoder")
+        return self.buckets[i] if i is not None else None
+
+    def owns_point(self, module, name: str) -> bool:
+        return self._point_modules.get(name) == id(module)
 
     def overlap_ready(self) -> bool:
-        return self.enabled and self.overlap and self.early is not None
+        return self.enabled and self.overlap and bool(self.points)
 
     def broadcast_parameters(self, module: torch.nn.Module, src: int = 0):
         """C-01: one broadcast of the flat parameter buffer + remaining buffers."""
@@ -124,6 +248,29 @@ class FlatGradReducer:
             if p.data_ptr() not in flat_ptrs:
                 dist.broadcast(p.data, src=src)
 
+    # -- the step protocol ----------------------------------------------------------------
+    def _join(self):
+        if self._side is not None:
+            torch.cuda.current_stream(self.flat.device).wait_stream(self._side)
+
+    def arm(self):
+        """Before the forward of an optimizer step's last micro-batch."""
+        if any(self._counts):
+            raise RuntimeError("FlatGradReducer.arm: buckets of a previous backward were never finished "
+                               f"(launched: {[i for i, c in enumerate(self._counts) if c]})")
+        capturing = _capturing(self.flat.device)
+        self._armed = self.overlap_ready() and (not capturing or self.in_graph)
+
+    def disarm(self):
+        self._armed = False
+
+    def reset(self):
+        """Abandon a step (e.g. after an exception inside it): join outstanding launches, clear."""
+        if any(self._counts) and not _capturing(self.flat.device):
+            self._join()
+        self._counts = [0] * len(self.buckets)
+        self._armed = False
+
     def _reduce(self, lo: int, hi: int):
         g = self.flat.grad[lo:hi]
         if self.wire_dtype is not None and self.wire_dtype != g.dtype:
@@ -133,11 +280,11 @@ class FlatGradReducer:
         else:
             dist.all_reduce(g)
 
-    def ready(self, bucket: int):
-        """Launch one bucket's all-reduce (on the side stream when overlapping on a GPU)."""
-        if not self.enabled or bucket in self._launched:
-            return
-        self._launched.add(bucket)
+    def _launch(self, bucket: int):
+        if _capturing(self.flat.device) and not self.in_graph:
+            raise RuntimeError("FlatGradReducer: a collective inside a hipGraph capture on a node where the "
+                               "collectives are not capturable (in_graph=False)")
+        self._counts[bucket] += 1
         lo, hi = self.buckets[bucket]
         if self._side is not None:
             self._side.wait_stream(torch.cuda.current_stream(self.flat.device))
@@ -146,26 +293,52 @@ class FlatGradReducer:
         else:
             self._reduce(lo, hi)
 
-    def early_ready(self):
-        """Backward reached the decoder input: the tail bucket is final → launch it."""
-        if not self.overlap_ready() or 0 in self._launched:
+    def point_reached(self, name: str):
+        """Backward reached ready point ``name``: its bucket is final → launch it."""
+        if not (self._armed and self.enabled):
             return
+        i = self.points[name]
+        if self._counts[i]:
+            raise RuntimeError(f"FlatGradReducer: ready point {name!r} reached twice in one backward")
         from ..ops.fused import flush_pending
 
-        flush_pending()  # deferred weight-gradient slab reductions of the decoder/head kernels
+        flush_pending()  # deferred weight-gradient slab reductions of the covered kernels
         self.early_launches += 1
-        self.ready(0)
+        self.launch_log.append(name)
+        self._launch(i)
 
     def finish(self):
-        """All remaining buckets, then join the side stream."""
+        """All remaining buckets, then join the side stream; every bucket exactly once."""
         if not self.enabled:
+            self._armed = False
             return
         self.flat.fold()  # replicated fused-layer gradients → grad before they are reduced
         for i in range(len(self.buckets)):
-            self.ready(i)
-        if self._side is not None:
-            torch.cuda.current_stream(self.flat.device).wait_stream(self._side)
-        self._launched.clear()
+            if not self._counts[i]:
+                self._launch(i)
+        self._join()
+        if any(c != 1 for c in self._counts):
+            raise RuntimeError(f"FlatGradReducer.finish: bucket launch counts {self._counts} (each must be 1)")
+        self._counts = [0] * len(self.buckets)
+        self._armed = False
 
     def grad_scale(self) -> float:
         return 1.0 / self.world
+
+
+def params_in_sync(flat_or_params, src: int = 0) -> float:
+    """max |p − p_rank0| over every parameter (all ranks agree on the value; 0.0 = bitwise in
+    sync).  One broadcast of the flat buffer + one max all-reduce — a cheap end-of-run check."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() < 2:
+        return 0.0
+    if isinstance(flat_or_params, torch.Tensor):
+        mine = flat_or_params.detach().float().reshape(-1)
+    elif hasattr(flat_or_params, "data") and isinstance(flat_or_params.data, torch.Tensor):
+        mine = flat_or_params.data.detach().float().reshape(-1)
+    else:
+        mine = torch.cat([p.detach().float().reshape(-1) for p in flat_or_params])
+    ref = mine.clone()
+    dist.broadcast(ref, src=src)
+    d = (mine - ref).abs().max().reshape(1)
+    dist.all_reduce(d, op=dist.ReduceOp.MAX)
+    return float(d.item())

@@ -104,6 +104,21 @@ class _Captured:
         self.seed_grad = seed_grad  # read by the captured backward: kept alive with the graph
 
 
+class ClosureGraph:
+    """Host stand-in for a hipGraph (``StepEngine(graph_impl="closure")``, CPU tests): "capture"
+    records the step body without running it, ``replay`` re-runs it and copies its loss into the
+    static output — so the engine's capture/replay sequence (warm-ups, what runs inside vs after
+    the graph, the reducer protocol) executes unchanged on CPU ranks over gloo."""
+
+    def __init__(self):
+        self.body = None
+        self.loss = None
+
+    def replay(self):
+        out = self.body()
+        self.loss.copy_(out.detach())
+
+
 def _to(obj, device):
     if isinstance(obj, torch.Tensor):
         return obj.to(device, non_blocking=True)
@@ -119,11 +134,18 @@ class StepEngine:
 
     ``optimizer`` is a :class:`perceiver_io_amd.ops.optim.FusedAdamW` (flat buffers; the
     capturable path) or any ``torch.optim.Optimizer`` (eager only).
+
+    With ``graph`` on, a step of ``accumulate`` micro-batches replays ``accumulate - 1``
+    "micro" graphs (forward + backward adding into the flat gradient buffer) and one "last"
+    graph (forward + backward + the gradient all-reduce + fused AdamW, which also clears the
+    gradient it consumes).  Every graph of a step is captured before the step's first
+    micro-batch runs (the capture warm-ups clear the gradient buffer).  ``graph_impl``:
+    ``"cuda"`` (hipGraph; default on a GPU) or ``"closure"`` (:class:`ClosureGraph`, tests).
     """
 
     def __init__(self, loss_fn: Callable, optimizer, scheduler=None, reducer=None, device=None,
                  graph: bool = False, accumulate: int = 1, warmup_eager: int = 2, max_graphs: int = 12,
-                 state_hooks=None):
+                 state_hooks=None, graph_impl: Optional[str] = None):
         from ..ops.optim import FusedAdamW
 
         self.loss_fn = loss_fn
@@ -132,18 +154,19 @@ class StepEngine:
         self.reducer = reducer
         self.device = torch.device(device) if device is not None else torch.device("cpu")
         self.fused = isinstance(optimizer, FusedAdamW)
-        self.graph_enabled = bool(graph) and self.fused and self.device.type == "cuda"
+        self.graph_impl = graph_impl or ("cuda" if self.device.type == "cuda" else None)
+        self.graph_enabled = bool(graph) and self.fused and self.graph_impl is not None
         self.accumulate = max(1, int(accumulate))
         self.warmup_eager = warmup_eager
-        self.max_graphs = max(1, int(max_graphs))
+        self.max_graphs = max(2, int(max_graphs))
         # state_hooks = (save, restore): side state produced while capturing (e.g. the
         # trainer's logged metric tensors, which are static outputs of that graph) is saved per
         # graph and restored before each replay of it
         self.state_hooks = state_hooks
         self._graphs: "OrderedDict[tuple, _Captured]" = OrderedDict()
         self.captures = 0  # graphs captured so far (evictions included)
+        self.replays = 0
         self._eager_steps = 0
-        self._micro = 0
         # every step (eager warmups, capture, replays) runs on ONE dedicated stream: autograd's
         # AccumulateGrad nodes bind to the stream they were created on, and a capture whose
         # accumulations land on another stream silently leaves them outside the graph
@@ -153,7 +176,13 @@ class StepEngine:
         self.grad_scale_base = getattr(optimizer, "grad_scale", 1.0)
 
     # -- eager -----------------------------------------------------------------------------
+    def _arm(self, last: bool):
+        r = self.reducer
+        if r is not None and r.enabled:
+            r.arm() if last else r.disarm()
+
     def _eager_micro(self, batch, last: bool):
+        self._arm(last)
         loss = self.loss_fn(batch)
         (loss / self.accumulate if self.accumulate > 1 else loss).backward()
         if last:
@@ -178,50 +207,76 @@ class StepEngine:
             self.opt.zero_grad()
 
     # -- graph -----------------------------------------------------------------------------
-    def _capture(self, batch) -> _Captured:
-        opt = self.opt
+    @property
+    def _self_zeroing(self) -> bool:
+        # with the optimizer in the graph, the AdamW kernel clears the gradient it consumes, so a
+        # step needs no leading zero fill (gradients are zero between steps on every path: the
+        # capture's fill, eager steps' zero_grad, and the previous replay's update)
+        return self._opt_in_graph and self.opt.flat.grad_rep is None
+
+    def _capture(self, batch, kind: str) -> _Captured:
+        """Capture one step graph for ``batch``'s shape.  ``kind``: ``"last"`` (the optimizer
+        step's final micro-batch: backward + all-reduce + AdamW) or ``"micro"`` (an earlier
+        micro-batch of an accumulated step: backward only, adding into the gradient)."""
+        opt, red = self.opt, self.reducer
+        ddp = red is not None and red.enabled
         static = _clone_to(batch, self.device)
-        # warmup on the capture stream (allocator + lazy init); no optimizer update → nothing to undo
+        # warm-ups on the capture stream (allocator + lazy init), reducer disarmed: no collective
+        # is launched and nothing is left half-done for the captured backward; no optimizer
+        # update → nothing to undo but the gradient
+        if ddp:
+            red.disarm()
         for _ in range(2):
             opt.flat.zero_grad_buffers()
             loss = self.loss_fn(static)
             loss.backward()
             del loss
         opt.flat.zero_grad_buffers()
+        last = kind == "last"
         # the backward seed lives outside the graph (autograd would fill a fresh ones tensor
-        # inside it on every replay)
-        one = torch.ones((), device=self.device)
-        g = torch.cuda.CUDAGraph()
-        # with the optimizer in the graph, the AdamW kernel clears the gradient it consumes, so the
-        # replay needs no leading zero fill (gradients are zero between steps on every path: the
-        # fill above, eager steps' zero_grad, and the previous replay's update)
-        self_zeroing = self._opt_in_graph and opt.flat.grad_rep is None
-        with torch.cuda.graph(g, stream=self.stream):
-            if not self_zeroing:
+        # inside it on every replay); 1/accumulate averages the micro-batches
+        one = torch.full((), 1.0 / self.accumulate, device=self.device)
+        in_graph = last and self._opt_in_graph
+        zero_inside = last and self.accumulate == 1 and not self._self_zeroing
+
+        def body():
+            if zero_inside:
                 opt.flat.zero_grad_buffers()
+            if ddp:  # ready points fire inside the graph only when the collectives are captured
+                self._arm(in_graph)
             loss = self.loss_fn(static)
             loss.backward(one if loss.dim() == 0 and loss.dtype == one.dtype else None)
-            if self._opt_in_graph:
-                if self.reducer is not None and self.reducer.enabled:
-                    self.reducer.finish()
-                opt.device_update(zero_grad=self_zeroing)
+            if in_graph:
+                if ddp:
+                    red.finish()
+                opt.device_update(zero_grad=self._self_zeroing)
+            return loss
+
+        if self.graph_impl == "closure":
+            g = ClosureGraph()
+            g.body = body
+            g.loss = loss = torch.zeros((), device=self.device)
+        else:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=self.stream):
+                loss = body()
+            if ddp:
+                red.disarm()
         state = self.state_hooks[0]() if self.state_hooks is not None else None
         self.captures += 1
         return _Captured(g, static, loss, state, one)
 
-    def _graph_for(self, batch) -> _Captured:
+    def _graph_for(self, batch, kind: str = "last") -> _Captured:
         """The captured step for this batch's shape (captured on first sight, LRU-cached)."""
-        key = shape_key(batch)
+        key = (kind,) + shape_key(batch)
         ent = self._graphs.get(key)
         if ent is not None:
             self._graphs.move_to_end(key)
-            if self.state_hooks is not None:
-                self.state_hooks[1](ent.state)
             return ent
         while len(self._graphs) >= self.max_graphs:
             _, old = self._graphs.popitem(last=False)
             del old  # its private pool is released with the graph
-        ent = self._capture(batch)
+        ent = self._capture(batch, kind)
         self._graphs[key] = ent
         return ent
 
@@ -234,12 +289,16 @@ class StepEngine:
         r = self.reducer
         return r is None or not r.enabled or getattr(r, "in_graph", False)
 
+    def _kinds(self, n: int):
+        return ["micro"] * (n - 1) + ["last"]
+
     def step(self, batch):
         """One optimizer step (``accumulate`` micro-batches must be passed as a list)."""
         if self.stream is None:
             return self._step(batch)
-        if (self.graph_enabled and self.accumulate == 1 and self._eager_steps >= self.warmup_eager
-                and self._opt_in_graph and shape_key(batch) in self._graphs):
+        batches = batch if (self.accumulate > 1 and isinstance(batch, list)) else [batch]
+        if (self.graph_enabled and self._eager_steps >= self.warmup_eager and self._opt_in_graph
+                and all((k,) + shape_key(b) in self._graphs for k, b in zip(self._kinds(len(batches)), batches))):
             # a replay needs no autograd stream binding: staging, graph and loss copy go straight
             # onto the caller's stream (a cross-stream event hop costs ~10 µs of GPU idle each way)
             return self._step(batch)
@@ -251,27 +310,47 @@ class StepEngine:
         return out
 
     def _step(self, batch):
+        try:
+            return self._step_inner(batch)
+        except BaseException:
+            if self.reducer is not None:
+                self.reducer.reset()
+            raise
+
+    def _stage(self, ent, b, hyper: bool):
+        if self.graph_impl == "closure":
+            _copy_into(ent.batch, b)
+            if hyper:
+                self.opt.stage_hyper()
+        else:
+            _stage_step(ent.batch, b, self.opt if hyper else None)
+
+    def _step_inner(self, batch):
         batches = batch if (self.accumulate > 1 and isinstance(batch, list)) else [batch]
-        if self.graph_enabled and self.accumulate == 1:
-            b = batches[0]
-            if self._eager_steps < self.warmup_eager:
-                self._eager_steps += 1
-                loss = self._eager_micro(_to(b, self.device), True)
-                self._optimizer_step()
-                return loss.detach()
-            ent = self._graph_for(b)
+        if self.graph_enabled and self._eager_steps >= self.warmup_eager:
+            kinds = self._kinds(len(batches))
+            # every graph of this step first: a capture's warm-ups clear the gradient buffer
+            ents = [self._graph_for(b, k) for b, k in zip(batches, kinds)]
+            if len(batches) > 1 and not self._self_zeroing:
+                self.opt.flat.zero_grad_buffers()
+            for i, (b, ent) in enumerate(zip(batches, ents)):
+                last = i == len(batches) - 1
+                if self.state_hooks is not None:
+                    self.state_hooks[1](ent.state)
+                # batch copies (+ the optimizer's hyper-parameters before the update graph): one launch
+                self._stage(ent, b, last and self._opt_in_graph)
+                ent.graph.replay()
+                self.replays += 1
             if self._opt_in_graph:
-                _stage_step(ent.batch, b, self.opt)  # batch copies + hyper-parameters: one launch
-                ent.graph.replay()
                 self.opt._step += 1
-            else:  # forward+backward replayed; RCCL all-reduce + update eager (3 launches)
-                _stage_step(ent.batch, b)
-                ent.graph.replay()
+            else:  # forward+backward replayed; the all-reduce + update eagerly (3 launches)
                 self.reducer.finish()
                 self.opt.step()
             if self.sched is not None:
                 self.sched.step()
-            return ent.loss.detach().clone()
+            return ents[-1].loss.detach().clone()
+        if self.graph_enabled:
+            self._eager_steps += 1
         loss = None
         for i, b in enumerate(batches):
             loss = self._eager_micro(_to(b, self.device), i == len(batches) - 1)

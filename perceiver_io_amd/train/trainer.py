@@ -324,9 +324,9 @@ class Trainer:
                 flat = getattr(opt, "flat", None) or FlatParameterSpace(
                     [p for p in model.parameters() if p.requires_grad], with_shadow=False)
                 reducer = FlatGradReducer(flat)
-                dec = getattr(getattr(model, "model", None), "decoder", None)
-                if dec is not None:  # decoder + head gradients are final first: the early bucket
-                    reducer.set_early_params(dec.parameters())
+                net = getattr(model, "model", None)
+                if net is not None:  # ready points: decoder + head, then layer_n (overlapped all-reduce)
+                    reducer.plan(net)
                 reducer.broadcast_parameters(model)
             if not self.fused and self.gradient_clip_val:
                 warnings.warn("gradient clipping on the eager path uses torch.nn.utils.clip_grad_norm_")
@@ -338,8 +338,7 @@ class Trainer:
             # graph, restored before its replays
             hooks = (lambda: dict(self._step_logs), self._restore_step_logs)
             self._engine = StepEngine(self._training_loss, opt, sched, reducer=reducer, device=self.device,
-                                      graph=bool(use_graph) and self.accumulate == 1, accumulate=self.accumulate,
-                                      state_hooks=hooks)
+                                      graph=bool(use_graph), accumulate=self.accumulate, state_hooks=hooks)
             if self.logger is not None and self.is_global_zero:
                 self.logger.log_hyperparams(dict(model.hparams))
             for cb in self.callbacks:
@@ -348,7 +347,11 @@ class Trainer:
                 self.sanity_checking = True
                 self._run_eval(val_dl, "validation", limit=self.num_sanity_val_steps)
                 self.sanity_checking = False
-            self._fit_loop(train_dl, val_dl)
+            try:
+                self._fit_loop(train_dl, val_dl)
+            finally:
+                if reducer is not None:
+                    reducer.close()  # never the target of a later fit's ready points
             for cb in self.callbacks:
                 cb.on_fit_end(self, model)
         if self.logger is not None:
@@ -468,10 +471,12 @@ class Trainer:
 
     def _eager_clip_step(self, batches):
         opt = self.optimizers[0]
-        for b in batches:
+        red = self._engine.reducer
+        for i, b in enumerate(batches):
+            if red is not None and red.enabled:  # ready points only in the last micro-batch's backward
+                red.arm() if i == len(batches) - 1 else red.disarm()
             loss = self._training_loss(b)
             (loss / len(batches)).backward()
-        red = self._engine.reducer
         if red is not None:
             red.finish()
             if red.enabled:  # all-reduced SUM → mean before clipping (clip the mean's norm)

@@ -1,0 +1,127 @@
+"""Data parallelism on the GPU (one MI355X): the step engine's hipGraph path with the reducer.
+
+* 2 ranks on the one card over gloo (RCCL refuses two ranks on one device): the captured
+  forward/backward replays, the all-reduce + fused AdamW run after it (gloo collectives are not
+  capturable).  Deterministic mode: after 5 steps both ranks hold bitwise-identical parameters,
+  equal to the same ranks' eager steps.
+* RCCL collectives INSIDE the step graph (the 8-GPU path, ``in_graph``), on a 1-rank RCCL group
+  with the reducer forced on: the ready points fire during capture, their all-reduces run on the
+  side stream inside the graph, and the replayed steps equal the plain single-GPU graph bitwise.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+STEPS = 5
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _setup(seed=0):
+    from perceiver_io_amd import ops
+    from perceiver_io_amd.tasks import LitMaskedLanguageModel
+
+    ops.set_deterministic(True)
+    ops.masking.reset_mask_state()  # recreated from the seeded generator at the first masking
+    torch.manual_seed(seed)
+    lit = LitMaskedLanguageModel(vocab_size=1000, max_seq_len=128,
+                                 optimizer_init={"class_path": "torch.optim.AdamW", "init_args": {"lr": 1e-3}},
+                                 num_latents=64, num_latent_channels=64, num_encoder_layers=3,
+                                 num_encoder_self_attention_layers_per_block=2, masked_samples=None)
+    return lit.model.cuda()
+
+
+def _data(rank, n):
+    g = torch.Generator().manual_seed(123 + rank)
+    out = []
+    for _ in range(n):
+        ids = torch.randint(3, 1000, (8, 128), generator=g)
+        pad = torch.zeros(8, 128, dtype=torch.bool)
+        pad[2, 100:] = True
+        out.append((ids.cuda(), pad.cuda()))
+    return out
+
+
+def _run(model, red, graph, data):
+    from perceiver_io_amd.ops.optim import FusedAdamW
+    from perceiver_io_amd.train.engine import StepEngine
+
+    opt = FusedAdamW(model.parameters(), lr=1e-3, weight_decay=0.01)
+    if red is not None:
+        red = red(opt.flat)
+        red.plan(model)
+        red.broadcast_parameters(model)
+    eng = StepEngine(lambda b: model.loss(b[0], b[1]), opt, reducer=red, device="cuda", graph=graph)
+    for b in data:
+        eng.step(b)
+    torch.cuda.synchronize()
+    return opt, red, eng
+
+
+def _worker_gloo(rank, world, port, out):
+    os.environ.update(RANK=str(rank), LOCAL_RANK="0", WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), PERCEIVER_DIST_BACKEND="gloo")
+    from perceiver_io_amd.parallel import FlatGradReducer, dist
+    from perceiver_io_amd.parallel.reducer import params_in_sync
+
+    dist.init()
+    res = {}
+    for graph in (True, False):
+        model = _setup()
+        opt, red, eng = _run(model, lambda f: FlatGradReducer(f), graph, _data(rank, STEPS))
+        res[graph] = dict(params=opt.flat.data.cpu(), sync=params_in_sync(opt.flat), in_graph=red.in_graph,
+                          log=list(red.launch_log), replays=eng.replays)
+        red.close()
+    out[rank] = res
+    dist.shutdown()
+
+
+def test_two_ranks_graph_steps_bitwise_in_sync():
+    world, port = 2, _port()
+    out = mp.get_context("spawn").Manager().dict()
+    mp.spawn(_worker_gloo, args=(world, port, out), nprocs=world, join=True)
+    for r in range(world):
+        g, e = out[r][True], out[r][False]
+        assert g["sync"] == 0.0 and e["sync"] == 0.0
+        assert not g["in_graph"]  # gloo: the collectives run after the replayed backward
+        assert g["replays"] == STEPS - 2  # 2 eager warm-up steps, then captured steps
+        assert g["log"] == ["decoder", "layer_n"] * 2  # ready points fire in the eager steps only
+        assert e["log"] == ["decoder", "layer_n"] * STEPS
+        assert torch.equal(g["params"], e["params"]), (g["params"] - e["params"]).abs().max()
+    assert torch.equal(out[0][True]["params"], out[1][True]["params"])
+
+
+def test_rccl_collectives_inside_the_step_graph():
+    import torch.distributed as tdist
+
+    from perceiver_io_amd.parallel import FlatGradReducer
+
+    tdist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1,
+                             device_id=torch.device("cuda", 0))
+    try:
+        data = _data(0, STEPS)
+        model = _setup()
+        opt, red, eng = _run(model, lambda f: FlatGradReducer(f, in_graph=True, force=True), True, data)
+        assert red.enabled and red.in_graph and eng.replays == STEPS - 2
+        # eager steps 1, 2 and the capture's backward (the replays run no Python)
+        assert red.launch_log == ["decoder", "layer_n"] * 3
+        red.close()
+        ref_model = _setup()
+        ref_opt, _, _ = _run(ref_model, None, True, data)
+        assert torch.equal(opt.flat.data, ref_opt.flat.data), (opt.flat.data - ref_opt.flat.data).abs().max()
+    finally:
+        from perceiver_io_amd import ops
+
+        ops.set_deterministic(False)
+        tdist.destroy_process_group()

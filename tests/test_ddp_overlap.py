@@ -1,8 +1,8 @@
 """Overlapped, bucketed gradient all-reduce and gradient clipping under data parallelism
 (gloo on CPU, 2 and 4 ranks).
 
-* The early bucket (decoder + head, the tail of the flat buffer) is launched from the backward
-  pass when autograd reaches the decoder input (``parallel/reducer.py`` ``_ReadyFn``).  If any
+* The ready-point buckets (decoder + head, the tail of the flat buffer; then layer_n) are launched
+  from the backward pass when autograd reaches the decoder input / layer_n's input (``parallel/reducer.py`` ``_ReadyFn``).  If any
   decoder-side gradient were still incomplete at that point the reduced values would differ, so
   bit-identity with the non-overlapped reducer pins the readiness ordering — here with the FUSED
   executor (kernel emulation on CPU: deferred weight-gradient slab jobs, in-place gradient
@@ -69,8 +69,9 @@ def _worker_overlap(rank, world, port, fused, out):
     res = {}
     for overlap in (False, True):
         red = FlatGradReducer(flat, bucket_bytes=16 << 10, overlap=overlap)
-        red.set_early_params(model.decoder.parameters())
+        red.plan(model)
         flat.zero_grad()
+        red.arm()
         loss = model.loss(x, pad, labels=lab, x_masked=xm)
         loss.backward()
         red.finish()
@@ -87,8 +88,8 @@ def test_overlapped_buckets_bit_identical(world, fused):
     mp.spawn(_worker_overlap, args=(world, port, fused, out), nprocs=world, join=True)
     for r in range(world):
         (g0, n0, nb0, e0), (g1, n1, nb1, e1) = out[r][False], out[r][True]
-        assert e0 is not None and e0[1] > e0[0]  # the decoder is a contiguous tail bucket
-        assert n0 == 0 and n1 == 1  # only the overlapped reducer launched from the backward
+        assert e1 is not None and e1[1] > e1[0]  # the decoder is a contiguous tail bucket
+        assert n0 == 0 and n1 == 2  # only the overlapped reducer launched from the backward (decoder, layer_n)
         assert nb0 == nb1 >= 2
         assert torch.equal(g0, g1), (r, (g0 - g1).abs().max())
     assert all(torch.equal(out[0][True][0], out[r][True][0]) for r in range(world))

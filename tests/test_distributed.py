@@ -116,3 +116,24 @@ def test_two_rank_trainer_fit(tmp_path):
     assert out[0][1] == 2 and out[1][1] == 2
     assert torch.allclose(out[0][0], out[1][0])  # replicas stay in sync
     assert os.path.exists(out[0][2])
+
+
+def test_bench_self_spawns_ranks_cpu_dry_run():
+    """``python bench.py --gpus 2`` without a torchrun environment starts 2 ranks itself (a CPU
+    dry run over gloo here); the JSON line reports both and that their parameters agree."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+                        "--batch", "2", "--seq-len", "32", "--latents", "16", "--channels", "32", "--vocab", "300"],
+                       capture_output=True, text=True, env=env, timeout=600, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 4
+    assert out["dist_backend"] == "gloo" and out["params_in_sync"] is True
+    assert out["config"]["allreduce_overlap"] == ["decoder", "layer_n"]
