@@ -43,13 +43,20 @@ def _setup(seed=0):
 
 
 def _data(rank, n):
+    """Batches with their masking drawn up front (ids, pad, labels, masked ids): the capture
+    warm-ups of the graph path run extra forwards, which would advance the device masking RNG
+    and make graph and eager runs see different masks."""
+    from perceiver_io_amd.models.perceiver import TextMasking
+
     g = torch.Generator().manual_seed(123 + rank)
+    masking = TextMasking(1000)
     out = []
     for _ in range(n):
         ids = torch.randint(3, 1000, (8, 128), generator=g)
         pad = torch.zeros(8, 128, dtype=torch.bool)
         pad[2, 100:] = True
-        out.append((ids.cuda(), pad.cuda()))
+        xm, lab = masking(ids, pad, generator=g)
+        out.append(tuple(t.cuda() for t in (ids, pad, lab, xm)))
     return out
 
 
@@ -62,7 +69,7 @@ def _run(model, red, graph, data):
         red = red(opt.flat)
         red.plan(model)
         red.broadcast_parameters(model)
-    eng = StepEngine(lambda b: model.loss(b[0], b[1]), opt, reducer=red, device="cuda", graph=graph)
+    eng = StepEngine(lambda b: model.loss(b[0], b[1], labels=b[2], x_masked=b[3]), opt, reducer=red, device="cuda", graph=graph)
     for b in data:
         eng.step(b)
     torch.cuda.synchronize()
