@@ -7,10 +7,13 @@ saved to ``<data_dir>/imdb-tokenizer-<vocab>.json`` when missing (``Replace('<br
 + NFD/Lowercase/StripAccents, like the reference).  Validation uses the IMDB *test* split.
 
 Tokenizer: the reference ships its trained WordPiece tokenizer as
-``.cache/imdb-tokenizer-10003.json`` (vocab 10003, [PAD]/[UNK]/[MASK] = 0/1/2).  Copy that file
-to ``<data_dir>/imdb-tokenizer-<vocab>.json`` (the default ``data_dir`` is ``.cache``, so the
-reference's location works as is) or pass ``tokenizer_path=``: an existing file is loaded as is
-and never retrained, so token ids match checkpoints trained by the reference.
+``.cache/imdb-tokenizer-10003.json`` (vocab 10003, [PAD]/[UNK]/[MASK] = 0/1/2; reference
+``data/imdb.py:82,96-106`` loads it from ``<data_dir>`` or trains one).  The same vocabulary
+ships here as package data (``data/assets/imdb-tokenizer-10003.json``, Apache-2.0, a data
+artifact of the reference): a real-data run at vocab 10003 with no tokenizer in ``<data_dir>``
+installs it there instead of training a new one, so default runs use the reference's token ids.
+An existing ``<data_dir>/imdb-tokenizer-<vocab>.json`` or ``tokenizer_path=`` is loaded as is
+and never retrained.
 
 ``synthetic=True`` generates token sequences of the same shape (and a matching tokenizer)
 so every task runs without the dataset: ``synthetic_structure="topic"`` (default) mixes Zipf,
@@ -77,6 +80,11 @@ class Collator:
         return self.collate([(0, s) for s in samples])[1:]
 
 
+def shipped_tokenizer(vocab_size: int = 10003) -> str:
+    """Path of the packaged reference tokenizer for ``vocab_size`` (exists for 10003 only)."""
+    return os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", f"imdb-tokenizer-{vocab_size}.json")
+
+
 @register_datamodule
 class IMDBDataModule:
     def __init__(self, data_dir: str = ".cache", vocab_size: int = 10003, max_seq_len: int = 512, batch_size: int = 64,
@@ -119,6 +127,11 @@ class IMDBDataModule:
             raise FileNotFoundError(f"tokenizer_path={self.tokenizer_path} does not exist")
         if not os.path.exists(self.tokenizer_path):
             os.makedirs(self.data_dir, exist_ok=True)
+            if not self.synthetic and os.path.exists(shipped_tokenizer(self.vocab_size)):
+                import shutil
+
+                shutil.copyfile(shipped_tokenizer(self.vocab_size), self.tokenizer_path)  # the reference vocabulary
+                return
             if self.synthetic:
                 ds = self._synthetic("train")
                 text = (ds[i][1] for i in range(min(len(ds), 2000)))

@@ -9,11 +9,16 @@ a single :class:`_LayerFn` whose forward is
 
 i.e. 3 kernel launches, and whose backward is the hand-written reverse chain
 (post_attn_bwd → attn_bwd → ln_linear_bwd), 3 launches as well: each weight gradient is an
-extra MFMA pass over LDS tiles the producing kernel already holds, and all parameter gradients
-are accumulated by the kernels straight into ``p.grad`` (views of the flat gradient buffer) with
-device atomics — no per-parameter autograd accumulation, no reduction pass.  Activations
-kept for backward: the bf16 Q/K/V and attention output, fp32 post-attention residual,
-LN statistics, the bf16 pre-GELU tensor — LN outputs and GELU outputs are recomputed.
+extra MFMA pass over LDS tiles the producing kernel already holds.  Parameter gradients go
+through per-tile slabs by default (``WGRAD_SLAB``, see ``_GradSlab``): each 64-row tile STORES
+its partial into one slab row, and the slab rows are summed into ``p.grad`` (views of the flat
+gradient buffer) by extra workgroups appended to the next backward kernel, or by an
+end-of-backward flush — no float atomics, no per-parameter autograd accumulation
+(``PERCEIVER_WGRAD_SLAB=0`` restores in-kernel atomics into replicated accumulators).
+Self-attention blocks run as one node (``_SABlockFn``): one launch per layer forward and per
+layer boundary backward.  Activations kept for backward: the bf16 Q/K/V and attention output,
+fp32 post-attention residual, LN statistics, the bf16 pre-GELU tensor — LN outputs and GELU
+outputs are recomputed.
 
 Encoder-specific savings over the reference forward:
   * the learned latent array enters the first layer un-expanded (batch stride 0): its

@@ -6,11 +6,14 @@ The Perceiver step is launch/latency-bound on MI355X (the referenc
 engine captures the step once into a hipGraph (``torch.cuda.CUDAGraph`` is hipGraph on
 ROCm) and replays it: one host call per step, no per-kernel launch overhead, no Python in
 the loop.  Everything inside the step is capture-safe by construction: no host syncs
-(sync-free masking, fixed-capacity MLM row compaction), RNG via the graph-aware torch
-generator, optimizer hyper-parameters read from device memory (staged before replay).
+(sync-free masking, fixed-capacity MLM row compaction); masking draws from its own device
+counter-hash state (``ops/masking.py``) and dropout seeds from torch's graph-aware generator,
+both advanced on every replay; optimizer hyper-parameters are read from device memory (staged
+before replay).
 
 Gradient accumulation: ``accumulate`` micro-batches per optimizer step (the all-reduce and
-update run only on the last one, as in Lightning's ``accumulate_grad_batches``).
+update run only on the last one, as in Lightning's ``accumulate_grad_batches``) — on the graph
+path as ``accumulate - 1`` "micro" graph replays plus one "last" graph.
 
 Variable batch shapes (the reference's IMDB collator pads to the longest sequence of each
 batch, ``data/imdb.py:52-63``, and its loaders keep the partial last batch): captured graphs

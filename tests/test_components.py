@@ -235,3 +235,32 @@ def test_checked_variant_is_built_and_flagged():
     except ImportError as e:  # pragma: no cover - depends on the build state
         pytest.skip(f"extension not built: {e}")
     assert not rel.checked_build() and chk.checked_build()
+
+
+def test_shipped_reference_tokenizer_installed_for_real_data(tmp_path):
+    """A real-data IMDB run at vocab 10003 without a tokenizer in data_dir installs the shipped
+    reference vocabulary (reference .cache/imdb-tokenizer-10003.json) instead of training one."""
+    import filecmp
+    import os
+
+    from perceiver_io_amd.data.imdb import IMDBDataModule, shipped_tokenizer
+    from perceiver_io_amd.utils.tokenizer import MASK_TOKEN, PAD_TOKEN, UNK_TOKEN
+
+    for split in ("train", "test"):
+        for lab in ("neg", "pos"):
+            d = tmp_path / "IMDB" / "aclImdb" / split / lab
+            d.mkdir(parents=True)
+            (d / "0_1.txt").write_text("a tiny review<br />of a movie")
+    dm = IMDBDataModule(data_dir=str(tmp_path), vocab_size=10003, max_seq_len=16, batch_size=2, num_workers=0)
+    dm.prepare_data()
+    path = os.path.join(str(tmp_path), "imdb-tokenizer-10003.json")
+    assert filecmp.cmp(path, shipped_tokenizer(10003), shallow=False)
+    dm.setup("fit")
+    tok = dm.tokenizer
+    assert tok.get_vocab_size() == 10003
+    assert [tok.token_to_id(t) for t in (PAD_TOKEN, UNK_TOKEN, MASK_TOKEN)] == [0, 1, 2]
+    ref = "/root/reference/.cache/imdb-tokenizer-10003.json"
+    if os.path.exists(ref):  # byte-identical to the reference's shipped file
+        assert filecmp.cmp(ref, shipped_tokenizer(10003), shallow=False)
+    ids = tok.encode("i have watched this [MASK] and it was awesome").ids
+    assert 2 in ids and 1 not in ids
