@@ -25,6 +25,13 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
+# MFMA results in VGPRs (no AGPR staging) for the translation units whose kernels post-process
+# accumulators with VALU (softmax, LayerNorm, GELU) and fit 256 VGPRs; rowgemm.hip keeps the
+# default (its 160-channel LN-linear backward would spill without the AGPR file)
+_VGPR_FORM = ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]
+PER_FILE_FLAGS = {"chain.hip": _VGPR_FORM}
+
+
 def _torch_paths():
     import torch.utils.cpp_extension as ce
 
@@ -67,10 +74,11 @@ def build(force: bool = False, jobs: int = 0, debug: bool = False, verbose: bool
     objs = []
     todo = []
     for src in hip_srcs:
-        obj = bdir / f"{src.stem}.{_digest([src] + headers, hip_flags)}.o"
+        flags = hip_flags + PER_FILE_FLAGS.get(src.name, [])
+        obj = bdir / f"{src.stem}.{_digest([src] + headers, flags)}.o"
         objs.append(obj)
         if force or not obj.exists():
-            todo.append([HIPCC, *hip_flags, "-I", str(HERE), "-c", str(src), "-o", str(obj)])
+            todo.append([HIPCC, *flags, "-I", str(HERE), "-c", str(src), "-o", str(obj)])
     inc, libdir = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
     name = "_C_check" if check else "_C"

@@ -331,12 +331,60 @@ __device__ __forceinline__ void slab_reduce_block(const SlabJob& j, int b, float
   }
 }
 
+// fp32 gradient targets of the post-attention block (views of the flat gradient buffer).
+// Two sinks for a workgroup's parameter-gradient partials:
+//  * atomic (slab = 0): targets may be replicated: workgroup i adds into replica
+//    i % kGradReplicas, vrs floats apart (vrs = 0: one copy), folded once per step;
+//  * slab (slab = 1): workgroup i STORES its partials into row i of a (tiles, P) fp32 slab
+//    (vrs = P floats per row).  Float atomics execute at the memory side at ≈1.3 TB/s
+//    chip-wide, so 256 tiles × 50 KB of partials per kernel cost ≈10 µs of a ≈25 µs kernel;
+//    plain stores cost ≈0.3 µs per CU, and the slab rows are summed by a SlabJob.
+constexpr int kGradReplicas = 8;
+struct PostAttnGrads {
+  float *dWo, *dbo, *dg2, *dbe2, *dW1, *db1, *dW2, *db2;
+  int vrs;
+  int slab;
+};
+__device__ __forceinline__ float* rep(float* p, int vrs, int slab) {
+  return p + (long long)(slab ? blockIdx.x : (blockIdx.x & (kGradReplicas - 1))) * vrs;
+}
+__device__ __forceinline__ void gadd(float* p, float v, int slab) {
+  if (slab) *p = v;
+  else atomicAdd(p, v);
+}
+
+
 // ---- GELU (erf form, nn.GELU default) ------------------------------------------------
-__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+// Branch-free: erf(|z|) = 1 − t·P(t)·exp(−z²), t = 1/(1 + 0.3275911·|z|) (Abramowitz & Stegun
+// 7.1.26, |error| ≤ 1.5e-7), z = x/√2 — one v_rcp, one v_exp and five FMAs.  The device
+// library's erff branches on |z| < 1 (both sides run when the lanes of a wave straddle it) and
+// its expf adds a range reduction: ≈45 instructions per call against ≈12 here, and exp(−z²) is
+// the Gaussian factor of the derivative too (gelu_pair: both for one exp).
+__device__ __forceinline__ float gelu_cdf_e(float x, float& e) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.f));
+  e = __builtin_amdgcn_exp2f(-0.72134752044448170f * x * x);  // exp(−x²/2) = exp(−z²)
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float erf_abs = fmaf(-p * t, e, 1.f);
+  return 0.5f + 0.5f * copysignf(erf_abs, x);  // Φ(x) = ½(1 + erf(x/√2))
+}
+__device__ __forceinline__ float gelu_f(float x) {
+  float e;
+  return x * gelu_cdf_e(x, e);
+}
 __device__ __forceinline__ float gelu_grad(float x) {
-  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
+  float e;
+  const float cdf = gelu_cdf_e(x, e);
+  return fmaf(x * 0.39894228040143268f, e, cdf);  // Φ(x) + x·φ(x)
+}
+__device__ __forceinline__ void gelu_pair(float x, float& gelu, float& grad) {
+  float e;
+  const float cdf = gelu_cdf_e(x, e);
+  gelu = x * cdf;
+  grad = fmaf(x * 0.39894228040143268f, e, cdf);
 }
 
 // ---- counter-based RNG for dropout (regenerated in backward, no mask storage) -------

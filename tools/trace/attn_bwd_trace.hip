@@ -45,7 +45,7 @@ int main(int argc, char** argv) {
   const long long bs = (long long)N * 3 * C;
   auto launch = [&]() {
     pio::attn_bwd_launch(a, D, nullptr, dO, lse, delta, dqkv, bs, 3 * C, dqkv + C, bs, 3 * C, dqkv + 2 * C, bs, 3 * C,
-                         false, false, 0, 0, 0);
+                         false, false, 0, 1, 0, 0);
   };
   long long *tb, *twg;
   const int nwg = B * H * ((N + 255) / 256);
