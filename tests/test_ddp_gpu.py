@@ -132,3 +132,55 @@ def test_rccl_collectives_inside_the_step_graph():
 
         ops.set_deterministic(False)
         tdist.destroy_process_group()
+
+
+def test_graph_gradient_accumulation_matches_eager_and_big_batch():
+    """accumulate_grad_batches = 4 on the graph path (3 "micro" replays + 1 "last" replay per
+    optimizer step, no eager step after the warm-up): bitwise equal to eager accumulation in
+    deterministic mode, and equal to one step on the 4× batch up to the mean-of-means weighting
+    (identical here: every micro-batch selects the same number of MLM targets)."""
+    from perceiver_io_amd import ops
+    from perceiver_io_amd.ops.optim import FusedAdamW
+    from perceiver_io_amd.train.engine import StepEngine
+
+    steps, acc = 4, 4
+    data = _data(0, steps * acc)
+    # equal target counts per micro-batch, so the mean of the micro means is the big-batch mean
+    for i, (ids, pad, lab, xm) in enumerate(data):
+        lab = torch.full_like(lab, -100)
+        lab[:, 5:29] = ids[:, 5:29]  # 24 targets per row: within the MLM row capacities
+        data[i] = (ids, pad, lab, xm)
+    res = {}
+    try:
+        for mode in ("graph", "eager", "big"):
+            model = _setup()
+            # eps ≫ |g|: the update is ~linear in the gradient, so comparing updates compares the
+            # accumulated gradients (with eps = 1e-8 Adam turns round-off in near-zero gradient
+            # entries into full ±lr steps)
+            opt = FusedAdamW(model.parameters(), lr=1e-2, eps=1.0, weight_decay=0.0)
+
+            def loss_fn(b):
+                return model.loss(b[0], b[1], labels=b[2], x_masked=b[3])
+
+            if mode == "big":
+                eng = StepEngine(loss_fn, opt, device="cuda", graph=False)
+                for s in range(steps):
+                    micro = data[s * acc:(s + 1) * acc]
+                    eng.step(tuple(torch.cat([m[j] for m in micro]) for j in range(4)))
+            else:
+                eng = StepEngine(loss_fn, opt, device="cuda", graph=mode == "graph", accumulate=acc)
+                for s in range(steps):
+                    eng.step(data[s * acc:(s + 1) * acc])
+            torch.cuda.synchronize()
+            res[mode] = (opt.flat.data.clone(), eng.replays, eng.captures)
+    finally:
+        ops.set_deterministic(False)
+    g, e, big = res["graph"], res["eager"], res["big"]
+    assert g[2] == 2 and g[1] == (steps - 2) * acc  # micro + last graphs; eager warm-up steps 1, 2
+    assert torch.equal(g[0], e[0]), (g[0] - e[0]).abs().max()
+    init = _setup()
+    from perceiver_io_amd.ops.optim import FlatParameterSpace
+
+    p0 = FlatParameterSpace(list(init.parameters()), with_shadow=False).data.cuda()
+    rel = ((g[0] - big[0]).norm() / (big[0] - p0).norm()).item()
+    assert rel < 2e-2, rel  # bf16 kernels: different row grouping, same maths
