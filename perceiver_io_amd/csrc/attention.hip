@@ -535,7 +535,32 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
     lds_sync();
     PIO_TS(4 + 4 * ((qt0 - qt_begin) / NQS));
     // dQ of tile j = w: Σ over the block's keys of dS[key][q] · K[key][d]
-    if (w < NQS && qt0 + w < nqt) {
+    if constexpr (D == 16 && NW == 8 && NQS == 4) {
+      // head width 16: every wave takes 16 queries (tile w & 3, half w >> 2) × the 16 head dims
+      // with 16x16x32 MFMAs over the KB keys — no idle waves, and none of the 32x32 tile's
+      // padding columns (the 32x32x16 form below computes 32 dims of which 16 are real)
+      const int j = w & 3, mh = w >> 2, g = l >> 4;
+      if (qt0 + j < nqt) {
+        const uint16_t* tS = sdS + j * KB * LDS_;
+        f32x4 a0 = f32x4{0.f, 0.f, 0.f, 0.f}, a1 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k0 = 0; k0 < KB; k0 += 64) {
+          a0 = mfma16(frag16_tr(tS, LDS_, 16 * mh, k0), frag16_tr(sK, LD, 0, k0), a0);
+          a1 = mfma16(frag16_tr(tS, LDS_, 16 * mh, k0 + 32), frag16_tr(sK, LD, 0, k0 + 32), a1);
+        }
+        // accumulator: col = l & 15 = head dim, row = 4g + i = query within the 16
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int qq = (qt0 + j) * 32 + 16 * mh + 4 * g + i;
+          if (qq < a.Nq) {
+            float* dst = dq + (long long)b * dq_bs + (long long)qq * dq_rs + h * D + (l & 15);
+            const float v = (a0[i] + a1[i]) * a.scale;
+            if (dq_atomic) atomicAdd(dst, v);
+            else *dst = v;
+          }
+        }
+      }
+    } else if (w < NQS && qt0 + w < nqt) {
       const uint16_t* tS = sdS + w * KB * LDS_;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
@@ -639,6 +664,17 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
     }
   PIO_TS(41);
   PIO_WG_END();
+}
+
+// host ABI check (binding.cpp mirrors these structs)
+int abi_struct_size(int which) {
+  switch (which) {
+    case 0: return (int)sizeof(DropCfg);
+    case 1: return (int)sizeof(PostAttnGrads);
+    case 2: return (int)sizeof(SlabJob);
+    case 3: return (int)sizeof(AttnArgs);
+    default: return -1;
+  }
 }
 
 // zero rows of a strided fp32 (B, N, W) view (dQ accumulator when several key blocks add into it)

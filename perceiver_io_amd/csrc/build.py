@@ -88,7 +88,10 @@ def build(force: bool = False, jobs: int = 0, debug: bool = False, verbose: bool
                  *san,
                  "-isystem", "/opt/rocm/include", "-isystem", py_inc] + sum((["-isystem", p] for p in inc), [])
     bsrc = HERE / "binding.cpp"
-    bobj = bdir / f"binding.{_digest([bsrc], cxx_flags)}.o"
+    # binding.cpp includes common.h (SlabJob, DropCfg, … are passed by value to the launchers):
+    # its object must be rebuilt when a header changes, or the host and the kernels disagree on
+    # a struct layout
+    bobj = bdir / f"binding.{_digest([bsrc] + headers, cxx_flags)}.o"
     if force or not bobj.exists():
         todo.append(["g++", *cxx_flags, "-c", str(bsrc), "-o", str(bobj)])
     if todo:

@@ -21,9 +21,6 @@ namespace pio {
 // residual, LN2, W1, GELU, W2, residual, LN1 + the next projection — runs per wave, from
 // registers, with no LDS round trip of an activation and no workgroup barrier.
 // ------------------------------------------------------------------------------------
-__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
 // B fragment of k-step t from a CL activation (permuted k order)
 template <int NM>
 __device__ __forceinline__ bf16x8 cl_bfrag(const float (&v)[NM][4], int t) {
@@ -387,17 +384,6 @@ __global__ __launch_bounds__(256) void sa_layer_fwd_chain_kernel(
 //      LayerNorm-ed operand is applied in the epilogue (dW = γ∘(Gᵀ·x̂) + β⊗db), so only x̂ is
 //      staged.  Partials go to this tile's slab row (plain stores).
 // ------------------------------------------------------------------------------------
-// 16x16x32 operand from a k-strided LDS image (element (i, k) at base[k·ld + i]), natural k
-__device__ __forceinline__ bf16x8 frag16_tr(const uint16_t* lds, int ld, int i0, int k0) {
-  const int l = lane_id(), g = l >> 4, i = l & 15;
-  const uint16_t* base = lds + (k0 + 8 * g + (i >> 2)) * ld + i0 + 4 * (i & 3);
-  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(base));
-  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(base + 4 * ld));
-  bf16x8 r;
-  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
-  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
-  return r;
-}
 // the same in the CL k order of k-step t (element j ↔ k = 32t + 16(j >> 2) + 4g + (j & 3))
 __device__ __forceinline__ bf16x8 frag16_tr_cl(const uint16_t* lds, int ld, int i0, int t) {
   const int l = lane_id(), g = l >> 4, i = l & 15;
@@ -437,9 +423,14 @@ __device__ __forceinline__ bf16x8 ones_frag() {
 // slab partial of one 16-row block (m-tile mt) of a 64-column weight gradient
 //   dW[m][n] = Σ_r A[r][m]·B[r][n]  (A, B bf16 row-major LDS images over the 64 rows)
 // and its bias db[m] = Σ_r A[r][m]; with an LN affine (γ, β over n): dW = γ[n]·dW + β[n]·db[m]
+// slab partial stores: fp32, or bf16 (half the slab traffic; summed in fp32 by the slab job)
+__device__ __forceinline__ void st_slab(float* p, float v) { *p = v; }
+__device__ __forceinline__ void st_slab(uint16_t* p, float v) { *p = f2bf(v); }
+
+template <typename TS>
 __device__ __forceinline__ void cl_wgrad_block(const uint16_t* sA, int lda, int mt, const uint16_t* sB, int ldb,
-                                               const float* gam, const float* bet, float* __restrict__ dW,
-                                               float* __restrict__ db) {
+                                               const float* gam, const float* bet, TS* __restrict__ dW,
+                                               TS* __restrict__ db) {
   const int l = lane_id(), g = l >> 4, c = l & 15;
   f32x4 acc[5];
 #pragma unroll
@@ -458,16 +449,17 @@ __device__ __forceinline__ void cl_wgrad_block(const uint16_t* sA, int lda, int 
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = 16 * mt + 4 * g + i;
-      dW[m * 64 + n] = acc[nt][i] * gn + acc[4][i] * bn;
+      st_slab(dW + m * 64 + n, acc[nt][i] * gn + acc[4][i] * bn);
     }
   }
   if (c == 0)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) db[16 * mt + 4 * g + i] = acc[4][i];
+    for (int i = 0; i < 4; ++i) st_slab(db + 16 * mt + 4 * g + i, acc[4][i]);
 }
 // LayerNorm parameter gradients of channel block mt: dγ = diag(dXnᵀ·x̂), dβ = Σ_r dXn
+template <typename TS>
 __device__ __forceinline__ void cl_ln_grads(const uint16_t* sD, const uint16_t* sXh, int ld, int mt,
-                                            float* __restrict__ dg, float* __restrict__ dbt) {
+                                            TS* __restrict__ dg, TS* __restrict__ dbt) {
   const int l = lane_id(), g = l >> 4, c = l & 15;
   f32x4 dia = f32x4{0.f, 0.f, 0.f, 0.f}, sum = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -477,10 +469,10 @@ __device__ __forceinline__ void cl_ln_grads(const uint16_t* sD, const uint16_t* 
     sum = mfma16(a, ones_frag(), sum);
   }
   const int i = c - 4 * g;  // acc row 4g + i is channel column c on the diagonal
-  if (i >= 0 && i < 4) dg[16 * mt + c] = i == 0 ? dia[0] : i == 1 ? dia[1] : i == 2 ? dia[2] : dia[3];
+  if (i >= 0 && i < 4) st_slab(dg + 16 * mt + c, i == 0 ? dia[0] : i == 1 ? dia[1] : i == 2 ? dia[2] : dia[3]);
   if (c == 0)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) dbt[16 * mt + 4 * g + k] = sum[k];
+    for (int k = 0; k < 4; ++k) st_slab(dbt + 16 * mt + 4 * g + k, sum[k]);
 }
 
 template <int NQ>
@@ -490,7 +482,7 @@ constexpr int lpb_chain_smem() {
          2 * (NQ * 64 * 72 > 7 * 64 * 72 ? NQ * 64 * 72 : 7 * 64 * 72) + 4 * 4 * 64;
 }
 
-template <int NQ>
+template <int NQ, typename TS>
 __global__ __launch_bounds__(256) void ln_linear_post_attn_bwd_chain_kernel(
     const float* __restrict__ G, const uint16_t* __restrict__ Wq, const float* __restrict__ X,
     const float* __restrict__ mean1, const float* __restrict__ rstd1, const float* __restrict__ lnw,
@@ -703,18 +695,19 @@ __global__ __launch_bounds__(256) void ln_linear_post_attn_bwd_chain_kernel(
   PIO_TS(10);
 
   // ---- C: parameter gradients of the tile → slab row blockIdx.x ----
-  const int vrs = gr_out.vrs;
+  const int vrs = gr_out.vrs;  // slab row stride in elements of TS
   const long long so = (long long)blockIdx.x * vrs;
   const float *gam1 = sVec, *bet1 = sVec + C, *gam2 = sVec + 2 * C, *bet2 = sVec + 3 * C;
-  cl_wgrad_block(sZm, LD, w, sGu, LD, nullptr, nullptr, gr_out.dW2 + so, gr_out.db2 + so);
-  cl_wgrad_block(sDu, LD, w, sYh, LD, gam2, bet2, gr_out.dW1 + so, gr_out.db1 + so);
-  cl_wgrad_block(sYm, LD, w, sOt, LD, nullptr, nullptr, gr_out.dWo + so, gr_out.dbo + so);
-  cl_ln_grads(sD2, sYh, LD, w, gr_out.dg2 + so, gr_out.dbe2 + so);
+  auto sp = [&](float* p) { return reinterpret_cast<TS*>(p) + so; };  // this tile's slab row
+  cl_wgrad_block(sZm, LD, w, sGu, LD, nullptr, nullptr, sp(gr_out.dW2), sp(gr_out.db2));
+  cl_wgrad_block(sDu, LD, w, sYh, LD, gam2, bet2, sp(gr_out.dW1), sp(gr_out.db1));
+  cl_wgrad_block(sYm, LD, w, sOt, LD, nullptr, nullptr, sp(gr_out.dWo), sp(gr_out.dbo));
+  cl_ln_grads(sD2, sYh, LD, w, sp(gr_out.dg2), sp(gr_out.dbe2));
   PIO_TS(11);
 #pragma unroll
   for (int q = 0; q < NQ; ++q)  // 16-row blocks w, w + 4, w + 8 of dWq (nq rows)
-    cl_wgrad_block(sG, LDG, w + 4 * q, sX1, LD, gam1, bet1, dWq + so, dbq + so);
-  cl_ln_grads(sD1, sX1, LD, w, dlnw + so, dlnb + so);
+    cl_wgrad_block(sG, LDG, w + 4 * q, sX1, LD, gam1, bet1, sp(dWq), sp(dbq));
+  cl_ln_grads(sD1, sX1, LD, w, sp(dlnw), sp(dlnb));
   PIO_TS(12);
 }
 
@@ -748,15 +741,26 @@ bool ln_linear_post_attn_bwd_chain_launch(const float* G, const uint16_t* Wq, co
                                           const uint16_t* Wo, const uint16_t* W1, const uint16_t* W2, const float* g2,
                                           const float* be2, float* dY, uint16_t* dO, float* delta,
                                           const PostAttnGrads& grads, int R, const SlabJob& job, const DropCfg& dr,
-                                          int nq, hipStream_t st) {
+                                          int nq, bool bf16_slab, hipStream_t st) {
   if (nq != 192 && nq != 64) return false;
-  dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0));
-#define LPC(NQ)                                                                                                        \
-  hipLaunchKernelGGL((ln_linear_post_attn_bwd_chain_kernel<NQ>), grid, dim3(256), 0, st, G, Wq, X, mean1, rstd1, lnw, \
-                     lnb, dres, dlnw, dlnb, dWq, dbq, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO, delta,   \
-                     grads, R, job, dr)
-  if (nq == 192) LPC(3);
-  else LPC(1);
+  // the carried slab job in the wide layout: this kernel's LDS leaves one workgroup per CU, so
+  // ≈ 256 fat job blocks run in one round after the tiles instead of ~800 narrow ones in several
+  SlabJob jw = job;
+  if (jw.slab != nullptr) {
+    const int p4 = (jw.P + 3) / 4;
+    jw.wide_c4 = (p4 + 255) / 256 < 1 ? 1 : (p4 + 255) / 256;
+    if (jw.wide_c4 > 256) jw.wide_c4 = 256;
+    jw.nblk = (p4 + jw.wide_c4 - 1) / jw.wide_c4;
+  }
+  dim3 grid((R + 63) / 64 + (jw.slab ? jw.nblk : 0));
+#define LPC(NQ, TS)                                                                                                    \
+  hipLaunchKernelGGL((ln_linear_post_attn_bwd_chain_kernel<NQ, TS>), grid, dim3(256), 0, st, G, Wq, X, mean1, rstd1,  \
+                     lnw, lnb, dres, dlnw, dlnb, dWq, dbq, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO,     \
+                     delta, grads, R, jw, dr)
+  if (nq == 192 && bf16_slab) LPC(3, uint16_t);
+  else if (nq == 192) LPC(3, float);
+  else if (bf16_slab) LPC(1, uint16_t);
+  else LPC(1, float);
 #undef LPC
   return true;
 }

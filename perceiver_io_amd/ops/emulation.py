@@ -590,7 +590,7 @@ def slab_reduce(slab, dsts, offs):
     for d, o in zip(dsts, offs):
         n = d.numel()
         if n:
-            d += slab[:, o:o + n].sum(0).view(d.shape)
+            d += slab[:, o:o + n].float().sum(0).view(d.shape)  # bf16 slabs are summed in fp32
 
 
 def set_deterministic(flag):
