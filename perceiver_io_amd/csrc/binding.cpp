@@ -33,8 +33,6 @@ struct SlabJob {
   const float* slab;
   int S, P, nbx, nblk;
   int det;
-  int wide_c4;
-  int bf16;
   int n;
   float* dst[kMaxSlabSegs];
   int off[kMaxSlabSegs];
@@ -67,12 +65,12 @@ void sa_layer_fwd_launch(const uint16_t*, int, float, uint16_t*, float*, const f
                          const float*, const float*, float, const uint16_t*, const float*, const uint16_t*, const float*,
                          float*, float*, float*, float*, uint16_t*, int, const float*, const float*, const uint16_t*,
                          const float*, uint16_t*, float*, float*, const DropCfg&, int, hipStream_t);
-int ln_linear_post_attn_bwd_launch(int, const float*, const uint16_t*, const float*, const float*, const float*,
+void ln_linear_post_attn_bwd_launch(int, const float*, const uint16_t*, const float*, const float*, const float*,
                                     const float*, const float*, const float*, float*, float*, float*, float*,
                                     const float*, const float*, const float*, const uint16_t*, const uint16_t*,
                                     const uint16_t*, const uint16_t*, const uint16_t*, const float*, const float*,
                                     float*, uint16_t*, float*, int, const PostAttnGrads&, int, const SlabJob&,
-                                    const DropCfg&, int, bool, hipStream_t);
+                                    const DropCfg&, int, hipStream_t);
 void post_attn_bwd_launch(int, const float*, const float*, const float*, const float*, const uint16_t*,
                           const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*, const float*,
                           const float*, float*, uint16_t*, float*, int, const PostAttnGrads&, int, const SlabJob&,
@@ -459,15 +457,6 @@ constexpr int kGradReplicas = 8;
 // i % 8).  A 2-D target counts as replicated only when it is (8, K) with K == its numel / 8.
 // Slab mode (slab_rows > 0): every target is an (slab_rows, K) view of ONE (tiles, P) slab —
 // workgroup i stores its partial into row i (no atomics; ops/fused.py reduces the slab).
-// slab target of the chain backward: fp32 or bf16 (all targets of a call share the dtype)
-float* slab_target(Tensor& t, int64_t K, const char* what, int& vrs, int64_t slab_rows, torch::ScalarType dt) {
-  TORCH_CHECK(t.scalar_type() == dt, "slab targets must share one dtype (", what, ")");
-  TORCH_CHECK(t.dim() == 2 && t.size(0) == slab_rows && t.size(1) == K && t.stride(1) == 1,
-              "slab target ", what, " must be a (tiles, K) view");
-  TORCH_CHECK(vrs < 0 || vrs == (int)t.stride(0), "slab targets must share one row stride");
-  vrs = (int)t.stride(0);
-  return reinterpret_cast<float*>(t.data_ptr());
-}
 float* vec_target(Tensor& t, int64_t K, const char* what, int& vrs, int64_t slab_rows = 0) {
   CHECK_DT(t, torch::kFloat32);
   if (slab_rows > 0) {
@@ -492,8 +481,7 @@ pio::SlabJob make_job(const OptT& slab, std::vector<Tensor>& dsts, const std::ve
   pio::SlabJob j{};
   if (!slab.has_value()) return j;
   const Tensor& t = *slab;
-  TORCH_CHECK(t.scalar_type() == torch::kFloat32 || t.scalar_type() == torch::kBFloat16,
-              "slab must be fp32 or bf16");
+  CHECK_DT(t, torch::kFloat32);
   TORCH_CHECK(t.dim() == 2 && t.is_contiguous() && t.size(1) % 4 == 0, "slab must be (S, P), P % 4 == 0");
   TORCH_CHECK(dsts.size() == offs.size() && dsts.size() <= (size_t)pio::kMaxSlabSegs, "slab job: ≤ 16 segments");
   const int P = (int)t.size(1);
@@ -506,8 +494,7 @@ pio::SlabJob make_job(const OptT& slab, std::vector<Tensor>& dsts, const std::ve
     j.dst[j.n] = d.data_ptr<float>(); j.off[j.n] = (int)offs[q]; j.len[j.n] = (int)d.numel(); ++j.n;
   }
   if (j.n == 0 || t.size(0) == 0) return j;
-  j.slab = reinterpret_cast<const float*>(t.data_ptr());
-  j.bf16 = t.scalar_type() == torch::kBFloat16 ? 1 : 0;
+  j.slab = t.data_ptr<float>();
   j.S = (int)t.size(0);
   j.P = P;
   j.nbx = (P + 255) / 256;
@@ -588,9 +575,7 @@ std::vector<Tensor> ln_linear_post_attn_bwd(Tensor g, Tensor wq, Tensor x, Tenso
   TORCH_CHECK(ll_grads.size() == 4 && pa_grads.size() == 8, "4 + 8 slab targets expected");
   const int64_t sr = (R + 63) / 64, CC = (int64_t)C * C;
   int vrs = -1;
-  const auto dt = ll_grads[0].scalar_type();  // fp32, or bf16 partials (chain kernel)
-  TORCH_CHECK(dt == torch::kFloat32 || dt == torch::kBFloat16, "slab targets must be fp32 or bf16");
-  auto T = [&](Tensor& t, int64_t K, const char* what) { return slab_target(t, K, what, vrs, sr, dt); };
+  auto T = [&](Tensor& t, int64_t K, const char* what) { return vec_target(t, K, what, vrs, sr); };
   float* dg1 = T(ll_grads[0], C, "dlnw");
   float* db1 = T(ll_grads[1], C, "dlnb");
   float* dwq = T(ll_grads[2], (int64_t)nq * C, "dWqkv");
@@ -602,14 +587,11 @@ std::vector<Tensor> ln_linear_post_attn_bwd(Tensor g, Tensor wq, Tensor x, Tenso
   Tensor dy = torch::empty({R, C}, f32);
   Tensor dO = torch::empty({R, C}, y.options().dtype(torch::kBFloat16));
   Tensor delta = torch::empty({R, H}, f32);
-  const int rc = pio::ln_linear_post_attn_bwd_launch(
+  pio::ln_linear_post_attn_bwd_launch(
       C, f32p(g), bfp(wq), f32p(x), f32p(mean1), f32p(rstd1), f32p(lnw), f32p(lnb), f32p(dres), dg1, db1, dwq, dbq,
       f32p(y), f32p(m2), f32p(r2), bfp(u), bfp(o), bfp(wo), bfp(w1), bfp(w2), f32p(g2), f32p(be2),
       dy.data_ptr<float>(), bfp_mut(dO), delta.data_ptr<float>(), (int)H, pg, R,
-      with_zero_span(make_job(job_slab, job_dsts, job_offs), zero_out, y), make_drop(seed, site, p), nq,
-      dt == torch::kBFloat16, stream());
-  TORCH_CHECK(rc == 0, "ln_linear_post_attn_bwd: bf16 slab targets need the chain kernel (C = 64, H = 4, 16-byte "
-              "aligned operands, R % 64 == 0, PIO_CHAIN on)");
+      with_zero_span(make_job(job_slab, job_dsts, job_offs), zero_out, y), make_drop(seed, site, p), nq, stream());
   return {dy, dO, delta};
 }
 

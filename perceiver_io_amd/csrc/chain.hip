@@ -423,14 +423,9 @@ __device__ __forceinline__ bf16x8 ones_frag() {
 // slab partial of one 16-row block (m-tile mt) of a 64-column weight gradient
 //   dW[m][n] = Σ_r A[r][m]·B[r][n]  (A, B bf16 row-major LDS images over the 64 rows)
 // and its bias db[m] = Σ_r A[r][m]; with an LN affine (γ, β over n): dW = γ[n]·dW + β[n]·db[m]
-// slab partial stores: fp32, or bf16 (half the slab traffic; summed in fp32 by the slab job)
-__device__ __forceinline__ void st_slab(float* p, float v) { *p = v; }
-__device__ __forceinline__ void st_slab(uint16_t* p, float v) { *p = f2bf(v); }
-
-template <typename TS>
 __device__ __forceinline__ void cl_wgrad_block(const uint16_t* sA, int lda, int mt, const uint16_t* sB, int ldb,
-                                               const float* gam, const float* bet, TS* __restrict__ dW,
-                                               TS* __restrict__ db) {
+                                               const float* gam, const float* bet, float* __restrict__ dW,
+                                               float* __restrict__ db) {
   const int l = lane_id(), g = l >> 4, c = l & 15;
   f32x4 acc[5];
 #pragma unroll
@@ -449,17 +444,16 @@ __device__ __forceinline__ void cl_wgrad_block(const uint16_t* sA, int lda, int 
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = 16 * mt + 4 * g + i;
-      st_slab(dW + m * 64 + n, acc[nt][i] * gn + acc[4][i] * bn);
+      dW[m * 64 + n] = acc[nt][i] * gn + acc[4][i] * bn;
     }
   }
   if (c == 0)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) st_slab(db + 16 * mt + 4 * g + i, acc[4][i]);
+    for (int i = 0; i < 4; ++i) db[16 * mt + 4 * g + i] = acc[4][i];
 }
 // LayerNorm parameter gradients of channel block mt: dγ = diag(dXnᵀ·x̂), dβ = Σ_r dXn
-template <typename TS>
 __device__ __forceinline__ void cl_ln_grads(const uint16_t* sD, const uint16_t* sXh, int ld, int mt,
-                                            TS* __restrict__ dg, TS* __restrict__ dbt) {
+                                            float* __restrict__ dg, float* __restrict__ dbt) {
   const int l = lane_id(), g = l >> 4, c = l & 15;
   f32x4 dia = f32x4{0.f, 0.f, 0.f, 0.f}, sum = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -469,10 +463,10 @@ __device__ __forceinline__ void cl_ln_grads(const uint16_t* sD, const uint16_t* 
     sum = mfma16(a, ones_frag(), sum);
   }
   const int i = c - 4 * g;  // acc row 4g + i is channel column c on the diagonal
-  if (i >= 0 && i < 4) st_slab(dg + 16 * mt + c, i == 0 ? dia[0] : i == 1 ? dia[1] : i == 2 ? dia[2] : dia[3]);
+  if (i >= 0 && i < 4) dg[16 * mt + c] = i == 0 ? dia[0] : i == 1 ? dia[1] : i == 2 ? dia[2] : dia[3];
   if (c == 0)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) st_slab(dbt + 16 * mt + 4 * g + k, sum[k]);
+    for (int k = 0; k < 4; ++k) dbt[16 * mt + 4 * g + k] = sum[k];
 }
 
 template <int NQ>
@@ -482,7 +476,7 @@ constexpr int lpb_chain_smem() {
          2 * (NQ * 64 * 72 > 7 * 64 * 72 ? NQ * 64 * 72 : 7 * 64 * 72) + 4 * 4 * 64;
 }
 
-template <int NQ, typename TS>
+template <int NQ>
 __global__ __launch_bounds__(256) void ln_linear_post_attn_bwd_chain_kernel(
     const float* __restrict__ G, const uint16_t* __restrict__ Wq, const float* __restrict__ X,
     const float* __restrict__ mean1, const float* __restrict__ rstd1, const float* __restrict__ lnw,
@@ -695,10 +689,10 @@ __global__ __launch_bounds__(256) void ln_linear_post_attn_bwd_chain_kernel(
   PIO_TS(10);
 
   // ---- C: parameter gradients of the tile → slab row blockIdx.x ----
-  const int vrs = gr_out.vrs;  // slab row stride in elements of TS
+  const int vrs = gr_out.vrs;
   const long long so = (long long)blockIdx.x * vrs;
   const float *gam1 = sVec, *bet1 = sVec + C, *gam2 = sVec + 2 * C, *bet2 = sVec + 3 * C;
-  auto sp = [&](float* p) { return reinterpret_cast<TS*>(p) + so; };  // this tile's slab row
+  auto sp = [&](float* p) { return p + so; };  // this tile's slab row
   cl_wgrad_block(sZm, LD, w, sGu, LD, nullptr, nullptr, sp(gr_out.dW2), sp(gr_out.db2));
   cl_wgrad_block(sDu, LD, w, sYh, LD, gam2, bet2, sp(gr_out.dW1), sp(gr_out.db1));
   cl_wgrad_block(sYm, LD, w, sOt, LD, nullptr, nullptr, sp(gr_out.dWo), sp(gr_out.dbo));
@@ -741,26 +735,15 @@ bool ln_linear_post_attn_bwd_chain_launch(const float* G, const uint16_t* Wq, co
                                           const uint16_t* Wo, const uint16_t* W1, const uint16_t* W2, const float* g2,
                                           const float* be2, float* dY, uint16_t* dO, float* delta,
                                           const PostAttnGrads& grads, int R, const SlabJob& job, const DropCfg& dr,
-                                          int nq, bool bf16_slab, hipStream_t st) {
+                                          int nq, hipStream_t st) {
   if (nq != 192 && nq != 64) return false;
-  // the carried slab job in the wide layout: this kernel's LDS leaves one workgroup per CU, so
-  // ≈ 256 fat job blocks run in one round after the tiles instead of ~800 narrow ones in several
-  SlabJob jw = job;
-  if (jw.slab != nullptr) {
-    const int p4 = (jw.P + 3) / 4;
-    jw.wide_c4 = (p4 + 255) / 256 < 1 ? 1 : (p4 + 255) / 256;
-    if (jw.wide_c4 > 256) jw.wide_c4 = 256;
-    jw.nblk = (p4 + jw.wide_c4 - 1) / jw.wide_c4;
-  }
-  dim3 grid((R + 63) / 64 + (jw.slab ? jw.nblk : 0));
-#define LPC(NQ, TS)                                                                                                    \
-  hipLaunchKernelGGL((ln_linear_post_attn_bwd_chain_kernel<NQ, TS>), grid, dim3(256), 0, st, G, Wq, X, mean1, rstd1,  \
-                     lnw, lnb, dres, dlnw, dlnb, dWq, dbq, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO,     \
-                     delta, grads, R, jw, dr)
-  if (nq == 192 && bf16_slab) LPC(3, uint16_t);
-  else if (nq == 192) LPC(3, float);
-  else if (bf16_slab) LPC(1, uint16_t);
-  else LPC(1, float);
+  dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0));
+#define LPC(NQ)                                                                                                        \
+  hipLaunchKernelGGL((ln_linear_post_attn_bwd_chain_kernel<NQ>), grid, dim3(256), 0, st, G, Wq, X, mean1, rstd1, lnw, \
+                     lnb, dres, dlnw, dlnb, dWq, dbq, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO, delta,   \
+                     grads, R, job, dr)
+  if (nq == 192) LPC(3);
+  else LPC(1);
 #undef LPC
   return true;
 }

@@ -280,8 +280,6 @@ struct SlabJob {
   const float* slab;  // nullptr: no job
   int S, P, nbx, nblk;
   int det;            // deterministic mode: one block per column range sums ALL rows, plain add
-  int wide_c4;        // > 0: "wide" blocks of wide_c4 float4 columns over ALL rows (see below)
-  int bf16;           // the slab holds bf16 partials (summed in fp32)
   int n;
   float* dst[kMaxSlabSegs];
   int off[kMaxSlabSegs];
@@ -300,70 +298,8 @@ __device__ __forceinline__ void zero_span_block(const SlabJob& j) {
   for (long long i = z0 + threadIdx.x; i < z1; i += blockDim.x)
     reinterpret_cast<float4*>(j.zero_p)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
-// four consecutive slab values (columns c .. c + 3 of row s) as fp32
-__device__ __forceinline__ float4 slab_ld4(const SlabJob& j, long long s, int c) {
-  if (j.bf16) {
-    const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(j.slab) + s * j.P + c);
-    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xFFFF0000u), __uint_as_float(u.y << 16),
-                       __uint_as_float(u.y & 0xFFFF0000u));
-  }
-  return *reinterpret_cast<const float4*>(j.slab + s * j.P + c);
-}
-
-// Wide layout (carrier kernels whose LDS footprint leaves one workgroup per CU, so appended job
-// workgroups run in rounds after the tiles): ≈ one block per CU, block b owns wide_c4 float4
-// columns and sums ALL S rows — thread t covers column t % wide_c4, rows ≡ t / wide_c4 (mod the
-// row-group count), an LDS combine in a fixed order, then a plain add (single writer per element:
-// no atomics, deterministic).  256 threads.
-template <bool DUMMY = false>
-__device__ __forceinline__ void slab_reduce_block_wide(const SlabJob& j, int b, float4* part) {
-  const int c4 = j.wide_c4, ng = 256 / c4, t = threadIdx.x;
-  const int col4 = t % c4, grp = t / c4;
-  const int c = 4 * (b * c4 + col4), P = j.P;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  const bool act = grp < ng && c < P;
-  // every row of the thread in flight at once (address selects, no conditional loads): one memory
-  // latency per block instead of one per batch of rows
-  constexpr int kMaxRows = 32;
-  for (int s0 = grp; s0 < j.S; s0 += kMaxRows * ng) {
-    float4 v[kMaxRows];
-#pragma unroll
-    for (int i = 0; i < kMaxRows; ++i) {
-      const int s = s0 + i * ng;
-      const bool ok = act && s < j.S;
-      v[i] = slab_ld4(j, ok ? s : 0, ok ? c : 0);
-      if (!ok) v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int i = 0; i < kMaxRows; ++i) {
-      acc.x += v[i].x; acc.y += v[i].y; acc.z += v[i].z; acc.w += v[i].w;
-    }
-  }
-  part[t] = acc;
-  __syncthreads();
-  if (t >= c4 || c >= P) return;
-  float4 sum = part[t];
-  for (int g = 1; g < ng; ++g) {
-    const float4 v = part[g * c4 + t];
-    sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
-  }
-  const float sv[4] = {sum.x, sum.y, sum.z, sum.w};
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int col = c + e;
-    for (int q = 0; q < j.n; ++q) {
-      const int lo = j.off[q];
-      if (col >= lo && col < lo + j.len[q]) j.dst[q][col - lo] += sv[e];
-    }
-  }
-}
-
 // part: ≥ 4 KiB of 16-B aligned LDS
 __device__ __forceinline__ void slab_reduce_block(const SlabJob& j, int b, float4* part) {
-  if (j.wide_c4 > 0) {
-    slab_reduce_block_wide(j, b, part);
-    return;
-  }
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int bx = b % j.nbx, by = b / j.nbx;
   const int cb = bx * 256, c = cb + 4 * l, P = j.P;
@@ -372,7 +308,7 @@ __device__ __forceinline__ void slab_reduce_block(const SlabJob& j, int b, float
   if (j.det) {  // fixed summation order, a single writer per element: bitwise reproducible
     if (c < P)
       for (int s = w; s < j.S; s += 4) {
-        const float4 v = slab_ld4(j, s, c);
+        const float4 v = *reinterpret_cast<const float4*>(j.slab + (long long)s * P + c);
         acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
       }
     part[w * 64 + l] = acc;
@@ -392,7 +328,7 @@ __device__ __forceinline__ void slab_reduce_block(const SlabJob& j, int b, float
 #pragma unroll
     for (int i = 0; i < kSlabRowsPerBlock / 4; ++i) {
       const int s = s0 + w + 4 * i;
-      v[i] = s < s1 ? slab_ld4(j, s, c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[i] = s < s1 ? *reinterpret_cast<const float4*>(j.slab + (long long)s * P + c) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int i = 0; i < kSlabRowsPerBlock / 4; ++i) {

@@ -1455,7 +1455,7 @@ bool ln_linear_post_attn_bwd_chain_launch(const float* G, const uint16_t* Wq, co
                                           const uint16_t* Wo, const uint16_t* W1, const uint16_t* W2, const float* g2,
                                           const float* be2, float* dY, uint16_t* dO, float* delta,
                                           const PostAttnGrads& grads, int R, const SlabJob& job, const DropCfg& dr,
-                                          int nq, bool bf16_slab, hipStream_t st);
+                                          int nq, hipStream_t st);
 static bool use_chain() {
   static const bool on = [] {
     const char* e = getenv("PIO_CHAIN");
@@ -1611,22 +1611,20 @@ void post_attn_bwd_launch(int C, const float* dZ, const float* Ysave, const floa
 #undef PAB
 }
 
-int ln_linear_post_attn_bwd_launch(int C, const float* G, const uint16_t* Wq, const float* X, const float* mean1,
+void ln_linear_post_attn_bwd_launch(int C, const float* G, const uint16_t* Wq, const float* X, const float* mean1,
                                     const float* rstd1, const float* lnw, const float* lnb, const float* dres,
                                     float* dlnw, float* dlnb, float* dWq, float* dbq, const float* Ysave,
                                     const float* mean2, const float* rstd2, const uint16_t* U, const uint16_t* O,
                                     const uint16_t* Wo, const uint16_t* W1, const uint16_t* W2, const float* g2,
                                     const float* be2, float* dY, uint16_t* dO, float* delta, int H,
                                     const PostAttnGrads& grads, int R, const SlabJob& job, const DropCfg& dr,
-                                    int nq, bool bf16_slab, hipStream_t st) {
+                                    int nq, hipStream_t st) {
   dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0));
   const bool av = av_ok({G, Wq, X, lnw, lnb, dres, Ysave, U, O, Wo, W1, W2, dY, dO}, {});
   if (av && C == 64 && H == 4 && grads.slab && (R % 64) == 0 && use_chain() &&
       ln_linear_post_attn_bwd_chain_launch(G, Wq, X, mean1, rstd1, lnw, lnb, dres, dlnw, dlnb, dWq, dbq, Ysave, mean2,
-                                           rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO, delta, grads, R, job, dr, nq,
-                                           bf16_slab, st))
-    return 0;
-  if (bf16_slab) return 1;  // bf16 slab partials: chain kernel only
+                                           rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO, delta, grads, R, job, dr, nq, st))
+    return;
 #define LPB(CC, NQ)                                                                                               \
   if (av) hipLaunchKernelGGL((ln_linear_post_attn_bwd_kernel<CC, true, NQ>), grid, dim3(256), 0, st, G, Wq, X, mean1, \
                              rstd1, lnw, lnb, dres, dlnw, dlnb, dWq, dbq, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, \
@@ -1641,7 +1639,6 @@ int ln_linear_post_attn_bwd_launch(int C, const float* G, const uint16_t* Wq, co
   else if (nq == 3 * C) { LPB(32, 3); }
   else { LPB(32, 1); }
 #undef LPB
-  return 0;
 }
 
 template <typename TG, typename TX, int NCH>

@@ -150,13 +150,13 @@ class _GradSlab:
     replayed hipGraph).  Reductions still pending when the backward pass ends are launched by
     an autograd final callback, so gradients are complete when ``backward()`` returns."""
 
-    def __init__(self, R: int, sizes, like: torch.Tensor, dtype: torch.dtype = torch.float32):
+    def __init__(self, R: int, sizes, like: torch.Tensor):
         self.offs, P = [], 0
         for n in sizes:
             self.offs.append(P)
             P += (n + 3) // 4 * 4
         self.sizes = list(sizes)
-        self.t = torch.empty(((R + 63) // 64, P), dtype=dtype, device=like.device)
+        self.t = torch.empty(((R + 63) // 64, P), dtype=torch.float32, device=like.device)
 
     def targets(self):
         return [self.t[:, o:o + n] for o, n in zip(self.offs, self.sizes)]
@@ -172,22 +172,6 @@ class _GradSlab:
                 ds.append(t.view(-1))
                 os_.append(self.offs[i] + extra)
         defer_slab(K, self.t, ds, os_)
-
-
-# bf16 slab partials for the layer-boundary backward's chain kernel (half the slab write + read
-# traffic — at the headline shape each boundary's slab is 256 tiles × 25 k partials; each
-# partial is a 64-row fp32 MFMA sum rounded once, the rows are summed in fp32).
-# PERCEIVER_SLAB_BF16=0 keeps fp32 partials.
-SLAB_BF16 = os.environ.get("PERCEIVER_SLAB_BF16", "1") != "0"
-
-
-def _lpb_slab_dtype(K, C: int, H: int, R: int) -> torch.dtype:
-    """Slab dtype of an ln_linear_post_attn_bwd call: bf16 where the chain kernel runs it
-    (C = 64, H = 4, R % 64 == 0)."""
-    chain = K is emulation or getattr(K, "chain_enabled", lambda: False)()
-    if SLAB_BF16 and chain and C == 64 and H == 4 and R % 64 == 0:
-        return torch.bfloat16
-    return torch.float32
 
 
 def _grad_of(p: torch.Tensor):
@@ -561,7 +545,7 @@ class _LayerFn(torch.autograd.Function):
         if ho is not None:
             # the following block's first LN1/QKV backward (its dX = this layer's dZ) and this
             # layer's post-attention backward in one launch; both weight-gradient sets in one slab
-            sl = _GradSlab(R, LL_SIZES(C) + PA_SIZES(C), dz2, _lpb_slab_dtype(K, C, H, R))
+            sl = _GradSlab(R, LL_SIZES(C) + PA_SIZES(C), dz2)
             tg = sl.targets()
             dy, do, delta = K.ln_linear_post_attn_bwd(ho["g"], ho["wq"], ho["x"], ho["mean1"], ho["rstd1"], ho["lnw"],
                                                       ho["lnb"], ho["dres"], tg[:4], y, m2, r2, u, o2, wo, w1, w2, g2,
@@ -856,7 +840,7 @@ class _SABlockFn(torch.autograd.Function):
         if ho is not None:
             # the next cross-attention layer's LN + query-projection backward (dX = this block's
             # dZ) fused with the last layer's post-attention backward
-            sl = _GradSlab(R, [C, C, C * C, C] + PA_SIZES(C), dz2, _lpb_slab_dtype(K, C, H, R))
+            sl = _GradSlab(R, [C, C, C * C, C] + PA_SIZES(C), dz2)
             tg = sl.targets()
             dy, do, delta = K.ln_linear_post_attn_bwd(ho["g"], ho["wq"], ho["x"], ho["mean1"], ho["rstd1"], ho["lnw"],
                                                       ho["lnb"], ho["dres"], tg[:4], *pa_args(L - 1), H, tg[4:],
@@ -877,7 +861,7 @@ class _SABlockFn(torch.autograd.Function):
                        dqkv[:, :, 2 * C:], site=i, dq_zeroed=bool(zp & 1), kv_zeroed=bool(zp & 2))
             if i > 0:
                 dqkv_next, zkw = new_dqkv()
-                sl = _GradSlab(R, LL_SIZES(C) + PA_SIZES(C), dz2, _lpb_slab_dtype(K, C, H, R))
+                sl = _GradSlab(R, LL_SIZES(C) + PA_SIZES(C), dz2)
                 tg = sl.targets()
                 dy, do, delta = K.ln_linear_post_attn_bwd(dqkv.view(R, 3 * C), bws[i][0], xl, mean1, rstd1, P[i][0],
                                                           P[i][1], dy, tg[:4], *pa_args(i - 1), H, tg[4:],

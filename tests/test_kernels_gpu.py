@@ -756,9 +756,8 @@ def _slab_sum(sl):
     return [tot[o:o + n] for o, n in zip(sl.offs, sl.sizes)]
 
 
-@pytest.mark.parametrize("nq,p,R,sdt", [(192, 0.0, 512, "f32"), (192, 0.1, 256, "f32"), (64, 0.0, 320, "f32"),
-                                         (192, 0.0, 512, "bf16"), (64, 0.1, 256, "bf16")])
-def test_ln_linear_post_attn_bwd_isolated(nq, p, R, sdt):
+@pytest.mark.parametrize("nq,p,R", [(192, 0.0, 512), (192, 0.1, 256), (64, 0.0, 320)])
+def test_ln_linear_post_attn_bwd_isolated(nq, p, R):
     """The layer-boundary backward (LN1/QKV backward of layer l+1 fused with the post-attention
     backward of layer l; 30 % of the headline step) in isolation against the emulation: every
     output and every slab-reduced parameter gradient within 1 % relative Frobenius error."""
@@ -784,7 +783,7 @@ def test_ln_linear_post_attn_bwd_isolated(nq, p, R, sdt):
     seed = torch.tensor([1234567], dtype=torch.int64, device=DEV) if p > 0 else None
     res = {}
     for name, K in (("hip", _ext()), ("emu", _emu())):
-        sl = _GradSlab(R, [C, C, nq * C, nq] + PA_SIZES(C), x, torch.bfloat16 if sdt == "bf16" else torch.float32)
+        sl = _GradSlab(R, [C, C, nq * C, nq] + PA_SIZES(C), x)
         sl.t.fill_(float("nan") if name == "hip" else 0.0)
         tg = sl.targets()
         outs = K.ln_linear_post_attn_bwd(g, wq, x, mean1, rstd1, lnw, lnb, dres, tg[:4], y, m2, r2, u, o, wo, w1, w2,

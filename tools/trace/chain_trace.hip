@@ -115,7 +115,7 @@ int main(int argc, char** argv) {
   pio::SlabJob job{};
   trace("ln_linear_post_attn_bwd_chain", R, [&]() {
     pio::ln_linear_post_attn_bwd_launch(C, G, W[3], Z, m1, r1, vec[5], vec[6], dres, dg1, db1, dwq, dbq, Y, m2, r2, U, O,
-                                        W[0], W[1], W[2], vec[3], vec[4], dY, dO, delta, H, g, R, job, dr, 3 * C, false, 0);
+                                        W[0], W[1], W[2], vec[3], vec[4], dY, dO, delta, H, g, R, job, dr, 3 * C, 0);
   });
   // the same launch carrying the previous boundary's slab reduction (what the step runs)
   float* slab2;
@@ -129,7 +129,7 @@ int main(int argc, char** argv) {
   job2.n = 1; job2.dst[0] = gdst; job2.off[0] = 0; job2.len[0] = P;
   trace("ln_linear_post_attn_bwd_chain + slab job", R, [&]() {
     pio::ln_linear_post_attn_bwd_launch(C, G, W[3], Z, m1, r1, vec[5], vec[6], dres, dg1, db1, dwq, dbq, Y, m2, r2, U, O,
-                                        W[0], W[1], W[2], vec[3], vec[4], dY, dO, delta, H, g, R, job2, dr, 3 * C, false, 0);
+                                        W[0], W[1], W[2], vec[3], vec[4], dY, dO, delta, H, g, R, job2, dr, 3 * C, 0);
   });
   return 0;
 }
