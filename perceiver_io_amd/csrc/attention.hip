@@ -724,6 +724,13 @@ void attn_fwd_launch(const AttnArgs& a, int D, uint16_t* O, float* LSE, float* O
   }
 }
 
+void attn_combine_launch(const float* Opart, const float* MLpart, uint16_t* O, float* LSE, int nsplit, long long rows,
+                         int D, hipStream_t st) {
+  const long long n = rows * D;
+  hipLaunchKernelGGL(attn_combine_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, Opart, MLpart, O, LSE, nsplit,
+                     (int)rows, D);
+}
+
 static bool getenv_flag(const char* name) {
   static int cached = -1;  // one knob; read once
   if (cached < 0) {

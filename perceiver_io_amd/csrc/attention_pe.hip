@@ -31,33 +31,218 @@
 // (__syncthreads' workgroup fence would drain them).  Each (key block, head) owns its D columns:
 // no atomics on D unless the batch is split over several workgroups (small images).
 #include "common.h"
+#include "pe_args.h"
 
 namespace pio {
 
-struct PeBwdArgs {
-  const uint16_t* q; long long q_bs; int q_rs;  // (1 | B, Nq, ≥ C) bf16; head h = cols [32h, 32h + 32)
-  const uint16_t* kv; int kv_rs;                 // (B·M, ≥ 2C) bf16: K = cols [0, C), V = [C, 2C)
-  const uint16_t* dO;                            // (B, Nq, C) bf16 contiguous
-  const float* lse;                              // (B, Nq, H), log2 units
-  const float* delta;                            // (B, Nq, H) = rowsum(dO∘O)
-  const float* mean; const float* rstd;          // (B·M) LayerNorm row statistics of the K/V input
-  const float* pix;                              // (B·M, nc) pixel channels
-  float* dq;                                     // (Nq, C) Σ over the batch (q_bs = 0) or (B, Nq, C); zeroed
-  float* D;                                      // (M, 2C)
-  float* part;                                   // (gridDim.x · gridDim.z, (2 + nc) · 2C)
-  int B, H, Nq, M, C, nc, bper;
-  float scale, scale_log2;
-  int accumulate;  // add onto D / part (a later application of the weight-shared layer)
-  int d_atomic;    // batch split over several workgroups: D by atomics
-  long long dq_kbs;  // deterministic mode: dq slice per key block (plain stores, summed by the caller)
-};
+// PeBwdArgs: pe_args.h (shared with the host binding)
 
 constexpr int PD = 32;          // head dim
 constexpr int PLD = PD + 8;     // LDS row stride (bf16) of the Q / dO / dS tiles
 constexpr int PMAXC = 4;        // pixel channels
 constexpr int PNSEG = 8;        // weight rows of the column-sum MFMA: 1, μ·rσ, x̂_c (≤ 6 used)
 
-template <int NW, bool QB>
+
+// ---- implicit K/V (SURVEY K-03/K-05: the encoder's K/V are never materialised) -------------
+// K/V row m of sample b, column o (K: o < C, V: C ≤ o < 2C), from the factored projection:
+//     y = rσ·P'[m, o] + Σ_c x̂_c·wpg[c, o] + μrσ·(Σ_c wpg[c, o] − gw[o]) + bw[o]
+// with P' = (E⊙γ_e)·W_eᵀ the batch-independent PE part (bf16, one GEMM per step) and x̂_c =
+// (p_c − μ)·rσ the normalised pixel channels.  Both attention directions generate their K/V
+// tiles with THESE two functions from the same operands, so forward and backward see identical
+// bits.  Per key: PE_NST statistics {rσ, μrσ, x̂_0..x̂_3}; per column: the table rows
+// wt = {wpg_0..wpg_3, Σwpg − gw, bw} (pe_weight_prep_kernel).
+constexpr int PE_NST = 6;
+constexpr int PE_NWT = 6;
+
+__device__ __forceinline__ void pe_key_stats(float pes, float pesq, const float (&px)[PMAXC], int nc, float inv_k,
+                                             float eps, float (&st)[PE_NST]) {
+  float s = pes, sq = pesq;
+#pragma unroll
+  for (int c = 0; c < PMAXC; ++c)
+    if (c < nc) {
+      s += px[c];
+      sq += px[c] * px[c];
+    }
+  const float mu = s * inv_k;
+  const float rs = rsqrtf(fmaxf(sq * inv_k - mu * mu, 0.f) + eps);
+  st[0] = rs;
+  st[1] = mu * rs;
+#pragma unroll
+  for (int c = 0; c < PMAXC; ++c) st[2 + c] = c < nc ? (px[c] - mu) * rs : 0.f;
+}
+
+__device__ __forceinline__ float pe_kv_elem(float p, const float (&st)[PE_NST], const float (&wt)[PE_NWT]) {
+  float y = fmaf(st[1], wt[4], wt[5]);
+#pragma unroll
+  for (int c = 0; c < PMAXC; ++c) y = fmaf(st[2 + c], wt[c], y);
+  return fmaf(st[0], p, y);
+}
+
+// 8 consecutive columns of one key row → bf16x8 (w: the columns' table rows, w[j][e])
+__device__ __forceinline__ bf16x8 pe_kv_row8(const bf16x8& p8, const float (&st)[PE_NST],
+                                             const float (&w)[PE_NWT][8]) {
+  bf16x8 out;
+#pragma unroll
+  for (int e = 0; e < 8; e += 2) {
+    float wa[PE_NWT], wb[PE_NWT];
+#pragma unroll
+    for (int j = 0; j < PE_NWT; ++j) {
+      wa[j] = w[j][e];
+      wb[j] = w[j][e + 1];
+    }
+    const uint32_t pk = pack2(pe_kv_elem(bf2f(p8[e]), st, wa), pe_kv_elem(bf2f(p8[e + 1]), st, wb));
+    out[e] = (short)(pk & 0xFFFF);
+    out[e + 1] = (short)(pk >> 16);
+  }
+  return out;
+}
+
+// ------------------------------------------------------------------------------------
+// Encoder cross-attention forward over implicit K/V (head dim 32, Nq ≤ 32, no mask, no dropout).
+// Every wave is independent: it owns one (batch element, head, key split) and sweeps its keys
+// in 32-key chunks — P' rows of the chunk (bf16, the next chunk's register-prefetched), the
+// chunk's key statistics (lanes < 32, one key each, through a wave-private LDS table), the K/V
+// tile generated into wave-private LDS (lane: 4 keys × 8 columns), then the flash step of
+// attention.hip's forward (Sᵀ = K·Qᵀ with the query on the lane, online softmax in registers,
+// Oᵀ += Vᵀ·Pᵀ).  The 4 waves of a workgroup are 4 batch elements of one (split, head): they
+// read the same P' rows, and the XCD-aware block order keeps one (split, head) on one L2.
+// Unnormalised partials in attention.hip's split-KV format, combined by attn_combine_kernel.
+// ------------------------------------------------------------------------------------
+// PeFwdArgs: pe_args.h
+
+__global__ __launch_bounds__(256) void attn_fwd_pe_kernel(PeFwdArgs a) {
+  constexpr int LDT = PD + 8;  // K / V tile row stride (bf16)
+  __shared__ __attribute__((aligned(16))) uint16_t sK[4][32 * LDT];
+  __shared__ __attribute__((aligned(16))) uint16_t sV[4][32 * LDT];
+  __shared__ __attribute__((aligned(16))) float sSt[4][PE_NST][32];
+  const int w = wave_id(), l = lane_id(), r = l & 31, hh = l >> 5;
+  const Blk3 blk = xcd_block3();  // x: batch quad (fastest), y: split, z: head
+  const int b = 4 * blk.x + w, split = blk.y, h = blk.z;
+  if (b >= a.B) return;  // no workgroup barriers below
+  const int C = a.C;
+  const int kbeg = split * a.chunks * 32;
+  const int kend = min(a.M, kbeg + a.chunks * 32);
+  const int qi = r, qc = min(qi, a.Nq - 1);
+
+  bf16x8 qf[2];
+  {
+    const uint16_t* qp = a.q + (long long)b * a.q_bs + (long long)qc * a.q_rs + h * PD + 8 * hh;
+    qf[0] = *reinterpret_cast<const bf16x8*>(qp);
+    qf[1] = *reinterpret_cast<const bf16x8*>(qp + 16);
+  }
+  // generation mapping: keys gk..gk+3 of the chunk, columns gc..gc+7 of [K | V] (head h)
+  const int gk = 4 * (l & 7), gc = 8 * (l >> 3);
+  const bool isv = gc >= PD;
+  const int pcol = isv ? C + h * PD + gc - PD : h * PD + gc;
+  float wr[PE_NWT][8];
+#pragma unroll
+  for (int j = 0; j < PE_NWT; ++j) {
+    const float4 w0 = *reinterpret_cast<const float4*>(a.wt + (long long)j * 2 * C + pcol);
+    const float4 w1 = *reinterpret_cast<const float4*>(a.wt + (long long)j * 2 * C + pcol + 4);
+    wr[j][0] = w0.x; wr[j][1] = w0.y; wr[j][2] = w0.z; wr[j][3] = w0.w;
+    wr[j][4] = w1.x; wr[j][5] = w1.y; wr[j][6] = w1.z; wr[j][7] = w1.w;
+  }
+  uint16_t* tK = sK[w];
+  uint16_t* tV = sV[w];
+  float(*tS)[32] = sSt[w];
+  uint16_t* trow = (isv ? tV : tK) + (gc & (PD - 1));
+
+  // register staging of one chunk: P' rows (all lanes), statistics inputs (lanes < 32: key r)
+  bf16x8 pv[4];
+  float spx[PMAXC], spe = 0.f, spq = 0.f;
+  const long long pixb = (long long)b * a.M;
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int key = min(k0 + gk + i, a.M - 1);
+      pv[i] = *reinterpret_cast<const bf16x8*>(a.P + (long long)key * 2 * C + pcol);
+    }
+    const int key = min(k0 + r, a.M - 1);
+    spe = a.pes[key];
+    spq = a.pesq[key];
+#pragma unroll
+    for (int c = 0; c < PMAXC; ++c) spx[c] = a.pix[(pixb + key) * a.nc + min(c, a.nc - 1)];
+  };
+  auto wave_lds_sync = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  f32x16 o = f32x16{};
+  float m_run = -1e30f, l_run = 0.f;
+  fetch(kbeg);
+  for (int k0 = kbeg; k0 < kend; k0 += 32) {
+    bf16x8 pc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pc[i] = pv[i];
+    float st[PE_NST];
+    pe_key_stats(spe, spq, spx, a.nc, a.inv_k, a.eps, st);
+    fetch(k0 + 32);  // past the split: clamped rows, never used
+    wave_lds_sync();  // the previous chunk's tile reads are done
+    if (hh == 0) {
+#pragma unroll
+      for (int j = 0; j < PE_NST; ++j) tS[j][r] = st[j];
+    }
+    wave_lds_sync();
+    {
+      float4 s4[PE_NST];
+#pragma unroll
+      for (int j = 0; j < PE_NST; ++j) s4[j] = *reinterpret_cast<const float4*>(&tS[j][gk]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float sk[PE_NST];
+#pragma unroll
+        for (int j = 0; j < PE_NST; ++j) sk[j] = i == 0 ? s4[j].x : i == 1 ? s4[j].y : i == 2 ? s4[j].z : s4[j].w;
+        *reinterpret_cast<bf16x8*>(trow + (gk + i) * LDT) = pe_kv_row8(pc[i], sk, wr);
+      }
+    }
+    wave_lds_sync();
+    f32x16 s = f32x16{};
+    s = mfma32(frag_kc(tK, LDT, 0, 0), qf[0], s);
+    s = mfma32(frag_kc(tK, LDT, 0, 16), qf[1], s);
+    float mt = -INFINITY;
+    if (k0 + 32 <= kend) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) mt = fmaxf(mt, s[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float v = k0 + acc_row(i, hh) < kend ? s[i] : -INFINITY;
+        s[i] = v;
+        mt = fmaxf(mt, v);
+      }
+    }
+    mt = xor32_max(mt);
+    const float m_new = fmaxf(m_run, mt * a.scale_log2);
+    const float alpha = fast_exp2(m_run - m_new);
+    m_run = m_new;
+    float ls = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      s[i] = fast_exp2(fmaf(s[i], a.scale_log2, -m_new));
+      ls += s[i];
+    }
+    l_run = l_run * alpha + ls;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[i] *= alpha;
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) o = mfma32(frag_ks_perm(tV, LDT, 0, 16 * ss), pack_acc(s, ss), o);
+  }
+  const float l_tot = xor32_sum(l_run);
+  if (qi >= a.Nq) return;
+  const long long row = (((long long)split * a.B + b) * a.Nq + qi) * a.H + h;
+  float* op = a.Opart + row * PD;
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+    *reinterpret_cast<float4*>(op + 8 * g + 4 * hh) = make_float4(o[4 * g], o[4 * g + 1], o[4 * g + 2], o[4 * g + 3]);
+  if (hh == 0) {
+    a.MLpart[row * 2] = m_run;
+    a.MLpart[row * 2 + 1] = l_tot;
+  }
+}
+
+template <int NW, bool QB, bool IMPL>
 __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
   constexpr int KB = 32 * NW, NTH = 64 * NW;
   constexpr int KVLD = 2 * PD + 8;  // K|V row stride of the per-wave K/V tile
@@ -69,11 +254,18 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
   __shared__ __attribute__((aligned(16))) float sL[2][32], sDl[2][32];
   __shared__ __attribute__((aligned(16))) float sRs[2][KB];                 // rσ per key
   __shared__ __attribute__((aligned(16))) uint16_t sW[2][PNSEG * WLD];      // [seg][key] bf16 weights
-  __shared__ __attribute__((aligned(16))) uint16_t sKV[2][NW][32 * KVLD];   // per wave: [key][K | V]
+  // per wave: [key][K | V] — double-buffered staging of loaded rows, or (IMPL) one tile generated
+  // at the top of each iteration
+  __shared__ __attribute__((aligned(16))) uint16_t sKV[IMPL ? 1 : 2][NW][32 * KVLD];
   __shared__ __attribute__((aligned(16))) uint16_t sS[NW][32 * PLD];        // per wave: dS slab [key][q]
-  // epilogue aliases over the K/V tiles: dQ partials [w][q][d], column sums [w][2][seg][d]
+  __shared__ __attribute__((aligned(16))) float sX[IMPL ? 2 : 1][IMPL ? PE_NST : 1][KB];  // key statistics
+  __shared__ __attribute__((aligned(16))) float sWt[IMPL ? PE_NWT : 1][64];               // head h's table columns
+  // epilogue aliases over the consumed tiles: dQ partials [w][q][d], column sums [w][2][seg][d]
   float(*sDQ)[32 * 33] = reinterpret_cast<float(*)[32 * 33]>(&sKV[0][0][0]);
-  float(*sCS)[2][PNSEG][32] = reinterpret_cast<float(*)[2][PNSEG][32]>(&sKV[1][0][0]);
+  float(*sCS)[2][PNSEG][32] =
+      reinterpret_cast<float(*)[2][PNSEG][32]>(IMPL ? &sS[0][0] : &sKV[IMPL ? 0 : 1][0][0]);
+  static_assert(sizeof(float) * NW * 32 * 33 <= sizeof(uint16_t) * NW * 32 * KVLD, "dQ partial alias");
+  static_assert(sizeof(float) * NW * 2 * PNSEG * 32 <= sizeof(uint16_t) * NW * 32 * PLD, "column-sum alias");
 
   const int w = wave_id(), l = lane_id(), r = l & 31, hh = l >> 5;
   const int kb = blockIdx.x, h = blockIdx.y, bg = blockIdx.z;
@@ -87,10 +279,11 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
   // clamped addresses (a branch around a load, or arithmetic on a loaded value, makes hipcc wait
   // for every outstanding load at that point); stage() masks, transforms and writes LDS one
   // iteration later.
-  bf16x8 kv8[4];   // this lane's 4 chunks of its wave's 32 K|V rows: rows (l >> 3) + 8j, 8 columns
+  bf16x8 kv8[IMPL ? 1 : 4];  // this lane's 4 chunks of its wave's 32 K|V rows: rows (l >> 3) + 8j, 8 columns
   bf16x8 qd;       // a 16-byte chunk of the Q (threads < 128, QB) / dO (threads 128..255) tile
   float ld = 0.f;  // LSE / delta (threads 256..319)
   float smu = 0.f, srs = 0.f, spx[PMAXC];  // raw statistics + pixels of key kbase + threadIdx.x
+  float spe = 0.f, spq = 0.f;              // IMPL: PE row sums of that key (batch-invariant)
   const int qrow = min((int)(threadIdx.x & 127) >> 2, a.Nq - 1), qcol = (threadIdx.x & 3) * 8;
   const int lrow_i = min((int)(threadIdx.x & 31), a.Nq - 1);
   const int skey = min(kbase + (int)(threadIdx.x % KB), a.M - 1);
@@ -98,10 +291,12 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
   const int kvsrc = kvcol < PD ? h * PD + kvcol : C + h * PD + kvcol - PD;
   auto fetch = [&](int b) {
     const long long rb = (long long)b * a.M;
+    if constexpr (!IMPL) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int row = min(kbase + 32 * w + (l >> 3) + 8 * j, a.M - 1);
-      kv8[j] = *reinterpret_cast<const bf16x8*>(a.kv + (rb + row) * a.kv_rs + kvsrc);
+      for (int j = 0; j < 4; ++j) {
+        const int row = min(kbase + 32 * w + (l >> 3) + 8 * j, a.M - 1);
+        kv8[j] = *reinterpret_cast<const bf16x8*>(a.kv + (rb + row) * a.kv_rs + kvsrc);
+      }
     }
     if (threadIdx.x < 256) {
       if (QB && threadIdx.x < 128)
@@ -109,8 +304,10 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
       else
         qd = *reinterpret_cast<const bf16x8*>(a.dO + ((long long)b * a.Nq + qrow) * C + h * PD + qcol);
       const long long rr = rb + skey;
-      smu = a.mean[rr];
-      srs = a.rstd[rr];
+      if constexpr (!IMPL) {
+        smu = a.mean[rr];
+        srs = a.rstd[rr];
+      }
 #pragma unroll
       for (int c = 0; c < PMAXC; ++c) spx[c] = a.pix[rr * nc + min(c, nc - 1)];
     } else if (threadIdx.x < 320) {
@@ -119,9 +316,11 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
     }
   };
   auto stage = [&](int buf) {
-    uint16_t* t = sKV[buf][w];
+    if constexpr (!IMPL) {
+      uint16_t* t = sKV[buf][w];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) *reinterpret_cast<bf16x8*>(t + ((l >> 3) + 8 * j) * KVLD + kvcol) = kv8[j];
+      for (int j = 0; j < 4; ++j) *reinterpret_cast<bf16x8*>(t + ((l >> 3) + 8 * j) * KVLD + kvcol) = kv8[j];
+    }
     if (threadIdx.x < 256) {
       if (QB || threadIdx.x >= 128) {
         const int c = threadIdx.x & 127;
@@ -131,12 +330,23 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
       }
       const int k = threadIdx.x;
       const bool ok = kbase + k < a.M;
-      sRs[buf][k] = ok ? srs : 0.f;
+      float st[PE_NST];  // rσ, μrσ, x̂_c
+      if constexpr (IMPL) {
+        pe_key_stats(spe, spq, spx, nc, a.inv_k, a.eps, st);
+#pragma unroll
+        for (int j = 0; j < PE_NST; ++j) sX[buf][j][k] = st[j];
+      } else {
+        st[0] = srs;
+        st[1] = smu * srs;
+#pragma unroll
+        for (int c = 0; c < PMAXC; ++c) st[2 + c] = c < nc ? (spx[c] - smu) * srs : 0.f;
+      }
+      sRs[buf][k] = ok ? st[0] : 0.f;
       uint16_t* wcol = sW[buf] + k;
       wcol[0] = f2bf(ok ? 1.f : 0.f);
-      wcol[WLD] = f2bf(ok ? smu * srs : 0.f);
+      wcol[WLD] = f2bf(ok ? st[1] : 0.f);
 #pragma unroll
-      for (int c = 0; c < PMAXC; ++c) wcol[(2 + c) * WLD] = f2bf((ok && c < nc) ? (spx[c] - smu) * srs : 0.f);
+      for (int c = 0; c < PMAXC; ++c) wcol[(2 + c) * WLD] = f2bf((ok && c < nc) ? st[2 + c] : 0.f);
 #pragma unroll
       for (int c = 2 + PMAXC; c < PNSEG; ++c) wcol[c * WLD] = 0;
     } else if (threadIdx.x < 320) {
@@ -164,6 +374,26 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
     if ((c >> 2) >= a.Nq) v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
     *reinterpret_cast<bf16x8*>(sQb[0] + (c >> 2) * PLD + (c & 3) * 8) = v;
   }
+  // IMPL: this lane's P' rows for the tile generation (batch-invariant: loaded once) — keys
+  // 32w + gk + i, columns gc..gc+7 of the wave's [K | V] tile — and the head's table columns
+  const int gk = 4 * (l & 7), gc = 8 * (l >> 3);
+  bf16x8 pc[IMPL ? 4 : 1];
+  if constexpr (IMPL) {
+    const int pcol = gc < PD ? h * PD + gc : C + h * PD + gc - PD;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int key = min(kbase + 32 * w + gk + i, a.M - 1);
+      pc[i] = *reinterpret_cast<const bf16x8*>(a.P + (long long)key * O + pcol);
+    }
+    if (threadIdx.x < 64 * PE_NWT) {
+      const int j = threadIdx.x >> 6, c = threadIdx.x & 63;
+      sWt[j][c] = a.wt[(long long)j * O + (c < PD ? h * PD + c : C + h * PD + c - PD)];
+    }
+    if (threadIdx.x < 256) {
+      spe = a.pes[skey];
+      spq = a.pesq[skey];
+    }
+  }
   if (b0 < b1) {
     fetch(b0);
     stage(b0 & 1);
@@ -173,6 +403,30 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
 
   for (int b = b0; b < b1; ++b) {
     const int cur = b & 1;
+    if constexpr (IMPL) {
+      // (0) element b's K/V tile from its key statistics (staged last iteration) and P'
+      uint16_t* t = sKV[0][w];
+      float wr[PE_NWT][8];
+#pragma unroll
+      for (int j = 0; j < PE_NWT; ++j) {
+        const float4 w0 = *reinterpret_cast<const float4*>(&sWt[j][gc]);
+        const float4 w1 = *reinterpret_cast<const float4*>(&sWt[j][gc + 4]);
+        wr[j][0] = w0.x; wr[j][1] = w0.y; wr[j][2] = w0.z; wr[j][3] = w0.w;
+        wr[j][4] = w1.x; wr[j][5] = w1.y; wr[j][6] = w1.z; wr[j][7] = w1.w;
+      }
+      float4 s4[PE_NST];
+#pragma unroll
+      for (int j = 0; j < PE_NST; ++j) s4[j] = *reinterpret_cast<const float4*>(&sX[cur][j][32 * w + gk]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float sk[PE_NST];
+#pragma unroll
+        for (int j = 0; j < PE_NST; ++j) sk[j] = i == 0 ? s4[j].x : i == 1 ? s4[j].y : i == 2 ? s4[j].z : s4[j].w;
+        *reinterpret_cast<bf16x8*>(t + (gk + i) * KVLD + gc) = pe_kv_row8(pc[i], sk, wr);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+    }
     // (1) element b+1 → LDS (its loads were issued one iteration ago), loads of b+2
     if (b + 1 < b1) {
       stage(cur ^ 1);
@@ -182,7 +436,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
     // B[k = d][col = key] straight from this wave's LDS rows
     const uint16_t* tdO = sdO[cur];
     const uint16_t* sQ = sQb[QB ? cur : 0];
-    const uint16_t* tKV = sKV[cur][w];
+    const uint16_t* tKV = sKV[IMPL ? 0 : cur][w];
     f32x16 S = f32x16{}, dP = f32x16{};
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -343,10 +597,23 @@ void attn_bwd_pe_launch(const PeBwdArgs& a0, int nkb, int bsplit, hipStream_t st
   a.bper = (a.B + bsplit - 1) / bsplit;
   a.d_atomic = bsplit > 1 ? 1 : 0;
   constexpr int NW = 8;
-  if (a.q_bs == 0)
-    hipLaunchKernelGGL((attn_bwd_pe_kernel<NW, false>), dim3(nkb, a.H, bsplit), dim3(64 * NW), 0, st, a);
-  else
-    hipLaunchKernelGGL((attn_bwd_pe_kernel<NW, true>), dim3(nkb, a.H, bsplit), dim3(64 * NW), 0, st, a);
+  const dim3 grid(nkb, a.H, bsplit);
+  if (a.P) {
+    if (a.q_bs == 0) hipLaunchKernelGGL((attn_bwd_pe_kernel<NW, false, true>), grid, dim3(64 * NW), 0, st, a);
+    else hipLaunchKernelGGL((attn_bwd_pe_kernel<NW, true, true>), grid, dim3(64 * NW), 0, st, a);
+  } else {
+    if (a.q_bs == 0) hipLaunchKernelGGL((attn_bwd_pe_kernel<NW, false, false>), grid, dim3(64 * NW), 0, st, a);
+    else hipLaunchKernelGGL((attn_bwd_pe_kernel<NW, true, false>), grid, dim3(64 * NW), 0, st, a);
+  }
+}
+
+// splits × 32-key chunks covering M keys; grid (batch quads, splits, heads), 4 waves each
+void attn_fwd_pe_launch(const PeFwdArgs& a0, hipStream_t st) {
+  PeFwdArgs a = a0;
+  const int nch = (a.M + 31) / 32;
+  a.chunks = (nch + a.nsplit - 1) / a.nsplit;
+  hipLaunchKernelGGL(attn_fwd_pe_kernel, dim3((unsigned)((a.B + 3) / 4), (unsigned)a.nsplit, (unsigned)a.H), dim3(256), 0,
+                     st, a);
 }
 
 }  // namespace pio

@@ -5,6 +5,8 @@
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
 
+#include "pe_args.h"
+
 #include <unordered_map>
 #include <vector>
 
@@ -103,13 +105,13 @@ int stage_step_launch(void* const*, const void* const*, const long long*, int, f
 void sumsq_launch(const float*, long long, float*, hipStream_t);
 void index_add_rows_launch(float*, long long, const int64_t*, const float*, long long, int, hipStream_t);
 void batch_sum2_launch(const float*, const float*, float*, float*, int, long long, hipStream_t);
-void pe_gemm_launch(const uint16_t*, const uint16_t*, float*, int, int, int, hipStream_t);
+void pe_gemm_launch(const uint16_t*, const uint16_t*, void*, bool, int, int, int, hipStream_t);
 struct PeGradTargets { float *dWa, *dWb, *db, *dg, *dbeta; };
 int pe_grad_splits(int);
 void pe_grads_launch(const uint16_t*, const float*, int, int, int, const float*, int, float*, float*, float*,
                      const float*, const float*, const float*, const float*, int, int, int, PeGradTargets, hipStream_t);
 void pe_weight_prep_launch(const float*, const float*, const float*, const float*, int, int, int, int, uint16_t*, float*,
-                           float*, float*, hipStream_t);
+                           float*, float*, float*, hipStream_t);
 int pixel_ce_blocks(long long);
 void pixel_ce_fwd_launch(int, int, const float*, const float*, const float*, const int64_t*, const float*, long long,
                          float*, float*, float*, hipStream_t);
@@ -124,23 +126,8 @@ void slab_reduce_launch(const SlabJob&, hipStream_t);
 void pe_proj_fwd_launch(const float*, int, const float*, const float*, const float*, const float*, const float*,
                         const float*, long long, int, int, int, float, uint16_t*, float*, float*, hipStream_t);
 int pe_proj_bwd_blocks(int);
-struct PeBwdArgs {  // attention_pe.hip
-  const uint16_t* q; long long q_bs; int q_rs;
-  const uint16_t* kv; int kv_rs;
-  const uint16_t* dO;
-  const float* lse;
-  const float* delta;
-  const float* mean; const float* rstd;
-  const float* pix;
-  float* dq;
-  float* D;
-  float* part;
-  int B, H, Nq, M, C, nc, bper;
-  float scale, scale_log2;
-  int accumulate;
-  int d_atomic;
-  long long dq_kbs;
-};
+void attn_fwd_pe_launch(const PeFwdArgs&, hipStream_t);
+void attn_combine_launch(const float*, const float*, uint16_t*, float*, int, long long, int, hipStream_t);
 void attn_bwd_pe_launch(const PeBwdArgs&, int, int, hipStream_t);
 void pe_proj_bwd_launch(const float*, const float*, int, const float*, const float*, int, int, int, float*, float*,
                         hipStream_t);
@@ -1022,8 +1009,9 @@ std::vector<Tensor> pe_proj_fwd(Tensor pix, Tensor P, Tensor pes, Tensor pesq, T
   return {y, mean, rstd};
 }
 
-// C (M, N) fp32 = A (M, K) bf16 · B (N, K) bf16ᵀ — the factored projection's per-step PE GEMM
-Tensor pe_gemm(Tensor A, Tensor B) {
+// C (M, N) fp32 (bf16 if bf16_out) = A (M, K) bf16 · B (N, K) bf16ᵀ — the factored projection's
+// per-step PE GEMM
+Tensor pe_gemm(Tensor A, Tensor B, bool bf16_out) {
   CHECK_CUDA(A); CHECK_DT(A, torch::kBFloat16); CHECK_DT(B, torch::kBFloat16);
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.is_contiguous() && B.is_contiguous() && A.size(1) == B.size(1),
               "pe_gemm: A (M, K), B (N, K) contiguous");
@@ -1031,8 +1019,8 @@ Tensor pe_gemm(Tensor A, Tensor B) {
   TORCH_CHECK(K % 32 == 0 && N % 128 == 0 && K > 0, "pe_gemm: K a multiple of 32, N a multiple of 128");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(B.data_ptr()) % 16 == 0,
               "pe_gemm: 16-byte aligned operands");
-  Tensor C = torch::empty({M, N}, A.options().dtype(torch::kFloat32));
-  if (M > 0) pio::pe_gemm_launch(bfp(A), bfp(B), C.data_ptr<float>(), M, N, K, stream());
+  Tensor C = torch::empty({M, N}, A.options().dtype(bf16_out ? torch::kBFloat16 : torch::kFloat32));
+  if (M > 0) pio::pe_gemm_launch(bfp(A), bfp(B), C.data_ptr(), bf16_out, M, N, K, stream());
   return C;
 }
 
@@ -1082,10 +1070,12 @@ std::vector<Tensor> pe_weight_prep(Tensor W, Tensor g, Tensor b, Tensor bias, in
   auto f32 = W.options();
   Tensor Wg = torch::empty({O, Kp}, f32.dtype(torch::kBFloat16));
   Tensor wpg = torch::empty({nc, O}, f32), gw = torch::empty({O}, f32), bw = torch::empty({O}, f32);
+  Tensor wt = torch::empty({6, O}, f32);  // implicit-K/V generation table (attention_pe.hip)
+  TORCH_CHECK(nc <= 4, "pe_weight_prep: at most 4 pixel channels");
   pio::pe_weight_prep_launch(W.data_ptr<float>(), g.data_ptr<float>(), b.data_ptr<float>(), bias.data_ptr<float>(), O,
                              (int)nc, kin, (int)Kp, bfp_mut(Wg), wpg.data_ptr<float>(), gw.data_ptr<float>(),
-                             bw.data_ptr<float>(), stream());
-  return {Wg, wpg, gw, bw};
+                             bw.data_ptr<float>(), wt.data_ptr<float>(), stream());
+  return {Wg, wpg, gw, bw, wt};
 }
 
 // backward pass over dY (R, O): D (M, O) and per-block partials (nblk, (2 + nc)·O) of
@@ -1112,9 +1102,14 @@ std::vector<Tensor> pe_proj_bwd(Tensor dy, Tensor pix, Tensor mean, Tensor rstd,
 // (attention_pe.hip): queries (1 | B, Nq ≤ 32, ·), head dim 32, no key mask, no dropout.
 // Writes dq (zeroed here) — (Nq, C) summed over the batch for broadcast queries, else (B, Nq, C)
 // — and D (M, 2C), part (nkb·bsplit, (2 + nc)·2C), both added onto when accumulate.
-void attn_bwd_pe(Tensor q, Tensor kv, Tensor dO, Tensor lse, Tensor delta, Tensor mean, Tensor rstd, Tensor pix,
-                 Tensor dq, Tensor D, Tensor part, int64_t H, double scale, bool accumulate, int64_t bsplit) {
-  for (const Tensor* t : {&q, &kv, &dO, &lse, &delta, &mean, &rstd, &pix, &dq, &D, &part}) CHECK_CUDA(*t);
+// implicit K/V (impl != null): kv / mean / rstd are absent and K/V are generated from P' (M, 2C)
+// bf16, the PE row sums pes / pesq (M) and the generation table wt (6, 2C) of pe_weight_prep
+struct PeImplicit { Tensor P, pes, pesq, wt; double kin, eps; };
+
+static void attn_bwd_pe_impl(Tensor q, const Tensor* kv, Tensor dO, Tensor lse, Tensor delta, const Tensor* mean,
+                             const Tensor* rstd, Tensor pix, Tensor dq, Tensor D, Tensor part, int64_t H, double scale,
+                             bool accumulate, int64_t bsplit, const PeImplicit* impl) {
+  for (const Tensor* t : {&q, &dO, &lse, &delta, &pix, &dq, &D, &part}) CHECK_CUDA(*t);
   const int C = (int)(H * 32);
   TORCH_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.size(2) >= C, "q must be (B|1, Nq, >= C) with unit inner stride");
   const int Nq = (int)q.size(1);
@@ -1123,17 +1118,36 @@ void attn_bwd_pe(Tensor q, Tensor kv, Tensor dO, Tensor lse, Tensor delta, Tenso
   const int B = (int)dO.size(0);
   TORCH_CHECK(q.size(0) == 1 || q.size(0) == B, "q batch must be 1 (broadcast) or B");
   const bool qb = q.size(0) == B && B > 1;
-  TORCH_CHECK(kv.dim() == 2 && kv.stride(1) == 1 && kv.size(1) >= 2 * C && kv.size(0) % B == 0,
-              "kv must be (B*M, >= 2C) rows");
-  const int M = (int)(kv.size(0) / B);
-  TORCH_CHECK(kv.stride(0) % 8 == 0 && q.stride(1) % 8 == 0 && (!qb || q.stride(0) % 8 == 0) &&
-                  reinterpret_cast<uintptr_t>(kv.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(q.data_ptr()) % 16 == 0,
-              "attn_bwd_pe: 16-byte aligned rows");
+  int M;
+  if (impl) {
+    const Tensor& P = impl->P;
+    CHECK_CUDA(P); CHECK_DT(P, torch::kBFloat16);
+    TORCH_CHECK(P.dim() == 2 && P.is_contiguous() && P.size(1) == 2 * C && P.size(0) > 0, "P must be (M, 2C) contiguous");
+    M = (int)P.size(0);
+    for (const Tensor* t : {&impl->pes, &impl->pesq, &impl->wt}) {
+      CHECK_CUDA(*t); CHECK_DT(*t, torch::kFloat32);
+      TORCH_CHECK(t->is_contiguous(), "attn_bwd_pe: contiguous PE operands");
+    }
+    TORCH_CHECK(impl->pes.numel() == M && impl->pesq.numel() == M && impl->wt.numel() == 6 * 2 * C,
+                "attn_bwd_pe: pes / pesq (M), wt (6, 2C)");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(P.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(impl->wt.data_ptr()) % 16 == 0,
+                "attn_bwd_pe: 16-byte aligned P / wt");
+  } else {
+    CHECK_CUDA(*kv);
+    TORCH_CHECK(kv->dim() == 2 && kv->stride(1) == 1 && kv->size(1) >= 2 * C && kv->size(0) % B == 0,
+                "kv must be (B*M, >= 2C) rows");
+    M = (int)(kv->size(0) / B);
+    TORCH_CHECK(kv->stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(kv->data_ptr()) % 16 == 0,
+                "attn_bwd_pe: 16-byte aligned kv rows");
+    TORCH_CHECK(mean->numel() == (int64_t)B * M && rstd->numel() == (int64_t)B * M && mean->is_contiguous() &&
+                    rstd->is_contiguous(), "row statistics must be (B*M)");
+    CHECK_DT(*mean, torch::kFloat32); CHECK_DT(*rstd, torch::kFloat32);
+  }
+  TORCH_CHECK(q.stride(1) % 8 == 0 && (!qb || q.stride(0) % 8 == 0) && reinterpret_cast<uintptr_t>(q.data_ptr()) % 16 == 0,
+              "attn_bwd_pe: 16-byte aligned q rows");
   TORCH_CHECK(pix.dim() == 2 && pix.is_contiguous() && pix.size(0) == (int64_t)B * M && pix.size(1) >= 1 && pix.size(1) <= 4,
               "pix must be (B*M, nc <= 4)");
   const int nc = (int)pix.size(1);
-  TORCH_CHECK(mean.numel() == (int64_t)B * M && rstd.numel() == (int64_t)B * M && mean.is_contiguous() && rstd.is_contiguous(),
-              "row statistics must be (B*M)");
   TORCH_CHECK(lse.is_contiguous() && delta.is_contiguous() && lse.numel() == (int64_t)B * Nq * H && delta.numel() == lse.numel(),
               "lse / delta must be (B, Nq, H)");
   TORCH_CHECK(dq.is_contiguous() && dq.numel() == (int64_t)(qb ? B : 1) * Nq * C,
@@ -1143,15 +1157,20 @@ void attn_bwd_pe(Tensor q, Tensor kv, Tensor dO, Tensor lse, Tensor delta, Tenso
   TORCH_CHECK(bsplit >= 1 && bsplit <= B, "bsplit in [1, B]");
   TORCH_CHECK(part.is_contiguous() && part.size(0) == (int64_t)nkb * bsplit && part.size(1) == (int64_t)(2 + nc) * 2 * C,
               "part must be (ceil(M/256)*bsplit, (2+nc)*2C)");
-  for (const Tensor* t : {&lse, &delta, &mean, &rstd, &pix, &dq, &D, &part}) CHECK_DT(*t, torch::kFloat32);
+  for (const Tensor* t : {&lse, &delta, &pix, &dq, &D, &part}) CHECK_DT(*t, torch::kFloat32);
   TORCH_CHECK(!(g_det && bsplit > 1), "deterministic mode: attn_bwd_pe needs bsplit = 1");
   Tensor dq_part;
   if (g_det) dq_part = torch::empty({nkb, dq.numel()}, dq.options());
   else dq.zero_();
   pio::PeBwdArgs a{};
   a.q = bfp(q); a.q_bs = qb ? q.stride(0) : 0; a.q_rs = (int)q.stride(1);
-  a.kv = bfp(kv); a.kv_rs = (int)kv.stride(0);
-  a.dO = bfp(dO); a.lse = f32p(lse); a.delta = f32p(delta); a.mean = f32p(mean); a.rstd = f32p(rstd); a.pix = f32p(pix);
+  if (impl) {
+    a.P = bfp(impl->P); a.pes = f32p(impl->pes); a.pesq = f32p(impl->pesq); a.wt = f32p(impl->wt);
+    a.inv_k = (float)(1.0 / impl->kin); a.eps = (float)impl->eps;
+  } else {
+    a.kv = bfp(*kv); a.kv_rs = (int)kv->stride(0); a.mean = f32p(*mean); a.rstd = f32p(*rstd);
+  }
+  a.dO = bfp(dO); a.lse = f32p(lse); a.delta = f32p(delta); a.pix = f32p(pix);
   a.dq = g_det ? dq_part.data_ptr<float>() : dq.data_ptr<float>();
   a.dq_kbs = g_det ? dq.numel() : 0;
   a.D = D.data_ptr<float>(); a.part = part.data_ptr<float>();
@@ -1161,6 +1180,60 @@ void attn_bwd_pe(Tensor q, Tensor kv, Tensor dO, Tensor lse, Tensor delta, Tenso
   if (bsplit > 1 && !accumulate) D.zero_();  // atomics add onto it
   pio::attn_bwd_pe_launch(a, nkb, (int)bsplit, stream());
   if (g_det) dq.view({-1}).copy_(dq_part.sum(0));
+}
+
+void attn_bwd_pe(Tensor q, Tensor kv, Tensor dO, Tensor lse, Tensor delta, Tensor mean, Tensor rstd, Tensor pix,
+                 Tensor dq, Tensor D, Tensor part, int64_t H, double scale, bool accumulate, int64_t bsplit) {
+  attn_bwd_pe_impl(q, &kv, dO, lse, delta, &mean, &rstd, pix, dq, D, part, H, scale, accumulate, bsplit, nullptr);
+}
+
+// the same over implicit K/V (attention_pe.hip pe_kv_elem): no (B·M, 2C) K/V tensor, no row statistics
+void attn_bwd_pe_implicit(Tensor q, Tensor P, Tensor pes, Tensor pesq, Tensor wt, Tensor dO, Tensor lse, Tensor delta,
+                          Tensor pix, Tensor dq, Tensor D, Tensor part, int64_t H, double scale, int64_t kin, double eps,
+                          bool accumulate, int64_t bsplit) {
+  PeImplicit im{P, pes, pesq, wt, (double)kin, eps};
+  attn_bwd_pe_impl(q, nullptr, dO, lse, delta, nullptr, nullptr, pix, dq, D, part, H, scale, accumulate, bsplit, &im);
+}
+
+// encoder cross-attention forward over implicit K/V (attention_pe.hip attn_fwd_pe_kernel): queries
+// (1 | B, Nq ≤ 32, ≥ C) bf16, head dim 32, no mask, no dropout; P' (M, 2C) bf16, pix (B·M, nc ≤ 4),
+// pes / pesq (M), wt (6, 2C) → O (B, Nq, C) bf16, LSE (B, Nq, H) log2 units.  nsplit key splits.
+std::vector<Tensor> attn_fwd_pe(Tensor q, Tensor P, Tensor pix, Tensor pes, Tensor pesq, Tensor wt, int64_t H,
+                                double scale, int64_t kin, double eps, int64_t nsplit) {
+  for (const Tensor* t : {&q, &P, &pix, &pes, &pesq, &wt}) CHECK_CUDA(*t);
+  CHECK_DT(q, torch::kBFloat16); CHECK_DT(P, torch::kBFloat16);
+  for (const Tensor* t : {&pix, &pes, &pesq, &wt}) {
+    CHECK_DT(*t, torch::kFloat32);
+    TORCH_CHECK(t->is_contiguous(), "attn_fwd_pe: contiguous fp32 operands");
+  }
+  const int C = (int)(H * 32);
+  TORCH_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.size(2) >= C && q.stride(1) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(q.data_ptr()) % 16 == 0, "q must be (B|1, Nq, >= C), 16-byte aligned rows");
+  const int Nq = (int)q.size(1);
+  TORCH_CHECK(Nq >= 1 && Nq <= 32, "attn_fwd_pe: at most 32 queries");
+  TORCH_CHECK(P.dim() == 2 && P.is_contiguous() && P.size(1) == 2 * C && P.size(0) > 0 &&
+                  reinterpret_cast<uintptr_t>(P.data_ptr()) % 16 == 0, "P must be (M, 2C) contiguous");
+  const int M = (int)P.size(0);
+  TORCH_CHECK(pix.dim() == 2 && pix.size(0) % M == 0 && pix.size(1) >= 1 && pix.size(1) <= 4, "pix must be (B*M, nc <= 4)");
+  const int B = (int)(pix.size(0) / M);
+  TORCH_CHECK(q.size(0) == 1 || q.size(0) == B, "q batch must be 1 (broadcast) or B");
+  TORCH_CHECK(q.size(0) == 1 || q.stride(0) % 8 == 0, "q batch stride");
+  TORCH_CHECK(pes.numel() == M && pesq.numel() == M && wt.numel() == 6 * 2 * C &&
+                  reinterpret_cast<uintptr_t>(wt.data_ptr()) % 16 == 0, "attn_fwd_pe: pes / pesq (M), wt (6, 2C)");
+  const int ns = (int)std::max<int64_t>(1, std::min<int64_t>(nsplit, (M + 31) / 32));
+  auto o = torch::empty({B, Nq, C}, q.options());
+  auto lse = torch::empty({B, Nq, H}, pix.options());
+  auto Opart = torch::empty({(int64_t)ns * B * Nq * H * 32}, pix.options());
+  auto MLpart = torch::empty({(int64_t)ns * B * Nq * H * 2}, pix.options());
+  pio::PeFwdArgs a{};
+  a.q = bfp(q); a.q_bs = q.size(0) == 1 ? 0 : q.stride(0); a.q_rs = (int)q.stride(1);
+  a.P = bfp(P); a.pix = f32p(pix); a.pes = f32p(pes); a.pesq = f32p(pesq); a.wt = f32p(wt);
+  a.Opart = Opart.data_ptr<float>(); a.MLpart = MLpart.data_ptr<float>();
+  a.B = B; a.H = (int)H; a.Nq = Nq; a.M = M; a.C = C; a.nc = (int)pix.size(1); a.nsplit = ns;
+  a.scale_log2 = (float)(scale * 1.4426950408889634); a.inv_k = (float)(1.0 / (double)kin); a.eps = (float)eps;
+  pio::attn_fwd_pe_launch(a, stream());
+  pio::attn_combine_launch(a.Opart, a.MLpart, bfp_mut(o), lse.data_ptr<float>(), ns, (long long)B * Nq * H, 32, stream());
+  return {o, lse};
 }
 
 void set_deterministic(bool on) { g_det = on; }
@@ -1246,7 +1319,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fold_replicas", &fold_replicas);
   m.def("slab_reduce", &slab_reduce);
   m.def("pe_proj_fwd", &pe_proj_fwd);
-  m.def("pe_gemm", &pe_gemm);
+  m.def("pe_gemm", &pe_gemm, py::arg("A"), py::arg("B"), py::arg("bf16_out") = false);
+  m.def("attn_fwd_pe", &attn_fwd_pe);
+  m.def("attn_bwd_pe_implicit", &attn_bwd_pe_implicit);
   m.def("pe_weight_prep", &pe_weight_prep);
   m.def("pe_grads", &pe_grads);
   m.def("pe_proj_bwd", &pe_proj_bwd);

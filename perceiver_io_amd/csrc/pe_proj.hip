@@ -187,8 +187,9 @@ __global__ __launch_bounds__(256) void pe_proj_bwd_kernel(
 // ------------------------------------------------------------------------------------
 constexpr int GT = 128, GKC = 32, GLD = GKC + 8;
 
+template <bool BF16OUT>
 __global__ __launch_bounds__(256) void pe_gemm_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bw,
-                                                      float* __restrict__ C, int M, int N, int K) {
+                                                      void* __restrict__ Cv, int M, int N, int K) {
   __shared__ __attribute__((aligned(16))) uint16_t sA[2][GT * GLD];
   __shared__ __attribute__((aligned(16))) uint16_t sB[2][GT * GLD];
   const int w = wave_id(), l = lane_id(), hh = l >> 5;
@@ -249,7 +250,10 @@ __global__ __launch_bounds__(256) void pe_gemm_kernel(const uint16_t* __restrict
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + 64 * wm + 32 * i + acc_row(r, hh);
-        if (m < M) C[(long long)m * N + n] = acc[i][j][r];
+        if (m < M) {
+          if constexpr (BF16OUT) reinterpret_cast<uint16_t*>(Cv)[(long long)m * N + n] = f2bf(acc[i][j][r]);
+          else reinterpret_cast<float*>(Cv)[(long long)m * N + n] = acc[i][j][r];
+        }
       }
     }
 }
@@ -257,11 +261,13 @@ __global__ __launch_bounds__(256) void pe_gemm_kernel(const uint16_t* __restrict
 // one workgroup per output row o of the factored projection (O ≤ 65535 rows, blockDim 256):
 //   Wg[o, k] = W[o, k]·γ[k] for k in [nc, kin), 0 elsewhere (k < Kp), bf16
 //   wpg[c, o] = W[o, c]·γ[c] (c < nc), gw[o] = Σ_k W[o, k]γ[k], bw[o] = Σ_k W[o, k]β[k] + bias[o]
+// and (wt non-null) the implicit-K/V generation table of attention_pe.hip, wt (PE_NWT, O):
+//   rows c < 4: wpg[c, o] (0 for c ≥ nc),  row 4: Σ_c wpg[c, o] − gw[o],  row 5: bw[o]
 __global__ __launch_bounds__(256) void pe_weight_prep_kernel(const float* __restrict__ W, const float* __restrict__ g,
                                                              const float* __restrict__ b, const float* __restrict__ bias,
                                                              int O, int nc, int kin, int Kp, uint16_t* __restrict__ Wg,
                                                              float* __restrict__ wpg, float* __restrict__ gw,
-                                                             float* __restrict__ bw) {
+                                                             float* __restrict__ bw, float* __restrict__ wt) {
   __shared__ float red[2][4];
   const int o = blockIdx.x;
   float sg = 0.f, sb = 0.f;
@@ -281,8 +287,20 @@ __global__ __launch_bounds__(256) void pe_weight_prep_kernel(const float* __rest
   if (lane_id() == 0) { red[0][wave_id()] = sg; red[1][wave_id()] = sb; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    gw[o] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
-    bw[o] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]) + bias[o];
+    const float gsum = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    const float bsum = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]) + bias[o];
+    gw[o] = gsum;
+    bw[o] = bsum;
+    if (wt) {
+      float ps = 0.f;
+      for (int c = 0; c < 4; ++c) {
+        const float v = c < nc ? W[(long long)o * kin + c] * g[c] : 0.f;  // = wpg[c, o]
+        wt[(long long)c * O + o] = v;
+        ps += v;
+      }
+      wt[4LL * O + o] = ps - gsum;
+      wt[5LL * O + o] = bsum;
+    }
   }
 }
 
@@ -479,14 +497,15 @@ void pe_grads_launch(const uint16_t* E, const float* D, int M, int Kp, int O, co
                      nc, t);
 }
 
-void pe_gemm_launch(const uint16_t* A, const uint16_t* Bw, float* C, int M, int N, int K, hipStream_t st) {
-  hipLaunchKernelGGL(pe_gemm_kernel, dim3((unsigned)((M + GT - 1) / GT), (unsigned)(N / GT)), dim3(256), 0, st, A, Bw, C,
-                     M, N, K);
+void pe_gemm_launch(const uint16_t* A, const uint16_t* Bw, void* C, bool bf16_out, int M, int N, int K, hipStream_t st) {
+  const dim3 grid((unsigned)((M + GT - 1) / GT), (unsigned)(N / GT));
+  if (bf16_out) hipLaunchKernelGGL(pe_gemm_kernel<true>, grid, dim3(256), 0, st, A, Bw, C, M, N, K);
+  else hipLaunchKernelGGL(pe_gemm_kernel<false>, grid, dim3(256), 0, st, A, Bw, C, M, N, K);
 }
 void pe_weight_prep_launch(const float* W, const float* g, const float* b, const float* bias, int O, int nc, int kin,
-                           int Kp, uint16_t* Wg, float* wpg, float* gw, float* bw, hipStream_t st) {
+                           int Kp, uint16_t* Wg, float* wpg, float* gw, float* bw, float* wt, hipStream_t st) {
   hipLaunchKernelGGL(pe_weight_prep_kernel, dim3((unsigned)O), dim3(256), 0, st, W, g, b, bias, O, nc, kin, Kp, Wg, wpg,
-                     gw, bw);
+                     gw, bw, wt);
 }
 
 void pe_proj_fwd_launch(const float* pix, int nc, const float* P, const float* pes, const float* pesq,

@@ -107,9 +107,10 @@ def ln_linear_fwd(x, lnw, lnb, eps, w, bias, act, res, out_bf16, save_stats, pe=
     return out
 
 
-def pe_gemm(A, B):
-    """bf16 operands, fp32 accumulation and output (csrc/pe_proj.hip pe_gemm_kernel)."""
-    return A.float() @ B.float().t()
+def pe_gemm(A, B, bf16_out=False):
+    """bf16 operands, fp32 accumulation, fp32 (or bf16) output (csrc/pe_proj.hip pe_gemm_kernel)."""
+    y = A.float() @ B.float().t()
+    return y.to(torch.bfloat16) if bf16_out else y
 
 
 def pe_weight_prep(W, g, b, bias, nc, Kp):
@@ -117,7 +118,12 @@ def pe_weight_prep(W, g, b, bias, nc, Kp):
     wg = W * g[None, :]
     Wg = torch.zeros((O, Kp), device=W.device, dtype=torch.float32)
     Wg[:, nc:kin] = wg[:, nc:]
-    return [Wg.to(torch.bfloat16), wg[:, :nc].t().contiguous(), wg.sum(1), W @ b + bias]
+    wpg, gw, bw = wg[:, :nc].t().contiguous(), wg.sum(1), W @ b + bias
+    wt = torch.zeros((6, O), device=W.device, dtype=torch.float32)  # implicit-K/V generation table
+    wt[:nc] = wpg
+    wt[4] = wpg.sum(0) - gw
+    wt[5] = bw
+    return [Wg.to(torch.bfloat16), wpg, gw, bw, wt]
 
 
 def pe_grads(D, part, E, Wa, Wb, g, b, nc, dWa=None, dWb=None, db=None, dg=None, dbeta=None):
@@ -156,6 +162,33 @@ def pe_proj_bwd(dy, pix, mean, rstd, M):
     xh = (pix - mean[:, None]) * rstd[:, None]
     part = torch.cat([dy.sum(0), (dy * (mean * rstd)[:, None]).sum(0), (xh.t() @ dy).reshape(-1)])
     return [D, part[None]]
+
+
+def pe_kv(P, pix, pes, pesq, wt, kin, eps):
+    """csrc/attention_pe.hip pe_key_stats / pe_kv_elem: the implicit K/V rows (B·M, 2C) bf16 from
+    the bf16 PE product P' (M, 2C), the pixel channels and the generation table, plus μ, rσ."""
+    M = P.shape[0]
+    R, nc = pix.shape
+    m = torch.arange(R, device=pix.device) % M
+    mu = (pes[m] + pix.sum(1)) / kin
+    rs = torch.rsqrt(((pesq[m] + (pix * pix).sum(1)) / kin - mu * mu).clamp(min=0) + eps)
+    xh = (pix - mu[:, None]) * rs[:, None]
+    y = rs[:, None] * P[m].float() + xh @ wt[:nc] + (mu * rs)[:, None] * wt[4] + wt[5]
+    return y.to(torch.bfloat16), mu, rs
+
+
+def attn_fwd_pe(q, P, pix, pes, pesq, wt, H, scale, kin, eps, nsplit):
+    """csrc/attention_pe.hip attn_fwd_pe_kernel: encoder cross-attention over implicit K/V."""
+    C = H * 32
+    B = pix.shape[0] // P.shape[0]
+    kv = pe_kv(P, pix, pes, pesq, wt, kin, eps)[0].view(B, P.shape[0], 2 * C)
+    return attn_fwd(q, kv[:, :, :C], kv[:, :, C:], None, H, 32, scale, 0.0, None, nsplit)
+
+
+def attn_bwd_pe_implicit(q, P, pes, pesq, wt, dO, lse, delta, pix, dq, D, part, H, scale, kin, eps, accumulate, bsplit):
+    """attn_bwd_pe over implicit K/V (the same generation as attn_fwd_pe)."""
+    kv, mu, rs = pe_kv(P, pix, pes, pesq, wt, kin, eps)
+    attn_bwd_pe(q, kv, dO, lse, delta, mu, rs, pix, dq, D, part, H, scale, accumulate, bsplit)
 
 
 def attn_bwd_pe(q, kv, dO, lse, delta, mean, rstd, pix, dq, D, part, H, scale, accumulate, bsplit):

@@ -322,12 +322,38 @@ def _pe_proj_fwd(K, pix, pe, g, b, W, bias):
     O = W.shape[0]
     if O % 128 == 0 and hasattr(K, "pe_gemm"):
         wg, wpg, gw, bw = K.pe_weight_prep(W.contiguous(), g.contiguous(), b.contiguous(), bias.contiguous(), nc,
-                                           ebf.shape[1])
+                                           ebf.shape[1])[:4]
         P = K.pe_gemm(ebf, wg)
     else:
-        wg, wpg, gw, bw = emulation.pe_weight_prep(W, g, b, bias, nc, ebf.shape[1])
+        wg, wpg, gw, bw = emulation.pe_weight_prep(W, g, b, bias, nc, ebf.shape[1])[:4]
         P = torch.mm(ebf, wg.t()).float()
     return K.pe_proj_fwd(pix, P, pes, pesq, wpg, gw, bw, kin, EPS)
+
+
+# implicit K/V for the encoder cross-attention over [pixels ‖ Fourier PE] (csrc/attention_pe.hip):
+# the attention kernels generate each K/V tile from the bf16 PE product P' = Ebf·(W⊙γ)ᵀ, the
+# sample's pixels and a per-column table, so the (B·M, 2C) K/V tensor (0.8 GB at ImageNet shape)
+# is never written or read.  PERCEIVER_PE_IMPLICIT=0 restores the materialised factored path.
+PE_IMPLICIT = os.environ.get("PERCEIVER_PE_IMPLICIT", "1") != "0"
+
+
+def _pe_implicit_operands(K, nc, pe, g, b, W, bias):
+    """(P' (M, 2C) bf16, Σe, Σe², generation table (6, 2C), Kin) of one K/V projection."""
+    kin = g.shape[0]
+    ebf, pes, pesq = _pe_table(pe, nc, kin)
+    if W.shape[0] % 128 == 0 and hasattr(K, "pe_gemm"):
+        wg, _, _, _, wt = K.pe_weight_prep(W.contiguous(), g.contiguous(), b.contiguous(), bias.contiguous(), nc,
+                                           ebf.shape[1])
+        P = K.pe_gemm(ebf, wg, bf16_out=True)
+    else:
+        wg, _, _, _, wt = emulation.pe_weight_prep(W, g, b, bias, nc, ebf.shape[1])
+        P = torch.mm(ebf.float(), wg.float().t()).to(torch.bfloat16)
+    return P, pes, pesq, wt, kin
+
+
+def pe_fwd_splits(B: int, H: int, M: int) -> int:
+    """Key splits of the implicit-K/V forward: ≈ 4096 waves (two per SIMD, two rounds)."""
+    return max(1, min((M + 31) // 32, -(-4096 // (B * H))))
 
 
 def _mm_tn_split(a, b):
@@ -412,7 +438,14 @@ class _LayerFn(torch.autograd.Function):
             if ent is None:  # first application of this layer: project K/V (LN over [pixels ‖ PE] if split)
                 factored = (PE_FACTORED and src is not None and src.pe is not None and not spec.packed
                             and not ctx.needs_input_grad[6] and 1 <= xkv2.shape[1] <= 4 and 2 * C <= 512)
-                if factored:
+                implicit = (factored and PE_IMPLICIT and PE_ATTN_FUSED and D == 32 and Nq <= 32 and kmask is None
+                            and p_attn == 0.0 and hasattr(K, "attn_fwd_pe"))
+                imp = None
+                if implicit:
+                    imp = _pe_implicit_operands(K, xkv2.shape[1], src.pe, g_kv, b_kv, torch.cat([ps[5], ps[6]], 0),
+                                                bin_[C:])
+                    kv = mean_kv = rstd_kv = None
+                elif factored:
                     kv, mean_kv, rstd_kv = _pe_proj_fwd(K, xkv2, src.pe, g_kv, b_kv,
                                                         torch.cat([ps[5], ps[6]], 0), bin_[C:])
                 else:
@@ -429,15 +462,17 @@ class _LayerFn(torch.autograd.Function):
                         kv, mean_kv, rstd_kv = K.ln_linear_fwd(xkv2, g_kv, b_kv, EPS, wkv, bin_[C:], 0, None, True,
                                                                True, src.pe if src is not None else None,
                                                                g_kv.shape[0])
-                ent = {"kv": kv, "mean": mean_kv, "rstd": rstd_kv, "dkv": None, "factored": factored, "wkv": wkv}
+                ent = {"kv": kv, "mean": mean_kv, "rstd": rstd_kv, "dkv": None, "factored": factored, "wkv": wkv,
+                       "implicit": imp}
                 if src is not None:
                     src.entries[key] = ent
             kv, mean_kv, rstd_kv = ent["kv"], ent["mean"], ent["rstd"]
             ctx.kv_entry = ent
             ctx.kv_pe = src.pe if src is not None else None
             q3 = q.view(Bq, Nq, C)
-            kv3 = kv.view(B, M, 2 * C)
-            k3, v3 = kv3[:, :, :C], kv3[:, :, C:]
+            if ent.get("implicit") is None:
+                kv3 = kv.view(B, M, 2 * C)
+                k3, v3 = kv3[:, :, :C], kv3[:, :, C:]
         else:
             B = Bq
             qkv, mean_q, rstd_q = K.ln_linear_fwd(xq2, g_q, b_q, EPS, wq, bin_, 0, None, True, True)
@@ -446,8 +481,13 @@ class _LayerFn(torch.autograd.Function):
             xkv2 = kv = mean_kv = rstd_kv = None
         from .attention import pick_splits
 
-        nsplit = pick_splits(B, H, Nq, k3.shape[1])
-        o, lse = K.attn_fwd(q3, k3, v3, kmask, H, D, scale, p_attn, seed, nsplit)
+        imp = ent.get("implicit") if spec.cross else None
+        if imp is not None:
+            P, pes, pesq, wt, kin = imp
+            o, lse = K.attn_fwd_pe(q3, P, xkv2, pes, pesq, wt, H, scale, kin, EPS, pe_fwd_splits(B, H, M))
+        else:
+            nsplit = pick_splits(B, H, Nq, k3.shape[1])
+            o, lse = K.attn_fwd(q3, k3, v3, kmask, H, D, scale, p_attn, seed, nsplit)
         o2 = o.view(B * Nq, C)
         # a batch-broadcast query stream (Bq = 1) is added as the residual without expanding it;
         # residual dropout (p_attn: the layer's one dropout rate) in the kernel epilogues
@@ -562,9 +602,10 @@ class _LayerFn(torch.autograd.Function):
         delta3 = delta.view(B, Nq, H)
         # --- attention backward + input-side projections (weight grads fused into ln_linear_bwd) ----
         if spec.cross:
-            M = kv.shape[0] // B
-            kv3 = kv.view(B, M, 2 * C)
             ent = ctx.kv_entry
+            imp = ent.get("implicit")
+            M = imp[0].shape[0] if imp is not None else kv.shape[0] // B
+            kv3 = kv.view(B, M, 2 * C) if imp is None else None
             if pe_fused:
                 # dK/dV folded into the factored projection's reductions (D, partials), which every
                 # application of this layer accumulates (attention_pe.hip): no dK/dV tensor
@@ -576,8 +617,13 @@ class _LayerFn(torch.autograd.Function):
                     ent["pe_bsplit"] = bs
                 # broadcast latent queries (layer_1): dq comes back summed over the batch
                 dq = torch.empty((Bq, Nq, C), **f32)
-                K.attn_bwd_pe(qx, kv, do.view(B, Nq, C), lse, delta3, mean_kv, rstd_kv, xkv2, dq, ent["pe_D"],
-                              ent["pe_part"], H, scale, acc, ent["pe_bsplit"])
+                if imp is not None:
+                    P, pes, pesq, wt, kin = imp
+                    K.attn_bwd_pe_implicit(qx, P, pes, pesq, wt, do.view(B, Nq, C), lse, delta3, xkv2, dq, ent["pe_D"],
+                                           ent["pe_part"], H, scale, kin, EPS, acc, ent["pe_bsplit"])
+                else:
+                    K.attn_bwd_pe(qx, kv, do.view(B, Nq, C), lse, delta3, mean_kv, rstd_kv, xkv2, dq, ent["pe_D"],
+                                  ent["pe_part"], H, scale, acc, ent["pe_bsplit"])
             else:
                 # dK/dV of every application of this layer land in one buffer (K-06); the first
                 # writer stores, later ones accumulate

@@ -579,6 +579,64 @@ def test_attention_bwd_pe_fused(B, Bq, Nq, M, H, nc, bsplit):
         close(a, b, 2e-2, n)
 
 
+def _pe_implicit_operands(M, H, nc, kin=133):
+    """Realistic operands of the implicit K/V: a Fourier-like PE table (Σe, Σe² → LayerNorm
+    statistics with the pixels), W ~ N(0, 1/kin) so K/V are O(1), and P' = Ebf·(W⊙γ)ᵀ in bf16."""
+    C = 32 * H
+    E = torch.rand(M, kin - nc, device=DEV) * 2 - 1
+    W = torch.randn(2 * C, kin, device=DEV) / math.sqrt(kin)
+    g, b = 1 + 0.1 * torch.randn(kin, device=DEV), 0.1 * torch.randn(kin, device=DEV)
+    bias = 0.1 * torch.randn(2 * C, device=DEV)
+    Kp = -(-kin // 32) * 32
+    Ebf = torch.zeros(M, Kp, device=DEV)
+    Ebf[:, nc:kin] = E
+    Ebf = bf(Ebf)
+    wg, _, _, _, wt = _emu().pe_weight_prep(W, g, b, bias, nc, Kp)
+    P = _ext().pe_gemm(Ebf, wg, bf16_out=True) if (2 * C) % 128 == 0 else bf(Ebf.float() @ wg.float().t())
+    return P, E.sum(1).contiguous(), (E * E).sum(1).contiguous(), wt, kin
+
+
+@pytest.mark.parametrize("B,Bq,Nq,M,H,nc,bsplit,nsplit", [
+    (3, 1, 32, 600, 4, 3, 1, 7),
+    (4, 1, 17, 300, 4, 1, 2, 3),
+    (2, 1, 32, 50176, 4, 3, 1, 64),
+    (8, 1, 32, 784, 2, 4, 8, 5),
+    (3, 3, 32, 600, 4, 3, 1, 1),
+    (2, 2, 32, 50176, 4, 3, 1, 32),
+    (5, 5, 20, 784, 4, 1, 4, 25),
+])
+def test_attention_pe_implicit_kv(B, Bq, Nq, M, H, nc, bsplit, nsplit):
+    """Encoder cross-attention over implicit K/V (attention_pe.hip attn_fwd_pe_kernel and the IMPL
+    backward: K/V tiles generated from P', pixels and the table, never materialised) vs the
+    emulation (materialised pe_kv → attn_fwd / attn_bwd → pe_proj_bwd): O, LSE, and dq, D and
+    the partials over two accumulating applications (the weight-shared layer_n)."""
+    torch.manual_seed(13)
+    C = 32 * H
+    P, pes, pesq, wt, kin = _pe_implicit_operands(M, H, nc)
+    pix = torch.randn(B * M, nc, device=DEV)
+    q = bf(torch.randn(Bq, Nq, 3 * C, device=DEV))[:, :, :C]
+    dO = bf(torch.randn(B, Nq, C, device=DEV))
+    scale = 1 / math.sqrt(32)
+    eps = 1e-5
+    o1, l1 = _ext().attn_fwd_pe(q, P, pix, pes, pesq, wt, H, scale, kin, eps, nsplit)
+    o2, l2 = _emu().attn_fwd_pe(q, P, pix, pes, pesq, wt, H, scale, kin, eps, 1)
+    close(o1, o2, 1e-2, "O")
+    close(l1, l2, 1e-4, "LSE")
+    delta = (dO.float().view(B, Nq, H, 32) * o2.float().view(B, Nq, H, 32)).sum(-1).contiguous()
+    nkb = (M + 255) // 256
+    res = []
+    for K in (_ext(), _emu()):
+        dq = torch.empty(Bq, Nq, C, device=DEV)
+        D = torch.empty(M, 2 * C, device=DEV)
+        part = torch.empty(nkb * bsplit, (2 + nc) * 2 * C, device=DEV)
+        K.attn_bwd_pe_implicit(q, P, pes, pesq, wt, dO, l2, delta, pix, dq, D, part, H, scale, kin, eps, False, bsplit)
+        dq1 = dq.clone()
+        K.attn_bwd_pe_implicit(q, P, pes, pesq, wt, dO, l2, delta, pix, dq, D, part, H, scale, kin, eps, True, bsplit)
+        res.append((dq1, dq, D, part.sum(0)))
+    for a, b, n in zip(res[0], res[1], ("dq", "dq (2nd)", "D (2 applications)", "partials")):
+        close(a, b, 2e-2, n)
+
+
 def test_index_add_rows_and_sumsq():
     torch.manual_seed(11)
     dst = torch.randn(1000, 64, device=DEV)
@@ -638,13 +696,15 @@ def test_pe_gemm_and_weight_prep(M, N, K):
     c1 = _ext().pe_gemm(A, B)
     c2 = A.float() @ B.float().t()
     close(c1, c2, 1e-4, "pe_gemm")
+    c3 = _ext().pe_gemm(A, B, bf16_out=True)  # the implicit-K/V operand P'
+    assert c3.dtype == torch.bfloat16 and torch.equal(c3, c1.to(torch.bfloat16))
     kin, nc = K - 5, 3
     W = torch.randn(N, kin, device=DEV)
     g, b = torch.randn(kin, device=DEV), torch.randn(kin, device=DEV)
     bias = torch.randn(N, device=DEV)
     r1 = _ext().pe_weight_prep(W, g, b, bias, nc, K)
     r2 = _emu().pe_weight_prep(W, g, b, bias, nc, K)
-    for x, y, n in zip(r1, r2, ("Wg", "wpg", "gw", "bw")):
+    for x, y, n in zip(r1, r2, ("Wg", "wpg", "gw", "bw", "wt")):
         close(x, y, 1e-5, n)
 
 

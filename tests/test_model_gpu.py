@@ -132,16 +132,20 @@ def test_mlm_fused_matches_eager(latents):
     _check_grads(g_hip, g_ref, floor=floor)
 
 
-def test_image_classifier_fused_matches_eager():
+@pytest.mark.parametrize("heads,shape", [(1, (28, 28, 1)), (4, (28, 28, 1)), (4, (64, 64, 3))])
+def test_image_classifier_fused_matches_eager(heads, shape):
+    """heads = 4 (head dim 32): the encoder cross-attention runs over implicit K/V
+    (attention_pe.hip), both directions, the weight-shared layer_n applied twice."""
     from perceiver_io_amd import ops
     from perceiver_io_amd.tasks import LitImageClassifier
 
     torch.manual_seed(1)
-    lit = LitImageClassifier(image_shape=(28, 28, 1), num_classes=10,
+    lit = LitImageClassifier(image_shape=shape, num_classes=10,
                              optimizer_init={"class_path": "torch.optim.AdamW", "init_args": {"lr": 1e-3}},
-                             num_latents=32, num_latent_channels=128, num_encoder_layers=2,
+                             num_latents=32, num_latent_channels=128, num_encoder_layers=2 if heads == 1 else 3,
+                             num_encoder_cross_attention_heads=heads,
                              num_encoder_self_attention_layers_per_block=2, num_decoder_cross_attention_heads=1).cuda()
-    x = torch.randn(4, 28, 28, 1, device="cuda")
+    x = torch.randn(4, *shape, device="cuda")
     y = torch.randint(0, 10, (4,), device="cuda")
 
     def run(xx=x):

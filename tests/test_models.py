@@ -228,9 +228,13 @@ def test_reference_backend_matches_nn_multihead_attention():
 
 
 @pytest.mark.parametrize("slab", [True, False])
-@pytest.mark.parametrize("kind", ["mlm", "image", "image128"])
+@pytest.mark.parametrize("kind", ["mlm", "image", "image128", "image128_materialised"])
 def test_fused_executor_matches_eager_via_emulation(kind, slab, monkeypatch):
+    """image128: head dim 32, the encoder cross-attention over implicit K/V (attention_pe.hip);
+    image128_materialised: the same with the K/V tensor written by pe_proj_fwd."""
     monkeypatch.setattr(ops.fused, "WGRAD_SLAB", slab)
+    monkeypatch.setattr(ops.fused, "PE_IMPLICIT", kind != "image128_materialised")
+    kind = kind.replace("_materialised", "")
     torch.manual_seed(3)
     if kind == "mlm":
         m = mlm_model()
