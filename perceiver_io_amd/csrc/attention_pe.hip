@@ -30,6 +30,10 @@
 // The barrier waits for LDS traffic only (lgkmcnt), never for the global loads in flight
 // (__syncthreads' workgroup fence would drain them).  Each (key block, head) owns its D columns:
 // no atomics on D unless the batch is split over several workgroups (small images).
+#include <stdlib.h>
+
+#include <type_traits>
+
 #include "common.h"
 #include "pe_args.h"
 
@@ -100,26 +104,33 @@ __device__ __forceinline__ bf16x8 pe_kv_row8(const bf16x8& p8, const float (&st)
 // ------------------------------------------------------------------------------------
 // Encoder cross-attention forward over implicit K/V (head dim 32, Nq ≤ 32, no mask, no dropout).
 // Every wave is independent: it owns one (batch element, head, key split) and sweeps its keys
-// in 32-key chunks — P' rows of the chunk (bf16, the next chunk's register-prefetched), the
-// chunk's key statistics (lanes < 32, one key each, through a wave-private LDS table), the K/V
-// tile generated into wave-private LDS (lane: 4 keys × 8 columns), then the flash step of
-// attention.hip's forward (Sᵀ = K·Qᵀ with the query on the lane, online softmax in registers,
-// Oᵀ += Vᵀ·Pᵀ).  The 4 waves of a workgroup are 4 batch elements of one (split, head): they
-// read the same P' rows, and the XCD-aware block order keeps one (split, head) on one L2.
+// in 32-key chunks — P' rows of the chunk (bf16; the next chunk's loads issued as soon as the
+// current rows are consumed), the chunk's key statistics (lanes < 32, one key each, through a
+// wave-private LDS table), the K/V tile generated into wave-private LDS (lane: 4 keys × 8
+// columns, the workgroup's generation table in LDS), then the flash step of attention.hip's
+// forward (Sᵀ = K·Qᵀ with the query on the lane, online softmax in registers, Oᵀ += Vᵀ·Pᵀ).
+// The 4 waves of a workgroup are 4 batch elements of one (split, head): they read the same P'
+// rows, and the XCD-aware block order keeps one (split, head) on one L2.  ≤ 128 VGPRs: four
+// waves per SIMD.  P' carries ≥ 32 zero rows past M (the last prefetch reads them).
 // Unnormalised partials in attention.hip's split-KV format, combined by attn_combine_kernel.
 // ------------------------------------------------------------------------------------
-// PeFwdArgs: pe_args.h
-
-__global__ __launch_bounds__(256) void attn_fwd_pe_kernel(PeFwdArgs a) {
+template <int NC, int OCC>
+__global__ __launch_bounds__(256, OCC) void attn_fwd_pe_kernel(PeFwdArgs a) {
   constexpr int LDT = PD + 8;  // K / V tile row stride (bf16)
   __shared__ __attribute__((aligned(16))) uint16_t sK[4][32 * LDT];
   __shared__ __attribute__((aligned(16))) uint16_t sV[4][32 * LDT];
   __shared__ __attribute__((aligned(16))) float sSt[4][PE_NST][32];
+  __shared__ __attribute__((aligned(16))) float sWt[PE_NWT][64];  // head h's table: K columns | V columns
   const int w = wave_id(), l = lane_id(), r = l & 31, hh = l >> 5;
   const Blk3 blk = xcd_block3();  // x: batch quad (fastest), y: split, z: head
   const int b = 4 * blk.x + w, split = blk.y, h = blk.z;
-  if (b >= a.B) return;  // no workgroup barriers below
   const int C = a.C;
+  for (int t = threadIdx.x; t < 64 * PE_NWT; t += 256) {
+    const int j = t >> 6, c = t & 63;
+    sWt[j][c] = a.wt[(long long)j * 2 * C + (c < PD ? h * PD + c : C + h * PD + c - PD)];
+  }
+  __syncthreads();
+  if (b >= a.B) return;  // no workgroup barriers below
   const int kbeg = split * a.chunks * 32;
   const int kend = min(a.M, kbeg + a.chunks * 32);
   const int qi = r, qc = min(qi, a.Nq - 1);
@@ -132,36 +143,30 @@ __global__ __launch_bounds__(256) void attn_fwd_pe_kernel(PeFwdArgs a) {
   }
   // generation mapping: keys gk..gk+3 of the chunk, columns gc..gc+7 of [K | V] (head h)
   const int gk = 4 * (l & 7), gc = 8 * (l >> 3);
-  const bool isv = gc >= PD;
-  const int pcol = isv ? C + h * PD + gc - PD : h * PD + gc;
-  float wr[PE_NWT][8];
-#pragma unroll
-  for (int j = 0; j < PE_NWT; ++j) {
-    const float4 w0 = *reinterpret_cast<const float4*>(a.wt + (long long)j * 2 * C + pcol);
-    const float4 w1 = *reinterpret_cast<const float4*>(a.wt + (long long)j * 2 * C + pcol + 4);
-    wr[j][0] = w0.x; wr[j][1] = w0.y; wr[j][2] = w0.z; wr[j][3] = w0.w;
-    wr[j][4] = w1.x; wr[j][5] = w1.y; wr[j][6] = w1.z; wr[j][7] = w1.w;
-  }
+  const int pcol = gc < PD ? h * PD + gc : C + h * PD + gc - PD;
   uint16_t* tK = sK[w];
   uint16_t* tV = sV[w];
   float(*tS)[32] = sSt[w];
-  uint16_t* trow = (isv ? tV : tK) + (gc & (PD - 1));
+  uint16_t* trow = (gc < PD ? tK : tV) + (gc & (PD - 1));
 
-  // register staging of one chunk: P' rows (all lanes), statistics inputs (lanes < 32: key r)
+  // chunk staging: P' rows (all lanes; pointer advanced per chunk, padded rows past M), the
+  // statistics inputs of key k0 + r (clamped: the last prefetch may pass M)
+  const long long prs = 2LL * C;
+  const uint16_t* pp = a.P + (long long)(min(kbeg, a.M) + gk) * prs + pcol;  // an empty split reads pad rows
   bf16x8 pv[4];
-  float spx[PMAXC], spe = 0.f, spq = 0.f;
-  const long long pixb = (long long)b * a.M;
-  auto fetch = [&](int k0) {
+  float spx[NC], spe, spq;
+  const float* pixb = a.pix + (long long)b * a.M * NC;
+  auto fetch_p = [&]() {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int key = min(k0 + gk + i, a.M - 1);
-      pv[i] = *reinterpret_cast<const bf16x8*>(a.P + (long long)key * 2 * C + pcol);
-    }
+    for (int i = 0; i < 4; ++i) pv[i] = *reinterpret_cast<const bf16x8*>(pp + i * prs);
+    pp += 32 * prs;
+  };
+  auto fetch_s = [&](int k0) {
     const int key = min(k0 + r, a.M - 1);
     spe = a.pes[key];
     spq = a.pesq[key];
 #pragma unroll
-    for (int c = 0; c < PMAXC; ++c) spx[c] = a.pix[(pixb + key) * a.nc + min(c, a.nc - 1)];
+    for (int c = 0; c < NC; ++c) spx[c] = pixb[(long long)key * NC + c];
   };
   auto wave_lds_sync = [] {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -171,30 +176,47 @@ __global__ __launch_bounds__(256) void attn_fwd_pe_kernel(PeFwdArgs a) {
 
   f32x16 o = f32x16{};
   float m_run = -1e30f, l_run = 0.f;
-  fetch(kbeg);
-  for (int k0 = kbeg; k0 < kend; k0 += 32) {
-    bf16x8 pc[4];
+  auto chunk = [&](int k0, auto masked) {
+    float px[PMAXC];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) pc[i] = pv[i];
+    for (int c = 0; c < PMAXC; ++c) px[c] = c < NC ? spx[c < NC ? c : 0] : 0.f;
     float st[PE_NST];
-    pe_key_stats(spe, spq, spx, a.nc, a.inv_k, a.eps, st);
-    fetch(k0 + 32);  // past the split: clamped rows, never used
+    pe_key_stats(spe, spq, px, NC, a.inv_k, a.eps, st);
+    fetch_s(k0 + 32);
     wave_lds_sync();  // the previous chunk's tile reads are done
     if (hh == 0) {
 #pragma unroll
-      for (int j = 0; j < PE_NST; ++j) tS[j][r] = st[j];
+      for (int j = 0; j < 2 + NC; ++j) tS[j][r] = st[j];
     }
     wave_lds_sync();
     {
-      float4 s4[PE_NST];
+      float4 s4[2 + NC];
 #pragma unroll
-      for (int j = 0; j < PE_NST; ++j) s4[j] = *reinterpret_cast<const float4*>(&tS[j][gk]);
+      for (int j = 0; j < 2 + NC; ++j) s4[j] = *reinterpret_cast<const float4*>(&tS[j][gk]);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float sk[PE_NST];
+      for (int e4 = 0; e4 < 8; e4 += 4) {  // 4 columns at a time: their table entries, 4 keys
+        uint32_t pk[4][2];  // [key][column pair]
+        float4 w4[PE_NWT];
 #pragma unroll
-        for (int j = 0; j < PE_NST; ++j) sk[j] = i == 0 ? s4[j].x : i == 1 ? s4[j].y : i == 2 ? s4[j].z : s4[j].w;
-        *reinterpret_cast<bf16x8*>(trow + (gk + i) * LDT) = pe_kv_row8(pc[i], sk, wr);
+        for (int j = 0; j < PE_NWT; ++j)
+          if (j < NC || j >= 4) w4[j] = *reinterpret_cast<const float4*>(&sWt[j][gc + e4]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float y[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            auto sel = [&](const float4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; };
+            float acc = fmaf(sel(s4[1], i), sel(w4[4], e), sel(w4[5], e));
+#pragma unroll
+            for (int c = 0; c < NC; ++c) acc = fmaf(sel(s4[2 + c], i), sel(w4[c], e), acc);
+            y[e] = fmaf(sel(s4[0], i), bf2f(pv[i][e4 + e]), acc);
+          }
+          pk[i][0] = pack2(y[0], y[1]);
+          pk[i][1] = pack2(y[2], y[3]);
+        }
+        if (e4 == 4) fetch_p();  // this chunk's rows are consumed: the next loads fly during the flash step
+#pragma unroll
+        for (int i = 0; i < 4; ++i) *reinterpret_cast<uint2*>(trow + (gk + i) * LDT + e4) = make_uint2(pk[i][0], pk[i][1]);
       }
     }
     wave_lds_sync();
@@ -202,16 +224,10 @@ __global__ __launch_bounds__(256) void attn_fwd_pe_kernel(PeFwdArgs a) {
     s = mfma32(frag_kc(tK, LDT, 0, 0), qf[0], s);
     s = mfma32(frag_kc(tK, LDT, 0, 16), qf[1], s);
     float mt = -INFINITY;
-    if (k0 + 32 <= kend) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) mt = fmaxf(mt, s[i]);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float v = k0 + acc_row(i, hh) < kend ? s[i] : -INFINITY;
-        s[i] = v;
-        mt = fmaxf(mt, v);
-      }
+    for (int i = 0; i < 16; ++i) {
+      if constexpr (decltype(masked)::value) s[i] = k0 + acc_row(i, hh) < kend ? s[i] : -INFINITY;
+      mt = fmaxf(mt, s[i]);
     }
     mt = xor32_max(mt);
     const float m_new = fmaxf(m_run, mt * a.scale_log2);
@@ -228,7 +244,12 @@ __global__ __launch_bounds__(256) void attn_fwd_pe_kernel(PeFwdArgs a) {
     for (int i = 0; i < 16; ++i) o[i] *= alpha;
 #pragma unroll
     for (int ss = 0; ss < 2; ++ss) o = mfma32(frag_ks_perm(tV, LDT, 0, 16 * ss), pack_acc(s, ss), o);
-  }
+  };
+  fetch_p();
+  fetch_s(kbeg);
+  int k0 = kbeg;
+  for (; k0 + 32 <= kend; k0 += 32) chunk(k0, std::false_type{});
+  if (k0 < kend) chunk(k0, std::true_type{});  // the last chunk of M % 32 ≠ 0
   const float l_tot = xor32_sum(l_run);
   if (qi >= a.Nq) return;
   const long long row = (((long long)split * a.B + b) * a.Nq + qi) * a.H + h;
@@ -268,12 +289,51 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
   static_assert(sizeof(float) * NW * 2 * PNSEG * 32 <= sizeof(uint16_t) * NW * 32 * PLD, "column-sum alias");
 
   const int w = wave_id(), l = lane_id(), r = l & 31, hh = l >> 5;
-  const int kb = blockIdx.x, h = blockIdx.y, bg = blockIdx.z;
+  const int C = a.C, O = 2 * C, nc = a.nc;
+
+  // one run = one (key block, head) over a contiguous batch range [b0, b1).  Grid mode: the run
+  // of this workgroup's (key block, head, batch group).  Persistent mode (a.nbg > 0): workgroup
+  // g owns items [g·T/G, (g+1)·T/G) of the T = pairs × nbg (key block, head, batch group) items,
+  // pair-major, and sweeps them as runs of consecutive items of one pair — the same work per
+  // workgroup to within one item, instead of grid rounds that leave most CUs idle in the last
+  // one.  A pair is shared by at most two workgroups; its first contributor (the run holding
+  // batch group 0) writes D as in grid mode, the other one (a workgroup's leading partial run)
+  // writes its D slice to its side slot (added into D by attn_pe_side_add_kernel) and its column
+  // sums to partial row nkb + g.
+  const int nkb = (a.M + KB - 1) / KB;
+  long long it = 0, it_end = 0;
+  if (a.nbg > 0) {
+    const long long T = (long long)nkb * a.H * a.nbg;
+    it = T * blockIdx.x / gridDim.x;
+    it_end = T * (blockIdx.x + 1) / gridDim.x;
+    if (threadIdx.x == 0) a.side_pair[blockIdx.x] = (it % a.nbg) != 0 ? (int)(it / a.nbg) : -1;
+  }
+  for (bool first_run = true;; first_run = false) {
+  int kb, h, b0, b1, side = -1;
+  long long prow;
+  if (a.nbg > 0) {
+    if (it >= it_end) break;
+    if (!first_run) __syncthreads();  // the previous run's epilogue LDS traffic is done
+    const int pair = (int)(it / a.nbg), bgs = (int)(it % a.nbg);
+    const int bge = (int)min((long long)a.nbg, bgs + (it_end - it));
+    kb = pair / a.H;
+    h = pair % a.H;
+    b0 = bgs * a.bper;
+    b1 = min(a.B, bge * a.bper);
+    if (bgs > 0) side = blockIdx.x;
+    prow = bgs > 0 ? nkb + blockIdx.x : kb;
+    it += bge - bgs;
+  } else {
+    if (!first_run) break;
+    kb = blockIdx.x;
+    h = blockIdx.y;
+    b0 = blockIdx.z * a.bper;
+    b1 = min(a.B, b0 + a.bper);
+    prow = (long long)blockIdx.x * gridDim.z + blockIdx.z;
+  }
   const int kbase = kb * KB;
   const int key = kbase + 32 * w + r;  // this lane's key (S / dP column)
   const bool kval = key < a.M;
-  const int b0 = bg * a.bper, b1 = min(a.B, b0 + a.bper);
-  const int C = a.C, O = 2 * C, nc = a.nc;
 
   // ---- register staging of one batch element.  fetch() only ISSUES loads — unconditional, with
   // clamped addresses (a branch around a load, or arithmetic on a loaded value, makes hipcc wait
@@ -545,7 +605,11 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
       float* dk = a.D + (long long)m * O + h * PD + r;
       float* dv = dk + C;
       const float vk = accD[0][i] * a.scale, vv = accD[1][i];
-      if (a.d_atomic) {
+      if (side >= 0) {  // the slot holds this application's contribution only (added after the kernel)
+        float* sd = a.Dside + ((long long)side * KB + m - kbase) * 64 + r;
+        sd[0] = vk;
+        sd[PD] = vv;
+      } else if (a.d_atomic) {
         atomicAdd(dk, vk);
         atomicAdd(dv, vv);
       } else if (a.accumulate) {
@@ -579,7 +643,6 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
       else atomicAdd(dst, v * a.scale);
     }
   }
-  const long long prow = (long long)blockIdx.x * gridDim.z + blockIdx.z;
   const int nseg = 2 + nc;
   for (int e = threadIdx.x; e < 2 * nseg * 32; e += NTH) {
     const int p = e / (nseg * 32), rem = e % (nseg * 32), seg = rem / 32, j = rem % 32;
@@ -590,14 +653,35 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
     float* dst = a.part + prow * (long long)(nseg * O) + (long long)seg * O + p * C + h * PD + j;
     *dst = a.accumulate ? *dst + v : v;
   }
+  }  // runs
+}
+
+// D[pair rows] += Dside[slot] for every slot holding a leading partial run (persistent mode)
+__global__ __launch_bounds__(256) void attn_pe_side_add_kernel(const float* __restrict__ Dside,
+                                                               const int* __restrict__ side_pair, float* __restrict__ D,
+                                                               int M, int H, int C) {
+  const int pair = side_pair[blockIdx.x];
+  if (pair < 0) return;
+  const int kb = pair / H, h = pair % H;
+  const float* src = Dside + (long long)blockIdx.x * 256 * 64;
+  for (int e = threadIdx.x; e < 256 * 64; e += 256) {
+    const int k = e >> 6, c = e & 63, m = kb * 256 + k;
+    if (m < M) D[(long long)m * 2 * C + (c < PD ? h * PD + c : C + h * PD + c - PD)] += src[e];
+  }
 }
 
 void attn_bwd_pe_launch(const PeBwdArgs& a0, int nkb, int bsplit, hipStream_t st) {
   PeBwdArgs a = a0;
-  a.bper = (a.B + bsplit - 1) / bsplit;
-  a.d_atomic = bsplit > 1 ? 1 : 0;
   constexpr int NW = 8;
-  const dim3 grid(nkb, a.H, bsplit);
+  dim3 grid(nkb, a.H, bsplit);
+  if (a.nbg > 0) {  // persistent: a.nslots workgroups, batch groups of bper
+    a.bper = (a.B + a.nbg - 1) / a.nbg;
+    a.d_atomic = 0;
+    grid = dim3((unsigned)a.nslots, 1, 1);
+  } else {
+    a.bper = (a.B + bsplit - 1) / bsplit;
+    a.d_atomic = bsplit > 1 ? 1 : 0;
+  }
   if (a.P) {
     if (a.q_bs == 0) hipLaunchKernelGGL((attn_bwd_pe_kernel<NW, false, true>), grid, dim3(64 * NW), 0, st, a);
     else hipLaunchKernelGGL((attn_bwd_pe_kernel<NW, true, true>), grid, dim3(64 * NW), 0, st, a);
@@ -605,6 +689,14 @@ void attn_bwd_pe_launch(const PeBwdArgs& a0, int nkb, int bsplit, hipStream_t st
     if (a.q_bs == 0) hipLaunchKernelGGL((attn_bwd_pe_kernel<NW, false, false>), grid, dim3(64 * NW), 0, st, a);
     else hipLaunchKernelGGL((attn_bwd_pe_kernel<NW, true, false>), grid, dim3(64 * NW), 0, st, a);
   }
+  if (a.nbg > 0)
+    hipLaunchKernelGGL(attn_pe_side_add_kernel, dim3((unsigned)a.nslots), dim3(256), 0, st, a.Dside, a.side_pair, a.D, a.M,
+                       a.H, a.C);
+}
+
+int attn_fwd_pe_occupancy() {
+  const char* v = getenv("PIO_PEF_OCC");
+  return (v && v[0] == '3') ? 3 : 4;
 }
 
 // splits × 32-key chunks covering M keys; grid (batch quads, splits, heads), 4 waves each
@@ -612,8 +704,22 @@ void attn_fwd_pe_launch(const PeFwdArgs& a0, hipStream_t st) {
   PeFwdArgs a = a0;
   const int nch = (a.M + 31) / 32;
   a.chunks = (nch + a.nsplit - 1) / a.nsplit;
-  hipLaunchKernelGGL(attn_fwd_pe_kernel, dim3((unsigned)((a.B + 3) / 4), (unsigned)a.nsplit, (unsigned)a.H), dim3(256), 0,
-                     st, a);
+  const dim3 grid((unsigned)((a.B + 3) / 4), (unsigned)a.nsplit, (unsigned)a.H);
+  // occupancy variant: 4 waves / SIMD (≤ 128 VGPRs) unless PIO_PEF_OCC=3
+  static const int occ = [] {
+    const char* v = getenv("PIO_PEF_OCC");
+    return (v && v[0] == '3') ? 3 : 4;
+  }();
+#define PIO_PEF(NC_)                                                                                   \
+  if (occ == 3) hipLaunchKernelGGL((attn_fwd_pe_kernel<NC_, 3>), grid, dim3(256), 0, st, a);           \
+  else hipLaunchKernelGGL((attn_fwd_pe_kernel<NC_, 4>), grid, dim3(256), 0, st, a);
+  switch (a.nc) {
+    case 1: PIO_PEF(1) break;
+    case 2: PIO_PEF(2) break;
+    case 3: PIO_PEF(3) break;
+    default: PIO_PEF(4) break;
+  }
+#undef PIO_PEF
 }
 
 }  // namespace pio

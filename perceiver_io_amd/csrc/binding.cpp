@@ -127,6 +127,7 @@ void pe_proj_fwd_launch(const float*, int, const float*, const float*, const flo
                         const float*, long long, int, int, int, float, uint16_t*, float*, float*, hipStream_t);
 int pe_proj_bwd_blocks(int);
 void attn_fwd_pe_launch(const PeFwdArgs&, hipStream_t);
+int attn_fwd_pe_occupancy();
 void attn_combine_launch(const float*, const float*, uint16_t*, float*, int, long long, int, hipStream_t);
 void attn_bwd_pe_launch(const PeBwdArgs&, int, int, hipStream_t);
 void pe_proj_bwd_launch(const float*, const float*, int, const float*, const float*, int, int, int, float*, float*,
@@ -1011,7 +1012,7 @@ std::vector<Tensor> pe_proj_fwd(Tensor pix, Tensor P, Tensor pes, Tensor pesq, T
 
 // C (M, N) fp32 (bf16 if bf16_out) = A (M, K) bf16 · B (N, K) bf16ᵀ — the factored projection's
 // per-step PE GEMM
-Tensor pe_gemm(Tensor A, Tensor B, bool bf16_out) {
+Tensor pe_gemm(Tensor A, Tensor B, bool bf16_out, int64_t pad_rows) {
   CHECK_CUDA(A); CHECK_DT(A, torch::kBFloat16); CHECK_DT(B, torch::kBFloat16);
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.is_contiguous() && B.is_contiguous() && A.size(1) == B.size(1),
               "pe_gemm: A (M, K), B (N, K) contiguous");
@@ -1019,7 +1020,9 @@ Tensor pe_gemm(Tensor A, Tensor B, bool bf16_out) {
   TORCH_CHECK(K % 32 == 0 && N % 128 == 0 && K > 0, "pe_gemm: K a multiple of 32, N a multiple of 128");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(B.data_ptr()) % 16 == 0,
               "pe_gemm: 16-byte aligned operands");
-  Tensor C = torch::empty({M, N}, A.options().dtype(bf16_out ? torch::kBFloat16 : torch::kFloat32));
+  TORCH_CHECK(pad_rows >= 0, "pe_gemm: pad_rows >= 0");
+  Tensor C = torch::empty({M + pad_rows, N}, A.options().dtype(bf16_out ? torch::kBFloat16 : torch::kFloat32));
+  if (pad_rows > 0) C.narrow(0, M, pad_rows).zero_();  // zero rows past M (read by prefetches, never used)
   if (M > 0) pio::pe_gemm_launch(bfp(A), bfp(B), C.data_ptr(), bf16_out, M, N, K, stream());
   return C;
 }
@@ -1106,6 +1109,29 @@ std::vector<Tensor> pe_proj_bwd(Tensor dy, Tensor pix, Tensor mean, Tensor rstd,
 // bf16, the PE row sums pes / pesq (M) and the generation table wt (6, 2C) of pe_weight_prep
 struct PeImplicit { Tensor P, pes, pesq, wt; double kin, eps; };
 
+// persistent mode of the PE attention backward (attention_pe.hip): one workgroup per CU over
+// (key block, head, batch group) items when there are at least as many pairs as CUs
+static int pe_bwd_slots(int M, int H, int64_t bsplit) {
+  static const bool off = [] {
+    const char* v = getenv("PIO_PE_PERSIST");
+    return v && v[0] == '0';
+  }();
+  if (off || g_det || bsplit != 1) return 0;
+  int dev = 0, ncu = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  const int nkb = (M + 255) / 256;
+  return (int64_t)nkb * H >= ncu ? ncu : 0;
+}
+
+// rows of the `part` buffer the PE attention backward writes for this shape
+int64_t attn_bwd_pe_part_rows(int64_t M, int64_t H, int64_t B, int64_t bsplit) {
+  const int64_t nkb = (M + 255) / 256;
+  const int slots = pe_bwd_slots((int)M, (int)H, bsplit);
+  (void)B;
+  return slots > 0 ? nkb + slots : nkb * bsplit;
+}
+
 static void attn_bwd_pe_impl(Tensor q, const Tensor* kv, Tensor dO, Tensor lse, Tensor delta, const Tensor* mean,
                              const Tensor* rstd, Tensor pix, Tensor dq, Tensor D, Tensor part, int64_t H, double scale,
                              bool accumulate, int64_t bsplit, const PeImplicit* impl) {
@@ -1122,8 +1148,9 @@ static void attn_bwd_pe_impl(Tensor q, const Tensor* kv, Tensor dO, Tensor lse, 
   if (impl) {
     const Tensor& P = impl->P;
     CHECK_CUDA(P); CHECK_DT(P, torch::kBFloat16);
-    TORCH_CHECK(P.dim() == 2 && P.is_contiguous() && P.size(1) == 2 * C && P.size(0) > 0, "P must be (M, 2C) contiguous");
-    M = (int)P.size(0);
+    M = (int)impl->pes.numel();
+    TORCH_CHECK(P.dim() == 2 && P.is_contiguous() && P.size(1) == 2 * C && P.size(0) >= M && M > 0,
+                "P must be (>= M, 2C) contiguous, M = pes.numel()");
     for (const Tensor* t : {&impl->pes, &impl->pesq, &impl->wt}) {
       CHECK_CUDA(*t); CHECK_DT(*t, torch::kFloat32);
       TORCH_CHECK(t->is_contiguous(), "attn_bwd_pe: contiguous PE operands");
@@ -1155,8 +1182,10 @@ static void attn_bwd_pe_impl(Tensor q, const Tensor* kv, Tensor dO, Tensor lse, 
   TORCH_CHECK(D.is_contiguous() && D.size(0) == M && D.size(1) == 2 * C, "D must be (M, 2C) contiguous");
   const int nkb = (M + 255) / 256;
   TORCH_CHECK(bsplit >= 1 && bsplit <= B, "bsplit in [1, B]");
-  TORCH_CHECK(part.is_contiguous() && part.size(0) == (int64_t)nkb * bsplit && part.size(1) == (int64_t)(2 + nc) * 2 * C,
-              "part must be (ceil(M/256)*bsplit, (2+nc)*2C)");
+  const int slots = pe_bwd_slots(M, (int)H, bsplit);
+  const int64_t prows = slots > 0 ? nkb + slots : (int64_t)nkb * bsplit;
+  TORCH_CHECK(part.is_contiguous() && part.size(0) == prows && part.size(1) == (int64_t)(2 + nc) * 2 * C,
+              "part must be (attn_bwd_pe_part_rows(M, H, B, bsplit), (2+nc)*2C)");
   for (const Tensor* t : {&lse, &delta, &pix, &dq, &D, &part}) CHECK_DT(*t, torch::kFloat32);
   TORCH_CHECK(!(g_det && bsplit > 1), "deterministic mode: attn_bwd_pe needs bsplit = 1");
   Tensor dq_part;
@@ -1178,6 +1207,13 @@ static void attn_bwd_pe_impl(Tensor q, const Tensor* kv, Tensor dO, Tensor lse, 
   a.scale = (float)scale; a.scale_log2 = (float)(scale * 1.4426950408889634);
   a.accumulate = accumulate ? 1 : 0;
   if (bsplit > 1 && !accumulate) D.zero_();  // atomics add onto it
+  Tensor dside, spair;
+  if (slots > 0) {
+    dside = torch::empty({slots, 256, 64}, D.options());
+    spair = torch::empty({slots}, D.options().dtype(torch::kInt32));
+    a.nbg = 4; a.nslots = slots; a.Dside = dside.data_ptr<float>(); a.side_pair = spair.data_ptr<int>();
+    if (!accumulate) part.narrow(0, nkb, slots).zero_();  // a slot row only gets its head's columns
+  }
   pio::attn_bwd_pe_launch(a, nkb, (int)bsplit, stream());
   if (g_det) dq.view({-1}).copy_(dq_part.sum(0));
 }
@@ -1211,15 +1247,22 @@ std::vector<Tensor> attn_fwd_pe(Tensor q, Tensor P, Tensor pix, Tensor pes, Tens
                   reinterpret_cast<uintptr_t>(q.data_ptr()) % 16 == 0, "q must be (B|1, Nq, >= C), 16-byte aligned rows");
   const int Nq = (int)q.size(1);
   TORCH_CHECK(Nq >= 1 && Nq <= 32, "attn_fwd_pe: at most 32 queries");
-  TORCH_CHECK(P.dim() == 2 && P.is_contiguous() && P.size(1) == 2 * C && P.size(0) > 0 &&
-                  reinterpret_cast<uintptr_t>(P.data_ptr()) % 16 == 0, "P must be (M, 2C) contiguous");
-  const int M = (int)P.size(0);
+  const int M = (int)pes.numel();
+  TORCH_CHECK(M > 0 && P.dim() == 2 && P.is_contiguous() && P.size(1) == 2 * C && P.size(0) >= M + 64 &&
+                  reinterpret_cast<uintptr_t>(P.data_ptr()) % 16 == 0,
+              "P must be (M + >= 64 zero pad rows, 2C) contiguous (pe_gemm pad_rows), M = pes.numel()");
   TORCH_CHECK(pix.dim() == 2 && pix.size(0) % M == 0 && pix.size(1) >= 1 && pix.size(1) <= 4, "pix must be (B*M, nc <= 4)");
   const int B = (int)(pix.size(0) / M);
   TORCH_CHECK(q.size(0) == 1 || q.size(0) == B, "q batch must be 1 (broadcast) or B");
   TORCH_CHECK(q.size(0) == 1 || q.stride(0) % 8 == 0, "q batch stride");
-  TORCH_CHECK(pes.numel() == M && pesq.numel() == M && wt.numel() == 6 * 2 * C &&
+  TORCH_CHECK(pesq.numel() == M && wt.numel() == 6 * 2 * C &&
                   reinterpret_cast<uintptr_t>(wt.data_ptr()) % 16 == 0, "attn_fwd_pe: pes / pesq (M), wt (6, 2C)");
+  if (nsplit <= 0) {  // one round of waves at the kernel's occupancy on this device
+    int dev = 0, ncu = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    nsplit = std::max<int64_t>(1, (int64_t)pio::attn_fwd_pe_occupancy() * 4 * ncu / (4 * ((B + 3) / 4) * H));
+  }
   const int ns = (int)std::max<int64_t>(1, std::min<int64_t>(nsplit, (M + 31) / 32));
   auto o = torch::empty({B, Nq, C}, q.options());
   auto lse = torch::empty({B, Nq, H}, pix.options());
@@ -1319,8 +1362,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fold_replicas", &fold_replicas);
   m.def("slab_reduce", &slab_reduce);
   m.def("pe_proj_fwd", &pe_proj_fwd);
-  m.def("pe_gemm", &pe_gemm, py::arg("A"), py::arg("B"), py::arg("bf16_out") = false);
+  m.def("pe_gemm", &pe_gemm, py::arg("A"), py::arg("B"), py::arg("bf16_out") = false, py::arg("pad_rows") = 0);
   m.def("attn_fwd_pe", &attn_fwd_pe);
+  m.def("attn_bwd_pe_part_rows", &attn_bwd_pe_part_rows);
   m.def("attn_bwd_pe_implicit", &attn_bwd_pe_implicit);
   m.def("pe_weight_prep", &pe_weight_prep);
   m.def("pe_grads", &pe_grads);

@@ -25,6 +25,13 @@ struct PeBwdArgs {
   int accumulate;  // add onto D / part (a later application of the weight-shared layer)
   int d_atomic;    // batch split over several workgroups: D by atomics
   long long dq_kbs;  // deterministic mode: dq slice per key block (plain stores, summed by the caller)
+  // persistent mode (nbg > 0): nslots workgroups over (key block, head, batch group) items, nbg
+  // batch groups per pair; leading partial runs write D to Dside (nslots, 256, 64) and record
+  // their pair in side_pair (nslots); part has nkb + nslots rows (the extra rows zeroed when
+  // not accumulating)
+  int nbg, nslots;
+  float* Dside;
+  int* side_pair;
 };
 
 struct PeFwdArgs {

@@ -107,9 +107,12 @@ def ln_linear_fwd(x, lnw, lnb, eps, w, bias, act, res, out_bf16, save_stats, pe=
     return out
 
 
-def pe_gemm(A, B, bf16_out=False):
-    """bf16 operands, fp32 accumulation, fp32 (or bf16) output (csrc/pe_proj.hip pe_gemm_kernel)."""
+def pe_gemm(A, B, bf16_out=False, pad_rows=0):
+    """bf16 operands, fp32 accumulation, fp32 (or bf16) output (csrc/pe_proj.hip pe_gemm_kernel),
+    pad_rows zero rows appended."""
     y = A.float() @ B.float().t()
+    if pad_rows:
+        y = torch.cat([y, y.new_zeros(pad_rows, y.shape[1])])
     return y.to(torch.bfloat16) if bf16_out else y
 
 
@@ -167,7 +170,7 @@ def pe_proj_bwd(dy, pix, mean, rstd, M):
 def pe_kv(P, pix, pes, pesq, wt, kin, eps):
     """csrc/attention_pe.hip pe_key_stats / pe_kv_elem: the implicit K/V rows (B·M, 2C) bf16 from
     the bf16 PE product P' (M, 2C), the pixel channels and the generation table, plus μ, rσ."""
-    M = P.shape[0]
+    M = pes.shape[0]  # P may carry zero pad rows past M
     R, nc = pix.shape
     m = torch.arange(R, device=pix.device) % M
     mu = (pes[m] + pix.sum(1)) / kin
@@ -179,9 +182,9 @@ def pe_kv(P, pix, pes, pesq, wt, kin, eps):
 
 def attn_fwd_pe(q, P, pix, pes, pesq, wt, H, scale, kin, eps, nsplit):
     """csrc/attention_pe.hip attn_fwd_pe_kernel: encoder cross-attention over implicit K/V."""
-    C = H * 32
-    B = pix.shape[0] // P.shape[0]
-    kv = pe_kv(P, pix, pes, pesq, wt, kin, eps)[0].view(B, P.shape[0], 2 * C)
+    C, M = H * 32, pes.shape[0]
+    B = pix.shape[0] // M
+    kv = pe_kv(P, pix, pes, pesq, wt, kin, eps)[0].view(B, M, 2 * C)
     return attn_fwd(q, kv[:, :, :C], kv[:, :, C:], None, H, 32, scale, 0.0, None, nsplit)
 
 
@@ -189,6 +192,11 @@ def attn_bwd_pe_implicit(q, P, pes, pesq, wt, dO, lse, delta, pix, dq, D, part, 
     """attn_bwd_pe over implicit K/V (the same generation as attn_fwd_pe)."""
     kv, mu, rs = pe_kv(P, pix, pes, pesq, wt, kin, eps)
     attn_bwd_pe(q, kv, dO, lse, delta, mu, rs, pix, dq, D, part, H, scale, accumulate, bsplit)
+
+
+def attn_bwd_pe_part_rows(M, H, B, bsplit):
+    """rows of attn_bwd_pe's partial buffer (the kernel's grid mode; the emulation fills row 0)."""
+    return ((M + 255) // 256) * bsplit
 
 
 def attn_bwd_pe(q, kv, dO, lse, delta, mean, rstd, pix, dq, D, part, H, scale, accumulate, bsplit):

@@ -337,6 +337,9 @@ def _pe_proj_fwd(K, pix, pe, g, b, W, bias):
 PE_IMPLICIT = os.environ.get("PERCEIVER_PE_IMPLICIT", "1") != "0"
 
 
+PE_PAD_ROWS = 64  # zero rows after P' (the forward kernel's last prefetch reads them)
+
+
 def _pe_implicit_operands(K, nc, pe, g, b, W, bias):
     """(P' (M, 2C) bf16, Σe, Σe², generation table (6, 2C), Kin) of one K/V projection."""
     kin = g.shape[0]
@@ -344,16 +347,13 @@ def _pe_implicit_operands(K, nc, pe, g, b, W, bias):
     if W.shape[0] % 128 == 0 and hasattr(K, "pe_gemm"):
         wg, _, _, _, wt = K.pe_weight_prep(W.contiguous(), g.contiguous(), b.contiguous(), bias.contiguous(), nc,
                                            ebf.shape[1])
-        P = K.pe_gemm(ebf, wg, bf16_out=True)
+        P = K.pe_gemm(ebf, wg, bf16_out=True, pad_rows=PE_PAD_ROWS)
     else:
         wg, _, _, _, wt = emulation.pe_weight_prep(W, g, b, bias, nc, ebf.shape[1])
-        P = torch.mm(ebf.float(), wg.float().t()).to(torch.bfloat16)
+        P = emulation.pe_gemm(ebf, wg, bf16_out=True, pad_rows=PE_PAD_ROWS)
     return P, pes, pesq, wt, kin
 
 
-def pe_fwd_splits(B: int, H: int, M: int) -> int:
-    """Key splits of the implicit-K/V forward: ≈ 4096 waves (two per SIMD, two rounds)."""
-    return max(1, min((M + 31) // 32, -(-4096 // (B * H))))
 
 
 def _mm_tn_split(a, b):
@@ -484,7 +484,7 @@ class _LayerFn(torch.autograd.Function):
         imp = ent.get("implicit") if spec.cross else None
         if imp is not None:
             P, pes, pesq, wt, kin = imp
-            o, lse = K.attn_fwd_pe(q3, P, xkv2, pes, pesq, wt, H, scale, kin, EPS, pe_fwd_splits(B, H, M))
+            o, lse = K.attn_fwd_pe(q3, P, xkv2, pes, pesq, wt, H, scale, kin, EPS, 0)  # 0: one round of waves
         else:
             nsplit = pick_splits(B, H, Nq, k3.shape[1])
             o, lse = K.attn_fwd(q3, k3, v3, kmask, H, D, scale, p_attn, seed, nsplit)
@@ -604,7 +604,7 @@ class _LayerFn(torch.autograd.Function):
         if spec.cross:
             ent = ctx.kv_entry
             imp = ent.get("implicit")
-            M = imp[0].shape[0] if imp is not None else kv.shape[0] // B
+            M = imp[1].shape[0] if imp is not None else kv.shape[0] // B
             kv3 = kv.view(B, M, 2 * C) if imp is None else None
             if pe_fused:
                 # dK/dV folded into the factored projection's reductions (D, partials), which every
@@ -613,7 +613,9 @@ class _LayerFn(torch.autograd.Function):
                 if not acc:
                     bs = pe_attn_bsplit(B, M, H)
                     ent["pe_D"] = torch.empty((M, 2 * C), **f32)
-                    ent["pe_part"] = torch.empty((((M + 255) // 256) * bs, (2 + xkv2.shape[1]) * 2 * C), **f32)
+                    prows = (K.attn_bwd_pe_part_rows(M, H, B, bs) if hasattr(K, "attn_bwd_pe_part_rows")
+                             else ((M + 255) // 256) * bs)
+                    ent["pe_part"] = torch.empty((prows, (2 + xkv2.shape[1]) * 2 * C), **f32)
                     ent["pe_bsplit"] = bs
                 # broadcast latent queries (layer_1): dq comes back summed over the batch
                 dq = torch.empty((Bq, Nq, C), **f32)

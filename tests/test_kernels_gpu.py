@@ -570,7 +570,7 @@ def test_attention_bwd_pe_fused(B, Bq, Nq, M, H, nc, bsplit):
     for K in (_ext(), _emu()):
         dq = torch.empty(Bq, Nq, C, device=DEV)
         D = torch.empty(M, 2 * C, device=DEV)
-        part = torch.empty(nkb * bsplit, (2 + nc) * 2 * C, device=DEV)
+        part = torch.empty(K.attn_bwd_pe_part_rows(M, H, B, bsplit), (2 + nc) * 2 * C, device=DEV)
         K.attn_bwd_pe(q, kv, dO, lse, delta, mean, rstd, pix, dq, D, part, H, scale, False, bsplit)
         dq1 = dq.clone()
         K.attn_bwd_pe(q, kv, dO, lse, delta, mean, rstd, pix, dq, D, part, H, scale, True, bsplit)
@@ -592,7 +592,11 @@ def _pe_implicit_operands(M, H, nc, kin=133):
     Ebf[:, nc:kin] = E
     Ebf = bf(Ebf)
     wg, _, _, _, wt = _emu().pe_weight_prep(W, g, b, bias, nc, Kp)
-    P = _ext().pe_gemm(Ebf, wg, bf16_out=True) if (2 * C) % 128 == 0 else bf(Ebf.float() @ wg.float().t())
+    if (2 * C) % 128 == 0:  # 64 zero pad rows: the forward's last prefetch reads past M
+        P = _ext().pe_gemm(Ebf, wg, bf16_out=True, pad_rows=64)
+        assert torch.equal(P[M:].float(), torch.zeros(64, 2 * C, device=DEV))
+    else:
+        P = _emu().pe_gemm(Ebf, wg, bf16_out=True, pad_rows=64)
     return P, E.sum(1).contiguous(), (E * E).sum(1).contiguous(), wt, kin
 
 
@@ -604,6 +608,8 @@ def _pe_implicit_operands(M, H, nc, kin=133):
     (3, 3, 32, 600, 4, 3, 1, 1),
     (2, 2, 32, 50176, 4, 3, 1, 32),
     (5, 5, 20, 784, 4, 1, 4, 25),
+    (2, 1, 32, 288, 4, 3, 1, 4),   # the last split is empty
+    (6, 6, 32, 1000, 4, 2, 1, 0),  # 0: the kernel's own split count
 ])
 def test_attention_pe_implicit_kv(B, Bq, Nq, M, H, nc, bsplit, nsplit):
     """Encoder cross-attention over implicit K/V (attention_pe.hip attn_fwd_pe_kernel and the IMPL
@@ -628,7 +634,7 @@ def test_attention_pe_implicit_kv(B, Bq, Nq, M, H, nc, bsplit, nsplit):
     for K in (_ext(), _emu()):
         dq = torch.empty(Bq, Nq, C, device=DEV)
         D = torch.empty(M, 2 * C, device=DEV)
-        part = torch.empty(nkb * bsplit, (2 + nc) * 2 * C, device=DEV)
+        part = torch.empty(K.attn_bwd_pe_part_rows(M, H, B, bsplit), (2 + nc) * 2 * C, device=DEV)
         K.attn_bwd_pe_implicit(q, P, pes, pesq, wt, dO, l2, delta, pix, dq, D, part, H, scale, kin, eps, False, bsplit)
         dq1 = dq.clone()
         K.attn_bwd_pe_implicit(q, P, pes, pesq, wt, dO, l2, delta, pix, dq, D, part, H, scale, kin, eps, True, bsplit)
