@@ -52,18 +52,6 @@ __device__ __forceinline__ int vocab_reg(int j) {
   if (j < 0 || j >= 32 || ((j >> 2) & 1) != (lane_id() >> 5)) return -1;
   return (j & 3) + 4 * (j >> 3);
 }
-// this lane's row of a dl tile -> LDS [row][vocab] bf16, four 8-byte writes
-__device__ __forceinline__ void store_dl_row(uint16_t* sL, int ldl, int row, const float (&d)[16]) {
-  uint16_t* p = sL + row * ldl + 32 * (wave_id() & 1) + 4 * (lane_id() >> 5);
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    uint2 pk;
-    pk.x = pack2(d[4 * q], d[4 * q + 1]);
-    pk.y = pack2(d[4 * q + 2], d[4 * q + 3]);
-    *reinterpret_cast<uint2*>(p + 8 * q) = pk;
-  }
-}
-
 // Row r of the head input is H[idx[r]] (idx == nullptr: H[r]) of the fp32 decoder output: the
 // compaction gather and the bf16 cast happen on load, no gathered copy is ever written.
 template <int C>
@@ -296,200 +284,6 @@ __device__ __forceinline__ void dl_regs(const f32x16& acc, const float (&b)[16],
     for (int i = 0; i < 16; ++i) d[i] -= i == lab_reg ? g : 0.f;
   }
 }
-
-// bwd-a: dH[r][c] += sum_v dl[r][v] W[v][c]  over this split's vocab chunks (fp32 atomics)
-template <int C>
-__global__ __launch_bounds__(256) void ce_bwd_dh_kernel(const uint16_t* __restrict__ Hm,
-                                                        const int64_t* __restrict__ labels,
-                                                        const uint16_t* __restrict__ W, const float* __restrict__ bias,
-                                                        const float* __restrict__ lse, const float* __restrict__ gout,
-                                                        const float* __restrict__ count, int M, int V,
-                                                        int chunks_per_split, float* __restrict__ dH,
-                                                        const int64_t* __restrict__ rowmap, long long dh_rows) {
-  constexpr int LD = C + 8, LDL = VB + 8, NT = C / 32;
-  __shared__ __attribute__((aligned(16))) uint16_t sH[HB * LD];
-  __shared__ __attribute__((aligned(16))) uint16_t sW[VB * LD];
-  __shared__ __attribute__((aligned(16))) uint16_t sL[HB * LDL];
-  __shared__ __attribute__((aligned(16))) float sB[VB];
-  __shared__ long long sDst[HB];  // dH row of each tile row (-1: ignored row)
-  const int w = wave_id(), l = lane_id(), hh = l >> 5;
-  const int m0 = blockIdx.x * HB, split = blockIdx.y;
-  const int nchunks = (V + VB - 1) / VB;
-  const int c_begin = split * chunks_per_split, c_end = min(nchunks, c_begin + chunks_per_split);
-  stage_rows<C>(sH, LD, Hm, m0, M);
-  if (threadIdx.x < HB) {
-    const int gr = m0 + threadIdx.x;
-    const long long r = (gr < M && labels[gr] >= 0) ? (rowmap ? rowmap[gr] : gr) : -1;
-    sDst[threadIdx.x] = r < dh_rows ? r : -1;  // a row outside dH is dropped, never written
-  }
-  const int rl = 32 * (w >> 1) + (l & 31), gr = m0 + rl;
-  const int lab = gr < M ? (int)labels[gr] : -100;
-  const float lse_l2 = gr < M ? lse[gr] * kL2E : 0.f;
-  const float g = lab >= 0 ? gout[0] / fmaxf(count[0], 1.f) : 0.f;  // d(mean loss) / d(row loss)
-  // output dH tile 64 x C: sub-tiles (2 x NT), wave w owns tiles w, w+4
-  constexpr int MAXT = (2 * NT + 3) / 4;
-  f32x16 acc_o[MAXT];
-#pragma unroll
-  for (int t = 0; t < MAXT; ++t) acc_o[t] = f32x16{};
-  bf16x8 wr[C / 32];
-  float bnext = 0.f;
-  auto fetch = [&](int c) {
-    fetch_rows<C>(wr, W, c * VB, V);
-    const int v = c * VB + threadIdx.x;
-    if (threadIdx.x < VB) bnext = v < V ? bias[v] * kL2E : -__builtin_inff();
-  };
-  if (c_begin < c_end) fetch(c_begin);
-  for (int c = c_begin; c < c_end; ++c) {
-    const int v0 = c * VB;
-    lds_sync();
-    store_rows<C>(wr, sW, LD);
-    if (threadIdx.x < VB) sB[threadIdx.x] = bnext;
-    lds_sync();
-    if (c + 1 < c_end) fetch(c + 1);
-    const f32x16 acc = logits_tile_t<C>(sH, sW, LD);
-    float b[16], d[16];
-    vocab_regs(sB, b);
-    dl_regs(acc, b, lse_l2, g, vocab_reg(lab - v0 - 32 * (w & 1)), d);
-    store_dl_row(sL, LDL, rl, d);
-    lds_sync();
-    // dH += dl (64 x 64 vocab) . Wchunk (64 vocab x C): A k-contiguous, B = W[v][c] k-strided
-#pragma unroll
-    for (int t = 0; t < MAXT; ++t) {
-      const int tg = w + 4 * t;
-      if (tg < 2 * NT) {
-        const int r0 = 32 * (tg / NT), n0 = 32 * (tg % NT);
-#pragma unroll
-        for (int k0 = 0; k0 < VB; k0 += 16) acc_o[t] = mfma32(frag_kc(sL, LDL, r0, k0), frag_ks(sW, LD, n0, k0), acc_o[t]);
-      }
-    }
-  }
-  lds_sync();  // sDst is read across waves (no in-loop barrier has run for an empty split)
-#pragma unroll
-  for (int t = 0; t < MAXT; ++t) {
-    const int tg = w + 4 * t;
-    if (tg < 2 * NT) {
-      const int r0 = 32 * (tg / NT), n0 = 32 * (tg % NT);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        // dH row: the compacted row's source position (rowmap) or the row itself; ignored rows
-        // (label -100, incl. compaction padding) carry no gradient
-        const long long dst = sDst[r0 + acc_row(i, hh)];
-        if (dst >= 0) atomicAdd(dH + dst * C + n0 + (l & 31), acc_o[t][i]);
-      }
-    }
-  }
-}
-
-// bwd-b: dW[v][c] += sum_r dl[r][v] H[r][c], db[v] += sum_r dl[r][v]; grid (vocab chunk, row split),
-// H tiles (+ their LSE / labels) register-prefetched one tile ahead, partials added atomically
-template <int C>
-__global__ __launch_bounds__(256) void ce_bwd_dw_kernel(const uint16_t* __restrict__ Hm,
-                                                        const int64_t* __restrict__ labels,
-                                                        const uint16_t* __restrict__ W, const float* __restrict__ bias,
-                                                        const float* __restrict__ lse, const float* __restrict__ gout,
-                                                        const float* __restrict__ count, int M, int V,
-                                                        int tiles_per_split, float* __restrict__ dW,
-                                                        float* __restrict__ db, float* __restrict__ slab) {
-  constexpr int LD = C + 8, LDL = VB + 8, NT = C / 32;
-  __shared__ __attribute__((aligned(16))) uint16_t sH[HB * LD];
-  __shared__ __attribute__((aligned(16))) uint16_t sW[VB * LD];
-  __shared__ __attribute__((aligned(16))) uint16_t sL[HB * LDL];
-  __shared__ __attribute__((aligned(16))) float sB[VB];
-  __shared__ float sLse[HB];
-  __shared__ int sLab[HB];
-  __shared__ float sBs[2][64];
-  const int w = wave_id(), l = lane_id(), hh = l >> 5;
-  const int v0 = blockIdx.x * VB;
-  const int mt_begin = blockIdx.y * tiles_per_split;
-  const int mt_end = min((M + HB - 1) / HB, mt_begin + tiles_per_split);
-  const float gs = gout[0] / fmaxf(count[0], 1.f);
-  stage_rows<C>(sW, LD, W, v0, V);
-  if (threadIdx.x < VB) sB[threadIdx.x] = v0 + (int)threadIdx.x < V ? bias[v0 + threadIdx.x] * kL2E : -__builtin_inff();
-  const int rl = 32 * (w >> 1) + (l & 31);
-  constexpr int MAXT = (2 * NT + 3) / 4;
-  f32x16 acc_o[MAXT];
-#pragma unroll
-  for (int t = 0; t < MAXT; ++t) acc_o[t] = f32x16{};
-  float bsum[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) bsum[i] = 0.f;
-  bf16x8 hr[C / 32];
-  float aux = 0.f;  // threads [0,64): LSE * log2e of row tid, [64,128): label of row tid-64
-  auto fetch = [&](int mt) {
-    fetch_rows<C>(hr, Hm, mt * HB, M);
-    const int t = threadIdx.x & 63, gr = mt * HB + t;
-    if (threadIdx.x < 64) aux = gr < M ? lse[gr] * kL2E : 0.f;
-    else if (threadIdx.x < 128) aux = __int_as_float(gr < M ? (int)labels[gr] : -100);
-  };
-  if (mt_begin < mt_end) fetch(mt_begin);
-  lds_sync();
-  float b[16];
-  vocab_regs(sB, b);
-  for (int mt = mt_begin; mt < mt_end; ++mt) {
-    lds_sync();
-    store_rows<C>(hr, sH, LD);
-    if (threadIdx.x < 64) sLse[threadIdx.x] = aux;
-    else if (threadIdx.x < 128) sLab[threadIdx.x - 64] = __float_as_int(aux);
-    lds_sync();
-    if (mt + 1 < mt_end) fetch(mt + 1);
-    const f32x16 acc = logits_tile_t<C>(sH, sW, LD);
-    const int lab = sLab[rl];
-    float d[16];
-    dl_regs(acc, b, sLse[rl], lab >= 0 ? gs : 0.f, vocab_reg(lab - v0 - 32 * (w & 1)), d);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) bsum[i] += d[i];
-    store_dl_row(sL, LDL, rl, d);
-    lds_sync();
-    // dW chunk (64 vocab x C) += dl^T . H : A = dl stored [r][v] (k=r strided), B = H [r][c] (k strided)
-#pragma unroll
-    for (int t = 0; t < MAXT; ++t) {
-      const int tg = w + 4 * t;
-      if (tg < 2 * NT) {
-        const int r0 = 32 * (tg / NT), n0 = 32 * (tg % NT);
-#pragma unroll
-        for (int k0 = 0; k0 < HB; k0 += 16) acc_o[t] = mfma32(frag_ks(sL, LDL, r0, k0), frag_ks(sH, LD, n0, k0), acc_o[t]);
-      }
-    }
-  }
-  // bias: register i of lane l <-> vocab entry 32(w & 1) + acc_row(i, hh): sum over the 32 lanes
-  // of the half (their rows), then over the two waves sharing the vocab block
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const float v = half_sum(bsum[i]);
-    if ((l & 31) == 0) sBs[w >> 1][32 * (w & 1) + acc_row(i, hh)] = v;
-  }
-  lds_sync();
-  // partials: atomics into dW / db, or (slab) plain stores into row blockIdx.y of a
-  // (row splits, V·C + V₄) slab that a SlabJob later sums into dW | db (common.h)
-  float* dWp = dW;
-  float* dbp = db;
-  if (slab) {
-    dWp = slab + (long long)blockIdx.y * ((long long)V * C + ((V + 3) & ~3));
-    dbp = dWp + (long long)V * C;
-  }
-  if (threadIdx.x < 64 && v0 + threadIdx.x < V) {
-    const float v = sBs[0][threadIdx.x] + sBs[1][threadIdx.x];
-    if (slab) dbp[v0 + threadIdx.x] = v;
-    else atomicAdd(dbp + v0 + threadIdx.x, v);
-  }
-#pragma unroll
-  for (int t = 0; t < MAXT; ++t) {
-    const int tg = w + 4 * t;
-    if (tg < 2 * NT) {
-      const int r0 = 32 * (tg / NT), n0 = 32 * (tg % NT);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int vv = v0 + r0 + acc_row(i, hh);
-        float* p = dWp + (long long)vv * C + n0 + (l & 31);
-        if (vv < V) {
-          if (slab) *p = acc_o[t][i];
-          else atomicAdd(p, acc_o[t][i]);
-        }
-      }
-    }
-  }
-}
-
 
 // ---- register-operand variants (default): the dl tile never goes through LDS -------------
 // The logits tile's accumulator is used directly as an MFMA operand (pack_acc: the 16 values of
@@ -916,20 +710,11 @@ void ce_bwd_launch(int C, const uint16_t* Hm, const int64_t* labels, const uint1
     (void)hipMemsetAsync(db, 0, sizeof(float) * (size_t)V, st);
   }
   dim3 ga((M + HB - 1) / HB, nsplit), gb(nchunks, rsplit);
-  // PIO_CE_BWD_LDS=1: the variants that pass the dl tile through LDS (A/B reference)
-  static const bool lds_dl = [] { const char* v = getenv("PIO_CE_BWD_LDS"); return v && v[0] == '1'; }();
-#define CEB(CC)                                                                                                  \
-  if (lds_dl) {                                                                                                  \
-    hipLaunchKernelGGL(ce_bwd_dh_kernel<CC>, ga, dim3(256), 0, st, Hm, labels, W, bias, lse, gout, count, M, V, cps, \
-                       dH, rowmap, dh_rows);                                                                     \
-    hipLaunchKernelGGL(ce_bwd_dw_kernel<CC>, gb, dim3(256), 0, st, Hm, labels, W, bias, lse, gout, count, M, V, tps, \
-                       dW, db, slab);                                                                            \
-  } else {                                                                                                       \
-    hipLaunchKernelGGL(ce_bwd_dh_reg_kernel<CC>, ga, dim3(256), 0, st, Hm, labels, W, bias, lse, gout, count, M, V, \
-                       cps, dH, rowmap, dh_rows);                                                                \
-    hipLaunchKernelGGL(ce_bwd_dw_reg_kernel<CC>, gb, dim3(256), 0, st, Hm, labels, W, bias, lse, gout, count, M, V, \
-                       tps, dW, db, slab);                                                                       \
-  }
+#define CEB(CC)                                                                                                 \
+  hipLaunchKernelGGL(ce_bwd_dh_reg_kernel<CC>, ga, dim3(256), 0, st, Hm, labels, W, bias, lse, gout, count, M, V,   \
+                     cps, dH, rowmap, dh_rows);                                                                    \
+  hipLaunchKernelGGL(ce_bwd_dw_reg_kernel<CC>, gb, dim3(256), 0, st, Hm, labels, W, bias, lse, gout, count, M, V,   \
+                     tps, dW, db, slab)
   if (C == 64) { CEB(64); }
   else if (C == 128) { CEB(128); }
   else if (C == 32) { CEB(32); }
