@@ -30,7 +30,7 @@ struct DropCfg {  // common.h
   float scale;
 };
 struct PostAttnGrads { float *dWo, *dbo, *dg2, *dbe2, *dW1, *db1, *dW2, *db2; int vrs; int slab; };
-constexpr int kMaxSlabSegs = 16, kSlabRowsPerBlock = 32;  // common.h
+constexpr int kMaxSlabSegs = 16, kSlabColsPerBlock = 1024;  // common.h
 struct SlabJob {
   const float* slab;
   int S, P, nbx, nblk;
@@ -430,6 +430,16 @@ std::vector<Tensor> sa_layer_fwd(Tensor qkv, Tensor x, int64_t N, double scale, 
   return {o, lse, z, y, m, r, u};
 }
 
+// workgroups of a non-deterministic SlabJob (PIO_SLAB_WGS overrides; 128 measured best on the MLM step: 96–128 ≈ equal, 256 and 64 slower)
+int slab_job_target() {
+  static const int t = [] {
+    const char* v = getenv("PIO_SLAB_WGS");
+    const int x = v ? atoi(v) : 0;
+    return x > 0 ? x : 128;
+  }();
+  return t;
+}
+
 // the backward entry points below ACCUMULATE parameter gradients into caller-provided fp32
 // tensors (normally views of the flat gradient buffer) with device atomics: no partial slabs,
 // no reduction pass, no autograd AccumulateGrad adds
@@ -485,9 +495,17 @@ pio::SlabJob make_job(const OptT& slab, std::vector<Tensor>& dsts, const std::ve
   j.slab = t.data_ptr<float>();
   j.S = (int)t.size(0);
   j.P = P;
-  j.nbx = (P + 255) / 256;
   j.det = g_det ? 1 : 0;
-  j.nblk = g_det ? j.nbx : j.nbx * ((j.S + pio::kSlabRowsPerBlock - 1) / pio::kSlabRowsPerBlock);
+  if (g_det) {  // one workgroup per 256 columns, all rows (common.h slab_reduce_block)
+    j.nbx = (P + 255) / 256;
+    j.nblk = j.nbx;
+  } else {  // 1024-column blocks × row splits: ≈ slab_job_target() workgroups, one round
+    j.nbx = (P + pio::kSlabColsPerBlock - 1) / pio::kSlabColsPerBlock;
+    int nsy = std::max(1, std::min(j.S, slab_job_target() / j.nbx));
+    const int rb = (j.S + nsy - 1) / nsy;
+    nsy = (j.S + rb - 1) / rb;
+    j.nblk = j.nbx * nsy;
+  }
   return j;
 }
 

@@ -252,7 +252,7 @@ __device__ int trace_bx, trace_by, trace_bz;
 // (all loads in flight), LDS combine, then wave w adds columns 64w..64w+63 with one
 // contiguous 256-B no-return atomic instruction: S/32 adds per element in all.
 constexpr int kMaxSlabSegs = 16;
-constexpr int kSlabRowsPerBlock = 32;
+
 // 32 bytes of zeros in global memory: the source of every out-of-range element of a fetch.  A
 // load whose predicate is false reads here instead (an address select), so a phase's loads
 // are straight-line code.  hipcc waits for a load at the first branch, phi copy or arithmetic
@@ -298,14 +298,22 @@ __device__ __forceinline__ void zero_span_block(const SlabJob& j) {
   for (long long i = z0 + threadIdx.x; i < z1; i += blockDim.x)
     reinterpret_cast<float4*>(j.zero_p)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
-// part: ≥ 4 KiB of 16-B aligned LDS
+// Column blocks of a SlabJob: kSlabColsPerBlock columns per workgroup (256 threads × 4).
+// Non-deterministic mode: workgroup b sums rows [by·RB, (by + 1)·RB) of column block bx
+// (b = by·nbx + bx, RB = ⌈S / (nblk / nbx)⌉, the host sizes nblk ≈ 128 workgroups) with
+// every row's load in flight at once (16 per batch), and adds its 4 column sums per thread
+// atomically — nblk / nbx partial sums per column.  A job carried by a one-workgroup-per-CU
+// kernel (≈100 KB of LDS) runs in one round after the carrier's tiles.
+// Deterministic mode: one workgroup per column block sums all S rows in a fixed order and
+// adds once (single writer).
+constexpr int kSlabColsPerBlock = 1024;
+// part: ≥ 4 KiB of 16-B aligned LDS (deterministic path)
 __device__ __forceinline__ void slab_reduce_block(const SlabJob& j, int b, float4* part) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const int bx = b % j.nbx, by = b / j.nbx;
-  const int cb = bx * 256, c = cb + 4 * l, P = j.P;
-  const int s0 = by * kSlabRowsPerBlock, s1 = min(j.S, s0 + kSlabRowsPerBlock);
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int P = j.P;
   if (j.det) {  // fixed summation order, a single writer per element: bitwise reproducible
+    const int cb = b * 256, c = cb + 4 * l;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     if (c < P)
       for (int s = w; s < j.S; s += 4) {
         const float4 v = *reinterpret_cast<const float4*>(j.slab + (long long)s * P + c);
@@ -323,27 +331,32 @@ __device__ __forceinline__ void slab_reduce_block(const SlabJob& j, int b, float
     }
     return;
   }
-  if (c < P) {
-    float4 v[kSlabRowsPerBlock / 4];
+  const int nsy = j.nblk / j.nbx, rb = (j.S + nsy - 1) / nsy;
+  const int bx = b % j.nbx, by = b / j.nbx;
+  const int c = bx * kSlabColsPerBlock + 4 * (int)threadIdx.x;
+  const int s0 = by * rb, s1 = min(j.S, s0 + rb);
+  const bool cin = c < P;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int s = s0; s < s1; s += 16) {
+    float4 v[16];
 #pragma unroll
-    for (int i = 0; i < kSlabRowsPerBlock / 4; ++i) {
-      const int s = s0 + w + 4 * i;
-      v[i] = s < s1 ? *reinterpret_cast<const float4*>(j.slab + (long long)s * P + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = 0; i < 16; ++i) {  // address selects: rows past s1 / columns past P read zeros
+      const bool ok = cin && s + i < s1;
+      v[i] = *reinterpret_cast<const float4*>(ok ? j.slab + (long long)(s + i) * P + c : kZero32B);
     }
 #pragma unroll
-    for (int i = 0; i < kSlabRowsPerBlock / 4; ++i) {
+    for (int i = 0; i < 16; ++i) {
       acc.x += v[i].x; acc.y += v[i].y; acc.z += v[i].z; acc.w += v[i].w;
     }
   }
-  part[w * 64 + l] = acc;
-  __syncthreads();
-  const float* pf = reinterpret_cast<const float*>(part);
-  const int k = 64 * w + l, col = cb + k;
-  if (col >= P) return;
-  const float sum = pf[k] + pf[256 + k] + pf[512 + k] + pf[768 + k];
+  if (!cin) return;
+  const float a4[4] = {acc.x, acc.y, acc.z, acc.w};
   for (int q = 0; q < j.n; ++q) {
-    const int lo = j.off[q];
-    if (col >= lo && col < lo + j.len[q]) atomicAdd(j.dst[q] + (col - lo), sum);
+    const int lo = j.off[q], hi = lo + j.len[q];
+    if (c + 4 <= lo || c >= hi) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (c + e >= lo && c + e < hi) atomicAdd(j.dst[q] + (c + e - lo), a4[e]);
   }
 }
 

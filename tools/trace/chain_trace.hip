@@ -10,6 +10,7 @@
 #include "../../perceiver_io_amd/csrc/rowgemm.hip"
 #include "../../perceiver_io_amd/csrc/chain.hip"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -124,8 +125,8 @@ int main(int argc, char** argv) {
   float* gdst;
   CK(hipMalloc(&gdst, (size_t)P * 4));
   pio::SlabJob job2{};
-  job2.slab = slab2; job2.S = tiles; job2.P = P; job2.nbx = (P + 255) / 256;
-  job2.nblk = job2.nbx * ((tiles + pio::kSlabRowsPerBlock - 1) / pio::kSlabRowsPerBlock);
+  job2.slab = slab2; job2.S = tiles; job2.P = P; job2.nbx = (P + pio::kSlabColsPerBlock - 1) / pio::kSlabColsPerBlock;
+  { const int t = getenv("PIO_SLAB_WGS") ? atoi(getenv("PIO_SLAB_WGS")) : 128; int nsy = std::max(1, std::min(tiles, t / job2.nbx)); const int rb = (tiles + nsy - 1) / nsy; job2.nblk = job2.nbx * ((tiles + rb - 1) / rb); }
   job2.n = 1; job2.dst[0] = gdst; job2.off[0] = 0; job2.len[0] = P;
   trace("ln_linear_post_attn_bwd_chain + slab job", R, [&]() {
     pio::ln_linear_post_attn_bwd_launch(C, G, W[3], Z, m1, r1, vec[5], vec[6], dres, dg1, db1, dwq, dbq, Y, m2, r2, U, O,
