@@ -332,7 +332,10 @@ __global__ void attn_bwd_prep_kernel(const uint16_t* __restrict__ dO, const uint
 // QR > 0 fixes the query tiles per round (QR = 1 for ≤ 32 queries, 2 for ≤ 64: a quarter / half
 // of the LDS, so several workgroups share a CU on the few-query / many-key cross-attention;
 // PIO_ATTN_BWD_FULL_LDS=1 restores the 4-tile rounds)
-template <int D, int NW, int QR = 0>
+// OBF: dQ / dK / dV stored as bf16 (the pointers are uint16_t views; every element written once:
+// a single key block, no query split, no accumulation — host-checked), for a consumer that reads
+// them as bf16 MFMA operands anyway (the chain-layout layer-boundary backward)
+template <int D, int NW, int QR = 0, bool OBF = false>
 __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uint16_t* __restrict__ dO,
                                                            const float* __restrict__ LSE,
                                                            const float* __restrict__ delta, float* __restrict__ dq,
@@ -553,10 +556,11 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
         for (int i = 0; i < 4; ++i) {
           const int qq = (qt0 + j) * 32 + 16 * mh + 4 * g + i;
           if (qq < a.Nq) {
-            float* dst = dq + (long long)b * dq_bs + (long long)qq * dq_rs + h * D + (l & 15);
+            const long long di = (long long)b * dq_bs + (long long)qq * dq_rs + h * D + (l & 15);
             const float v = (a0[i] + a1[i]) * a.scale;
-            if (dq_atomic) atomicAdd(dst, v);
-            else *dst = v;
+            if constexpr (OBF) reinterpret_cast<uint16_t*>(dq)[di] = f2bf(v);
+            else if (dq_atomic) atomicAdd(dq + di, v);
+            else dq[di] = v;
           }
         }
       }
@@ -629,8 +633,16 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
         const int kl = cc / CPR, col = (cc % CPR) * 4, kk = kbase + kl;
         if (kk < a.Nk) {
           float4 v = *reinterpret_cast<const float4*>(sE + ((isv ? KB : 0) + kl) * LDE + col);
-          float* dst = (isv ? dv + (long long)b * dv_bs + (long long)kk * dv_rs
-                            : dk + (long long)b * dk_bs + (long long)kk * dk_rs) + h * D + col;
+          const long long di = (isv ? (long long)b * dv_bs + (long long)kk * dv_rs
+                                    : (long long)b * dk_bs + (long long)kk * dk_rs) + h * D + col;
+          if constexpr (OBF) {
+            uint2 pk;
+            pk.x = pack2(v.x, v.y);
+            pk.y = pack2(v.z, v.w);
+            *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(isv ? dv : dk) + di) = pk;
+            continue;
+          }
+          float* dst = (isv ? dv : dk) + di;
           if (kv_acc) {
             const float4 o = *reinterpret_cast<const float4*>(dst);
             v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
@@ -651,6 +663,12 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
       const int dd = 32 * t + r;
       if (kk < a.Nk && dd < D) {
         // kv_acc: add onto earlier contributions (K/V shared by several applications, K-06)
+        if constexpr (OBF) {
+          reinterpret_cast<uint16_t*>(dk)[(long long)b * dk_bs + (long long)kk * dk_rs + h * D + dd] =
+              f2bf(dK[t][i] * a.scale);
+          reinterpret_cast<uint16_t*>(dv)[(long long)b * dv_bs + (long long)kk * dv_rs + h * D + dd] = f2bf(dV[t][i]);
+          continue;
+        }
         float* pk = dk + (long long)b * dk_bs + (long long)kk * dk_rs + h * D + dd;
         float* pv = dv + (long long)b * dv_bs + (long long)kk * dv_rs + h * D + dd;
         if (nqs > 1) {
@@ -824,6 +842,24 @@ void attn_bwd_launch(const AttnArgs& a, int D, const uint16_t* O, const uint16_t
     case 128: bwd_launch_t<128, 4>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, qsplit_ok, dq_zeroed, st); break;
     default: break;
   }
+}
+
+// bf16 dQ / dK / dV (attn_bwd_kernel OBF): head width 16, one key block (Nk ≤ 256), no query
+// split, more than 64 queries (the full-LDS variant), nothing to accumulate onto; false (nothing
+// launched) when the shape does not qualify
+bool attn_bwd_bf16_ok(const AttnArgs& a, int D) {
+  return D == 16 && a.Nk <= 32 * 8 && a.Nq > 64 && bwd_query_splits(1, a.H, a.B, a.Nq, 1) == 1;
+}
+bool attn_bwd_bf16_launch(const AttnArgs& a, int D, const uint16_t* dO, const float* LSE, const float* delta,
+                          uint16_t* dq, long long dq_bs, int dq_rs, uint16_t* dk, long long dk_bs, int dk_rs,
+                          uint16_t* dv, long long dv_bs, int dv_rs, hipStream_t st) {
+  if (!attn_bwd_bf16_ok(a, D)) return false;
+  const int nqt = (a.Nq + 31) / 32;
+  dim3 grid(1, a.H, a.B);
+  hipLaunchKernelGGL((attn_bwd_kernel<16, 8, 0, true>), grid, dim3(512), 0, st, a, dO, LSE, delta,
+                     reinterpret_cast<float*>(dq), dq_bs, dq_rs, reinterpret_cast<float*>(dk), dk_bs, dk_rs,
+                     reinterpret_cast<float*>(dv), dv_bs, dv_rs, 0, 0, 0LL, 1, nqt);
+  return true;
 }
 
 }  // namespace pio

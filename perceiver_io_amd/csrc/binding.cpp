@@ -51,6 +51,9 @@ void attn_fwd_launch(const AttnArgs&, int, uint16_t*, float*, float*, float*, in
 void attn_bwd_launch(const AttnArgs&, int, const uint16_t*, const uint16_t*, const float*, float*, float*, long long,
                      int, float*, long long, int, float*, long long, int, bool, bool, long long, int, int, hipStream_t);
 int attn_bwd_key_blocks(int, int);
+bool attn_bwd_bf16_ok(const AttnArgs&, int);
+bool attn_bwd_bf16_launch(const AttnArgs&, int, const uint16_t*, const float*, const float*, uint16_t*, long long, int,
+                          uint16_t*, long long, int, uint16_t*, long long, int, hipStream_t);
 int attn_bwd_zero_plan(int, int, int, int, int);
 void ln_linear_fwd_launch(const void*, bool, int, int, int, const float*, const float*, float, const uint16_t*, int,
                           const float*, int, int, const float*, int, void*, bool, int, float*, float*, const float*, int,
@@ -67,7 +70,7 @@ void sa_layer_fwd_launch(const uint16_t*, int, float, uint16_t*, float*, const f
                          const float*, const float*, float, const uint16_t*, const float*, const uint16_t*, const float*,
                          float*, float*, float*, float*, uint16_t*, int, const float*, const float*, const uint16_t*,
                          const float*, uint16_t*, float*, float*, const DropCfg&, int, hipStream_t);
-void ln_linear_post_attn_bwd_launch(int, const float*, const uint16_t*, const float*, const float*, const float*,
+bool ln_linear_post_attn_bwd_launch(int, const void*, bool, const uint16_t*, const float*, const float*, const float*,
                                     const float*, const float*, const float*, float*, float*, float*, float*,
                                     const float*, const float*, const float*, const uint16_t*, const uint16_t*,
                                     const uint16_t*, const uint16_t*, const uint16_t*, const float*, const float*,
@@ -272,6 +275,28 @@ std::vector<Tensor> attn_bwd(Tensor q, Tensor k, Tensor v, OptT kmask, Tensor o,
   auto a = make_args(q, k, v, kmask, (int)H, (int)D, scale, dropout_p, seed, site);
   TORCH_CHECK(dO.is_contiguous() && o.is_contiguous(), "O / dO must be contiguous (B, Nq, H*D)");
   auto f32 = q.options().dtype(torch::kFloat32);
+  if (dq_out.has_value() && dq_out->scalar_type() == torch::kBFloat16) {
+    // bf16 outputs (all three, stored once each): the self-attention backward feeding the
+    // chain-layout layer-boundary kernel, which reads them as bf16 operands
+    TORCH_CHECK(dk_out.has_value() && dv_out.has_value() && dk_out->scalar_type() == torch::kBFloat16 &&
+                    dv_out->scalar_type() == torch::kBFloat16 && delta_in.has_value() && !kv_accumulate,
+                "bf16 attn_bwd outputs: dq/dk/dv all bf16, delta given, no accumulation");
+    Tensor dq = *dq_out, dk = *dk_out, dv = *dv_out;
+    TORCH_CHECK(dq.stride(2) == 1 && dk.stride(2) == 1 && dv.stride(2) == 1, "dq/dk/dv need unit inner stride");
+    Tensor delta = *delta_in;
+    TORCH_CHECK(delta.is_contiguous() && delta.numel() == (int64_t)a.B * a.Nq * H, "delta must be (B, Nq, H)");
+    CHECK_DT(delta, torch::kFloat32);
+    if (pio::attn_bwd_bf16_ok(a, (int)D)) {
+      pio::attn_bwd_bf16_launch(a, (int)D, bfp(dO), f32p(lse), delta.data_ptr<float>(), bfp_mut(dq), dq.stride(0),
+                                (int)dq.stride(1), bfp_mut(dk), dk.stride(0), (int)dk.stride(1), bfp_mut(dv),
+                                dv.stride(0), (int)dv.stride(1), stream());
+    } else {  // shape not covered by the bf16 variant: fp32, then narrowed
+      auto r = attn_bwd(q, k, v, kmask, o, dO, lse, delta_in, H, D, scale, dropout_p, seed, c10::nullopt, c10::nullopt,
+                        c10::nullopt, false, site, false, false);
+      dq.copy_(r[0]); dk.copy_(r[1]); dv.copy_(r[2]);
+    }
+    return {dq, dk, dv};
+  }
   Tensor dq = dq_out.has_value() ? *dq_out : torch::empty({a.B, a.Nq, H * D}, f32);
   Tensor dk = dk_out.has_value() ? *dk_out : torch::empty({a.B, a.Nk, H * D}, f32);
   Tensor dv = dv_out.has_value() ? *dv_out : torch::empty({a.B, a.Nk, H * D}, f32);
@@ -576,7 +601,7 @@ std::vector<Tensor> ln_linear_post_attn_bwd(Tensor g, Tensor wq, Tensor x, Tenso
   const int nq = (int)wq.size(0);  // 3C: packed QKV of a self-attention layer; C: a cross-attention query projection
   TORCH_CHECK(wq.is_contiguous() && (nq == 3 * C || nq == C) && wq.size(1) == C, "wq must be (3C, C) or (C, C)");
   TORCH_CHECK(g.is_contiguous() && g.size(0) == R && g.size(1) == nq, "g must be (R, rows(wq)) contiguous");
-  CHECK_DT(g, torch::kFloat32);
+  TORCH_CHECK(g.scalar_type() == torch::kFloat32 || g.scalar_type() == torch::kBFloat16, "g must be fp32 or bf16");
   TORCH_CHECK(x.size(0) == R && x.size(1) == C && dres.size(0) == R && dres.size(1) == C, "x / dres must be (R, C)");
   TORCH_CHECK(ll_grads.size() == 4 && pa_grads.size() == 8, "4 + 8 slab targets expected");
   const int64_t sr = (R + 63) / 64, CC = (int64_t)C * C;
@@ -593,11 +618,18 @@ std::vector<Tensor> ln_linear_post_attn_bwd(Tensor g, Tensor wq, Tensor x, Tenso
   Tensor dy = torch::empty({R, C}, f32);
   Tensor dO = torch::empty({R, C}, y.options().dtype(torch::kBFloat16));
   Tensor delta = torch::empty({R, H}, f32);
-  pio::ln_linear_post_attn_bwd_launch(
-      C, f32p(g), bfp(wq), f32p(x), f32p(mean1), f32p(rstd1), f32p(lnw), f32p(lnb), f32p(dres), dg1, db1, dwq, dbq,
-      f32p(y), f32p(m2), f32p(r2), bfp(u), bfp(o), bfp(wo), bfp(w1), bfp(w2), f32p(g2), f32p(be2),
-      dy.data_ptr<float>(), bfp_mut(dO), delta.data_ptr<float>(), (int)H, pg, R,
-      with_zero_span(make_job(job_slab, job_dsts, job_offs), zero_out, y), make_drop(seed, site, p), nq, stream());
+  const auto job = with_zero_span(make_job(job_slab, job_dsts, job_offs), zero_out, y);
+  const auto dr = make_drop(seed, site, p);
+  auto launch = [&](const Tensor& gg) {
+    const bool gbf = gg.scalar_type() == torch::kBFloat16;
+    return pio::ln_linear_post_attn_bwd_launch(
+        C, gg.data_ptr(), gbf, bfp(wq), f32p(x), f32p(mean1), f32p(rstd1), f32p(lnw), f32p(lnb), f32p(dres), dg1, db1,
+        dwq, dbq, f32p(y), f32p(m2), f32p(r2), bfp(u), bfp(o), bfp(wo), bfp(w1), bfp(w2), f32p(g2), f32p(be2),
+        dy.data_ptr<float>(), bfp_mut(dO), delta.data_ptr<float>(), (int)H, pg, R, job, dr, nq, stream());
+  };
+  // a bf16 G (from attn_bwd's bf16 outputs) is taken by the chain-layout kernel; any other
+  // kernel gets it widened to fp32 (same values)
+  if (!launch(g)) TORCH_CHECK(launch(g.to(torch::kFloat32)), "ln_linear_post_attn_bwd: launch failed");
   return {dy, dO, delta};
 }
 

@@ -476,9 +476,11 @@ constexpr int lpb_chain_smem() {
          2 * (NQ * 64 * 72 > 7 * 64 * 72 ? NQ * 64 * 72 : 7 * 64 * 72) + 4 * 4 * 64;
 }
 
-template <int NQ>
+// TG: the element type of G (float, or uint16_t = bf16 straight from the attention backward's
+// bf16 outputs: the kernel consumes G only as bf16 MFMA operands, so both give identical results)
+template <int NQ, typename TG>
 __global__ __launch_bounds__(256) void ln_linear_post_attn_bwd_chain_kernel(
-    const float* __restrict__ G, const uint16_t* __restrict__ Wq, const float* __restrict__ X,
+    const TG* __restrict__ G, const uint16_t* __restrict__ Wq, const float* __restrict__ X,
     const float* __restrict__ mean1, const float* __restrict__ rstd1, const float* __restrict__ lnw,
     const float* __restrict__ lnb, const float* __restrict__ dres, float* __restrict__ dlnw, float* __restrict__ dlnb,
     float* __restrict__ dWq, float* __restrict__ dbq, const float* __restrict__ Ysave, const float* __restrict__ mean2,
@@ -522,12 +524,18 @@ __global__ __launch_bounds__(256) void ln_linear_post_attn_bwd_chain_kernel(
                         : row < 3 * C ? W2 + (row - 2 * C) * C : Wq + (row - 3 * C) * C;
     wr[i] = *reinterpret_cast<const bf16x8*>(src + col);
   }
-  float4 gv[KT][2];
+  constexpr bool GBF = sizeof(TG) == 2;
+  float4 gv[GBF ? 1 : KT][2];
+  bf16x8 gvb[GBF ? KT : 1];
 #pragma unroll
   for (int t = 0; t < KT; ++t) {
-    const float* p = G + (long long)gr * nq + 32 * t + 8 * g;
-    gv[t][0] = *reinterpret_cast<const float4*>(p);
-    gv[t][1] = *reinterpret_cast<const float4*>(p + 4);
+    const TG* p = G + (long long)gr * nq + 32 * t + 8 * g;
+    if constexpr (GBF) {
+      gvb[t] = *reinterpret_cast<const bf16x8*>(p);
+    } else {
+      gv[t][0] = *reinterpret_cast<const float4*>(p);
+      gv[t][1] = *reinterpret_cast<const float4*>(p + 4);
+    }
   }
   float xv[NM][4], dv[NM][4], yv[NM][4];
   cl_load_f32<NM>(xv, X, C, gr);
@@ -566,9 +574,13 @@ __global__ __launch_bounds__(256) void ln_linear_post_attn_bwd_chain_kernel(
     bf16x8 gb[KT];
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
-      const float4 a = gv[t][0], b = gv[t][1];
-      gb[t][0] = (short)f2bf(a.x); gb[t][1] = (short)f2bf(a.y); gb[t][2] = (short)f2bf(a.z); gb[t][3] = (short)f2bf(a.w);
-      gb[t][4] = (short)f2bf(b.x); gb[t][5] = (short)f2bf(b.y); gb[t][6] = (short)f2bf(b.z); gb[t][7] = (short)f2bf(b.w);
+      if constexpr (GBF) {
+        gb[t] = gvb[t];
+      } else {
+        const float4 a = gv[t][0], b = gv[t][1];
+        gb[t][0] = (short)f2bf(a.x); gb[t][1] = (short)f2bf(a.y); gb[t][2] = (short)f2bf(a.z); gb[t][3] = (short)f2bf(a.w);
+        gb[t][4] = (short)f2bf(b.x); gb[t][5] = (short)f2bf(b.y); gb[t][6] = (short)f2bf(b.z); gb[t][7] = (short)f2bf(b.w);
+      }
       *reinterpret_cast<bf16x8*>(sG + (16 * w + (l & 15)) * LDG + 32 * t + 8 * g) = gb[t];
     }
 #pragma unroll
@@ -728,7 +740,7 @@ bool sa_layer_fwd_chain_launch(const uint16_t* QKV, int N, float scale_log2, uin
   return true;
 }
 
-bool ln_linear_post_attn_bwd_chain_launch(const float* G, const uint16_t* Wq, const float* X, const float* mean1,
+bool ln_linear_post_attn_bwd_chain_launch(const void* G, bool g_bf16, const uint16_t* Wq, const float* X, const float* mean1,
                                           const float* rstd1, const float* lnw, const float* lnb, const float* dres,
                                           float* dlnw, float* dlnb, float* dWq, float* dbq, const float* Ysave,
                                           const float* mean2, const float* rstd2, const uint16_t* U, const uint16_t* O,
@@ -738,12 +750,18 @@ bool ln_linear_post_attn_bwd_chain_launch(const float* G, const uint16_t* Wq, co
                                           int nq, hipStream_t st) {
   if (nq != 192 && nq != 64) return false;
   dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0));
-#define LPC(NQ)                                                                                                        \
-  hipLaunchKernelGGL((ln_linear_post_attn_bwd_chain_kernel<NQ>), grid, dim3(256), 0, st, G, Wq, X, mean1, rstd1, lnw, \
-                     lnb, dres, dlnw, dlnb, dWq, dbq, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO, delta,   \
-                     grads, R, job, dr)
-  if (nq == 192) LPC(3);
-  else LPC(1);
+#define LPC(NQ, TG)                                                                                                    \
+  hipLaunchKernelGGL((ln_linear_post_attn_bwd_chain_kernel<NQ, TG>), grid, dim3(256), 0, st, static_cast<const TG*>(G), \
+                     Wq, X, mean1, rstd1, lnw, lnb, dres, dlnw, dlnb, dWq, dbq, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2,  \
+                     be2, dY, dO, delta, grads, R, job, dr)
+  if (g_bf16) {
+    if (nq != 192) return false;  // bf16 G only from the self-attention backward (nq = 3C)
+    LPC(3, uint16_t);
+  } else if (nq == 192) {
+    LPC(3, float);
+  } else {
+    LPC(1, float);
+  }
 #undef LPC
   return true;
 }

@@ -1448,7 +1448,7 @@ bool sa_layer_fwd_chain_launch(const uint16_t* QKV, int N, float scale_log2, uin
                                float* Ysave, float* mean2, float* rstd2, uint16_t* Usave, int R, const float* lnw,
                                const float* lnb, const uint16_t* Wq, const float* bq, uint16_t* QKVn, float* mean1,
                                float* rstd1, const DropCfg& dr, int nq, hipStream_t st);
-bool ln_linear_post_attn_bwd_chain_launch(const float* G, const uint16_t* Wq, const float* X, const float* mean1,
+bool ln_linear_post_attn_bwd_chain_launch(const void* G, bool g_bf16, const uint16_t* Wq, const float* X, const float* mean1,
                                           const float* rstd1, const float* lnw, const float* lnb, const float* dres,
                                           float* dlnw, float* dlnb, float* dWq, float* dbq, const float* Ysave,
                                           const float* mean2, const float* rstd2, const uint16_t* U, const uint16_t* O,
@@ -1611,7 +1611,9 @@ void post_attn_bwd_launch(int C, const float* dZ, const float* Ysave, const floa
 #undef PAB
 }
 
-void ln_linear_post_attn_bwd_launch(int C, const float* G, const uint16_t* Wq, const float* X, const float* mean1,
+// G: fp32, or (g_bf16) bf16 — taken by the chain-layout kernel only; returns false (nothing
+// launched) for a bf16 G the chain kernel cannot take (the caller converts it to fp32)
+bool ln_linear_post_attn_bwd_launch(int C, const void* Gv, bool g_bf16, const uint16_t* Wq, const float* X, const float* mean1,
                                     const float* rstd1, const float* lnw, const float* lnb, const float* dres,
                                     float* dlnw, float* dlnb, float* dWq, float* dbq, const float* Ysave,
                                     const float* mean2, const float* rstd2, const uint16_t* U, const uint16_t* O,
@@ -1620,11 +1622,14 @@ void ln_linear_post_attn_bwd_launch(int C, const float* G, const uint16_t* Wq, c
                                     const PostAttnGrads& grads, int R, const SlabJob& job, const DropCfg& dr,
                                     int nq, hipStream_t st) {
   dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0));
-  const bool av = av_ok({G, Wq, X, lnw, lnb, dres, Ysave, U, O, Wo, W1, W2, dY, dO}, {});
+  const float* G = static_cast<const float*>(Gv);
+  const bool av = av_ok({Gv, Wq, X, lnw, lnb, dres, Ysave, U, O, Wo, W1, W2, dY, dO}, {});
   if (av && C == 64 && H == 4 && grads.slab && (R % 64) == 0 && use_chain() &&
-      ln_linear_post_attn_bwd_chain_launch(G, Wq, X, mean1, rstd1, lnw, lnb, dres, dlnw, dlnb, dWq, dbq, Ysave, mean2,
-                                           rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO, delta, grads, R, job, dr, nq, st))
-    return;
+      ln_linear_post_attn_bwd_chain_launch(Gv, g_bf16, Wq, X, mean1, rstd1, lnw, lnb, dres, dlnw, dlnb, dWq, dbq, Ysave,
+                                           mean2, rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO, delta, grads, R, job, dr, nq,
+                                           st))
+    return true;
+  if (g_bf16) return false;
 #define LPB(CC, NQ)                                                                                               \
   if (av) hipLaunchKernelGGL((ln_linear_post_attn_bwd_kernel<CC, true, NQ>), grid, dim3(256), 0, st, G, Wq, X, mean1, \
                              rstd1, lnw, lnb, dres, dlnw, dlnb, dWq, dbq, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, \
@@ -1639,6 +1644,7 @@ void ln_linear_post_attn_bwd_launch(int C, const float* G, const uint16_t* Wq, c
   else if (nq == 3 * C) { LPB(32, 3); }
   else { LPB(32, 1); }
 #undef LPB
+  return true;
 }
 
 template <typename TG, typename TX, int NCH>

@@ -44,6 +44,9 @@ EPS = 1e-5
 # per-tile weight-gradient partials go to a slab reduced on a side stream (see _GradSlab);
 # PERCEIVER_WGRAD_SLAB=0 restores in-kernel float atomics into the replicated accumulators
 WGRAD_SLAB = os.environ.get("PERCEIVER_WGRAD_SLAB", "1") != "0"
+# self-attention dQKV stored as bf16 for the chain-layout boundary kernel (identical results);
+# PERCEIVER_BF16_DQKV=0 keeps it fp32 (A/B)
+BF16_DQKV = os.environ.get("PERCEIVER_BF16_DQKV", "1") != "0"
 TALL_ROWS = 1 << 17  # kTallRows in csrc/binding.cpp: taller projections stream their dW (wgrad kernel)
 
 
@@ -875,12 +878,19 @@ class _SABlockFn(torch.autograd.Function):
         # attention-backward accumulators the launcher would clear itself (several key blocks /
         # query splits adding up, e.g. 512 latents): cleared instead by the kernel before it
         zp = _zero_plan(K, B, H, N, N, D)
+        # dQKV of layers 1..L-1 feeds the chain-layout boundary kernel, which reads it as bf16
+        # MFMA operands only: the attention backward stores it as bf16 (half the bytes both
+        # ways, identical results) when it writes every element once (zp == 0: one key block)
+        g_bf16 = (BF16_DQKV and K is not emulation and zp == 0 and C == 64 and H == 4 and R % 64 == 0 and 64 < N <= 256
+                  and K.chain_enabled())
 
-        def new_dqkv():  # every column block is written (or accumulated onto a cleared buffer) by attn_bwd
+        def new_dqkv(i):  # every column block is written (or accumulated onto a cleared buffer) by attn_bwd
+            if g_bf16 and i > 0:
+                return torch.empty((B, N, 3 * C), device=dz.device, dtype=torch.bfloat16), {}
             t_ = torch.empty((B, N, 3 * C), **f32)
             return t_, (dict(zero_out=t_) if zp else {})
 
-        dqkv_next, zkw = new_dqkv()
+        dqkv_next, zkw = new_dqkv(L - 1)
         ho, _LOOKAHEAD["bwd_q"] = _LOOKAHEAD["bwd_q"], None
         if ho is not None and ho["key"] != getattr(ctx, "out_ptr", None):
             raise RuntimeError("fused encoder: a cross-attention layer handed its query-path backward to the wrong "
@@ -908,7 +918,7 @@ class _SABlockFn(torch.autograd.Function):
                        delta.view(B, N, H), H, D, scale, ctx.p, ctx.seed, dqkv[:, :, :C], dqkv[:, :, C:2 * C],
                        dqkv[:, :, 2 * C:], site=i, dq_zeroed=bool(zp & 1), kv_zeroed=bool(zp & 2))
             if i > 0:
-                dqkv_next, zkw = new_dqkv()
+                dqkv_next, zkw = new_dqkv(i - 1)
                 sl = _GradSlab(R, LL_SIZES(C) + PA_SIZES(C), dz2)
                 tg = sl.targets()
                 dy, do, delta = K.ln_linear_post_attn_bwd(dqkv.view(R, 3 * C), bws[i][0], xl, mean1, rstd1, P[i][0],

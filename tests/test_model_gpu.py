@@ -473,3 +473,33 @@ def test_lartpc_run_graph_engine(tmp_path):
               "--device", "cuda", "--workers", "0"])
     state = torch.load(ck / "model_0.ckpt", weights_only=True)
     assert all(torch.isfinite(v).all() for v in state["model_state_dict"].values() if v.is_floating_point())
+
+
+def test_bf16_dqkv_handoff_is_bitwise_neutral(monkeypatch):
+    """The self-attention backward stores dQKV as bf16 for the chain-layout boundary kernel
+    (``ops.fused.BF16_DQKV``): that kernel rounds a fp32 dQKV to the same bf16 values itself, so
+    the gradients are bitwise those of the fp32 hand-off (deterministic mode: no atomics)."""
+    from perceiver_io_amd import ops
+    from perceiver_io_amd.ops import fused
+
+    ops.set_deterministic(True)
+    try:
+        res = []
+        for flag in (True, False):
+            monkeypatch.setattr(fused, "BF16_DQKV", flag)
+            torch.manual_seed(5)
+            lit = _mlm(L=96, latents=128, sa=3)
+            m = lit.model
+            ids = torch.randint(3, 500, (8, 96), device="cuda")
+            pad = torch.zeros(8, 96, dtype=torch.bool, device="cuda")
+            pad[1, 50:] = True
+            with torch.no_grad():
+                xm, lab = m.masking(ids, pad, generator=torch.Generator(device="cuda").manual_seed(3))
+            m.loss(ids, pad, labels=lab, x_masked=xm).backward()
+            res.append(_grads(m))
+    finally:
+        ops.set_deterministic(False)
+    a, b = res
+    assert a.keys() == b.keys()
+    for n in a:
+        assert torch.equal(a[n], b[n]), n

@@ -115,7 +115,7 @@ int main(int argc, char** argv) {
                        pa + 2 * C * C + 3 * C, pa + 2 * C * C + 4 * C, pa + 3 * C * C + 4 * C, P, 1};
   pio::SlabJob job{};
   trace("ln_linear_post_attn_bwd_chain", R, [&]() {
-    pio::ln_linear_post_attn_bwd_launch(C, G, W[3], Z, m1, r1, vec[5], vec[6], dres, dg1, db1, dwq, dbq, Y, m2, r2, U, O,
+    pio::ln_linear_post_attn_bwd_launch(C, G, false, W[3], Z, m1, r1, vec[5], vec[6], dres, dg1, db1, dwq, dbq, Y, m2, r2, U, O,
                                         W[0], W[1], W[2], vec[3], vec[4], dY, dO, delta, H, g, R, job, dr, 3 * C, 0);
   });
   // the same launch carrying the previous boundary's slab reduction (what the step runs)
@@ -129,8 +129,14 @@ int main(int argc, char** argv) {
   { const int t = getenv("PIO_SLAB_WGS") ? atoi(getenv("PIO_SLAB_WGS")) : 128; int nsy = std::max(1, std::min(tiles, t / job2.nbx)); const int rb = (tiles + nsy - 1) / nsy; job2.nblk = job2.nbx * ((tiles + rb - 1) / rb); }
   job2.n = 1; job2.dst[0] = gdst; job2.off[0] = 0; job2.len[0] = P;
   trace("ln_linear_post_attn_bwd_chain + slab job", R, [&]() {
-    pio::ln_linear_post_attn_bwd_launch(C, G, W[3], Z, m1, r1, vec[5], vec[6], dres, dg1, db1, dwq, dbq, Y, m2, r2, U, O,
+    pio::ln_linear_post_attn_bwd_launch(C, G, false, W[3], Z, m1, r1, vec[5], vec[6], dres, dg1, db1, dwq, dbq, Y, m2, r2, U, O,
                                         W[0], W[1], W[2], vec[3], vec[4], dY, dO, delta, H, g, R, job2, dr, 3 * C, 0);
+  });
+  // G as bf16 (the attention backward's bf16 dQKV)
+  uint16_t* Gb = dev_fill<uint16_t>((size_t)R * 3 * C, 1.f, true);
+  trace("ln_linear_post_attn_bwd_chain bf16 G + slab job", R, [&]() {
+    pio::ln_linear_post_attn_bwd_launch(C, Gb, true, W[3], Z, m1, r1, vec[5], vec[6], dres, dg1, db1, dwq, dbq, Y, m2, r2,
+                                        U, O, W[0], W[1], W[2], vec[3], vec[4], dY, dO, delta, H, g, R, job2, dr, 3 * C, 0);
   });
   return 0;
 }
