@@ -32,6 +32,8 @@
 // no atomics on D unless the batch is split over several workgroups (small images).
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include <type_traits>
 
 #include "common.h"
@@ -260,6 +262,237 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_pe_kernel(PeFwdArgs a) {
   if (hh == 0) {
     a.MLpart[row * 2] = m_run;
     a.MLpart[row * 2 + 1] = l_tot;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Factored forward (default; PIO_PEF_FACT=0 restores the generating kernel above): the K/V
+// tiles are never formed.  With K/V row m of sample b written as (pe_kv_elem)
+//     y[m, o] = rσ_m·(P'[m, o] + Σ_c (p_c − μ)_m·wt[c][o] + μ_m·wt[4][o]) + wt[5][o],
+// the scores and the output of one head factor into products with the BATCH-INDEPENDENT P':
+//     S[q, m]  = rσ_m·(P'_K[m]·Q[q] + Σ_c (p_c − μ)_m·β_c[q] + μ_m·γ[q]) + cq[q]
+//                (β_c = Q·wt[c], γ = Q·wt[4], cq = Q·wt[5] over the head's K columns; cq is a
+//                per-query constant: softmax-invariant, added to the LSE only)
+//     O[q]·l   = Σ_m p̃·P'_V[m] + Σ_c A_c·wt_V[c] + A_μ·wt_V[4] + l·wt_V[5],   p̃ = p·rσ_m,
+//                A_c = Σ_m p̃·(p_c − μ)_m, A_μ = Σ_m p̃·μ_m, l = Σ_m p̃ / rσ_m.
+// So Sᵀ = [P'_K | p − μ | μ]·[Q | β | γ]ᵀ is one 32×32×(32 + 16) MFMA product whose 16-wide
+// augmentation carries the per-sample terms, rσ_m·scale and log2 rσ_m (→ p̃ straight out of
+// the exponential) are folded into the score's one FMA, and the P̃ᵀ product runs against the
+// shared P'_V tile plus a per-sample augmentation tile [p − μ | μ | 1/rσ] whose row NC + 1 is
+// the softmax denominator l.  Per key and sample: no K/V generation (≈400 VALU ops per key and
+// head in the generating kernel); per score element one FMA (scale, rσ and log2 rσ), the max
+// and the exponential; the accumulators are rescaled only when a lazy softmax offset moves.  The P' chunk (32 keys × the
+// head's 64 K|V columns) is staged ONCE per workgroup in LDS (one 16-byte load per thread,
+// double-buffered, one barrier per chunk) and serves 4·NS samples: wave w owns samples
+// 4·NS·bg + NS·w + [0, NS).
+// ------------------------------------------------------------------------------------
+template <int NC, int NS>
+__global__ __launch_bounds__(256, 2) void attn_fwd_pe_fact_kernel(PeFwdArgs a) {
+  constexpr int LDT = PD + 8;       // augmentation tile row stride (bf16)
+  constexpr int LKV = 2 * PD + 8;   // P' chunk row stride: K columns [0, 32), V columns [32, 64)
+  static_assert(NC + 2 <= 8, "augmentation rows live in accumulator registers 0..3 of both halves");
+  __shared__ __attribute__((aligned(16))) uint16_t sKV[2][32 * LKV];
+  __shared__ __attribute__((aligned(16))) uint16_t sA[4][NS][32 * LDT];  // [key][aug row], rows ≥ NC + 2 zero
+  __shared__ __attribute__((aligned(16))) float sCL[4][NS][2][32];       // [key]: rσ·scale_log2, log2 rσ
+  __shared__ __attribute__((aligned(16))) float sWt[PE_NWT][64];         // head h's table: K | V columns
+  const int w = wave_id(), l = lane_id(), r = l & 31, hh = l >> 5;
+  const Blk3 blk = xcd_block3();  // x: batch group (fastest), y: split, z: head
+  const int split = blk.y, h = blk.z;
+  const int C = a.C, M = a.M;
+  for (int t = threadIdx.x; t < 64 * PE_NWT; t += 256) {
+    const int j = t >> 6, c = t & 63;
+    sWt[j][c] = a.wt[(long long)j * 2 * C + (c < PD ? h * PD + c : C + h * PD + c - PD)];
+  }
+  for (int t = threadIdx.x; t < 4 * NS * 32 * LDT / 8; t += 256)
+    reinterpret_cast<bf16x8*>(&sA[0][0][0])[t] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  const int kbeg = split * a.chunks * 32;
+  const int kend = min(M, kbeg + a.chunks * 32);
+  const int bw0 = (blk.x * 4 + w) * NS;  // this wave's first sample (waves past B idle but keep barriers)
+  __syncthreads();
+
+  // queries (lane = query, clamped) and their augmentation β / γ / cq per sample
+  const int qi = r, qc = min(qi, a.Nq - 1);
+  bf16x8 qa[NS][3];
+  float cq[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int b = min(bw0 + s, a.B - 1);
+    const uint16_t* qp = a.q + (long long)b * a.q_bs + (long long)qc * a.q_rs + h * PD + 8 * hh;
+    qa[s][0] = *reinterpret_cast<const bf16x8*>(qp);
+    qa[s][1] = *reinterpret_cast<const bf16x8*>(qp + 16);
+    float part[NC + 2];
+#pragma unroll
+    for (int j = 0; j < NC + 2; ++j) part[j] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float qv = bf2f(qa[s][t][e]);
+        const int d = 16 * t + 8 * hh + e;
+#pragma unroll
+        for (int j = 0; j < NC + 2; ++j) part[j] = fmaf(qv, sWt[j < NC ? j : j + 4 - NC][d], part[j]);
+      }
+    bf16x8 au = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < NC + 2; ++j) part[j] = xor32_sum(part[j]);
+#pragma unroll
+    for (int j = 0; j < NC + 1; ++j) au[j] = (short)f2bf(part[j]);  // β_0..β_{NC-1}, γ
+    qa[s][2] = hh == 0 ? au : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    cq[s] = part[NC + 1];
+  }
+
+  // per-chunk staging registers: one 16-byte piece of the P' chunk per thread (row tid >> 3,
+  // columns 8·(tid & 7): K for < 32), the lane's key statistics inputs per sample
+  const int srow = threadIdx.x >> 3, scol = 8 * (threadIdx.x & 7);
+  const long long prs = 2LL * C;
+  const uint16_t* pp = a.P + (long long)(min(kbeg, M) + srow) * prs + (scol < PD ? h * PD + scol : C + h * PD + scol - PD);
+  bf16x8 pst;
+  float spe = 0.f, spq = 0.f, spx[NS][NC];
+  auto fetch = [&](int k0) {  // loads only (rows past M are the zero pad rows of P')
+    pst = *reinterpret_cast<const bf16x8*>(pp);
+    pp += 32 * prs;
+    const int key = min(k0 + r, M - 1);
+    spe = a.pes[key];
+    spq = a.pesq[key];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int b = min(bw0 + s, a.B - 1);
+      const float* px = a.pix + ((long long)b * M + key) * NC;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) spx[s][c] = px[c];
+    }
+  };
+
+  f32x16 om[NS], oa[NS];
+  float m_run[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    om[s] = f32x16{};
+    oa[s] = f32x16{};
+    m_run[s] = -1e30f;
+  }
+  const float sl2 = a.scale_log2;
+  const int nch = kend > kbeg ? (kend - kbeg + 31) / 32 : 0;  // an empty split (kbeg ≥ M) has none
+  auto chunk = [&](int ci, auto masked_t) {
+    constexpr bool masked = decltype(masked_t)::value;
+    const int k0 = kbeg + 32 * ci;
+    uint16_t* kv = sKV[ci & 1];
+    *reinterpret_cast<bf16x8*>(kv + srow * LKV + scol) = pst;
+    bf16x8 ka[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {  // key k0 + r of sample s: statistics → tables + A augmentation
+      float sm = spe, sq = spq;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        sm += spx[s][c];
+        sq = fmaf(spx[s][c], spx[s][c], sq);
+      }
+      const float mu = sm * a.inv_k;
+      const float var = fmaxf(sq * a.inv_k - mu * mu, 0.f) + a.eps;
+      const float rs = rsqrtf(var);
+      bf16x8 au = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int c = 0; c < NC; ++c) au[c] = (short)f2bf(spx[s][c] - mu);
+      au[NC] = (short)f2bf(mu);
+      if (hh == 0) {
+        sCL[w][s][0][r] = rs * sl2;
+        sCL[w][s][1][r] = -0.5f * __log2f(var);  // log2 rσ
+        bf16x8 vrow = au;
+        vrow[NC + 1] = (short)f2bf(var * rs);    // 1/rσ: row NC + 1 of P̃ᵀ·A = the denominator l
+        *reinterpret_cast<bf16x8*>(&sA[w][s][r * LDT]) = vrow;
+      }
+      ka[s] = hh == 0 ? au : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+    __syncthreads();  // the chunk and the tables are in LDS; buffer (ci + 1) & 1 is free
+    if (ci + 1 < nch) fetch(k0 + 32);
+    if (bw0 >= a.B) return;
+    const bf16x8 pk0 = frag_kc(kv, LKV, 0, 0), pk1 = frag_kc(kv, LKV, 0, 16);
+    f32x16 sc[NS];  // every sample's scores first: their MFMAs overlap the softmax VALU below
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      sc[s] = mfma32(pk0, qa[s][0], f32x16{});
+      sc[s] = mfma32(pk1, qa[s][1], sc[s]);
+      sc[s] = mfma32(ka[s], qa[s][2], sc[s]);
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      float mt = -INFINITY;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {  // keys 8g + 4hh + (0..3) of the chunk: registers 4g..4g+3
+        const float4 cf = *reinterpret_cast<const float4*>(&sCL[w][s][0][8 * g + 4 * hh]);
+        const float4 lf = *reinterpret_cast<const float4*>(&sCL[w][s][1][8 * g + 4 * hh]);
+        const float cv[4] = {cf.x, cf.y, cf.z, cf.w}, lv[4] = {lf.x, lf.y, lf.z, lf.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * g + e;
+          float t = fmaf(sc[s][i], cv[e], lv[e]);
+          if constexpr (masked) t = k0 + acc_row(i, hh) < kend ? t : -INFINITY;
+          sc[s][i] = t;
+          mt = fmaxf(mt, t);
+        }
+      }
+      mt = xor32_max(mt);
+      // lazy offset: moved only when a score exceeds it by more than 2^8 (p̃ ≤ 2^8 is exact in fp32
+      // and in range for bf16), so the accumulators are rescaled on a handful of chunks, not on
+      // nearly every one (a new maximum among 32 queries is the rule for the first ~50 chunks)
+      const float m_new = mt > m_run[s] + 8.f ? mt : m_run[s];
+      const float alpha = fast_exp2(m_run[s] - m_new);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sc[s][i] = fast_exp2(sc[s][i] - m_new);
+      if (__ballot(m_new != m_run[s])) {  // some query's offset moved: rescale
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          om[s][i] *= alpha;
+          oa[s][i] *= alpha;
+        }
+      }
+      m_run[s] = m_new;
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const bf16x8 pb = pack_acc(sc[s], ss);
+        om[s] = mfma32(frag_ks_perm(kv + PD, LKV, 0, 16 * ss), pb, om[s]);
+        oa[s] = mfma32(frag_ks_perm(&sA[w][s][0], LDT, 0, 16 * ss), pb, oa[s]);
+      }
+    }
+  };
+  if (nch > 0) fetch(kbeg);
+  const int nfull = kend > kbeg ? (kend - kbeg) / 32 : 0;
+  for (int ci = 0; ci < nfull; ++ci) chunk(ci, std::false_type{});
+  if (nfull < nch) chunk(nfull, std::true_type{});  // the last chunk of a split ending mid-chunk
+  if (bw0 >= a.B) return;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int b = bw0 + s;
+    if (b >= a.B) break;
+    // augmentation rows R < 8 of query r: R < 4 in registers R of the lower half, 4..7 in the upper
+    float aug[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float own = oa[s][i], oth = __shfl_xor(own, 32);
+      aug[hh == 0 ? i : i + 4] = own;
+      aug[hh == 0 ? i + 4 : i] = oth;
+    }
+    const float lsum = aug[NC + 1];
+    if (qi >= a.Nq) continue;
+    const long long row = (((long long)split * a.B + b) * a.Nq + qi) * a.H + h;
+    float* op = a.Opart + row * PD;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float ov[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = 4 * g + e, d = PD + acc_row(i, hh);  // V column of the head
+        float y = fmaf(aug[NC], sWt[4][d], fmaf(lsum, sWt[5][d], om[s][i]));
+#pragma unroll
+        for (int c = 0; c < NC; ++c) y = fmaf(aug[c], sWt[c][d], y);
+        ov[e] = y;
+      }
+      *reinterpret_cast<float4*>(op + 8 * g + 4 * hh) = make_float4(ov[0], ov[1], ov[2], ov[3]);
+    }
+    if (hh == 0) {
+      a.MLpart[row * 2] = m_run[s] + cq[s] * sl2;
+      a.MLpart[row * 2 + 1] = lsum;
+    }
   }
 }
 
@@ -699,17 +932,61 @@ int attn_fwd_pe_occupancy() {
   return (v && v[0] == '3') ? 3 : 4;
 }
 
-// splits × 32-key chunks covering M keys; grid (batch quads, splits, heads), 4 waves each
+// the factored forward (default) unless PIO_PEF_FACT=0; PIO_PEF_NS: samples per wave (2 | 3;
+// 4 spills at 2 waves / SIMD)
+static bool pef_fact() {
+  static const bool on = [] {
+    const char* v = getenv("PIO_PEF_FACT");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+static int pef_ns() {
+  static const int ns = [] {
+    const char* v = getenv("PIO_PEF_NS");
+    const int n = v ? atoi(v) : 2;
+    return n == 3 ? 3 : 2;
+  }();
+  return ns;
+}
+
+// key splits of one launch: about one round of workgroups at the kernel's occupancy
+// (PIO_PEF_WGS overrides the workgroup target of the factored kernel, for sweeps)
+int attn_fwd_pe_auto_splits(int B, int H, int ncu) {
+  if (pef_fact()) {
+    const char* v = getenv("PIO_PEF_WGS");
+    const int target = (v && atoi(v) > 0) ? atoi(v) : 2 * ncu;
+    const int bg = (B + 4 * pef_ns() - 1) / (4 * pef_ns());
+    return std::max(1, target / (bg * H));
+  }
+  return std::max(1, attn_fwd_pe_occupancy() * 4 * ncu / (4 * ((B + 3) / 4) * H));
+}
+
+// splits × 32-key chunks covering M keys; grid (batch groups, splits, heads), 4 waves each
 void attn_fwd_pe_launch(const PeFwdArgs& a0, hipStream_t st) {
   PeFwdArgs a = a0;
   const int nch = (a.M + 31) / 32;
   a.chunks = (nch + a.nsplit - 1) / a.nsplit;
+  if (pef_fact()) {
+    const int ns = pef_ns();
+    const dim3 grid((unsigned)((a.B + 4 * ns - 1) / (4 * ns)), (unsigned)a.nsplit, (unsigned)a.H);
+#define PIO_PEFF(NC_, NS_) hipLaunchKernelGGL((attn_fwd_pe_fact_kernel<NC_, NS_>), grid, dim3(256), 0, st, a)
+#define PIO_PEFF_NC(NC_)         \
+  if (ns == 3) PIO_PEFF(NC_, 3); \
+  else PIO_PEFF(NC_, 2);
+    switch (a.nc) {
+      case 1: PIO_PEFF_NC(1) break;
+      case 2: PIO_PEFF_NC(2) break;
+      case 3: PIO_PEFF_NC(3) break;
+      default: PIO_PEFF_NC(4) break;
+    }
+#undef PIO_PEFF_NC
+#undef PIO_PEFF
+    return;
+  }
   const dim3 grid((unsigned)((a.B + 3) / 4), (unsigned)a.nsplit, (unsigned)a.H);
   // occupancy variant: 4 waves / SIMD (≤ 128 VGPRs) unless PIO_PEF_OCC=3
-  static const int occ = [] {
-    const char* v = getenv("PIO_PEF_OCC");
-    return (v && v[0] == '3') ? 3 : 4;
-  }();
+  static const int occ = attn_fwd_pe_occupancy();
 #define PIO_PEF(NC_)                                                                                   \
   if (occ == 3) hipLaunchKernelGGL((attn_fwd_pe_kernel<NC_, 3>), grid, dim3(256), 0, st, a);           \
   else hipLaunchKernelGGL((attn_fwd_pe_kernel<NC_, 4>), grid, dim3(256), 0, st, a);

@@ -600,6 +600,22 @@ def _pe_implicit_operands(M, H, nc, kin=133):
     return P, E.sum(1).contiguous(), (E * E).sum(1).contiguous(), wt, kin
 
 
+def _pe_fwd_fp32(q, P, pix, pes, pesq, wt, H, scale, kin, eps):
+    """fp32 reference of the implicit-K/V cross-attention: K/V rows (pe_kv_elem) in fp32 from the
+    bf16 P', softmax attention in fp32 → O (B, Nq, C), LSE (B, Nq, H) in log2 units."""
+    C, M = H * 32, pes.shape[0]
+    B, nc = pix.shape[0] // M, pix.shape[1]
+    m = torch.arange(B * M, device=pix.device) % M
+    mu = (pes[m] + pix.sum(1)) / kin
+    rs = torch.rsqrt(((pesq[m] + (pix * pix).sum(1)) / kin - mu * mu).clamp(min=0) + eps)
+    y = rs[:, None] * (P[m].float() + (pix - mu[:, None]) @ wt[:nc] + mu[:, None] * wt[4]) + wt[5]
+    kv = y.view(B, M, 2, H, 32)
+    qf = q.float().expand(B, -1, -1).reshape(B, -1, H, 32)
+    s = torch.einsum("bqhd,bmhd->bhqm", qf, kv[:, :, 0]) * scale
+    o = torch.einsum("bhqm,bmhd->bqhd", torch.softmax(s, -1), kv[:, :, 1]).reshape(B, -1, C)
+    return o, (torch.logsumexp(s, -1) / math.log(2)).permute(0, 2, 1).contiguous()
+
+
 @pytest.mark.parametrize("B,Bq,Nq,M,H,nc,bsplit,nsplit", [
     (3, 1, 32, 600, 4, 3, 1, 7),
     (4, 1, 17, 300, 4, 1, 2, 3),
@@ -627,7 +643,14 @@ def test_attention_pe_implicit_kv(B, Bq, Nq, M, H, nc, bsplit, nsplit):
     o1, l1 = _ext().attn_fwd_pe(q, P, pix, pes, pesq, wt, H, scale, kin, eps, nsplit)
     o2, l2 = _emu().attn_fwd_pe(q, P, pix, pes, pesq, wt, H, scale, kin, eps, 1)
     close(o1, o2, 1e-2, "O")
-    close(l1, l2, 1e-4, "LSE")
+    # the factored forward (default) never forms the bf16 K/V the emulation rounds: judge both
+    # against the fp32 reference (K/V in fp32 from the same bf16 P'), the kernel's LSE error at
+    # most that of the emulation's (bf16 K/V) path plus 1e-4 of the LSE scale
+    o3, l3 = _pe_fwd_fp32(q, P, pix, pes, pesq, wt, H, scale, kin, eps)
+    e_kernel = (l1.float() - l3).abs().max().item()
+    e_emu = (l2.float() - l3).abs().max().item()
+    assert e_kernel <= 1.25 * e_emu + 1e-4 * l3.abs().max().item(), ("LSE", e_kernel, e_emu)
+    close(o1, o3, 1e-2, "O vs fp32")
     delta = (dO.float().view(B, Nq, H, 32) * o2.float().view(B, Nq, H, 32)).sum(-1).contiguous()
     nkb = (M + 255) // 256
     res = []

@@ -52,8 +52,6 @@ for step in "$@"; do
     prof)     run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 3 ;;
     lartpc)   run lartpc 600 python run.py --epochs 1 --events 8 --val-events 4 --size 512 --batch-size 4 --max-steps 2 --log-dir /tmp/lartpc_runs --ckpt-dir /tmp/lartpc_ckpt ;;
     lartpc_test) run lartpc_test 300 python -u -m pytest tests/test_components.py -m gpu -x -v --timeout 240 --timeout-method thread -p no:cacheprovider ;;
-    dbg0)     run dbg0 300 env AMD_SERIALIZE_KERNEL=3 python tools/debug_engine.py 0 ;;
-    dbg1)     run dbg1 300 python tools/debug_engine.py 1 ;;
     *) echo "unknown step $step" ;;
   esac
 done
