@@ -270,6 +270,19 @@ def main(argv=None):
     sched = None if lar else torch.optim.lr_scheduler.OneCycleLR(opt, max_lr=lr, total_steps=50000, pct_start=0.1,
                                                                  cycle_momentum=False)
     reducer = None
+    # PERCEIVER_BENCH_FORCE_REDUCER=1 (one GPU, diagnostics): a 1-rank RCCL group with the reducer
+    # forced on and its collectives captured in the step graph — the in-graph all-reduce / fork
+    # overhead of the multi-GPU path, measured without the transfers
+    force_red = world == 1 and cuda and fused and os.environ.get("PERCEIVER_BENCH_FORCE_REDUCER", "0") == "1"
+    if force_red:
+        import torch.distributed as tdist
+
+        if not tdist.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29517")
+            tdist.init_process_group("nccl", rank=0, world_size=1, device_id=device)
+        reducer = FlatGradReducer(opt.flat, in_graph=True, force=True)
+        reducer.plan(model)
     if world > 1:
         from perceiver_io_amd.ops.optim import FlatParameterSpace
 

@@ -288,21 +288,47 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(AttnArgs a, uint16_t
   }
 }
 
-// combine split-KV partials: one thread per (b, q, h, d)
+// combine split-KV partials: one thread per (b, q, h, d).  One online pass over the splits, four
+// at a time with their twelve loads independent (a two-pass loop of dependent loads is latency
+// bound: 21 µs for 32 splits at the ImageNet encoder shape)
 __global__ void attn_combine_kernel(const float* __restrict__ Opart, const float* __restrict__ MLpart,
                                     uint16_t* __restrict__ O, float* __restrict__ LSE, int nsplit, int rows, int D) {
   const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (long long)rows * D) return;
   const long long row = idx / D;
   const int d = idx % D;
-  float M = -1e30f;
-  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, MLpart[((long long)s * rows + row) * 2]);
-  float L = 0.f, acc = 0.f;
-  for (int s = 0; s < nsplit; ++s) {
-    const float m = MLpart[((long long)s * rows + row) * 2];
-    const float w = exp2f(m - M);
-    L += MLpart[((long long)s * rows + row) * 2 + 1] * w;
-    acc += Opart[((long long)s * rows + row) * D + d] * w;
+  const long long sstride = (long long)rows;
+  float M = -1e30f, L = 0.f, acc = 0.f;
+  int s = 0;
+  for (; s + 4 <= nsplit; s += 4) {
+    float m[4], l[4], o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long long r = (s + j) * sstride + row;
+      m[j] = MLpart[r * 2];
+      l[j] = MLpart[r * 2 + 1];
+      o[j] = Opart[r * D + d];
+    }
+    const float mx = fmaxf(fmaxf(M, fmaxf(m[0], m[1])), fmaxf(m[2], m[3]));
+    const float sc = exp2f(M - mx);
+    L *= sc;
+    acc *= sc;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float w = exp2f(m[j] - mx);
+      L = fmaf(l[j], w, L);
+      acc = fmaf(o[j], w, acc);
+    }
+    M = mx;
+  }
+  for (; s < nsplit; ++s) {
+    const long long r = s * sstride + row;
+    const float m = MLpart[r * 2];
+    const float mx = fmaxf(M, m);
+    const float sc = exp2f(M - mx), w = exp2f(m - mx);
+    L = fmaf(MLpart[r * 2 + 1], w, L * sc);
+    acc = fmaf(Opart[r * D + d], w, acc * sc);
+    M = mx;
   }
   O[row * D + d] = f2bf(L > 0.f ? acc / L : 0.f);  // rows ordered (b, q, h) → O[(b*Nq+q)*HD + h*D + d]
   if (d == 0) LSE[row] = L > 0.f ? M + __log2f(L) : INFINITY;

@@ -120,7 +120,7 @@ def graph_collectives_ok(device) -> bool:
 
 def barrier():
     if dist.is_available() and dist.is_initialized():
-        if _INFO.backend == "nccl":
+        if dist.get_backend() == "nccl":
             dist.barrier(device_ids=[torch.cuda.current_device()])
         else:
             dist.barrier()
@@ -129,7 +129,7 @@ def barrier():
 def all_reduce_max(x: float) -> float:
     if not (dist.is_available() and dist.is_initialized()):
         return x
-    dev = "cuda" if _INFO.backend == "nccl" else "cpu"
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
     t = torch.tensor([x], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
@@ -138,7 +138,7 @@ def all_reduce_max(x: float) -> float:
 def all_reduce_mean(x: float) -> float:
     if not (dist.is_available() and dist.is_initialized()):
         return x
-    dev = "cuda" if _INFO.backend == "nccl" else "cpu"
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
     t = torch.tensor([x], dtype=torch.float64, device=dev)
     dist.all_reduce(t)
     return float(t.item()) / _INFO.world_size

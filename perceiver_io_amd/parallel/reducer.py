@@ -35,6 +35,7 @@ into the graph (``in_graph``: RCCL capturable on this node, probed once by
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Iterable, List, Optional, Tuple
 
 import torch
@@ -80,7 +81,7 @@ def _capturing(device) -> bool:
 
 
 class FlatGradReducer:
-    def __init__(self, flat, bucket_bytes: int = 4 << 20, overlap: bool = True, in_graph: Optional[bool] = None,
+    def __init__(self, flat, bucket_bytes: int = 4 << 20, overlap: Optional[bool] = None, in_graph: Optional[bool] = None,
                  wire_dtype: Optional[torch.dtype] = None, force: bool = False):
         self.flat = flat
         self.world = dist.get_world_size() if (dist.is_available() and dist.is_initialized()) else 1
@@ -92,6 +93,9 @@ class FlatGradReducer:
         self._point_modules: Dict[str, int] = {}  # ready point → id() of the module it was planned on
         # overlap needs every parameter gradient to land in flat.grad directly (no 8-way replicas
         # that a later fold() would still add into an early bucket's range)
+        # overlap=None: on unless PERCEIVER_DDP_OVERLAP=0 (collectives inline on the compute stream)
+        if overlap is None:
+            overlap = os.environ.get("PERCEIVER_DDP_OVERLAP", "1") != "0"
         self.overlap = bool(overlap) and getattr(flat, "grad_rep", None) is None
         self.wire_dtype = wire_dtype
         self.on_gpu = flat.device.type == "cuda"
