@@ -239,6 +239,11 @@ def main(argv=None):
     args = parse(argv)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(_spawn_self(args, argv))
+    # stdout carries exactly one JSON line: everything else written to fd 1 while the run is set
+    # up and timed (RCCL's version banner, library notices) goes to stderr
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     import torch
 
     from perceiver_io_amd import ops
@@ -377,6 +382,8 @@ def main(argv=None):
             "dist_backend": info.backend if world > 1 else None,
             "params_in_sync": sync_diff == 0.0, "params_max_abs_diff": sync_diff,
         }
+        sys.stdout.flush()
+        os.dup2(json_fd, 1)
         print(json.dumps(out), flush=True)
     if reducer is not None:
         reducer.close()

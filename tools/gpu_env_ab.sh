@@ -16,6 +16,6 @@ for e in "$@"; do
   [ "$e" = "-" ] && e="PIO_NOTHING=1"
   for i in 1 2; do
     env $e timeout -k 10 200 python bench.py --config $cfg --steps 30 --warmup 5 > gpurun_out/ab/b.json 2> gpurun_out/ab/b.err || { echo bench failed; tail gpurun_out/ab/b.err; exit 4; }
-    python -c "import json; d=json.load(open('gpurun_out/ab/b.json')); print('$e', '$cfg', d['ms_per_step'], d['value'])"
+    python -c "import json; d=json.loads(open('gpurun_out/ab/b.json').read().strip().splitlines()[-1]); print('$e', '$cfg', d['ms_per_step'], d['value'])"
   done
 done
