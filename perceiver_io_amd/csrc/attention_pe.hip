@@ -535,6 +535,10 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
   // sums to partial row nkb + g.
   const int nkb = (a.M + KB - 1) / KB;
   long long it = 0, it_end = 0;
+  if (a.nbg > 0 && !a.accumulate) {  // this workgroup's slot row of the partials, before any run writes it
+    float* prow0 = a.part + (long long)(nkb + blockIdx.x) * ((2 + nc) * O);
+    for (int e = threadIdx.x; e < (2 + nc) * O; e += NTH) prow0[e] = 0.f;
+  }
   if (a.nbg > 0) {
     const long long T = (long long)nkb * a.H * a.nbg;
     it = T * blockIdx.x / gridDim.x;

@@ -1184,7 +1184,7 @@ int64_t attn_bwd_pe_part_rows(int64_t M, int64_t H, int64_t B, int64_t bsplit) {
 
 static void attn_bwd_pe_impl(Tensor q, const Tensor* kv, Tensor dO, Tensor lse, Tensor delta, const Tensor* mean,
                              const Tensor* rstd, Tensor pix, Tensor dq, Tensor D, Tensor part, int64_t H, double scale,
-                             bool accumulate, int64_t bsplit, const PeImplicit* impl) {
+                             bool accumulate, int64_t bsplit, const PeImplicit* impl, bool dq_zeroed = false) {
   for (const Tensor* t : {&q, &dO, &lse, &delta, &pix, &dq, &D, &part}) CHECK_CUDA(*t);
   const int C = (int)(H * 32);
   TORCH_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.size(2) >= C, "q must be (B|1, Nq, >= C) with unit inner stride");
@@ -1240,7 +1240,7 @@ static void attn_bwd_pe_impl(Tensor q, const Tensor* kv, Tensor dO, Tensor lse, 
   TORCH_CHECK(!(g_det && bsplit > 1), "deterministic mode: attn_bwd_pe needs bsplit = 1");
   Tensor dq_part;
   if (g_det) dq_part = torch::empty({nkb, dq.numel()}, dq.options());
-  else dq.zero_();
+  else if (!dq_zeroed) dq.zero_();  // dq_zeroed: cleared by the preceding kernel's zero span
   pio::PeBwdArgs a{};
   a.q = bfp(q); a.q_bs = qb ? q.stride(0) : 0; a.q_rs = (int)q.stride(1);
   if (impl) {
@@ -1262,7 +1262,7 @@ static void attn_bwd_pe_impl(Tensor q, const Tensor* kv, Tensor dO, Tensor lse, 
     dside = torch::empty({slots, 256, 64}, D.options());
     spair = torch::empty({slots}, D.options().dtype(torch::kInt32));
     a.nbg = 4; a.nslots = slots; a.Dside = dside.data_ptr<float>(); a.side_pair = spair.data_ptr<int>();
-    if (!accumulate) part.narrow(0, nkb, slots).zero_();  // a slot row only gets its head's columns
+    // slot rows (a side run writes only its head's columns) are cleared by the kernel itself
   }
   pio::attn_bwd_pe_launch(a, nkb, (int)bsplit, stream());
   if (g_det) dq.view({-1}).copy_(dq_part.sum(0));
@@ -1276,9 +1276,10 @@ void attn_bwd_pe(Tensor q, Tensor kv, Tensor dO, Tensor lse, Tensor delta, Tenso
 // the same over implicit K/V (attention_pe.hip pe_kv_elem): no (B·M, 2C) K/V tensor, no row statistics
 void attn_bwd_pe_implicit(Tensor q, Tensor P, Tensor pes, Tensor pesq, Tensor wt, Tensor dO, Tensor lse, Tensor delta,
                           Tensor pix, Tensor dq, Tensor D, Tensor part, int64_t H, double scale, int64_t kin, double eps,
-                          bool accumulate, int64_t bsplit) {
+                          bool accumulate, int64_t bsplit, bool dq_zeroed) {
   PeImplicit im{P, pes, pesq, wt, (double)kin, eps};
-  attn_bwd_pe_impl(q, nullptr, dO, lse, delta, nullptr, nullptr, pix, dq, D, part, H, scale, accumulate, bsplit, &im);
+  attn_bwd_pe_impl(q, nullptr, dO, lse, delta, nullptr, nullptr, pix, dq, D, part, H, scale, accumulate, bsplit, &im,
+                   dq_zeroed);
 }
 
 // encoder cross-attention forward over implicit K/V (attention_pe.hip attn_fwd_pe_kernel): queries
@@ -1415,7 +1416,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pe_gemm", &pe_gemm, py::arg("A"), py::arg("B"), py::arg("bf16_out") = false, py::arg("pad_rows") = 0);
   m.def("attn_fwd_pe", &attn_fwd_pe);
   m.def("attn_bwd_pe_part_rows", &attn_bwd_pe_part_rows);
-  m.def("attn_bwd_pe_implicit", &attn_bwd_pe_implicit);
+  m.def("attn_bwd_pe_implicit", &attn_bwd_pe_implicit, py::arg("q"), py::arg("P"), py::arg("pes"), py::arg("pesq"),
+        py::arg("wt"), py::arg("dO"), py::arg("lse"), py::arg("delta"), py::arg("pix"), py::arg("dq"), py::arg("D"),
+        py::arg("part"), py::arg("H"), py::arg("scale"), py::arg("kin"), py::arg("eps"), py::arg("accumulate"),
+        py::arg("bsplit"), py::arg("dq_zeroed") = false);
   m.def("pe_weight_prep", &pe_weight_prep);
   m.def("pe_grads", &pe_grads);
   m.def("pe_proj_bwd", &pe_proj_bwd);

@@ -188,7 +188,8 @@ def attn_fwd_pe(q, P, pix, pes, pesq, wt, H, scale, kin, eps, nsplit):
     return attn_fwd(q, kv[:, :, :C], kv[:, :, C:], None, H, 32, scale, 0.0, None, nsplit)
 
 
-def attn_bwd_pe_implicit(q, P, pes, pesq, wt, dO, lse, delta, pix, dq, D, part, H, scale, kin, eps, accumulate, bsplit):
+def attn_bwd_pe_implicit(q, P, pes, pesq, wt, dO, lse, delta, pix, dq, D, part, H, scale, kin, eps, accumulate, bsplit,
+                         dq_zeroed=False):
     """attn_bwd_pe over implicit K/V (the same generation as attn_fwd_pe)."""
     kv, mu, rs = pe_kv(P, pix, pes, pesq, wt, kin, eps)
     attn_bwd_pe(q, kv, dO, lse, delta, mu, rs, pix, dq, D, part, H, scale, accumulate, bsplit)

@@ -578,8 +578,11 @@ class _LayerFn(torch.autograd.Function):
         pe_fused = spec.cross and bool(ctx.kv_entry.get("factored") and PE_ATTN_FUSED and D == 32 and Nq <= 32
                                        and kmask is None and ctx.p_attn == 0.0 and xkv2.shape[1] <= 4)
         dq_pre = None
-        if spec.cross and not pe_fused and not deterministic():
-            dq_pre = torch.empty((B, Nq, C), **f32)
+        if spec.cross and not deterministic():
+            # the attention backward's atomically accumulated dQ, cleared by the post-attention
+            # backward on the way (no fill launch); broadcast latent queries on the fused PE path
+            # come back summed over the batch
+            dq_pre = torch.empty((Bq if pe_fused else B, Nq, C), **f32)
             drop["zero_out"] = dq_pre
         ho, _LOOKAHEAD["bwd"] = _LOOKAHEAD["bwd"], None
         if ho is not None and ho["key"] != getattr(ctx, "lookahead_z", None):
@@ -621,11 +624,12 @@ class _LayerFn(torch.autograd.Function):
                     ent["pe_part"] = torch.empty((prows, (2 + xkv2.shape[1]) * 2 * C), **f32)
                     ent["pe_bsplit"] = bs
                 # broadcast latent queries (layer_1): dq comes back summed over the batch
-                dq = torch.empty((Bq, Nq, C), **f32)
+                dq = dq_pre if dq_pre is not None else torch.empty((Bq, Nq, C), **f32)
                 if imp is not None:
                     P, pes, pesq, wt, kin = imp
                     K.attn_bwd_pe_implicit(qx, P, pes, pesq, wt, do.view(B, Nq, C), lse, delta3, xkv2, dq, ent["pe_D"],
-                                           ent["pe_part"], H, scale, kin, EPS, acc, ent["pe_bsplit"])
+                                           ent["pe_part"], H, scale, kin, EPS, acc, ent["pe_bsplit"],
+                                           dq_zeroed=dq_pre is not None)
                 else:
                     K.attn_bwd_pe(qx, kv, do.view(B, Nq, C), lse, delta3, mean_kv, rstd_kv, xkv2, dq, ent["pe_D"],
                                   ent["pe_part"], H, scale, acc, ent["pe_bsplit"])
