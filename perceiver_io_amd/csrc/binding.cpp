@@ -108,7 +108,7 @@ int stage_step_launch(void* const*, const void* const*, const long long*, int, f
 void sumsq_launch(const float*, long long, float*, hipStream_t);
 void index_add_rows_launch(float*, long long, const int64_t*, const float*, long long, int, hipStream_t);
 void batch_sum2_launch(const float*, const float*, float*, float*, int, long long, hipStream_t);
-void pe_gemm_launch(const uint16_t*, const uint16_t*, void*, bool, int, int, int, hipStream_t);
+void pe_gemm_launch(const uint16_t*, const uint16_t*, void*, bool, int, int, int, int, hipStream_t);
 struct PeGradTargets { float *dWa, *dWb, *db, *dg, *dbeta; };
 int pe_grad_splits(int);
 void pe_grads_launch(const uint16_t*, const float*, int, int, int, const float*, int, float*, float*, float*,
@@ -1072,8 +1072,8 @@ Tensor pe_gemm(Tensor A, Tensor B, bool bf16_out, int64_t pad_rows) {
               "pe_gemm: 16-byte aligned operands");
   TORCH_CHECK(pad_rows >= 0, "pe_gemm: pad_rows >= 0");
   Tensor C = torch::empty({M + pad_rows, N}, A.options().dtype(bf16_out ? torch::kBFloat16 : torch::kFloat32));
-  if (pad_rows > 0) C.narrow(0, M, pad_rows).zero_();  // zero rows past M (read by prefetches, never used)
-  if (M > 0) pio::pe_gemm_launch(bfp(A), bfp(B), C.data_ptr(), bf16_out, M, N, K, stream());
+  // the zero rows past M (read by prefetches, never used) are written by the GEMM launch itself
+  if (M + pad_rows > 0) pio::pe_gemm_launch(bfp(A), bfp(B), C.data_ptr(), bf16_out, M, N, K, (int)(M + pad_rows), stream());
   return C;
 }
 

@@ -189,7 +189,7 @@ constexpr int GT = 128, GKC = 32, GLD = GKC + 8;
 
 template <bool BF16OUT>
 __global__ __launch_bounds__(256) void pe_gemm_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bw,
-                                                      void* __restrict__ Cv, int M, int N, int K) {
+                                                      void* __restrict__ Cv, int M, int N, int K, int Mst) {
   __shared__ __attribute__((aligned(16))) uint16_t sA[2][GT * GLD];
   __shared__ __attribute__((aligned(16))) uint16_t sB[2][GT * GLD];
   const int w = wave_id(), l = lane_id(), hh = l >> 5;
@@ -250,7 +250,7 @@ __global__ __launch_bounds__(256) void pe_gemm_kernel(const uint16_t* __restrict
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + 64 * wm + 32 * i + acc_row(r, hh);
-        if (m < M) {
+        if (m < Mst) {  // rows [M, Mst): A rows read as zeros → the zero pad rows of C
           if constexpr (BF16OUT) reinterpret_cast<uint16_t*>(Cv)[(long long)m * N + n] = f2bf(acc[i][j][r]);
           else reinterpret_cast<float*>(Cv)[(long long)m * N + n] = acc[i][j][r];
         }
@@ -497,10 +497,12 @@ void pe_grads_launch(const uint16_t* E, const float* D, int M, int Kp, int O, co
                      nc, t);
 }
 
-void pe_gemm_launch(const uint16_t* A, const uint16_t* Bw, void* C, bool bf16_out, int M, int N, int K, hipStream_t st) {
-  const dim3 grid((unsigned)((M + GT - 1) / GT), (unsigned)(N / GT));
-  if (bf16_out) hipLaunchKernelGGL(pe_gemm_kernel<true>, grid, dim3(256), 0, st, A, Bw, C, M, N, K);
-  else hipLaunchKernelGGL(pe_gemm_kernel<false>, grid, dim3(256), 0, st, A, Bw, C, M, N, K);
+// C has Mst ≥ M rows; rows past M are written as zeros by the same launch
+void pe_gemm_launch(const uint16_t* A, const uint16_t* Bw, void* C, bool bf16_out, int M, int N, int K, int Mst,
+                    hipStream_t st) {
+  const dim3 grid((unsigned)((Mst + GT - 1) / GT), (unsigned)(N / GT));
+  if (bf16_out) hipLaunchKernelGGL(pe_gemm_kernel<true>, grid, dim3(256), 0, st, A, Bw, C, M, N, K, Mst);
+  else hipLaunchKernelGGL(pe_gemm_kernel<false>, grid, dim3(256), 0, st, A, Bw, C, M, N, K, Mst);
 }
 void pe_weight_prep_launch(const float* W, const float* g, const float* b, const float* bias, int O, int nc, int kin,
                            int Kp, uint16_t* Wg, float* wpg, float* gw, float* bw, float* wt, hipStream_t st) {
