@@ -133,6 +133,7 @@ def test_bench_self_spawns_ranks_cpu_dry_run():
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout  # rank 0 only
+    assert [ln for ln in r.stdout.splitlines() if ln.strip()] == lines, r.stdout  # nothing else on stdout
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 4
     assert out["dist_backend"] == "gloo" and out["params_in_sync"] is True

@@ -112,6 +112,7 @@ def test_bench_json_contract_cpu():
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1
+    assert [l for l in out.stdout.splitlines() if l.strip()] == lines  # nothing else on stdout
     rec = json.loads(lines[0])
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
               "vs_baseline", "dtype", "data", "config"):
