@@ -221,11 +221,9 @@ def _spawn_self(args, argv) -> int:
     """``--gpus N`` without a torchrun environment: start N ranks of this script (one per GPU,
     RCCL) and return the worst exit code.  The parent only counts devices — it never initialises
     the GPU.  With no GPU at all it is a CPU dry run over gloo; with fewer than N GPUs it fails."""
-    import torch
+    from perceiver_io_amd.parallel.launch import gpu_count, spawn
 
-    from perceiver_io_amd.parallel.launch import spawn
-
-    n = torch.cuda.device_count()
+    n = gpu_count()  # no HIP call in this process
     if 0 < n < args.gpus:
         print(f"bench.py: --gpus {args.gpus} but only {n} GPU(s) visible", file=sys.stderr)
         return 2

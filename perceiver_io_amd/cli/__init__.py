@@ -220,9 +220,9 @@ class CLI:
         acc = str(t.get("accelerator") or "auto").lower()
         if acc not in ("gpu", "cuda", "auto"):
             return 1
-        import torch
+        from ..parallel.launch import gpu_count
 
-        if torch.cuda.device_count() == 0:  # does not initialise the GPU on this image
+        if gpu_count() == 0:  # counted without initialising HIP in this (launcher) process
             return 1
         return Trainer._parse_devices(t.get("devices") if t.get("devices") is not None else t.get("gpus"))
 

@@ -87,7 +87,7 @@ void wgrad_launch(const void*, bool, int, int, const void*, bool, int, int, int,
                   const float*, const float*, int, int, float*, float*, int, int, const float*, int, int, int,
                   hipStream_t);
 void ce_fwd_launch(int, const float*, const int64_t*, const int64_t*, const uint16_t*, const float*, int, int, float*,
-                   float*, float*, const float*, float*, float*, unsigned*, uint16_t*, int, float*, long long, hipStream_t);
+                   float*, float*, float*, float*, float*, unsigned*, uint16_t*, int, float*, long long, int, hipStream_t);
 int ce_combine_blocks(int);
 int ce_num_splits(int, int);
 int ce_dw_splits(int, int);
@@ -768,7 +768,10 @@ static const int64_t* opt_idx(const OptT& idx, int64_t n) {
 // label ≥ 0: → {loss (0-dim) = Σ rows / max(count, 1), per-row lse (M,), the compact bf16 rows
 // hs (M, C) the backward kernels read}.  count: fp32 (1,).
 // zero_out: an optional fp32 buffer the kernel clears on the way (the backward's dH accumulator)
-std::vector<Tensor> ce_fwd(Tensor h, OptT idx, Tensor labels, Tensor w, Tensor bias, Tensor count, OptT zero_out) {
+// count_labels: count is an OUTPUT — the combine kernel writes the number of rows with a label
+// ≥ 0 into it (no framework compare + reduce kernels ahead of the head; the backward reads it)
+std::vector<Tensor> ce_fwd(Tensor h, OptT idx, Tensor labels, Tensor w, Tensor bias, Tensor count, OptT zero_out,
+                           bool count_labels) {
   TORCH_CHECK(h.is_contiguous() && w.is_contiguous() && labels.is_contiguous() && bias.is_contiguous());
   CHECK_DT(labels, torch::kInt64);
   CHECK_DT(h, torch::kFloat32);
@@ -781,7 +784,8 @@ std::vector<Tensor> ce_fwd(Tensor h, OptT idx, Tensor labels, Tensor w, Tensor b
   const int ns = pio::ce_num_splits(M, V);
   Tensor part = torch::empty({ns, M, 2}, f32), picked = torch::empty({M}, f32);
   Tensor lse = torch::empty({M}, f32), loss = torch::empty({}, f32);
-  Tensor blk = torch::empty({pio::ce_combine_blocks(M)}, f32);
+  Tensor blk = torch::empty({2 * pio::ce_combine_blocks(M)}, f32);
+  TORCH_CHECK(count.numel() >= 1 && count.is_contiguous(), "ce_fwd: count must hold one fp32 value");
   Tensor hs = torch::empty({M, C}, h.options().dtype(torch::kBFloat16));
   Tensor& tk = ce_ticket(h);
   float* zp = nullptr;
@@ -795,9 +799,9 @@ std::vector<Tensor> ce_fwd(Tensor h, OptT idx, Tensor labels, Tensor w, Tensor b
     zn = zero_out->numel();
   }
   pio::ce_fwd_launch(C, h.data_ptr<float>(), ip, labels.data_ptr<int64_t>(), bfp(w), f32p(bias), M, V,
-                     part.data_ptr<float>(), picked.data_ptr<float>(), lse.data_ptr<float>(), f32p(count),
+                     part.data_ptr<float>(), picked.data_ptr<float>(), lse.data_ptr<float>(), count.data_ptr<float>(),
                      loss.data_ptr<float>(), blk.data_ptr<float>(), reinterpret_cast<unsigned*>(tk.data_ptr<int>()),
-                     bfp_mut(hs), ns, zp, zn, stream());
+                     bfp_mut(hs), ns, zp, zn, count_labels ? 1 : 0, stream());
   checked_sync("ce_fwd");
   return {loss, lse, hs};
 }
@@ -1396,7 +1400,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stage_step", &stage_step, py::arg("dsts"), py::arg("srcs"), py::arg("hyper_dst") = py::none(),
         py::arg("hyper") = std::vector<double>{});
   m.def("ce_fwd", &ce_fwd, py::arg("h"), py::arg("idx"), py::arg("labels"), py::arg("w"), py::arg("bias"),
-        py::arg("count"), py::arg("zero_out") = py::none());
+        py::arg("count"), py::arg("zero_out") = py::none(), py::arg("count_labels") = false);
   m.def("ce_bwd", &ce_bwd, py::arg("h"), py::arg("labels"), py::arg("w"), py::arg("bias"),
         py::arg("lse"), py::arg("gout"), py::arg("count"), py::arg("dH"), py::arg("dW"), py::arg("db"),
         py::arg("accumulate"), py::arg("rowmap") = py::none(), py::arg("slab") = false);

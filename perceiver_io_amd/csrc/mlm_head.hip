@@ -220,9 +220,9 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ H
 constexpr int kCombineRows = 64, kCombineQ = 16;
 __global__ __launch_bounds__(kCombineRows * kCombineQ) void ce_combine_kernel(
     const float* __restrict__ part_ms, const float* __restrict__ picked, const int64_t* __restrict__ labels, int M,
-    int nsplit, float* __restrict__ lse, const float* __restrict__ count, float* __restrict__ loss,
-    float* __restrict__ blk, unsigned* __restrict__ ticket) {
-  __shared__ float sM[kCombineQ][kCombineRows], sS[kCombineQ][kCombineRows], red[16];
+    int nsplit, float* __restrict__ lse, float* __restrict__ count, float* __restrict__ loss,
+    float* __restrict__ blk, unsigned* __restrict__ ticket, int count_labels) {
+  __shared__ float sM[kCombineQ][kCombineRows], sS[kCombineQ][kCombineRows], red[32];
   __shared__ int last;
   const int rr = threadIdx.x % kCombineRows, q = threadIdx.x / kCombineRows;
   const int r = blockIdx.x * kCombineRows + rr;
@@ -238,7 +238,7 @@ __global__ __launch_bounds__(kCombineRows * kCombineQ) void ce_combine_kernel(
   sM[q][rr] = mx;
   sS[q][rr] = sx;
   __syncthreads();
-  float lr = 0.f;
+  float lr = 0.f, nr = 0.f;
   if (q == 0 && r < M) {
     float mm = sM[0][rr];
 #pragma unroll
@@ -248,26 +248,36 @@ __global__ __launch_bounds__(kCombineRows * kCombineQ) void ce_combine_kernel(
     for (int k = 0; k < kCombineQ; ++k) ss += sS[k][rr] * __expf(sM[k][rr] - mm);
     const float L = mm + __logf(ss);
     lse[r] = L;
-    lr = labels[r] >= 0 ? L - picked[r] : 0.f;
+    const bool has = labels[r] >= 0;
+    lr = has ? L - picked[r] : 0.f;
+    nr = has ? 1.f : 0.f;
   }
   lr = wave_sum(lr);  // rows of q == 0 live in wave 0
+  if (count_labels) nr = wave_sum(nr);
   if (threadIdx.x == 0) {
     blk[blockIdx.x] = lr;
+    if (count_labels) blk[gridDim.x + blockIdx.x] = nr;
     __threadfence();
     last = atomicAdd(ticket, 1u) == gridDim.x - 1;
   }
   __syncthreads();
   if (!last) return;
   __threadfence();
-  float t = 0.f;
-  for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x) t += *(volatile const float*)(blk + i);
+  float t = 0.f, n = 0.f;
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x) {
+    t += *(volatile const float*)(blk + i);
+    if (count_labels) n += *(volatile const float*)(blk + gridDim.x + i);
+  }
   t = wave_sum(t);
-  if (lane_id() == 0) red[wave_id()] = t;
+  n = wave_sum(n);
+  if (lane_id() == 0) { red[wave_id()] = t; red[8 + wave_id()] = n; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    float tt = 0.f;
-    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) tt += red[k];
-    loss[0] = tt / fmaxf(count[0], 1.f);
+    float tt = 0.f, nn = 0.f;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) { tt += red[k]; nn += red[8 + k]; }
+    // count_labels: the denominator is the number of rows with a label (written for the backward)
+    if (count_labels) count[0] = nn;
+    loss[0] = tt / fmaxf(count_labels ? nn : count[0], 1.f);
     *ticket = 0u;
   }
 }
@@ -661,9 +671,9 @@ static int ce_target(const char* name, int dflt) {
 
 // tickets: one zeroed counter (the combine kernel's)
 void ce_fwd_launch(int C, const float* Hm, const int64_t* hidx, const int64_t* labels, const uint16_t* W,
-                   const float* bias, int M, int V, float* part_ms, float* picked, float* lse, const float* count,
+                   const float* bias, int M, int V, float* part_ms, float* picked, float* lse, float* count,
                    float* loss, float* blk, unsigned* tickets, uint16_t* hs_out, int nsplit, float* zero_out,
-                   long long zero_n, hipStream_t st) {
+                   long long zero_n, int count_labels, hipStream_t st) {
   const int nchunks = (V + VB - 1) / VB;
   const int cps = (nchunks + nsplit - 1) / nsplit;
   dim3 grid((M + HB - 1) / HB, nsplit);
@@ -676,7 +686,7 @@ void ce_fwd_launch(int C, const float* Hm, const int64_t* hidx, const int64_t* l
 #undef CEF
   hipLaunchKernelGGL(ce_combine_kernel, dim3(ce_combine_blocks(M)), dim3(kCombineRows * kCombineQ), 0, st, part_ms, picked,
                      labels, M, nsplit,
-                     lse, count, loss, blk, tickets);
+                     lse, count, loss, blk, tickets, count_labels);
 }
 
 int ce_combine_blocks(int M) { return (M + kCombineRows - 1) / kCombineRows; }

@@ -506,11 +506,14 @@ def _ce_rows(h, idx):
     return h if idx is None else h.index_select(0, idx)
 
 
-def ce_fwd(h, idx, labels, w, bias, count, zero_out=None):
+def ce_fwd(h, idx, labels, w, bias, count, zero_out=None, count_labels=False):
     """→ (mean loss Σ rows / max(count, 1) as a 0-dim tensor, per-row lse); rows of ``h`` are
-    gathered through ``idx`` when given; ``zero_out`` (the backward's dH accumulator) is cleared."""
+    gathered through ``idx`` when given; ``zero_out`` (the backward's dH accumulator) is cleared.
+    ``count_labels``: ``count`` is written with the number of rows whose label is ≥ 0."""
     if zero_out is not None:
         zero_out.zero_()
+    if count_labels:
+        count.reshape(-1)[0] = (labels >= 0).sum()
     logits = _bf(_ce_rows(h, idx).float()) @ _bf(w.float()).t() + bias
     lse = torch.logsumexp(logits, -1)
     valid = labels >= 0

@@ -81,15 +81,19 @@ class _MaskedCE(torch.autograd.Function):
         h2 = h.reshape(-1, c)
         if h2.dtype != torch.float32 or not h2.is_contiguous():
             h2 = h2.float().contiguous()
-        cnt = count.reshape(1)
-        if cnt.dtype != torch.float32:
-            cnt = cnt.to(torch.float32)
+        count_labels = count is None  # the combine kernel counts the rows with a label itself
+        if count_labels:
+            cnt = torch.empty(1, device=h2.device, dtype=torch.float32)
+        else:
+            cnt = count.reshape(1)
+            if cnt.dtype != torch.float32:
+                cnt = cnt.to(torch.float32)
         from .fused import weight_cache
 
         wb = weight_cache.get(weight)  # bf16 shadow written by the fused optimizer
         # the backward's dH accumulator (atomic partials) is cleared by the forward kernel
         dh = torch.empty((h2.shape[0], c), device=h2.device, dtype=torch.float32)
-        loss, lse, hs = ext.ce_fwd(h2, idx, labels_c, wb, bias.contiguous(), cnt, dh)
+        loss, lse, hs = ext.ce_fwd(h2, idx, labels_c, wb, bias.contiguous(), cnt, dh, count_labels)
         ctx.dh = dh
         ctx.save_for_backward(hs, wb, bias, lse, idx if idx is not None else torch.empty(0, dtype=torch.int64),
                               labels_c, cnt)
@@ -309,8 +313,7 @@ def classification_loss(decoder, x_latent: torch.Tensor, labels: torch.Tensor):
     lin = getattr(ad, "linear", None)
     if (lin is not None and use_hip(h) and h.dim() == 3 and h.shape[1] == 1 and h.shape[-1] in (32, 64, 128)
             and labels.dim() == 1 and labels.shape[0] == h.shape[0]):
-        lab = labels.to(torch.int64).contiguous()
-        cnt = (lab >= 0).sum(dtype=torch.float32).reshape(1)
-        return _MaskedCE.apply(h, lin.weight, lin.bias, None, lab, cnt)
+        lab = labels if labels.dtype == torch.int64 and labels.is_contiguous() else labels.to(torch.int64).contiguous()
+        return _MaskedCE.apply(h, lin.weight, lin.bias, None, lab, None)  # count: rows with a label, in-kernel
     return F.cross_entropy(ad(h).float(), labels)
 

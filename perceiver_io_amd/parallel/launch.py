@@ -24,6 +24,42 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
+def _visible_list(v: str) -> int:
+    return len([t for t in v.split(",") if t.strip() != ""])
+
+
+def gpu_count() -> int:
+    """Number of GPUs this process would see, WITHOUT initialising HIP in this process (the
+    launcher parent must hold no GPU state when it starts the ranks).
+
+    Order: an explicit ``HIP_VISIBLE_DEVICES`` / ``ROCR_VISIBLE_DEVICES`` / ``CUDA_VISIBLE_DEVICES``
+    list; else the GPU nodes of the KFD topology (``/sys/class/kfd/kfd/topology/nodes/*``, a
+    node with ``simd_count > 0``); else a short-lived child process that asks torch (its HIP
+    runtime dies with it)."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return _visible_list(v)
+    topo = "/sys/class/kfd/kfd/topology/nodes"
+    if os.path.isdir(topo):
+        n = 0
+        for node in os.listdir(topo):
+            try:
+                with open(os.path.join(topo, node, "properties")) as f:
+                    props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+                if int(props.get("simd_count", "0")) > 0:
+                    n += 1
+            except (OSError, ValueError):
+                continue
+        return n
+    try:
+        r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                           stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True, timeout=300)
+        return int(r.stdout.strip().splitlines()[-1])
+    except (subprocess.SubprocessError, ValueError, IndexError, OSError):
+        return 0
+
+
 def spawn(nprocs: int, cmd: List[str], env: Optional[dict] = None, port: Optional[int] = None) -> int:
     base = dict(os.environ if env is None else env)
     base.setdefault("MASTER_ADDR", "127.0.0.1")

@@ -248,7 +248,9 @@ class StepEngine:
             if ddp:  # ready points fire inside the graph only when the collectives are captured
                 self._arm(in_graph)
             loss = self.loss_fn(static)
-            loss.backward(one if loss.dim() == 0 and loss.dtype == one.dtype else None)
+            if loss.dim() != 0:  # the 1/accumulate seed averages micro-batches: a scalar loss only
+                raise ValueError(f"StepEngine: the loss must be a scalar, got shape {tuple(loss.shape)}")
+            loss.backward(one if loss.dtype == one.dtype else one.to(loss.dtype))
             if in_graph:
                 if ddp:
                     red.finish()

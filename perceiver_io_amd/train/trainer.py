@@ -187,19 +187,21 @@ class Trainer:
 
     @staticmethod
     def _parse_devices(d) -> int:
+        from ..parallel.launch import gpu_count as _gpu_count  # no HIP init (launcher parent)
+
         if d is None:
             return 1
         if isinstance(d, str):
             d = d.strip()
             if d in ("-1", "auto"):
-                return max(1, torch.cuda.device_count())
+                return max(1, _gpu_count())
             if "," in d:
                 return len([x for x in d.split(",") if x.strip()])
             d = int(d)
         if isinstance(d, (list, tuple)):
             return len(d)
         d = int(d)
-        return max(1, torch.cuda.device_count()) if d == -1 else max(1, d)
+        return max(1, _gpu_count()) if d == -1 else max(1, d)
 
     # ------------------------------------------------------------------------------------
     @property
