@@ -178,6 +178,10 @@ class FusedAdamW(torch.optim.Optimizer):
         self._step = 0
         self._ring = _HostRing(8, 8, dev) if dev.type == "cuda" else None
         self.grad_scale = 1.0
+        # bucket mode (set by the step engine with a data-parallel reducer): each gradient bucket
+        # is updated by range_update right after its all-reduce lands, on the reducer's side
+        # stream, so device_update has nothing left to do
+        self.bucket_mode = False
 
     # -- the update ---------------------------------------------------------------------
     def hyper_values(self):
@@ -194,10 +198,30 @@ class FusedAdamW(torch.optim.Optimizer):
         else:
             self.hyper.copy_(torch.tensor(vals))
 
+    def bucket_updates_ok(self) -> bool:
+        """Per-bucket updates are exact only without a global gradient norm (clipping) and without
+        replicated gradient accumulators (a later fold would add into an updated range)."""
+        return self.max_grad_norm <= 0 and self.flat.grad_rep is None
+
+    def range_update(self, lo: int, hi: int):
+        """Fused AdamW over flat elements [lo, hi) only (the same per-element arithmetic as the
+        whole-buffer kernel, so a step made of range updates is bitwise the full update); the
+        gradient range is cleared as it is consumed.  Reads the hyper-parameters already staged
+        for this step."""
+        K = ext.require() if self.flat.device.type == "cuda" else emulation
+        g = self.param_groups[0]
+        f = self.flat
+        K.adamw(f.data[lo:hi], f.grad[lo:hi], self.exp_avg[lo:hi], self.exp_avg_sq[lo:hi],
+                None if f.shadow is None else f.shadow[lo:hi], self.hyper, g["eps"], g["weight_decay"], 0.0,
+                self.grad_scale, l2=self.l2, zero_grad=True)
+
     def device_update(self, zero_grad: bool = False):
         """The capturable part: (grad-norm) + fused AdamW kernel over the flat buffers.
         ``zero_grad``: the kernel clears the gradient as it consumes it (flat buffers without
-        replicas only; the step engine's captured step then skips its leading zero fill)."""
+        replicas only; the step engine's captured step then skips its leading zero fill).
+        In bucket mode the reducer has already updated every bucket: nothing to do."""
+        if self.bucket_mode:
+            return
         K = ext.require() if self.flat.device.type == "cuda" else emulation
         g = self.param_groups[0]
         self.flat.fold()

@@ -102,6 +102,10 @@ class FlatGradReducer:
         self._side = torch.cuda.Stream(device=flat.device) if (self.on_gpu and self.overlap) else None
         self._counts = [0] * len(self.buckets)
         self._armed = False
+        # updater(lo, hi): the optimizer's range update, run right after a bucket's all-reduce on
+        # the same (side) stream — the whole update overlaps the backward except for the buckets
+        # finish() reduces (attach_updater)
+        self.updater = None
         self.early_launches = 0  # buckets launched from a backward (tests / diagnostics)
         self.launch_log: List[str] = []  # names of the ready points that fired, in order (tests)
         if in_graph is None:
@@ -284,6 +288,11 @@ class FlatGradReducer:
         else:
             dist.all_reduce(g)
 
+    def attach_updater(self, fn) -> None:
+        """Update each bucket's parameters as soon as its all-reduce lands (``fn(lo, hi)``, e.g.
+        :meth:`FusedAdamW.range_update`); None detaches."""
+        self.updater = fn
+
     def _launch(self, bucket: int):
         if _capturing(self.flat.device) and not self.in_graph:
             raise RuntimeError("FlatGradReducer: a collective inside a hipGraph capture on a node where the "
@@ -294,8 +303,12 @@ class FlatGradReducer:
             self._side.wait_stream(torch.cuda.current_stream(self.flat.device))
             with torch.cuda.stream(self._side):
                 self._reduce(lo, hi)
+                if self.updater is not None:
+                    self.updater(lo, hi)
         else:
             self._reduce(lo, hi)
+            if self.updater is not None:
+                self.updater(lo, hi)
 
     def point_reached(self, name: str):
         """Backward reached ready point ``name``: its bucket is final → launch it."""

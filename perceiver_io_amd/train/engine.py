@@ -25,6 +25,8 @@ semantics), so an epoch of pad-to-longest batches needs a handful of graphs, not
 """
 from __future__ import annotations
 
+import os
+
 from collections import OrderedDict
 from typing import Callable, Dict, Optional
 
@@ -148,7 +150,7 @@ class StepEngine:
 
     def __init__(self, loss_fn: Callable, optimizer, scheduler=None, reducer=None, device=None,
                  graph: bool = False, accumulate: int = 1, warmup_eager: int = 2, max_graphs: int = 12,
-                 state_hooks=None, graph_impl: Optional[str] = None):
+                 state_hooks=None, graph_impl: Optional[str] = None, bucket_update: Optional[bool] = None):
         from ..ops.optim import FusedAdamW
 
         self.loss_fn = loss_fn
@@ -177,6 +179,17 @@ class StepEngine:
         if self.fused and reducer is not None and reducer.enabled:
             optimizer.grad_scale = reducer.grad_scale()
         self.grad_scale_base = getattr(optimizer, "grad_scale", 1.0)
+        # per-bucket optimizer updates: each gradient bucket's AdamW runs right behind its
+        # all-reduce on the reducer's side stream (overlapping the rest of the backward), so
+        # only the buckets finish() reduces stay on the critical path.  Needs no clipping (a
+        # global norm) and no replicated accumulators; PERCEIVER_BUCKET_UPDATE=0 disables it.
+        if bucket_update is None:
+            bucket_update = os.environ.get("PERCEIVER_BUCKET_UPDATE", "1") != "0"
+        self.bucket_update = bool(bucket_update and self.fused and reducer is not None and reducer.enabled
+                                  and optimizer.bucket_updates_ok())
+        if self.bucket_update:
+            optimizer.bucket_mode = True
+            reducer.attach_updater(optimizer.range_update)
 
     # -- eager -----------------------------------------------------------------------------
     def _arm(self, last: bool):
@@ -185,6 +198,8 @@ class StepEngine:
             r.arm() if last else r.disarm()
 
     def _eager_micro(self, batch, last: bool):
+        if last and self.bucket_update:
+            self.opt.stage_hyper()  # the bucket updates fire during this backward
         self._arm(last)
         loss = self.loss_fn(batch)
         (loss / self.accumulate if self.accumulate > 1 else loss).backward()
@@ -195,7 +210,7 @@ class StepEngine:
 
     def _optimizer_step(self):
         if self.fused:
-            self.opt.step()
+            self.opt.step(staged=self.bucket_update)
         else:
             if self.reducer is not None and self.reducer.enabled:
                 for p in self.opt.param_groups[0]["params"]:
@@ -349,8 +364,10 @@ class StepEngine:
             if self._opt_in_graph:
                 self.opt._step += 1
             else:  # forward+backward replayed; the all-reduce + update eagerly (3 launches)
+                if self.bucket_update:
+                    self.opt.stage_hyper()
                 self.reducer.finish()
-                self.opt.step()
+                self.opt.step(staged=self.bucket_update)
             if self.sched is not None:
                 self.sched.step()
             return ents[-1].loss.detach().clone()

@@ -91,28 +91,31 @@ def _worker(rank, world, port, cases, steps, out):
 
     dist.init(device_type="cpu")
     res = {}
-    for name, (graph, in_graph, overlap, acc) in cases.items():
+    for name, (graph, in_graph, overlap, acc, *extra) in cases.items():
+        bucket = extra[0] if extra else True
+        wire = extra[1] if len(extra) > 1 else None
         model = _model()
         opt = FusedAdamW(model.parameters(), lr=1e-2, eps=0.1, weight_decay=0.01)
-        red = FlatGradReducer(opt.flat, bucket_bytes=16 << 10, overlap=overlap, in_graph=in_graph)
+        red = FlatGradReducer(opt.flat, bucket_bytes=16 << 10, overlap=overlap, in_graph=in_graph, wire_dtype=wire)
         red.plan(model)
         red.broadcast_parameters(model)
         eng = StepEngine(_loss_fn(model), opt, reducer=red, graph=graph, accumulate=acc, warmup_eager=1,
-                         graph_impl="closure" if graph else None)
+                         graph_impl="closure" if graph else None, bucket_update=bucket)
         data = _batches(rank, steps, acc)
         sync = []
         for s in range(steps):
             eng.step(data[s] if acc > 1 else data[s][0])
             sync.append(params_in_sync(opt.flat))
         res[name] = dict(params=opt.flat.data.clone(), sync=sync, log=list(red.launch_log), points=dict(red.points),
-                         replays=eng.replays, captures=eng.captures, buckets=list(red.buckets))
+                         replays=eng.replays, captures=eng.captures, buckets=list(red.buckets),
+                         bucket_mode=eng.bucket_update)
         red.close()
     out[rank] = res
     dist.shutdown()
 
 
 CASES = {
-    # name: (graph, in_graph, overlap, accumulate)
+    # name: (graph, in_graph, overlap, accumulate[, per-bucket optimizer updates (default on)[, wire dtype]])
     "eager": (False, False, True, 1),
     "eager_nooverlap": (False, False, False, 1),
     "graph_in": (True, True, True, 1),
@@ -120,6 +123,13 @@ CASES = {
     "eager_acc2": (False, False, True, 2),
     "graph_in_acc2": (True, True, True, 2),
     "graph_out_acc2": (True, False, True, 2),
+    # one whole-buffer AdamW after finish() (the pre-bucket-update path)
+    "eager_whole": (False, False, True, 1, False),
+    "graph_in_whole": (True, True, True, 1, False),
+    "graph_out_whole": (True, False, True, 1, False),
+    "graph_in_acc2_whole": (True, True, True, 2, False),
+    # bf16 on the wire (SURVEY C-03's optional format)
+    "eager_bf16wire": (False, False, True, 1, True, torch.bfloat16),
 }
 STEPS = 4
 
@@ -149,6 +159,33 @@ def test_graph_path_equals_eager_bitwise(ddp_runs):
     assert torch.equal(p["eager_acc2"], p["graph_in_acc2"])
     assert torch.equal(p["eager_acc2"], p["graph_out_acc2"])
     assert not torch.equal(p["eager"], p["eager_acc2"])
+
+
+def test_bucket_updates_equal_whole_buffer_update_bitwise(ddp_runs):
+    """AdamW run per bucket right behind each all-reduce (overlapping the backward) gives exactly
+    the bits of one whole-buffer update after finish(), on every path."""
+    runs, _ = ddp_runs
+    r = runs[0]
+    assert r["eager"]["bucket_mode"] and not r["eager_whole"]["bucket_mode"]
+    for a, b in (("eager", "eager_whole"), ("graph_in", "graph_in_whole"), ("graph_out", "graph_out_whole"),
+                 ("graph_in_acc2", "graph_in_acc2_whole")):
+        assert torch.equal(r[a]["params"], r[b]["params"]), (a, b)
+
+
+def test_bf16_wire_format_close_to_fp32(ddp_runs):
+    """bf16 all-reduce (half the bytes on xGMI): ranks stay bitwise in sync (checked for every
+    case above) and the trajectory stays within bf16 rounding of the fp32-wire one."""
+    runs, _ = ddp_runs
+    a, b = runs[0]["eager_bf16wire"]["params"], runs[0]["eager"]["params"]
+    init = _flat_init()
+    rel = ((a - b).norm() / (b - init).norm()).item()
+    assert 0.0 < rel < 5e-2, rel
+
+
+def _flat_init():
+    from perceiver_io_amd.ops.optim import FlatParameterSpace
+
+    return FlatParameterSpace(list(_model().parameters()), with_shadow=False).data
 
 
 def test_ready_points_fire_where_expected(ddp_runs):

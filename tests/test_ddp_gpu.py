@@ -184,3 +184,116 @@ def test_graph_gradient_accumulation_matches_eager_and_big_batch():
     p0 = FlatParameterSpace(list(init.parameters()), with_shadow=False).data.cuda()
     rel = ((g[0] - big[0]).norm() / (big[0] - p0).norm()).item()
     assert rel < 2e-2, rel  # bf16 kernels: different row grouping, same maths
+
+
+def _data_equal_targets(rank, n):
+    """Like _data, with exactly 24 MLM targets per row: every rank's loss is a mean over the same
+    number of targets, so the mean of the ranks' losses is the loss of the concatenated batch."""
+    out = []
+    for ids, pad, lab, xm in _data(rank, n):
+        lab = torch.full_like(lab, -100)
+        lab[:, 5:29] = ids[:, 5:29]
+        out.append((ids, pad, lab, xm))
+    return out
+
+
+def _worker_rccl(rank, world, port, out):
+    # a fresh process per rank, one GPU each: nothing touched the GPU before this point
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), PERCEIVER_DIST_BACKEND="nccl")
+    from perceiver_io_amd.ops.optim import FusedAdamW
+    from perceiver_io_amd.parallel import FlatGradReducer, dist
+    from perceiver_io_amd.parallel.reducer import params_in_sync
+    from perceiver_io_amd.train.engine import StepEngine
+
+    dist.init()
+    model = _setup()
+    opt = FusedAdamW(model.parameters(), lr=1e-2, eps=1.0, weight_decay=0.0)
+    red = FlatGradReducer(opt.flat)
+    red.plan(model)
+    red.broadcast_parameters(model)
+    eng = StepEngine(lambda b: model.loss(b[0], b[1], labels=b[2], x_masked=b[3]), opt, reducer=red, device="cuda",
+                     graph=True)
+    for b in _data_equal_targets(rank, STEPS):
+        eng.step(b)
+    torch.cuda.synchronize()
+    out[rank] = dict(params=opt.flat.data.cpu(), sync=params_in_sync(opt.flat), in_graph=red.in_graph,
+                     replays=eng.replays, bucket=eng.bucket_update, log=list(red.launch_log))
+    red.close()
+    dist.shutdown()
+
+
+def test_rccl_multi_gpu_ranks_graph_steps():
+    """min(#GPUs, 8) RCCL ranks, one GPU each (skipped on a one-GPU box): captured steps with the
+    all-reduces inside the graph where RCCL capture works, per-bucket AdamW behind each
+    all-reduce; ranks bitwise in sync after 5 steps and equal (update-relative) to one process
+    stepping the concatenated batch."""
+    n = torch.cuda.device_count()
+    if n < 2:
+        pytest.skip("needs >= 2 GPUs")
+    world, port = min(n, 8), _port()
+    out = mp.get_context("spawn").Manager().dict()
+    mp.spawn(_worker_rccl, args=(world, port, out), nprocs=world, join=True)
+    for r in range(world):
+        assert out[r]["sync"] == 0.0, (r, out[r]["sync"])
+        assert out[r]["replays"] == STEPS - 2 and out[r]["bucket"]
+        assert torch.equal(out[r]["params"], out[0]["params"])
+    # one process, the concatenated batch, same deterministic kernels
+    from perceiver_io_amd import ops
+    from perceiver_io_amd.ops.optim import FlatParameterSpace, FusedAdamW
+    from perceiver_io_amd.train.engine import StepEngine
+
+    try:
+        model = _setup()
+        p0 = FlatParameterSpace(list(_setup().parameters()), with_shadow=False).data.cuda()
+        opt = FusedAdamW(model.parameters(), lr=1e-2, eps=1.0, weight_decay=0.0)
+        eng = StepEngine(lambda b: model.loss(b[0], b[1], labels=b[2], x_masked=b[3]), opt, device="cuda", graph=False)
+        data = [_data_equal_targets(r, STEPS) for r in range(world)]
+        for s in range(STEPS):
+            eng.step(tuple(torch.cat([data[r][s][j] for r in range(world)]) for j in range(4)))
+        torch.cuda.synchronize()
+        got = out[0]["params"].cuda()
+        rel = ((got - opt.flat.data).norm() / (opt.flat.data - p0).norm()).item()
+        assert rel < 2e-3, rel
+    finally:
+        ops.set_deterministic(False)
+
+
+def _worker_gloo_overlap(rank, world, port, out):
+    """Default (non-deterministic) kernels, eager steps with the ready points firing DURING the
+    backward and per-bucket updates on the side stream: a bucket reduced before its gradients
+    are final would leave later contributions rank-local and the ranks would drift apart."""
+    os.environ.update(RANK=str(rank), LOCAL_RANK="0", WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), PERCEIVER_DIST_BACKEND="gloo")
+    from perceiver_io_amd import ops
+    from perceiver_io_amd.ops.optim import FusedAdamW
+    from perceiver_io_amd.parallel import FlatGradReducer, dist
+    from perceiver_io_amd.parallel.reducer import params_in_sync
+    from perceiver_io_amd.train.engine import StepEngine
+
+    dist.init()
+    model = _setup()
+    ops.set_deterministic(False)
+    opt = FusedAdamW(model.parameters(), lr=1e-3, weight_decay=0.01)
+    red = FlatGradReducer(opt.flat)
+    red.plan(model)
+    red.broadcast_parameters(model)
+    eng = StepEngine(lambda b: model.loss(b[0], b[1], labels=b[2], x_masked=b[3]), opt, reducer=red, device="cuda",
+                     graph=False)
+    sync = []
+    for b in _data(rank, 6):
+        eng.step(b)
+        sync.append(params_in_sync(opt.flat))
+    out[rank] = dict(sync=sync, log=list(red.launch_log), bucket=eng.bucket_update)
+    red.close()
+    dist.shutdown()
+
+
+def test_two_ranks_overlapped_nondeterministic_in_sync():
+    world, port = 2, _port()
+    out = mp.get_context("spawn").Manager().dict()
+    mp.spawn(_worker_gloo_overlap, args=(world, port, out), nprocs=world, join=True)
+    for r in range(world):
+        assert out[r]["bucket"]
+        assert out[r]["log"] == ["decoder", "layer_n"] * 6
+        assert out[r]["sync"] == [0.0] * 6, out[r]["sync"]
