@@ -67,6 +67,8 @@ def parse(argv=None):
     ap.add_argument("--backend", default="hip", choices=["hip", "torch", "reference"])
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture of the step")
+    ap.add_argument("--allreduce-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="gradient all-reduce wire format (N > 1)")
     ap.add_argument("--dense", action="store_true", help="lartpc: evaluate all pixels (the reference's cost)")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--profile-stacks", type=int, default=0,
@@ -290,7 +292,7 @@ def main(argv=None):
         from perceiver_io_amd.ops.optim import FlatParameterSpace
 
         flat = opt.flat if fused else FlatParameterSpace(params, with_shadow=False, replicate=False)
-        reducer = FlatGradReducer(flat)
+        reducer = FlatGradReducer(flat, wire_dtype=torch.bfloat16 if args.allreduce_dtype == "bf16" else None)
         reducer.plan(model)  # ready points: decoder + head, layer_n — all-reduced during the backward
         reducer.broadcast_parameters(model)
 
@@ -375,7 +377,9 @@ def main(argv=None):
                        "graph": bool(fused and not args.no_graph), "name": args.config,
                        "dist_backend": info.backend if world > 1 else None,
                        "allreduce_in_graph": bool(reducer is not None and getattr(reducer, "in_graph", False)),
-                       "allreduce_overlap": sorted(reducer.points) if reducer is not None else []},
+                       "allreduce_overlap": sorted(reducer.points) if reducer is not None else [],
+                       "allreduce_dtype": args.allreduce_dtype if world > 1 else None,
+                       "bucket_update": bool(getattr(engine, "bucket_update", False))},
             "final_loss": round(final_loss, 4),
             "dist_backend": info.backend if world > 1 else None,
             "params_in_sync": sync_diff == 0.0, "params_max_abs_diff": sync_diff,

@@ -110,7 +110,7 @@ class Trainer:
                  resume_from_checkpoint: Optional[str] = None, profiler: Optional[str] = None, benchmark: bool = False,
                  deterministic: bool = False, detect_anomaly: bool = False, terminate_on_nan: Optional[bool] = None,
                  replace_sampler_ddp: bool = True, graph_capture: Optional[bool] = None, seed: Optional[int] = None,
-                 **ignored: Any):
+                 allreduce_dtype: Optional[str] = None, **ignored: Any):
         for k, v in ignored.items():
             if v not in (None, False, 0, 0.0, "", [], {}) and k not in _KNOWN_NOOP:
                 warnings.warn(f"Trainer flag {k}={v!r} has no effect in this framework")
@@ -145,6 +145,11 @@ class Trainer:
         self.replace_sampler_ddp = replace_sampler_ddp
         self.graph_capture = graph_capture
         self.seed = seed
+        # gradient all-reduce wire format (SURVEY C-03): None / "fp32" (parity default) or "bf16"
+        # (half the bytes over xGMI; every rank still applies the same reduced gradient)
+        if allreduce_dtype not in (None, "fp32", "float32", "bf16", "bfloat16"):
+            raise ValueError(f"allreduce_dtype must be fp32 or bf16, got {allreduce_dtype!r}")
+        self.allreduce_dtype = torch.bfloat16 if allreduce_dtype in ("bf16", "bfloat16") else None
         if fast_dev_run:
             n = 1 if fast_dev_run is True else int(fast_dev_run)
             self.limit_train_batches = self.limit_val_batches = self.limit_test_batches = n
@@ -325,7 +330,7 @@ class Trainer:
 
                 flat = getattr(opt, "flat", None) or FlatParameterSpace(
                     [p for p in model.parameters() if p.requires_grad], with_shadow=False)
-                reducer = FlatGradReducer(flat)
+                reducer = FlatGradReducer(flat, wire_dtype=self.allreduce_dtype)
                 net = getattr(model, "model", None)
                 if net is not None:  # ready points: decoder + head, then layer_n (overlapped all-reduce)
                     reducer.plan(net)

@@ -121,3 +121,26 @@ def test_bench_json_contract_cpu():
     assert rec["scaling"] == "weak" and rec["value"] > 0
     assert {"model", "global_batch", "seq_len", "parallelism"} <= set(rec["config"])
     assert rec["config"]["global_batch"] == 2 and rec["config"]["seq_len"] == 32
+
+
+def test_allreduce_dtype_flag(tmp_path):
+    """--trainer.allreduce_dtype (the gradient all-reduce wire format, SURVEY C-03) reaches the trainer;
+    a bad value is rejected.  The bf16 wire itself is exercised on 2 gloo ranks in
+    test_ddp_engine.py::test_bf16_wire_format_close_to_fp32."""
+    from perceiver_io_amd.train.trainer import Trainer
+
+    cli = _run_cli("img_clf", tmp_path, "fit", *IMG_FLAGS, "--trainer.fast_dev_run=true",
+                   "--trainer.allreduce_dtype=bf16")
+    assert cli.trainer.allreduce_dtype == torch.bfloat16 and cli.trainer.global_step == 1
+    with pytest.raises(ValueError, match="allreduce_dtype"):
+        Trainer(logger=False, allreduce_dtype="fp8")
+
+
+def test_gpu_count_respects_visible_devices(monkeypatch):
+    """The launcher parent counts GPUs without initialising HIP (no HIP call in this process)."""
+    from perceiver_io_amd.parallel.launch import gpu_count
+
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,3,5")
+    assert gpu_count() == 3
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
+    assert gpu_count() == 0
