@@ -4,45 +4,29 @@
 // VGPRs, so the softmax and LayerNorm VALU work reads them directly instead of copying every
 // accumulator out of (and back into) AGPRs (≈1,300 v_accvgpr moves per wave in the attention
 // phase otherwise).
+#include <type_traits>
+
 #include "common.h"
 
 namespace pio {
 
 // ------------------------------------------------------------------------------------
 // Chain layout (CL): register-resident row chains with v_mfma_f32_16x16x32_bf16.
-// Wave w of a 64-row tile owns rows 16w + (l & 15); lane group g = l >> 4 holds channels
-// 16·mt + 4g + i (i < 4) of every 16-channel block mt — exactly the accumulator layout of a
-// TRANSPOSED product Yᵀ = W·Xᵀ (col = lane & 15 = row, acc row = 4g + i = channel).  Such an
-// accumulator feeds the next transposed product as its B operand with no lane movement: the
+// A row lives on lane (l & 15) of a wave; lane group g = l >> 4 holds channels
+// 16·mt + 4g + i (i < 4) of every 16-channel block (m-tile) mt — exactly the accumulator layout
+// of a TRANSPOSED product Yᵀ = W·Xᵀ (col = lane & 15 = row, acc row = 4g + i = channel).  Such
+// an accumulator feeds the next transposed product as its B operand with no lane movement: the
 // k order of step t is permuted to channel 32t + 16(j >> 2) + 4g + (j & 3) for element j, and
-// the weight (A operand) is staged into LDS with its columns permuted the same way, so every
-// A fragment is one ds_read_b128.  A row's reductions (LayerNorm, per-head sums) are 16 local
-// values + two lane swaps (l ^ 16, l ^ 32).  So a whole post-attention block — out-projection,
-// residual, LN2, W1, GELU, W2, residual, LN1 + the next projection — runs per wave, from
-// registers, with no LDS round trip of an activation and no workgroup barrier.
+// the weight (A operand) is staged into LDS with its columns permuted the same way, so every A
+// fragment is one ds_read_b128.  A row's reductions (LayerNorm, per-head sums) are local values
+// + two lane swaps (l ^ 16, l ^ 32).  So a whole post-attention block — out-projection,
+// residual, LN2, W1, GELU, W2, residual, LN1 + the next projection — runs from registers with no
+// LDS round trip of an activation except the pair hand-offs of CL2 below.
 // ------------------------------------------------------------------------------------
-// B fragment of k-step t from a CL activation (permuted k order)
-template <int NM>
-__device__ __forceinline__ bf16x8 cl_bfrag(const float (&v)[NM][4], int t) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (short)f2bf(v[2 * t + (j >> 2)][j & 3]);
-  return r;
-}
 // A fragment (m-tile mt, k-step t) of a weight image in LDS ([rows][ld], permuted or natural)
 __device__ __forceinline__ bf16x8 cl_afrag(const uint16_t* sW, int ld, int mt, int t) {
   const int l = lane_id();
   return *reinterpret_cast<const bf16x8*>(sW + (16 * mt + (l & 15)) * ld + 32 * t + 8 * (l >> 4));
-}
-// Y^T (NMO m-tiles) = W·X^T over K = 32·KT channels; acc in CL
-template <int NMO, int KT>
-__device__ __forceinline__ void cl_gemm(const uint16_t* sW, int ld, const bf16x8 (&b)[KT], f32x4 (&acc)[NMO]) {
-#pragma unroll
-  for (int mt = 0; mt < NMO; ++mt) {
-    acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int t = 0; t < KT; ++t) acc[mt] = mfma16(cl_afrag(sW, ld, mt, t), b[t], acc[mt]);
-  }
 }
 // one 16-byte chunk (row r, source columns c0 .. c0 + 7 of a 64-wide bf16 row) of a weight into
 // its LDS image: natural, or columns permuted to the CL k order (two 8-byte pieces)
@@ -58,100 +42,121 @@ __device__ __forceinline__ void cl_wstore(uint16_t* sW, int ld, int r, int c0, c
   *reinterpret_cast<bf16x4*>(sW + r * ld + 32 * t + 8 * gp + 4 * s) = lo;
   *reinterpret_cast<bf16x4*>(sW + r * ld + 32 * t + 8 * (gp + 1) + 4 * s) = hi;
 }
-// row sums over the 64 channels of a CL row (all four lane groups get the total)
-template <int NM>
-__device__ __forceinline__ float cl_rowsum(const float (&v)[NM][4]) {
-  float s = 0.f;
+
+// ------------------------------------------------------------------------------------
+// Paired chain layout (CL2): 8 waves per 64-row tile, two waves per 16-row chain.  Wave w owns
+// rows 16·(w & 3) + (l & 15) and the channel half hf = w >> 2, i.e. m-tiles 2hf, 2hf + 1 of the
+// CL layout (channels 32hf + 16i + 4g + j).  Every product Yᵀ = W·Xᵀ over K = 64 splits over the
+// pair by OUTPUT channels: a wave computes its two m-tiles over both k-steps.  The B fragment of
+// k-step t is built from m-tiles 2t, 2t + 1, i.e. exactly the activations wave hf = t holds, so
+// each wave packs its own fragment and takes its partner's (w ^ 4) through a 1 KB LDS slot —
+// one barrier per product.  Row reductions (LayerNorm) combine the pair's two 32-channel
+// partial (mean, M2) by Chan's formula through an 8-byte-per-row slot: one barrier per LN.
+// Half the MFMA / VALU work per wave, and two waves per SIMD to hide each other's latency.
+// ------------------------------------------------------------------------------------
+// own k-step fragment (local m-tiles 0, 1 = global 2hf, 2hf + 1), CL k order
+__device__ __forceinline__ bf16x8 cl2_frag(const float (&v)[2][4]) {
+  bf16x8 r;
 #pragma unroll
-  for (int mt = 0; mt < NM; ++mt)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) s += v[mt][i];
-  return xor32_sum(xor16_sum(s));
+  for (int j = 0; j < 8; ++j) r[j] = (short)f2bf(v[j >> 2][j & 3]);
+  return r;
 }
-// LayerNorm of CL rows in place (affine from LDS vectors, 16-byte broadcast reads)
-template <int NM>
-__device__ __forceinline__ void cl_layernorm(float (&v)[NM][4], const float* sg, const float* sb, float eps,
-                                             float& mean, float& rstd) {
-  constexpr int C = 16 * NM;
-  const int g = lane_id() >> 4;
-  mean = cl_rowsum<NM>(v) / C;
-  float d[NM][4];
+// pair exchange of a bf16x8 fragment through slot sx (8 waves × 64 lanes × 16 B): b[hf] = own,
+// b[1 - hf] = the partner's
+__device__ __forceinline__ void cl2_swap_frag(bf16x8* sx, const bf16x8& own, int hf, bf16x8 (&b)[2]) {
+  const int w = wave_id(), l = lane_id();
+  sx[w * 64 + l] = own;
+  lds_sync();
+  const bf16x8 o = sx[(w ^ 4) * 64 + l];
+  b[0] = hf ? o : own;
+  b[1] = hf ? own : o;
+}
+// Yᵀ (this wave's two m-tiles) = W·Xᵀ over K = 64 (two k-steps)
+__device__ __forceinline__ void cl2_gemm(const uint16_t* sW, int ld, int hf, const bf16x8 (&b)[2], f32x4 (&acc)[2]) {
 #pragma unroll
-  for (int mt = 0; mt < NM; ++mt)
+  for (int i = 0; i < 2; ++i) {
+    acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) { d[mt][i] = v[mt][i] - mean; d[mt][i] *= d[mt][i]; }
-  rstd = rsqrtf(cl_rowsum<NM>(d) / C + eps);
-#pragma unroll
-  for (int mt = 0; mt < NM; ++mt) {
-    const float4 gg = *reinterpret_cast<const float4*>(sg + 16 * mt + 4 * g);
-    const float4 bb = *reinterpret_cast<const float4*>(sb + 16 * mt + 4 * g);
-    v[mt][0] = (v[mt][0] - mean) * rstd * gg.x + bb.x;
-    v[mt][1] = (v[mt][1] - mean) * rstd * gg.y + bb.y;
-    v[mt][2] = (v[mt][2] - mean) * rstd * gg.z + bb.z;
-    v[mt][3] = (v[mt][3] - mean) * rstd * gg.w + bb.w;
+    for (int t = 0; t < 2; ++t) acc[i] = mfma16(cl_afrag(sW, ld, 2 * hf + i, t), b[t], acc[i]);
   }
 }
-// CL residual dropout (same element hash as drop_rows: index row·C + channel)
-template <int NM>
-__device__ __forceinline__ void cl_drop(float (&v)[NM][4], const DropCfg& d, uint32_t sub, int gr) {
+// LayerNorm over the pair's 64 channels (in place on this wave's 32); sr: 8 waves × 16 rows float2
+__device__ __forceinline__ void cl2_layernorm(float (&v)[2][4], float2* sr, int hf, const float* sg, const float* sb,
+                                              float eps, float& mean, float& rstd) {
+  const int w = wave_id(), l = lane_id(), g = l >> 4;
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s += v[i][j];
+  const float ma = xor32_sum(xor16_sum(s)) * (1.f / 32.f);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { const float d = v[i][j] - ma; q = fmaf(d, d, q); }
+  const float m2a = xor32_sum(xor16_sum(q));
+  if (g == 0) sr[w * 16 + (l & 15)] = make_float2(ma, m2a);
+  lds_sync();
+  const float2 o = sr[(w ^ 4) * 16 + (l & 15)];
+  const float dm = ma - o.x;
+  mean = 0.5f * (ma + o.x);
+  rstd = rsqrtf((m2a + o.y + 16.f * dm * dm) * (1.f / 64.f) + eps);  // Chan: M2 = M2a + M2b + δ²·32·32/64
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = 16 * (2 * hf + i) + 4 * g;
+    const float4 gg = *reinterpret_cast<const float4*>(sg + c);
+    const float4 bb = *reinterpret_cast<const float4*>(sb + c);
+    v[i][0] = (v[i][0] - mean) * rstd * gg.x + bb.x;
+    v[i][1] = (v[i][1] - mean) * rstd * gg.y + bb.y;
+    v[i][2] = (v[i][2] - mean) * rstd * gg.z + bb.z;
+    v[i][3] = (v[i][3] - mean) * rstd * gg.w + bb.w;
+  }
+}
+// acc + bias (own channels)
+__device__ __forceinline__ void cl2_bias(float (&v)[2][4], const f32x4 (&acc)[2], const float* sb, int hf) {
+  const int g = lane_id() >> 4;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const float4 bb = *reinterpret_cast<const float4*>(sb + 16 * (2 * hf + i) + 4 * g);
+    v[i][0] = acc[i][0] + bb.x; v[i][1] = acc[i][1] + bb.y; v[i][2] = acc[i][2] + bb.z; v[i][3] = acc[i][3] + bb.w;
+  }
+}
+__device__ __forceinline__ void cl2_drop(float (&v)[2][4], const DropCfg& d, uint32_t sub, int gr, int hf) {
   if (d.thresh == 0u) return;
-  constexpr int C = 16 * NM;
   const uint32_t key = drop_key(d.seed, d.site, sub);
   const int g = lane_id() >> 4;
 #pragma unroll
-  for (int mt = 0; mt < NM; ++mt)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t idx = (uint32_t)gr * (uint32_t)C + (uint32_t)(16 * mt + 4 * g + i);
-      v[mt][i] = keep_elem(key, 0u, idx, d.thresh) ? v[mt][i] * d.scale : 0.f;
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t idx = (uint32_t)gr * 64u + (uint32_t)(16 * (2 * hf + i) + 4 * g + j);
+      v[i][j] = keep_elem(key, 0u, idx, d.thresh) ? v[i][j] * d.scale : 0.f;
     }
 }
-template <int NM>
-__device__ __forceinline__ void cl_store_f32(float* __restrict__ Y, int ld, int gr, const float (&v)[NM][4]) {
+__device__ __forceinline__ void cl2_store_f32(float* __restrict__ Y, int ld, int gr, int hf, const float (&v)[2][4]) {
   const int g = lane_id() >> 4;
 #pragma unroll
-  for (int mt = 0; mt < NM; ++mt)
-    *reinterpret_cast<float4*>(Y + (long long)gr * ld + 16 * mt + 4 * g) = make_float4(v[mt][0], v[mt][1], v[mt][2], v[mt][3]);
+  for (int i = 0; i < 2; ++i)
+    *reinterpret_cast<float4*>(Y + (long long)gr * ld + 16 * (2 * hf + i) + 4 * g) =
+        make_float4(v[i][0], v[i][1], v[i][2], v[i][3]);
 }
-template <int NM>
-__device__ __forceinline__ void cl_store_bf16(uint16_t* __restrict__ Y, int ld, int gr, const float (&v)[NM][4]) {
+__device__ __forceinline__ void cl2_store_bf16(uint16_t* __restrict__ Y, int ld, int gr, int hf, const float (&v)[2][4]) {
   const int g = lane_id() >> 4;
 #pragma unroll
-  for (int mt = 0; mt < NM; ++mt) {
+  for (int i = 0; i < 2; ++i) {
     uint2 pk;
-    pk.x = pack2(v[mt][0], v[mt][1]);
-    pk.y = pack2(v[mt][2], v[mt][3]);
-    *reinterpret_cast<uint2*>(Y + (long long)gr * ld + 16 * mt + 4 * g) = pk;
-  }
-}
-template <int NM>
-__device__ __forceinline__ void cl_load_f32(float (&v)[NM][4], const float* __restrict__ X, int ld, int gr) {
-  const int g = lane_id() >> 4;
-#pragma unroll
-  for (int mt = 0; mt < NM; ++mt) {
-    const float4 a = *reinterpret_cast<const float4*>(X + (long long)gr * ld + 16 * mt + 4 * g);
-    v[mt][0] = a.x; v[mt][1] = a.y; v[mt][2] = a.z; v[mt][3] = a.w;
-  }
-}
-// acc (CL) + bias vector from LDS
-template <int NM>
-__device__ __forceinline__ void cl_bias(float (&v)[NM][4], const f32x4 (&acc)[NM], const float* sb) {
-  const int g = lane_id() >> 4;
-#pragma unroll
-  for (int mt = 0; mt < NM; ++mt) {
-    const float4 bb = *reinterpret_cast<const float4*>(sb + 16 * mt + 4 * g);
-    v[mt][0] = acc[mt][0] + bb.x; v[mt][1] = acc[mt][1] + bb.y; v[mt][2] = acc[mt][2] + bb.z; v[mt][3] = acc[mt][3] + bb.w;
+    pk.x = pack2(v[i][0], v[i][1]);
+    pk.y = pack2(v[i][2], v[i][3]);
+    *reinterpret_cast<uint2*>(Y + (long long)gr * ld + 16 * (2 * hf + i) + 4 * g) = pk;
   }
 }
 
-// Fused latent self-attention layer forward, chain variant (same operands and results as
-// sa_layer_fwd_kernel; all operands 16-byte aligned, host-checked).  Phase 0 issues every load
-// and stages V, the four weight matrices (W1, W2, Wq permuted; Wo natural: its B operand, the
-// attention output, is read from LDS in natural order) and the bias / LN vectors into LDS; the
-// attention (wave = head) leaves O in LDS; after ONE barrier each wave runs the post-attention
-// chain of its 16 rows from registers.
+// The fused latent self-attention layer forward on 8 waves (same operands and results as
+// sa_layer_fwd_chain_kernel).  Attention: wave w = (head w & 3, 32-query block w >> 2).  The
+// post-attention chain: the paired CL2 layout above (5 pair exchanges: LN2, W1, W2, LN1, Wq).
 template <bool NEXT, int NQ>
-__global__ __launch_bounds__(256) void sa_layer_fwd_chain_kernel(
+__global__ __launch_bounds__(512) void sa_layer_fwd_chain8_kernel(
     const uint16_t* __restrict__ QKV, int N, float scale_log2, uint16_t* __restrict__ Oout, float* __restrict__ LSE,
     const float* __restrict__ X, const uint16_t* __restrict__ Wo, const float* __restrict__ bo,
     const float* __restrict__ g2, const float* __restrict__ be2, float eps, const uint16_t* __restrict__ W1,
@@ -160,82 +165,87 @@ __global__ __launch_bounds__(256) void sa_layer_fwd_chain_kernel(
     const float* __restrict__ lnw, const float* __restrict__ lnb, const uint16_t* __restrict__ Wq,
     const float* __restrict__ bq, uint16_t* __restrict__ QKVn, float* __restrict__ mean1, float* __restrict__ rstd1,
     DropCfg dr) {
-  constexpr int C = 64, H = 4, D = 16, LD = C + 8, LDV = C + 8, C3 = 3 * C, MAXKT = 8, NM = 4;
+  constexpr int C = 64, H = 4, D = 16, LD = C + 8, LDV = C + 8, C3 = 3 * C, MAXKT = 8, NT = 512;
   constexpr int nq = NQ * C, NWR = 3 * C + (NEXT ? nq : 0);  // weight rows staged: Wo, W1, W2 (+ Wq)
-  constexpr int NWC = NWR * 8 / 256;                          // 16-byte weight chunks per thread
+  constexpr int NWC = NWR * 8 / NT;                           // 16-byte weight chunks per thread
+  static_assert(NWR * 8 % NT == 0, "weight staging");
   __shared__ __attribute__((aligned(16))) uint16_t sV[256 * LDV + 64];  // V rows of the batch element (+ overrun)
   __shared__ __attribute__((aligned(16))) uint16_t sO[64 * LD];
   __shared__ __attribute__((aligned(16))) uint16_t sW[NWR * LD];        // Wo | W1 | W2 | Wq
   __shared__ __attribute__((aligned(16))) float sVec[7 * C + (NEXT ? nq : 0)];  // bo b1 b2 γ2 β2 γ1 β1 | bq
+  __shared__ __attribute__((aligned(16))) bf16x8 sX[2][8 * 64];           // pair fragment slots
+  __shared__ __attribute__((aligned(16))) float2 sR[2][8 * 16];           // pair LN slots
+  // the body is instantiated once per wave half (hf = qb = w >> 2, compile-time inside)
+  auto body = [&](auto hfc) {
+  constexpr int hf = decltype(hfc)::value, qb = hf;
   const int w = wave_id(), l = lane_id(), hh = l >> 5, r = l & 31;
-  const int m0 = blockIdx.x * 64;
+  // consecutive tiles (the tiles of one batch element, which all read its K / V) on one XCD, so
+  // the K / V rows come through that XCD's L2 once instead of once per tile
+  const int m0 = xcd_remap(blockIdx.x, gridDim.x) * 64;
   const int b = m0 / N;
   const long long rb = (long long)b * N;
   const int nkt = N / 32;
-  const int h = w;
+  const int h = w & 3;  // attention role: head h, query block qb; chain role: rows of pair w & 3, channel half hf
   const uint16_t* zp = reinterpret_cast<const uint16_t*>(kZero32B);
 
   // ---- phase 0: every load issued, branch-free (address selects) ----
   PIO_TS(0);
-  bf16x8 kf[MAXKT], qf[2], vr[8], wr[NWC];
+  bf16x8 kf[MAXKT], qf, vr[4], wr[NWC];
 #pragma unroll
   for (int kt = 0; kt < MAXKT; ++kt)
     kf[kt] = *reinterpret_cast<const bf16x8*>(kt < nkt ? QKV + (rb + 32 * kt + r) * C3 + C + h * D + 8 * hh : zp);
+  qf = *reinterpret_cast<const bf16x8*>(QKV + (long long)(m0 + 32 * qb + r) * C3 + h * D + 8 * hh);
 #pragma unroll
-  for (int qb = 0; qb < 2; ++qb)
-    qf[qb] = *reinterpret_cast<const bf16x8*>(QKV + (long long)(m0 + 32 * qb + r) * C3 + h * D + 8 * hh);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int c = threadIdx.x + 256 * i, key = c >> 3, col = (c & 7) * 8;
+  for (int i = 0; i < 4; ++i) {
+    const int c = threadIdx.x + NT * i, key = c >> 3, col = (c & 7) * 8;
     vr[i] = *reinterpret_cast<const bf16x8*>(key < N ? QKV + (rb + key) * C3 + 2 * C + col : zp);
   }
 #pragma unroll
   for (int i = 0; i < NWC; ++i) {
-    const int c = threadIdx.x + 256 * i, row = c >> 3, col = (c & 7) * 8;
+    const int c = threadIdx.x + NT * i, row = c >> 3, col = (c & 7) * 8;
     const uint16_t* src = row < C ? Wo + row * C : row < 2 * C ? W1 + (row - C) * C
                         : row < 3 * C ? W2 + (row - 2 * C) * C : Wq + (row - 3 * C) * C;
     wr[i] = *reinterpret_cast<const bf16x8*>(src + col);
   }
-  const int gr = m0 + 16 * w + (l & 15);  // this lane's chain row
-  float xr[NM][4];
-  cl_load_f32<NM>(xr, X, C, gr);
-  // bias / LN vectors: unconditional loads (address selects), predicated LDS stores
-  PIO_TS(1);
-  float pv[8];
-  {
-    const int k = threadIdx.x & (C - 1);
-    pv[0] = bo[k]; pv[1] = b1[k]; pv[2] = b2[k]; pv[3] = g2[k]; pv[4] = be2[k];
-    if constexpr (NEXT) {
-      pv[5] = lnw[k]; pv[6] = lnb[k];
-      pv[7] = bq[threadIdx.x < nq ? threadIdx.x : 0];
-    }
-  }
+  const int g = l >> 4;
+  const int gr = m0 + 16 * (w & 3) + (l & 15);  // this lane's chain row
+  float xr[2][4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int c = threadIdx.x + 256 * i, key = c >> 3, col = (c & 7) * 8;
+  for (int i = 0; i < 2; ++i) {
+    const float4 a = *reinterpret_cast<const float4*>(X + (long long)gr * C + 16 * (2 * hf + i) + 4 * g);
+    xr[i][0] = a.x; xr[i][1] = a.y; xr[i][2] = a.z; xr[i][3] = a.w;
+  }
+  PIO_TS(1);
+  float pv = 0.f;
+  {
+    // vector slots: [0, 7C) = bo b1 b2 γ2 β2 γ1 β1, [7C, 7C + nq) = bq (address selects)
+    const int k = threadIdx.x;
+    const int vi = k >> 6, kk = k & 63;
+    const float* src = vi == 0 ? bo : vi == 1 ? b1 : vi == 2 ? b2 : vi == 3 ? g2 : vi == 4 ? be2
+                     : vi == 5 ? (NEXT ? lnw : bo) : vi == 6 ? (NEXT ? lnb : bo) : bo;
+    pv = src[kk];  // unconditional (threads past 7C read bo and store nothing)
+  }
+  float pq = 0.f;
+  if constexpr (NEXT) pq = bq[(int)threadIdx.x < nq ? threadIdx.x : 0];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = threadIdx.x + NT * i, key = c >> 3, col = (c & 7) * 8;
     *reinterpret_cast<bf16x8*>(sV + key * LDV + col) = vr[i];
   }
-  if (threadIdx.x < C) {
-    const int k = threadIdx.x;
-    sVec[k] = pv[0]; sVec[C + k] = pv[1]; sVec[2 * C + k] = pv[2]; sVec[3 * C + k] = pv[3]; sVec[4 * C + k] = pv[4];
-    if constexpr (NEXT) { sVec[5 * C + k] = pv[5]; sVec[6 * C + k] = pv[6]; }
-  }
+  if ((int)threadIdx.x < 7 * C) sVec[threadIdx.x] = pv;
   if constexpr (NEXT)
-    if ((int)threadIdx.x < nq) sVec[7 * C + threadIdx.x] = pv[7];
+    if ((int)threadIdx.x < nq) sVec[7 * C + threadIdx.x] = pq;
 #pragma unroll
   for (int i = 0; i < NWC; ++i) {
-    const int c = threadIdx.x + 256 * i, row = c >> 3, col = (c & 7) * 8;
+    const int c = threadIdx.x + NT * i, row = c >> 3, col = (c & 7) * 8;
     cl_wstore(sW, LD, row, col, wr[i], row >= C);  // Wo natural, the rest permuted
   }
   PIO_TS(2);
   lds_sync();
   PIO_TS(3);
 
-  // ---- attention: wave h, two 32-query blocks; keys in chunks of 128 with an online softmax, so
-  // one chunk's 64 scores per lane live at a time (all 256 keys at once kept 128 accumulators
-  // live, which the allocator moved to AGPRs: ≈1,300 accvgpr copies per wave) ----
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
+  // ---- attention: head h, query block qb; keys in chunks of 128 with an online softmax ----
+  {
     float m_run = -INFINITY, l_run = 0.f;
     f32x16 o = f32x16{};
 #pragma unroll
@@ -248,7 +258,7 @@ __global__ __launch_bounds__(256) void sa_layer_fwd_chain_kernel(
           const int kt = 4 * ch + k;
           sc[k] = f32x16{};
           if (kt < nkt) {
-            sc[k] = mfma32(kf[kt], qf[qb], sc[k]);
+            sc[k] = mfma32(kf[kt], qf, sc[k]);
 #pragma unroll
             for (int i = 0; i < 16; ++i) mt = fmaxf(mt, sc[k][i]);
           }
@@ -295,76 +305,76 @@ __global__ __launch_bounds__(256) void sa_layer_fwd_chain_kernel(
   PIO_TS(4);
   lds_sync();
   PIO_TS(5);
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {  // the O tile for the backward
-    const int c = threadIdx.x + 256 * i, row = c >> 3, col = (c & 7) * 8;
-    *reinterpret_cast<bf16x8*>(Oout + (long long)(m0 + row) * C + col) =
-        *reinterpret_cast<const bf16x8*>(sO + row * LD + col);
+  {  // the O tile for the backward: one 16-byte chunk per thread
+    const int row = threadIdx.x >> 3, col = (threadIdx.x & 7) * 8;
+    *reinterpret_cast<bf16x8*>(Oout + (long long)(m0 + row) * C + col) = *reinterpret_cast<const bf16x8*>(sO + row * LD + col);
   }
 
-  // ---- the post-attention chain of this wave's 16 rows ----
-  const int g = l >> 4, lr = 16 * w + (l & 15);
+  // ---- the post-attention chain: pair w & 3, channel half hf ----
+  const int lr = 16 * (w & 3) + (l & 15);
   const uint16_t *sWo = sW, *sW1 = sW + C * LD, *sW2 = sW + 2 * C * LD, *sWq = sW + 3 * C * LD;
-  f32x4 acc[NM];
+  f32x4 acc[2];
   {
     bf16x8 bo_[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) bo_[t] = *reinterpret_cast<const bf16x8*>(sO + lr * LD + 32 * t + 8 * g);
-    cl_gemm<NM, 2>(sWo, LD, bo_, acc);
+    cl2_gemm(sWo, LD, hf, bo_, acc);
   }
   PIO_TS(6);
-  float y[NM][4], t0[NM][4];
-  cl_bias<NM>(t0, acc, sVec);
-  cl_drop<NM>(t0, dr, 0u, gr);
+  float y[2][4], t0[2][4];
+  cl2_bias(t0, acc, sVec, hf);
+  cl2_drop(t0, dr, 0u, gr, hf);
 #pragma unroll
-  for (int mt = 0; mt < NM; ++mt)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) y[mt][i] = xr[mt][i] + t0[mt][i];
-  cl_store_f32<NM>(Ysave, C, gr, y);
+    for (int j = 0; j < 4; ++j) { y[i][j] = xr[i][j] + t0[i][j]; t0[i][j] = y[i][j]; }
+  cl2_store_f32(Ysave, C, gr, hf, y);
   float mu, rs;
-#pragma unroll
-  for (int mt = 0; mt < NM; ++mt)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) t0[mt][i] = y[mt][i];
-  cl_layernorm<NM>(t0, sVec + 3 * C, sVec + 4 * C, eps, mu, rs);
-  if (g == 0) { mean2[gr] = mu; rstd2[gr] = rs; }
+  cl2_layernorm(t0, sR[0], hf, sVec + 3 * C, sVec + 4 * C, eps, mu, rs);
+  if (g == 0 && hf == 0) { mean2[gr] = mu; rstd2[gr] = rs; }
   PIO_TS(7);
   {
-    bf16x8 bb[2] = {cl_bfrag<NM>(t0, 0), cl_bfrag<NM>(t0, 1)};
-    cl_gemm<NM, 2>(sW1, LD, bb, acc);
+    bf16x8 bb[2];
+    cl2_swap_frag(sX[0], cl2_frag(t0), hf, bb);
+    cl2_gemm(sW1, LD, hf, bb, acc);
   }
-  cl_bias<NM>(t0, acc, sVec + C);
-  cl_store_bf16<NM>(Usave, C, gr, t0);
+  cl2_bias(t0, acc, sVec + C, hf);
+  cl2_store_bf16(Usave, C, gr, hf, t0);
 #pragma unroll
-  for (int mt = 0; mt < NM; ++mt)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) t0[mt][i] = gelu_f(t0[mt][i]);
+    for (int j = 0; j < 4; ++j) t0[i][j] = gelu_f(t0[i][j]);
   {
-    bf16x8 bb[2] = {cl_bfrag<NM>(t0, 0), cl_bfrag<NM>(t0, 1)};
-    cl_gemm<NM, 2>(sW2, LD, bb, acc);
+    bf16x8 bb[2];
+    cl2_swap_frag(sX[1], cl2_frag(t0), hf, bb);
+    cl2_gemm(sW2, LD, hf, bb, acc);
   }
-  cl_bias<NM>(t0, acc, sVec + 2 * C);
-  cl_drop<NM>(t0, dr, 1u, gr);
+  cl2_bias(t0, acc, sVec + 2 * C, hf);
+  cl2_drop(t0, dr, 1u, gr, hf);
 #pragma unroll
-  for (int mt = 0; mt < NM; ++mt)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) t0[mt][i] += y[mt][i];
-  cl_store_f32<NM>(Z, C, gr, t0);
+    for (int j = 0; j < 4; ++j) t0[i][j] += y[i][j];
+  cl2_store_f32(Z, C, gr, hf, t0);
   PIO_TS(8);
   if constexpr (NEXT) {
-    cl_layernorm<NM>(t0, sVec + 5 * C, sVec + 6 * C, eps, mu, rs);
-    if (g == 0) { mean1[gr] = mu; rstd1[gr] = rs; }
-    bf16x8 bb[2] = {cl_bfrag<NM>(t0, 0), cl_bfrag<NM>(t0, 1)};
+    cl2_layernorm(t0, sR[1], hf, sVec + 5 * C, sVec + 6 * C, eps, mu, rs);
+    if (g == 0 && hf == 0) { mean1[gr] = mu; rstd1[gr] = rs; }
+    bf16x8 bb[2];
+    cl2_swap_frag(sX[0], cl2_frag(t0), hf, bb);
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {  // 64 output channels at a time
-      f32x4 aq[NM];
-      cl_gemm<NM, 2>(sWq + q * C * LD, LD, bb, aq);
-      float v[NM][4];
-      cl_bias<NM>(v, aq, sVec + 7 * C + q * C);
-      cl_store_bf16<NM>(QKVn + q * C, nq, gr, v);
+    for (int q = 0; q < NQ; ++q) {  // 64 output channels at a time, this wave's half of them
+      f32x4 aq[2];
+      cl2_gemm(sWq + q * C * LD, LD, hf, bb, aq);
+      float v[2][4];
+      cl2_bias(v, aq, sVec + 7 * C + q * C, hf);
+      cl2_store_bf16(QKVn + q * C, nq, gr, hf, v);
     }
   }
   PIO_TS(9);
+  };
+  if (wave_id() >> 2) body(std::integral_constant<int, 1>{});
+  else body(std::integral_constant<int, 0>{});
 }
 
 // ------------------------------------------------------------------------------------
@@ -394,27 +404,6 @@ __device__ __forceinline__ bf16x8 frag16_tr_cl(const uint16_t* lds, int ld, int 
   r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
   r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
   return r;
-}
-// dXᵀ (4 m-tiles over C = 64 input channels) = Wᵀ·dYᵀ for a CL gradient dY (2 k-steps)
-__device__ __forceinline__ void cl_gemm_t(const uint16_t* sW, int ld, const bf16x8 (&b)[2], f32x4 (&acc)[4]) {
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-    acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int t = 0; t < 2; ++t) acc[mt] = mfma16(frag16_tr_cl(sW, ld, 16 * mt, t), b[t], acc[mt]);
-  }
-}
-// CL rows → a row-major bf16 LDS image [64][ld] (this wave's 16 rows)
-template <int NM>
-__device__ __forceinline__ void cl_tile_store(uint16_t* sT, int ld, const float (&v)[NM][4]) {
-  const int l = lane_id(), row = 16 * wave_id() + (l & 15), g = l >> 4;
-#pragma unroll
-  for (int mt = 0; mt < NM; ++mt) {
-    uint2 pk;
-    pk.x = pack2(v[mt][0], v[mt][1]);
-    pk.y = pack2(v[mt][2], v[mt][3]);
-    *reinterpret_cast<uint2*>(sT + row * ld + 16 * mt + 4 * g) = pk;
-  }
 }
 __device__ __forceinline__ bf16x8 ones_frag() {
   const short o = (short)0x3F80;  // bf16 1.0
@@ -476,10 +465,62 @@ constexpr int lpb_chain_smem() {
          2 * (NQ * 64 * 72 > 7 * 64 * 72 ? NQ * 64 * 72 : 7 * 64 * 72) + 4 * 4 * 64;
 }
 
-// TG: the element type of G (float, or uint16_t = bf16 straight from the attention backward's
-// bf16 outputs: the kernel consumes G only as bf16 MFMA operands, so both give identical results)
+// ------------------------------------------------------------------------------------
+// The layer-boundary backward on 8 waves (same operands and results as
+// ln_linear_post_attn_bwd_chain_kernel), paired chain layout CL2: wave w owns rows
+// 16(w & 3) + (l & 15), channel half hf = w >> 2.  The transposed products dXᵀ = Wᵀ·dYᵀ split
+// over the pair by output channels; each wave's k-step fragment of dY comes from its own
+// registers, the partner's from the bf16 row-major image of dY that phase C needs anyway
+// (written by the partner, one barrier).  LayerNorm backward sums: one float2 exchange each.
+// Phase C splits the parameter-gradient blocks over all 8 waves.
+// ------------------------------------------------------------------------------------
+// CL k-order fragment of k-step t of row lr from a row-major bf16 image [64][ld]
+__device__ __forceinline__ bf16x8 cl2_img_frag(const uint16_t* sT, int ld, int lr, int t) {
+  const int g = lane_id() >> 4;
+  const bf16x4 lo = *reinterpret_cast<const bf16x4*>(sT + lr * ld + 32 * t + 4 * g);
+  const bf16x4 hi = *reinterpret_cast<const bf16x4*>(sT + lr * ld + 32 * t + 16 + 4 * g);
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+// this wave's channels of its rows → a row-major bf16 image
+__device__ __forceinline__ void cl2_tile_store(uint16_t* sT, int ld, int lr, int hf, const float (&v)[2][4]) {
+  const int g = lane_id() >> 4;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    uint2 pk;
+    pk.x = pack2(v[i][0], v[i][1]);
+    pk.y = pack2(v[i][2], v[i][3]);
+    *reinterpret_cast<uint2*>(sT + lr * ld + 16 * (2 * hf + i) + 4 * g) = pk;
+  }
+}
+// dXᵀ (this wave's two m-tiles of the 64 input channels) = Wᵀ·dYᵀ over 2 k-steps
+__device__ __forceinline__ void cl2_gemm_t(const uint16_t* sW, int ld, int hf, const bf16x8 (&b)[2], f32x4 (&acc)[2]) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 2; ++t) acc[i] = mfma16(frag16_tr_cl(sW, ld, 16 * (2 * hf + i), t), b[t], acc[i]);
+  }
+}
+// pair totals of two per-row partial sums (each over this wave's 32 channels)
+__device__ __forceinline__ void cl2_pair_sums(float a, float b, float2* sr, float& ta, float& tb) {
+  const int w = wave_id(), l = lane_id();
+  a = xor32_sum(xor16_sum(a));
+  b = xor32_sum(xor16_sum(b));
+  if ((l >> 4) == 0) sr[w * 16 + (l & 15)] = make_float2(a, b);
+  lds_sync();
+  const float2 o = sr[(w ^ 4) * 16 + (l & 15)];
+  ta = a + o.x;
+  tb = b + o.y;
+}
+
+template <int NQ>
+constexpr int lpb_chain8_smem() { return lpb_chain_smem<NQ>() + 2 * 8 * 16 * 8; }
+
 template <int NQ, typename TG>
-__global__ __launch_bounds__(256) void ln_linear_post_attn_bwd_chain_kernel(
+__global__ __launch_bounds__(512) void ln_linear_post_attn_bwd_chain8_kernel(
     const TG* __restrict__ G, const uint16_t* __restrict__ Wq, const float* __restrict__ X,
     const float* __restrict__ mean1, const float* __restrict__ rstd1, const float* __restrict__ lnw,
     const float* __restrict__ lnb, const float* __restrict__ dres, float* __restrict__ dlnw, float* __restrict__ dlnb,
@@ -488,9 +529,10 @@ __global__ __launch_bounds__(256) void ln_linear_post_attn_bwd_chain_kernel(
     const uint16_t* __restrict__ Wo, const uint16_t* __restrict__ W1, const uint16_t* __restrict__ W2,
     const float* __restrict__ g2, const float* __restrict__ be2, float* __restrict__ dY, uint16_t* __restrict__ dO,
     float* __restrict__ delta, PostAttnGrads gr_out, int R, SlabJob job, DropCfg dr) {
-  constexpr int C = 64, LD = 72, NM = 4, nq = NQ * C, LDG = nq + 8, KT = nq / 32;
-  constexpr int NWC = (3 * C + nq) * 8 / 256;  // 16-byte weight chunks per thread
-  __shared__ __attribute__((aligned(16))) unsigned char smem[lpb_chain_smem<NQ>()];
+  constexpr int C = 64, LD = 72, nq = NQ * C, LDG = nq + 8, KT = nq / 32, NT = 512;
+  constexpr int NWC = (3 * C + nq) * 8 / NT;  // 16-byte weight chunks per thread
+  static_assert((3 * C + nq) * 8 % NT == 0 && KT % 2 == 0, "staging split");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[lpb_chain8_smem<NQ>()];
   uint16_t* sWo = reinterpret_cast<uint16_t*>(smem);
   uint16_t* sW1 = sWo + C * LD;
   uint16_t* sW2 = sW1 + C * LD;
@@ -506,215 +548,250 @@ __global__ __launch_bounds__(256) void ln_linear_post_attn_bwd_chain_kernel(
   uint16_t* sYm = sD2 + 64 * LD;       //   dY∘m₀
   uint16_t* sOt = sYm + 64 * LD;       //   O
   float* sVec = reinterpret_cast<float*>(smem + lpb_chain_smem<NQ>() - 4 * 4 * 64);  // γ1 β1 γ2 β2
+  float2* sR = reinterpret_cast<float2*>(smem + lpb_chain_smem<NQ>());              // 2 pair-sum slots
   zero_span_block(job);
   if ((int)blockIdx.x >= (R + 63) / 64) {  // appended workgroups: the previous kernel's slab job
     slab_reduce_block(job, blockIdx.x - (R + 63) / 64, reinterpret_cast<float4*>(smem));
     return;
   }
+  // the body is instantiated once per channel half (hf = w >> 2, a compile-time constant inside):
+  // every channel offset folds into the instructions instead of living in scalar registers
+  auto body = [&](auto hfc) {
+  constexpr int hf = decltype(hfc)::value;
   const int w = wave_id(), l = lane_id(), g = l >> 4;
-  const int gr = blockIdx.x * 64 + 16 * w + (l & 15);
+  const int lr = 16 * (w & 3) + (l & 15);
+  const int gr = blockIdx.x * 64 + lr;
 
-  // ---- phase 0: every load in flight ----
+  // ---- phase 0: every load in flight; G: this wave's half of the k-steps (t ≡ hf mod 2) ----
   PIO_TS(0);
   bf16x8 wr[NWC];
 #pragma unroll
   for (int i = 0; i < NWC; ++i) {
-    const int c = threadIdx.x + 256 * i, row = c >> 3, col = (c & 7) * 8;
+    const int c = threadIdx.x + NT * i, row = c >> 3, col = (c & 7) * 8;
     const uint16_t* src = row < C ? Wo + row * C : row < 2 * C ? W1 + (row - C) * C
                         : row < 3 * C ? W2 + (row - 2 * C) * C : Wq + (row - 3 * C) * C;
     wr[i] = *reinterpret_cast<const bf16x8*>(src + col);
   }
   constexpr bool GBF = sizeof(TG) == 2;
-  float4 gv[GBF ? 1 : KT][2];
-  bf16x8 gvb[GBF ? KT : 1];
+  constexpr int KH = KT / 2;
+  float4 gv[GBF ? 1 : KH][2];
+  bf16x8 gvb[GBF ? KH : 1];
 #pragma unroll
-  for (int t = 0; t < KT; ++t) {
+  for (int u = 0; u < KH; ++u) {
+    const int t = 2 * u + hf;
     const TG* p = G + (long long)gr * nq + 32 * t + 8 * g;
     if constexpr (GBF) {
-      gvb[t] = *reinterpret_cast<const bf16x8*>(p);
+      gvb[u] = *reinterpret_cast<const bf16x8*>(p);
     } else {
-      gv[t][0] = *reinterpret_cast<const float4*>(p);
-      gv[t][1] = *reinterpret_cast<const float4*>(p + 4);
+      gv[u][0] = *reinterpret_cast<const float4*>(p);
+      gv[u][1] = *reinterpret_cast<const float4*>(p + 4);
     }
   }
-  float xv[NM][4], dv[NM][4], yv[NM][4];
-  cl_load_f32<NM>(xv, X, C, gr);
-  cl_load_f32<NM>(dv, dres, C, gr);
-  cl_load_f32<NM>(yv, Ysave, C, gr);
-  uint2 ub[NM], obv[NM];
+  float xv[2][4], dv[2][4], yv[2][4];
+  uint2 ub[2], obv[2];
 #pragma unroll
-  for (int mt = 0; mt < NM; ++mt) {
-    ub[mt] = *reinterpret_cast<const uint2*>(U + (long long)gr * C + 16 * mt + 4 * g);
-    obv[mt] = *reinterpret_cast<const uint2*>(O + (long long)gr * C + 16 * mt + 4 * g);
+  for (int i = 0; i < 2; ++i) {
+    const int c = 16 * (2 * hf + i) + 4 * g;
+    const float4 a = *reinterpret_cast<const float4*>(X + (long long)gr * C + c);
+    const float4 d = *reinterpret_cast<const float4*>(dres + (long long)gr * C + c);
+    const float4 y = *reinterpret_cast<const float4*>(Ysave + (long long)gr * C + c);
+    xv[i][0] = a.x; xv[i][1] = a.y; xv[i][2] = a.z; xv[i][3] = a.w;
+    dv[i][0] = d.x; dv[i][1] = d.y; dv[i][2] = d.z; dv[i][3] = d.w;
+    yv[i][0] = y.x; yv[i][1] = y.y; yv[i][2] = y.z; yv[i][3] = y.w;
+    ub[i] = *reinterpret_cast<const uint2*>(U + (long long)gr * C + c);
+    obv[i] = *reinterpret_cast<const uint2*>(O + (long long)gr * C + c);
   }
   const float mu1 = mean1[gr], rs1 = rstd1[gr], mu2 = mean2[gr], rs2 = rstd2[gr];
   PIO_TS(1);
-  float pv[4];
+  float pv;
   {
-    const int k = threadIdx.x & (C - 1);
-    pv[0] = lnw[k]; pv[1] = lnb[k]; pv[2] = g2[k]; pv[3] = be2[k];
+    const int k = threadIdx.x & (C - 1), vi = (threadIdx.x >> 6) & 3;
+    pv = (vi == 0 ? lnw : vi == 1 ? lnb : vi == 2 ? g2 : be2)[k];
   }
 #pragma unroll
   for (int i = 0; i < NWC; ++i) {
-    const int c = threadIdx.x + 256 * i, row = c >> 3, col = (c & 7) * 8;
+    const int c = threadIdx.x + NT * i, row = c >> 3, col = (c & 7) * 8;
     uint16_t* dst = row < 3 * C ? sWo + row * LD : sWq + (row - 3 * C) * LD;
     *reinterpret_cast<bf16x8*>(dst + col) = wr[i];
   }
-  if (threadIdx.x < C) {
-    const int k = threadIdx.x;
-    sVec[k] = pv[0]; sVec[C + k] = pv[1]; sVec[2 * C + k] = pv[2]; sVec[3 * C + k] = pv[3];
+  if (threadIdx.x < 4 * C) sVec[threadIdx.x] = pv;
+  bf16x8 gb[KT];
+#pragma unroll
+  for (int u = 0; u < KH; ++u) {
+    const int t = 2 * u + hf;
+    if constexpr (GBF) {
+      gb[t] = gvb[u];
+    } else {
+      const float4 a = gv[u][0], b = gv[u][1];
+      gb[t][0] = (short)f2bf(a.x); gb[t][1] = (short)f2bf(a.y); gb[t][2] = (short)f2bf(a.z); gb[t][3] = (short)f2bf(a.w);
+      gb[t][4] = (short)f2bf(b.x); gb[t][5] = (short)f2bf(b.y); gb[t][6] = (short)f2bf(b.z); gb[t][7] = (short)f2bf(b.w);
+    }
+    *reinterpret_cast<bf16x8*>(sG + lr * LDG + 32 * t + 8 * g) = gb[t];
   }
   PIO_TS(2);
   lds_sync();
   PIO_TS(3);
+#pragma unroll
+  for (int u = 0; u < KH; ++u) {  // the partner's k-steps of G, from the image
+    const int t = 2 * u + 1 - hf;
+    gb[t] = *reinterpret_cast<const bf16x8*>(sG + lr * LDG + 32 * t + 8 * g);
+  }
 
-  // ---- A: LN1 + QKV backward of layer l+1 → dZ of layer l ----
-  f32x4 acc[NM];
-  {
-    bf16x8 gb[KT];
+  // ---- A: LN1 + QKV backward of layer l+1 → dZ of layer l (this wave's channels) ----
+  f32x4 acc[2];
 #pragma unroll
-    for (int t = 0; t < KT; ++t) {
-      if constexpr (GBF) {
-        gb[t] = gvb[t];
-      } else {
-        const float4 a = gv[t][0], b = gv[t][1];
-        gb[t][0] = (short)f2bf(a.x); gb[t][1] = (short)f2bf(a.y); gb[t][2] = (short)f2bf(a.z); gb[t][3] = (short)f2bf(a.w);
-        gb[t][4] = (short)f2bf(b.x); gb[t][5] = (short)f2bf(b.y); gb[t][6] = (short)f2bf(b.z); gb[t][7] = (short)f2bf(b.w);
-      }
-      *reinterpret_cast<bf16x8*>(sG + (16 * w + (l & 15)) * LDG + 32 * t + 8 * g) = gb[t];
-    }
+  for (int i = 0; i < 2; ++i) {
+    acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int mt = 0; mt < NM; ++mt) {
-      acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int t = 0; t < KT; ++t) acc[mt] = mfma16(frag16_tr(sWq, LD, 16 * mt, 32 * t), gb[t], acc[mt]);
-    }
+    for (int t = 0; t < KT; ++t) acc[i] = mfma16(frag16_tr(sWq, LD, 16 * (2 * hf + i), 32 * t), gb[t], acc[i]);
   }
   PIO_TS(4);
-  float dz[NM][4], t0[NM][4];
+  float dz[2][4], t0[2][4];
   {
-    float gg[NM][4];
+    float gg[2][4], s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int mt = 0; mt < NM; ++mt) {
-      const float4 ga = *reinterpret_cast<const float4*>(sVec + 16 * mt + 4 * g);
+    for (int i = 0; i < 2; ++i) {
+      const float4 ga = *reinterpret_cast<const float4*>(sVec + 16 * (2 * hf + i) + 4 * g);
       const float gw[4] = {ga.x, ga.y, ga.z, ga.w};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        xv[mt][i] = (xv[mt][i] - mu1) * rs1;  // x̂
-        t0[mt][i] = acc[mt][i];               // dXn1
-        gg[mt][i] = acc[mt][i] * gw[i];
-        dz[mt][i] = gg[mt][i] * xv[mt][i];
+      for (int j = 0; j < 4; ++j) {
+        xv[i][j] = (xv[i][j] - mu1) * rs1;  // x̂
+        t0[i][j] = acc[i][j];               // dXn1
+        gg[i][j] = acc[i][j] * gw[j];
+        s1 += gg[i][j];
+        s2 += gg[i][j] * xv[i][j];
       }
     }
-    const float s1 = cl_rowsum<NM>(gg) / C, s2 = cl_rowsum<NM>(dz) / C;
+    // also the barrier after which no wave reads the Wq image any more (the PA images overlay it)
+    cl2_pair_sums(s1, s2, sR, s1, s2);
+    s1 *= 1.f / C;
+    s2 *= 1.f / C;
 #pragma unroll
-    for (int mt = 0; mt < NM; ++mt)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) dz[mt][i] = rs1 * (gg[mt][i] - s1 - xv[mt][i] * s2) + dv[mt][i];
+      for (int j = 0; j < 4; ++j) dz[i][j] = rs1 * (gg[i][j] - s1 - xv[i][j] * s2) + dv[i][j];
   }
-  cl_tile_store<NM>(sX1, LD, xv);
-  cl_tile_store<NM>(sD1, LD, t0);
+  cl2_tile_store(sX1, LD, lr, hf, xv);
+  cl2_tile_store(sD1, LD, lr, hf, t0);
   PIO_TS(5);
-  lds_sync();  // every wave is done with the Wq image: the PA images overlay it
-  PIO_TS(6);
 
   // ---- B: post-attention backward of layer l ----
-  float gp[NM][4];
+  float gp[2][4];
 #pragma unroll
-  for (int mt = 0; mt < NM; ++mt) {
-    const float u4[4] = {bf2f((uint16_t)(ub[mt].x & 0xFFFF)), bf2f((uint16_t)(ub[mt].x >> 16)),
-                         bf2f((uint16_t)(ub[mt].y & 0xFFFF)), bf2f((uint16_t)(ub[mt].y >> 16))};
+  for (int i = 0; i < 2; ++i) {
+    const float u4[4] = {bf2f((uint16_t)(ub[i].x & 0xFFFF)), bf2f((uint16_t)(ub[i].x >> 16)),
+                         bf2f((uint16_t)(ub[i].y & 0xFFFF)), bf2f((uint16_t)(ub[i].y >> 16))};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) gelu_pair(u4[i], t0[mt][i], gp[mt][i]);
+    for (int j = 0; j < 4; ++j) gelu_pair(u4[j], t0[i][j], gp[i][j]);
   }
-  cl_tile_store<NM>(sGu, LD, t0);
+  cl2_tile_store(sGu, LD, lr, hf, t0);
 #pragma unroll
-  for (int mt = 0; mt < NM; ++mt)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) t0[mt][i] = dz[mt][i];
-  cl_drop<NM>(t0, dr, 1u, gr);  // dZ∘m₁: the MLP output layer's gradient
-  cl_tile_store<NM>(sZm, LD, t0);
+    for (int j = 0; j < 4; ++j) t0[i][j] = dz[i][j];
+  cl2_drop(t0, dr, 1u, gr, hf);  // dZ∘m₁: the MLP output layer's gradient
+  cl2_tile_store(sZm, LD, lr, hf, t0);
   {
-    bf16x8 bb[2] = {cl_bfrag<NM>(t0, 0), cl_bfrag<NM>(t0, 1)};
-    cl_gemm_t(sW2, LD, bb, acc);  // dH
+    bf16x8 bb[2];
+    bb[hf] = cl2_frag(t0);
+    lds_sync();
+    bb[1 - hf] = cl2_img_frag(sZm, LD, lr, 1 - hf);
+    cl2_gemm_t(sW2, LD, hf, bb, acc);  // dH
+  }
+  PIO_TS(6);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) t0[i][j] = acc[i][j] * gp[i][j];  // dU
+  cl2_tile_store(sDu, LD, lr, hf, t0);
+  {
+    bf16x8 bb[2];
+    bb[hf] = cl2_frag(t0);
+    lds_sync();
+    bb[1 - hf] = cl2_img_frag(sDu, LD, lr, 1 - hf);
+    cl2_gemm_t(sW1, LD, hf, bb, acc);  // dXn2
   }
   PIO_TS(7);
-#pragma unroll
-  for (int mt = 0; mt < NM; ++mt)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) t0[mt][i] = acc[mt][i] * gp[mt][i];  // dU
-  cl_tile_store<NM>(sDu, LD, t0);
   {
-    bf16x8 bb[2] = {cl_bfrag<NM>(t0, 0), cl_bfrag<NM>(t0, 1)};
-    cl_gemm_t(sW1, LD, bb, acc);  // dXn2
-  }
-  {
-    float gg[NM][4];
+    float gg[2][4], s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int mt = 0; mt < NM; ++mt) {
-      const float4 ga = *reinterpret_cast<const float4*>(sVec + 2 * C + 16 * mt + 4 * g);
+    for (int i = 0; i < 2; ++i) {
+      const float4 ga = *reinterpret_cast<const float4*>(sVec + 2 * C + 16 * (2 * hf + i) + 4 * g);
       const float gw[4] = {ga.x, ga.y, ga.z, ga.w};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        yv[mt][i] = (yv[mt][i] - mu2) * rs2;  // ŷ
-        t0[mt][i] = acc[mt][i];               // dXn2
-        gg[mt][i] = acc[mt][i] * gw[i];
-        gp[mt][i] = gg[mt][i] * yv[mt][i];
+      for (int j = 0; j < 4; ++j) {
+        yv[i][j] = (yv[i][j] - mu2) * rs2;  // ŷ
+        t0[i][j] = acc[i][j];               // dXn2
+        gg[i][j] = acc[i][j] * gw[j];
+        s1 += gg[i][j];
+        s2 += gg[i][j] * yv[i][j];
       }
     }
-    const float s1 = cl_rowsum<NM>(gg) / C, s2 = cl_rowsum<NM>(gp) / C;
+    cl2_pair_sums(s1, s2, sR + 8 * 16, s1, s2);
+    s1 *= 1.f / C;
+    s2 *= 1.f / C;
 #pragma unroll
-    for (int mt = 0; mt < NM; ++mt)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) dz[mt][i] += rs2 * (gg[mt][i] - s1 - yv[mt][i] * s2);  // dY
+      for (int j = 0; j < 4; ++j) dz[i][j] += rs2 * (gg[i][j] - s1 - yv[i][j] * s2);  // dY
+  }
+  cl2_tile_store(sYh, LD, lr, hf, yv);
+  cl2_tile_store(sD2, LD, lr, hf, t0);
+  cl2_store_f32(dY, C, gr, hf, dz);
+  cl2_drop(dz, dr, 0u, gr, hf);  // dY∘m₀: the out-projection's gradient
+  cl2_tile_store(sYm, LD, lr, hf, dz);
+  {
+    bf16x8 bb[2];
+    bb[hf] = cl2_frag(dz);
+    lds_sync();
+    bb[1 - hf] = cl2_img_frag(sYm, LD, lr, 1 - hf);
+    cl2_gemm_t(sWo, LD, hf, bb, acc);  // dO
   }
   PIO_TS(8);
-  cl_tile_store<NM>(sYh, LD, yv);
-  cl_tile_store<NM>(sD2, LD, t0);
-  cl_store_f32<NM>(dY, C, gr, dz);
-  cl_drop<NM>(dz, dr, 0u, gr);  // dY∘m₀: the out-projection's gradient
-  cl_tile_store<NM>(sYm, LD, dz);
   {
-    bf16x8 bb[2] = {cl_bfrag<NM>(dz, 0), cl_bfrag<NM>(dz, 1)};
-    cl_gemm_t(sWo, LD, bb, acc);  // dO
-  }
-  {
-    float ov[NM][4], dd[NM];
+    float ov[2][4], dd[2];
 #pragma unroll
-    for (int mt = 0; mt < NM; ++mt) {
-      ov[mt][0] = bf2f((uint16_t)(obv[mt].x & 0xFFFF)); ov[mt][1] = bf2f((uint16_t)(obv[mt].x >> 16));
-      ov[mt][2] = bf2f((uint16_t)(obv[mt].y & 0xFFFF)); ov[mt][3] = bf2f((uint16_t)(obv[mt].y >> 16));
-      float s = 0.f;
+    for (int i = 0; i < 2; ++i) {
+      ov[i][0] = bf2f((uint16_t)(obv[i].x & 0xFFFF)); ov[i][1] = bf2f((uint16_t)(obv[i].x >> 16));
+      ov[i][2] = bf2f((uint16_t)(obv[i].y & 0xFFFF)); ov[i][3] = bf2f((uint16_t)(obv[i].y >> 16));
+      float sacc = 0.f;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        t0[mt][i] = bf2f(f2bf(acc[mt][i]));  // dO as the attention backward sees it
-        s += t0[mt][i] * ov[mt][i];
+      for (int j = 0; j < 4; ++j) {
+        t0[i][j] = bf2f(f2bf(acc[i][j]));  // dO as the attention backward sees it
+        sacc += t0[i][j] * ov[i][j];
       }
-      dd[mt] = xor32_sum(xor16_sum(s));  // head mt = channels 16mt .. 16mt + 15
+      dd[i] = xor32_sum(xor16_sum(sacc));  // head 2hf + i = channels 16(2hf + i) .. + 15
     }
-    cl_store_bf16<NM>(dO, C, gr, t0);
-    if (g == 0) *reinterpret_cast<float4*>(delta + (long long)gr * 4) = make_float4(dd[0], dd[1], dd[2], dd[3]);
-    cl_tile_store<NM>(sOt, LD, ov);
+    cl2_store_bf16(dO, C, gr, hf, t0);
+    if (g == 0) *reinterpret_cast<float2*>(delta + (long long)gr * 4 + 2 * hf) = make_float2(dd[0], dd[1]);
+    cl2_tile_store(sOt, LD, lr, hf, ov);
   }
   PIO_TS(9);
   lds_sync();
   PIO_TS(10);
 
-  // ---- C: parameter gradients of the tile → slab row blockIdx.x ----
+  // ---- C: parameter gradients of the tile → slab row blockIdx.x, 16-row blocks over 8 waves ----
   const int vrs = gr_out.vrs;
   const long long so = (long long)blockIdx.x * vrs;
   const float *gam1 = sVec, *bet1 = sVec + C, *gam2 = sVec + 2 * C, *bet2 = sVec + 3 * C;
   auto sp = [&](float* p) { return p + so; };  // this tile's slab row
-  cl_wgrad_block(sZm, LD, w, sGu, LD, nullptr, nullptr, sp(gr_out.dW2), sp(gr_out.db2));
-  cl_wgrad_block(sDu, LD, w, sYh, LD, gam2, bet2, sp(gr_out.dW1), sp(gr_out.db1));
-  cl_wgrad_block(sYm, LD, w, sOt, LD, nullptr, nullptr, sp(gr_out.dWo), sp(gr_out.dbo));
-  cl_ln_grads(sD2, sYh, LD, w, sp(gr_out.dg2), sp(gr_out.dbe2));
-  PIO_TS(11);
+  const int p4 = w & 3;
+  if constexpr (hf == 0) {
+    cl_wgrad_block(sZm, LD, p4, sGu, LD, nullptr, nullptr, sp(gr_out.dW2), sp(gr_out.db2));
+    cl_wgrad_block(sYm, LD, p4, sOt, LD, nullptr, nullptr, sp(gr_out.dWo), sp(gr_out.dbo));
+    cl_wgrad_block(sG, LDG, p4, sX1, LD, gam1, bet1, sp(dWq), sp(dbq));  // dWq rows 16p4 ..
+    cl_ln_grads(sD2, sYh, LD, p4, sp(gr_out.dg2), sp(gr_out.dbe2));
+  } else {
+    cl_wgrad_block(sDu, LD, p4, sYh, LD, gam2, bet2, sp(gr_out.dW1), sp(gr_out.db1));
 #pragma unroll
-  for (int q = 0; q < NQ; ++q)  // 16-row blocks w, w + 4, w + 8 of dWq (nq rows)
-    cl_wgrad_block(sG, LDG, w + 4 * q, sX1, LD, gam1, bet1, sp(dWq), sp(dbq));
-  cl_ln_grads(sD1, sX1, LD, w, sp(dlnw), sp(dlnb));
-  PIO_TS(12);
+    for (int q = 1; q < NQ; ++q)  // dWq 16-row blocks p4 + 4q
+      cl_wgrad_block(sG, LDG, p4 + 4 * q, sX1, LD, gam1, bet1, sp(dWq), sp(dbq));
+    cl_ln_grads(sD1, sX1, LD, p4, sp(dlnw), sp(dlnb));
+  }
+  PIO_TS(11);
+  };
+  if (wave_id() >> 2) body(std::integral_constant<int, 1>{});
+  else body(std::integral_constant<int, 0>{});
 }
 
 // ---- launchers (called by rowgemm.hip's launchers once the operands qualify: C = 64, H = 4,
@@ -728,14 +805,19 @@ bool sa_layer_fwd_chain_launch(const uint16_t* QKV, int N, float scale_log2, uin
   const bool next = Wq != nullptr;
   if (next && nq != 64 && nq != 128 && nq != 192) return false;
   dim3 grid(R / 64);
-#define SAC(NX, NQ)                                                                                                   \
-  hipLaunchKernelGGL((sa_layer_fwd_chain_kernel<NX, NQ>), grid, dim3(256), 0, st, QKV, N, scale_log2, O, LSE, X, Wo, bo, \
+#define SAC(NX, NQ)                                                                                                 \
+  hipLaunchKernelGGL((sa_layer_fwd_chain8_kernel<NX, NQ>), grid, dim3(512), 0, st, QKV, N, scale_log2, O, LSE, X, Wo, bo, \
                      g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, lnw, lnb, Wq, bq, QKVn, mean1,      \
                      rstd1, dr)
-  if (!next) SAC(false, 3);
-  else if (nq == 64) SAC(true, 1);
-  else if (nq == 128) SAC(true, 2);
-  else SAC(true, 3);
+  if (!next) {
+    SAC(false, 3);
+  } else if (nq == 64) {
+    SAC(true, 1);
+  } else if (nq == 128) {
+    SAC(true, 2);
+  } else {
+    SAC(true, 3);
+  }
 #undef SAC
   return true;
 }
@@ -751,9 +833,9 @@ bool ln_linear_post_attn_bwd_chain_launch(const void* G, bool g_bf16, const uint
   if (nq != 192 && nq != 64) return false;
   dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0));
 #define LPC(NQ, TG)                                                                                                    \
-  hipLaunchKernelGGL((ln_linear_post_attn_bwd_chain_kernel<NQ, TG>), grid, dim3(256), 0, st, static_cast<const TG*>(G), \
-                     Wq, X, mean1, rstd1, lnw, lnb, dres, dlnw, dlnb, dWq, dbq, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2,  \
-                     be2, dY, dO, delta, grads, R, job, dr)
+  hipLaunchKernelGGL((ln_linear_post_attn_bwd_chain8_kernel<NQ, TG>), grid, dim3(512), 0, st, static_cast<const TG*>(G), \
+                     Wq, X, mean1, rstd1, lnw, lnb, dres, dlnw, dlnb, dWq, dbq, Ysave, mean2, rstd2, U, O, Wo, W1, W2,    \
+                     g2, be2, dY, dO, delta, grads, R, job, dr)
   if (g_bf16) {
     if (nq != 192) return false;  // bf16 G only from the self-attention backward (nq = 3C)
     LPC(3, uint16_t);

@@ -307,20 +307,22 @@ __device__ __forceinline__ void zero_span_block(const SlabJob& j) {
 // Deterministic mode: one workgroup per column block sums all S rows in a fixed order and
 // adds once (single writer).
 constexpr int kSlabColsPerBlock = 1024;
-// part: ≥ 4 KiB of 16-B aligned LDS (deterministic path)
+// part: ≥ 4 KiB of 16-B aligned LDS (deterministic path).  The job runs on the first 256
+// threads of the carrier's workgroup (256 or 512 threads; the others only join the barrier).
 __device__ __forceinline__ void slab_reduce_block(const SlabJob& j, int b, float4* part) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int P = j.P;
   if (j.det) {  // fixed summation order, a single writer per element: bitwise reproducible
     const int cb = b * 256, c = cb + 4 * l;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (c < P)
+    if (c < P && w < 4)
       for (int s = w; s < j.S; s += 4) {
         const float4 v = *reinterpret_cast<const float4*>(j.slab + (long long)s * P + c);
         acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
       }
-    part[w * 64 + l] = acc;
+    if (w < 4) part[w * 64 + l] = acc;
     __syncthreads();
+    if (w >= 4) return;
     const float* pf = reinterpret_cast<const float*>(part);
     const int k = 64 * w + l, col = cb + k;
     if (col >= P) return;
@@ -331,6 +333,7 @@ __device__ __forceinline__ void slab_reduce_block(const SlabJob& j, int b, float
     }
     return;
   }
+  if (threadIdx.x >= 256) return;
   const int nsy = j.nblk / j.nbx, rb = (j.S + nsy - 1) / nsy;
   const int bx = b % j.nbx, by = b / j.nbx;
   const int c = bx * kSlabColsPerBlock + 4 * (int)threadIdx.x;

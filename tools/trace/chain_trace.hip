@@ -63,7 +63,7 @@ static void trace(const char* name, int R, F launch) {
   CK(hipDeviceSynchronize());
   std::vector<long long> t(16 * 64);
   CK(hipMemcpy(t.data(), tb, t.size() * 8, hipMemcpyDeviceToHost));
-  for (int wv = 0; wv < 4; ++wv) {
+  for (int wv = 0; wv < 16; ++wv) {
     long long prev = t[wv * 64];
     if (!prev) continue;
     printf("  wave %d:", wv);
