@@ -53,7 +53,7 @@ void attn_bwd_launch(const AttnArgs&, int, const uint16_t*, const uint16_t*, con
 int attn_bwd_key_blocks(int, int);
 bool attn_bwd_bf16_ok(const AttnArgs&, int);
 bool attn_bwd_bf16_launch(const AttnArgs&, int, const uint16_t*, const float*, const float*, uint16_t*, long long, int,
-                          uint16_t*, long long, int, uint16_t*, long long, int, hipStream_t);
+                          uint16_t*, long long, int, uint16_t*, long long, int, const SlabJob&, hipStream_t);
 int attn_bwd_zero_plan(int, int, int, int, int);
 void ln_linear_fwd_launch(const void*, bool, int, int, int, const float*, const float*, float, const uint16_t*, int,
                           const float*, int, int, const float*, int, void*, bool, int, float*, float*, const float*, int,
@@ -89,6 +89,15 @@ void wgrad_launch(const void*, bool, int, int, const void*, bool, int, int, int,
 void ce_fwd_launch(int, const float*, const int64_t*, const int64_t*, const uint16_t*, const float*, int, int, float*,
                    float*, float*, float*, float*, float*, unsigned*, uint16_t*, int, float*, long long, int, hipStream_t);
 int ce_combine_blocks(int);
+int ce2_num_splits(int, int);
+int ce2_bwd_splits(int, int);
+int ce2_combine_blocks(int);
+void ce2_fwd_launch(const float*, const int64_t*, const int64_t*, const uint16_t*, const float*, int, int, int, float2*,
+                    float*, float*, uint16_t*, float*, float*, float*, int, float*, float*, unsigned*, float*, long long,
+                    hipStream_t);
+void ce2_bwd_launch(const uint16_t*, const int64_t*, const uint16_t*, const float*, const float*, const float*,
+                    const float*, const float*, int, int, float*, float*, float*, int, float*, long long, const int64_t*,
+                    hipStream_t);
 int ce_num_splits(int, int);
 int ce_dw_splits(int, int);
 void mlm_select_launch(const int64_t*, int, int, int, int, int64_t*, int64_t*, int*, int64_t*, int64_t*, float*, bool*, bool*,
@@ -268,10 +277,14 @@ std::vector<Tensor> attn_fwd(Tensor q, Tensor k, Tensor v, OptT kmask, int64_t H
 // a dq_out view must be batch-dense (batch stride == Nq * row stride); it needs no zero fill
 // (the launcher clears it itself when several key blocks accumulate into it).  delta_in ((B, Nq, H) fp32 rowsum(dO∘O), e.g. from post_attn_bwd)
 // skips the delta pass.
+void slab_reduce(Tensor slab, std::vector<Tensor> dsts, std::vector<int64_t> offs);
+namespace {
+pio::SlabJob make_job(const OptT& slab, std::vector<Tensor>& dsts, const std::vector<int64_t>& offs);
+}
 std::vector<Tensor> attn_bwd(Tensor q, Tensor k, Tensor v, OptT kmask, Tensor o, Tensor dO, Tensor lse, OptT delta_in,
                              int64_t H, int64_t D, double scale, double dropout_p, OptT seed, OptT dq_out,
                              OptT dk_out, OptT dv_out, bool kv_accumulate, int64_t site, bool dq_zeroed,
-                             bool kv_zeroed) {
+                             bool kv_zeroed, OptT job_slab, std::vector<Tensor> job_dsts, std::vector<int64_t> job_offs) {
   auto a = make_args(q, k, v, kmask, (int)H, (int)D, scale, dropout_p, seed, site);
   TORCH_CHECK(dO.is_contiguous() && o.is_contiguous(), "O / dO must be contiguous (B, Nq, H*D)");
   auto f32 = q.options().dtype(torch::kFloat32);
@@ -289,13 +302,17 @@ std::vector<Tensor> attn_bwd(Tensor q, Tensor k, Tensor v, OptT kmask, Tensor o,
     if (pio::attn_bwd_bf16_ok(a, (int)D)) {
       pio::attn_bwd_bf16_launch(a, (int)D, bfp(dO), f32p(lse), delta.data_ptr<float>(), bfp_mut(dq), dq.stride(0),
                                 (int)dq.stride(1), bfp_mut(dk), dk.stride(0), (int)dk.stride(1), bfp_mut(dv),
-                                dv.stride(0), (int)dv.stride(1), stream());
+                                dv.stride(0), (int)dv.stride(1), make_job(job_slab, job_dsts, job_offs), stream());
     } else {  // shape not covered by the bf16 variant: fp32, then narrowed
       auto r = attn_bwd(q, k, v, kmask, o, dO, lse, delta_in, H, D, scale, dropout_p, seed, c10::nullopt, c10::nullopt,
-                        c10::nullopt, false, site, false, false);
+                        c10::nullopt, false, site, false, false, job_slab, job_dsts, job_offs);
       dq.copy_(r[0]); dk.copy_(r[1]); dv.copy_(r[2]);
     }
     return {dq, dk, dv};
+  }
+  if (job_slab.has_value()) {  // the fp32 variants carry no job: run it as its own launch first
+    auto jd = job_dsts;
+    slab_reduce(*job_slab, jd, job_offs);
   }
   Tensor dq = dq_out.has_value() ? *dq_out : torch::empty({a.B, a.Nq, H * D}, f32);
   Tensor dk = dk_out.has_value() ? *dk_out : torch::empty({a.B, a.Nk, H * D}, f32);
@@ -781,6 +798,35 @@ std::vector<Tensor> ce_fwd(Tensor h, OptT idx, Tensor labels, Tensor w, Tensor b
   TORCH_CHECK(idx.has_value() || h.size(0) == M, "ce_fwd: h must have one row per label without idx");
   const int64_t* ip = opt_idx(idx, M);
   auto f32 = h.options().dtype(torch::kFloat32);
+  if (C == 64) {
+    // two-pass head (ce_head.hip): the forward also forms u = Σ_v p·W − W[label] per row, the
+    // hidden-state gradient up to the row-loss scale; returned as a 4th output for ce_bwd
+    const int ns = pio::ce2_num_splits(M, V);
+    Tensor pml = torch::empty({ns, M, 2}, f32), pacc = torch::empty({ns, M, C}, f32);
+    Tensor picked = torch::empty({M}, f32), lse = torch::empty({M}, f32), loss = torch::empty({}, f32);
+    Tensor u = torch::empty({M, C}, f32);
+    Tensor blk = torch::empty({2 * pio::ce2_combine_blocks(M)}, f32);
+    Tensor hs = torch::empty({M, C}, h.options().dtype(torch::kBFloat16));
+    TORCH_CHECK(count.numel() >= 1 && count.is_contiguous(), "ce_fwd: count must hold one fp32 value");
+    float* zp = nullptr;
+    int64_t zn = 0;
+    if (zero_out.has_value()) {
+      CHECK_DT(*zero_out, torch::kFloat32);
+      TORCH_CHECK(zero_out->is_contiguous() && zero_out->numel() % 4 == 0 && zero_out->get_device() == h.get_device() &&
+                      reinterpret_cast<uintptr_t>(zero_out->data_ptr()) % 16 == 0,
+                  "ce_fwd: zero_out must be a contiguous, 16-byte aligned fp32 buffer of 4k elements");
+      zp = zero_out->data_ptr<float>();
+      zn = zero_out->numel();
+    }
+    Tensor& tk = ce_ticket(h);
+    pio::ce2_fwd_launch(h.data_ptr<float>(), ip, labels.data_ptr<int64_t>(), bfp(w), f32p(bias), M, V, ns,
+                        reinterpret_cast<float2*>(pml.data_ptr<float>()), pacc.data_ptr<float>(), picked.data_ptr<float>(),
+                        bfp_mut(hs), lse.data_ptr<float>(), u.data_ptr<float>(), count.data_ptr<float>(),
+                        count_labels ? 1 : 0, loss.data_ptr<float>(), blk.data_ptr<float>(),
+                        reinterpret_cast<unsigned*>(tk.data_ptr<int>()), zp, zn, stream());
+    checked_sync("ce_fwd");
+    return {loss, lse, hs, u};
+  }
   const int ns = pio::ce_num_splits(M, V);
   Tensor part = torch::empty({ns, M, 2}, f32), picked = torch::empty({M}, f32);
   Tensor lse = torch::empty({M}, f32), loss = torch::empty({}, f32);
@@ -813,7 +859,7 @@ std::vector<Tensor> ce_fwd(Tensor h, OptT idx, Tensor labels, Tensor w, Tensor b
 // slab: the dW kernel stores its row-split partials into a returned (splits, V·C + V₄) slab
 // instead of adding them (the caller sums it into dW | db with a slab job, offsets 0 and V·C).
 OptT ce_bwd(Tensor h, Tensor labels, Tensor w, Tensor bias, Tensor lse, Tensor gout, Tensor count, Tensor dH,
-            Tensor dW, Tensor db, bool accumulate, OptT rowmap, bool slab) {
+            Tensor dW, Tensor db, bool accumulate, OptT rowmap, bool slab, OptT u) {
   const int M = (int)labels.numel(), C = (int)h.size(1), V = (int)w.size(0);
   CHECK_DT(h, torch::kBFloat16);
   TORCH_CHECK(h.size(0) == M, "ce_bwd: h must be the compact (M, C) bf16 rows of ce_fwd");
@@ -830,6 +876,17 @@ OptT ce_bwd(Tensor h, Tensor labels, Tensor w, Tensor bias, Tensor lse, Tensor g
     TORCH_CHECK(dH.size(0) == M, "dH must be (M, C) without a rowmap");
   }
   Tensor sl;
+  if (u.has_value()) {  // the two-pass head's backward: dW / db pass + the dH rows g·u
+    CHECK_DT(*u, torch::kFloat32);
+    TORCH_CHECK(C == 64 && u->is_contiguous() && u->size(0) == M && u->size(1) == C, "ce_bwd: u must be (M, 64) fp32");
+    if (slab) sl = torch::empty({pio::ce2_bwd_splits(M, V), (int64_t)V * C + ((V + 3) & ~3)}, dW.options());
+    pio::ce2_bwd_launch(bfp(h), labels.data_ptr<int64_t>(), bfp(w), f32p(bias), f32p(lse), u->data_ptr<float>(),
+                        f32p(gout), f32p(count), M, V, dW.data_ptr<float>(), db.data_ptr<float>(),
+                        slab ? sl.data_ptr<float>() : nullptr, accumulate ? 1 : 0, dH.data_ptr<float>(), dH.size(0), rm,
+                        stream());
+    if (slab) return sl;
+    return c10::nullopt;
+  }
   if (slab) sl = torch::empty({pio::ce_dw_splits(M, V), (int64_t)V * C + ((V + 3) & ~3)}, dW.options());
   pio::ce_bwd_launch(C, bfp(h), labels.data_ptr<int64_t>(), bfp(w), f32p(bias), f32p(lse), f32p(gout),
                      f32p(count), M, V, dH.data_ptr<float>(), dH.size(0), rm, dW.data_ptr<float>(), db.data_ptr<float>(),
@@ -1353,7 +1410,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_bwd", &attn_bwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("kmask"), py::arg("o"), py::arg("dO"),
         py::arg("lse"), py::arg("delta_in"), py::arg("H"), py::arg("D"), py::arg("scale"), py::arg("dropout_p"),
         py::arg("seed"), py::arg("dq_out"), py::arg("dk_out"), py::arg("dv_out"), py::arg("kv_accumulate") = false,
-        py::arg("site") = 0, py::arg("dq_zeroed") = false, py::arg("kv_zeroed") = false);
+        py::arg("site") = 0, py::arg("dq_zeroed") = false, py::arg("kv_zeroed") = false,
+        py::arg("job_slab") = py::none(), py::arg("job_dsts") = std::vector<Tensor>(),
+        py::arg("job_offs") = std::vector<int64_t>());
   m.def("attn_bwd_zero_plan", &pio::attn_bwd_zero_plan, py::arg("B"), py::arg("H"), py::arg("Nq"), py::arg("Nk"),
         py::arg("D"));
   m.def("ln_linear_fwd", &ln_linear_fwd, py::arg("x"), py::arg("lnw"), py::arg("lnb"), py::arg("eps"), py::arg("w"),
@@ -1403,7 +1462,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("count"), py::arg("zero_out") = py::none(), py::arg("count_labels") = false);
   m.def("ce_bwd", &ce_bwd, py::arg("h"), py::arg("labels"), py::arg("w"), py::arg("bias"),
         py::arg("lse"), py::arg("gout"), py::arg("count"), py::arg("dH"), py::arg("dW"), py::arg("db"),
-        py::arg("accumulate"), py::arg("rowmap") = py::none(), py::arg("slab") = false);
+        py::arg("accumulate"), py::arg("rowmap") = py::none(), py::arg("slab") = false, py::arg("u") = py::none());
   m.def("embed_fwd", &embed_fwd);
   m.def("embed_bwd", &embed_bwd);
   m.def("text_mask", &text_mask, py::arg("x"), py::arg("pad"), py::arg("state"), py::arg("unk"), py::arg("mask"),

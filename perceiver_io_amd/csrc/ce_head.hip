@@ -1,0 +1,489 @@
+// Vocab projection + softmax cross-entropy head, two streaming passes (C = 64; SURVEY K-12/K-13).
+//
+// Reference: TextOutputAdapter linear (perceiver/adapter.py:146-149) + CrossEntropyLoss over the
+// (B, V, L) logits with ignore_index -100 (perceiver/lightning.py:223-226).  Only the ~15 %
+// selected rows are passed in (compacted on device).  Logits exist only as MFMA tiles.
+//
+//   pass 1 (forward)  rows × vocab split: transposed logit tiles Sᵀ = W·Hᵀ (vocab on the
+//                     accumulator rows, one query row per lane) with an online log-sum-exp, AND
+//                     the softmax-weighted vocab sum Σ_v p[r, v]·W[v] — a flash-attention forward
+//                     whose keys and values are both W — so the hidden-state gradient needs no
+//                     further pass over the vocabulary: dH[r] = g·(Σ_v p[r, v]·W[v] − W[label]).
+//   combine           merges the vocab splits: per-row lse, loss (mean by a deterministic ticket
+//                     reduction) and u[r] = Σ_v p·W − W[label] (fp32), kept for the backward.
+//   pass 2 (backward) vocab × row split: logit tiles S = H·Wᵀ (vocab on the lane), dl = (p −
+//                     onehot)·g, dW += dlᵀ·H and db += Σ dl (partials stored into a slab row),
+//                     plus the dH rows g·u[r] scattered to their source positions by appended
+//                     workgroups.
+//
+// LDS images ([rows][64] bf16, 128 B per row, no padding) are XOR-swizzled on their 16-byte
+// slots with sw(v) = v₁·4 + v₂·2 + v₃ (bits of the row index): a k-contiguous ds_read_b128
+// fragment (16 rows of a lane group, one slot each) and a transposed ds_read_b64_tr_b16
+// fragment (4 consecutive rows × 4 slots per 32 lanes) both land on distinct banks.
+// Stats are kept in the log2 domain; the online rescale of the running sum and the W-weighted
+// accumulator is lazy: only when a row's max grows by more than kRescale (2^8 headroom, far
+// inside fp32 / bf16 range), a wave-uniform branch taken a handful of times per row.
+#include "common.h"
+
+namespace pio {
+
+namespace ce2 {
+
+constexpr int C = 64;            // head width (the C = 64 specialisation)
+constexpr int RB = 128;          // pass 1: rows per workgroup (4 waves × 32)
+constexpr int VC = 64;           // pass 1: vocab entries per staged chunk
+constexpr int VB2 = 128;         // pass 2: vocab entries per workgroup (4 waves × 32)
+constexpr int HT = 64;           // pass 2: rows per staged H tile
+constexpr float kL2E = 1.4426950408889634f;
+constexpr float kLN2 = 0.6931471805599453f;
+constexpr float kRescale = 8.f;  // lazy-rescale threshold (log2 units)
+
+// element offset of (row v, 16-byte slot s) in a swizzled [rows][64] bf16 image
+__device__ __forceinline__ int swz(int v, int s) {
+  const int sw = ((v >> 1) & 1) << 2 | ((v >> 2) & 1) << 1 | ((v >> 3) & 1);
+  return v * C + 8 * (s ^ sw);
+}
+// k-contiguous 32x32x16 operand: row i0 + (l & 31), k = 16·ks + 8·(l >> 5) .. + 7
+__device__ __forceinline__ bf16x8 img_kc(const uint16_t* img, int i0, int ks) {
+  const int l = lane_id();
+  return *reinterpret_cast<const bf16x8*>(img + swz(i0 + (l & 31), 2 * ks + (l >> 5)));
+}
+// transposed operand with the permuted k order of an accumulator used as the other operand
+// (frag_ks_perm of common.h on a swizzled image): image rows = k (k0 + …), columns = i (i0 + …)
+__device__ __forceinline__ bf16x8 img_ks_perm(const uint16_t* img, int i0, int k0) {
+  const int l = lane_id();
+  const int g = l >> 4, i = l & 15, q = i >> 2, p = i & 3;
+  const int row = k0 + 4 * (g >> 1) + q, col = i0 + 16 * (g & 1) + 4 * p;
+  const uint16_t* a = img + swz(row, col >> 3) + (col & 7);
+  const uint16_t* b = img + swz(row + 8, col >> 3) + (col & 7);
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(a));
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(b));
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+}  // namespace ce2
+
+// ---- pass 1 ---------------------------------------------------------------------------
+// grid (⌈M / 128⌉, splits); wave w: rows m0 + 32w + (l & 31).  Per split: part_ml[split][row] =
+// (max, sum) in log2 units, part_acc[split][row][c] = Σ_v 2^(t_v − max)·W[v][c] over the split's
+// vocabulary; picked[row] = the label's logit (natural units, written by the split holding it);
+// split 0 also writes the compact bf16 rows hs for pass 2.
+__global__ __launch_bounds__(256) void ce2_fwd_kernel(const float* __restrict__ Hm, const int64_t* __restrict__ hidx,
+                                                      const int64_t* __restrict__ labels, const uint16_t* __restrict__ W,
+                                                      const float* __restrict__ bias, int M, int V, int chunks_per_split,
+                                                      float2* __restrict__ part_ml, float* __restrict__ part_acc,
+                                                      float* __restrict__ picked, uint16_t* __restrict__ hs_out) {
+  using namespace ce2;
+  __shared__ __attribute__((aligned(16))) uint16_t sW[2][VC * C];
+  __shared__ __attribute__((aligned(16))) float sB[2][VC];  // bias·log2e (−inf past V)
+  const int w = wave_id(), l = lane_id(), hh = l >> 5;
+  const int m0 = blockIdx.x * RB, split = blockIdx.y;
+  const int nchunks = (V + VC - 1) / VC;
+  const int c_begin = split * chunks_per_split, c_end = min(nchunks, c_begin + chunks_per_split);
+  const int gr = m0 + 32 * w + (l & 31);
+  const bool rin = gr < M;
+  // this lane's half row (c = 16s + 8hh .. + 7, s < 4) as the B operand of Sᵀ = W·Hᵀ, gathered
+  // from the fp32 decoder output and cast on load
+  bf16x8 hb[4];
+  {
+    const long long src = hidx ? hidx[rin ? gr : 0] : (long long)(rin ? gr : 0);
+    const float* hp = Hm + src * C + 8 * hh;
+    float4 a[4], b[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      a[s] = *reinterpret_cast<const float4*>(rin ? hp + 16 * s : kZero32B);
+      b[s] = *reinterpret_cast<const float4*>(rin ? hp + 16 * s + 4 : kZero32B);
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      hb[s][0] = (short)f2bf(a[s].x); hb[s][1] = (short)f2bf(a[s].y); hb[s][2] = (short)f2bf(a[s].z);
+      hb[s][3] = (short)f2bf(a[s].w); hb[s][4] = (short)f2bf(b[s].x); hb[s][5] = (short)f2bf(b[s].y);
+      hb[s][6] = (short)f2bf(b[s].z); hb[s][7] = (short)f2bf(b[s].w);
+    }
+    if (split == 0 && hs_out != nullptr && rin)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) *reinterpret_cast<bf16x8*>(hs_out + (long long)gr * C + 16 * s + 8 * hh) = hb[s];
+  }
+  const int lab = rin ? (int)labels[gr] : -100;
+  // chunk staging: 64 vocab rows × 8 slots = 512 16-byte pieces, two per thread (+ the bias)
+  bf16x8 wr[2];
+  float bnext = 0.f;
+  auto fetch = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = threadIdx.x + 256 * i, v = c * VC + (e >> 3);
+      wr[i] = *reinterpret_cast<const bf16x8*>(v < V ? W + (long long)v * C + 8 * (e & 7)
+                                                     : reinterpret_cast<const uint16_t*>(kZero32B));
+    }
+    const int v = c * VC + (threadIdx.x & (VC - 1));
+    const float bv = bias[v < V ? v : 0];  // unconditional load (address select)
+    bnext = v < V ? bv * kL2E : -__builtin_inff();
+  };
+  auto stage = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = threadIdx.x + 256 * i;
+      *reinterpret_cast<bf16x8*>(&sW[buf][swz(e >> 3, e & 7)]) = wr[i];
+    }
+    if (threadIdx.x < VC) sB[buf][threadIdx.x] = bnext;
+  };
+  float m_ref = -__builtin_inff(), l_run = 0.f, pk = 0.f;
+  bool have_pk = false;
+  f32x16 acc[2] = {f32x16{}, f32x16{}};  // Σ p·W, transposed: [c = 32ct + acc_row][row = lane]
+  if (c_begin < c_end) {
+    fetch(c_begin);
+    stage(0);
+  }
+  lds_sync();
+  for (int c = c_begin; c < c_end; ++c) {
+    const int buf = (c - c_begin) & 1;
+    if (c + 1 < c_end) fetch(c + 1);  // in flight under this chunk's MFMAs
+    const uint16_t* img = sW[buf];
+#pragma unroll
+    for (int vb = 0; vb < 2; ++vb) {  // two 32-vocab blocks per chunk
+      f32x16 st = f32x16{};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) st = mfma32(ce2::img_kc(img, 32 * vb, s), hb[s], st);
+      // register i: vocab 32vb + acc_row(i, hh) of the chunk (log2 units, bias added)
+      float t[16];
+      {
+        const float* bp = sB[buf] + 32 * vb + 4 * hh;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 bb = *reinterpret_cast<const float4*>(bp + 8 * q);
+          t[4 * q] = fmaf(st[4 * q], kL2E, bb.x);
+          t[4 * q + 1] = fmaf(st[4 * q + 1], kL2E, bb.y);
+          t[4 * q + 2] = fmaf(st[4 * q + 2], kL2E, bb.z);
+          t[4 * q + 3] = fmaf(st[4 * q + 3], kL2E, bb.w);
+        }
+      }
+      float mx = t[0];
+#pragma unroll
+      for (int i = 1; i < 16; ++i) mx = fmaxf(mx, t[i]);
+      mx = xor32_max(mx);  // both halves of the row share its reference max
+      if (__ballot(mx > m_ref + ce2::kRescale)) {  // rare, wave-uniform
+        const float mn = fmaxf(m_ref, mx);
+        const float alpha = fast_exp2(m_ref - mn);  // 0 on the first block
+        l_run *= alpha;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { acc[0][i] *= alpha; acc[1][i] *= alpha; }
+        m_ref = mn;
+      }
+      // the label's logit, if this lane holds it
+      const int j = lab - (c * VC + 32 * vb);
+      if (j >= 0 && j < 32 && ((j >> 2) & 1) == hh) {
+        const int ri = (j & 3) + 4 * (j >> 3);
+        float v = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v = i == ri ? t[i] : v;
+        pk = v;
+        have_pk = true;
+      }
+      f32x16 p;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        p[i] = fast_exp2(t[i] - m_ref);
+        l_run += p[i];
+      }
+      // Σ p·W: accᵀ[c][row] += Wᵀ[c][v]·Pᵀ[v][row] (the logits accumulator as the B operand)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const bf16x8 pb = pack_acc(p, ss);
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) acc[ct] = mfma32(ce2::img_ks_perm(img, 32 * ct, 32 * vb + 16 * ss), pb, acc[ct]);
+      }
+    }
+    if (c + 1 < c_end) stage(buf ^ 1);
+    lds_sync();
+  }
+  if (!rin) return;
+  const float ls = xor32_sum(l_run);
+  if (hh == 0) part_ml[(long long)split * M + gr] = make_float2(m_ref, ls);
+  if (have_pk) picked[gr] = pk * ce2::kLN2;
+  float* pa = part_acc + ((long long)split * M + gr) * C;
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)  // registers 4q .. 4q+3 = c 32ct + 8q + 4hh + 0..3
+      *reinterpret_cast<float4*>(pa + 32 * ct + 8 * q + 4 * hh) =
+          make_float4(acc[ct][4 * q], acc[ct][4 * q + 1], acc[ct][4 * q + 2], acc[ct][4 * q + 3]);
+}
+
+// ---- combine --------------------------------------------------------------------------
+// 16 rows per workgroup, 16 threads per row (4 channels each).  lse[r] (natural), u[r][c] =
+// Σ_v p[r, v]·W[v][c] − W[label][c] (0 for ignored rows), loss = Σ (lse − picked) / max(count, 1)
+// with the deterministic last-workgroup ticket of mlm_head.hip.  Also clears zero_out (the
+// backward's dH buffer, float4 slices per workgroup).
+constexpr int kC2Rows = 16;
+__global__ __launch_bounds__(256) void ce2_combine_kernel(const float2* __restrict__ part_ml,
+                                                          const float* __restrict__ part_acc,
+                                                          const float* __restrict__ picked,
+                                                          const int64_t* __restrict__ labels,
+                                                          const uint16_t* __restrict__ W, int M, int V, int nsplit,
+                                                          float* __restrict__ lse, float* __restrict__ u,
+                                                          float* __restrict__ count, int count_labels,
+                                                          float* __restrict__ loss, float* __restrict__ blk,
+                                                          unsigned* __restrict__ ticket, float* __restrict__ zero_out,
+                                                          long long zero_n4) {
+  using namespace ce2;
+  __shared__ float red[2][16];
+  __shared__ int last;
+  const int rr = threadIdx.x >> 4, cq = threadIdx.x & 15;
+  const int r = blockIdx.x * kC2Rows + rr;
+  float lr = 0.f, nr = 0.f;
+  if (r < M) {
+    float mx = -__builtin_inff();
+    for (int s = 0; s < nsplit; ++s) mx = fmaxf(mx, part_ml[(long long)s * M + r].x);
+    float L = 0.f;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int s = 0; s < nsplit; ++s) {
+      const float2 ml = part_ml[(long long)s * M + r];
+      const float f = fast_exp2(ml.x - mx);
+      L += ml.y * f;
+      const float4 v = *reinterpret_cast<const float4*>(part_acc + ((long long)s * M + r) * C + 4 * cq);
+      a.x = fmaf(v.x, f, a.x); a.y = fmaf(v.y, f, a.y); a.z = fmaf(v.z, f, a.z); a.w = fmaf(v.w, f, a.w);
+    }
+    const int lab = (int)labels[r];
+    const float inv = 1.f / L;
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (lab >= 0 && lab < V) {
+      const uint2 wv = *reinterpret_cast<const uint2*>(W + (long long)lab * C + 4 * cq);
+      o = make_float4(a.x * inv - bf2f((uint16_t)(wv.x & 0xFFFF)), a.y * inv - bf2f((uint16_t)(wv.x >> 16)),
+                      a.z * inv - bf2f((uint16_t)(wv.y & 0xFFFF)), a.w * inv - bf2f((uint16_t)(wv.y >> 16)));
+    }
+    *reinterpret_cast<float4*>(u + (long long)r * C + 4 * cq) = o;
+    if (cq == 0) {
+      const float L2 = (mx + __log2f(L)) * kLN2;
+      lse[r] = L2;
+      lr = lab >= 0 ? L2 - picked[r] : 0.f;
+      nr = lab >= 0 ? 1.f : 0.f;
+    }
+  }
+  if (zero_out != nullptr) {
+    const long long nwg = gridDim.x, per = (zero_n4 + nwg - 1) / nwg, z1 = min(zero_n4, ((long long)blockIdx.x + 1) * per);
+    for (long long i = (long long)blockIdx.x * per + threadIdx.x; i < z1; i += blockDim.x)
+      reinterpret_cast<float4*>(zero_out)[i] = float4{0.f, 0.f, 0.f, 0.f};
+  }
+  lr = wave_sum(lr);
+  nr = wave_sum(nr);
+  if (lane_id() == 0) { red[0][wave_id()] = lr; red[1][wave_id()] = nr; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    blk[blockIdx.x] = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+    blk[gridDim.x + blockIdx.x] = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+    __threadfence();
+    last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  float t = 0.f, n = 0.f;
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x) {
+    t += *(volatile const float*)(blk + i);
+    n += *(volatile const float*)(blk + gridDim.x + i);
+  }
+  t = wave_sum(t);
+  n = wave_sum(n);
+  __syncthreads();
+  if (lane_id() == 0) { red[0][wave_id()] = t; red[1][wave_id()] = n; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float tt = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+    const float nn = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+    if (count_labels) count[0] = nn;
+    loss[0] = tt / fmaxf(count_labels ? nn : count[0], 1.f);
+    *ticket = 0u;
+  }
+}
+
+// ---- pass 2 ---------------------------------------------------------------------------
+// grid (⌈V / 128⌉, rsplit + 1).  y < rsplit: wave w owns vocab v0 = 128·x + 32w + (l & 31) (its
+// 32 rows of W as the B operand of S = H·Wᵀ, in registers) and streams the rows of split y in
+// 64-row tiles (bf16 H, lse, labels) through LDS; dl = (2^(t − lse) − [label = v])·g;
+// dW[v] += dlᵀ·H, db[v] += Σ dl; partials stored into slab row y (or added atomically).
+// y = rsplit: dH[rowmap[r]] (+)= g·u[r] for the rows of slice x (appended workgroups).
+__global__ __launch_bounds__(256) void ce2_bwd_kernel(const uint16_t* __restrict__ Hs, const int64_t* __restrict__ labels,
+                                                      const uint16_t* __restrict__ W, const float* __restrict__ bias,
+                                                      const float* __restrict__ lse, const float* __restrict__ u,
+                                                      const float* __restrict__ gout, const float* __restrict__ count,
+                                                      int M, int V, int rsplit, int tiles_per_split,
+                                                      float* __restrict__ dW, float* __restrict__ db,
+                                                      float* __restrict__ slab, float* __restrict__ dH,
+                                                      const int64_t* __restrict__ rowmap, long long dh_rows) {
+  using namespace ce2;
+  __shared__ __attribute__((aligned(16))) uint16_t sH[2][HT * C];
+  __shared__ __attribute__((aligned(16))) float sL[2][HT];  // lse·log2e
+  __shared__ __attribute__((aligned(16))) int sLab[2][HT];
+  const int w = wave_id(), l = lane_id(), hh = l >> 5;
+  const float g = gout[0] / fmaxf(count[0], 1.f);
+  if ((int)blockIdx.y == rsplit) {  // the dH scatter of the forward's u rows
+    const int per = (M + gridDim.x - 1) / gridDim.x, r0 = blockIdx.x * per, r1 = min(M, r0 + per);
+    for (int e = threadIdx.x; e < (r1 - r0) * (C / 4); e += blockDim.x) {
+      const int r = r0 + e / (C / 4), c4 = e % (C / 4);
+      if (labels[r] < 0) continue;
+      const long long dst = rowmap ? rowmap[r] : (long long)r;
+      if (dst < 0 || dst >= dh_rows) continue;
+      const float4 v = *reinterpret_cast<const float4*>(u + (long long)r * C + 4 * c4);
+      float4* d = reinterpret_cast<float4*>(dH + dst * C) + c4;
+      float4 o = *d;
+      o.x = fmaf(v.x, g, o.x); o.y = fmaf(v.y, g, o.y); o.z = fmaf(v.z, g, o.z); o.w = fmaf(v.w, g, o.w);
+      *d = o;
+    }
+    return;
+  }
+  const int vl = 32 * w + (l & 31), vg = blockIdx.x * VB2 + vl;
+  const bool vin = vg < V;
+  // this lane's vocab row as the B operand (k = c = 16s + 8hh .. + 7)
+  bf16x8 wb[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+    wb[s] = *reinterpret_cast<const bf16x8*>(vin ? W + (long long)vg * C + 16 * s + 8 * hh
+                                                 : reinterpret_cast<const uint16_t*>(kZero32B));
+  const float bl2 = vin ? bias[vg] * kL2E : -__builtin_inff();
+  const int ntiles = (M + HT - 1) / HT;
+  const int t_begin = blockIdx.y * tiles_per_split, t_end = min(ntiles, t_begin + tiles_per_split);
+  bf16x8 hr[2];
+  float aux = 0.f;
+  auto fetch = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = threadIdx.x + 256 * i, r = t * HT + (e >> 3);
+      hr[i] = *reinterpret_cast<const bf16x8*>(r < M ? Hs + (long long)r * C + 8 * (e & 7)
+                                                     : reinterpret_cast<const uint16_t*>(kZero32B));
+    }
+    const int r = t * HT + (threadIdx.x & (HT - 1));
+    if (threadIdx.x < HT) aux = r < M ? lse[r] * kL2E : 0.f;
+    else if (threadIdx.x < 2 * HT) aux = __int_as_float(r < M ? (int)labels[r] : -100);
+  };
+  auto stage = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = threadIdx.x + 256 * i;
+      *reinterpret_cast<bf16x8*>(&sH[buf][swz(e >> 3, e & 7)]) = hr[i];
+    }
+    if (threadIdx.x < HT) sL[buf][threadIdx.x] = aux;
+    else if (threadIdx.x < 2 * HT) sLab[buf][threadIdx.x - HT] = __float_as_int(aux);
+  };
+  f32x16 acc[2] = {f32x16{}, f32x16{}};  // dW: [v = acc_row][c = 32ct + lane]
+  float bsum = 0.f;
+  if (t_begin < t_end) {
+    fetch(t_begin);
+    stage(0);
+  }
+  lds_sync();
+  for (int t = t_begin; t < t_end; ++t) {
+    const int buf = (t - t_begin) & 1;
+    if (t + 1 < t_end) fetch(t + 1);
+    const uint16_t* img = sH[buf];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {  // two 32-row blocks per tile
+      f32x16 st = f32x16{};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) st = mfma32(ce2::img_kc(img, 32 * rb, s), wb[s], st);
+      // register i: row 32rb + acc_row(i, hh) of the tile; lane: vocab vg
+      f32x16 d;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = 32 * rb + 8 * q + 4 * hh;
+        const float4 ls = *reinterpret_cast<const float4*>(&sL[buf][r]);
+        const int4 lb = *reinterpret_cast<const int4*>(&sLab[buf][r]);
+        const float lsv[4] = {ls.x, ls.y, ls.z, ls.w};
+        const int lbv[4] = {lb.x, lb.y, lb.z, lb.w};
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const float gr = lbv[jj] >= 0 ? g : 0.f;
+          const float p = fast_exp2(fmaf(st[4 * q + jj], kL2E, bl2 - lsv[jj])) * gr;
+          d[4 * q + jj] = lbv[jj] == vg ? p - gr : p;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) bsum += d[i];
+      // dW[v][c] += Σ_r dl[r][v]·H[r][c]: the dl accumulator as the A operand (Xᵀ·B)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const bf16x8 pa = pack_acc(d, ss);
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) acc[ct] = mfma32(pa, ce2::img_ks_perm(img, 32 * ct, 32 * rb + 16 * ss), acc[ct]);
+      }
+    }
+    if (t + 1 < t_end) stage(buf ^ 1);
+    lds_sync();
+  }
+  bsum = xor32_sum(bsum);
+  float* dWp = dW;
+  float* dbp = db;
+  if (slab) {
+    dWp = slab + (long long)blockIdx.y * ((long long)V * C + ((V + 3) & ~3));
+    dbp = dWp + (long long)V * C;
+  }
+  if (hh == 0 && vin) {
+    if (slab) dbp[vg] = bsum;
+    else atomicAdd(dbp + vg, bsum);
+  }
+  // accumulator: col = lane & 31 = c (within tile ct), row = acc_row(i, hh) = vocab within the wave's 32
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int vv = blockIdx.x * VB2 + 32 * w + acc_row(i, hh);
+      if (vv < V) {
+        float* p = dWp + (long long)vv * C + 32 * ct + (l & 31);
+        if (slab) *p = acc[ct][i];
+        else atomicAdd(p, acc[ct][i]);
+      }
+    }
+}
+
+// ---- host side --------------------------------------------------------------------------
+int ce2_num_splits(int M, int V) {
+  // ≈ 2 workgroups per CU over (row blocks × vocab splits); every split ≥ 4 chunks
+  const int rb = (M + ce2::RB - 1) / ce2::RB, nchunks = (V + ce2::VC - 1) / ce2::VC;
+  int s = (512 + rb - 1) / rb;
+  s = s < 1 ? 1 : s;
+  const int cap = (nchunks + 3) / 4;
+  s = s > cap ? cap : s;
+  const int cps = (nchunks + s - 1) / s;
+  return (nchunks + cps - 1) / cps;
+}
+int ce2_bwd_splits(int M, int V) {
+  // row splits of pass 2: ≈ 512 workgroups, every split ≥ 4 tiles (the slab height)
+  const int vb = (V + ce2::VB2 - 1) / ce2::VB2, nt = (M + ce2::HT - 1) / ce2::HT;
+  int s = (512 + vb - 1) / vb;
+  const int cap = (nt + 3) / 4;
+  s = s > cap ? cap : s;
+  s = s < 1 ? 1 : s;
+  const int tps = (nt + s - 1) / s;
+  return (nt + tps - 1) / tps;
+}
+int ce2_combine_blocks(int M) { return (M + kC2Rows - 1) / kC2Rows; }
+
+void ce2_fwd_launch(const float* Hm, const int64_t* hidx, const int64_t* labels, const uint16_t* W, const float* bias,
+                    int M, int V, int nsplit, float2* part_ml, float* part_acc, float* picked, uint16_t* hs_out,
+                    float* lse, float* u, float* count, int count_labels, float* loss, float* blk, unsigned* ticket,
+                    float* zero_out, long long zero_n, hipStream_t st) {
+  const int nchunks = (V + ce2::VC - 1) / ce2::VC;
+  const int cps = (nchunks + nsplit - 1) / nsplit;
+  hipLaunchKernelGGL(ce2_fwd_kernel, dim3((M + ce2::RB - 1) / ce2::RB, nsplit), dim3(256), 0, st, Hm, hidx, labels, W,
+                     bias, M, V, cps, part_ml, part_acc, picked, hs_out);
+  hipLaunchKernelGGL(ce2_combine_kernel, dim3(ce2_combine_blocks(M)), dim3(256), 0, st, part_ml, part_acc, picked, labels,
+                     W, M, V, nsplit, lse, u, count, count_labels, loss, blk, ticket, zero_out, zero_n / 4);
+}
+
+void ce2_bwd_launch(const uint16_t* Hs, const int64_t* labels, const uint16_t* W, const float* bias, const float* lse,
+                    const float* u, const float* gout, const float* count, int M, int V, float* dW, float* db,
+                    float* slab, int accumulate, float* dH, long long dh_rows, const int64_t* rowmap, hipStream_t st) {
+  const int rsplit = ce2_bwd_splits(M, V);
+  const int nt = (M + ce2::HT - 1) / ce2::HT;
+  const int tps = (nt + rsplit - 1) / rsplit;
+  if (!accumulate && slab == nullptr) {
+    (void)hipMemsetAsync(dW, 0, sizeof(float) * (size_t)V * ce2::C, st);
+    (void)hipMemsetAsync(db, 0, sizeof(float) * (size_t)V, st);
+  }
+  hipLaunchKernelGGL(ce2_bwd_kernel, dim3((V + ce2::VB2 - 1) / ce2::VB2, rsplit + 1), dim3(256), 0, st, Hs, labels, W, bias,
+                     lse, u, gout, count, M, V, rsplit, tps, dW, db, slab, dH, rowmap, dh_rows);
+}
+
+}  // namespace pio

@@ -205,12 +205,13 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 // logical 3-D block index (x fastest) after the remap: the (x, y) blocks of one z are
 // consecutive, i.e. all heads / key blocks of one batch element read their rows through one L2
 struct Blk3 { int x, y, z; };
-__device__ __forceinline__ Blk3 xcd_block3() {
+__device__ __forceinline__ Blk3 xcd_block3(int gz) {  // gz: the z extent of the remapped part of the grid
   const int gx = gridDim.x, gy = gridDim.y;
-  const int nwg = gx * gy * gridDim.z;
+  const int nwg = gx * gy * gz;
   const int m = xcd_remap(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), nwg);
   return Blk3{m % gx, (m / gx) % gy, m / (gx * gy)};
 }
+__device__ __forceinline__ Blk3 xcd_block3() { return xcd_block3(gridDim.z); }
 
 // ---- phase timestamps (tools/trace only; compiled out unless PIO_TRACE is defined) ----
 // PIO_TS(slot): lane 0 of every wave of workgroup (trace_bx, trace_by, trace_bz) records the

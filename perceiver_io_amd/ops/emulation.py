@@ -309,7 +309,8 @@ def attn_fwd(q, k, v, kmask, H, D, scale, dropout_p, seed, nsplit, site=0):
 
 
 def attn_bwd(q, k, v, kmask, o, dO, lse, delta_in, H, D, scale, dropout_p, seed, dq_out, dk_out, dv_out,
-             kv_accumulate=False, site=0, dq_zeroed=False, kv_zeroed=False):
+             kv_accumulate=False, site=0, dq_zeroed=False, kv_zeroed=False, job_slab=None, job_dsts=(), job_offs=()):
+    _run_job(job_slab, job_dsts, job_offs)
     B, qf, kf, vf = _qkv(q, k, v, H, D)
     s = _scores(qf, kf, kmask, scale)
     l2 = lse.permute(0, 2, 1)  # (B, H, Nq)
@@ -522,9 +523,10 @@ def ce_fwd(h, idx, labels, w, bias, count, zero_out=None, count_labels=False):
     return loss.sum() / count.reshape(()).clamp(min=1), lse, _ce_rows(h, idx).to(torch.bfloat16).contiguous()
 
 
-def ce_bwd(h, labels, w, bias, lse, gout, count, dH, dW, db, accumulate, rowmap=None, slab=False):
+def ce_bwd(h, labels, w, bias, lse, gout, count, dH, dW, db, accumulate, rowmap=None, slab=False, u=None):
     """h: the compact bf16 rows returned by ce_fwd.  slab=True: dW | db are returned as a one-row
-    (1, V·C + V₄) slab instead of being added."""
+    (1, V·C + V₄) slab instead of being added.  ``u`` (the HIP two-pass head's forward output) is
+    not needed here: dH is formed from the logits."""
     if slab:
         gw, gb = torch.zeros_like(dW), torch.zeros_like(db)
         ce_bwd(h, labels, w, bias, lse, gout, count, dH, gw, gb, False, rowmap)

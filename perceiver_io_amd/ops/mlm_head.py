@@ -93,7 +93,11 @@ class _MaskedCE(torch.autograd.Function):
         wb = weight_cache.get(weight)  # bf16 shadow written by the fused optimizer
         # the backward's dH accumulator (atomic partials) is cleared by the forward kernel
         dh = torch.empty((h2.shape[0], c), device=h2.device, dtype=torch.float32)
-        loss, lse, hs = ext.ce_fwd(h2, idx, labels_c, wb, bias.contiguous(), cnt, dh, count_labels)
+        outs = ext.ce_fwd(h2, idx, labels_c, wb, bias.contiguous(), cnt, dh, count_labels)
+        loss, lse, hs = outs[:3]
+        # C = 64: the two-pass head also returns u = Σ_v p·W − W[label] per row (the hidden-state
+        # gradient up to the row-loss scale), so the backward makes only the dW / db pass
+        ctx.u = outs[3] if len(outs) > 3 else None
         ctx.dh = dh
         ctx.save_for_backward(hs, wb, bias, lse, idx if idx is not None else torch.empty(0, dtype=torch.int64),
                               labels_c, cnt)
@@ -119,8 +123,9 @@ class _MaskedCE(torch.autograd.Function):
         from . import fused
 
         ix = idx if idx.numel() else None
+        u, ctx.u = ctx.u, None
         slab = ext.ce_bwd(hs, labels_c, wb, bias.contiguous(), lse, gout.contiguous(), cnt, dh, weight.grad,
-                          ctx.bias_p.grad, True, ix, slab=fused.WGRAD_SLAB)
+                          ctx.bias_p.grad, True, ix, slab=fused.WGRAD_SLAB, u=u)
         if slab is not None:  # dW / db row-split partials: reduced by the next backward kernel
             fused.defer_slab(ext, slab, [weight.grad.view(-1), ctx.bias_p.grad.view(-1)], [0, weight.numel()])
         return dh.view(shp), None, None, None, None, None

@@ -450,20 +450,27 @@ def test_fused_cross_entropy(M, V, C):
     lab[::7] = -100
     hf = h.float()  # bf16-exact fp32 rows (the kernels cast on load)
     cnt = torch.tensor([float((lab >= 0).sum())], device=DEV)
-    l2, s2, hs2 = _emu().ce_fwd(hf, None, lab, w, bias, cnt)
+    l2, s2, hs2 = _emu().ce_fwd(hf, None, lab, w, bias, cnt)[:3]
+    u = None  # C = 64: the two-pass head's 4th output (Σ p·W − W[label] per row) feeds ce_bwd
     for _ in range(3):  # the loss finalisation's ticket is reset by every launch
-        l1, s1, hs1 = _ext().ce_fwd(hf, None, lab, w, bias, cnt)
-        close(l1, l2, 1e-3, "loss")
-        close(s1, s2, 1e-3, "lse")
+        o = _ext().ce_fwd(hf, None, lab, w, bias, cnt)
+        l1, s1, hs1 = o[:3]
+        u = o[3] if len(o) > 3 else None
+        assert rel_fro(l1, l2) < 1e-3 and rel_fro(s1, s2) < 1e-3, (rel_fro(l1, l2), rel_fro(s1, s2))
         assert torch.equal(hs1, hs2)
+    assert (u is not None) == (C == 64)
     # gathered rows: row r of the head input is hbig[idx[r]]
     idx = torch.randperm(2 * M, device=DEV)[:M]
     hbig = torch.zeros(2 * M, C, device=DEV)
     hbig[idx] = hf
-    lg, sg, hsg = _ext().ce_fwd(hbig, idx, lab, w, bias, cnt)
-    close(lg, l2, 1e-3, "loss gathered")
-    close(sg, s2, 1e-3, "lse gathered")
+    o = _ext().ce_fwd(hbig, idx, lab, w, bias, cnt)
+    lg, sg, hsg = o[:3]
+    assert rel_fro(lg, l2) < 1e-3 and rel_fro(sg, s2) < 1e-3
     assert torch.equal(hsg, hs2)  # the compact rows: gathered and cast on load
+    # count_labels: the head counts the labelled rows itself (classifier heads)
+    cnt_out = torch.full((1,), -5.0, device=DEV)
+    lc = _ext().ce_fwd(hf, None, lab, w, bias, cnt_out, None, True)[0]
+    assert cnt_out.item() == cnt.item() and rel_fro(lc, l2) < 1e-3
     gout = torch.tensor([0.37], device=DEV)
     rowmap = torch.randperm(3 * M, device=DEV)[:M]  # scatter rows into a larger (3M, C) gradient
     outs = []
@@ -471,13 +478,17 @@ def test_fused_cross_entropy(M, V, C):
         dH = torch.zeros(M, C, device=DEV)
         dW = torch.full((V, C), 7.0, device=DEV)  # overwritten (accumulate=False)
         db = torch.zeros(V, device=DEV)
-        K.ce_bwd(hs2, lab, w, bias, s2, gout, cnt, dH, dW, db, False, None)
+        K.ce_bwd(hs2, lab, w, bias, s2, gout, cnt, dH, dW, db, False, None, u=u)
         dHs = torch.zeros(3 * M, C, device=DEV)
         dW2, db2 = dW.clone(), db.clone()
-        K.ce_bwd(hs2, lab, w, bias, s2, gout, cnt, dHs, dW2, db2, True, rowmap)
-        outs.append((dH, dW, db, dHs, dW2, db2))
-    for a, b, n in zip(outs[0], outs[1], ("dH", "dW", "db", "dH rowmap", "dW acc", "db acc")):
-        close(a, b, 3e-2, n)
+        K.ce_bwd(hs2, lab, w, bias, s2, gout, cnt, dHs, dW2, db2, True, rowmap, u=u)
+        sl = K.ce_bwd(hs2, lab, w, bias, s2, gout, cnt, torch.zeros(M, C, device=DEV), dW.clone(), db.clone(), False,
+                      None, slab=True, u=u)
+        slab_sum = sl.sum(0)
+        outs.append((dH, dW, db, dHs, dW2, db2, slab_sum[:V * C].view(V, C), slab_sum[V * C:V * C + V]))
+    names = ("dH", "dW", "db", "dH rowmap", "dW acc", "db acc", "dW slab", "db slab")
+    errs = {n: rel_fro(a, b) for a, b, n in zip(outs[0], outs[1], names)}
+    assert all(e < 1e-2 for e in errs.values()), errs
 
 
 def test_embed_mask_adamw():
