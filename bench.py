@@ -344,7 +344,8 @@ def main(argv=None):
         if info.is_main:
             print(prof.key_averages().table(sort_by="cuda_time_total", row_limit=40), file=sys.stderr)
             if args.profile_stacks:
-                keep = ("aten::copy_", "aten::fill_", "aten::zero_", "aten::sum", "aten::clone")
+                keep = ("aten::copy_", "aten::fill_", "aten::zero_", "aten::sum", "aten::clone", "aten::add", "aten::add_",
+                        "aten::mul", "aten::ge", "aten::to", "aten::_to_copy")
                 rows = [e for e in prof.key_averages(group_by_stack_n=args.profile_stacks) if e.key in keep]
                 rows.sort(key=lambda e: -e.count)
                 for e in rows[:40]:

@@ -356,8 +356,7 @@ __global__ void attn_bwd_prep_kernel(const uint16_t* __restrict__ dO, const uint
 }
 
 // QR > 0 fixes the query tiles per round (QR = 1 for ≤ 32 queries, 2 for ≤ 64: a quarter / half
-// of the LDS, so several workgroups share a CU on the few-query / many-key cross-attention;
-// PIO_ATTN_BWD_FULL_LDS=1 restores the 4-tile rounds)
+// of the LDS, so several workgroups share a CU on the few-query / many-key cross-attention)
 // OBF: dQ / dK / dV stored as bf16 (the pointers are uint16_t views; every element written once:
 // a single key block, no query split, no accumulation — host-checked), for a consumer that reads
 // them as bf16 MFMA operands anyway (the chain-layout layer-boundary backward)
@@ -781,14 +780,6 @@ void attn_combine_launch(const float* Opart, const float* MLpart, uint16_t* O, f
                      (int)rows, D);
 }
 
-static bool getenv_flag(const char* name) {
-  static int cached = -1;  // one knob; read once
-  if (cached < 0) {
-    const char* v = getenv(name);
-    cached = (v && v[0] && v[0] != '0') ? 1 : 0;
-  }
-  return cached == 1;
-}
 
 // query splits of the backward grid when key blocks × heads × batch leave the GPU idle (≥ 4
 // query tiles each; no empty split)
@@ -837,7 +828,7 @@ static void bwd_launch_t(const AttnArgs& a, const uint16_t* dO, const float* LSE
                        st, dq, dq_bs, dq_rs, a.Nq, a.H * D, total);
   }
   dim3 grid(nkb * nqs, a.H, a.B);
-  const bool small_lds = !getenv_flag("PIO_ATTN_BWD_FULL_LDS");
+  constexpr bool small_lds = true;
   // ≤ 64 queries (few-query cross-attention): the small-LDS variants let several workgroups
   // share a CU
   if (a.Nq <= 32 && small_lds)

@@ -103,171 +103,10 @@ __device__ __forceinline__ bf16x8 pe_kv_row8(const bf16x8& p8, const float (&st)
   return out;
 }
 
-// ------------------------------------------------------------------------------------
-// Encoder cross-attention forward over implicit K/V (head dim 32, Nq ≤ 32, no mask, no dropout).
-// Every wave is independent: it owns one (batch element, head, key split) and sweeps its keys
-// in 32-key chunks — P' rows of the chunk (bf16; the next chunk's loads issued as soon as the
-// current rows are consumed), the chunk's key statistics (lanes < 32, one key each, through a
-// wave-private LDS table), the K/V tile generated into wave-private LDS (lane: 4 keys × 8
-// columns, the workgroup's generation table in LDS), then the flash step of attention.hip's
-// forward (Sᵀ = K·Qᵀ with the query on the lane, online softmax in registers, Oᵀ += Vᵀ·Pᵀ).
-// The 4 waves of a workgroup are 4 batch elements of one (split, head): they read the same P'
-// rows, and the XCD-aware block order keeps one (split, head) on one L2.  ≤ 128 VGPRs: four
-// waves per SIMD.  P' carries ≥ 32 zero rows past M (the last prefetch reads them).
-// Unnormalised partials in attention.hip's split-KV format, combined by attn_combine_kernel.
-// ------------------------------------------------------------------------------------
-template <int NC, int OCC>
-__global__ __launch_bounds__(256, OCC) void attn_fwd_pe_kernel(PeFwdArgs a) {
-  constexpr int LDT = PD + 8;  // K / V tile row stride (bf16)
-  __shared__ __attribute__((aligned(16))) uint16_t sK[4][32 * LDT];
-  __shared__ __attribute__((aligned(16))) uint16_t sV[4][32 * LDT];
-  __shared__ __attribute__((aligned(16))) float sSt[4][PE_NST][32];
-  __shared__ __attribute__((aligned(16))) float sWt[PE_NWT][64];  // head h's table: K columns | V columns
-  const int w = wave_id(), l = lane_id(), r = l & 31, hh = l >> 5;
-  const Blk3 blk = xcd_block3();  // x: batch quad (fastest), y: split, z: head
-  const int b = 4 * blk.x + w, split = blk.y, h = blk.z;
-  const int C = a.C;
-  for (int t = threadIdx.x; t < 64 * PE_NWT; t += 256) {
-    const int j = t >> 6, c = t & 63;
-    sWt[j][c] = a.wt[(long long)j * 2 * C + (c < PD ? h * PD + c : C + h * PD + c - PD)];
-  }
-  __syncthreads();
-  if (b >= a.B) return;  // no workgroup barriers below
-  const int kbeg = split * a.chunks * 32;
-  const int kend = min(a.M, kbeg + a.chunks * 32);
-  const int qi = r, qc = min(qi, a.Nq - 1);
-
-  bf16x8 qf[2];
-  {
-    const uint16_t* qp = a.q + (long long)b * a.q_bs + (long long)qc * a.q_rs + h * PD + 8 * hh;
-    qf[0] = *reinterpret_cast<const bf16x8*>(qp);
-    qf[1] = *reinterpret_cast<const bf16x8*>(qp + 16);
-  }
-  // generation mapping: keys gk..gk+3 of the chunk, columns gc..gc+7 of [K | V] (head h)
-  const int gk = 4 * (l & 7), gc = 8 * (l >> 3);
-  const int pcol = gc < PD ? h * PD + gc : C + h * PD + gc - PD;
-  uint16_t* tK = sK[w];
-  uint16_t* tV = sV[w];
-  float(*tS)[32] = sSt[w];
-  uint16_t* trow = (gc < PD ? tK : tV) + (gc & (PD - 1));
-
-  // chunk staging: P' rows (all lanes; pointer advanced per chunk, padded rows past M), the
-  // statistics inputs of key k0 + r (clamped: the last prefetch may pass M)
-  const long long prs = 2LL * C;
-  const uint16_t* pp = a.P + (long long)(min(kbeg, a.M) + gk) * prs + pcol;  // an empty split reads pad rows
-  bf16x8 pv[4];
-  float spx[NC], spe, spq;
-  const float* pixb = a.pix + (long long)b * a.M * NC;
-  auto fetch_p = [&]() {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) pv[i] = *reinterpret_cast<const bf16x8*>(pp + i * prs);
-    pp += 32 * prs;
-  };
-  auto fetch_s = [&](int k0) {
-    const int key = min(k0 + r, a.M - 1);
-    spe = a.pes[key];
-    spq = a.pesq[key];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) spx[c] = pixb[(long long)key * NC + c];
-  };
-  auto wave_lds_sync = [] {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
-  };
-
-  f32x16 o = f32x16{};
-  float m_run = -1e30f, l_run = 0.f;
-  auto chunk = [&](int k0, auto masked) {
-    float px[PMAXC];
-#pragma unroll
-    for (int c = 0; c < PMAXC; ++c) px[c] = c < NC ? spx[c < NC ? c : 0] : 0.f;
-    float st[PE_NST];
-    pe_key_stats(spe, spq, px, NC, a.inv_k, a.eps, st);
-    fetch_s(k0 + 32);
-    wave_lds_sync();  // the previous chunk's tile reads are done
-    if (hh == 0) {
-#pragma unroll
-      for (int j = 0; j < 2 + NC; ++j) tS[j][r] = st[j];
-    }
-    wave_lds_sync();
-    {
-      float4 s4[2 + NC];
-#pragma unroll
-      for (int j = 0; j < 2 + NC; ++j) s4[j] = *reinterpret_cast<const float4*>(&tS[j][gk]);
-#pragma unroll
-      for (int e4 = 0; e4 < 8; e4 += 4) {  // 4 columns at a time: their table entries, 4 keys
-        uint32_t pk[4][2];  // [key][column pair]
-        float4 w4[PE_NWT];
-#pragma unroll
-        for (int j = 0; j < PE_NWT; ++j)
-          if (j < NC || j >= 4) w4[j] = *reinterpret_cast<const float4*>(&sWt[j][gc + e4]);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float y[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            auto sel = [&](const float4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; };
-            float acc = fmaf(sel(s4[1], i), sel(w4[4], e), sel(w4[5], e));
-#pragma unroll
-            for (int c = 0; c < NC; ++c) acc = fmaf(sel(s4[2 + c], i), sel(w4[c], e), acc);
-            y[e] = fmaf(sel(s4[0], i), bf2f(pv[i][e4 + e]), acc);
-          }
-          pk[i][0] = pack2(y[0], y[1]);
-          pk[i][1] = pack2(y[2], y[3]);
-        }
-        if (e4 == 4) fetch_p();  // this chunk's rows are consumed: the next loads fly during the flash step
-#pragma unroll
-        for (int i = 0; i < 4; ++i) *reinterpret_cast<uint2*>(trow + (gk + i) * LDT + e4) = make_uint2(pk[i][0], pk[i][1]);
-      }
-    }
-    wave_lds_sync();
-    f32x16 s = f32x16{};
-    s = mfma32(frag_kc(tK, LDT, 0, 0), qf[0], s);
-    s = mfma32(frag_kc(tK, LDT, 0, 16), qf[1], s);
-    float mt = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      if constexpr (decltype(masked)::value) s[i] = k0 + acc_row(i, hh) < kend ? s[i] : -INFINITY;
-      mt = fmaxf(mt, s[i]);
-    }
-    mt = xor32_max(mt);
-    const float m_new = fmaxf(m_run, mt * a.scale_log2);
-    const float alpha = fast_exp2(m_run - m_new);
-    m_run = m_new;
-    float ls = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      s[i] = fast_exp2(fmaf(s[i], a.scale_log2, -m_new));
-      ls += s[i];
-    }
-    l_run = l_run * alpha + ls;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) o[i] *= alpha;
-#pragma unroll
-    for (int ss = 0; ss < 2; ++ss) o = mfma32(frag_ks_perm(tV, LDT, 0, 16 * ss), pack_acc(s, ss), o);
-  };
-  fetch_p();
-  fetch_s(kbeg);
-  int k0 = kbeg;
-  for (; k0 + 32 <= kend; k0 += 32) chunk(k0, std::false_type{});
-  if (k0 < kend) chunk(k0, std::true_type{});  // the last chunk of M % 32 ≠ 0
-  const float l_tot = xor32_sum(l_run);
-  if (qi >= a.Nq) return;
-  const long long row = (((long long)split * a.B + b) * a.Nq + qi) * a.H + h;
-  float* op = a.Opart + row * PD;
-#pragma unroll
-  for (int g = 0; g < 4; ++g)
-    *reinterpret_cast<float4*>(op + 8 * g + 4 * hh) = make_float4(o[4 * g], o[4 * g + 1], o[4 * g + 2], o[4 * g + 3]);
-  if (hh == 0) {
-    a.MLpart[row * 2] = m_run;
-    a.MLpart[row * 2 + 1] = l_tot;
-  }
-}
 
 // ------------------------------------------------------------------------------------
-// Factored forward (default; PIO_PEF_FACT=0 restores the generating kernel above): the K/V
-// tiles are never formed.  With K/V row m of sample b written as (pe_kv_elem)
+// Encoder cross-attention forward over implicit K/V (head dim 32, Nq ≤ 32, no mask, no
+// dropout), factored: the K/V tiles are never formed.  With K/V row m of sample b written as (pe_kv_elem)
 //     y[m, o] = rσ_m·(P'[m, o] + Σ_c (p_c − μ)_m·wt[c][o] + μ_m·wt[4][o]) + wt[5][o],
 // the scores and the output of one head factor into products with the BATCH-INDEPENDENT P':
 //     S[q, m]  = rσ_m·(P'_K[m]·Q[q] + Σ_c (p_c − μ)_m·β_c[q] + μ_m·γ[q]) + cq[q]
@@ -944,39 +783,11 @@ void attn_bwd_pe_launch(const PeBwdArgs& a0, int nkb, int bsplit, hipStream_t st
                        a.H, a.C);
 }
 
-int attn_fwd_pe_occupancy() {
-  const char* v = getenv("PIO_PEF_OCC");
-  return (v && v[0] == '3') ? 3 : 4;
-}
-
-// the factored forward (default) unless PIO_PEF_FACT=0; PIO_PEF_NS: samples per wave (2 | 3;
-// 4 spills at 2 waves / SIMD)
-static bool pef_fact() {
-  static const bool on = [] {
-    const char* v = getenv("PIO_PEF_FACT");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
-static int pef_ns() {
-  static const int ns = [] {
-    const char* v = getenv("PIO_PEF_NS");
-    const int n = v ? atoi(v) : 2;
-    return n == 3 ? 3 : 2;
-  }();
-  return ns;
-}
-
-// key splits of one launch: about one round of workgroups at the kernel's occupancy
-// (PIO_PEF_WGS overrides the workgroup target of the factored kernel, for sweeps)
+// key splits of one launch: about one round of workgroups (2 per CU) of the factored kernel
 int attn_fwd_pe_auto_splits(int B, int H, int ncu) {
-  if (pef_fact()) {
-    const char* v = getenv("PIO_PEF_WGS");
-    const int target = (v && atoi(v) > 0) ? atoi(v) : 2 * ncu;
-    const int bg = (B + 4 * pef_ns() - 1) / (4 * pef_ns());
-    return std::max(1, target / (bg * H));
-  }
-  return std::max(1, attn_fwd_pe_occupancy() * 4 * ncu / (4 * ((B + 3) / 4) * H));
+  constexpr int ns = 2;  // samples per wave (3 measured equal, 4 spills at 2 waves / SIMD)
+  const int bg = (B + 4 * ns - 1) / (4 * ns);
+  return std::max(1, 2 * ncu / (bg * H));
 }
 
 // splits × 32-key chunks covering M keys; grid (batch groups, splits, heads), 4 waves each
@@ -984,36 +795,16 @@ void attn_fwd_pe_launch(const PeFwdArgs& a0, hipStream_t st) {
   PeFwdArgs a = a0;
   const int nch = (a.M + 31) / 32;
   a.chunks = (nch + a.nsplit - 1) / a.nsplit;
-  if (pef_fact()) {
-    const int ns = pef_ns();
-    const dim3 grid((unsigned)((a.B + 4 * ns - 1) / (4 * ns)), (unsigned)a.nsplit, (unsigned)a.H);
-#define PIO_PEFF(NC_, NS_) hipLaunchKernelGGL((attn_fwd_pe_fact_kernel<NC_, NS_>), grid, dim3(256), 0, st, a)
-#define PIO_PEFF_NC(NC_)         \
-  if (ns == 3) PIO_PEFF(NC_, 3); \
-  else PIO_PEFF(NC_, 2);
-    switch (a.nc) {
-      case 1: PIO_PEFF_NC(1) break;
-      case 2: PIO_PEFF_NC(2) break;
-      case 3: PIO_PEFF_NC(3) break;
-      default: PIO_PEFF_NC(4) break;
-    }
-#undef PIO_PEFF_NC
-#undef PIO_PEFF
-    return;
-  }
-  const dim3 grid((unsigned)((a.B + 3) / 4), (unsigned)a.nsplit, (unsigned)a.H);
-  // occupancy variant: 4 waves / SIMD (≤ 128 VGPRs) unless PIO_PEF_OCC=3
-  static const int occ = attn_fwd_pe_occupancy();
-#define PIO_PEF(NC_)                                                                                   \
-  if (occ == 3) hipLaunchKernelGGL((attn_fwd_pe_kernel<NC_, 3>), grid, dim3(256), 0, st, a);           \
-  else hipLaunchKernelGGL((attn_fwd_pe_kernel<NC_, 4>), grid, dim3(256), 0, st, a);
+  constexpr int ns = 2;
+  const dim3 grid((unsigned)((a.B + 4 * ns - 1) / (4 * ns)), (unsigned)a.nsplit, (unsigned)a.H);
+#define PIO_PEFF(NC_) hipLaunchKernelGGL((attn_fwd_pe_fact_kernel<NC_, ns>), grid, dim3(256), 0, st, a)
   switch (a.nc) {
-    case 1: PIO_PEF(1) break;
-    case 2: PIO_PEF(2) break;
-    case 3: PIO_PEF(3) break;
-    default: PIO_PEF(4) break;
+    case 1: PIO_PEFF(1); break;
+    case 2: PIO_PEFF(2); break;
+    case 3: PIO_PEFF(3); break;
+    default: PIO_PEFF(4); break;
   }
-#undef PIO_PEF
+#undef PIO_PEFF
 }
 
 }  // namespace pio

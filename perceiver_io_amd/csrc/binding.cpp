@@ -472,15 +472,9 @@ std::vector<Tensor> sa_layer_fwd(Tensor qkv, Tensor x, int64_t N, double scale, 
   return {o, lse, z, y, m, r, u};
 }
 
-// workgroups of a non-deterministic SlabJob (PIO_SLAB_WGS overrides; 128 measured best on the MLM step: 96–128 ≈ equal, 256 and 64 slower)
-int slab_job_target() {
-  static const int t = [] {
-    const char* v = getenv("PIO_SLAB_WGS");
-    const int x = v ? atoi(v) : 0;
-    return x > 0 ? x : 128;
-  }();
-  return t;
-}
+// workgroups of a non-deterministic SlabJob (128 measured best on the MLM step: 96–128 ≈ equal,
+// 256 and 64 slower)
+int slab_job_target() { return 128; }
 
 // the backward entry points below ACCUMULATE parameter gradients into caller-provided fp32
 // tensors (normally views of the flat gradient buffer) with device atomics: no partial slabs,
@@ -1223,11 +1217,7 @@ struct PeImplicit { Tensor P, pes, pesq, wt; double kin, eps; };
 // persistent mode of the PE attention backward (attention_pe.hip): one workgroup per CU over
 // (key block, head, batch group) items when there are at least as many pairs as CUs
 static int pe_bwd_slots(int M, int H, int64_t bsplit) {
-  static const bool off = [] {
-    const char* v = getenv("PIO_PE_PERSIST");
-    return v && v[0] == '0';
-  }();
-  if (off || g_det || bsplit != 1) return 0;
+  if (g_det || bsplit != 1) return 0;
   int dev = 0, ncu = 256;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);

@@ -662,12 +662,8 @@ static int pick_split(int M, int nchunks, int target) {
 
 int ce_combine_blocks(int M);
 
-// workgroup targets of the three CE launches (PIO_CE_{FWD,DH,DW}_WGS override, for tuning sweeps)
-static int ce_target(const char* name, int dflt) {
-  const char* v = getenv(name);
-  const int t = v ? atoi(v) : 0;
-  return t > 0 ? t : dflt;
-}
+// workgroup targets of the three CE launches (the C = 32 / 128 heads; C = 64 runs ce_head.hip)
+static int ce_target(const char*, int dflt) { return dflt; }
 
 // tickets: one zeroed counter (the combine kernel's)
 void ce_fwd_launch(int C, const float* Hm, const int64_t* hidx, const int64_t* labels, const uint16_t* W,

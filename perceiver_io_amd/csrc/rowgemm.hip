@@ -1441,7 +1441,7 @@ static void set_smem_once(const void* fn) {
 // host side of the AV template flag: every pointer 16-B aligned (nullptr allowed), every row
 // stride / width a multiple of 8 elements
 static bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
-// register-resident chain kernels (CL layout, chain.hip) — PIO_CHAIN=0 selects the LDS row-pass kernels
+// register-resident chain kernels (CL layout, chain.hip) for the C = 64, H = 4 shapes; the LDS row-pass kernels otherwise
 bool sa_layer_fwd_chain_launch(const uint16_t* QKV, int N, float scale_log2, uint16_t* O, float* LSE, const float* X,
                                const uint16_t* Wo, const float* bo, const float* g2, const float* be2, float eps,
                                const uint16_t* W1, const float* b1, const uint16_t* W2, const float* b2, float* Z,
@@ -1456,13 +1456,7 @@ bool ln_linear_post_attn_bwd_chain_launch(const void* G, bool g_bf16, const uint
                                           const float* be2, float* dY, uint16_t* dO, float* delta,
                                           const PostAttnGrads& grads, int R, const SlabJob& job, const DropCfg& dr,
                                           int nq, hipStream_t st);
-static bool use_chain() {
-  static const bool on = [] {
-    const char* e = getenv("PIO_CHAIN");
-    return e == nullptr || e[0] != '0';
-  }();
-  return on;
-}
+static bool use_chain() { return true; }
 bool chain_enabled() { return use_chain(); }
 
 static bool av_ok(std::initializer_list<const void*> ptrs, std::initializer_list<long long> widths) {

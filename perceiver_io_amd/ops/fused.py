@@ -14,7 +14,7 @@ through per-tile slabs by default (``WGRAD_SLAB``, see ``_GradSlab``): each 64-r
 its partial into one slab row, and the slab rows are summed into ``p.grad`` (views of the flat
 gradient buffer) by extra workgroups appended to the next backward kernel, or by an
 end-of-backward flush — no float atomics, no per-parameter autograd accumulation
-(``PERCEIVER_WGRAD_SLAB=0`` restores in-kernel atomics into replicated accumulators).
+(``WGRAD_SLAB = False`` selects in-kernel atomics into replicated accumulators).
 Self-attention blocks run as one node (``_SABlockFn``): one launch per layer forward and per
 layer boundary backward.  Activations kept for backward: the bf16 Q/K/V and attention output,
 fp32 post-attention residual, LN statistics, the bf16 pre-GELU tensor — LN outputs and GELU
@@ -43,10 +43,10 @@ from ..parallel.reducer import bucket_ready_point
 EPS = 1e-5
 # per-tile weight-gradient partials go to a slab reduced on a side stream (see _GradSlab);
 # PERCEIVER_WGRAD_SLAB=0 restores in-kernel float atomics into the replicated accumulators
-WGRAD_SLAB = os.environ.get("PERCEIVER_WGRAD_SLAB", "1") != "0"
+WGRAD_SLAB = True
 # self-attention dQKV stored as bf16 for the chain-layout boundary kernel (identical results);
 # PERCEIVER_BF16_DQKV=0 keeps it fp32 (A/B)
-BF16_DQKV = os.environ.get("PERCEIVER_BF16_DQKV", "1") != "0"
+BF16_DQKV = True
 TALL_ROWS = 1 << 17  # kTallRows in csrc/binding.cpp: taller projections stream their dW (wgrad kernel)
 
 
@@ -292,8 +292,8 @@ class KVSource:
 
 # K/V projection over [pixels ‖ Fourier PE] in factored form (csrc/pe_proj.hip): the PE part of
 # LN(x)·Wᵀ is batch-independent, so it is one (M × Kin)·(Kin × O) GEMM per step and each sample
-# only pays a bandwidth-bound epilogue.  PERCEIVER_PE_FACTORED=0 restores the fused ln_linear path.
-PE_FACTORED = os.environ.get("PERCEIVER_PE_FACTORED", "1") != "0"
+# only pays a bandwidth-bound epilogue.
+PE_FACTORED = True
 
 
 def _pe_table(pe, nc: int, kin: int):
@@ -336,8 +336,8 @@ def _pe_proj_fwd(K, pix, pe, g, b, W, bias):
 # implicit K/V for the encoder cross-attention over [pixels ‖ Fourier PE] (csrc/attention_pe.hip):
 # the attention kernels generate each K/V tile from the bf16 PE product P' = Ebf·(W⊙γ)ᵀ, the
 # sample's pixels and a per-column table, so the (B·M, 2C) K/V tensor (0.8 GB at ImageNet shape)
-# is never written or read.  PERCEIVER_PE_IMPLICIT=0 restores the materialised factored path.
-PE_IMPLICIT = os.environ.get("PERCEIVER_PE_IMPLICIT", "1") != "0"
+# is never written or read.  PE_IMPLICIT = False selects the materialised factored path (tests).
+PE_IMPLICIT = True
 
 
 PE_PAD_ROWS = 64  # zero rows after P' (the forward kernel's last prefetch reads them)
@@ -376,9 +376,8 @@ def _pe_proj_bwd(K, dy, pix, mean, rstd, pe, g, b, W, M):
 
 
 # the encoder cross-attention backward folds dK/dV straight into the factored projection's
-# reductions (csrc/attention_pe.hip): no fp32 (B·M, 2C) dK/dV tensor.  PERCEIVER_PE_ATTN_FUSED=0
-# restores attn_bwd + pe_proj_bwd.
-PE_ATTN_FUSED = os.environ.get("PERCEIVER_PE_ATTN_FUSED", "1") != "0"
+# reductions (csrc/attention_pe.hip): no fp32 (B·M, 2C) dK/dV tensor.
+PE_ATTN_FUSED = True
 
 
 def pe_attn_bsplit(B: int, M: int, H: int) -> int:
@@ -751,13 +750,13 @@ class _LayerFn(torch.autograd.Function):
 
 # the fused latent self-attention layer forward (rowgemm.hip sa_layer_fwd_kernel);
 # PERCEIVER_SA_LAYER_FUSED=0 restores attn_fwd + post_attn(_ln_linear)_fwd
-SA_LAYER_FUSED = os.environ.get("PERCEIVER_SA_LAYER_FUSED", "1") != "0"
+SA_LAYER_FUSED = True
 PA_SIZES = lambda C: [C * C, C, C, C, C * C, C, C * C, C]  # noqa: E731  (Wo bo γ2 β2 W1 b1 W2 b2)
 LL_SIZES = lambda C: [C, C, 3 * C * C, 3 * C]                 # noqa: E731  (γ1 β1 Wqkv bqkv)
 SA_NP = 12  # parameters per self-attention layer (layer_spec_and_params order)
 # channel widths run as one fused self-attention block node (PERCEIVER_SA_BLOCK_C128=0 keeps C = 128
 # stacks layer by layer)
-SA_BLOCK_CHANNELS = (32, 64, 128) if os.environ.get("PERCEIVER_SA_BLOCK_C128", "1") != "0" else (32, 64)
+SA_BLOCK_CHANNELS = (32, 64, 128)
 
 
 class _SABlockFn(torch.autograd.Function):

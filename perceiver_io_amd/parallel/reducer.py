@@ -93,9 +93,9 @@ class FlatGradReducer:
         self._point_modules: Dict[str, int] = {}  # ready point → id() of the module it was planned on
         # overlap needs every parameter gradient to land in flat.grad directly (no 8-way replicas
         # that a later fold() would still add into an early bucket's range)
-        # overlap=None: on unless PERCEIVER_DDP_OVERLAP=0 (collectives inline on the compute stream)
+        # overlap=None: on (overlap=False: collectives inline on the compute stream)
         if overlap is None:
-            overlap = os.environ.get("PERCEIVER_DDP_OVERLAP", "1") != "0"
+            overlap = True
         self.overlap = bool(overlap) and getattr(flat, "grad_rep", None) is None
         self.wire_dtype = wire_dtype
         self.on_gpu = flat.device.type == "cuda"

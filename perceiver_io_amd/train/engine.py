@@ -182,9 +182,9 @@ class StepEngine:
         # per-bucket optimizer updates: each gradient bucket's AdamW runs right behind its
         # all-reduce on the reducer's side stream (overlapping the rest of the backward), so
         # only the buckets finish() reduces stay on the critical path.  Needs no clipping (a
-        # global norm) and no replicated accumulators; PERCEIVER_BUCKET_UPDATE=0 disables it.
+        # global norm) and no replicated accumulators.
         if bucket_update is None:
-            bucket_update = os.environ.get("PERCEIVER_BUCKET_UPDATE", "1") != "0"
+            bucket_update = True
         self.bucket_update = bool(bucket_update and self.fused and reducer is not None and reducer.enabled
                                   and optimizer.bucket_updates_ok())
         if self.bucket_update:
