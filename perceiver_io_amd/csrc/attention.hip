@@ -367,8 +367,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
                                                            long long dq_bs, int dq_rs, float* __restrict__ dk,
                                                            long long dk_bs, int dk_rs, float* __restrict__ dv,
                                                            long long dv_bs, int dv_rs, int dq_atomic, int kv_acc,
-                                                           long long dq_kbs, int nqs, int q_tiles_per_split,
-                                                           SlabJob job) {
+                                                           long long dq_kbs, int nqs, int q_tiles_per_split) {
   constexpr int LD = (D < 32 ? 32 : D) + 8;  // Q / dO / K tiles [row][d] (D=16 zero-padded to 32 cols)
   constexpr int NT = (D < 32) ? 1 : D / 32;
   constexpr int KS = D / 16;
@@ -389,15 +388,10 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
   __shared__ __attribute__((aligned(16))) float sL[NQS * 32];
   __shared__ __attribute__((aligned(16))) float sDl[NQS * 32];
 
-  if ((int)blockIdx.z >= a.B) {  // appended workgroups: a slab job of the previous backward kernel
-    const int id = ((blockIdx.z - a.B) * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-    if (id < job.nblk) slab_reduce_block(job, id, reinterpret_cast<float4*>(sdS));
-    return;
-  }
   PIO_WG_BEGIN();
   PIO_TS(0);
   const int w = wave_id(), l = lane_id(), r = l & 31, hh = l >> 5;
-  const Blk3 blk = xcd_block3(a.B);  // the heads / key blocks of one batch element share an L2
+  const Blk3 blk = xcd_block3();  // the heads / key blocks of one batch element share an L2
   const int h = blk.y, b = blk.z;
   // blk.x = key block × nqs + query split: many-query / few-key shapes (a decoder's pixel or
   // token queries over a few dozen latents) split the query range across workgroups, whose
@@ -833,13 +827,13 @@ static void bwd_launch_t(const AttnArgs& a, const uint16_t* dO, const float* LSE
   // share a CU
   if (a.Nq <= 32 && small_lds)
     hipLaunchKernelGGL((attn_bwd_kernel<D, NW, 1>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs,
-                       dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs, nqs, tps, SlabJob{});
+                       dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs, nqs, tps);
   else if (a.Nq <= 64 && small_lds)
     hipLaunchKernelGGL((attn_bwd_kernel<D, NW, 2>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs,
-                       dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs, nqs, tps, SlabJob{});
+                       dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs, nqs, tps);
   else
     hipLaunchKernelGGL((attn_bwd_kernel<D, NW>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs, dk,
-                       dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs, nqs, tps, SlabJob{});
+                       dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs, nqs, tps);
 }
 
 // key blocks of the backward grid (dQ partial slices in deterministic mode)
@@ -873,19 +867,15 @@ void attn_bwd_launch(const AttnArgs& a, int D, const uint16_t* O, const uint16_t
 bool attn_bwd_bf16_ok(const AttnArgs& a, int D) {
   return D == 16 && a.Nk <= 32 * 8 && a.Nq > 64 && bwd_query_splits(1, a.H, a.B, a.Nq, 1) == 1;
 }
-// job: a slab reduction of the previous backward kernel, run by workgroups appended to the grid
-// (z ≥ B): the latency-bound attention backward leaves the memory system idle, where the
-// following layer-boundary kernel would pay for the job at its own bandwidth-bound start
 bool attn_bwd_bf16_launch(const AttnArgs& a, int D, const uint16_t* dO, const float* LSE, const float* delta,
                           uint16_t* dq, long long dq_bs, int dq_rs, uint16_t* dk, long long dk_bs, int dk_rs,
-                          uint16_t* dv, long long dv_bs, int dv_rs, const SlabJob& job, hipStream_t st) {
+                          uint16_t* dv, long long dv_bs, int dv_rs, hipStream_t st) {
   if (!attn_bwd_bf16_ok(a, D)) return false;
   const int nqt = (a.Nq + 31) / 32;
-  const int zextra = job.slab ? (job.nblk + a.H - 1) / a.H : 0;
-  dim3 grid(1, a.H, a.B + zextra);
+  dim3 grid(1, a.H, a.B);
   hipLaunchKernelGGL((attn_bwd_kernel<16, 8, 0, true>), grid, dim3(512), 0, st, a, dO, LSE, delta,
                      reinterpret_cast<float*>(dq), dq_bs, dq_rs, reinterpret_cast<float*>(dk), dk_bs, dk_rs,
-                     reinterpret_cast<float*>(dv), dv_bs, dv_rs, 0, 0, 0LL, 1, nqt, job);
+                     reinterpret_cast<float*>(dv), dv_bs, dv_rs, 0, 0, 0LL, 1, nqt);
   return true;
 }
 

@@ -53,7 +53,7 @@ void attn_bwd_launch(const AttnArgs&, int, const uint16_t*, const uint16_t*, con
 int attn_bwd_key_blocks(int, int);
 bool attn_bwd_bf16_ok(const AttnArgs&, int);
 bool attn_bwd_bf16_launch(const AttnArgs&, int, const uint16_t*, const float*, const float*, uint16_t*, long long, int,
-                          uint16_t*, long long, int, uint16_t*, long long, int, const SlabJob&, hipStream_t);
+                          uint16_t*, long long, int, uint16_t*, long long, int, hipStream_t);
 int attn_bwd_zero_plan(int, int, int, int, int);
 void ln_linear_fwd_launch(const void*, bool, int, int, int, const float*, const float*, float, const uint16_t*, int,
                           const float*, int, int, const float*, int, void*, bool, int, float*, float*, const float*, int,
@@ -108,6 +108,7 @@ void embed_fwd_launch(const int64_t*, const float*, const float*, float*, long l
                       hipStream_t);
 unsigned check_errors_elementwise(bool);
 unsigned check_errors_mlm_head(bool);
+unsigned check_errors_ce_head(bool);
 void embed_bwd_launch(const int64_t*, const float*, float*, float*, int, int, int, float, hipStream_t);
 void embed_bwd_sorted_launch(const int64_t*, const int64_t*, const float*, float*, long long, int, float, hipStream_t);
 bool embed_bwd_local_launch(const int64_t*, const float*, float*, float*, int, int, int, float, hipStream_t);
@@ -159,7 +160,8 @@ hipStream_t stream() { return at::hip::getCurrentHIPStream(); }
 // outside the embedding table, 2: a gather row outside its destination, 4: a class label
 // outside [0, V) ∪ {-100}); reset clears them
 int64_t check_errors(bool reset) {
-  return (int64_t)(pio::check_errors_elementwise(reset) | pio::check_errors_mlm_head(reset));
+  return (int64_t)(pio::check_errors_elementwise(reset) | pio::check_errors_mlm_head(reset) |
+                   pio::check_errors_ce_head(reset));
 }
 bool checked_build() { return PIO_CHECKS != 0; }
 // checked builds, outside graph capture: wait for the kernel just launched and raise on any
@@ -277,14 +279,10 @@ std::vector<Tensor> attn_fwd(Tensor q, Tensor k, Tensor v, OptT kmask, int64_t H
 // a dq_out view must be batch-dense (batch stride == Nq * row stride); it needs no zero fill
 // (the launcher clears it itself when several key blocks accumulate into it).  delta_in ((B, Nq, H) fp32 rowsum(dO∘O), e.g. from post_attn_bwd)
 // skips the delta pass.
-void slab_reduce(Tensor slab, std::vector<Tensor> dsts, std::vector<int64_t> offs);
-namespace {
-pio::SlabJob make_job(const OptT& slab, std::vector<Tensor>& dsts, const std::vector<int64_t>& offs);
-}
 std::vector<Tensor> attn_bwd(Tensor q, Tensor k, Tensor v, OptT kmask, Tensor o, Tensor dO, Tensor lse, OptT delta_in,
                              int64_t H, int64_t D, double scale, double dropout_p, OptT seed, OptT dq_out,
                              OptT dk_out, OptT dv_out, bool kv_accumulate, int64_t site, bool dq_zeroed,
-                             bool kv_zeroed, OptT job_slab, std::vector<Tensor> job_dsts, std::vector<int64_t> job_offs) {
+                             bool kv_zeroed) {
   auto a = make_args(q, k, v, kmask, (int)H, (int)D, scale, dropout_p, seed, site);
   TORCH_CHECK(dO.is_contiguous() && o.is_contiguous(), "O / dO must be contiguous (B, Nq, H*D)");
   auto f32 = q.options().dtype(torch::kFloat32);
@@ -302,17 +300,13 @@ std::vector<Tensor> attn_bwd(Tensor q, Tensor k, Tensor v, OptT kmask, Tensor o,
     if (pio::attn_bwd_bf16_ok(a, (int)D)) {
       pio::attn_bwd_bf16_launch(a, (int)D, bfp(dO), f32p(lse), delta.data_ptr<float>(), bfp_mut(dq), dq.stride(0),
                                 (int)dq.stride(1), bfp_mut(dk), dk.stride(0), (int)dk.stride(1), bfp_mut(dv),
-                                dv.stride(0), (int)dv.stride(1), make_job(job_slab, job_dsts, job_offs), stream());
+                                dv.stride(0), (int)dv.stride(1), stream());
     } else {  // shape not covered by the bf16 variant: fp32, then narrowed
       auto r = attn_bwd(q, k, v, kmask, o, dO, lse, delta_in, H, D, scale, dropout_p, seed, c10::nullopt, c10::nullopt,
-                        c10::nullopt, false, site, false, false, job_slab, job_dsts, job_offs);
+                        c10::nullopt, false, site, false, false);
       dq.copy_(r[0]); dk.copy_(r[1]); dv.copy_(r[2]);
     }
     return {dq, dk, dv};
-  }
-  if (job_slab.has_value()) {  // the fp32 variants carry no job: run it as its own launch first
-    auto jd = job_dsts;
-    slab_reduce(*job_slab, jd, job_offs);
   }
   Tensor dq = dq_out.has_value() ? *dq_out : torch::empty({a.B, a.Nq, H * D}, f32);
   Tensor dk = dk_out.has_value() ? *dk_out : torch::empty({a.B, a.Nk, H * D}, f32);
@@ -1400,9 +1394,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_bwd", &attn_bwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("kmask"), py::arg("o"), py::arg("dO"),
         py::arg("lse"), py::arg("delta_in"), py::arg("H"), py::arg("D"), py::arg("scale"), py::arg("dropout_p"),
         py::arg("seed"), py::arg("dq_out"), py::arg("dk_out"), py::arg("dv_out"), py::arg("kv_accumulate") = false,
-        py::arg("site") = 0, py::arg("dq_zeroed") = false, py::arg("kv_zeroed") = false,
-        py::arg("job_slab") = py::none(), py::arg("job_dsts") = std::vector<Tensor>(),
-        py::arg("job_offs") = std::vector<int64_t>());
+        py::arg("site") = 0, py::arg("dq_zeroed") = false, py::arg("kv_zeroed") = false);
   m.def("attn_bwd_zero_plan", &pio::attn_bwd_zero_plan, py::arg("B"), py::arg("H"), py::arg("Nq"), py::arg("Nk"),
         py::arg("D"));
   m.def("ln_linear_fwd", &ln_linear_fwd, py::arg("x"), py::arg("lnw"), py::arg("lnb"), py::arg("eps"), py::arg("w"),

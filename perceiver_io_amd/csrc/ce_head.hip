@@ -108,6 +108,9 @@ __global__ __launch_bounds__(256) void ce2_fwd_kernel(const float* __restrict__ 
       for (int s = 0; s < 4; ++s) *reinterpret_cast<bf16x8*>(hs_out + (long long)gr * C + 16 * s + 8 * hh) = hb[s];
   }
   const int lab = rin ? (int)labels[gr] : -100;
+#if PIO_CHECKS
+  if (split == 0 && hh == 0 && (lab >= V || (lab < 0 && lab != -100))) pio_flag(kErrLabel);
+#endif
   // chunk staging: 64 vocab rows × 8 slots = 512 16-byte pieces, two per thread (+ the bias)
   bf16x8 wr[2];
   float bnext = 0.f;
@@ -218,6 +221,7 @@ __global__ __launch_bounds__(256) void ce2_fwd_kernel(const float* __restrict__ 
 // with the deterministic last-workgroup ticket of mlm_head.hip.  Also clears zero_out (the
 // backward's dH buffer, float4 slices per workgroup).
 constexpr int kC2Rows = 16;
+constexpr int kCeMaxSplits = 16;  // ce2_num_splits caps the vocab splits here
 __global__ __launch_bounds__(256) void ce2_combine_kernel(const float2* __restrict__ part_ml,
                                                           const float* __restrict__ part_acc,
                                                           const float* __restrict__ picked,
@@ -235,16 +239,25 @@ __global__ __launch_bounds__(256) void ce2_combine_kernel(const float2* __restri
   const int r = blockIdx.x * kC2Rows + rr;
   float lr = 0.f, nr = 0.f;
   if (r < M) {
+    // every split's loads in flight at once (kMaxSplits-unrolled, address selects past nsplit)
+    float2 ml[kCeMaxSplits];
+    float4 v[kCeMaxSplits];
+#pragma unroll
+    for (int s = 0; s < kCeMaxSplits; ++s) {
+      const int ss = s < nsplit ? s : 0;
+      ml[s] = part_ml[(long long)ss * M + r];
+      v[s] = *reinterpret_cast<const float4*>(part_acc + ((long long)ss * M + r) * C + 4 * cq);
+    }
     float mx = -__builtin_inff();
-    for (int s = 0; s < nsplit; ++s) mx = fmaxf(mx, part_ml[(long long)s * M + r].x);
+#pragma unroll
+    for (int s = 0; s < kCeMaxSplits; ++s) mx = s < nsplit ? fmaxf(mx, ml[s].x) : mx;
     float L = 0.f;
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int s = 0; s < nsplit; ++s) {
-      const float2 ml = part_ml[(long long)s * M + r];
-      const float f = fast_exp2(ml.x - mx);
-      L += ml.y * f;
-      const float4 v = *reinterpret_cast<const float4*>(part_acc + ((long long)s * M + r) * C + 4 * cq);
-      a.x = fmaf(v.x, f, a.x); a.y = fmaf(v.y, f, a.y); a.z = fmaf(v.z, f, a.z); a.w = fmaf(v.w, f, a.w);
+#pragma unroll
+    for (int s = 0; s < kCeMaxSplits; ++s) {
+      const float f = s < nsplit ? fast_exp2(ml[s].x - mx) : 0.f;
+      L = fmaf(ml[s].y, f, L);
+      a.x = fmaf(v[s].x, f, a.x); a.y = fmaf(v[s].y, f, a.y); a.z = fmaf(v[s].z, f, a.z); a.w = fmaf(v[s].w, f, a.w);
     }
     const int lab = (int)labels[r];
     const float inv = 1.f / L;
@@ -445,6 +458,7 @@ int ce2_num_splits(int M, int V) {
   s = s < 1 ? 1 : s;
   const int cap = (nchunks + 3) / 4;
   s = s > cap ? cap : s;
+  s = s > kCeMaxSplits ? kCeMaxSplits : s;
   const int cps = (nchunks + s - 1) / s;
   return (nchunks + cps - 1) / cps;
 }
@@ -485,5 +499,7 @@ void ce2_bwd_launch(const uint16_t* Hs, const int64_t* labels, const uint16_t* W
   hipLaunchKernelGGL(ce2_bwd_kernel, dim3((V + ce2::VB2 - 1) / ce2::VB2, rsplit + 1), dim3(256), 0, st, Hs, labels, W, bias,
                      lse, u, gout, count, M, V, rsplit, tps, dW, db, slab, dH, rowmap, dh_rows);
 }
+
+unsigned check_errors_ce_head(bool reset) { return pio_read_errors(reset); }
 
 }  // namespace pio

@@ -270,11 +270,11 @@ __global__ __launch_bounds__(kCombineRows * kCombineQ) void ce_combine_kernel(
   }
   t = wave_sum(t);
   n = wave_sum(n);
-  if (lane_id() == 0) { red[wave_id()] = t; red[8 + wave_id()] = n; }
+  if (lane_id() == 0) { red[wave_id()] = t; red[16 + wave_id()] = n; }  // 16 waves
   __syncthreads();
   if (threadIdx.x == 0) {
     float tt = 0.f, nn = 0.f;
-    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) { tt += red[k]; nn += red[8 + k]; }
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) { tt += red[k]; nn += red[16 + k]; }
     // count_labels: the denominator is the number of rows with a label (written for the backward)
     if (count_labels) count[0] = nn;
     loss[0] = tt / fmaxf(count_labels ? nn : count[0], 1.f);

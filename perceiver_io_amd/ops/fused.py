@@ -917,11 +917,9 @@ class _SABlockFn(torch.autograd.Function):
             xl, qkv, mean1, rstd1, o, lse, y, m2, r2, u = S[i]
             qkv3 = qkv.view(B, N, 3 * C)
             dqkv = dqkv_next
-            # the attention backward carries the previous boundary kernel's slab reduction (its
-            # memory system is idle; the boundary kernel's own start is bandwidth-bound)
             K.attn_bwd(qkv3[:, :, :C], qkv3[:, :, C:2 * C], qkv3[:, :, 2 * C:], None, o, do.view(B, N, C), lse,
                        delta.view(B, N, H), H, D, scale, ctx.p, ctx.seed, dqkv[:, :, :C], dqkv[:, :, C:2 * C],
-                       dqkv[:, :, 2 * C:], site=i, dq_zeroed=bool(zp & 1), kv_zeroed=bool(zp & 2), **_take_job())
+                       dqkv[:, :, 2 * C:], site=i, dq_zeroed=bool(zp & 1), kv_zeroed=bool(zp & 2))
             if i > 0:
                 dqkv_next, zkw = new_dqkv(i - 1)
                 sl = _GradSlab(R, LL_SIZES(C) + PA_SIZES(C), dz2)

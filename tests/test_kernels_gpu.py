@@ -26,6 +26,9 @@ def _emu():
 
 
 def close(a, b, rel=2e-2, name=""):
+    """Per output: relative Frobenius error ≤ min(rel, 1 %) (sensitive to errors anywhere, also in
+    small-magnitude regions) AND max-abs error ≤ rel × the reference's largest value (a local
+    outlier cannot hide in the norm); identical non-finite patterns."""
     a, b = a.float().cpu(), b.float().cpu()
     assert a.shape == b.shape, (name, a.shape, b.shape)
     fin = torch.isfinite(b)
@@ -33,6 +36,8 @@ def close(a, b, rel=2e-2, name=""):
     a, b = a[fin], b[fin]
     if b.numel() == 0:
         return
+    fro = ((a.double() - b.double()).norm() / (b.double().norm() + 1e-30)).item()
+    assert fro <= min(rel, 1e-2), f"{name}: relative Frobenius error {fro:.3e}"
     scale = b.abs().max().item() + 1e-6
     err = (a - b).abs().max().item()
     assert err <= rel * scale, f"{name}: max err {err:.3e} vs scale {scale:.3e}"
