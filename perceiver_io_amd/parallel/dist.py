@@ -62,6 +62,11 @@ def init(backend: str | None = None, timeout_s: float = 1800.0, device_type: str
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     if device_type == "cuda":
         torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+    elif "OMP_NUM_THREADS" not in os.environ:
+        # CPU ranks of one node share its cores: without a split every rank's intra-op pool spans
+        # all of them, and the oversubscribed, spinning pools run ~10x slower than split ones
+        local_ws = int(os.environ.get("LOCAL_WORLD_SIZE", str(ws)))
+        torch.set_num_threads(max(1, (os.cpu_count() or 1) // max(1, local_ws)))
     if not dist.is_initialized():
         kw = dict(backend=backend, rank=rank, world_size=ws, timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
