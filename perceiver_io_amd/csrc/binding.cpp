@@ -117,7 +117,7 @@ void text_mask_launch(const int64_t*, const bool*, int64_t*, int64_t*, int64_t*,
 int stage_step_launch(void* const*, const void* const*, const long long*, int, float*, const float*, int, hipStream_t);
 void sumsq_launch(const float*, long long, float*, hipStream_t);
 void index_add_rows_launch(float*, long long, const int64_t*, const float*, long long, int, hipStream_t);
-void batch_sum2_launch(const float*, const float*, float*, float*, int, long long, hipStream_t);
+void batch_sum2_launch(const float*, const float*, float*, float*, int, long long, long long, int, hipStream_t);
 void pe_gemm_launch(const uint16_t*, const uint16_t*, void*, bool, int, int, int, int, hipStream_t);
 struct PeGradTargets { float *dWa, *dWb, *db, *dg, *dbeta; };
 int pe_grad_splits(int);
@@ -644,7 +644,7 @@ constexpr int kTallRows = 1 << 17;
 
 OptT ln_linear_bwd(Tensor g, Tensor w, Tensor x, OptT mean, OptT rstd, OptT lnw, OptT lnb, OptT dres, bool need_dx,
                    OptT dlnw, OptT dlnb, OptT dW, OptT db, OptT pe, int64_t kin, bool slab, OptT job_slab,
-                   std::vector<Tensor> job_dsts, std::vector<int64_t> job_offs) {
+                   std::vector<Tensor> job_dsts, std::vector<int64_t> job_offs, OptT dx_out) {
   TORCH_CHECK(g.dim() == 2 && g.stride(1) == 1 && x.dim() == 2 && x.stride(1) == 1, "g / x must be 2-D rows");
   const int R = (int)g.size(0), N = (int)g.size(1);
   TORCH_CHECK(!(slab && R >= kTallRows), "slab gradients are for R < ", kTallRows, " rows");
@@ -662,7 +662,17 @@ OptT ln_linear_bwd(Tensor g, Tensor w, Tensor x, OptT mean, OptT rstd, OptT lnw,
   Tensor dx;
   float *dxp = nullptr, *dgp = nullptr, *dbp = nullptr, *dwp = nullptr, *dbiasp = nullptr;
   int vrs = -1;
-  if (need_dx) { dx = torch::empty({R, Kin}, f32); dxp = dx.data_ptr<float>(); }
+  int dx_rs = Kin;
+  if (need_dx && dx_out.has_value()) {
+    // dX into a given (R, Kin) fp32 buffer (e.g. a parameter's gradient view); it may BE dres
+    // (read and written element-wise by the same thread: dX = LN_bwd(...) + dres in place)
+    CHECK_DT(*dx_out, torch::kFloat32);
+    TORCH_CHECK(dx_out->dim() == 2 && dx_out->size(0) == R && dx_out->size(1) == Kin && dx_out->stride(1) == 1,
+                "dx_out must be (R, Kin) rows");
+    TORCH_CHECK(!dres.has_value() || dres->data_ptr() != dx_out->data_ptr() || dres->stride(0) == dx_out->stride(0),
+                "dx_out aliasing dres needs the same row stride");
+    dx = *dx_out; dxp = dx.data_ptr<float>(); dx_rs = (int)dx.stride(0);
+  } else if (need_dx) { dx = torch::empty({R, Kin}, f32); dxp = dx.data_ptr<float>(); }
   if (lnw.has_value()) {
     TORCH_CHECK(lnb.has_value() && mean.has_value() && rstd.has_value(), "LN weight needs bias and row stats");
     TORCH_CHECK(dlnw.has_value() && dlnb.has_value(), "LN grad targets required");
@@ -680,7 +690,7 @@ OptT ln_linear_bwd(Tensor g, Tensor w, Tensor x, OptT mean, OptT rstd, OptT lnw,
   const bool tall = dwp != nullptr && R >= kTallRows;
   pio::ln_linear_bwd_launch(g.data_ptr(), is_bf16(g), (int)g.stride(0), N, bfp(w), (int)w.size(1), Kin, x.data_ptr(),
                             is_bf16(x), (int)x.stride(0), f32o(mean), f32o(rstd), f32o(lnw), f32o(lnb), dr, drs, dxp,
-                            Kin, dgp, dbp, tall ? nullptr : dwp, tall ? nullptr : dbiasp, vrs < 0 ? 0 : vrs,
+                            dx_rs, dgp, dbp, tall ? nullptr : dwp, tall ? nullptr : dbiasp, vrs < 0 ? 0 : vrs,
                             wrs < 0 ? 0 : wrs, slab ? 1 : 0, R, pp, prs, prows, npix,
                             make_job(job_slab, job_dsts, job_offs), stream());
   if (tall)
@@ -973,16 +983,32 @@ void stage_step(std::vector<Tensor> dsts, std::vector<Tensor> srcs, OptT hyper_d
 void sumsq(Tensor g, Tensor out) { pio::sumsq_launch(f32p(g), g.numel(), out.data_ptr<float>(), stream()); }
 
 // a, b: (B, ...) fp32 contiguous, equal shapes → (Σ_b a[b], Σ_b b[b]) in one launch
-std::vector<Tensor> batch_sum2(Tensor a, Tensor b) {
-  CHECK_DT(a, torch::kFloat32); CHECK_DT(b, torch::kFloat32);
-  TORCH_CHECK(a.is_contiguous() && b.is_contiguous() && a.sizes() == b.sizes() && a.dim() >= 2, "batch_sum2: shapes");
-  const long long n = a.numel() / a.size(0);
-  TORCH_CHECK(n % 4 == 0 && reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 &&
-              reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0, "batch_sum2: 16-byte rows");
-  std::vector<int64_t> shp(a.sizes().begin() + 1, a.sizes().end());
-  Tensor oa = torch::empty(shp, a.options()), ob = torch::empty(shp, a.options());
-  pio::batch_sum2_launch(a.data_ptr<float>(), b.data_ptr<float>(), oa.data_ptr<float>(), ob.data_ptr<float>(),
-                         (int)a.size(0), n, stream());
+// oa = Σ_b a[b] (a optional), ob = Σ_b b[b] — or, with ob_acc, ob_acc += Σ_b b[b] in place (the
+// gradient of a batch-broadcast parameter straight into its gradient buffer)
+std::vector<Tensor> batch_sum2(OptT a, Tensor b, OptT ob_acc) {
+  CHECK_DT(b, torch::kFloat32);
+  TORCH_CHECK(b.is_contiguous() && b.dim() >= 2, "batch_sum2: b must be contiguous (B, ...)");
+  const long long n = b.numel() / b.size(0);
+  TORCH_CHECK(n % 4 == 0 && reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0, "batch_sum2: 16-byte rows");
+  if (a.has_value()) {
+    CHECK_DT(*a, torch::kFloat32);
+    TORCH_CHECK(a->is_contiguous() && a->sizes() == b.sizes() && reinterpret_cast<uintptr_t>(a->data_ptr()) % 16 == 0,
+                "batch_sum2: a must match b");
+  }
+  std::vector<int64_t> shp(b.sizes().begin() + 1, b.sizes().end());
+  Tensor oa = a.has_value() ? torch::empty(shp, b.options()) : Tensor();
+  Tensor ob;
+  if (ob_acc.has_value()) {
+    CHECK_DT(*ob_acc, torch::kFloat32);
+    TORCH_CHECK(ob_acc->is_contiguous() && ob_acc->numel() == n && reinterpret_cast<uintptr_t>(ob_acc->data_ptr()) % 16 == 0,
+                "batch_sum2: ob_acc must be a contiguous, 16-byte aligned tensor of one batch element's size");
+    ob = ob_acc->view(shp);
+  } else {
+    ob = torch::empty(shp, b.options());
+  }
+  pio::batch_sum2_launch(a.has_value() ? a->data_ptr<float>() : nullptr, b.data_ptr<float>(),
+                         a.has_value() ? oa.data_ptr<float>() : nullptr, ob.data_ptr<float>(), (int)b.size(0), n, n,
+                         ob_acc.has_value() ? 1 : 0, stream());
   return {oa, ob};
 }
 
@@ -1428,14 +1454,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("lnw"), py::arg("lnb"), py::arg("dres"), py::arg("need_dx"), py::arg("dlnw"), py::arg("dlnb"),
         py::arg("dW"), py::arg("db"), py::arg("pe") = py::none(), py::arg("kin") = -1, py::arg("slab") = false,
         py::arg("job_slab") = py::none(), py::arg("job_dsts") = std::vector<Tensor>(),
-        py::arg("job_offs") = std::vector<int64_t>());
+        py::arg("job_offs") = std::vector<int64_t>(), py::arg("dx_out") = py::none());
   m.def("wgrad", &wgrad, py::arg("g"), py::arg("a"), py::arg("amode"), py::arg("mean"), py::arg("rstd"), py::arg("lnw"),
         py::arg("lnb"), py::arg("rows_per_wg"), py::arg("dW"), py::arg("db"), py::arg("pe") = py::none(),
         py::arg("kin") = -1);
   m.def("mlm_select", &mlm_select, py::arg("labels"), py::arg("cap"), py::arg("gcap"), py::arg("sticky") = py::none(),
         py::arg("queries") = py::none());
   m.def("index_add_rows", &index_add_rows);
-  m.def("batch_sum2", &batch_sum2);
+  m.def("batch_sum2", &batch_sum2, py::arg("a"), py::arg("b"), py::arg("ob_acc") = py::none());
   m.def("pixel_ce_fwd", &pixel_ce_fwd);
   m.def("pixel_ce_bwd", &pixel_ce_bwd);
   m.def("stage_step", &stage_step, py::arg("dsts"), py::arg("srcs"), py::arg("hyper_dst") = py::none(),

@@ -376,14 +376,14 @@ void index_add_rows_launch(float* dst, long long nrows, const int64_t* idx, cons
 // order (deterministic).  n a multiple of 4, 16-byte aligned rows.
 __global__ __launch_bounds__(256) void batch_sum2_kernel(const float* __restrict__ a, const float* __restrict__ b,
                                                          float* __restrict__ oa, float* __restrict__ ob, int B,
-                                                         long long n4) {
+                                                         long long na4, long long nb4, int acc_b) {
   __shared__ float4 part[4][64];
   const int l = threadIdx.x & 63, g = threadIdx.x >> 6;
   const long long c = (long long)blockIdx.x * 64 + l;  // float4 column of [a | b]
-  const bool second = c >= n4;
-  const long long cc = second ? c - n4 : c;
+  const bool second = c >= na4;
+  const long long cc = second ? c - na4 : c, n4 = second ? nb4 : na4;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (c < 2 * n4) {
+  if (c < na4 + nb4) {
     const float4* src = reinterpret_cast<const float4*>(second ? b : a) + cc;
 #pragma unroll 8
     for (int bb = g; bb < B; bb += 4) {
@@ -393,19 +393,26 @@ __global__ __launch_bounds__(256) void batch_sum2_kernel(const float* __restrict
   }
   part[g][l] = acc;
   __syncthreads();
-  if (g == 0 && c < 2 * n4) {
+  if (g == 0 && c < na4 + nb4) {
     float4 r = part[0][l];
 #pragma unroll
     for (int k = 1; k < 4; ++k) {
       const float4 v = part[k][l];
       r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
     }
-    reinterpret_cast<float4*>(second ? ob : oa)[cc] = r;
+    float4* dst = reinterpret_cast<float4*>(second ? ob : oa) + cc;
+    if (second && acc_b) {  // ob += Σ_b b (e.g. straight into a parameter's gradient)
+      const float4 o = *dst;
+      r.x += o.x; r.y += o.y; r.z += o.z; r.w += o.w;
+    }
+    *dst = r;
   }
 }
-void batch_sum2_launch(const float* a, const float* b, float* oa, float* ob, int B, long long n, hipStream_t st) {
-  const long long n4 = n / 4;
-  hipLaunchKernelGGL(batch_sum2_kernel, dim3((unsigned)((2 * n4 + 63) / 64)), dim3(256), 0, st, a, b, oa, ob, B, n4);
+void batch_sum2_launch(const float* a, const float* b, float* oa, float* ob, int B, long long na, long long nb, int acc_b,
+                       hipStream_t st) {
+  const long long na4 = a ? na / 4 : 0, nb4 = nb / 4;
+  hipLaunchKernelGGL(batch_sum2_kernel, dim3((unsigned)((na4 + nb4 + 63) / 64)), dim3(256), 0, st, a, b, oa, ob, B, na4,
+                     nb4, acc_b);
 }
 void adamw_launch(float* p, float* g, float* m, float* v, uint16_t* shadow, long long n, const float* hyper,
                   float eps, float wd, float clip, float gscale, int l2, int zero_g, hipStream_t st) {

@@ -428,15 +428,19 @@ def _post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, be2, H, grads, seed=None
 
 
 def ln_linear_bwd(g, w, x, mean, rstd, lnw, lnb, dres, need_dx, dlnw=None, dlnb=None, dW=None, db=None, pe=None,
-                  kin=-1, slab=False, job_slab=None, job_dsts=(), job_offs=()):
+                  kin=-1, slab=False, job_slab=None, job_dsts=(), job_offs=(), dx_out=None):
     """Returns dX (or None); LN grads accumulate into dlnw / dlnb and, when given,
     dW += gᵀ·LN(x), db += Σ_rows g (slab: stored into (tiles, ·) slab views)."""
     _run_job(job_slab, job_dsts, job_offs)
     _SLAB[0] = slab
     try:
-        return _ln_linear_bwd(g, w, x, mean, rstd, lnw, lnb, dres, need_dx, dlnw, dlnb, dW, db, pe, kin)
+        dx = _ln_linear_bwd(g, w, x, mean, rstd, lnw, lnb, dres, need_dx, dlnw, dlnb, dW, db, pe, kin)
     finally:
         _SLAB[0] = False
+    if dx is not None and dx_out is not None:
+        dx_out.copy_(dx)
+        return dx_out
+    return dx
 
 
 def _ln_linear_bwd(g, w, x, mean, rstd, lnw, lnb, dres, need_dx, dlnw, dlnb, dW, db, pe, kin):
@@ -651,8 +655,12 @@ def cast_bf16(x, y):
     y.copy_(x.to(torch.bfloat16).view(y.shape))
 
 
-def batch_sum2(a, b):
-    return a.sum(0), b.sum(0)
+def batch_sum2(a, b, ob_acc=None):
+    sb = b.sum(0)
+    if ob_acc is not None:
+        ob_acc.add_(sb.view_as(ob_acc))
+        sb = ob_acc.view_as(sb)
+    return (a.sum(0) if a is not None else None), sb
 
 
 def index_add_rows(dst, idx, src):

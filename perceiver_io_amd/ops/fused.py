@@ -408,6 +408,12 @@ class _LayerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, spec: LayerSpec, bw, seed, p_attn, src, x_q, x_kv, kmask, *ps):
         K = kernels(x_q)
+        # broadcast queries that are a leaf parameter's (1, N, C) view (the encoder's latent array):
+        # the backward adds their gradient straight into the parameter's gradient buffer (no
+        # autograd AccumulateGrad add kernel)
+        base = x_q._base
+        ctx.q_leaf = (base if spec.cross and base is not None and base.is_leaf and base.requires_grad
+                      and x_q.shape[0] == 1 and tuple(base.shape) == tuple(x_q.shape[1:]) else None)
         C, H = spec.C, spec.heads
         D = C // H
         scale = 1.0 / math.sqrt(D)
@@ -642,13 +648,22 @@ class _LayerFn(torch.autograd.Function):
                 dq, _, _ = K.attn_bwd(qx, kv3[:, :, :C], kv3[:, :, C:], kmask, o, do.view(B, Nq, C), lse, delta3, H,
                                       D, scale, ctx.p_attn, ctx.seed, dq_pre, dkv[:, :, :C], dkv[:, :, C:], acc,
                                       dq_zeroed=dq_pre is not None)
+            # the latent array's gradient, written by the kernels below in place: += Σ_b dY by the
+            # batch sum, then dX = LN_bwd(·) + that into the same buffer
+            leaf_g = None
+            if ctx.q_leaf is not None and Bq == 1 and B > 1 and not getattr(ctx, "q_handoff", False):
+                leaf_g = _grad_of(ctx.q_leaf)
+                if leaf_g is not None and not (leaf_g.is_contiguous() and leaf_g.data_ptr() % 16 == 0):
+                    leaf_g = None
             if Bq == 1 and B > 1 and dq.shape[0] == B:
                 # broadcast latent queries: both batch sums in one deterministic kernel
-                dq2, dres = K.batch_sum2(dq.contiguous(), dy.view(B, Nq, C))
+                dq2, dres = K.batch_sum2(dq.contiguous(), dy.view(B, Nq, C), ob_acc=leaf_g)
             elif Bq == 1 and B > 1:  # dq already summed (fused pe path)
-                dq2, dres = dq.reshape(Nq, C), dy.view(B, Nq, C).sum(0)
+                dq2 = dq.reshape(Nq, C)
+                _, dres = K.batch_sum2(None, dy.view(B, Nq, C).contiguous(), ob_acc=leaf_g)
             else:
                 dq2, dres = dq.reshape(B * Nq, C), dy
+            q_out = dict(dx_out=dres.view(Nq, C)) if leaf_g is not None else {}
             Ckv = g_kv.shape[0]
             Rq = dq2.shape[0]
             if getattr(ctx, "q_handoff", False):
@@ -662,12 +677,12 @@ class _LayerFn(torch.autograd.Function):
             elif WGRAD_SLAB and Rq < TALL_ROWS:
                 sl = _GradSlab(Rq, [C, C, C * C, C], dz2)
                 dx_q = K.ln_linear_bwd(dq2, wq, xq2, mean_q, rstd_q, g_q, b_q, dres, True, *sl.targets(), slab=True,
-                                       **_take_job())
+                                       **_take_job(), **q_out)
                 sl.defer(K, [flat(g_q), flat(b_q), flat(ps[4], 0, C * C), flat(bin_, 0, C)])
             else:
                 gwq = rows(gb(ps[4]), 0, C, C) if spec.packed else gb(ps[4])
                 dx_q = K.ln_linear_bwd(dq2, wq, xq2, mean_q, rstd_q, g_q, b_q, dres, True, gb(g_q), gb(b_q), gwq,
-                                       rows(gb(bin_), 0, C, 1))
+                                       rows(gb(bin_), 0, C, 1), **q_out)
             dx_kv = None
             if ctx.kv_owner:  # the projection's backward, once, over the summed dK/dV
                 if ent.get("pe_D") is not None:
@@ -726,7 +741,7 @@ class _LayerFn(torch.autograd.Function):
                         gb(ps[5]).add_(rows(gwkv, 0, C, Ckv))
                         gb(ps[6]).add_(rows(gwkv, C, 2 * C, Ckv))
                 ent["dkv"] = ent["pe_D"] = ent["pe_part"] = None
-            dx_q = dx_q.view(Bq, Nq, C)
+            dx_q = None if leaf_g is not None else dx_q.view(Bq, Nq, C)  # already in the leaf's gradient
             dx_kv = dx_kv.view(B, M, -1) if (ctx.kv_grad and dx_kv is not None) else None
         else:
             qkv3 = qx.view(B, Nq, 3 * C)
