@@ -360,7 +360,9 @@ __global__ void attn_bwd_prep_kernel(const uint16_t* __restrict__ dO, const uint
 // OBF: dQ / dK / dV stored as bf16 (the pointers are uint16_t views; every element written once:
 // a single key block, no query split, no accumulation — host-checked), for a consumer that reads
 // them as bf16 MFMA operands anyway (the chain-layout layer-boundary backward)
-template <int D, int NW, int QR = 0, bool OBF = false>
+// KM = false: no key padding mask and every key of the grid's blocks exists (Nk a multiple of the
+// block's keys): no per-element masking select in the softmax
+template <int D, int NW, int QR = 0, bool OBF = false, bool KM = true>
 __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uint16_t* __restrict__ dO,
                                                            const float* __restrict__ LSE,
                                                            const float* __restrict__ delta, float* __restrict__ dq,
@@ -403,10 +405,13 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
   const int kc = key < a.Nk ? key : a.Nk - 1;
   const uint32_t dkey = a.drop_thresh ? drop_key(a.seedp, a.site, 2u) : 0u;
   const bool kin = key < a.Nk;
-  const unsigned char* kmp = (a.kmask && kin) ? a.kmask + (long long)b * a.Nk + key
-                                              : reinterpret_cast<const unsigned char*>(kZero32B);
-  const unsigned char kmv = *kmp;  // unconditional load (address select)
-  const bool kpad = (kmv != 0) | !kin;
+  bool kpad = false;
+  if constexpr (KM) {
+    const unsigned char* kmp = (a.kmask && kin) ? a.kmask + (long long)b * a.Nk + key
+                                                : reinterpret_cast<const unsigned char*>(kZero32B);
+    const unsigned char kmv = *kmp;  // unconditional load (address select)
+    kpad = (kmv != 0) | !kin;
+  }
 
   const int HD = a.H * D;
   // 16-byte output rows possible (fp32 dQ / dK / dV views 16-byte aligned)
@@ -540,23 +545,26 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
         }
       }
       // dV += P^T dO ; dK += dS^T Q   (accumulator as A operand: X^T · B)
+      bf16x8 sa[2];
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
-        const bf16x8 pa = pack_acc(P, ss), sa = pack_acc(dS, ss);
+        const bf16x8 pa = pack_acc(P, ss);
+        sa[ss] = pack_acc(dS, ss);
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           dV[t] = mfma32(pa, frag_ks_perm(tdO, LD, 32 * t, 16 * ss), dV[t]);
-          dK[t] = mfma32(sa, frag_ks_perm(tQ, LD, 32 * t, 16 * ss), dK[t]);
+          dK[t] = mfma32(sa[ss], frag_ks_perm(tQ, LD, 32 * t, 16 * ss), dK[t]);
         }
       }
-      // dS slab of (this wave's 32 keys) × (tile j's 32 queries) as [key][q]
+      // dS slab of (this wave's 32 keys) × (tile j's 32 queries) as [key][q]: the packed dS
+      // halves above (registers 4g .. 4g + 3 = queries 8g + 4hh .. + 3)
       uint16_t* slab = sdS + (j * KB + 32 * w) * LDS_;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        uint2 pk;
-        pk.x = pack2(dS[4 * g], dS[4 * g + 1]);
-        pk.y = pack2(dS[4 * g + 2], dS[4 * g + 3]);
-        *reinterpret_cast<uint2*>(slab + r * LDS_ + 8 * g + 4 * hh) = pk;
+        const bf16x8& v = sa[g >> 1];
+        const int o = 4 * (g & 1);
+        const bf16x4 q4 = {v[o], v[o + 1], v[o + 2], v[o + 3]};
+        *reinterpret_cast<bf16x4*>(slab + r * LDS_ + 8 * g + 4 * hh) = q4;
       }
     }
     PIO_TS(3 + 4 * ((qt0 - qt_begin) / NQS));
@@ -831,6 +839,9 @@ static void bwd_launch_t(const AttnArgs& a, const uint16_t* dO, const float* LSE
   else if (a.Nq <= 64 && small_lds)
     hipLaunchKernelGGL((attn_bwd_kernel<D, NW, 2>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs,
                        dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs, nqs, tps);
+  else if (a.kmask == nullptr && a.Nk % (32 * NW) == 0)
+    hipLaunchKernelGGL((attn_bwd_kernel<D, NW, 0, false, false>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq,
+                       dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs, nqs, tps);
   else
     hipLaunchKernelGGL((attn_bwd_kernel<D, NW>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs, dk,
                        dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs, nqs, tps);
@@ -873,9 +884,13 @@ bool attn_bwd_bf16_launch(const AttnArgs& a, int D, const uint16_t* dO, const fl
   if (!attn_bwd_bf16_ok(a, D)) return false;
   const int nqt = (a.Nq + 31) / 32;
   dim3 grid(1, a.H, a.B);
-  hipLaunchKernelGGL((attn_bwd_kernel<16, 8, 0, true>), grid, dim3(512), 0, st, a, dO, LSE, delta,
-                     reinterpret_cast<float*>(dq), dq_bs, dq_rs, reinterpret_cast<float*>(dk), dk_bs, dk_rs,
-                     reinterpret_cast<float*>(dv), dv_bs, dv_rs, 0, 0, 0LL, 1, nqt);
+#define BF16L(KM_)                                                                                                  \
+  hipLaunchKernelGGL((attn_bwd_kernel<16, 8, 0, true, KM_>), grid, dim3(512), 0, st, a, dO, LSE, delta,             \
+                     reinterpret_cast<float*>(dq), dq_bs, dq_rs, reinterpret_cast<float*>(dk), dk_bs, dk_rs,         \
+                     reinterpret_cast<float*>(dv), dv_bs, dv_rs, 0, 0, 0LL, 1, nqt)
+  if (a.kmask == nullptr && a.Nk == 256) BF16L(false);
+  else BF16L(true);
+#undef BF16L
   return true;
 }
 

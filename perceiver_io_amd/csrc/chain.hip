@@ -176,6 +176,7 @@ __global__ __launch_bounds__(512) void sa_layer_fwd_chain8_kernel(
   __shared__ __attribute__((aligned(16))) bf16x8 sX[2][8 * 64];           // pair fragment slots
   __shared__ __attribute__((aligned(16))) float2 sR[2][8 * 16];           // pair LN slots
   // the body is instantiated once per wave half (hf = qb = w >> 2, compile-time inside)
+  PIO_WG_BEGIN();
   auto body = [&](auto hfc) {
   constexpr int hf = decltype(hfc)::value, qb = hf;
   const int w = wave_id(), l = lane_id(), hh = l >> 5, r = l & 31;
@@ -375,6 +376,7 @@ __global__ __launch_bounds__(512) void sa_layer_fwd_chain8_kernel(
   };
   if (wave_id() >> 2) body(std::integral_constant<int, 1>{});
   else body(std::integral_constant<int, 0>{});
+  PIO_WG_END();
 }
 
 // ------------------------------------------------------------------------------------
@@ -549,9 +551,11 @@ __global__ __launch_bounds__(512) void ln_linear_post_attn_bwd_chain8_kernel(
   uint16_t* sOt = sYm + 64 * LD;       //   O
   float* sVec = reinterpret_cast<float*>(smem + lpb_chain_smem<NQ>() - 4 * 4 * 64);  // γ1 β1 γ2 β2
   float2* sR = reinterpret_cast<float2*>(smem + lpb_chain_smem<NQ>());              // 2 pair-sum slots
+  PIO_WG_BEGIN();
   zero_span_block(job);
   if ((int)blockIdx.x >= (R + 63) / 64) {  // appended workgroups: the previous kernel's slab job
     slab_reduce_block(job, blockIdx.x - (R + 63) / 64, reinterpret_cast<float4*>(smem));
+    PIO_WG_END();
     return;
   }
   // the body is instantiated once per channel half (hf = w >> 2, a compile-time constant inside):
@@ -560,7 +564,11 @@ __global__ __launch_bounds__(512) void ln_linear_post_attn_bwd_chain8_kernel(
   constexpr int hf = decltype(hfc)::value;
   const int w = wave_id(), l = lane_id(), g = l >> 4;
   const int lr = 16 * (w & 3) + (l & 15);
-  const int gr = blockIdx.x * 64 + lr;
+  // the tiles of one batch element on one XCD, the same tile → XCD map as the attention backward
+  // (xcd_block3) and the layer forward (xcd_remap): the dO / dY rows this kernel stores are read
+  // back by the next kernels through the same L2, and so is the dQKV it loads
+  const int tile = xcd_remap(blockIdx.x, (R + 63) / 64);
+  const int gr = tile * 64 + lr;
 
   // ---- phase 0: every load in flight; G: this wave's half of the k-steps (t ≡ hf mod 2) ----
   PIO_TS(0);
@@ -772,7 +780,7 @@ __global__ __launch_bounds__(512) void ln_linear_post_attn_bwd_chain8_kernel(
 
   // ---- C: parameter gradients of the tile → slab row blockIdx.x, 16-row blocks over 8 waves ----
   const int vrs = gr_out.vrs;
-  const long long so = (long long)blockIdx.x * vrs;
+  const long long so = (long long)tile * vrs;
   const float *gam1 = sVec, *bet1 = sVec + C, *gam2 = sVec + 2 * C, *bet2 = sVec + 3 * C;
   auto sp = [&](float* p) { return p + so; };  // this tile's slab row
   const int p4 = w & 3;
@@ -792,6 +800,7 @@ __global__ __launch_bounds__(512) void ln_linear_post_attn_bwd_chain8_kernel(
   };
   if (wave_id() >> 2) body(std::integral_constant<int, 1>{});
   else body(std::integral_constant<int, 0>{});
+  PIO_WG_END();
 }
 
 // ---- launchers (called by rowgemm.hip's launchers once the operands qualify: C = 64, H = 4,

@@ -216,7 +216,8 @@ __device__ __forceinline__ Blk3 xcd_block3() { return xcd_block3(gridDim.z); }
 // ---- phase timestamps (tools/trace only; compiled out unless PIO_TRACE is defined) ----
 // PIO_TS(slot): lane 0 of every wave of workgroup (trace_bx, trace_by, trace_bz) records the
 // shader clock into trace_buf[wave * 64 + slot]; slot 63 of every workgroup's wave 0 goes to
-// trace_wg[2 * wg + {0, 1}] via PIO_WG_BEGIN / PIO_WG_END (dispatch timeline).
+// trace_wg[2 * wg + {0, 1}] via PIO_WG_BEGIN / PIO_WG_END (dispatch timeline, on the 100 MHz
+// s_memrealtime clock: the shader clocks of different XCDs are not aligned).
 #ifdef PIO_TRACE
 __device__ long long* trace_buf;
 __device__ long long* trace_wg;
@@ -231,7 +232,7 @@ __device__ int trace_bx, trace_by, trace_bz;
   do {                                                                                               \
     if (threadIdx.x == 0 && trace_wg)                                                                \
       trace_wg[2 * ((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) + (which)] =     \
-          __builtin_amdgcn_s_memtime();                                                              \
+          __builtin_amdgcn_s_memrealtime();                                                          \
   } while (0)
 #define PIO_WG_BEGIN() PIO_WG_MARK(0)
 #define PIO_WG_END() PIO_WG_MARK(1)

@@ -99,8 +99,7 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(w.data(), twg, w.size() * 8, hipMemcpyDeviceToHost));
   long long g0 = w[0], g1 = w[1];
   for (int i = 0; i < nwg; ++i) { g0 = std::min(g0, w[2 * i]); g1 = std::max(g1, w[2 * i + 1]); }
-  const double tick_us = ms * 1e3 / (double)(g1 - g0);  // upper bound on µs per tick (event ≥ kernel span)
-  printf("traced launch: %.2f us (events), WG span %lld ticks -> <= %.4f us/tick\n", ms * 1e3, g1 - g0, tick_us);
+  printf("traced launch: %.2f us (events), WG span %.2f us (s_memrealtime, 100 MHz)\n", ms * 1e3, (g1 - g0) / 100.0);
   const double clk = 100.0;  // s_memtime counts the shader clock; report ticks and µs at 2.4 GHz
   (void)clk;
   auto us = [&](long long d) { return d / 2400.0; };
@@ -121,11 +120,12 @@ int main(int argc, char** argv) {
     if (t[wv * 64]) printf(" %.2f", us(t[wv * 64] - t[0]));
   printf("\n");
   std::vector<double> st, du;
-  for (int i = 0; i < nwg; ++i) { st.push_back(us(w[2 * i] - g0)); du.push_back(us(w[2 * i + 1] - w[2 * i])); }
+  auto rt = [](long long d) { return d / 100.0; };  // s_memrealtime ticks → µs
+  for (int i = 0; i < nwg; ++i) { st.push_back(rt(w[2 * i] - g0)); du.push_back(rt(w[2 * i + 1] - w[2 * i])); }
   std::sort(st.begin(), st.end());
   std::sort(du.begin(), du.end());
   printf("WG start offsets (us): min %.2f p50 %.2f p90 %.2f max %.2f\n", st[0], st[nwg / 2], st[nwg * 9 / 10], st[nwg - 1]);
   printf("WG durations (us):     min %.2f p50 %.2f p90 %.2f max %.2f\n", du[0], du[nwg / 2], du[nwg * 9 / 10], du[nwg - 1]);
-  printf("grid span (us at 2.4 GHz): %.2f\n", us(g1 - g0));
+  printf("grid span (us): %.2f\n", rt(g1 - g0));
   return 0;
 }

@@ -34,8 +34,17 @@ static T* dev_fill(size_t n, float scale, bool bf, float offset = 0.f) {
   return p;
 }
 
+static void wg_summary(const char* what, std::vector<double> st, std::vector<double> du) {
+  if (st.empty()) return;
+  std::sort(st.begin(), st.end());
+  std::sort(du.begin(), du.end());
+  const size_t n = st.size();
+  printf("  %s (%zu WGs): start min %.2f p50 %.2f p90 %.2f max %.2f | duration min %.2f p50 %.2f p90 %.2f max %.2f us\n",
+         what, n, st[0], st[n / 2], st[n * 9 / 10], st[n - 1], du[0], du[n / 2], du[n * 9 / 10], du[n - 1]);
+}
+
 template <typename F>
-static void trace(const char* name, int R, F launch) {
+static void trace(const char* name, int R, F launch, int nwg_total = 0) {
   long long* tb;
   CK(hipMalloc(&tb, 16 * 64 * 8));
   long long* nul = nullptr;
@@ -74,6 +83,30 @@ static void trace(const char* name, int R, F launch) {
     }
     printf("  total %.2f\n", (prev - t[wv * 64]) / 2400.0);
   }
+  // dispatch timeline (s_memrealtime, 100 MHz): tile workgroups and appended (slab job) ones
+  const int tiles = R / 64, nwg = nwg_total > tiles ? nwg_total : tiles;
+  long long* twg;
+  CK(hipMalloc(&twg, (size_t)2 * nwg * 8));
+  CK(hipMemset(twg, 0, (size_t)2 * nwg * 8));
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(pio::trace_wg), &twg, sizeof(twg)));
+  launch();
+  CK(hipDeviceSynchronize());
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(pio::trace_wg), &nul, sizeof(nul)));
+  std::vector<long long> w(2 * nwg);
+  CK(hipMemcpy(w.data(), twg, w.size() * 8, hipMemcpyDeviceToHost));
+  long long g0 = -1, g1 = 0;
+  for (int i = 0; i < nwg; ++i)
+    if (w[2 * i]) { g0 = g0 < 0 ? w[2 * i] : std::min(g0, w[2 * i]); g1 = std::max(g1, w[2 * i + 1]); }
+  std::vector<double> st, du, st2, du2;
+  for (int i = 0; i < nwg; ++i) {
+    if (!w[2 * i]) continue;
+    (i < tiles ? st : st2).push_back((w[2 * i] - g0) / 100.0);
+    (i < tiles ? du : du2).push_back((w[2 * i + 1] - w[2 * i]) / 100.0);
+  }
+  printf("  grid span %.2f us\n", (g1 - g0) / 100.0);
+  wg_summary("tiles", st, du);
+  wg_summary("appended", st2, du2);
+  CK(hipFree(twg));
   CK(hipFree(tb));
 }
 
@@ -131,12 +164,12 @@ int main(int argc, char** argv) {
   trace("ln_linear_post_attn_bwd_chain + slab job", R, [&]() {
     pio::ln_linear_post_attn_bwd_launch(C, G, false, W[3], Z, m1, r1, vec[5], vec[6], dres, dg1, db1, dwq, dbq, Y, m2, r2, U, O,
                                         W[0], W[1], W[2], vec[3], vec[4], dY, dO, delta, H, g, R, job2, dr, 3 * C, 0);
-  });
+  }, R / 64 + job2.nblk);
   // G as bf16 (the attention backward's bf16 dQKV)
   uint16_t* Gb = dev_fill<uint16_t>((size_t)R * 3 * C, 1.f, true);
   trace("ln_linear_post_attn_bwd_chain bf16 G + slab job", R, [&]() {
     pio::ln_linear_post_attn_bwd_launch(C, Gb, true, W[3], Z, m1, r1, vec[5], vec[6], dres, dg1, db1, dwq, dbq, Y, m2, r2,
                                         U, O, W[0], W[1], W[2], vec[3], vec[4], dY, dO, delta, H, g, R, job2, dr, 3 * C, 0);
-  });
+  }, R / 64 + job2.nblk);
   return 0;
 }
