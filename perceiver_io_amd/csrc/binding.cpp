@@ -91,13 +91,13 @@ void ce_fwd_launch(int, const float*, const int64_t*, const int64_t*, const uint
 int ce_combine_blocks(int);
 int ce2_num_splits(int, int);
 int ce2_bwd_splits(int, int);
-int ce2_combine_blocks(int);
+int ce2_row_blocks(int);
 void ce2_fwd_launch(const float*, const int64_t*, const int64_t*, const uint16_t*, const float*, int, int, int, float2*,
-                    float*, float*, uint16_t*, float*, float*, float*, int, float*, float*, unsigned*, float*, long long,
-                    hipStream_t);
+                    float*, float*, uint16_t*, float*, float*, int, float*, float*, unsigned*, unsigned*, float*,
+                    long long, hipStream_t);
 void ce2_bwd_launch(const uint16_t*, const int64_t*, const uint16_t*, const float*, const float*, const float*,
-                    const float*, const float*, int, int, float*, float*, float*, int, float*, long long, const int64_t*,
-                    hipStream_t);
+                    const float2*, int, const float*, const float*, int, int, float*, float*, float*, int, float*, long long,
+                    const int64_t*, hipStream_t);
 int ce_num_splits(int, int);
 int ce_dw_splits(int, int);
 void mlm_select_launch(const int64_t*, int, int, int, int, int64_t*, int64_t*, int*, int64_t*, int64_t*, float*, bool*, bool*,
@@ -734,6 +734,16 @@ static Tensor& ce_ticket(const Tensor& like) {
   if (it == tickets.end()) it = tickets.emplace(d, torch::zeros({kCeTickets}, like.options().dtype(torch::kInt32))).first;
   return it->second;
 }
+// per-row-block arrival counters of the two-pass head's forward (re-armed by the kernel itself)
+constexpr int64_t kCeRowBlockTickets = 4096;
+static Tensor& ce_rb_tickets(const Tensor& like) {
+  static std::unordered_map<int, Tensor> tickets;
+  const int d = like.get_device();
+  auto it = tickets.find(d);
+  if (it == tickets.end())
+    it = tickets.emplace(d, torch::zeros({kCeRowBlockTickets}, like.options().dtype(torch::kInt32))).first;
+  return it->second;
+}
 
 // labels (B, L) → [idx_b (B, cap), labels_b (B, cap), gidx (gcap), glabels (gcap), total (1) fp32,
 // overflow (1) bool (+ q (B, cap, C) = queries[idx_b] when the output-query array is given)]:
@@ -797,13 +807,15 @@ std::vector<Tensor> ce_fwd(Tensor h, OptT idx, Tensor labels, Tensor w, Tensor b
   const int64_t* ip = opt_idx(idx, M);
   auto f32 = h.options().dtype(torch::kFloat32);
   if (C == 64) {
-    // two-pass head (ce_head.hip): the forward also forms u = Σ_v p·W − W[label] per row, the
-    // hidden-state gradient up to the row-loss scale; returned as a 4th output for ce_bwd
+    // two-pass head (ce_head.hip): the forward also forms the per-split Σ_v p·W partials of each
+    // row (the hidden-state gradient up to the row-loss scale once merged); returned with the
+    // splits' (max, sum) as a 4th and 5th output for ce_bwd, which merges them
     const int ns = pio::ce2_num_splits(M, V);
     Tensor pml = torch::empty({ns, M, 2}, f32), pacc = torch::empty({ns, M, C}, f32);
     Tensor picked = torch::empty({M}, f32), lse = torch::empty({M}, f32), loss = torch::empty({}, f32);
-    Tensor u = torch::empty({M, C}, f32);
-    Tensor blk = torch::empty({2 * pio::ce2_combine_blocks(M)}, f32);
+    const int nrb = pio::ce2_row_blocks(M);
+    TORCH_CHECK(nrb <= kCeRowBlockTickets, "ce_fwd: too many rows for the row-block tickets");
+    Tensor blk = torch::empty({2 * nrb}, f32);
     Tensor hs = torch::empty({M, C}, h.options().dtype(torch::kBFloat16));
     TORCH_CHECK(count.numel() >= 1 && count.is_contiguous(), "ce_fwd: count must hold one fp32 value");
     float* zp = nullptr;
@@ -817,13 +829,14 @@ std::vector<Tensor> ce_fwd(Tensor h, OptT idx, Tensor labels, Tensor w, Tensor b
       zn = zero_out->numel();
     }
     Tensor& tk = ce_ticket(h);
+    Tensor& rbt = ce_rb_tickets(h);
     pio::ce2_fwd_launch(h.data_ptr<float>(), ip, labels.data_ptr<int64_t>(), bfp(w), f32p(bias), M, V, ns,
                         reinterpret_cast<float2*>(pml.data_ptr<float>()), pacc.data_ptr<float>(), picked.data_ptr<float>(),
-                        bfp_mut(hs), lse.data_ptr<float>(), u.data_ptr<float>(), count.data_ptr<float>(),
-                        count_labels ? 1 : 0, loss.data_ptr<float>(), blk.data_ptr<float>(),
+                        bfp_mut(hs), lse.data_ptr<float>(), count.data_ptr<float>(), count_labels ? 1 : 0,
+                        loss.data_ptr<float>(), blk.data_ptr<float>(), reinterpret_cast<unsigned*>(rbt.data_ptr<int>()),
                         reinterpret_cast<unsigned*>(tk.data_ptr<int>()), zp, zn, stream());
     checked_sync("ce_fwd");
-    return {loss, lse, hs, u};
+    return {loss, lse, hs, pacc, pml};
   }
   const int ns = pio::ce_num_splits(M, V);
   Tensor part = torch::empty({ns, M, 2}, f32), picked = torch::empty({M}, f32);
@@ -857,7 +870,7 @@ std::vector<Tensor> ce_fwd(Tensor h, OptT idx, Tensor labels, Tensor w, Tensor b
 // slab: the dW kernel stores its row-split partials into a returned (splits, V·C + V₄) slab
 // instead of adding them (the caller sums it into dW | db with a slab job, offsets 0 and V·C).
 OptT ce_bwd(Tensor h, Tensor labels, Tensor w, Tensor bias, Tensor lse, Tensor gout, Tensor count, Tensor dH,
-            Tensor dW, Tensor db, bool accumulate, OptT rowmap, bool slab, OptT u) {
+            Tensor dW, Tensor db, bool accumulate, OptT rowmap, bool slab, OptT u, OptT u_ml) {
   const int M = (int)labels.numel(), C = (int)h.size(1), V = (int)w.size(0);
   CHECK_DT(h, torch::kBFloat16);
   TORCH_CHECK(h.size(0) == M, "ce_bwd: h must be the compact (M, C) bf16 rows of ce_fwd");
@@ -875,11 +888,18 @@ OptT ce_bwd(Tensor h, Tensor labels, Tensor w, Tensor bias, Tensor lse, Tensor g
   }
   Tensor sl;
   if (u.has_value()) {  // the two-pass head's backward: dW / db pass + the dH rows g·u
+    // u: the forward's per-split Σ p·W partials (splits, M, 64), u_ml: their (max, sum) (splits, M, 2)
     CHECK_DT(*u, torch::kFloat32);
-    TORCH_CHECK(C == 64 && u->is_contiguous() && u->size(0) == M && u->size(1) == C, "ce_bwd: u must be (M, 64) fp32");
+    TORCH_CHECK(u_ml.has_value(), "ce_bwd: the two-pass head needs the split (max, sum) pairs");
+    CHECK_DT(*u_ml, torch::kFloat32);
+    TORCH_CHECK(C == 64 && u->is_contiguous() && u->dim() == 3 && u->size(1) == M && u->size(2) == C &&
+                    u_ml->is_contiguous() && u_ml->dim() == 3 && u_ml->size(0) == u->size(0) && u_ml->size(1) == M &&
+                    u_ml->size(2) == 2 && u->size(0) <= 16,
+                "ce_bwd: u must be (splits, M, 64) and u_ml (splits, M, 2) fp32");
     if (slab) sl = torch::empty({pio::ce2_bwd_splits(M, V), (int64_t)V * C + ((V + 3) & ~3)}, dW.options());
     pio::ce2_bwd_launch(bfp(h), labels.data_ptr<int64_t>(), bfp(w), f32p(bias), f32p(lse), u->data_ptr<float>(),
-                        f32p(gout), f32p(count), M, V, dW.data_ptr<float>(), db.data_ptr<float>(),
+                        reinterpret_cast<const float2*>(u_ml->data_ptr<float>()), (int)u->size(0), f32p(gout),
+                        f32p(count), M, V, dW.data_ptr<float>(), db.data_ptr<float>(),
                         slab ? sl.data_ptr<float>() : nullptr, accumulate ? 1 : 0, dH.data_ptr<float>(), dH.size(0), rm,
                         stream());
     if (slab) return sl;
@@ -1470,7 +1490,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("count"), py::arg("zero_out") = py::none(), py::arg("count_labels") = false);
   m.def("ce_bwd", &ce_bwd, py::arg("h"), py::arg("labels"), py::arg("w"), py::arg("bias"),
         py::arg("lse"), py::arg("gout"), py::arg("count"), py::arg("dH"), py::arg("dW"), py::arg("db"),
-        py::arg("accumulate"), py::arg("rowmap") = py::none(), py::arg("slab") = false, py::arg("u") = py::none());
+        py::arg("accumulate"), py::arg("rowmap") = py::none(), py::arg("slab") = false, py::arg("u") = py::none(),
+        py::arg("u_ml") = py::none());
   m.def("embed_fwd", &embed_fwd);
   m.def("embed_bwd", &embed_bwd);
   m.def("text_mask", &text_mask, py::arg("x"), py::arg("pad"), py::arg("state"), py::arg("unk"), py::arg("mask"),

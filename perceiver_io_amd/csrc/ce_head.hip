@@ -9,12 +9,14 @@
 //                     the softmax-weighted vocab sum Σ_v p[r, v]·W[v] — a flash-attention forward
 //                     whose keys and values are both W — so the hidden-state gradient needs no
 //                     further pass over the vocabulary: dH[r] = g·(Σ_v p[r, v]·W[v] − W[label]).
-//   combine           merges the vocab splits: per-row lse, loss (mean by a deterministic ticket
-//                     reduction) and u[r] = Σ_v p·W − W[label] (fp32), kept for the backward.
+//   pass 1 tail       the last split workgroup of each row block (arrival ticket) merges the
+//                     splits' (max, sum) into the rows' lse and the block's loss partial; the last
+//                     row block (second ticket) finalises the mean loss — no combine launch.
 //   pass 2 (backward) vocab × row split: logit tiles S = H·Wᵀ (vocab on the lane), dl = (p −
 //                     onehot)·g, dW += dlᵀ·H and db += Σ dl (partials stored into a slab row),
-//                     plus the dH rows g·u[r] scattered to their source positions by appended
-//                     workgroups.
+//                     plus, in appended workgroups, the dH rows g·u[r] with u[r] = Σ_v p·W −
+//                     W[label] merged from pass 1's per-split partials, scattered to their source
+//                     positions.
 //
 // LDS images ([rows][64] bf16, 128 B per row, no padding) are XOR-swizzled on their 16-byte
 // slots with sw(v) = v₁·4 + v₂·2 + v₃ (bits of the row index): a k-contiguous ds_read_b128
@@ -37,6 +39,7 @@ constexpr int HT = 64;           // pass 2: rows per staged H tile
 constexpr float kL2E = 1.4426950408889634f;
 constexpr float kLN2 = 0.6931471805599453f;
 constexpr float kRescale = 8.f;  // lazy-rescale threshold (log2 units)
+constexpr int kCeMaxSplitsFwd = 16;  // ce2_num_splits caps the vocab splits of pass 1 here
 
 // element offset of (row v, 16-byte slot s) in a swizzled [rows][64] bf16 image
 __device__ __forceinline__ int swz(int v, int s) {
@@ -75,7 +78,11 @@ __global__ __launch_bounds__(256) void ce2_fwd_kernel(const float* __restrict__ 
                                                       const int64_t* __restrict__ labels, const uint16_t* __restrict__ W,
                                                       const float* __restrict__ bias, int M, int V, int chunks_per_split,
                                                       float2* __restrict__ part_ml, float* __restrict__ part_acc,
-                                                      float* __restrict__ picked, uint16_t* __restrict__ hs_out) {
+                                                      float* __restrict__ picked, uint16_t* __restrict__ hs_out,
+                                                      float* __restrict__ lse, float* __restrict__ count, int count_labels,
+                                                      float* __restrict__ loss, float* __restrict__ blk,
+                                                      unsigned* __restrict__ rb_ticket, unsigned* __restrict__ ticket,
+                                                      float* __restrict__ zero_out, long long zero_n4) {
   using namespace ce2;
   __shared__ __attribute__((aligned(16))) uint16_t sW[2][VC * C];
   __shared__ __attribute__((aligned(16))) float sB[2][VC];  // bias·log2e (−inf past V)
@@ -202,101 +209,93 @@ __global__ __launch_bounds__(256) void ce2_fwd_kernel(const float* __restrict__ 
     if (c + 1 < c_end) stage(buf ^ 1);
     lds_sync();
   }
-  if (!rin) return;
   const float ls = xor32_sum(l_run);
-  if (hh == 0) part_ml[(long long)split * M + gr] = make_float2(m_ref, ls);
-  if (have_pk) picked[gr] = pk * ce2::kLN2;
-  float* pa = part_acc + ((long long)split * M + gr) * C;
+  // (max, sum) and the picked logit are read back inside this launch by the row block's last
+  // split: stored write-through (sc1, agent-scope relaxed atomic stores), so no release fence is
+  // needed; the Σ p·W partials are read by the next launch only (plain stores)
+  if (rin) {
+    if (hh == 0)
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(part_ml + (long long)split * M + gr),
+                         (unsigned long long)__float_as_uint(m_ref) | ((unsigned long long)__float_as_uint(ls) << 32),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (have_pk)
+      __hip_atomic_store(reinterpret_cast<unsigned*>(picked + gr), __float_as_uint(pk * ce2::kLN2), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    float* pa = part_acc + ((long long)split * M + gr) * C;
 #pragma unroll
-  for (int ct = 0; ct < 2; ++ct)
+    for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
-    for (int q = 0; q < 4; ++q)  // registers 4q .. 4q+3 = c 32ct + 8q + 4hh + 0..3
-      *reinterpret_cast<float4*>(pa + 32 * ct + 8 * q + 4 * hh) =
-          make_float4(acc[ct][4 * q], acc[ct][4 * q + 1], acc[ct][4 * q + 2], acc[ct][4 * q + 3]);
-}
-
-// ---- combine --------------------------------------------------------------------------
-// 16 rows per workgroup, 16 threads per row (4 channels each).  lse[r] (natural), u[r][c] =
-// Σ_v p[r, v]·W[v][c] − W[label][c] (0 for ignored rows), loss = Σ (lse − picked) / max(count, 1)
-// with the deterministic last-workgroup ticket of mlm_head.hip.  Also clears zero_out (the
-// backward's dH buffer, float4 slices per workgroup).
-constexpr int kC2Rows = 16;
-constexpr int kCeMaxSplits = 16;  // ce2_num_splits caps the vocab splits here
-__global__ __launch_bounds__(256) void ce2_combine_kernel(const float2* __restrict__ part_ml,
-                                                          const float* __restrict__ part_acc,
-                                                          const float* __restrict__ picked,
-                                                          const int64_t* __restrict__ labels,
-                                                          const uint16_t* __restrict__ W, int M, int V, int nsplit,
-                                                          float* __restrict__ lse, float* __restrict__ u,
-                                                          float* __restrict__ count, int count_labels,
-                                                          float* __restrict__ loss, float* __restrict__ blk,
-                                                          unsigned* __restrict__ ticket, float* __restrict__ zero_out,
-                                                          long long zero_n4) {
-  using namespace ce2;
-  __shared__ float red[2][16];
-  __shared__ int last;
-  const int rr = threadIdx.x >> 4, cq = threadIdx.x & 15;
-  const int r = blockIdx.x * kC2Rows + rr;
+      for (int q = 0; q < 4; ++q)  // registers 4q .. 4q+3 = c 32ct + 8q + 4hh + 0..3
+        *reinterpret_cast<float4*>(pa + 32 * ct + 8 * q + 4 * hh) =
+            make_float4(acc[ct][4 * q], acc[ct][4 * q + 1], acc[ct][4 * q + 2], acc[ct][4 * q + 3]);
+  }
+  // a slice of the backward's dH accumulator cleared on the way (no fill launch)
+  if (zero_out != nullptr) {
+    const long long nwg = (long long)gridDim.x * gridDim.y, wg = (long long)blockIdx.y * gridDim.x + blockIdx.x;
+    const long long per = (zero_n4 + nwg - 1) / nwg, z1 = min(zero_n4, (wg + 1) * per);
+    for (long long i = wg * per + threadIdx.x; i < z1; i += blockDim.x)
+      reinterpret_cast<float4*>(zero_out)[i] = float4{0.f, 0.f, 0.f, 0.f};
+  }
+  // ---- arrival ticket of the row block: every wave drains its stores, one lane counts ----
+  __shared__ unsigned last;
+  __shared__ float red[2][4];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(rb_ticket + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.y - 1;
+  __syncthreads();
+  if (!last) return;
+  // the last split merges the splits' (max, sum) of the block's rows (sc1 loads of the sc1 stores)
   float lr = 0.f, nr = 0.f;
-  if (r < M) {
-    // every split's loads in flight at once (kMaxSplits-unrolled, address selects past nsplit)
-    float2 ml[kCeMaxSplits];
-    float4 v[kCeMaxSplits];
+  if (threadIdx.x < RB) {
+    const int r = m0 + threadIdx.x;
+    if (r < M) {
+      float2 ml[kCeMaxSplitsFwd];
 #pragma unroll
-    for (int s = 0; s < kCeMaxSplits; ++s) {
-      const int ss = s < nsplit ? s : 0;
-      ml[s] = part_ml[(long long)ss * M + r];
-      v[s] = *reinterpret_cast<const float4*>(part_acc + ((long long)ss * M + r) * C + 4 * cq);
-    }
-    float mx = -__builtin_inff();
+      for (int s = 0; s < kCeMaxSplitsFwd; ++s) {  // every split's load in flight (address selects)
+        const unsigned long long x = __hip_atomic_load(
+            reinterpret_cast<unsigned long long*>(part_ml + (long long)(s < (int)gridDim.y ? s : 0) * M + r),
+            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ml[s] = make_float2(__uint_as_float((unsigned)x), __uint_as_float((unsigned)(x >> 32)));
+      }
+      float mx = -__builtin_inff();
 #pragma unroll
-    for (int s = 0; s < kCeMaxSplits; ++s) mx = s < nsplit ? fmaxf(mx, ml[s].x) : mx;
-    float L = 0.f;
-    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int s = 0; s < kCeMaxSplitsFwd; ++s) mx = s < (int)gridDim.y ? fmaxf(mx, ml[s].x) : mx;
+      float L = 0.f;
 #pragma unroll
-    for (int s = 0; s < kCeMaxSplits; ++s) {
-      const float f = s < nsplit ? fast_exp2(ml[s].x - mx) : 0.f;
-      L = fmaf(ml[s].y, f, L);
-      a.x = fmaf(v[s].x, f, a.x); a.y = fmaf(v[s].y, f, a.y); a.z = fmaf(v[s].z, f, a.z); a.w = fmaf(v[s].w, f, a.w);
-    }
-    const int lab = (int)labels[r];
-    const float inv = 1.f / L;
-    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (lab >= 0 && lab < V) {
-      const uint2 wv = *reinterpret_cast<const uint2*>(W + (long long)lab * C + 4 * cq);
-      o = make_float4(a.x * inv - bf2f((uint16_t)(wv.x & 0xFFFF)), a.y * inv - bf2f((uint16_t)(wv.x >> 16)),
-                      a.z * inv - bf2f((uint16_t)(wv.y & 0xFFFF)), a.w * inv - bf2f((uint16_t)(wv.y >> 16)));
-    }
-    *reinterpret_cast<float4*>(u + (long long)r * C + 4 * cq) = o;
-    if (cq == 0) {
+      for (int s = 0; s < kCeMaxSplitsFwd; ++s) L += s < (int)gridDim.y ? ml[s].y * fast_exp2(ml[s].x - mx) : 0.f;
       const float L2 = (mx + __log2f(L)) * kLN2;
-      lse[r] = L2;
-      lr = lab >= 0 ? L2 - picked[r] : 0.f;
+      lse[r] = L2;  // read by the next launch
+      const int lab = (int)labels[r];
+      const float pk_r = __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned*>(picked + r), __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT));
+      lr = lab >= 0 ? L2 - pk_r : 0.f;
       nr = lab >= 0 ? 1.f : 0.f;
     }
-  }
-  if (zero_out != nullptr) {
-    const long long nwg = gridDim.x, per = (zero_n4 + nwg - 1) / nwg, z1 = min(zero_n4, ((long long)blockIdx.x + 1) * per);
-    for (long long i = (long long)blockIdx.x * per + threadIdx.x; i < z1; i += blockDim.x)
-      reinterpret_cast<float4*>(zero_out)[i] = float4{0.f, 0.f, 0.f, 0.f};
   }
   lr = wave_sum(lr);
   nr = wave_sum(nr);
   if (lane_id() == 0) { red[0][wave_id()] = lr; red[1][wave_id()] = nr; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    blk[blockIdx.x] = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
-    blk[gridDim.x + blockIdx.x] = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
-    __threadfence();
-    last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    const float bl = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+    const float bn = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+    __hip_atomic_store(reinterpret_cast<unsigned*>(blk + blockIdx.x), __float_as_uint(bl), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(reinterpret_cast<unsigned*>(blk + gridDim.x + blockIdx.x), __float_as_uint(bn), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    rb_ticket[blockIdx.x] = 0u;  // re-armed for the next call (graph replays)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   }
   __syncthreads();
   if (!last) return;
-  __threadfence();
+  // ---- the last row block: the mean loss over all row blocks, fixed order ----
   float t = 0.f, n = 0.f;
   for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x) {
-    t += *(volatile const float*)(blk + i);
-    n += *(volatile const float*)(blk + gridDim.x + i);
+    t += __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned*>(blk + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    n += __uint_as_float(
+        __hip_atomic_load(reinterpret_cast<unsigned*>(blk + gridDim.x + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   }
   t = wave_sum(t);
   n = wave_sum(n);
@@ -320,7 +319,8 @@ __global__ __launch_bounds__(256) void ce2_combine_kernel(const float2* __restri
 // y = rsplit: dH[rowmap[r]] (+)= g·u[r] for the rows of slice x (appended workgroups).
 __global__ __launch_bounds__(256) void ce2_bwd_kernel(const uint16_t* __restrict__ Hs, const int64_t* __restrict__ labels,
                                                       const uint16_t* __restrict__ W, const float* __restrict__ bias,
-                                                      const float* __restrict__ lse, const float* __restrict__ u,
+                                                      const float* __restrict__ lse, const float* __restrict__ part_acc,
+                                                      const float2* __restrict__ part_ml, int nsplit,
                                                       const float* __restrict__ gout, const float* __restrict__ count,
                                                       int M, int V, int rsplit, int tiles_per_split,
                                                       float* __restrict__ dW, float* __restrict__ db,
@@ -332,17 +332,43 @@ __global__ __launch_bounds__(256) void ce2_bwd_kernel(const uint16_t* __restrict
   __shared__ __attribute__((aligned(16))) int sLab[2][HT];
   const int w = wave_id(), l = lane_id(), hh = l >> 5;
   const float g = gout[0] / fmaxf(count[0], 1.f);
-  if ((int)blockIdx.y == rsplit) {  // the dH scatter of the forward's u rows
+  if ((int)blockIdx.y == rsplit) {
+    // dH rows: u[r] = Σ_v p·W − W[label] merged from pass 1's split partials (a row per 16
+    // threads, 4 channels each), then dH[rowmap[r]] += g·u[r]
     const int per = (M + gridDim.x - 1) / gridDim.x, r0 = blockIdx.x * per, r1 = min(M, r0 + per);
-    for (int e = threadIdx.x; e < (r1 - r0) * (C / 4); e += blockDim.x) {
-      const int r = r0 + e / (C / 4), c4 = e % (C / 4);
-      if (labels[r] < 0) continue;
+    const int cq = threadIdx.x & 15;
+    for (int r = r0 + (int)(threadIdx.x >> 4); r < r1; r += 16) {
+      const int lab = (int)labels[r];
+      if (lab < 0 || lab >= V) continue;
       const long long dst = rowmap ? rowmap[r] : (long long)r;
       if (dst < 0 || dst >= dh_rows) continue;
-      const float4 v = *reinterpret_cast<const float4*>(u + (long long)r * C + 4 * c4);
-      float4* d = reinterpret_cast<float4*>(dH + dst * C) + c4;
+      float2 ml[kCeMaxSplitsFwd];
+      float4 v[kCeMaxSplitsFwd];
+#pragma unroll
+      for (int s = 0; s < kCeMaxSplitsFwd; ++s) {  // every split's loads in flight (address selects)
+        const int ss = s < nsplit ? s : 0;
+        ml[s] = part_ml[(long long)ss * M + r];
+        v[s] = *reinterpret_cast<const float4*>(part_acc + ((long long)ss * M + r) * C + 4 * cq);
+      }
+      float mx = -__builtin_inff();
+#pragma unroll
+      for (int s = 0; s < kCeMaxSplitsFwd; ++s) mx = s < nsplit ? fmaxf(mx, ml[s].x) : mx;
+      float L = 0.f;
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int s = 0; s < kCeMaxSplitsFwd; ++s) {
+        const float f = s < nsplit ? fast_exp2(ml[s].x - mx) : 0.f;
+        L = fmaf(ml[s].y, f, L);
+        a.x = fmaf(v[s].x, f, a.x); a.y = fmaf(v[s].y, f, a.y); a.z = fmaf(v[s].z, f, a.z); a.w = fmaf(v[s].w, f, a.w);
+      }
+      const float inv = g / L;
+      const uint2 wv = *reinterpret_cast<const uint2*>(W + (long long)lab * C + 4 * cq);
+      float4* d = reinterpret_cast<float4*>(dH + dst * C) + cq;
       float4 o = *d;
-      o.x = fmaf(v.x, g, o.x); o.y = fmaf(v.y, g, o.y); o.z = fmaf(v.z, g, o.z); o.w = fmaf(v.w, g, o.w);
+      o.x += fmaf(a.x, inv, -g * bf2f((uint16_t)(wv.x & 0xFFFF)));
+      o.y += fmaf(a.y, inv, -g * bf2f((uint16_t)(wv.x >> 16)));
+      o.z += fmaf(a.z, inv, -g * bf2f((uint16_t)(wv.y & 0xFFFF)));
+      o.w += fmaf(a.w, inv, -g * bf2f((uint16_t)(wv.y >> 16)));
       *d = o;
     }
     return;
@@ -458,7 +484,7 @@ int ce2_num_splits(int M, int V) {
   s = s < 1 ? 1 : s;
   const int cap = (nchunks + 3) / 4;
   s = s > cap ? cap : s;
-  s = s > kCeMaxSplits ? kCeMaxSplits : s;
+  s = s > ce2::kCeMaxSplitsFwd ? ce2::kCeMaxSplitsFwd : s;
   const int cps = (nchunks + s - 1) / s;
   return (nchunks + cps - 1) / cps;
 }
@@ -472,23 +498,23 @@ int ce2_bwd_splits(int M, int V) {
   const int tps = (nt + s - 1) / s;
   return (nt + tps - 1) / tps;
 }
-int ce2_combine_blocks(int M) { return (M + kC2Rows - 1) / kC2Rows; }
+int ce2_row_blocks(int M) { return (M + ce2::RB - 1) / ce2::RB; }
 
 void ce2_fwd_launch(const float* Hm, const int64_t* hidx, const int64_t* labels, const uint16_t* W, const float* bias,
                     int M, int V, int nsplit, float2* part_ml, float* part_acc, float* picked, uint16_t* hs_out,
-                    float* lse, float* u, float* count, int count_labels, float* loss, float* blk, unsigned* ticket,
-                    float* zero_out, long long zero_n, hipStream_t st) {
+                    float* lse, float* count, int count_labels, float* loss, float* blk, unsigned* rb_ticket,
+                    unsigned* ticket, float* zero_out, long long zero_n, hipStream_t st) {
   const int nchunks = (V + ce2::VC - 1) / ce2::VC;
   const int cps = (nchunks + nsplit - 1) / nsplit;
-  hipLaunchKernelGGL(ce2_fwd_kernel, dim3((M + ce2::RB - 1) / ce2::RB, nsplit), dim3(256), 0, st, Hm, hidx, labels, W,
-                     bias, M, V, cps, part_ml, part_acc, picked, hs_out);
-  hipLaunchKernelGGL(ce2_combine_kernel, dim3(ce2_combine_blocks(M)), dim3(256), 0, st, part_ml, part_acc, picked, labels,
-                     W, M, V, nsplit, lse, u, count, count_labels, loss, blk, ticket, zero_out, zero_n / 4);
+  hipLaunchKernelGGL(ce2_fwd_kernel, dim3(ce2_row_blocks(M), nsplit), dim3(256), 0, st, Hm, hidx, labels, W, bias, M, V,
+                     cps, part_ml, part_acc, picked, hs_out, lse, count, count_labels, loss, blk, rb_ticket, ticket,
+                     zero_out, zero_n / 4);
 }
 
 void ce2_bwd_launch(const uint16_t* Hs, const int64_t* labels, const uint16_t* W, const float* bias, const float* lse,
-                    const float* u, const float* gout, const float* count, int M, int V, float* dW, float* db,
-                    float* slab, int accumulate, float* dH, long long dh_rows, const int64_t* rowmap, hipStream_t st) {
+                    const float* part_acc, const float2* part_ml, int nsplit, const float* gout, const float* count,
+                    int M, int V, float* dW, float* db, float* slab, int accumulate, float* dH, long long dh_rows,
+                    const int64_t* rowmap, hipStream_t st) {
   const int rsplit = ce2_bwd_splits(M, V);
   const int nt = (M + ce2::HT - 1) / ce2::HT;
   const int tps = (nt + rsplit - 1) / rsplit;
@@ -497,7 +523,7 @@ void ce2_bwd_launch(const uint16_t* Hs, const int64_t* labels, const uint16_t* W
     (void)hipMemsetAsync(db, 0, sizeof(float) * (size_t)V, st);
   }
   hipLaunchKernelGGL(ce2_bwd_kernel, dim3((V + ce2::VB2 - 1) / ce2::VB2, rsplit + 1), dim3(256), 0, st, Hs, labels, W, bias,
-                     lse, u, gout, count, M, V, rsplit, tps, dW, db, slab, dH, rowmap, dh_rows);
+                     lse, part_acc, part_ml, nsplit, gout, count, M, V, rsplit, tps, dW, db, slab, dH, rowmap, dh_rows);
 }
 
 unsigned check_errors_ce_head(bool reset) { return pio_read_errors(reset); }

@@ -43,6 +43,22 @@ __device__ __forceinline__ void cl_wstore(uint16_t* sW, int ld, int r, int c0, c
   *reinterpret_cast<bf16x4*>(sW + r * ld + 32 * t + 8 * (gp + 1) + 4 * s) = hi;
 }
 
+// frag_ks_perm (common.h) whose A rows 16..31 read a ones image instead (sOnes: 16 × 16 bf16 1.0):
+// the lanes that supply those rows address the ones block, so no select follows the read
+__device__ __forceinline__ bf16x8 frag_ks_perm_ones(const uint16_t* lds, int ld, int i0, int k0, const uint16_t* sOnes) {
+  const int l = lane_id();
+  const int g = l >> 4, i = l & 15, q = i >> 2, p = i & 3;
+  const uint16_t* base = (g & 1) ? sOnes + (4 * (g >> 1) + q) * 16 + 4 * p
+                                 : lds + (k0 + 4 * (g >> 1) + q) * ld + i0 + 4 * p;
+  const int hs = (g & 1) ? 8 * 16 : 8 * ld;
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(base));
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(base + hs));
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
 // ------------------------------------------------------------------------------------
 // Paired chain layout (CL2): 8 waves per 64-row tile, two waves per 16-row chain.  Wave w owns
 // rows 16·(w & 3) + (l & 15) and the channel half hf = w >> 2, i.e. m-tiles 2hf, 2hf + 1 of the
@@ -175,6 +191,7 @@ __global__ __launch_bounds__(512) void sa_layer_fwd_chain8_kernel(
   __shared__ __attribute__((aligned(16))) float sVec[7 * C + (NEXT ? nq : 0)];  // bo b1 b2 γ2 β2 γ1 β1 | bq
   __shared__ __attribute__((aligned(16))) bf16x8 sX[2][8 * 64];           // pair fragment slots
   __shared__ __attribute__((aligned(16))) float2 sR[2][8 * 16];           // pair LN slots
+  __shared__ __attribute__((aligned(16))) uint16_t sOnes[16 * 16];          // bf16 ones (P·V denominator rows)
   // the body is instantiated once per wave half (hf = qb = w >> 2, compile-time inside)
   PIO_WG_BEGIN();
   auto body = [&](auto hfc) {
@@ -234,6 +251,7 @@ __global__ __launch_bounds__(512) void sa_layer_fwd_chain8_kernel(
     *reinterpret_cast<bf16x8*>(sV + key * LDV + col) = vr[i];
   }
   if ((int)threadIdx.x < 7 * C) sVec[threadIdx.x] = pv;
+  if (threadIdx.x < 128) reinterpret_cast<uint32_t*>(sOnes)[threadIdx.x] = 0x3F803F80u;
   if constexpr (NEXT)
     if ((int)threadIdx.x < nq) sVec[7 * C + threadIdx.x] = pq;
 #pragma unroll
@@ -245,9 +263,13 @@ __global__ __launch_bounds__(512) void sa_layer_fwd_chain8_kernel(
   lds_sync();
   PIO_TS(3);
 
-  // ---- attention: head h, query block qb; keys in chunks of 128 with an online softmax ----
+  // ---- attention: head h, query block qb; keys in chunks of 128 with an online softmax.  The
+  // P·V product's A operand (Vᵀ, 32 rows) has only 16 rows of this head (D = 16): rows 16..31
+  // are ones, so accumulator rows 16..31 (registers 8..15) collect the softmax denominator
+  // Σ_k P[k][q] — no per-element VALU sum (and the denominator of exactly the bf16 P that
+  // weights V) ----
   {
-    float m_run = -INFINITY, l_run = 0.f;
+    float m_run = -INFINITY;
     f32x16 o = f32x16{};
 #pragma unroll
     for (int ch = 0; ch < MAXKT / 4; ++ch) {
@@ -266,17 +288,13 @@ __global__ __launch_bounds__(512) void sa_layer_fwd_chain8_kernel(
         }
         const float m_new = fmaxf(m_run, xor32_max(mt) * scale_log2);
         const float alpha = fast_exp2(m_run - m_new);  // 0 on the first chunk
-        l_run *= alpha;
 #pragma unroll
         for (int i = 0; i < 16; ++i) o[i] *= alpha;
 #pragma unroll
         for (int k = 0; k < 4; ++k)
           if (4 * ch + k < nkt) {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-              sc[k][i] = fast_exp2(fmaf(sc[k][i], scale_log2, -m_new));
-              l_run += sc[k][i];
-            }
+            for (int i = 0; i < 16; ++i) sc[k][i] = fast_exp2(fmaf(sc[k][i], scale_log2, -m_new));
           }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -284,14 +302,14 @@ __global__ __launch_bounds__(512) void sa_layer_fwd_chain8_kernel(
           if (kt < nkt) {
 #pragma unroll
             for (int ss = 0; ss < 2; ++ss)
-              o = mfma32(frag_ks_perm(sV, LDV, h * D, 32 * kt + 16 * ss), pack_acc(sc[k], ss), o);
+              o = mfma32(frag_ks_perm_ones(sV, LDV, h * D, 32 * kt + 16 * ss, sOnes), pack_acc(sc[k], ss), o);
           }
         }
         m_run = m_new;
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    const float ls = xor32_sum(l_run);
+    const float ls = o[8];  // row 16 (a ones row): Σ_k P[k][q] of this lane's query
     const float inv = 1.f / ls;
     const int row = 32 * qb + r;
 #pragma unroll

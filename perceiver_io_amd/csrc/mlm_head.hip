@@ -254,19 +254,25 @@ __global__ __launch_bounds__(kCombineRows * kCombineQ) void ce_combine_kernel(
   }
   lr = wave_sum(lr);  // rows of q == 0 live in wave 0
   if (count_labels) nr = wave_sum(nr);
+  // partials published write-through (sc1 agent-scope stores) and read back with sc1 loads by the
+  // last arriver: no release / acquire fences (an L2 write-back per workgroup otherwise)
   if (threadIdx.x == 0) {
-    blk[blockIdx.x] = lr;
-    if (count_labels) blk[gridDim.x + blockIdx.x] = nr;
-    __threadfence();
-    last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    __hip_atomic_store(reinterpret_cast<unsigned*>(blk + blockIdx.x), __float_as_uint(lr), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    if (count_labels)
+      __hip_atomic_store(reinterpret_cast<unsigned*>(blk + gridDim.x + blockIdx.x), __float_as_uint(nr), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   }
   __syncthreads();
   if (!last) return;
-  __threadfence();
   float t = 0.f, n = 0.f;
   for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x) {
-    t += *(volatile const float*)(blk + i);
-    if (count_labels) n += *(volatile const float*)(blk + gridDim.x + i);
+    t += __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned*>(blk + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if (count_labels)
+      n += __uint_as_float(
+          __hip_atomic_load(reinterpret_cast<unsigned*>(blk + gridDim.x + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   }
   t = wave_sum(t);
   n = wave_sum(n);

@@ -526,10 +526,10 @@ def ce_fwd(h, idx, labels, w, bias, count, zero_out=None, count_labels=False):
     return loss.sum() / count.reshape(()).clamp(min=1), lse, _ce_rows(h, idx).to(torch.bfloat16).contiguous()
 
 
-def ce_bwd(h, labels, w, bias, lse, gout, count, dH, dW, db, accumulate, rowmap=None, slab=False, u=None):
+def ce_bwd(h, labels, w, bias, lse, gout, count, dH, dW, db, accumulate, rowmap=None, slab=False, u=None, u_ml=None):
     """h: the compact bf16 rows returned by ce_fwd.  slab=True: dW | db are returned as a one-row
-    (1, V·C + V₄) slab instead of being added.  ``u`` (the HIP two-pass head's forward output) is
-    not needed here: dH is formed from the logits."""
+    (1, V·C + V₄) slab instead of being added.  ``u`` / ``u_ml`` (the HIP two-pass head's forward
+    outputs) are not needed here: dH is formed from the logits."""
     if slab:
         gw, gb = torch.zeros_like(dW), torch.zeros_like(db)
         ce_bwd(h, labels, w, bias, lse, gout, count, dH, gw, gb, False, rowmap)

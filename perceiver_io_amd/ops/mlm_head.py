@@ -95,9 +95,10 @@ class _MaskedCE(torch.autograd.Function):
         dh = torch.empty((h2.shape[0], c), device=h2.device, dtype=torch.float32)
         outs = ext.ce_fwd(h2, idx, labels_c, wb, bias.contiguous(), cnt, dh, count_labels)
         loss, lse, hs = outs[:3]
-        # C = 64: the two-pass head also returns u = Σ_v p·W − W[label] per row (the hidden-state
-        # gradient up to the row-loss scale), so the backward makes only the dW / db pass
-        ctx.u = outs[3] if len(outs) > 3 else None
+        # C = 64: the two-pass head also returns the per-split Σ_v p·W partials of every row and
+        # the splits' (max, sum): the backward merges them into the hidden-state gradient rows, so
+        # it makes only the dW / db pass over the vocabulary
+        ctx.u = (outs[3], outs[4]) if len(outs) > 4 else None
         ctx.dh = dh
         ctx.save_for_backward(hs, wb, bias, lse, idx if idx is not None else torch.empty(0, dtype=torch.int64),
                               labels_c, cnt)
@@ -125,7 +126,8 @@ class _MaskedCE(torch.autograd.Function):
         ix = idx if idx.numel() else None
         u, ctx.u = ctx.u, None
         slab = ext.ce_bwd(hs, labels_c, wb, bias.contiguous(), lse, gout.contiguous(), cnt, dh, weight.grad,
-                          ctx.bias_p.grad, True, ix, slab=fused.WGRAD_SLAB, u=u)
+                          ctx.bias_p.grad, True, ix, slab=fused.WGRAD_SLAB, u=u[0] if u else None,
+                          u_ml=u[1] if u else None)
         if slab is not None:  # dW / db row-split partials: reduced by the next backward kernel
             fused.defer_slab(ext, slab, [weight.grad.view(-1), ctx.bias_p.grad.view(-1)], [0, weight.numel()])
         return dh.view(shp), None, None, None, None, None

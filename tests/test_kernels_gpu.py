@@ -456,14 +456,14 @@ def test_fused_cross_entropy(M, V, C):
     hf = h.float()  # bf16-exact fp32 rows (the kernels cast on load)
     cnt = torch.tensor([float((lab >= 0).sum())], device=DEV)
     l2, s2, hs2 = _emu().ce_fwd(hf, None, lab, w, bias, cnt)[:3]
-    u = None  # C = 64: the two-pass head's 4th output (Σ p·W − W[label] per row) feeds ce_bwd
-    for _ in range(3):  # the loss finalisation's ticket is reset by every launch
+    u = {}  # C = 64: the two-pass head's per-split Σ p·W partials and (max, sum) pairs feed ce_bwd
+    for _ in range(3):  # the row-block and loss tickets are re-armed by every launch
         o = _ext().ce_fwd(hf, None, lab, w, bias, cnt)
         l1, s1, hs1 = o[:3]
-        u = o[3] if len(o) > 3 else None
+        u = dict(u=o[3], u_ml=o[4]) if len(o) > 4 else {}
         assert rel_fro(l1, l2) < 1e-3 and rel_fro(s1, s2) < 1e-3, (rel_fro(l1, l2), rel_fro(s1, s2))
         assert torch.equal(hs1, hs2)
-    assert (u is not None) == (C == 64)
+    assert bool(u) == (C == 64)
     # gathered rows: row r of the head input is hbig[idx[r]]
     idx = torch.randperm(2 * M, device=DEV)[:M]
     hbig = torch.zeros(2 * M, C, device=DEV)
@@ -483,12 +483,12 @@ def test_fused_cross_entropy(M, V, C):
         dH = torch.zeros(M, C, device=DEV)
         dW = torch.full((V, C), 7.0, device=DEV)  # overwritten (accumulate=False)
         db = torch.zeros(V, device=DEV)
-        K.ce_bwd(hs2, lab, w, bias, s2, gout, cnt, dH, dW, db, False, None, u=u)
+        K.ce_bwd(hs2, lab, w, bias, s2, gout, cnt, dH, dW, db, False, None, **u)
         dHs = torch.zeros(3 * M, C, device=DEV)
         dW2, db2 = dW.clone(), db.clone()
-        K.ce_bwd(hs2, lab, w, bias, s2, gout, cnt, dHs, dW2, db2, True, rowmap, u=u)
+        K.ce_bwd(hs2, lab, w, bias, s2, gout, cnt, dHs, dW2, db2, True, rowmap, **u)
         sl = K.ce_bwd(hs2, lab, w, bias, s2, gout, cnt, torch.zeros(M, C, device=DEV), dW.clone(), db.clone(), False,
-                      None, slab=True, u=u)
+                      None, slab=True, **u)
         slab_sum = sl.sum(0)
         outs.append((dH, dW, db, dHs, dW2, db2, slab_sum[:V * C].view(V, C), slab_sum[V * C:V * C + V]))
     names = ("dH", "dW", "db", "dH rowmap", "dW acc", "db acc", "dW slab", "db slab")
