@@ -5,8 +5,10 @@ reviews ask for.
     python tools/pmc_summary.py gpurun_out/ce/pmc1 gpurun_out/ce/pmc2 [--match ce2_] [--md]
 
 Derived (when the counters are present):
-  lds_conflict_pct  SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS  (extra LDS cycles per LDS-active cycle)
-  mfma_util_pct     SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE · CUs · 4 SIMDs)
+  lds_conflict_pct  SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE (extra bank-conflict cycles per LDS-array
+                    cycle; falls back to SQ_ACTIVE_INST_LDS when SQ_LDS_IDX_ACTIVE was not collected)
+  mfma_util_pct     SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs · CUs · 4 SIMDs)
+                    (GRBM_GUI_ACTIVE is summed over the 8 XCDs)
   valu_active_pct   SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES      (per-wave share of cycles issuing VALU)
   wait_pct          SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES
   valu_per_mfma     SQ_INSTS_VALU / SQ_INSTS_MFMA
@@ -39,10 +41,11 @@ def load(dirs, match):
 
 def derived(d, cus):
     x = {}
-    if d.get("SQ_ACTIVE_INST_LDS"):
-        x["lds_conflict_pct"] = 100.0 * d.get("SQ_LDS_BANK_CONFLICT", 0.0) / d["SQ_ACTIVE_INST_LDS"]
+    den = d.get("SQ_LDS_IDX_ACTIVE") or d.get("SQ_ACTIVE_INST_LDS")
+    if den:
+        x["lds_conflict_pct"] = 100.0 * d.get("SQ_LDS_BANK_CONFLICT", 0.0) / den
     if d.get("GRBM_GUI_ACTIVE") and "SQ_VALU_MFMA_BUSY_CYCLES" in d:
-        x["mfma_util_pct"] = 100.0 * d["SQ_VALU_MFMA_BUSY_CYCLES"] / (d["GRBM_GUI_ACTIVE"] * cus * 4)
+        x["mfma_util_pct"] = 100.0 * d["SQ_VALU_MFMA_BUSY_CYCLES"] / (d["GRBM_GUI_ACTIVE"] / 8.0 * cus * 4)
     if d.get("SQ_WAVE_CYCLES"):
         if "SQ_ACTIVE_INST_VALU" in d:
             x["valu_active_pct"] = 100.0 * d["SQ_ACTIVE_INST_VALU"] / d["SQ_WAVE_CYCLES"]
