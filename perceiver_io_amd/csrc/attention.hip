@@ -89,10 +89,15 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(AttnArgs a, uint16_t
     for (int s = 0; s < KS; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qp + 16 * s);
   }
 
-  if (D < 32) {  // zero the unused head-dim columns 16..31 of the V tiles once
+  // D = 16: head-dim columns 16..31 of the V tiles (O^T rows 16..31) are padding.  Without
+  // dropout they hold ones, so those O^T rows accumulate the softmax denominator Σ_k P (no
+  // per-element VALU sum); with dropout zeros (the denominator is over the undropped P)
+  const bool ones_den = D < 32 && !a.drop_thresh;
+  if (D < 32) {
+    const short pv = ones_den ? (short)0x3F80 : (short)0;  // bf16 1.0 / 0
+    const bf16x8 pad8 = {pv, pv, pv, pv, pv, pv, pv, pv};
     for (int i = threadIdx.x; i < NST * KT; i += NTH)
-      *reinterpret_cast<bf16x8*>(sV + i * LDV + 16) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0},
-      *reinterpret_cast<bf16x8*>(sV + i * LDV + 24) = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      *reinterpret_cast<bf16x8*>(sV + i * LDV + 16) = pad8, *reinterpret_cast<bf16x8*>(sV + i * LDV + 24) = pad8;
   }
 
   f32x16 o[NT];
@@ -215,13 +220,20 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(AttnArgs a, uint16_t
       const float alpha = fast_exp2(m_run - m_new);
       m_run = m_new;
       float ls = 0.f;
+      if (ones_den) {  // wave-uniform; the denominator comes out of the P·V product
 #pragma unroll
-      for (int kh = 0; kh < 2; ++kh)
+        for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          s[kh][i] = fast_exp2(fmaf(s[kh][i], a.scale_log2, -m_new));
-          ls += s[kh][i];
-        }
+          for (int i = 0; i < 16; ++i) s[kh][i] = fast_exp2(fmaf(s[kh][i], a.scale_log2, -m_new));
+      } else {
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            s[kh][i] = fast_exp2(fmaf(s[kh][i], a.scale_log2, -m_new));
+            ls += s[kh][i];
+          }
+      }
       if (a.drop_thresh) {  // uniform: the element loop above stays branch-free
 #pragma unroll
         for (int kh = 0; kh < 2; ++kh)
@@ -250,7 +262,8 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(AttnArgs a, uint16_t
     }
   }
 
-  const float l_tot = xor32_sum(l_run);
+  // O^T row 16 (a ones row when ones_den) = Σ_k P of this lane's query, complete in every lane
+  const float l_tot = ones_den ? o[0][8] : xor32_sum(l_run);
   if (qi >= a.Nq) return;
   const int HD = a.H * D;
   if (nsplit == 1) {

@@ -732,6 +732,437 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
   }  // runs
 }
 
+// ------------------------------------------------------------------------------------
+// Encoder cross-attention backward over implicit K/V, factored like attn_fwd_pe_fact_kernel: no
+// K/V tile is ever formed.  With K/V row m of sample b written as
+//     y[m, o] = rσ_m·(P'[m, o] + Σ_j a_j[m]·T_j[o]) + wt5[o],   a = [p_c − μ (c < NC) | μ | 1/rσ],
+//     T = [wt_c | wt4 | wt5]   (the 1/rσ row of a carries the bias row wt5)
+// the products of one (sample, 32-key slice, head) are
+//     S   = rσ·(Q·P'_Kᵀ + β·aᵀ) + cq             β = Q·T_K (NC + 1 columns), cq = Q·wt5_K
+//     dP  = rσ·(dO·P'_Vᵀ + ω·aᵀ) + d5            ω = dO·T_V,                 d5 = dO·wt5_V
+//     P̃ = P·rσ, dS̃ = dS·rσ = P̃·(dP − δ)        (rσ of the lane's key)
+//     dQ  = dS̃·P'_K + (dS̃·a)·T_K
+//     dK̃, dṼ = dS̃ᵀ·Q, P̃ᵀ·dO = rσ·dK, rσ·dV      → D += dK̃ | dṼ;  column sums Σ_key a_j·dỸ
+// (Σ W·dY with W = rσ·a = [x̂_c | μrσ | 1], the [1 | μrσ | x̂_c] segments of attn_bwd_pe_kernel).
+// β / ω / cq / d5 are formed ONCE per sample by the staging threads (8 threads per query row,
+// 4 dims each, DPP sums over the 8) and land in LDS as ready bf16 operand rows; cq / d5 are folded
+// into the per-query exponent offset cq·scale·log2e − LSE and the dS offset d5 − δ in fp32, so the
+// only bf16-rounded per-sample terms are the ones the forward rounds the same way.  Every lane forms
+// the statistics of its own key (pixels prefetched one sample ahead, PE row sums in registers) and
+// writes its row of a (wave-private LDS: the transposed products read it); the batch-invariant
+// P' fragments of S / dP and the dQ table operand stay in registers for the whole run.  Per
+// 32-key slice and sample: 19 MFMAs, one workgroup barrier (two with per-sample queries).  Same
+// run structure, outputs and partial-row layout as attn_bwd_pe_kernel.
+// ------------------------------------------------------------------------------------
+template <int NC, bool QB>
+__global__ __launch_bounds__(512) void attn_bwd_pe_fact_kernel(PeBwdArgs a) {
+  constexpr int NW = 8, KB = 256, NTH = 512;
+  constexpr int PPL = 2 * PD + 8;  // P' tile row stride (bf16): K columns [0, 32), V [32, 64)
+  constexpr int NA = NC + 2;       // rows of a: p_c − μ, μ, 1/rσ
+  static_assert(NA <= 6, "a fits the first 8 slots of one operand half");
+  __shared__ __attribute__((aligned(16))) uint16_t sQ[QB ? 2 : 1][32 * PLD];
+  __shared__ __attribute__((aligned(16))) uint16_t sdO[2][32 * PLD];
+  // per query: the augmentation operand row [β_c | γ] / [ω_c | ω_4] (slots 0..7: lane half 0;
+  // slots 8..15 stay zero: lane half 1)
+  __shared__ __attribute__((aligned(16))) uint16_t sAq[QB ? 2 : 1][32 * 16];
+  __shared__ __attribute__((aligned(16))) uint16_t sAo[2][32 * 16];
+  __shared__ __attribute__((aligned(16))) float sL[2][32], sDl[2][32];  // cq·sl2 − LSE, d5 − δ
+  __shared__ __attribute__((aligned(16))) float sWt[PE_NWT][64];        // head h's table: K | V columns
+  __shared__ __attribute__((aligned(16))) uint16_t sP[NW][32 * PPL];    // run setup: the wave's P' rows
+  __shared__ __attribute__((aligned(16))) uint16_t sS[NW][32 * PLD];    // dS̃ slab [key][q]
+  __shared__ __attribute__((aligned(16))) uint16_t sA[NW][33 * 16];     // [key][j]: a (j < NA), 0 (j 8..15)
+  __shared__ __attribute__((aligned(16))) float sDQb[QB ? NW : 1][QB ? 32 * 36 : 1];  // per wave: dQ_b [d][q]
+  // epilogue aliases over the consumed tiles: dQ partials [w][q][d], column sums [w][2][seg][d]
+  float(*sDQ)[32 * 33] = reinterpret_cast<float(*)[32 * 33]>(&sP[0][0]);
+  float(*sCS)[2][PNSEG][32] = reinterpret_cast<float(*)[2][PNSEG][32]>(&sS[0][0]);
+  static_assert(sizeof(float) * NW * 32 * 33 <= sizeof(uint16_t) * NW * 32 * PPL, "dQ partial alias");
+  static_assert(sizeof(float) * NW * 2 * PNSEG * 32 <= sizeof(uint16_t) * NW * 32 * PLD, "column-sum alias");
+
+  const int w = wave_id(), l = lane_id(), r = l & 31, hh = l >> 5;
+  const int C = a.C, O = 2 * C;
+  const float sl2 = a.scale_log2;
+  const bf16x8 z8 = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+
+  // zero slots that are never rewritten: operand-row halves 8..15, a's slots 8..15
+  for (int t = threadIdx.x; t < (QB ? 2 : 1) * 32; t += NTH) *reinterpret_cast<bf16x8*>(&sAq[t >> 5][(t & 31) * 16 + 8]) = z8;
+  for (int t = threadIdx.x; t < 2 * 32; t += NTH) *reinterpret_cast<bf16x8*>(&sAo[t >> 5][(t & 31) * 16 + 8]) = z8;
+  for (int t = threadIdx.x; t < NW * 33; t += NTH) *reinterpret_cast<bf16x8*>(&sA[t / 33][(t % 33) * 16 + 8]) = z8;
+
+  // run bookkeeping: identical to attn_bwd_pe_kernel
+  const int nkb = (a.M + KB - 1) / KB;
+  long long it = 0, it_end = 0;
+  if (a.nbg > 0 && !a.accumulate) {
+    float* prow0 = a.part + (long long)(nkb + blockIdx.x) * ((2 + NC) * O);
+    for (int e = threadIdx.x; e < (2 + NC) * O; e += NTH) prow0[e] = 0.f;
+  }
+  if (a.nbg > 0) {
+    const long long T = (long long)nkb * a.H * a.nbg;
+    it = T * blockIdx.x / gridDim.x;
+    it_end = T * (blockIdx.x + 1) / gridDim.x;
+    if (threadIdx.x == 0) a.side_pair[blockIdx.x] = (it % a.nbg) != 0 ? (int)(it / a.nbg) : -1;
+  }
+  // staging roles (per sample): thread t → tensor t >> 8 (0: Q, 1: dO), query row (t >> 3) & 31,
+  // dims 4·(t & 7) .. +3; the row's first thread also loads the row's LSE / δ
+  const int st_ten = threadIdx.x >> 8, st_row = (threadIdx.x >> 3) & 31, st_c = 4 * (threadIdx.x & 7);
+  const bool st_lead = (threadIdx.x & 7) == 0;
+  const int st_rowc = min(st_row, a.Nq - 1);
+  const bool st_ok = st_row < a.Nq;
+
+  for (bool first_run = true;; first_run = false) {
+    int kb, h, b0, b1, side = -1;
+    long long prow;
+    if (a.nbg > 0) {
+      if (it >= it_end) break;
+      if (!first_run) __syncthreads();  // the previous run's epilogue LDS traffic is done
+      const int pair = (int)(it / a.nbg), bgs = (int)(it % a.nbg);
+      const int bge = (int)min((long long)a.nbg, bgs + (it_end - it));
+      kb = pair / a.H;
+      h = pair % a.H;
+      b0 = bgs * a.bper;
+      b1 = min(a.B, bge * a.bper);
+      if (bgs > 0) side = blockIdx.x;
+      prow = bgs > 0 ? nkb + blockIdx.x : kb;
+      it += bge - bgs;
+    } else {
+      if (!first_run) break;
+      kb = blockIdx.x;
+      h = blockIdx.y;
+      b0 = blockIdx.z * a.bper;
+      b1 = min(a.B, b0 + a.bper);
+      prow = (long long)blockIdx.x * gridDim.z + blockIdx.z;
+    }
+    const int kbase = kb * KB;
+    const int key = kbase + 32 * w + r;  // this lane's key (S / dP column)
+    const bool kval = key < a.M;
+    const int keyc = min(key, a.M - 1);
+    const bool masked = kbase + KB > a.M;  // uniform: the run's last key block is partial
+
+    // ---- run setup: table columns of head h, the wave's P' rows, the lane's PE row sums
+    for (int t = threadIdx.x; t < 64 * PE_NWT; t += NTH) {
+      const int j = t >> 6, c = t & 63;
+      sWt[j][c] = a.wt[(long long)j * O + (c < PD ? h * PD + c : C + h * PD + c - PD)];
+    }
+    const uint16_t* prp = a.P + (long long)keyc * O + h * PD;
+    bf16x8 pk[2], pv[2];  // S / dP B operands: P'_K / P'_V [key r][d = 16s + 8hh .. +7]
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      pk[s] = *reinterpret_cast<const bf16x8*>(prp + 16 * s + 8 * hh);
+      pv[s] = *reinterpret_cast<const bf16x8*>(prp + C + 16 * s + 8 * hh);
+      *reinterpret_cast<bf16x8*>(&sP[w][r * PPL + 16 * s + 8 * hh]) = pk[s];
+    }
+    const float pes = a.pes[keyc], pesq = a.pesq[keyc];
+    __syncthreads();  // sWt, sP
+    // dQ B operands: P'_K [k = key 16s + 8hh + j][n = d = r], and the table operand of the dQ
+    // augmentation: slot t of half hh ↔ row j = 4hh + (t & 3) + 8(t >> 2) of Gᵀ (pack_acc order)
+    bf16x8 tq;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int j = 4 * hh + (t & 3) + 8 * (t >> 2);
+      const int row = j < NC ? j : (j == NC ? 4 : 5);
+      tq[t] = (short)f2bf(j < NA ? sWt[row][r] : 0.f);
+    }
+    // table values of this staging thread's 4 dims (K table for Q rows, V table for dO rows)
+    // rows [wt_c | wt4 | wt5] → NA dot products per staged row
+    float cq_keep = 0.f;  // broadcast queries: this row's Q·wt5_K (staging leaders of tensor 0)
+
+    // dot products of one staged 4-dim piece with the table rows, summed over the row's 8
+    // threads; the leader writes the operand row (slots 0..NC) and returns the wt5 product
+    auto stage_aug = [&](const bf16x4& v, uint16_t* arow) -> float {
+      float part[NA];
+#pragma unroll
+      for (int j = 0; j < NA; ++j) {
+        const int trow = j < NC ? j : (j == NC ? 4 : 5);
+        const f32x4 tw = *reinterpret_cast<const f32x4*>(&sWt[trow][32 * st_ten + st_c]);
+        float s = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s = fmaf(bf2f(v[e]), tw[e], s);
+        s += dpp<0xB1>(s);
+        s += dpp<0x4E>(s);
+        s += dpp<0x141>(s);  // row_half_mirror: lanes 0-7 ↔ 7-0 (sums the two quads of 8)
+        part[j] = s;
+      }
+      if (st_lead) {
+        bf16x8 au = z8;
+#pragma unroll
+        for (int j = 0; j < NC + 1; ++j) au[j] = (short)f2bf(part[j]);
+        *reinterpret_cast<bf16x8*>(arow) = au;
+      }
+      return part[NA - 1];
+    };
+
+    // ---- per-sample register staging: fetch() only issues loads (clamped addresses)
+    bf16x4 st_v = bf16x4{0, 0, 0, 0};
+    float st_ld = 0.f;
+    float px[NC], pxn[NC];
+    // per-thread sample-0 addresses + wave-uniform per-sample strides (scalar multiplies)
+    const int wten = __builtin_amdgcn_readfirstlane(st_ten);
+    const uint16_t* st_src = wten == 0 ? a.q + (long long)st_rowc * a.q_rs + h * PD + st_c
+                                       : a.dO + (long long)st_rowc * C + h * PD + st_c;
+    const long long st_bs = wten == 0 ? a.q_bs : (long long)a.Nq * C;
+    const float* ld_src = (wten == 0 ? a.lse : a.delta) + (long long)st_rowc * a.H + h;
+    const long long ld_bs = (long long)a.Nq * a.H;
+    const float* px_src = a.pix + (long long)keyc * NC;
+    const long long px_bs = (long long)a.M * NC;
+    auto fetch = [&](int b) {
+      if (QB || wten == 1) st_v = *reinterpret_cast<const bf16x4*>(st_src + b * st_bs);
+      if (st_lead) st_ld = ld_src[b * ld_bs];
+    };
+    auto fetch_px = [&](int b, float (&dst)[NC]) {
+      const float* pp = px_src + b * px_bs;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) dst[c] = pp[c];
+    };
+    auto stage = [&](int buf) {
+      float cst;
+      if (QB || wten == 1) {
+        const bf16x4 v = st_ok ? st_v : bf16x4{0, 0, 0, 0};
+        uint16_t* tile = wten == 0 ? sQ[QB ? buf : 0] : sdO[buf];
+        *reinterpret_cast<bf16x4*>(tile + st_row * PLD + st_c) = v;
+        cst = stage_aug(v, wten == 0 ? &sAq[QB ? buf : 0][st_row * 16] : &sAo[buf][st_row * 16]);
+      } else {
+        cst = cq_keep;
+      }
+      if (st_lead) {
+        if (wten == 0) sL[buf][st_row] = st_ok ? fmaf(cst, sl2, -st_ld) : -INFINITY;
+        else sDl[buf][st_row] = st_ok ? cst - st_ld : 0.f;
+      }
+    };
+    auto lds_barrier = [] {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    };
+
+    // broadcast queries: the Q tile, its augmentation row and cq once per run
+    if (!QB && st_ten == 0) {
+      const bf16x4 v = st_ok ? *reinterpret_cast<const bf16x4*>(a.q + (long long)st_rowc * a.q_rs + h * PD + st_c)
+                             : bf16x4{0, 0, 0, 0};
+      *reinterpret_cast<bf16x4*>(&sQ[0][st_row * PLD + st_c]) = v;
+      cq_keep = stage_aug(v, &sAq[0][st_row * 16]);
+    }
+
+    f32x16 accD[2];  // D for this wave's 32 keys × 32 columns of head h: [0] K part, [1] V part
+    f32x16 accX[2];  // column sums: rows = segment j of W, columns = d; [0] K part, [1] V part
+    f32x16 accQ;     // dQ Σ over the batch (broadcast queries): rows = query, columns = d
+    accD[0] = accD[1] = accX[0] = accX[1] = accQ = f32x16{};
+
+    if (b0 < b1) {
+      fetch(b0);
+      fetch_px(b0, px);
+      stage(b0 & 1);
+      if (b0 + 1 < b1) {
+        fetch(b0 + 1);
+        fetch_px(b0 + 1, pxn);
+      }
+    }
+    lds_barrier();
+
+    auto body = [&](int b, auto masked_t) {
+      constexpr bool MK = decltype(masked_t)::value;
+      const int cur = b & 1;
+      // (0) statistics of key `key` for sample b → a, W, rσ rows (wave-private) and the key-side
+      // augmentation operand of S / dP
+      float sm = pes, sq = pesq;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        sm += px[c];
+        sq = fmaf(px[c], px[c], sq);
+      }
+      const float mu = sm * a.inv_k;
+      const float var = fmaxf(sq * a.inv_k - mu * mu, 0.f) + a.eps;
+      const float rs = rsqrtf(var);
+      float av[NA];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) av[c] = px[c] - mu;
+      av[NC] = mu;
+      av[NC + 1] = var * rs;  // 1/rσ
+      if constexpr (MK) {
+        if (!kval) {
+#pragma unroll
+          for (int j = 0; j < NA; ++j) av[j] = 0.f;
+        }
+      }
+      bf16x8 kaug = z8, row = z8;
+#pragma unroll
+      for (int j = 0; j < NA; ++j) row[j] = (short)f2bf(av[j]);
+      if (hh == 0) {
+#pragma unroll
+        for (int j = 0; j < NC + 1; ++j) kaug[j] = row[j];
+        *reinterpret_cast<bf16x8*>(&sA[w][r * 16]) = row;
+      }
+      // pixels of sample b + 1 move up; loads of b + 2 are issued after the staging below
+#pragma unroll
+      for (int c = 0; c < NC; ++c) px[c] = pxn[c];
+      // (1) sample b+1 → LDS (its loads were issued one iteration ago), loads of b+2
+      if (b + 1 < b1) {
+        stage(cur ^ 1);
+        if (b + 2 < b1) {
+          fetch(b + 2);
+          fetch_px(b + 2, pxn);
+        }
+      }
+      // (2) S and dP: rows = queries, lane = key
+      const uint16_t* tQ = sQ[QB ? cur : 0];
+      const uint16_t* tdO = sdO[cur];
+      const bf16x8 qaug = *reinterpret_cast<const bf16x8*>(&sAq[QB ? cur : 0][r * 16 + 8 * hh]);
+      const bf16x8 oaug = *reinterpret_cast<const bf16x8*>(&sAo[cur][r * 16 + 8 * hh]);
+      f32x16 S = mfma32(qaug, kaug, f32x16{}), dP = mfma32(oaug, kaug, f32x16{});
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        S = mfma32(frag_kc(tQ, PLD, 0, 16 * s), pk[s], S);
+        dP = mfma32(frag_kc(tdO, PLD, 0, 16 * s), pv[s], dP);
+      }
+      // P̃ = P·rσ and dS̃ = dS·rσ (rσ of the lane's key): dṼ = P̃ᵀ·dO = rσ·dV and dK̃ = dS̃ᵀ·Q =
+      // rσ·dK are exactly the D increments, and the column sums Σ W·dY = Σ a·dỸ
+      const float cl = rs * sl2;
+      f32x16 P, dS;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 lr = *reinterpret_cast<const f32x4*>(&sL[cur][8 * g + 4 * hh]);
+        const f32x4 dr = *reinterpret_cast<const f32x4*>(&sDl[cur][8 * g + 4 * hh]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * g + e;
+          float p = fast_exp2(fmaf(S[i], cl, lr[e])) * rs;
+          if constexpr (MK) p = kval ? p : 0.f;
+          P[i] = p;
+          dS[i] = p * fmaf(dP[i], rs, dr[e]);
+        }
+      }
+      // dṼ_b = P̃ᵀ·dO, dK̃_b = dS̃ᵀ·Q (rows: this wave's keys, lane: head-dim column; dK̃ unscaled)
+      f32x16 dV = f32x16{}, dK = f32x16{};
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        dV = mfma32(pack_acc(P, ss), frag_ks_perm(tdO, PLD, 0, 16 * ss), dV);
+        dK = mfma32(pack_acc(dS, ss), frag_ks_perm(tQ, PLD, 0, 16 * ss), dK);
+      }
+      // dS̃ slab [key][q] (wave-private) for the dQ products
+      uint16_t* tS = sS[w];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint2 pkd;
+        pkd.x = pack2(dS[4 * g], dS[4 * g + 1]);
+        pkd.y = pack2(dS[4 * g + 2], dS[4 * g + 3]);
+        *reinterpret_cast<uint2*>(&tS[r * PLD + 8 * g + 4 * hh]) = pkd;
+      }
+      accD[0] += dK;
+      accD[1] += dV;
+      // column sums Σ_key a[j][key]·dỸ[key][d]: A = a (k order permuted to the accumulator's rows)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 wa = frag_ks_perm(&sA[w][0], 16, 0, 16 * s);
+        accX[0] = mfma32(wa, pack_acc(dK, s), accX[0]);
+        accX[1] = mfma32(wa, pack_acc(dV, s), accX[1]);
+      }
+      // dQ_b = dS̃·P'_K + (dS̃·a)·T_K from the wave's own slab and a rows
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      bf16x8 ts[2];
+      f32x16 G = f32x16{};  // Gᵀ: rows = j, columns = q
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        ts[s] = frag_ks(tS, PLD, 0, 16 * s);
+        G = mfma32(frag_ks(&sA[w][0], 16, 0, 16 * s), ts[s], G);
+      }
+      if constexpr (QB) {
+        f32x16 dq = mfma32(ts[0], frag_ks(&sP[w][0], PPL, 0, 0), f32x16{});
+        dq = mfma32(ts[1], frag_ks(&sP[w][0], PPL, 0, 16), dq);
+        dq = mfma32(pack_acc(G, 0), tq, dq);
+        // partial [d][q]: registers 4g..4g+3 are 4 consecutive queries → one 16-byte store
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<f32x4*>(&sDQb[w][r * 36 + 8 * g + 4 * hh]) =
+              f32x4{dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]};
+        lds_barrier();
+        if (threadIdx.x < 256) {  // Σ over the waves: thread t → d = t >> 3, queries 4·(t & 7) .. +3
+          const int dd = threadIdx.x >> 3, q0 = 4 * (threadIdx.x & 7);
+          f32x4 v = *reinterpret_cast<const f32x4*>(&sDQb[0][dd * 36 + q0]);
+#pragma unroll
+          for (int ww = 1; ww < NW; ++ww) v += *reinterpret_cast<const f32x4*>(&sDQb[ww][dd * 36 + q0]);
+          float* dst = a.dq + (long long)kb * a.dq_kbs + ((long long)b * a.Nq) * C + h * PD + dd;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (q0 + e < a.Nq) {
+              if (a.dq_kbs) dst[(long long)(q0 + e) * C] = v[e] * a.scale;
+              else atomicAdd(dst + (long long)(q0 + e) * C, v[e] * a.scale);
+            }
+          }
+        }
+      } else {
+        accQ = mfma32(ts[0], frag_ks(&sP[w][0], PPL, 0, 0), accQ);
+        accQ = mfma32(ts[1], frag_ks(&sP[w][0], PPL, 0, 16), accQ);
+        accQ = mfma32(pack_acc(G, 0), tq, accQ);
+      }
+      lds_barrier();
+    };
+    if (masked) {  // two loops: one register assignment each (no copies at a merged loop head)
+      for (int b = b0; b < b1; ++b) body(b, std::true_type{});
+    } else {
+      for (int b = b0; b < b1; ++b) body(b, std::false_type{});
+    }
+
+    // ---- D rows of this wave's keys (K part columns 32h + r, V part C + 32h + r)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int m = kbase + 32 * w + acc_row(i, hh);
+      if (m < a.M) {
+        float* dk = a.D + (long long)m * O + h * PD + r;
+        float* dv = dk + C;
+        const float vk = accD[0][i] * a.scale, vv = accD[1][i];
+        if (side >= 0) {
+          float* sd = a.Dside + ((long long)side * KB + m - kbase) * 64 + r;
+          sd[0] = vk;
+          sd[PD] = vv;
+        } else if (a.d_atomic) {
+          atomicAdd(dk, vk);
+          atomicAdd(dv, vv);
+        } else if (a.accumulate) {
+          *dk += vk;
+          *dv += vv;
+        } else {
+          *dk = vk;
+          *dv = vv;
+        }
+      }
+    }
+    // ---- dQ and column sums: per-wave partials through LDS (aliases of the consumed tiles)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int row = acc_row(i, hh);
+      if (!QB) sDQ[w][row * 33 + r] = accQ[i];
+      if (row < PNSEG) {
+        sCS[w][0][row][r] = accX[0][i];
+        sCS[w][1][row][r] = accX[1][i];
+      }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < (QB ? 0 : 32 * PD); e += NTH) {
+      const int qq = e >> 5, dd = e & 31;
+      float v = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < NW; ++ww) v += sDQ[ww][qq * 33 + dd];
+      if (qq < a.Nq) {
+        float* dst = a.dq + (long long)kb * a.dq_kbs + (long long)qq * C + h * PD + dd;
+        if (a.dq_kbs) *dst = v * a.scale;
+        else atomicAdd(dst, v * a.scale);
+      }
+    }
+    // partial segments in attn_bwd_pe_kernel's order: 0 ↔ Σ dY (W row NC + 1 = 1),
+    // 1 ↔ Σ dY·μrσ (W row NC), 2 + c ↔ Σ dY·x̂_c (W row c)
+    constexpr int nseg = 2 + NC;
+    for (int e = threadIdx.x; e < 2 * nseg * 32; e += NTH) {
+      const int p = e / (nseg * 32), rem = e % (nseg * 32), seg = rem / 32, j = rem % 32;
+      const int wrow = seg == 0 ? NC + 1 : (seg == 1 ? NC : seg - 2);
+      float v = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < NW; ++ww) v += sCS[ww][p][wrow][j];
+      if (p == 0) v *= a.scale;
+      float* dst = a.part + prow * (long long)(nseg * O) + (long long)seg * O + p * C + h * PD + j;
+      *dst = a.accumulate ? *dst + v : v;
+    }
+  }  // runs
+}
+
 // D[pair rows] += Dside[slot] for every slot holding a leading partial run (persistent mode)
 __global__ __launch_bounds__(256) void attn_pe_side_add_kernel(const float* __restrict__ Dside,
                                                                const int* __restrict__ side_pair, float* __restrict__ D,
@@ -771,9 +1202,17 @@ void attn_bwd_pe_launch(const PeBwdArgs& a0, int nkb, int bsplit, hipStream_t st
     a.bper = (a.B + bsplit - 1) / bsplit;
     a.d_atomic = bsplit > 1 ? 1 : 0;
   }
-  if (a.P) {
-    if (a.q_bs == 0) hipLaunchKernelGGL((attn_bwd_pe_kernel<NW, false, true>), grid, dim3(64 * NW), 0, st, a);
-    else hipLaunchKernelGGL((attn_bwd_pe_kernel<NW, true, true>), grid, dim3(64 * NW), 0, st, a);
+  if (a.P) {  // implicit K/V: the factored kernel
+#define PIO_PEBF(NC_)                                                                                      \
+  if (a.q_bs == 0) hipLaunchKernelGGL((attn_bwd_pe_fact_kernel<NC_, false>), grid, dim3(64 * NW), 0, st, a); \
+  else hipLaunchKernelGGL((attn_bwd_pe_fact_kernel<NC_, true>), grid, dim3(64 * NW), 0, st, a)
+    switch (a.nc) {
+      case 1: PIO_PEBF(1); break;
+      case 2: PIO_PEBF(2); break;
+      case 3: PIO_PEBF(3); break;
+      default: PIO_PEBF(4); break;
+    }
+#undef PIO_PEBF
   } else {
     if (a.q_bs == 0) hipLaunchKernelGGL((attn_bwd_pe_kernel<NW, false, false>), grid, dim3(64 * NW), 0, st, a);
     else hipLaunchKernelGGL((attn_bwd_pe_kernel<NW, true, false>), grid, dim3(64 * NW), 0, st, a);

@@ -414,12 +414,34 @@ __global__ __launch_bounds__(512) void sa_layer_fwd_chain8_kernel(
 //      LayerNorm-ed operand is applied in the epilogue (dW = γ∘(Gᵀ·x̂) + β⊗db), so only x̂ is
 //      staged.  Partials go to this tile's slab row (plain stores).
 // ------------------------------------------------------------------------------------
-// the same in the CL k order of k-step t (element j ↔ k = 32t + 16(j >> 2) + 4g + (j & 3))
+// The boundary kernel's LDS images are unpadded ([rows][64·k] bf16, 128-byte multiples) with
+// the column bits 3..5 of row r XOR-ed with 8·ψ(r), ψ(r) = r₃ | r₁·2 | (r₂ ⊕ r₃)·4 (rₖ = bit k
+// of r).  Every access of the kernel — 16-byte row chunks (weights, G), 8-byte row pieces
+// (cl2_tile_store / cl2_img_frag) and the transposed ds_read_b64_tr_b16 fragments (frag16_tr_sw,
+// frag16_tr_cl: 8 rows × 32 bytes per 32 lanes) — then touches 64 distinct banks per lane group
+// (a padded 72-column layout conflicts 2-way on the transposed reads).
+__device__ __forceinline__ int swz8(int r) {
+  return 8 * (((r >> 3) & 1) | (((r >> 1) & 1) << 1) | ((((r >> 2) ^ (r >> 3)) & 1) << 2));
+}
+// element (r, c) of a swizzled image; c may be any column of a 4-aligned (8-byte) piece
+__device__ __forceinline__ int swzi(int r, int ld, int c) { return r * ld + (c ^ swz8(r)); }
+// frag16_tr (common.h) on a swizzled image
+__device__ __forceinline__ bf16x8 frag16_tr_sw(const uint16_t* lds, int ld, int i0, int k0) {
+  const int l = lane_id(), g = l >> 4, i = l & 15;
+  const int r = k0 + 8 * g + (i >> 2), c = i0 + 4 * (i & 3);
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(lds + swzi(r, ld, c)));
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(lds + swzi(r + 4, ld, c)));
+  bf16x8 v;
+  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+  return v;
+}
+// the same in the CL k order of k-step t (element j ↔ k = 32t + 16(j >> 2) + 4g + (j & 3)), swizzled
 __device__ __forceinline__ bf16x8 frag16_tr_cl(const uint16_t* lds, int ld, int i0, int t) {
   const int l = lane_id(), g = l >> 4, i = l & 15;
-  const uint16_t* base = lds + (32 * t + 4 * g + (i >> 2)) * ld + i0 + 4 * (i & 3);
-  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(base));
-  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(base + 16 * ld));
+  const int rr = 32 * t + 4 * g + (i >> 2), c = i0 + 4 * (i & 3);
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(lds + swzi(rr, ld, c)));
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(lds + swzi(rr + 16, ld, c)));
   bf16x8 r;
   r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
   r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
@@ -441,9 +463,9 @@ __device__ __forceinline__ void cl_wgrad_block(const uint16_t* sA, int lda, int 
   for (int n = 0; n < 5; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    const bf16x8 a = frag16_tr(sA, lda, 16 * mt, 32 * t);
+    const bf16x8 a = frag16_tr_sw(sA, lda, 16 * mt, 32 * t);
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) acc[nt] = mfma16(a, frag16_tr(sB, ldb, 16 * nt, 32 * t), acc[nt]);
+    for (int nt = 0; nt < 4; ++nt) acc[nt] = mfma16(a, frag16_tr_sw(sB, ldb, 16 * nt, 32 * t), acc[nt]);
     acc[4] = mfma16(a, ones_frag(), acc[4]);
   }
 #pragma unroll
@@ -451,10 +473,7 @@ __device__ __forceinline__ void cl_wgrad_block(const uint16_t* sA, int lda, int 
     const int n = 16 * nt + c;
     const float gn = gam ? gam[n] : 1.f, bn = bet ? bet[n] : 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = 16 * mt + 4 * g + i;
-      dW[m * 64 + n] = acc[nt][i] * gn + acc[4][i] * bn;
-    }
+    for (int i = 0; i < 4; ++i) dW[(16 * mt + 4 * g + i) * 64 + n] = acc[nt][i] * gn + acc[4][i] * bn;
   }
   if (c == 0)
 #pragma unroll
@@ -467,8 +486,8 @@ __device__ __forceinline__ void cl_ln_grads(const uint16_t* sD, const uint16_t* 
   f32x4 dia = f32x4{0.f, 0.f, 0.f, 0.f}, sum = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    const bf16x8 a = frag16_tr(sD, ld, 16 * mt, 32 * t);
-    dia = mfma16(a, frag16_tr(sXh, ld, 16 * mt, 32 * t), dia);
+    const bf16x8 a = frag16_tr_sw(sD, ld, 16 * mt, 32 * t);
+    dia = mfma16(a, frag16_tr_sw(sXh, ld, 16 * mt, 32 * t), dia);
     sum = mfma16(a, ones_frag(), sum);
   }
   const int i = c - 4 * g;  // acc row 4g + i is channel column c on the diagonal
@@ -481,8 +500,9 @@ __device__ __forceinline__ void cl_ln_grads(const uint16_t* sD, const uint16_t* 
 template <int NQ>
 constexpr int lpb_chain_smem() {
   // W images (Wo W1 W2) | LL images (G, x̂1, dXn1) | Wq image, overlaid by the 7 PA images | vectors
-  return 2 * (3 * 64 * 72) + 2 * (64 * (NQ * 64 + 8) + 2 * 64 * 72) +
-         2 * (NQ * 64 * 72 > 7 * 64 * 72 ? NQ * 64 * 72 : 7 * 64 * 72) + 4 * 4 * 64;
+  // (swizzled, unpadded rows: swz8 / swzi)
+  return 2 * (3 * 64 * 64) + 2 * (64 * (NQ * 64) + 2 * 64 * 64) +
+         2 * (NQ * 64 * 64 > 7 * 64 * 64 ? NQ * 64 * 64 : 7 * 64 * 64) + 4 * 4 * 64;
 }
 
 // ------------------------------------------------------------------------------------
@@ -497,8 +517,8 @@ constexpr int lpb_chain_smem() {
 // CL k-order fragment of k-step t of row lr from a row-major bf16 image [64][ld]
 __device__ __forceinline__ bf16x8 cl2_img_frag(const uint16_t* sT, int ld, int lr, int t) {
   const int g = lane_id() >> 4;
-  const bf16x4 lo = *reinterpret_cast<const bf16x4*>(sT + lr * ld + 32 * t + 4 * g);
-  const bf16x4 hi = *reinterpret_cast<const bf16x4*>(sT + lr * ld + 32 * t + 16 + 4 * g);
+  const bf16x4 lo = *reinterpret_cast<const bf16x4*>(sT + swzi(lr, ld, 32 * t + 4 * g));
+  const bf16x4 hi = *reinterpret_cast<const bf16x4*>(sT + swzi(lr, ld, 32 * t + 16 + 4 * g));
   bf16x8 r;
   r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
   r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
@@ -512,7 +532,7 @@ __device__ __forceinline__ void cl2_tile_store(uint16_t* sT, int ld, int lr, int
     uint2 pk;
     pk.x = pack2(v[i][0], v[i][1]);
     pk.y = pack2(v[i][2], v[i][3]);
-    *reinterpret_cast<uint2*>(sT + lr * ld + 16 * (2 * hf + i) + 4 * g) = pk;
+    *reinterpret_cast<uint2*>(sT + swzi(lr, ld, 16 * (2 * hf + i) + 4 * g)) = pk;
   }
 }
 // dXᵀ (this wave's two m-tiles of the 64 input channels) = Wᵀ·dYᵀ over 2 k-steps
@@ -549,7 +569,7 @@ __global__ __launch_bounds__(512) void ln_linear_post_attn_bwd_chain8_kernel(
     const uint16_t* __restrict__ Wo, const uint16_t* __restrict__ W1, const uint16_t* __restrict__ W2,
     const float* __restrict__ g2, const float* __restrict__ be2, float* __restrict__ dY, uint16_t* __restrict__ dO,
     float* __restrict__ delta, PostAttnGrads gr_out, int R, SlabJob job, DropCfg dr) {
-  constexpr int C = 64, LD = 72, nq = NQ * C, LDG = nq + 8, KT = nq / 32, NT = 512;
+  constexpr int C = 64, LD = 64, nq = NQ * C, LDG = nq, KT = nq / 32, NT = 512;  // swizzled images (swz8)
   constexpr int NWC = (3 * C + nq) * 8 / NT;  // 16-byte weight chunks per thread
   static_assert((3 * C + nq) * 8 % NT == 0 && KT % 2 == 0, "staging split");
   __shared__ __attribute__((aligned(16))) unsigned char smem[lpb_chain8_smem<NQ>()];
@@ -637,8 +657,8 @@ __global__ __launch_bounds__(512) void ln_linear_post_attn_bwd_chain8_kernel(
 #pragma unroll
   for (int i = 0; i < NWC; ++i) {
     const int c = threadIdx.x + NT * i, row = c >> 3, col = (c & 7) * 8;
-    uint16_t* dst = row < 3 * C ? sWo + row * LD : sWq + (row - 3 * C) * LD;
-    *reinterpret_cast<bf16x8*>(dst + col) = wr[i];
+    uint16_t* dst = row < 3 * C ? sWo + swzi(row, LD, col) : sWq + swzi(row - 3 * C, LD, col);
+    *reinterpret_cast<bf16x8*>(dst) = wr[i];
   }
   if (threadIdx.x < 4 * C) sVec[threadIdx.x] = pv;
   bf16x8 gb[KT];
@@ -652,7 +672,7 @@ __global__ __launch_bounds__(512) void ln_linear_post_attn_bwd_chain8_kernel(
       gb[t][0] = (short)f2bf(a.x); gb[t][1] = (short)f2bf(a.y); gb[t][2] = (short)f2bf(a.z); gb[t][3] = (short)f2bf(a.w);
       gb[t][4] = (short)f2bf(b.x); gb[t][5] = (short)f2bf(b.y); gb[t][6] = (short)f2bf(b.z); gb[t][7] = (short)f2bf(b.w);
     }
-    *reinterpret_cast<bf16x8*>(sG + lr * LDG + 32 * t + 8 * g) = gb[t];
+    *reinterpret_cast<bf16x8*>(sG + swzi(lr, LDG, 32 * t + 8 * g)) = gb[t];
   }
   PIO_TS(2);
   lds_sync();
@@ -660,7 +680,7 @@ __global__ __launch_bounds__(512) void ln_linear_post_attn_bwd_chain8_kernel(
 #pragma unroll
   for (int u = 0; u < KH; ++u) {  // the partner's k-steps of G, from the image
     const int t = 2 * u + 1 - hf;
-    gb[t] = *reinterpret_cast<const bf16x8*>(sG + lr * LDG + 32 * t + 8 * g);
+    gb[t] = *reinterpret_cast<const bf16x8*>(sG + swzi(lr, LDG, 32 * t + 8 * g));
   }
 
   // ---- A: LN1 + QKV backward of layer l+1 → dZ of layer l (this wave's channels) ----
@@ -669,7 +689,7 @@ __global__ __launch_bounds__(512) void ln_linear_post_attn_bwd_chain8_kernel(
   for (int i = 0; i < 2; ++i) {
     acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int t = 0; t < KT; ++t) acc[i] = mfma16(frag16_tr(sWq, LD, 16 * (2 * hf + i), 32 * t), gb[t], acc[i]);
+    for (int t = 0; t < KT; ++t) acc[i] = mfma16(frag16_tr_sw(sWq, LD, 16 * (2 * hf + i), 32 * t), gb[t], acc[i]);
   }
   PIO_TS(4);
   float dz[2][4], t0[2][4];
@@ -796,12 +816,12 @@ __global__ __launch_bounds__(512) void ln_linear_post_attn_bwd_chain8_kernel(
   lds_sync();
   PIO_TS(10);
 
-  // ---- C: parameter gradients of the tile → slab row blockIdx.x, 16-row blocks over 8 waves ----
+  // ---- C: parameter gradients of the tile → its slab row, 16-row blocks over 8 waves ----
   const int vrs = gr_out.vrs;
   const long long so = (long long)tile * vrs;
   const float *gam1 = sVec, *bet1 = sVec + C, *gam2 = sVec + 2 * C, *bet2 = sVec + 3 * C;
-  auto sp = [&](float* p) { return p + so; };  // this tile's slab row
   const int p4 = w & 3;
+  auto sp = [&](float* p) { return p + so; };  // this tile's slab row
   if constexpr (hf == 0) {
     cl_wgrad_block(sZm, LD, p4, sGu, LD, nullptr, nullptr, sp(gr_out.dW2), sp(gr_out.db2));
     cl_wgrad_block(sYm, LD, p4, sOt, LD, nullptr, nullptr, sp(gr_out.dWo), sp(gr_out.dbo));

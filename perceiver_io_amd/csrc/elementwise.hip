@@ -287,6 +287,46 @@ __global__ void adamw_kernel(float* __restrict__ p, float* __restrict__ g, float
   }
 }
 
+// the same update on 4 elements per thread (16-byte loads / stores; every pointer 16-byte
+// aligned, the shadow 8-byte aligned, n % 4 == 0 — checked by the launcher): a quarter of the
+// memory instructions of the scalar loop, which is issue-bound at ≈40 % of HBM bandwidth
+__global__ __launch_bounds__(256) void adamw4_kernel(float4* __restrict__ p, float4* __restrict__ g,
+                                                     float4* __restrict__ m, float4* __restrict__ v,
+                                                     uint2* __restrict__ shadow, long long n4,
+                                                     const float* __restrict__ hyper, float eps, float wd, float clip,
+                                                     float gscale, int l2, int zero_g) {
+  const float lr = hyper[0], step = hyper[1], beta1 = hyper[3], beta2 = hyper[4];
+  const float bc1 = 1.f - powf(beta1, step), bc2 = 1.f - powf(beta2, step);
+  float gs = gscale;
+  if (clip > 0.f) {
+    const float norm = sqrtf(hyper[2]) * gscale;
+    const float f = clip / (norm + 1e-6f);
+    if (f < 1.f) gs *= f;
+  }
+  const float step_size = lr / bc1;
+  const float bc2s = sqrtf(bc2);
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    const float4 p4 = p[i], g4 = g[i], m4 = m[i], v4 = v[i];
+    if (zero_g) g[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float pa[4] = {p4.x, p4.y, p4.z, p4.w}, ga[4] = {g4.x, g4.y, g4.z, g4.w};
+    const float ma[4] = {m4.x, m4.y, m4.z, m4.w}, va[4] = {v4.x, v4.y, v4.z, v4.w};
+    float po[4], mo[4], vo[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {  // the scalar kernel's arithmetic, element by element
+      float pi = pa[e];
+      const float gi = l2 ? fmaf(wd, pi, ga[e] * gs) : ga[e] * gs;
+      if (!l2) pi *= 1.f - lr * wd;
+      mo[e] = beta1 * ma[e] + (1.f - beta1) * gi;
+      vo[e] = beta2 * va[e] + (1.f - beta2) * gi * gi;
+      po[e] = pi - step_size * mo[e] / (sqrtf(vo[e]) / bc2s + eps);
+    }
+    m[i] = make_float4(mo[0], mo[1], mo[2], mo[3]);
+    v[i] = make_float4(vo[0], vo[1], vo[2], vo[3]);
+    p[i] = make_float4(po[0], po[1], po[2], po[3]);
+    if (shadow) shadow[i] = make_uint2(pack2(po[0], po[1]), pack2(po[2], po[3]));
+  }
+}
+
 __global__ void cast_bf16_kernel(const float* __restrict__ x, uint16_t* __restrict__ y, long long n) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
     y[i] = f2bf(x[i]);
@@ -416,8 +456,16 @@ void batch_sum2_launch(const float* a, const float* b, float* oa, float* ob, int
 }
 void adamw_launch(float* p, float* g, float* m, float* v, uint16_t* shadow, long long n, const float* hyper,
                   float eps, float wd, float clip, float gscale, int l2, int zero_g, hipStream_t st) {
-  hipLaunchKernelGGL(adamw_kernel, grid_for(n), dim3(256), 0, st, p, g, m, v, shadow, n, hyper, eps, wd, clip, gscale, l2,
-                     zero_g);
+  const bool vec = n % 4 == 0 && ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) |
+                                    reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v)) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(shadow) & 7) == 0;
+  if (vec)
+    hipLaunchKernelGGL(adamw4_kernel, grid_for(n / 4), dim3(256), 0, st, reinterpret_cast<float4*>(p),
+                       reinterpret_cast<float4*>(g), reinterpret_cast<float4*>(m), reinterpret_cast<float4*>(v),
+                       reinterpret_cast<uint2*>(shadow), n / 4, hyper, eps, wd, clip, gscale, l2, zero_g);
+  else
+    hipLaunchKernelGGL(adamw_kernel, grid_for(n), dim3(256), 0, st, p, g, m, v, shadow, n, hyper, eps, wd, clip, gscale,
+                       l2, zero_g);
 }
 // grad[i] += Σ_r rep[r][i], rep[r][i] ← 0 (replicated gradient accumulators, see ops/optim.py)
 __global__ void fold_replicas_kernel(float* __restrict__ grad, float* __restrict__ rep, long long n, int nrep) {
