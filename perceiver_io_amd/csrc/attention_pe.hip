@@ -751,7 +751,8 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
 // the statistics of its own key (pixels prefetched one sample ahead, PE row sums in registers) and
 // writes its row of a (wave-private LDS: the transposed products read it); the batch-invariant
 // P' fragments of S / dP and the dQ table operand stay in registers for the whole run.  Per
-// 32-key slice and sample: 19 MFMAs, one workgroup barrier (two with per-sample queries).  Same
+// 32-key slice and sample: 19 MFMAs and one workgroup barrier (per-sample queries: the wave
+// partials of dQ_b are double-buffered and summed during sample b + 1).  Same
 // run structure, outputs and partial-row layout as attn_bwd_pe_kernel.
 // ------------------------------------------------------------------------------------
 template <int NC, bool QB>
@@ -771,7 +772,9 @@ __global__ __launch_bounds__(512) void attn_bwd_pe_fact_kernel(PeBwdArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t sP[NW][32 * PPL];    // run setup: the wave's P' rows
   __shared__ __attribute__((aligned(16))) uint16_t sS[NW][32 * PLD];    // dS̃ slab [key][q]
   __shared__ __attribute__((aligned(16))) uint16_t sA[NW][33 * 16];     // [key][j]: a (j < NA), 0 (j 8..15)
-  __shared__ __attribute__((aligned(16))) float sDQb[QB ? NW : 1][QB ? 32 * 36 : 1];  // per wave: dQ_b [d][q]
+  // per-sample queries: per wave dQ_b [d][q], double-buffered (sample b's partials are summed
+  // during sample b + 1: one workgroup barrier per sample)
+  __shared__ __attribute__((aligned(16))) float sDQb[QB ? 2 : 1][QB ? NW : 1][QB ? 32 * 36 : 1];
   // epilogue aliases over the consumed tiles: dQ partials [w][q][d], column sums [w][2][seg][d]
   float(*sDQ)[32 * 33] = reinterpret_cast<float(*)[32 * 33]>(&sP[0][0]);
   float(*sCS)[2][PNSEG][32] = reinterpret_cast<float(*)[2][PNSEG][32]>(&sS[0][0]);
@@ -957,6 +960,24 @@ __global__ __launch_bounds__(512) void attn_bwd_pe_fact_kernel(PeBwdArgs a) {
     }
     lds_barrier();
 
+    // Σ over the waves of sample bb's dQ partials (threads < 256: d = t >> 3, queries 4·(t & 7) .. +3)
+    auto dq_reduce = [&](int bb) {
+      if (threadIdx.x >= 256) return;
+      const int dd = threadIdx.x >> 3, q0 = 4 * (threadIdx.x & 7);
+      const float(*src)[32 * 36] = reinterpret_cast<const float(*)[32 * 36]>(&sDQb[QB ? (bb & 1) : 0][0][0]);
+      f32x4 v = *reinterpret_cast<const f32x4*>(&src[0][dd * 36 + q0]);
+#pragma unroll
+      for (int ww = 1; ww < NW; ++ww) v += *reinterpret_cast<const f32x4*>(&src[ww][dd * 36 + q0]);
+      float* dst = a.dq + (long long)kb * a.dq_kbs + ((long long)bb * a.Nq) * C + h * PD + dd;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (q0 + e < a.Nq) {
+          if (a.dq_kbs) dst[(long long)(q0 + e) * C] = v[e] * a.scale;
+          else atomicAdd(dst + (long long)(q0 + e) * C, v[e] * a.scale);
+        }
+      }
+    };
+
     auto body = [&](int b, auto masked_t) {
       constexpr bool MK = decltype(masked_t)::value;
       const int cur = b & 1;
@@ -1000,6 +1021,9 @@ __global__ __launch_bounds__(512) void attn_bwd_pe_fact_kernel(PeBwdArgs a) {
           fetch(b + 2);
           fetch_px(b + 2, pxn);
         }
+      }
+      if constexpr (QB) {
+        if (b > b0) dq_reduce(b - 1);  // written last iteration, before its barrier
       }
       // (2) S and dP: rows = queries, lane = key
       const uint16_t* tQ = sQ[QB ? cur : 0];
@@ -1071,23 +1095,8 @@ __global__ __launch_bounds__(512) void attn_bwd_pe_fact_kernel(PeBwdArgs a) {
         // partial [d][q]: registers 4g..4g+3 are 4 consecutive queries → one 16-byte store
 #pragma unroll
         for (int g = 0; g < 4; ++g)
-          *reinterpret_cast<f32x4*>(&sDQb[w][r * 36 + 8 * g + 4 * hh]) =
+          *reinterpret_cast<f32x4*>(&sDQb[cur][w][r * 36 + 8 * g + 4 * hh]) =
               f32x4{dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]};
-        lds_barrier();
-        if (threadIdx.x < 256) {  // Σ over the waves: thread t → d = t >> 3, queries 4·(t & 7) .. +3
-          const int dd = threadIdx.x >> 3, q0 = 4 * (threadIdx.x & 7);
-          f32x4 v = *reinterpret_cast<const f32x4*>(&sDQb[0][dd * 36 + q0]);
-#pragma unroll
-          for (int ww = 1; ww < NW; ++ww) v += *reinterpret_cast<const f32x4*>(&sDQb[ww][dd * 36 + q0]);
-          float* dst = a.dq + (long long)kb * a.dq_kbs + ((long long)b * a.Nq) * C + h * PD + dd;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            if (q0 + e < a.Nq) {
-              if (a.dq_kbs) dst[(long long)(q0 + e) * C] = v[e] * a.scale;
-              else atomicAdd(dst + (long long)(q0 + e) * C, v[e] * a.scale);
-            }
-          }
-        }
       } else {
         accQ = mfma32(ts[0], frag_ks(&sP[w][0], PPL, 0, 0), accQ);
         accQ = mfma32(ts[1], frag_ks(&sP[w][0], PPL, 0, 16), accQ);
@@ -1099,6 +1108,9 @@ __global__ __launch_bounds__(512) void attn_bwd_pe_fact_kernel(PeBwdArgs a) {
       for (int b = b0; b < b1; ++b) body(b, std::true_type{});
     } else {
       for (int b = b0; b < b1; ++b) body(b, std::false_type{});
+    }
+    if constexpr (QB) {
+      if (b1 > b0) dq_reduce(b1 - 1);  // the last sample's partials (after its barrier)
     }
 
     // ---- D rows of this wave's keys (K part columns 32h + r, V part C + 32h + r)

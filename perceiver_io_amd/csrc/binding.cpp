@@ -66,7 +66,7 @@ void post_attn_ln_linear_fwd_launch(int, const uint16_t*, const float*, const ui
                                     float*, float*, float*, float*, uint16_t*, int, int, const float*, const float*,
                                     const uint16_t*, const float*, uint16_t*, float*, float*, const DropCfg&,
                                     hipStream_t);
-void sa_layer_fwd_launch(const uint16_t*, int, float, uint16_t*, float*, const float*, const uint16_t*, const float*,
+bool sa_layer_fwd_launch(const uint16_t*, int, float, uint16_t*, float*, const float*, const uint16_t*, const float*,
                          const float*, const float*, float, const uint16_t*, const float*, const uint16_t*, const float*,
                          float*, float*, float*, float*, uint16_t*, int, const float*, const float*, const uint16_t*,
                          const float*, uint16_t*, float*, float*, const DropCfg&, int, hipStream_t);
@@ -429,7 +429,8 @@ std::vector<Tensor> post_attn_ln_linear_fwd(Tensor o, Tensor x, Tensor wo, Tenso
   return {z, y, m, r, u, qkv, m1, r1};
 }
 
-// fused latent self-attention layer forward (C = 64, H = 4, N ≤ 256, N % 64 == 0, no attention
+// fused latent self-attention layer forward (C = 64, H = 4, N ≤ 512 (> 256: 16-byte aligned
+// operands, the chain kernel), N % 64 == 0, no attention
 // dropout; residual dropout allowed): qkv (R, 3C) bf16 of this layer, x (R, C) fp32 its input →
 // [o, lse, z, y, m2, r2, u] (+ [qkv, mean1, rstd1] of the next layer when lnw/lnb/wq/bq given)
 std::vector<Tensor> sa_layer_fwd(Tensor qkv, Tensor x, int64_t N, double scale, Tensor wo, Tensor bo, Tensor g2,
@@ -439,7 +440,7 @@ std::vector<Tensor> sa_layer_fwd(Tensor qkv, Tensor x, int64_t N, double scale, 
   TORCH_CHECK(qkv.is_contiguous() && x.is_contiguous(), "qkv/x must be contiguous");
   const int R = (int)x.size(0);
   TORCH_CHECK(x.size(1) == C && qkv.size(0) == R && qkv.size(1) == 3 * C, "sa_layer_fwd: C = 64, qkv (R, 192)");
-  TORCH_CHECK(N > 0 && N <= 256 && N % 64 == 0 && R % N == 0, "sa_layer_fwd: N <= 256, N % 64 == 0, R = B·N");
+  TORCH_CHECK(N > 0 && N <= 512 && N % 64 == 0 && R % N == 0, "sa_layer_fwd: N <= 512, N % 64 == 0, R = B·N");
   const bool next = wq.has_value();
   if (next)
     TORCH_CHECK(lnw.has_value() && lnb.has_value() && bq.has_value() && wq->is_contiguous() &&
@@ -455,13 +456,14 @@ std::vector<Tensor> sa_layer_fwd(Tensor qkv, Tensor x, int64_t N, double scale, 
   Tensor m = torch::empty({R}, f32), r = torch::empty({R}, f32), u = torch::empty({R, C}, b16);
   Tensor qn, m1, r1;
   if (next) { qn = torch::empty({R, nq}, b16); m1 = torch::empty({R}, f32); r1 = torch::empty({R}, f32); }
-  pio::sa_layer_fwd_launch(bfp(qkv), (int)N, (float)(scale * 1.4426950408889634), bfp_mut(o), lse.data_ptr<float>(),
+  const bool launched = pio::sa_layer_fwd_launch(bfp(qkv), (int)N, (float)(scale * 1.4426950408889634), bfp_mut(o), lse.data_ptr<float>(),
                            f32p(x), bfp(wo), f32p(bo), f32p(g2), f32p(be2), (float)eps, bfp(w1), f32p(b1), bfp(w2),
                            f32p(b2), z.data_ptr<float>(), y.data_ptr<float>(), m.data_ptr<float>(), r.data_ptr<float>(),
                            bfp_mut(u), R, next ? f32p(*lnw) : nullptr, next ? f32p(*lnb) : nullptr,
                            next ? bfp(*wq) : nullptr, next ? f32p(*bq) : nullptr, next ? bfp_mut(qn) : nullptr,
                            next ? m1.data_ptr<float>() : nullptr, next ? r1.data_ptr<float>() : nullptr,
                            make_drop(seed, site, p), nq, stream());
+  TORCH_CHECK(launched, "sa_layer_fwd: N > 256 needs the chain kernel (16-byte aligned operands)");
   if (next) return {o, lse, z, y, m, r, u, qn, m1, r1};
   return {o, lse, z, y, m, r, u};
 }

@@ -171,7 +171,9 @@ __device__ __forceinline__ void cl2_store_bf16(uint16_t* __restrict__ Y, int ld,
 // The fused latent self-attention layer forward on 8 waves (same operands and results as
 // sa_layer_fwd_chain_kernel).  Attention: wave w = (head w & 3, 32-query block w >> 2).  The
 // post-attention chain: the paired CL2 layout above (5 pair exchanges: LN2, W1, W2, LN1, Wq).
-template <bool NEXT, int NQ>
+// MAXKT: 32-key tiles of the K / V operand (8: N ≤ 256, 16: N ≤ 512 — the long-context MLM's
+// 512 latents; every K fragment is loaded in phase 0, the V rows of the batch element live in LDS).
+template <bool NEXT, int NQ, int MAXKT>
 __global__ __launch_bounds__(512) void sa_layer_fwd_chain8_kernel(
     const uint16_t* __restrict__ QKV, int N, float scale_log2, uint16_t* __restrict__ Oout, float* __restrict__ LSE,
     const float* __restrict__ X, const uint16_t* __restrict__ Wo, const float* __restrict__ bo,
@@ -181,11 +183,13 @@ __global__ __launch_bounds__(512) void sa_layer_fwd_chain8_kernel(
     const float* __restrict__ lnw, const float* __restrict__ lnb, const uint16_t* __restrict__ Wq,
     const float* __restrict__ bq, uint16_t* __restrict__ QKVn, float* __restrict__ mean1, float* __restrict__ rstd1,
     DropCfg dr) {
-  constexpr int C = 64, H = 4, D = 16, LD = C + 8, LDV = C + 8, C3 = 3 * C, MAXKT = 8, NT = 512;
+  constexpr int C = 64, H = 4, D = 16, LD = C + 8, LDV = C + 8, C3 = 3 * C, NT = 512;
+  constexpr int NVI = MAXKT * 32 * 8 / NT;  // 16-byte V chunks per thread
+  static_assert(MAXKT % 4 == 0 && MAXKT * 32 * 8 % NT == 0, "key tiles");
   constexpr int nq = NQ * C, NWR = 3 * C + (NEXT ? nq : 0);  // weight rows staged: Wo, W1, W2 (+ Wq)
   constexpr int NWC = NWR * 8 / NT;                           // 16-byte weight chunks per thread
   static_assert(NWR * 8 % NT == 0, "weight staging");
-  __shared__ __attribute__((aligned(16))) uint16_t sV[256 * LDV + 64];  // V rows of the batch element (+ overrun)
+  __shared__ __attribute__((aligned(16))) uint16_t sV[MAXKT * 32 * LDV + 64];  // V rows of the batch element (+ overrun)
   __shared__ __attribute__((aligned(16))) uint16_t sO[64 * LD];
   __shared__ __attribute__((aligned(16))) uint16_t sW[NWR * LD];        // Wo | W1 | W2 | Wq
   __shared__ __attribute__((aligned(16))) float sVec[7 * C + (NEXT ? nq : 0)];  // bo b1 b2 γ2 β2 γ1 β1 | bq
@@ -208,13 +212,13 @@ __global__ __launch_bounds__(512) void sa_layer_fwd_chain8_kernel(
 
   // ---- phase 0: every load issued, branch-free (address selects) ----
   PIO_TS(0);
-  bf16x8 kf[MAXKT], qf, vr[4], wr[NWC];
+  bf16x8 kf[MAXKT], qf, vr[NVI], wr[NWC];
 #pragma unroll
   for (int kt = 0; kt < MAXKT; ++kt)
     kf[kt] = *reinterpret_cast<const bf16x8*>(kt < nkt ? QKV + (rb + 32 * kt + r) * C3 + C + h * D + 8 * hh : zp);
   qf = *reinterpret_cast<const bf16x8*>(QKV + (long long)(m0 + 32 * qb + r) * C3 + h * D + 8 * hh);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NVI; ++i) {
     const int c = threadIdx.x + NT * i, key = c >> 3, col = (c & 7) * 8;
     vr[i] = *reinterpret_cast<const bf16x8*>(key < N ? QKV + (rb + key) * C3 + 2 * C + col : zp);
   }
@@ -246,7 +250,7 @@ __global__ __launch_bounds__(512) void sa_layer_fwd_chain8_kernel(
   float pq = 0.f;
   if constexpr (NEXT) pq = bq[(int)threadIdx.x < nq ? threadIdx.x : 0];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NVI; ++i) {
     const int c = threadIdx.x + NT * i, key = c >> 3, col = (c & 7) * 8;
     *reinterpret_cast<bf16x8*>(sV + key * LDV + col) = vr[i];
   }
@@ -851,20 +855,28 @@ bool sa_layer_fwd_chain_launch(const uint16_t* QKV, int N, float scale_log2, uin
                                float* rstd1, const DropCfg& dr, int nq, hipStream_t st) {
   const bool next = Wq != nullptr;
   if (next && nq != 64 && nq != 128 && nq != 192) return false;
+  if (N > 512) return false;
   dim3 grid(R / 64);
-#define SAC(NX, NQ)                                                                                                 \
-  hipLaunchKernelGGL((sa_layer_fwd_chain8_kernel<NX, NQ>), grid, dim3(512), 0, st, QKV, N, scale_log2, O, LSE, X, Wo, bo, \
-                     g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, lnw, lnb, Wq, bq, QKVn, mean1,      \
+#define SAC(NX, NQ, KT)                                                                                                 \
+  hipLaunchKernelGGL((sa_layer_fwd_chain8_kernel<NX, NQ, KT>), grid, dim3(512), 0, st, QKV, N, scale_log2, O, LSE, X, Wo, \
+                     bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, lnw, lnb, Wq, bq, QKVn, mean1,  \
                      rstd1, dr)
-  if (!next) {
-    SAC(false, 3);
-  } else if (nq == 64) {
-    SAC(true, 1);
-  } else if (nq == 128) {
-    SAC(true, 2);
-  } else {
-    SAC(true, 3);
+#define SAK(KT)              \
+  if (!next) {               \
+    SAC(false, 3, KT);       \
+  } else if (nq == 64) {     \
+    SAC(true, 1, KT);        \
+  } else if (nq == 128) {    \
+    SAC(true, 2, KT);        \
+  } else {                   \
+    SAC(true, 3, KT);        \
   }
+  if (N <= 256) {
+    SAK(8)
+  } else {
+    SAK(16)
+  }
+#undef SAK
 #undef SAC
   return true;
 }

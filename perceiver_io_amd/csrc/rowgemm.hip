@@ -1556,7 +1556,8 @@ void post_attn_ln_linear_fwd_launch(int C, const uint16_t* O, const float* X, co
 }
 
 // fused self-attention layer forward (C = 64, H = 4): see sa_layer_fwd_kernel; NEXT = Wq != nullptr
-void sa_layer_fwd_launch(const uint16_t* QKV, int N, float scale_log2, uint16_t* O, float* LSE, const float* X,
+// false (nothing launched) for N > 256 when the chain kernel cannot take the operands
+bool sa_layer_fwd_launch(const uint16_t* QKV, int N, float scale_log2, uint16_t* O, float* LSE, const float* X,
                          const uint16_t* Wo, const float* bo, const float* g2, const float* be2, float eps,
                          const uint16_t* W1, const float* b1, const uint16_t* W2, const float* b2, float* Z,
                          float* Ysave, float* mean2, float* rstd2, uint16_t* Usave, int R, const float* lnw,
@@ -1568,7 +1569,8 @@ void sa_layer_fwd_launch(const uint16_t* QKV, int N, float scale_log2, uint16_t*
   if (av && use_chain() &&
       sa_layer_fwd_chain_launch(QKV, N, scale_log2, O, LSE, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2,
                                 rstd2, Usave, R, lnw, lnb, Wq, bq, QKVn, mean1, rstd1, dr, nq, st))
-    return;
+    return true;
+  if (N > 256) return false;  // the 4-wave kernel holds at most 256 keys
 #define SAL(NX, A)                                                                                                 \
   if (nq == 64) hipLaunchKernelGGL((sa_layer_fwd_kernel<NX, A, 1>), grid, dim3(256), 0, st, QKV, N, scale_log2, O, LSE, X, \
                                    Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, lnw, lnb, Wq, bq, \
@@ -1585,6 +1587,7 @@ void sa_layer_fwd_launch(const uint16_t* QKV, int N, float scale_log2, uint16_t*
     if (av) SAL(false, true); else SAL(false, false);
   }
 #undef SAL
+  return true;
 }
 
 void post_attn_bwd_launch(int C, const float* dZ, const float* Ysave, const float* mean2, const float* rstd2,

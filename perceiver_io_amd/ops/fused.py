@@ -812,8 +812,9 @@ class _SABlockFn(torch.autograd.Function):
             qkv, mean1, rstd1 = K.ln_linear_fwd(xl, P[0][0], P[0][1], EPS, bws[0][0], P[0][3], 0, None, True, True)
         saved = []
         # one fused launch per layer (attention + post-attention + next LN1/QKV) for the
-        # C = 64, H = 4 latent stacks without attention dropout (sa_layer_fwd_kernel)
-        fused_layer = SA_LAYER_FUSED and C == 64 and H == 4 and N <= 256 and N % 64 == 0 and pdrop == 0.0
+        # C = 64, H = 4 latent stacks without attention dropout (csrc/chain.hip
+        # sa_layer_fwd_chain8_kernel: up to 512 latents)
+        fused_layer = SA_LAYER_FUSED and C == 64 and H == 4 and N <= 512 and N % 64 == 0 and pdrop == 0.0
         for i in range(L):
             p = P[i]
             _, _, wo, w1, w2 = bws[i]

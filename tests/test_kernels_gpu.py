@@ -902,11 +902,13 @@ def test_ln_linear_post_attn_bwd_isolated(nq, p, R):
     assert not bad, errs
 
 
-@pytest.mark.parametrize("B,N,nq,p", [(4, 256, 64, 0.0), (2, 128, 128, 0.1), (3, 64, 192, 0.1), (2, 256, 0, 0.1)])
+@pytest.mark.parametrize("B,N,nq,p", [(4, 256, 64, 0.0), (2, 128, 128, 0.1), (3, 64, 192, 0.1), (2, 256, 0, 0.1),
+                                     (2, 512, 192, 0.0), (3, 320, 0, 0.1)])
 def test_sa_layer_fwd_widths_and_dropout(B, N, nq, p):
     """The fused self-attention layer forward for every next-projection width the encoder uses
     (a cross layer's query projection C, a decoder's K/V 2C, the next layer's QKV 3C; 0 = last
-    layer) with residual dropout, per output within 1 % relative Frobenius error."""
+    layer) with residual dropout, per output within 1 % relative Frobenius error; N up to the
+    long-context MLM's 512 latents (16 key tiles)."""
     torch.manual_seed(13)
     C, R = 64, B * N
     qkv = bf(torch.randn(R, 3 * C, device=DEV))
