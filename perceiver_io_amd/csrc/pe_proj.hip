@@ -314,16 +314,22 @@ __global__ __launch_bounds__(256) void pe_weight_prep_kernel(const float* __rest
 // W / dW are split in two row blocks (the separate K and V projection weights, rows [0, Ch) and
 // [Ch, O)).  Every gradient element has exactly one writer: deterministic.
 // ------------------------------------------------------------------------------------
-constexpr int TN_MAXT = 9;  // ≤ 4 × 9 = 36 output 32 × 32 tiles per workgroup (Kp ≤ 288 with 128 columns)
+// LDS row stride (bf16) of the transposed-read tiles: ≡ 32 (mod 128), i.e. 16 (mod 64) dwords, so the
+// 8-byte pieces of ds_read_b64_tr_b16 (4 rows × 4 pieces per 16-lane group, two groups 16 columns
+// apart per pass) land on 64 distinct banks
+__host__ __device__ constexpr int tn_ld(int x) { return x + ((32 - x) % 128 + 128) % 128; }
 
 // grid (row splits, column groups): workgroup (s, c) accumulates output columns [c·on, c·on + on)
-// over rows [s·rps, (s+1)·rps) in 32-row chunks (register prefetch one chunk ahead, double-
-// buffered LDS), and stores its (Kp × on) partial into slab[s]
+// over rows [s·rps, (s+1)·rps) in 32-row chunks — two chunks of loads in flight (two register
+// sets, the loop unrolled by two), double-buffered LDS, one barrier per chunk — and stores its
+// (Kp × on) partial into slab[s].  MAXT: output 32 × 32 tiles per wave (⌈(Kp/32)·(on/32) / 4⌉),
+// NE / ND: 16-byte E pieces / float4 D pieces per thread and chunk (⌈Kp / 64⌉, ⌈on / 32⌉).
+template <int MAXT, int NE, int ND>
 __global__ __launch_bounds__(256) void pe_gemm_tn_kernel(const uint16_t* __restrict__ E, const float* __restrict__ D,
                                                          float* __restrict__ slab, int M, int Kp, int O, int on,
                                                          int rows_per_split) {
   extern __shared__ __attribute__((aligned(16))) uint16_t tsm[];
-  const int LDE = Kp + 8, LDD = on + 8;
+  const int LDE = tn_ld(Kp), LDD = tn_ld(on);
   uint16_t* sE[2] = {tsm, tsm + 32 * LDE};
   uint16_t* sD[2] = {tsm + 64 * LDE, tsm + 64 * LDE + 32 * LDD};
   const int w = wave_id(), l = lane_id(), hh = l >> 5;
@@ -331,54 +337,51 @@ __global__ __launch_bounds__(256) void pe_gemm_tn_kernel(const uint16_t* __restr
   const int c0 = blockIdx.y * on;
   const int ntj = on / 32, ntiles = (Kp / 32) * ntj;
   const int ce = Kp / 8, cd = on / 4;  // 16-byte pieces per E row, float4 per D row slice
-  bf16x8 re[6];  // 32 × Kp/8 ≤ 1536 pieces (Kp ≤ 384)
-  float4 rd[8];  // 32 × on/4 ≤ 2048 (on ≤ 256)
-  // branch-free: rows past the split (or the matrix) read zeros, so the prefetch of the chunk
-  // after the last one is harmless and every fetch is straight-line code (see kZero32B)
-  auto fetch = [&](int r0) {
+  struct Regs {
+    bf16x8 e[NE];
+    float4 d[ND];
+  } ra, rb;
+  // branch-free: rows past the split (or the matrix) read zeros, so a prefetch past the last
+  // chunk is harmless and every fetch is straight-line code (see kZero32B)
+  auto fetch = [&](Regs& R, int r0) {
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
+    for (int i = 0; i < NE; ++i) {
       const int c = threadIdx.x + 256 * i, row = c / ce, col = (c % ce) * 8;
       const bool ok = (c < 32 * ce) & (r0 + row < r_end);
       const uint16_t* p = ok ? E + (long long)(r0 + row) * Kp + col : reinterpret_cast<const uint16_t*>(kZero32B);
-      re[i] = *reinterpret_cast<const bf16x8*>(p);
+      R.e[i] = *reinterpret_cast<const bf16x8*>(p);
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < ND; ++i) {
       const int c = threadIdx.x + 256 * i, row = c / cd, col = (c % cd) * 4;
       const bool ok = (c < 32 * cd) & (r0 + row < r_end);
       const float* p = ok ? D + (long long)(r0 + row) * O + c0 + col : kZero32B;
-      rd[i] = *reinterpret_cast<const float4*>(p);
+      R.d[i] = *reinterpret_cast<const float4*>(p);
     }
   };
-  auto stash = [&](int buf) {
+  auto stash = [&](const Regs& R, int buf) {
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
+    for (int i = 0; i < NE; ++i) {
       const int c = threadIdx.x + 256 * i, row = c / ce, col = (c % ce) * 8;
-      if (c < 32 * ce) *reinterpret_cast<bf16x8*>(sE[buf] + row * LDE + col) = re[i];
+      if (c < 32 * ce) *reinterpret_cast<bf16x8*>(sE[buf] + row * LDE + col) = R.e[i];
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < ND; ++i) {
       const int c = threadIdx.x + 256 * i, row = c / cd, col = (c % cd) * 4;
       if (c < 32 * cd) {
         uint2 pk;
-        pk.x = pack2(rd[i].x, rd[i].y);
-        pk.y = pack2(rd[i].z, rd[i].w);
+        pk.x = pack2(R.d[i].x, R.d[i].y);
+        pk.y = pack2(R.d[i].z, R.d[i].w);
         *reinterpret_cast<uint2*>(sD[buf] + row * LDD + col) = pk;
       }
     }
   };
-  f32x16 acc[TN_MAXT];
+  f32x16 acc[MAXT];
 #pragma unroll
-  for (int t = 0; t < TN_MAXT; ++t) acc[t] = f32x16{};
-  fetch(r_begin);
-  int buf = 0;
-  for (int r0 = r_begin; r0 < r_end; r0 += 32, buf ^= 1) {
-    stash(buf);
-    lds_sync();
-    fetch(r0 + 32);
+  for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
+  auto compute = [&](int buf) {
 #pragma unroll
-    for (int t = 0; t < TN_MAXT; ++t) {
+    for (int t = 0; t < MAXT; ++t) {
       const int tile = w + 4 * t;
       if (tile < ntiles) {  // wave-uniform
         const int ti = tile / ntj, tj = tile % ntj;
@@ -387,11 +390,23 @@ __global__ __launch_bounds__(256) void pe_gemm_tn_kernel(const uint16_t* __restr
           acc[t] = mfma32(frag_ks(sE[buf], LDE, 32 * ti, ks), frag_ks(sD[buf], LDD, 32 * tj, ks), acc[t]);
       }
     }
+  };
+  fetch(ra, r_begin);
+  fetch(rb, r_begin + 32);
+  for (int r0 = r_begin; r0 < r_end; r0 += 64) {
+    stash(ra, 0);
+    lds_sync();
+    fetch(ra, r0 + 64);
+    compute(0);
+    stash(rb, 1);
+    lds_sync();
+    fetch(rb, r0 + 96);
+    compute(1);  // an odd last chunk: zero rows
   }
   // accumulator: col = lane & 31 → o, row = acc_row → k
   float* out = slab + (long long)blockIdx.x * Kp * O + c0;
 #pragma unroll
-  for (int t = 0; t < TN_MAXT; ++t) {
+  for (int t = 0; t < MAXT; ++t) {
     const int tile = w + 4 * t;
     if (tile < ntiles) {
       const int ti = tile / ntj, tj = tile % ntj;
@@ -470,8 +485,8 @@ __global__ __launch_bounds__(256) void pe_grad_finalize_kernel(const float* __re
 }
 
 int pe_grad_splits(int M) {
-  const int s = (M + 511) / 512;  // ≈ 512 rows (16 chunks) per workgroup, ≤ 96 slab rows
-  return s < 1 ? 1 : (s > 96 ? 96 : s);
+  const int s = (M + 383) / 384;  // ≈ 384 rows (12 chunks) per workgroup, ≤ 128 slab rows
+  return s < 1 ? 1 : (s > 128 ? 128 : s);
 }
 
 void pe_grads_launch(const uint16_t* E, const float* D, int M, int Kp, int O, const float* part, int nblk, float* slab,
@@ -481,15 +496,22 @@ void pe_grads_launch(const uint16_t* E, const float* D, int M, int Kp, int O, co
   const int rps = ((M + S0 - 1) / S0 + 31) / 32 * 32;
   const int S = (M + rps - 1) / rps;
   const int on = O % 128 == 0 ? 128 : O;  // output columns per workgroup
-  const size_t lds = (size_t)2 * 32 * ((Kp + 8) + (on + 8)) * sizeof(uint16_t);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pe_gemm_tn_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
+  const size_t lds = (size_t)2 * 32 * (tn_ld(Kp) + tn_ld(on)) * sizeof(uint16_t);
+  const int tiles = (Kp / 32) * (on / 32), ne = (Kp + 63) / 64, nd = (on + 31) / 32;
+  const dim3 grid((unsigned)S, (unsigned)(O / on));
+#define TNL(MT, NE_, ND_)                                                                                      \
+  {                                                                                                          \
+    static bool attr = false;                                                                                \
+    if (!attr) {                                                                                             \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pe_gemm_tn_kernel<MT, NE_, ND_>),              \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                     \
+      attr = true;                                                                                           \
+    }                                                                                                        \
+    hipLaunchKernelGGL((pe_gemm_tn_kernel<MT, NE_, ND_>), grid, dim3(256), lds, st, E, D, slab, M, Kp, O, on, rps); \
   }
-  hipLaunchKernelGGL(pe_gemm_tn_kernel, dim3((unsigned)S, (unsigned)(O / on)), dim3(256), lds, st, E, D, slab, M, Kp, O,
-                     on, rps);
+  if (tiles <= 20 && ne <= 3 && nd <= 4) TNL(5, 3, 4)  // the ImageNet shape: Kp = 160, 128 columns
+  else TNL(9, 6, 8)
+#undef TNL
   const long long KO4 = (long long)Kp * O / 4, W4 = (long long)(2 + nc) * O / 4;
   hipLaunchKernelGGL(pe_grad_reduce_kernel, dim3((unsigned)((KO4 + W4 + 63) / 64)), dim3(256), 0, st, slab, S, KO4, part,
                      nblk, W4, Graw, tot);
