@@ -52,57 +52,12 @@ constexpr int PNSEG = 8;        // weight rows of the column-sum MFMA: 1, Î¼Â·rÏ
 // ---- implicit K/V (SURVEY K-03/K-05: the encoder's K/V are never materialised) -------------
 // K/V row m of sample b, column o (K: o < C, V: C â‰¤ o < 2C), from the factored projection:
 //     y = rÏƒÂ·P'[m, o] + Î£_c xÌ‚_cÂ·wpg[c, o] + Î¼rÏƒÂ·(Î£_c wpg[c, o] âˆ’ gw[o]) + bw[o]
-// with P' = (EâŠ™Î³_e)Â·W_eáµ€ the batch-independent PE part (bf16, one GEMM per step) and xÌ‚_c =
-// (p_c âˆ’ Î¼)Â·rÏƒ the normalised pixel channels.  Both attention directions generate their K/V
-// tiles with THESE two functions from the same operands, so forward and backward see identical
-// bits.  Per key: PE_NST statistics {rÏƒ, Î¼rÏƒ, xÌ‚_0..xÌ‚_3}; per column: the table rows
-// wt = {wpg_0..wpg_3, Î£wpg âˆ’ gw, bw} (pe_weight_prep_kernel).
-constexpr int PE_NST = 6;
+// with P' = (EâŠ™Î³_e)Â·W_eáµ€ the batch-independent PE part (bf16, one GEMM per step), xÌ‚_c =
+// (p_c âˆ’ Î¼)Â·rÏƒ the normalised pixel channels and the per-column table rows
+// wt = {wpg_0..wpg_3, Î£wpg âˆ’ gw, bw} (pe_weight_prep_kernel).  Neither direction forms these rows:
+// both factor the products over P' plus a per-sample augmentation (attn_fwd_pe_fact_kernel,
+// attn_bwd_pe_fact_kernel); ops/emulation.py pe_kv materialises them for the reference.
 constexpr int PE_NWT = 6;
-
-__device__ __forceinline__ void pe_key_stats(float pes, float pesq, const float (&px)[PMAXC], int nc, float inv_k,
-                                             float eps, float (&st)[PE_NST]) {
-  float s = pes, sq = pesq;
-#pragma unroll
-  for (int c = 0; c < PMAXC; ++c)
-    if (c < nc) {
-      s += px[c];
-      sq += px[c] * px[c];
-    }
-  const float mu = s * inv_k;
-  const float rs = rsqrtf(fmaxf(sq * inv_k - mu * mu, 0.f) + eps);
-  st[0] = rs;
-  st[1] = mu * rs;
-#pragma unroll
-  for (int c = 0; c < PMAXC; ++c) st[2 + c] = c < nc ? (px[c] - mu) * rs : 0.f;
-}
-
-__device__ __forceinline__ float pe_kv_elem(float p, const float (&st)[PE_NST], const float (&wt)[PE_NWT]) {
-  float y = fmaf(st[1], wt[4], wt[5]);
-#pragma unroll
-  for (int c = 0; c < PMAXC; ++c) y = fmaf(st[2 + c], wt[c], y);
-  return fmaf(st[0], p, y);
-}
-
-// 8 consecutive columns of one key row â†’ bf16x8 (w: the columns' table rows, w[j][e])
-__device__ __forceinline__ bf16x8 pe_kv_row8(const bf16x8& p8, const float (&st)[PE_NST],
-                                             const float (&w)[PE_NWT][8]) {
-  bf16x8 out;
-#pragma unroll
-  for (int e = 0; e < 8; e += 2) {
-    float wa[PE_NWT], wb[PE_NWT];
-#pragma unroll
-    for (int j = 0; j < PE_NWT; ++j) {
-      wa[j] = w[j][e];
-      wb[j] = w[j][e + 1];
-    }
-    const uint32_t pk = pack2(pe_kv_elem(bf2f(p8[e]), st, wa), pe_kv_elem(bf2f(p8[e + 1]), st, wb));
-    out[e] = (short)(pk & 0xFFFF);
-    out[e + 1] = (short)(pk >> 16);
-  }
-  return out;
-}
-
 
 // ------------------------------------------------------------------------------------
 // Encoder cross-attention forward over implicit K/V (head dim 32, Nq â‰¤ 32, no mask, no
@@ -118,8 +73,7 @@ __device__ __forceinline__ bf16x8 pe_kv_row8(const bf16x8& p8, const float (&st)
 // augmentation carries the per-sample terms, rÏƒ_mÂ·scale and log2 rÏƒ_m (â†’ pÌƒ straight out of
 // the exponential) are folded into the score's one FMA, and the PÌƒáµ€ product runs against the
 // shared P'_V tile plus a per-sample augmentation tile [p âˆ’ Î¼ | Î¼ | 1/rÏƒ] whose row NC + 1 is
-// the softmax denominator l.  Per key and sample: no K/V generation (â‰ˆ400 VALU ops per key and
-// head in the generating kernel); per score element one FMA (scale, rÏƒ and log2 rÏƒ), the max
+// the softmax denominator l.  Per key and sample: no K/V row is formed; per score element one FMA (scale, rÏƒ and log2 rÏƒ), the max
 // and the exponential; the accumulators are rescaled only when a lazy softmax offset moves.  The P' chunk (32 keys Ã— the
 // head's 64 K|V columns) is staged ONCE per workgroup in LDS (one 16-byte load per thread,
 // double-buffered, one barrier per chunk) and serves 4Â·NS samples: wave w owns samples
@@ -335,7 +289,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pe_fact_kernel(PeFwdArgs a) {
   }
 }
 
-template <int NW, bool QB, bool IMPL>
+template <int NW, bool QB>
 __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
   constexpr int KB = 32 * NW, NTH = 64 * NW;
   constexpr int KVLD = 2 * PD + 8;  // K|V row stride of the per-wave K/V tile
@@ -347,16 +301,13 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
   __shared__ __attribute__((aligned(16))) float sL[2][32], sDl[2][32];
   __shared__ __attribute__((aligned(16))) float sRs[2][KB];                 // rÏƒ per key
   __shared__ __attribute__((aligned(16))) uint16_t sW[2][PNSEG * WLD];      // [seg][key] bf16 weights
-  // per wave: [key][K | V] â€” double-buffered staging of loaded rows, or (IMPL) one tile generated
-  // at the top of each iteration
-  __shared__ __attribute__((aligned(16))) uint16_t sKV[IMPL ? 1 : 2][NW][32 * KVLD];
+  // per wave: [key][K | V] â€” double-buffered staging of the loaded rows
+  __shared__ __attribute__((aligned(16))) uint16_t sKV[2][NW][32 * KVLD];
   __shared__ __attribute__((aligned(16))) uint16_t sS[NW][32 * PLD];        // per wave: dS slab [key][q]
-  __shared__ __attribute__((aligned(16))) float sX[IMPL ? 2 : 1][IMPL ? PE_NST : 1][KB];  // key statistics
-  __shared__ __attribute__((aligned(16))) float sWt[IMPL ? PE_NWT : 1][64];               // head h's table columns
   // epilogue aliases over the consumed tiles: dQ partials [w][q][d], column sums [w][2][seg][d]
   float(*sDQ)[32 * 33] = reinterpret_cast<float(*)[32 * 33]>(&sKV[0][0][0]);
   float(*sCS)[2][PNSEG][32] =
-      reinterpret_cast<float(*)[2][PNSEG][32]>(IMPL ? &sS[0][0] : &sKV[IMPL ? 0 : 1][0][0]);
+      reinterpret_cast<float(*)[2][PNSEG][32]>(&sKV[1][0][0]);
   static_assert(sizeof(float) * NW * 32 * 33 <= sizeof(uint16_t) * NW * 32 * KVLD, "dQ partial alias");
   static_assert(sizeof(float) * NW * 2 * PNSEG * 32 <= sizeof(uint16_t) * NW * 32 * PLD, "column-sum alias");
 
@@ -415,11 +366,10 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
   // clamped addresses (a branch around a load, or arithmetic on a loaded value, makes hipcc wait
   // for every outstanding load at that point); stage() masks, transforms and writes LDS one
   // iteration later.
-  bf16x8 kv8[IMPL ? 1 : 4];  // this lane's 4 chunks of its wave's 32 K|V rows: rows (l >> 3) + 8j, 8 columns
+  bf16x8 kv8[4];  // this lane's 4 chunks of its wave's 32 K|V rows: rows (l >> 3) + 8j, 8 columns
   bf16x8 qd;       // a 16-byte chunk of the Q (threads < 128, QB) / dO (threads 128..255) tile
   float ld = 0.f;  // LSE / delta (threads 256..319)
   float smu = 0.f, srs = 0.f, spx[PMAXC];  // raw statistics + pixels of key kbase + threadIdx.x
-  float spe = 0.f, spq = 0.f;              // IMPL: PE row sums of that key (batch-invariant)
   const int qrow = min((int)(threadIdx.x & 127) >> 2, a.Nq - 1), qcol = (threadIdx.x & 3) * 8;
   const int lrow_i = min((int)(threadIdx.x & 31), a.Nq - 1);
   const int skey = min(kbase + (int)(threadIdx.x % KB), a.M - 1);
@@ -427,12 +377,10 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
   const int kvsrc = kvcol < PD ? h * PD + kvcol : C + h * PD + kvcol - PD;
   auto fetch = [&](int b) {
     const long long rb = (long long)b * a.M;
-    if constexpr (!IMPL) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = min(kbase + 32 * w + (l >> 3) + 8 * j, a.M - 1);
-        kv8[j] = *reinterpret_cast<const bf16x8*>(a.kv + (rb + row) * a.kv_rs + kvsrc);
-      }
+    for (int j = 0; j < 4; ++j) {
+      const int row = min(kbase + 32 * w + (l >> 3) + 8 * j, a.M - 1);
+      kv8[j] = *reinterpret_cast<const bf16x8*>(a.kv + (rb + row) * a.kv_rs + kvsrc);
     }
     if (threadIdx.x < 256) {
       if (QB && threadIdx.x < 128)
@@ -440,10 +388,8 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
       else
         qd = *reinterpret_cast<const bf16x8*>(a.dO + ((long long)b * a.Nq + qrow) * C + h * PD + qcol);
       const long long rr = rb + skey;
-      if constexpr (!IMPL) {
-        smu = a.mean[rr];
-        srs = a.rstd[rr];
-      }
+      smu = a.mean[rr];
+      srs = a.rstd[rr];
 #pragma unroll
       for (int c = 0; c < PMAXC; ++c) spx[c] = a.pix[rr * nc + min(c, nc - 1)];
     } else if (threadIdx.x < 320) {
@@ -452,7 +398,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
     }
   };
   auto stage = [&](int buf) {
-    if constexpr (!IMPL) {
+    {
       uint16_t* t = sKV[buf][w];
 #pragma unroll
       for (int j = 0; j < 4; ++j) *reinterpret_cast<bf16x8*>(t + ((l >> 3) + 8 * j) * KVLD + kvcol) = kv8[j];
@@ -466,17 +412,11 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
       }
       const int k = threadIdx.x;
       const bool ok = kbase + k < a.M;
-      float st[PE_NST];  // rÏƒ, Î¼rÏƒ, xÌ‚_c
-      if constexpr (IMPL) {
-        pe_key_stats(spe, spq, spx, nc, a.inv_k, a.eps, st);
+      float st[2 + PMAXC];  // rÏƒ, Î¼rÏƒ, xÌ‚_c
+      st[0] = srs;
+      st[1] = smu * srs;
 #pragma unroll
-        for (int j = 0; j < PE_NST; ++j) sX[buf][j][k] = st[j];
-      } else {
-        st[0] = srs;
-        st[1] = smu * srs;
-#pragma unroll
-        for (int c = 0; c < PMAXC; ++c) st[2 + c] = c < nc ? (spx[c] - smu) * srs : 0.f;
-      }
+      for (int c = 0; c < PMAXC; ++c) st[2 + c] = c < nc ? (spx[c] - smu) * srs : 0.f;
       sRs[buf][k] = ok ? st[0] : 0.f;
       uint16_t* wcol = sW[buf] + k;
       wcol[0] = f2bf(ok ? 1.f : 0.f);
@@ -510,26 +450,6 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
     if ((c >> 2) >= a.Nq) v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
     *reinterpret_cast<bf16x8*>(sQb[0] + (c >> 2) * PLD + (c & 3) * 8) = v;
   }
-  // IMPL: this lane's P' rows for the tile generation (batch-invariant: loaded once) â€” keys
-  // 32w + gk + i, columns gc..gc+7 of the wave's [K | V] tile â€” and the head's table columns
-  const int gk = 4 * (l & 7), gc = 8 * (l >> 3);
-  bf16x8 pc[IMPL ? 4 : 1];
-  if constexpr (IMPL) {
-    const int pcol = gc < PD ? h * PD + gc : C + h * PD + gc - PD;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int key = min(kbase + 32 * w + gk + i, a.M - 1);
-      pc[i] = *reinterpret_cast<const bf16x8*>(a.P + (long long)key * O + pcol);
-    }
-    if (threadIdx.x < 64 * PE_NWT) {
-      const int j = threadIdx.x >> 6, c = threadIdx.x & 63;
-      sWt[j][c] = a.wt[(long long)j * O + (c < PD ? h * PD + c : C + h * PD + c - PD)];
-    }
-    if (threadIdx.x < 256) {
-      spe = a.pes[skey];
-      spq = a.pesq[skey];
-    }
-  }
   if (b0 < b1) {
     fetch(b0);
     stage(b0 & 1);
@@ -539,30 +459,6 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
 
   for (int b = b0; b < b1; ++b) {
     const int cur = b & 1;
-    if constexpr (IMPL) {
-      // (0) element b's K/V tile from its key statistics (staged last iteration) and P'
-      uint16_t* t = sKV[0][w];
-      float wr[PE_NWT][8];
-#pragma unroll
-      for (int j = 0; j < PE_NWT; ++j) {
-        const float4 w0 = *reinterpret_cast<const float4*>(&sWt[j][gc]);
-        const float4 w1 = *reinterpret_cast<const float4*>(&sWt[j][gc + 4]);
-        wr[j][0] = w0.x; wr[j][1] = w0.y; wr[j][2] = w0.z; wr[j][3] = w0.w;
-        wr[j][4] = w1.x; wr[j][5] = w1.y; wr[j][6] = w1.z; wr[j][7] = w1.w;
-      }
-      float4 s4[PE_NST];
-#pragma unroll
-      for (int j = 0; j < PE_NST; ++j) s4[j] = *reinterpret_cast<const float4*>(&sX[cur][j][32 * w + gk]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float sk[PE_NST];
-#pragma unroll
-        for (int j = 0; j < PE_NST; ++j) sk[j] = i == 0 ? s4[j].x : i == 1 ? s4[j].y : i == 2 ? s4[j].z : s4[j].w;
-        *reinterpret_cast<bf16x8*>(t + (gk + i) * KVLD + gc) = pe_kv_row8(pc[i], sk, wr);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
-    }
     // (1) element b+1 â†’ LDS (its loads were issued one iteration ago), loads of b+2
     if (b + 1 < b1) {
       stage(cur ^ 1);
@@ -572,7 +468,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_pe_kernel(PeBwdArgs a) {
     // B[k = d][col = key] straight from this wave's LDS rows
     const uint16_t* tdO = sdO[cur];
     const uint16_t* sQ = sQb[QB ? cur : 0];
-    const uint16_t* tKV = sKV[IMPL ? 0 : cur][w];
+    const uint16_t* tKV = sKV[cur][w];
     f32x16 S = f32x16{}, dP = f32x16{};
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -1226,8 +1122,8 @@ void attn_bwd_pe_launch(const PeBwdArgs& a0, int nkb, int bsplit, hipStream_t st
     }
 #undef PIO_PEBF
   } else {
-    if (a.q_bs == 0) hipLaunchKernelGGL((attn_bwd_pe_kernel<NW, false, false>), grid, dim3(64 * NW), 0, st, a);
-    else hipLaunchKernelGGL((attn_bwd_pe_kernel<NW, true, false>), grid, dim3(64 * NW), 0, st, a);
+    if (a.q_bs == 0) hipLaunchKernelGGL((attn_bwd_pe_kernel<NW, false>), grid, dim3(64 * NW), 0, st, a);
+    else hipLaunchKernelGGL((attn_bwd_pe_kernel<NW, true>), grid, dim3(64 * NW), 0, st, a);
   }
   if (a.nbg > 0)
     hipLaunchKernelGGL(attn_pe_side_add_kernel, dim3((unsigned)a.nslots), dim3(256), 0, st, a.Dside, a.side_pair, a.D, a.M,

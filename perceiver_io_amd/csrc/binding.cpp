@@ -1252,8 +1252,8 @@ std::vector<Tensor> pe_proj_bwd(Tensor dy, Tensor pix, Tensor mean, Tensor rstd,
 // (attention_pe.hip): queries (1 | B, Nq ≤ 32, ·), head dim 32, no key mask, no dropout.
 // Writes dq (zeroed here) — (Nq, C) summed over the batch for broadcast queries, else (B, Nq, C)
 // — and D (M, 2C), part (nkb·bsplit, (2 + nc)·2C), both added onto when accumulate.
-// implicit K/V (impl != null): kv / mean / rstd are absent and K/V are generated from P' (M, 2C)
-// bf16, the PE row sums pes / pesq (M) and the generation table wt (6, 2C) of pe_weight_prep
+// implicit K/V (impl != null): kv / mean / rstd are absent; the factored kernel works from P' (M, 2C)
+// bf16, the PE row sums pes / pesq (M) and the per-column table wt (6, 2C) of pe_weight_prep
 struct PeImplicit { Tensor P, pes, pesq, wt; double kin, eps; };
 
 // persistent mode of the PE attention backward (attention_pe.hip): one workgroup per CU over

@@ -334,9 +334,9 @@ def _pe_proj_fwd(K, pix, pe, g, b, W, bias):
 
 
 # implicit K/V for the encoder cross-attention over [pixels ‖ Fourier PE] (csrc/attention_pe.hip):
-# the attention kernels generate each K/V tile from the bf16 PE product P' = Ebf·(W⊙γ)ᵀ, the
-# sample's pixels and a per-column table, so the (B·M, 2C) K/V tensor (0.8 GB at ImageNet shape)
-# is never written or read.  PE_IMPLICIT = False selects the materialised factored path (tests).
+# both attention directions factor their products over the bf16 PE product P' = Ebf·(W⊙γ)ᵀ plus a
+# per-sample augmentation from the sample's pixels and a per-column table, so the (B·M, 2C) K/V
+# tensor (0.8 GB at ImageNet shape) is never written or read, nor any K/V tile formed.  PE_IMPLICIT = False selects the materialised factored path (tests).
 PE_IMPLICIT = True
 
 
