@@ -72,13 +72,53 @@ def parse(argv=None):
     ap.add_argument("--dense", action="store_true", help="lartpc: evaluate all pixels (the reference's cost)")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--profile-stacks", type=int, default=0,
-                    help="with --profile-steps: group copy/fill ops by N Python stack frames (finds stray copies)")
+                    help="with --profile-steps: list the framework (aten) ops that touch device tensors in the "
+                         "profiled steps with N Python stack frames each (finds stray copies / fills)")
     a = ap.parse_args(argv)
     cfg = CONFIGS[a.config]
     for k in ("batch", "seq_len", "latents", "channels"):
         if getattr(a, k) is None:
             setattr(a, k, cfg[k])
     return a
+
+
+def _aten_stacks(engine, data, steps, depth):
+    """Every aten op that touches a device tensor during `steps` eager steps, grouped by op and
+    the innermost `depth` Python frames (a dispatch-mode hook: sees the ops issued from C++
+    extension code and from the autograd threads too)."""
+    import collections
+    import traceback
+
+    import torch
+    from torch.utils._python_dispatch import TorchDispatchMode
+    from torch.utils._pytree import tree_flatten
+
+    quiet = ("aten::view", "aten::_unsafe_view", "aten::slice", "aten::as_strided", "aten::empty", "aten::empty_strided",
+             "aten::detach", "aten::alias", "aten::t", "aten::transpose", "aten::permute", "aten::expand",
+             "aten::select", "aten::unsqueeze", "aten::squeeze", "aten::reshape", "aten::_reshape_alias",
+             "aten::lift_fresh", "aten::set_", "aten::resize_", "aten::split", "aten::unbind", "aten::chunk",
+             "aten::narrow", "aten::diagonal", "aten::new_empty", "aten::new_empty_strided", "aten::is_nonzero")
+    seen = collections.Counter()
+
+    class _Rec(TorchDispatchMode):
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            out = func(*args, **(kwargs or {}))
+            name = func._schema.name
+            if name not in quiet:
+                flat, _ = tree_flatten((args, kwargs or {}))
+                if any(isinstance(t, torch.Tensor) and t.device.type == "cuda" for t in flat):
+                    frames = traceback.extract_stack()[:-1][-depth:]
+                    seen[(str(func), tuple(f"{f.filename.split('/repo/')[-1]}:{f.lineno} {f.name}" for f in frames))] += 1
+            return out
+
+    with _Rec():
+        for i in range(steps):
+            engine.step(data[i % 4])
+        torch.cuda.synchronize()
+    for (op, frames), n in seen.most_common(60):
+        print(f"{op} x{n}", file=sys.stderr)
+        for fr in frames:
+            print(f"    {fr}", file=sys.stderr)
 
 
 def _opt(lr=3e-3, wd=0.0):
@@ -336,22 +376,14 @@ def main(argv=None):
     if args.profile_steps and cuda:
         from torch.profiler import ProfilerActivity, profile
 
-        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA],
-                     with_stack=args.profile_stacks > 0) as prof:
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
             for i in range(args.profile_steps):
                 engine.step(data[i % 4])
             torch.cuda.synchronize()
         if info.is_main:
             print(prof.key_averages().table(sort_by="cuda_time_total", row_limit=40), file=sys.stderr)
-            if args.profile_stacks:
-                keep = ("aten::copy_", "aten::fill_", "aten::zero_", "aten::sum", "aten::clone", "aten::add", "aten::add_",
-                        "aten::mul", "aten::ge", "aten::to", "aten::_to_copy")
-                rows = [e for e in prof.key_averages(group_by_stack_n=args.profile_stacks) if e.key in keep]
-                rows.sort(key=lambda e: -e.count)
-                for e in rows[:40]:
-                    print(f"{e.key} x{e.count} dev_us={e.device_time_total:.0f}", file=sys.stderr)
-                    for fr in e.stack[:args.profile_stacks]:
-                        print(f"    {fr}", file=sys.stderr)
+        if args.profile_stacks and info.is_main:
+            _aten_stacks(engine, data, args.profile_steps, args.profile_stacks)
     B = args.batch
     ms = dt / args.steps * 1e3
     value = B * world * args.steps / dt

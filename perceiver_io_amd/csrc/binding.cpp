@@ -123,15 +123,15 @@ struct PeGradTargets { float *dWa, *dWb, *db, *dg, *dbeta; };
 int pe_grad_splits(int);
 void pe_grads_launch(const uint16_t*, const float*, int, int, int, const float*, int, float*, float*, float*,
                      const float*, const float*, const float*, const float*, int, int, int, PeGradTargets, hipStream_t);
-void pe_weight_prep_launch(const float*, const float*, const float*, const float*, int, int, int, int, uint16_t*, float*,
-                           float*, float*, float*, hipStream_t);
+void pe_weight_prep_launch(const float*, const float*, int, const float*, const float*, const float*, int, int, int, int,
+                           uint16_t*, float*, float*, float*, float*, hipStream_t);
 int pixel_ce_blocks(long long);
 void pixel_ce_fwd_launch(int, int, const float*, const float*, const float*, const int64_t*, const float*, long long,
                          float*, float*, float*, hipStream_t);
 void pixel_ce_bwd_launch(int, int, const float*, const float*, const float*, const int64_t*, const float*,
                          const float*, const float*, long long, float*, float*, float*, float*, hipStream_t);
 void adamw_launch(float*, float*, float*, float*, uint16_t*, long long, const float*, float, float, float, float,
-                  int, int, hipStream_t);
+                  int, int, const float*, float*, int, hipStream_t);
 void cast_bf16_launch(const float*, uint16_t*, long long, hipStream_t);
 void reduce_probe_launch(const float*, float*, hipStream_t);
 void fold_replicas_launch(float*, float*, long long, int, hipStream_t);
@@ -1095,14 +1095,22 @@ void pixel_ce_bwd(Tensor h, Tensor w, Tensor b, Tensor labels, Tensor wts, Tenso
 }
 
 void adamw(Tensor p, Tensor g, Tensor m, Tensor v, OptT shadow, Tensor hyper, double eps, double wd, double clip,
-           double gscale, bool l2, bool zero_grad) {
+           double gscale, bool l2, bool zero_grad, OptT loss_src, OptT loss_ring) {
   TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && m.is_contiguous() && v.is_contiguous());
   TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel());
   uint16_t* sp = nullptr;
   if (shadow.has_value()) { TORCH_CHECK(shadow->numel() == p.numel()); sp = reinterpret_cast<uint16_t*>(shadow->data_ptr()); }
+  TORCH_CHECK(loss_src.has_value() == loss_ring.has_value(), "adamw: loss_src and loss_ring go together");
+  if (loss_src.has_value()) {
+    CHECK_DT(*loss_src, torch::kFloat32); CHECK_DT(*loss_ring, torch::kFloat32);
+    TORCH_CHECK(loss_src->numel() == 1 && loss_ring->is_contiguous() && loss_ring->numel() >= 1 && hyper.numel() >= 8,
+                "adamw: scalar loss_src, contiguous loss_ring, hyper[7] = ring slot");
+  }
   pio::adamw_launch(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), sp, p.numel(),
                     f32p(hyper), (float)eps, (float)wd, (float)clip, (float)gscale, l2 ? 1 : 0, zero_grad ? 1 : 0,
-                    stream());
+                    loss_src.has_value() ? f32p(*loss_src) : nullptr,
+                    loss_ring.has_value() ? loss_ring->data_ptr<float>() : nullptr,
+                    loss_ring.has_value() ? (int)loss_ring->numel() : 1, stream());
 }
 
 // self-test of the device cross-lane reductions: (6, 64) = wave_sum, wave_max, half_sum,
@@ -1207,14 +1215,20 @@ void pe_grads(Tensor D, Tensor part, Tensor E, Tensor Wa, Tensor Wb, Tensor g, T
                        Wb.data_ptr<float>(), g.data_ptr<float>(), b.data_ptr<float>(), Ch, kin, (int)nc, tg, stream());
 }
 
-// W (O, kin) fp32, γ/β (kin), bias (O) → [Wg (O, Kp) bf16 = W⊙γ on columns [nc, kin) else 0,
+// W (O, kin) fp32 — or the row blocks W (O1, kin) and W2 (O − O1, kin) of a separate K / V pair,
+// never concatenated — γ/β (kin), bias (O) → [Wg (O, Kp) bf16 = W⊙γ on columns [nc, kin) else 0,
 // wpg (nc, O) = (W⊙γ)[:, :nc]ᵀ, gw (O) = W·γ, bw (O) = W·β + bias]
-std::vector<Tensor> pe_weight_prep(Tensor W, Tensor g, Tensor b, Tensor bias, int64_t nc, int64_t Kp) {
+std::vector<Tensor> pe_weight_prep(Tensor W, Tensor g, Tensor b, Tensor bias, int64_t nc, int64_t Kp, OptT W2) {
   for (const Tensor* t : {&W, &g, &b, &bias}) {
     CHECK_CUDA(*t); CHECK_DT(*t, torch::kFloat32);
     TORCH_CHECK(t->is_contiguous(), "pe_weight_prep: contiguous operands");
   }
-  const int O = (int)W.size(0), kin = (int)W.size(1);
+  const int O1 = (int)W.size(0), kin = (int)W.size(1);
+  if (W2.has_value()) {
+    CHECK_CUDA(*W2); CHECK_DT(*W2, torch::kFloat32);
+    TORCH_CHECK(W2->is_contiguous() && W2->dim() == 2 && W2->size(1) == kin, "pe_weight_prep: W2 (O2, kin) contiguous");
+  }
+  const int O = O1 + (W2.has_value() ? (int)W2->size(0) : 0);
   TORCH_CHECK(g.numel() == kin && b.numel() == kin && bias.numel() == O && nc >= 1 && nc < kin && Kp >= kin,
               "pe_weight_prep: shapes");
   auto f32 = W.options();
@@ -1222,7 +1236,8 @@ std::vector<Tensor> pe_weight_prep(Tensor W, Tensor g, Tensor b, Tensor bias, in
   Tensor wpg = torch::empty({nc, O}, f32), gw = torch::empty({O}, f32), bw = torch::empty({O}, f32);
   Tensor wt = torch::empty({6, O}, f32);  // implicit-K/V generation table (attention_pe.hip)
   TORCH_CHECK(nc <= 4, "pe_weight_prep: at most 4 pixel channels");
-  pio::pe_weight_prep_launch(W.data_ptr<float>(), g.data_ptr<float>(), b.data_ptr<float>(), bias.data_ptr<float>(), O,
+  pio::pe_weight_prep_launch(W.data_ptr<float>(), W2.has_value() ? W2->data_ptr<float>() : nullptr, O1,
+                             g.data_ptr<float>(), b.data_ptr<float>(), bias.data_ptr<float>(), O,
                              (int)nc, kin, (int)Kp, bfp_mut(Wg), wpg.data_ptr<float>(), gw.data_ptr<float>(),
                              bw.data_ptr<float>(), wt.data_ptr<float>(), stream());
   return {Wg, wpg, gw, bw, wt};
@@ -1501,7 +1516,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sumsq", &sumsq);
   m.def("adamw", &adamw, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("shadow"), py::arg("hyper"),
         py::arg("eps"), py::arg("wd"), py::arg("clip"), py::arg("gscale"), py::arg("l2") = false,
-        py::arg("zero_grad") = false);
+        py::arg("zero_grad") = false, py::arg("loss_src") = py::none(), py::arg("loss_ring") = py::none());
   m.def("cast_bf16", &cast_bf16);
   m.def("reduce_probe", &reduce_probe);
   m.def("fold_replicas", &fold_replicas);
@@ -1514,7 +1529,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("wt"), py::arg("dO"), py::arg("lse"), py::arg("delta"), py::arg("pix"), py::arg("dq"), py::arg("D"),
         py::arg("part"), py::arg("H"), py::arg("scale"), py::arg("kin"), py::arg("eps"), py::arg("accumulate"),
         py::arg("bsplit"), py::arg("dq_zeroed") = false);
-  m.def("pe_weight_prep", &pe_weight_prep);
+  m.def("pe_weight_prep", &pe_weight_prep, py::arg("W"), py::arg("g"), py::arg("b"), py::arg("bias"), py::arg("nc"),
+        py::arg("Kp"), py::arg("W2") = py::none());
   m.def("pe_grads", &pe_grads);
   m.def("pe_proj_bwd", &pe_proj_bwd);
   m.def("attn_bwd_pe", &attn_bwd_pe, py::arg("q"), py::arg("kv"), py::arg("dO"), py::arg("lse"), py::arg("delta"),

@@ -249,15 +249,19 @@ __global__ void sumsq_kernel(const float* __restrict__ g, long long n, float* __
 }
 
 // hyper[0] = lr, [1] = step (already incremented), [2] = grad sum of squares (if clip > 0),
-// [3] = beta1, [4] = beta2 — read from device memory so schedulers can change them between
-// replays of a captured step.
+// [3] = beta1, [4] = beta2, [7] = loss-ring slot — read from device memory so schedulers can
+// change them between replays of a captured step.
+// loss_src (optional): the step's scalar loss, copied by thread 0 into loss_ring[hyper[7] % ring_n]
+// (the step engine hands that slot back as the step's loss: no separate copy launch per step)
 // zero_g: the gradient is cleared as it is consumed (a replayed step then needs no separate
 // zero fill of the flat gradient buffer before its backward)
 __global__ void adamw_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                              float* __restrict__ v, uint16_t* __restrict__ shadow, long long n,
                              const float* __restrict__ hyper, float eps, float wd, float clip, float gscale,
-                             int l2, int zero_g) {
+                             int l2, int zero_g, const float* __restrict__ loss_src, float* __restrict__ loss_ring,
+                             int ring_n) {
   const float lr = hyper[0], step = hyper[1], beta1 = hyper[3], beta2 = hyper[4];
+  if (loss_src != nullptr && blockIdx.x == 0 && threadIdx.x == 0) loss_ring[(int)hyper[7] % ring_n] = *loss_src;
   const float bc1 = 1.f - powf(beta1, step), bc2 = 1.f - powf(beta2, step);
   // g holds the all-reduced SUM over ranks (gscale = 1 / world makes it the mean): the clip
   // threshold applies to the norm of the MEAN gradient, as in single-process training
@@ -294,8 +298,10 @@ __global__ __launch_bounds__(256) void adamw4_kernel(float4* __restrict__ p, flo
                                                      float4* __restrict__ m, float4* __restrict__ v,
                                                      uint2* __restrict__ shadow, long long n4,
                                                      const float* __restrict__ hyper, float eps, float wd, float clip,
-                                                     float gscale, int l2, int zero_g) {
+                                                     float gscale, int l2, int zero_g, const float* __restrict__ loss_src,
+                                                     float* __restrict__ loss_ring, int ring_n) {
   const float lr = hyper[0], step = hyper[1], beta1 = hyper[3], beta2 = hyper[4];
+  if (loss_src != nullptr && blockIdx.x == 0 && threadIdx.x == 0) loss_ring[(int)hyper[7] % ring_n] = *loss_src;
   const float bc1 = 1.f - powf(beta1, step), bc2 = 1.f - powf(beta2, step);
   float gs = gscale;
   if (clip > 0.f) {
@@ -455,17 +461,19 @@ void batch_sum2_launch(const float* a, const float* b, float* oa, float* ob, int
                      nb4, acc_b);
 }
 void adamw_launch(float* p, float* g, float* m, float* v, uint16_t* shadow, long long n, const float* hyper,
-                  float eps, float wd, float clip, float gscale, int l2, int zero_g, hipStream_t st) {
+                  float eps, float wd, float clip, float gscale, int l2, int zero_g, const float* loss_src,
+                  float* loss_ring, int ring_n, hipStream_t st) {
   const bool vec = n % 4 == 0 && ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) |
                                     reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v)) & 15) == 0 &&
                    (reinterpret_cast<uintptr_t>(shadow) & 7) == 0;
   if (vec)
     hipLaunchKernelGGL(adamw4_kernel, grid_for(n / 4), dim3(256), 0, st, reinterpret_cast<float4*>(p),
                        reinterpret_cast<float4*>(g), reinterpret_cast<float4*>(m), reinterpret_cast<float4*>(v),
-                       reinterpret_cast<uint2*>(shadow), n / 4, hyper, eps, wd, clip, gscale, l2, zero_g);
+                       reinterpret_cast<uint2*>(shadow), n / 4, hyper, eps, wd, clip, gscale, l2, zero_g, loss_src,
+                       loss_ring, ring_n);
   else
     hipLaunchKernelGGL(adamw_kernel, grid_for(n), dim3(256), 0, st, p, g, m, v, shadow, n, hyper, eps, wd, clip, gscale,
-                       l2, zero_g);
+                       l2, zero_g, loss_src, loss_ring, ring_n);
 }
 // grad[i] += Σ_r rep[r][i], rep[r][i] ← 0 (replicated gradient accumulators, see ops/optim.py)
 __global__ void fold_replicas_kernel(float* __restrict__ grad, float* __restrict__ rep, long long n, int nrep) {

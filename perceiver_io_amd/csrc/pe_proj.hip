@@ -263,18 +263,21 @@ __global__ __launch_bounds__(256) void pe_gemm_kernel(const uint16_t* __restrict
 //   wpg[c, o] = W[o, c]·γ[c] (c < nc), gw[o] = Σ_k W[o, k]γ[k], bw[o] = Σ_k W[o, k]β[k] + bias[o]
 // and (wt non-null) the implicit-K/V generation table of attention_pe.hip, wt (PE_NWT, O):
 //   rows c < 4: wpg[c, o] (0 for c ≥ nc),  row 4: Σ_c wpg[c, o] − gw[o],  row 5: bw[o]
-__global__ __launch_bounds__(256) void pe_weight_prep_kernel(const float* __restrict__ W, const float* __restrict__ g,
+// W2 (optional): rows [O1, O) come from W2 (the V projection weight of a separate K / V pair)
+__global__ __launch_bounds__(256) void pe_weight_prep_kernel(const float* __restrict__ W, const float* __restrict__ W2,
+                                                             int O1, const float* __restrict__ g,
                                                              const float* __restrict__ b, const float* __restrict__ bias,
                                                              int O, int nc, int kin, int Kp, uint16_t* __restrict__ Wg,
                                                              float* __restrict__ wpg, float* __restrict__ gw,
                                                              float* __restrict__ bw, float* __restrict__ wt) {
   __shared__ float red[2][4];
   const int o = blockIdx.x;
+  const float* Wr = W2 != nullptr && o >= O1 ? W2 + (long long)(o - O1) * kin : W + (long long)o * kin;
   float sg = 0.f, sb = 0.f;
   for (int k = threadIdx.x; k < Kp; k += blockDim.x) {
     float wgk = 0.f;
     if (k < kin) {
-      const float wv = W[(long long)o * kin + k];
+      const float wv = Wr[k];
       wgk = wv * g[k];
       sg += wgk;
       sb += wv * b[k];
@@ -294,7 +297,7 @@ __global__ __launch_bounds__(256) void pe_weight_prep_kernel(const float* __rest
     if (wt) {
       float ps = 0.f;
       for (int c = 0; c < 4; ++c) {
-        const float v = c < nc ? W[(long long)o * kin + c] * g[c] : 0.f;  // = wpg[c, o]
+        const float v = c < nc ? Wr[c] * g[c] : 0.f;  // = wpg[c, o]
         wt[(long long)c * O + o] = v;
         ps += v;
       }
@@ -526,10 +529,11 @@ void pe_gemm_launch(const uint16_t* A, const uint16_t* Bw, void* C, bool bf16_ou
   if (bf16_out) hipLaunchKernelGGL(pe_gemm_kernel<true>, grid, dim3(256), 0, st, A, Bw, C, M, N, K, Mst);
   else hipLaunchKernelGGL(pe_gemm_kernel<false>, grid, dim3(256), 0, st, A, Bw, C, M, N, K, Mst);
 }
-void pe_weight_prep_launch(const float* W, const float* g, const float* b, const float* bias, int O, int nc, int kin,
-                           int Kp, uint16_t* Wg, float* wpg, float* gw, float* bw, float* wt, hipStream_t st) {
-  hipLaunchKernelGGL(pe_weight_prep_kernel, dim3((unsigned)O), dim3(256), 0, st, W, g, b, bias, O, nc, kin, Kp, Wg, wpg,
-                     gw, bw, wt);
+void pe_weight_prep_launch(const float* W, const float* W2, int O1, const float* g, const float* b, const float* bias,
+                           int O, int nc, int kin, int Kp, uint16_t* Wg, float* wpg, float* gw, float* bw, float* wt,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(pe_weight_prep_kernel, dim3((unsigned)O), dim3(256), 0, st, W, W2, O1, g, b, bias, O, nc, kin, Kp, Wg,
+                     wpg, gw, bw, wt);
 }
 
 void pe_proj_fwd_launch(const float* pix, int nc, const float* P, const float* pes, const float* pesq,

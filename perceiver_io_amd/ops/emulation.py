@@ -116,7 +116,9 @@ def pe_gemm(A, B, bf16_out=False, pad_rows=0):
     return y.to(torch.bfloat16) if bf16_out else y
 
 
-def pe_weight_prep(W, g, b, bias, nc, Kp):
+def pe_weight_prep(W, g, b, bias, nc, Kp, W2=None):
+    if W2 is not None:  # separate K / V weights (the kernel reads the two row blocks in place)
+        W = torch.cat([W, W2], 0)
     O, kin = W.shape
     wg = W * g[None, :]
     Wg = torch.zeros((O, Kp), device=W.device, dtype=torch.float32)
@@ -606,8 +608,10 @@ def sumsq(g, out):
     out += (g.float() ** 2).sum()
 
 
-def adamw(p, g, m, v, shadow, hyper, eps, wd, clip, gscale, l2=False, zero_grad=False):
+def adamw(p, g, m, v, shadow, hyper, eps, wd, clip, gscale, l2=False, zero_grad=False, loss_src=None, loss_ring=None):
     lr, step, b1, b2 = float(hyper[0]), float(hyper[1]), float(hyper[3]), float(hyper[4])
+    if loss_src is not None:  # the step's loss into the engine's ring slot hyper[7]
+        loss_ring.view(-1)[int(float(hyper[7])) % loss_ring.numel()] = loss_src.reshape(())
     gs = gscale
     if clip > 0:
         norm = math.sqrt(float(hyper[2])) * gscale  # norm of the mean (all-reduced sum × 1/world)

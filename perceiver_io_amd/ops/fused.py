@@ -344,15 +344,18 @@ PE_PAD_ROWS = 64  # zero rows after P' (the forward kernel's last prefetch reads
 
 
 def _pe_implicit_operands(K, nc, pe, g, b, W, bias):
-    """(P' (M, 2C) bf16, Σe, Σe², generation table (6, 2C), Kin) of one K/V projection."""
+    """(P' (M, 2C) bf16, Σe, Σe², column table (6, 2C), Kin) of one K/V projection; W = (W_k, W_v)
+    (read in place by the weight prep kernel) or the stacked (2C, Kin) weight."""
     kin = g.shape[0]
     ebf, pes, pesq = _pe_table(pe, nc, kin)
-    if W.shape[0] % 128 == 0 and hasattr(K, "pe_gemm"):
-        wg, _, _, _, wt = K.pe_weight_prep(W.contiguous(), g.contiguous(), b.contiguous(), bias.contiguous(), nc,
-                                           ebf.shape[1])
+    Wk, Wv = W if isinstance(W, tuple) else (W, None)
+    O = Wk.shape[0] + (0 if Wv is None else Wv.shape[0])
+    if O % 128 == 0 and hasattr(K, "pe_gemm"):
+        wg, _, _, _, wt = K.pe_weight_prep(Wk.contiguous(), g.contiguous(), b.contiguous(), bias.contiguous(), nc,
+                                           ebf.shape[1], None if Wv is None else Wv.contiguous())
         P = K.pe_gemm(ebf, wg, bf16_out=True, pad_rows=PE_PAD_ROWS)
     else:
-        wg, _, _, _, wt = emulation.pe_weight_prep(W, g, b, bias, nc, ebf.shape[1])
+        wg, _, _, _, wt = emulation.pe_weight_prep(Wk, g, b, bias, nc, ebf.shape[1], Wv)
         P = emulation.pe_gemm(ebf, wg, bf16_out=True, pad_rows=PE_PAD_ROWS)
     return P, pes, pesq, wt, kin
 
@@ -450,8 +453,7 @@ class _LayerFn(torch.autograd.Function):
                             and p_attn == 0.0 and hasattr(K, "attn_fwd_pe"))
                 imp = None
                 if implicit:
-                    imp = _pe_implicit_operands(K, xkv2.shape[1], src.pe, g_kv, b_kv, torch.cat([ps[5], ps[6]], 0),
-                                                bin_[C:])
+                    imp = _pe_implicit_operands(K, xkv2.shape[1], src.pe, g_kv, b_kv, (ps[5], ps[6]), bin_[C:])
                     kv = mean_kv = rstd_kv = None
                 elif factored:
                     kv, mean_kv, rstd_kv = _pe_proj_fwd(K, xkv2, src.pe, g_kv, b_kv,

@@ -182,13 +182,18 @@ class FusedAdamW(torch.optim.Optimizer):
         # is updated by range_update right after its all-reduce lands, on the reducer's side
         # stream, so device_update has nothing left to do
         self.bucket_mode = False
+        # set by the step engine around a captured update: the kernel also copies the step's
+        # loss (loss_out[0]) into loss_out[1][hyper[7]] (see StepEngine's loss ring)
+        self.loss_out = None
+        self.loss_slot = 0
 
     # -- the update ---------------------------------------------------------------------
     def hyper_values(self):
-        """lr / step / betas of the NEXT update, in ``self.hyper``'s layout."""
+        """lr / step / betas of the NEXT update (and the step engine's loss-ring slot), in
+        ``self.hyper``'s layout."""
         g = self.param_groups[0]
         b1, b2 = g["betas"]
-        return [float(g["lr"]), float(self._step + 1), 0.0, float(b1), float(b2), 0.0, 0.0, 0.0]
+        return [float(g["lr"]), float(self._step + 1), 0.0, float(b1), float(b2), 0.0, 0.0, float(self.loss_slot)]
 
     def stage_hyper(self):
         """Write lr / step / betas for the NEXT update into device memory (outside any graph)."""
@@ -233,9 +238,11 @@ class FusedAdamW(torch.optim.Optimizer):
             else:
                 self.hyper[2:3].zero_()
                 K.sumsq(self.flat.grad, self.hyper[2:3])
+        lo = self.loss_out
         K.adamw(self.flat.data, self.flat.grad, self.exp_avg, self.exp_avg_sq, self.flat.shadow, self.hyper,
                 g["eps"], g["weight_decay"], self.max_grad_norm, self.grad_scale, l2=self.l2,
-                zero_grad=zero_grad and self.flat.grad_rep is None)
+                zero_grad=zero_grad and self.flat.grad_rep is None,
+                loss_src=None if lo is None else lo[0], loss_ring=None if lo is None else lo[1])
 
     @torch.no_grad()
     def step(self, closure=None, staged: bool = False):

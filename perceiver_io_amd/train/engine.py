@@ -99,14 +99,20 @@ def shape_key(obj):
     return ("V", obj)
 
 
+# replayed steps return their loss as a slot of a device ring written by the captured update
+# kernel: a returned loss stays valid for this many steps (no per-step copy launch)
+LOSS_RING = 1024
+
+
 class _Captured:
     """One captured step: the graph, its static input batch and its static outputs."""
 
-    __slots__ = ("graph", "batch", "loss", "state", "seed_grad")
+    __slots__ = ("graph", "batch", "loss", "state", "seed_grad", "ring")
 
-    def __init__(self, graph, batch, loss, state, seed_grad=None):
+    def __init__(self, graph, batch, loss, state, seed_grad=None, ring=False):
         self.graph, self.batch, self.loss, self.state = graph, batch, loss, state
         self.seed_grad = seed_grad  # read by the captured backward: kept alive with the graph
+        self.ring = ring  # the captured update copies the loss into the engine's loss ring
 
 
 class ClosureGraph:
@@ -170,6 +176,8 @@ class StepEngine:
         self.state_hooks = state_hooks
         self._graphs: "OrderedDict[tuple, _Captured]" = OrderedDict()
         self.captures = 0  # graphs captured so far (evictions included)
+        self._loss_ring = None  # (LOSS_RING,) fp32: the returned per-step losses of replayed steps
+        self._ring_pos = 0
         self.replays = 0
         self._eager_steps = 0
         # every step (eager warmups, capture, replays) runs on ONE dedicated stream: autograd's
@@ -256,6 +264,11 @@ class StepEngine:
         one = torch.full((), 1.0 / self.accumulate, device=self.device)
         in_graph = last and self._opt_in_graph
         zero_inside = last and self.accumulate == 1 and not self._self_zeroing
+        # the step's loss leaves through the update kernel (a slot of a device ring, chosen per
+        # replay by the staged hyper-parameters) instead of a copy launch after every replay
+        ring = in_graph and not opt.bucket_mode
+        if ring and self._loss_ring is None:
+            self._loss_ring = torch.zeros(LOSS_RING, device=self.device)
 
         def body():
             if zero_inside:
@@ -269,7 +282,11 @@ class StepEngine:
             if in_graph:
                 if ddp:
                     red.finish()
+                if ring:
+                    lv = loss.detach()
+                    opt.loss_out = (lv if lv.dtype == torch.float32 else lv.float(), self._loss_ring)
                 opt.device_update(zero_grad=self._self_zeroing)
+                opt.loss_out = None
             return loss
 
         if self.graph_impl == "closure":
@@ -284,7 +301,7 @@ class StepEngine:
                 red.disarm()
         state = self.state_hooks[0]() if self.state_hooks is not None else None
         self.captures += 1
-        return _Captured(g, static, loss, state, one)
+        return _Captured(g, static, loss, state, one, ring=ring)
 
     def _graph_for(self, batch, kind: str = "last") -> _Captured:
         """The captured step for this batch's shape (captured on first sight, LRU-cached)."""
@@ -358,6 +375,8 @@ class StepEngine:
                 if self.state_hooks is not None:
                     self.state_hooks[1](ent.state)
                 # batch copies (+ the optimizer's hyper-parameters before the update graph): one launch
+                if last and ent.ring:
+                    self.opt.loss_slot = self._ring_pos
                 self._stage(ent, b, last and self._opt_in_graph)
                 ent.graph.replay()
                 self.replays += 1
@@ -370,6 +389,10 @@ class StepEngine:
                 self.opt.step(staged=self.bucket_update)
             if self.sched is not None:
                 self.sched.step()
+            if ents[-1].ring:  # valid for the next LOSS_RING - 1 steps
+                out = self._loss_ring[self._ring_pos]
+                self._ring_pos = (self._ring_pos + 1) % LOSS_RING
+                return out
             return ents[-1].loss.detach().clone()
         if self.graph_enabled:
             self._eager_steps += 1

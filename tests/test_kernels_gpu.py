@@ -751,6 +751,10 @@ def test_pe_gemm_and_weight_prep(M, N, K):
     r2 = _emu().pe_weight_prep(W, g, b, bias, nc, K)
     for x, y, n in zip(r1, r2, ("Wg", "wpg", "gw", "bw", "wt")):
         close(x, y, 1e-5, n)
+    # separate K / V weights read in place (no concatenation): bitwise the stacked call
+    r3 = _ext().pe_weight_prep(W[: N // 2].contiguous(), g, b, bias, nc, K, W[N // 2:].contiguous())
+    for x, y, n in zip(r3, r1, ("Wg", "wpg", "gw", "bw", "wt")):
+        assert torch.equal(x, y), n
 
 
 @pytest.mark.parametrize("M,O,Kp,kin,nc,nblk", [(50176, 256, 288, 261, 3, 37), (784, 256, 160, 131, 1, 5),
