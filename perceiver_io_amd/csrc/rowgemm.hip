@@ -896,6 +896,13 @@ __device__ __forceinline__ void wgrad_tile(const uint16_t* sG, int ldg, const ui
 // U, O and (C ≤ 64) all weights at once; the rest of the kernel touches global memory only
 // to store results and to add parameter gradients.
 // ------------------------------------------------------------------------------------
+// which of the nparts workgroups sharing a tile stores output group g (0: dW2, 1: dW1, 2: dWo,
+// 3: the row outputs, the vector and LayerNorm gradients); the QKV weight chunks of the fused
+// boundary kernel go round-robin (chunk j → part j mod nparts)
+__host__ __device__ constexpr int tile_part_owner(int g, int nparts) {
+  return nparts == 1 ? 0 : nparts == 2 ? (g == 0 || g == 3 ? 0 : 1) : (g == 0 ? 0 : g == 1 ? 1 : g == 2 ? 2 : 3);
+}
+
 // LDS bytes of post_attn_bwd_body: sG, sX, sW[NWB], sF, sPart, sDb1, sP
 template <int C>
 constexpr int post_attn_bwd_smem() {
@@ -910,9 +917,16 @@ __device__ __forceinline__ void post_attn_bwd_body(
     const float* __restrict__ rstd2, const uint16_t* __restrict__ U, const uint16_t* __restrict__ O,
     const uint16_t* __restrict__ Wo, const uint16_t* __restrict__ W1, const uint16_t* __restrict__ W2,
     const float* __restrict__ g2, const float* __restrict__ be2, float* __restrict__ dY, uint16_t* __restrict__ dO,
-    float* __restrict__ delta, int H, PostAttnGrads gr_out, int R, const DropCfg& dr, unsigned char* smem) {
+    float* __restrict__ delta, int H, PostAttnGrads gr_out, int R, const DropCfg& dr, unsigned char* smem,
+    int part = 0, int nparts = 1) {
   // residual dropout: the MLP output layer sees dZ∘m₁, the out-projection dY∘m₀; the residual
-  // gradients (dZ into dY, dY out of the kernel) stay unmasked
+  // gradients (dZ into dY, dY out of the kernel) stay unmasked.
+  // nparts > 1: that many workgroups share the tile (small row counts: more workgroups on the
+  // chip); all run the whole row chain, each stores its share of the outputs (tile_part_owner) —
+  // every output and gradient element keeps exactly one writer
+  const bool own_w2 = tile_part_owner(0, nparts) == part, own_w1 = tile_part_owner(1, nparts) == part;
+  const bool own_wo = tile_part_owner(2, nparts) == part, own_rows = tile_part_owner(3, nparts) == part;
+
   constexpr int LD = C + 8, LDF = C + 4, MAXT = (2 * C / 32 + 3) / 4, MAXW = ((C / 32) * (C / 32) + 3) / 4;
   constexpr int NCH = C / 32, NWB = C <= 64 ? 3 : 1, NIW = (C * C / 8 + 255) / 256;
   uint16_t* sG = reinterpret_cast<uint16_t*>(smem);  // [64][LD] dZ → dU → dY
@@ -975,7 +989,7 @@ __device__ __forceinline__ void post_attn_bwd_body(
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
   tile_gemm<MAXT, true, false>(sG, LD, sW[0], LD, 64, C, C, acc);  // dH = dZ · W2
   PIO_TS(4);
-  wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, rep(gr_out.dW2, gr_out.vrs, gr_out.slab), C, gr_out.slab);
+  if (own_w2) wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, rep(gr_out.dW2, gr_out.vrs, gr_out.slab), C, gr_out.slab);
   PIO_TS(5);
   {
     constexpr int NTN = C / 32;
@@ -1000,7 +1014,7 @@ __device__ __forceinline__ void post_attn_bwd_body(
   PIO_TS(6);
   lds_sync();
   PIO_TS(7);
-  for (int k = threadIdx.x; k < C; k += blockDim.x) {
+  for (int k = threadIdx.x; k < (own_rows ? C : 0); k += blockDim.x) {
     gadd(rep(gr_out.db1, gr_out.vrs, gr_out.slab) + k,
          sDb1[0][k] + sDb1[1][k], gr_out.slab);
     gadd(rep(gr_out.db2, gr_out.vrs, gr_out.slab) + k,
@@ -1029,7 +1043,7 @@ __device__ __forceinline__ void post_attn_bwd_body(
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
   tile_gemm<MAXT, true, false>(sG, LD, sW[NWB == 3 ? 1 : 0], LD, 64, C, C, acc);  // dXn2 = dU · W1
-  wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, rep(gr_out.dW1, gr_out.vrs, gr_out.slab), C, gr_out.slab);
+  if (own_w1) wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, rep(gr_out.dW1, gr_out.vrs, gr_out.slab), C, gr_out.slab);
   for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) { sF[m * LDF + n] = acc[t][i]; });
   PIO_TS(10);
   lds_sync();
@@ -1060,7 +1074,7 @@ __device__ __forceinline__ void post_attn_bwd_body(
       }
     colsum_partial<NCH>(yv, sPart[1], C);
     colsum_partial<NCH>(dxn, sPart[2], C);
-    row_store<NCH>(dz, dY, C, gr, R, C, av);
+    if (own_rows) row_store<NCH>(dz, dY, C, gr, R, C, av);
     drop_rows<NCH>(dz, dr, 0u, gr, C);  // dY∘m₀: the out-projection's gradient
     colsum_partial<NCH>(dz, sPart[3], C);
     lds_row_write_bf16<NCH>(sG, LD, dz);
@@ -1070,7 +1084,7 @@ __device__ __forceinline__ void post_attn_bwd_body(
   PIO_TS(12);
   lds_sync();
   PIO_TS(13);
-  for (int k = threadIdx.x; k < C; k += blockDim.x) {
+  for (int k = threadIdx.x; k < (own_rows ? C : 0); k += blockDim.x) {
     gadd(rep(gr_out.dg2, gr_out.vrs, gr_out.slab) + k,
          sPart[1][k] + sPart[1][C + k] + sPart[1][2 * C + k] + sPart[1][3 * C + k], gr_out.slab);
     gadd(rep(gr_out.dbe2, gr_out.vrs, gr_out.slab) + k,
@@ -1083,12 +1097,12 @@ __device__ __forceinline__ void post_attn_bwd_body(
 #pragma unroll
   for (int t = 0; t < MAXT; ++t) acc[t] = f32x16{};
   tile_gemm<MAXT, true, false>(sG, LD, sW[NWB == 3 ? 2 : 0], LD, 64, C, C, acc);  // dO = dY · Wo
-  wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, rep(gr_out.dWo, gr_out.vrs, gr_out.slab), C, gr_out.slab);
+  if (own_wo) wgrad_tile<MAXW>(sG, LD, sX, LD, C, C, C, C, rep(gr_out.dWo, gr_out.vrs, gr_out.slab), C, gr_out.slab);
   PIO_TS(14);
   for_acc<MAXT>(64, C, [&](int t, int m, int n, int i) { sF[m * LDF + n] = bf2f(f2bf(acc[t][i])); });
   lds_sync();
   PIO_TS(15);
-  {
+  if (own_rows) {
     float dov[NCH][8];
     lds_row_read<NCH>(dov, sF, LDF);
     row_store<NCH>(dov, dO, C, gr, R, C, av);
@@ -1118,14 +1132,15 @@ __global__ __launch_bounds__(256) void post_attn_bwd_kernel(
     const float* __restrict__ g2, const float* __restrict__ be2, float* __restrict__ dY, uint16_t* __restrict__ dO,
     float* __restrict__ delta, int H, PostAttnGrads gr_out, int R, SlabJob job, DropCfg dr) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[post_attn_bwd_smem<C>()];
-  zero_span_block(job);
+  if (blockIdx.y == 0) zero_span_block(job);
   if ((int)blockIdx.x >= (R + 63) / 64) {  // appended workgroups: the previous kernel's slab job
-    slab_reduce_block(job, blockIdx.x - (R + 63) / 64, reinterpret_cast<float4*>(smem));
+    if (blockIdx.y == 0) slab_reduce_block(job, blockIdx.x - (R + 63) / 64, reinterpret_cast<float4*>(smem));
     return;
   }
   float dz[C / 32][8];
   row_load<C / 32>(dz, dZ, C, blockIdx.x * 64 + rp_row(), R, C, AV);
-  post_attn_bwd_body<C, AV>(dz, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO, delta, H, gr_out, R, dr, smem);
+  post_attn_bwd_body<C, AV>(dz, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO, delta, H, gr_out, R, dr, smem,
+                            (int)blockIdx.y, (int)gridDim.y);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1146,7 +1161,10 @@ __device__ __forceinline__ void ln_linear_bwd_body(
     int x_rs, const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ lnw,
     const float* __restrict__ lnb, const float* __restrict__ dres, int dres_rs, float* __restrict__ dX, int dx_rs,
     float* __restrict__ dlnw, float* __restrict__ dlnb, float* __restrict__ dW, float* __restrict__ db, int vrs,
-    int wrs, int slab, int R, PeSplit ps, uint16_t* smem, float (&dxo)[NCH][8]) {
+    int wrs, int slab, int R, PeSplit ps, uint16_t* smem, float (&dxo)[NCH][8], int part = 0, int nparts = 1) {
+  // nparts > 1: workgroups sharing the tile; the weight / bias gradient of 64-column chunk j is
+  // part (j mod nparts)'s, the LN gradients and dX the row-output owner's (tile_part_owner)
+  const bool own_rows = tile_part_owner(3, nparts) == part;
   constexpr int KP = 32 * NCH, LD = KP + 8, LDG = 64 + 8, LDF = KP + 4;
   uint16_t* sG = smem;                                   // [64][LDG]  G chunk
   uint16_t* sW = sG + 64 * LDG;                          // [64][LD]   W chunk
@@ -1206,7 +1224,8 @@ __device__ __forceinline__ void ln_linear_bwd_body(
       tile_fetch<NCH>(wb, W, w_rs, nc + 64, N, 64, wk, KP, wvec);
     }
     tile_gemm<MAXT, true, false>(sG, LDG, sW, LD, 64, KP, 64, acc);
-    if (dW) {
+    const bool mine = (nc >> 6) % nparts == part;
+    if (dW && mine) {
       wgrad_tile<MAXT>(sG, LDG, sXn, LD, 64, KP, N - nc, Kin, rep(dW, wrs, slab) + (long long)nc * Kin, Kin, slab);
       if (db) {
 #pragma unroll
@@ -1217,7 +1236,7 @@ __device__ __forceinline__ void ln_linear_bwd_body(
       }
     }
     lds_sync();
-    if (dW && db && threadIdx.x < 64 && nc + (int)threadIdx.x < N) {
+    if (dW && mine && db && threadIdx.x < 64 && nc + (int)threadIdx.x < N) {
       const int t = threadIdx.x;
       gadd(rep(db, vrs, slab) + nc + t, sPb[t] + sPb[64 + t] + sPb[128 + t] + sPb[192 + t], slab);
     }
@@ -1272,12 +1291,12 @@ __device__ __forceinline__ void ln_linear_bwd_body(
 #pragma unroll
       for (int e = 0; e < 8; ++e) gw[j][e] += dr[j][e];
   }
-  if (dX) row_store<NCH>(gw, dX, dx_rs, gr, R, Kin, kvec && (dx_rs & 7) == 0 && aligned16(dX));
+  if (dX && own_rows) row_store<NCH>(gw, dX, dx_rs, gr, R, Kin, kvec && (dx_rs & 7) == 0 && aligned16(dX));
 #pragma unroll
   for (int j = 0; j < NCH; ++j)
 #pragma unroll
     for (int e = 0; e < 8; ++e) dxo[j][e] = gw[j][e];
-  if (lnw && dlnw) {
+  if (lnw && dlnw && own_rows) {
     lds_sync();
     colsum_flush(sPart, KP, rep(dlnw, vrs, slab), Kin, slab);
     colsum_flush(sPart + 4 * KP, KP, rep(dlnb, vrs, slab), Kin, slab);
@@ -1326,17 +1345,19 @@ __global__ __launch_bounds__(256) void ln_linear_post_attn_bwd_kernel(
   // ONE buffer for both halves (used one after the other): ≈69 KB at C = 64, two workgroups per
   // CU, so the appended slab-job workgroups run beside the tiles instead of after them
   __shared__ __attribute__((aligned(16))) unsigned char smem[SM];
-  zero_span_block(job);
+  if (blockIdx.y == 0) zero_span_block(job);
   if ((int)blockIdx.x >= (R + 63) / 64) {  // appended workgroups: the previous kernel's slab job
-    slab_reduce_block(job, blockIdx.x - (R + 63) / 64, reinterpret_cast<float4*>(smem));
+    if (blockIdx.y == 0) slab_reduce_block(job, blockIdx.x - (R + 63) / 64, reinterpret_cast<float4*>(smem));
     return;
   }
+  const int part = (int)blockIdx.y, nparts = (int)gridDim.y;  // workgroups per tile (split_tiles)
   float dz[NCH][8];
   ln_linear_bwd_body<float, float, NCH, AV>(G, nq, nq, Wq, C, C, X, C, mean1, rstd1, lnw, lnb, dres, C, nullptr, C,
                                         dlnw, dlnb, dWq, dbq, gr_out.vrs, gr_out.vrs, gr_out.slab, R, PeSplit{},
-                                        reinterpret_cast<uint16_t*>(smem), dz);
+                                        reinterpret_cast<uint16_t*>(smem), dz, part, nparts);
   lds_sync();  // the ln_linear half's LDS traffic is done before the post-attention half reuses it
-  post_attn_bwd_body<C, AV>(dz, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO, delta, H, gr_out, R, dr, smem);
+  post_attn_bwd_body<C, AV>(dz, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO, delta, H, gr_out, R, dr, smem,
+                            part, nparts);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1590,12 +1611,21 @@ bool sa_layer_fwd_launch(const uint16_t* QKV, int N, float scale_log2, uint16_t*
   return true;
 }
 
+// workgroups per 64-row tile of the post-attention backward kernels when the tiles fill only a
+// fraction of the chip (the C = 128 image latent stacks: 16-64 tiles): each runs the tile's row
+// chain and stores its share of the outputs (tile_part_owner); measured: 2 per tile took the
+// ImageNet step's boundary backward from 50 to 40 µs per launch
+static unsigned split_tiles(int R) {
+  const int t = (R + 63) / 64;
+  return t < 32 ? 4u : t < 128 ? 2u : 1u;
+}
+
 void post_attn_bwd_launch(int C, const float* dZ, const float* Ysave, const float* mean2, const float* rstd2,
                           const uint16_t* U, const uint16_t* O, const uint16_t* Wo, const uint16_t* W1,
                           const uint16_t* W2, const float* g2, const float* be2, float* dY, uint16_t* dO,
                           float* delta, int H, const PostAttnGrads& grads, int R, const SlabJob& job, const DropCfg& dr,
                           hipStream_t st) {
-  dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0));
+  dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0), split_tiles(R));
   const bool av = av_ok({dZ, Ysave, U, O, Wo, W1, W2, dY, dO}, {});
 #define PAB(CC)                                                                                                  \
   if (av) hipLaunchKernelGGL((post_attn_bwd_kernel<CC, true>), grid, dim3(256), 0, st, dZ, Ysave, mean2, rstd2, U, \
@@ -1627,6 +1657,7 @@ bool ln_linear_post_attn_bwd_launch(int C, const void* Gv, bool g_bf16, const ui
                                            st))
     return true;
   if (g_bf16) return false;
+  grid.y = split_tiles(R);
 #define LPB(CC, NQ)                                                                                               \
   if (av) hipLaunchKernelGGL((ln_linear_post_attn_bwd_kernel<CC, true, NQ>), grid, dim3(256), 0, st, G, Wq, X, mean1, \
                              rstd1, lnw, lnb, dres, dlnw, dlnb, dWq, dbq, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, \
