@@ -903,6 +903,15 @@ __host__ __device__ constexpr int tile_part_owner(int g, int nparts) {
   return nparts == 1 ? 0 : nparts == 2 ? (g == 0 || g == 3 ? 0 : 1) : (g == 0 ? 0 : g == 1 ? 1 : g == 2 ? 2 : 3);
 }
 
+// workgroups per 64-row tile of the post-attention backward kernels when the tiles fill only a
+// fraction of the chip (the C = 128 image latent stacks: 16-64 tiles): each runs the tile's row
+// chain and stores its share of the outputs (tile_part_owner); measured: 2 per tile took the
+// ImageNet step's boundary backward from 50 to 40 µs per launch
+static inline unsigned split_tiles(int R) {
+  const int t = (R + 63) / 64;
+  return t <= 64 ? 4u : t < 128 ? 2u : 1u;
+}
+
 // LDS bytes of post_attn_bwd_body: sG, sX, sW[NWB], sF, sPart, sDb1, sP
 template <int C>
 constexpr int post_attn_bwd_smem() {
@@ -1313,12 +1322,13 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
     int wrs, int slab, int R, PeSplit ps, SlabJob job) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   if ((int)blockIdx.x >= (R + 63) / 64) {  // appended workgroups: the previous kernel's slab job
-    slab_reduce_block(job, blockIdx.x - (R + 63) / 64, reinterpret_cast<float4*>(smem));
+    if (blockIdx.y == 0) slab_reduce_block(job, blockIdx.x - (R + 63) / 64, reinterpret_cast<float4*>(smem));
     return;
   }
   float dxo[NCH][8];
   ln_linear_bwd_body<TG, TX, NCH, AV>(G, g_rs, N, W, w_rs, Kin, X, x_rs, mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs,
-                                  dlnw, dlnb, dW, db, vrs, wrs, slab, R, ps, smem, dxo);
+                                  dlnw, dlnb, dW, db, vrs, wrs, slab, R, ps, smem, dxo, (int)blockIdx.y,
+                                  (int)gridDim.y);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1611,15 +1621,6 @@ bool sa_layer_fwd_launch(const uint16_t* QKV, int N, float scale_log2, uint16_t*
   return true;
 }
 
-// workgroups per 64-row tile of the post-attention backward kernels when the tiles fill only a
-// fraction of the chip (the C = 128 image latent stacks: 16-64 tiles): each runs the tile's row
-// chain and stores its share of the outputs (tile_part_owner); measured: 2 per tile took the
-// ImageNet step's boundary backward from 50 to 40 µs per launch
-static unsigned split_tiles(int R) {
-  const int t = (R + 63) / 64;
-  return t < 32 ? 4u : t < 128 ? 2u : 1u;
-}
-
 void post_attn_bwd_launch(int C, const float* dZ, const float* Ysave, const float* mean2, const float* rstd2,
                           const uint16_t* U, const uint16_t* O, const uint16_t* Wo, const uint16_t* W1,
                           const uint16_t* W2, const float* g2, const float* be2, float* dY, uint16_t* dO,
@@ -1685,7 +1686,8 @@ static void ln_linear_bwd_t(const void* G, int g_rs, int N, const uint16_t* W, i
   const bool av = av_ok({G, W, X, lnw, lnb, dres}, {N, g_rs, w_rs, Kin, x_rs, dres ? dres_rs : 0});
   auto fn = av ? ln_linear_bwd_kernel<TG, TX, NCH, true> : ln_linear_bwd_kernel<TG, TX, NCH, false>;
   set_smem_once((const void*)fn);
-  const dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0));  // + the appended slab-job workgroups
+  // + the appended slab-job workgroups; few tiles: several workgroups per tile (split_tiles)
+  const dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0), split_tiles(R));
   hipLaunchKernelGGL(fn, grid, dim3(256), smem, st, (const TG*)G, g_rs, N, W, w_rs, Kin, (const TX*)X, x_rs,
                      mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, dlnw, dlnb, dW, db, vrs, wrs, slab, R, ps, job);
 }
