@@ -405,7 +405,9 @@ __device__ __forceinline__ void ln_linear_fwd_tile(float (&xv)[NCH][8], bf16x8 (
                                                    const float* __restrict__ bias, int N, int act,
                                                    const float* __restrict__ res, int res_rs, TOut* __restrict__ Y,
                                                    int y_rs, float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                   uint16_t* smem) {
+                                                   uint16_t* smem, int part = 0, int nparts = 1) {
+  // nparts > 1: workgroups sharing the tile; this one forms output chunks part, part + nparts, …
+  // (wb must hold chunk `part`), the row statistics are the last part's to store
   constexpr int KP = 32 * NCH, LD = KP + 8, LDO = 64 + 4;
   uint16_t* sA = smem;                                  // [64][LD]  LN(X), bf16
   uint16_t* sW = sA + 64 * LD;                          // [64][LD]  W chunk
@@ -431,7 +433,7 @@ __device__ __forceinline__ void ln_linear_fwd_tile(float (&xv)[NCH][8], bf16x8 (
         q += d * d;
       }
     const float rstd = rsqrtf(quad_sum(q) / Kin + eps);
-    if ((threadIdx.x & 3) == 0 && gr < R && mean_out) { mean_out[gr] = mean; rstd_out[gr] = rstd; }
+    if ((threadIdx.x & 3) == 0 && gr < R && mean_out && part == nparts - 1) { mean_out[gr] = mean; rstd_out[gr] = rstd; }
 #pragma unroll
     for (int j = 0; j < NCH; ++j)
 #pragma unroll
@@ -439,10 +441,10 @@ __device__ __forceinline__ void ln_linear_fwd_tile(float (&xv)[NCH][8], bf16x8 (
   }
   lds_row_write_bf16<NCH>(sA, LD, xv);
 
-  for (int n0 = 0; n0 < N; n0 += 64) {
+  for (int n0 = 64 * part; n0 < N; n0 += 64 * nparts) {
     tile_store<NCH>(wb, sW, LD, 64, KP);
     lds_sync();
-    if (n0 + 64 < N) tile_fetch<NCH>(wb, W, w_rs, n0 + 64, N, 64, wk, KP, wvec);
+    if (n0 + 64 * nparts < N) tile_fetch<NCH>(wb, W, w_rs, n0 + 64 * nparts, N, 64, wk, KP, wvec);
     const int bc = n0 + 32 * (w & 1) + (l & 31);
     const float bv = (bias && bc < N) ? bias[bc] : 0.f;
     f32x16 acc[1] = {f32x16{}};
@@ -538,7 +540,9 @@ __device__ __forceinline__ void post_attn_fwd_body(
     const uint16_t* __restrict__ W1, const float* __restrict__ b1, const uint16_t* __restrict__ W2,
     const float* __restrict__ b2, float* __restrict__ Z, float* __restrict__ Ysave, float* __restrict__ mean2,
     float* __restrict__ rstd2, uint16_t* __restrict__ Usave, int R, int Rx, const DropCfg& dr, float (&z)[C / 32][8],
-    PaPre<C>& pre, const uint16_t* sO = nullptr) {
+    PaPre<C>& pre, const uint16_t* sO = nullptr, bool store_rows = true) {
+  // store_rows = false: a workgroup sharing the tile with the one that stores Y, U, Z, the LN2
+  // statistics (post_attn_ln_linear_fwd_kernel split over the next projection's columns)
   // X has Rx rows, row r of the tile adds X[r % Rx] (Rx < R: batch-broadcast residual).
   // Residual dropout (dr.thresh > 0): Y = X + drop₀(attn-out), Z = Y + drop₁(MLP(Y)), masks
   // hashed from (device seed, site, row·C + col) and regenerated by the backward.
@@ -583,7 +587,7 @@ __device__ __forceinline__ void post_attn_fwd_body(
     for (int j = 0; j < NCH; ++j)
 #pragma unroll
       for (int e = 0; e < 8; ++e) { yv[j][e] += t[j][e]; s += yv[j][e]; }
-    row_store<NCH>(yv, Ysave, C, gr, R, C, av);
+    if (store_rows) row_store<NCH>(yv, Ysave, C, gr, R, C, av);
     const float mean = quad_sum(s) / C;
     float q = 0.f;
 #pragma unroll
@@ -591,7 +595,7 @@ __device__ __forceinline__ void post_attn_fwd_body(
 #pragma unroll
       for (int e = 0; e < 8; ++e) { const float d = yv[j][e] - mean; q += d * d; }
     const float rstd = rsqrtf(quad_sum(q) / C + eps);
-    if ((threadIdx.x & 3) == 0 && gr < R) { mean2[gr] = mean; rstd2[gr] = rstd; }
+    if ((threadIdx.x & 3) == 0 && gr < R && store_rows) { mean2[gr] = mean; rstd2[gr] = rstd; }
 #pragma unroll
     for (int j = 0; j < NCH; ++j)
 #pragma unroll
@@ -612,7 +616,7 @@ __device__ __forceinline__ void post_attn_fwd_body(
   {
     float u[NCH][8];
     lds_row_read<NCH>(u, sF, LDF);
-    row_store<NCH>(u, Usave, C, gr, R, C, av);
+    if (store_rows) row_store<NCH>(u, Usave, C, gr, R, C, av);
 #pragma unroll
     for (int j = 0; j < NCH; ++j)
 #pragma unroll
@@ -631,7 +635,7 @@ __device__ __forceinline__ void post_attn_fwd_body(
   for (int j = 0; j < NCH; ++j)
 #pragma unroll
     for (int e = 0; e < 8; ++e) z[j][e] += yv[j][e];
-  row_store<NCH>(z, Z, C, gr, R, C, av);
+  if (store_rows) row_store<NCH>(z, Z, C, gr, R, C, av);
 }
 
 template <int C, bool AV>
@@ -666,17 +670,21 @@ __global__ __launch_bounds__(256) void post_attn_ln_linear_fwd_kernel(
     uint16_t* __restrict__ QKV, float* __restrict__ mean1, float* __restrict__ rstd1, DropCfg dr) {
   constexpr int NCH = C / 32, KP = 32 * NCH;
   __shared__ __attribute__((aligned(16))) uint16_t smem[ln_linear_fwd_smem<NCH>() / 2];  // LN1+QKV half
+  // gridDim.y workgroups per tile (split_tiles): each runs the post-attention chain and forms every
+  // gridDim.y-th 64-column chunk of the next QKV; part 0 stores the chain's row outputs
+  const int part = (int)blockIdx.y, nparts = (int)gridDim.y;
   bf16x8 wb[NCH];
-  tile_fetch<NCH>(wb, Wq, C, 0, 3 * C, 64, C, KP, AV);
+  tile_fetch<NCH>(wb, Wq, C, 64 * part, 3 * C, 64, C, KP, AV);
   float gw[NCH][8], gb[NCH][8];
   row_load<NCH>(gw, lnw, 0, 0, 1, C, AV);
   row_load<NCH>(gb, lnb, 0, 0, 1, C, AV);
   float z[NCH][8];
   PaPre<C> pre;
   post_attn_fwd_prefetch<C, AV>(pre, X, Wo, bo, g2, be2, W1, b1, W2, b2, R, Rx);
-  post_attn_fwd_body<C, AV>(O, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, Rx, dr, z, pre);
+  post_attn_fwd_body<C, AV>(O, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, Rx, dr, z, pre,
+                            nullptr, part == 0);
   ln_linear_fwd_tile<uint16_t, NCH, AV>(z, wb, gw, gb, true, blockIdx.x * 64, R, C, eps, Wq, C, bq, 3 * C, 0, nullptr, 0,
-                                    QKV, 3 * C, mean1, rstd1, smem);
+                                    QKV, 3 * C, mean1, rstd1, smem, part, nparts);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1572,7 +1580,7 @@ void post_attn_ln_linear_fwd_launch(int C, const uint16_t* O, const float* X, co
                                     const uint16_t* Wq, const float* bq, uint16_t* QKV, float* mean1, float* rstd1,
                                     const DropCfg& dr, hipStream_t st) {
   const bool av = av_ok({O, X, Wo, W1, W2, Z, Ysave, Usave, Wq, lnw, lnb, QKV}, {});
-  dim3 grid((R + 63) / 64);
+  dim3 grid((R + 63) / 64, split_tiles(R));
 #define PLF(CC)                                                                                                  \
   if (av) hipLaunchKernelGGL((post_attn_ln_linear_fwd_kernel<CC, true>), grid, dim3(256), 0, st, O, X, Wo, bo, g2, \
                              be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, Rx, lnw, lnb, Wq, bq, QKV,  \
