@@ -480,18 +480,19 @@ __global__ __launch_bounds__(256) void ln_linear_fwd_kernel(const TIn* __restric
   constexpr int KP = 32 * NCH;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   const int m0 = blockIdx.x * 64, gr = m0 + rp_row();
-  // phase 0: X rows, the first W chunk and the LN affine in flight together
+  const int part = (int)blockIdx.y, nparts = (int)gridDim.y;  // workgroups per tile (split_tiles)
+  // phase 0: X rows, the first W chunk (of this part) and the LN affine in flight together
   float xv[NCH][8];
   row_load_x<NCH>(xv, X, x_rs, gr, R, Kin, AV, ps);
   bf16x8 wb[NCH];
-  tile_fetch<NCH>(wb, W, w_rs, 0, N, 64, w_rs > Kin ? w_rs : Kin, KP, AV);
+  tile_fetch<NCH>(wb, W, w_rs, 64 * part, N, 64, w_rs > Kin ? w_rs : Kin, KP, AV);
   float gw[NCH][8], gb[NCH][8];
   if (lnw) {
     row_load<NCH>(gw, lnw, 0, 0, 1, Kin, AV);
     row_load<NCH>(gb, lnb, 0, 0, 1, Kin, AV);
   }
   ln_linear_fwd_tile<TOut, NCH, AV>(xv, wb, gw, gb, lnw != nullptr, m0, R, Kin, eps, W, w_rs, bias, N, act, res, res_rs, Y,
-                                y_rs, mean_out, rstd_out, smem);
+                                y_rs, mean_out, rstd_out, smem, part, nparts);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1520,8 +1521,9 @@ static void ln_linear_fwd_t(const void* X, int x_rs, int R, int Kin, const float
   const bool av = av_ok({X, W, lnw, lnb}, {Kin, x_rs, w_rs});
   auto fn = av ? ln_linear_fwd_kernel<TI, TO, NCH, true> : ln_linear_fwd_kernel<TI, TO, NCH, false>;
   set_smem_once((const void*)fn);
-  hipLaunchKernelGGL(fn, dim3((R + 63) / 64), dim3(256), smem, st, (const TI*)X, x_rs, R, Kin, lnw, lnb, eps, W, w_rs, bias,
-                     N, act, res, res_rs, (TO*)Y, y_rs, mean, rstd, ps);
+  // few tiles: several workgroups per tile, each forming every split_tiles(R)-th 64-column chunk
+  hipLaunchKernelGGL(fn, dim3((R + 63) / 64, split_tiles(R)), dim3(256), smem, st, (const TI*)X, x_rs, R, Kin, lnw, lnb,
+                     eps, W, w_rs, bias, N, act, res, res_rs, (TO*)Y, y_rs, mean, rstd, ps);
 }
 
 template <typename TI, typename TO>
