@@ -878,7 +878,10 @@ void attn_bwd_launch(const AttnArgs& a, int D, const uint16_t* O, const uint16_t
                        rows, a.H, D, dq_rs);
   switch (D) {  // waves per workgroup: 8 for d ≤ 32, 4 above (keys per block = 32 × waves)
     case 16: bwd_launch_t<16, 8>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, qsplit_ok, dq_zeroed, st); break;
-    case 32: bwd_launch_t<32, 8>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, qsplit_ok, dq_zeroed, st); break;
+    case 32:  // ≤ 64 keys (the image configs' 32-latent self-attention): 2 waves, not 6 idle of 8
+      if (a.Nk <= 64) bwd_launch_t<32, 2>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, qsplit_ok, dq_zeroed, st);
+      else bwd_launch_t<32, 8>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, qsplit_ok, dq_zeroed, st);
+      break;
     case 64: bwd_launch_t<64, 4>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, qsplit_ok, dq_zeroed, st); break;
     case 128: bwd_launch_t<128, 4>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, qsplit_ok, dq_zeroed, st); break;
     default: break;
