@@ -112,9 +112,12 @@ __global__ __launch_bounds__(256) void embed_bwd_local_kernel(const int64_t* __r
                                                               int L, float scale) {
   __shared__ uint32_t sKey[ET];
   const int t = threadIdx.x;
-  if ((int)blockIdx.x >= nblk_e) {  // position-table gradient: block (l, batch group)
-    const int pb = blockIdx.x - nblk_e, l = pb % L, b0 = (pb / L) * EB;
-    for (int c = t; c < C; c += blockDim.x) {
+  if ((int)blockIdx.x >= nblk_e) {  // position-table gradient: block (256 / C positions, batch group)
+    constexpr int TPP = C < 256 ? C : 256, PPB = 256 / TPP;
+    const int nlb = (L + PPB - 1) / PPB;
+    const int pb = blockIdx.x - nblk_e, l = (pb % nlb) * PPB + t / TPP, b0 = (pb / nlb) * EB;
+    if (l >= L) return;
+    for (int c = t % TPP; c < C; c += TPP) {
       float v[EB];
 #pragma unroll
       for (int j = 0; j < EB; ++j) v[j] = b0 + j < B ? g[((long long)(b0 + j) * L + l) * C + c] : 0.f;
@@ -359,7 +362,8 @@ bool embed_bwd_local_launch(const int64_t* ids, const float* g, float* dE, float
                             hipStream_t st) {
   const long long n = (long long)B * L;
   const int nblk_e = dE ? (int)((n + ET - 1) / ET) : 0;
-  const int nblk_p = dP ? L * ((B + EB - 1) / EB) : 0;
+  const int ppb = 256 / (C < 256 ? C : 256);
+  const int nblk_p = dP ? ((L + ppb - 1) / ppb) * ((B + EB - 1) / EB) : 0;
   const dim3 grid(nblk_e + nblk_p);
   if (nblk_e + nblk_p == 0) return true;
   switch (C) {
