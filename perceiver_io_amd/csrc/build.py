@@ -29,7 +29,8 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # accumulators with VALU (softmax, LayerNorm, GELU) and fit 256 VGPRs; rowgemm.hip keeps the
 # default (its 160-channel LN-linear backward would spill without the AGPR file)
 _VGPR_FORM = ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]
-PER_FILE_FLAGS = {"chain.hip": _VGPR_FORM, "attention_pe.hip": _VGPR_FORM, "ce_head.hip": _VGPR_FORM}
+PER_FILE_FLAGS = {"chain.hip": _VGPR_FORM, "attention_pe.hip": _VGPR_FORM, "ce_head.hip": _VGPR_FORM,
+                  "persist.hip": _VGPR_FORM}
 
 
 def _torch_paths():
