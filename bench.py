@@ -113,7 +113,7 @@ def _aten_stacks(engine, data, steps, depth):
 
     with _Rec():
         for i in range(steps):
-            engine.step(data[i % 4])
+            engine.step(data[i % 4], ring_view=True)
         torch.cuda.synchronize()
     for (op, frames), n in seen.most_common(60):
         print(f"{op} x{n}", file=sys.stderr)
@@ -352,7 +352,7 @@ def main(argv=None):
 
     data = [to_dev(make_batch(g)) for _ in range(4)]
     for i in range(args.warmup):
-        loss = engine.step(data[i % 4])
+        loss = engine.step(data[i % 4], ring_view=True)
     if cuda:
         torch.cuda.synchronize()
     pdist.barrier()
@@ -360,7 +360,7 @@ def main(argv=None):
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        loss = engine.step(data[i % 4])
+        loss = engine.step(data[i % 4], ring_view=True)
     if cuda:
         torch.cuda.synchronize()
     pdist.barrier()
@@ -378,7 +378,7 @@ def main(argv=None):
 
         with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
             for i in range(args.profile_steps):
-                engine.step(data[i % 4])
+                engine.step(data[i % 4], ring_view=True)
             torch.cuda.synchronize()
         if info.is_main:
             print(prof.key_averages().table(sort_by="cuda_time_total", row_limit=40), file=sys.stderr)

@@ -237,6 +237,13 @@ __global__ __launch_bounds__(256) void ce2_fwd_kernel(const float* __restrict__ 
       reinterpret_cast<float4*>(zero_out)[i] = float4{0.f, 0.f, 0.f, 0.f};
   }
   // ---- arrival ticket of the row block: every wave drains its stores, one lane counts ----
+  // Hand-off form (cdna_hip_programming.md Guideline 16; MI355X_MICROARCH.md § visibility, the
+  // write-through table's first row): every handed-off word is stored sc1 (agent-scope relaxed
+  // atomic stores) and drained by its storing wave (vmcnt(0)) before the barrier behind which
+  // one lane adds to ONE unsharded counter; only the workgroup whose add returned last reads,
+  // and only with sc1 loads (L1 bypass), after that add returned (its other waves after a
+  // barrier).  No release/acquire fence is needed in this form (each costs ≈1.7 µs).  The
+  // ticket words assume one ce_fwd in flight per device (every launch is on the step's stream).
   __shared__ unsigned last;
   __shared__ float red[2][4];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -82,9 +82,14 @@ class PerceiverEncoder(nn.Module):
         if attn_mask is None and ops.use_hip(self.latent):
             return ops.fused.encode_inputs(self, x_in, pad_mask)
         x_latent = self.latent.unsqueeze(0).expand(x_in.shape[0], -1, -1)
-        for i, layer in enumerate(self.layers()):
+        layers = self.layers()
+        for i, layer in enumerate(layers):
             if i == 1:  # DDP: layer_n's gradients are final here (parallel/reducer.py)
                 x_latent = bucket_ready_point(x_latent, self, "layer_n")
+            if i == 0 and len(layers) > 1:  # DDP: layer_1's self-attention block gradients final here
+                x_latent = layer[0](x_latent, x_in, pad_mask, attn_mask)
+                x_latent = layer[1](bucket_ready_point(x_latent, self, "layer_1_sa"))
+                continue
             x_latent = layer(x_latent, x_in, pad_mask, attn_mask)
         return x_latent
 

@@ -413,9 +413,12 @@ class _LayerFn(torch.autograd.Function):
         K = kernels(x_q)
         # broadcast queries that are a leaf parameter's (1, N, C) view (the encoder's latent array):
         # the backward adds their gradient straight into the parameter's gradient buffer (no
-        # autograd AccumulateGrad add kernel)
+        # autograd AccumulateGrad add kernel) — only when that buffer is an optimizer's flat
+        # gradient view (FlatParameterSpace sets _pio_flat); otherwise the gradient goes back
+        # through autograd, so torch.autograd.grad(..., inputs=[latent]) and hooks still work
         base = x_q._base
         ctx.q_leaf = (base if spec.cross and base is not None and base.is_leaf and base.requires_grad
+                      and getattr(base, "_pio_flat", False)
                       and x_q.shape[0] == 1 and tuple(base.shape) == tuple(x_q.shape[1:]) else None)
         C, H = spec.C, spec.heads
         D = C // H
@@ -1194,6 +1197,8 @@ def _encode(encoder, src: KVSource, pad_mask):
             _LOOKAHEAD["want_q"] = cross_q_lookahead(nxt_cross, src)
         elif nxt_cross is None:  # a decoder's K/V over the encoder output, when its caller asked for it
             _LOOKAHEAD["want_q"] = _LOOKAHEAD["want_kv"]
+        if li == 0 and len(layers) > 1:  # DDP: layer_1's block gradients (but its first LN1/QKV) final here
+            lat = bucket_ready_point(lat, encoder, "layer_1_sa")
         try:
             lat = self_attention_block(block, lat)
         finally:

@@ -75,6 +75,7 @@ class FlatParameterSpace:
                 self.data[o:o + n].copy_(p.detach().reshape(-1).float())
                 p.data = self.data[o:o + n].view_as(p)
                 p.grad = self.grad[o:o + n].view_as(p)
+                p._pio_flat = True  # its gradient is a view of this flat buffer (ops/fused.py in-place paths)
                 if self.grad_rep is not None and o < self.n_rep:
                     p._pio_grad_rep = self.grad_rep[:, o:o + n]  # (8, numel) replica view
         if self.shadow is not None:

@@ -106,7 +106,17 @@ def graph_collectives_ok(device) -> bool:
         with torch.cuda.graph(g, stream=side):
             dist.all_reduce(t)
     except Exception:  # noqa: BLE001 - any capture failure means "not capturable"
-        captured, g = 0.0, None
+        captured = 0.0
+        # torch.cuda.graph ends the capture when the with-block exits, also on an exception; a
+        # capture left open half-way would poison the side stream (and, in global capture mode,
+        # every later launch of the process): end it here before anything else runs
+        with torch.cuda.stream(side):
+            if g is not None and torch.cuda.is_current_stream_capturing():
+                try:
+                    g.capture_end()
+                except Exception:  # noqa: BLE001 - an invalidated capture still ends capture mode
+                    pass
+        g = None
     flag = torch.tensor([captured], device=device)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)
     ok = bool(flag.item() > 0.5)

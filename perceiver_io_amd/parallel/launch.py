@@ -28,29 +28,43 @@ def _visible_list(v: str) -> int:
     return len([t for t in v.split(",") if t.strip() != ""])
 
 
+def topology_gpu_count(topo: str = "/sys/class/kfd/kfd/topology/nodes", dri: str = "/dev/dri") -> Optional[int]:
+    """GPUs of the KFD topology that this process can open, or None without a topology.
+
+    A node counts when it has SIMDs (``simd_count > 0``) AND its render node
+    ``{dri}/renderD<drm_render_minor>`` is readable and writable — the filter ROCr applies: a
+    container given only some of the host's render nodes still lists every host GPU in the
+    topology, and HIP skips the ones it cannot open."""
+    if not os.path.isdir(topo):
+        return None
+    n = 0
+    for node in os.listdir(topo):
+        try:
+            with open(os.path.join(topo, node, "properties")) as f:
+                props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+            if int(props.get("simd_count", "0")) <= 0:
+                continue
+            minor = int(props["drm_render_minor"])
+        except (OSError, ValueError, KeyError):
+            continue
+        if os.access(os.path.join(dri, f"renderD{minor}"), os.R_OK | os.W_OK):
+            n += 1
+    return n
+
+
 def gpu_count() -> int:
     """Number of GPUs this process would see, WITHOUT initialising HIP in this process (the
     launcher parent must hold no GPU state when it starts the ranks).
 
     Order: an explicit ``HIP_VISIBLE_DEVICES`` / ``ROCR_VISIBLE_DEVICES`` / ``CUDA_VISIBLE_DEVICES``
-    list; else the GPU nodes of the KFD topology (``/sys/class/kfd/kfd/topology/nodes/*``, a
-    node with ``simd_count > 0``); else a short-lived child process that asks torch (its HIP
-    runtime dies with it)."""
+    list; else the openable GPU nodes of the KFD topology (``topology_gpu_count``); else a
+    short-lived child process that asks torch (its HIP runtime dies with it)."""
     for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
         v = os.environ.get(var)
         if v is not None:
             return _visible_list(v)
-    topo = "/sys/class/kfd/kfd/topology/nodes"
-    if os.path.isdir(topo):
-        n = 0
-        for node in os.listdir(topo):
-            try:
-                with open(os.path.join(topo, node, "properties")) as f:
-                    props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
-                if int(props.get("simd_count", "0")) > 0:
-                    n += 1
-            except (OSError, ValueError):
-                continue
+    n = topology_gpu_count()
+    if n:
         return n
     try:
         r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],

@@ -152,7 +152,7 @@ class FlatGradReducer:
             j = next((i for i in idx if self.flat.params[i] is lo_param), None)
             if j is None:
                 return None
-            lo = offs[j] + lo_extra
+            lo = offs[j] + (lo_extra + 3) // 4 * 4  # 4-element aligned: the vector update kernel's ranges
         return (lo, hi) if hi > lo else None
 
     def set_ready_ranges(self, ranges: Dict[str, Tuple[Tuple[int, int], torch.nn.Module]]):
@@ -177,7 +177,7 @@ class FlatGradReducer:
             hi = lo_r
         if hi > 0:
             gaps.append((0, hi))
-        cap = max(64, self.bucket_bytes // 4)
+        cap = max(64, self.bucket_bytes // 4 // 64 * 64)  # bucket boundaries stay 64-element (256-B) aligned
         for lo, hi in gaps:
             while hi - lo > cap:
                 self.buckets.append((hi - cap, hi))
@@ -187,7 +187,8 @@ class FlatGradReducer:
 
     def plan(self, model) -> Dict[str, Tuple[int, int]]:
         """Ready points for a Perceiver model (anything with ``.decoder`` and/or ``.encoder``):
-        ``"decoder"`` and, for a weight-shared encoder (``layer_n``), ``"layer_n"``.  Returns the
+        ``"decoder"`` and, for a weight-shared encoder (``layer_n``), ``"layer_n"`` and
+        ``"layer_1_sa"`` (layer_1's self-attention block).  Returns the
         planned flat ranges (empty when nothing can overlap, e.g. a frozen encoder's decoder-only
         training keeps one bucket)."""
         ranges = {}
@@ -211,6 +212,21 @@ class FlatGradReducer:
                 r = self._param_range(ps, lo_param=bias, lo_extra=c)
                 if r is not None:
                     ranges["layer_n"] = (r, enc)
+        l1 = getattr(enc, "layer_1", None) if isinstance(enc, torch.nn.Module) else None
+        blk = l1[1] if isinstance(l1, torch.nn.Sequential) and len(l1) > 1 else None
+        if blk is not None and lay is not None:
+            # layer_1's self-attention block: final once the backward leaves it, but for its first
+            # layer's LN1 + QKV projection (on the fused path the preceding cross layer's kernel
+            # computes that backward) — the range starts at that layer's out-projection
+            bps = [p for p in blk.parameters() if p.requires_grad]
+            try:
+                first_out = blk[0][0].module.attention.attention.out_proj.weight
+            except (AttributeError, IndexError, TypeError):
+                first_out = None
+            if bps and first_out is not None and first_out.requires_grad:
+                r = self._param_range(bps, lo_param=first_out)
+                if r is not None:
+                    ranges["layer_1_sa"] = (r, enc)
         if not self.overlap:
             # overlap off: same bucket layout (so results stay bit-comparable), no ready points
             self.set_ready_ranges(ranges)

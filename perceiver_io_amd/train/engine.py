@@ -329,8 +329,18 @@ class StepEngine:
     def _kinds(self, n: int):
         return ["micro"] * (n - 1) + ["last"]
 
-    def step(self, batch):
-        """One optimizer step (``accumulate`` micro-batches must be passed as a list)."""
+    def step(self, batch, ring_view: bool = False):
+        """One optimizer step (``accumulate`` micro-batches must be passed as a list); returns the
+        step's loss.  A replayed step's loss lives in a slot of a device ring that the captured
+        update kernel writes (no copy launch per replay): with ``ring_view=True`` the caller gets
+        that slot itself — valid for the next ``LOSS_RING - 1`` steps, for callers that convert it
+        right away (Trainer, bench); by default an independent copy, like an eager step's."""
+        out = self._step_dispatch(batch)
+        if not ring_view and self._loss_ring is not None and out._base is self._loss_ring:
+            out = out.clone()
+        return out
+
+    def _step_dispatch(self, batch):
         if self.stream is None:
             return self._step(batch)
         batches = batch if (self.accumulate > 1 and isinstance(batch, list)) else [batch]

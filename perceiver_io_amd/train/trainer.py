@@ -441,7 +441,7 @@ class Trainer:
                     if not self.fused and self.gradient_clip_val:
                         loss = self._eager_clip_step(acc_buf)
                     else:
-                        loss = self._engine.step(acc_buf if self.accumulate > 1 else acc_buf[0])
+                        loss = self._engine.step(acc_buf if self.accumulate > 1 else acc_buf[0], ring_view=True)
                 acc_buf = []
                 self._in_train = False
                 self.global_step += 1

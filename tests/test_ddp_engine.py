@@ -191,17 +191,19 @@ def _flat_init():
 def test_ready_points_fire_where_expected(ddp_runs):
     runs, _ = ddp_runs
     r = runs[0]
-    assert set(r["eager"]["points"]) == {"decoder", "layer_n"}
-    # backward order: the decoder first, then layer_n — once per optimizer step
-    assert r["eager"]["log"] == ["decoder", "layer_n"] * STEPS
+    order = ["decoder", "layer_n", "layer_1_sa"]
+    assert set(r["eager"]["points"]) == set(order)
+    # backward order: the decoder first, then layer_n, then layer_1's self-attention block — once
+    # per optimizer step
+    assert r["eager"]["log"] == order * STEPS
     assert r["eager_nooverlap"]["log"] == []
     # collectives in the graph: every replay's backward launches them (closure replays run Python);
     # not capturable: only the eager warm-up step does, the replays reduce everything in finish()
-    assert r["graph_in"]["log"] == ["decoder", "layer_n"] * STEPS
-    assert r["graph_out"]["log"] == ["decoder", "layer_n"]
+    assert r["graph_in"]["log"] == order * STEPS
+    assert r["graph_out"]["log"] == order
     # accumulation: ready points only in the last micro-batch's backward
-    assert r["eager_acc2"]["log"] == ["decoder", "layer_n"] * STEPS
-    assert r["graph_in_acc2"]["log"] == ["decoder", "layer_n"] * STEPS
+    assert r["eager_acc2"]["log"] == order * STEPS
+    assert r["graph_in_acc2"]["log"] == order * STEPS
     assert r["graph_in_acc2"]["captures"] == 2 and r["graph_in_acc2"]["replays"] == 2 * (STEPS - 1)
     # disjoint buckets covering the whole flat buffer
     bk = sorted(r["eager"]["buckets"])
@@ -283,5 +285,5 @@ def test_reducer_protocol_fails_loudly_on_stale_launch():
     mp.spawn(_worker_protocol, args=(world, port, out), nprocs=world, join=True)
     for r in range(world):
         assert out[r]["disarmed_launches"] == 0
-        assert out[r]["armed_launches"] == 2
+        assert out[r]["armed_launches"] == 3  # decoder, layer_n, layer_1_sa
         assert "never finished" in out[r]["stale"]

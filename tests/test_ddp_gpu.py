@@ -103,8 +103,8 @@ def test_two_ranks_graph_steps_bitwise_in_sync():
         assert g["sync"] == 0.0 and e["sync"] == 0.0
         assert not g["in_graph"]  # gloo: the collectives run after the replayed backward
         assert g["replays"] == STEPS - 2  # 2 eager warm-up steps, then captured steps
-        assert g["log"] == ["decoder", "layer_n"] * 2  # ready points fire in the eager steps only
-        assert e["log"] == ["decoder", "layer_n"] * STEPS
+        assert g["log"] == ["decoder", "layer_n", "layer_1_sa"] * 2  # ready points fire in the eager steps only
+        assert e["log"] == ["decoder", "layer_n", "layer_1_sa"] * STEPS
         assert torch.equal(g["params"], e["params"]), (g["params"] - e["params"]).abs().max()
     assert torch.equal(out[0][True]["params"], out[1][True]["params"])
 
@@ -122,7 +122,7 @@ def test_rccl_collectives_inside_the_step_graph():
         opt, red, eng = _run(model, lambda f: FlatGradReducer(f, in_graph=True, force=True), True, data)
         assert red.enabled and red.in_graph and eng.replays == STEPS - 2
         # eager steps 1, 2 and the capture's backward (the replays run no Python)
-        assert red.launch_log == ["decoder", "layer_n"] * 3
+        assert red.launch_log == ["decoder", "layer_n", "layer_1_sa"] * 3
         red.close()
         ref_model = _setup()
         ref_opt, _, _ = _run(ref_model, None, True, data)
@@ -295,5 +295,58 @@ def test_two_ranks_overlapped_nondeterministic_in_sync():
     mp.spawn(_worker_gloo_overlap, args=(world, port, out), nprocs=world, join=True)
     for r in range(world):
         assert out[r]["bucket"]
-        assert out[r]["log"] == ["decoder", "layer_n"] * 6
+        assert out[r]["log"] == ["decoder", "layer_n", "layer_1_sa"] * 6
         assert out[r]["sync"] == [0.0] * 6, out[r]["sync"]
+
+
+def _worker_probe_failure(port, out):
+    # a fresh process: a 1-rank RCCL group whose all-reduce raises while a capture is open
+    os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      PERCEIVER_DIST_BACKEND="nccl")
+    os.environ.pop("PERCEIVER_GRAPH_COLLECTIVES", None)
+    from perceiver_io_amd.ops.optim import FlatParameterSpace
+    from perceiver_io_amd.parallel import FlatGradReducer, dist
+    from perceiver_io_amd.parallel import dist as pdist
+
+    dist.init()
+    real = pdist.dist.all_reduce
+
+    def failing(t, *a, **k):
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("injected: collective not capturable")
+        return real(t, *a, **k)
+
+    pdist.dist.all_reduce = failing
+    try:
+        ok = pdist.graph_collectives_ok(torch.device("cuda:0"))
+    finally:
+        pdist.dist.all_reduce = real
+    res = dict(ok=ok, capturing=torch.cuda.is_current_stream_capturing())
+    # every stream still usable: a collective and a kernel on a fresh side stream, then a sync
+    side = torch.cuda.Stream()
+    t = torch.ones(32, device="cuda")
+    with torch.cuda.stream(side):
+        res["side_capturing"] = torch.cuda.is_current_stream_capturing()
+        real(t)
+        t.mul_(3.0)
+    torch.cuda.synchronize()
+    res["value"] = float(t[0])
+    flat = FlatParameterSpace([torch.nn.Parameter(torch.ones(16, device="cuda"))], with_shadow=False)
+    red = FlatGradReducer(flat, force=True)  # asks the (cached) probe
+    res["in_graph"] = red.in_graph
+    red.close()
+    out[0] = res
+    dist.shutdown()
+
+
+def test_graph_collectives_probe_capture_failure_fails_closed():
+    """The capture probe's failure branch (dist.graph_collectives_ok): a collective that raises
+    inside the capture leaves no open capture behind, the probe answers False, later work on any
+    stream runs, and a reducer then keeps its collectives outside the graph (in_graph False)."""
+    port = _port()
+    out = mp.get_context("spawn").Manager().dict()
+    mp.spawn(_worker_probe_failure, args=(port, out), nprocs=1, join=True)
+    r = out[0]
+    assert r["ok"] is False and r["in_graph"] is False
+    assert not r["capturing"] and not r["side_capturing"]
+    assert r["value"] == 3.0  # 1-rank all-reduce (x1) then x3

@@ -40,7 +40,7 @@ def _batches(model, steps):
     return out
 
 
-def _run(graph, steps=5):
+def _run(graph, steps=5, ring_view=True):
     from perceiver_io_amd.ops.optim import FusedAdamW
     from perceiver_io_amd.train.engine import StepEngine
 
@@ -55,7 +55,7 @@ def _run(graph, steps=5):
     data = _batches(model, steps)
     losses, snap = [], []
     for s in range(steps):
-        out = eng.step(data[s])
+        out = eng.step(data[s], ring_view=ring_view)
         losses.append(out)
         snap.append(float(out))
     return eng, losses, snap
@@ -71,3 +71,14 @@ def test_replayed_losses_from_the_ring_equal_eager(monkeypatch):
     assert [float(t) for t in graph] == graph_snap
     # the replayed steps' losses are ring slots, not copies of the static output
     assert all(t.data_ptr() != graph[-1].data_ptr() for t in graph[1:-1])
+
+
+def test_default_step_returns_an_independent_loss(monkeypatch):
+    """Without ring_view the caller owns its loss tensor (a copy, like an eager step's): a later
+    step's update kernel rewriting the ring slot cannot change it."""
+    _fused_on_cpu(monkeypatch)
+    eng, graph, snap = _run(True, ring_view=False)
+    assert eng.replays >= 3
+    assert all(t._base is None or t._base is not eng._loss_ring for t in graph)
+    eng._loss_ring.fill_(-1.0)  # what LOSS_RING later steps would do to every slot
+    assert [float(t) for t in graph] == snap

@@ -144,3 +144,27 @@ def test_gpu_count_respects_visible_devices(monkeypatch):
     assert gpu_count() == 3
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
     assert gpu_count() == 0
+
+
+def test_topology_gpu_count_skips_unopenable_render_nodes(tmp_path):
+    """A container that sees only some of the host's render nodes still lists every host GPU in
+    the KFD topology: only nodes with SIMDs whose /dev/dri/renderD<minor> is openable count (the
+    filter ROCr applies), so devices=-1 never starts more ranks than usable GPUs."""
+    import os
+
+    from perceiver_io_amd.parallel.launch import topology_gpu_count
+
+    topo, dri = tmp_path / "nodes", tmp_path / "dri"
+    dri.mkdir()
+    # node 0: the CPU (no SIMDs); nodes 1-4: GPUs with render minors 128..131
+    for i, (simds, minor) in enumerate([(0, 0), (256, 128), (256, 129), (256, 130), (256, 131)]):
+        d = topo / str(i)
+        d.mkdir(parents=True)
+        (d / "properties").write_text(f"cpu_cores_count 0\nsimd_count {simds}\ndrm_render_minor {minor}\n")
+    for minor in (128, 130):  # only two render nodes are present and accessible here
+        (dri / f"renderD{minor}").write_text("")
+    assert topology_gpu_count(str(topo), str(dri)) == 2
+    os.chmod(dri / "renderD130", 0o000)
+    if not os.access(dri / "renderD130", os.R_OK):  # (root ignores the mode bits)
+        assert topology_gpu_count(str(topo), str(dri)) == 1
+    assert topology_gpu_count(str(tmp_path / "missing"), str(dri)) is None
