@@ -1,0 +1,56 @@
+// Argument blocks of the per-sample latent-block kernels (sample_block.hip), shared by the kernel
+// translation unit and the host binding (binding.cpp).  Plain C++ (stdint only).
+#pragma once
+#include <stdint.h>
+
+namespace pio {
+
+constexpr int kSBMaxLayers = 4;  // self-attention layers per block (the image configs run 3)
+
+// one self-attention layer (reference model.py:36-44: x → LN1 → MHA → +x → LN2 → MLP → +) of a
+// C = 128, H = 4 block over N = 32 latents: weights, then the forward's saved rows (every one
+// an operand of the backward or of the weight-gradient GEMMs)
+struct SBLayer {
+  const uint16_t *Wqkv, *Wo, *W1, *W2;         // bf16 [3C][C], [C][C] ×3 (nn.Linear layout)
+  const float *bqkv, *g1, *be1, *bo, *g2, *be2, *b1, *b2;
+  uint16_t *LN1X, *QKV, *O, *LN2Y, *U, *GU;    // bf16 rows: LN1(x), packed QKV, attention out, LN2(y), W1 out, GELU
+  float *Y, *Z, *mean1, *rstd1, *mean2, *rstd2;  // fp32: residual after attention, layer output, LN stats
+};
+struct SBFwdArgs {
+  SBLayer ly[kSBMaxLayers];
+  const float* X0;  // block input rows (B·32, C) fp32
+  int L, B;
+  float scale_log2, eps;
+};
+// backward: the gradient rows the weight-gradient GEMMs need (bf16) and the LayerNorm affine
+// gradient targets (fp32, atomically added)
+struct SBGrad {
+  uint16_t *dQKV, *dY, *dU, *dZ;
+  float *dg1, *dbe1, *dg2, *dbe2;
+};
+struct SBBwdArgs {
+  SBLayer ly[kSBMaxLayers];
+  SBGrad gr[kSBMaxLayers];
+  const float* X0;   // the block input (layer 0's LN1 input)
+  const float* dZ;   // gradient of the block output (B·32, C) fp32
+  float* dX;         // gradient of the block input (B·32, C) fp32 (written)
+  int L, B;
+  float scale_log2, eps;
+};
+// grouped weight-gradient GEMMs: dW[n][k] += Σ_rows G[r][n] · A[r][k], db[n] += Σ_rows G[r][n]
+// (A is 128 wide: every self-attention weight's input); one job per weight
+constexpr int kSBMaxJobs = 4 * kSBMaxLayers;
+struct SBWgradJob {
+  const uint16_t* G;  // bf16 [R][N]
+  const uint16_t* A;  // bf16 [R][128]
+  float* dW;          // fp32 [N][128] (added to)
+  float* db;          // fp32 [N] (added to)
+  int N;              // 128 or 384
+  int tile0;          // first 64-column tile index of this job in the grid
+};
+struct SBWgradArgs {
+  SBWgradJob job[kSBMaxJobs];
+  int njobs, R, rows_per_split;
+};
+
+}  // namespace pio

@@ -1019,11 +1019,15 @@ def _sa_block_plan(block, rows: int):
     return layers, specs, pss, ok
 
 
-def sa_block_lookahead(block, rows: int):
+def sa_block_lookahead(block, rows: int, n: Optional[int] = None, device=None):
     """The (γ1, β1, Wqkv bf16, bqkv) a preceding cross-attention layer can fuse into its
-    post-attention kernel, or None when the block will not run fused."""
-    _, specs, pss, ok = _sa_block_plan(block, rows)
+    post-attention kernel, or None when the block will not run fused (or runs as a per-sample
+    block, which projects its own first layer)."""
+    layers, specs, pss, ok = _sa_block_plan(block, rows)
     if not ok:
+        return None
+    p = specs[0].dropout if layers[0].training else 0.0
+    if n is not None and _sample_block_ok(specs, n, p, device is not None and torch.device(device).type == "cuda"):
         return None
     ps = pss[0]
     return (ps[0], ps[1], _bf16_weights(specs[0], ps)[0], ps[3])
@@ -1053,7 +1057,88 @@ def self_attention_block(block, x):
     bws = tuple(_bf16_weights(sp, ps) for sp, ps in zip(specs, pss))
     flat_ps = [p for ps in pss for p in ps]
     p = specs[0].dropout if layers[0].training else 0.0
+    if _sample_block_ok(specs, x.shape[1], p, x.is_cuda):
+        return _SampleBlockFn.apply(tuple(specs), bws, x, *flat_ps)
     return _SABlockFn.apply(tuple(specs), bws, _seed(p, x.device), p, x, *flat_ps)
+
+
+# the image configs' latent blocks (C = 128, H = 4, 32 latents, no dropout): one workgroup per
+# sample runs every layer of the block, forward and backward (csrc/sample_block.hip), plus one
+# grouped weight-gradient GEMM launch; PERCEIVER_SAMPLE_BLOCK=0 keeps the per-layer kernels
+SAMPLE_BLOCK = os.environ.get("PERCEIVER_SAMPLE_BLOCK", "1") != "0"
+
+
+def _sample_block_ok(specs, n: int, p: float, cuda: bool) -> bool:
+    from . import deterministic
+
+    sp = specs[0]
+    return (SAMPLE_BLOCK and cuda and sp.C == 128 and sp.heads == 4 and n == 32 and p == 0.0 and not sp.cross
+            and 1 <= len(specs) <= 4 and all(s == sp for s in specs) and not deterministic())
+
+
+class _SampleBlockFn(torch.autograd.Function):
+    """A C = 128, 32-latent self-attention block as per-sample kernels (reference model.py:36-44):
+    forward saves, per layer, the rows the backward and the weight-gradient GEMMs read (LN1(x),
+    QKV, O, LN2(y), u, GELU(u) in bf16; y, z and the LayerNorm statistics in fp32); backward runs
+    the per-sample backward (activation gradients + LayerNorm affine gradients) and one grouped
+    GEMM launch for every weight / bias gradient of the block."""
+
+    @staticmethod
+    def forward(ctx, specs, bws, x, *ps):
+        K = kernels(x)
+        B, N, C = x.shape
+        L = len(specs)
+        xl = x.reshape(B * N, C)
+        if not xl.is_contiguous():
+            xl = xl.contiguous()
+        params = []
+        for i in range(L):
+            p = ps[SA_NP * i:SA_NP * (i + 1)]
+            wq, _, wo, w1, w2 = bws[i]
+            params += [p[0], p[1], wq, p[3], wo, p[5], p[6], p[7], w1, p[9], w2, p[11]]
+        scale = 1.0 / math.sqrt(C // specs[0].heads)
+        saved = K.sb_fwd(xl, params, scale, EPS)
+        z = saved[12 * (L - 1) + 7]
+        # the block output is not a backward operand: a placeholder in its slot
+        ctx.save_for_backward(xl, *saved[:12 * (L - 1) + 7], xl, *saved[12 * (L - 1) + 8:])
+        ctx.params, ctx.ps, ctx.dims = params, ps, (B, N, C, L, scale)
+        return z.view(B, N, C)
+
+    @staticmethod
+    def backward(ctx, dz):
+        K = kernels(dz)
+        B, N, C, L, scale = ctx.dims
+        xl, *saved = ctx.saved_tensors
+        ps = ctx.ps
+        dz2 = dz.reshape(B * N, C)
+        if not dz2.is_contiguous():
+            dz2 = dz2.contiguous()
+        scratch = []
+
+        def target(p, n):
+            g = _grad_of(p)
+            if g is None:
+                g = torch.zeros(n, device=dz.device, dtype=torch.float32)
+                scratch.append(g)
+            return g.view(-1)
+
+        ln = []
+        for i in range(L):
+            p = ps[SA_NP * i:SA_NP * (i + 1)]
+            ln += [target(p[0], C), target(p[1], C), target(p[6], C), target(p[7], C)]
+        out = K.sb_bwd(dz2, xl, saved, ctx.params, ln, scale, EPS)
+        jobs = []
+        for i in range(L):
+            p = ps[SA_NP * i:SA_NP * (i + 1)]
+            dq, dy, du, dzz = out[1 + 4 * i:5 + 4 * i]
+            sv = saved[12 * i:12 * (i + 1)]
+            for G, A, W, b in ((dq, sv[0], p[2], p[3]), (dy, sv[2], p[4], p[5]), (du, sv[3], p[8], p[9]),
+                               (dzz, sv[5], p[10], p[11])):
+                if W.requires_grad or b.requires_grad:
+                    jobs += [G, A, target(W, W.numel()), target(b, b.numel())]
+        if jobs:
+            K.sb_wgrad(jobs)
+        return (None, None, out[0].view(B, N, C)) + (None,) * len(ps)
 
 
 def _seed(p: float, device) -> Optional[torch.Tensor]:
@@ -1185,7 +1270,7 @@ def _encode(encoder, src: KVSource, pad_mask):
         if lat.shape[0] == 1 and not can_fuse(cross, src):
             lat = lat.expand(b, -1, -1)
         # the block's first LN1 + QKV projection rides on the cross layer's post-attention kernel
-        _LOOKAHEAD["want"] = sa_block_lookahead(block, b * n) if can_fuse(cross, src) else None
+        _LOOKAHEAD["want"] = sa_block_lookahead(block, b * n, n, lat.device) if can_fuse(cross, src) else None
         try:
             lat = cross_attention_layer(cross, lat, src, pad_mask)
         finally:

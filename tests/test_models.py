@@ -294,7 +294,7 @@ def test_cross_self_attention_boundary_fusion(latents, monkeypatch):
         with monkeypatch.context() as mp:
             mp.setattr(ops.fused, "kernels", lambda t: Counting())
             if not fuse:
-                mp.setattr(ops.fused, "sa_block_lookahead", lambda block, rows: None)
+                mp.setattr(ops.fused, "sa_block_lookahead", lambda block, rows, *a: None)
                 mp.setattr(ops.fused, "cross_q_lookahead", lambda cross, src: None)
             calls.clear()
             enc.zero_grad(set_to_none=True)
