@@ -57,7 +57,6 @@ int persist_sync_words(int);
 // sizes of the structs above as the kernel translation units see them (checked at import: a
 // mirror that drifts from common.h / attention.hip would hand the kernels garbage pointers)
 int abi_struct_size(int which);
-bool chain_enabled();
 void attn_fwd_launch(const AttnArgs&, int, uint16_t*, float*, float*, float*, int, hipStream_t);
 void attn_bwd_launch(const AttnArgs&, int, const uint16_t*, const uint16_t*, const float*, float*, float*, long long,
                      int, float*, long long, int, float*, long long, int, bool, bool, long long, int, int, hipStream_t);
@@ -474,7 +473,7 @@ std::vector<Tensor> sa_layer_fwd(Tensor qkv, Tensor x, int64_t N, double scale, 
                            next ? bfp(*wq) : nullptr, next ? f32p(*bq) : nullptr, next ? bfp_mut(qn) : nullptr,
                            next ? m1.data_ptr<float>() : nullptr, next ? r1.data_ptr<float>() : nullptr,
                            make_drop(seed, site, p), nq, stream());
-  TORCH_CHECK(launched, "sa_layer_fwd: N > 256 needs the chain kernel (16-byte aligned operands)");
+  TORCH_CHECK(launched, "sa_layer_fwd: every operand must be 16-byte aligned");
   if (next) return {o, lse, z, y, m, r, u, qn, m1, r1};
   return {o, lse, z, y, m, r, u};
 }
@@ -1694,7 +1693,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("post_attn_fwd", &post_attn_fwd, py::arg("o"), py::arg("x"), py::arg("wo"), py::arg("bo"), py::arg("g2"),
         py::arg("be2"), py::arg("eps"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("b2"),
         py::arg("seed") = py::none(), py::arg("site") = 0, py::arg("p") = 0.0);
-  m.def("chain_enabled", &pio::chain_enabled, "register-resident chain kernels in use (PIO_CHAIN != 0)");
   m.def("sa_layer_fwd", &sa_layer_fwd, py::arg("qkv"), py::arg("x"), py::arg("N"), py::arg("scale"), py::arg("wo"),
         py::arg("bo"), py::arg("g2"), py::arg("be2"), py::arg("eps"), py::arg("w1"), py::arg("b1"), py::arg("w2"),
         py::arg("b2"), py::arg("lnw") = py::none(), py::arg("lnb") = py::none(), py::arg("wq") = py::none(),

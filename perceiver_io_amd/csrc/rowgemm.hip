@@ -689,139 +689,6 @@ __global__ __launch_bounds__(256) void post_attn_ln_linear_fwd_kernel(
 }
 
 // ------------------------------------------------------------------------------------
-// Fused latent self-attention layer forward (C = 64, H = 4, D = 16, N ≤ 256 latents with
-// N % 64 == 0, no attention dropout): ONE launch per layer instead of attn_fwd +
-// post_attn(_ln_linear)_fwd.  A workgroup owns a 64-row tile (64 queries of one batch element):
-//   phase 0  every operand load in flight together — K fragments straight from global (the
-//            A operand of Sᵀ = K·Qᵀ is one 16-byte row piece per lane), Q fragments, the batch
-//            element's V rows (→ LDS), the post-attention weights / residual / bias vectors and
-//            the next layer's LN1 affine and first QKV weight chunk;
-//   attention wave h = head h: per 32-query block all N keys at once (N/32 MFMAs, one max, one
-//            fma + exp2 per score, no online rescaling), Oᵀ += Vᵀ·Pᵀ straight from the
-//            accumulators (Vᵀ by transposed LDS reads of the all-head V tile; the rows past the
-//            head's 16 columns are never used), O → LDS tile (and to global for the backward),
-//            LSE (log2 units);
-//   then the post-attention block on the LDS O tile and (NEXT) LN1 + QKV of the next layer —
-// the attention output never makes a global round trip before its consumer.
-// ------------------------------------------------------------------------------------
-template <bool NEXT, bool AV, int NQ = 3>
-__global__ __launch_bounds__(256) void sa_layer_fwd_kernel(
-    const uint16_t* __restrict__ QKV, int N, float scale_log2, uint16_t* __restrict__ Oout, float* __restrict__ LSE,
-    const float* __restrict__ X, const uint16_t* __restrict__ Wo, const float* __restrict__ bo,
-    const float* __restrict__ g2, const float* __restrict__ be2, float eps, const uint16_t* __restrict__ W1,
-    const float* __restrict__ b1, const uint16_t* __restrict__ W2, const float* __restrict__ b2, float* __restrict__ Z,
-    float* __restrict__ Ysave, float* __restrict__ mean2, float* __restrict__ rstd2, uint16_t* __restrict__ Usave, int R,
-    const float* __restrict__ lnw, const float* __restrict__ lnb, const uint16_t* __restrict__ Wq,
-    const float* __restrict__ bq, uint16_t* __restrict__ QKVn, float* __restrict__ mean1, float* __restrict__ rstd1,
-    DropCfg dr) {
-  // NQ·C: width of the next projection (3C: the next self-attention layer's packed QKV; C: the
-  // query projection of a following cross-attention layer; 2C: the K/V projection of a decoder
-  // cross-attention over this block's output)
-  constexpr int C = 64, H = 4, D = 16, NCH = 2, KP = 64, LD = C + 8, LDV = C + 8, C3 = 3 * C, MAXKT = 8;
-  constexpr int nq = NQ * C;
-  __shared__ __attribute__((aligned(16))) uint16_t sV[256 * LDV + 64];  // V rows of the batch element (+ overrun)
-  __shared__ __attribute__((aligned(16))) uint16_t sO[64 * LD];
-  __shared__ __attribute__((aligned(16))) uint16_t smem[NEXT ? ln_linear_fwd_smem<NCH>() / 2 : 8];
-  const int w = wave_id(), l = lane_id(), hh = l >> 5, r = l & 31;
-  const int m0 = blockIdx.x * 64;
-  const int b = m0 / N;
-  const long long rb = (long long)b * N;  // first row of the batch element
-  const int nkt = N / 32;
-  const int h = w;
-  const uint16_t* zp = reinterpret_cast<const uint16_t*>(kZero32B);
-
-  // ---- phase 0: every load issued, branch-free (address selects) ----
-  bf16x8 kf[MAXKT], qf[2], vr[8];
-#pragma unroll
-  for (int kt = 0; kt < MAXKT; ++kt)
-    kf[kt] = *reinterpret_cast<const bf16x8*>(kt < nkt ? QKV + (rb + 32 * kt + r) * C3 + C + h * D + 8 * hh : zp);
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb)
-    qf[qb] = *reinterpret_cast<const bf16x8*>(QKV + (long long)(m0 + 32 * qb + r) * C3 + h * D + 8 * hh);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {  // 256 keys × 8 pieces of 16 bytes: key c >> 3, columns (c & 7)·8
-    const int c = threadIdx.x + 256 * i, key = c >> 3, col = (c & 7) * 8;
-    vr[i] = *reinterpret_cast<const bf16x8*>(key < N ? QKV + (rb + key) * C3 + 2 * C + col : zp);
-  }
-  PaPre<C> pre;
-  post_attn_fwd_prefetch<C, AV>(pre, X, Wo, bo, g2, be2, W1, b1, W2, b2, R, R);
-  bf16x8 wb[NCH];
-  float gw[NCH][8], gb[NCH][8];
-  if constexpr (NEXT) {
-    tile_fetch<NCH>(wb, Wq, C, 0, nq, 64, C, KP, AV);
-    row_load<NCH>(gw, lnw, 0, 0, 1, C, AV);
-    row_load<NCH>(gb, lnb, 0, 0, 1, C, AV);
-  }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int c = threadIdx.x + 256 * i, key = c >> 3, col = (c & 7) * 8;
-    *reinterpret_cast<bf16x8*>(sV + key * LDV + col) = vr[i];
-  }
-  lds_sync();
-
-  // ---- attention: wave h, two 32-query blocks ----
-#pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
-    f32x16 s[MAXKT];
-    float mt = -INFINITY;
-#pragma unroll
-    for (int kt = 0; kt < MAXKT; ++kt) {
-      s[kt] = f32x16{};
-      if (kt < nkt) {  // wave-uniform
-        s[kt] = mfma32(kf[kt], qf[qb], s[kt]);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) mt = fmaxf(mt, s[kt][i]);
-      }
-    }
-    const float m = xor32_max(mt) * scale_log2;
-    float ls = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < MAXKT; ++kt)
-      if (kt < nkt) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          s[kt][i] = fast_exp2(fmaf(s[kt][i], scale_log2, -m));
-          ls += s[kt][i];
-        }
-      }
-    ls = xor32_sum(ls);
-    f32x16 o = f32x16{};
-#pragma unroll
-    for (int kt = 0; kt < MAXKT; ++kt)
-      if (kt < nkt) {
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss)
-          o = mfma32(frag_ks_perm(sV, LDV, h * D, 32 * kt + 16 * ss), pack_acc(s[kt], ss), o);
-      }
-    // Oᵀ: column = query (lane), rows = head dims acc_row(i, hh) (< 16 for i < 8)
-    const float inv = 1.f / ls;
-    const int row = 32 * qb + r;
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-      uint2 pk;
-      pk.x = pack2(o[4 * g] * inv, o[4 * g + 1] * inv);
-      pk.y = pack2(o[4 * g + 2] * inv, o[4 * g + 3] * inv);
-      *reinterpret_cast<uint2*>(sO + row * LD + h * D + 8 * g + 4 * hh) = pk;
-    }
-    if (hh == 0) LSE[(long long)(m0 + row) * H + h] = m + __log2f(ls);
-  }
-  lds_sync();
-  // the O tile for the backward: 64 rows × 128 bytes, 16-byte row stores
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int c = threadIdx.x + 256 * i, row = c >> 3, col = (c & 7) * 8;
-    *reinterpret_cast<bf16x8*>(Oout + (long long)(m0 + row) * C + col) =
-        *reinterpret_cast<const bf16x8*>(sO + row * LD + col);
-  }
-  float z[NCH][8];
-  post_attn_fwd_body<C, AV, true>(nullptr, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, R,
-                                  dr, z, pre, sO);
-  if constexpr (NEXT)
-    ln_linear_fwd_tile<uint16_t, NCH, AV>(z, wb, gw, gb, true, m0, R, C, eps, Wq, C, bq, nq, 0, nullptr, 0, QKVn, nq,
-                                          mean1, rstd1, smem);
-}
-
-// ------------------------------------------------------------------------------------
 // activation tile staging with the forward transform re-applied on load:
 // mode 0 plain, 1 LayerNorm (row stats + affine), 2 GELU.  Rows ≥ R and cols ≥ Kin are zero.
 // ------------------------------------------------------------------------------------
@@ -1496,9 +1363,6 @@ bool ln_linear_post_attn_bwd_chain_launch(const void* G, bool g_bf16, const uint
                                           const float* be2, float* dY, uint16_t* dO, float* delta,
                                           const PostAttnGrads& grads, int R, const SlabJob& job, const DropCfg& dr,
                                           int nq, hipStream_t st);
-static bool use_chain() { return true; }
-bool chain_enabled() { return use_chain(); }
-
 static bool av_ok(std::initializer_list<const void*> ptrs, std::initializer_list<long long> widths) {
   for (const void* p : ptrs)
     if (!al16(p)) return false;
@@ -1596,39 +1460,18 @@ void post_attn_ln_linear_fwd_launch(int C, const uint16_t* O, const float* X, co
 #undef PLF
 }
 
-// fused self-attention layer forward (C = 64, H = 4): see sa_layer_fwd_kernel; NEXT = Wq != nullptr
-// false (nothing launched) for N > 256 when the chain kernel cannot take the operands
+// fused self-attention layer forward (C = 64, H = 4): the chain kernel (chain.hip
+// sa_layer_fwd_chain8_kernel); false (nothing launched) when the operands do not qualify (every
+// pointer 16-byte aligned, N <= 512) — the binding turns that into an error
 bool sa_layer_fwd_launch(const uint16_t* QKV, int N, float scale_log2, uint16_t* O, float* LSE, const float* X,
                          const uint16_t* Wo, const float* bo, const float* g2, const float* be2, float eps,
                          const uint16_t* W1, const float* b1, const uint16_t* W2, const float* b2, float* Z,
                          float* Ysave, float* mean2, float* rstd2, uint16_t* Usave, int R, const float* lnw,
                          const float* lnb, const uint16_t* Wq, const float* bq, uint16_t* QKVn, float* mean1,
                          float* rstd1, const DropCfg& dr, int nq, hipStream_t st) {
-  const bool next = Wq != nullptr;
   const bool av = av_ok({QKV, O, X, Wo, W1, W2, Z, Ysave, Usave, Wq, lnw, lnb, QKVn}, {});
-  dim3 grid(R / 64);
-  if (av && use_chain() &&
-      sa_layer_fwd_chain_launch(QKV, N, scale_log2, O, LSE, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2,
-                                rstd2, Usave, R, lnw, lnb, Wq, bq, QKVn, mean1, rstd1, dr, nq, st))
-    return true;
-  if (N > 256) return false;  // the 4-wave kernel holds at most 256 keys
-#define SAL(NX, A)                                                                                                 \
-  if (nq == 64) hipLaunchKernelGGL((sa_layer_fwd_kernel<NX, A, 1>), grid, dim3(256), 0, st, QKV, N, scale_log2, O, LSE, X, \
-                                   Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, lnw, lnb, Wq, bq, \
-                                   QKVn, mean1, rstd1, dr);                                                            \
-  else if (nq == 128) hipLaunchKernelGGL((sa_layer_fwd_kernel<NX, A, 2>), grid, dim3(256), 0, st, QKV, N, scale_log2, O,  \
-                                         LSE, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R,  \
-                                         lnw, lnb, Wq, bq, QKVn, mean1, rstd1, dr);                                    \
-  else hipLaunchKernelGGL((sa_layer_fwd_kernel<NX, A>), grid, dim3(256), 0, st, QKV, N, scale_log2, O, LSE, X, Wo, bo,   \
-                          g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, lnw, lnb, Wq, bq, QKVn, mean1,  \
-                          rstd1, dr)
-  if (next) {
-    if (av) SAL(true, true); else SAL(true, false);
-  } else {
-    if (av) SAL(false, true); else SAL(false, false);
-  }
-#undef SAL
-  return true;
+  return av && sa_layer_fwd_chain_launch(QKV, N, scale_log2, O, LSE, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave,
+                                         mean2, rstd2, Usave, R, lnw, lnb, Wq, bq, QKVn, mean1, rstd1, dr, nq, st);
 }
 
 void post_attn_bwd_launch(int C, const float* dZ, const float* Ysave, const float* mean2, const float* rstd2,
@@ -1662,7 +1505,7 @@ bool ln_linear_post_attn_bwd_launch(int C, const void* Gv, bool g_bf16, const ui
   dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0));
   const float* G = static_cast<const float*>(Gv);
   const bool av = av_ok({Gv, Wq, X, lnw, lnb, dres, Ysave, U, O, Wo, W1, W2, dY, dO}, {});
-  if (av && C == 64 && H == 4 && grads.slab && (R % 64) == 0 && use_chain() &&
+  if (av && C == 64 && H == 4 && grads.slab && (R % 64) == 0 &&
       ln_linear_post_attn_bwd_chain_launch(Gv, g_bf16, Wq, X, mean1, rstd1, lnw, lnb, dres, dlnw, dlnb, dWq, dbq, Ysave,
                                            mean2, rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO, delta, grads, R, job, dr, nq,
                                            st))

@@ -245,7 +245,7 @@ def _acc(t, v):
 
 def sa_layer_fwd(qkv, x, N, scale, wo, bo, g2, be2, eps, w1, b1, w2, b2, lnw=None, lnb=None, wq=None, bq=None,
                  seed=None, site=0, p=0.0):
-    """The fused self-attention layer forward (rowgemm.hip sa_layer_fwd_kernel): attention of the
+    """The fused self-attention layer forward (chain.hip sa_layer_fwd_chain8_kernel): attention of the
     packed qkv (C = 64, H = 4, no attention dropout), then the post-attention block and, when the
     next layer's LN1 / in-projection are given, its QKV."""
     C, H = 64, 4

@@ -768,7 +768,7 @@ class _LayerFn(torch.autograd.Function):
         return (None, None, None, None, None, dx_q, dx_kv, None) + (None,) * len(ps)
 
 
-# the fused latent self-attention layer forward (rowgemm.hip sa_layer_fwd_kernel);
+# the fused latent self-attention layer forward (chain.hip sa_layer_fwd_chain8_kernel);
 # PERCEIVER_SA_LAYER_FUSED=0 restores attn_fwd + post_attn(_ln_linear)_fwd
 SA_LAYER_FUSED = True
 PA_SIZES = lambda C: [C * C, C, C, C, C * C, C, C * C, C]  # noqa: E731  (Wo bo γ2 β2 W1 b1 W2 b2)
@@ -934,8 +934,8 @@ class _SABlockFn(torch.autograd.Function):
         # dQKV of layers 1..L-1 feeds the chain-layout boundary kernel, which reads it as bf16
         # MFMA operands only: the attention backward stores it as bf16 (half the bytes both
         # ways, identical results) when it writes every element once (zp == 0: one key block)
-        g_bf16 = (BF16_DQKV and K is not emulation and zp == 0 and C == 64 and H == 4 and R % 64 == 0 and 64 < N <= 256
-                  and K.chain_enabled())
+        g_bf16 = (BF16_DQKV and K is not emulation and zp == 0 and C == 64 and H == 4 and R % 64 == 0
+                  and 64 < N <= 256)
 
         def new_dqkv(i):  # every column block is written (or accumulated onto a cleared buffer) by attn_bwd
             if g_bf16 and i > 0:
