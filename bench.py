@@ -8,7 +8,7 @@ bf16 compute.  Synthetic token ids of that shape, random-init weights (no networ
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, RCCL)
-    python bench.py --config {mlm256,seq_clf,imagenet,long_mlm,mnist,lartpc} ...
+    python bench.py --config {mlm256,seq_clf,seq_clf_ft,imagenet,long_mlm,mnist,lartpc} ...
 
 Other configs (BASELINE.json configs 1, 3-5): ``seq_clf`` = IMDB text classifier with a frozen
 encoder (decoder-only training, batch 128/GPU, README seq_clf command); ``imagenet`` =
@@ -42,6 +42,9 @@ CONFIGS = {
     "mlm256": dict(batch=64, seq_len=512, latents=256, channels=64, metric=HEADLINE_METRIC),
     "seq_clf": dict(batch=128, seq_len=512, latents=64, channels=64,
                     metric="samples/sec (whole node) IMDB seq_clf frozen encoder seq_len=512"),
+    # the README's joint fine-tune (README.md:91-107): encoder unfrozen, dropout 0.1, lr 1e-4
+    "seq_clf_ft": dict(batch=128, seq_len=512, latents=64, channels=64,
+                       metric="samples/sec (whole node) IMDB seq_clf joint fine-tune dropout 0.1 seq_len=512"),
     "imagenet": dict(batch=32, seq_len=224 * 224, latents=32, channels=128,
                      metric="samples/sec (whole node) ImageNet-shape 224x224x3 img_clf Fourier PE"),
     "long_mlm": dict(batch=8, seq_len=8192, latents=512, channels=64,
@@ -158,13 +161,15 @@ def build(args, device):
 
         desc = f"perceiver-io-mlm latents={args.latents}x{args.channels} layers=3x(1+6) vocab={args.vocab}"
         return lit, loss_fn, make_batch, desc, 3e-3, 0.0
-    if args.config == "seq_clf":
+    if args.config in ("seq_clf", "seq_clf_ft"):
+        ft = args.config == "seq_clf_ft"
+        lr, wd = (1e-4, 0.01) if ft else (1e-3, 0.01)
         lit = LitTextClassifier(
-            num_classes=2, vocab_size=args.vocab, max_seq_len=L, freeze_encoder=True,
-            optimizer_init=_opt(1e-3, 0.01), scheduler_init=None, num_latents=args.latents,
+            num_classes=2, vocab_size=args.vocab, max_seq_len=L, freeze_encoder=not ft,
+            optimizer_init=_opt(lr, wd), scheduler_init=None, num_latents=args.latents,
             num_latent_channels=args.channels, num_encoder_layers=3, num_encoder_cross_attention_heads=4,
             num_encoder_self_attention_heads=4, num_encoder_self_attention_layers_per_block=6,
-            num_decoder_cross_attention_heads=1, dropout=0.0)
+            num_decoder_cross_attention_heads=1, dropout=0.1 if ft else 0.0)
         model = lit.model
 
         def loss_fn(batch):  # = cross_entropy(model(ids, pad), y); fused head on the HIP backend
@@ -175,9 +180,9 @@ def build(args, device):
             ids = torch.randint(3, args.vocab, (B, L), generator=g)
             return (torch.randint(0, 2, (B,), generator=g), ids, torch.zeros(B, L, dtype=torch.bool))
 
-        desc = (f"perceiver-io-seq-clf frozen-encoder latents={args.latents}x{args.channels} layers=3x(1+6) "
-                f"vocab={args.vocab}")
-        return lit, loss_fn, make_batch, desc, 1e-3, 0.01
+        desc = (f"perceiver-io-seq-clf {'joint-fine-tune dropout=0.1' if ft else 'frozen-encoder'} "
+                f"latents={args.latents}x{args.channels} layers=3x(1+6) vocab={args.vocab}")
+        return lit, loss_fn, make_batch, desc, lr, wd
     # image classifiers
     if args.config == "imagenet":
         side = int(round(args.seq_len ** 0.5))

@@ -51,7 +51,6 @@ bool sb_bwd_launch(const SBBwdArgs&, hipStream_t);
 bool sb_wgrad_launch(SBWgradArgs, hipStream_t);
 bool sa_block_fwd_launch(const SABlockFwdArgs&, hipStream_t);
 unsigned persist_errors(bool);
-void persist_debug(unsigned long long*);
 int persist_sync_words(int);
 
 // sizes of the structs above as the kernel translation units see them (checked at import: a
@@ -567,11 +566,6 @@ std::vector<Tensor> sa_block_fwd(Tensor qkv0, Tensor x0, int64_t N, double scale
 }
 
 unsigned persist_errors(bool reset) { return pio::persist_errors(reset); }
-std::vector<int64_t> persist_debug() {
-  unsigned long long v[8];
-  pio::persist_debug(v);
-  return std::vector<int64_t>(v, v + 8);
-}
 
 // ---- per-sample latent-block kernels (csrc/sample_block.hip): C = 128, H = 4, N = 32 ----
 namespace {
@@ -1706,7 +1700,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sb_bwd", &sb_bwd, py::arg("dz"), py::arg("x0"), py::arg("saved"), py::arg("params"), py::arg("ln_grads"),
         py::arg("scale"), py::arg("eps"));
   m.def("sb_wgrad", &sb_wgrad, py::arg("jobs"));
-  m.def("persist_debug", &persist_debug);
   m.def("post_attn_ln_linear_fwd", &post_attn_ln_linear_fwd, py::arg("o"), py::arg("x"), py::arg("wo"), py::arg("bo"),
         py::arg("g2"), py::arg("be2"), py::arg("eps"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("b2"),
         py::arg("lnw"), py::arg("lnb"), py::arg("wq"), py::arg("bq"), py::arg("seed") = py::none(),

@@ -14,7 +14,7 @@ namespace pio {
 // post-attention chain: the paired CL2 layout above (5 pair exchanges: LN2, W1, W2, LN1, Wq).
 // MAXKT: 32-key tiles of the K / V operand (8: N ≤ 256, 16: N ≤ 512 — the long-context MLM's
 // 512 latents; every K fragment is loaded in phase 0, the V rows of the batch element live in LDS).
-template <bool NEXT, int NQ, int MAXKT>
+template <bool NEXT, int NQ, int MAXKT, bool ADROP>
 __global__ __launch_bounds__(512) void sa_layer_fwd_chain8_kernel(
     const uint16_t* __restrict__ QKV, int N, float scale_log2, uint16_t* __restrict__ Oout, float* __restrict__ LSE,
     const float* __restrict__ X, const uint16_t* __restrict__ Wo, const float* __restrict__ bo,
@@ -114,7 +114,7 @@ __global__ __launch_bounds__(512) void sa_layer_fwd_chain8_kernel(
   // Σ_k P[k][q] — no per-element VALU sum (and the denominator of exactly the bf16 P that
   // weights V) ----
   {
-    float m_run = -INFINITY;
+    float m_run = -INFINITY, l_run = 0.f;
     f32x16 o = f32x16{};
 #pragma unroll
     for (int ch = 0; ch < MAXKT / 4; ++ch) {
@@ -135,11 +135,26 @@ __global__ __launch_bounds__(512) void sa_layer_fwd_chain8_kernel(
         const float alpha = fast_exp2(m_run - m_new);  // 0 on the first chunk
 #pragma unroll
         for (int i = 0; i < 16; ++i) o[i] *= alpha;
+        if constexpr (ADROP) l_run *= alpha;
 #pragma unroll
         for (int k = 0; k < 4; ++k)
           if (4 * ch + k < nkt) {
 #pragma unroll
             for (int i = 0; i < 16; ++i) sc[k][i] = fast_exp2(fmaf(sc[k][i], scale_log2, -m_new));
+            if constexpr (ADROP) {
+              // attention-probability dropout (reference model.py:66-71, nn.MultiheadAttention's
+              // dropout): the softmax denominator sums the kept AND the dropped probabilities, the
+              // P·V product sees P∘mask/(1−p); masks as attn_bwd regenerates them (stream b·H + h,
+              // element q·N + key of the sample)
+              const uint32_t dkey = drop_key(dr.seed, dr.site, 2u);
+#pragma unroll
+              for (int i = 0; i < 16; ++i) {
+                l_run += sc[k][i];
+                const uint32_t key = 32 * (4 * ch + k) + acc_row(i, hh);
+                const uint32_t idx = (uint32_t)(m0 - rb + 32 * qb + r) * (uint32_t)N + key;
+                sc[k][i] = keep_elem(dkey, (uint32_t)(b * H + h), idx, dr.thresh) ? sc[k][i] * dr.scale : 0.f;
+              }
+            }
           }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -154,7 +169,9 @@ __global__ __launch_bounds__(512) void sa_layer_fwd_chain8_kernel(
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    const float ls = o[8];  // row 16 (a ones row): Σ_k P[k][q] of this lane's query
+    // row 16 (a ones row): Σ_k P[k][q] of this lane's query; with dropout the explicit sum of the
+    // undropped probabilities (the ones rows summed the dropped ones)
+    const float ls = ADROP ? xor32_sum(l_run) : o[8];
     const float inv = 1.f / ls;
     const int row = 32 * qb + r;
 #pragma unroll
@@ -554,10 +571,15 @@ bool sa_layer_fwd_chain_launch(const uint16_t* QKV, int N, float scale_log2, uin
   if (next && nq != 64 && nq != 128 && nq != 192) return false;
   if (N > 512) return false;
   dim3 grid(R / 64);
-#define SAC(NX, NQ, KT)                                                                                                 \
-  hipLaunchKernelGGL((sa_layer_fwd_chain8_kernel<NX, NQ, KT>), grid, dim3(512), 0, st, QKV, N, scale_log2, O, LSE, X, Wo, \
-                     bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, lnw, lnb, Wq, bq, QKVn, mean1,  \
-                     rstd1, dr)
+#define SAC(NX, NQ, KT)                                                                                                  \
+  if (dr.thresh)                                                                                                         \
+    hipLaunchKernelGGL((sa_layer_fwd_chain8_kernel<NX, NQ, KT, true>), grid, dim3(512), 0, st, QKV, N, scale_log2, O, LSE, \
+                       X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, lnw, lnb, Wq, bq, QKVn,  \
+                       mean1, rstd1, dr);                                                                                \
+  else                                                                                                                   \
+    hipLaunchKernelGGL((sa_layer_fwd_chain8_kernel<NX, NQ, KT, false>), grid, dim3(512), 0, st, QKV, N, scale_log2, O,    \
+                       LSE, X, Wo, bo, g2, be2, eps, W1, b1, W2, b2, Z, Ysave, mean2, rstd2, Usave, R, lnw, lnb, Wq, bq,  \
+                       QKVn, mean1, rstd1, dr)
 #define SAK(KT)              \
   if (!next) {               \
     SAC(false, 3, KT);       \

@@ -25,14 +25,14 @@
 // buffer that is zero before every launch: the LAST workgroup to finish (arrival count) resets
 // them for the next launch on the stream.  No memset node (a hipMemsetAsync issued during stream
 // capture is not replayed on this stack: measured, tools/persist_diag2.py) and no extra launch.
+#include <cstdlib>
+
 #include "chain_cl.h"
 #include "persist_args.h"
 
 namespace pio {
 
 static __device__ unsigned pio_persist_err;  // sticky: bit 0 = a bounded spin timed out, bit 1 = bad ticket
-// what workgroup 0 of the latest launch saw (diagnostics: persist_debug)
-static __device__ unsigned long long pio_persist_dbg[8];
 
 unsigned persist_errors(bool reset) {
   unsigned h = 0;
@@ -42,9 +42,6 @@ unsigned persist_errors(bool reset) {
     (void)hipMemcpyToSymbol(HIP_SYMBOL(pio_persist_err), &z, sizeof(z), 0, hipMemcpyHostToDevice);
   }
   return h;
-}
-void persist_debug(unsigned long long* out) {
-  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(pio_persist_dbg), sizeof(pio_persist_dbg), 0, hipMemcpyDeviceToHost);
 }
 
 // buffer descriptor over [p, p + bytes) from wave-uniform values (kernel arguments)
@@ -105,7 +102,10 @@ __device__ __forceinline__ void publish_count(unsigned* p) {
 // Forward: per layer exactly the math of sa_layer_fwd_chain8_kernel<NEXT, NQ, MAXKT> (chain.hip),
 // so the block's outputs are bitwise those of the per-layer launches.
 // ------------------------------------------------------------------------------------
-template <int MAXKT>
+// KLDS: the sample's K rows are staged in LDS once per workgroup (as V is) and every wave reads
+// its head's fragments from there — the two query-block waves of a head no longer both fetch the
+// head's K through the memory system (64 → 32 KB of K loads per workgroup and layer)
+template <int MAXKT, bool KLDS, bool ADROP>
 __global__ __launch_bounds__(512) void sa_block_fwd_kernel(SABlockFwdArgs a) {
   constexpr int C = 64, H = 4, D = 16, LD = C + 8, LDV = C + 8, C3 = 3 * C, NT = 512;
   constexpr int NVI = MAXKT * 32 * 8 / NT;  // 16-byte V chunks per thread
@@ -113,6 +113,7 @@ __global__ __launch_bounds__(512) void sa_block_fwd_kernel(SABlockFwdArgs a) {
   constexpr int NWR = 6 * C;                // weight rows staged: Wo, W1, W2 | up to 3C rows of Wq
   constexpr int NWC = NWR * 8 / NT;         // 16-byte weight chunks per thread
   __shared__ __attribute__((aligned(16))) uint16_t sV[MAXKT * 32 * LDV + 64];
+  __shared__ __attribute__((aligned(16))) uint16_t sK[KLDS ? MAXKT * 32 * LDV : 8];
   __shared__ __attribute__((aligned(16))) uint16_t sO[64 * LD];
   __shared__ __attribute__((aligned(16))) uint16_t sW[NWR * LD];
   __shared__ __attribute__((aligned(16))) float sVec[10 * C];  // bo b1 b2 γ2 β2 γ1 β1 | bq (≤ 3C)
@@ -126,16 +127,6 @@ __global__ __launch_bounds__(512) void sa_block_fwd_kernel(SABlockFwdArgs a) {
   if (threadIdx.x < 128) reinterpret_cast<uint32_t*>(sOnes)[threadIdx.x] = 0x3F803F80u;
   __syncthreads();
   const int tile = sTicket;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    pio_persist_dbg[0] = (unsigned long long)a.R;
-    pio_persist_dbg[1] = (unsigned long long)a.N;
-    pio_persist_dbg[2] = (unsigned long long)a.L;
-    pio_persist_dbg[3] = (unsigned long long)(uintptr_t)a.sync;
-    pio_persist_dbg[4] = (unsigned long long)(uintptr_t)a.QKV0;
-    pio_persist_dbg[5] = (unsigned long long)(unsigned)tile;
-    pio_persist_dbg[6] = (unsigned long long)(uintptr_t)a.ly[0].Wo;
-    pio_persist_dbg[7] = (unsigned long long)(uintptr_t)a.X0;
-  }
   const int nsync = kSyncCounters + a.R / a.N;
   if (tile < 0 || tile >= a.R / 64) {  // never with a zeroed ticket and grid = R / 64 (uniform)
     if (threadIdx.x == 0) atomicOr(&pio_persist_err, 2u);
@@ -194,10 +185,18 @@ __global__ __launch_bounds__(512) void sa_block_fwd_kernel(SABlockFwdArgs a) {
       __syncthreads();
     }
     const __amdgpu_buffer_rsrc_t rq = pbuf(qkv, qkv_bytes);
-    bf16x8 kf[MAXKT], qf, vr[NVI];
+    bf16x8 kf[MAXKT], qf, vr[NVI], kr[KLDS ? NVI : 1];
+    if constexpr (KLDS) {
 #pragma unroll
-    for (int kt = 0; kt < MAXKT; ++kt)
-      kf[kt] = ld16_sc1(rq, kt < nkt ? ((rb + 32 * kt + r) * C3 + C + h * D + 8 * hh) * 2u : kOffNone);
+      for (int k = 0; k < NVI; ++k) {
+        const int c = threadIdx.x + NT * k, key = c >> 3, col = (c & 7) * 8;
+        kr[k] = ld16_sc1(rq, key < N ? ((rb + key) * C3 + C + col) * 2u : kOffNone);
+      }
+    } else {
+#pragma unroll
+      for (int kt = 0; kt < MAXKT; ++kt)
+        kf[kt] = ld16_sc1(rq, kt < nkt ? ((rb + 32 * kt + r) * C3 + C + h * D + 8 * hh) * 2u : kOffNone);
+    }
     qf = ld16_sc1(rq, ((unsigned)(m0 + 32 * qb + r) * C3 + h * D + 8 * hh) * 2u);
 #pragma unroll
     for (int k = 0; k < NVI; ++k) {
@@ -217,14 +216,16 @@ __global__ __launch_bounds__(512) void sa_block_fwd_kernel(SABlockFwdArgs a) {
     for (int k = 0; k < NVI; ++k) {
       const int c = threadIdx.x + NT * k, key = c >> 3, col = (c & 7) * 8;
       *reinterpret_cast<bf16x8*>(sV + key * LDV + col) = vr[k];
+      if constexpr (KLDS) *reinterpret_cast<bf16x8*>(sK + key * LDV + col) = kr[k];
     }
     PTS(2);
     lds_sync();
     PTS(3);
 
+
     // ---- attention: head h, query block qb (sa_layer_fwd_chain8_kernel) ----
     {
-      float m_run = -INFINITY;
+      float m_run = -INFINITY, l_run = 0.f;
       f32x16 o = f32x16{};
 #pragma unroll
       for (int ch = 0; ch < MAXKT / 4; ++ch) {
@@ -236,7 +237,9 @@ __global__ __launch_bounds__(512) void sa_block_fwd_kernel(SABlockFwdArgs a) {
             const int kt = 4 * ch + k;
             sc[k] = f32x16{};
             if (kt < nkt) {
-              sc[k] = mfma32(kf[kt], qf, sc[k]);
+              const bf16x8 kfr = KLDS ? *reinterpret_cast<const bf16x8*>(sK + (32 * kt + r) * LDV + h * D + 8 * hh)
+                                      : kf[kt];
+              sc[k] = mfma32(kfr, qf, sc[k]);
 #pragma unroll
               for (int e = 0; e < 16; ++e) mt = fmaxf(mt, sc[k][e]);
             }
@@ -245,11 +248,22 @@ __global__ __launch_bounds__(512) void sa_block_fwd_kernel(SABlockFwdArgs a) {
           const float alpha = fast_exp2(m_run - m_new);
 #pragma unroll
           for (int e = 0; e < 16; ++e) o[e] *= alpha;
+          if constexpr (ADROP) l_run *= alpha;
 #pragma unroll
           for (int k = 0; k < 4; ++k)
             if (4 * ch + k < nkt) {
 #pragma unroll
               for (int e = 0; e < 16; ++e) sc[k][e] = fast_exp2(fmaf(sc[k][e], a.scale_log2, -m_new));
+              if constexpr (ADROP) {  // attention-probability dropout, as sa_layer_fwd_chain8_kernel
+                const uint32_t dkey = drop_key(a.dr.seed, (uint32_t)i, 2u);
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                  l_run += sc[k][e];
+                  const uint32_t key = 32 * (4 * ch + k) + acc_row(e, hh);
+                  const uint32_t idx = (uint32_t)(m0 - (int)rb + 32 * qb + r) * (uint32_t)N + key;
+                  sc[k][e] = keep_elem(dkey, (uint32_t)(b * H + h), idx, a.dr.thresh) ? sc[k][e] * a.dr.scale : 0.f;
+                }
+              }
             }
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
@@ -264,7 +278,7 @@ __global__ __launch_bounds__(512) void sa_block_fwd_kernel(SABlockFwdArgs a) {
         }
         __builtin_amdgcn_sched_barrier(0);
       }
-      const float ls = o[8];
+      const float ls = ADROP ? xor32_sum(l_run) : o[8];
       const float inv = 1.f / ls;
       const int row = 32 * qb + r;
 #pragma unroll
@@ -380,7 +394,15 @@ bool sa_block_fwd_launch(const SABlockFwdArgs& a, hipStream_t st) {
     if (nq != 0 && nq != 64 && nq != 128 && nq != 192) return false;
     if (i + 1 < a.L && nq != 192) return false;  // layers before the last feed the next layer's QKV
   }
-  hipLaunchKernelGGL((sa_block_fwd_kernel<8>), dim3(a.R / 64), dim3(512), 0, st, a);
+  static const bool klds = getenv("PIO_PERSIST_KLDS") == nullptr || getenv("PIO_PERSIST_KLDS")[0] != '0';
+  const dim3 grid(a.R / 64);
+  if (a.dr.thresh) {
+    if (klds) hipLaunchKernelGGL((sa_block_fwd_kernel<8, true, true>), grid, dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((sa_block_fwd_kernel<8, false, true>), grid, dim3(512), 0, st, a);
+  } else {
+    if (klds) hipLaunchKernelGGL((sa_block_fwd_kernel<8, true, false>), grid, dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((sa_block_fwd_kernel<8, false, false>), grid, dim3(512), 0, st, a);
+  }
   return true;
 }
 

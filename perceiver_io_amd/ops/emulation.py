@@ -246,12 +246,12 @@ def _acc(t, v):
 def sa_layer_fwd(qkv, x, N, scale, wo, bo, g2, be2, eps, w1, b1, w2, b2, lnw=None, lnb=None, wq=None, bq=None,
                  seed=None, site=0, p=0.0):
     """The fused self-attention layer forward (chain.hip sa_layer_fwd_chain8_kernel): attention of the
-    packed qkv (C = 64, H = 4, no attention dropout), then the post-attention block and, when the
+    packed qkv (C = 64, H = 4, probability dropout p), then the post-attention block and, when the
     next layer's LN1 / in-projection are given, its QKV."""
     C, H = 64, 4
     R = x.shape[0]
     q3 = qkv.view(R // N, N, 3 * C)
-    o, lse = attn_fwd(q3[:, :, :C], q3[:, :, C:2 * C], q3[:, :, 2 * C:], None, H, C // H, scale, 0.0, None, 1)
+    o, lse = attn_fwd(q3[:, :, :C], q3[:, :, C:2 * C], q3[:, :, 2 * C:], None, H, C // H, scale, p, seed, 1, site=site)
     o2 = o.reshape(R, C)
     if wq is None:
         return [o, lse] + list(post_attn_fwd(o2, x, wo, bo, g2, be2, eps, w1, b1, w2, b2, seed, site, p))

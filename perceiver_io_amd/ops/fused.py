@@ -820,9 +820,9 @@ class _SABlockFn(torch.autograd.Function):
             qkv, mean1, rstd1 = K.ln_linear_fwd(xl, P[0][0], P[0][1], EPS, bws[0][0], P[0][3], 0, None, True, True)
         saved = []
         # one fused launch per layer (attention + post-attention + next LN1/QKV) for the
-        # C = 64, H = 4 latent stacks without attention dropout (csrc/chain.hip
+        # C = 64, H = 4 latent stacks, attention-probability dropout included (csrc/chain.hip
         # sa_layer_fwd_chain8_kernel: up to 512 latents)
-        fused_layer = SA_LAYER_FUSED and C == 64 and H == 4 and N <= 512 and N % 64 == 0 and pdrop == 0.0
+        fused_layer = SA_LAYER_FUSED and C == 64 and H == 4 and N <= 512 and N % 64 == 0
         res = None
         if fused_layer and PERSIST_BLOCK and N <= 256 and hasattr(K, "sa_block_fwd"):
             wantq = _LOOKAHEAD["want_q"]
