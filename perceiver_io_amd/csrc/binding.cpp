@@ -46,9 +46,9 @@ struct SlabJob {
 #include "persist_args.h"
 #include "sb_args.h"
 namespace pio {
-bool sb_fwd_launch(const SBFwdArgs&, hipStream_t);
-bool sb_bwd_launch(const SBBwdArgs&, hipStream_t);
-bool sb_wgrad_launch(SBWgradArgs, hipStream_t);
+bool sb_fwd_launch(const SBFwdArgs&, int C, hipStream_t);
+bool sb_bwd_launch(const SBBwdArgs&, int C, hipStream_t);
+bool sb_wgrad_launch(SBWgradArgs, int C, hipStream_t);
 bool sa_block_fwd_launch(const SABlockFwdArgs&, hipStream_t);
 unsigned persist_errors(bool);
 int persist_sync_words(int);
@@ -567,13 +567,13 @@ std::vector<Tensor> sa_block_fwd(Tensor qkv0, Tensor x0, int64_t N, double scale
 
 unsigned persist_errors(bool reset) { return pio::persist_errors(reset); }
 
-// ---- per-sample latent-block kernels (csrc/sample_block.hip): C = 128, H = 4, N = 32 ----
+// ---- per-sample latent-block kernels (csrc/sample_block.hip): C ∈ {64, 128}, H = 4, N = 32 ----
 namespace {
-constexpr int kSBC = 128, kSBN = 32;
-void sb_check_w(const Tensor& t, int rows, const char* what) {
-  TORCH_CHECK(t.is_contiguous() && t.dim() == 2 && t.size(0) == rows && t.size(1) == kSBC &&
+constexpr int kSBN = 32;
+void sb_check_w(const Tensor& t, int rows, int C, const char* what) {
+  TORCH_CHECK(t.is_contiguous() && t.dim() == 2 && t.size(0) == rows && t.size(1) == C &&
                   t.scalar_type() == torch::kBFloat16 && (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0,
-              "sample block: ", what, " must be a contiguous 16-byte aligned bf16 (", rows, ", 128) weight");
+              "sample block: ", what, " must be a contiguous 16-byte aligned bf16 (", rows, ", ", C, ") weight");
 }
 void sb_check_v(const Tensor& t, int n, const char* what) {
   TORCH_CHECK(t.is_contiguous() && t.numel() == n && t.scalar_type() == torch::kFloat32 &&
@@ -582,18 +582,24 @@ void sb_check_v(const Tensor& t, int n, const char* what) {
 }
 // per layer the 12 parameters in layer_spec_and_params order with the bf16 weight shadows:
 // (g1, be1, wqkv_bf16, bqkv, wo_bf16, bo, g2, be2, w1_bf16, b1, w2_bf16, b2)
-void sb_fill_params(pio::SBLayer& y, const std::vector<Tensor>& p, int i) {
+void sb_fill_params(pio::SBLayer& y, const std::vector<Tensor>& p, int i, int C) {
   const Tensor* q = &p[12 * i];
-  sb_check_v(q[0], kSBC, "γ1"); sb_check_v(q[1], kSBC, "β1"); sb_check_w(q[2], 3 * kSBC, "Wqkv");
-  sb_check_v(q[3], 3 * kSBC, "bqkv"); sb_check_w(q[4], kSBC, "Wo"); sb_check_v(q[5], kSBC, "bo");
-  sb_check_v(q[6], kSBC, "γ2"); sb_check_v(q[7], kSBC, "β2"); sb_check_w(q[8], kSBC, "W1");
-  sb_check_v(q[9], kSBC, "b1"); sb_check_w(q[10], kSBC, "W2"); sb_check_v(q[11], kSBC, "b2");
+  sb_check_v(q[0], C, "γ1"); sb_check_v(q[1], C, "β1"); sb_check_w(q[2], 3 * C, C, "Wqkv");
+  sb_check_v(q[3], 3 * C, "bqkv"); sb_check_w(q[4], C, C, "Wo"); sb_check_v(q[5], C, "bo");
+  sb_check_v(q[6], C, "γ2"); sb_check_v(q[7], C, "β2"); sb_check_w(q[8], C, C, "W1");
+  sb_check_v(q[9], C, "b1"); sb_check_w(q[10], C, C, "W2"); sb_check_v(q[11], C, "b2");
   y.g1 = f32p(q[0]); y.be1 = f32p(q[1]); y.Wqkv = bfp(q[2]); y.bqkv = f32p(q[3]); y.Wo = bfp(q[4]); y.bo = f32p(q[5]);
   y.g2 = f32p(q[6]); y.be2 = f32p(q[7]); y.W1 = bfp(q[8]); y.b1 = f32p(q[9]); y.W2 = bfp(q[10]); y.b2 = f32p(q[11]);
 }
 constexpr int kSBSaved = 12;  // LN1X QKV O LN2Y U GU Y Z mean1 rstd1 mean2 rstd2
-void sb_fill_saved(pio::SBLayer& y, const std::vector<Tensor>& sv, int i) {
+void sb_fill_saved(pio::SBLayer& y, const std::vector<Tensor>& sv, int i, int R, int C) {
   const Tensor* t = &sv[kSBSaved * i];
+  for (int k = 0; k < kSBSaved; ++k) {
+    const int64_t want = k < 8 ? (int64_t)R * (k == 1 ? 3 * C : C) : R;
+    TORCH_CHECK(t[k].is_contiguous() && t[k].numel() == want &&
+                    t[k].scalar_type() == (k < 6 ? torch::kBFloat16 : torch::kFloat32),
+                "sample block: saved tensor ", k, " of layer ", i, " has the wrong shape / dtype");
+  }
   y.LN1X = reinterpret_cast<uint16_t*>(t[0].data_ptr()); y.QKV = reinterpret_cast<uint16_t*>(t[1].data_ptr());
   y.O = reinterpret_cast<uint16_t*>(t[2].data_ptr()); y.LN2Y = reinterpret_cast<uint16_t*>(t[3].data_ptr());
   y.U = reinterpret_cast<uint16_t*>(t[4].data_ptr()); y.GU = reinterpret_cast<uint16_t*>(t[5].data_ptr());
@@ -602,11 +608,13 @@ void sb_fill_saved(pio::SBLayer& y, const std::vector<Tensor>& sv, int i) {
 }
 }  // namespace
 
-// forward of a whole block, one workgroup per sample: x (B·32, 128) fp32 → per layer
+// forward of a whole block, one workgroup per sample: x (B·32, C) fp32 → per layer
 // [LN1X, QKV, O, LN2Y, U, GU (bf16), Y, Z, mean1, rstd1, mean2, rstd2 (fp32)]; the block output is
 // the last layer's Z
 std::vector<Tensor> sb_fwd(Tensor x, std::vector<Tensor> params, double scale, double eps) {
-  TORCH_CHECK(x.is_contiguous() && x.dim() == 2 && x.size(1) == kSBC && x.size(0) % kSBN == 0, "sb_fwd: x (B·32, 128)");
+  const int C = x.dim() == 2 ? (int)x.size(1) : 0;
+  TORCH_CHECK(x.is_contiguous() && (C == 64 || C == 128) && x.size(0) % kSBN == 0 && x.size(0) > 0,
+              "sb_fwd: x (B·32, C), C ∈ {64, 128}");
   CHECK_DT(x, torch::kFloat32);
   const int L = (int)params.size() / 12, R = (int)x.size(0);
   TORCH_CHECK(L >= 1 && L <= pio::kSBMaxLayers && (int)params.size() == 12 * L, "sb_fwd: 1..4 layers × 12 parameters");
@@ -618,28 +626,32 @@ std::vector<Tensor> sb_fwd(Tensor x, std::vector<Tensor> params, double scale, d
   a.eps = (float)eps;
   std::vector<Tensor> out;
   for (int i = 0; i < L; ++i) {
-    sb_fill_params(a.ly[i], params, i);
-    std::vector<Tensor> sv{torch::empty({R, kSBC}, b16), torch::empty({R, 3 * kSBC}, b16), torch::empty({R, kSBC}, b16),
-                           torch::empty({R, kSBC}, b16), torch::empty({R, kSBC}, b16), torch::empty({R, kSBC}, b16),
-                           torch::empty({R, kSBC}, f32), torch::empty({R, kSBC}, f32), torch::empty({R}, f32),
+    sb_fill_params(a.ly[i], params, i, C);
+    std::vector<Tensor> sv{torch::empty({R, C}, b16), torch::empty({R, 3 * C}, b16), torch::empty({R, C}, b16),
+                           torch::empty({R, C}, b16), torch::empty({R, C}, b16), torch::empty({R, C}, b16),
+                           torch::empty({R, C}, f32), torch::empty({R, C}, f32), torch::empty({R}, f32),
                            torch::empty({R}, f32), torch::empty({R}, f32), torch::empty({R}, f32)};
     out.insert(out.end(), sv.begin(), sv.end());
-    sb_fill_saved(a.ly[i], out, i);
+    sb_fill_saved(a.ly[i], out, i, R, C);
   }
-  TORCH_CHECK(pio::sb_fwd_launch(a, stream()), "sb_fwd: launch refused");
+  TORCH_CHECK(pio::sb_fwd_launch(a, C, stream()), "sb_fwd: launch refused");
   return out;
 }
 
-// backward of a block: dz (B·32, 128) fp32, x0 the block input, saved = sb_fwd's outputs, params
+// backward of a block: dz (B·32, C) fp32, x0 the block input, saved = sb_fwd's outputs, params
 // as sb_fwd's; ln_grads = per layer (dγ1, dβ1, dγ2, dβ2) fp32 targets (added to).  Returns
 // [dx, then per layer the gradient rows dQKV, dY, dU, dZ (bf16)] for sb_wgrad
 std::vector<Tensor> sb_bwd(Tensor dz, Tensor x0, std::vector<Tensor> saved, std::vector<Tensor> params,
                            std::vector<Tensor> ln_grads, double scale, double eps) {
-  TORCH_CHECK(dz.is_contiguous() && x0.is_contiguous() && dz.sizes() == x0.sizes() && dz.size(1) == kSBC,
-              "sb_bwd: dz / x0 (B·32, 128)");
+  const int C = x0.dim() == 2 ? (int)x0.size(1) : 0;
+  TORCH_CHECK(dz.is_contiguous() && x0.is_contiguous() && dz.sizes() == x0.sizes() && (C == 64 || C == 128) &&
+                  x0.size(0) % kSBN == 0 && x0.size(0) > 0,
+              "sb_bwd: dz / x0 (B·32, C), C ∈ {64, 128}");
   CHECK_DT(dz, torch::kFloat32);
+  CHECK_DT(x0, torch::kFloat32);
   const int L = (int)params.size() / 12, R = (int)x0.size(0);
-  TORCH_CHECK(L >= 1 && L <= pio::kSBMaxLayers && (int)saved.size() == kSBSaved * L && (int)ln_grads.size() == 4 * L,
+  TORCH_CHECK(L >= 1 && L <= pio::kSBMaxLayers && (int)params.size() == 12 * L && (int)saved.size() == kSBSaved * L &&
+                  (int)ln_grads.size() == 4 * L,
               "sb_bwd: saved / ln_grads per layer");
   auto f32 = x0.options().dtype(torch::kFloat32);
   auto b16 = x0.options().dtype(torch::kBFloat16);
@@ -647,46 +659,49 @@ std::vector<Tensor> sb_bwd(Tensor dz, Tensor x0, std::vector<Tensor> saved, std:
   a.X0 = f32p(x0); a.dZ = f32p(dz); a.L = L; a.B = R / kSBN;
   a.scale_log2 = (float)(scale * 1.4426950408889634);
   a.eps = (float)eps;
-  Tensor dx = torch::empty({R, kSBC}, f32);
+  Tensor dx = torch::empty({R, C}, f32);
   a.dX = dx.data_ptr<float>();
   std::vector<Tensor> out{dx};
   for (int i = 0; i < L; ++i) {
-    sb_fill_params(a.ly[i], params, i);
-    sb_fill_saved(a.ly[i], saved, i);
+    sb_fill_params(a.ly[i], params, i, C);
+    sb_fill_saved(a.ly[i], saved, i, R, C);
     pio::SBGrad& g = a.gr[i];
-    Tensor dq = torch::empty({R, 3 * kSBC}, b16), dy = torch::empty({R, kSBC}, b16), du = torch::empty({R, kSBC}, b16),
-           dzz = torch::empty({R, kSBC}, b16);
+    Tensor dq = torch::empty({R, 3 * C}, b16), dy = torch::empty({R, C}, b16), du = torch::empty({R, C}, b16),
+           dzz = torch::empty({R, C}, b16);
     g.dQKV = reinterpret_cast<uint16_t*>(dq.data_ptr()); g.dY = reinterpret_cast<uint16_t*>(dy.data_ptr());
     g.dU = reinterpret_cast<uint16_t*>(du.data_ptr()); g.dZ = reinterpret_cast<uint16_t*>(dzz.data_ptr());
-    for (int k = 0; k < 4; ++k) sb_check_v(ln_grads[4 * i + k], kSBC, "LN gradient target");
+    for (int k = 0; k < 4; ++k) sb_check_v(ln_grads[4 * i + k], C, "LN gradient target");
     g.dg1 = ln_grads[4 * i].data_ptr<float>(); g.dbe1 = ln_grads[4 * i + 1].data_ptr<float>();
     g.dg2 = ln_grads[4 * i + 2].data_ptr<float>(); g.dbe2 = ln_grads[4 * i + 3].data_ptr<float>();
     out.insert(out.end(), {dq, dy, du, dzz});
   }
-  TORCH_CHECK(pio::sb_bwd_launch(a, stream()), "sb_bwd: launch refused");
+  TORCH_CHECK(pio::sb_bwd_launch(a, C, stream()), "sb_bwd: launch refused");
   return out;
 }
 
-// grouped weight gradients of a block: jobs = [G (R, N) bf16, A (R, 128) bf16, dW (N, 128) fp32,
-// db (N) fp32] × n (added to dW / db)
+// grouped weight gradients of a block: jobs = [G (R, N) bf16, A (R, C) bf16, dW (N, C) fp32,
+// db (N) fp32] × n (added to dW / db); one C for every job
 void sb_wgrad(std::vector<Tensor> jobs) {
   TORCH_CHECK(jobs.size() % 4 == 0 && !jobs.empty() && (int)jobs.size() / 4 <= pio::kSBMaxJobs, "sb_wgrad: 1..16 jobs");
   pio::SBWgradArgs a{};
   a.njobs = (int)jobs.size() / 4;
   a.R = (int)jobs[0].size(0);
+  const int C = jobs[1].dim() == 2 ? (int)jobs[1].size(1) : 0;
+  TORCH_CHECK(C == 64 || C == 128, "sb_wgrad: A (R, C), C ∈ {64, 128}");
   for (int j = 0; j < a.njobs; ++j) {
     const Tensor &G = jobs[4 * j], &A = jobs[4 * j + 1], &dW = jobs[4 * j + 2], &db = jobs[4 * j + 3];
     const int N = (int)G.size(1);
-    TORCH_CHECK(G.is_contiguous() && A.is_contiguous() && G.size(0) == a.R && A.size(0) == a.R && A.size(1) == kSBC &&
-                    G.scalar_type() == torch::kBFloat16 && A.scalar_type() == torch::kBFloat16 && N % 64 == 0,
-                "sb_wgrad: G (R, N) / A (R, 128) bf16");
-    TORCH_CHECK(dW.is_contiguous() && dW.numel() == (int64_t)N * kSBC && db.is_contiguous() && db.numel() == N,
-                "sb_wgrad: dW (N, 128) / db (N)");
+    TORCH_CHECK(G.is_contiguous() && A.is_contiguous() && G.dim() == 2 && A.dim() == 2 && G.size(0) == a.R &&
+                    A.size(0) == a.R && A.size(1) == C && G.scalar_type() == torch::kBFloat16 &&
+                    A.scalar_type() == torch::kBFloat16 && N % 64 == 0 && N > 0,
+                "sb_wgrad: G (R, N) / A (R, C) bf16");
+    TORCH_CHECK(dW.is_contiguous() && dW.numel() == (int64_t)N * C && db.is_contiguous() && db.numel() == N,
+                "sb_wgrad: dW (N, C) / db (N)");
     CHECK_DT(dW, torch::kFloat32);
     CHECK_DT(db, torch::kFloat32);
     a.job[j] = pio::SBWgradJob{bfp(G), bfp(A), dW.data_ptr<float>(), db.data_ptr<float>(), N, 0};
   }
-  TORCH_CHECK(pio::sb_wgrad_launch(a, stream()), "sb_wgrad: launch refused");
+  TORCH_CHECK(pio::sb_wgrad_launch(a, C, stream()), "sb_wgrad: launch refused");
 }
 
 // workgroups of a non-deterministic SlabJob (128 measured best on the MLM step: 96–128 ≈ equal,

@@ -12,11 +12,14 @@
 //   pass 1 tail       the last split workgroup of each row block (arrival ticket) merges the
 //                     splits' (max, sum) into the rows' lse and the block's loss partial; the last
 //                     row block (second ticket) finalises the mean loss — no combine launch.
-//   pass 2 (backward) vocab × row split: logit tiles S = H·Wᵀ (vocab on the lane), dl = (p −
-//                     onehot)·g, dW += dlᵀ·H and db += Σ dl (partials stored into a slab row),
-//                     plus, in appended workgroups, the dH rows g·u[r] with u[r] = Σ_v p·W −
-//                     W[label] merged from pass 1's per-split partials, scattered to their source
-//                     positions.
+//   pass 2 (backward) vocab × row split: logit tiles S = H·Wᵀ (vocab on the lane), p, dW += g·pᵀ·H
+//                     and db += g·Σ p (partials stored into a slab row), plus, in appended
+//                     workgroups, the one-hot terms dW[label] −= g·H[r], db[label] −= g and the dH
+//                     rows g·u[r] with u[r] = Σ_v p·W − W[label] merged from pass 1's per-split
+//                     partials, scattered to their source positions.
+// Per-logit VALU work is what bounds both passes (MFMA busy ≈ 13 %): the logit accumulators start
+// at the bias (the MFMAs add it), the exp2 argument is one fma, and pass 2 keeps g and the label
+// compare out of its tiles.
 //
 // LDS images ([rows][64] bf16, 128 B per row, no padding) are XOR-swizzled on their 16-byte
 // slots with sw(v) = v₁·4 + v₂·2 + v₃ (bits of the row index): a k-contiguous ds_read_b128
@@ -85,7 +88,7 @@ __global__ __launch_bounds__(256) void ce2_fwd_kernel(const float* __restrict__ 
                                                       float* __restrict__ zero_out, long long zero_n4) {
   using namespace ce2;
   __shared__ __attribute__((aligned(16))) uint16_t sW[2][VC * C];
-  __shared__ __attribute__((aligned(16))) float sB[2][VC];  // bias·log2e (−inf past V)
+  __shared__ __attribute__((aligned(16))) float sB[2][VC];  // bias (−inf past V): the logit accumulators' initial value
   const int w = wave_id(), l = lane_id(), hh = l >> 5;
   const int m0 = blockIdx.x * RB, split = blockIdx.y;
   const int nchunks = (V + VC - 1) / VC;
@@ -130,7 +133,7 @@ __global__ __launch_bounds__(256) void ce2_fwd_kernel(const float* __restrict__ 
     }
     const int v = c * VC + (threadIdx.x & (VC - 1));
     const float bv = bias[v < V ? v : 0];  // unconditional load (address select)
-    bnext = v < V ? bv * kL2E : -__builtin_inff();
+    bnext = v < V ? bv : -__builtin_inff();
   };
   auto stage = [&](int buf) {
 #pragma unroll
@@ -154,26 +157,24 @@ __global__ __launch_bounds__(256) void ce2_fwd_kernel(const float* __restrict__ 
     const uint16_t* img = sW[buf];
 #pragma unroll
     for (int vb = 0; vb < 2; ++vb) {  // two 32-vocab blocks per chunk
-      f32x16 st = f32x16{};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) st = mfma32(ce2::img_kc(img, 32 * vb, s), hb[s], st);
-      // register i: vocab 32vb + acc_row(i, hh) of the chunk (log2 units, bias added)
-      float t[16];
+      // register i: vocab 32vb + acc_row(i, hh) of the chunk; the accumulator starts at the bias,
+      // so the MFMAs add it (no per-logit VALU add) and the logit stays in natural units until
+      // the exp2 argument (one fma)
+      f32x16 st;
       {
         const float* bp = sB[buf] + 32 * vb + 4 * hh;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const float4 bb = *reinterpret_cast<const float4*>(bp + 8 * q);
-          t[4 * q] = fmaf(st[4 * q], kL2E, bb.x);
-          t[4 * q + 1] = fmaf(st[4 * q + 1], kL2E, bb.y);
-          t[4 * q + 2] = fmaf(st[4 * q + 2], kL2E, bb.z);
-          t[4 * q + 3] = fmaf(st[4 * q + 3], kL2E, bb.w);
+          st[4 * q] = bb.x; st[4 * q + 1] = bb.y; st[4 * q + 2] = bb.z; st[4 * q + 3] = bb.w;
         }
       }
-      float mx = t[0];
 #pragma unroll
-      for (int i = 1; i < 16; ++i) mx = fmaxf(mx, t[i]);
-      mx = xor32_max(mx);  // both halves of the row share its reference max
+      for (int s = 0; s < 4; ++s) st = mfma32(ce2::img_kc(img, 32 * vb, s), hb[s], st);
+      float mx = st[0];
+#pragma unroll
+      for (int i = 1; i < 16; ++i) mx = fmaxf(mx, st[i]);
+      mx = xor32_max(mx) * kL2E;  // both halves of the row share its reference max (log2 units)
       if (__ballot(mx > m_ref + ce2::kRescale)) {  // rare, wave-uniform
         const float mn = fmaxf(m_ref, mx);
         const float alpha = fast_exp2(m_ref - mn);  // 0 on the first block
@@ -188,14 +189,14 @@ __global__ __launch_bounds__(256) void ce2_fwd_kernel(const float* __restrict__ 
         const int ri = (j & 3) + 4 * (j >> 3);
         float v = 0.f;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) v = i == ri ? t[i] : v;
-        pk = v;
+        for (int i = 0; i < 16; ++i) v = i == ri ? st[i] : v;
+        pk = v * kL2E;
         have_pk = true;
       }
       f32x16 p;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        p[i] = fast_exp2(t[i] - m_ref);
+        p[i] = fast_exp2(fmaf(st[i], kL2E, -m_ref));
         l_run += p[i];
       }
       // Σ p·W: accᵀ[c][row] += Wᵀ[c][v]·Pᵀ[v][row] (the logits accumulator as the B operand)
@@ -335,8 +336,7 @@ __global__ __launch_bounds__(256) void ce2_bwd_kernel(const uint16_t* __restrict
                                                       const int64_t* __restrict__ rowmap, long long dh_rows) {
   using namespace ce2;
   __shared__ __attribute__((aligned(16))) uint16_t sH[2][HT * C];
-  __shared__ __attribute__((aligned(16))) float sL[2][HT];  // lse·log2e
-  __shared__ __attribute__((aligned(16))) int sLab[2][HT];
+  __shared__ __attribute__((aligned(16))) float sL[2][HT];  // lse·log2e; +inf for a row without a label
   const int w = wave_id(), l = lane_id(), hh = l >> 5;
   const float g = gout[0] / fmaxf(count[0], 1.f);
   if ((int)blockIdx.y == rsplit) {
@@ -347,6 +347,15 @@ __global__ __launch_bounds__(256) void ce2_bwd_kernel(const uint16_t* __restrict
     for (int r = r0 + (int)(threadIdx.x >> 4); r < r1; r += 16) {
       const int lab = (int)labels[r];
       if (lab < 0 || lab >= V) continue;
+      {  // the one-hot part of the vocab gradients, left out of the tiles: dW[label] −= g·H[r], db[label] −= g
+        const uint2 hv = *reinterpret_cast<const uint2*>(Hs + (long long)r * C + 4 * cq);
+        float* dw = dW + (long long)lab * C + 4 * cq;
+        atomicAdd(dw, -g * bf2f((uint16_t)(hv.x & 0xFFFF)));
+        atomicAdd(dw + 1, -g * bf2f((uint16_t)(hv.x >> 16)));
+        atomicAdd(dw + 2, -g * bf2f((uint16_t)(hv.y & 0xFFFF)));
+        atomicAdd(dw + 3, -g * bf2f((uint16_t)(hv.y >> 16)));
+        if (cq == 0) atomicAdd(db + lab, -g);
+      }
       const long long dst = rowmap ? rowmap[r] : (long long)r;
       if (dst < 0 || dst >= dh_rows) continue;
       float2 ml[kCeMaxSplitsFwd];
@@ -388,7 +397,7 @@ __global__ __launch_bounds__(256) void ce2_bwd_kernel(const uint16_t* __restrict
   for (int s = 0; s < 4; ++s)
     wb[s] = *reinterpret_cast<const bf16x8*>(vin ? W + (long long)vg * C + 16 * s + 8 * hh
                                                  : reinterpret_cast<const uint16_t*>(kZero32B));
-  const float bl2 = vin ? bias[vg] * kL2E : -__builtin_inff();
+  const float bnat = vin ? bias[vg] : 0.f;  // the logit accumulators' initial value
   const int ntiles = (M + HT - 1) / HT;
   const int t_begin = blockIdx.y * tiles_per_split, t_end = min(ntiles, t_begin + tiles_per_split);
   bf16x8 hr[2];
@@ -401,8 +410,10 @@ __global__ __launch_bounds__(256) void ce2_bwd_kernel(const uint16_t* __restrict
                                                      : reinterpret_cast<const uint16_t*>(kZero32B));
     }
     const int r = t * HT + (threadIdx.x & (HT - 1));
-    if (threadIdx.x < HT) aux = r < M ? lse[r] * kL2E : 0.f;
-    else if (threadIdx.x < 2 * HT) aux = __int_as_float(r < M ? (int)labels[r] : -100);
+    if (threadIdx.x < HT) {  // a row without a label (capacity padding, r ≥ M): p = 2^−inf = 0
+      const bool lv = r < M && labels[r < M ? r : 0] >= 0;
+      aux = lv ? lse[r] * kL2E : __builtin_inff();
+    }
   };
   auto stage = [&](int buf) {
 #pragma unroll
@@ -411,7 +422,6 @@ __global__ __launch_bounds__(256) void ce2_bwd_kernel(const uint16_t* __restrict
       *reinterpret_cast<bf16x8*>(&sH[buf][swz(e >> 3, e & 7)]) = hr[i];
     }
     if (threadIdx.x < HT) sL[buf][threadIdx.x] = aux;
-    else if (threadIdx.x < 2 * HT) sLab[buf][threadIdx.x - HT] = __float_as_int(aux);
   };
   f32x16 acc[2] = {f32x16{}, f32x16{}};  // dW: [v = acc_row][c = 32ct + lane]
   float bsum = 0.f;
@@ -426,24 +436,22 @@ __global__ __launch_bounds__(256) void ce2_bwd_kernel(const uint16_t* __restrict
     const uint16_t* img = sH[buf];
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb) {  // two 32-row blocks per tile
-      f32x16 st = f32x16{};
+      f32x16 st;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) st[i] = bnat;
 #pragma unroll
       for (int s = 0; s < 4; ++s) st = mfma32(ce2::img_kc(img, 32 * rb, s), wb[s], st);
-      // register i: row 32rb + acc_row(i, hh) of the tile; lane: vocab vg
+      // register i: row 32rb + acc_row(i, hh) of the tile; lane: vocab vg.  d = p (the softmax;
+      // the gradient scale g and the one-hot term are applied outside the tile loop: g on the
+      // sums, −g·H[r] at the label by the appended row workgroups)
       f32x16 d;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int r = 32 * rb + 8 * q + 4 * hh;
-        const float4 ls = *reinterpret_cast<const float4*>(&sL[buf][r]);
-        const int4 lb = *reinterpret_cast<const int4*>(&sLab[buf][r]);
-        const float lsv[4] = {ls.x, ls.y, ls.z, ls.w};
-        const int lbv[4] = {lb.x, lb.y, lb.z, lb.w};
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const float gr = lbv[jj] >= 0 ? g : 0.f;
-          const float p = fast_exp2(fmaf(st[4 * q + jj], kL2E, bl2 - lsv[jj])) * gr;
-          d[4 * q + jj] = lbv[jj] == vg ? p - gr : p;
-        }
+        const float4 ls = *reinterpret_cast<const float4*>(&sL[buf][32 * rb + 8 * q + 4 * hh]);
+        d[4 * q] = fast_exp2(fmaf(st[4 * q], kL2E, -ls.x));
+        d[4 * q + 1] = fast_exp2(fmaf(st[4 * q + 1], kL2E, -ls.y));
+        d[4 * q + 2] = fast_exp2(fmaf(st[4 * q + 2], kL2E, -ls.z));
+        d[4 * q + 3] = fast_exp2(fmaf(st[4 * q + 3], kL2E, -ls.w));
       }
 #pragma unroll
       for (int i = 0; i < 16; ++i) bsum += d[i];
@@ -458,7 +466,7 @@ __global__ __launch_bounds__(256) void ce2_bwd_kernel(const uint16_t* __restrict
     if (t + 1 < t_end) stage(buf ^ 1);
     lds_sync();
   }
-  bsum = xor32_sum(bsum);
+  bsum = xor32_sum(bsum) * g;
   float* dWp = dW;
   float* dbp = db;
   if (slab) {
@@ -477,8 +485,8 @@ __global__ __launch_bounds__(256) void ce2_bwd_kernel(const uint16_t* __restrict
       const int vv = blockIdx.x * VB2 + 32 * w + acc_row(i, hh);
       if (vv < V) {
         float* p = dWp + (long long)vv * C + 32 * ct + (l & 31);
-        if (slab) *p = acc[ct][i];
-        else atomicAdd(p, acc[ct][i]);
+        if (slab) *p = acc[ct][i] * g;
+        else atomicAdd(p, acc[ct][i] * g);
       }
     }
 }

@@ -1,67 +1,85 @@
-// Per-sample latent self-attention block kernels for the image configs: C = 128 channels, H = 4
-// heads (d = 32), N = 32 latents (reference scripts/img_clf.py:14-22: 32×128 latents, 3 × (1 cross
-// + 3 self-attention layers); model.py:36-44 self_attention_block).
+// Per-sample latent self-attention block kernels for 32-latent stacks: C = 128 channels, H = 4 heads
+// (d = 32) for the image configs (reference scripts/img_clf.py:14-22: 32×128 latents, 3 × (1 cross
+// + 3 self-attention layers)) and C = 64 (d = 16) for the LArTPC experiment (run.py:72-112:
+// 32×64 latents); model.py:36-44 self_attention_block.
 //
 // With 32 latents a sample's keys and values are its own 32 rows, so ONE workgroup can run every
 // layer of a block for one sample — forward or backward — with no cross-workgroup dependency at
 // all: one launch per block each way instead of 2 (forward) + 2 (backward) launches per layer,
 // and no intermediate row ever leaves the CU between the kernels of a layer.
 //
-// Layout (4 waves, wave w): every C-wide product is computed TRANSPOSED, Yᵀ = W·Xᵀ on
-// v_mfma_f32_32x32x16_bf16 with the weight as the A operand (16-byte fragments straight from
-// global memory / L2) and the activation image (bf16 [32 rows][C] in LDS) as B.  The accumulator
-// then holds, in lane l, row r = l & 31 and channels n0 + (i & 3) + 8(i >> 2) + 4(l >> 5) of
-// the wave's 32-channel tile ("T layout"): a row's values are lane-local, row reductions are 16
-// local values + one lane swap (+ a 4-wave exchange for LayerNorm).  Wave w owns channels
-// 32w .. 32w + 31 of every C-wide result and, of the packed QKV projection, exactly head w's Q,
-// K and V — so the attention of head w (32 × 32) runs inside wave w: Sᵀ = K·Qᵀ from the packed
-// T-layout registers (the contraction order of d is permuted identically on both operands),
-// softmax over keys lane-locally, Oᵀ = Vᵀ·Pᵀ with Vᵀ read transposed from a wave-private LDS tile.
+// Layout (NW = C / 32 waves per workgroup, wave w): every C-wide product is computed TRANSPOSED,
+// Yᵀ = W·Xᵀ on v_mfma_f32_32x32x16_bf16 with the weight as the A operand (16-byte fragments
+// straight from global memory / L2) and the activation image (bf16 [32 rows][C] in LDS) as B.
+// The accumulator then holds, in lane l, row r = l & 31 and channels n0 + (i & 3) + 8(i >> 2) +
+// 4(l >> 5) of the wave's 32-channel tile ("T layout"): a row's values are lane-local, row
+// reductions are 16 local values + one lane swap (+ an NW-wave exchange for LayerNorm).  Wave w
+// owns channels 32w .. 32w + 31 of every C-wide result and, of the packed QKV projection, exactly
+// its HPW = 32 / d heads' Q, K and V — so those heads' attention (32 × 32 each) runs inside wave w:
+// Sᵀ = K·Qᵀ from the packed T-layout registers (the contraction order of d is permuted identically
+// on both operands; a head's d channels are register groups of 8), softmax over keys lane-locally,
+// Oᵀ = Vᵀ·Pᵀ with Vᵀ read transposed from a wave-private LDS tile (with two heads per wave the rows
+// of the other head are computed and dropped).
 //
 // Backward: the transposed products dXᵀ = Wᵀ·dYᵀ read the weight transposed from an LDS image
-// (staged per 128 × 128 block, double-buffered), attention backward of head w again inside wave
-// w.  Weight gradients are NOT formed here: the kernel stores the gradient rows (dQKV, dY, dU, dZ;
-// bf16) and one grouped GEMM launch (sb_wgrad_kernel) forms dW = Σ Gᵀ·A for all weights of the
-// block against the forward's saved operand rows (LN1(x), O, LN2(y), GELU(u)) — the row sums of a
-// weight gradient need every sample, which no per-sample workgroup has.  LayerNorm γ/β gradients
-// (128 values per LN) are reduced over the sample's rows in registers and added atomically.
+// (staged per C × C block, double-buffered), attention backward of the wave's heads again inside
+// the wave.  Weight gradients are NOT formed here: the kernel stores the gradient rows (dQKV, dY,
+// dU, dZ; bf16) and one grouped GEMM launch (sb_wgrad_kernel) forms dW = Σ Gᵀ·A for all weights of
+// the block against the forward's saved operand rows (LN1(x), O, LN2(y), GELU(u)) — the row sums
+// of a weight gradient need every sample, which no per-sample workgroup has.  LayerNorm γ/β
+// gradients (C values per LN) are reduced over the sample's rows in registers and added atomically.
 #include "common.h"
 #include "sb_args.h"
 
 namespace pio {
 namespace sb {
 
-constexpr int C = 128, NR = 32, H = 4, D = 32, NT = 256;
-constexpr int LDI = C + 8;        // activation images [32][136] bf16
-constexpr int LDQ = 3 * C + 8;    // dQKV image [32][392]
-constexpr int LDA = D + 8;        // per-wave 32 × 32 attention tiles [32][40]
-constexpr int LDW = C + 8;        // staged weight block [128][136]
+constexpr int NR = 32, H = 4;
+constexpr int LDA = 32 + 8;  // per-wave 32 × 32 attention tiles [32][40]
+
+template <int C>
+struct Shape {
+  static constexpr int NW = C / 32;         // waves per workgroup (one sample)
+  static constexpr int NT = 64 * NW;
+  static constexpr int D = C / H;           // head width
+  static constexpr int HPW = 32 / D;        // heads per wave
+  static constexpr int KSD = D / 16;        // 16-wide k-steps per head
+  static constexpr int KS = C / 16;         // k-steps of a C-deep product
+  static constexpr int LDI = C + 8;         // activation images [32][C + 8]
+  static constexpr int LDQ = 3 * C + 8;     // dQKV image [32][3C + 8]
+  static constexpr int LDW = C + 8;         // staged weight block [C][C + 8]
+  static constexpr int WCH = C / 16;        // 16-byte chunks per thread of a C × C weight block
+};
 
 __device__ __forceinline__ int tch(int i, int hh) { return (i & 3) + 8 * (i >> 2) + 4 * hh; }
 
-// 8 A fragments (k-steps over K = 128) of the 32-row tile n0.. of a row-major bf16 weight [N][128]
-__device__ __forceinline__ void load_wtile(bf16x8 (&f)[8], const uint16_t* W, int n0) {
+// KS A fragments (k-steps over K = C) of the 32-row tile n0.. of a row-major bf16 weight [N][C]
+template <int C>
+__device__ __forceinline__ void load_wtile(bf16x8 (&f)[C / 16], const uint16_t* W, int n0) {
   const int l = lane_id();
   const uint16_t* p = W + (long long)(n0 + (l & 31)) * C + 8 * (l >> 5);
 #pragma unroll
-  for (int t = 0; t < 8; ++t) f[t] = *reinterpret_cast<const bf16x8*>(p + 16 * t);
+  for (int t = 0; t < C / 16; ++t) f[t] = *reinterpret_cast<const bf16x8*>(p + 16 * t);
 }
-// Yᵀ tile = W tile · Xᵀ, X = an LDS image [32][ld] (columns k0 .. k0 + 127)
-__device__ __forceinline__ f32x16 gemm_t(const bf16x8 (&f)[8], const uint16_t* sX, int ld, int k0 = 0) {
+// Yᵀ tile = W tile · Xᵀ, X = an LDS image [32][ld]
+template <int C>
+__device__ __forceinline__ f32x16 gemm_t(const bf16x8 (&f)[C / 16], const uint16_t* sX, int ld) {
   const int l = lane_id();
-  const uint16_t* p = sX + (l & 31) * ld + k0 + 8 * (l >> 5);
+  const uint16_t* p = sX + (l & 31) * ld + 8 * (l >> 5);
   f32x16 acc = f32x16{};
 #pragma unroll
-  for (int t = 0; t < 8; ++t) acc = mfma32(f[t], *reinterpret_cast<const bf16x8*>(p + 16 * t), acc);
+  for (int t = 0; t < C / 16; ++t) acc = mfma32(f[t], *reinterpret_cast<const bf16x8*>(p + 16 * t), acc);
   return acc;
 }
-// dXᵀ tile (output channels i0 .. i0 + 31) = Wᵀ · dYᵀ over a staged weight block sW [128 n][LDW]
+// dXᵀ tile (output channels i0 .. i0 + 31) = Wᵀ · dYᵀ over a staged weight block sW [C n][LDW]
 // (the contraction index n is the block's row) and dY = an LDS image [32][ld] (columns k0 ..)
+template <int C>
 __device__ __forceinline__ f32x16 gemm_tt(const uint16_t* sW, int i0, const uint16_t* sX, int ld, int k0, f32x16 acc) {
   const int l = lane_id();
   const uint16_t* p = sX + (l & 31) * ld + k0 + 8 * (l >> 5);
 #pragma unroll
-  for (int t = 0; t < 8; ++t) acc = mfma32(frag_ks(sW, LDW, i0, 16 * t), *reinterpret_cast<const bf16x8*>(p + 16 * t), acc);
+  for (int t = 0; t < C / 16; ++t)
+    acc = mfma32(frag_ks(sW, Shape<C>::LDW, i0, 16 * t), *reinterpret_cast<const bf16x8*>(p + 16 * t), acc);
   return acc;
 }
 // T-layout values of this lane (row r, 16 channels of tile n0) → a row-major bf16 array / image
@@ -112,9 +130,11 @@ __device__ __forceinline__ bf16x8 pack8(const float (&v)[16], int s) {
   return r;
 }
 
-// LayerNorm statistics of row r over the 4 waves' 32-channel slices (Chan's combination of the
+// LayerNorm statistics of row r over the NW waves' 32-channel slices (Chan's combination of the
 // per-wave (mean, M2)); one workgroup barrier
+template <int C>
 __device__ __forceinline__ void ln_stats(const float (&v)[16], float2* sRed, float eps, float& mean, float& rstd) {
+  constexpr int NW = Shape<C>::NW;
   const int w = wave_id(), l = lane_id(), r = l & 31, hh = l >> 5;
   float s = 0.f;
 #pragma unroll
@@ -126,17 +146,21 @@ __device__ __forceinline__ void ln_stats(const float (&v)[16], float2* sRed, flo
   q = xor32_sum(q);
   if (hh == 0) sRed[w * NR + r] = make_float2(mw, q);
   __syncthreads();
-  float2 p[4];
+  float2 p[NW];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) p[k] = sRed[k * NR + r];
-  mean = 0.25f * ((p[0].x + p[1].x) + (p[2].x + p[3].x));
-  float m2 = (p[0].y + p[1].y) + (p[2].y + p[3].y);
+  for (int k = 0; k < NW; ++k) p[k] = sRed[k * NR + r];
+  float sm = 0.f, m2 = 0.f;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) { const float d = p[k].x - mean; m2 = fmaf(32.f * d, d, m2); }
+  for (int k = 0; k < NW; ++k) { sm += p[k].x; m2 += p[k].y; }
+  mean = sm * (1.f / NW);
+#pragma unroll
+  for (int k = 0; k < NW; ++k) { const float d = p[k].x - mean; m2 = fmaf(32.f * d, d, m2); }
   rstd = rsqrtf(m2 * (1.f / C) + eps);
 }
-// sums over the 4 waves of two per-row partials (each lane-local over 16 channels); one barrier
+// sums over the NW waves of two per-row partials (each lane-local over 16 channels); one barrier
+template <int C>
 __device__ __forceinline__ float2 row_sums2(float a, float b, float2* sRed) {
+  constexpr int NW = Shape<C>::NW;
   const int w = wave_id(), l = lane_id(), r = l & 31, hh = l >> 5;
   a = xor32_sum(a);
   b = xor32_sum(b);
@@ -144,54 +168,79 @@ __device__ __forceinline__ float2 row_sums2(float a, float b, float2* sRed) {
   __syncthreads();
   float2 t = make_float2(0.f, 0.f);
 #pragma unroll
-  for (int k = 0; k < 4; ++k) { const float2 p = sRed[k * NR + r]; t.x += p.x; t.y += p.y; }
+  for (int k = 0; k < NW; ++k) { const float2 p = sRed[k * NR + r]; t.x += p.x; t.y += p.y; }
   return t;
 }
 
+// Sᵀ (keys × queries, lane = query) of head hp of the wave, softmax over keys (probabilities
+// normalised; `inv` = 1 / Σ)
+template <int C>
+__device__ __forceinline__ void softmax_t(const float (&q)[16], const float (&k)[16], int hp, float scale_log2,
+                                          float (&p)[16], float& inv) {
+  constexpr int KSD = Shape<C>::KSD;
+  f32x16 s = f32x16{};
+#pragma unroll
+  for (int j = 0; j < KSD; ++j) s = mfma32(pack8(k, hp * KSD + j), pack8(q, hp * KSD + j), s);
+  float m = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) m = fmaxf(m, s[i]);
+  m = xor32_max(m) * scale_log2;
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { p[i] = fast_exp2(fmaf(s[i], scale_log2, -m)); sum += p[i]; }
+  inv = 1.f / xor32_sum(sum);
+}
+// the registers of head hp in a wave's 32-channel T-layout tile
+template <int C>
+__device__ __forceinline__ bool head_reg(int i, int hp) { return (i >> 3) / Shape<C>::KSD == hp; }
+
 // ------------------------------------------------------------------------------------
-// forward: grid = B samples, 256 threads
+// forward: grid = B samples, NT threads
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(NT) void sb_fwd_kernel(SBFwdArgs a) {
+template <int C>
+__global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
+  using S = Shape<C>;
+  constexpr int KS = S::KS, LDI = S::LDI;
   __shared__ __attribute__((aligned(16))) uint16_t sImg[2][NR * LDI];
-  __shared__ __attribute__((aligned(16))) uint16_t sV[4][NR * LDA];
-  __shared__ __attribute__((aligned(16))) float2 sRed[4 * NR];
+  __shared__ __attribute__((aligned(16))) uint16_t sV[S::NW][NR * LDA];
+  __shared__ __attribute__((aligned(16))) float2 sRed[S::NW * NR];
   const int w = wave_id(), l = lane_id(), r = l & 31;
   const long long row = (long long)blockIdx.x * NR + r;
   const int n0 = 32 * w;  // this wave's channel tile
   float x[16];
   ld_f32(x, a.X0, C, row, n0);
-  bf16x8 wq[3][8];
-  load_wtile(wq[0], a.ly[0].Wqkv, n0);
-  load_wtile(wq[1], a.ly[0].Wqkv, C + n0);
-  load_wtile(wq[2], a.ly[0].Wqkv, 2 * C + n0);
+  bf16x8 wq[3][KS];
+  load_wtile<C>(wq[0], a.ly[0].Wqkv, n0);
+  load_wtile<C>(wq[1], a.ly[0].Wqkv, C + n0);
+  load_wtile<C>(wq[2], a.ly[0].Wqkv, 2 * C + n0);
   for (int li = 0; li < a.L; ++li) {
     const SBLayer& y = a.ly[li];
     // ---- LN1 → image 0 (the QKV product's operand) ----
     float mu, rs, gv[16], bv[16], t[16];
     ld_vec(gv, y.g1, n0);
     ld_vec(bv, y.be1, n0);
-    ln_stats(x, sRed, a.eps, mu, rs);
+    ln_stats<C>(x, sRed, a.eps, mu, rs);
 #pragma unroll
     for (int i = 0; i < 16; ++i) t[i] = (x[i] - mu) * rs * gv[i] + bv[i];
     if (w == 0 && l < 32) { y.mean1[row] = mu; y.rstd1[row] = rs; }
     st_bf16(sImg[0], LDI, r, n0, t);
     st_bf16(y.LN1X, C, row, n0, t);
-    bf16x8 wo[8];
-    load_wtile(wo, y.Wo, n0);
+    bf16x8 wo[KS];
+    load_wtile<C>(wo, y.Wo, n0);
     __syncthreads();
-    // ---- Q, K, V of head w ----
+    // ---- Q, K, V of the wave's heads ----
     float q[16], k[16], v[16];
     {
       float bb[16];
-      f32x16 acc = gemm_t(wq[0], sImg[0], LDI);
+      f32x16 acc = gemm_t<C>(wq[0], sImg[0], LDI);
       ld_vec(bb, y.bqkv, n0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) q[i] = acc[i] + bb[i];
-      acc = gemm_t(wq[1], sImg[0], LDI);
+      acc = gemm_t<C>(wq[1], sImg[0], LDI);
       ld_vec(bb, y.bqkv, C + n0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) k[i] = acc[i] + bb[i];
-      acc = gemm_t(wq[2], sImg[0], LDI);
+      acc = gemm_t<C>(wq[2], sImg[0], LDI);
       ld_vec(bb, y.bqkv, 2 * C + n0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) v[i] = acc[i] + bb[i];
@@ -199,43 +248,36 @@ __global__ __launch_bounds__(NT) void sb_fwd_kernel(SBFwdArgs a) {
     st_bf16(y.QKV, 3 * C, row, n0, q);
     st_bf16(y.QKV, 3 * C, row, C + n0, k);
     st_bf16(y.QKV, 3 * C, row, 2 * C + n0, v);
-    bf16x8 w1[8];
-    load_wtile(w1, y.W1, n0);
-    // ---- attention of head w: Sᵀ = K·Qᵀ (keys × queries; lane = query), softmax over keys ----
+    bf16x8 w1[KS];
+    load_wtile<C>(w1, y.W1, n0);
+    // ---- attention of the wave's heads: Sᵀ = K·Qᵀ (lane = query), softmax over keys, Oᵀ = Vᵀ·Pᵀ
+    // with Vᵀ read transposed from a wave-private LDS tile [key][32 channels] ----
     float o[16];
     {
-      // the attention operands as the later layers see them (bf16): Q, K packed from the
-      // registers, V through a wave-private LDS tile [key][d] read transposed
       st_bf16(sV[w], LDA, r, 0, v);
-      f32x16 s = f32x16{};
-      s = mfma32(pack8(k, 0), pack8(q, 0), s);
-      s = mfma32(pack8(k, 1), pack8(q, 1), s);
-      float m = -INFINITY;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) m = fmaxf(m, s[i]);
-      m = xor32_max(m) * a.scale_log2;
-      float p[16], sum = 0.f;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) { p[i] = fast_exp2(fmaf(s[i], a.scale_log2, -m)); sum += p[i]; }
-      sum = xor32_sum(sum);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's V tile written
-      f32x16 oa = f32x16{};
-      oa = mfma32(frag_ks_perm(sV[w], LDA, 0, 0), pack8(p, 0), oa);
-      oa = mfma32(frag_ks_perm(sV[w], LDA, 0, 16), pack8(p, 1), oa);
-      const float inv = 1.f / sum;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) o[i] = oa[i] * inv;
+      for (int hp = 0; hp < S::HPW; ++hp) {
+        float p[16], inv;
+        softmax_t<C>(q, k, hp, a.scale_log2, p, inv);
+        f32x16 oa = f32x16{};
+        oa = mfma32(frag_ks_perm(sV[w], LDA, 0, 0), pack8(p, 0), oa);
+        oa = mfma32(frag_ks_perm(sV[w], LDA, 0, 16), pack8(p, 1), oa);
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (head_reg<C>(i, hp)) o[i] = oa[i] * inv;
+      }
     }
     st_bf16(sImg[1], LDI, r, n0, o);
     st_bf16(y.O, C, row, n0, o);
-    bf16x8 w2[8];
-    load_wtile(w2, y.W2, n0);
+    bf16x8 w2[KS];
+    load_wtile<C>(w2, y.W2, n0);
     __syncthreads();
     // ---- out-projection + residual → y; LN2 → image 0 ----
     float yv[16];
     {
       float bb[16];
-      const f32x16 acc = gemm_t(wo, sImg[1], LDI);
+      const f32x16 acc = gemm_t<C>(wo, sImg[1], LDI);
       ld_vec(bb, y.bo, n0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) yv[i] = acc[i] + bb[i] + x[i];
@@ -243,7 +285,7 @@ __global__ __launch_bounds__(NT) void sb_fwd_kernel(SBFwdArgs a) {
     st_f32(y.Y, C, row, n0, yv);
     ld_vec(gv, y.g2, n0);
     ld_vec(bv, y.be2, n0);
-    ln_stats(yv, sRed, a.eps, mu, rs);
+    ln_stats<C>(yv, sRed, a.eps, mu, rs);
 #pragma unroll
     for (int i = 0; i < 16; ++i) t[i] = (yv[i] - mu) * rs * gv[i] + bv[i];
     if (w == 0 && l < 32) { y.mean2[row] = mu; y.rstd2[row] = rs; }
@@ -253,7 +295,7 @@ __global__ __launch_bounds__(NT) void sb_fwd_kernel(SBFwdArgs a) {
     // ---- MLP: u = W1·LN2(y) + b1, GELU → image 1, z = W2·GELU(u) + b2 + y ----
     {
       float bb[16];
-      const f32x16 acc = gemm_t(w1, sImg[0], LDI);
+      const f32x16 acc = gemm_t<C>(w1, sImg[0], LDI);
       ld_vec(bb, y.b1, n0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) t[i] = acc[i] + bb[i];
@@ -264,14 +306,14 @@ __global__ __launch_bounds__(NT) void sb_fwd_kernel(SBFwdArgs a) {
     st_bf16(sImg[1], LDI, r, n0, t);
     st_bf16(y.GU, C, row, n0, t);
     if (li + 1 < a.L) {  // the next layer's QKV weights, in flight during the MLP
-      load_wtile(wq[0], a.ly[li + 1].Wqkv, n0);
-      load_wtile(wq[1], a.ly[li + 1].Wqkv, C + n0);
-      load_wtile(wq[2], a.ly[li + 1].Wqkv, 2 * C + n0);
+      load_wtile<C>(wq[0], a.ly[li + 1].Wqkv, n0);
+      load_wtile<C>(wq[1], a.ly[li + 1].Wqkv, C + n0);
+      load_wtile<C>(wq[2], a.ly[li + 1].Wqkv, 2 * C + n0);
     }
     __syncthreads();
     {
       float bb[16];
-      const f32x16 acc = gemm_t(w2, sImg[1], LDI);
+      const f32x16 acc = gemm_t<C>(w2, sImg[1], LDI);
       ld_vec(bb, y.b2, n0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) x[i] = acc[i] + bb[i] + yv[i];
@@ -281,22 +323,23 @@ __global__ __launch_bounds__(NT) void sb_fwd_kernel(SBFwdArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
-// backward: grid = B samples, 256 threads
+// backward: grid = B samples, NT threads
 // ------------------------------------------------------------------------------------
-// one 128 × 128 block of a row-major bf16 weight (rows n0 ..) into registers: 8 16-byte chunks
-// per thread, then into an LDS image [128][LDW]
-__device__ __forceinline__ void wblock_load(bf16x8 (&f)[8], const uint16_t* W, int n0) {
+// one C × C block of a row-major bf16 weight (rows n0 ..) into registers, then into an LDS image
+template <int C>
+__device__ __forceinline__ void wblock_load(bf16x8 (&f)[C / 16], const uint16_t* W, int n0) {
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int c = threadIdx.x + NT * k, rr = c >> 4, col = (c & 15) * 8;
+  for (int k = 0; k < C / 16; ++k) {
+    const int c = threadIdx.x + Shape<C>::NT * k, rr = c / (C / 8), col = (c % (C / 8)) * 8;
     f[k] = *reinterpret_cast<const bf16x8*>(W + (long long)(n0 + rr) * C + col);
   }
 }
-__device__ __forceinline__ void wblock_store(uint16_t* sW, const bf16x8 (&f)[8]) {
+template <int C>
+__device__ __forceinline__ void wblock_store(uint16_t* sW, const bf16x8 (&f)[C / 16]) {
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int c = threadIdx.x + NT * k, rr = c >> 4, col = (c & 15) * 8;
-    *reinterpret_cast<bf16x8*>(sW + rr * LDW + col) = f[k];
+  for (int k = 0; k < C / 16; ++k) {
+    const int c = threadIdx.x + Shape<C>::NT * k, rr = c / (C / 8), col = (c % (C / 8)) * 8;
+    *reinterpret_cast<bf16x8*>(sW + rr * Shape<C>::LDW + col) = f[k];
   }
 }
 // LayerNorm γ/β gradients of this sample: Σ_rows dxn·x̂ and Σ_rows dxn per channel (the 32 rows
@@ -314,19 +357,23 @@ __device__ __forceinline__ void ln_affine_grads(const float (&dxn)[16], const fl
   }
 }
 
-__global__ __launch_bounds__(NT) void sb_bwd_kernel(SBBwdArgs a) {
+template <int C>
+__global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
+  using S = Shape<C>;
+  constexpr int KS = S::KS, LDI = S::LDI, LDQ = S::LDQ, LDW = S::LDW, NW = S::NW;
   __shared__ __attribute__((aligned(16))) uint16_t sW[2][C * LDW];
   __shared__ __attribute__((aligned(16))) uint16_t sImg[2][NR * LDI];
   __shared__ __attribute__((aligned(16))) uint16_t sQ[NR * LDQ];
-  __shared__ __attribute__((aligned(16))) uint16_t sAt[4][4][NR * LDA];  // per wave: K, Q, dO, P / dS
-  __shared__ __attribute__((aligned(16))) float2 sRed[4 * NR];
+  __shared__ __attribute__((aligned(16))) uint16_t sAt[NW][4][NR * LDA];  // per wave: K, Q, dO, P / dS
+  __shared__ __attribute__((aligned(16))) float2 sRed[NW * NR];
   const int w = wave_id(), l = lane_id(), r = l & 31;
   const long long row = (long long)blockIdx.x * NR + r;
   const int n0 = 32 * w;
+  const float sc = a.scale_log2 * 0.69314718055994531f;  // the softmax scale 1/√d
   float dz[16];
   ld_f32(dz, a.dZ, C, row, n0);
-  bf16x8 pw[8];
-  wblock_load(pw, a.ly[a.L - 1].W2, 0);
+  bf16x8 pw[KS];
+  wblock_load<C>(pw, a.ly[a.L - 1].W2, 0);
   for (int li = a.L - 1; li >= 0; --li) {
     const SBLayer& y = a.ly[li];
     const SBGrad& gd = a.gr[li];
@@ -334,22 +381,22 @@ __global__ __launch_bounds__(NT) void sb_bwd_kernel(SBBwdArgs a) {
     // ---- dZ image; W2 block ----
     st_bf16(sImg[0], LDI, r, n0, dz);
     st_bf16(gd.dZ, C, row, n0, dz);
-    wblock_store(sW[0], pw);
-    wblock_load(pw, y.W1, 0);
+    wblock_store<C>(sW[0], pw);
+    wblock_load<C>(pw, y.W1, 0);
     float uv[16];
     ld_bf16(uv, y.U, C, row, n0);
     __syncthreads();
     // ---- dU = (W2ᵀ·dZ)∘GELU'(u) ----
     float t[16];
     {
-      const f32x16 acc = gemm_tt(sW[0], n0, sImg[0], LDI, 0, f32x16{});
+      const f32x16 acc = gemm_tt<C>(sW[0], n0, sImg[0], LDI, 0, f32x16{});
 #pragma unroll
       for (int i = 0; i < 16; ++i) t[i] = acc[i] * gelu_grad(uv[i]);
     }
     st_bf16(sImg[1], LDI, r, n0, t);
     st_bf16(gd.dU, C, row, n0, t);
-    wblock_store(sW[1], pw);
-    wblock_load(pw, y.Wo, 0);
+    wblock_store<C>(sW[1], pw);
+    wblock_load<C>(pw, y.Wo, 0);
     float yv[16], gv[16];
     ld_f32(yv, y.Y, C, row, n0);
     ld_vec(gv, y.g2, n0);
@@ -358,7 +405,7 @@ __global__ __launch_bounds__(NT) void sb_bwd_kernel(SBBwdArgs a) {
     // ---- dXn2 = W1ᵀ·dU; LN2 backward → dY ----
     float dy[16];
     {
-      const f32x16 acc = gemm_tt(sW[1], n0, sImg[1], LDI, 0, f32x16{});
+      const f32x16 acc = gemm_tt<C>(sW[1], n0, sImg[1], LDI, 0, f32x16{});
       float s1 = 0.f, s2 = 0.f, gg[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -368,7 +415,7 @@ __global__ __launch_bounds__(NT) void sb_bwd_kernel(SBBwdArgs a) {
         s1 += gg[i];
         s2 += gg[i] * yv[i];
       }
-      const float2 s = row_sums2(s1, s2, sRed);
+      const float2 s = row_sums2<C>(s1, s2, sRed);
       const float m1 = s.x * (1.f / C), m2 = s.y * (1.f / C);
 #pragma unroll
       for (int i = 0; i < 16; ++i) dy[i] = dz[i] + rs2 * (gg[i] - m1 - yv[i] * m2);
@@ -376,99 +423,88 @@ __global__ __launch_bounds__(NT) void sb_bwd_kernel(SBBwdArgs a) {
     ln_affine_grads(t, yv, gd.dg2, gd.dbe2, n0);
     st_bf16(sImg[0], LDI, r, n0, dy);
     st_bf16(gd.dY, C, row, n0, dy);
-    wblock_store(sW[0], pw);
-    wblock_load(pw, y.Wqkv, 0);
-    // the attention operands of head w (the forward's bf16 rows)
+    wblock_store<C>(sW[0], pw);
+    wblock_load<C>(pw, y.Wqkv, 0);
+    // the attention operands of the wave's heads (the forward's bf16 rows)
     float qv[16], kv[16], vv[16], ov[16];
     ld_bf16(qv, y.QKV, 3 * C, row, n0);
     ld_bf16(kv, y.QKV, 3 * C, row, C + n0);
     ld_bf16(vv, y.QKV, 3 * C, row, 2 * C + n0);
     ld_bf16(ov, y.O, C, row, n0);
     __syncthreads();
-    // ---- dO = Woᵀ·dY (head w) ----
+    // ---- dO = Woᵀ·dY (the wave's heads) ----
     float dov[16];
-    to_f(dov, gemm_tt(sW[0], n0, sImg[0], LDI, 0, f32x16{}));
-    // ---- attention backward of head w (wave-local) ----
+    to_f(dov, gemm_tt<C>(sW[0], n0, sImg[0], LDI, 0, f32x16{}));
+    // ---- attention backward of the wave's heads (wave-local) ----
     {
       uint16_t *tK = sAt[w][0], *tQ = sAt[w][1], *tdO = sAt[w][2], *tP = sAt[w][3];
       st_bf16(tK, LDA, r, 0, kv);
       st_bf16(tQ, LDA, r, 0, qv);
-      // dO as bf16, as the products see it
 #pragma unroll
-      for (int i = 0; i < 16; ++i) dov[i] = bf2f(f2bf(dov[i]));
+      for (int i = 0; i < 16; ++i) dov[i] = bf2f(f2bf(dov[i]));  // dO as bf16, as the products see it
       st_bf16(tdO, LDA, r, 0, dov);
-      // Sᵀ, Pᵀ exactly as the forward formed them
-      f32x16 s = f32x16{};
-      s = mfma32(pack8(kv, 0), pack8(qv, 0), s);
-      s = mfma32(pack8(kv, 1), pack8(qv, 1), s);
-      float m = -INFINITY;
+      float gq[16], gk[16], gvv[16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) m = fmaxf(m, s[i]);
-      m = xor32_max(m) * a.scale_log2;
-      float p[16], sum = 0.f;
+      for (int hp = 0; hp < S::HPW; ++hp) {
+        // Pᵀ exactly as the forward formed it, dPᵀ = V·dOᵀ, δ = rowsum(dO∘O) over the head
+        float p[16], inv;
+        softmax_t<C>(qv, kv, hp, a.scale_log2, p, inv);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) { p[i] = fast_exp2(fmaf(s[i], a.scale_log2, -m)); sum += p[i]; }
-      sum = xor32_sum(sum);
-      const float inv = 1.f / sum;
+        for (int i = 0; i < 16; ++i) p[i] *= inv;
+        f32x16 dp = f32x16{};
 #pragma unroll
-      for (int i = 0; i < 16; ++i) p[i] *= inv;
-      // dPᵀ = V·dOᵀ, δ = rowsum(dO∘O)
-      f32x16 dp = f32x16{};
-      dp = mfma32(pack8(vv, 0), pack8(dov, 0), dp);
-      dp = mfma32(pack8(vv, 1), pack8(dov, 1), dp);
-      float dl = 0.f;
+        for (int j = 0; j < S::KSD; ++j) dp = mfma32(pack8(vv, hp * S::KSD + j), pack8(dov, hp * S::KSD + j), dp);
+        float dl = 0.f;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) dl = fmaf(dov[i], ov[i], dl);
-      dl = xor32_sum(dl);
-      float ds[16];
+        for (int i = 0; i < 16; ++i)
+          if (head_reg<C>(i, hp)) dl = fmaf(dov[i], ov[i], dl);
+        dl = xor32_sum(dl);
+        float ds[16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) ds[i] = p[i] * (dp[i] - dl);
-      // P as [query][key] (row = this lane's query) for dV
-      st_bf16(tP, LDA, r, 0, p);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      // dVᵀ = dOᵀ·P, dKᵀ = Qᵀ·dS (scaled), dQᵀ = Kᵀ·dSᵀ (scaled): T layout, rows = keys / queries
-      f32x16 dv = f32x16{}, dk = f32x16{}, dq = f32x16{};
+        for (int i = 0; i < 16; ++i) ds[i] = p[i] * (dp[i] - dl);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous head's reads of tP done
+        st_bf16(tP, LDA, r, 0, p);  // P as [query][key] (row = this lane's query) for dV
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // dVᵀ = dOᵀ·P, dQᵀ = Kᵀ·dSᵀ, dKᵀ = Qᵀ·dS: T layout (rows = keys / queries); the rows of
+        // the wave's other head (two heads per wave) are dropped
+        f32x16 dv = f32x16{}, dk = f32x16{}, dq = f32x16{};
 #pragma unroll
-      for (int ss = 0; ss < 2; ++ss) dv = mfma32(frag_ks_perm(tdO, LDA, 0, 16 * ss), frag_ks_perm(tP, LDA, 0, 16 * ss), dv);
+        for (int ss = 0; ss < 2; ++ss) dv = mfma32(frag_ks_perm(tdO, LDA, 0, 16 * ss), frag_ks_perm(tP, LDA, 0, 16 * ss), dv);
 #pragma unroll
-      for (int ss = 0; ss < 2; ++ss) dq = mfma32(frag_ks_perm(tK, LDA, 0, 16 * ss), pack8(ds, ss), dq);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // P tile consumed: dS over it
-      st_bf16(tP, LDA, r, 0, ds);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        for (int ss = 0; ss < 2; ++ss) dq = mfma32(frag_ks_perm(tK, LDA, 0, 16 * ss), pack8(ds, ss), dq);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // P tile consumed: dS over it
+        st_bf16(tP, LDA, r, 0, ds);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-      for (int ss = 0; ss < 2; ++ss) dk = mfma32(frag_ks_perm(tQ, LDA, 0, 16 * ss), frag_ks_perm(tP, LDA, 0, 16 * ss), dk);
-      const float sc = a.scale_log2 * 0.69314718055994531f;  // the softmax scale 1/√d
-      float o3[16];
+        for (int ss = 0; ss < 2; ++ss) dk = mfma32(frag_ks_perm(tQ, LDA, 0, 16 * ss), frag_ks_perm(tP, LDA, 0, 16 * ss), dk);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) o3[i] = dq[i] * sc;
-      st_bf16(sQ, LDQ, r, n0, o3);
-      st_bf16(gd.dQKV, 3 * C, row, n0, o3);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) o3[i] = dk[i] * sc;
-      st_bf16(sQ, LDQ, r, C + n0, o3);
-      st_bf16(gd.dQKV, 3 * C, row, C + n0, o3);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) o3[i] = dv[i];
-      st_bf16(sQ, LDQ, r, 2 * C + n0, o3);
-      st_bf16(gd.dQKV, 3 * C, row, 2 * C + n0, o3);
+        for (int i = 0; i < 16; ++i)
+          if (head_reg<C>(i, hp)) { gq[i] = dq[i] * sc; gk[i] = dk[i] * sc; gvv[i] = dv[i]; }
+      }
+      st_bf16(sQ, LDQ, r, n0, gq);
+      st_bf16(gd.dQKV, 3 * C, row, n0, gq);
+      st_bf16(sQ, LDQ, r, C + n0, gk);
+      st_bf16(gd.dQKV, 3 * C, row, C + n0, gk);
+      st_bf16(sQ, LDQ, r, 2 * C + n0, gvv);
+      st_bf16(gd.dQKV, 3 * C, row, 2 * C + n0, gvv);
     }
-    wblock_store(sW[1], pw);
-    wblock_load(pw, y.Wqkv, C);
+    wblock_store<C>(sW[1], pw);
+    wblock_load<C>(pw, y.Wqkv, C);
     float xv[16];
     ld_f32(xv, X, C, row, n0);
     ld_vec(gv, y.g1, n0);
     const float mu1 = y.mean1[row], rs1 = y.rstd1[row];
     __syncthreads();
-    // ---- dXn1 = Wqkvᵀ·dQKV in three 128-row blocks of Wqkv ----
-    f32x16 acc = gemm_tt(sW[1], n0, sQ, LDQ, 0, f32x16{});
-    wblock_store(sW[0], pw);
-    wblock_load(pw, y.Wqkv, 2 * C);
+    // ---- dXn1 = Wqkvᵀ·dQKV in three C-row blocks of Wqkv ----
+    f32x16 acc = gemm_tt<C>(sW[1], n0, sQ, LDQ, 0, f32x16{});
+    wblock_store<C>(sW[0], pw);
+    wblock_load<C>(pw, y.Wqkv, 2 * C);
     __syncthreads();
-    acc = gemm_tt(sW[0], n0, sQ, LDQ, C, acc);
-    wblock_store(sW[1], pw);
-    if (li > 0) wblock_load(pw, a.ly[li - 1].W2, 0);
+    acc = gemm_tt<C>(sW[0], n0, sQ, LDQ, C, acc);
+    wblock_store<C>(sW[1], pw);
+    if (li > 0) wblock_load<C>(pw, a.ly[li - 1].W2, 0);
     __syncthreads();
-    acc = gemm_tt(sW[1], n0, sQ, LDQ, 2 * C, acc);
+    acc = gemm_tt<C>(sW[1], n0, sQ, LDQ, 2 * C, acc);
     // ---- LN1 backward → dX (the previous layer's dZ) ----
     {
       float s1 = 0.f, s2 = 0.f, gg[16];
@@ -480,7 +516,7 @@ __global__ __launch_bounds__(NT) void sb_bwd_kernel(SBBwdArgs a) {
         s1 += gg[i];
         s2 += gg[i] * xv[i];
       }
-      const float2 s = row_sums2(s1, s2, sRed);
+      const float2 s = row_sums2<C>(s1, s2, sRed);
       const float m1 = s.x * (1.f / C), m2 = s.y * (1.f / C);
 #pragma unroll
       for (int i = 0; i < 16; ++i) dz[i] = dy[i] + rs1 * (gg[i] - m1 - xv[i] * m2);
@@ -492,13 +528,14 @@ __global__ __launch_bounds__(NT) void sb_bwd_kernel(SBBwdArgs a) {
 
 // ------------------------------------------------------------------------------------
 // grouped weight gradients: grid (Σ_jobs N/64 column tiles, row splits), 256 threads.
-// Workgroup (tile, split): dW[n0 .. n0 + 63][0 .. 127] += Σ_{rows of the split} G[r][n]·A[r][k] and
-// db[n] += Σ G[r][n]; wave w owns dW rows n0 + 32(w >> 1) .., columns 64(w & 1) .. (two 32 × 32
-// MFMA tiles), the bias column sums by a ones operand.  Rows are staged 32 at a time in LDS
-// (G tile [32][64], A tile [32][128]) with the next 32 register-prefetched.
+// Workgroup (tile, split): dW[n0 .. n0 + 63][0 .. C) += Σ_{rows of the split} G[r][n]·A[r][k] and
+// db[n] += Σ G[r][n]; wave w owns dW rows n0 + 32(w >> 1) .., columns (C/2)(w & 1) .. (C/64
+// 32 × 32 MFMA tiles), the bias column sums by a ones operand.  Rows are staged 32 at a time in
+// LDS (G tile [32][64], A tile [32][C]) with the next 32 register-prefetched.
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(NT) void sb_wgrad_kernel(SBWgradArgs a) {
-  constexpr int LG = 64 + 8, LA = C + 8;
+template <int C>
+__global__ __launch_bounds__(256) void sb_wgrad_kernel(SBWgradArgs a) {
+  constexpr int LG = 64 + 8, LA = C + 8, TT = C / 64, AC = C / 64;  // A chunks (16 B) per thread
   __shared__ __attribute__((aligned(16))) uint16_t sG[2][NR * LG];
   __shared__ __attribute__((aligned(16))) uint16_t sA[2][NR * LA];
   const int w = wave_id(), l = lane_id();
@@ -507,27 +544,29 @@ __global__ __launch_bounds__(NT) void sb_wgrad_kernel(SBWgradArgs a) {
   const SBWgradJob& jb = a.job[j];
   const int n0 = 64 * ((int)blockIdx.x - jb.tile0);
   const int r_begin = blockIdx.y * a.rows_per_split, r_end = min(a.R, r_begin + a.rows_per_split);
-  // staging: thread t loads G chunk (row t >> 3, 8 columns) and A chunks (row t >> 3, 16 columns)
-  const int sr = threadIdx.x >> 3, gc = (threadIdx.x & 7) * 8, ac = (threadIdx.x & 7) * 16;
-  bf16x8 g0, a0, a1;
+  // staging: thread t loads a G chunk (row t >> 3, 8 columns) and AC A chunks (row t >> 3)
+  const int sr = threadIdx.x >> 3, gc = (threadIdx.x & 7) * 8, ac = (threadIdx.x & 7) * 8 * AC;
+  bf16x8 g0, av[AC];
   auto fetch = [&](int r0) {
     const long long rr = r0 + sr;
     g0 = *reinterpret_cast<const bf16x8*>(jb.G + rr * jb.N + n0 + gc);
-    a0 = *reinterpret_cast<const bf16x8*>(jb.A + rr * C + ac);
-    a1 = *reinterpret_cast<const bf16x8*>(jb.A + rr * C + ac + 8);
+#pragma unroll
+    for (int q = 0; q < AC; ++q) av[q] = *reinterpret_cast<const bf16x8*>(jb.A + rr * C + ac + 8 * q);
   };
-  f32x16 acc[2] = {f32x16{}, f32x16{}};
+  f32x16 acc[TT];
+#pragma unroll
+  for (int tt = 0; tt < TT; ++tt) acc[tt] = f32x16{};
   f32x16 bacc = f32x16{};
-  const int mi = 32 * (w >> 1);  // dW rows (G columns) of this wave within the tile
-  const int kc = 64 * (w & 1);   // dW columns (A columns)
+  const int mi = 32 * (w >> 1);        // dW rows (G columns) of this wave within the tile
+  const int kc = (C / 2) * (w & 1);    // dW columns (A columns)
   const short one = (short)0x3F80;
   const bf16x8 ones = bf16x8{one, one, one, one, one, one, one, one};
   if (r_begin < r_end) fetch(r_begin);
   int buf = 0;
   for (int r0 = r_begin; r0 < r_end; r0 += NR, buf ^= 1) {
     *reinterpret_cast<bf16x8*>(sG[buf] + sr * LG + gc) = g0;
-    *reinterpret_cast<bf16x8*>(sA[buf] + sr * LA + ac) = a0;
-    *reinterpret_cast<bf16x8*>(sA[buf] + sr * LA + ac + 8) = a1;
+#pragma unroll
+    for (int q = 0; q < AC; ++q) *reinterpret_cast<bf16x8*>(sA[buf] + sr * LA + ac + 8 * q) = av[q];
     __syncthreads();
     if (r0 + NR < r_end) fetch(r0 + NR);
     // contraction over the 32 rows: A operand Gᵀ (element (n, r) at sG[r][n]), B operand A
@@ -536,14 +575,14 @@ __global__ __launch_bounds__(NT) void sb_wgrad_kernel(SBWgradArgs a) {
     for (int ks = 0; ks < 2; ++ks) {
       const bf16x8 ga = frag_ks(sG[buf], LG, mi, 16 * ks);
 #pragma unroll
-      for (int tt = 0; tt < 2; ++tt) acc[tt] = mfma32(ga, frag_ks(sA[buf], LA, kc + 32 * tt, 16 * ks), acc[tt]);
+      for (int tt = 0; tt < TT; ++tt) acc[tt] = mfma32(ga, frag_ks(sA[buf], LA, kc + 32 * tt, 16 * ks), acc[tt]);
       if ((w & 1) == 0) bacc = mfma32(ga, ones, bacc);
     }
   }
   // accumulator: col = k (lane), row = n = acc_row(i, hh)
   const int hh = l >> 5;
 #pragma unroll
-  for (int tt = 0; tt < 2; ++tt)
+  for (int tt = 0; tt < TT; ++tt)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int n = n0 + mi + acc_row(i, hh), k = kc + 32 * tt + (l & 31);
@@ -556,19 +595,23 @@ __global__ __launch_bounds__(NT) void sb_wgrad_kernel(SBWgradArgs a) {
 
 }  // namespace sb
 
-bool sb_fwd_launch(const SBFwdArgs& a, hipStream_t st) {
+bool sb_fwd_launch(const SBFwdArgs& a, int C, hipStream_t st) {
   if (a.L < 1 || a.L > kSBMaxLayers || a.B < 1) return false;
-  hipLaunchKernelGGL(sb::sb_fwd_kernel, dim3(a.B), dim3(sb::NT), 0, st, a);
+  if (C == 128) hipLaunchKernelGGL(sb::sb_fwd_kernel<128>, dim3(a.B), dim3(256), 0, st, a);
+  else if (C == 64) hipLaunchKernelGGL(sb::sb_fwd_kernel<64>, dim3(a.B), dim3(128), 0, st, a);
+  else return false;
   return true;
 }
-bool sb_bwd_launch(const SBBwdArgs& a, hipStream_t st) {
+bool sb_bwd_launch(const SBBwdArgs& a, int C, hipStream_t st) {
   if (a.L < 1 || a.L > kSBMaxLayers || a.B < 1) return false;
-  hipLaunchKernelGGL(sb::sb_bwd_kernel, dim3(a.B), dim3(sb::NT), 0, st, a);
+  if (C == 128) hipLaunchKernelGGL(sb::sb_bwd_kernel<128>, dim3(a.B), dim3(256), 0, st, a);
+  else if (C == 64) hipLaunchKernelGGL(sb::sb_bwd_kernel<64>, dim3(a.B), dim3(128), 0, st, a);
+  else return false;
   return true;
 }
 // rows per split: about 512 rows per workgroup (≥ 1 split; a multiple of 32)
-bool sb_wgrad_launch(SBWgradArgs a, hipStream_t st) {
-  if (a.njobs < 1 || a.njobs > kSBMaxJobs || a.R % sb::NR != 0) return false;
+bool sb_wgrad_launch(SBWgradArgs a, int C, hipStream_t st) {
+  if (a.njobs < 1 || a.njobs > kSBMaxJobs || a.R % sb::NR != 0 || (C != 64 && C != 128)) return false;
   int tiles = 0;
   for (int j = 0; j < a.njobs; ++j) {
     if (a.job[j].N % 64 != 0) return false;
@@ -578,7 +621,8 @@ bool sb_wgrad_launch(SBWgradArgs a, hipStream_t st) {
   int splits = (a.R + 511) / 512;
   a.rows_per_split = (a.R / sb::NR + splits - 1) / splits * sb::NR;
   splits = (a.R + a.rows_per_split - 1) / a.rows_per_split;
-  hipLaunchKernelGGL(sb::sb_wgrad_kernel, dim3(tiles, splits), dim3(sb::NT), 0, st, a);
+  if (C == 128) hipLaunchKernelGGL(sb::sb_wgrad_kernel<128>, dim3(tiles, splits), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(sb::sb_wgrad_kernel<64>, dim3(tiles, splits), dim3(256), 0, st, a);
   return true;
 }
 

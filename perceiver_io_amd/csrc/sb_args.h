@@ -8,7 +8,7 @@ namespace pio {
 constexpr int kSBMaxLayers = 4;  // self-attention layers per block (the image configs run 3)
 
 // one self-attention layer (reference model.py:36-44: x → LN1 → MHA → +x → LN2 → MLP → +) of a
-// C = 128, H = 4 block over N = 32 latents: weights, then the forward's saved rows (every one
+// C ∈ {64, 128}, H = 4 block over N = 32 latents: weights, then the forward's saved rows (every one
 // an operand of the backward or of the weight-gradient GEMMs)
 struct SBLayer {
   const uint16_t *Wqkv, *Wo, *W1, *W2;         // bf16 [3C][C], [C][C] ×3 (nn.Linear layout)
@@ -38,14 +38,14 @@ struct SBBwdArgs {
   float scale_log2, eps;
 };
 // grouped weight-gradient GEMMs: dW[n][k] += Σ_rows G[r][n] · A[r][k], db[n] += Σ_rows G[r][n]
-// (A is 128 wide: every self-attention weight's input); one job per weight
+// (A is C wide: every self-attention weight's input); one job per weight
 constexpr int kSBMaxJobs = 4 * kSBMaxLayers;
 struct SBWgradJob {
   const uint16_t* G;  // bf16 [R][N]
-  const uint16_t* A;  // bf16 [R][128]
-  float* dW;          // fp32 [N][128] (added to)
+  const uint16_t* A;  // bf16 [R][C]
+  float* dW;          // fp32 [N][C] (added to)
   float* db;          // fp32 [N] (added to)
-  int N;              // 128 or 384
+  int N;              // C or 3C (a multiple of 64)
   int tile0;          // first 64-column tile index of this job in the grid
 };
 struct SBWgradArgs {

@@ -1072,12 +1072,12 @@ def _sample_block_ok(specs, n: int, p: float, cuda: bool) -> bool:
     from . import deterministic
 
     sp = specs[0]
-    return (SAMPLE_BLOCK and cuda and sp.C == 128 and sp.heads == 4 and n == 32 and p == 0.0 and not sp.cross
+    return (SAMPLE_BLOCK and cuda and sp.C in (64, 128) and sp.heads == 4 and n == 32 and p == 0.0 and not sp.cross
             and 1 <= len(specs) <= 4 and all(s == sp for s in specs) and not deterministic())
 
 
 class _SampleBlockFn(torch.autograd.Function):
-    """A C = 128, 32-latent self-attention block as per-sample kernels (reference model.py:36-44):
+    """A C ∈ {64, 128}, 4-head, 32-latent self-attention block as per-sample kernels (reference model.py:36-44):
     forward saves, per layer, the rows the backward and the weight-gradient GEMMs read (LN1(x),
     QKV, O, LN2(y), u, GELU(u) in bf16; y, z and the LayerNorm statistics in fp32); backward runs
     the per-sample backward (activation gradients + LayerNorm affine gradients) and one grouped
