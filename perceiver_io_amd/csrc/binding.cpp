@@ -66,7 +66,7 @@ bool attn_bwd_bf16_launch(const AttnArgs&, int, const uint16_t*, const float*, c
 int attn_bwd_zero_plan(int, int, int, int, int);
 void ln_linear_fwd_launch(const void*, bool, int, int, int, const float*, const float*, float, const uint16_t*, int,
                           const float*, int, int, const float*, int, void*, bool, int, float*, float*, const float*, int,
-                          int, int, hipStream_t);
+                          int, int, const long long*, hipStream_t);
 void post_attn_fwd_launch(int, const uint16_t*, const float*, const uint16_t*, const float*, const float*,
                           const float*, float, const uint16_t*, const float*, const uint16_t*, const float*, float*,
                           float*, float*, float*, uint16_t*, int, int, const DropCfg&, hipStream_t);
@@ -91,10 +91,11 @@ void post_attn_bwd_launch(int, const float*, const float*, const float*, const f
                           const DropCfg&, hipStream_t);
 void ln_linear_bwd_launch(const void*, bool, int, int, const uint16_t*, int, int, const void*, bool, int, const float*,
                           const float*, const float*, const float*, const float*, int, float*, int, float*, float*,
-                          float*, float*, int, int, int, int, const float*, int, int, int, const SlabJob&, hipStream_t);
+                          float*, float*, int, int, int, int, const float*, int, int, int, const long long*, const SlabJob&,
+                          hipStream_t);
 void wgrad_launch(const void*, bool, int, int, const void*, bool, int, int, int, const float*, const float*,
                   const float*, const float*, int, int, float*, float*, int, int, const float*, int, int, int,
-                  hipStream_t);
+                  const long long*, hipStream_t);
 void ce_fwd_launch(int, const float*, const int64_t*, const int64_t*, const uint16_t*, const float*, int, int, float*,
                    float*, float*, float*, float*, float*, unsigned*, uint16_t*, int, float*, long long, int, hipStream_t);
 int ce_combine_blocks(int);
@@ -349,16 +350,25 @@ std::vector<Tensor> attn_bwd(Tensor q, Tensor k, Tensor v, OptT kmask, Tensor o,
 }
 
 // pe (optional, SURVEY K-03): x holds only the npix pixel channels of each row and row r's
-// input is pe[r mod rows(pe)] with the pixels added into its npix leading (zero) columns;
-// pe is (M, pe_rs) fp32 contiguous with pe_rs a multiple of 8, ≥ Kin = w.size(1)
+// input is pe[r mod rows(pe)] — or pe[pe_index[r]] when the (R,) int64 pe_index is given (sparse
+// images) — with the pixels added into its npix leading (zero) columns; pe is (M, pe_rs) fp32
+// contiguous with pe_rs a multiple of 8, ≥ Kin = w.size(1)
 namespace {
-void pe_args(const OptT& pe, const Tensor& x, int R, int Kin, const float*& pp, int& prs, int& prows, int& npix) {
-  pp = nullptr; prs = 0; prows = 1; npix = 0;
+void pe_args(const OptT& pe, const Tensor& x, int R, int Kin, const float*& pp, int& prs, int& prows, int& npix,
+             const OptT& pe_index, const long long*& pidx) {
+  pp = nullptr; prs = 0; prows = 1; npix = 0; pidx = nullptr;
+  TORCH_CHECK(!pe_index.has_value() || pe.has_value(), "pe_index needs a pe table");
   if (!pe.has_value()) return;
   CHECK_DT(*pe, torch::kFloat32);
   TORCH_CHECK(pe->dim() == 2 && pe->is_contiguous() && pe->size(1) % 8 == 0 && pe->size(1) >= Kin,
               "pe must be (M, pe_rs) contiguous fp32, pe_rs a multiple of 8 and >= Kin");
-  TORCH_CHECK(R % pe->size(0) == 0, "rows must be a multiple of the PE rows");
+  if (pe_index.has_value()) {
+    CHECK_DT(*pe_index, torch::kInt64);
+    TORCH_CHECK(pe_index->is_contiguous() && pe_index->numel() == R, "pe_index must be R contiguous int64 rows");
+    pidx = reinterpret_cast<const long long*>(pe_index->data_ptr<int64_t>());
+  } else {
+    TORCH_CHECK(R % pe->size(0) == 0, "rows must be a multiple of the PE rows");
+  }
   TORCH_CHECK(reinterpret_cast<uintptr_t>(pe->data_ptr()) % 16 == 0, "pe must be 16-byte aligned");
   pp = pe->data_ptr<float>(); prs = (int)pe->size(1); prows = (int)pe->size(0); npix = (int)x.size(1);
   TORCH_CHECK(npix <= Kin, "more pixel channels than inputs");
@@ -367,7 +377,7 @@ void pe_args(const OptT& pe, const Tensor& x, int R, int Kin, const float*& pp, 
 
 // kin (optional): the logical input width when w's rows are zero padded past it (w (N, ≥ kin))
 std::vector<Tensor> ln_linear_fwd(Tensor x, OptT lnw, OptT lnb, double eps, Tensor w, OptT bias, int64_t act, OptT res,
-                                  bool out_bf16, bool save_stats, OptT pe, int64_t kin) {
+                                  bool out_bf16, bool save_stats, OptT pe, int64_t kin, OptT pe_index) {
   CHECK_CUDA(x); CHECK_CUDA(w);
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be 2-D rows");
   const int R = (int)x.size(0), N = (int)w.size(0);
@@ -375,8 +385,8 @@ std::vector<Tensor> ln_linear_fwd(Tensor x, OptT lnw, OptT lnb, double eps, Tens
   TORCH_CHECK(w.dim() == 2 && w.is_contiguous() && w.size(1) >= Kin, "w must be (N, >= Kin) contiguous");
   TORCH_CHECK(pe.has_value() || x.size(1) == Kin, "x must be (R, Kin)");
   TORCH_CHECK(Kin <= 256, "Kin > 256 unsupported");
-  const float* pp; int prs, prows, npix;
-  pe_args(pe, x, R, Kin, pp, prs, prows, npix);
+  const float* pp; int prs, prows, npix; const long long* pidx;
+  pe_args(pe, x, R, Kin, pp, prs, prows, npix, pe_index, pidx);
   auto opts = x.options();
   Tensor y = torch::empty({R, N}, opts.dtype(out_bf16 ? torch::kBFloat16 : torch::kFloat32));
   Tensor mean, rstd;
@@ -390,7 +400,7 @@ std::vector<Tensor> ln_linear_fwd(Tensor x, OptT lnw, OptT lnb, double eps, Tens
   if (res.has_value()) { rptr = f32p(*res); res_rs = (int)res->stride(0); TORCH_CHECK(res->stride(1) == 1); }
   pio::ln_linear_fwd_launch(x.data_ptr(), is_bf16(x), (int)x.stride(0), R, Kin, f32o(lnw), f32o(lnb), (float)eps, bfp(w),
                             (int)w.size(1), f32o(bias), N, (int)act, rptr, res_rs, y.data_ptr(), out_bf16, N, mp, rp, pp, prs, prows,
-                            npix, stream());
+                            npix, pidx, stream());
   std::vector<Tensor> out{y};
   if (mp) { out.push_back(mean); out.push_back(rstd); }
   return out;
@@ -882,7 +892,7 @@ constexpr int kTallRows = 1 << 17;
 
 OptT ln_linear_bwd(Tensor g, Tensor w, Tensor x, OptT mean, OptT rstd, OptT lnw, OptT lnb, OptT dres, bool need_dx,
                    OptT dlnw, OptT dlnb, OptT dW, OptT db, OptT pe, int64_t kin, bool slab, OptT job_slab,
-                   std::vector<Tensor> job_dsts, std::vector<int64_t> job_offs, OptT dx_out) {
+                   std::vector<Tensor> job_dsts, std::vector<int64_t> job_offs, OptT dx_out, OptT pe_index) {
   TORCH_CHECK(g.dim() == 2 && g.stride(1) == 1 && x.dim() == 2 && x.stride(1) == 1, "g / x must be 2-D rows");
   const int R = (int)g.size(0), N = (int)g.size(1);
   TORCH_CHECK(!(slab && R >= kTallRows), "slab gradients are for R < ", kTallRows, " rows");
@@ -893,8 +903,8 @@ OptT ln_linear_bwd(Tensor g, Tensor w, Tensor x, OptT mean, OptT rstd, OptT lnw,
   TORCH_CHECK(w.size(0) == N && w.is_contiguous() && w.size(1) >= Kin, "w must be (N, >= Kin) contiguous, N = g columns");
   TORCH_CHECK(x.size(0) == R && (pe.has_value() || x.size(1) == Kin), "x must be (R, Kin)");
   TORCH_CHECK(!(pe.has_value() && need_dx), "no input gradient for a split (pixels + PE) input");
-  const float* pp; int prs, prows, npix;
-  pe_args(pe, x, R, Kin, pp, prs, prows, npix);
+  const float* pp; int prs, prows, npix; const long long* pidx;
+  pe_args(pe, x, R, Kin, pp, prs, prows, npix, pe_index, pidx);
   TORCH_CHECK(Kin <= 160, "ln_linear_bwd supports Kin <= 160");
   auto f32 = g.options().dtype(torch::kFloat32);
   Tensor dx;
@@ -929,19 +939,19 @@ OptT ln_linear_bwd(Tensor g, Tensor w, Tensor x, OptT mean, OptT rstd, OptT lnw,
   pio::ln_linear_bwd_launch(g.data_ptr(), is_bf16(g), (int)g.stride(0), N, bfp(w), (int)w.size(1), Kin, x.data_ptr(),
                             is_bf16(x), (int)x.stride(0), f32o(mean), f32o(rstd), f32o(lnw), f32o(lnb), dr, drs, dxp,
                             dx_rs, dgp, dbp, tall ? nullptr : dwp, tall ? nullptr : dbiasp, vrs < 0 ? 0 : vrs,
-                            wrs < 0 ? 0 : wrs, slab ? 1 : 0, R, pp, prs, prows, npix,
+                            wrs < 0 ? 0 : wrs, slab ? 1 : 0, R, pp, prs, prows, npix, pidx,
                             make_job(job_slab, job_dsts, job_offs), stream());
   if (tall)
     pio::wgrad_launch(g.data_ptr(), is_bf16(g), (int)g.stride(0), N, x.data_ptr(), is_bf16(x), (int)x.stride(0), Kin,
                       lnw.has_value() ? 1 : 0, f32o(mean), f32o(rstd), f32o(lnw), f32o(lnb), R, 0, dwp, dbiasp,
-                      vrs < 0 ? 0 : vrs, wrs < 0 ? 0 : wrs, pp, prs, prows, npix, stream());
+                      vrs < 0 ? 0 : vrs, wrs < 0 ? 0 : wrs, pp, prs, prows, npix, pidx, stream());
   if (need_dx) return dx;
   return c10::nullopt;
 }
 
 // dW (+)= gᵀ·A', db (+)= Σ rows g  (A' = a | LN(a) | GELU(a); a may be pixels with a PE table)
 void wgrad(Tensor g, Tensor a, int64_t amode, OptT mean, OptT rstd, OptT lnw, OptT lnb, int64_t rows_per_wg, Tensor dW,
-           OptT db, OptT pe, int64_t kin) {
+           OptT db, OptT pe, int64_t kin, OptT pe_index) {
   TORCH_CHECK(g.dim() == 2 && a.dim() == 2 && g.stride(1) == 1 && a.stride(1) == 1, "2-D row tensors expected");
   const int R = (int)g.size(0), N = (int)g.size(1);
   const int Kin = kin >= 0 ? (int)kin : (int)a.size(1);
@@ -951,14 +961,14 @@ void wgrad(Tensor g, Tensor a, int64_t amode, OptT mean, OptT rstd, OptT lnw, Op
   TORCH_CHECK(!g_det, "deterministic mode: the streaming wgrad kernel adds partials with atomics");
   TORCH_CHECK(amode != 1 || (mean.has_value() && rstd.has_value() && lnw.has_value() && lnb.has_value()),
               "LN mode needs stats and affine");
-  const float* pp; int prs, prows, npix;
-  pe_args(pe, a, R, Kin, pp, prs, prows, npix);
+  const float* pp; int prs, prows, npix; const long long* pidx;
+  pe_args(pe, a, R, Kin, pp, prs, prows, npix, pe_index, pidx);
   int wrs = -1, vrs = -1;
   float* dwp = vec_target(dW, (int64_t)N * Kin, "dW", wrs);
   float* dbp = db.has_value() ? vec_target(*db, N, "db", vrs) : nullptr;
   pio::wgrad_launch(g.data_ptr(), is_bf16(g), (int)g.stride(0), N, a.data_ptr(), is_bf16(a), (int)a.stride(0), Kin,
                     (int)amode, f32o(mean), f32o(rstd), f32o(lnw), f32o(lnb), R, (int)rows_per_wg, dwp, dbp,
-                    vrs < 0 ? 0 : vrs, wrs < 0 ? 0 : wrs, pp, prs, prows, npix, stream());
+                    vrs < 0 ? 0 : vrs, wrs < 0 ? 0 : wrs, pp, prs, prows, npix, pidx, stream());
 }
 
 // per-device ticket of the CE combine kernel (its last workgroup sums the per-block partials):
@@ -1698,7 +1708,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("D"));
   m.def("ln_linear_fwd", &ln_linear_fwd, py::arg("x"), py::arg("lnw"), py::arg("lnb"), py::arg("eps"), py::arg("w"),
         py::arg("bias"), py::arg("act"), py::arg("res"), py::arg("out_bf16"), py::arg("save_stats"),
-        py::arg("pe") = py::none(), py::arg("kin") = -1);
+        py::arg("pe") = py::none(), py::arg("kin") = -1, py::arg("pe_index") = py::none());
   m.def("post_attn_fwd", &post_attn_fwd, py::arg("o"), py::arg("x"), py::arg("wo"), py::arg("bo"), py::arg("g2"),
         py::arg("be2"), py::arg("eps"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("b2"),
         py::arg("seed") = py::none(), py::arg("site") = 0, py::arg("p") = 0.0);
@@ -1735,10 +1745,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("lnw"), py::arg("lnb"), py::arg("dres"), py::arg("need_dx"), py::arg("dlnw"), py::arg("dlnb"),
         py::arg("dW"), py::arg("db"), py::arg("pe") = py::none(), py::arg("kin") = -1, py::arg("slab") = false,
         py::arg("job_slab") = py::none(), py::arg("job_dsts") = std::vector<Tensor>(),
-        py::arg("job_offs") = std::vector<int64_t>(), py::arg("dx_out") = py::none());
+        py::arg("job_offs") = std::vector<int64_t>(), py::arg("dx_out") = py::none(), py::arg("pe_index") = py::none());
   m.def("wgrad", &wgrad, py::arg("g"), py::arg("a"), py::arg("amode"), py::arg("mean"), py::arg("rstd"), py::arg("lnw"),
         py::arg("lnb"), py::arg("rows_per_wg"), py::arg("dW"), py::arg("db"), py::arg("pe") = py::none(),
-        py::arg("kin") = -1);
+        py::arg("kin") = -1, py::arg("pe_index") = py::none());
   m.def("mlm_select", &mlm_select, py::arg("labels"), py::arg("cap"), py::arg("gcap"), py::arg("sticky") = py::none(),
         py::arg("queries") = py::none());
   m.def("index_add_rows", &index_add_rows);

@@ -188,11 +188,19 @@ __device__ __forceinline__ void row_load(float (&v)[NCH][8], const T* __restrict
 // Fourier-PE split input (SURVEY K-03): logical row r = pe[r mod M] (row stride pe_rs, a
 // multiple of 8, with npix leading zero columns and zero padding past Kin) + the npix pixel
 // values of row r in those leading columns.  The (B, M, npix + C_pe) concatenation is never
-// materialised; the PE table stays L2/MALL-resident across the batch.
+// materialised; the PE table stays L2/MALL-resident across the batch.  With idx given (sparse
+// images: the LArTPC events' non-zero pixels, models/lartpc.py) row r reads pe[idx[r]] instead
+// (clamped into the table), so the gathered [pixel ‖ PE] rows are not materialised either.
 struct PeSplit {
   const float* pe;
   int pe_rs, M, npix;
+  const long long* idx;
 };
+__device__ __forceinline__ int pe_row(const PeSplit& ps, int gr) {
+  if (ps.idx == nullptr) return gr % ps.M;
+  const long long i = ps.idx[gr];
+  return i < 0 ? 0 : (i >= ps.M ? ps.M - 1 : (int)i);
+}
 
 template <int NCH, typename T>
 __device__ __forceinline__ void row_load_x(float (&v)[NCH][8], const T* __restrict__ X, long long x_rs, int gr, int R,
@@ -201,7 +209,7 @@ __device__ __forceinline__ void row_load_x(float (&v)[NCH][8], const T* __restri
     row_load<NCH>(v, X, x_rs, gr, R, Kin, vec);
     return;
   }
-  row_load<NCH>(v, ps.pe, ps.pe_rs, gr < R ? gr % ps.M : 0, gr < R ? ps.M : 0, ps.pe_rs, true);
+  row_load<NCH>(v, ps.pe, ps.pe_rs, gr < R ? pe_row(ps, gr) : 0, gr < R ? ps.M : 0, ps.pe_rs, true);
   if (gr < R) {
 #pragma unroll
     for (int j = 0; j < NCH; ++j) {
@@ -1410,9 +1418,9 @@ static void ln_linear_fwd_n(int nch, const void* X, int x_rs, int R, int Kin, co
 void ln_linear_fwd_launch(const void* X, bool x_bf16, int x_rs, int R, int Kin, const float* lnw, const float* lnb,
                           float eps, const uint16_t* W, int w_rs, const float* bias, int N, int act, const float* res,
                           int res_rs, void* Y, bool y_bf16, int y_rs, float* mean, float* rstd, const float* pe, int pe_rs,
-                          int pe_rows, int npix, hipStream_t st) {
+                          int pe_rows, int npix, const long long* pe_idx, hipStream_t st) {
   const int nch = pick_nch(Kin);
-  const PeSplit ps{pe, pe_rs, pe_rows, npix};
+  const PeSplit ps{pe, pe_rs, pe_rows, npix, pe_idx};
 #define LNL(TI, TO) \
   ln_linear_fwd_n<TI, TO>(nch, X, x_rs, R, Kin, lnw, lnb, eps, W, w_rs, bias, N, act, res, res_rs, Y, y_rs, mean, rstd, ps, st)
   if (x_bf16 && y_bf16) LNL(uint16_t, uint16_t);
@@ -1567,9 +1575,9 @@ void ln_linear_bwd_launch(const void* G, bool g_bf16, int g_rs, int N, const uin
                           bool x_bf16, int x_rs, const float* mean, const float* rstd, const float* lnw,
                           const float* lnb, const float* dres, int dres_rs, float* dX, int dx_rs, float* dlnw,
                           float* dlnb, float* dW, float* db, int vrs, int wrs, int slab, int R, const float* pe,
-                          int pe_rs, int pe_rows, int npix, const SlabJob& job, hipStream_t st) {
+                          int pe_rs, int pe_rows, int npix, const long long* pe_idx, const SlabJob& job, hipStream_t st) {
   const int nch = pick_nch(Kin);  // Kin ≤ 160 → ≤ 5
-  const PeSplit ps{pe, pe_rs, pe_rows, npix};
+  const PeSplit ps{pe, pe_rs, pe_rows, npix, pe_idx};
 #define LDG(TG, TX)                                                                                           \
   ln_linear_bwd_n<TG, TX>(nch, G, g_rs, N, W, w_rs, Kin, X, x_rs, mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, \
                           dlnw, dlnb, dW, db, vrs, wrs, slab, R, ps, job, st)
@@ -1611,7 +1619,7 @@ static void wgrad_n(int nch, const void* G, int g_rs, int N, const void* A, int 
 void wgrad_launch(const void* G, bool g_bf16, int g_rs, int N, const void* A, bool a_bf16, int a_rs, int Kin,
                   int amode, const float* mean, const float* rstd, const float* lnw, const float* lnb, int R,
                   int rows_per_wg, float* dW, float* db, int vrs, int wrs, const float* pe, int pe_rs, int pe_rows,
-                  int npix, hipStream_t st) {
+                  int npix, const long long* pe_idx, hipStream_t st) {
   const int nblk = (N + 63) / 64;
   int rps = rows_per_wg;
   if (rps <= 0) {
@@ -1619,7 +1627,7 @@ void wgrad_launch(const void* G, bool g_bf16, int g_rs, int N, const void* A, bo
     rps = (R + splits - 1) / splits;
   }
   rps = round_up(rps < 64 ? 64 : rps, 64);
-  const PeSplit ps{pe, pe_rs, pe_rows, npix};
+  const PeSplit ps{pe, pe_rs, pe_rows, npix, pe_idx};
   const int nch = pick_nch(Kin);
 #define WG(TG, TA) wgrad_n<TG, TA>(nch, G, g_rs, N, A, a_rs, Kin, amode, mean, rstd, lnw, lnb, R, rps, dW, db, vrs, wrs, ps, st)
   if (g_bf16 && a_bf16) WG(uint16_t, uint16_t);

@@ -87,9 +87,13 @@ class LArPerceiver(torch.nn.Module):
 
     def sparse_hidden(self, values, index, kmask, qidx):
         """Decoder output ``(B, K', C)`` at output pixels ``qidx``, from the non-zero pixels only."""
+        from .. import ops
+
         enc, dec = self.perceiver.encoder, self.perceiver.decoder
-        x_in = sparse_inputs(enc.input_adapter, values, index)
-        lat = enc.forward_inputs(x_in, kmask)
+        if ops.use_hip(enc.latent):  # PE rows read at `index` inside the K/V projection kernels
+            lat = ops.fused.encode_sparse(enc, values, index, kmask)
+        else:
+            lat = enc.forward_inputs(sparse_inputs(enc.input_adapter, values, index), kmask)
         return dec.hidden_at(lat, qidx)
 
     def sparse_logits(self, values, index, kmask, qidx):

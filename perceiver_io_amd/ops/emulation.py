@@ -73,21 +73,25 @@ def _ln(x, w, b, eps):
     return (x - mean[:, None]) * rstd[:, None] * w + b, mean, rstd
 
 
-def _split_x(x, pe, kin):
-    """Logical input rows: x itself, or pe[r mod M] (first kin columns) with x's pixel
-    channels added into the leading columns (SURVEY K-03 split input)."""
+def _split_x(x, pe, kin, pe_index=None):
+    """Logical input rows: x itself, or pe[r mod M] — pe[pe_index[r]] when given (sparse
+    images) — (first kin columns) with x's pixel channels added into the leading columns
+    (SURVEY K-03 split input)."""
     if pe is None:
         return x.float()
     r, m = x.shape[0], pe.shape[0]
-    full = pe.repeat(r // m, 1)[:, :kin].clone()
+    if pe_index is not None:
+        full = pe.index_select(0, pe_index.reshape(-1).clamp(0, m - 1))[:, :kin].clone()
+    else:
+        full = pe.repeat(r // m, 1)[:, :kin].clone()
     full[:, : x.shape[1]] += x.float()
     return full
 
 
-def ln_linear_fwd(x, lnw, lnb, eps, w, bias, act, res, out_bf16, save_stats, pe=None, kin=-1):
+def ln_linear_fwd(x, lnw, lnb, eps, w, bias, act, res, out_bf16, save_stats, pe=None, kin=-1, pe_index=None):
     if kin >= 0:
         w = w[:, :kin]
-    xf = _split_x(x, pe, w.shape[1])
+    xf = _split_x(x, pe, w.shape[1], pe_index)
     mean = rstd = None
     if lnw is not None:
         xn, mean, rstd = _ln(xf, lnw, lnb, eps)
@@ -446,13 +450,13 @@ def _post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, be2, H, grads, seed=None
 
 
 def ln_linear_bwd(g, w, x, mean, rstd, lnw, lnb, dres, need_dx, dlnw=None, dlnb=None, dW=None, db=None, pe=None,
-                  kin=-1, slab=False, job_slab=None, job_dsts=(), job_offs=(), dx_out=None):
+                  kin=-1, slab=False, job_slab=None, job_dsts=(), job_offs=(), dx_out=None, pe_index=None):
     """Returns dX (or None); LN grads accumulate into dlnw / dlnb and, when given,
     dW += gᵀ·LN(x), db += Σ_rows g (slab: stored into (tiles, ·) slab views)."""
     _run_job(job_slab, job_dsts, job_offs)
     _SLAB[0] = slab
     try:
-        dx = _ln_linear_bwd(g, w, x, mean, rstd, lnw, lnb, dres, need_dx, dlnw, dlnb, dW, db, pe, kin)
+        dx = _ln_linear_bwd(g, w, x, mean, rstd, lnw, lnb, dres, need_dx, dlnw, dlnb, dW, db, pe, kin, pe_index)
     finally:
         _SLAB[0] = False
     if dx is not None and dx_out is not None:
@@ -461,12 +465,12 @@ def ln_linear_bwd(g, w, x, mean, rstd, lnw, lnb, dres, need_dx, dlnw=None, dlnb=
     return dx
 
 
-def _ln_linear_bwd(g, w, x, mean, rstd, lnw, lnb, dres, need_dx, dlnw, dlnb, dW, db, pe, kin):
+def _ln_linear_bwd(g, w, x, mean, rstd, lnw, lnb, dres, need_dx, dlnw, dlnb, dW, db, pe, kin, pe_index=None):
     if kin >= 0:
         w = w[:, :kin]
     gf = g.float()
     dxn = _bf(gf) @ _bf(w.float())
-    xf = _split_x(x, pe, w.shape[1])
+    xf = _split_x(x, pe, w.shape[1], pe_index)
     if dW is not None:
         xn = (xf - mean[:, None]) * rstd[:, None] * lnw + lnb if lnw is not None else xf
         _acc(dW, _bf(gf).t() @ _bf(xn))
@@ -483,9 +487,9 @@ def _ln_linear_bwd(g, w, x, mean, rstd, lnw, lnb, dres, need_dx, dlnw, dlnb, dW,
     return None
 
 
-def wgrad(g, a, amode, mean, rstd, lnw, lnb, rows_per_wg, dW, db=None, pe=None, kin=-1):
+def wgrad(g, a, amode, mean, rstd, lnw, lnb, rows_per_wg, dW, db=None, pe=None, kin=-1, pe_index=None):
     """dW += Gᵀ·A(transformed), db += Σ_rows G (accumulated in place)."""
-    af = _split_x(a, pe, kin if kin >= 0 else a.shape[1])
+    af = _split_x(a, pe, kin if kin >= 0 else a.shape[1], pe_index)
     if amode == 1:
         af = (af - mean[:, None]) * rstd[:, None] * lnw + lnb
     elif amode == 2:

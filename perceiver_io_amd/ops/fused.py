@@ -262,12 +262,16 @@ class KVSource:
       queries depend on its output).
     * K-03 (``adapter.py:99-109`` materialises ``[pixels ‖ Fourier PE]``): with ``pe`` given, ``x``
       holds only the pixels ``(B, M, C_img)`` and the projection kernels add them into the
-      zero leading columns of the padded PE table ``pe`` ``(M, round_up(Kin, 8))``.
+      zero leading columns of the padded PE table ``pe`` ``(M, round_up(Kin, 8))``; with ``index``
+      (B, M) int64 given (sparse images, ``models/lartpc.py``) row (b, m) reads PE row
+      ``index[b, m]`` instead of ``m``, so the gathered ``[pixel ‖ PE]`` rows are never formed.
     """
 
-    def __init__(self, x: torch.Tensor, pe: Optional[torch.Tensor] = None, kin: Optional[int] = None):
+    def __init__(self, x: torch.Tensor, pe: Optional[torch.Tensor] = None, kin: Optional[int] = None,
+                 index: Optional[torch.Tensor] = None):
         self.x = x
         self.pe = pe
+        self.index = index
         self.kin = kin if kin is not None else x.shape[-1]
         self.entries = {}
         # input-gradient hand-off between the projections of different layers (layer_1 and
@@ -285,7 +289,10 @@ class KVSource:
         if self.pe is None:
             return self.x
         b, m = self.x.shape[0], self.x.shape[1]
-        full = self.pe[:, : self.kin].unsqueeze(0).repeat(b, 1, 1)
+        if self.index is not None:
+            full = self.pe[:, : self.kin].index_select(0, self.index.reshape(-1)).view(b, m, self.kin)
+        else:
+            full = self.pe[:, : self.kin].unsqueeze(0).repeat(b, 1, 1)
         full[:, :, : self.x.shape[2]] += self.x
         return full
 
@@ -294,6 +301,13 @@ class KVSource:
 # LN(x)·Wᵀ is batch-independent, so it is one (M × Kin)·(Kin × O) GEMM per step and each sample
 # only pays a bandwidth-bound epilogue.
 PE_FACTORED = True
+
+
+def _pe_index(src):
+    """(R,) int64 PE row of every K/V input row of a sparse source, else None."""
+    if src is None or src.index is None:
+        return None
+    return src.index.reshape(-1)
 
 
 def _pe_table(pe, nc: int, kin: int):
@@ -450,7 +464,8 @@ class _LayerFn(torch.autograd.Function):
             ent = src.entries.get(key) if src is not None else None
             ctx.kv_owner = ent is None
             if ent is None:  # first application of this layer: project K/V (LN over [pixels ‖ PE] if split)
-                factored = (PE_FACTORED and src is not None and src.pe is not None and not spec.packed
+                factored = (PE_FACTORED and src is not None and src.pe is not None and src.index is None
+                            and not spec.packed
                             and not ctx.needs_input_grad[6] and 1 <= xkv2.shape[1] <= 4 and 2 * C <= 512)
                 implicit = (factored and PE_IMPLICIT and PE_ATTN_FUSED and D == 32 and Nq <= 32 and kmask is None
                             and p_attn == 0.0 and hasattr(K, "attn_fwd_pe"))
@@ -474,7 +489,7 @@ class _LayerFn(torch.autograd.Function):
                     else:
                         kv, mean_kv, rstd_kv = K.ln_linear_fwd(xkv2, g_kv, b_kv, EPS, wkv, bin_[C:], 0, None, True,
                                                                True, src.pe if src is not None else None,
-                                                               g_kv.shape[0])
+                                                               g_kv.shape[0], _pe_index(src))
                 ent = {"kv": kv, "mean": mean_kv, "rstd": rstd_kv, "dkv": None, "factored": factored, "wkv": wkv,
                        "implicit": imp}
                 if src is not None:
@@ -482,6 +497,7 @@ class _LayerFn(torch.autograd.Function):
             kv, mean_kv, rstd_kv = ent["kv"], ent["mean"], ent["rstd"]
             ctx.kv_entry = ent
             ctx.kv_pe = src.pe if src is not None else None
+            ctx.kv_pe_index = _pe_index(src)
             q3 = q.view(Bq, Nq, C)
             if ent.get("implicit") is None:
                 kv3 = kv.view(B, M, 2 * C)
@@ -721,7 +737,8 @@ class _LayerFn(torch.autograd.Function):
                         src.owners_left = len(src.entries)
                     dx_kv = K.ln_linear_bwd(dkv2, wkv, xkv2, mean_kv, rstd_kv, g_kv, b_kv,
                                             src.pending_dx if chain else None, ctx.kv_grad,
-                                            *sl.targets(), ctx.kv_pe, Ckv, slab=True, **_take_job())
+                                            *sl.targets(), ctx.kv_pe, Ckv, slab=True, pe_index=ctx.kv_pe_index,
+                                            **_take_job())
                     if chain:  # hand the partial input gradient on; the last projection returns it
                         src.owners_left -= 1
                         if src.owners_left > 0:
@@ -741,7 +758,8 @@ class _LayerFn(torch.autograd.Function):
                     else:
                         gwkv = torch.zeros((8, 2 * C * Ckv) if rep_mode else (2 * C, Ckv), **f32)
                     dx_kv = K.ln_linear_bwd(dkv2, wkv, xkv2, mean_kv, rstd_kv, g_kv, b_kv, None, ctx.kv_grad,
-                                            gb(g_kv), gb(b_kv), gwkv, rows(gbias, C, 3 * C, 1), ctx.kv_pe, Ckv)
+                                            gb(g_kv), gb(b_kv), gwkv, rows(gbias, C, 3 * C, 1), ctx.kv_pe, Ckv,
+                                            pe_index=ctx.kv_pe_index)
                     if not spec.packed:
                         gb(ps[5]).add_(rows(gwkv, 0, C, Ckv))
                         gb(ps[6]).add_(rows(gwkv, C, 2 * C, Ckv))
@@ -1256,6 +1274,17 @@ def encode_inputs(encoder, x_in, pad_mask=None):
     """The encoder body over already adapted inputs ``x_in`` (B, M, Kin) — e.g. the gathered
     ``[pixel ‖ PE]`` rows of a sparse image (``models/lartpc.py``)."""
     return _encode(encoder, KVSource(x_in.float().contiguous()), pad_mask)
+
+
+def encode_sparse(encoder, values, index, pad_mask=None):
+    """The encoder over a sparse image: ``values`` (B, K, C_img) pixel values at flat pixel
+    positions ``index`` (B, K) int64; the K/V projections read the Fourier PE rows at ``index``
+    from the adapter's padded table inside their kernels (no gathered input rows)."""
+    ad = encoder.input_adapter
+    pix = values.reshape(values.shape[0], values.shape[1], ad.num_image_channels).float().contiguous()
+    idx = index if index.dtype == torch.int64 and index.is_contiguous() else index.long().contiguous()
+    src = KVSource(pix, pe=ad.padded_position_encoding(), kin=ad.num_input_channels, index=idx)
+    return _encode(encoder, src, pad_mask)
 
 
 def _encode(encoder, src: KVSource, pad_mask):
