@@ -26,13 +26,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def build(task, seed):
+def build(task, seed, latents=64):
     from perceiver_io_amd.tasks import LitImageClassifier, LitMaskedLanguageModel
 
     torch.manual_seed(seed)
     opt = {"class_path": "torch.optim.AdamW", "init_args": {"lr": 1e-3}}
     if task == "mlm":
-        return LitMaskedLanguageModel(vocab_size=2003, max_seq_len=128, optimizer_init=opt, num_latents=64,
+        return LitMaskedLanguageModel(vocab_size=2003, max_seq_len=128, optimizer_init=opt, num_latents=latents,
                                       num_latent_channels=64, num_encoder_layers=3,
                                       num_encoder_self_attention_layers_per_block=4)
     return LitImageClassifier(image_shape=(28, 28, 1), num_classes=10, optimizer_init=opt, num_latents=32,
@@ -64,12 +64,12 @@ def data(task, n_batches, B, seed, device, noise=1.5, phase=True):
     return out
 
 
-def run(task, fused, steps, train, val, lr, wd, seed, dev):
+def run(task, fused, steps, train, val, lr, wd, seed, dev, latents=64):
     from perceiver_io_amd import ops
     from perceiver_io_amd.ops.optim import FusedAdamW
     from perceiver_io_amd.train.engine import StepEngine
 
-    lit = build(task, seed).to(dev)
+    lit = build(task, seed, latents).to(dev)
     params = [p for p in lit.parameters() if p.requires_grad]
     if fused:
         opt = FusedAdamW(params, lr=lr, weight_decay=wd)
@@ -128,6 +128,7 @@ def main():
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--img-noise", type=float, default=2.0)
     ap.add_argument("--img-phase", type=int, default=0)
+    ap.add_argument("--latents", type=int, default=64, help="mlm: latent count (256 = the headline model's)")
     a = ap.parse_args()
     dev = torch.device(a.device)
     lr, wd = (3e-3, 0.0) if a.task == "mlm" else (1e-3, 0.01)
@@ -138,7 +139,7 @@ def main():
     res = {n: [] for n in names}
     for seed in seeds:
         for name, fused in zip(names, (True, False)):
-            r = run(a.task, fused, a.steps, train, val, lr, wd, seed=seed, dev=dev)
+            r = run(a.task, fused, a.steps, train, val, lr, wd, seed=seed, dev=dev, latents=a.latents)
             res[name].append(r)
             print(f"{a.task} seed {seed} {name}: final val {r['val'][-1][1]}, last-100 train "
                   f"{sum(r['train_loss'][-100:]) / 100:.4f}, {r['seconds']:.1f}s", flush=True)
@@ -156,6 +157,7 @@ def main():
     fl, el = final[names[0]]["loss"], final[names[1]]["loss"]
     summary = {
         "task": a.task, "steps": a.steps, "batch": a.batch, "seeds": seeds, "lr": lr, "weight_decay": wd,
+        **({"latents": a.latents} if a.task == "mlm" else {}),
         **({"img_noise": a.img_noise, "img_random_phase": bool(a.img_phase)} if a.task == "img" else {}),
         "chance_loss": math.log(2003) if a.task == "mlm" else math.log(10),
         "final_val": final,
