@@ -127,6 +127,7 @@ void text_mask_launch(const int64_t*, const bool*, int64_t*, int64_t*, int64_t*,
 int stage_step_launch(void* const*, const void* const*, const long long*, int, float*, const float*, int, hipStream_t);
 void sumsq_launch(const float*, long long, float*, hipStream_t);
 void index_add_rows_launch(float*, long long, const int64_t*, const float*, long long, int, hipStream_t);
+void gather_rows_launch(float*, const float*, long long, const int64_t*, long long, int, hipStream_t);
 void batch_sum2_launch(const float*, const float*, float*, float*, int, long long, long long, int, hipStream_t);
 void pe_gemm_launch(const uint16_t*, const uint16_t*, void*, bool, int, int, int, int, hipStream_t);
 struct PeGradTargets { float *dWa, *dWb, *db, *dg, *dbeta; };
@@ -1295,6 +1296,20 @@ void index_add_rows(Tensor dst, Tensor idx, Tensor src) {
   checked_sync("index_add_rows");
 }
 
+// src (N, C) fp32 rows at idx (R) → (R, C) — a row gather (decoder output queries of a sparse image)
+Tensor gather_rows(Tensor src, Tensor idx) {
+  CHECK_DT(src, torch::kFloat32); CHECK_DT(idx, torch::kInt64);
+  TORCH_CHECK(src.dim() == 2 && src.is_contiguous() && idx.is_contiguous() && src.size(1) % 4 == 0 &&
+                  reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0,
+              "gather_rows: contiguous 16-byte aligned src (N, C), C % 4 == 0, contiguous idx");
+  Tensor out = torch::empty({idx.numel(), src.size(1)}, src.options());
+  if (idx.numel() == 0) return out;
+  pio::gather_rows_launch(out.data_ptr<float>(), f32p(src), src.size(0), idx.data_ptr<int64_t>(), idx.numel(),
+                          (int)src.size(1), stream());
+  checked_sync("gather_rows");
+  return out;
+}
+
 namespace {
 void check_pixel_head(const Tensor& h, const Tensor& w, const Tensor& b, const Tensor& labels, const Tensor& wts) {
   CHECK_DT(h, torch::kFloat32); CHECK_DT(w, torch::kFloat32); CHECK_DT(b, torch::kFloat32);
@@ -1752,6 +1767,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mlm_select", &mlm_select, py::arg("labels"), py::arg("cap"), py::arg("gcap"), py::arg("sticky") = py::none(),
         py::arg("queries") = py::none());
   m.def("index_add_rows", &index_add_rows);
+  m.def("gather_rows", &gather_rows, py::arg("src"), py::arg("idx"));
   m.def("batch_sum2", &batch_sum2, py::arg("a"), py::arg("b"), py::arg("ob_acc") = py::none());
   m.def("pixel_ce_fwd", &pixel_ce_fwd);
   m.def("pixel_ce_bwd", &pixel_ce_bwd);

@@ -420,6 +420,28 @@ void index_add_rows_launch(float* dst, long long nrows, const int64_t* idx, cons
                            hipStream_t st) {
   hipLaunchKernelGGL(index_add_rows_kernel, grid_for(R * (C / 4)), dim3(256), 0, st, dst, nrows, idx, src, R, C);
 }
+// out (R, C) = src[idx] (the forward of that gather: a decoder's output queries at the pixels of a
+// sparse image); an index outside [0, nrows) yields a zero row
+__global__ void gather_rows_kernel(float* __restrict__ out, const float* __restrict__ src, long long nrows,
+                                   const int64_t* __restrict__ idx, long long R, int C) {
+  const int c4 = C >> 2;
+  const long long total = R * c4;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / c4;
+    const int c = (int)(i - r * c4) * 4;
+    const long long d = idx[r];
+#if PIO_CHECKS
+    if (d < 0 || d >= nrows) pio_flag(kErrGatherRow);
+#endif
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (d >= 0 && d < nrows) v = *reinterpret_cast<const float4*>(src + d * C + c);
+    *reinterpret_cast<float4*>(out + r * C + c) = v;
+  }
+}
+void gather_rows_launch(float* out, const float* src, long long nrows, const int64_t* idx, long long R, int C,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(gather_rows_kernel, grid_for(R * (C / 4)), dim3(256), 0, st, out, src, nrows, idx, R, C);
+}
 // Σ over the batch of two (B, n) fp32 tensors in one launch: oa = Σ_b a[b], ob = Σ_b b[b] (the
 // gradients of a batch-broadcast query stream: dQ and the residual dY of the first cross-attention
 // over the shared latent array).  Block = 64 float4 columns × 4 batch groups, fixed summation

@@ -145,7 +145,7 @@ __device__ __forceinline__ void ln_stats(const float (&v)[16], float2* sRed, flo
   for (int i = 0; i < 16; ++i) { const float d = v[i] - mw; q = fmaf(d, d, q); }
   q = xor32_sum(q);
   if (hh == 0) sRed[w * NR + r] = make_float2(mw, q);
-  __syncthreads();
+  lds_sync();
   float2 p[NW];
 #pragma unroll
   for (int k = 0; k < NW; ++k) p[k] = sRed[k * NR + r];
@@ -165,7 +165,7 @@ __device__ __forceinline__ float2 row_sums2(float a, float b, float2* sRed) {
   a = xor32_sum(a);
   b = xor32_sum(b);
   if (hh == 0) sRed[w * NR + r] = make_float2(a, b);
-  __syncthreads();
+  lds_sync();
   float2 t = make_float2(0.f, 0.f);
 #pragma unroll
   for (int k = 0; k < NW; ++k) { const float2 p = sRed[k * NR + r]; t.x += p.x; t.y += p.y; }
@@ -227,7 +227,7 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
     st_bf16(y.LN1X, C, row, n0, t);
     bf16x8 wo[KS];
     load_wtile<C>(wo, y.Wo, n0);
-    __syncthreads();
+    lds_sync();
     // ---- Q, K, V of the wave's heads ----
     float q[16], k[16], v[16];
     {
@@ -272,7 +272,7 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
     st_bf16(y.O, C, row, n0, o);
     bf16x8 w2[KS];
     load_wtile<C>(w2, y.W2, n0);
-    __syncthreads();
+    lds_sync();
     // ---- out-projection + residual → y; LN2 → image 0 ----
     float yv[16];
     {
@@ -291,7 +291,7 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
     if (w == 0 && l < 32) { y.mean2[row] = mu; y.rstd2[row] = rs; }
     st_bf16(sImg[0], LDI, r, n0, t);
     st_bf16(y.LN2Y, C, row, n0, t);
-    __syncthreads();
+    lds_sync();
     // ---- MLP: u = W1·LN2(y) + b1, GELU → image 1, z = W2·GELU(u) + b2 + y ----
     {
       float bb[16];
@@ -310,7 +310,7 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
       load_wtile<C>(wq[1], a.ly[li + 1].Wqkv, C + n0);
       load_wtile<C>(wq[2], a.ly[li + 1].Wqkv, 2 * C + n0);
     }
-    __syncthreads();
+    lds_sync();
     {
       float bb[16];
       const f32x16 acc = gemm_t<C>(w2, sImg[1], LDI);
@@ -385,7 +385,7 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
     wblock_load<C>(pw, y.W1, 0);
     float uv[16];
     ld_bf16(uv, y.U, C, row, n0);
-    __syncthreads();
+    lds_sync();
     // ---- dU = (W2ᵀ·dZ)∘GELU'(u) ----
     float t[16];
     {
@@ -401,7 +401,7 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
     ld_f32(yv, y.Y, C, row, n0);
     ld_vec(gv, y.g2, n0);
     const float mu2 = y.mean2[row], rs2 = y.rstd2[row];
-    __syncthreads();
+    lds_sync();
     // ---- dXn2 = W1ᵀ·dU; LN2 backward → dY ----
     float dy[16];
     {
@@ -431,7 +431,7 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
     ld_bf16(kv, y.QKV, 3 * C, row, C + n0);
     ld_bf16(vv, y.QKV, 3 * C, row, 2 * C + n0);
     ld_bf16(ov, y.O, C, row, n0);
-    __syncthreads();
+    lds_sync();
     // ---- dO = Woᵀ·dY (the wave's heads) ----
     float dov[16];
     to_f(dov, gemm_tt<C>(sW[0], n0, sImg[0], LDI, 0, f32x16{}));
@@ -494,16 +494,16 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
     ld_f32(xv, X, C, row, n0);
     ld_vec(gv, y.g1, n0);
     const float mu1 = y.mean1[row], rs1 = y.rstd1[row];
-    __syncthreads();
+    lds_sync();
     // ---- dXn1 = Wqkvᵀ·dQKV in three C-row blocks of Wqkv ----
     f32x16 acc = gemm_tt<C>(sW[1], n0, sQ, LDQ, 0, f32x16{});
     wblock_store<C>(sW[0], pw);
     wblock_load<C>(pw, y.Wqkv, 2 * C);
-    __syncthreads();
+    lds_sync();
     acc = gemm_tt<C>(sW[0], n0, sQ, LDQ, C, acc);
     wblock_store<C>(sW[1], pw);
     if (li > 0) wblock_load<C>(pw, a.ly[li - 1].W2, 0);
-    __syncthreads();
+    lds_sync();
     acc = gemm_tt<C>(sW[1], n0, sQ, LDQ, 2 * C, acc);
     // ---- LN1 backward → dX (the previous layer's dZ) ----
     {
@@ -567,7 +567,7 @@ __global__ __launch_bounds__(256) void sb_wgrad_kernel(SBWgradArgs a) {
     *reinterpret_cast<bf16x8*>(sG[buf] + sr * LG + gc) = g0;
 #pragma unroll
     for (int q = 0; q < AC; ++q) *reinterpret_cast<bf16x8*>(sA[buf] + sr * LA + ac + 8 * q) = av[q];
-    __syncthreads();
+    lds_sync();
     if (r0 + NR < r_end) fetch(r0 + NR);
     // contraction over the 32 rows: A operand Gᵀ (element (n, r) at sG[r][n]), B operand A
     // (element (r, k) at sA[r][k]); two 16-row k-steps

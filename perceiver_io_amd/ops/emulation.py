@@ -691,6 +691,11 @@ def index_add_rows(dst, idx, src):
     dst.index_add_(0, idx, src.to(dst.dtype))
 
 
+def gather_rows(src, idx):
+    ok = (idx >= 0) & (idx < src.shape[0])
+    return torch.where(ok[:, None], src.index_select(0, idx.clamp(0, src.shape[0] - 1)), torch.zeros((), dtype=src.dtype))
+
+
 def _pixel_logits(h, w, b):
     return h.float() @ w.float().t() + b.float()
 

@@ -226,6 +226,12 @@ def _kv_weight(spec: LayerSpec, ps):
     wc = weight_cache
     wk, wv = wc.get(ps[5]), wc.get(ps[6])
     kin = wk.shape[1]
+    if (wk.is_contiguous() and wv.is_contiguous() and wk.shape == wv.shape
+            and wv.untyped_storage().data_ptr() == wk.untyped_storage().data_ptr()
+            and wv.data_ptr() == wk.data_ptr() + wk.numel() * wk.element_size()):
+        # adjacent bf16 shadows in the optimizer's flat shadow buffer: K‖V is already one
+        # (2C, kin) matrix (unpadded rows: the kernels take the row stride) — no per-step copy
+        return torch.as_strided(wk, (2 * spec.C, kin), (kin, 1))
     wkv = torch.zeros((2 * spec.C, (kin + 7) // 8 * 8), dtype=wk.dtype, device=wk.device)
     wkv[: spec.C, :kin] = wk
     wkv[spec.C:, :kin] = wv

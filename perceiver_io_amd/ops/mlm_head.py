@@ -240,8 +240,15 @@ class _GatherQueries(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, param, idx):
+        from . import use_hip
+
         ctx.save_for_backward(idx)
         ctx.param = param
+        if (use_hip(param) and param.dim() == 2 and param.dtype == torch.float32 and param.is_contiguous()
+                and param.shape[1] % 4 == 0 and idx.dtype == torch.int64):
+            from .fused import kernels
+
+            return kernels(param).gather_rows(param.detach(), idx.contiguous())
         return param.index_select(0, idx)
 
     @staticmethod

@@ -221,7 +221,7 @@ class FusedAdamW(torch.optim.Optimizer):
                 None if f.shadow is None else f.shadow[lo:hi], self.hyper, g["eps"], g["weight_decay"], 0.0,
                 self.grad_scale, l2=self.l2, zero_grad=True)
 
-    def device_update(self, zero_grad: bool = False):
+    def device_update(self, zero_grad: bool = False, norm_staged: bool = False):
         """The capturable part: (grad-norm) + fused AdamW kernel over the flat buffers.
         ``zero_grad``: the kernel clears the gradient as it consumes it (flat buffers without
         replicas only; the step engine's captured step then skips its leading zero fill).
@@ -237,7 +237,8 @@ class FusedAdamW(torch.optim.Optimizer):
             if deterministic():  # torch's tree reduction instead of per-block atomics
                 torch.sum(self.flat.grad * self.flat.grad, dim=0, keepdim=True, out=self.hyper[2:3])
             else:
-                self.hyper[2:3].zero_()
+                if not norm_staged:  # else the per-step staging (stage_step / stage_hyper) zeroed it
+                    self.hyper[2:3].zero_()
                 K.sumsq(self.flat.grad, self.hyper[2:3])
         lo = self.loss_out
         K.adamw(self.flat.data, self.flat.grad, self.exp_avg, self.exp_avg_sq, self.flat.shadow, self.hyper,

@@ -285,7 +285,9 @@ class StepEngine:
                 if ring:
                     lv = loss.detach()
                     opt.loss_out = (lv if lv.dtype == torch.float32 else lv.float(), self._loss_ring)
-                opt.device_update(zero_grad=self._self_zeroing)
+                # every replay of this graph is preceded by a staging of the hyper-parameters
+                # (_stage), which also zeroes the gradient-norm accumulator
+                opt.device_update(zero_grad=self._self_zeroing, norm_staged=True)
                 opt.loss_out = None
             return loss
 

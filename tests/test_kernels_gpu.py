@@ -690,6 +690,8 @@ def test_index_add_rows_and_sumsq():
     ref = dst.clone().index_add_(0, idx, src)
     _ext().index_add_rows(dst, idx, src)
     close(dst, ref, 1e-5, "index_add_rows")
+    got = _ext().gather_rows(src, idx[:3000] % 5000)  # the forward gather (bitwise a copy)
+    assert torch.equal(got, src.index_select(0, idx[:3000] % 5000))
     for n in (1, 1000, 17 * 1024 * 1024 + 3):
         g = torch.randn(n, device=DEV)
         out = torch.zeros(1, device=DEV)
