@@ -17,17 +17,21 @@
 //                     workgroups, the one-hot terms dW[label] −= g·H[r], db[label] −= g and the dH
 //                     rows g·u[r] with u[r] = Σ_v p·W − W[label] merged from pass 1's per-split
 //                     partials, scattered to their source positions.
-// Per-logit VALU work is what bounds both passes (MFMA busy ≈ 13 %): the logit accumulators start
-// at the bias (the MFMAs add it), the exp2 argument is one fma, and pass 2 keeps g and the label
-// compare out of its tiles.
+// Per-logit VALU work is what bounds both passes (MFMA busy ≈ 13 % in round 4): the logit
+// accumulators start at the bias (the MFMAs add it); the exp2 arguments and the sums are packed
+// fp32 pairs (v_pk_fma_f32, v_pk_add_f32); pass 1 tests a tile's Σ p against 2^kRescale instead of
+// forming its max (the max only on the rare rescale branch) and takes the label's logit from one
+// dot product in split 0 instead of a per-tile label test; pass 2 keeps g and the one-hot term out
+// of its tiles.
 //
 // LDS images ([rows][64] bf16, 128 B per row, no padding) are XOR-swizzled on their 16-byte
 // slots with sw(v) = v₁·4 + v₂·2 + v₃ (bits of the row index): a k-contiguous ds_read_b128
 // fragment (16 rows of a lane group, one slot each) and a transposed ds_read_b64_tr_b16
 // fragment (4 consecutive rows × 4 slots per 32 lanes) both land on distinct banks.
 // Stats are kept in the log2 domain; the online rescale of the running sum and the W-weighted
-// accumulator is lazy: only when a row's max grows by more than kRescale (2^8 headroom, far
-// inside fp32 / bf16 range), a wave-uniform branch taken a handful of times per row.
+// accumulator is lazy: only when a tile's Σ p exceeds 2^kRescale (a logit ≳ kRescale above the
+// reference max; 2^8 headroom, far inside fp32 / bf16 range), a wave-uniform branch taken a
+// handful of times per row.
 #include "common.h"
 
 namespace pio {
@@ -42,7 +46,24 @@ constexpr int HT = 64;           // pass 2: rows per staged H tile
 constexpr float kL2E = 1.4426950408889634f;
 constexpr float kLN2 = 0.6931471805599453f;
 constexpr float kRescale = 8.f;  // lazy-rescale threshold (log2 units)
+constexpr float kRescaleSum = 256.f;  // 2^kRescale: a tile's Σ p above it takes the rescale branch
 constexpr int kCeMaxSplitsFwd = 16;  // ce2_num_splits caps the vocab splits of pass 1 here
+typedef float f2v __attribute__((ext_vector_type(2)));  // packed fp32 (v_pk_fma_f32 / v_pk_add_f32)
+
+// p = 2^(t·log2e − m) for the 16 logits of a tile (natural units) in packed pairs; returns Σ p
+__device__ __forceinline__ float exp_tile(const f32x16& t, float m, f32x16& p) {
+  const f2v k2 = {kL2E, kL2E}, nm = {-m, -m};
+  f2v sum = {0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 16; i += 2) {
+    const f2v x = {t[i], t[i + 1]};
+    const f2v y = __builtin_elementwise_fma(x, k2, nm);
+    p[i] = __builtin_amdgcn_exp2f(y.x);
+    p[i + 1] = __builtin_amdgcn_exp2f(y.y);
+    sum += f2v{p[i], p[i + 1]};
+  }
+  return sum.x + sum.y;
+}
 
 // element offset of (row v, 16-byte slot s) in a swizzled [rows][64] bf16 image
 __device__ __forceinline__ int swz(int v, int s) {
@@ -121,6 +142,21 @@ __global__ __launch_bounds__(256) void ce2_fwd_kernel(const float* __restrict__ 
 #if PIO_CHECKS
   if (split == 0 && hh == 0 && (lab >= V || (lab < 0 && lab != -100))) pio_flag(kErrLabel);
 #endif
+  // the label's logit (natural units) by split 0: the row's bf16 operand · W[label] + bias, the
+  // products the logit tiles form (fp32 sums in another order) — no per-tile label test
+  if (split == 0 && rin && lab >= 0 && lab < V) {
+    float d = 0.f;
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const bf16x8 wl = *reinterpret_cast<const bf16x8*>(W + (long long)lab * C + 16 * s2 + 8 * hh);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d = fmaf(bf2f((uint16_t)hb[s2][j]), bf2f((uint16_t)wl[j]), d);
+    }
+    d += __shfl_xor(d, 32);
+    if (hh == 0)
+      __hip_atomic_store(reinterpret_cast<unsigned*>(picked + gr), __float_as_uint(d + bias[lab]), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  }
   // chunk staging: 64 vocab rows × 8 slots = 512 16-byte pieces, two per thread (+ the bias)
   bf16x8 wr[2];
   float bnext = 0.f;
@@ -143,8 +179,7 @@ __global__ __launch_bounds__(256) void ce2_fwd_kernel(const float* __restrict__ 
     }
     if (threadIdx.x < VC) sB[buf][threadIdx.x] = bnext;
   };
-  float m_ref = -__builtin_inff(), l_run = 0.f, pk = 0.f;
-  bool have_pk = false;
+  float m_ref = -__builtin_inff(), l_run = 0.f;
   f32x16 acc[2] = {f32x16{}, f32x16{}};  // Σ p·W, transposed: [c = 32ct + acc_row][row = lane]
   if (c_begin < c_end) {
     fetch(c_begin);
@@ -171,34 +206,25 @@ __global__ __launch_bounds__(256) void ce2_fwd_kernel(const float* __restrict__ 
       }
 #pragma unroll
       for (int s = 0; s < 4; ++s) st = mfma32(ce2::img_kc(img, 32 * vb, s), hb[s], st);
-      float mx = st[0];
+      // p against the running reference max; a tile whose sum leaves [0, 2^kRescale] (a logit
+      // more than ~kRescale above the reference, or the first tile: m_ref = −inf → inf) takes
+      // the rare wave-uniform branch: new reference = the row max, lazy rescale, p again
+      f32x16 p;
+      float ps = exp_tile(st, m_ref, p);
+      if (__ballot(!(ps <= ce2::kRescaleSum))) {
+        float mx = st[0];
 #pragma unroll
-      for (int i = 1; i < 16; ++i) mx = fmaxf(mx, st[i]);
-      mx = xor32_max(mx) * kL2E;  // both halves of the row share its reference max (log2 units)
-      if (__ballot(mx > m_ref + ce2::kRescale)) {  // rare, wave-uniform
+        for (int i = 1; i < 16; ++i) mx = fmaxf(mx, st[i]);
+        mx = xor32_max(mx) * kL2E;  // both halves of the row share its reference max (log2 units)
         const float mn = fmaxf(m_ref, mx);
         const float alpha = fast_exp2(m_ref - mn);  // 0 on the first block
         l_run *= alpha;
 #pragma unroll
         for (int i = 0; i < 16; ++i) { acc[0][i] *= alpha; acc[1][i] *= alpha; }
         m_ref = mn;
+        ps = exp_tile(st, m_ref, p);
       }
-      // the label's logit, if this lane holds it
-      const int j = lab - (c * VC + 32 * vb);
-      if (j >= 0 && j < 32 && ((j >> 2) & 1) == hh) {
-        const int ri = (j & 3) + 4 * (j >> 3);
-        float v = 0.f;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) v = i == ri ? st[i] : v;
-        pk = v * kL2E;
-        have_pk = true;
-      }
-      f32x16 p;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        p[i] = fast_exp2(fmaf(st[i], kL2E, -m_ref));
-        l_run += p[i];
-      }
+      l_run += ps;
       // Σ p·W: accᵀ[c][row] += Wᵀ[c][v]·Pᵀ[v][row] (the logits accumulator as the B operand)
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
@@ -219,9 +245,6 @@ __global__ __launch_bounds__(256) void ce2_fwd_kernel(const float* __restrict__ 
       __hip_atomic_store(reinterpret_cast<unsigned long long*>(part_ml + (long long)split * M + gr),
                          (unsigned long long)__float_as_uint(m_ref) | ((unsigned long long)__float_as_uint(ls) << 32),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (have_pk)
-      __hip_atomic_store(reinterpret_cast<unsigned*>(picked + gr), __float_as_uint(pk * ce2::kLN2), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
     float* pa = part_acc + ((long long)split * M + gr) * C;
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct)
@@ -445,16 +468,20 @@ __global__ __launch_bounds__(256) void ce2_bwd_kernel(const uint16_t* __restrict
       // the gradient scale g and the one-hot term are applied outside the tile loop: g on the
       // sums, −g·H[r] at the label by the appended row workgroups)
       f32x16 d;
+      f2v bs2 = {0.f, 0.f};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float4 ls = *reinterpret_cast<const float4*>(&sL[buf][32 * rb + 8 * q + 4 * hh]);
-        d[4 * q] = fast_exp2(fmaf(st[4 * q], kL2E, -ls.x));
-        d[4 * q + 1] = fast_exp2(fmaf(st[4 * q + 1], kL2E, -ls.y));
-        d[4 * q + 2] = fast_exp2(fmaf(st[4 * q + 2], kL2E, -ls.z));
-        d[4 * q + 3] = fast_exp2(fmaf(st[4 * q + 3], kL2E, -ls.w));
+        const f2v k2 = {kL2E, kL2E};
+        const f2v y0 = __builtin_elementwise_fma(f2v{st[4 * q], st[4 * q + 1]}, k2, f2v{-ls.x, -ls.y});
+        const f2v y1 = __builtin_elementwise_fma(f2v{st[4 * q + 2], st[4 * q + 3]}, k2, f2v{-ls.z, -ls.w});
+        d[4 * q] = fast_exp2(y0.x);
+        d[4 * q + 1] = fast_exp2(y0.y);
+        d[4 * q + 2] = fast_exp2(y1.x);
+        d[4 * q + 3] = fast_exp2(y1.y);
+        bs2 += f2v{d[4 * q], d[4 * q + 1]} + f2v{d[4 * q + 2], d[4 * q + 3]};
       }
-#pragma unroll
-      for (int i = 0; i < 16; ++i) bsum += d[i];
+      bsum += bs2.x + bs2.y;
       // dW[v][c] += Σ_r dl[r][v]·H[r][c]: the dl accumulator as the A operand (Xᵀ·B)
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {

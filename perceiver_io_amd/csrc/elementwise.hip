@@ -227,10 +227,13 @@ __global__ void sumsq_kernel(const float* __restrict__ g, long long n, float* __
   const long long stride = (long long)gridDim.x * blockDim.x;
   const float4* g4 = reinterpret_cast<const float4*>(g);
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  for (; i + stride < n4; i += 2 * stride) {
-    const float4 a = g4[i], b = g4[i + stride];
+  // four independent 16-byte loads in flight per thread (HBM-bound on the LArTPC output-query table)
+  for (; i + 3 * stride < n4; i += 4 * stride) {
+    const float4 a = g4[i], b = g4[i + stride], c = g4[i + 2 * stride], d = g4[i + 3 * stride];
     s0 = fmaf(a.x, a.x, s0); s1 = fmaf(a.y, a.y, s1); s2 = fmaf(a.z, a.z, s2); s3 = fmaf(a.w, a.w, s3);
     s0 = fmaf(b.x, b.x, s0); s1 = fmaf(b.y, b.y, s1); s2 = fmaf(b.z, b.z, s2); s3 = fmaf(b.w, b.w, s3);
+    s0 = fmaf(c.x, c.x, s0); s1 = fmaf(c.y, c.y, s1); s2 = fmaf(c.z, c.z, s2); s3 = fmaf(c.w, c.w, s3);
+    s0 = fmaf(d.x, d.x, s0); s1 = fmaf(d.y, d.y, s1); s2 = fmaf(d.z, d.z, s2); s3 = fmaf(d.w, d.w, s3);
   }
   for (; i < n4; i += stride) {
     const float4 a = g4[i];
@@ -386,7 +389,7 @@ void text_mask_launch(const int64_t* x, const bool* pad, int64_t* state, int64_t
 }
 void sumsq_launch(const float* g, long long n, float* out, hipStream_t st) {
   long long b = (n + 4095) / 4096;
-  b = b > 1024 ? 1024 : (b < 1 ? 1 : b);
+  b = b > 2048 ? 2048 : (b < 1 ? 1 : b);
   hipLaunchKernelGGL(sumsq_kernel, dim3((unsigned)b), dim3(256), 0, st, g, n, out);
 }
 

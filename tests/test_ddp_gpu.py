@@ -299,7 +299,7 @@ def test_two_ranks_overlapped_nondeterministic_in_sync():
         assert out[r]["sync"] == [0.0] * 6, out[r]["sync"]
 
 
-def _worker_probe_failure(port, out):
+def _worker_probe_failure(rank, port, out):
     # a fresh process: a 1-rank RCCL group whose all-reduce raises while a capture is open
     os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                       PERCEIVER_DIST_BACKEND="nccl")
