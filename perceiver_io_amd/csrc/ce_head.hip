@@ -13,8 +13,9 @@
 //                     splits' (max, sum) into the rows' lse and the block's loss partial; the last
 //                     row block (second ticket) finalises the mean loss — no combine launch.
 //   pass 2 (backward) vocab × row split: logit tiles S = H·Wᵀ (vocab on the lane), p, dW += g·pᵀ·H
-//                     and db += g·Σ p (partials stored into a slab row), plus, in appended
-//                     workgroups, the one-hot terms dW[label] −= g·H[r], db[label] −= g and the dH
+//                     and db += g·Σ p, the one-hot terms dW[label] −= g·H[r], db[label] −= g of
+//                     each tile's few rows whose label the wave holds (a ballot scan per tile),
+//                     partials stored into a slab row (or added); in appended workgroups the dH
 //                     rows g·u[r] with u[r] = Σ_v p·W − W[label] merged from pass 1's per-split
 //                     partials, scattered to their source positions.
 // Per-logit VALU work is what bounds both passes (MFMA busy ≈ 13 % in round 4): the logit
@@ -22,7 +23,7 @@
 // fp32 pairs (v_pk_fma_f32, v_pk_add_f32); pass 1 tests a tile's Σ p against 2^kRescale instead of
 // forming its max (the max only on the rare rescale branch) and takes the label's logit from one
 // dot product in split 0 instead of a per-tile label test; pass 2 keeps g and the one-hot term out
-// of its tiles.
+// of its tiles (a per-tile ballot over the rows' labels instead).
 //
 // LDS images ([rows][64] bf16, 128 B per row, no padding) are XOR-swizzled on their 16-byte
 // slots with sw(v) = v₁·4 + v₂·2 + v₃ (bits of the row index): a k-contiguous ds_read_b128
@@ -360,6 +361,8 @@ __global__ __launch_bounds__(256) void ce2_bwd_kernel(const uint16_t* __restrict
   using namespace ce2;
   __shared__ __attribute__((aligned(16))) uint16_t sH[2][HT * C];
   __shared__ __attribute__((aligned(16))) float sL[2][HT];  // lse·log2e; +inf for a row without a label
+  __shared__ int sLab[2][HT];                                  // the rows' labels (−1: none)
+  static_assert(HT == 64, "one tile row per lane in the one-hot scan");
   const int w = wave_id(), l = lane_id(), hh = l >> 5;
   const float g = gout[0] / fmaxf(count[0], 1.f);
   if ((int)blockIdx.y == rsplit) {
@@ -370,15 +373,6 @@ __global__ __launch_bounds__(256) void ce2_bwd_kernel(const uint16_t* __restrict
     for (int r = r0 + (int)(threadIdx.x >> 4); r < r1; r += 16) {
       const int lab = (int)labels[r];
       if (lab < 0 || lab >= V) continue;
-      {  // the one-hot part of the vocab gradients, left out of the tiles: dW[label] −= g·H[r], db[label] −= g
-        const uint2 hv = *reinterpret_cast<const uint2*>(Hs + (long long)r * C + 4 * cq);
-        float* dw = dW + (long long)lab * C + 4 * cq;
-        atomicAdd(dw, -g * bf2f((uint16_t)(hv.x & 0xFFFF)));
-        atomicAdd(dw + 1, -g * bf2f((uint16_t)(hv.x >> 16)));
-        atomicAdd(dw + 2, -g * bf2f((uint16_t)(hv.y & 0xFFFF)));
-        atomicAdd(dw + 3, -g * bf2f((uint16_t)(hv.y >> 16)));
-        if (cq == 0) atomicAdd(db + lab, -g);
-      }
       const long long dst = rowmap ? rowmap[r] : (long long)r;
       if (dst < 0 || dst >= dh_rows) continue;
       float2 ml[kCeMaxSplitsFwd];
@@ -425,6 +419,7 @@ __global__ __launch_bounds__(256) void ce2_bwd_kernel(const uint16_t* __restrict
   const int t_begin = blockIdx.y * tiles_per_split, t_end = min(ntiles, t_begin + tiles_per_split);
   bf16x8 hr[2];
   float aux = 0.f;
+  int labn = -1;
   auto fetch = [&](int t) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -434,8 +429,10 @@ __global__ __launch_bounds__(256) void ce2_bwd_kernel(const uint16_t* __restrict
     }
     const int r = t * HT + (threadIdx.x & (HT - 1));
     if (threadIdx.x < HT) {  // a row without a label (capacity padding, r ≥ M): p = 2^−inf = 0
-      const bool lv = r < M && labels[r < M ? r : 0] >= 0;
+      const int lb = r < M ? (int)labels[r] : -1;
+      const bool lv = lb >= 0;
       aux = lv ? lse[r] * kL2E : __builtin_inff();
+      labn = lv ? lb : -1;
     }
   };
   auto stage = [&](int buf) {
@@ -444,7 +441,10 @@ __global__ __launch_bounds__(256) void ce2_bwd_kernel(const uint16_t* __restrict
       const int e = threadIdx.x + 256 * i;
       *reinterpret_cast<bf16x8*>(&sH[buf][swz(e >> 3, e & 7)]) = hr[i];
     }
-    if (threadIdx.x < HT) sL[buf][threadIdx.x] = aux;
+    if (threadIdx.x < HT) {
+      sL[buf][threadIdx.x] = aux;
+      sLab[buf][threadIdx.x] = labn;
+    }
   };
   f32x16 acc[2] = {f32x16{}, f32x16{}};  // dW: [v = acc_row][c = 32ct + lane]
   float bsum = 0.f;
@@ -488,6 +488,29 @@ __global__ __launch_bounds__(256) void ce2_bwd_kernel(const uint16_t* __restrict
         const bf16x8 pa = pack_acc(d, ss);
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct) acc[ct] = mfma32(pa, ce2::img_ks_perm(img, 32 * ct, 32 * rb + 16 * ss), acc[ct]);
+      }
+    }
+    // the one-hot term of the tile's rows whose label is one of this wave's 32 vocab entries (on
+    // average 64·32/V of them per tile: a ballot, rarely a hit): dW[label] −= H[r], db[label] −= 1
+    // (g applied at the store), so the slab / accumulators hold the whole vocab gradient
+    {
+      const int v0w = blockIdx.x * VB2 + 32 * w;
+      const int lb = sLab[buf][l];  // lane l: row l of the tile
+      unsigned long long hits = __ballot(lb >= v0w && lb < v0w + 32);
+      while (hits) {
+        const int r = __builtin_ctzll(hits);
+        hits &= hits - 1;
+        const int j = sLab[buf][r] - v0w;  // wave-uniform
+        const int it = (j & 3) + 4 * (j >> 3), ht = (j >> 2) & 1;
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+          const int c = 32 * ct + (l & 31);
+          const float hv = bf2f(img[ce2::swz(r, c >> 3) + (c & 7)]);
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (i == it && hh == ht) acc[ct][i] -= hv;
+        }
+        if (hh == 0 && (l & 31) == j) bsum -= 1.f;
       }
     }
     if (t + 1 < t_end) stage(buf ^ 1);
