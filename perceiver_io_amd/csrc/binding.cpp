@@ -893,7 +893,8 @@ constexpr int kTallRows = 1 << 17;
 
 OptT ln_linear_bwd(Tensor g, Tensor w, Tensor x, OptT mean, OptT rstd, OptT lnw, OptT lnb, OptT dres, bool need_dx,
                    OptT dlnw, OptT dlnb, OptT dW, OptT db, OptT pe, int64_t kin, bool slab, OptT job_slab,
-                   std::vector<Tensor> job_dsts, std::vector<int64_t> job_offs, OptT dx_out, OptT pe_index) {
+                   std::vector<Tensor> job_dsts, std::vector<int64_t> job_offs, OptT dx_out, OptT pe_index,
+                   bool tall_wgrad) {
   TORCH_CHECK(g.dim() == 2 && g.stride(1) == 1 && x.dim() == 2 && x.stride(1) == 1, "g / x must be 2-D rows");
   const int R = (int)g.size(0), N = (int)g.size(1);
   TORCH_CHECK(!(slab && R >= kTallRows), "slab gradients are for R < ", kTallRows, " rows");
@@ -934,9 +935,11 @@ OptT ln_linear_bwd(Tensor g, Tensor w, Tensor x, OptT mean, OptT rstd, OptT lnw,
   TORCH_CHECK(!slab || vrs < 0 || wrs < 0 || vrs == wrs, "slab targets must share one slab");
   const float* dr = nullptr; int drs = 0;
   if (dres.has_value()) { dr = f32p(*dres); drs = (int)dres->stride(0); TORCH_CHECK(dres->stride(1) == 1); }
-  // very tall inputs (image K/V projections): the weight gradient leaves the row-tile kernel
-  // for the streaming tall-wgrad kernel (one partial per ~R/128 rows instead of per 64)
-  const bool tall = dwp != nullptr && R >= kTallRows;
+  // very tall inputs (image K/V projections; tall_wgrad: the caller's choice below kTallRows): the
+  // weight gradient leaves the row-tile kernel for the streaming tall-wgrad kernel (one partial
+  // per ~R/128 rows instead of per 64)
+  TORCH_CHECK(!(tall_wgrad && slab), "tall_wgrad and slab exclude each other");
+  const bool tall = dwp != nullptr && (R >= kTallRows || tall_wgrad);
   pio::ln_linear_bwd_launch(g.data_ptr(), is_bf16(g), (int)g.stride(0), N, bfp(w), (int)w.size(1), Kin, x.data_ptr(),
                             is_bf16(x), (int)x.stride(0), f32o(mean), f32o(rstd), f32o(lnw), f32o(lnb), dr, drs, dxp,
                             dx_rs, dgp, dbp, tall ? nullptr : dwp, tall ? nullptr : dbiasp, vrs < 0 ? 0 : vrs,
@@ -1760,7 +1763,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("lnw"), py::arg("lnb"), py::arg("dres"), py::arg("need_dx"), py::arg("dlnw"), py::arg("dlnb"),
         py::arg("dW"), py::arg("db"), py::arg("pe") = py::none(), py::arg("kin") = -1, py::arg("slab") = false,
         py::arg("job_slab") = py::none(), py::arg("job_dsts") = std::vector<Tensor>(),
-        py::arg("job_offs") = std::vector<int64_t>(), py::arg("dx_out") = py::none(), py::arg("pe_index") = py::none());
+        py::arg("job_offs") = std::vector<int64_t>(), py::arg("dx_out") = py::none(), py::arg("pe_index") = py::none(),
+        py::arg("tall_wgrad") = false);
   m.def("wgrad", &wgrad, py::arg("g"), py::arg("a"), py::arg("amode"), py::arg("mean"), py::arg("rstd"), py::arg("lnw"),
         py::arg("lnb"), py::arg("rows_per_wg"), py::arg("dW"), py::arg("db"), py::arg("pe") = py::none(),
         py::arg("kin") = -1, py::arg("pe_index") = py::none());

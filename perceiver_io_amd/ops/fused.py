@@ -262,12 +262,11 @@ def _kv_weight(spec: LayerSpec, ps):
     wc = weight_cache
     wk, wv = wc.get(ps[5]), wc.get(ps[6])
     kin = wk.shape[1]
-    if (wk.is_contiguous() and wv.is_contiguous() and wk.shape == wv.shape
-            and wv.untyped_storage().data_ptr() == wk.untyped_storage().data_ptr()
-            and wv.data_ptr() == wk.data_ptr() + wk.numel() * wk.element_size()):
+    both = _adjacent_rows(wk, wv)
+    if both is not None:
         # adjacent bf16 shadows in the optimizer's flat shadow buffer: K‖V is already one
         # (2C, kin) matrix (unpadded rows: the kernels take the row stride) — no per-step copy
-        return torch.as_strided(wk, (2 * spec.C, kin), (kin, 1))
+        return both
     wkv = torch.zeros((2 * spec.C, (kin + 7) // 8 * 8), dtype=wk.dtype, device=wk.device)
     wkv[: spec.C, :kin] = wk
     wkv[spec.C:, :kin] = wv
@@ -343,6 +342,31 @@ class KVSource:
 # LN(x)·Wᵀ is batch-independent, so it is one (M × Kin)·(Kin × O) GEMM per step and each sample
 # only pays a bandwidth-bound epilogue.
 PE_FACTORED = True
+
+
+# the cross-attention K/V projection's weight gradient from the streaming tall-wgrad kernel (one
+# partial per row range; the LN affine gradients by atomics) instead of per-64-row-tile slabs
+# once the input has at least this many rows — for wide inputs (the LArTPC [pixel ‖ PE] rows,
+# Kin = 131) whose slab rows are large; PERCEIVER_KV_TALL_MIN overrides (rows; 0 = never)
+KV_TALL_MIN = int(os.environ.get("PERCEIVER_KV_TALL_MIN", str(1 << 17)))
+
+
+def _kv_tall(R: int, kin: int) -> bool:
+    from . import deterministic
+
+    return KV_TALL_MIN > 0 and R >= KV_TALL_MIN and not deterministic()
+
+
+def _adjacent_rows(a: torch.Tensor, b: torch.Tensor):
+    """(2N, K) view over two contiguous (N, K) tensors that lie back to back in one storage (e.g.
+    the k / v projection gradients in the optimizer's flat buffer), else None."""
+    if not (a.is_contiguous() and b.is_contiguous() and a.shape == b.shape and a.dim() == 2 and a.dtype == b.dtype):
+        return None
+    if a.untyped_storage().data_ptr() != b.untyped_storage().data_ptr():
+        return None
+    if b.data_ptr() != a.data_ptr() + a.numel() * a.element_size():
+        return None
+    return torch.as_strided(a, (2 * a.shape[0], a.shape[1]), (a.shape[1], 1))
 
 
 def _pe_index(src):
@@ -771,7 +795,7 @@ class _LayerFn(torch.autograd.Function):
                     K.pe_grads(Dm, part, ebf, ps[5].detach(), ps[6].detach(), g_kv.detach(), b_kv.detach(), nc,
                                tg(ps[5]), tg(ps[6]), gbias[0, C:3 * C] if rep_mode else gbias[C:3 * C], tg(g_kv),
                                tg(b_kv))
-                elif WGRAD_SLAB and Rkv < TALL_ROWS:
+                elif WGRAD_SLAB and Rkv < TALL_ROWS and not (ctx.kv_pe is not None and _kv_tall(Rkv, Ckv)):
                     sl = _GradSlab(Rkv, [Ckv, Ckv, 2 * C * Ckv, 2 * C], dz2)
                     src = ctx.src
                     chain = src is not None and ctx.kv_grad and ctx.kv_pe is None
@@ -795,14 +819,19 @@ class _LayerFn(torch.autograd.Function):
                     sl.defer(K, [flat(g_kv), flat(b_kv), dwkv, flat(bin_, C, 3 * C)])
                 else:
                     gbias = gb(bin_)
+                    sep = False
                     if spec.packed:
                         gwkv = rows(gb(ps[4]), C, 3 * C, C)
                     else:
-                        gwkv = torch.zeros((8, 2 * C * Ckv) if rep_mode else (2 * C, Ckv), **f32)
+                        gwkv = None if rep_mode else _adjacent_rows(gb(ps[5]), gb(ps[6]))
+                        sep = gwkv is None
+                        if sep:
+                            gwkv = torch.zeros((8, 2 * C * Ckv) if rep_mode else (2 * C, Ckv), **f32)
                     dx_kv = K.ln_linear_bwd(dkv2, wkv, xkv2, mean_kv, rstd_kv, g_kv, b_kv, None, ctx.kv_grad,
                                             gb(g_kv), gb(b_kv), gwkv, rows(gbias, C, 3 * C, 1), ctx.kv_pe, Ckv,
-                                            pe_index=ctx.kv_pe_index)
-                    if not spec.packed:
+                                            pe_index=ctx.kv_pe_index,
+                                            tall_wgrad=ctx.kv_pe is not None and _kv_tall(Rkv, Ckv))
+                    if sep:
                         gb(ps[5]).add_(rows(gwkv, 0, C, Ckv))
                         gb(ps[6]).add_(rows(gwkv, C, 2 * C, Ckv))
                 ent["dkv"] = ent["pe_D"] = ent["pe_part"] = None
