@@ -98,31 +98,11 @@ weight_cache = WeightCache()
 # ------------------------------------------------------------------------------------------
 _pending = []          # deferred slab reductions: (K, slab, dsts, offsets, stream)
 _flush_queued = [False]
-# PERCEIVER_SLAB_SIDE=1: each slab reduction runs at once on a side stream (its small-LDS
-# workgroups share the CUs of the latency-bound backward kernels, whose own LDS keeps appended
-# workgroups from starting before their tiles end); the main stream joins once per backward
-SLAB_SIDE = os.environ.get("PERCEIVER_SLAB_SIDE", "0") == "1"
-_side = {}             # device index → side stream
-_side_events = []      # outstanding side-stream reductions: (main stream, event)
-
-
-def _side_stream(dev):
-    st = _side.get(dev.index)
-    if st is None:
-        st = _side[dev.index] = torch.cuda.Stream(device=dev)
-    return st
-
-
-def _join_side():
-    while _side_events:
-        main, ev = _side_events.pop(0)
-        main.wait_event(ev)
 
 
 def _flush_pending():
     """Run every deferred slab reduction as a standalone launch (end of a backward pass)."""
     _flush_queued[0] = False
-    _join_side()
     while _pending:
         K, t, ds, os_, st = _pending.pop(0)
         if st is None:
@@ -144,22 +124,6 @@ def defer_slab(K, t: torch.Tensor, dsts, offs):
     if not dsts:
         return
     st = torch.cuda.current_stream(t.device) if t.is_cuda else None
-    if SLAB_SIDE and st is not None:
-        side = _side_stream(t.device)
-        side.wait_stream(st)
-        with torch.cuda.stream(side):
-            K.slab_reduce(t, list(dsts), list(offs))
-        t.record_stream(side)
-        ev = torch.cuda.Event()
-        ev.record(side)
-        _side_events.append((st, ev))
-        if not _flush_queued[0]:
-            try:
-                torch.autograd.Variable._execution_engine.queue_callback(_flush_pending)
-                _flush_queued[0] = True
-            except RuntimeError:
-                _flush_pending()
-        return
     _pending.append((K, t, list(dsts), list(offs), st))
     if not _flush_queued[0]:
         try:
@@ -186,7 +150,8 @@ class _GradSlab:
     reduction of the slab into the parameter gradients; the next backward kernel of the chain
     runs it in appended workgroups, overlapped with its own latency-bound tiles, on the same
     stream (a side-stream branch costs 10–15 µs of cross-queue hand-off per fork in a
-    replayed hipGraph).  Reductions still pending when the backward pass ends are launched by
+    replayed hipGraph; round 5 re-measured every reduction on a side stream: 1.712 against
+    1.424 ms per headline step, profiles/r5_slab_side_ab.md).  Reductions still pending when the backward pass ends are launched by
     an autograd final callback, so gradients are complete when ``backward()`` returns."""
 
     def __init__(self, R: int, sizes, like: torch.Tensor):

@@ -305,10 +305,14 @@ def _worker_probe_failure(rank, port, out):
                       PERCEIVER_DIST_BACKEND="nccl")
     os.environ.pop("PERCEIVER_GRAPH_COLLECTIVES", None)
     from perceiver_io_amd.ops.optim import FlatParameterSpace
-    from perceiver_io_amd.parallel import FlatGradReducer, dist
+    import torch.distributed as tdist
+
+    from perceiver_io_amd.parallel import FlatGradReducer
     from perceiver_io_amd.parallel import dist as pdist
 
-    dist.init()
+    # a real 1-rank RCCL group (dist.init() leaves a single process without one)
+    tdist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
+    pdist._INFO = pdist.DistInfo(rank=0, local_rank=0, world_size=1, backend="nccl")
     real = pdist.dist.all_reduce
 
     def failing(t, *a, **k):
@@ -336,7 +340,7 @@ def _worker_probe_failure(rank, port, out):
     res["in_graph"] = red.in_graph
     red.close()
     out[0] = res
-    dist.shutdown()
+    tdist.destroy_process_group()
 
 
 def test_graph_collectives_probe_capture_failure_fails_closed():
