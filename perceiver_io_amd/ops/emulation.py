@@ -740,3 +740,106 @@ def pixel_ce_bwd(h, w, b, labels, wts, gout, stats, dH, dW, db):
     dH.copy_(coef @ w.float())
     dW += (coef.t() @ h.float()).view_as(dW)
     db += coef.sum(0)
+
+
+# ---- per-sample latent-block kernels (csrc/sample_block.hip): 32 latents, 4 heads -------------
+# the same operands, bf16 rounding points and outputs as sb_fwd / sb_bwd / sb_wgrad
+_SB_N, _SB_H = 32, 4
+
+
+def _sb_unpack(params, i):
+    return params[12 * i:12 * (i + 1)]
+
+
+def _sb_heads(t, B, C):  # (B·32, C) → (B, H, 32, d)
+    return t.view(B, _SB_N, _SB_H, C // _SB_H).transpose(1, 2)
+
+
+def _sb_probs(q, k, scale):
+    """normalised softmax probabilities (fp32) from bf16 q, k (B, H, 32, d)"""
+    s = q @ k.transpose(-1, -2)
+    return torch.softmax(s * scale, dim=-1)
+
+
+def sb_fwd(x, params, scale, eps):
+    R, C = x.shape
+    B = R // _SB_N
+    L = len(params) // 12
+    out = []
+    for i in range(L):
+        g1, be1, wqkv, bqkv, wo, bo, g2, be2, w1, b1, w2, b2 = _sb_unpack(params, i)
+        t, mean1, rstd1 = _ln(x, g1, be1, eps)
+        ln1x = _bf(t)
+        qkv = _bf(ln1x @ wqkv.float().t() + bqkv)
+        q, k, v = (_sb_heads(qkv[:, j * C:(j + 1) * C], B, C) for j in range(3))
+        p = _sb_probs(q, k, scale)
+        # O = Σ bf16(p̃)·v / Σ p̃ with p̃ = exp(s − max): the kernel rounds the unnormalised probabilities
+        s = (q @ k.transpose(-1, -2)) * scale
+        pt = torch.exp(s - s.amax(-1, keepdim=True))
+        o = (_bf(pt) @ v) / pt.sum(-1, keepdim=True)
+        o = _bf(o.transpose(1, 2).reshape(R, C))
+        y = o @ wo.float().t() + bo + x
+        t2, mean2, rstd2 = _ln(y, g2, be2, eps)
+        ln2y = _bf(t2)
+        u = ln2y @ w1.float().t() + b1
+        gu = _bf(F.gelu(u))
+        z = gu @ w2.float().t() + b2 + y
+        bf = torch.bfloat16
+        out += [ln1x.to(bf), qkv.to(bf), o.to(bf), ln2y.to(bf), u.to(bf), gu.to(bf), y, z, mean1, rstd1, mean2, rstd2]
+        del p
+        x = z
+    return out
+
+
+def sb_bwd(dz, x0, saved, params, ln_grads, scale, eps):
+    R, C = x0.shape
+    B = R // _SB_N
+    L = len(params) // 12
+    d = C // _SB_H
+    grads = [None] * L
+    dz = dz.float()
+    for i in reversed(range(L)):
+        g1, be1, wqkv, bqkv, wo, bo, g2, be2, w1, b1, w2, b2 = _sb_unpack(params, i)
+        ln1x, qkv, o, ln2y, u, gu, y, z, mean1, rstd1, mean2, rstd2 = saved[12 * i:12 * (i + 1)]
+        x = saved[12 * (i - 1) + 7] if i > 0 else x0
+        dzb = _bf(dz)
+        du = _bf((dzb @ w2.float()) * _gelu_grad(u.float()))
+        dxn2 = du @ w1.float()
+        dyl, yh = _ln_bwd(dxn2, y, mean2, rstd2, g2)
+        dy = dz + dyl
+        ln_grads[4 * i + 2].view(-1).add_((dxn2 * yh).sum(0))
+        ln_grads[4 * i + 3].view(-1).add_(dxn2.sum(0))
+        dyb = _bf(dy)
+        do = _bf(dyb @ wo.float())
+        qf = qkv.float()
+        q, k, v = (_sb_heads(qf[:, j * C:(j + 1) * C], B, C) for j in range(3))
+        doh = _sb_heads(do, B, C)
+        oh = _sb_heads(o.float(), B, C)
+        p = _sb_probs(q, k, scale)
+        dp = doh @ v.transpose(-1, -2)
+        delta = (doh * oh).sum(-1, keepdim=True)
+        ds = p * (dp - delta)
+        dv = _bf(p).transpose(-1, -2) @ doh
+        dq = (_bf(ds) @ k) * scale
+        dk = (_bf(ds).transpose(-1, -2) @ q) * scale
+        dqkv = torch.cat([t.transpose(1, 2).reshape(R, C) for t in (dq, dk, dv)], 1)
+        dqkvb = _bf(dqkv)
+        dxn1 = dqkvb @ wqkv.float()
+        dxl, xh = _ln_bwd(dxn1, x, mean1, rstd1, g1)
+        ln_grads[4 * i].view(-1).add_((dxn1 * xh).sum(0))
+        ln_grads[4 * i + 1].view(-1).add_(dxn1.sum(0))
+        bf = torch.bfloat16
+        grads[i] = [dqkvb.to(bf), dyb.to(bf), du.to(bf), dzb.to(bf)]
+        dz = dy + dxl
+    out = [dz]
+    for g in grads:
+        out += g
+    return out
+
+
+def sb_wgrad(jobs):
+    for j in range(0, len(jobs), 4):
+        G, A, dW, db = jobs[j:j + 4]
+        Gf = G.float()
+        dW.view(Gf.shape[1], A.shape[1]).add_(Gf.t() @ A.float())
+        db.view(-1).add_(Gf.sum(0))
