@@ -893,8 +893,7 @@ constexpr int kTallRows = 1 << 17;
 
 OptT ln_linear_bwd(Tensor g, Tensor w, Tensor x, OptT mean, OptT rstd, OptT lnw, OptT lnb, OptT dres, bool need_dx,
                    OptT dlnw, OptT dlnb, OptT dW, OptT db, OptT pe, int64_t kin, bool slab, OptT job_slab,
-                   std::vector<Tensor> job_dsts, std::vector<int64_t> job_offs, OptT dx_out, OptT pe_index,
-                   bool tall_wgrad) {
+                   std::vector<Tensor> job_dsts, std::vector<int64_t> job_offs, OptT dx_out, OptT pe_index) {
   TORCH_CHECK(g.dim() == 2 && g.stride(1) == 1 && x.dim() == 2 && x.stride(1) == 1, "g / x must be 2-D rows");
   const int R = (int)g.size(0), N = (int)g.size(1);
   TORCH_CHECK(!(slab && R >= kTallRows), "slab gradients are for R < ", kTallRows, " rows");
@@ -935,11 +934,9 @@ OptT ln_linear_bwd(Tensor g, Tensor w, Tensor x, OptT mean, OptT rstd, OptT lnw,
   TORCH_CHECK(!slab || vrs < 0 || wrs < 0 || vrs == wrs, "slab targets must share one slab");
   const float* dr = nullptr; int drs = 0;
   if (dres.has_value()) { dr = f32p(*dres); drs = (int)dres->stride(0); TORCH_CHECK(dres->stride(1) == 1); }
-  // very tall inputs (image K/V projections; tall_wgrad: the caller's choice below kTallRows): the
-  // weight gradient leaves the row-tile kernel for the streaming tall-wgrad kernel (one partial
-  // per ~R/128 rows instead of per 64)
-  TORCH_CHECK(!(tall_wgrad && slab), "tall_wgrad and slab exclude each other");
-  const bool tall = dwp != nullptr && (R >= kTallRows || tall_wgrad);
+  // very tall inputs (image K/V projections): the weight gradient leaves the row-tile kernel
+  // for the streaming tall-wgrad kernel (one partial per ~R/128 rows instead of per 64)
+  const bool tall = dwp != nullptr && R >= kTallRows;
   pio::ln_linear_bwd_launch(g.data_ptr(), is_bf16(g), (int)g.stride(0), N, bfp(w), (int)w.size(1), Kin, x.data_ptr(),
                             is_bf16(x), (int)x.stride(0), f32o(mean), f32o(rstd), f32o(lnw), f32o(lnb), dr, drs, dxp,
                             dx_rs, dgp, dbp, tall ? nullptr : dwp, tall ? nullptr : dbiasp, vrs < 0 ? 0 : vrs,
@@ -1333,7 +1330,9 @@ std::vector<Tensor> pixel_ce_fwd(Tensor h, Tensor w, Tensor b, Tensor labels, Te
   check_pixel_head(h, w, b, labels, wts);
   const long long R = h.size(0);
   const int K = (int)w.size(0);
-  Tensor part = torch::zeros({pio::pixel_ce_blocks(R), 4 + 2 * K}, h.options());
+  // every block of the launch stores its whole partial row (zeros only for an empty input)
+  Tensor part = R > 0 ? torch::empty({pio::pixel_ce_blocks(R), 4 + 2 * K}, h.options())
+                      : torch::zeros({pio::pixel_ce_blocks(R), 4 + 2 * K}, h.options());
   Tensor stats = torch::empty({4 + 2 * K + K}, h.options()), loss = torch::empty({}, h.options());
   pio::pixel_ce_fwd_launch((int)h.size(1), K, f32p(h), f32p(w), f32p(b), labels.data_ptr<int64_t>(), f32p(wts), R,
                            part.data_ptr<float>(), stats.data_ptr<float>(), loss.data_ptr<float>(), stream());
@@ -1352,7 +1351,8 @@ void pixel_ce_bwd(Tensor h, Tensor w, Tensor b, Tensor labels, Tensor wts, Tenso
               "pixel head bwd: dW / db like w / b");
   const long long R = h.size(0);
   const int K = (int)w.size(0), C = (int)h.size(1);
-  Tensor part = torch::zeros({pio::pixel_ce_blocks(R), (int64_t)K * C + K}, h.options());
+  Tensor part = R > 0 ? torch::empty({pio::pixel_ce_blocks(R), (int64_t)K * C + K}, h.options())
+                      : torch::zeros({pio::pixel_ce_blocks(R), (int64_t)K * C + K}, h.options());
   pio::pixel_ce_bwd_launch(C, K, f32p(h), f32p(w), f32p(b), labels.data_ptr<int64_t>(), f32p(wts), f32p(gout),
                            f32p(stats), R, dH.data_ptr<float>(), part.data_ptr<float>(), dW.data_ptr<float>(),
                            db.data_ptr<float>(), stream());
@@ -1763,8 +1763,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("lnw"), py::arg("lnb"), py::arg("dres"), py::arg("need_dx"), py::arg("dlnw"), py::arg("dlnb"),
         py::arg("dW"), py::arg("db"), py::arg("pe") = py::none(), py::arg("kin") = -1, py::arg("slab") = false,
         py::arg("job_slab") = py::none(), py::arg("job_dsts") = std::vector<Tensor>(),
-        py::arg("job_offs") = std::vector<int64_t>(), py::arg("dx_out") = py::none(), py::arg("pe_index") = py::none(),
-        py::arg("tall_wgrad") = false);
+        py::arg("job_offs") = std::vector<int64_t>(), py::arg("dx_out") = py::none(), py::arg("pe_index") = py::none());
   m.def("wgrad", &wgrad, py::arg("g"), py::arg("a"), py::arg("amode"), py::arg("mean"), py::arg("rstd"), py::arg("lnw"),
         py::arg("lnb"), py::arg("rows_per_wg"), py::arg("dW"), py::arg("db"), py::arg("pe") = py::none(),
         py::arg("kin") = -1, py::arg("pe_index") = py::none());

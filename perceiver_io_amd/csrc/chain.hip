@@ -4,8 +4,6 @@
 // VGPRs, so the softmax and LayerNorm VALU work reads them directly instead of copying every
 // accumulator out of (and back into) AGPRs (≈1,300 v_accvgpr moves per wave in the attention
 // phase otherwise).  The CL / CL2 helpers live in chain_cl.h (shared with persist.hip).
-#include <algorithm>
-
 #include "chain_cl.h"
 
 namespace pio {
@@ -311,9 +309,8 @@ __global__ __launch_bounds__(512) void ln_linear_post_attn_bwd_chain8_kernel(
   float2* sR = reinterpret_cast<float2*>(smem + lpb_chain_smem<NQ>());              // 2 pair-sum slots
   PIO_WG_BEGIN();
   zero_span_block(job);
-  const int ntiles = (R + 63) / 64;
-  if ((int)blockIdx.x >= ntiles) {  // appended workgroups: (a share of) the previous kernel's slab job
-    slab_reduce_block(job, job.det ? blockIdx.x - ntiles : blockIdx.x, reinterpret_cast<float4*>(smem));
+  if ((int)blockIdx.x >= (R + 63) / 64) {  // appended workgroups: the previous kernel's slab job
+    slab_reduce_block(job, blockIdx.x - (R + 63) / 64, reinterpret_cast<float4*>(smem));
     PIO_WG_END();
     return;
   }
@@ -559,11 +556,6 @@ __global__ __launch_bounds__(512) void ln_linear_post_attn_bwd_chain8_kernel(
   };
   if (wave_id() >> 2) body(std::integral_constant<int, 1>{});
   else body(std::integral_constant<int, 0>{});
-  // the tile's share of the previous kernel's slab reduction (non-deterministic jobs: block b =
-  // this tile, sized by the launcher to the tile count): every CU streams its share as its tile
-  // ends, instead of ~half the CUs running appended workgroups after all tiles (the ≈124 KB of
-  // LDS per tile keeps appended workgroups from starting earlier)
-  if (job.slab != nullptr && !job.det && (int)blockIdx.x < job.nblk) slab_reduce_block(job, blockIdx.x, nullptr);
   PIO_WG_END();
 }
 
@@ -617,22 +609,11 @@ bool ln_linear_post_attn_bwd_chain_launch(const void* G, bool g_bf16, const uint
                                           const PostAttnGrads& grads, int R, const SlabJob& job, const DropCfg& dr,
                                           int nq, hipStream_t st) {
   if (nq != 192 && nq != 64) return false;
-  // a non-deterministic slab job runs inside the tiles (see the kernel's end): its row splits
-  // re-sized to fill the tile count; blocks beyond it (and deterministic jobs) are appended
-  const int ntiles = (R + 63) / 64;
-  SlabJob jb = job;
-  if (jb.slab != nullptr && !jb.det) {
-    int nsy = std::max(1, std::min(jb.S, ntiles / std::max(1, jb.nbx)));
-    const int rb = (jb.S + nsy - 1) / nsy;
-    nsy = (jb.S + rb - 1) / rb;
-    jb.nblk = jb.nbx * nsy;
-  }
-  const int extra = jb.slab == nullptr ? 0 : (jb.det ? jb.nblk : std::max(0, jb.nblk - ntiles));
-  dim3 grid(ntiles + extra);
+  dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0));
 #define LPC(NQ, TG)                                                                                                    \
   hipLaunchKernelGGL((ln_linear_post_attn_bwd_chain8_kernel<NQ, TG>), grid, dim3(512), 0, st, static_cast<const TG*>(G), \
                      Wq, X, mean1, rstd1, lnw, lnb, dres, dlnw, dlnb, dWq, dbq, Ysave, mean2, rstd2, U, O, Wo, W1, W2,    \
-                     g2, be2, dY, dO, delta, grads, R, jb, dr)
+                     g2, be2, dY, dO, delta, grads, R, job, dr)
   if (g_bf16) {
     if (nq != 192) return false;  // bf16 G only from the self-attention backward (nq = 3C)
     LPC(3, uint16_t);

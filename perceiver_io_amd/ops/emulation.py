@@ -450,8 +450,7 @@ def _post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, be2, H, grads, seed=None
 
 
 def ln_linear_bwd(g, w, x, mean, rstd, lnw, lnb, dres, need_dx, dlnw=None, dlnb=None, dW=None, db=None, pe=None,
-                  kin=-1, slab=False, job_slab=None, job_dsts=(), job_offs=(), dx_out=None, pe_index=None,
-                  tall_wgrad=False):
+                  kin=-1, slab=False, job_slab=None, job_dsts=(), job_offs=(), dx_out=None, pe_index=None):
     """Returns dX (or None); LN grads accumulate into dlnw / dlnb and, when given,
     dW += gᵀ·LN(x), db += Σ_rows g (slab: stored into (tiles, ·) slab views)."""
     _run_job(job_slab, job_dsts, job_offs)

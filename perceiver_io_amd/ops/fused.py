@@ -309,19 +309,6 @@ class KVSource:
 PE_FACTORED = True
 
 
-# the cross-attention K/V projection's weight gradient from the streaming tall-wgrad kernel (one
-# partial per row range; the LN affine gradients by atomics) instead of per-64-row-tile slabs
-# once the input has at least this many rows — for wide inputs (the LArTPC [pixel ‖ PE] rows,
-# Kin = 131) whose slab rows are large; PERCEIVER_KV_TALL_MIN overrides (rows; 0 = never)
-KV_TALL_MIN = int(os.environ.get("PERCEIVER_KV_TALL_MIN", str(1 << 17)))
-
-
-def _kv_tall(R: int, kin: int) -> bool:
-    from . import deterministic
-
-    return KV_TALL_MIN > 0 and R >= KV_TALL_MIN and not deterministic()
-
-
 def _adjacent_rows(a: torch.Tensor, b: torch.Tensor):
     """(2N, K) view over two contiguous (N, K) tensors that lie back to back in one storage (e.g.
     the k / v projection gradients in the optimizer's flat buffer), else None."""
@@ -760,7 +747,7 @@ class _LayerFn(torch.autograd.Function):
                     K.pe_grads(Dm, part, ebf, ps[5].detach(), ps[6].detach(), g_kv.detach(), b_kv.detach(), nc,
                                tg(ps[5]), tg(ps[6]), gbias[0, C:3 * C] if rep_mode else gbias[C:3 * C], tg(g_kv),
                                tg(b_kv))
-                elif WGRAD_SLAB and Rkv < TALL_ROWS and not (ctx.kv_pe is not None and _kv_tall(Rkv, Ckv)):
+                elif WGRAD_SLAB and Rkv < TALL_ROWS:
                     sl = _GradSlab(Rkv, [Ckv, Ckv, 2 * C * Ckv, 2 * C], dz2)
                     src = ctx.src
                     chain = src is not None and ctx.kv_grad and ctx.kv_pe is None
@@ -794,8 +781,7 @@ class _LayerFn(torch.autograd.Function):
                             gwkv = torch.zeros((8, 2 * C * Ckv) if rep_mode else (2 * C, Ckv), **f32)
                     dx_kv = K.ln_linear_bwd(dkv2, wkv, xkv2, mean_kv, rstd_kv, g_kv, b_kv, None, ctx.kv_grad,
                                             gb(g_kv), gb(b_kv), gwkv, rows(gbias, C, 3 * C, 1), ctx.kv_pe, Ckv,
-                                            pe_index=ctx.kv_pe_index,
-                                            tall_wgrad=ctx.kv_pe is not None and _kv_tall(Rkv, Ckv))
+                                            pe_index=ctx.kv_pe_index)
                     if sep:
                         gb(ps[5]).add_(rows(gwkv, 0, C, Ckv))
                         gb(ps[6]).add_(rows(gwkv, C, 2 * C, Ckv))

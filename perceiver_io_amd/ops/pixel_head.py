@@ -36,12 +36,15 @@ class _PixelCE(torch.autograd.Function):
         ctx.save_for_backward(h2, lab, wts, stats)
         ctx.w, ctx.b, ctx.hshape = w, b, h.shape
         ctx.mark_non_differentiable(stats)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics output
         return loss, stats
 
     @staticmethod
     def backward(ctx, g, _gstats):
         from .fused import kernels
 
+        if g is None:
+            return None, None, None, None, None
         K = kernels(g)
         h2, lab, wts, stats = ctx.saved_tensors
         w, b = ctx.w, ctx.b
