@@ -108,6 +108,19 @@ __device__ __forceinline__ void ld_f32(float (&v)[16], const float* base, long l
     v[4 * g] = a.x; v[4 * g + 1] = a.y; v[4 * g + 2] = a.z; v[4 * g + 3] = a.w;
   }
 }
+// this lane's 16 bf16 values of tile n0 kept packed (4 × 8 bytes) until cvt_raw
+__device__ __forceinline__ void ld_raw(uint2 (&v)[4], const uint16_t* base, long long ld, long long row, int n0) {
+  const int hh = lane_id() >> 5;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) v[g] = *reinterpret_cast<const uint2*>(base + row * ld + n0 + 8 * g + 4 * hh);
+}
+__device__ __forceinline__ void cvt_raw(float (&v)[16], const uint2 (&a)[4]) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    v[4 * g] = bf2f((uint16_t)(a[g].x & 0xFFFF)); v[4 * g + 1] = bf2f((uint16_t)(a[g].x >> 16));
+    v[4 * g + 2] = bf2f((uint16_t)(a[g].y & 0xFFFF)); v[4 * g + 3] = bf2f((uint16_t)(a[g].y >> 16));
+  }
+}
 __device__ __forceinline__ void ld_bf16(float (&v)[16], const uint16_t* base, long long ld, long long row, int n0) {
   const int hh = lane_id() >> 5;
 #pragma unroll
@@ -117,8 +130,15 @@ __device__ __forceinline__ void ld_bf16(float (&v)[16], const uint16_t* base, lo
     v[4 * g + 2] = bf2f((uint16_t)(a.y & 0xFFFF)); v[4 * g + 3] = bf2f((uint16_t)(a.y >> 16));
   }
 }
-// per-channel vector (bias, γ, β) at this lane's 16 channels of tile n0
+// per-channel vector (bias, γ, β) at this lane's 16 channels of tile n0 (from an LDS copy: vmcnt
+// counts loads and stores together in issue order, so a global load consumed right after a
+// phase's stores would wait for every one of them)
 __device__ __forceinline__ void ld_vec(float (&v)[16], const float* p, int n0) { ld_f32(v, p, 0, 0, n0); }
+// stage n (float4-aligned, 16-byte aligned) floats of global vectors into LDS: all threads, no barrier
+__device__ __forceinline__ void stage_vec(float* dst, const float* src, int n) {
+  for (int i = threadIdx.x; i < n / 4; i += blockDim.x)
+    reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>(src)[i];
+}
 __device__ __forceinline__ void to_f(float (&v)[16], const f32x16& a) {
 #pragma unroll
   for (int i = 0; i < 16; ++i) v[i] = a[i];
@@ -204,9 +224,25 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t sImg[2][NR * LDI];
   __shared__ __attribute__((aligned(16))) uint16_t sV[S::NW][NR * LDA];
   __shared__ __attribute__((aligned(16))) float2 sRed[S::NW * NR];
+  // every layer's per-channel vectors, staged once before any store of the kernel:
+  // [γ1 | β1 | bqkv (3C) | bo | γ2 | β2 | b1 | b2]
+  constexpr int NV = 10 * C;
+  __shared__ __attribute__((aligned(16))) float sVec[kSBMaxLayers][NV];
   const int w = wave_id(), l = lane_id(), r = l & 31;
   const long long row = (long long)blockIdx.x * NR + r;
   const int n0 = 32 * w;  // this wave's channel tile
+  for (int li = 0; li < a.L; ++li) {
+    const SBLayer& y = a.ly[li];
+    float* v = sVec[li];
+    stage_vec(v, y.g1, C);
+    stage_vec(v + C, y.be1, C);
+    stage_vec(v + 2 * C, y.bqkv, 3 * C);
+    stage_vec(v + 5 * C, y.bo, C);
+    stage_vec(v + 6 * C, y.g2, C);
+    stage_vec(v + 7 * C, y.be2, C);
+    stage_vec(v + 8 * C, y.b1, C);
+    stage_vec(v + 9 * C, y.b2, C);
+  }
   float x[16];
   ld_f32(x, a.X0, C, row, n0);
   bf16x8 wq[3][KS];
@@ -215,41 +251,44 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
   load_wtile<C>(wq[2], a.ly[0].Wqkv, 2 * C + n0);
   for (int li = 0; li < a.L; ++li) {
     const SBLayer& y = a.ly[li];
+    const float* vec = sVec[li];
     // ---- LN1 → image 0 (the QKV product's operand) ----
     float mu, rs, gv[16], bv[16], t[16];
-    ld_vec(gv, y.g1, n0);
-    ld_vec(bv, y.be1, n0);
-    ln_stats<C>(x, sRed, a.eps, mu, rs);
+    ln_stats<C>(x, sRed, a.eps, mu, rs);  // (its barrier also publishes the staged vectors)
+    ld_vec(gv, vec, n0);
+    ld_vec(bv, vec + C, n0);
 #pragma unroll
     for (int i = 0; i < 16; ++i) t[i] = (x[i] - mu) * rs * gv[i] + bv[i];
-    if (w == 0 && l < 32) { y.mean1[row] = mu; y.rstd1[row] = rs; }
     st_bf16(sImg[0], LDI, r, n0, t);
-    st_bf16(y.LN1X, C, row, n0, t);
+    // each phase issues its weight prefetch before its global stores (vmcnt counts both in issue
+    // order: a load behind the stores would make its consumer wait for them)
     bf16x8 wo[KS];
     load_wtile<C>(wo, y.Wo, n0);
+    if (w == 0 && l < 32) { y.mean1[row] = mu; y.rstd1[row] = rs; }
+    st_bf16(y.LN1X, C, row, n0, t);
     lds_sync();
     // ---- Q, K, V of the wave's heads ----
     float q[16], k[16], v[16];
     {
       float bb[16];
       f32x16 acc = gemm_t<C>(wq[0], sImg[0], LDI);
-      ld_vec(bb, y.bqkv, n0);
+      ld_vec(bb, vec + 2 * C, n0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) q[i] = acc[i] + bb[i];
       acc = gemm_t<C>(wq[1], sImg[0], LDI);
-      ld_vec(bb, y.bqkv, C + n0);
+      ld_vec(bb, vec + 3 * C, n0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) k[i] = acc[i] + bb[i];
       acc = gemm_t<C>(wq[2], sImg[0], LDI);
-      ld_vec(bb, y.bqkv, 2 * C + n0);
+      ld_vec(bb, vec + 4 * C, n0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) v[i] = acc[i] + bb[i];
     }
+    bf16x8 w1[KS];
+    load_wtile<C>(w1, y.W1, n0);
     st_bf16(y.QKV, 3 * C, row, n0, q);
     st_bf16(y.QKV, 3 * C, row, C + n0, k);
     st_bf16(y.QKV, 3 * C, row, 2 * C + n0, v);
-    bf16x8 w1[KS];
-    load_wtile<C>(w1, y.W1, n0);
     // ---- attention of the wave's heads: Sᵀ = K·Qᵀ (lane = query), softmax over keys, Oᵀ = Vᵀ·Pᵀ
     // with Vᵀ read transposed from a wave-private LDS tile [key][32 channels] ----
     float o[16];
@@ -269,22 +308,22 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
       }
     }
     st_bf16(sImg[1], LDI, r, n0, o);
-    st_bf16(y.O, C, row, n0, o);
     bf16x8 w2[KS];
     load_wtile<C>(w2, y.W2, n0);
+    st_bf16(y.O, C, row, n0, o);
     lds_sync();
     // ---- out-projection + residual → y; LN2 → image 0 ----
     float yv[16];
     {
       float bb[16];
       const f32x16 acc = gemm_t<C>(wo, sImg[1], LDI);
-      ld_vec(bb, y.bo, n0);
+      ld_vec(bb, vec + 5 * C, n0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) yv[i] = acc[i] + bb[i] + x[i];
     }
     st_f32(y.Y, C, row, n0, yv);
-    ld_vec(gv, y.g2, n0);
-    ld_vec(bv, y.be2, n0);
+    ld_vec(gv, vec + 6 * C, n0);
+    ld_vec(bv, vec + 7 * C, n0);
     ln_stats<C>(yv, sRed, a.eps, mu, rs);
 #pragma unroll
     for (int i = 0; i < 16; ++i) t[i] = (yv[i] - mu) * rs * gv[i] + bv[i];
@@ -296,25 +335,26 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
     {
       float bb[16];
       const f32x16 acc = gemm_t<C>(w1, sImg[0], LDI);
-      ld_vec(bb, y.b1, n0);
+      ld_vec(bb, vec + 8 * C, n0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) t[i] = acc[i] + bb[i];
     }
-    st_bf16(y.U, C, row, n0, t);
+    float gu[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) t[i] = gelu_f(t[i]);
-    st_bf16(sImg[1], LDI, r, n0, t);
-    st_bf16(y.GU, C, row, n0, t);
+    for (int i = 0; i < 16; ++i) gu[i] = gelu_f(t[i]);
+    st_bf16(sImg[1], LDI, r, n0, gu);
     if (li + 1 < a.L) {  // the next layer's QKV weights, in flight during the MLP
       load_wtile<C>(wq[0], a.ly[li + 1].Wqkv, n0);
       load_wtile<C>(wq[1], a.ly[li + 1].Wqkv, C + n0);
       load_wtile<C>(wq[2], a.ly[li + 1].Wqkv, 2 * C + n0);
     }
+    st_bf16(y.U, C, row, n0, t);
+    st_bf16(y.GU, C, row, n0, gu);
     lds_sync();
     {
       float bb[16];
       const f32x16 acc = gemm_t<C>(w2, sImg[1], LDI);
-      ld_vec(bb, y.b2, n0);
+      ld_vec(bb, vec + 9 * C, n0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) x[i] = acc[i] + bb[i] + yv[i];
     }
@@ -366,45 +406,65 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t sQ[NR * LDQ];
   __shared__ __attribute__((aligned(16))) uint16_t sAt[NW][4][NR * LDA];  // per wave: K, Q, dO, P / dS
   __shared__ __attribute__((aligned(16))) float2 sRed[NW * NR];
+  __shared__ __attribute__((aligned(16))) float sG[kSBMaxLayers][2][C];  // γ1, γ2 of every layer
   const int w = wave_id(), l = lane_id(), r = l & 31;
   const long long row = (long long)blockIdx.x * NR + r;
   const int n0 = 32 * w;
   const float sc = a.scale_log2 * 0.69314718055994531f;  // the softmax scale 1/√d
+  for (int li = 0; li < a.L; ++li) {
+    stage_vec(sG[li][0], a.ly[li].g1, C);
+    stage_vec(sG[li][1], a.ly[li].g2, C);
+  }
   float dz[16];
   ld_f32(dz, a.dZ, C, row, n0);
   bf16x8 pw[KS];
   wblock_load<C>(pw, a.ly[a.L - 1].W2, 0);
+  // Every phase issues its global loads (the next weight block, the layer's saved rows) BEFORE its
+  // global stores: vmcnt counts both in issue order, so a load issued behind a phase's stores
+  // would make its consumer wait for all of them
   for (int li = a.L - 1; li >= 0; --li) {
     const SBLayer& y = a.ly[li];
     const SBGrad& gd = a.gr[li];
     const float* X = li > 0 ? a.ly[li - 1].Z : a.X0;
-    // ---- dZ image; W2 block ----
-    st_bf16(sImg[0], LDI, r, n0, dz);
-    st_bf16(gd.dZ, C, row, n0, dz);
+    // ---- the layer's first saved rows; dZ image; W2 block ----
+    uint2 ur[4];
+    float yv[16];
+    ld_raw(ur, y.U, C, row, n0);
+    ld_f32(yv, y.Y, C, row, n0);
+    const float mu2 = y.mean2[row], rs2 = y.rstd2[row];
     wblock_store<C>(sW[0], pw);
     wblock_load<C>(pw, y.W1, 0);
-    float uv[16];
-    ld_bf16(uv, y.U, C, row, n0);
+    st_bf16(sImg[0], LDI, r, n0, dz);
+    st_bf16(gd.dZ, C, row, n0, dz);
     lds_sync();
     // ---- dU = (W2ᵀ·dZ)∘GELU'(u) ----
     float t[16];
     {
+      float uv[16];
+      cvt_raw(uv, ur);
       const f32x16 acc = gemm_tt<C>(sW[0], n0, sImg[0], LDI, 0, f32x16{});
 #pragma unroll
       for (int i = 0; i < 16; ++i) t[i] = acc[i] * gelu_grad(uv[i]);
     }
     st_bf16(sImg[1], LDI, r, n0, t);
-    st_bf16(gd.dU, C, row, n0, t);
     wblock_store<C>(sW[1], pw);
     wblock_load<C>(pw, y.Wo, 0);
-    float yv[16], gv[16];
-    ld_f32(yv, y.Y, C, row, n0);
-    ld_vec(gv, y.g2, n0);
-    const float mu2 = y.mean2[row], rs2 = y.rstd2[row];
+    // the attention operands of the wave's heads (the forward's bf16 rows) and the LN1 input
+    uint2 qr[4], kr[4], vr[4], orw[4];
+    float xv[16];
+    ld_raw(qr, y.QKV, 3 * C, row, n0);
+    ld_raw(kr, y.QKV, 3 * C, row, C + n0);
+    ld_raw(vr, y.QKV, 3 * C, row, 2 * C + n0);
+    ld_raw(orw, y.O, C, row, n0);
+    ld_f32(xv, X, C, row, n0);
+    const float mu1 = y.mean1[row], rs1 = y.rstd1[row];
+    st_bf16(gd.dU, C, row, n0, t);
     lds_sync();
     // ---- dXn2 = W1ᵀ·dU; LN2 backward → dY ----
     float dy[16];
     {
+      float gv[16];
+      ld_vec(gv, sG[li][1], n0);
       const f32x16 acc = gemm_tt<C>(sW[1], n0, sImg[1], LDI, 0, f32x16{});
       float s1 = 0.f, s2 = 0.f, gg[16];
 #pragma unroll
@@ -420,30 +480,29 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) dy[i] = dz[i] + rs2 * (gg[i] - m1 - yv[i] * m2);
     }
-    ln_affine_grads(t, yv, gd.dg2, gd.dbe2, n0);
     st_bf16(sImg[0], LDI, r, n0, dy);
-    st_bf16(gd.dY, C, row, n0, dy);
     wblock_store<C>(sW[0], pw);
     wblock_load<C>(pw, y.Wqkv, 0);
-    // the attention operands of the wave's heads (the forward's bf16 rows)
-    float qv[16], kv[16], vv[16], ov[16];
-    ld_bf16(qv, y.QKV, 3 * C, row, n0);
-    ld_bf16(kv, y.QKV, 3 * C, row, C + n0);
-    ld_bf16(vv, y.QKV, 3 * C, row, 2 * C + n0);
-    ld_bf16(ov, y.O, C, row, n0);
+    ln_affine_grads(t, yv, gd.dg2, gd.dbe2, n0);
+    st_bf16(gd.dY, C, row, n0, dy);
     lds_sync();
     // ---- dO = Woᵀ·dY (the wave's heads) ----
     float dov[16];
     to_f(dov, gemm_tt<C>(sW[0], n0, sImg[0], LDI, 0, f32x16{}));
     // ---- attention backward of the wave's heads (wave-local) ----
+    float gq[16], gk[16], gvv[16];
     {
+      float qv[16], kv[16], vv[16], ov[16];
+      cvt_raw(qv, qr);
+      cvt_raw(kv, kr);
+      cvt_raw(vv, vr);
+      cvt_raw(ov, orw);
       uint16_t *tK = sAt[w][0], *tQ = sAt[w][1], *tdO = sAt[w][2], *tP = sAt[w][3];
       st_bf16(tK, LDA, r, 0, kv);
       st_bf16(tQ, LDA, r, 0, qv);
 #pragma unroll
       for (int i = 0; i < 16; ++i) dov[i] = bf2f(f2bf(dov[i]));  // dO as bf16, as the products see it
       st_bf16(tdO, LDA, r, 0, dov);
-      float gq[16], gk[16], gvv[16];
 #pragma unroll
       for (int hp = 0; hp < S::HPW; ++hp) {
         // Pᵀ exactly as the forward formed it, dPᵀ = V·dOᵀ, δ = rowsum(dO∘O) over the head
@@ -481,19 +540,15 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
         for (int i = 0; i < 16; ++i)
           if (head_reg<C>(i, hp)) { gq[i] = dq[i] * sc; gk[i] = dk[i] * sc; gvv[i] = dv[i]; }
       }
-      st_bf16(sQ, LDQ, r, n0, gq);
-      st_bf16(gd.dQKV, 3 * C, row, n0, gq);
-      st_bf16(sQ, LDQ, r, C + n0, gk);
-      st_bf16(gd.dQKV, 3 * C, row, C + n0, gk);
-      st_bf16(sQ, LDQ, r, 2 * C + n0, gvv);
-      st_bf16(gd.dQKV, 3 * C, row, 2 * C + n0, gvv);
     }
+    st_bf16(sQ, LDQ, r, n0, gq);
+    st_bf16(sQ, LDQ, r, C + n0, gk);
+    st_bf16(sQ, LDQ, r, 2 * C + n0, gvv);
     wblock_store<C>(sW[1], pw);
     wblock_load<C>(pw, y.Wqkv, C);
-    float xv[16];
-    ld_f32(xv, X, C, row, n0);
-    ld_vec(gv, y.g1, n0);
-    const float mu1 = y.mean1[row], rs1 = y.rstd1[row];
+    st_bf16(gd.dQKV, 3 * C, row, n0, gq);
+    st_bf16(gd.dQKV, 3 * C, row, C + n0, gk);
+    st_bf16(gd.dQKV, 3 * C, row, 2 * C + n0, gvv);
     lds_sync();
     // ---- dXn1 = Wqkvᵀ·dQKV in three C-row blocks of Wqkv ----
     f32x16 acc = gemm_tt<C>(sW[1], n0, sQ, LDQ, 0, f32x16{});
@@ -507,6 +562,8 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
     acc = gemm_tt<C>(sW[1], n0, sQ, LDQ, 2 * C, acc);
     // ---- LN1 backward → dX (the previous layer's dZ) ----
     {
+      float gv[16];
+      ld_vec(gv, sG[li][0], n0);
       float s1 = 0.f, s2 = 0.f, gg[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
