@@ -650,10 +650,11 @@ std::vector<Tensor> sb_fwd(Tensor x, std::vector<Tensor> params, double scale, d
 }
 
 // backward of a block: dz (B·32, C) fp32, x0 the block input, saved = sb_fwd's outputs, params
-// as sb_fwd's; ln_grads = per layer (dγ1, dβ1, dγ2, dβ2) fp32 targets (added to).  Returns
-// [dx, then per layer the gradient rows dQKV, dY, dU, dZ (bf16)] for sb_wgrad
-std::vector<Tensor> sb_bwd(Tensor dz, Tensor x0, std::vector<Tensor> saved, std::vector<Tensor> params,
-                           std::vector<Tensor> ln_grads, double scale, double eps) {
+// as sb_fwd's.  Returns [dx, the (B, 4·L·C) fp32 LayerNorm partial slab (row b: sample b's
+// [dγ1 | dβ1 | dγ2 | dβ2] of layer 0, then layer 1, …; sum the rows into the gradients), then per
+// layer the gradient rows dQKV, dY, dU, dZ (bf16)] for sb_wgrad
+std::vector<Tensor> sb_bwd(Tensor dz, Tensor x0, std::vector<Tensor> saved, std::vector<Tensor> params, double scale,
+                           double eps) {
   const int C = x0.dim() == 2 ? (int)x0.size(1) : 0;
   TORCH_CHECK(dz.is_contiguous() && x0.is_contiguous() && dz.sizes() == x0.sizes() && (C == 64 || C == 128) &&
                   x0.size(0) % kSBN == 0 && x0.size(0) > 0,
@@ -661,9 +662,8 @@ std::vector<Tensor> sb_bwd(Tensor dz, Tensor x0, std::vector<Tensor> saved, std:
   CHECK_DT(dz, torch::kFloat32);
   CHECK_DT(x0, torch::kFloat32);
   const int L = (int)params.size() / 12, R = (int)x0.size(0);
-  TORCH_CHECK(L >= 1 && L <= pio::kSBMaxLayers && (int)params.size() == 12 * L && (int)saved.size() == kSBSaved * L &&
-                  (int)ln_grads.size() == 4 * L,
-              "sb_bwd: saved / ln_grads per layer");
+  TORCH_CHECK(L >= 1 && L <= pio::kSBMaxLayers && (int)params.size() == 12 * L && (int)saved.size() == kSBSaved * L,
+              "sb_bwd: saved per layer");
   auto f32 = x0.options().dtype(torch::kFloat32);
   auto b16 = x0.options().dtype(torch::kBFloat16);
   pio::SBBwdArgs a{};
@@ -672,7 +672,9 @@ std::vector<Tensor> sb_bwd(Tensor dz, Tensor x0, std::vector<Tensor> saved, std:
   a.eps = (float)eps;
   Tensor dx = torch::empty({R, C}, f32);
   a.dX = dx.data_ptr<float>();
-  std::vector<Tensor> out{dx};
+  Tensor lns = torch::empty({(int64_t)a.B, (int64_t)4 * L * C}, f32);  // every element stored by the kernel
+  a.ln_rs = 4 * L * C;
+  std::vector<Tensor> out{dx, lns};
   for (int i = 0; i < L; ++i) {
     sb_fill_params(a.ly[i], params, i, C);
     sb_fill_saved(a.ly[i], saved, i, R, C);
@@ -681,9 +683,8 @@ std::vector<Tensor> sb_bwd(Tensor dz, Tensor x0, std::vector<Tensor> saved, std:
            dzz = torch::empty({R, C}, b16);
     g.dQKV = reinterpret_cast<uint16_t*>(dq.data_ptr()); g.dY = reinterpret_cast<uint16_t*>(dy.data_ptr());
     g.dU = reinterpret_cast<uint16_t*>(du.data_ptr()); g.dZ = reinterpret_cast<uint16_t*>(dzz.data_ptr());
-    for (int k = 0; k < 4; ++k) sb_check_v(ln_grads[4 * i + k], C, "LN gradient target");
-    g.dg1 = ln_grads[4 * i].data_ptr<float>(); g.dbe1 = ln_grads[4 * i + 1].data_ptr<float>();
-    g.dg2 = ln_grads[4 * i + 2].data_ptr<float>(); g.dbe2 = ln_grads[4 * i + 3].data_ptr<float>();
+    float* lp = lns.data_ptr<float>() + (int64_t)4 * i * C;
+    g.dg1 = lp; g.dbe1 = lp + C; g.dg2 = lp + 2 * C; g.dbe2 = lp + 3 * C;
     out.insert(out.end(), {dq, dy, du, dzz});
   }
   TORCH_CHECK(pio::sb_bwd_launch(a, C, stream()), "sb_bwd: launch refused");
@@ -1740,7 +1741,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("p") = 0.0);
   m.def("persist_errors", &persist_errors, py::arg("reset") = true);
   m.def("sb_fwd", &sb_fwd, py::arg("x"), py::arg("params"), py::arg("scale"), py::arg("eps"));
-  m.def("sb_bwd", &sb_bwd, py::arg("dz"), py::arg("x0"), py::arg("saved"), py::arg("params"), py::arg("ln_grads"),
+  m.def("sb_bwd", &sb_bwd, py::arg("dz"), py::arg("x0"), py::arg("saved"), py::arg("params"),
         py::arg("scale"), py::arg("eps"));
   m.def("sb_wgrad", &sb_wgrad, py::arg("jobs"));
   m.def("post_attn_ln_linear_fwd", &post_attn_ln_linear_fwd, py::arg("o"), py::arg("x"), py::arg("wo"), py::arg("bo"),

@@ -383,7 +383,7 @@ __device__ __forceinline__ void wblock_store(uint16_t* sW, const bf16x8 (&f)[C /
   }
 }
 // LayerNorm γ/β gradients of this sample: Σ_rows dxn·x̂ and Σ_rows dxn per channel (the 32 rows
-// are the 32 lanes of each half), added to the targets by lanes 0 and 32
+// are the 32 lanes of each half), stored into the sample's slab row by lanes 0 and 32
 __device__ __forceinline__ void ln_affine_grads(const float (&dxn)[16], const float (&xh)[16], float* dg, float* db, int n0) {
   const int l = lane_id(), hh = l >> 5;
 #pragma unroll
@@ -391,8 +391,8 @@ __device__ __forceinline__ void ln_affine_grads(const float (&dxn)[16], const fl
     const float sg = half_sum(dxn[i] * xh[i]);
     const float sb = half_sum(dxn[i]);
     if ((l & 31) == 0) {
-      atomicAdd(dg + n0 + tch(i, hh), sg);
-      atomicAdd(db + n0 + tch(i, hh), sb);
+      dg[n0 + tch(i, hh)] = sg;
+      db[n0 + tch(i, hh)] = sb;
     }
   }
 }
@@ -411,6 +411,7 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
   const long long row = (long long)blockIdx.x * NR + r;
   const int n0 = 32 * w;
   const float sc = a.scale_log2 * 0.69314718055994531f;  // the softmax scale 1/√d
+  const long long lnr = (long long)blockIdx.x * a.ln_rs;  // this sample's LayerNorm partial row
   for (int li = 0; li < a.L; ++li) {
     stage_vec(sG[li][0], a.ly[li].g1, C);
     stage_vec(sG[li][1], a.ly[li].g2, C);
@@ -483,7 +484,7 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
     st_bf16(sImg[0], LDI, r, n0, dy);
     wblock_store<C>(sW[0], pw);
     wblock_load<C>(pw, y.Wqkv, 0);
-    ln_affine_grads(t, yv, gd.dg2, gd.dbe2, n0);
+    ln_affine_grads(t, yv, gd.dg2 + lnr, gd.dbe2 + lnr, n0);
     st_bf16(gd.dY, C, row, n0, dy);
     lds_sync();
     // ---- dO = Woᵀ·dY (the wave's heads) ----
@@ -578,7 +579,7 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) dz[i] = dy[i] + rs1 * (gg[i] - m1 - xv[i] * m2);
     }
-    ln_affine_grads(t, xv, gd.dg1, gd.dbe1, n0);
+    ln_affine_grads(t, xv, gd.dg1 + lnr, gd.dbe1 + lnr, n0);
   }
   st_f32(a.dX, C, row, n0, dz);
 }

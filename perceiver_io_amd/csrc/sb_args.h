@@ -22,8 +22,10 @@ struct SBFwdArgs {
   int L, B;
   float scale_log2, eps;
 };
-// backward: the gradient rows the weight-gradient GEMMs need (bf16) and the LayerNorm affine
-// gradient targets (fp32, atomically added)
+// backward: the gradient rows the weight-gradient GEMMs need (bf16) and the sample's LayerNorm
+// affine gradient partials (fp32 slab rows: row b = sample b, stride ln_rs floats in SBBwdArgs;
+// every element stored once, summed over the samples by a slab reduction — per-sample atomics
+// on the same 4·C addresses serialise at the L2)
 struct SBGrad {
   uint16_t *dQKV, *dY, *dU, *dZ;
   float *dg1, *dbe1, *dg2, *dbe2;
@@ -35,6 +37,7 @@ struct SBBwdArgs {
   const float* dZ;   // gradient of the block output (B·32, C) fp32
   float* dX;         // gradient of the block input (B·32, C) fp32 (written)
   int L, B;
+  int ln_rs;         // row stride of the LayerNorm partial slab (floats)
   float scale_log2, eps;
 };
 // grouped weight-gradient GEMMs: dW[n][k] += Σ_rows G[r][n] · A[r][k], db[n] += Σ_rows G[r][n]

@@ -790,12 +790,15 @@ def sb_fwd(x, params, scale, eps):
     return out
 
 
-def sb_bwd(dz, x0, saved, params, ln_grads, scale, eps):
+def sb_bwd(dz, x0, saved, params, scale, eps):
     R, C = x0.shape
     B = R // _SB_N
     L = len(params) // 12
-    d = C // _SB_H
     grads = [None] * L
+    lns = torch.empty(B, 4 * L * C, dtype=torch.float32, device=x0.device)
+
+    def per_sample(t):  # (B·32, C) → the sample sums (B, C)
+        return t.view(B, _SB_N, C).sum(1)
     dz = dz.float()
     for i in reversed(range(L)):
         g1, be1, wqkv, bqkv, wo, bo, g2, be2, w1, b1, w2, b2 = _sb_unpack(params, i)
@@ -806,8 +809,8 @@ def sb_bwd(dz, x0, saved, params, ln_grads, scale, eps):
         dxn2 = du @ w1.float()
         dyl, yh = _ln_bwd(dxn2, y, mean2, rstd2, g2)
         dy = dz + dyl
-        ln_grads[4 * i + 2].view(-1).add_((dxn2 * yh).sum(0))
-        ln_grads[4 * i + 3].view(-1).add_(dxn2.sum(0))
+        lns[:, (4 * i + 2) * C:(4 * i + 3) * C] = per_sample(dxn2 * yh)
+        lns[:, (4 * i + 3) * C:(4 * i + 4) * C] = per_sample(dxn2)
         dyb = _bf(dy)
         do = _bf(dyb @ wo.float())
         qf = qkv.float()
@@ -825,12 +828,12 @@ def sb_bwd(dz, x0, saved, params, ln_grads, scale, eps):
         dqkvb = _bf(dqkv)
         dxn1 = dqkvb @ wqkv.float()
         dxl, xh = _ln_bwd(dxn1, x, mean1, rstd1, g1)
-        ln_grads[4 * i].view(-1).add_((dxn1 * xh).sum(0))
-        ln_grads[4 * i + 1].view(-1).add_(dxn1.sum(0))
+        lns[:, 4 * i * C:(4 * i + 1) * C] = per_sample(dxn1 * xh)
+        lns[:, (4 * i + 1) * C:(4 * i + 2) * C] = per_sample(dxn1)
         bf = torch.bfloat16
         grads[i] = [dqkvb.to(bf), dyb.to(bf), du.to(bf), dzb.to(bf)]
         dz = dy + dxl
-    out = [dz]
+    out = [dz, lns]
     for g in grads:
         out += g
     return out

@@ -1162,15 +1162,22 @@ class _SampleBlockFn(torch.autograd.Function):
                 scratch.append(g)
             return g.view(-1)
 
-        ln = []
+        out = K.sb_bwd(dz2, xl, saved, ctx.params, scale, EPS)
+        # the per-sample LayerNorm affine partials (B, 4·L·C): summed into the gradients by a
+        # deferred slab reduction (the next backward kernel's appended workgroups)
+        dsts, offs = [], []
         for i in range(L):
             p = ps[SA_NP * i:SA_NP * (i + 1)]
-            ln += [target(p[0], C), target(p[1], C), target(p[6], C), target(p[7], C)]
-        out = K.sb_bwd(dz2, xl, saved, ctx.params, ln, scale, EPS)
+            for j, q in enumerate((p[0], p[1], p[6], p[7])):
+                g = _grad_of(q)
+                if g is not None:
+                    dsts.append(g.view(-1))
+                    offs.append((4 * i + j) * C)
+        defer_slab(K, out[1], dsts, offs)
         jobs = []
         for i in range(L):
             p = ps[SA_NP * i:SA_NP * (i + 1)]
-            dq, dy, du, dzz = out[1 + 4 * i:5 + 4 * i]
+            dq, dy, du, dzz = out[2 + 4 * i:6 + 4 * i]
             sv = saved[12 * i:12 * (i + 1)]
             for G, A, W, b in ((dq, sv[0], p[2], p[3]), (dy, sv[2], p[4], p[5]), (du, sv[3], p[8], p[9]),
                                (dzz, sv[5], p[10], p[11])):
