@@ -252,9 +252,11 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
   for (int li = 0; li < a.L; ++li) {
     const SBLayer& y = a.ly[li];
     const float* vec = sVec[li];
+    PIO_TS(12 * li);
     // ---- LN1 → image 0 (the QKV product's operand) ----
     float mu, rs, gv[16], bv[16], t[16];
     ln_stats<C>(x, sRed, a.eps, mu, rs);  // (its barrier also publishes the staged vectors)
+    PIO_TS(12 * li + 1);
     ld_vec(gv, vec, n0);
     ld_vec(bv, vec + C, n0);
 #pragma unroll
@@ -267,6 +269,7 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
     if (w == 0 && l < 32) { y.mean1[row] = mu; y.rstd1[row] = rs; }
     st_bf16(y.LN1X, C, row, n0, t);
     lds_sync();
+    PIO_TS(12 * li + 2);
     // ---- Q, K, V of the wave's heads ----
     float q[16], k[16], v[16];
     {
@@ -284,6 +287,7 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) v[i] = acc[i] + bb[i];
     }
+    PIO_TS(12 * li + 3);
     bf16x8 w1[KS];
     load_wtile<C>(w1, y.W1, n0);
     st_bf16(y.QKV, 3 * C, row, n0, q);
@@ -307,11 +311,13 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
           if (head_reg<C>(i, hp)) o[i] = oa[i] * inv;
       }
     }
+    PIO_TS(12 * li + 4);
     st_bf16(sImg[1], LDI, r, n0, o);
     bf16x8 w2[KS];
     load_wtile<C>(w2, y.W2, n0);
     st_bf16(y.O, C, row, n0, o);
     lds_sync();
+    PIO_TS(12 * li + 5);
     // ---- out-projection + residual → y; LN2 → image 0 ----
     float yv[16];
     {
@@ -321,16 +327,19 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) yv[i] = acc[i] + bb[i] + x[i];
     }
+    PIO_TS(12 * li + 6);
     st_f32(y.Y, C, row, n0, yv);
     ld_vec(gv, vec + 6 * C, n0);
     ld_vec(bv, vec + 7 * C, n0);
     ln_stats<C>(yv, sRed, a.eps, mu, rs);
+    PIO_TS(12 * li + 7);
 #pragma unroll
     for (int i = 0; i < 16; ++i) t[i] = (yv[i] - mu) * rs * gv[i] + bv[i];
     if (w == 0 && l < 32) { y.mean2[row] = mu; y.rstd2[row] = rs; }
     st_bf16(sImg[0], LDI, r, n0, t);
     st_bf16(y.LN2Y, C, row, n0, t);
     lds_sync();
+    PIO_TS(12 * li + 8);
     // ---- MLP: u = W1·LN2(y) + b1, GELU → image 1, z = W2·GELU(u) + b2 + y ----
     {
       float bb[16];
@@ -339,6 +348,7 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) t[i] = acc[i] + bb[i];
     }
+    PIO_TS(12 * li + 9);
     float gu[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) gu[i] = gelu_f(t[i]);
@@ -351,6 +361,7 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
     st_bf16(y.U, C, row, n0, t);
     st_bf16(y.GU, C, row, n0, gu);
     lds_sync();
+    PIO_TS(12 * li + 10);
     {
       float bb[16];
       const f32x16 acc = gemm_t<C>(w2, sImg[1], LDI);
@@ -358,6 +369,7 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) x[i] = acc[i] + bb[i] + yv[i];
     }
+    PIO_TS(12 * li + 11);
     st_f32(y.Z, C, row, n0, x);
   }
 }
@@ -427,6 +439,7 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
     const SBLayer& y = a.ly[li];
     const SBGrad& gd = a.gr[li];
     const float* X = li > 0 ? a.ly[li - 1].Z : a.X0;
+    PIO_TS(16 * li);
     // ---- the layer's first saved rows; dZ image; W2 block ----
     uint2 ur[4];
     float yv[16];
@@ -438,6 +451,7 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
     st_bf16(sImg[0], LDI, r, n0, dz);
     st_bf16(gd.dZ, C, row, n0, dz);
     lds_sync();
+    PIO_TS(16 * li + 1);
     // ---- dU = (W2ᵀ·dZ)∘GELU'(u) ----
     float t[16];
     {
@@ -447,6 +461,7 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) t[i] = acc[i] * gelu_grad(uv[i]);
     }
+    PIO_TS(16 * li + 2);
     st_bf16(sImg[1], LDI, r, n0, t);
     wblock_store<C>(sW[1], pw);
     wblock_load<C>(pw, y.Wo, 0);
@@ -461,12 +476,14 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
     const float mu1 = y.mean1[row], rs1 = y.rstd1[row];
     st_bf16(gd.dU, C, row, n0, t);
     lds_sync();
+    PIO_TS(16 * li + 3);
     // ---- dXn2 = W1ᵀ·dU; LN2 backward → dY ----
     float dy[16];
     {
       float gv[16];
       ld_vec(gv, sG[li][1], n0);
       const f32x16 acc = gemm_tt<C>(sW[1], n0, sImg[1], LDI, 0, f32x16{});
+      PIO_TS(16 * li + 4);
       float s1 = 0.f, s2 = 0.f, gg[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -481,15 +498,19 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) dy[i] = dz[i] + rs2 * (gg[i] - m1 - yv[i] * m2);
     }
+    PIO_TS(16 * li + 5);
     st_bf16(sImg[0], LDI, r, n0, dy);
     wblock_store<C>(sW[0], pw);
     wblock_load<C>(pw, y.Wqkv, 0);
     ln_affine_grads(t, yv, gd.dg2 + lnr, gd.dbe2 + lnr, n0);
+    PIO_TS(16 * li + 6);
     st_bf16(gd.dY, C, row, n0, dy);
     lds_sync();
+    PIO_TS(16 * li + 7);
     // ---- dO = Woᵀ·dY (the wave's heads) ----
     float dov[16];
     to_f(dov, gemm_tt<C>(sW[0], n0, sImg[0], LDI, 0, f32x16{}));
+    PIO_TS(16 * li + 8);
     // ---- attention backward of the wave's heads (wave-local) ----
     float gq[16], gk[16], gvv[16];
     {
@@ -542,6 +563,7 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
           if (head_reg<C>(i, hp)) { gq[i] = dq[i] * sc; gk[i] = dk[i] * sc; gvv[i] = dv[i]; }
       }
     }
+    PIO_TS(16 * li + 9);
     st_bf16(sQ, LDQ, r, n0, gq);
     st_bf16(sQ, LDQ, r, C + n0, gk);
     st_bf16(sQ, LDQ, r, 2 * C + n0, gvv);
@@ -551,15 +573,19 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
     st_bf16(gd.dQKV, 3 * C, row, C + n0, gk);
     st_bf16(gd.dQKV, 3 * C, row, 2 * C + n0, gvv);
     lds_sync();
+    PIO_TS(16 * li + 10);
     // ---- dXn1 = Wqkvᵀ·dQKV in three C-row blocks of Wqkv ----
     f32x16 acc = gemm_tt<C>(sW[1], n0, sQ, LDQ, 0, f32x16{});
+    PIO_TS(16 * li + 11);
     wblock_store<C>(sW[0], pw);
     wblock_load<C>(pw, y.Wqkv, 2 * C);
     lds_sync();
+    PIO_TS(16 * li + 12);
     acc = gemm_tt<C>(sW[0], n0, sQ, LDQ, C, acc);
     wblock_store<C>(sW[1], pw);
     if (li > 0) wblock_load<C>(pw, a.ly[li - 1].W2, 0);
     lds_sync();
+    PIO_TS(16 * li + 13);
     acc = gemm_tt<C>(sW[1], n0, sQ, LDQ, 2 * C, acc);
     // ---- LN1 backward → dX (the previous layer's dZ) ----
     {
@@ -579,7 +605,9 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) dz[i] = dy[i] + rs1 * (gg[i] - m1 - xv[i] * m2);
     }
+    PIO_TS(16 * li + 14);
     ln_affine_grads(t, xv, gd.dg1 + lnr, gd.dbe1 + lnr, n0);
+    PIO_TS(16 * li + 15);
   }
   st_f32(a.dX, C, row, n0, dz);
 }
