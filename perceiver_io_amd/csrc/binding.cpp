@@ -121,7 +121,8 @@ unsigned check_errors_mlm_head(bool);
 unsigned check_errors_ce_head(bool);
 void embed_bwd_launch(const int64_t*, const float*, float*, float*, int, int, int, float, hipStream_t);
 void embed_bwd_sorted_launch(const int64_t*, const int64_t*, const float*, float*, long long, int, float, hipStream_t);
-bool embed_bwd_local_launch(const int64_t*, const float*, float*, float*, int, int, int, float, hipStream_t);
+bool embed_bwd_local_launch(const int64_t*, const float*, float*, float*, int, int, int, float, const SlabJob&,
+                            hipStream_t);
 void text_mask_launch(const int64_t*, const bool*, int64_t*, int64_t*, int64_t*, long long, int, int, float, int,
                       uint32_t, int, hipStream_t);
 int stage_step_launch(void* const*, const void* const*, const long long*, int, float*, const float*, int, hipStream_t);
@@ -1176,16 +1177,20 @@ Tensor embed_fwd(Tensor ids, Tensor E, Tensor P, double scale) {
   return out;
 }
 
-void embed_bwd(Tensor ids, Tensor g, OptT dE, OptT dP, double scale) {
+void embed_bwd(Tensor ids, Tensor g, OptT dE, OptT dP, double scale, OptT job_slab, std::vector<Tensor> job_dsts,
+               std::vector<int64_t> job_offs) {
   TORCH_CHECK(g.is_contiguous() && ids.is_contiguous());
+  const pio::SlabJob job = make_job(job_slab, job_dsts, job_offs);
   const int B = (int)ids.size(0), L = (int)ids.size(1), C = (int)g.size(2);
   if (dE.has_value()) TORCH_CHECK(dE->is_contiguous() && dE->size(1) == C, "dE must be (V, C) contiguous");
   if (dP.has_value()) TORCH_CHECK(dP->is_contiguous() && dP->size(1) == C && dP->size(0) >= L, "dP must be (>= L, C)");
   // one launch: block-local sort + run folding for dE, batch sums for dP (C ∈ {64, 128, 256}, ids < 2^24)
   if ((!dE.has_value() || dE->size(0) < (1 << 24)) &&
       pio::embed_bwd_local_launch(ids.data_ptr<int64_t>(), f32p(g), dE.has_value() ? dE->data_ptr<float>() : nullptr,
-                                  dP.has_value() ? dP->data_ptr<float>() : nullptr, B, L, C, (float)scale, stream()))
+                                  dP.has_value() ? dP->data_ptr<float>() : nullptr, B, L, C, (float)scale, job,
+                                  stream()))
     return;
+  if (job.slab) pio::slab_reduce_launch(job, stream());  // the fallback paths carry no job
   if (dE.has_value()) {  // token-embedding rows: sort positions by id, fold equal-id runs, then add
     TORCH_CHECK(dE->is_contiguous() && dE->size(1) == C, "dE must be (V, C) contiguous");
     const bool small = dE->size(0) <= 32767;  // int16 keys: a 2-pass radix sort instead of 8
@@ -1784,7 +1789,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("accumulate"), py::arg("rowmap") = py::none(), py::arg("slab") = false, py::arg("u") = py::none(),
         py::arg("u_ml") = py::none());
   m.def("embed_fwd", &embed_fwd);
-  m.def("embed_bwd", &embed_bwd);
+  m.def("embed_bwd", &embed_bwd, py::arg("ids"), py::arg("g"), py::arg("dE"), py::arg("dP"), py::arg("scale"),
+        py::arg("job_slab") = py::none(), py::arg("job_dsts") = std::vector<Tensor>(),
+        py::arg("job_offs") = std::vector<int64_t>());
   m.def("text_mask", &text_mask, py::arg("x"), py::arg("pad"), py::arg("state"), py::arg("unk"), py::arg("mask"),
         py::arg("p"), py::arg("lo"), py::arg("hi"), py::arg("advance") = true);
   m.def("sumsq", &sumsq);

@@ -109,9 +109,14 @@ template <int C>
 __global__ __launch_bounds__(256) void embed_bwd_local_kernel(const int64_t* __restrict__ ids,
                                                               const float* __restrict__ g, float* __restrict__ dE,
                                                               float* __restrict__ dP, long long n, int nblk_e, int B,
-                                                              int L, float scale) {
+                                                              int L, float scale, int nblk_ep, SlabJob job) {
   __shared__ uint32_t sKey[ET];
+  __shared__ __attribute__((aligned(16))) float4 sPart[256];  // a deterministic slab job's partials
   const int t = threadIdx.x;
+  if ((int)blockIdx.x >= nblk_ep) {  // appended workgroups: the previous backward kernel's slab job
+    slab_reduce_block(job, blockIdx.x - nblk_ep, sPart);
+    return;
+  }
   if ((int)blockIdx.x >= nblk_e) {  // position-table gradient: block (256 / C positions, batch group)
     constexpr int TPP = C < 256 ? C : 256, PPB = 256 / TPP;
     const int nlb = (L + PPB - 1) / PPB;
@@ -361,19 +366,22 @@ void embed_bwd_launch(const int64_t* ids, const float* g, float* dE, float* dP, 
                      C, scale);
 }
 // C a multiple of 64 (≤ 256); dE and/or dP
+// + the previous backward kernel's slab job in appended workgroups (small LDS: they share the CUs
+// with the embedding blocks instead of running after them)
 bool embed_bwd_local_launch(const int64_t* ids, const float* g, float* dE, float* dP, int B, int L, int C, float scale,
-                            hipStream_t st) {
+                            const SlabJob& job, hipStream_t st) {
+  if (C != 64 && C != 128 && C != 256) return false;
   const long long n = (long long)B * L;
   const int nblk_e = dE ? (int)((n + ET - 1) / ET) : 0;
   const int ppb = 256 / (C < 256 ? C : 256);
   const int nblk_p = dP ? ((L + ppb - 1) / ppb) * ((B + EB - 1) / EB) : 0;
-  const dim3 grid(nblk_e + nblk_p);
-  if (nblk_e + nblk_p == 0) return true;
+  const int nblk_ep = nblk_e + nblk_p;
+  const dim3 grid(nblk_ep + (job.slab ? job.nblk : 0));
+  if (grid.x == 0) return true;
   switch (C) {
-    case 64: hipLaunchKernelGGL(embed_bwd_local_kernel<64>, grid, dim3(256), 0, st, ids, g, dE, dP, n, nblk_e, B, L, scale); break;
-    case 128: hipLaunchKernelGGL(embed_bwd_local_kernel<128>, grid, dim3(256), 0, st, ids, g, dE, dP, n, nblk_e, B, L, scale); break;
-    case 256: hipLaunchKernelGGL(embed_bwd_local_kernel<256>, grid, dim3(256), 0, st, ids, g, dE, dP, n, nblk_e, B, L, scale); break;
-    default: return false;
+    case 64: hipLaunchKernelGGL(embed_bwd_local_kernel<64>, grid, dim3(256), 0, st, ids, g, dE, dP, n, nblk_e, B, L, scale, nblk_ep, job); break;
+    case 128: hipLaunchKernelGGL(embed_bwd_local_kernel<128>, grid, dim3(256), 0, st, ids, g, dE, dP, n, nblk_e, B, L, scale, nblk_ep, job); break;
+    default: hipLaunchKernelGGL(embed_bwd_local_kernel<256>, grid, dim3(256), 0, st, ids, g, dE, dP, n, nblk_e, B, L, scale, nblk_ep, job); break;
   }
   return true;
 }

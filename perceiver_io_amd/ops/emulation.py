@@ -587,7 +587,8 @@ def embed_fwd(ids, E, P, scale):
     return E[ids] * scale + P[: ids.shape[1]].unsqueeze(0)
 
 
-def embed_bwd(ids, g, dE, dP, scale):
+def embed_bwd(ids, g, dE, dP, scale, job_slab=None, job_dsts=(), job_offs=()):
+    _run_job(job_slab, job_dsts, job_offs)
     C = g.shape[-1]
     if dE is not None:
         dE.index_add_(0, ids.reshape(-1), g.reshape(-1, C) * scale)

@@ -1273,7 +1273,7 @@ class _TextEmbedFn(torch.autograd.Function):
                 targets[1][: ids.shape[1]] += g.sum(0)
             return None, None, None, None
         # scatter-add straight into the (flat-buffer) gradients
-        K.embed_bwd(ids, g.contiguous(), targets[0], targets[1], ctx.scale)
+        K.embed_bwd(ids, g.contiguous(), targets[0], targets[1], ctx.scale, **_take_job())
         return None, None, None, None
 
 
