@@ -820,12 +820,6 @@ int attn_bwd_zero_plan(int B, int H, int Nq, int Nk, int D) {
   return (nkb > 1 ? 1 : 0) | (bwd_query_splits(nkb, H, B, Nq, 1) > 1 ? 2 : 0);
 }
 
-// PIO_ATTN_BWD_QR2=0 keeps the full-LDS variant on grids wider than the chip (A/B switch)
-static bool qr2_wide(const dim3& g) {
-  static const int on = [] { const char* e = getenv("PIO_ATTN_BWD_QR2"); return e == nullptr || e[0] != '0'; }();
-  return on && (long long)g.x * g.y * g.z > 256;
-}
-
 template <int D, int NW>
 static void bwd_launch_t(const AttnArgs& a, const uint16_t* dO, const float* LSE, float* delta, float* dq,
                          long long dq_bs, int dq_rs, float* dk, long long dk_bs, int dk_rs, float* dv, long long dv_bs,
@@ -858,11 +852,6 @@ static void bwd_launch_t(const AttnArgs& a, const uint16_t* dO, const float* LSE
   else if (a.Nq <= 64 && small_lds)
     hipLaunchKernelGGL((attn_bwd_kernel<D, NW, 2>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs,
                        dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs, nqs, tps);
-  else if (a.kmask == nullptr && a.Nk % (32 * NW) == 0 && qr2_wide(grid))
-    // more workgroups than CUs (the MLM encoder cross-attention: 2 key blocks × 4 heads × 64):
-    // two 32-query tiles per round (≈70 KB of LDS instead of ≈122 KB), two workgroups per CU
-    hipLaunchKernelGGL((attn_bwd_kernel<D, NW, 2, false, false>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq,
-                       dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs, nqs, tps);
   else if (a.kmask == nullptr && a.Nk % (32 * NW) == 0)
     hipLaunchKernelGGL((attn_bwd_kernel<D, NW, 0, false, false>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq,
                        dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs, nqs, tps);

@@ -130,6 +130,25 @@ __device__ __forceinline__ void ld_bf16(float (&v)[16], const uint16_t* base, lo
     v[4 * g + 2] = bf2f((uint16_t)(a.y & 0xFFFF)); v[4 * g + 3] = bf2f((uint16_t)(a.y >> 16));
   }
 }
+// whole-row copy of a staged LDS tile [32][ld] (W elements per row, 16-byte chunks) to the sample's
+// 32 global rows (row stride gld), by every thread: a T-layout store from registers (8 or 16
+// bytes per lane at a row stride) touches a cache line per lane, this one 4 lines per wave
+template <int W, typename T>
+__device__ __forceinline__ void copy_rows(T* g, long long gld, const T* img, int ld) {
+  constexpr int E = 16 / sizeof(T), CPR = W / E;
+  T* gb = g + (long long)blockIdx.x * NR * gld;
+  for (int c = threadIdx.x; c < NR * CPR; c += blockDim.x) {
+    const int rr = c / CPR, col = (c % CPR) * E;
+    *reinterpret_cast<uint4*>(gb + rr * gld + col) = *reinterpret_cast<const uint4*>(img + rr * ld + col);
+  }
+}
+// T-layout fp32 values of this lane → an LDS fp32 tile [32][ld]
+__device__ __forceinline__ void st_f32s(float* img, int ld, int r, int n0, const float (&v)[16]) {
+  const int hh = lane_id() >> 5;
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+    *reinterpret_cast<float4*>(img + r * ld + n0 + 8 * g + 4 * hh) = make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+}
 // per-channel vector (bias, γ, β) at this lane's 16 channels of tile n0 (from an LDS copy: vmcnt
 // counts loads and stores together in issue order, so a global load consumed right after a
 // phase's stores would wait for every one of them)
@@ -228,6 +247,10 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
   // [γ1 | β1 | bqkv (3C) | bo | γ2 | β2 | b1 | b2]
   constexpr int NV = 10 * C;
   __shared__ __attribute__((aligned(16))) float sVec[kSBMaxLayers][NV];
+  // staging of the saved rows for whole-row stores: QKV then U (bf16 [32][3C + 8]), Y then Z (fp32)
+  constexpr int LDS3 = 3 * C + 8, LDF = C + 4;
+  __shared__ __attribute__((aligned(16))) uint16_t sS[NR * LDS3];
+  __shared__ __attribute__((aligned(16))) float sF[NR * LDF];
   const int w = wave_id(), l = lane_id(), r = l & 31;
   const long long row = (long long)blockIdx.x * NR + r;
   const int n0 = 32 * w;  // this wave's channel tile
@@ -267,9 +290,10 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
     bf16x8 wo[KS];
     load_wtile<C>(wo, y.Wo, n0);
     if (w == 0 && l < 32) { y.mean1[row] = mu; y.rstd1[row] = rs; }
-    st_bf16(y.LN1X, C, row, n0, t);
     lds_sync();
     PIO_TS(12 * li + 2);
+    copy_rows<C>(y.LN1X, C, sImg[0], LDI);
+    if (li > 0) copy_rows<C>(a.ly[li - 1].Z, C, sF, LDF);  // the previous layer's output
     // ---- Q, K, V of the wave's heads ----
     float q[16], k[16], v[16];
     {
@@ -290,9 +314,9 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
     PIO_TS(12 * li + 3);
     bf16x8 w1[KS];
     load_wtile<C>(w1, y.W1, n0);
-    st_bf16(y.QKV, 3 * C, row, n0, q);
-    st_bf16(y.QKV, 3 * C, row, C + n0, k);
-    st_bf16(y.QKV, 3 * C, row, 2 * C + n0, v);
+    st_bf16(sS, LDS3, r, n0, q);
+    st_bf16(sS, LDS3, r, C + n0, k);
+    st_bf16(sS, LDS3, r, 2 * C + n0, v);
     // ---- attention of the wave's heads: Sᵀ = K·Qᵀ (lane = query), softmax over keys, Oᵀ = Vᵀ·Pᵀ
     // with Vᵀ read transposed from a wave-private LDS tile [key][32 channels] ----
     float o[16];
@@ -315,9 +339,10 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
     st_bf16(sImg[1], LDI, r, n0, o);
     bf16x8 w2[KS];
     load_wtile<C>(w2, y.W2, n0);
-    st_bf16(y.O, C, row, n0, o);
     lds_sync();
     PIO_TS(12 * li + 5);
+    copy_rows<3 * C>(y.QKV, 3 * C, sS, LDS3);
+    copy_rows<C>(y.O, C, sImg[1], LDI);
     // ---- out-projection + residual → y; LN2 → image 0 ----
     float yv[16];
     {
@@ -328,7 +353,7 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
       for (int i = 0; i < 16; ++i) yv[i] = acc[i] + bb[i] + x[i];
     }
     PIO_TS(12 * li + 6);
-    st_f32(y.Y, C, row, n0, yv);
+    st_f32s(sF, LDF, r, n0, yv);
     ld_vec(gv, vec + 6 * C, n0);
     ld_vec(bv, vec + 7 * C, n0);
     ln_stats<C>(yv, sRed, a.eps, mu, rs);
@@ -337,9 +362,10 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
     for (int i = 0; i < 16; ++i) t[i] = (yv[i] - mu) * rs * gv[i] + bv[i];
     if (w == 0 && l < 32) { y.mean2[row] = mu; y.rstd2[row] = rs; }
     st_bf16(sImg[0], LDI, r, n0, t);
-    st_bf16(y.LN2Y, C, row, n0, t);
     lds_sync();
     PIO_TS(12 * li + 8);
+    copy_rows<C>(y.Y, C, sF, LDF);
+    copy_rows<C>(y.LN2Y, C, sImg[0], LDI);
     // ---- MLP: u = W1·LN2(y) + b1, GELU → image 1, z = W2·GELU(u) + b2 + y ----
     {
       float bb[16];
@@ -358,10 +384,11 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
       load_wtile<C>(wq[1], a.ly[li + 1].Wqkv, C + n0);
       load_wtile<C>(wq[2], a.ly[li + 1].Wqkv, 2 * C + n0);
     }
-    st_bf16(y.U, C, row, n0, t);
-    st_bf16(y.GU, C, row, n0, gu);
+    st_bf16(sS, LDS3, r, n0, t);  // U (the QKV rows were copied out behind the last barrier)
     lds_sync();
     PIO_TS(12 * li + 10);
+    copy_rows<C>(y.U, C, sS, LDS3);
+    copy_rows<C>(y.GU, C, sImg[1], LDI);
     {
       float bb[16];
       const f32x16 acc = gemm_t<C>(w2, sImg[1], LDI);
@@ -370,8 +397,12 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
       for (int i = 0; i < 16; ++i) x[i] = acc[i] + bb[i] + yv[i];
     }
     PIO_TS(12 * li + 11);
-    st_f32(y.Z, C, row, n0, x);
+    // Z: staged (the Y rows were copied out behind the last barrier but one), copied out behind
+    // the next layer's first barrier, or here after the last layer's
+    st_f32s(sF, LDF, r, n0, x);
   }
+  lds_sync();
+  copy_rows<C>(a.ly[a.L - 1].Z, C, sF, LDF);
 }
 
 // ------------------------------------------------------------------------------------
@@ -449,9 +480,9 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
     wblock_store<C>(sW[0], pw);
     wblock_load<C>(pw, y.W1, 0);
     st_bf16(sImg[0], LDI, r, n0, dz);
-    st_bf16(gd.dZ, C, row, n0, dz);
     lds_sync();
     PIO_TS(16 * li + 1);
+    copy_rows<C>(gd.dZ, C, sImg[0], LDI);  // whole-row stores of the staged gradient rows
     // ---- dU = (W2ᵀ·dZ)∘GELU'(u) ----
     float t[16];
     {
@@ -474,9 +505,9 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
     ld_raw(orw, y.O, C, row, n0);
     ld_f32(xv, X, C, row, n0);
     const float mu1 = y.mean1[row], rs1 = y.rstd1[row];
-    st_bf16(gd.dU, C, row, n0, t);
     lds_sync();
     PIO_TS(16 * li + 3);
+    copy_rows<C>(gd.dU, C, sImg[1], LDI);
     // ---- dXn2 = W1ᵀ·dU; LN2 backward → dY ----
     float dy[16];
     {
@@ -504,9 +535,9 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
     wblock_load<C>(pw, y.Wqkv, 0);
     ln_affine_grads(t, yv, gd.dg2 + lnr, gd.dbe2 + lnr, n0);
     PIO_TS(16 * li + 6);
-    st_bf16(gd.dY, C, row, n0, dy);
     lds_sync();
     PIO_TS(16 * li + 7);
+    copy_rows<C>(gd.dY, C, sImg[0], LDI);
     // ---- dO = Woᵀ·dY (the wave's heads) ----
     float dov[16];
     to_f(dov, gemm_tt<C>(sW[0], n0, sImg[0], LDI, 0, f32x16{}));
@@ -569,11 +600,9 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
     st_bf16(sQ, LDQ, r, 2 * C + n0, gvv);
     wblock_store<C>(sW[1], pw);
     wblock_load<C>(pw, y.Wqkv, C);
-    st_bf16(gd.dQKV, 3 * C, row, n0, gq);
-    st_bf16(gd.dQKV, 3 * C, row, C + n0, gk);
-    st_bf16(gd.dQKV, 3 * C, row, 2 * C + n0, gvv);
     lds_sync();
     PIO_TS(16 * li + 10);
+    copy_rows<3 * C>(gd.dQKV, 3 * C, sQ, LDQ);
     // ---- dXn1 = Wqkvᵀ·dQKV in three C-row blocks of Wqkv ----
     f32x16 acc = gemm_tt<C>(sW[1], n0, sQ, LDQ, 0, f32x16{});
     PIO_TS(16 * li + 11);
