@@ -1,0 +1,5 @@
+# round-end evidence: bench + per-step kernel breakdown of every bench config
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+bash tools/gpu_configs.sh ${END_CONFIGS:-mlm256 seq_clf seq_clf_ft imagenet mnist long_mlm lartpc}
