@@ -48,7 +48,7 @@ struct SlabJob {
 namespace pio {
 bool sb_fwd_launch(const SBFwdArgs&, int C, hipStream_t);
 bool sb_bwd_launch(const SBBwdArgs&, int C, hipStream_t);
-bool sb_wgrad_launch(SBWgradArgs, int C, hipStream_t);
+bool sb_wgrad_launch(SBWgradArgs, int C, const SlabJob&, hipStream_t);
 bool sa_block_fwd_launch(const SABlockFwdArgs&, hipStream_t);
 unsigned persist_errors(bool);
 int persist_sync_words(int);
@@ -579,6 +579,8 @@ std::vector<Tensor> sa_block_fwd(Tensor qkv0, Tensor x0, int64_t N, double scale
 
 unsigned persist_errors(bool reset) { return pio::persist_errors(reset); }
 
+pio::SlabJob make_job(const OptT& slab, std::vector<Tensor>& dsts, const std::vector<int64_t>& offs);
+
 // ---- per-sample latent-block kernels (csrc/sample_block.hip): C ∈ {64, 128}, H = 4, N = 32 ----
 namespace {
 constexpr int kSBN = 32;
@@ -693,8 +695,9 @@ std::vector<Tensor> sb_bwd(Tensor dz, Tensor x0, std::vector<Tensor> saved, std:
 }
 
 // grouped weight gradients of a block: jobs = [G (R, N) bf16, A (R, C) bf16, dW (N, C) fp32,
-// db (N) fp32] × n (added to dW / db); one C for every job
-void sb_wgrad(std::vector<Tensor> jobs) {
+// db (N) fp32] × n (added to dW / db); one C for every job.  job_slab / job_dsts / job_offs: a
+// slab reduction run by appended workgroups (the block's LayerNorm partials from sb_bwd)
+void sb_wgrad(std::vector<Tensor> jobs, OptT job_slab, std::vector<Tensor> job_dsts, std::vector<int64_t> job_offs) {
   TORCH_CHECK(jobs.size() % 4 == 0 && !jobs.empty() && (int)jobs.size() / 4 <= pio::kSBMaxJobs, "sb_wgrad: 1..16 jobs");
   pio::SBWgradArgs a{};
   a.njobs = (int)jobs.size() / 4;
@@ -714,7 +717,7 @@ void sb_wgrad(std::vector<Tensor> jobs) {
     CHECK_DT(db, torch::kFloat32);
     a.job[j] = pio::SBWgradJob{bfp(G), bfp(A), dW.data_ptr<float>(), db.data_ptr<float>(), N, 0};
   }
-  TORCH_CHECK(pio::sb_wgrad_launch(a, C, stream()), "sb_wgrad: launch refused");
+  TORCH_CHECK(pio::sb_wgrad_launch(a, C, make_job(job_slab, job_dsts, job_offs), stream()), "sb_wgrad: launch refused");
 }
 
 // workgroups of a non-deterministic SlabJob (128 measured best on the MLM step: 96–128 ≈ equal,
@@ -1748,7 +1751,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sb_fwd", &sb_fwd, py::arg("x"), py::arg("params"), py::arg("scale"), py::arg("eps"));
   m.def("sb_bwd", &sb_bwd, py::arg("dz"), py::arg("x0"), py::arg("saved"), py::arg("params"),
         py::arg("scale"), py::arg("eps"));
-  m.def("sb_wgrad", &sb_wgrad, py::arg("jobs"));
+  m.def("sb_wgrad", &sb_wgrad, py::arg("jobs"), py::arg("job_slab") = py::none(),
+        py::arg("job_dsts") = std::vector<Tensor>(), py::arg("job_offs") = std::vector<int64_t>());
   m.def("post_attn_ln_linear_fwd", &post_attn_ln_linear_fwd, py::arg("o"), py::arg("x"), py::arg("wo"), py::arg("bo"),
         py::arg("g2"), py::arg("be2"), py::arg("eps"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("b2"),
         py::arg("lnw"), py::arg("lnb"), py::arg("wq"), py::arg("bq"), py::arg("seed") = py::none(),

@@ -649,10 +649,14 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
 // LDS (G tile [32][64], A tile [32][C]) with the next 32 register-prefetched.
 // ------------------------------------------------------------------------------------
 template <int C>
-__global__ __launch_bounds__(256) void sb_wgrad_kernel(SBWgradArgs a) {
+__global__ __launch_bounds__(256) void sb_wgrad_kernel(SBWgradArgs a, SlabJob sj, int tiles) {
   constexpr int LG = 64 + 8, LA = C + 8, TT = C / 64, AC = C / 64;  // A chunks (16 B) per thread
   __shared__ __attribute__((aligned(16))) uint16_t sG[2][NR * LG];
   __shared__ __attribute__((aligned(16))) uint16_t sA[2][NR * LA];
+  if ((int)blockIdx.x >= tiles) {  // appended (row split 0 only): the block's LayerNorm partial slab
+    if (blockIdx.y == 0) slab_reduce_block(sj, blockIdx.x - tiles, reinterpret_cast<float4*>(&sG[0][0]));
+    return;
+  }
   const int w = wave_id(), l = lane_id();
   int j = 0;
   while (j + 1 < a.njobs && (int)blockIdx.x >= a.job[j + 1].tile0) ++j;
@@ -725,7 +729,8 @@ bool sb_bwd_launch(const SBBwdArgs& a, int C, hipStream_t st) {
   return true;
 }
 // rows per split: about 512 rows per workgroup (≥ 1 split; a multiple of 32)
-bool sb_wgrad_launch(SBWgradArgs a, int C, hipStream_t st) {
+// sj: a slab reduction (the sample-block backward's LayerNorm partials) run by appended workgroups
+bool sb_wgrad_launch(SBWgradArgs a, int C, const SlabJob& sj, hipStream_t st) {
   if (a.njobs < 1 || a.njobs > kSBMaxJobs || a.R % sb::NR != 0 || (C != 64 && C != 128)) return false;
   int tiles = 0;
   for (int j = 0; j < a.njobs; ++j) {
@@ -736,8 +741,9 @@ bool sb_wgrad_launch(SBWgradArgs a, int C, hipStream_t st) {
   int splits = (a.R + 511) / 512;
   a.rows_per_split = (a.R / sb::NR + splits - 1) / splits * sb::NR;
   splits = (a.R + a.rows_per_split - 1) / a.rows_per_split;
-  if (C == 128) hipLaunchKernelGGL(sb::sb_wgrad_kernel<128>, dim3(tiles, splits), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(sb::sb_wgrad_kernel<64>, dim3(tiles, splits), dim3(256), 0, st, a);
+  const dim3 grid(tiles + (sj.slab ? sj.nblk : 0), splits);
+  if (C == 128) hipLaunchKernelGGL(sb::sb_wgrad_kernel<128>, grid, dim3(256), 0, st, a, sj, tiles);
+  else hipLaunchKernelGGL(sb::sb_wgrad_kernel<64>, grid, dim3(256), 0, st, a, sj, tiles);
   return true;
 }
 

@@ -840,7 +840,8 @@ def sb_bwd(dz, x0, saved, params, scale, eps):
     return out
 
 
-def sb_wgrad(jobs):
+def sb_wgrad(jobs, job_slab=None, job_dsts=(), job_offs=()):
+    _run_job(job_slab, job_dsts, job_offs)
     for j in range(0, len(jobs), 4):
         G, A, dW, db = jobs[j:j + 4]
         Gf = G.float()

@@ -1163,8 +1163,8 @@ class _SampleBlockFn(torch.autograd.Function):
             return g.view(-1)
 
         out = K.sb_bwd(dz2, xl, saved, ctx.params, scale, EPS)
-        # the per-sample LayerNorm affine partials (B, 4·L·C): summed into the gradients by a
-        # deferred slab reduction (the next backward kernel's appended workgroups)
+        # the per-sample LayerNorm affine partials (B, 4·L·C): summed into the gradients by the
+        # grouped weight-gradient launch's appended workgroups (or a deferred slab reduction)
         dsts, offs = [], []
         for i in range(L):
             p = ps[SA_NP * i:SA_NP * (i + 1)]
@@ -1173,7 +1173,6 @@ class _SampleBlockFn(torch.autograd.Function):
                 if g is not None:
                     dsts.append(g.view(-1))
                     offs.append((4 * i + j) * C)
-        defer_slab(K, out[1], dsts, offs)
         jobs = []
         for i in range(L):
             p = ps[SA_NP * i:SA_NP * (i + 1)]
@@ -1184,7 +1183,9 @@ class _SampleBlockFn(torch.autograd.Function):
                 if W.requires_grad or b.requires_grad:
                     jobs += [G, A, target(W, W.numel()), target(b, b.numel())]
         if jobs:
-            K.sb_wgrad(jobs)
+            K.sb_wgrad(jobs, job_slab=out[1] if dsts else None, job_dsts=dsts, job_offs=offs)
+        else:
+            defer_slab(K, out[1], dsts, offs)
         return (None, None, out[0].view(B, N, C)) + (None,) * len(ps)
 
 
