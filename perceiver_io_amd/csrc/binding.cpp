@@ -579,7 +579,9 @@ std::vector<Tensor> sa_block_fwd(Tensor qkv0, Tensor x0, int64_t N, double scale
 
 unsigned persist_errors(bool reset) { return pio::persist_errors(reset); }
 
+namespace {
 pio::SlabJob make_job(const OptT& slab, std::vector<Tensor>& dsts, const std::vector<int64_t>& offs);
+}  // namespace
 
 // ---- per-sample latent-block kernels (csrc/sample_block.hip): C ∈ {64, 128}, H = 4, N = 32 ----
 namespace {

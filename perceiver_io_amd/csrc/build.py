@@ -102,13 +102,17 @@ def build(force: bool = False, jobs: int = 0, debug: bool = False, verbose: bool
         with ThreadPoolExecutor(max_workers=n) as ex:
             list(ex.map(_run, todo))
     out = ext_path(name)
-    link = ["g++", "-shared", *(["-fsanitize=undefined"] if check else []), "-o", str(out), str(bobj),
+    # linked to a temporary name and renamed into place: a snapshot of the tree taken during a
+    # build sees the previous or the new library, never a partly written one
+    tmp = out.with_name(out.name + ".partial")
+    link = ["g++", "-shared", *(["-fsanitize=undefined"] if check else []), "-o", str(tmp), str(bobj),
             *map(str, objs), f"-L{libdir}", "-L/opt/rocm/lib",
             "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lamdhip64", "-lc10_hip", "-ltorch_hip",
             f"-Wl,-rpath,{libdir}", "-Wl,-rpath,/opt/rocm/lib"]
     newest = max(p.stat().st_mtime for p in objs + [bobj])
     if force or todo or not out.exists() or out.stat().st_mtime < newest:
         _run(link)
+        os.replace(tmp, out)
         if verbose:
             print(f"[perceiver_io_amd] linked {out.relative_to(PKG.parent)}")
     keep = {p.name for p in objs + [bobj]}
