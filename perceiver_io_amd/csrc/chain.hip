@@ -604,12 +604,6 @@ bool sa_layer_fwd_chain_launch(const uint16_t* QKV, int N, float scale_log2, uin
   return true;
 }
 
-// PIO_SLAB_XCD=0 keeps the dispatch-order row splits (A/B switch)
-static bool slab_xcd_local() {
-  static const int on = [] { const char* e = getenv("PIO_SLAB_XCD"); return e == nullptr || e[0] != '0'; }();
-  return on != 0;
-}
-
 bool ln_linear_post_attn_bwd_chain_launch(const void* G, bool g_bf16, const uint16_t* Wq, const float* X, const float* mean1,
                                           const float* rstd1, const float* lnw, const float* lnb, const float* dres,
                                           float* dlnw, float* dlnb, float* dWq, float* dbq, const float* Ysave,
@@ -619,23 +613,11 @@ bool ln_linear_post_attn_bwd_chain_launch(const void* G, bool g_bf16, const uint
                                           const PostAttnGrads& grads, int R, const SlabJob& job, const DropCfg& dr,
                                           int nq, hipStream_t st) {
   if (nq != 192 && nq != 64) return false;
-  // a non-deterministic job from a 1-D producer: XCD-local row ranges (common.h kSlabXcdLocal),
-  // 8 XCDs × column blocks × row splits appended workgroups
-  const int ntiles = (R + 63) / 64;
-  SlabJob jb = job;
-  if (jb.slab != nullptr && jb.det == 0 && slab_xcd_local()) {
-    jb.det = kSlabXcdLocal;
-    const int per_xcd = (jb.S + 7) / 8;
-    int nsy = std::max(1, std::min(per_xcd, 128 / std::max(1, jb.nbx)));
-    const int rb = (per_xcd + nsy - 1) / nsy;
-    nsy = (per_xcd + rb - 1) / rb;
-    jb.nblk = 8 * jb.nbx * nsy;
-  }
-  dim3 grid(ntiles + (jb.slab ? jb.nblk : 0));
+  dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0));
 #define LPC(NQ, TG)                                                                                                    \
   hipLaunchKernelGGL((ln_linear_post_attn_bwd_chain8_kernel<NQ, TG>), grid, dim3(512), 0, st, static_cast<const TG*>(G), \
                      Wq, X, mean1, rstd1, lnw, lnb, dres, dlnw, dlnb, dWq, dbq, Ysave, mean2, rstd2, U, O, Wo, W1, W2,    \
-                     g2, be2, dY, dO, delta, grads, R, jb, dr)
+                     g2, be2, dY, dO, delta, grads, R, job, dr)
   if (g_bf16) {
     if (nq != 192) return false;  // bf16 G only from the self-attention backward (nq = 3C)
     LPC(3, uint16_t);

@@ -281,8 +281,7 @@ __device__ __forceinline__ void lds_sync() {
 struct SlabJob {
   const float* slab;  // nullptr: no job
   int S, P, nbx, nblk;
-  int det;            // 1: deterministic mode (one block per column range sums ALL rows, plain add);
-                      // 2: XCD-local row ranges (kSlabXcdLocal, set by a 1-D carrier's launcher)
+  int det;            // deterministic mode: one block per column range sums ALL rows, plain add
   int n;
   float* dst[kMaxSlabSegs];
   int off[kMaxSlabSegs];
@@ -310,24 +309,12 @@ __device__ __forceinline__ void zero_span_block(const SlabJob& j) {
 // Deterministic mode: one workgroup per column block sums all S rows in a fixed order and
 // adds once (single writer).
 constexpr int kSlabColsPerBlock = 1024;
-// det == 2: the slab's rows were stored by a 1-D grid of S workgroups in xcd_remap order (row t by
-// a workgroup on XCD x when t lies in x's contiguous xcd_remap range), and the carrier appends
-// its job workgroups to a 1-D grid, so appended workgroup b runs on XCD (blockIdx.x mod 8): it
-// sums the column block of its work item over the rows of its own XCD — L2 hits instead of
-// cross-XCD reads — and adds them atomically (8 · row-split partials per column).  A slab from
-// another producer layout is still summed exactly once (only the locality is lost).
-constexpr int kSlabXcdLocal = 2;
-__host__ __device__ inline void slab_xcd_rows(int S, int x, int& start, int& cnt) {
-  const int q = S / 8, r = S % 8;
-  start = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
-  cnt = q + (x < r ? 1 : 0);
-}
 // part: ≥ 4 KiB of 16-B aligned LDS (deterministic path).  The job runs on the first 256
 // threads of the carrier's workgroup (256 or 512 threads; the others only join the barrier).
 __device__ __forceinline__ void slab_reduce_block(const SlabJob& j, int b, float4* part) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int P = j.P;
-  if (j.det == 1) {  // fixed summation order, a single writer per element: bitwise reproducible
+  if (j.det) {  // fixed summation order, a single writer per element: bitwise reproducible
     const int cb = b * 256, c = cb + 4 * l;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     if (c < P && w < 4)
@@ -349,23 +336,10 @@ __device__ __forceinline__ void slab_reduce_block(const SlabJob& j, int b, float
     return;
   }
   if (threadIdx.x >= 256) return;
-  int bx, s0, s1;
-  if (j.det == kSlabXcdLocal) {  // work item k = b / 8 on this workgroup's XCD
-    const int x = (int)(blockIdx.x & 7), k = b / 8, nsy = j.nblk / (8 * j.nbx);
-    bx = k % j.nbx;
-    const int sy = k / j.nbx;
-    int start, cnt;
-    slab_xcd_rows(j.S, x, start, cnt);
-    const int rb = (cnt + nsy - 1) / nsy;
-    s0 = start + sy * rb;
-    s1 = min(start + cnt, s0 + rb);
-  } else {
-    const int nsy = j.nblk / j.nbx, rb = (j.S + nsy - 1) / nsy;
-    bx = b % j.nbx;
-    s0 = (b / j.nbx) * rb;
-    s1 = min(j.S, s0 + rb);
-  }
+  const int nsy = j.nblk / j.nbx, rb = (j.S + nsy - 1) / nsy;
+  const int bx = b % j.nbx, by = b / j.nbx;
   const int c = bx * kSlabColsPerBlock + 4 * (int)threadIdx.x;
+  const int s0 = by * rb, s1 = min(j.S, s0 + rb);
   const bool cin = c < P;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int s = s0; s < s1; s += 16) {
