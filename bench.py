@@ -425,6 +425,13 @@ def main(argv=None):
         sys.stdout.flush()
         os.dup2(json_fd, 1)
         print(json.dumps(out), flush=True)
+    # captured step graphs (with their in-graph collectives) go before the communicator does
+    engine = None
+    if cuda:
+        import gc
+
+        gc.collect()
+        torch.cuda.synchronize()
     if reducer is not None:
         reducer.close()
     pdist.shutdown()

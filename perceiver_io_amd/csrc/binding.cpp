@@ -724,7 +724,13 @@ void sb_wgrad(std::vector<Tensor> jobs, OptT job_slab, std::vector<Tensor> job_d
 
 // workgroups of a non-deterministic SlabJob (128 measured best on the MLM step: 96–128 ≈ equal,
 // 256 and 64 slower)
-int slab_job_target() { return 128; }
+int slab_job_target() {  // PIO_SLAB_TARGET: A/B knob for the appended reduction's width
+  static const int t = [] {
+    const char* e = getenv("PIO_SLAB_TARGET");
+    return e ? std::max(1, atoi(e)) : 128;
+  }();
+  return t;
+}
 
 // the backward entry points below ACCUMULATE parameter gradients into caller-provided fp32
 // tensors (normally views of the flat gradient buffer) with device atomics: no partial slabs,
@@ -1567,7 +1573,8 @@ int64_t attn_bwd_pe_part_rows(int64_t M, int64_t H, int64_t B, int64_t bsplit) {
 
 static void attn_bwd_pe_impl(Tensor q, const Tensor* kv, Tensor dO, Tensor lse, Tensor delta, const Tensor* mean,
                              const Tensor* rstd, Tensor pix, Tensor dq, Tensor D, Tensor part, int64_t H, double scale,
-                             bool accumulate, int64_t bsplit, const PeImplicit* impl, bool dq_zeroed = false) {
+                             bool accumulate, int64_t bsplit, const PeImplicit* impl, bool dq_zeroed = false,
+                             bool d_zeroed = false) {
   for (const Tensor* t : {&q, &dO, &lse, &delta, &pix, &dq, &D, &part}) CHECK_CUDA(*t);
   const int C = (int)(H * 32);
   TORCH_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.size(2) >= C, "q must be (B|1, Nq, >= C) with unit inner stride");
@@ -1639,7 +1646,8 @@ static void attn_bwd_pe_impl(Tensor q, const Tensor* kv, Tensor dO, Tensor lse, 
   a.B = B; a.H = (int)H; a.Nq = Nq; a.M = M; a.C = C; a.nc = nc;
   a.scale = (float)scale; a.scale_log2 = (float)(scale * 1.4426950408889634);
   a.accumulate = accumulate ? 1 : 0;
-  if (bsplit > 1 && !accumulate) D.zero_();  // atomics add onto it
+  // the split batch groups add into D atomically; d_zeroed: cleared by the preceding kernel's zero span
+  if (bsplit > 1 && !accumulate && !d_zeroed) D.zero_();
   Tensor dside, spair;
   if (slots > 0) {
     dside = torch::empty({slots, 256, 64}, D.options());
@@ -1652,17 +1660,19 @@ static void attn_bwd_pe_impl(Tensor q, const Tensor* kv, Tensor dO, Tensor lse, 
 }
 
 void attn_bwd_pe(Tensor q, Tensor kv, Tensor dO, Tensor lse, Tensor delta, Tensor mean, Tensor rstd, Tensor pix,
-                 Tensor dq, Tensor D, Tensor part, int64_t H, double scale, bool accumulate, int64_t bsplit) {
-  attn_bwd_pe_impl(q, &kv, dO, lse, delta, &mean, &rstd, pix, dq, D, part, H, scale, accumulate, bsplit, nullptr);
+                 Tensor dq, Tensor D, Tensor part, int64_t H, double scale, bool accumulate, int64_t bsplit,
+                 bool dq_zeroed, bool d_zeroed) {
+  attn_bwd_pe_impl(q, &kv, dO, lse, delta, &mean, &rstd, pix, dq, D, part, H, scale, accumulate, bsplit, nullptr,
+                   dq_zeroed, d_zeroed);
 }
 
 // the same over implicit K/V (attention_pe.hip pe_kv_elem): no (B·M, 2C) K/V tensor, no row statistics
 void attn_bwd_pe_implicit(Tensor q, Tensor P, Tensor pes, Tensor pesq, Tensor wt, Tensor dO, Tensor lse, Tensor delta,
                           Tensor pix, Tensor dq, Tensor D, Tensor part, int64_t H, double scale, int64_t kin, double eps,
-                          bool accumulate, int64_t bsplit, bool dq_zeroed) {
+                          bool accumulate, int64_t bsplit, bool dq_zeroed, bool d_zeroed) {
   PeImplicit im{P, pes, pesq, wt, (double)kin, eps};
   attn_bwd_pe_impl(q, nullptr, dO, lse, delta, nullptr, nullptr, pix, dq, D, part, H, scale, accumulate, bsplit, &im,
-                   dq_zeroed);
+                   dq_zeroed, d_zeroed);
 }
 
 // encoder cross-attention forward over implicit K/V (attention_pe.hip attn_fwd_pe_kernel): queries
@@ -1815,13 +1825,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_bwd_pe_implicit", &attn_bwd_pe_implicit, py::arg("q"), py::arg("P"), py::arg("pes"), py::arg("pesq"),
         py::arg("wt"), py::arg("dO"), py::arg("lse"), py::arg("delta"), py::arg("pix"), py::arg("dq"), py::arg("D"),
         py::arg("part"), py::arg("H"), py::arg("scale"), py::arg("kin"), py::arg("eps"), py::arg("accumulate"),
-        py::arg("bsplit"), py::arg("dq_zeroed") = false);
+        py::arg("bsplit"), py::arg("dq_zeroed") = false, py::arg("d_zeroed") = false);
   m.def("pe_weight_prep", &pe_weight_prep, py::arg("W"), py::arg("g"), py::arg("b"), py::arg("bias"), py::arg("nc"),
         py::arg("Kp"), py::arg("W2") = py::none());
   m.def("pe_grads", &pe_grads);
   m.def("pe_proj_bwd", &pe_proj_bwd);
   m.def("attn_bwd_pe", &attn_bwd_pe, py::arg("q"), py::arg("kv"), py::arg("dO"), py::arg("lse"), py::arg("delta"),
         py::arg("mean"), py::arg("rstd"), py::arg("pix"), py::arg("dq"), py::arg("D"), py::arg("part"), py::arg("H"),
-        py::arg("scale"), py::arg("accumulate"), py::arg("bsplit"));
+        py::arg("scale"), py::arg("accumulate"), py::arg("bsplit"), py::arg("dq_zeroed") = false,
+        py::arg("d_zeroed") = false);
   m.attr("arch") = "gfx950";
 }

@@ -335,11 +335,16 @@ __device__ __forceinline__ void slab_reduce_block(const SlabJob& j, int b, float
     }
     return;
   }
-  if (threadIdx.x >= 256) return;
+  // a 512-thread carrier (the chain backward) splits the block's rows between its two halves:
+  // twice the loads in flight per CU, the halves combined through LDS before the atomics
+  const bool two = blockDim.x >= 512;
+  const int t = threadIdx.x & 255, h = threadIdx.x >> 8;
+  if (h > (two ? 1 : 0)) return;
   const int nsy = j.nblk / j.nbx, rb = (j.S + nsy - 1) / nsy;
   const int bx = b % j.nbx, by = b / j.nbx;
-  const int c = bx * kSlabColsPerBlock + 4 * (int)threadIdx.x;
-  const int s0 = by * rb, s1 = min(j.S, s0 + rb);
+  const int c = bx * kSlabColsPerBlock + 4 * t;
+  const int r0 = by * rb, r1 = min(j.S, r0 + rb), rm = two ? r0 + (r1 - r0 + 1) / 2 : r1;
+  const int s0 = h ? rm : r0, s1 = h ? r1 : rm;
   const bool cin = c < P;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int s = s0; s < s1; s += 16) {
@@ -353,6 +358,13 @@ __device__ __forceinline__ void slab_reduce_block(const SlabJob& j, int b, float
     for (int i = 0; i < 16; ++i) {
       acc.x += v[i].x; acc.y += v[i].y; acc.z += v[i].z; acc.w += v[i].w;
     }
+  }
+  if (two) {
+    if (h) part[t] = acc;
+    __syncthreads();
+    if (h) return;
+    const float4 o = part[t];
+    acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
   }
   if (!cin) return;
   const float a4[4] = {acc.x, acc.y, acc.z, acc.w};

@@ -195,7 +195,7 @@ def attn_fwd_pe(q, P, pix, pes, pesq, wt, H, scale, kin, eps, nsplit):
 
 
 def attn_bwd_pe_implicit(q, P, pes, pesq, wt, dO, lse, delta, pix, dq, D, part, H, scale, kin, eps, accumulate, bsplit,
-                         dq_zeroed=False):
+                         dq_zeroed=False, d_zeroed=False):
     """attn_bwd_pe over implicit K/V (the same generation as attn_fwd_pe)."""
     kv, mu, rs = pe_kv(P, pix, pes, pesq, wt, kin, eps)
     attn_bwd_pe(q, kv, dO, lse, delta, mu, rs, pix, dq, D, part, H, scale, accumulate, bsplit)
@@ -206,7 +206,8 @@ def attn_bwd_pe_part_rows(M, H, B, bsplit):
     return ((M + 255) // 256) * bsplit
 
 
-def attn_bwd_pe(q, kv, dO, lse, delta, mean, rstd, pix, dq, D, part, H, scale, accumulate, bsplit):
+def attn_bwd_pe(q, kv, dO, lse, delta, mean, rstd, pix, dq, D, part, H, scale, accumulate, bsplit, dq_zeroed=False,
+                d_zeroed=False):
     """csrc/attention_pe.hip: encoder cross-attention backward whose dK/dV are folded into the
     factored projection's reductions D = Σ_b dY·rσ and [Σ dY | Σ dY·μ·rσ | Σ dY·x̂_c] (one
     partial row here; the kernel writes one per (key block, batch group)).  q is batch-broadcast

@@ -112,10 +112,21 @@ def _flush_pending():
                 K.slab_reduce(t, ds, os_)
 
 
-def flush_pending():
+def flush_pending(stream=None):
     """Launch every deferred slab reduction now (e.g. before a gradient bucket that depends on
-    them is all-reduced mid-backward, parallel/reducer.py)."""
-    _flush_pending()
+    them is all-reduced mid-backward, parallel/reducer.py).  ``stream``: run them there instead
+    (the caller has made it wait for the producing stream; the slabs are recorded on it so the
+    allocator keeps them until it is done) — the reducer's side stream, which is the only
+    consumer of a completed bucket, so the main chain does not carry the reductions."""
+    if stream is None:
+        _flush_pending()
+        return
+    _flush_queued[0] = False
+    with torch.cuda.stream(stream):
+        while _pending:
+            K, t, ds, os_, _ = _pending.pop(0)
+            t.record_stream(stream)
+            K.slab_reduce(t, ds, os_)
 
 
 def defer_slab(K, t: torch.Tensor, dsts, offs):
@@ -621,13 +632,24 @@ class _LayerFn(torch.autograd.Function):
 
         pe_fused = spec.cross and bool(ctx.kv_entry.get("factored") and PE_ATTN_FUSED and D == 32 and Nq <= 32
                                        and kmask is None and ctx.p_attn == 0.0 and xkv2.shape[1] <= 4)
-        dq_pre = None
+        dq_pre, d_pre = None, None
         if spec.cross and not deterministic():
             # the attention backward's atomically accumulated dQ, cleared by the post-attention
             # backward on the way (no fill launch); broadcast latent queries on the fused PE path
             # come back summed over the batch
-            dq_pre = torch.empty((Bq if pe_fused else B, Nq, C), **f32)
-            drop["zero_out"] = dq_pre
+            nq = (Bq if pe_fused else B) * Nq * C
+            ent = ctx.kv_entry
+            imp = ent.get("implicit")
+            pm = imp[1].shape[0] if imp is not None else kv.shape[0] // B
+            if pe_fused and ent.get("pe_D") is None and pe_attn_bsplit(B, pm, H) > 1:
+                # the first application's factored reduction D (M, 2C), which the split batch
+                # groups add into atomically, shares the span: [dQ | D] in one buffer
+                zbuf = torch.empty(nq + pm * 2 * C, **f32)
+                d_pre = zbuf[nq:].view(pm, 2 * C)
+            else:
+                zbuf = torch.empty(nq, **f32)
+            dq_pre = zbuf[:nq].view(-1, Nq, C)
+            drop["zero_out"] = zbuf
         ho, _LOOKAHEAD["bwd"] = _LOOKAHEAD["bwd"], None
         if ho is not None and ho["key"] != getattr(ctx, "lookahead_z", None):
             raise RuntimeError("fused encoder: a self-attention block handed its LN1/QKV backward to the wrong "
@@ -662,7 +684,7 @@ class _LayerFn(torch.autograd.Function):
                 acc = ent.get("pe_D") is not None
                 if not acc:
                     bs = pe_attn_bsplit(B, M, H)
-                    ent["pe_D"] = torch.empty((M, 2 * C), **f32)
+                    ent["pe_D"] = d_pre if d_pre is not None else torch.empty((M, 2 * C), **f32)
                     prows = (K.attn_bwd_pe_part_rows(M, H, B, bs) if hasattr(K, "attn_bwd_pe_part_rows")
                              else ((M + 255) // 256) * bs)
                     ent["pe_part"] = torch.empty((prows, (2 + xkv2.shape[1]) * 2 * C), **f32)
@@ -673,10 +695,11 @@ class _LayerFn(torch.autograd.Function):
                     P, pes, pesq, wt, kin = imp
                     K.attn_bwd_pe_implicit(qx, P, pes, pesq, wt, do.view(B, Nq, C), lse, delta3, xkv2, dq, ent["pe_D"],
                                            ent["pe_part"], H, scale, kin, EPS, acc, ent["pe_bsplit"],
-                                           dq_zeroed=dq_pre is not None)
+                                           dq_zeroed=dq_pre is not None, d_zeroed=d_pre is not None)
                 else:
                     K.attn_bwd_pe(qx, kv, do.view(B, Nq, C), lse, delta3, mean_kv, rstd_kv, xkv2, dq, ent["pe_D"],
-                                  ent["pe_part"], H, scale, acc, ent["pe_bsplit"])
+                                  ent["pe_part"], H, scale, acc, ent["pe_bsplit"], dq_zeroed=dq_pre is not None,
+                                  d_zeroed=d_pre is not None)
             else:
                 # dK/dV of every application of this layer land in one buffer (K-06); the first
                 # writer stores, later ones accumulate

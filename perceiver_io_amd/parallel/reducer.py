@@ -309,19 +309,25 @@ class FlatGradReducer:
         :meth:`FusedAdamW.range_update`); None detaches."""
         self.updater = fn
 
-    def _launch(self, bucket: int):
+    def _launch(self, bucket: int, flush: bool = False):
         if _capturing(self.flat.device) and not self.in_graph:
             raise RuntimeError("FlatGradReducer: a collective inside a hipGraph capture on a node where the "
                                "collectives are not capturable (in_graph=False)")
         self._counts[bucket] += 1
         lo, hi = self.buckets[bucket]
+        from ..ops.fused import flush_pending
+
         if self._side is not None:
             self._side.wait_stream(torch.cuda.current_stream(self.flat.device))
+            if flush:  # the covered kernels' deferred slab reductions, ahead of the collective
+                flush_pending(self._side)
             with torch.cuda.stream(self._side):
                 self._reduce(lo, hi)
                 if self.updater is not None:
                     self.updater(lo, hi)
         else:
+            if flush:
+                flush_pending()
             self._reduce(lo, hi)
             if self.updater is not None:
                 self.updater(lo, hi)
@@ -333,12 +339,11 @@ class FlatGradReducer:
         i = self.points[name]
         if self._counts[i]:
             raise RuntimeError(f"FlatGradReducer: ready point {name!r} reached twice in one backward")
-        from ..ops.fused import flush_pending
-
-        flush_pending()  # deferred weight-gradient slab reductions of the covered kernels
         self.early_launches += 1
         self.launch_log.append(name)
-        self._launch(i)
+        # the deferred weight-gradient slab reductions of the covered kernels run first, on the
+        # side stream (the bucket's only consumer) when there is one
+        self._launch(i, flush=True)
 
     def finish(self):
         """All remaining buckets, then join the side stream; every bucket exactly once."""
