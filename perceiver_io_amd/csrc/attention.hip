@@ -375,14 +375,17 @@ __global__ void attn_bwd_prep_kernel(const uint16_t* __restrict__ dO, const uint
 // them as bf16 MFMA operands anyway (the chain-layout layer-boundary backward)
 // KM = false: no key padding mask and every key of the grid's blocks exists (Nk a multiple of the
 // block's keys): no per-element masking select in the softmax
-template <int D, int NW, int QR = 0, bool OBF = false, bool KM = true>
-__global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uint16_t* __restrict__ dO,
+// DRP = false: no attention-probability dropout compiled in (host-checked), for the register
+// budget of the slab-carrying variant (≤ 128 VGPRs: two 8-wave workgroups per CU)
+template <int D, int NW, int QR = 0, bool OBF = false, bool KM = true, bool DRP = true>
+__global__ __launch_bounds__(64 * NW, (QR == 2 && OBF && !DRP) ? 4 : 1) void attn_bwd_kernel(AttnArgs a, const uint16_t* __restrict__ dO,
                                                            const float* __restrict__ LSE,
                                                            const float* __restrict__ delta, float* __restrict__ dq,
                                                            long long dq_bs, int dq_rs, float* __restrict__ dk,
                                                            long long dk_bs, int dk_rs, float* __restrict__ dv,
                                                            long long dv_bs, int dv_rs, int dq_atomic, int kv_acc,
-                                                           long long dq_kbs, int nqs, int q_tiles_per_split) {
+                                                           long long dq_kbs, int nqs, int q_tiles_per_split,
+                                                           SlabJob job) {
   constexpr int LD = (D < 32 ? 32 : D) + 8;  // Q / dO / K tiles [row][d] (D=16 zero-padded to 32 cols)
   constexpr int NT = (D < 32) ? 1 : D / 32;
   constexpr int KS = D / 16;
@@ -404,9 +407,15 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
   __shared__ __attribute__((aligned(16))) float sDl[NQS * 32];
 
   PIO_WG_BEGIN();
+  if ((int)blockIdx.z >= a.B) {  // z-slices past the batch: the previous kernel's slab job
+    const int jb = ((blockIdx.z - a.B) * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    if (jb < job.nblk) slab_reduce_block(job, jb, reinterpret_cast<float4*>(sdS));
+    PIO_WG_END();
+    return;
+  }
   PIO_TS(0);
   const int w = wave_id(), l = lane_id(), r = l & 31, hh = l >> 5;
-  const Blk3 blk = xcd_block3();  // the heads / key blocks of one batch element share an L2
+  const Blk3 blk = xcd_block3(a.B);  // the heads / key blocks of one batch element share an L2
   const int h = blk.y, b = blk.z;
   // blk.x = key block × nqs + query split: many-query / few-key shapes (a decoder's pixel or
   // token queries over a few dozen latents) split the query range across workgroups, whose
@@ -416,7 +425,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
   dq += (long long)kblk * dq_kbs;  // deterministic mode: one dQ partial slice per key block
   const int key = kbase + 32 * w + r;  // this lane's key (column of S / dP)
   const int kc = key < a.Nk ? key : a.Nk - 1;
-  const uint32_t dkey = a.drop_thresh ? drop_key(a.seedp, a.site, 2u) : 0u;
+  const uint32_t dkey = DRP && a.drop_thresh ? drop_key(a.seedp, a.site, 2u) : 0u;
   const bool kin = key < a.Nk;
   bool kpad = false;
   if constexpr (KM) {
@@ -529,14 +538,30 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
       // LSE / delta of this lane's accumulator rows (registers 4g..4g+3 = tile rows
       // 8g + 4hh + 0..3): 8 vector LDS reads, then a branch-free element loop (a per-element
       // condition around an LDS read serialises the loop on LDS latency)
-      f32x4 lrow[4], drow[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        lrow[g] = *reinterpret_cast<const f32x4*>(sL + j * 32 + 8 * g + 4 * hh);
-        drow[g] = *reinterpret_cast<const f32x4*>(sDl + j * 32 + 8 * g + 4 * hh);
-      }
       f32x16 P, dS;
-      if (!a.drop_thresh) {
+      if constexpr (!DRP) {  // register budget: the delta rows are read once P is formed
+        f32x4 lr[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) lr[g] = *reinterpret_cast<const f32x4*>(sL + j * 32 + 8 * g + 4 * hh);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) P[i] = fast_exp2(kpad ? -INFINITY : S[i] * a.scale_log2 - lr[i >> 2][i & 3]);
+        asm volatile("" ::: "memory");
+        f32x4 dr[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) dr[g] = *reinterpret_cast<const f32x4*>(sDl + j * 32 + 8 * g + 4 * hh);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dS[i] = P[i] * (dP[i] - dr[i >> 2][i & 3]);
+      }
+      f32x4 lrow[4], drow[4];
+      if constexpr (DRP) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          lrow[g] = *reinterpret_cast<const f32x4*>(sL + j * 32 + 8 * g + 4 * hh);
+          drow[g] = *reinterpret_cast<const f32x4*>(sDl + j * 32 + 8 * g + 4 * hh);
+        }
+      }
+      if (!DRP) {
+      } else if (!a.drop_thresh) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const float p = fast_exp2(kpad ? -INFINITY : S[i] * a.scale_log2 - lrow[i >> 2][i & 3]);
@@ -584,12 +609,12 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a, const uin
     lds_sync();
     PIO_TS(4 + 4 * ((qt0 - qt_begin) / NQS));
     // dQ of tile j = w: Σ over the block's keys of dS[key][q] · K[key][d]
-    if constexpr (D == 16 && NW == 8 && NQS == 4) {
-      // head width 16: every wave takes 16 queries (tile w & 3, half w >> 2) × the 16 head dims
-      // with 16x16x32 MFMAs over the KB keys — no idle waves, and none of the 32x32 tile's
-      // padding columns (the 32x32x16 form below computes 32 dims of which 16 are real)
-      const int j = w & 3, mh = w >> 2, g = l >> 4;
-      if (qt0 + j < nqt) {
+    if constexpr (D == 16 && NW == 8 && (NQS == 4 || NQS == 2)) {
+      // head width 16: a wave takes 16 queries (tile w % NQS, half w / NQS) × the 16 head dims
+      // with 16x16x32 MFMAs over the KB keys — none of the 32x32 tile's padding columns (the
+      // 32x32x16 form below computes 32 dims of which 16 are real); NQS = 4 leaves no wave idle
+      const int j = w % NQS, mh = w / NQS, g = l >> 4;
+      if (mh < 2 && qt0 + j < nqt) {
         const uint16_t* tS = sdS + j * KB * LDS_;
         f32x4 a0 = f32x4{0.f, 0.f, 0.f, 0.f}, a1 = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -848,17 +873,19 @@ static void bwd_launch_t(const AttnArgs& a, const uint16_t* dO, const float* LSE
   // share a CU
   if (a.Nq <= 32 && small_lds)
     hipLaunchKernelGGL((attn_bwd_kernel<D, NW, 1>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs,
-                       dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs, nqs, tps);
+                       dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs, nqs, tps, SlabJob{});
   else if (a.Nq <= 64 && small_lds)
     hipLaunchKernelGGL((attn_bwd_kernel<D, NW, 2>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs,
-                       dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs, nqs, tps);
+                       dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs, nqs, tps, SlabJob{});
   else if (a.kmask == nullptr && a.Nk % (32 * NW) == 0)
     hipLaunchKernelGGL((attn_bwd_kernel<D, NW, 0, false, false>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq,
-                       dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs, nqs, tps);
+                       dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs, nqs, tps, SlabJob{});
   else
     hipLaunchKernelGGL((attn_bwd_kernel<D, NW>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs, dk,
-                       dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs, nqs, tps);
+                       dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs, nqs, tps, SlabJob{});
 }
+
+void slab_reduce_launch(const SlabJob& job, hipStream_t st);  // elementwise.hip
 
 // key blocks of the backward grid (dQ partial slices in deterministic mode)
 int attn_bwd_key_blocks(int Nk, int D) {
@@ -894,19 +921,25 @@ void attn_bwd_launch(const AttnArgs& a, int D, const uint16_t* O, const uint16_t
 bool attn_bwd_bf16_ok(const AttnArgs& a, int D) {
   return D == 16 && a.Nk <= 32 * 8 && a.Nq > 64 && bwd_query_splits(1, a.H, a.B, a.Nq, 1) == 1;
 }
+// job: the previous kernel's slab reduction in z-slices appended past the batch.  Carrying one,
+// the two-query-tile variant runs (≈ 70 KB of LDS: two workgroups per CU), so the reduction
+// shares the CUs with the attention tiles instead of queueing behind a one-per-CU carrier's tiles.
 bool attn_bwd_bf16_launch(const AttnArgs& a, int D, const uint16_t* dO, const float* LSE, const float* delta,
                           uint16_t* dq, long long dq_bs, int dq_rs, uint16_t* dk, long long dk_bs, int dk_rs,
-                          uint16_t* dv, long long dv_bs, int dv_rs, hipStream_t st) {
+                          uint16_t* dv, long long dv_bs, int dv_rs, const SlabJob& job, hipStream_t st) {
   if (!attn_bwd_bf16_ok(a, D)) return false;
   const int nqt = (a.Nq + 31) / 32;
-  dim3 grid(1, a.H, a.B);
-#define BF16L(KM_)                                                                                                  \
-  hipLaunchKernelGGL((attn_bwd_kernel<16, 8, 0, true, KM_>), grid, dim3(512), 0, st, a, dO, LSE, delta,             \
+  const bool carry = job.slab != nullptr && job.nblk > 0 && a.kmask == nullptr && a.Nk == 256 && !a.drop_thresh;
+  dim3 grid(1, a.H, a.B + (carry ? (job.nblk + a.H - 1) / a.H : 0));
+#define BF16L(QR_, KM_, J_)                                                                                         \
+  hipLaunchKernelGGL((attn_bwd_kernel<16, 8, QR_, true, KM_, QR_ == 0>), grid, dim3(512), 0, st, a, dO, LSE, delta,           \
                      reinterpret_cast<float*>(dq), dq_bs, dq_rs, reinterpret_cast<float*>(dk), dk_bs, dk_rs,         \
-                     reinterpret_cast<float*>(dv), dv_bs, dv_rs, 0, 0, 0LL, 1, nqt)
-  if (a.kmask == nullptr && a.Nk == 256) BF16L(false);
-  else BF16L(true);
+                     reinterpret_cast<float*>(dv), dv_bs, dv_rs, 0, 0, 0LL, 1, nqt, J_)
+  if (carry) BF16L(2, false, job);
+  else if (a.kmask == nullptr && a.Nk == 256) BF16L(0, false, SlabJob{});
+  else BF16L(0, true, SlabJob{});
 #undef BF16L
+  if (job.slab != nullptr && !carry) slab_reduce_launch(job, st);
   return true;
 }
 

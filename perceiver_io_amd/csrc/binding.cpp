@@ -62,7 +62,7 @@ void attn_bwd_launch(const AttnArgs&, int, const uint16_t*, const uint16_t*, con
 int attn_bwd_key_blocks(int, int);
 bool attn_bwd_bf16_ok(const AttnArgs&, int);
 bool attn_bwd_bf16_launch(const AttnArgs&, int, const uint16_t*, const float*, const float*, uint16_t*, long long, int,
-                          uint16_t*, long long, int, uint16_t*, long long, int, hipStream_t);
+                          uint16_t*, long long, int, uint16_t*, long long, int, const SlabJob&, hipStream_t);
 int attn_bwd_zero_plan(int, int, int, int, int);
 void ln_linear_fwd_launch(const void*, bool, int, int, int, const float*, const float*, float, const uint16_t*, int,
                           const float*, int, int, const float*, int, void*, bool, int, float*, float*, const float*, int,
@@ -287,6 +287,10 @@ std::vector<Tensor> attn_fwd(Tensor q, Tensor k, Tensor v, OptT kmask, int64_t H
 }
 
 // returns (dq, dk, dv) fp32; dq is per batch even when q is batch-broadcast.  Optional
+namespace {
+pio::SlabJob make_job(const OptT& slab, std::vector<Tensor>& dsts, const std::vector<int64_t>& offs);
+}  // namespace
+
 // *_out tensors (B, N, >=HD views, unit inner stride) let the results land in packed buffers;
 // a dq_out view must be batch-dense (batch stride == Nq * row stride); it needs no zero fill
 // (the launcher clears it itself when several key blocks accumulate into it).  delta_in ((B, Nq, H) fp32 rowsum(dO∘O), e.g. from post_attn_bwd)
@@ -294,8 +298,11 @@ std::vector<Tensor> attn_fwd(Tensor q, Tensor k, Tensor v, OptT kmask, int64_t H
 std::vector<Tensor> attn_bwd(Tensor q, Tensor k, Tensor v, OptT kmask, Tensor o, Tensor dO, Tensor lse, OptT delta_in,
                              int64_t H, int64_t D, double scale, double dropout_p, OptT seed, OptT dq_out,
                              OptT dk_out, OptT dv_out, bool kv_accumulate, int64_t site, bool dq_zeroed,
-                             bool kv_zeroed) {
+                             bool kv_zeroed, OptT job_slab, std::vector<Tensor> job_dsts, std::vector<int64_t> job_offs) {
   auto a = make_args(q, k, v, kmask, (int)H, (int)D, scale, dropout_p, seed, site);
+  // job (optional): the previous kernel's slab reduction, carried by the bf16 variant (else a
+  // standalone launch first)
+  const pio::SlabJob job = make_job(job_slab, job_dsts, job_offs);
   TORCH_CHECK(dO.is_contiguous() && o.is_contiguous(), "O / dO must be contiguous (B, Nq, H*D)");
   auto f32 = q.options().dtype(torch::kFloat32);
   if (dq_out.has_value() && dq_out->scalar_type() == torch::kBFloat16) {
@@ -312,14 +319,17 @@ std::vector<Tensor> attn_bwd(Tensor q, Tensor k, Tensor v, OptT kmask, Tensor o,
     if (pio::attn_bwd_bf16_ok(a, (int)D)) {
       pio::attn_bwd_bf16_launch(a, (int)D, bfp(dO), f32p(lse), delta.data_ptr<float>(), bfp_mut(dq), dq.stride(0),
                                 (int)dq.stride(1), bfp_mut(dk), dk.stride(0), (int)dk.stride(1), bfp_mut(dv),
-                                dv.stride(0), (int)dv.stride(1), stream());
+                                dv.stride(0), (int)dv.stride(1), job, stream());
     } else {  // shape not covered by the bf16 variant: fp32, then narrowed
+      if (job.slab) pio::slab_reduce_launch(job, stream());
+      std::vector<Tensor> nd;
       auto r = attn_bwd(q, k, v, kmask, o, dO, lse, delta_in, H, D, scale, dropout_p, seed, c10::nullopt, c10::nullopt,
-                        c10::nullopt, false, site, false, false);
+                        c10::nullopt, false, site, false, false, c10::nullopt, nd, {});
       dq.copy_(r[0]); dk.copy_(r[1]); dv.copy_(r[2]);
     }
     return {dq, dk, dv};
   }
+  if (job.slab) pio::slab_reduce_launch(job, stream());
   Tensor dq = dq_out.has_value() ? *dq_out : torch::empty({a.B, a.Nq, H * D}, f32);
   Tensor dk = dk_out.has_value() ? *dk_out : torch::empty({a.B, a.Nk, H * D}, f32);
   Tensor dv = dv_out.has_value() ? *dv_out : torch::empty({a.B, a.Nk, H * D}, f32);
@@ -1742,7 +1752,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_bwd", &attn_bwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("kmask"), py::arg("o"), py::arg("dO"),
         py::arg("lse"), py::arg("delta_in"), py::arg("H"), py::arg("D"), py::arg("scale"), py::arg("dropout_p"),
         py::arg("seed"), py::arg("dq_out"), py::arg("dk_out"), py::arg("dv_out"), py::arg("kv_accumulate") = false,
-        py::arg("site") = 0, py::arg("dq_zeroed") = false, py::arg("kv_zeroed") = false);
+        py::arg("site") = 0, py::arg("dq_zeroed") = false, py::arg("kv_zeroed") = false,
+        py::arg("job_slab") = py::none(), py::arg("job_dsts") = std::vector<Tensor>{},
+        py::arg("job_offs") = std::vector<int64_t>{});
   m.def("attn_bwd_zero_plan", &pio::attn_bwd_zero_plan, py::arg("B"), py::arg("H"), py::arg("Nq"), py::arg("Nk"),
         py::arg("D"));
   m.def("ln_linear_fwd", &ln_linear_fwd, py::arg("x"), py::arg("lnw"), py::arg("lnb"), py::arg("eps"), py::arg("w"),

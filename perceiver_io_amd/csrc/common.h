@@ -309,8 +309,11 @@ __device__ __forceinline__ void zero_span_block(const SlabJob& j) {
 // Deterministic mode: one workgroup per column block sums all S rows in a fixed order and
 // adds once (single writer).
 constexpr int kSlabColsPerBlock = 1024;
-// part: ≥ 4 KiB of 16-B aligned LDS (deterministic path).  The job runs on the first 256
-// threads of the carrier's workgroup (256 or 512 threads; the others only join the barrier).
+// part: ≥ 4 KiB of 16-B aligned LDS.  Deterministic mode runs on the first 256 threads of the
+// carrier's workgroup (the others only join the barrier); the other mode splits the rows between
+// the two halves of a 512-thread carrier.  NV: row loads in flight per thread (a one-workgroup-
+// per-CU carrier has the registers for the whole share of its rows at once).
+template <int NV = 16>
 __device__ __forceinline__ void slab_reduce_block(const SlabJob& j, int b, float4* part) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int P = j.P;
@@ -347,15 +350,15 @@ __device__ __forceinline__ void slab_reduce_block(const SlabJob& j, int b, float
   const int s0 = h ? rm : r0, s1 = h ? r1 : rm;
   const bool cin = c < P;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int s = s0; s < s1; s += 16) {
-    float4 v[16];
+  for (int s = s0; s < s1; s += NV) {
+    float4 v[NV];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {  // address selects: rows past s1 / columns past P read zeros
+    for (int i = 0; i < NV; ++i) {  // address selects: rows past s1 / columns past P read zeros
       const bool ok = cin && s + i < s1;
       v[i] = *reinterpret_cast<const float4*>(ok ? j.slab + (long long)(s + i) * P + c : kZero32B);
     }
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
+    for (int i = 0; i < NV; ++i) {
       acc.x += v[i].x; acc.y += v[i].y; acc.z += v[i].z; acc.w += v[i].w;
     }
   }

@@ -332,7 +332,8 @@ def attn_fwd(q, k, v, kmask, H, D, scale, dropout_p, seed, nsplit, site=0):
 
 
 def attn_bwd(q, k, v, kmask, o, dO, lse, delta_in, H, D, scale, dropout_p, seed, dq_out, dk_out, dv_out,
-             kv_accumulate=False, site=0, dq_zeroed=False, kv_zeroed=False):
+             kv_accumulate=False, site=0, dq_zeroed=False, kv_zeroed=False, job_slab=None, job_dsts=(), job_offs=()):
+    _run_job(job_slab, job_dsts, job_offs)
     B, qf, kf, vf = _qkv(q, k, v, H, D)
     s = _scores(qf, kf, kmask, scale)
     l2 = lse.permute(0, 2, 1)  # (B, H, Nq)

@@ -41,12 +41,14 @@ from . import emulation, ext
 from ..parallel.reducer import bucket_ready_point
 
 EPS = 1e-5
-# per-tile weight-gradient partials go to a slab reduced on a side stream (see _GradSlab);
-# PERCEIVER_WGRAD_SLAB=0 restores in-kernel float atomics into the replicated accumulators
+# per-tile weight-gradient partials go to a slab whose reduction rides the next backward kernel
+# (see _GradSlab); False: in-kernel float atomics into the replicated accumulators
 WGRAD_SLAB = True
-# self-attention dQKV stored as bf16 for the chain-layout boundary kernel (identical results);
-# PERCEIVER_BF16_DQKV=0 keeps it fp32 (A/B)
+# self-attention dQKV stored as bf16 for the chain-layout boundary kernel (identical results)
 BF16_DQKV = True
+# the bf16 self-attention backward carries the pending slab reduction (PIO_ATTN_SLAB=0: the next
+# chain kernel does, A/B)
+ATTN_SLAB = os.environ.get("PIO_ATTN_SLAB", "1") != "0"
 TALL_ROWS = 1 << 17  # kTallRows in csrc/binding.cpp: taller projections stream their dW (wgrad kernel)
 
 
@@ -1001,7 +1003,9 @@ class _SABlockFn(torch.autograd.Function):
                   and 64 < N <= 256)
 
         def new_dqkv(i):  # every column block is written (or accumulated onto a cleared buffer) by attn_bwd
-            if g_bf16 and i > 0:
+            # layer 0's dQKV goes to the producing cross-attention layer's chain kernel when there
+            # is a hand-off (bf16 operand too), else to ln_linear_bwd (fp32)
+            if g_bf16 and (i > 0 or getattr(ctx, "handoff", None) is not None):
                 return torch.empty((B, N, 3 * C), device=dz.device, dtype=torch.bfloat16), {}
             t_ = torch.empty((B, N, 3 * C), **f32)
             return t_, (dict(zero_out=t_) if zp else {})
@@ -1030,9 +1034,12 @@ class _SABlockFn(torch.autograd.Function):
             xl, qkv, mean1, rstd1, o, lse, y, m2, r2, u = S[i]
             qkv3 = qkv.view(B, N, 3 * C)
             dqkv = dqkv_next
+            # the bf16 variant carries the previous kernel's slab reduction on the CUs it shares with
+            # its tiles (two workgroups per CU); the chain kernel after it then carries none
             K.attn_bwd(qkv3[:, :, :C], qkv3[:, :, C:2 * C], qkv3[:, :, 2 * C:], None, o, do.view(B, N, C), lse,
                        delta.view(B, N, H), H, D, scale, ctx.p, ctx.seed, dqkv[:, :, :C], dqkv[:, :, C:2 * C],
-                       dqkv[:, :, 2 * C:], site=i, dq_zeroed=bool(zp & 1), kv_zeroed=bool(zp & 2))
+                       dqkv[:, :, 2 * C:], site=i, dq_zeroed=bool(zp & 1), kv_zeroed=bool(zp & 2),
+                       **(_take_job() if ATTN_SLAB and dqkv.dtype == torch.bfloat16 else {}))
             if i > 0:
                 dqkv_next, zkw = new_dqkv(i - 1)
                 sl = _GradSlab(R, LL_SIZES(C) + PA_SIZES(C), dz2)
