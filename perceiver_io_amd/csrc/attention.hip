@@ -378,7 +378,7 @@ __global__ void attn_bwd_prep_kernel(const uint16_t* __restrict__ dO, const uint
 // DRP = false: no attention-probability dropout compiled in (host-checked), for the register
 // budget of the slab-carrying variant (≤ 128 VGPRs: two 8-wave workgroups per CU)
 template <int D, int NW, int QR = 0, bool OBF = false, bool KM = true, bool DRP = true>
-__global__ __launch_bounds__(64 * NW, (QR == 2 && OBF && !DRP) ? 4 : 1) void attn_bwd_kernel(AttnArgs a, const uint16_t* __restrict__ dO,
+__global__ __launch_bounds__(64 * NW, (QR == 2 && !DRP) ? 4 : 1) void attn_bwd_kernel(AttnArgs a, const uint16_t* __restrict__ dO,
                                                            const float* __restrict__ LSE,
                                                            const float* __restrict__ delta, float* __restrict__ dq,
                                                            long long dq_bs, int dq_rs, float* __restrict__ dk,
@@ -869,6 +869,23 @@ static void bwd_launch_t(const AttnArgs& a, const uint16_t* dO, const float* LSE
   }
   dim3 grid(nkb * nqs, a.H, a.B);
   constexpr bool small_lds = true;
+  // head width 16, no dropout, a grid wider than the chip: the two-query-tile variant at ≤ 128
+  // VGPRs runs two 8-wave workgroups per CU (PIO_ATTN_QR2W=0: the full-LDS variant, A/B)
+  static const bool qr2w = [] {
+    const char* e = getenv("PIO_ATTN_QR2W");
+    return !(e && e[0] == '0');
+  }();
+  const bool wide = D == 16 && NW == 8 && qr2w && !a.drop_thresh && a.Nq > 64 &&
+                    (long long)grid.x * grid.y * grid.z > 256;
+  if (wide) {
+    if (a.kmask == nullptr && a.Nk % (32 * NW) == 0)
+      hipLaunchKernelGGL((attn_bwd_kernel<D, NW, 2, false, false, false>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta,
+                         dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs, nqs, tps, SlabJob{});
+    else
+      hipLaunchKernelGGL((attn_bwd_kernel<D, NW, 2, false, true, false>), grid, dim3(64 * NW), 0, st, a, dO, LSE, delta,
+                         dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, atomic, kv_acc, dq_kbs, nqs, tps, SlabJob{});
+    return;
+  }
   // ≤ 64 queries (few-query cross-attention): the small-LDS variants let several workgroups
   // share a CU
   if (a.Nq <= 32 && small_lds)
