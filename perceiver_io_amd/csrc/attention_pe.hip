@@ -792,7 +792,9 @@ __global__ __launch_bounds__(512) void attn_bwd_pe_fact_kernel(PeBwdArgs a) {
     // ---- per-sample register staging: fetch() only issues loads (clamped addresses)
     bf16x4 st_v = bf16x4{0, 0, 0, 0};
     float st_ld = 0.f;
-    float px[NC], pxn[NC];
+    float px[NC];  // the current sample's pixels of this lane's key; refilled with the next
+                   // sample's once consumed (no second register set: no loop-carried copy of a
+                   // load still in flight, whose wait would drain every memory operation)
     // per-thread sample-0 addresses + wave-uniform per-sample strides (scalar multiplies)
     const int wten = __builtin_amdgcn_readfirstlane(st_ten);
     const uint16_t* st_src = wten == 0 ? a.q + (long long)st_rowc * a.q_rs + h * PD + st_c
@@ -845,22 +847,26 @@ __global__ __launch_bounds__(512) void attn_bwd_pe_fact_kernel(PeBwdArgs a) {
     f32x16 accQ;     // dQ Σ over the batch (broadcast queries): rows = query, columns = d
     accD[0] = accD[1] = accX[0] = accX[1] = accQ = f32x16{};
 
-    if (b0 < b1) {
-      fetch(b0);
-      fetch_px(b0, px);
-      stage(b0 & 1);
-      if (b0 + 1 < b1) {
-        fetch(b0 + 1);
-        fetch_px(b0 + 1, pxn);
+    // sample order b0 .. b1 - 1 (a workgroup-staggered start was measured: no change,
+    // profiles/r5_ab/README.md)
+    const int nb = b1 - b0;
+    auto perm = [&](int j) { return b0 + j; };
+    if (nb > 0) {
+      fetch(perm(0));
+      fetch_px(perm(0), px);
+      stage(0);
+      if (nb > 1) {
+        fetch(perm(1));
       }
     }
     lds_barrier();
 
     // Σ over the waves of sample bb's dQ partials (threads < 256: d = t >> 3, queries 4·(t & 7) .. +3)
-    auto dq_reduce = [&](int bb) {
+    auto dq_reduce = [&](int jj) {  // jj: position in the sample order
       if (threadIdx.x >= 256) return;
+      const int bb = perm(jj);
       const int dd = threadIdx.x >> 3, q0 = 4 * (threadIdx.x & 7);
-      const float(*src)[32 * 36] = reinterpret_cast<const float(*)[32 * 36]>(&sDQb[QB ? (bb & 1) : 0][0][0]);
+      const float(*src)[32 * 36] = reinterpret_cast<const float(*)[32 * 36]>(&sDQb[QB ? (jj & 1) : 0][0][0]);
       f32x4 v = *reinterpret_cast<const f32x4*>(&src[0][dd * 36 + q0]);
 #pragma unroll
       for (int ww = 1; ww < NW; ++ww) v += *reinterpret_cast<const f32x4*>(&src[ww][dd * 36 + q0]);
@@ -874,9 +880,9 @@ __global__ __launch_bounds__(512) void attn_bwd_pe_fact_kernel(PeBwdArgs a) {
       }
     };
 
-    auto body = [&](int b, auto masked_t) {
+    auto body = [&](int jb, auto masked_t) {  // jb: position in the sample order
       constexpr bool MK = decltype(masked_t)::value;
-      const int cur = b & 1;
+      const int cur = jb & 1;
       // (0) statistics of key `key` for sample b → a, W, rσ rows (wave-private) and the key-side
       // augmentation operand of S / dP
       float sm = pes, sq = pesq;
@@ -907,19 +913,15 @@ __global__ __launch_bounds__(512) void attn_bwd_pe_fact_kernel(PeBwdArgs a) {
         for (int j = 0; j < NC + 1; ++j) kaug[j] = row[j];
         *reinterpret_cast<bf16x8*>(&sA[w][r * 16]) = row;
       }
-      // pixels of sample b + 1 move up; loads of b + 2 are issued after the staging below
-#pragma unroll
-      for (int c = 0; c < NC; ++c) px[c] = pxn[c];
-      // (1) sample b+1 → LDS (its loads were issued one iteration ago), loads of b+2
-      if (b + 1 < b1) {
+      // this lane's pixels are consumed: the next sample's
+      if (jb + 1 < nb) fetch_px(perm(jb + 1), px);
+      // (1) the next sample → LDS (its loads were issued one iteration ago), loads of the one after
+      if (jb + 1 < nb) {
         stage(cur ^ 1);
-        if (b + 2 < b1) {
-          fetch(b + 2);
-          fetch_px(b + 2, pxn);
-        }
+        if (jb + 2 < nb) fetch(perm(jb + 2));
       }
       if constexpr (QB) {
-        if (b > b0) dq_reduce(b - 1);  // written last iteration, before its barrier
+        if (jb > 0) dq_reduce(jb - 1);  // written last iteration, before its barrier
       }
       // (2) S and dP: rows = queries, lane = key
       const uint16_t* tQ = sQ[QB ? cur : 0];
@@ -1001,12 +1003,12 @@ __global__ __launch_bounds__(512) void attn_bwd_pe_fact_kernel(PeBwdArgs a) {
       lds_barrier();
     };
     if (masked) {  // two loops: one register assignment each (no copies at a merged loop head)
-      for (int b = b0; b < b1; ++b) body(b, std::true_type{});
+      for (int jb = 0; jb < nb; ++jb) body(jb, std::true_type{});
     } else {
-      for (int b = b0; b < b1; ++b) body(b, std::false_type{});
+      for (int jb = 0; jb < nb; ++jb) body(jb, std::false_type{});
     }
     if constexpr (QB) {
-      if (b1 > b0) dq_reduce(b1 - 1);  // the last sample's partials (after its barrier)
+      if (nb > 0) dq_reduce(nb - 1);  // the last sample's partials (after its barrier)
     }
 
     // ---- D rows of this wave's keys (K part columns 32h + r, V part C + 32h + r)
