@@ -634,10 +634,41 @@ void sb_fill_saved(pio::SBLayer& y, const std::vector<Tensor>& sv, int i, int R,
 }
 }  // namespace
 
+// the pre stage's 10 tensors: [O (R, C) bf16, x_q (R, C) or (32, C) fp32, wo_bf16, bo, g2, be2,
+// w1_bf16, b1, w2_bf16, b2]
+namespace {
+void sb_fill_pre(pio::SBLayer& y, const std::vector<Tensor>& pre, int C) {
+  sb_check_w(pre[2], C, C, "pre Wo"); sb_check_v(pre[3], C, "pre bo"); sb_check_v(pre[4], C, "pre γ2");
+  sb_check_v(pre[5], C, "pre β2"); sb_check_w(pre[6], C, C, "pre W1"); sb_check_v(pre[7], C, "pre b1");
+  sb_check_w(pre[8], C, C, "pre W2"); sb_check_v(pre[9], C, "pre b2");
+  y.Wo = bfp(pre[2]); y.bo = f32p(pre[3]); y.g2 = f32p(pre[4]); y.be2 = f32p(pre[5]);
+  y.W1 = bfp(pre[6]); y.b1 = f32p(pre[7]); y.W2 = bfp(pre[8]); y.b2 = f32p(pre[9]);
+}
+constexpr int kSBPreSaved = 6;  // LN2Y U GU (bf16) Y mean2 rstd2 (fp32)
+void sb_fill_pre_saved(pio::SBLayer& y, const std::vector<Tensor>& sv, int R, int C) {
+  TORCH_CHECK((int)sv.size() == kSBPreSaved, "sample block: 6 saved pre-stage tensors");
+  for (int k = 0; k < kSBPreSaved; ++k) {
+    const int64_t want = k < 4 ? (int64_t)R * C : R;
+    TORCH_CHECK(sv[k].is_contiguous() && sv[k].numel() == want &&
+                    sv[k].scalar_type() == (k < 3 ? torch::kBFloat16 : torch::kFloat32),
+                "sample block: saved pre-stage tensor ", k, " has the wrong shape / dtype");
+  }
+  y.LN2Y = reinterpret_cast<uint16_t*>(sv[0].data_ptr()); y.U = reinterpret_cast<uint16_t*>(sv[1].data_ptr());
+  y.GU = reinterpret_cast<uint16_t*>(sv[2].data_ptr()); y.Y = sv[3].data_ptr<float>();
+  y.mean2 = sv[4].data_ptr<float>(); y.rstd2 = sv[5].data_ptr<float>();
+}
+void sb_check_pre_o(const Tensor& o, int R, int C) {
+  TORCH_CHECK(o.is_contiguous() && o.dim() == 2 && o.size(0) == R && o.size(1) == C && o.scalar_type() == torch::kBFloat16 &&
+                  (reinterpret_cast<uintptr_t>(o.data_ptr()) & 15) == 0,
+              "sample block: pre O must be (B·32, C) contiguous bf16");
+}
+}  // namespace
+
 // forward of a whole block, one workgroup per sample: x (B·32, C) fp32 → per layer
 // [LN1X, QKV, O, LN2Y, U, GU (bf16), Y, Z, mean1, rstd1, mean2, rstd2 (fp32)]; the block output is
-// the last layer's Z
-std::vector<Tensor> sb_fwd(Tensor x, std::vector<Tensor> params, double scale, double eps) {
+// the last layer's Z.  pre (10 tensors, see sb_fill_pre): the cross layer's post-attention half
+// runs first and WRITES x (its output, the block input); its 6 saved tensors are appended.
+std::vector<Tensor> sb_fwd(Tensor x, std::vector<Tensor> params, double scale, double eps, std::vector<Tensor> pre) {
   const int C = x.dim() == 2 ? (int)x.size(1) : 0;
   TORCH_CHECK(x.is_contiguous() && (C == 64 || C == 128) && x.size(0) % kSBN == 0 && x.size(0) > 0,
               "sb_fwd: x (B·32, C), C ∈ {64, 128}");
@@ -660,6 +691,24 @@ std::vector<Tensor> sb_fwd(Tensor x, std::vector<Tensor> params, double scale, d
     out.insert(out.end(), sv.begin(), sv.end());
     sb_fill_saved(a.ly[i], out, i, R, C);
   }
+  if (!pre.empty()) {
+    TORCH_CHECK(pre.size() == 10, "sb_fwd: pre = [O, x_q, wo, bo, g2, be2, w1, b1, w2, b2]");
+    sb_check_pre_o(pre[0], R, C);
+    const Tensor& xq = pre[1];
+    TORCH_CHECK(xq.is_contiguous() && xq.dim() == 2 && xq.size(1) == C && (xq.size(0) == R || xq.size(0) == kSBN) &&
+                    xq.scalar_type() == torch::kFloat32,
+                "sb_fwd: pre x_q must be (B·32, C) or broadcast (32, C) fp32");
+    sb_fill_pre(a.pre, pre, C);
+    std::vector<Tensor> sv{torch::empty({R, C}, b16), torch::empty({R, C}, b16), torch::empty({R, C}, b16),
+                           torch::empty({R, C}, f32), torch::empty({R}, f32), torch::empty({R}, f32)};
+    sb_fill_pre_saved(a.pre, sv, R, C);
+    a.pre.Z = x.data_ptr<float>();
+    a.preO = bfp(pre[0]);
+    a.preX = f32p(xq);
+    a.preX_bs = xq.size(0) == R ? kSBN : 0;
+    a.has_pre = 1;
+    out.insert(out.end(), sv.begin(), sv.end());
+  }
   TORCH_CHECK(pio::sb_fwd_launch(a, C, stream()), "sb_fwd: launch refused");
   return out;
 }
@@ -668,8 +717,13 @@ std::vector<Tensor> sb_fwd(Tensor x, std::vector<Tensor> params, double scale, d
 // as sb_fwd's.  Returns [dx, the (B, 4·L·C) fp32 LayerNorm partial slab (row b: sample b's
 // [dγ1 | dβ1 | dγ2 | dβ2] of layer 0, then layer 1, …; sum the rows into the gradients), then per
 // layer the gradient rows dQKV, dY, dU, dZ (bf16)] for sb_wgrad
+// pre (as sb_fwd's, x_q unused) + pre_saved (sb_fwd's 6 appended tensors): the cross layer's
+// post-attention backward runs last; dx is then the gradient of its residual input x_q, and
+// [dO (R, C) bf16, δ (R, 4) fp32, dY, dU, dZ (bf16 rows)] are appended; the LayerNorm slab rows
+// are 2C wider (the pre stage's dγ2 | dβ2 last).  zero_out: an fp32 buffer of 4k elements the
+// kernel clears (the cross attention backward's accumulators)
 std::vector<Tensor> sb_bwd(Tensor dz, Tensor x0, std::vector<Tensor> saved, std::vector<Tensor> params, double scale,
-                           double eps) {
+                           double eps, std::vector<Tensor> pre, std::vector<Tensor> pre_saved, OptT zero_out) {
   const int C = x0.dim() == 2 ? (int)x0.size(1) : 0;
   TORCH_CHECK(dz.is_contiguous() && x0.is_contiguous() && dz.sizes() == x0.sizes() && (C == 64 || C == 128) &&
                   x0.size(0) % kSBN == 0 && x0.size(0) > 0,
@@ -687,8 +741,9 @@ std::vector<Tensor> sb_bwd(Tensor dz, Tensor x0, std::vector<Tensor> saved, std:
   a.eps = (float)eps;
   Tensor dx = torch::empty({R, C}, f32);
   a.dX = dx.data_ptr<float>();
-  Tensor lns = torch::empty({(int64_t)a.B, (int64_t)4 * L * C}, f32);  // every element stored by the kernel
-  a.ln_rs = 4 * L * C;
+  const bool hp = !pre.empty();
+  a.ln_rs = 4 * L * C + (hp ? 2 * C : 0);
+  Tensor lns = torch::empty({(int64_t)a.B, (int64_t)a.ln_rs}, f32);  // every element stored by the kernel
   std::vector<Tensor> out{dx, lns};
   for (int i = 0; i < L; ++i) {
     sb_fill_params(a.ly[i], params, i, C);
@@ -702,6 +757,32 @@ std::vector<Tensor> sb_bwd(Tensor dz, Tensor x0, std::vector<Tensor> saved, std:
     g.dg1 = lp; g.dbe1 = lp + C; g.dg2 = lp + 2 * C; g.dbe2 = lp + 3 * C;
     out.insert(out.end(), {dq, dy, du, dzz});
   }
+  if (hp) {
+    TORCH_CHECK(pre.size() == 10, "sb_bwd: pre = [O, x_q, wo, bo, g2, be2, w1, b1, w2, b2]");
+    sb_check_pre_o(pre[0], R, C);
+    sb_fill_pre(a.pre, pre, C);
+    sb_fill_pre_saved(a.pre, pre_saved, R, C);
+    a.pre.O = reinterpret_cast<uint16_t*>(pre[0].data_ptr());
+    Tensor dO = torch::empty({R, C}, b16), delta = torch::empty({R, 4}, f32), dy = torch::empty({R, C}, b16),
+           du = torch::empty({R, C}, b16), dzz = torch::empty({R, C}, b16);
+    a.preDO = reinterpret_cast<uint16_t*>(dO.data_ptr());
+    a.preDelta = delta.data_ptr<float>();
+    pio::SBGrad& g = a.pgr;
+    g.dY = reinterpret_cast<uint16_t*>(dy.data_ptr()); g.dU = reinterpret_cast<uint16_t*>(du.data_ptr());
+    g.dZ = reinterpret_cast<uint16_t*>(dzz.data_ptr());
+    float* lp = lns.data_ptr<float>() + (int64_t)4 * L * C;
+    g.dg2 = lp; g.dbe2 = lp + C;
+    a.has_pre = 1;
+    out.insert(out.end(), {dO, delta, dy, du, dzz});
+  }
+  if (zero_out.has_value()) {
+    CHECK_DT(*zero_out, torch::kFloat32);
+    TORCH_CHECK(zero_out->is_contiguous() && zero_out->numel() % 4 == 0 &&
+                    reinterpret_cast<uintptr_t>(zero_out->data_ptr()) % 16 == 0,
+                "sb_bwd: zero_out must be a contiguous, 16-byte aligned fp32 buffer of 4k elements");
+    a.zero_p = zero_out->data_ptr<float>();
+    a.zero_n4 = zero_out->numel() / 4;
+  }
   TORCH_CHECK(pio::sb_bwd_launch(a, C, stream()), "sb_bwd: launch refused");
   return out;
 }
@@ -710,7 +791,7 @@ std::vector<Tensor> sb_bwd(Tensor dz, Tensor x0, std::vector<Tensor> saved, std:
 // db (N) fp32] × n (added to dW / db); one C for every job.  job_slab / job_dsts / job_offs: a
 // slab reduction run by appended workgroups (the block's LayerNorm partials from sb_bwd)
 void sb_wgrad(std::vector<Tensor> jobs, OptT job_slab, std::vector<Tensor> job_dsts, std::vector<int64_t> job_offs) {
-  TORCH_CHECK(jobs.size() % 4 == 0 && !jobs.empty() && (int)jobs.size() / 4 <= pio::kSBMaxJobs, "sb_wgrad: 1..16 jobs");
+  TORCH_CHECK(jobs.size() % 4 == 0 && !jobs.empty() && (int)jobs.size() / 4 <= pio::kSBMaxJobs, "sb_wgrad: 1..", pio::kSBMaxJobs, " jobs");
   pio::SBWgradArgs a{};
   a.njobs = (int)jobs.size() / 4;
   a.R = (int)jobs[0].size(0);
@@ -1772,9 +1853,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("b2"), py::arg("lnw"), py::arg("lnb"), py::arg("wq"), py::arg("bq"), py::arg("seed") = py::none(),
         py::arg("p") = 0.0);
   m.def("persist_errors", &persist_errors, py::arg("reset") = true);
-  m.def("sb_fwd", &sb_fwd, py::arg("x"), py::arg("params"), py::arg("scale"), py::arg("eps"));
+  m.def("sb_fwd", &sb_fwd, py::arg("x"), py::arg("params"), py::arg("scale"), py::arg("eps"),
+        py::arg("pre") = std::vector<Tensor>{});
   m.def("sb_bwd", &sb_bwd, py::arg("dz"), py::arg("x0"), py::arg("saved"), py::arg("params"),
-        py::arg("scale"), py::arg("eps"));
+        py::arg("scale"), py::arg("eps"), py::arg("pre") = std::vector<Tensor>{},
+        py::arg("pre_saved") = std::vector<Tensor>{}, py::arg("zero_out") = py::none());
   m.def("sb_wgrad", &sb_wgrad, py::arg("jobs"), py::arg("job_slab") = py::none(),
         py::arg("job_dsts") = std::vector<Tensor>(), py::arg("job_offs") = std::vector<int64_t>());
   m.def("post_attn_ln_linear_fwd", &post_attn_ln_linear_fwd, py::arg("o"), py::arg("x"), py::arg("wo"), py::arg("bo"),

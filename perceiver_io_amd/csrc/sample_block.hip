@@ -142,6 +142,17 @@ __device__ __forceinline__ void copy_rows(T* g, long long gld, const T* img, int
     *reinterpret_cast<uint4*>(gb + rr * gld + col) = *reinterpret_cast<const uint4*>(img + rr * ld + col);
   }
 }
+// the sample's 32 global bf16 rows (row stride gld, W elements) → an LDS image [32][ld], by every
+// thread in 16-byte chunks (no barrier)
+template <int W>
+__device__ __forceinline__ void load_rows(uint16_t* img, int ld, const uint16_t* g, long long gld) {
+  constexpr int CPR = W / 8;
+  const uint16_t* gb = g + (long long)blockIdx.x * NR * gld;
+  for (int c = threadIdx.x; c < NR * CPR; c += blockDim.x) {
+    const int rr = c / CPR, col = (c % CPR) * 8;
+    *reinterpret_cast<uint4*>(img + rr * ld + col) = *reinterpret_cast<const uint4*>(gb + rr * gld + col);
+  }
+}
 // T-layout fp32 values of this lane → an LDS fp32 tile [32][ld]
 __device__ __forceinline__ void st_f32s(float* img, int ld, int r, int n0, const float (&v)[16]) {
   const int hh = lane_id() >> 5;
@@ -246,7 +257,7 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
   // every layer's per-channel vectors, staged once before any store of the kernel:
   // [γ1 | β1 | bqkv (3C) | bo | γ2 | β2 | b1 | b2]
   constexpr int NV = 10 * C;
-  __shared__ __attribute__((aligned(16))) float sVec[kSBMaxLayers][NV];
+  __shared__ __attribute__((aligned(16))) float sVec[kSBMaxLayers + 1][NV];  // + the pre stage's
   // staging of the saved rows for whole-row stores: QKV then U (bf16 [32][3C + 8]), Y then Z (fp32)
   constexpr int LDS3 = 3 * C + 8, LDF = C + 4;
   __shared__ __attribute__((aligned(16))) uint16_t sS[NR * LDS3];
@@ -267,11 +278,76 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
     stage_vec(v + 9 * C, y.b2, C);
   }
   float x[16];
-  ld_f32(x, a.X0, C, row, n0);
   bf16x8 wq[3][KS];
-  load_wtile<C>(wq[0], a.ly[0].Wqkv, n0);
-  load_wtile<C>(wq[1], a.ly[0].Wqkv, C + n0);
-  load_wtile<C>(wq[2], a.ly[0].Wqkv, 2 * C + n0);
+  if (a.has_pre) {
+    // ---- pre: the cross layer's post-attention half, y = Wo·O + bo + x_q, z0 = y + MLP(LN2(y)),
+    // the same phases as a layer's second half below; z0 is the block input ----
+    const SBLayer& y = a.pre;
+    float* vec = sVec[kSBMaxLayers];
+    stage_vec(vec + 5 * C, y.bo, C);
+    stage_vec(vec + 6 * C, y.g2, C);
+    stage_vec(vec + 7 * C, y.be2, C);
+    stage_vec(vec + 8 * C, y.b1, C);
+    stage_vec(vec + 9 * C, y.b2, C);
+    bf16x8 wo[KS], w1[KS];
+    load_wtile<C>(wo, y.Wo, n0);
+    load_rows<C>(sImg[1], LDI, a.preO, C);
+    ld_f32(x, a.preX, C, (long long)(a.preX_bs ? (int)blockIdx.x * a.preX_bs : 0) + r, n0);
+    load_wtile<C>(w1, y.W1, n0);
+    lds_sync();  // the O image and every staged vector
+    float yv[16], mu, rs, gv[16], bv[16], t[16];
+    {
+      float bb[16];
+      const f32x16 acc = gemm_t<C>(wo, sImg[1], LDI);
+      ld_vec(bb, vec + 5 * C, n0);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) yv[i] = acc[i] + bb[i] + x[i];
+    }
+    bf16x8 w2[KS];
+    load_wtile<C>(w2, y.W2, n0);
+    st_f32s(sF, LDF, r, n0, yv);
+    ld_vec(gv, vec + 6 * C, n0);
+    ld_vec(bv, vec + 7 * C, n0);
+    ln_stats<C>(yv, sRed, a.eps, mu, rs);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t[i] = (yv[i] - mu) * rs * gv[i] + bv[i];
+    if (w == 0 && l < 32) { y.mean2[row] = mu; y.rstd2[row] = rs; }
+    st_bf16(sImg[0], LDI, r, n0, t);
+    lds_sync();
+    copy_rows<C>(y.Y, C, sF, LDF);
+    copy_rows<C>(y.LN2Y, C, sImg[0], LDI);
+    {
+      float bb[16];
+      const f32x16 acc = gemm_t<C>(w1, sImg[0], LDI);
+      ld_vec(bb, vec + 8 * C, n0);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) t[i] = acc[i] + bb[i];
+    }
+    float gu[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) gu[i] = gelu_f(t[i]);
+    st_bf16(sImg[1], LDI, r, n0, gu);
+    load_wtile<C>(wq[0], a.ly[0].Wqkv, n0);  // layer 0's QKV weights, in flight during the MLP
+    load_wtile<C>(wq[1], a.ly[0].Wqkv, C + n0);
+    load_wtile<C>(wq[2], a.ly[0].Wqkv, 2 * C + n0);
+    st_bf16(sS, LDS3, r, n0, t);
+    lds_sync();
+    copy_rows<C>(y.U, C, sS, LDS3);
+    copy_rows<C>(y.GU, C, sImg[1], LDI);
+    {
+      float bb[16];
+      const f32x16 acc = gemm_t<C>(w2, sImg[1], LDI);
+      ld_vec(bb, vec + 9 * C, n0);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) x[i] = acc[i] + bb[i] + yv[i];
+    }
+    st_f32s(sF, LDF, r, n0, x);  // z0: copied out to X0 behind layer 0's first barrier
+  } else {
+    ld_f32(x, a.X0, C, row, n0);
+    load_wtile<C>(wq[0], a.ly[0].Wqkv, n0);
+    load_wtile<C>(wq[1], a.ly[0].Wqkv, C + n0);
+    load_wtile<C>(wq[2], a.ly[0].Wqkv, 2 * C + n0);
+  }
   for (int li = 0; li < a.L; ++li) {
     const SBLayer& y = a.ly[li];
     const float* vec = sVec[li];
@@ -294,6 +370,7 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
     PIO_TS(12 * li + 2);
     copy_rows<C>(y.LN1X, C, sImg[0], LDI);
     if (li > 0) copy_rows<C>(a.ly[li - 1].Z, C, sF, LDF);  // the previous layer's output
+    else if (a.has_pre) copy_rows<C>(a.pre.Z, C, sF, LDF);  // the pre stage's (the block input)
     // ---- Q, K, V of the wave's heads ----
     float q[16], k[16], v[16];
     {
@@ -449,7 +526,7 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t sQ[NR * LDQ];
   __shared__ __attribute__((aligned(16))) uint16_t sAt[NW][4][NR * LDA];  // per wave: K, Q, dO, P / dS
   __shared__ __attribute__((aligned(16))) float2 sRed[NW * NR];
-  __shared__ __attribute__((aligned(16))) float sG[kSBMaxLayers][2][C];  // γ1, γ2 of every layer
+  __shared__ __attribute__((aligned(16))) float sG[kSBMaxLayers + 1][2][C];  // γ1, γ2 of every layer (+ pre's γ2)
   const int w = wave_id(), l = lane_id(), r = l & 31;
   const long long row = (long long)blockIdx.x * NR + r;
   const int n0 = 32 * w;
@@ -458,6 +535,13 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
   for (int li = 0; li < a.L; ++li) {
     stage_vec(sG[li][0], a.ly[li].g1, C);
     stage_vec(sG[li][1], a.ly[li].g2, C);
+  }
+  if (a.has_pre) stage_vec(sG[kSBMaxLayers][1], a.pre.g2, C);
+  if (a.zero_p != nullptr) {  // this workgroup's slice of the cross attention backward's accumulators
+    const long long per = (a.zero_n4 + gridDim.x - 1) / gridDim.x;
+    const long long z0 = (long long)blockIdx.x * per, z1 = z0 + per < a.zero_n4 ? z0 + per : a.zero_n4;
+    for (long long i = z0 + threadIdx.x; i < z1; i += blockDim.x)
+      reinterpret_cast<float4*>(a.zero_p)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   float dz[16];
   ld_f32(dz, a.dZ, C, row, n0);
@@ -613,6 +697,7 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
     acc = gemm_tt<C>(sW[0], n0, sQ, LDQ, C, acc);
     wblock_store<C>(sW[1], pw);
     if (li > 0) wblock_load<C>(pw, a.ly[li - 1].W2, 0);
+    else if (a.has_pre) wblock_load<C>(pw, a.pre.W2, 0);
     lds_sync();
     PIO_TS(16 * li + 13);
     acc = gemm_tt<C>(sW[1], n0, sQ, LDQ, 2 * C, acc);
@@ -637,6 +722,80 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
     PIO_TS(16 * li + 14);
     ln_affine_grads(t, xv, gd.dg1 + lnr, gd.dbe1 + lnr, n0);
     PIO_TS(16 * li + 15);
+  }
+  if (a.has_pre) {
+    // ---- pre: the cross layer's post-attention backward (a layer's first half) → dO, δ of the
+    // cross attention, dX = dY (the residual path to x_q) ----
+    const SBLayer& y = a.pre;
+    const SBGrad& gd = a.pgr;
+    uint2 ur[4], orw[4];
+    float yv[16];
+    ld_raw(ur, y.U, C, row, n0);
+    ld_f32(yv, y.Y, C, row, n0);
+    const float mu2 = y.mean2[row], rs2 = y.rstd2[row];
+    wblock_store<C>(sW[0], pw);
+    wblock_load<C>(pw, y.W1, 0);
+    st_bf16(sImg[0], LDI, r, n0, dz);
+    lds_sync();
+    copy_rows<C>(gd.dZ, C, sImg[0], LDI);
+    float t[16];
+    {
+      float uv[16];
+      cvt_raw(uv, ur);
+      const f32x16 acc = gemm_tt<C>(sW[0], n0, sImg[0], LDI, 0, f32x16{});
+#pragma unroll
+      for (int i = 0; i < 16; ++i) t[i] = acc[i] * gelu_grad(uv[i]);
+    }
+    st_bf16(sImg[1], LDI, r, n0, t);
+    wblock_store<C>(sW[1], pw);
+    wblock_load<C>(pw, y.Wo, 0);
+    ld_raw(orw, y.O, C, row, n0);
+    lds_sync();
+    copy_rows<C>(gd.dU, C, sImg[1], LDI);
+    float dy[16];
+    {
+      float gv[16];
+      ld_vec(gv, sG[kSBMaxLayers][1], n0);
+      const f32x16 acc = gemm_tt<C>(sW[1], n0, sImg[1], LDI, 0, f32x16{});
+      float s1 = 0.f, s2 = 0.f, gg[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        t[i] = acc[i];                     // dXn2
+        yv[i] = (yv[i] - mu2) * rs2;       // ŷ
+        gg[i] = acc[i] * gv[i];
+        s1 += gg[i];
+        s2 += gg[i] * yv[i];
+      }
+      const float2 s = row_sums2<C>(s1, s2, sRed);
+      const float m1 = s.x * (1.f / C), m2 = s.y * (1.f / C);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dy[i] = dz[i] + rs2 * (gg[i] - m1 - yv[i] * m2);
+    }
+    st_bf16(sImg[0], LDI, r, n0, dy);
+    wblock_store<C>(sW[0], pw);
+    ln_affine_grads(t, yv, gd.dg2 + lnr, gd.dbe2 + lnr, n0);
+    lds_sync();
+    copy_rows<C>(gd.dY, C, sImg[0], LDI);
+    // dO = Woᵀ·dY as the attention backward reads it (bf16), δ = rowsum(dO∘O) per head
+    float dov[16], ov[16];
+    to_f(dov, gemm_tt<C>(sW[0], n0, sImg[0], LDI, 0, f32x16{}));
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dov[i] = bf2f(f2bf(dov[i]));
+    cvt_raw(ov, orw);
+#pragma unroll
+    for (int hp = 0; hp < S::HPW; ++hp) {
+      float dl = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (head_reg<C>(i, hp)) dl = fmaf(dov[i], ov[i], dl);
+      dl = xor32_sum(dl);
+      if (l < 32) a.preDelta[row * H + w * S::HPW + hp] = dl;
+    }
+    st_bf16(sImg[1], LDI, r, n0, dov);
+    lds_sync();
+    copy_rows<C>(a.preDO, C, sImg[1], LDI);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dz[i] = dy[i];
   }
   st_f32(a.dX, C, row, n0, dz);
 }

@@ -16,9 +16,18 @@ struct SBLayer {
   uint16_t *LN1X, *QKV, *O, *LN2Y, *U, *GU;    // bf16 rows: LN1(x), packed QKV, attention out, LN2(y), W1 out, GELU
   float *Y, *Z, *mean1, *rstd1, *mean2, *rstd2;  // fp32: residual after attention, layer output, LN stats
 };
+// pre (has_pre): the post-attention half of the cross-attention layer in front of the block
+// (model.py:36-44 applied to the cross layer's attention output): z0 = y + MLP(LN2(y)),
+// y = Wo·O + bo + x_q.  Its Wo / W1 / W2 / bo / γ2 / β2 / b1 / b2 and saved LN2Y / U / GU / Y /
+// mean2 / rstd2 are those of an SBLayer; its Z is the block input (X0, written by the forward).
 struct SBFwdArgs {
   SBLayer ly[kSBMaxLayers];
-  const float* X0;  // block input rows (B·32, C) fp32
+  SBLayer pre;
+  const float* X0;        // block input rows (B·32, C) fp32 (pre: written, = pre.Z)
+  const uint16_t* preO;   // pre: the cross attention's output rows (B·32, C) bf16
+  const float* preX;      // pre: the residual rows x_q, (B·32, C) or (32, C) broadcast
+  int preX_bs;            // pre: rows between two samples' residual rows (32, or 0: broadcast)
+  int has_pre;
   int L, B;
   float scale_log2, eps;
 };
@@ -30,19 +39,31 @@ struct SBGrad {
   uint16_t *dQKV, *dY, *dU, *dZ;
   float *dg1, *dbe1, *dg2, *dbe2;
 };
+// pre (has_pre): the cross layer's post-attention backward after the block's: dX is then the
+// gradient of x_q's residual path (= dY of the pre stage); preDO / preDelta receive the cross
+// attention's dO (bf16) and δ = per-head rowsum(dO∘O) (fp32 (B·32, 4)); pgr its gradient rows and
+// LayerNorm partials (dg2 / dbe2 only).  zero_p / zero_n4: an fp32 buffer cleared on the way (the
+// cross attention backward's atomic accumulators), one slice per workgroup.
 struct SBBwdArgs {
   SBLayer ly[kSBMaxLayers];
   SBGrad gr[kSBMaxLayers];
+  SBLayer pre;
+  SBGrad pgr;
   const float* X0;   // the block input (layer 0's LN1 input)
   const float* dZ;   // gradient of the block output (B·32, C) fp32
   float* dX;         // gradient of the block input (B·32, C) fp32 (written)
+  uint16_t* preDO;
+  float* preDelta;
+  float* zero_p;
+  long long zero_n4;
+  int has_pre;
   int L, B;
   int ln_rs;         // row stride of the LayerNorm partial slab (floats)
   float scale_log2, eps;
 };
 // grouped weight-gradient GEMMs: dW[n][k] += Σ_rows G[r][n] · A[r][k], db[n] += Σ_rows G[r][n]
 // (A is C wide: every self-attention weight's input); one job per weight
-constexpr int kSBMaxJobs = 4 * kSBMaxLayers;
+constexpr int kSBMaxJobs = 4 * kSBMaxLayers + 3;  // + the pre stage's Wo, W1, W2
 struct SBWgradJob {
   const uint16_t* G;  // bf16 [R][N]
   const uint16_t* A;  // bf16 [R][C]

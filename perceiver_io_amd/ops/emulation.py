@@ -763,11 +763,32 @@ def _sb_probs(q, k, scale):
     return torch.softmax(s * scale, dim=-1)
 
 
-def sb_fwd(x, params, scale, eps):
+def _sb_pre_fwd(pre, R, C, eps):
+    """the pre stage: the cross layer's post-attention half (O, x_q → y, LN2, MLP → z0)."""
+    o, xq, wo, bo, g2, be2, w1, b1, w2, b2 = pre
+    if xq.shape[0] != R:  # broadcast latents
+        xq = xq.repeat(R // xq.shape[0], 1)
+    y = o.float() @ wo.float().t() + bo + xq
+    t2, mean2, rstd2 = _ln(y, g2, be2, eps)
+    ln2y = _bf(t2)
+    u = ln2y @ w1.float().t() + b1
+    gu = _bf(F.gelu(u))
+    z = gu @ w2.float().t() + b2 + y
+    bf = torch.bfloat16
+    return z, [ln2y.to(bf), u.to(bf), gu.to(bf), y, mean2, rstd2]
+
+
+def sb_fwd(x, params, scale, eps, pre=()):
+    """pre (10 tensors): the cross layer's post-attention half first; x (the block input) is
+    written with its output and its 6 saved tensors are appended."""
     R, C = x.shape
     B = R // _SB_N
     L = len(params) // 12
     out = []
+    pre_saved = []
+    if pre:
+        z0, pre_saved = _sb_pre_fwd(pre, R, C, eps)
+        x.copy_(z0)
     for i in range(L):
         g1, be1, wqkv, bqkv, wo, bo, g2, be2, w1, b1, w2, b2 = _sb_unpack(params, i)
         t, mean1, rstd1 = _ln(x, g1, be1, eps)
@@ -790,15 +811,17 @@ def sb_fwd(x, params, scale, eps):
         out += [ln1x.to(bf), qkv.to(bf), o.to(bf), ln2y.to(bf), u.to(bf), gu.to(bf), y, z, mean1, rstd1, mean2, rstd2]
         del p
         x = z
-    return out
+    return out + pre_saved
 
 
-def sb_bwd(dz, x0, saved, params, scale, eps):
+def sb_bwd(dz, x0, saved, params, scale, eps, pre=(), pre_saved=(), zero_out=None):
     R, C = x0.shape
     B = R // _SB_N
     L = len(params) // 12
     grads = [None] * L
-    lns = torch.empty(B, 4 * L * C, dtype=torch.float32, device=x0.device)
+    lns = torch.empty(B, 4 * L * C + (2 * C if pre else 0), dtype=torch.float32, device=x0.device)
+    if zero_out is not None:
+        zero_out.zero_()
 
     def per_sample(t):  # (B·32, C) → the sample sums (B, C)
         return t.view(B, _SB_N, C).sum(1)
@@ -836,10 +859,27 @@ def sb_bwd(dz, x0, saved, params, scale, eps):
         bf = torch.bfloat16
         grads[i] = [dqkvb.to(bf), dyb.to(bf), du.to(bf), dzb.to(bf)]
         dz = dy + dxl
+    tail = []
+    if pre:  # the cross layer's post-attention backward: dO, δ, and dX = dY (the x_q residual path)
+        o, _, wo, bo, g2, be2, w1, b1, w2, b2 = pre
+        ln2y, u, gu, y, mean2, rstd2 = pre_saved
+        dzb = _bf(dz)
+        du = _bf((dzb @ w2.float()) * _gelu_grad(u.float()))
+        dxn2 = du @ w1.float()
+        dyl, yh = _ln_bwd(dxn2, y, mean2, rstd2, g2)
+        dy = dz + dyl
+        lns[:, 4 * L * C:(4 * L + 1) * C] = per_sample(dxn2 * yh)
+        lns[:, (4 * L + 1) * C:(4 * L + 2) * C] = per_sample(dxn2)
+        dyb = _bf(dy)
+        do = _bf(dyb @ wo.float())
+        delta = (do * o.float()).view(R, 4, C // 4).sum(-1)
+        bf = torch.bfloat16
+        tail = [do.to(bf), delta, dyb.to(bf), du.to(bf), dzb.to(bf)]
+        dz = dy
     out = [dz, lns]
     for g in grads:
         out += g
-    return out
+    return out + tail
 
 
 def sb_wgrad(jobs, job_slab=None, job_dsts=(), job_offs=()):

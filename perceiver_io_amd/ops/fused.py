@@ -452,6 +452,30 @@ def _pe_proj_grads(D, part, nc, pe, g, b, W):
     return dW, S, (W * G).sum(0), torch.mv(W.t(), S)
 
 
+def _cross_zero_bufs(ctx, device):
+    """(zbuf, dq_pre, d_pre) of a fused cross-attention layer's backward: the attention backward's
+    atomically accumulated dQ — and, for the first backward application of a PE layer whose batch
+    groups add into its factored reduction D, that (M, 2C) buffer too — in one fp32 span that the
+    kernel before the attention backward clears on the way (no fill launch); (None, None, None)
+    for self-attention layers and in deterministic mode.  Broadcast latent queries on the fused PE
+    path come back summed over the batch."""
+    from . import deterministic
+
+    if not ctx.spec.cross or deterministic():
+        return None, None, None
+    B, Bq, Nq, C, H, D, scale = ctx.dims
+    pe_fused, pm = ctx.zplan
+    f32 = dict(device=device, dtype=torch.float32)
+    nq = (Bq if pe_fused else B) * Nq * C
+    d_pre = None
+    if pe_fused and ctx.kv_entry.get("pe_D") is None and pe_attn_bsplit(B, pm, H) > 1:
+        zbuf = torch.empty(nq + pm * 2 * C, **f32)
+        d_pre = zbuf[nq:].view(pm, 2 * C)
+    else:
+        zbuf = torch.empty(nq, **f32)
+    return zbuf, zbuf[:nq].view(-1, Nq, C), d_pre
+
+
 class _LayerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, spec: LayerSpec, bw, seed, p_attn, src, x_q, x_kv, kmask, *ps):
@@ -527,6 +551,11 @@ class _LayerFn(torch.autograd.Function):
                     src.entries[key] = ent
             kv, mean_kv, rstd_kv = ent["kv"], ent["mean"], ent["rstd"]
             ctx.kv_entry = ent
+            # the backward's accumulator plan (known here so a following per-sample block that runs
+            # this layer's post-attention backward can clear the accumulators: _cross_zero_bufs)
+            ctx.zplan = (bool(ent.get("factored") and PE_ATTN_FUSED and D == 32 and Nq <= 32 and kmask is None
+                              and p_attn == 0.0 and xkv2.shape[1] <= 4),
+                         ent["implicit"][1].shape[0] if ent.get("implicit") is not None else ent["kv"].shape[0] // B)
             ctx.kv_pe = src.pe if src is not None else None
             ctx.kv_pe_index = _pe_index(src)
             q3 = q.view(Bq, Nq, C)
@@ -552,7 +581,18 @@ class _LayerFn(torch.autograd.Function):
         # a batch-broadcast query stream (Bq = 1) is added as the residual without expanding it;
         # residual dropout (p_attn: the layer's one dropout rate) in the kernel epilogues
         nxt, _LOOKAHEAD["want"] = _LOOKAHEAD["want"], None
-        if nxt is not None and spec.cross:
+        want_pa, _LOOKAHEAD["want_pa"] = _LOOKAHEAD["want_pa"], None
+        if (want_pa and spec.cross and nxt is None and p_attn == 0.0 and Nq == 32 and Bq in (1, B)
+                and o2.is_contiguous()):
+            # the following per-sample block (_SampleBlockFn) runs this layer's post-attention half
+            # as the prologue of its kernels, forward and backward: z is its placeholder, written
+            # by that block's forward before anything reads it
+            z = torch.empty((B * Nq, C), device=o2.device, dtype=torch.float32)
+            _LOOKAHEAD["have_pa"] = dict(key=z.data_ptr(), ctx=ctx, pre=[o2, xq2, wo, bo, g2, be2, w1, b1, w2, b2],
+                                         ps=(rest[1], bo, g2, be2, rest[5], b1, rest[7], b2))
+            ctx.pa_key = z.data_ptr()
+            y = m2 = r2 = u = torch.empty(0, device=o2.device)
+        elif nxt is not None and spec.cross:
             # the following self-attention block's LN1 + QKV projection in the same launch (its
             # forward picks the result up instead of launching ln_linear_fwd)
             z, y, m2, r2, u, qkv_n, mean_n, rstd_n = K.post_attn_ln_linear_fwd(
@@ -632,31 +672,28 @@ class _LayerFn(torch.autograd.Function):
         # the post-attention backward kernel on the way (no fill launch on the chain)
         from . import deterministic
 
-        pe_fused = spec.cross and bool(ctx.kv_entry.get("factored") and PE_ATTN_FUSED and D == 32 and Nq <= 32
-                                       and kmask is None and ctx.p_attn == 0.0 and xkv2.shape[1] <= 4)
-        dq_pre, d_pre = None, None
-        if spec.cross and not deterministic():
-            # the attention backward's atomically accumulated dQ, cleared by the post-attention
-            # backward on the way (no fill launch); broadcast latent queries on the fused PE path
-            # come back summed over the batch
-            nq = (Bq if pe_fused else B) * Nq * C
-            ent = ctx.kv_entry
-            imp = ent.get("implicit")
-            pm = imp[1].shape[0] if imp is not None else kv.shape[0] // B
-            if pe_fused and ent.get("pe_D") is None and pe_attn_bsplit(B, pm, H) > 1:
-                # the first application's factored reduction D (M, 2C), which the split batch
-                # groups add into atomically, shares the span: [dQ | D] in one buffer
-                zbuf = torch.empty(nq + pm * 2 * C, **f32)
-                d_pre = zbuf[nq:].view(pm, 2 * C)
-            else:
-                zbuf = torch.empty(nq, **f32)
-            dq_pre = zbuf[:nq].view(-1, Nq, C)
+        pe_fused = spec.cross and ctx.zplan[0]
+        pa = None
+        if getattr(ctx, "pa_key", None) is not None:
+            pa, _LOOKAHEAD["bwd_pa"] = _LOOKAHEAD["bwd_pa"], None
+            if pa is None or pa["key"] != ctx.pa_key:
+                raise RuntimeError("fused encoder: the per-sample block that ran this cross-attention layer's "
+                                   "post-attention half did not hand its backward back")
+            zbuf, dq_pre, d_pre = pa["zbuf"]  # cleared by that block's backward kernel
+        else:
+            zbuf, dq_pre, d_pre = _cross_zero_bufs(ctx, dz.device)
+        if zbuf is not None and pa is None:
             drop["zero_out"] = zbuf
         ho, _LOOKAHEAD["bwd"] = _LOOKAHEAD["bwd"], None
         if ho is not None and ho["key"] != getattr(ctx, "lookahead_z", None):
             raise RuntimeError("fused encoder: a self-attention block handed its LN1/QKV backward to the wrong "
                                "cross-attention layer")
-        if ho is not None:
+        if pa is not None:
+            if ho is not None:
+                raise RuntimeError("fused encoder: a cross-attention layer with two backward hand-offs")
+            # post-attention backward done by the block: dY (the residual path) arrives as dz
+            dy, do, delta = dz2, pa["do"], pa["delta"]
+        elif ho is not None:
             # the following block's first LN1/QKV backward (its dX = this layer's dZ) and this
             # layer's post-attention backward in one launch; both weight-gradient sets in one slab
             sl = _GradSlab(R, LL_SIZES(C) + PA_SIZES(C), dz2)
@@ -1071,7 +1108,10 @@ class _SABlockFn(torch.autograd.Function):
 # The same in the other direction ("want_q" / "have_q" / "bwd_q"): a block's last fused layer
 # computes the next cross-attention layer's LN + query projection, and that layer hands the
 # backward of it back to the block.
+# "want_pa" / "have_pa" / "bwd_pa": a cross-attention layer's post-attention half run by the
+# per-sample block after it (forward prologue / backward epilogue of sb_fwd / sb_bwd).
 _LOOKAHEAD = {"want": None, "have": None, "bwd": None, "want_q": None, "have_q": None, "bwd_q": None,
+              "want_pa": None, "have_pa": None, "bwd_pa": None,
               "want_kv": None}
 
 
@@ -1101,6 +1141,23 @@ def sa_block_lookahead(block, rows: int, n: Optional[int] = None, device=None):
         return None
     ps = pss[0]
     return (ps[0], ps[1], _bf16_weights(specs[0], ps)[0], ps[3])
+
+
+# a cross-attention layer's post-attention half folded into the per-sample block after it
+# (PIO_SB_PRE=0: the cross layer runs it, A/B)
+SB_PRE = os.environ.get("PIO_SB_PRE", "1") != "0"
+
+
+def sample_block_runs(block, b: int, n: int, device) -> bool:
+    """True when ``block`` over (b, n) latents will run as a per-sample block (_SampleBlockFn)
+    that can take the preceding cross layer's post-attention half."""
+    if not SB_PRE:
+        return False
+    layers, specs, pss, ok = _sa_block_plan(block, b * n)
+    if not ok:
+        return False
+    p = specs[0].dropout if layers[0].training else 0.0
+    return _sample_block_ok(specs, n, p, device is not None and torch.device(device).type == "cuda")
 
 
 def _zero_plan(K, B, H, Nq, Nk, D) -> int:
@@ -1167,7 +1224,18 @@ class _SampleBlockFn(torch.autograd.Function):
             wq, _, wo, w1, w2 = bws[i]
             params += [p[0], p[1], wq, p[3], wo, p[5], p[6], p[7], w1, p[9], w2, p[11]]
         scale = 1.0 / math.sqrt(C // specs[0].heads)
-        saved = K.sb_fwd(xl, params, scale, EPS)
+        hp = _LOOKAHEAD["have_pa"]
+        ctx.pa = None
+        if hp is not None and hp["key"] == xl.data_ptr():
+            # the preceding cross layer's post-attention half: x is its placeholder output, written
+            # by this launch before the block's first layer reads it
+            _LOOKAHEAD["have_pa"] = None
+            saved = K.sb_fwd(xl, params, scale, EPS, pre=hp["pre"])
+            ctx.pa = hp
+            ctx.pre_saved = saved[12 * L:]
+            saved = saved[:12 * L]
+        else:
+            saved = K.sb_fwd(xl, params, scale, EPS)
         z = saved[12 * (L - 1) + 7]
         # the block output is not a backward operand: a placeholder in its slot
         ctx.save_for_backward(xl, *saved[:12 * (L - 1) + 7], xl, *saved[12 * (L - 1) + 8:])
@@ -1192,9 +1260,18 @@ class _SampleBlockFn(torch.autograd.Function):
                 scratch.append(g)
             return g.view(-1)
 
-        out = K.sb_bwd(dz2, xl, saved, ctx.params, scale, EPS)
-        # the per-sample LayerNorm affine partials (B, 4·L·C): summed into the gradients by the
-        # grouped weight-gradient launch's appended workgroups (or a deferred slab reduction)
+        pa = ctx.pa
+        if pa is not None:
+            # the cross layer's post-attention backward last: its dO / δ and cleared accumulators go
+            # to that layer's backward, the returned gradient is its residual path dY
+            zb = _cross_zero_bufs(pa["ctx"], dz.device)
+            out = K.sb_bwd(dz2, xl, saved, ctx.params, scale, EPS, pre=pa["pre"], pre_saved=ctx.pre_saved,
+                           zero_out=zb[0])
+            _LOOKAHEAD["bwd_pa"] = dict(key=pa["key"], do=out[-5], delta=out[-4], zbuf=zb)
+        else:
+            out = K.sb_bwd(dz2, xl, saved, ctx.params, scale, EPS)
+        # the per-sample LayerNorm affine partials (B, 4·L·C [+ 2C]): summed into the gradients by
+        # the grouped weight-gradient launch's appended workgroups (or a deferred slab reduction)
         dsts, offs = [], []
         for i in range(L):
             p = ps[SA_NP * i:SA_NP * (i + 1)]
@@ -1210,6 +1287,19 @@ class _SampleBlockFn(torch.autograd.Function):
             sv = saved[12 * i:12 * (i + 1)]
             for G, A, W, b in ((dq, sv[0], p[2], p[3]), (dy, sv[2], p[4], p[5]), (du, sv[3], p[8], p[9]),
                                (dzz, sv[5], p[10], p[11])):
+                if W.requires_grad or b.requires_grad:
+                    jobs += [G, A, target(W, W.numel()), target(b, b.numel())]
+        if pa is not None:
+            Wo, bo, g2, be2, W1, b1, W2, b2 = pa["ps"]
+            for j, q in enumerate((g2, be2)):
+                g = _grad_of(q)
+                if g is not None:
+                    dsts.append(g.view(-1))
+                    offs.append((4 * L + j) * C)
+            dyp, dup, dzp = out[-3:]
+            o_pre = pa["pre"][0]
+            ln2y, _, gu = ctx.pre_saved[:3]
+            for G, A, W, b in ((dyp, o_pre, Wo, bo), (dup, ln2y, W1, b1), (dzp, gu, W2, b2)):
                 if W.requires_grad or b.requires_grad:
                     jobs += [G, A, target(W, W.numel()), target(b, b.numel())]
         if jobs:
@@ -1358,12 +1448,14 @@ def _encode(encoder, src: KVSource, pad_mask):
             lat = bucket_ready_point(lat, encoder, "layer_n")
         if lat.shape[0] == 1 and not can_fuse(cross, src):
             lat = lat.expand(b, -1, -1)
-        # the block's first LN1 + QKV projection rides on the cross layer's post-attention kernel
+        # the block's first LN1 + QKV projection rides on the cross layer's post-attention kernel,
+        # or a per-sample block runs that post-attention half itself
         _LOOKAHEAD["want"] = sa_block_lookahead(block, b * n, n, lat.device) if can_fuse(cross, src) else None
+        _LOOKAHEAD["want_pa"] = can_fuse(cross, src) and sample_block_runs(block, b, n, lat.device)
         try:
             lat = cross_attention_layer(cross, lat, src, pad_mask)
         finally:
-            _LOOKAHEAD["want"] = None
+            _LOOKAHEAD["want"] = _LOOKAHEAD["want_pa"] = None
         if lat.shape[0] == 1 and b > 1:
             lat = lat.expand(b, -1, -1)
         nxt_cross = layers[li + 1][0] if li + 1 < len(layers) else None
@@ -1375,8 +1467,11 @@ def _encode(encoder, src: KVSource, pad_mask):
             lat = bucket_ready_point(lat, encoder, "layer_1_sa")
         try:
             lat = self_attention_block(block, lat)
+            if _LOOKAHEAD["have_pa"] is not None:
+                raise RuntimeError("fused encoder: a cross-attention layer left its post-attention half to a "
+                                   "per-sample block that did not run it")
         finally:
-            _LOOKAHEAD["have"] = _LOOKAHEAD["want_q"] = None
+            _LOOKAHEAD["have"] = _LOOKAHEAD["want_q"] = _LOOKAHEAD["have_pa"] = None
     if _LOOKAHEAD["want_kv"] is None:
         _LOOKAHEAD["have_q"] = None
     return lat

@@ -1,0 +1,61 @@
+"""The encoder cross-attention layer's post-attention half folded into the per-sample block after it
+(ops/fused.py "want_pa" / "have_pa" / "bwd_pa"; csrc/sample_block.hip pre stage), run on the CPU
+through the kernel emulation with the per-sample block routing forced on (it needs CUDA tensors
+otherwise): same outputs and gradients as the unfolded executor and as eager fp32, and the folded
+layers launch no post-attention kernels of their own."""
+import pytest
+import torch
+
+from perceiver_io_amd import ops
+from perceiver_io_amd.models import (ClassificationOutputAdapter, ImageInputAdapter, PerceiverDecoder,
+                                     PerceiverEncoder, PerceiverIO)
+
+
+def _model(c, layers, sa):
+    enc = PerceiverEncoder(ImageInputAdapter((28, 28, 1), 32), (32, c), layers, num_self_attention_layers_per_block=sa)
+    dec = PerceiverDecoder(ClassificationOutputAdapter(10, num_output_channels=c), (32, c), num_cross_attention_heads=1)
+    return PerceiverIO(enc, dec)
+
+
+@pytest.mark.parametrize("c", [64, 128])
+def test_cross_post_attention_folded_into_sample_block(c, monkeypatch):
+    torch.manual_seed(c)
+    enc = _model(c, 3, 2).encoder
+    x = torch.randn(3, 28, 28, 1)
+    ok = ops.fused._sample_block_ok
+    monkeypatch.setattr(ops.fused, "_sample_block_ok", lambda specs, n, p, cuda: ok(specs, n, p, True))
+    emu = ops.emulation
+    calls = {}
+
+    class Counting:  # the executor's kernel calls
+        def __getattr__(self, name):
+            calls[name] = calls.get(name, 0) + 1
+            return getattr(emu, name)
+
+    ref = enc(x, None)[0]
+    w = torch.randn_like(ref)
+    (ref * w).sum().backward()
+    g_ref = {n: p.grad.clone() for n, p in enc.named_parameters() if p.grad is not None}
+    res = []
+    for fold in (False, True):
+        with monkeypatch.context() as mp:
+            mp.setattr(ops.fused, "kernels", lambda t: Counting())
+            mp.setattr(ops.fused, "SB_PRE", fold)
+            calls.clear()
+            enc.zero_grad(set_to_none=True)
+            out = ops.fused.encoder_forward(enc, x, None)
+            (out * w).sum().backward()
+            res.append((out.detach(), {n: p.grad.clone() for n, p in enc.named_parameters() if p.grad is not None},
+                        dict(calls)))
+    (o0, g0, c0), (o1, g1, c1) = res
+    assert c0.get("sb_fwd", 0) == 3 and c1.get("sb_fwd", 0) == 3, (c0, c1)
+    # every cross layer is followed by a per-sample block: no post-attention kernels at all
+    assert c0.get("post_attn_fwd", 0) == 3 and c1.get("post_attn_fwd", 0) == 0, (c0, c1)
+    assert c0.get("post_attn_bwd", 0) == 3 and c1.get("post_attn_bwd", 0) == 0, (c0, c1)
+    assert set(g0) == set(g1) == set(g_ref)
+    torch.testing.assert_close(o1, o0, rtol=2e-3, atol=2e-3 * o0.abs().max().item())
+    gmax = max(g.abs().max() for g in g_ref.values())
+    assert (o1 - ref).abs().max() < 0.03 * ref.abs().max()
+    for n in g0:
+        assert (g1[n] - g0[n]).abs().max() < 0.01 * gmax, n
+        assert (g1[n] - g_ref[n]).abs().max() < 0.03 * gmax, n
