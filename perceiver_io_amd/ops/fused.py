@@ -582,8 +582,8 @@ class _LayerFn(torch.autograd.Function):
         # residual dropout (p_attn: the layer's one dropout rate) in the kernel epilogues
         nxt, _LOOKAHEAD["want"] = _LOOKAHEAD["want"], None
         want_pa, _LOOKAHEAD["want_pa"] = _LOOKAHEAD["want_pa"], None
-        if (want_pa and spec.cross and nxt is None and p_attn == 0.0 and Nq == 32 and Bq in (1, B)
-                and o2.is_contiguous()):
+        if (want_pa and spec.cross and nxt is None and p_attn == 0.0 and Nq == 32 and H == 4 and Bq in (1, B)
+                and o2.is_contiguous()):  # 4 heads: δ in the block's head layout
             # the following per-sample block (_SampleBlockFn) runs this layer's post-attention half
             # as the prologue of its kernels, forward and backward: z is its placeholder, written
             # by that block's forward before anything reads it
