@@ -1027,7 +1027,10 @@ __global__ __launch_bounds__(256) void post_attn_bwd_kernel(
   __shared__ __attribute__((aligned(16))) unsigned char smem[post_attn_bwd_smem<C>()];
   if (blockIdx.y == 0) zero_span_block(job);
   if ((int)blockIdx.x >= (R + 63) / 64) {  // appended workgroups: the previous kernel's slab job
-    if (blockIdx.y == 0) slab_reduce_block(job, blockIdx.x - (R + 63) / 64, reinterpret_cast<float4*>(smem));
+    {  // the appended job workgroups span every grid row: block (x − tiles)·gridDim.y + y
+      const int jb = (int)(blockIdx.x - (R + 63) / 64) * (int)gridDim.y + (int)blockIdx.y;
+      if (jb < job.nblk) slab_reduce_block(job, jb, reinterpret_cast<float4*>(smem));
+    }
     return;
   }
   float dz[C / 32][8];
@@ -1206,7 +1209,10 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
     int wrs, int slab, int R, PeSplit ps, SlabJob job) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   if ((int)blockIdx.x >= (R + 63) / 64) {  // appended workgroups: the previous kernel's slab job
-    if (blockIdx.y == 0) slab_reduce_block(job, blockIdx.x - (R + 63) / 64, reinterpret_cast<float4*>(smem));
+    {  // the appended job workgroups span every grid row: block (x − tiles)·gridDim.y + y
+      const int jb = (int)(blockIdx.x - (R + 63) / 64) * (int)gridDim.y + (int)blockIdx.y;
+      if (jb < job.nblk) slab_reduce_block(job, jb, reinterpret_cast<float4*>(smem));
+    }
     return;
   }
   float dxo[NCH][8];
@@ -1241,7 +1247,10 @@ __global__ __launch_bounds__(256) void ln_linear_post_attn_bwd_kernel(
   __shared__ __attribute__((aligned(16))) unsigned char smem[SM];
   if (blockIdx.y == 0) zero_span_block(job);
   if ((int)blockIdx.x >= (R + 63) / 64) {  // appended workgroups: the previous kernel's slab job
-    if (blockIdx.y == 0) slab_reduce_block(job, blockIdx.x - (R + 63) / 64, reinterpret_cast<float4*>(smem));
+    {  // the appended job workgroups span every grid row: block (x − tiles)·gridDim.y + y
+      const int jb = (int)(blockIdx.x - (R + 63) / 64) * (int)gridDim.y + (int)blockIdx.y;
+      if (jb < job.nblk) slab_reduce_block(job, jb, reinterpret_cast<float4*>(smem));
+    }
     return;
   }
   const int part = (int)blockIdx.y, nparts = (int)gridDim.y;  // workgroups per tile (split_tiles)
@@ -1487,7 +1496,8 @@ void post_attn_bwd_launch(int C, const float* dZ, const float* Ysave, const floa
                           const uint16_t* W2, const float* g2, const float* be2, float* dY, uint16_t* dO,
                           float* delta, int H, const PostAttnGrads& grads, int R, const SlabJob& job, const DropCfg& dr,
                           hipStream_t st) {
-  dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0), split_tiles(R));
+  const int spl = split_tiles(R);
+  dim3 grid((R + 63) / 64 + (job.slab ? (job.nblk + spl - 1) / spl : 0), spl);
   const bool av = av_ok({dZ, Ysave, U, O, Wo, W1, W2, dY, dO}, {});
 #define PAB(CC)                                                                                                  \
   if (av) hipLaunchKernelGGL((post_attn_bwd_kernel<CC, true>), grid, dim3(256), 0, st, dZ, Ysave, mean2, rstd2, U, \
@@ -1520,6 +1530,7 @@ bool ln_linear_post_attn_bwd_launch(int C, const void* Gv, bool g_bf16, const ui
     return true;
   if (g_bf16) return false;
   grid.y = split_tiles(R);
+  grid.x = (R + 63) / 64 + (job.slab ? (job.nblk + (int)grid.y - 1) / (int)grid.y : 0);
 #define LPB(CC, NQ)                                                                                               \
   if (av) hipLaunchKernelGGL((ln_linear_post_attn_bwd_kernel<CC, true, NQ>), grid, dim3(256), 0, st, G, Wq, X, mean1, \
                              rstd1, lnw, lnb, dres, dlnw, dlnb, dWq, dbq, Ysave, mean2, rstd2, U, O, Wo, W1, W2, g2, \
@@ -1548,7 +1559,8 @@ static void ln_linear_bwd_t(const void* G, int g_rs, int N, const uint16_t* W, i
   auto fn = av ? ln_linear_bwd_kernel<TG, TX, NCH, true> : ln_linear_bwd_kernel<TG, TX, NCH, false>;
   set_smem_once((const void*)fn);
   // + the appended slab-job workgroups; few tiles: several workgroups per tile (split_tiles)
-  const dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0), split_tiles(R));
+  const int spl = split_tiles(R);
+  const dim3 grid((R + 63) / 64 + (job.slab ? (job.nblk + spl - 1) / spl : 0), spl);
   hipLaunchKernelGGL(fn, grid, dim3(256), smem, st, (const TG*)G, g_rs, N, W, w_rs, Kin, (const TX*)X, x_rs,
                      mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, dlnw, dlnb, dW, db, vrs, wrs, slab, R, ps, job);
 }

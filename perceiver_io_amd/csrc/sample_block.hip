@@ -812,8 +812,9 @@ __global__ __launch_bounds__(256) void sb_wgrad_kernel(SBWgradArgs a, SlabJob sj
   constexpr int LG = 64 + 8, LA = C + 8, TT = C / 64, AC = C / 64;  // A chunks (16 B) per thread
   __shared__ __attribute__((aligned(16))) uint16_t sG[2][NR * LG];
   __shared__ __attribute__((aligned(16))) uint16_t sA[2][NR * LA];
-  if ((int)blockIdx.x >= tiles) {  // appended (row split 0 only): the block's LayerNorm partial slab
-    if (blockIdx.y == 0) slab_reduce_block(sj, blockIdx.x - tiles, reinterpret_cast<float4*>(&sG[0][0]));
+  if ((int)blockIdx.x >= tiles) {  // appended: the block's LayerNorm partial slab
+    const int jb = ((int)blockIdx.x - tiles) * (int)gridDim.y + (int)blockIdx.y;  // over every grid row
+    if (jb < sj.nblk) slab_reduce_block(sj, jb, reinterpret_cast<float4*>(&sG[0][0]));
     return;
   }
   const int w = wave_id(), l = lane_id();
@@ -900,7 +901,7 @@ bool sb_wgrad_launch(SBWgradArgs a, int C, const SlabJob& sj, hipStream_t st) {
   int splits = (a.R + 511) / 512;
   a.rows_per_split = (a.R / sb::NR + splits - 1) / splits * sb::NR;
   splits = (a.R + a.rows_per_split - 1) / a.rows_per_split;
-  const dim3 grid(tiles + (sj.slab ? sj.nblk : 0), splits);
+  const dim3 grid(tiles + (sj.slab ? (sj.nblk + splits - 1) / splits : 0), splits);
   if (C == 128) hipLaunchKernelGGL(sb::sb_wgrad_kernel<128>, grid, dim3(256), 0, st, a, sj, tiles);
   else hipLaunchKernelGGL(sb::sb_wgrad_kernel<64>, grid, dim3(256), 0, st, a, sj, tiles);
   return true;
