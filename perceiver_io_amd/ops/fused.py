@@ -1318,7 +1318,24 @@ def _seed(p: float, device) -> Optional[torch.Tensor]:
     masks are regenerated, never stored."""
     if p <= 0.0:
         return None
+    pool = _SEED_POOL
+    if pool["armed"]:
+        # inside one encoder pass: one draw of a small pool serves every fused call of the pass
+        # (one generator launch instead of one per layer / block; each call its own slot)
+        t = pool["t"]
+        if t is None or t.device != torch.device(device) or pool["i"] >= t.numel():
+            t = pool["t"] = torch.randint(-(2**62), 2**62, (_SEED_POOL_SIZE,), device=device, dtype=torch.int64)
+            pool["i"] = 0
+        pool["i"] += 1
+        return t[pool["i"] - 1:pool["i"]]
     return torch.randint(-(2**62), 2**62, (1,), device=device, dtype=torch.int64)
+
+
+# dropout seeds of one encoder pass (_encode arms the pool on entry and disarms it on exit, so a
+# pass always draws a fresh pool: a replayed step graph re-runs that draw; calls outside an
+# encoder pass draw their own seed)
+_SEED_POOL_SIZE = 16
+_SEED_POOL = {"armed": False, "t": None, "i": 0}
 
 
 def _run_layer(layer, x_q, x_kv=None, pad_mask=None, src: Optional[KVSource] = None):
@@ -1438,6 +1455,14 @@ def encode_sparse(encoder, values, index, pad_mask=None):
 
 
 def _encode(encoder, src: KVSource, pad_mask):
+    _SEED_POOL.update(armed=True, t=None, i=0)
+    try:
+        return _encode_layers(encoder, src, pad_mask)
+    finally:
+        _SEED_POOL.update(armed=False, t=None, i=0)
+
+
+def _encode_layers(encoder, src: KVSource, pad_mask):
     lat = encoder.latent.unsqueeze(0)  # (1, N, C): projected once, broadcast inside the kernels
     b = src.x.shape[0]
     n = lat.shape[1]

@@ -132,6 +132,45 @@ def test_device_seed_is_drawn_per_call():
     assert ops.fused._seed(0.0, torch.device("cpu")) is None
 
 
+def test_encoder_pass_draws_one_seed_pool(monkeypatch):
+    """Inside an encoder pass (ops.fused._encode) the fused calls take distinct slots of ONE drawn
+    pool (one generator launch per pass, not per layer); every pass draws a fresh pool; outside a
+    pass each call draws its own seed."""
+    from perceiver_io_amd.models import PerceiverEncoder, TextInputAdapter
+
+    torch.manual_seed(0)
+    enc = PerceiverEncoder(TextInputAdapter(300, 64, 64), (16, 64), 3, num_self_attention_layers_per_block=2,
+                           dropout=0.1).train()
+    x = torch.randint(3, 300, (2, 64))
+    draws = []
+    real = torch.randint
+
+    def counting(*a, **k):
+        draws.append(1)
+        return real(*a, **k)
+
+    monkeypatch.setattr(torch, "randint", counting)
+    seeds = []
+    real_seed = ops.fused._seed
+
+    def spy(p, device):
+        s = real_seed(p, device)
+        if s is not None:
+            seeds.append(s.clone())
+        return s
+
+    monkeypatch.setattr(ops.fused, "_seed", spy)
+    o1 = ops.fused.encoder_forward(enc, x)
+    n1, s1 = len(draws), list(seeds)
+    o2 = ops.fused.encoder_forward(enc, x)
+    assert n1 == 1 and len(draws) == 2, (n1, len(draws))
+    assert len(s1) >= 4 and len({int(t) for t in s1}) == len(s1)  # distinct slots
+    assert not torch.equal(o1, o2)  # a fresh pool: different masks
+    assert not ops.fused._SEED_POOL["armed"]
+    ops.fused._seed(0.1, torch.device("cpu"))
+    assert len(draws) == 3
+
+
 def test_mask_statistics_and_hash_reproducibility():
     seed = torch.tensor([7], dtype=torch.int64)
     m = emulation.row_drop_mask(seed, 3, 0, 512, 64, 0.25)
