@@ -668,7 +668,19 @@ void sb_check_pre_o(const Tensor& o, int R, int C) {
 // [LN1X, QKV, O, LN2Y, U, GU (bf16), Y, Z, mean1, rstd1, mean2, rstd2 (fp32)]; the block output is
 // the last layer's Z.  pre (10 tensors, see sb_fill_pre): the cross layer's post-attention half
 // runs first and WRITES x (its output, the block input); its 6 saved tensors are appended.
-std::vector<Tensor> sb_fwd(Tensor x, std::vector<Tensor> params, double scale, double eps, std::vector<Tensor> pre) {
+// post (4 tensors [γq, βq, wq_bf16 (C, C), bq]): the next cross layer's LN + query projection of the
+// block output; [Q (R, C) bf16, LN_q(z) (R, C) bf16, mean, rstd] are appended (after pre's)
+namespace {
+void sb_fill_post(pio::SBQPath& q, const std::vector<Tensor>& post, int C) {
+  TORCH_CHECK(post.size() == 4, "sample block: post = [γq, βq, wq, bq]");
+  sb_check_v(post[0], C, "post γ"); sb_check_v(post[1], C, "post β"); sb_check_w(post[2], C, C, "post Wq");
+  sb_check_v(post[3], C, "post bq");
+  q.g = f32p(post[0]); q.b = f32p(post[1]); q.Wq = bfp(post[2]); q.bq = f32p(post[3]);
+}
+}  // namespace
+
+std::vector<Tensor> sb_fwd(Tensor x, std::vector<Tensor> params, double scale, double eps, std::vector<Tensor> pre,
+                           std::vector<Tensor> post) {
   const int C = x.dim() == 2 ? (int)x.size(1) : 0;
   TORCH_CHECK(x.is_contiguous() && (C == 64 || C == 128) && x.size(0) % kSBN == 0 && x.size(0) > 0,
               "sb_fwd: x (B·32, C), C ∈ {64, 128}");
@@ -709,6 +721,15 @@ std::vector<Tensor> sb_fwd(Tensor x, std::vector<Tensor> params, double scale, d
     a.has_pre = 1;
     out.insert(out.end(), sv.begin(), sv.end());
   }
+  if (!post.empty()) {
+    sb_fill_post(a.post, post, C);
+    Tensor q = torch::empty({R, C}, b16), lnx = torch::empty({R, C}, b16), mean = torch::empty({R}, f32),
+           rstd = torch::empty({R}, f32);
+    a.post.Q = reinterpret_cast<uint16_t*>(q.data_ptr()); a.post.LNX = reinterpret_cast<uint16_t*>(lnx.data_ptr());
+    a.post.mean = mean.data_ptr<float>(); a.post.rstd = rstd.data_ptr<float>();
+    a.has_post = 1;
+    out.insert(out.end(), {q, lnx, mean, rstd});
+  }
   TORCH_CHECK(pio::sb_fwd_launch(a, C, stream()), "sb_fwd: launch refused");
   return out;
 }
@@ -722,8 +743,11 @@ std::vector<Tensor> sb_fwd(Tensor x, std::vector<Tensor> params, double scale, d
 // [dO (R, C) bf16, δ (R, 4) fp32, dY, dU, dZ (bf16 rows)] are appended; the LayerNorm slab rows
 // are 2C wider (the pre stage's dγ2 | dβ2 last).  zero_out: an fp32 buffer of 4k elements the
 // kernel clears (the cross attention backward's accumulators)
+// post (as sb_fwd's) + post_io [dQ (R, C) fp32, dres (R, C) fp32, mean, rstd (sb_fwd's)]: the query
+// path's backward runs first, dz is then unused; [dQ bf16 rows] is appended, the slab rows 2C wider
 std::vector<Tensor> sb_bwd(Tensor dz, Tensor x0, std::vector<Tensor> saved, std::vector<Tensor> params, double scale,
-                           double eps, std::vector<Tensor> pre, std::vector<Tensor> pre_saved, OptT zero_out) {
+                           double eps, std::vector<Tensor> pre, std::vector<Tensor> pre_saved, OptT zero_out,
+                           std::vector<Tensor> post, std::vector<Tensor> post_io) {
   const int C = x0.dim() == 2 ? (int)x0.size(1) : 0;
   TORCH_CHECK(dz.is_contiguous() && x0.is_contiguous() && dz.sizes() == x0.sizes() && (C == 64 || C == 128) &&
                   x0.size(0) % kSBN == 0 && x0.size(0) > 0,
@@ -741,8 +765,8 @@ std::vector<Tensor> sb_bwd(Tensor dz, Tensor x0, std::vector<Tensor> saved, std:
   a.eps = (float)eps;
   Tensor dx = torch::empty({R, C}, f32);
   a.dX = dx.data_ptr<float>();
-  const bool hp = !pre.empty();
-  a.ln_rs = 4 * L * C + (hp ? 2 * C : 0);
+  const bool hp = !pre.empty(), hq = !post.empty();
+  a.ln_rs = 4 * L * C + (hp ? 2 * C : 0) + (hq ? 2 * C : 0);
   Tensor lns = torch::empty({(int64_t)a.B, (int64_t)a.ln_rs}, f32);  // every element stored by the kernel
   std::vector<Tensor> out{dx, lns};
   for (int i = 0; i < L; ++i) {
@@ -774,6 +798,24 @@ std::vector<Tensor> sb_bwd(Tensor dz, Tensor x0, std::vector<Tensor> saved, std:
     g.dg2 = lp; g.dbe2 = lp + C;
     a.has_pre = 1;
     out.insert(out.end(), {dO, delta, dy, du, dzz});
+  }
+  if (hq) {
+    sb_fill_post(a.post, post, C);
+    TORCH_CHECK(post_io.size() == 4, "sb_bwd: post_io = [dQ, dres, mean, rstd]");
+    for (int k = 0; k < 4; ++k) {
+      CHECK_DT(post_io[k], torch::kFloat32);
+      TORCH_CHECK(post_io[k].is_contiguous() && post_io[k].numel() == (k < 2 ? (int64_t)R * C : R) &&
+                      (reinterpret_cast<uintptr_t>(post_io[k].data_ptr()) & 15) == 0,
+                  "sb_bwd: post_io tensor ", k, " must be contiguous fp32 (R, C) / (R)");
+    }
+    a.post.dQ = f32p(post_io[0]); a.post.dres = f32p(post_io[1]);
+    a.post.mean = post_io[2].data_ptr<float>(); a.post.rstd = post_io[3].data_ptr<float>();
+    Tensor dqb = torch::empty({R, C}, b16);
+    a.post.dQb = reinterpret_cast<uint16_t*>(dqb.data_ptr());
+    float* lp = lns.data_ptr<float>() + (int64_t)(4 * L + (hp ? 2 : 0)) * C;
+    a.post.dg = lp; a.post.db = lp + C;
+    a.has_post = 1;
+    out.push_back(dqb);
   }
   if (zero_out.has_value()) {
     CHECK_DT(*zero_out, torch::kFloat32);
@@ -1854,10 +1896,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("p") = 0.0);
   m.def("persist_errors", &persist_errors, py::arg("reset") = true);
   m.def("sb_fwd", &sb_fwd, py::arg("x"), py::arg("params"), py::arg("scale"), py::arg("eps"),
-        py::arg("pre") = std::vector<Tensor>{});
+        py::arg("pre") = std::vector<Tensor>{}, py::arg("post") = std::vector<Tensor>{});
   m.def("sb_bwd", &sb_bwd, py::arg("dz"), py::arg("x0"), py::arg("saved"), py::arg("params"),
         py::arg("scale"), py::arg("eps"), py::arg("pre") = std::vector<Tensor>{},
-        py::arg("pre_saved") = std::vector<Tensor>{}, py::arg("zero_out") = py::none());
+        py::arg("pre_saved") = std::vector<Tensor>{}, py::arg("zero_out") = py::none(),
+        py::arg("post") = std::vector<Tensor>{}, py::arg("post_io") = std::vector<Tensor>{});
   m.def("sb_wgrad", &sb_wgrad, py::arg("jobs"), py::arg("job_slab") = py::none(),
         py::arg("job_dsts") = std::vector<Tensor>(), py::arg("job_offs") = std::vector<int64_t>());
   m.def("post_attn_ln_linear_fwd", &post_attn_ln_linear_fwd, py::arg("o"), py::arg("x"), py::arg("wo"), py::arg("bo"),

@@ -277,6 +277,11 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
     stage_vec(v + 8 * C, y.b1, C);
     stage_vec(v + 9 * C, y.b2, C);
   }
+  if (a.has_post) {  // the query path's γ | β | bias (slot kSBMaxLayers, columns 0 .. 3C)
+    stage_vec(sVec[kSBMaxLayers], a.post.g, C);
+    stage_vec(sVec[kSBMaxLayers] + C, a.post.b, C);
+    stage_vec(sVec[kSBMaxLayers] + 2 * C, a.post.bq, C);
+  }
   float x[16];
   bf16x8 wq[3][KS];
   if (a.has_pre) {
@@ -460,6 +465,8 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
       load_wtile<C>(wq[0], a.ly[li + 1].Wqkv, n0);
       load_wtile<C>(wq[1], a.ly[li + 1].Wqkv, C + n0);
       load_wtile<C>(wq[2], a.ly[li + 1].Wqkv, 2 * C + n0);
+    } else if (a.has_post) {  // the query path's weight
+      load_wtile<C>(wq[0], a.post.Wq, n0);
     }
     st_bf16(sS, LDS3, r, n0, t);  // U (the QKV rows were copied out behind the last barrier)
     lds_sync();
@@ -480,6 +487,30 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
   }
   lds_sync();
   copy_rows<C>(a.ly[a.L - 1].Z, C, sF, LDF);
+  if (a.has_post) {
+    // ---- post: the next cross layer's LN + query projection of the block output ----
+    const float* vec = sVec[kSBMaxLayers];
+    float mu, rs, gv[16], bv[16], t[16];
+    ln_stats<C>(x, sRed, a.eps, mu, rs);
+    ld_vec(gv, vec, n0);
+    ld_vec(bv, vec + C, n0);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t[i] = (x[i] - mu) * rs * gv[i] + bv[i];
+    if (w == 0 && l < 32) { a.post.mean[row] = mu; a.post.rstd[row] = rs; }
+    st_bf16(sImg[0], LDI, r, n0, t);
+    lds_sync();
+    copy_rows<C>(a.post.LNX, C, sImg[0], LDI);
+    {
+      float bb[16];
+      const f32x16 acc = gemm_t<C>(wq[0], sImg[0], LDI);
+      ld_vec(bb, vec + 2 * C, n0);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) t[i] = acc[i] + bb[i];
+    }
+    st_bf16(sImg[1], LDI, r, n0, t);
+    lds_sync();
+    copy_rows<C>(a.post.Q, C, sImg[1], LDI);
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -537,6 +568,7 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
     stage_vec(sG[li][1], a.ly[li].g2, C);
   }
   if (a.has_pre) stage_vec(sG[kSBMaxLayers][1], a.pre.g2, C);
+  if (a.has_post) stage_vec(sG[kSBMaxLayers][0], a.post.g, C);
   if (a.zero_p != nullptr) {  // this workgroup's slice of the cross attention backward's accumulators
     const long long per = (a.zero_n4 + gridDim.x - 1) / gridDim.x;
     const long long z0 = (long long)blockIdx.x * per, z1 = z0 + per < a.zero_n4 ? z0 + per : a.zero_n4;
@@ -544,9 +576,41 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
       reinterpret_cast<float4*>(a.zero_p)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   float dz[16];
-  ld_f32(dz, a.dZ, C, row, n0);
   bf16x8 pw[KS];
-  wblock_load<C>(pw, a.ly[a.L - 1].W2, 0);
+  if (a.has_post) {
+    // ---- post: the next cross layer's query-path backward: dz = dres + LN_q backward of dQ·Wq ----
+    const SBQPath& q = a.post;
+    wblock_load<C>(pw, q.Wq, 0);
+    float dqv[16], xz[16];
+    ld_f32(dqv, q.dQ, C, row, n0);
+    ld_f32(xz, a.ly[a.L - 1].Z, C, row, n0);
+    ld_f32(dz, q.dres, C, row, n0);
+    const float mu = q.mean[row], rs = q.rstd[row];
+    st_bf16(sImg[0], LDI, r, n0, dqv);
+    wblock_store<C>(sW[1], pw);
+    wblock_load<C>(pw, a.ly[a.L - 1].W2, 0);
+    lds_sync();  // (also publishes the staged γ vectors)
+    copy_rows<C>(q.dQb, C, sImg[0], LDI);
+    const f32x16 acc = gemm_tt<C>(sW[1], n0, sImg[0], LDI, 0, f32x16{});
+    float gv[16], gg[16], t[16], s1 = 0.f, s2 = 0.f;
+    ld_vec(gv, sG[kSBMaxLayers][0], n0);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      t[i] = acc[i];               // dXn
+      xz[i] = (xz[i] - mu) * rs;   // x̂
+      gg[i] = acc[i] * gv[i];
+      s1 += gg[i];
+      s2 += gg[i] * xz[i];
+    }
+    const float2 sm = row_sums2<C>(s1, s2, sRed);  // (its barrier: every read of sImg[0] / sW[1] done)
+    const float m1 = sm.x * (1.f / C), m2 = sm.y * (1.f / C);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dz[i] += rs * (gg[i] - m1 - xz[i] * m2);
+    ln_affine_grads(t, xz, q.dg + lnr, q.db + lnr, n0);
+  } else {
+    ld_f32(dz, a.dZ, C, row, n0);
+    wblock_load<C>(pw, a.ly[a.L - 1].W2, 0);
+  }
   // Every phase issues its global loads (the next weight block, the layer's saved rows) BEFORE its
   // global stores: vmcnt counts both in issue order, so a load issued behind a phase's stores
   // would make its consumer wait for all of them

@@ -16,6 +16,21 @@ struct SBLayer {
   uint16_t *LN1X, *QKV, *O, *LN2Y, *U, *GU;    // bf16 rows: LN1(x), packed QKV, attention out, LN2(y), W1 out, GELU
   float *Y, *Z, *mean1, *rstd1, *mean2, *rstd2;  // fp32: residual after attention, layer output, LN stats
 };
+// post (has_post): the LayerNorm + query projection of the cross-attention layer after the block
+// (its query path, model.py:48-74 q = LN_q(z)·Wqᵀ + bq over the block output z).  Forward epilogue:
+// Q (bf16 rows), the LN statistics and LN_q(z) (bf16 rows, the dWq operand).  Backward prologue:
+// the block's output gradient is dres + LN_q backward of dQ·Wq (dQ fp32 rows in), with the dQ rows
+// (bf16, the dWq operand) and the LN_q affine partials (slab) out.
+struct SBQPath {
+  const uint16_t* Wq;  // bf16 [C][C]
+  const float *bq, *g, *b;
+  uint16_t *Q, *LNX;   // forward: bf16 rows out
+  float *mean, *rstd;  // forward: LN statistics out (backward: in)
+  const float* dQ;     // backward: fp32 rows in
+  const float* dres;   // backward: the residual-path gradient of z (fp32 rows in)
+  uint16_t* dQb;       // backward: bf16 rows out
+  float *dg, *db;      // backward: LN_q affine partials (slab row base)
+};
 // pre (has_pre): the post-attention half of the cross-attention layer in front of the block
 // (model.py:36-44 applied to the cross layer's attention output): z0 = y + MLP(LN2(y)),
 // y = Wo·O + bo + x_q.  Its Wo / W1 / W2 / bo / γ2 / β2 / b1 / b2 and saved LN2Y / U / GU / Y /
@@ -28,6 +43,8 @@ struct SBFwdArgs {
   const float* preX;      // pre: the residual rows x_q, (B·32, C) or (32, C) broadcast
   int preX_bs;            // pre: rows between two samples' residual rows (32, or 0: broadcast)
   int has_pre;
+  SBQPath post;
+  int has_post;
   int L, B;
   float scale_log2, eps;
 };
@@ -57,6 +74,8 @@ struct SBBwdArgs {
   float* zero_p;
   long long zero_n4;
   int has_pre;
+  SBQPath post;        // has_post: dZ is then unused (dres + the query path's LN backward)
+  int has_post;
   int L, B;
   int ln_rs;         // row stride of the LayerNorm partial slab (floats)
   float scale_log2, eps;

@@ -778,7 +778,7 @@ def _sb_pre_fwd(pre, R, C, eps):
     return z, [ln2y.to(bf), u.to(bf), gu.to(bf), y, mean2, rstd2]
 
 
-def sb_fwd(x, params, scale, eps, pre=()):
+def sb_fwd(x, params, scale, eps, pre=(), post=()):
     """pre (10 tensors): the cross layer's post-attention half first; x (the block input) is
     written with its output and its 6 saved tensors are appended."""
     R, C = x.shape
@@ -811,17 +811,37 @@ def sb_fwd(x, params, scale, eps, pre=()):
         out += [ln1x.to(bf), qkv.to(bf), o.to(bf), ln2y.to(bf), u.to(bf), gu.to(bf), y, z, mean1, rstd1, mean2, rstd2]
         del p
         x = z
-    return out + pre_saved
+    post_out = []
+    if post:  # the next cross layer's LN + query projection of the block output
+        g, b, wq, bq = post
+        t, mean, rstd = _ln(x, g, b, eps)
+        lnx = _bf(t)
+        q = _bf(lnx @ wq.float().t() + bq)
+        post_out = [q.to(torch.bfloat16), lnx.to(torch.bfloat16), mean, rstd]
+    return out + pre_saved + post_out
 
 
-def sb_bwd(dz, x0, saved, params, scale, eps, pre=(), pre_saved=(), zero_out=None):
+def sb_bwd(dz, x0, saved, params, scale, eps, pre=(), pre_saved=(), zero_out=None, post=(), post_io=()):
     R, C = x0.shape
     B = R // _SB_N
     L = len(params) // 12
     grads = [None] * L
-    lns = torch.empty(B, 4 * L * C + (2 * C if pre else 0), dtype=torch.float32, device=x0.device)
+    lns = torch.empty(B, 4 * L * C + (2 * C if pre else 0) + (2 * C if post else 0), dtype=torch.float32,
+                      device=x0.device)
     if zero_out is not None:
         zero_out.zero_()
+    post_tail = []
+    if post:  # the next cross layer's query-path backward first: dz = dres + LN_q backward of dQ·Wq
+        g, _, wq, _ = post
+        dq, dres, mean, rstd = post_io
+        dqb = _bf(dq.float())
+        dxn = dqb @ wq.float()
+        dxl, xh = _ln_bwd(dxn, saved[12 * (L - 1) + 7], mean, rstd, g)
+        o = (4 * L + (2 if pre else 0)) * C
+        lns[:, o:o + C] = (dxn * xh).view(B, _SB_N, C).sum(1)
+        lns[:, o + C:o + 2 * C] = dxn.view(B, _SB_N, C).sum(1)
+        dz = dres.float() + dxl
+        post_tail = [dqb.to(torch.bfloat16)]
 
     def per_sample(t):  # (B·32, C) → the sample sums (B, C)
         return t.view(B, _SB_N, C).sum(1)
@@ -879,7 +899,7 @@ def sb_bwd(dz, x0, saved, params, scale, eps, pre=(), pre_saved=(), zero_out=Non
     out = [dz, lns]
     for g in grads:
         out += g
-    return out + tail
+    return out + tail + post_tail
 
 
 def sb_wgrad(jobs, job_slab=None, job_dsts=(), job_offs=()):

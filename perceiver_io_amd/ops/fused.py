@@ -1146,6 +1146,8 @@ def sa_block_lookahead(block, rows: int, n: Optional[int] = None, device=None):
 # a cross-attention layer's post-attention half folded into the per-sample block after it
 # (PIO_SB_PRE=0: the cross layer runs it, A/B)
 SB_PRE = os.environ.get("PIO_SB_PRE", "1") != "0"
+# the next cross layer's LN + query projection in the per-sample block's kernels (PIO_SB_POST=0: A/B)
+SB_POST = os.environ.get("PIO_SB_POST", "1") != "0"
 
 
 def sample_block_runs(block, b: int, n: int, device) -> bool:
@@ -1226,19 +1228,33 @@ class _SampleBlockFn(torch.autograd.Function):
         scale = 1.0 / math.sqrt(C // specs[0].heads)
         hp = _LOOKAHEAD["have_pa"]
         ctx.pa = None
+        pre = []
         if hp is not None and hp["key"] == xl.data_ptr():
             # the preceding cross layer's post-attention half: x is its placeholder output, written
             # by this launch before the block's first layer reads it
             _LOOKAHEAD["have_pa"] = None
-            saved = K.sb_fwd(xl, params, scale, EPS, pre=hp["pre"])
             ctx.pa = hp
-            ctx.pre_saved = saved[12 * L:]
-            saved = saved[:12 * L]
-        else:
-            saved = K.sb_fwd(xl, params, scale, EPS)
+            pre = hp["pre"]
+        # the next cross layer's LN + query projection of the block output (its backward comes
+        # back as "bwd_q" and runs first in this block's backward)
+        wq_n = _LOOKAHEAD["want_q"] if SB_POST else None
+        post = [wq_n[0], wq_n[1], wq_n[2], wq_n[3]] if wq_n is not None and wq_n[2].shape == (C, C) else []
+        saved = K.sb_fwd(xl, params, scale, EPS, pre=pre, post=post)
+        ctx.pre_saved = saved[12 * L:12 * L + 6] if pre else None
+        ctx.post, ctx.post_saved = (post, saved[-3:]) if post else (None, None)
+        if post:
+            _LOOKAHEAD["want_q"] = None
+        post_q = saved[-4] if post else None
+        saved = saved[:12 * L]
         z = saved[12 * (L - 1) + 7]
-        # the block output is not a backward operand: a placeholder in its slot
-        ctx.save_for_backward(xl, *saved[:12 * (L - 1) + 7], xl, *saved[12 * (L - 1) + 8:])
+        if post:
+            _LOOKAHEAD["have_q"] = (z, post_q, ctx.post_saved[1], ctx.post_saved[2], post[0])
+            ctx.out_ptr = z.data_ptr()
+            # the block output is the query path's LayerNorm input: kept for the backward
+            ctx.save_for_backward(xl, *saved)
+        else:
+            # the block output is not a backward operand: a placeholder in its slot
+            ctx.save_for_backward(xl, *saved[:12 * (L - 1) + 7], xl, *saved[12 * (L - 1) + 8:])
         ctx.params, ctx.ps, ctx.dims = params, ps, (B, N, C, L, scale)
         return z.view(B, N, C)
 
@@ -1261,15 +1277,26 @@ class _SampleBlockFn(torch.autograd.Function):
             return g.view(-1)
 
         pa = ctx.pa
+        hq = None
+        if ctx.post is not None:
+            hq, _LOOKAHEAD["bwd_q"] = _LOOKAHEAD["bwd_q"], None
+            if hq is not None and hq["key"] != ctx.out_ptr:
+                raise RuntimeError("fused encoder: a cross-attention layer handed its query-path backward to the "
+                                   "wrong per-sample block")
+        kw = {}
+        if hq is not None:
+            _, mean_q, rstd_q = ctx.post_saved
+            kw = dict(post=ctx.post, post_io=[hq["g"], hq["dres"], mean_q, rstd_q])
+        zb = None
         if pa is not None:
             # the cross layer's post-attention backward last: its dO / δ and cleared accumulators go
             # to that layer's backward, the returned gradient is its residual path dY
             zb = _cross_zero_bufs(pa["ctx"], dz.device)
-            out = K.sb_bwd(dz2, xl, saved, ctx.params, scale, EPS, pre=pa["pre"], pre_saved=ctx.pre_saved,
-                           zero_out=zb[0])
+            kw.update(pre=pa["pre"], pre_saved=ctx.pre_saved, zero_out=zb[0])
+        out = K.sb_bwd(dz2, xl, saved, ctx.params, scale, EPS, **kw)
+        dqb = out.pop() if hq is not None else None
+        if pa is not None:
             _LOOKAHEAD["bwd_pa"] = dict(key=pa["key"], do=out[-5], delta=out[-4], zbuf=zb)
-        else:
-            out = K.sb_bwd(dz2, xl, saved, ctx.params, scale, EPS)
         # the per-sample LayerNorm affine partials (B, 4·L·C [+ 2C]): summed into the gradients by
         # the grouped weight-gradient launch's appended workgroups (or a deferred slab reduction)
         dsts, offs = [], []
@@ -1289,6 +1316,16 @@ class _SampleBlockFn(torch.autograd.Function):
                                (dzz, sv[5], p[10], p[11])):
                 if W.requires_grad or b.requires_grad:
                     jobs += [G, A, target(W, W.numel()), target(b, b.numel())]
+        if hq is not None:  # the query path: LN_q affine partials after the pre stage's, dWq / dbq
+            o = (4 * L + (2 if pa is not None else 0)) * C
+            for j in range(2):
+                if hq["ll_dsts"][j] is not None:
+                    dsts.append(hq["ll_dsts"][j])
+                    offs.append(o + j * C)
+            if hq["ll_dsts"][2] is not None or hq["ll_dsts"][3] is not None:
+                jobs += [dqb, ctx.post_saved[0],
+                         hq["ll_dsts"][2] if hq["ll_dsts"][2] is not None else torch.zeros(C * C, device=dz.device),
+                         hq["ll_dsts"][3] if hq["ll_dsts"][3] is not None else torch.zeros(C, device=dz.device)]
         if pa is not None:
             Wo, bo, g2, be2, W1, b1, W2, b2 = pa["ps"]
             for j, q in enumerate((g2, be2)):
@@ -1476,7 +1513,8 @@ def _encode_layers(encoder, src: KVSource, pad_mask):
         # the block's first LN1 + QKV projection rides on the cross layer's post-attention kernel,
         # or a per-sample block runs that post-attention half itself
         _LOOKAHEAD["want"] = sa_block_lookahead(block, b * n, n, lat.device) if can_fuse(cross, src) else None
-        _LOOKAHEAD["want_pa"] = can_fuse(cross, src) and sample_block_runs(block, b, n, lat.device)
+        sb_runs = sample_block_runs(block, b, n, lat.device)
+        _LOOKAHEAD["want_pa"] = can_fuse(cross, src) and sb_runs
         try:
             lat = cross_attention_layer(cross, lat, src, pad_mask)
         finally:
@@ -1485,7 +1523,7 @@ def _encode_layers(encoder, src: KVSource, pad_mask):
             lat = lat.expand(b, -1, -1)
         nxt_cross = layers[li + 1][0] if li + 1 < len(layers) else None
         if nxt_cross is not None and can_fuse(nxt_cross, src):
-            _LOOKAHEAD["want_q"] = cross_q_lookahead(nxt_cross, src)
+            _LOOKAHEAD["want_q"] = cross_q_lookahead(nxt_cross, src, sample_block=sb_runs)
         elif nxt_cross is None:  # a decoder's K/V over the encoder output, when its caller asked for it
             _LOOKAHEAD["want_q"] = _LOOKAHEAD["want_kv"]
         if li == 0 and len(layers) > 1:  # DDP: layer_1's block gradients (but its first LN1/QKV) final here
@@ -1519,11 +1557,12 @@ def decoder_kv_lookahead(cross):
     return (ps[2], ps[3], wkv, bin_[spec.C:])
 
 
-def cross_q_lookahead(cross, src):
+def cross_q_lookahead(cross, src, sample_block: bool = False):
     """(γq, βq, Wq bf16 (C, C), bq) of a cross-attention layer's query path, for the preceding
-    self-attention block's last kernel (C = 64, H = 4: the fused layer kernel's shape)."""
+    self-attention block's last kernel (C = 64, H = 4: the fused layer kernel's shape; a per-sample
+    block (sample_block): C ∈ {64, 128}, any head count)."""
     spec, ps = layer_spec_and_params(cross)
-    if not spec.cross or spec.C != 64 or spec.heads != 4:
+    if not spec.cross or (spec.C not in (64, 128) if sample_block else (spec.C != 64 or spec.heads != 4)):
         return None
     bw = _bf16_weights(spec, ps)
     bin_ = ps[5] if spec.packed else ps[7]

@@ -295,7 +295,7 @@ def test_cross_self_attention_boundary_fusion(latents, monkeypatch):
             mp.setattr(ops.fused, "kernels", lambda t: Counting())
             if not fuse:
                 mp.setattr(ops.fused, "sa_block_lookahead", lambda block, rows, *a: None)
-                mp.setattr(ops.fused, "cross_q_lookahead", lambda cross, src: None)
+                mp.setattr(ops.fused, "cross_q_lookahead", lambda cross, src, **kw: None)
             calls.clear()
             enc.zero_grad(set_to_none=True)
             out = ops.fused.encoder_forward(enc, x, pad)

@@ -1,5 +1,7 @@
 """The encoder cross-attention layer's post-attention half folded into the per-sample block after it
-(ops/fused.py "want_pa" / "have_pa" / "bwd_pa"; csrc/sample_block.hip pre stage), run on the CPU
+(ops/fused.py "want_pa" / "have_pa" / "bwd_pa"; csrc/sample_block.hip pre stage) and the next cross
+layer's LN + query projection into the block before it ("want_q" / "have_q" / "bwd_q"; the post
+stage), run on the CPU
 through the kernel emulation with the per-sample block routing forced on (it needs CUDA tensors
 otherwise): same outputs and gradients as the unfolded executor and as eager fp32, and the folded
 layers launch no post-attention kernels of their own."""
@@ -43,6 +45,7 @@ def test_cross_post_attention_folded_into_sample_block(c, cross_heads, monkeypat
         with monkeypatch.context() as mp:
             mp.setattr(ops.fused, "kernels", lambda t: Counting())
             mp.setattr(ops.fused, "SB_PRE", fold)
+            mp.setattr(ops.fused, "SB_POST", fold)
             calls.clear()
             enc.zero_grad(set_to_none=True)
             out = ops.fused.encoder_forward(enc, x, None)
@@ -55,6 +58,9 @@ def test_cross_post_attention_folded_into_sample_block(c, cross_heads, monkeypat
     folded = 3 if cross_heads == 4 else 0
     assert c0.get("post_attn_fwd", 0) == 3 and c1.get("post_attn_fwd", 0) == 3 - folded, (c0, c1)
     assert c0.get("post_attn_bwd", 0) == 3 and c1.get("post_attn_bwd", 0) == 3 - folded, (c0, c1)
+    # the query paths of the 2nd and 3rd cross layers run in the preceding blocks' kernels
+    assert c0["ln_linear_fwd"] - c1["ln_linear_fwd"] == 2, (c0, c1)
+    assert c0["ln_linear_bwd"] - c1["ln_linear_bwd"] == 2, (c0, c1)
     assert set(g0) == set(g1) == set(g_ref)
     torch.testing.assert_close(o1, o0, rtol=2e-3, atol=2e-3 * o0.abs().max().item())
     gmax = max(g.abs().max() for g in g_ref.values())
