@@ -452,36 +452,6 @@ def _pe_proj_grads(D, part, nc, pe, g, b, W):
     return dW, S, (W * G).sum(0), torch.mv(W.t(), S)
 
 
-# the factored PE projection's weight gradients of a cross-attention layer's last backward
-# application on a side stream (PIO_PE_SIDE=0: in line); not while a data-parallel reducer is armed
-# (its ready points order their collectives after the main stream only)
-PE_SIDE = os.environ.get("PIO_PE_SIDE", "1") != "0"
-_PE_SIDE_STREAMS = {}
-
-
-def _pe_side_stream(device):
-    if not PE_SIDE or device.type != "cuda":
-        return None
-    from ..parallel import reducer as _red
-
-    if any(r.armed for r in _red._ACTIVE):
-        return None
-    st = _PE_SIDE_STREAMS.get(device.index)
-    if st is None:
-        st = _PE_SIDE_STREAMS[device.index] = torch.cuda.Stream(device)
-    return st
-
-
-def _join_at_backward_end(cur, side):
-    """``cur`` waits for ``side`` once the current backward pass has run (or now, outside one)."""
-    def join():
-        cur.wait_stream(side)
-    try:
-        torch.autograd.Variable._execution_engine.queue_callback(join)
-    except RuntimeError:
-        join()
-
-
 def _cross_zero_bufs(ctx, device):
     """(zbuf, dq_pre, d_pre) of a fused cross-attention layer's backward: the attention backward's
     atomically accumulated dQ — and, for the first backward application of a PE layer whose batch
@@ -836,22 +806,9 @@ class _LayerFn(torch.autograd.Function):
                         return t[0] if rep_mode else t
 
                     gbias = gb(bin_)
-                    pe_args = (Dm, part, ebf, ps[5].detach(), ps[6].detach(), g_kv.detach(), b_kv.detach(), nc,
+                    K.pe_grads(Dm, part, ebf, ps[5].detach(), ps[6].detach(), g_kv.detach(), b_kv.detach(), nc,
                                tg(ps[5]), tg(ps[6]), gbias[0, C:3 * C] if rep_mode else gbias[C:3 * C], tg(g_kv),
                                tg(b_kv))
-                    side = _pe_side_stream(dz.device)
-                    if side is not None:
-                        # nothing else in the backward reads these gradients: they run on a side
-                        # stream beside the next (per-sample) blocks' kernels, joined at its end
-                        cur = torch.cuda.current_stream(dz.device)
-                        side.wait_stream(cur)
-                        with torch.cuda.stream(side):
-                            K.pe_grads(*pe_args)
-                        for t in (Dm, part, ebf):
-                            t.record_stream(side)
-                        _join_at_backward_end(cur, side)
-                    else:
-                        K.pe_grads(*pe_args)
                 elif WGRAD_SLAB and Rkv < TALL_ROWS:
                     sl = _GradSlab(Rkv, [Ckv, Ckv, 2 * C * Ckv, 2 * C], dz2)
                     src = ctx.src
