@@ -15,6 +15,10 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
+# an RCCL failure (e.g. the one abort seen in round 5 inside test_rccl_collectives_inside_the_step_graph,
+# which printed no reason) names its cause on stderr
+os.environ.setdefault("NCCL_DEBUG", "WARN")
+
 pytestmark = pytest.mark.gpu
 
 STEPS = 5
