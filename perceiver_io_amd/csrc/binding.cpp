@@ -672,10 +672,12 @@ void sb_check_pre_o(const Tensor& o, int R, int C) {
 // block output; [Q (R, C) bf16, LN_q(z) (R, C) bf16, mean, rstd] are appended (after pre's)
 namespace {
 void sb_fill_post(pio::SBQPath& q, const std::vector<Tensor>& post, int C) {
-  TORCH_CHECK(post.size() == 4, "sample block: post = [γq, βq, wq, bq]");
-  sb_check_v(post[0], C, "post γ"); sb_check_v(post[1], C, "post β"); sb_check_w(post[2], C, C, "post Wq");
-  sb_check_v(post[3], C, "post bq");
-  q.g = f32p(post[0]); q.b = f32p(post[1]); q.Wq = bfp(post[2]); q.bq = f32p(post[3]);
+  TORCH_CHECK(post.size() == 4, "sample block: post = [γ, β, w (N, C) bf16, bias (N)], N ∈ {C, 2C}");
+  const int N = post[2].dim() == 2 ? (int)post[2].size(0) : 0;
+  TORCH_CHECK(N == C || N == 2 * C, "sample block: the post projection has C or 2C outputs");
+  sb_check_v(post[0], C, "post γ"); sb_check_v(post[1], C, "post β"); sb_check_w(post[2], N, C, "post W");
+  sb_check_v(post[3], N, "post bias");
+  q.N = N; q.g = f32p(post[0]); q.b = f32p(post[1]); q.Wq = bfp(post[2]); q.bq = f32p(post[3]);
 }
 }  // namespace
 
@@ -723,7 +725,7 @@ std::vector<Tensor> sb_fwd(Tensor x, std::vector<Tensor> params, double scale, d
   }
   if (!post.empty()) {
     sb_fill_post(a.post, post, C);
-    Tensor q = torch::empty({R, C}, b16), lnx = torch::empty({R, C}, b16), mean = torch::empty({R}, f32),
+    Tensor q = torch::empty({R, (int64_t)a.post.N}, b16), lnx = torch::empty({R, C}, b16), mean = torch::empty({R}, f32),
            rstd = torch::empty({R}, f32);
     a.post.Q = reinterpret_cast<uint16_t*>(q.data_ptr()); a.post.LNX = reinterpret_cast<uint16_t*>(lnx.data_ptr());
     a.post.mean = mean.data_ptr<float>(); a.post.rstd = rstd.data_ptr<float>();
@@ -801,16 +803,19 @@ std::vector<Tensor> sb_bwd(Tensor dz, Tensor x0, std::vector<Tensor> saved, std:
   }
   if (hq) {
     sb_fill_post(a.post, post, C);
-    TORCH_CHECK(post_io.size() == 4, "sb_bwd: post_io = [dQ, dres, mean, rstd]");
+    TORCH_CHECK(post_io.size() == 4, "sb_bwd: post_io = [dQ, dres (or empty), mean, rstd]");
+    const bool has_dres = post_io[1].numel() > 0;
     for (int k = 0; k < 4; ++k) {
+      if (k == 1 && !has_dres) continue;
+      const int64_t want = k == 0 ? (int64_t)R * a.post.N : (k == 1 ? (int64_t)R * C : R);
       CHECK_DT(post_io[k], torch::kFloat32);
-      TORCH_CHECK(post_io[k].is_contiguous() && post_io[k].numel() == (k < 2 ? (int64_t)R * C : R) &&
+      TORCH_CHECK(post_io[k].is_contiguous() && post_io[k].numel() == want &&
                       (reinterpret_cast<uintptr_t>(post_io[k].data_ptr()) & 15) == 0,
-                  "sb_bwd: post_io tensor ", k, " must be contiguous fp32 (R, C) / (R)");
+                  "sb_bwd: post_io tensor ", k, " must be contiguous fp32 (R, N) / (R, C) / (R)");
     }
-    a.post.dQ = f32p(post_io[0]); a.post.dres = f32p(post_io[1]);
+    a.post.dQ = f32p(post_io[0]); a.post.dres = has_dres ? f32p(post_io[1]) : nullptr;
     a.post.mean = post_io[2].data_ptr<float>(); a.post.rstd = post_io[3].data_ptr<float>();
-    Tensor dqb = torch::empty({R, C}, b16);
+    Tensor dqb = torch::empty({R, (int64_t)a.post.N}, b16);
     a.post.dQb = reinterpret_cast<uint16_t*>(dqb.data_ptr());
     float* lp = lns.data_ptr<float>() + (int64_t)(4 * L + (hp ? 2 : 0)) * C;
     a.post.dg = lp; a.post.db = lp + C;

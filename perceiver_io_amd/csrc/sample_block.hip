@@ -280,7 +280,7 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
   if (a.has_post) {  // the query path's γ | β | bias (slot kSBMaxLayers, columns 0 .. 3C)
     stage_vec(sVec[kSBMaxLayers], a.post.g, C);
     stage_vec(sVec[kSBMaxLayers] + C, a.post.b, C);
-    stage_vec(sVec[kSBMaxLayers] + 2 * C, a.post.bq, C);
+    stage_vec(sVec[kSBMaxLayers] + 2 * C, a.post.bq, a.post.N);  // (≤ 4C: below the pre stage's 5C ..)
   }
   float x[16];
   bf16x8 wq[3][KS];
@@ -465,8 +465,9 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
       load_wtile<C>(wq[0], a.ly[li + 1].Wqkv, n0);
       load_wtile<C>(wq[1], a.ly[li + 1].Wqkv, C + n0);
       load_wtile<C>(wq[2], a.ly[li + 1].Wqkv, 2 * C + n0);
-    } else if (a.has_post) {  // the query path's weight
+    } else if (a.has_post) {  // the query path's weight (K and V tiles for a 2C-wide projection)
       load_wtile<C>(wq[0], a.post.Wq, n0);
+      if (a.post.N == 2 * C) load_wtile<C>(wq[1], a.post.Wq, C + n0);
     }
     st_bf16(sS, LDS3, r, n0, t);  // U (the QKV rows were copied out behind the last barrier)
     lds_sync();
@@ -500,16 +501,19 @@ __global__ __launch_bounds__(2 * C) void sb_fwd_kernel(SBFwdArgs a) {
     st_bf16(sImg[0], LDI, r, n0, t);
     lds_sync();
     copy_rows<C>(a.post.LNX, C, sImg[0], LDI);
-    {
+    auto out_tile = [&](const bf16x8(&wt)[KS], int j) {  // output tile j·C + n0 → the row image
       float bb[16];
-      const f32x16 acc = gemm_t<C>(wq[0], sImg[0], LDI);
-      ld_vec(bb, vec + 2 * C, n0);
+      const f32x16 acc = gemm_t<C>(wt, sImg[0], LDI);
+      ld_vec(bb, vec + 2 * C + j * C, n0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) t[i] = acc[i] + bb[i];
-    }
-    st_bf16(sImg[1], LDI, r, n0, t);
+      st_bf16(sS, LDS3, r, j * C + n0, t);
+    };
+    out_tile(wq[0], 0);
+    if (a.post.N == 2 * C) out_tile(wq[1], 1);
     lds_sync();
-    copy_rows<C>(a.post.Q, C, sImg[1], LDI);
+    if (a.post.N == C) copy_rows<C>(a.post.Q, C, sS, LDS3);
+    else copy_rows<2 * C>(a.post.Q, 2 * C, sS, LDS3);
   }
 }
 
@@ -580,18 +584,30 @@ __global__ __launch_bounds__(2 * C) void sb_bwd_kernel(SBBwdArgs a) {
   if (a.has_post) {
     // ---- post: the next cross layer's query-path backward: dz = dres + LN_q backward of dQ·Wq ----
     const SBQPath& q = a.post;
+    const bool two = q.N == 2 * C;
     wblock_load<C>(pw, q.Wq, 0);
-    float dqv[16], xz[16];
-    ld_f32(dqv, q.dQ, C, row, n0);
+    float dqv[16], dqv1[16], xz[16];
+    ld_f32(dqv, q.dQ, q.N, row, n0);
+    if (two) ld_f32(dqv1, q.dQ, q.N, row, C + n0);
     ld_f32(xz, a.ly[a.L - 1].Z, C, row, n0);
-    ld_f32(dz, q.dres, C, row, n0);
+    if (q.dres != nullptr) ld_f32(dz, q.dres, C, row, n0);
+    else
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dz[i] = 0.f;
     const float mu = q.mean[row], rs = q.rstd[row];
-    st_bf16(sImg[0], LDI, r, n0, dqv);
+    st_bf16(sQ, LDQ, r, n0, dqv);
+    if (two) st_bf16(sQ, LDQ, r, C + n0, dqv1);
     wblock_store<C>(sW[1], pw);
+    if (two) {  // the V block of the weight into the other buffer (free until the first layer)
+      wblock_load<C>(pw, q.Wq, C);
+      wblock_store<C>(sW[0], pw);
+    }
     wblock_load<C>(pw, a.ly[a.L - 1].W2, 0);
     lds_sync();  // (also publishes the staged γ vectors)
-    copy_rows<C>(q.dQb, C, sImg[0], LDI);
-    const f32x16 acc = gemm_tt<C>(sW[1], n0, sImg[0], LDI, 0, f32x16{});
+    if (two) copy_rows<2 * C>(q.dQb, 2 * C, sQ, LDQ);
+    else copy_rows<C>(q.dQb, C, sQ, LDQ);
+    f32x16 acc = gemm_tt<C>(sW[1], n0, sQ, LDQ, 0, f32x16{});
+    if (two) acc = gemm_tt<C>(sW[0], n0, sQ, LDQ, C, acc);
     float gv[16], gg[16], t[16], s1 = 0.f, s2 = 0.f;
     ld_vec(gv, sG[kSBMaxLayers][0], n0);
 #pragma unroll

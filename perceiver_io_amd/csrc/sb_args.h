@@ -22,12 +22,13 @@ struct SBLayer {
 // the block's output gradient is dres + LN_q backward of dQ·Wq (dQ fp32 rows in), with the dQ rows
 // (bf16, the dWq operand) and the LN_q affine partials (slab) out.
 struct SBQPath {
-  const uint16_t* Wq;  // bf16 [C][C]
+  int N;               // outputs: C (a query projection) or 2C (a decoder's packed K | V projection)
+  const uint16_t* Wq;  // bf16 [N][C]
   const float *bq, *g, *b;
   uint16_t *Q, *LNX;   // forward: bf16 rows out
   float *mean, *rstd;  // forward: LN statistics out (backward: in)
   const float* dQ;     // backward: fp32 rows in
-  const float* dres;   // backward: the residual-path gradient of z (fp32 rows in)
+  const float* dres;   // backward: the other gradient of z (fp32 rows in; nullptr: none)
   uint16_t* dQb;       // backward: bf16 rows out
   float *dg, *db;      // backward: LN_q affine partials (slab row base)
 };

@@ -31,7 +31,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from ..parallel.reducer import bucket_ready_point
+from ..parallel.reducer import bucket_ready_point, ready_point_armed
 from ..utils.tokenizer import MASK_TOKEN, SPECIAL_TOKENS, UNK_TOKEN
 from .adapters import InputAdapter, OutputAdapter
 from .blocks import Sequential, cross_attention_layer, init_latent_, self_attention_block
@@ -157,8 +157,18 @@ class PerceiverIO(Sequential):
     def loss(self, x, labels, pad_mask=None):
         """Training loss of a classifier: ``cross_entropy(self(x, pad_mask), labels)`` computed
         through the decoder's fused head (same value and gradients)."""
-        x_latent, _ = self.encoder(x, pad_mask)
-        return self.decoder.loss(x_latent, labels)
+        look = ops.fused._LOOKAHEAD
+        # on the fused path the encoder's last per-sample block also projects the decoder's K/V
+        # (and runs that projection's backward, unless a DDP ready point on the decoder input needs
+        # the decoder's gradients final before the encoder backward)
+        look["want_kv"] = (ops.fused.decoder_kv_lookahead(
+            self.decoder.cross_attention, sample_block=True,
+            backward=not ready_point_armed(self.decoder, "decoder")) if ops.use_hip(x) else None)
+        try:
+            x_latent, _ = self.encoder(x, pad_mask)
+            return self.decoder.loss(x_latent, labels)
+        finally:
+            look["want_kv"] = look["have_q"] = None
 
     @property
     def encoder(self) -> PerceiverEncoder:

@@ -452,6 +452,20 @@ def _pe_proj_grads(D, part, nc, pe, g, b, W):
     return dW, S, (W * G).sum(0), torch.mv(W.t(), S)
 
 
+_ZERO_STAND_INS = {}
+
+
+def _zero_stand_in(r: int, c: int, device) -> torch.Tensor:
+    """A persistent (r, c) fp32 zero tensor returned as an input gradient a later kernel overwrites
+    in effect (it only adds it): never written, so one tensor serves every step (no fill launch;
+    the reference kept here also stops autograd from accumulating into it in place)."""
+    key = (r, c, str(device))
+    t = _ZERO_STAND_INS.get(key)
+    if t is None:
+        t = _ZERO_STAND_INS[key] = torch.zeros((r, c), device=device, dtype=torch.float32)
+    return t
+
+
 def _cross_zero_bufs(ctx, device):
     """(zbuf, dq_pre, d_pre) of a fused cross-attention layer's backward: the attention backward's
     atomically accumulated dQ — and, for the first backward application of a PE layer whose batch
@@ -519,6 +533,7 @@ class _LayerFn(torch.autograd.Function):
             ent = src.entries.get(key) if src is not None else None
             ctx.kv_owner = ent is None
             if ent is None:  # first application of this layer: project K/V (LN over [pixels ‖ PE] if split)
+                kv_sb = False
                 factored = (PE_FACTORED and src is not None and src.pe is not None and src.index is None
                             and not spec.packed
                             and not ctx.needs_input_grad[6] and 1 <= xkv2.shape[1] <= 4 and 2 * C <= 512)
@@ -538,15 +553,17 @@ class _LayerFn(torch.autograd.Function):
                     if (src is None and hk is not None and hk[4] is g_kv and hk[0].data_ptr() == xkv2.data_ptr()
                             and hk[0].numel() == xkv2.numel()):
                         # K/V of a decoder over the encoder output: computed by the encoder's last
-                        # self-attention kernel (its backward stays here: plain ln_linear_bwd)
+                        # self-attention kernel.  Its backward stays here (plain ln_linear_bwd) unless
+                        # that kernel was a per-sample block offering to run it (hk[5])
                         kv, mean_kv, rstd_kv = hk[1:4]
+                        kv_sb = len(hk) > 5 and bool(hk[5]) and spec.packed and ctx.needs_input_grad[6]
                         _LOOKAHEAD["have_q"] = None
                     else:
                         kv, mean_kv, rstd_kv = K.ln_linear_fwd(xkv2, g_kv, b_kv, EPS, wkv, bin_[C:], 0, None, True,
                                                                True, src.pe if src is not None else None,
                                                                g_kv.shape[0], _pe_index(src))
                 ent = {"kv": kv, "mean": mean_kv, "rstd": rstd_kv, "dkv": None, "factored": factored, "wkv": wkv,
-                       "implicit": imp}
+                       "implicit": imp, "sb_bwd": kv_sb}
                 if src is not None:
                     src.entries[key] = ent
             kv, mean_kv, rstd_kv = ent["kv"], ent["mean"], ent["rstd"]
@@ -785,7 +802,17 @@ class _LayerFn(torch.autograd.Function):
                 dx_q = K.ln_linear_bwd(dq2, wq, xq2, mean_q, rstd_q, g_q, b_q, dres, True, gb(g_q), gb(b_q), gwq,
                                        rows(gb(bin_), 0, C, 1), **q_out)
             dx_kv = None
-            if ctx.kv_owner:  # the projection's backward, once, over the summed dK/dV
+            if ctx.kv_owner and ent.get("sb_bwd") and ent.get("pe_D") is None:
+                # a decoder's K/V projected by the encoder's last per-sample block: that block runs
+                # this LN + K|V projection backward first in its own backward (sample_block.hip post
+                # stage, 2C wide) and the gradient of its output arrives there; the input gradient
+                # returned here is a zero stand-in the block adds (no fill launch)
+                _LOOKAHEAD["bwd_q"] = dict(key=xkv2.data_ptr(), g=dkv.view(B * M, 2 * C), dres=None,
+                                           ll_dsts=[flat(g_kv), flat(b_kv), flat(ps[4], C * C, 3 * C * C),
+                                                    flat(bin_, C, 3 * C)])
+                dx_kv = _zero_stand_in(B * M, Ckv, dkv.device)
+                ent["dkv"] = None
+            elif ctx.kv_owner:  # the projection's backward, once, over the summed dK/dV
                 if ent.get("pe_D") is not None:
                     dkv2, Rkv = None, B * M
                 else:
@@ -1148,6 +1175,8 @@ def sa_block_lookahead(block, rows: int, n: Optional[int] = None, device=None):
 SB_PRE = os.environ.get("PIO_SB_PRE", "1") != "0"
 # the next cross layer's LN + query projection in the per-sample block's kernels (PIO_SB_POST=0: A/B)
 SB_POST = os.environ.get("PIO_SB_POST", "1") != "0"
+# ... and a decoder's K|V projection into the encoder's last block (PerceiverIO.loss; A/B knob)
+SB_KV = os.environ.get("PIO_SB_KV", "1") != "0"
 
 
 def sample_block_runs(block, b: int, n: int, device) -> bool:
@@ -1238,7 +1267,9 @@ class _SampleBlockFn(torch.autograd.Function):
         # the next cross layer's LN + query projection of the block output (its backward comes
         # back as "bwd_q" and runs first in this block's backward)
         wq_n = _LOOKAHEAD["want_q"] if SB_POST else None
-        post = [wq_n[0], wq_n[1], wq_n[2], wq_n[3]] if wq_n is not None and wq_n[2].shape == (C, C) else []
+        # (a decoder's K|V projection: a (2C, C) weight, the backward offered when wq_n[4])
+        post = ([wq_n[0], wq_n[1], wq_n[2], wq_n[3]]
+                if wq_n is not None and tuple(wq_n[2].shape) in ((C, C), (2 * C, C)) else [])
         saved = K.sb_fwd(xl, params, scale, EPS, pre=pre, post=post)
         ctx.pre_saved = saved[12 * L:12 * L + 6] if pre else None
         ctx.post, ctx.post_saved = (post, saved[-3:]) if post else (None, None)
@@ -1248,7 +1279,8 @@ class _SampleBlockFn(torch.autograd.Function):
         saved = saved[:12 * L]
         z = saved[12 * (L - 1) + 7]
         if post:
-            _LOOKAHEAD["have_q"] = (z, post_q, ctx.post_saved[1], ctx.post_saved[2], post[0])
+            _LOOKAHEAD["have_q"] = (z, post_q, ctx.post_saved[1], ctx.post_saved[2], post[0],
+                                    len(wq_n) > 4 and bool(wq_n[4]))
             ctx.out_ptr = z.data_ptr()
             # the block output is the query path's LayerNorm input: kept for the backward
             ctx.save_for_backward(xl, *saved)
@@ -1286,7 +1318,10 @@ class _SampleBlockFn(torch.autograd.Function):
         kw = {}
         if hq is not None:
             _, mean_q, rstd_q = ctx.post_saved
-            kw = dict(post=ctx.post, post_io=[hq["g"], hq["dres"], mean_q, rstd_q])
+            # a decoder's K/V path hands no residual: the gradient arriving here (its zero stand-in
+            # plus any other consumer's) is the residual
+            dres = hq["dres"] if hq["dres"] is not None else dz2
+            kw = dict(post=ctx.post, post_io=[hq["g"], dres, mean_q, rstd_q])
         zb = None
         if pa is not None:
             # the cross layer's post-attention backward last: its dO / δ and cleared accumulators go
@@ -1323,9 +1358,10 @@ class _SampleBlockFn(torch.autograd.Function):
                     dsts.append(hq["ll_dsts"][j])
                     offs.append(o + j * C)
             if hq["ll_dsts"][2] is not None or hq["ll_dsts"][3] is not None:
+                Nq = dqb.shape[1]  # C (a query projection) or 2C (a decoder's K|V)
                 jobs += [dqb, ctx.post_saved[0],
-                         hq["ll_dsts"][2] if hq["ll_dsts"][2] is not None else torch.zeros(C * C, device=dz.device),
-                         hq["ll_dsts"][3] if hq["ll_dsts"][3] is not None else torch.zeros(C, device=dz.device)]
+                         hq["ll_dsts"][2] if hq["ll_dsts"][2] is not None else torch.zeros(Nq * C, device=dz.device),
+                         hq["ll_dsts"][3] if hq["ll_dsts"][3] is not None else torch.zeros(Nq, device=dz.device)]
         if pa is not None:
             Wo, bo, g2, be2, W1, b1, W2, b2 = pa["ps"]
             for j, q in enumerate((g2, be2)):
@@ -1540,21 +1576,26 @@ def _encode_layers(encoder, src: KVSource, pad_mask):
     return lat
 
 
-def decoder_kv_lookahead(cross):
-    """(γkv, βkv, Wkv bf16 (2C, C), bkv) of a decoder cross-attention over the encoder's latents, for
-    the encoder's last self-attention kernel (C = 64, H = 4 latents: the fused layer kernel's
-    shape), or None.  Set by the caller for the duration of one encoder + decoder call only
-    (PerceiverMLM.loss), so the stashed K/V never outlives it."""
+def decoder_kv_lookahead(cross, sample_block: bool = False, backward: bool = False):
+    """(γkv, βkv, Wkv bf16 (2C, C), bkv[, backward]) of a decoder cross-attention over the encoder's
+    latents, for the encoder's last self-attention kernel (C = 64, H = 4 latents: the fused layer
+    kernel's shape; a per-sample block (sample_block): C ∈ {64, 128}), or None.  backward: that
+    block may also run the projection's backward (packed in-projection only; the caller passes False
+    while a DDP ready point on the decoder input is armed — the decoder's gradients must be final
+    when it fires).  Set by the caller for the duration of one encoder + decoder call only
+    (PerceiverMLM.loss, PerceiverIO.loss), so the stashed K/V never outlives it."""
+    if sample_block and not SB_KV:
+        return None
     spec, ps = layer_spec_and_params(cross)
-    if not spec.cross or spec.C != 64 or ps[2].shape[0] != 64:
+    if not spec.cross or spec.C not in ((64, 128) if sample_block else (64,)) or ps[2].shape[0] != spec.C:
         return None
     wkv = _bf16_weights(spec, ps)[1]
     if wkv is None:
         wkv = _kv_weight(spec, ps)
     bin_ = ps[5] if spec.packed else ps[7]
-    if not wkv.is_contiguous() or tuple(wkv.shape) != (2 * spec.C, 64):
+    if not wkv.is_contiguous() or tuple(wkv.shape) != (2 * spec.C, spec.C):
         return None
-    return (ps[2], ps[3], wkv, bin_[spec.C:])
+    return (ps[2], ps[3], wkv, bin_[spec.C:], backward and spec.packed)
 
 
 def cross_q_lookahead(cross, src, sample_block: bool = False):

@@ -64,6 +64,13 @@ class _ReadyFn(torch.autograd.Function):
         return g, None, None
 
 
+def ready_point_armed(module: torch.nn.Module, name: str) -> bool:
+    """Whether ready point ``name`` of ``module`` would fire in this step's backward (an armed
+    reducer planned it): gradients of that range must then be final when the point's gradient
+    arrives, so a caller may not defer part of their computation past it."""
+    return any(red.armed and red.owns_point(module, name) for red in _ACTIVE)
+
+
 def bucket_ready_point(x: torch.Tensor, module: torch.nn.Module, name: str) -> torch.Tensor:
     """Mark ``x`` as ready point ``name`` of the armed reducer that planned ``module``."""
     if not _ACTIVE or not torch.is_grad_enabled() or not x.requires_grad:

@@ -68,3 +68,58 @@ def test_cross_post_attention_folded_into_sample_block(c, cross_heads, monkeypat
     for n in g0:
         assert (g1[n] - g0[n]).abs().max() < 0.01 * gmax, n
         assert (g1[n] - g_ref[n]).abs().max() < 0.03 * gmax, n
+
+
+@pytest.mark.parametrize("c", [64, 128])
+def test_decoder_kv_folded_into_last_sample_block(c, monkeypatch):
+    """An image classifier's decoder K|V projection (LN_kv + the 2C-wide in-projection rows) runs
+    in the encoder's last per-sample block both ways ("want_kv" → the post stage with N = 2C): same
+    loss and gradients as the unfolded executor and eager fp32, one LN + projection kernel fewer
+    each way; with a DDP ready point armed on the decoder input only the forward is folded."""
+    from perceiver_io_amd.ops import emulation, ext
+    from perceiver_io_amd.parallel import reducer as red_mod
+
+    torch.manual_seed(c + 1)
+    model = _model(c, 3, 2)
+    x = torch.randn(3, 28, 28, 1)
+    y = torch.tensor([1, 7, 3])
+    ref = torch.nn.functional.cross_entropy(model(x), y)
+    ref.backward()
+    g_ref = {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
+    ok = ops.fused._sample_block_ok
+    monkeypatch.setattr(ops.fused, "_sample_block_ok", lambda specs, n, p, cuda: ok(specs, n, p, True))
+    monkeypatch.setattr(ext, "_mod", emulation)
+    monkeypatch.setattr(ops, "use_hip", lambda t: True)
+    calls = {}
+
+    class Counting:
+        def __getattr__(self, name):
+            calls[name] = calls.get(name, 0) + 1
+            return getattr(emulation, name)
+
+    monkeypatch.setattr(ops.fused, "kernels", lambda t: Counting())
+    res = []
+    for fold, armed in ((False, False), (True, False), (True, True)):
+        with monkeypatch.context() as mp:
+            mp.setattr(ops.fused, "SB_POST", fold)
+            mp.setattr(red_mod, "ready_point_armed", lambda m, n: armed)
+            mp.setattr("perceiver_io_amd.models.perceiver.ready_point_armed", lambda m, n: armed)
+            calls.clear()
+            model.zero_grad(set_to_none=True)
+            loss = model.loss(x, y)
+            loss.backward()
+            res.append((loss.detach(), {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None},
+                        dict(calls)))
+            assert ops.fused._LOOKAHEAD["bwd_q"] is None and ops.fused._LOOKAHEAD["have_q"] is None
+    (l0, g0, c0), (l1, g1, c1), (l2, g2, c2) = res
+    # unfolded: 2 next-cross query paths + the decoder's query and K/V paths
+    assert c0["ln_linear_fwd"] - c1["ln_linear_fwd"] == 3, (c0, c1)
+    assert c0["ln_linear_bwd"] - c1["ln_linear_bwd"] == 3, (c0, c1)
+    assert c2["ln_linear_fwd"] == c1["ln_linear_fwd"] and c2["ln_linear_bwd"] == c1["ln_linear_bwd"] + 1, (c1, c2)
+    gmax = max(g.abs().max() for g in g_ref.values())
+    for l_, g_ in ((l1, g1), (l2, g2)):
+        assert abs(l_.item() - l0.item()) < 2e-3 * max(1.0, abs(l0.item()))
+        assert set(g_) == set(g0) == set(g_ref)
+        for n in g0:
+            assert (g_[n] - g0[n]).abs().max() < 0.01 * gmax, n
+            assert (g_[n] - g_ref[n]).abs().max() < 0.03 * gmax, n
