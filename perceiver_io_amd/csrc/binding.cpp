@@ -125,7 +125,8 @@ bool embed_bwd_local_launch(const int64_t*, const float*, float*, float*, int, i
                             hipStream_t);
 void text_mask_launch(const int64_t*, const bool*, int64_t*, int64_t*, int64_t*, long long, int, int, float, int,
                       uint32_t, int, hipStream_t);
-int stage_step_launch(void* const*, const void* const*, const long long*, int, float*, const float*, int, hipStream_t);
+int stage_step_launch(void* const*, const void* const*, const long long*, int, float*, const float*, int, long long*,
+                      const long long*, int, hipStream_t);
 void sumsq_launch(const float*, long long, float*, hipStream_t);
 void index_add_rows_launch(float*, long long, const int64_t*, const float*, long long, int, hipStream_t);
 void gather_rows_launch(float*, const float*, long long, const int64_t*, long long, int, hipStream_t);
@@ -1379,7 +1380,9 @@ std::vector<Tensor> text_mask(Tensor x, OptT pad, Tensor state, int64_t unk, int
 
 // one launch per replayed step: dsts[i] <- srcs[i] (same device, dtype-agnostic byte copies of
 // contiguous tensors of equal size) and hyper_dst[:len(hyper)] <- hyper (values by kernel argument)
-void stage_step(std::vector<Tensor> dsts, std::vector<Tensor> srcs, OptT hyper_dst, std::vector<double> hyper) {
+// seed_dst + seeds: a captured step's dropout seed slots (int64, ≤ 64 values) written in the same launch
+void stage_step(std::vector<Tensor> dsts, std::vector<Tensor> srcs, OptT hyper_dst, std::vector<double> hyper,
+                OptT seed_dst, std::vector<int64_t> seeds) {
   TORCH_CHECK(dsts.size() == srcs.size() && dsts.size() <= 8 && hyper.size() <= 8, "stage_step: at most 8 tensors / 8 values");
   std::vector<void*> d;
   std::vector<const void*> x;
@@ -1401,7 +1404,17 @@ void stage_step(std::vector<Tensor> dsts, std::vector<Tensor> srcs, OptT hyper_d
     TORCH_CHECK(hyper_dst->is_contiguous() && hyper_dst->numel() >= (int64_t)hv.size(), "stage_step: hyper_dst too small");
     hp = hyper_dst->data_ptr<float>();
   }
-  TORCH_CHECK(pio::stage_step_launch(d.data(), x.data(), n.data(), (int)d.size(), hp, hv.data(), (int)hv.size(), stream()) == 0);
+  long long* sp = nullptr;
+  if (!seeds.empty()) {
+    TORCH_CHECK(seed_dst.has_value() && seed_dst->is_cuda() && seed_dst->is_contiguous() &&
+                    seed_dst->scalar_type() == torch::kInt64 && seed_dst->numel() >= (int64_t)seeds.size() &&
+                    seeds.size() <= 64,
+                "stage_step: seed_dst must be a contiguous int64 device tensor of >= len(seeds) (<= 64) slots");
+    sp = reinterpret_cast<long long*>(seed_dst->data_ptr<int64_t>());
+  }
+  std::vector<long long> sv(seeds.begin(), seeds.end());
+  TORCH_CHECK(pio::stage_step_launch(d.data(), x.data(), n.data(), (int)d.size(), hp, hv.data(), (int)hv.size(), sp,
+                                     sv.data(), (int)sv.size(), stream()) == 0);
 }
 
 void sumsq(Tensor g, Tensor out) { pio::sumsq_launch(f32p(g), g.numel(), out.data_ptr<float>(), stream()); }
@@ -1940,7 +1953,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pixel_ce_fwd", &pixel_ce_fwd);
   m.def("pixel_ce_bwd", &pixel_ce_bwd);
   m.def("stage_step", &stage_step, py::arg("dsts"), py::arg("srcs"), py::arg("hyper_dst") = py::none(),
-        py::arg("hyper") = std::vector<double>{});
+        py::arg("hyper") = std::vector<double>{}, py::arg("seed_dst") = py::none(),
+        py::arg("seeds") = std::vector<int64_t>{});
   m.def("ce_fwd", &ce_fwd, py::arg("h"), py::arg("idx"), py::arg("labels"), py::arg("w"), py::arg("bias"),
         py::arg("count"), py::arg("zero_out") = py::none(), py::arg("count_labels") = false);
   m.def("ce_bwd", &ce_bwd, py::arg("h"), py::arg("labels"), py::arg("w"), py::arg("bias"),

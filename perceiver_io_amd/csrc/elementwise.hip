@@ -578,7 +578,7 @@ void cast_bf16_launch(const float* x, uint16_t* y, long long n, hipStream_t st) 
 // 16-byte units, the others byte-wise.
 // ------------------------------------------------------------------------------------------
 namespace pio {
-constexpr int kStageSegs = 8, kStageHyper = 8;
+constexpr int kStageSegs = 8, kStageHyper = 8, kStageSeeds = 64;
 struct StageArgs {
   void* dst[kStageSegs];
   const void* src[kStageSegs];
@@ -588,11 +588,15 @@ struct StageArgs {
   float* hyper_dst;
   float hyper[kStageHyper];
   int nhyper;
+  long long* seed_dst;  // a captured step's dropout seed slots (ops/fused.py static seeds)
+  long long seeds[kStageSeeds];
+  int nseeds;
 };
 
 __global__ __launch_bounds__(256) void stage_step_kernel(StageArgs a) {
   const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x, nt = (long long)gridDim.x * blockDim.x;
   if (blockIdx.x == 0 && threadIdx.x < a.nhyper && a.hyper_dst != nullptr) a.hyper_dst[threadIdx.x] = a.hyper[threadIdx.x];
+  if (blockIdx.x == 0 && threadIdx.x < a.nseeds) a.seed_dst[threadIdx.x] = a.seeds[threadIdx.x];
   for (int s = 0; s < a.nseg; ++s) {
     if (a.vec[s]) {
       const long long n = a.bytes[s] >> 4;
@@ -608,9 +612,13 @@ __global__ __launch_bounds__(256) void stage_step_kernel(StageArgs a) {
 }
 
 int stage_step_launch(void* const* dst, const void* const* src, const long long* bytes, int nseg, float* hyper_dst,
-                      const float* hyper, int nhyper, hipStream_t st) {
-  if (nseg > kStageSegs || nhyper > kStageHyper) return -1;
+                      const float* hyper, int nhyper, long long* seed_dst, const long long* seeds, int nseeds,
+                      hipStream_t st) {
+  if (nseg > kStageSegs || nhyper > kStageHyper || nseeds > kStageSeeds || (nseeds > 0 && seed_dst == nullptr)) return -1;
   StageArgs a{};
+  a.seed_dst = seed_dst;
+  a.nseeds = nseeds;
+  for (int i = 0; i < nseeds; ++i) a.seeds[i] = seeds[i];
   long long units = 0;
   for (int s = 0; s < nseg; ++s) {
     a.dst[s] = dst[s];

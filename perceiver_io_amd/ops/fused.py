@@ -1391,6 +1391,16 @@ def _seed(p: float, device) -> Optional[torch.Tensor]:
     masks are regenerated, never stored."""
     if p <= 0.0:
         return None
+    st = _STATIC_SEEDS
+    if st["on"] and torch.cuda.is_current_stream_capturing():
+        # a StepEngine capture: this call's own slot of the persistent pool the engine stages
+        # fresh values into before every replay (no generator kernel in the graph, no generator
+        # bookkeeping launches per replay)
+        i = st["n"]
+        if i >= _STATIC_SEED_SLOTS or st["t"] is None or st["t"].device != torch.device(device):
+            raise RuntimeError(f"fused dropout: more than {_STATIC_SEED_SLOTS} seeded calls in one captured step")
+        st["n"] = i + 1
+        return st["t"][i:i + 1]
     pool = _SEED_POOL
     if pool["armed"]:
         # inside one encoder pass: one draw of a small pool serves every fused call of the pass
@@ -1408,6 +1418,25 @@ def _seed(p: float, device) -> Optional[torch.Tensor]:
 # pass always draws a fresh pool: a replayed step graph re-runs that draw; calls outside an
 # encoder pass draw their own seed)
 _SEED_POOL_SIZE = 16
+_STATIC_SEED_SLOTS = 64  # csrc/elementwise.hip kStageSeeds
+_STATIC_SEEDS = {"on": False, "t": None, "n": 0}
+
+
+def begin_static_seeds(device) -> None:
+    """Start a graph capture's static dropout seeds (train/engine.py StepEngine): every seeded
+    fused call captured until end_static_seeds() reads its own slot of one persistent int64
+    pool.  Call OUTSIDE the capture (the pool is allocated here on first use)."""
+    t = _STATIC_SEEDS["t"]
+    if t is None or t.device != torch.device(device):
+        t = torch.zeros(_STATIC_SEED_SLOTS, dtype=torch.int64, device=device)
+    _STATIC_SEEDS.update(on=True, t=t, n=0)
+
+
+def end_static_seeds():
+    """(pool, slots used) of the capture just ended; the engine stages slots [0, used) — fresh
+    random values — in the launch before each replay (stage_step seed_dst / seeds)."""
+    _STATIC_SEEDS["on"] = False
+    return _STATIC_SEEDS["t"], _STATIC_SEEDS["n"]
 _SEED_POOL = {"armed": False, "t": None, "i": 0}
 
 

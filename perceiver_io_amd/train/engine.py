@@ -26,6 +26,7 @@ semantics), so an epoch of pad-to-longest batches needs a handful of graphs, not
 from __future__ import annotations
 
 import os
+import random
 
 from collections import OrderedDict
 from typing import Callable, Dict, Optional
@@ -56,10 +57,11 @@ def _pairs(dst, src, out):
     return out
 
 
-def _stage_step(dst, src, opt=None) -> None:
+def _stage_step(dst, src, opt=None, seeds=None) -> None:
     """Copy a batch into a captured graph's static buffers and (``opt``) stage the optimizer's
-    per-step hyper-parameters, in ONE kernel launch (``stage_step``) for the device-resident
-    tensors; host tensors or odd layouts take ``copy_``."""
+    per-step hyper-parameters and (``seeds`` = (pool, values)) the graph's dropout seeds, in ONE
+    kernel launch (``stage_step``) for the device-resident tensors; host tensors or odd layouts
+    take ``copy_``."""
     from ..ops import ext
 
     pairs = _pairs(dst, src, [])
@@ -71,9 +73,11 @@ def _stage_step(dst, src, opt=None) -> None:
     for d, s in slow:
         d.copy_(s, non_blocking=True)
     hyper = opt is not None and opt.hyper.is_cuda
-    if fast or hyper:
+    if fast or hyper or seeds is not None:
         ext.require().stage_step([d for d, _ in fast], [s for _, s in fast], opt.hyper if hyper else None,
-                                 opt.hyper_values() if hyper else [])
+                                 opt.hyper_values() if hyper else [],
+                                 seed_dst=seeds[0] if seeds is not None else None,
+                                 seeds=seeds[1] if seeds is not None else [])
     if opt is not None and not hyper:
         opt.stage_hyper()
 
@@ -107,12 +111,14 @@ LOSS_RING = 1024
 class _Captured:
     """One captured step: the graph, its static input batch and its static outputs."""
 
-    __slots__ = ("graph", "batch", "loss", "state", "seed_grad", "ring")
+    __slots__ = ("graph", "batch", "loss", "state", "seed_grad", "ring", "drop_seeds")
 
-    def __init__(self, graph, batch, loss, state, seed_grad=None, ring=False):
+    def __init__(self, graph, batch, loss, state, seed_grad=None, ring=False, drop_seeds=None):
         self.graph, self.batch, self.loss, self.state = graph, batch, loss, state
         self.seed_grad = seed_grad  # read by the captured backward: kept alive with the graph
         self.ring = ring  # the captured update copies the loss into the engine's loss ring
+        # (pool, slots): the dropout seed slots the graph reads, restaged before every replay
+        self.drop_seeds = drop_seeds
 
 
 class ClosureGraph:
@@ -179,6 +185,7 @@ class StepEngine:
         self._loss_ring = None  # (LOSS_RING,) fp32: the returned per-step losses of replayed steps
         self._ring_pos = 0
         self.replays = 0
+        self._seed_rng = None  # host stream of the captured graphs' dropout seeds (_stage)
         self._eager_steps = 0
         # every step (eager warmups, capture, replays) runs on ONE dedicated stream: autograd's
         # AccumulateGrad nodes bind to the stream they were created on, and a capture whose
@@ -291,19 +298,28 @@ class StepEngine:
                 opt.loss_out = None
             return loss
 
+        drop_seeds = None
         if self.graph_impl == "closure":
             g = ClosureGraph()
             g.body = body
             g.loss = loss = torch.zeros((), device=self.device)
         else:
+            from ..ops import fused
+
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=self.stream):
-                loss = body()
+            # dropout seeds: static slots staged per replay instead of generator draws in the graph
+            fused.begin_static_seeds(self.device)
+            try:
+                with torch.cuda.graph(g, stream=self.stream):
+                    loss = body()
+            finally:
+                pool, used = fused.end_static_seeds()
+            drop_seeds = (pool, used) if used else None
             if ddp:
                 red.disarm()
         state = self.state_hooks[0]() if self.state_hooks is not None else None
         self.captures += 1
-        return _Captured(g, static, loss, state, one, ring=ring)
+        return _Captured(g, static, loss, state, one, ring=ring, drop_seeds=drop_seeds)
 
     def _graph_for(self, batch, kind: str = "last") -> _Captured:
         """The captured step for this batch's shape (captured on first sight, LRU-cached)."""
@@ -372,7 +388,13 @@ class StepEngine:
             if hyper:
                 self.opt.stage_hyper()
         else:
-            _stage_step(ent.batch, b, self.opt if hyper else None)
+            seeds = None
+            if ent.drop_seeds is not None:
+                pool, used = ent.drop_seeds
+                if self._seed_rng is None:  # host draws: one process-wide stream from torch's seed
+                    self._seed_rng = random.Random(torch.initial_seed() ^ 0x5EED5EED)
+                seeds = (pool, [self._seed_rng.getrandbits(63) for _ in range(used)])
+            _stage_step(ent.batch, b, self.opt if hyper else None, seeds)
 
     def _step_inner(self, batch):
         batches = batch if (self.accumulate > 1 and isinstance(batch, list)) else [batch]

@@ -298,8 +298,8 @@ def test_graph_engine_variable_shapes():
 
 def test_graph_replays_draw_fresh_dropout_masks():
     """Dropout under graph capture: with lr = 0 the parameters never change, so consecutive
-    replays of one graph differ ONLY through the dropout masks — they must differ (device
-    seed drawn inside the graph) — while at p = 0 they are bit-identical."""
+    replays of one graph differ ONLY through the dropout masks — they must differ (seed slots
+    restaged before each replay) — while at p = 0 they are bit-identical."""
     ids = torch.randint(3, 500, (4, 96), device="cuda")
     pad = torch.zeros(4, 96, dtype=torch.bool, device="cuda")
     for p in (0.0, 0.2):
@@ -307,6 +307,10 @@ def test_graph_replays_draw_fresh_dropout_masks():
         lit = _mlm_dropout(p)
         eng = _fixed_mask_engine(lit, True, ids, pad, lr=0.0, warmup=0)
         losses = [eng.step((None, ids, pad)).item() for _ in range(4)]
+        # the seeds are static slots of the graph, restaged with fresh values before each replay
+        # (no generator kernel inside the graph)
+        ent = next(iter(eng._graphs.values()))
+        assert (ent.drop_seeds is not None) == (p > 0), ent.drop_seeds
         if p == 0.0:
             assert len(set(losses)) == 1, losses
         else:
