@@ -777,6 +777,130 @@ __global__ void zero_rows_kernel(float* __restrict__ p, long long bs, int rs, in
 }
 
 // ------------------------------------------------------------------------------------
+// few-key decode attention (a classifier decoder: one query per sample over the 32 latents,
+// head width 64 / 128): one wave per (sample, query, head), lane = key, VALU dot products —
+// the MFMA kernels above spend most of such a call staging 32×32 tiles for one useful row
+// ------------------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(64) void attn_decode_fwd_kernel(AttnArgs a, uint16_t* __restrict__ O,
+                                                             float* __restrict__ LSE) {
+  constexpr int DL = D / 64;  // output dims per lane
+  __shared__ __attribute__((aligned(16))) float sq[D];
+  const int l = threadIdx.x, h = blockIdx.y, qi = blockIdx.x % a.Nq, b = blockIdx.x / a.Nq;
+  const uint16_t* qp = a.q + (long long)b * a.q_bs + (long long)qi * a.q_rs + h * D;
+#pragma unroll
+  for (int i = 0; i < DL; ++i) sq[l + 64 * i] = bf2f(qp[l + 64 * i]);
+  __syncthreads();
+  const bool kv = l < a.Nk;
+  const uint16_t* kp = a.k + (long long)b * a.k_bs + (long long)(kv ? l : 0) * a.k_rs + h * D;
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < D / 8; ++c) {
+    const bf16x8 k8 = *reinterpret_cast<const bf16x8*>(kp + 8 * c);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s = fmaf(sq[8 * c + e], bf2f(k8[e]), s);
+  }
+  s = kv ? s * a.scale_log2 : -INFINITY;
+  float m = s;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  const float p = kv ? exp2f(s - m) : 0.f;
+  float lsum = p;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) lsum += __shfl_xor(lsum, o);
+  float acc[DL];
+#pragma unroll
+  for (int i = 0; i < DL; ++i) acc[i] = 0.f;
+  const uint16_t* vb = a.v + (long long)b * a.v_bs + h * D + l;
+  for (int j = 0; j < a.Nk; ++j) {
+    const float pj = __shfl(p, j);
+#pragma unroll
+    for (int i = 0; i < DL; ++i) acc[i] = fmaf(pj, bf2f(vb[(long long)j * a.v_rs + 64 * i]), acc[i]);
+  }
+  const float inv = 1.f / lsum;
+  const long long row = (long long)b * a.Nq + qi;
+  uint16_t* op = O + row * a.H * D + h * D;
+#pragma unroll
+  for (int i = 0; i < DL; ++i) op[l + 64 * i] = f2bf(acc[i] * inv);
+  if (l == 0) LSE[row * a.H + h] = m + __log2f(lsum);
+}
+
+// its backward for one query per sample (dK / dV rows belong to that query alone): p from the
+// forward's LSE, dP = dO·vⱼ, dS = p (dP − δ); dQ = scale Σⱼ dSⱼ kⱼ, dKⱼ = scale dSⱼ q, dVⱼ = pⱼ dO
+// (stored, or added with kv_acc)
+template <int D>
+__global__ __launch_bounds__(64) void attn_decode_bwd_kernel(AttnArgs a, const uint16_t* __restrict__ dO,
+                                                             const float* __restrict__ LSE,
+                                                             const float* __restrict__ delta, float* __restrict__ dq,
+                                                             long long dq_bs, int dq_rs, float* __restrict__ dk,
+                                                             long long dk_bs, int dk_rs, float* __restrict__ dv,
+                                                             long long dv_bs, int dv_rs, int kv_acc) {
+  constexpr int DL = D / 64;
+  __shared__ __attribute__((aligned(16))) float sq[D], sdo[D];
+  const int l = threadIdx.x, h = blockIdx.y, b = blockIdx.x;
+  const uint16_t* qp = a.q + (long long)b * a.q_bs + h * D;
+  const uint16_t* dop = dO + (long long)b * a.H * D + h * D;
+  float qv[DL], dov[DL];
+#pragma unroll
+  for (int i = 0; i < DL; ++i) {
+    qv[i] = bf2f(qp[l + 64 * i]);
+    dov[i] = bf2f(dop[l + 64 * i]);
+    sq[l + 64 * i] = qv[i];
+    sdo[l + 64 * i] = dov[i];
+  }
+  __syncthreads();
+  const bool kv = l < a.Nk;
+  const int key = kv ? l : 0;
+  const uint16_t* kp = a.k + (long long)b * a.k_bs + (long long)key * a.k_rs + h * D;
+  const uint16_t* vp = a.v + (long long)b * a.v_bs + (long long)key * a.v_rs + h * D;
+  float s = 0.f, dp = 0.f;
+#pragma unroll
+  for (int c = 0; c < D / 8; ++c) {
+    const bf16x8 k8 = *reinterpret_cast<const bf16x8*>(kp + 8 * c);
+    const bf16x8 v8 = *reinterpret_cast<const bf16x8*>(vp + 8 * c);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s = fmaf(sq[8 * c + e], bf2f(k8[e]), s);
+      dp = fmaf(sdo[8 * c + e], bf2f(v8[e]), dp);
+    }
+  }
+  const long long row = (long long)b * a.H + h;
+  const float p = kv ? exp2f(fmaf(s, a.scale_log2, -LSE[row])) : 0.f;
+  const float ds = p * (dp - delta[row]);
+  float dqa[DL];
+#pragma unroll
+  for (int i = 0; i < DL; ++i) dqa[i] = 0.f;
+  const uint16_t* kb = a.k + (long long)b * a.k_bs + h * D + l;
+  float* dkb = dk + (long long)b * dk_bs + h * D + l;
+  float* dvb = dv + (long long)b * dv_bs + h * D + l;
+  for (int j = 0; j < a.Nk; ++j) {
+    const float dsj = __shfl(ds, j), pj = __shfl(p, j);
+#pragma unroll
+    for (int i = 0; i < DL; ++i) {
+      dqa[i] = fmaf(dsj, bf2f(kb[(long long)j * a.k_rs + 64 * i]), dqa[i]);
+      float* dkp = dkb + (long long)j * dk_rs + 64 * i;
+      float* dvp = dvb + (long long)j * dv_rs + 64 * i;
+      const float gk = a.scale * dsj * qv[i], gv = pj * dov[i];
+      *dkp = kv_acc ? *dkp + gk : gk;
+      *dvp = kv_acc ? *dvp + gv : gv;
+    }
+  }
+  float* dqp = dq + (long long)b * dq_bs + h * D + l;
+#pragma unroll
+  for (int i = 0; i < DL; ++i) dqp[64 * i] = a.scale * dqa[i];
+  (void)dq_rs;
+}
+
+// the decode kernels' shapes: head width 64 / 128, ≤ 64 keys, no key mask, no dropout
+static bool decode_ok(const AttnArgs& a, int D) {
+  static const bool on = [] {  // PIO_ATTN_DECODE=1 (opt-in until validated on the GPU)
+    const char* e = getenv("PIO_ATTN_DECODE");
+    return e && e[0] == '1';
+  }();
+  return on && (D == 64 || D == 128) && a.Nk >= 1 && a.Nk <= 64 && a.kmask == nullptr && a.drop_thresh == 0;
+}
+
+// ------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------
 template <int D, int NWV>
@@ -798,6 +922,12 @@ static void fwd_dispatch(const AttnArgs& a, uint16_t* O, float* LSE, float* Opar
 
 void attn_fwd_launch(const AttnArgs& a, int D, uint16_t* O, float* LSE, float* Opart, float* MLpart, int nsplit,
                      hipStream_t st) {
+  if (decode_ok(a, D) && a.Nq <= 4) {  // final O / LSE directly, no split partials
+    const dim3 grid((unsigned)(a.B * a.Nq), (unsigned)a.H);
+    if (D == 128) hipLaunchKernelGGL((attn_decode_fwd_kernel<128>), grid, dim3(64), 0, st, a, O, LSE);
+    else hipLaunchKernelGGL((attn_decode_fwd_kernel<64>), grid, dim3(64), 0, st, a, O, LSE);
+    return;
+  }
   switch (D) {
     case 16: fwd_dispatch<16>(a, O, LSE, Opart, MLpart, nsplit, st); break;
     case 32: fwd_dispatch<32>(a, O, LSE, Opart, MLpart, nsplit, st); break;
@@ -920,6 +1050,16 @@ void attn_bwd_launch(const AttnArgs& a, int D, const uint16_t* O, const uint16_t
   if (compute_delta)
     hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, dO, O, delta, (float*)nullptr,
                        rows, a.H, D, dq_rs);
+  if (decode_ok(a, D) && a.Nq == 1) {  // one query: its dK / dV rows are its own (no sum over queries)
+    const dim3 grid((unsigned)a.B, (unsigned)a.H);
+    if (D == 128)
+      hipLaunchKernelGGL((attn_decode_bwd_kernel<128>), grid, dim3(64), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs, dk,
+                         dk_bs, dk_rs, dv, dv_bs, dv_rs, (int)kv_acc);
+    else
+      hipLaunchKernelGGL((attn_decode_bwd_kernel<64>), grid, dim3(64), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs, dk,
+                         dk_bs, dk_rs, dv, dv_bs, dv_rs, (int)kv_acc);
+    return;
+  }
   switch (D) {  // waves per workgroup: 8 for d ≤ 32, 4 above (keys per block = 32 × waves)
     case 16: bwd_launch_t<16, 8>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, qsplit_ok, dq_zeroed, st); break;
     case 32:  // ≤ 64 keys (the image configs' 32-latent self-attention): 2 waves, not 6 idle of 8
