@@ -812,7 +812,8 @@ __global__ __launch_bounds__(64) void attn_decode_fwd_kernel(AttnArgs a, uint16_
 #pragma unroll
   for (int i = 0; i < DL; ++i) acc[i] = 0.f;
   const uint16_t* vb = a.v + (long long)b * a.v_bs + h * D + l;
-  for (int j = 0; j < a.Nk; ++j) {
+#pragma unroll 8
+  for (int j = 0; j < a.Nk; ++j) {  // unrolled: 8 rows' loads in flight
     const float pj = __shfl(p, j);
 #pragma unroll
     for (int i = 0; i < DL; ++i) acc[i] = fmaf(pj, bf2f(vb[(long long)j * a.v_rs + 64 * i]), acc[i]);
@@ -873,6 +874,7 @@ __global__ __launch_bounds__(64) void attn_decode_bwd_kernel(AttnArgs a, const u
   const uint16_t* kb = a.k + (long long)b * a.k_bs + h * D + l;
   float* dkb = dk + (long long)b * dk_bs + h * D + l;
   float* dvb = dv + (long long)b * dv_bs + h * D + l;
+#pragma unroll 4
   for (int j = 0; j < a.Nk; ++j) {
     const float dsj = __shfl(ds, j), pj = __shfl(p, j);
 #pragma unroll
@@ -892,12 +894,19 @@ __global__ __launch_bounds__(64) void attn_decode_bwd_kernel(AttnArgs a, const u
 }
 
 // the decode kernels' shapes: head width 64 / 128, ≤ 64 keys, no key mask, no dropout
-static bool decode_ok(const AttnArgs& a, int D) {
-  static const bool on = [] {  // PIO_ATTN_DECODE=1 (opt-in until validated on the GPU)
+// PIO_ATTN_DECODE: 0 = off, 1 = backward only (default; head width 128: 9 µs vs 18 µs for the
+// MFMA kernel on the image decoders), 2 = forward and backward (A/B)
+static int decode_mode() {
+  static const int m = [] {
     const char* e = getenv("PIO_ATTN_DECODE");
-    return e && e[0] == '1';
+    return e ? atoi(e) : 1;
   }();
-  return on && (D == 64 || D == 128) && a.Nk >= 1 && a.Nk <= 64 && a.kmask == nullptr && a.drop_thresh == 0;
+  return m;
+}
+static bool decode_ok(const AttnArgs& a, int D, bool fwd) {
+  const int m = decode_mode();
+  return (fwd ? m >= 2 : m >= 1) && D == 128 && a.Nk >= 1 && a.Nk <= 64 && a.kmask == nullptr &&
+         a.drop_thresh == 0;
 }
 
 // ------------------------------------------------------------------------------------
@@ -922,7 +931,7 @@ static void fwd_dispatch(const AttnArgs& a, uint16_t* O, float* LSE, float* Opar
 
 void attn_fwd_launch(const AttnArgs& a, int D, uint16_t* O, float* LSE, float* Opart, float* MLpart, int nsplit,
                      hipStream_t st) {
-  if (decode_ok(a, D) && a.Nq <= 4) {  // final O / LSE directly, no split partials
+  if (decode_ok(a, D, true) && a.Nq <= 4) {  // final O / LSE directly, no split partials
     const dim3 grid((unsigned)(a.B * a.Nq), (unsigned)a.H);
     if (D == 128) hipLaunchKernelGGL((attn_decode_fwd_kernel<128>), grid, dim3(64), 0, st, a, O, LSE);
     else hipLaunchKernelGGL((attn_decode_fwd_kernel<64>), grid, dim3(64), 0, st, a, O, LSE);
@@ -1050,7 +1059,7 @@ void attn_bwd_launch(const AttnArgs& a, int D, const uint16_t* O, const uint16_t
   if (compute_delta)
     hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, dO, O, delta, (float*)nullptr,
                        rows, a.H, D, dq_rs);
-  if (decode_ok(a, D) && a.Nq == 1) {  // one query: its dK / dV rows are its own (no sum over queries)
+  if (decode_ok(a, D, false) && a.Nq == 1) {  // one query: its dK / dV rows are its own (no sum over queries)
     const dim3 grid((unsigned)a.B, (unsigned)a.H);
     if (D == 128)
       hipLaunchKernelGGL((attn_decode_bwd_kernel<128>), grid, dim3(64), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs, dk,
