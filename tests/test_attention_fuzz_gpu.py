@@ -83,3 +83,30 @@ def test_attention_shapes_fuzz(case):
     for a, b, n in zip(ga, gb, ("dq", "dk", "dv")):
         err = _rel(a, b, floor=1e-3)
         assert err < tol, (n, err, case)
+
+
+@pytest.mark.parametrize("D,H,Nk,B,Bq", [(128, 1, 32, 3, 1), (128, 2, 64, 2, 2), (128, 1, 1, 2, 2)])
+def test_decode_attention_shapes(D, H, Nk, B, Bq):
+    """The few-key one-query shapes of the classifier decoders (csrc/attention.hip
+    attn_decode_bwd_kernel for head width 128): the fuzz test's checks at fixed cases, plus the
+    backward accumulating onto existing dK / dV (a weight-shared layer's later application)."""
+    from perceiver_io_amd.ops import emulation, ext
+
+    test_attention_shapes_fuzz.hypothesis.inner_test((D, H, 1, Nk, B, Bq, 1, "none", 7 * D + Nk))
+    if Nk == 1:  # one key: dK is zero up to rounding, nothing to compare an accumulation against
+        return
+    K = ext.require()
+    g = torch.Generator(device=DEV).manual_seed(D + Nk)
+    E = H * D
+    q = torch.randn(Bq, 1, E, device=DEV, generator=g).to(torch.bfloat16)
+    kv = torch.randn(B, Nk, 2 * E, device=DEV, generator=g).to(torch.bfloat16)
+    k, v = kv[:, :, :E], kv[:, :, E:]
+    scale = 1.0 / math.sqrt(D)
+    o, lse = K.attn_fwd(q, k, v, None, H, D, scale, 0.0, None, 1)
+    do = torch.randn(B, 1, E, device=DEV, generator=g).to(torch.bfloat16)
+    dkv = torch.randn(B, Nk, 2 * E, device=DEV, generator=g)
+    base = dkv.clone()
+    K.attn_bwd(q, k, v, None, o, do, lse, None, H, D, scale, 0.0, None, None, dkv[:, :, :E], dkv[:, :, E:], True)
+    ref = emulation.attn_bwd(q, k, v, None, o, do, lse, None, H, D, scale, 0.0, None, None, None, None)
+    assert _rel(dkv[:, :, :E] - base[:, :, :E], ref[1], floor=1e-3) < 1e-2
+    assert _rel(dkv[:, :, E:] - base[:, :, E:], ref[2], floor=1e-3) < 1e-2
