@@ -72,6 +72,11 @@ def parse(argv=None):
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture of the step")
     ap.add_argument("--allreduce-dtype", default="fp32", choices=["fp32", "bf16"],
                     help="gradient all-reduce wire format (N > 1)")
+    ap.add_argument("--overlap", default="on", choices=["on", "off"],
+                    help="N > 1: bucket all-reduces at ready points on a side stream during the backward (on) or "
+                         "all of them after the backward on the compute stream (off)")
+    ap.add_argument("--bucket-update", default="on", choices=["on", "off"],
+                    help="N > 1: AdamW per bucket right behind its all-reduce (on) or one pass after all (off)")
     ap.add_argument("--dense", action="store_true", help="lartpc: evaluate all pixels (the reference's cost)")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--profile-stacks", type=int, default=0,
@@ -331,13 +336,14 @@ def main(argv=None):
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29517")
             tdist.init_process_group("nccl", rank=0, world_size=1, device_id=device)
-        reducer = FlatGradReducer(opt.flat, in_graph=True, force=True)
+        reducer = FlatGradReducer(opt.flat, in_graph=True, force=True, overlap=args.overlap == "on")
         reducer.plan(model)
     if world > 1:
         from perceiver_io_amd.ops.optim import FlatParameterSpace
 
         flat = opt.flat if fused else FlatParameterSpace(params, with_shadow=False, replicate=False)
-        reducer = FlatGradReducer(flat, wire_dtype=torch.bfloat16 if args.allreduce_dtype == "bf16" else None)
+        reducer = FlatGradReducer(flat, wire_dtype=torch.bfloat16 if args.allreduce_dtype == "bf16" else None,
+                                  overlap=args.overlap == "on")
         reducer.plan(model)  # ready points: decoder + head, layer_n — all-reduced during the backward
         reducer.broadcast_parameters(model)
 
@@ -349,7 +355,8 @@ def main(argv=None):
                 return loss_inner(batch)
         return loss_inner(batch)
 
-    engine = StepEngine(loss_fn, opt, sched, reducer=reducer, device=device, graph=fused and not args.no_graph)
+    engine = StepEngine(loss_fn, opt, sched, reducer=reducer, device=device, graph=fused and not args.no_graph,
+                        bucket_update=args.bucket_update == "on")
     g = torch.Generator(device="cpu").manual_seed(99 + info.rank)
 
     def to_dev(b):
@@ -374,6 +381,8 @@ def main(argv=None):
     dt = time.perf_counter() - t0
     dt = pdist.all_reduce_max(dt)
     final_loss = float(loss.float().item())
+    if fused:  # a checked-build index error seen inside the replayed graphs invalidates the run
+        ops.check_device_errors()
     # data parallelism must leave every rank with bitwise the same parameters
     from perceiver_io_amd.parallel.reducer import params_in_sync
 

@@ -27,8 +27,6 @@
 // Both directions stage the next K/V (forward) or Q/dO (backward) tile in registers while
 // the current tile's MFMAs run, so global latency is paid once per kernel, not per tile.
 // Fully-masked query rows produce O = 0 and zero gradients (defect D10 defined).
-#include <stdlib.h>
-
 #include "common.h"
 
 namespace pio {
@@ -777,58 +775,12 @@ __global__ void zero_rows_kernel(float* __restrict__ p, long long bs, int rs, in
 }
 
 // ------------------------------------------------------------------------------------
-// few-key decode attention (a classifier decoder: one query per sample over the 32 latents,
-// head width 64 / 128): one wave per (sample, query, head), lane = key, VALU dot products —
+// few-key decode attention backward (an image classifier's decoder: one query per sample over
+// the 32 latents, head width 128): one wave per (sample, head), lane = key, VALU dot products —
 // the MFMA kernels above spend most of such a call staging 32×32 tiles for one useful row
+// (9.2 vs 17.6 µs at the ImageNet / MNIST decoders; the forward analogue was slower than the MFMA
+// forward, 11.7 vs 10 µs, and is not built: profiles/r5_ab/README.md)
 // ------------------------------------------------------------------------------------
-template <int D>
-__global__ __launch_bounds__(64) void attn_decode_fwd_kernel(AttnArgs a, uint16_t* __restrict__ O,
-                                                             float* __restrict__ LSE) {
-  constexpr int DL = D / 64;  // output dims per lane
-  __shared__ __attribute__((aligned(16))) float sq[D];
-  const int l = threadIdx.x, h = blockIdx.y, qi = blockIdx.x % a.Nq, b = blockIdx.x / a.Nq;
-  const uint16_t* qp = a.q + (long long)b * a.q_bs + (long long)qi * a.q_rs + h * D;
-#pragma unroll
-  for (int i = 0; i < DL; ++i) sq[l + 64 * i] = bf2f(qp[l + 64 * i]);
-  __syncthreads();
-  const bool kv = l < a.Nk;
-  const uint16_t* kp = a.k + (long long)b * a.k_bs + (long long)(kv ? l : 0) * a.k_rs + h * D;
-  float s = 0.f;
-#pragma unroll
-  for (int c = 0; c < D / 8; ++c) {
-    const bf16x8 k8 = *reinterpret_cast<const bf16x8*>(kp + 8 * c);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) s = fmaf(sq[8 * c + e], bf2f(k8[e]), s);
-  }
-  s = kv ? s * a.scale_log2 : -INFINITY;
-  float m = s;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  const float p = kv ? exp2f(s - m) : 0.f;
-  float lsum = p;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) lsum += __shfl_xor(lsum, o);
-  float acc[DL];
-#pragma unroll
-  for (int i = 0; i < DL; ++i) acc[i] = 0.f;
-  const uint16_t* vb = a.v + (long long)b * a.v_bs + h * D + l;
-#pragma unroll 8
-  for (int j = 0; j < a.Nk; ++j) {  // unrolled: 8 rows' loads in flight
-    const float pj = __shfl(p, j);
-#pragma unroll
-    for (int i = 0; i < DL; ++i) acc[i] = fmaf(pj, bf2f(vb[(long long)j * a.v_rs + 64 * i]), acc[i]);
-  }
-  const float inv = 1.f / lsum;
-  const long long row = (long long)b * a.Nq + qi;
-  uint16_t* op = O + row * a.H * D + h * D;
-#pragma unroll
-  for (int i = 0; i < DL; ++i) op[l + 64 * i] = f2bf(acc[i] * inv);
-  if (l == 0) LSE[row * a.H + h] = m + __log2f(lsum);
-}
-
-// its backward for one query per sample (dK / dV rows belong to that query alone): p from the
-// forward's LSE, dP = dO·vⱼ, dS = p (dP − δ); dQ = scale Σⱼ dSⱼ kⱼ, dKⱼ = scale dSⱼ q, dVⱼ = pⱼ dO
-// (stored, or added with kv_acc)
 template <int D>
 __global__ __launch_bounds__(64) void attn_decode_bwd_kernel(AttnArgs a, const uint16_t* __restrict__ dO,
                                                              const float* __restrict__ LSE,
@@ -893,20 +845,9 @@ __global__ __launch_bounds__(64) void attn_decode_bwd_kernel(AttnArgs a, const u
   (void)dq_rs;
 }
 
-// the decode kernels' shapes: head width 64 / 128, ≤ 64 keys, no key mask, no dropout
-// PIO_ATTN_DECODE: 0 = off, 1 = backward only (default; head width 128: 9 µs vs 18 µs for the
-// MFMA kernel on the image decoders), 2 = forward and backward (A/B)
-static int decode_mode() {
-  static const int m = [] {
-    const char* e = getenv("PIO_ATTN_DECODE");
-    return e ? atoi(e) : 1;
-  }();
-  return m;
-}
-static bool decode_ok(const AttnArgs& a, int D, bool fwd) {
-  const int m = decode_mode();
-  return (fwd ? m >= 2 : m >= 1) && D == 128 && a.Nk >= 1 && a.Nk <= 64 && a.kmask == nullptr &&
-         a.drop_thresh == 0;
+// the decode backward's shape: head width 128, one query, ≤ 64 keys, no key mask, no dropout
+static bool decode_bwd_ok(const AttnArgs& a, int D) {
+  return D == 128 && a.Nq == 1 && a.Nk >= 1 && a.Nk <= 64 && a.kmask == nullptr && a.drop_thresh == 0;
 }
 
 // ------------------------------------------------------------------------------------
@@ -931,12 +872,6 @@ static void fwd_dispatch(const AttnArgs& a, uint16_t* O, float* LSE, float* Opar
 
 void attn_fwd_launch(const AttnArgs& a, int D, uint16_t* O, float* LSE, float* Opart, float* MLpart, int nsplit,
                      hipStream_t st) {
-  if (decode_ok(a, D, true) && a.Nq <= 4) {  // final O / LSE directly, no split partials
-    const dim3 grid((unsigned)(a.B * a.Nq), (unsigned)a.H);
-    if (D == 128) hipLaunchKernelGGL((attn_decode_fwd_kernel<128>), grid, dim3(64), 0, st, a, O, LSE);
-    else hipLaunchKernelGGL((attn_decode_fwd_kernel<64>), grid, dim3(64), 0, st, a, O, LSE);
-    return;
-  }
   switch (D) {
     case 16: fwd_dispatch<16>(a, O, LSE, Opart, MLpart, nsplit, st); break;
     case 32: fwd_dispatch<32>(a, O, LSE, Opart, MLpart, nsplit, st); break;
@@ -1009,12 +944,8 @@ static void bwd_launch_t(const AttnArgs& a, const uint16_t* dO, const float* LSE
   dim3 grid(nkb * nqs, a.H, a.B);
   constexpr bool small_lds = true;
   // head width 16, no dropout, a grid wider than the chip: the two-query-tile variant at ≤ 128
-  // VGPRs runs two 8-wave workgroups per CU (PIO_ATTN_QR2W=0: the full-LDS variant, A/B)
-  static const bool qr2w = [] {
-    const char* e = getenv("PIO_ATTN_QR2W");
-    return !(e && e[0] == '0');
-  }();
-  const bool wide = D == 16 && NW == 8 && qr2w && !a.drop_thresh && a.Nq > 64 &&
+  // VGPRs runs two 8-wave workgroups per CU (1.342 → 1.327 ms on the headline step, r5)
+  const bool wide = D == 16 && NW == 8 && !a.drop_thresh && a.Nq > 64 &&
                     (long long)grid.x * grid.y * grid.z > 256;
   if (wide) {
     if (a.kmask == nullptr && a.Nk % (32 * NW) == 0)
@@ -1059,14 +990,10 @@ void attn_bwd_launch(const AttnArgs& a, int D, const uint16_t* O, const uint16_t
   if (compute_delta)
     hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, dO, O, delta, (float*)nullptr,
                        rows, a.H, D, dq_rs);
-  if (decode_ok(a, D, false) && a.Nq == 1) {  // one query: its dK / dV rows are its own (no sum over queries)
+  if (decode_bwd_ok(a, D)) {  // one query: its dK / dV rows are its own (no sum over queries)
     const dim3 grid((unsigned)a.B, (unsigned)a.H);
-    if (D == 128)
-      hipLaunchKernelGGL((attn_decode_bwd_kernel<128>), grid, dim3(64), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs, dk,
-                         dk_bs, dk_rs, dv, dv_bs, dv_rs, (int)kv_acc);
-    else
-      hipLaunchKernelGGL((attn_decode_bwd_kernel<64>), grid, dim3(64), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs, dk,
-                         dk_bs, dk_rs, dv, dv_bs, dv_rs, (int)kv_acc);
+    hipLaunchKernelGGL((attn_decode_bwd_kernel<128>), grid, dim3(64), 0, st, a, dO, LSE, delta, dq, dq_bs, dq_rs, dk,
+                       dk_bs, dk_rs, dv, dv_bs, dv_rs, (int)kv_acc);
     return;
   }
   switch (D) {  // waves per workgroup: 8 for d ≤ 32, 4 above (keys per block = 32 × waves)

@@ -43,15 +43,11 @@ struct SlabJob {
   long long zero_n4;
 };
 }  // namespace pio
-#include "persist_args.h"
 #include "sb_args.h"
 namespace pio {
 bool sb_fwd_launch(const SBFwdArgs&, int C, hipStream_t);
 bool sb_bwd_launch(const SBBwdArgs&, int C, hipStream_t);
 bool sb_wgrad_launch(SBWgradArgs, int C, const SlabJob&, hipStream_t);
-bool sa_block_fwd_launch(const SABlockFwdArgs&, hipStream_t);
-unsigned persist_errors(bool);
-int persist_sync_words(int);
 
 // sizes of the structs above as the kernel translation units see them (checked at import: a
 // mirror that drifts from common.h / attention.hip would hand the kernels garbage pointers)
@@ -500,95 +496,6 @@ std::vector<Tensor> sa_layer_fwd(Tensor qkv, Tensor x, int64_t N, double scale, 
   return {o, lse, z, y, m, r, u};
 }
 
-// sync words of the persistent kernels (csrc/persist.hip): one zero-initialised buffer per
-// (device, stream), allocated on the first launch on that stream (never during a stream capture:
-// nullptr then, the caller runs the per-layer kernels), reset to zero by the last workgroup of
-// every launch — launches on one stream run one after another, so they can share it
-unsigned* persist_sync_buffer(const Tensor& like, int words) {
-  // grown buffers are kept alive too: a captured graph may still name an older one
-  static std::unordered_map<uint64_t, std::vector<Tensor>> bufs;
-  hipStream_t st = stream();
-  const uint64_t key = reinterpret_cast<uint64_t>(st) ^ ((uint64_t)like.get_device() << 56);
-  auto& v = bufs[key];
-  if (!v.empty() && v.back().numel() >= words) return reinterpret_cast<unsigned*>(v.back().data_ptr<int>());
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-  // the zero fill runs on the current stream: ordered before every launch that uses the buffer
-  v.push_back(torch::zeros({std::max(words, 1 << 14)}, like.options().dtype(torch::kInt32)));
-  return reinterpret_cast<unsigned*>(v.back().data_ptr<int>());
-}
-
-// persistent self-attention block forward (csrc/persist.hip): every layer of a C = 64, H = 4
-// block with N ≤ 256 latents in ONE launch.  Per layer i: wo..b2 (its post-attention block) and,
-// for i < L - 1, the next layer's (lnw, lnb, wq, bq); the last layer optionally gets the next
-// cross-attention layer's LN + query (64 rows) or K/V (128 rows) projection as an L-th entry.  Returns, per layer, [o, lse, z, y, m2, r2, u] + [qkv_n, mean_n, rstd_n] when that
-// layer has a next projection.  Empty list: the operands do not qualify (the caller runs the
-// per-layer kernels).
-std::vector<Tensor> sa_block_fwd(Tensor qkv0, Tensor x0, int64_t N, double scale, double eps, std::vector<Tensor> wo,
-                                 std::vector<Tensor> bo, std::vector<Tensor> g2, std::vector<Tensor> be2,
-                                 std::vector<Tensor> w1, std::vector<Tensor> b1, std::vector<Tensor> w2,
-                                 std::vector<Tensor> b2, std::vector<Tensor> lnw, std::vector<Tensor> lnb,
-                                 std::vector<Tensor> wq, std::vector<Tensor> bq, OptT seed, double p) {
-  const int C = 64, H = 4;
-  const int L = (int)wo.size();
-  TORCH_CHECK(L >= 1 && L <= pio::kPersistMaxLayers, "sa_block_fwd: 1..8 layers");
-  TORCH_CHECK(bo.size() == (size_t)L && g2.size() == (size_t)L && be2.size() == (size_t)L && w1.size() == (size_t)L &&
-                  b1.size() == (size_t)L && w2.size() == (size_t)L && b2.size() == (size_t)L,
-              "sa_block_fwd: one post-attention parameter set per layer");
-  const int nn = (int)wq.size();
-  TORCH_CHECK((nn == L - 1 || nn == L) && lnw.size() == (size_t)nn && lnb.size() == (size_t)nn && bq.size() == (size_t)nn,
-              "sa_block_fwd: L - 1 next projections (+ an optional last query projection)");
-  TORCH_CHECK(qkv0.is_contiguous() && x0.is_contiguous(), "sa_block_fwd: contiguous qkv / x");
-  const int R = (int)x0.size(0);
-  TORCH_CHECK(x0.size(1) == C && qkv0.size(0) == R && qkv0.size(1) == 3 * C, "sa_block_fwd: C = 64, qkv (R, 192)");
-  CHECK_DT(x0, torch::kFloat32);
-  if (N <= 0 || N > 256 || N % 64 != 0 || R % N != 0 || (long long)R * 3 * C * 2 >= (1LL << 31)) return {};
-  auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-  if (!al(qkv0.data_ptr()) || !al(x0.data_ptr())) return {};
-  auto f32 = x0.options().dtype(torch::kFloat32);
-  auto b16 = x0.options().dtype(torch::kBFloat16);
-  const int B = R / (int)N;
-  unsigned* sync = persist_sync_buffer(x0, pio::persist_sync_words(B));
-  if (sync == nullptr) return {};
-  pio::SABlockFwdArgs a{};
-  a.QKV0 = bfp(qkv0);
-  a.X0 = f32p(x0);
-  a.sync = sync;
-  a.L = L; a.N = (int)N; a.R = R;
-  a.scale_log2 = (float)(scale * 1.4426950408889634);
-  a.eps = (float)eps;
-  a.dr = make_drop(seed, 0, p);
-  std::vector<Tensor> out;
-  for (int i = 0; i < L; ++i) {
-    pio::SAFwdLayer& y = a.ly[i];
-    for (const Tensor* t : {&wo[i], &w1[i], &w2[i]})
-      TORCH_CHECK(t->is_contiguous() && t->size(0) == C && t->size(1) == C, "sa_block_fwd: (C, C) weights");
-    y.Wo = bfp(wo[i]); y.W1 = bfp(w1[i]); y.W2 = bfp(w2[i]);
-    y.bo = f32p(bo[i]); y.g2 = f32p(g2[i]); y.be2 = f32p(be2[i]); y.b1 = f32p(b1[i]); y.b2 = f32p(b2[i]);
-    if (!al(y.Wo) || !al(y.W1) || !al(y.W2) || !al(y.g2) || !al(y.be2) || !al(y.bo) || !al(y.b1) || !al(y.b2)) return {};
-    Tensor o = torch::empty({B, (int)N, C}, b16), lse = torch::empty({B, (int)N, H}, f32);
-    Tensor z = torch::empty({R, C}, f32), yy = torch::empty({R, C}, f32);
-    Tensor m = torch::empty({R}, f32), r = torch::empty({R}, f32), u = torch::empty({R, C}, b16);
-    y.O = bfp_mut(o); y.LSE = lse.data_ptr<float>(); y.Z = z.data_ptr<float>(); y.Y = yy.data_ptr<float>();
-    y.mean2 = m.data_ptr<float>(); y.rstd2 = r.data_ptr<float>(); y.U = bfp_mut(u);
-    out.insert(out.end(), {o, lse, z, yy, m, r, u});
-    if (i < nn) {
-      const int nq = (int)wq[i].size(0);
-      TORCH_CHECK(wq[i].is_contiguous() && wq[i].size(1) == C && (nq == 3 * C || (i == L - 1 && (nq == C || nq == 2 * C))) &&
-                      bq[i].numel() == nq && lnw[i].numel() == C && lnb[i].numel() == C,
-                  "sa_block_fwd: next projection (3C, C) (the last layer's may be a (C, C) query or (2C, C) K/V projection)");
-      y.Wq = bfp(wq[i]); y.lnw = f32p(lnw[i]); y.lnb = f32p(lnb[i]); y.bq = f32p(bq[i]); y.nq = nq;
-      if (!al(y.Wq) || !al(y.lnw) || !al(y.lnb) || !al(y.bq)) return {};
-      Tensor qn = torch::empty({R, nq}, b16), m1 = torch::empty({R}, f32), r1 = torch::empty({R}, f32);
-      y.QKVn = bfp_mut(qn); y.mean1n = m1.data_ptr<float>(); y.rstd1n = r1.data_ptr<float>();
-      out.insert(out.end(), {qn, m1, r1});
-    }
-  }
-  if (!pio::sa_block_fwd_launch(a, stream())) return {};
-  return out;
-}
-
-unsigned persist_errors(bool reset) { return pio::persist_errors(reset); }
 
 namespace {
 pio::SlabJob make_job(const OptT& slab, std::vector<Tensor>& dsts, const std::vector<int64_t>& offs);
@@ -862,14 +769,8 @@ void sb_wgrad(std::vector<Tensor> jobs, OptT job_slab, std::vector<Tensor> job_d
 }
 
 // workgroups of a non-deterministic SlabJob (128 measured best on the MLM step: 96–128 ≈ equal,
-// 256 and 64 slower)
-int slab_job_target() {  // PIO_SLAB_TARGET: A/B knob for the appended reduction's width
-  static const int t = [] {
-    const char* e = getenv("PIO_SLAB_TARGET");
-    return e ? std::max(1, atoi(e)) : 128;
-  }();
-  return t;
-}
+// 192 and 256 slower: profiles/r5_ab/README.md)
+int slab_job_target() { return 128; }
 
 // the backward entry points below ACCUMULATE parameter gradients into caller-provided fp32
 // tensors (normally views of the flat gradient buffer) with device atomics: no partial slabs,
@@ -1908,11 +1809,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bo"), py::arg("g2"), py::arg("be2"), py::arg("eps"), py::arg("w1"), py::arg("b1"), py::arg("w2"),
         py::arg("b2"), py::arg("lnw") = py::none(), py::arg("lnb") = py::none(), py::arg("wq") = py::none(),
         py::arg("bq") = py::none(), py::arg("seed") = py::none(), py::arg("site") = 0, py::arg("p") = 0.0);
-  m.def("sa_block_fwd", &sa_block_fwd, py::arg("qkv0"), py::arg("x0"), py::arg("N"), py::arg("scale"), py::arg("eps"),
-        py::arg("wo"), py::arg("bo"), py::arg("g2"), py::arg("be2"), py::arg("w1"), py::arg("b1"), py::arg("w2"),
-        py::arg("b2"), py::arg("lnw"), py::arg("lnb"), py::arg("wq"), py::arg("bq"), py::arg("seed") = py::none(),
-        py::arg("p") = 0.0);
-  m.def("persist_errors", &persist_errors, py::arg("reset") = true);
   m.def("sb_fwd", &sb_fwd, py::arg("x"), py::arg("params"), py::arg("scale"), py::arg("eps"),
         py::arg("pre") = std::vector<Tensor>{}, py::arg("post") = std::vector<Tensor>{});
   m.def("sb_bwd", &sb_bwd, py::arg("dz"), py::arg("x0"), py::arg("saved"), py::arg("params"),

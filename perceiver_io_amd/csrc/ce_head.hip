@@ -33,6 +33,11 @@
 // accumulator is lazy: only when a tile's Σ p exceeds 2^kRescale (a logit ≳ kRescale above the
 // reference max; 2^8 headroom, far inside fp32 / bf16 range), a wave-uniform branch taken a
 // handful of times per row.
+// The cross-workgroup hand-offs below rely on the write-through (sc1) store / L1-bypassing load
+// behaviour measured on gfx950 (MI355X_MICROARCH.md, inter-workgroup visibility): no other target.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "this translation unit's sc1 hand-off protocol is validated on gfx950 (MI355X) only"
+#endif
 #include "common.h"
 
 namespace pio {

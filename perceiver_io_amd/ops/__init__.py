@@ -60,6 +60,23 @@ def deterministic() -> bool:
     return _DETERMINISTIC[0]
 
 
+def check_device_errors(reset: bool = True) -> None:
+    """Checked builds (``PERCEIVER_CHECKED=1``): read the kernels' sticky index-validation words
+    (one host sync) and raise on any — token ids, gather rows and class labels outside their
+    tables (the kernels clamped / skipped the access).  Outside a graph capture every checked
+    launch raises at once (``checked_sync``); inside a replayed hipGraph nothing can, so the
+    Trainer calls this at every logging step and at the end of ``fit``, and ``bench.py`` after
+    its timed loop (SURVEY §5.3 failure detection).  A no-op in the regular build."""
+    if not ext.available() or not torch.cuda.is_available() or not torch.cuda.is_initialized():
+        return
+    K = ext.require()
+    if K.checked_build():
+        c = int(K.check_errors(reset))
+        if c:
+            raise RuntimeError(f"checked build: out-of-range indices seen on the device (error bits {c:#x}: "
+                               "1 token id >= vocab, 2 gather row out of range, 4 label outside [0, V) and != -100)")
+
+
 def use_hip(t: torch.Tensor) -> bool:
     """True when ``t`` should be processed by the HIP kernels."""
     if _BACKEND in ("torch", "reference") or not t.is_cuda:

@@ -46,9 +46,9 @@ EPS = 1e-5
 WGRAD_SLAB = True
 # self-attention dQKV stored as bf16 for the chain-layout boundary kernel (identical results)
 BF16_DQKV = True
-# the bf16 self-attention backward carries the pending slab reduction (PIO_ATTN_SLAB=0: the next
-# chain kernel does, A/B)
-ATTN_SLAB = os.environ.get("PIO_ATTN_SLAB", "1") != "0"
+# the bf16 self-attention backward carries the pending slab reduction in appended workgroups
+# (1.429 → 1.377 ms on the headline step against the next chain kernel carrying it, r5)
+ATTN_SLAB = True
 TALL_ROWS = 1 << 17  # kTallRows in csrc/binding.cpp: taller projections stream their dW (wgrad kernel)
 
 
@@ -114,21 +114,44 @@ def _flush_pending():
                 K.slab_reduce(t, ds, os_)
 
 
-def flush_pending(stream=None):
+def flush_pending(stream=None, inside=None):
     """Launch every deferred slab reduction now (e.g. before a gradient bucket that depends on
-    them is all-reduced mid-backward, parallel/reducer.py).  ``stream``: run them there instead
-    (the caller has made it wait for the producing stream; the slabs are recorded on it so the
-    allocator keeps them until it is done) — the reducer's side stream, which is the only
-    consumer of a completed bucket, so the main chain does not carry the reductions."""
-    if stream is None:
+    them is all-reduced mid-backward, parallel/reducer.py).
+
+    ``stream`` (the reducer's side stream, the only consumer of a completed bucket): the jobs whose
+    every destination satisfies ``inside`` (lies in the bucket, so nothing on the main stream adds
+    to it any more) run there, after the caller has made ``stream`` wait for the current stream;
+    the slabs are recorded on it so the allocator keeps them until it is done.  Every other job —
+    destinations still being accumulated by later kernels of the backward (e.g. ``layer_n``'s
+    query path, finished inside ``layer_1``'s block), or straddling the bucket — runs on the
+    current stream NOW, before that wait, so it stays ordered with those kernels.  In
+    deterministic mode everything runs on the current stream (fixed order, plain adds).
+    Returns the jobs to run on ``stream`` as a callable (call it after the wait)."""
+    from . import deterministic
+
+    if stream is None or inside is None or deterministic():
         _flush_pending()
-        return
+        return lambda: None
     _flush_queued[0] = False
-    with torch.cuda.stream(stream):
-        while _pending:
-            K, t, ds, os_, _ = _pending.pop(0)
-            t.record_stream(stream)
+    side = []
+    while _pending:
+        job = _pending.pop(0)
+        K, t, ds, os_, st = job
+        if all(inside(d) for d in ds):
+            side.append(job)
+        elif st is None:
             K.slab_reduce(t, ds, os_)
+        else:
+            with torch.cuda.stream(st):
+                K.slab_reduce(t, ds, os_)
+
+    def run_side():
+        with torch.cuda.stream(stream):
+            for K, t, ds, os_, _ in side:
+                t.record_stream(stream)
+                K.slab_reduce(t, ds, os_)
+
+    return run_side
 
 
 def defer_slab(K, t: torch.Tensor, dsts, offs):
@@ -903,9 +926,6 @@ SA_LAYER_FUSED = True
 PA_SIZES = lambda C: [C * C, C, C, C, C * C, C, C * C, C]  # noqa: E731  (Wo bo γ2 β2 W1 b1 W2 b2)
 LL_SIZES = lambda C: [C, C, 3 * C * C, 3 * C]                 # noqa: E731  (γ1 β1 Wqkv bqkv)
 SA_NP = 12  # parameters per self-attention layer (layer_spec_and_params order)
-# the fused C = 64 stacks with N <= 256 latents run every layer of a block in ONE persistent launch
-# each way (csrc/persist.hip); False (PERCEIVER_PERSIST=0): one launch per layer (chain.hip), for A/B runs
-PERSIST_BLOCK = os.environ.get("PERCEIVER_PERSIST", "1") != "0"
 # channel widths run as one fused self-attention block node (PERCEIVER_SA_BLOCK_C128=0 keeps C = 128
 # stacks layer by layer)
 SA_BLOCK_CHANNELS = (32, 64, 128)
@@ -952,33 +972,7 @@ class _SABlockFn(torch.autograd.Function):
         # C = 64, H = 4 latent stacks, attention-probability dropout included (csrc/chain.hip
         # sa_layer_fwd_chain8_kernel: up to 512 latents)
         fused_layer = SA_LAYER_FUSED and C == 64 and H == 4 and N <= 512 and N % 64 == 0
-        res = None
-        if fused_layer and PERSIST_BLOCK and N <= 256 and hasattr(K, "sa_block_fwd"):
-            wantq = _LOOKAHEAD["want_q"]
-            nxt = [(P[i + 1][0], P[i + 1][1], bws[i + 1][0], P[i + 1][3]) for i in range(L - 1)]
-            if wantq is not None:  # the following cross-attention layer's LN + query projection
-                nxt.append(tuple(wantq[:4]))
-            res = K.sa_block_fwd(qkv, xl, N, scale, EPS, [b[2] for b in bws], [p[5] for p in P], [p[6] for p in P],
-                                 [p[7] for p in P], [b[3] for b in bws], [p[9] for p in P], [b[4] for b in bws],
-                                 [p[11] for p in P], [n[0] for n in nxt], [n[1] for n in nxt], [n[2] for n in nxt],
-                                 [n[3] for n in nxt], seed=seed, p=pdrop)
-        if res:
-            k = 0
-            for i in range(L):
-                o, lse, z, y, m2, r2, u = res[k:k + 7]
-                k += 7
-                qkv_n = mean_n = rstd_n = None
-                if i < len(nxt):
-                    qkv_n, mean_n, rstd_n = res[k:k + 3]
-                    k += 3
-                saved += [xl, qkv, mean1, rstd1, o, lse, y, m2, r2, u]
-                if i == L - 1 and wantq is not None:
-                    _LOOKAHEAD["want_q"] = None
-                    _LOOKAHEAD["have_q"] = (z, qkv_n, mean_n, rstd_n, wantq[0])
-                    ctx.out_ptr = z.data_ptr()
-                    qkv_n = mean_n = rstd_n = None
-                xl, qkv, mean1, rstd1 = z, qkv_n, mean_n, rstd_n
-        for i in range(L if not res else 0):
+        for i in range(L):
             p = P[i]
             _, _, wo, w1, w2 = bws[i]
             bo, g2, be2, b1, b2 = p[5], p[6], p[7], p[9], p[11]
@@ -1175,8 +1169,8 @@ def sa_block_lookahead(block, rows: int, n: Optional[int] = None, device=None):
 SB_PRE = os.environ.get("PIO_SB_PRE", "1") != "0"
 # the next cross layer's LN + query projection in the per-sample block's kernels (PIO_SB_POST=0: A/B)
 SB_POST = os.environ.get("PIO_SB_POST", "1") != "0"
-# ... and a decoder's K|V projection into the encoder's last block (PerceiverIO.loss; A/B knob)
-SB_KV = os.environ.get("PIO_SB_KV", "1") != "0"
+# ... and a decoder's K|V projection into the encoder's last block (PerceiverIO.loss; MNIST −11 µs, r5)
+SB_KV = True
 
 
 def sample_block_runs(block, b: int, n: int, device) -> bool:
@@ -1230,8 +1224,11 @@ def _sample_block_ok(specs, n: int, p: float, cuda: bool) -> bool:
     from . import deterministic
 
     sp = specs[0]
+    # ≤ 3 layers: with the cross layers' pre / post folds a block's backward fills 4L + 4 slab
+    # segments (common.h kMaxSlabSegs = 16) and 4L + 3 weight-gradient jobs (sb_args.h
+    # kSBMaxJobs); 4 layers would overflow both, so such blocks keep the per-layer kernels
     return (SAMPLE_BLOCK and cuda and sp.C in (64, 128) and sp.heads == 4 and n == 32 and p == 0.0 and not sp.cross
-            and 1 <= len(specs) <= 4 and all(s == sp for s in specs) and not deterministic())
+            and 1 <= len(specs) <= 3 and all(s == sp for s in specs) and not deterministic())
 
 
 class _SampleBlockFn(torch.autograd.Function):

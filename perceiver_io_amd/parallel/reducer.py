@@ -325,9 +325,20 @@ class FlatGradReducer:
         from ..ops.fused import flush_pending
 
         if self._side is not None:
+            run_side = None
+            if flush:  # the covered kernels' deferred slab reductions, ahead of the collective:
+                # those entirely inside the bucket on the side stream, the rest (still being
+                # accumulated on the main stream) on the main stream before the fork
+                base = self.flat.grad.data_ptr()
+
+                def inside(d, lo=lo, hi=hi, base=base):
+                    off = (d.data_ptr() - base) // d.element_size()
+                    return d.dtype == self.flat.grad.dtype and lo <= off and off + d.numel() <= hi
+
+                run_side = flush_pending(self._side, inside)
             self._side.wait_stream(torch.cuda.current_stream(self.flat.device))
-            if flush:  # the covered kernels' deferred slab reductions, ahead of the collective
-                flush_pending(self._side)
+            if run_side is not None:
+                run_side()
             with torch.cuda.stream(self._side):
                 self._reduce(lo, hi)
                 if self.updater is not None:

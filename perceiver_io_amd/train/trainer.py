@@ -459,6 +459,7 @@ class Trainer:
                     self.callback_metrics.update(vals)
                     self.log_scalars(vals)
                     ops.mlm_head.check_overflow()  # fixed-capacity MLM rows: fail loudly, never truncate
+                    ops.check_device_errors()  # checked builds: index errors seen inside replayed graphs
                     if self.terminate_on_nan and not all(math.isfinite(v) for v in vals.values()):
                         raise ValueError(f"non-finite metric at step {self.global_step}: {vals}")
                     if self.enable_progress_bar and self.is_global_zero:
@@ -475,6 +476,7 @@ class Trainer:
             self.current_epoch += 1
         if tprof is not None:
             tprof.close()
+        ops.check_device_errors()
 
     def _eager_clip_step(self, batches):
         opt = self.optimizers[0]

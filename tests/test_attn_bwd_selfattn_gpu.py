@@ -1,0 +1,67 @@
+"""The latent self-attention backward with bf16 dQ / dK / dV (the operands of the chain-layout
+layer-boundary kernel; reference ``perceiver/model.py:59-74`` inside the self-attention block of
+``model.py:36-44``) at the C = 64, H = 4 latent shapes against the fp32 emulation
+(``ops/emulation.py:attn_bwd``): the full-LDS 8-wave workgroup, and the two-query-tile variant
+that carries the previous kernel's slab reduction in appended workgroups (whose result must equal
+the standalone reduction's).
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / max(b.norm().item(), 1e-30)).item()
+
+
+def _case(B, N, H=4, D=16, seed=0):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    E = H * D
+    qkv = torch.randn(B, N, 3 * E, device=DEV, generator=g).to(torch.bfloat16)
+    q, k, v = qkv[:, :, :E], qkv[:, :, E:2 * E], qkv[:, :, 2 * E:]
+    do = torch.randn(B, N, E, device=DEV, generator=g).to(torch.bfloat16)
+    return q, k, v, do
+
+
+def _fwd(K, q, k, v, do, H, D, scale):
+    B, N = q.shape[0], q.shape[1]
+    o, lse = K.attn_fwd(q, k, v, None, H, D, scale, 0.0, None, 1)
+    delta = (do.float().view(B, N, H, D) * o.float().view(B, N, H, D)).sum(-1).contiguous()
+    return o, lse, delta
+
+
+@pytest.mark.parametrize("carry", [False, True])
+@pytest.mark.parametrize("B,N", [(64, 256), (3, 256), (4, 128), (2, 192)])
+def test_selfattn_bwd_bf16(B, N, carry):
+    from perceiver_io_amd.ops import emulation, ext
+
+    K = ext.require()
+    H, D = 4, 16
+    E = H * D
+    scale = 1.0 / math.sqrt(D)
+    q, k, v, do = _case(B, N, H, D, seed=B * 1000 + N)
+    o, lse, delta = _fwd(K, q, k, v, do, H, D, scale)
+    ref = emulation.attn_bwd(q, k, v, None, o, do, lse, delta, H, D, scale, 0.0, None, None, None, None)
+    dqkv = torch.full((B, N, 3 * E), float("nan"), device=DEV).to(torch.bfloat16)
+    job = {}
+    if carry:  # a slab reduction of 64 rows × 1000 columns into two targets
+        g = torch.Generator(device=DEV).manual_seed(5)
+        slab = torch.randn(64, 1024, device=DEV, generator=g)
+        t0, t1 = torch.zeros(600, device=DEV), torch.zeros(400, device=DEV)
+        job = dict(job_slab=slab, job_dsts=[t0, t1], job_offs=[0, 600])
+    K.attn_bwd(q, k, v, None, o, do, lse, delta, H, D, scale, 0.0, None, dqkv[:, :, :E], dqkv[:, :, E:2 * E],
+               dqkv[:, :, 2 * E:], **job)
+    torch.cuda.synchronize()
+    assert torch.isfinite(dqkv.float()).all()
+    for got, want, name in zip((dqkv[:, :, :E], dqkv[:, :, E:2 * E], dqkv[:, :, 2 * E:]), ref, ("dq", "dk", "dv")):
+        err = _rel(got.float(), want.float())
+        assert err < 1.5e-2, f"{name}: rel err {err:.3e}"
+    if carry:
+        s = slab.sum(0)
+        assert _rel(t0, s[:600]) < 1e-5 and _rel(t1, s[600:1000]) < 1e-5

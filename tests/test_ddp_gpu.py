@@ -358,3 +358,50 @@ def test_graph_collectives_probe_capture_failure_fails_closed():
     assert r["ok"] is False and r["in_graph"] is False
     assert not r["capturing"] and not r["side_capturing"]
     assert r["value"] == 3.0  # 1-rank all-reduce (x1) then x3
+
+
+def test_rccl_overlap_and_bucket_update_variants_bitwise():
+    """The data-parallel step's variants on a 1-rank RCCL group with the reducer forced on
+    (collectives inside the step graph), deterministic kernels: ready-point all-reduces on the
+    side stream or inline after the backward (overlap on / off), AdamW per bucket behind each
+    all-reduce or one pass after all of them (bucket_update on / off) — the final parameters
+    agree bit for bit (the slab reductions a ready point flushes run on the side stream only when
+    every destination lies inside the bucket; in deterministic mode all of them stay on the
+    compute stream)."""
+    import torch.distributed as tdist
+
+    from perceiver_io_amd import ops
+    from perceiver_io_amd.ops.optim import FusedAdamW
+    from perceiver_io_amd.parallel import FlatGradReducer
+    from perceiver_io_amd.train.engine import StepEngine
+
+    tdist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1,
+                             device_id=torch.device("cuda", 0))
+    try:
+        data = _data(0, STEPS)
+        res = {}
+        for overlap in (True, False):
+            for bucket in (True, False):
+                model = _setup()
+                opt = FusedAdamW(model.parameters(), lr=1e-3, weight_decay=0.01)
+                red = FlatGradReducer(opt.flat, in_graph=True, force=True, overlap=overlap)
+                red.plan(model)
+                eng = StepEngine(lambda b, m=model: m.loss(b[0], b[1], labels=b[2], x_masked=b[3]), opt, reducer=red,
+                                 device="cuda", graph=True, bucket_update=bucket)
+                for b in data:
+                    eng.step(b)
+                torch.cuda.synchronize()
+                assert eng.bucket_update == bucket and red.overlap == overlap
+                res[(overlap, bucket)] = opt.flat.data.clone()
+                eng = None
+                import gc
+
+                gc.collect()  # the captured graphs (with their collectives) before the reducer
+                torch.cuda.synchronize()
+                red.close()
+        ref = res[(True, True)]
+        for k, v in res.items():
+            assert torch.equal(v, ref), (k, (v - ref).abs().max().item())
+    finally:
+        ops.set_deterministic(False)
+        tdist.destroy_process_group()

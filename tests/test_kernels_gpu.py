@@ -834,6 +834,24 @@ for name, fn in (
     except RuntimeError as e:
         out.append((name, "checked build" in str(e)))
 torch.cuda.synchronize()
+# inside a replayed hipGraph no launch can raise: the sticky words are read by
+# ops.check_device_errors() (the Trainer's logging-step / end-of-fit check, bench.py after timing)
+from perceiver_io_amd import ops
+ids = torch.randint(0, 50, (1, 8), device=dev)
+K.embed_fwd(ids, E, P, 1.0)
+torch.cuda.synchronize()
+g = torch.cuda.CUDAGraph()
+with torch.cuda.graph(g):
+    K.embed_fwd(ids, E, P, 1.0)
+ops.check_device_errors()  # clean after a valid capture
+ids[0, 1] = 50
+g.replay()
+torch.cuda.synchronize()
+try:
+    ops.check_device_errors()
+    out.append(("graph", "no error"))
+except RuntimeError as e:
+    out.append(("graph", "checked build" in str(e)))
 print(out)
 assert all(r is True for _, r in out), out
 assert K.check_errors(True) == 0

@@ -132,10 +132,13 @@ def test_mlm_fused_matches_eager(latents):
     _check_grads(g_hip, g_ref, floor=floor)
 
 
-@pytest.mark.parametrize("heads,shape", [(1, (28, 28, 1)), (4, (28, 28, 1)), (4, (64, 64, 3))])
-def test_image_classifier_fused_matches_eager(heads, shape):
+@pytest.mark.parametrize("heads,shape,sa", [(1, (28, 28, 1), 2), (4, (28, 28, 1), 2), (4, (64, 64, 3), 2),
+                                            (4, (28, 28, 1), 4)])
+def test_image_classifier_fused_matches_eager(heads, shape, sa):
     """heads = 4 (head dim 32): the encoder cross-attention runs over implicit K/V
-    (attention_pe.hip), both directions, the weight-shared layer_n applied twice."""
+    (attention_pe.hip), both directions, the weight-shared layer_n applied twice.  sa = 4
+    self-attention layers per block: past the per-sample block kernels' limits, the block runs
+    on the layer-boundary kernels."""
     from perceiver_io_amd import ops
     from perceiver_io_amd.tasks import LitImageClassifier
 
@@ -144,7 +147,7 @@ def test_image_classifier_fused_matches_eager(heads, shape):
                              optimizer_init={"class_path": "torch.optim.AdamW", "init_args": {"lr": 1e-3}},
                              num_latents=32, num_latent_channels=128, num_encoder_layers=2 if heads == 1 else 3,
                              num_encoder_cross_attention_heads=heads,
-                             num_encoder_self_attention_layers_per_block=2, num_decoder_cross_attention_heads=1).cuda()
+                             num_encoder_self_attention_layers_per_block=sa, num_decoder_cross_attention_heads=1).cuda()
     x = torch.randn(4, *shape, device="cuda")
     y = torch.randint(0, 10, (4,), device="cuda")
 

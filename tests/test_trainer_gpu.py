@@ -97,3 +97,4 @@ def test_seq_clf_dropout_fused_under_graph(tmp_path, monkeypatch):
     assert tr.fused and tr._engine.graph_enabled and tr._engine.num_graphs >= 1
     assert tr.global_step == 2 * 6
     assert torch.isfinite(torch.tensor(tr.callback_metrics["train_loss"]))
+
