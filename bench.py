@@ -8,8 +8,9 @@ bf16 compute.  Synthetic token ids of that shape, random-init weights (no networ
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, RCCL)
-    python bench.py --config {mlm256,seq_clf,seq_clf_ft,imagenet,long_mlm,mnist,lartpc} ...
+    python bench.py --config {mlm256,mlm64,seq_clf,seq_clf_ft,imagenet,long_mlm,mnist,lartpc} ...
 
+``mlm64`` = the reference README's MLM run itself (64 × 64 latents, batch 64, lr 3e-3).
 Other configs (BASELINE.json configs 1, 3-5): ``seq_clf`` = IMDB text classifier with a frozen
 encoder (decoder-only training, batch 128/GPU, README seq_clf command); ``imagenet`` =
 224×224×3 image classifier with Fourier position encoding (50,176 inputs × 133 channels,
@@ -40,6 +41,9 @@ HEADLINE_METRIC = "samples/sec (whole node) IMDB MLM seq_len=512 at 1/2/4/8 MI35
 # config name → defaults (batch per GPU, sequence length / inputs) and the metric string
 CONFIGS = {
     "mlm256": dict(batch=64, seq_len=512, latents=256, channels=64, metric=HEADLINE_METRIC),
+    # the reference README's own MLM run (README.md:33-44, scripts/mlm.py:19-29): 64 × 64 latents
+    "mlm64": dict(batch=64, seq_len=512, latents=64, channels=64,
+                  metric="samples/sec (whole node) IMDB MLM seq_len=512 64x64 latents (reference README run)"),
     "seq_clf": dict(batch=128, seq_len=512, latents=64, channels=64,
                     metric="samples/sec (whole node) IMDB seq_clf frozen encoder seq_len=512"),
     # the README's joint fine-tune (README.md:91-107): encoder unfrozen, dropout 0.1, lr 1e-4
@@ -72,11 +76,12 @@ def parse(argv=None):
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture of the step")
     ap.add_argument("--allreduce-dtype", default="fp32", choices=["fp32", "bf16"],
                     help="gradient all-reduce wire format (N > 1)")
-    ap.add_argument("--overlap", default="on", choices=["on", "off"],
+    ap.add_argument("--overlap", default="off", choices=["on", "off"],
                     help="N > 1: bucket all-reduces at ready points on a side stream during the backward (on) or "
-                         "all of them after the backward on the compute stream (off)")
-    ap.add_argument("--bucket-update", default="on", choices=["on", "off"],
-                    help="N > 1: AdamW per bucket right behind its all-reduce (on) or one pass after all (off)")
+                         "one all-reduce after the backward on the compute stream (off, default)")
+    ap.add_argument("--bucket-update", default="auto", choices=["auto", "on", "off"],
+                    help="N > 1: AdamW per bucket right behind its all-reduce (on; auto = with --overlap on) or one "
+                         "pass after all (off)")
     ap.add_argument("--dense", action="store_true", help="lartpc: evaluate all pixels (the reference's cost)")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--profile-stacks", type=int, default=0,
@@ -147,7 +152,7 @@ def build(args, device):
     B, L = args.batch, args.seq_len
     if args.config == "lartpc":
         return _build_lartpc(args)
-    if args.config in ("mlm256", "long_mlm"):
+    if args.config in ("mlm256", "mlm64", "long_mlm"):
         lit = LitMaskedLanguageModel(
             vocab_size=args.vocab, max_seq_len=L, optimizer_init=_opt(), scheduler_init=_sched(),
             num_latents=args.latents, num_latent_channels=args.channels, num_encoder_layers=3,
@@ -356,7 +361,7 @@ def main(argv=None):
         return loss_inner(batch)
 
     engine = StepEngine(loss_fn, opt, sched, reducer=reducer, device=device, graph=fused and not args.no_graph,
-                        bucket_update=args.bucket_update == "on")
+                        bucket_update=None if args.bucket_update == "auto" else args.bucket_update == "on")
     g = torch.Generator(device="cpu").manual_seed(99 + info.rank)
 
     def to_dev(b):

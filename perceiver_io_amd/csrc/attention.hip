@@ -394,8 +394,11 @@ __global__ __launch_bounds__(64 * NW, (QR == 2 && !DRP) ? 4 : 1) void attn_bwd_k
   // next round register-prefetched.  Every wave writes its dS slab of each tile into LDS;
   // after one barrier wave j (< NQS) forms tile j's dQ over all KB keys of the block with
   // MFMAs (no cross-wave reduction, no atomics inside the block).
+  // (the generic dQ step below gives one query tile per wave: at most NW tiles per round)
   constexpr int NQS0 = 4 * NTH / (64 * CH);
-  constexpr int NQS = QR > 0 ? QR : (NQS0 >= 4 ? 4 : (NQS0 >= 1 ? NQS0 : 1));
+  constexpr int NQS1 = NQS0 >= 4 ? 4 : (NQS0 >= 1 ? NQS0 : 1);
+  constexpr int NQS = QR > 0 ? QR : (NQS1 < NW ? NQS1 : NW);
+  static_assert(NQS <= NW || (D == 16 && NW == 8), "one dQ query tile per wave");
   constexpr int NI = (NQS * 64 * CH + NTH - 1) / NTH;
   __shared__ __attribute__((aligned(16))) uint16_t sQ[NQS * 32 * LD + 64];
   __shared__ __attribute__((aligned(16))) uint16_t sdO[NQS * 32 * LD + 64];
@@ -997,7 +1000,10 @@ void attn_bwd_launch(const AttnArgs& a, int D, const uint16_t* O, const uint16_t
     return;
   }
   switch (D) {  // waves per workgroup: 8 for d ≤ 32, 4 above (keys per block = 32 × waves)
-    case 16: bwd_launch_t<16, 8>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, qsplit_ok, dq_zeroed, st); break;
+    case 16:  // ≤ 64 keys (the 64-latent self-attention of the text classifiers / MLM-64): 2 waves, not 6 idle of 8
+      if (a.Nk <= 64) bwd_launch_t<16, 2>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, qsplit_ok, dq_zeroed, st);
+      else bwd_launch_t<16, 8>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, qsplit_ok, dq_zeroed, st);
+      break;
     case 32:  // ≤ 64 keys (the image configs' 32-latent self-attention): 2 waves, not 6 idle of 8
       if (a.Nk <= 64) bwd_launch_t<32, 2>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, qsplit_ok, dq_zeroed, st);
       else bwd_launch_t<32, 8>(a, dO, LSE, delta, dq, dq_bs, dq_rs, dk, dk_bs, dk_rs, dv, dv_bs, dv_rs, kv_acc, dq_kbs, qsplit_ok, dq_zeroed, st);

@@ -492,10 +492,12 @@ def _zero_stand_in(r: int, c: int, device) -> torch.Tensor:
 def _cross_zero_bufs(ctx, device):
     """(zbuf, dq_pre, d_pre) of a fused cross-attention layer's backward: the attention backward's
     atomically accumulated dQ — and, for the first backward application of a PE layer whose batch
-    groups add into its factored reduction D, that (M, 2C) buffer too — in one fp32 span that the
-    kernel before the attention backward clears on the way (no fill launch); (None, None, None)
-    for self-attention layers and in deterministic mode.  Broadcast latent queries on the fused PE
-    path come back summed over the batch."""
+    groups add into its factored reduction D, that (M, 2C) buffer too; for the first application
+    of a plain layer whose query splits add into dK / dV (many queries over few keys: the MLM
+    decoder's selected positions over the latents), that (B, M, 2C) buffer — in one fp32 span
+    that the kernel before the attention backward clears on the way (no fill launch);
+    (None, None, None) for self-attention layers and in deterministic mode.  Broadcast latent
+    queries on the fused PE path come back summed over the batch."""
     from . import deterministic
 
     if not ctx.spec.cross or deterministic():
@@ -505,9 +507,14 @@ def _cross_zero_bufs(ctx, device):
     f32 = dict(device=device, dtype=torch.float32)
     nq = (Bq if pe_fused else B) * Nq * C
     d_pre = None
+    K = ext.require() if torch.device(device).type == "cuda" else emulation
     if pe_fused and ctx.kv_entry.get("pe_D") is None and pe_attn_bsplit(B, pm, H) > 1:
         zbuf = torch.empty(nq + pm * 2 * C, **f32)
         d_pre = zbuf[nq:].view(pm, 2 * C)
+    elif (not pe_fused and ctx.kv_entry.get("dkv") is None and hasattr(K, "attn_bwd_zero_plan")
+          and int(K.attn_bwd_zero_plan(B, H, Nq, pm, D)) & 2):
+        zbuf = torch.empty(nq + B * pm * 2 * C, **f32)
+        d_pre = zbuf[nq:].view(B, pm, 2 * C)
     else:
         zbuf = torch.empty(nq, **f32)
     return zbuf, zbuf[:nq].view(-1, Nq, C), d_pre
@@ -783,12 +790,13 @@ class _LayerFn(torch.autograd.Function):
                 # dK/dV of every application of this layer land in one buffer (K-06); the first
                 # writer stores, later ones accumulate
                 acc = ent["dkv"] is not None
+                kv_pre = not acc and d_pre is not None and d_pre.dim() == 3  # cleared with dQ (_cross_zero_bufs)
                 if not acc:
-                    ent["dkv"] = torch.empty((B, M, 2 * C), **f32)
+                    ent["dkv"] = d_pre if kv_pre else torch.empty((B, M, 2 * C), **f32)
                 dkv = ent["dkv"]
                 dq, _, _ = K.attn_bwd(qx, kv3[:, :, :C], kv3[:, :, C:], kmask, o, do.view(B, Nq, C), lse, delta3, H,
                                       D, scale, ctx.p_attn, ctx.seed, dq_pre, dkv[:, :, :C], dkv[:, :, C:], acc,
-                                      dq_zeroed=dq_pre is not None)
+                                      dq_zeroed=dq_pre is not None, kv_zeroed=kv_pre)
             # the latent array's gradient, written by the kernels below in place: += Σ_b dY by the
             # batch sum, then dX = LN_bwd(·) + that into the same buffer
             leaf_g = None

@@ -88,22 +88,38 @@ def _capturing(device) -> bool:
 
 
 class FlatGradReducer:
-    def __init__(self, flat, bucket_bytes: int = 4 << 20, overlap: Optional[bool] = None, in_graph: Optional[bool] = None,
-                 wire_dtype: Optional[torch.dtype] = None, force: bool = False):
+    def __init__(self, flat, bucket_bytes: Optional[int] = None, overlap: Optional[bool] = None,
+                 in_graph: Optional[bool] = None, wire_dtype: Optional[torch.dtype] = None, force: bool = False):
         self.flat = flat
         self.world = dist.get_world_size() if (dist.is_available() and dist.is_initialized()) else 1
         # force: run the collectives even for a 1-rank group (tests of the capture mechanics on one GPU)
         self.force = bool(force) and dist.is_available() and dist.is_initialized()
+        # bucket_bytes=None: 4 MB buckets with overlap, the whole buffer in one all-reduce without
+        # (an explicit size keeps the overlapped layout, ready-point ranges included, also when
+        # overlap is off: the two paths then add in the same order — bit-comparable)
+        self._one_bucket = bucket_bytes is None
+        bucket_bytes = 4 << 20 if bucket_bytes is None else bucket_bytes
         self.bucket_bytes = bucket_bytes
         self.buckets: List[Tuple[int, int]] = flat.bucket_ranges(bucket_bytes)
         self.points: Dict[str, int] = {}          # ready point → bucket index
         self._point_modules: Dict[str, int] = {}  # ready point → id() of the module it was planned on
         # overlap needs every parameter gradient to land in flat.grad directly (no 8-way replicas
         # that a later fold() would still add into an early bucket's range)
-        # overlap=None: on (overlap=False: collectives inline on the compute stream)
+        # overlap=None → off: the inline path — ONE all-reduce over the whole flat gradient on the
+        # compute stream after the backward (inside the step graph where RCCL is capturable), then
+        # one fused AdamW.  Measured on one MI355X with the collectives forced on (1-rank RCCL,
+        # profiles/r6_reducer_ab.md): the side-stream ready points + per-bucket AdamW expose
+        # ≈150 µs per headline step (cross-queue gaps, contention, five AdamW launches), the
+        # inline path ≈5 µs; at 4–11 MB of gradients per step an 8-GPU xGMI ring all-reduce
+        # costs less than that overlap machinery, so it is not worth hiding.  overlap=True keeps
+        # the ready points (tests, A/B: bench.py --overlap on).
         if overlap is None:
-            overlap = True
+            overlap = False
         self.overlap = bool(overlap) and getattr(flat, "grad_rep", None) is None
+        self._one_bucket = self._one_bucket and not self.overlap
+        if self._one_bucket:  # one large message: the ring pays its per-hop latency once
+            self.bucket_bytes = 256 << 20
+            self.buckets = flat.bucket_ranges(self.bucket_bytes)
         self.wire_dtype = wire_dtype
         self.on_gpu = flat.device.type == "cuda"
         self._side = torch.cuda.Stream(device=flat.device) if (self.on_gpu and self.overlap) else None
@@ -235,8 +251,10 @@ class FlatGradReducer:
                 if r is not None:
                     ranges["layer_1_sa"] = (r, enc)
         if not self.overlap:
-            # overlap off: same bucket layout (so results stay bit-comparable), no ready points
-            self.set_ready_ranges(ranges)
+            # overlap off: no ready points; the whole buffer in one bucket (default), or the
+            # overlapped layout when a bucket size was given (bit-comparable A/B)
+            if not self._one_bucket:
+                self.set_ready_ranges(ranges)
             self.points, self._point_modules = {}, {}
             return {}
         self.set_ready_ranges(ranges)

@@ -198,8 +198,8 @@ class StepEngine:
         # all-reduce on the reducer's side stream (overlapping the rest of the backward), so
         # only the buckets finish() reduces stay on the critical path.  Needs no clipping (a
         # global norm) and no replicated accumulators.
-        if bucket_update is None:
-            bucket_update = True
+        if bucket_update is None:  # with the reducer's ready points (overlap on) only
+            bucket_update = reducer is not None and getattr(reducer, "overlap", False)
         self.bucket_update = bool(bucket_update and self.fused and reducer is not None and reducer.enabled
                                   and optimizer.bucket_updates_ok())
         if self.bucket_update:

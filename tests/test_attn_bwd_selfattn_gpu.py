@@ -65,3 +65,30 @@ def test_selfattn_bwd_bf16(B, N, carry):
     if carry:
         s = slab.sum(0)
         assert _rel(t0, s[:600]) < 1e-5 and _rel(t1, s[600:1000]) < 1e-5
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+@pytest.mark.parametrize("B,Nq,Nk", [(128, 64, 64), (3, 33, 64), (4, 64, 48)])
+def test_few_key_selfattn_bwd_two_wave(B, Nq, Nk, p):
+    """Head width 16 over ≤ 64 keys (the text classifiers' / MLM-64's latent self-attention,
+    reference README.md:91-107): the two-wave workgroup (64 keys) instead of eight waves of which
+    six would sweep padded keys; no key mask, attention-probability dropout on and off."""
+    from perceiver_io_amd.ops import emulation, ext
+
+    K = ext.require()
+    H, D = 4, 16
+    E = H * D
+    scale = 1.0 / math.sqrt(D)
+    g = torch.Generator(device=DEV).manual_seed(B + Nq + Nk)
+    q = torch.randn(B, Nq, E, device=DEV, generator=g).to(torch.bfloat16)
+    kv = torch.randn(B, Nk, 2 * E, device=DEV, generator=g).to(torch.bfloat16)
+    k, v = kv[:, :, :E], kv[:, :, E:]
+    do = torch.randn(B, Nq, E, device=DEV, generator=g).to(torch.bfloat16)
+    sd = torch.tensor([31337], dtype=torch.int64, device=DEV) if p > 0 else None
+    o, lse = K.attn_fwd(q, k, v, None, H, D, scale, p, sd, 1, site=2)
+    ga = K.attn_bwd(q, k, v, None, o, do, lse, None, H, D, scale, p, sd, None, None, None, site=2)
+    gb = emulation.attn_bwd(q, k, v, None, o, do, lse, None, H, D, scale, p, sd, None, None, None, site=2)
+    torch.cuda.synchronize()
+    for a, b, n in zip(ga, gb, ("dq", "dk", "dv")):
+        err = _rel(a.float(), b.float())
+        assert err < 2e-2, f"{n}: rel err {err:.3e}"

@@ -96,7 +96,8 @@ def _worker(rank, world, port, cases, steps, out):
         wire = extra[1] if len(extra) > 1 else None
         model = _model()
         opt = FusedAdamW(model.parameters(), lr=1e-2, eps=0.1, weight_decay=0.01)
-        red = FlatGradReducer(opt.flat, bucket_bytes=16 << 10, overlap=overlap, in_graph=in_graph, wire_dtype=wire)
+        red = FlatGradReducer(opt.flat, bucket_bytes=None if overlap is None else 16 << 10, overlap=overlap,
+                              in_graph=in_graph, wire_dtype=wire)
         red.plan(model)
         red.broadcast_parameters(model)
         eng = StepEngine(_loss_fn(model), opt, reducer=red, graph=graph, accumulate=acc, warmup_eager=1,
@@ -130,6 +131,10 @@ CASES = {
     "graph_in_acc2_whole": (True, True, True, 2, False),
     # bf16 on the wire (SURVEY C-03's optional format)
     "eager_bf16wire": (False, False, True, 1, True, torch.bfloat16),
+    # the defaults (overlap=None, bucket_update=None): one all-reduce of the whole buffer after the
+    # backward, one AdamW pass — in and out of the graph
+    "eager_default": (False, False, None, 1, None),
+    "graph_in_default": (True, True, None, 1, None),
 }
 STEPS = 4
 
@@ -159,6 +164,19 @@ def test_graph_path_equals_eager_bitwise(ddp_runs):
     assert torch.equal(p["eager_acc2"], p["graph_in_acc2"])
     assert torch.equal(p["eager_acc2"], p["graph_out_acc2"])
     assert not torch.equal(p["eager"], p["eager_acc2"])
+    assert torch.equal(p["eager"], p["eager_default"])
+    assert torch.equal(p["eager"], p["graph_in_default"])
+
+
+def test_default_is_one_inline_allreduce(ddp_runs):
+    """The default data-parallel step: no ready points, the whole flat gradient as one bucket,
+    one optimizer pass (profiles/r6_reducer_ab.md: the side-stream overlap costs more than it
+    hides at these gradient sizes)."""
+    runs, _ = ddp_runs
+    for name in ("eager_default", "graph_in_default"):
+        r = runs[0][name]
+        assert r["log"] == [] and r["points"] == {} and not r["bucket_mode"], name
+        assert len(r["buckets"]) == 1 and r["buckets"][0][0] == 0, (name, r["buckets"])
 
 
 def test_bucket_updates_equal_whole_buffer_update_bitwise(ddp_runs):
@@ -254,7 +272,7 @@ def _worker_protocol(rank, world, port, out):
     dist.init(device_type="cpu")
     model = _model()
     flat = FlatParameterSpace(model.parameters(), with_shadow=False, replicate=False)
-    red = FlatGradReducer(flat, bucket_bytes=16 << 10)
+    red = FlatGradReducer(flat, bucket_bytes=16 << 10, overlap=True)
     red.plan(model)
     f = _loss_fn(model)
     b = _batches(rank, 1, 1)[0][0]

@@ -90,7 +90,7 @@ def _worker_gloo(rank, world, port, out):
     res = {}
     for graph in (True, False):
         model = _setup()
-        opt, red, eng = _run(model, lambda f: FlatGradReducer(f), graph, _data(rank, STEPS))
+        opt, red, eng = _run(model, lambda f: FlatGradReducer(f, overlap=True), graph, _data(rank, STEPS))
         res[graph] = dict(params=opt.flat.data.cpu(), sync=params_in_sync(opt.flat), in_graph=red.in_graph,
                           log=list(red.launch_log), replays=eng.replays)
         red.close()
@@ -123,7 +123,7 @@ def test_rccl_collectives_inside_the_step_graph():
     try:
         data = _data(0, STEPS)
         model = _setup()
-        opt, red, eng = _run(model, lambda f: FlatGradReducer(f, in_graph=True, force=True), True, data)
+        opt, red, eng = _run(model, lambda f: FlatGradReducer(f, in_graph=True, force=True, overlap=True), True, data)
         assert red.enabled and red.in_graph and eng.replays == STEPS - 2
         # eager steps 1, 2 and the capture's backward (the replays run no Python)
         assert red.launch_log == ["decoder", "layer_n", "layer_1_sa"] * 3
@@ -213,7 +213,7 @@ def _worker_rccl(rank, world, port, out):
     dist.init()
     model = _setup()
     opt = FusedAdamW(model.parameters(), lr=1e-2, eps=1.0, weight_decay=0.0)
-    red = FlatGradReducer(opt.flat)
+    red = FlatGradReducer(opt.flat)  # the default: one all-reduce after the backward, inside the graph
     red.plan(model)
     red.broadcast_parameters(model)
     eng = StepEngine(lambda b: model.loss(b[0], b[1], labels=b[2], x_masked=b[3]), opt, reducer=red, device="cuda",
@@ -240,7 +240,7 @@ def test_rccl_multi_gpu_ranks_graph_steps():
     mp.spawn(_worker_rccl, args=(world, port, out), nprocs=world, join=True)
     for r in range(world):
         assert out[r]["sync"] == 0.0, (r, out[r]["sync"])
-        assert out[r]["replays"] == STEPS - 2 and out[r]["bucket"]
+        assert out[r]["replays"] == STEPS - 2 and not out[r]["bucket"] and out[r]["log"] == []
         assert torch.equal(out[r]["params"], out[0]["params"])
     # one process, the concatenated batch, same deterministic kernels
     from perceiver_io_amd import ops
@@ -279,7 +279,7 @@ def _worker_gloo_overlap(rank, world, port, out):
     model = _setup()
     ops.set_deterministic(False)
     opt = FusedAdamW(model.parameters(), lr=1e-3, weight_decay=0.01)
-    red = FlatGradReducer(opt.flat)
+    red = FlatGradReducer(opt.flat, overlap=True)
     red.plan(model)
     red.broadcast_parameters(model)
     eng = StepEngine(lambda b: model.loss(b[0], b[1], labels=b[2], x_masked=b[3]), opt, reducer=red, device="cuda",

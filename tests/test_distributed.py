@@ -137,4 +137,5 @@ def test_bench_self_spawns_ranks_cpu_dry_run():
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 4
     assert out["dist_backend"] == "gloo" and out["params_in_sync"] is True
-    assert out["config"]["allreduce_overlap"] == ["decoder", "layer_1_sa", "layer_n"]
+    assert out["config"]["allreduce_overlap"] == []  # default: one all-reduce after the backward
+    assert out["config"]["bucket_update"] is False

@@ -165,6 +165,12 @@ def test_attention_dropout_statistics():
     (2, 1, 32, 900, 4, 32, 3, 0.3),
     (2, 2, 96, 64, 1, 64, 1, 0.5),
     (2, 2, 1500, 32, 1, 64, 1, 0.2),
+    # head width 16 over ≤ 64 keys (the 64-latent self-attention): the two-wave backward
+    (5, 5, 64, 64, 4, 16, 1, 0.1),
+    (5, 5, 64, 64, 4, 16, 1, 0.0),
+    (3, 3, 33, 64, 4, 16, 1, 0.1),
+    (3, 3, 33, 64, 4, 16, 1, 0.0),
+    (2, 2, 130, 40, 4, 16, 1, 0.1),
 ])
 def test_attention_dropout_matches_emulation(B, Bq, Nq, Nk, H, D, ns, p):
     """The kernels' hashed masks are reproduced bit-exactly by the emulation, so fwd AND bwd

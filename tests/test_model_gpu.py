@@ -96,18 +96,20 @@ def _three_way(mod, run, loss_tol=1e-2, tol=2e-2, jitter_run=None):
     _check_grads(g1, g0, tol=tol, floor=floor)
 
 
-@pytest.mark.parametrize("latents", [64, 512])
-def test_mlm_fused_matches_eager(latents):
+@pytest.mark.parametrize("latents,L,B", [(64, 96, 6), (512, 96, 6), (64, 2048, 2)])
+def test_mlm_fused_matches_eager(latents, L, B):
     """(512 latents: the self-attention backward has 2 key blocks and query splits, whose
-    accumulators the preceding kernel clears — csrc attn_bwd_zero_plan)"""
+    accumulators the preceding kernel clears — csrc attn_bwd_zero_plan; L = 2048: ~300 selected
+    positions per sequence, so the decoder's attention backward splits its queries and adds into
+    dK / dV, which the decoder's post-attention backward clears on the way)"""
     from perceiver_io_amd import ops
 
     torch.manual_seed(0)
-    lit = _mlm(latents=latents)
+    lit = _mlm(latents=latents, L=L)
     m = lit.model
-    ids = torch.randint(3, 500, (6, 96), device="cuda")
-    pad = torch.zeros(6, 96, dtype=torch.bool, device="cuda")
-    pad[2, 60:] = True
+    ids = torch.randint(3, 500, (B, L), device="cuda")
+    pad = torch.zeros(B, L, dtype=torch.bool, device="cuda")
+    pad[B // 2, 2 * L // 3:] = True
     xm, lab = m.masking(ids, pad)
     with ops.backend("torch"):
         l_ref = m.loss(ids, pad, labels=lab, x_masked=xm)
