@@ -386,7 +386,7 @@ def main(argv=None):
     dt = time.perf_counter() - t0
     dt = pdist.all_reduce_max(dt)
     final_loss = float(loss.float().item())
-    if fused:  # a checked-build index error seen inside the replayed graphs invalidates the run
+    if fused:  # a persistent-kernel spin timeout or a checked-build index error invalidates the run
         ops.check_device_errors()
     # data parallelism must leave every rank with bitwise the same parameters
     from perceiver_io_amd.parallel.reducer import params_in_sync

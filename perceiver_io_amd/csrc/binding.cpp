@@ -43,11 +43,16 @@ struct SlabJob {
   long long zero_n4;
 };
 }  // namespace pio
+#include "persist_args.h"
 #include "sb_args.h"
 namespace pio {
 bool sb_fwd_launch(const SBFwdArgs&, int C, hipStream_t);
 bool sb_bwd_launch(const SBBwdArgs&, int C, hipStream_t);
 bool sb_wgrad_launch(SBWgradArgs, int C, const SlabJob&, hipStream_t);
+bool sa_block_fwd_launch(const SABlockFwdArgs&, hipStream_t);
+unsigned persist_errors(bool);
+void persist_set_spin_limit(unsigned);
+int persist_sync_words(int);
 
 // sizes of the structs above as the kernel translation units see them (checked at import: a
 // mirror that drifts from common.h / attention.hip would hand the kernels garbage pointers)
@@ -140,7 +145,7 @@ void pixel_ce_fwd_launch(int, int, const float*, const float*, const float*, con
 void pixel_ce_bwd_launch(int, int, const float*, const float*, const float*, const int64_t*, const float*,
                          const float*, const float*, long long, float*, float*, float*, float*, hipStream_t);
 void adamw_launch(float*, float*, float*, float*, uint16_t*, long long, const float*, float, float, float, float,
-                  int, int, const float*, float*, int, hipStream_t);
+                  int, int, const float*, float*, int, const float*, hipStream_t);
 void cast_bf16_launch(const float*, uint16_t*, long long, hipStream_t);
 void reduce_probe_launch(const float*, float*, hipStream_t);
 void fold_replicas_launch(float*, float*, long long, int, hipStream_t);
@@ -496,6 +501,96 @@ std::vector<Tensor> sa_layer_fwd(Tensor qkv, Tensor x, int64_t N, double scale, 
   return {o, lse, z, y, m, r, u};
 }
 
+
+// sync words of the persistent kernels (csrc/persist.hip): one zero-initialised buffer per
+// (device, stream), allocated on the first launch on that stream (never during a stream capture:
+// nullptr then, the caller runs the per-layer kernels), reset to zero by the last workgroup of
+// every launch — launches on one stream run one after another, so they can share it
+unsigned* persist_sync_buffer(const Tensor& like, int words) {
+  // grown buffers are kept alive too: a captured graph may still name an older one
+  static std::unordered_map<uint64_t, std::vector<Tensor>> bufs;
+  hipStream_t st = stream();
+  const uint64_t key = reinterpret_cast<uint64_t>(st) ^ ((uint64_t)like.get_device() << 56);
+  auto& v = bufs[key];
+  if (!v.empty() && v.back().numel() >= words) return reinterpret_cast<unsigned*>(v.back().data_ptr<int>());
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  // the zero fill runs on the current stream: ordered before every launch that uses the buffer
+  v.push_back(torch::zeros({std::max(words, 1 << 14)}, like.options().dtype(torch::kInt32)));
+  return reinterpret_cast<unsigned*>(v.back().data_ptr<int>());
+}
+
+// persistent self-attention block forward (csrc/persist.hip): every layer of a C = 64, H = 4
+// block with N ≤ 256 latents in ONE launch.  Per layer i: wo..b2 (its post-attention block) and,
+// for i < L - 1, the next layer's (lnw, lnb, wq, bq); the last layer optionally gets the next
+// cross-attention layer's LN + query (64 rows) or K/V (128 rows) projection as an L-th entry.  Returns, per layer, [o, lse, z, y, m2, r2, u] + [qkv_n, mean_n, rstd_n] when that
+// layer has a next projection.  Empty list: the operands do not qualify (the caller runs the
+// per-layer kernels).
+std::vector<Tensor> sa_block_fwd(Tensor qkv0, Tensor x0, int64_t N, double scale, double eps, std::vector<Tensor> wo,
+                                 std::vector<Tensor> bo, std::vector<Tensor> g2, std::vector<Tensor> be2,
+                                 std::vector<Tensor> w1, std::vector<Tensor> b1, std::vector<Tensor> w2,
+                                 std::vector<Tensor> b2, std::vector<Tensor> lnw, std::vector<Tensor> lnb,
+                                 std::vector<Tensor> wq, std::vector<Tensor> bq, OptT seed, double p) {
+  const int C = 64, H = 4;
+  const int L = (int)wo.size();
+  TORCH_CHECK(L >= 1 && L <= pio::kPersistMaxLayers, "sa_block_fwd: 1..8 layers");
+  TORCH_CHECK(bo.size() == (size_t)L && g2.size() == (size_t)L && be2.size() == (size_t)L && w1.size() == (size_t)L &&
+                  b1.size() == (size_t)L && w2.size() == (size_t)L && b2.size() == (size_t)L,
+              "sa_block_fwd: one post-attention parameter set per layer");
+  const int nn = (int)wq.size();
+  TORCH_CHECK((nn == L - 1 || nn == L) && lnw.size() == (size_t)nn && lnb.size() == (size_t)nn && bq.size() == (size_t)nn,
+              "sa_block_fwd: L - 1 next projections (+ an optional last query projection)");
+  TORCH_CHECK(qkv0.is_contiguous() && x0.is_contiguous(), "sa_block_fwd: contiguous qkv / x");
+  const int R = (int)x0.size(0);
+  TORCH_CHECK(x0.size(1) == C && qkv0.size(0) == R && qkv0.size(1) == 3 * C, "sa_block_fwd: C = 64, qkv (R, 192)");
+  CHECK_DT(x0, torch::kFloat32);
+  if (N <= 0 || N > 256 || N % 64 != 0 || R % N != 0 || (long long)R * 3 * C * 2 >= (1LL << 31)) return {};
+  auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  if (!al(qkv0.data_ptr()) || !al(x0.data_ptr())) return {};
+  auto f32 = x0.options().dtype(torch::kFloat32);
+  auto b16 = x0.options().dtype(torch::kBFloat16);
+  const int B = R / (int)N;
+  unsigned* sync = persist_sync_buffer(x0, pio::persist_sync_words(B));
+  if (sync == nullptr) return {};
+  pio::SABlockFwdArgs a{};
+  a.QKV0 = bfp(qkv0);
+  a.X0 = f32p(x0);
+  a.sync = sync;
+  a.L = L; a.N = (int)N; a.R = R;
+  a.scale_log2 = (float)(scale * 1.4426950408889634);
+  a.eps = (float)eps;
+  a.dr = make_drop(seed, 0, p);
+  std::vector<Tensor> out;
+  for (int i = 0; i < L; ++i) {
+    pio::SAFwdLayer& y = a.ly[i];
+    for (const Tensor* t : {&wo[i], &w1[i], &w2[i]})
+      TORCH_CHECK(t->is_contiguous() && t->size(0) == C && t->size(1) == C, "sa_block_fwd: (C, C) weights");
+    y.Wo = bfp(wo[i]); y.W1 = bfp(w1[i]); y.W2 = bfp(w2[i]);
+    y.bo = f32p(bo[i]); y.g2 = f32p(g2[i]); y.be2 = f32p(be2[i]); y.b1 = f32p(b1[i]); y.b2 = f32p(b2[i]);
+    if (!al(y.Wo) || !al(y.W1) || !al(y.W2) || !al(y.g2) || !al(y.be2) || !al(y.bo) || !al(y.b1) || !al(y.b2)) return {};
+    Tensor o = torch::empty({B, (int)N, C}, b16), lse = torch::empty({B, (int)N, H}, f32);
+    Tensor z = torch::empty({R, C}, f32), yy = torch::empty({R, C}, f32);
+    Tensor m = torch::empty({R}, f32), r = torch::empty({R}, f32), u = torch::empty({R, C}, b16);
+    y.O = bfp_mut(o); y.LSE = lse.data_ptr<float>(); y.Z = z.data_ptr<float>(); y.Y = yy.data_ptr<float>();
+    y.mean2 = m.data_ptr<float>(); y.rstd2 = r.data_ptr<float>(); y.U = bfp_mut(u);
+    out.insert(out.end(), {o, lse, z, yy, m, r, u});
+    if (i < nn) {
+      const int nq = (int)wq[i].size(0);
+      TORCH_CHECK(wq[i].is_contiguous() && wq[i].size(1) == C && (nq == 3 * C || (i == L - 1 && (nq == C || nq == 2 * C))) &&
+                      bq[i].numel() == nq && lnw[i].numel() == C && lnb[i].numel() == C,
+                  "sa_block_fwd: next projection (3C, C) (the last layer's may be a (C, C) query or (2C, C) K/V projection)");
+      y.Wq = bfp(wq[i]); y.lnw = f32p(lnw[i]); y.lnb = f32p(lnb[i]); y.bq = f32p(bq[i]); y.nq = nq;
+      if (!al(y.Wq) || !al(y.lnw) || !al(y.lnb) || !al(y.bq)) return {};
+      Tensor qn = torch::empty({R, nq}, b16), m1 = torch::empty({R}, f32), r1 = torch::empty({R}, f32);
+      y.QKVn = bfp_mut(qn); y.mean1n = m1.data_ptr<float>(); y.rstd1n = r1.data_ptr<float>();
+      out.insert(out.end(), {qn, m1, r1});
+    }
+  }
+  if (!pio::sa_block_fwd_launch(a, stream())) return {};
+  return out;
+}
+
+unsigned persist_errors(bool reset) { return pio::persist_errors(reset); }
 
 namespace {
 pio::SlabJob make_job(const OptT& slab, std::vector<Tensor>& dsts, const std::vector<int64_t>& offs);
@@ -1318,7 +1413,14 @@ void stage_step(std::vector<Tensor> dsts, std::vector<Tensor> srcs, OptT hyper_d
                                      sv.data(), (int)sv.size(), stream()) == 0);
 }
 
-void sumsq(Tensor g, Tensor out) { pio::sumsq_launch(f32p(g), g.numel(), out.data_ptr<float>(), stream()); }
+// Σ g² as kSumsqBlocks fixed-order partials (part: ≥ kSumsqBlocks fp32), read by adamw(norm_part=)
+constexpr int kSumsqParts = 512;  // common.h kSumsqBlocks
+void sumsq(Tensor g, Tensor part) {
+  CHECK_DT(g, torch::kFloat32); CHECK_DT(part, torch::kFloat32);
+  TORCH_CHECK(g.is_contiguous() && part.is_contiguous() && part.numel() >= kSumsqParts,
+              "sumsq: contiguous gradient, a contiguous partial buffer of >= 512 floats");
+  pio::sumsq_launch(f32p(g), g.numel(), part.data_ptr<float>(), stream());
+}
 
 // a, b: (B, ...) fp32 contiguous, equal shapes → (Σ_b a[b], Σ_b b[b]) in one launch
 // oa = Σ_b a[b] (a optional), ob = Σ_b b[b] — or, with ob_acc, ob_acc += Σ_b b[b] in place (the
@@ -1428,7 +1530,10 @@ void pixel_ce_bwd(Tensor h, Tensor w, Tensor b, Tensor labels, Tensor wts, Tenso
 }
 
 void adamw(Tensor p, Tensor g, Tensor m, Tensor v, OptT shadow, Tensor hyper, double eps, double wd, double clip,
-           double gscale, bool l2, bool zero_grad, OptT loss_src, OptT loss_ring) {
+           double gscale, bool l2, bool zero_grad, OptT loss_src, OptT loss_ring, OptT norm_part) {
+  TORCH_CHECK(clip <= 0 || (norm_part.has_value() && norm_part->is_contiguous() && norm_part->numel() >= kSumsqParts &&
+                            norm_part->scalar_type() == torch::kFloat32),
+              "adamw: clip > 0 needs norm_part (the sumsq partials of the gradient)");
   TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && m.is_contiguous() && v.is_contiguous());
   TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel());
   uint16_t* sp = nullptr;
@@ -1443,7 +1548,8 @@ void adamw(Tensor p, Tensor g, Tensor m, Tensor v, OptT shadow, Tensor hyper, do
                     f32p(hyper), (float)eps, (float)wd, (float)clip, (float)gscale, l2 ? 1 : 0, zero_grad ? 1 : 0,
                     loss_src.has_value() ? f32p(*loss_src) : nullptr,
                     loss_ring.has_value() ? loss_ring->data_ptr<float>() : nullptr,
-                    loss_ring.has_value() ? (int)loss_ring->numel() : 1, stream());
+                    loss_ring.has_value() ? (int)loss_ring->numel() : 1,
+                    clip > 0 ? f32p(*norm_part) : nullptr, stream());
 }
 
 // self-test of the device cross-lane reductions: (6, 64) = wave_sum, wave_max, half_sum,
@@ -1866,7 +1972,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sumsq", &sumsq);
   m.def("adamw", &adamw, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("shadow"), py::arg("hyper"),
         py::arg("eps"), py::arg("wd"), py::arg("clip"), py::arg("gscale"), py::arg("l2") = false,
-        py::arg("zero_grad") = false, py::arg("loss_src") = py::none(), py::arg("loss_ring") = py::none());
+        py::arg("zero_grad") = false, py::arg("loss_src") = py::none(), py::arg("loss_ring") = py::none(),
+        py::arg("norm_part") = py::none());
   m.def("cast_bf16", &cast_bf16);
   m.def("reduce_probe", &reduce_probe);
   m.def("fold_replicas", &fold_replicas);
@@ -1874,6 +1981,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pe_proj_fwd", &pe_proj_fwd);
   m.def("pe_gemm", &pe_gemm, py::arg("A"), py::arg("B"), py::arg("bf16_out") = false, py::arg("pad_rows") = 0);
   m.def("attn_fwd_pe", &attn_fwd_pe);
+  m.def("sa_block_fwd", &sa_block_fwd, py::arg("qkv0"), py::arg("x0"), py::arg("N"), py::arg("scale"), py::arg("eps"),
+        py::arg("wo"), py::arg("bo"), py::arg("g2"), py::arg("be2"), py::arg("w1"), py::arg("b1"), py::arg("w2"),
+        py::arg("b2"), py::arg("lnw"), py::arg("lnb"), py::arg("wq"), py::arg("bq"), py::arg("seed") = py::none(),
+        py::arg("p") = 0.0);
+  m.def("persist_errors", &persist_errors, py::arg("reset") = true);
+  m.def("persist_set_spin_limit", [](int64_t n) { pio::persist_set_spin_limit((unsigned)n); }, py::arg("n"));
   m.def("attn_bwd_pe_part_rows", &attn_bwd_pe_part_rows);
   m.def("attn_bwd_pe_implicit", &attn_bwd_pe_implicit, py::arg("q"), py::arg("P"), py::arg("pes"), py::arg("pesq"),
         py::arg("wt"), py::arg("dO"), py::arg("lse"), py::arg("delta"), py::arg("pix"), py::arg("dq"), py::arg("D"),

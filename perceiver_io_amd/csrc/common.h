@@ -309,6 +309,8 @@ __device__ __forceinline__ void zero_span_block(const SlabJob& j) {
 // Deterministic mode: one workgroup per column block sums all S rows in a fixed order and
 // adds once (single writer).
 constexpr int kSlabColsPerBlock = 1024;
+// blocks of the gradient sum-of-squares pass: one fp32 partial each (elementwise.hip sumsq_kernel)
+constexpr int kSumsqBlocks = 512;
 // part: ≥ 4 KiB of 16-B aligned LDS.  Deterministic mode runs on the first 256 threads of the
 // carrier's workgroup (the others only join the barrier); the other mode splits the rows between
 // the two halves of a 512-thread carrier.  NV: row loads in flight per thread (a one-workgroup-

@@ -226,62 +226,76 @@ __global__ void text_mask_kernel(const int64_t* __restrict__ x, const bool* __re
 
 // sum of squares of the flat gradient (for clip_grad_norm) → atomic into out[0]
 // 16-byte loads, four independent accumulation chains, ≈4 workgroups per CU
-__global__ void sumsq_kernel(const float* __restrict__ g, long long n, float* __restrict__ out) {
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+// Σ g² in fixed order, no atomics: block b writes its partial to part[b] (kSumsqBlocks blocks,
+// grid-stride, 8 independent 16-byte loads in flight per thread); the AdamW kernels sum the
+// partials themselves (adam_clip_scale).  The previous single-address atomic per block put
+// 2048 serialised adds at the end of an HBM-bound pass (36 µs for the 68 MB LArTPC gradient).
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g, long long n, float* __restrict__ part) {
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const long long n4 = ((reinterpret_cast<uintptr_t>(g) & 15) == 0) ? n >> 2 : 0;
   const long long stride = (long long)gridDim.x * blockDim.x;
   const float4* g4 = reinterpret_cast<const float4*>(g);
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  // four independent 16-byte loads in flight per thread (HBM-bound on the LArTPC output-query table)
-  for (; i + 3 * stride < n4; i += 4 * stride) {
-    const float4 a = g4[i], b = g4[i + stride], c = g4[i + 2 * stride], d = g4[i + 3 * stride];
-    s0 = fmaf(a.x, a.x, s0); s1 = fmaf(a.y, a.y, s1); s2 = fmaf(a.z, a.z, s2); s3 = fmaf(a.w, a.w, s3);
-    s0 = fmaf(b.x, b.x, s0); s1 = fmaf(b.y, b.y, s1); s2 = fmaf(b.z, b.z, s2); s3 = fmaf(b.w, b.w, s3);
-    s0 = fmaf(c.x, c.x, s0); s1 = fmaf(c.y, c.y, s1); s2 = fmaf(c.z, c.z, s2); s3 = fmaf(c.w, c.w, s3);
-    s0 = fmaf(d.x, d.x, s0); s1 = fmaf(d.y, d.y, s1); s2 = fmaf(d.z, d.z, s2); s3 = fmaf(d.w, d.w, s3);
+  for (; i + 7 * stride < n4; i += 8 * stride) {
+    float4 a[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] = g4[i + k * stride];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      s[k] = fmaf(a[k].x, a[k].x, fmaf(a[k].y, a[k].y, fmaf(a[k].z, a[k].z, fmaf(a[k].w, a[k].w, s[k]))));
   }
   for (; i < n4; i += stride) {
     const float4 a = g4[i];
-    s0 = fmaf(a.x, a.x, s0); s1 = fmaf(a.y, a.y, s1); s2 = fmaf(a.z, a.z, s2); s3 = fmaf(a.w, a.w, s3);
+    s[0] = fmaf(a.x, a.x, fmaf(a.y, a.y, fmaf(a.z, a.z, fmaf(a.w, a.w, s[0]))));
   }
   for (long long j = (n4 << 2) + (long long)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
     const float v = g[j];
-    s0 = fmaf(v, v, s0);
+    s[1] = fmaf(v, v, s[1]);
   }
-  float s = wave_sum((s0 + s1) + (s2 + s3));
-  __shared__ float red[16];
-  if (lane_id() == 0) red[wave_id()] = s;
+  float t = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  t = wave_sum(t);
+  __shared__ float red[4];
+  if (lane_id() == 0) red[wave_id()] = t;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    float t = 0.f;
-    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
-    atomicAdd(out, t);
-  }
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-// hyper[0] = lr, [1] = step (already incremented), [2] = grad sum of squares (if clip > 0),
-// [3] = beta1, [4] = beta2, [7] = loss-ring slot — read from device memory so schedulers can
+// the clip factor of a step from sumsq_kernel's partials, in a fixed order (every block of the
+// AdamW grid the same value): wave 0 sums the kSumsqBlocks partials, LDS broadcast
+__device__ __forceinline__ float adam_clip_scale(const float* __restrict__ part, float clip, float gscale) {
+  __shared__ float s_norm2;
+  if (threadIdx.x < 64) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < kSumsqBlocks / 64; ++k) t += part[threadIdx.x + 64 * k];
+    t = wave_sum(t);
+    if (threadIdx.x == 0) s_norm2 = t;
+  }
+  __syncthreads();
+  const float norm = sqrtf(s_norm2) * gscale;
+  const float f = clip / (norm + 1e-6f);
+  return f < 1.f ? f : 1.f;
+}
+
+// hyper[0] = lr, [1] = step (already incremented), [3] = beta1, [4] = beta2, [7] = loss-ring slot — read from device memory so schedulers can
 // change them between replays of a captured step.
 // loss_src (optional): the step's scalar loss, copied by thread 0 into loss_ring[hyper[7] % ring_n]
 // (the step engine hands that slot back as the step's loss: no separate copy launch per step)
 // zero_g: the gradient is cleared as it is consumed (a replayed step then needs no separate
 // zero fill of the flat gradient buffer before its backward)
+// clip > 0: the gradient's sum of squares comes as sumsq_kernel's per-block partials (norm_part)
 __global__ void adamw_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                              float* __restrict__ v, uint16_t* __restrict__ shadow, long long n,
                              const float* __restrict__ hyper, float eps, float wd, float clip, float gscale,
                              int l2, int zero_g, const float* __restrict__ loss_src, float* __restrict__ loss_ring,
-                             int ring_n) {
+                             int ring_n, const float* __restrict__ norm_part) {
   const float lr = hyper[0], step = hyper[1], beta1 = hyper[3], beta2 = hyper[4];
   if (loss_src != nullptr && blockIdx.x == 0 && threadIdx.x == 0) loss_ring[(int)hyper[7] % ring_n] = *loss_src;
   const float bc1 = 1.f - powf(beta1, step), bc2 = 1.f - powf(beta2, step);
   // g holds the all-reduced SUM over ranks (gscale = 1 / world makes it the mean): the clip
   // threshold applies to the norm of the MEAN gradient, as in single-process training
   float gs = gscale;
-  if (clip > 0.f) {
-    const float norm = sqrtf(hyper[2]) * gscale;
-    const float f = clip / (norm + 1e-6f);
-    if (f < 1.f) gs *= f;
-  }
+  if (clip > 0.f) gs *= adam_clip_scale(norm_part, clip, gscale);
   const float step_size = lr / bc1;
   const float bc2s = sqrtf(bc2);
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
@@ -310,16 +324,13 @@ __global__ __launch_bounds__(256) void adamw4_kernel(float4* __restrict__ p, flo
                                                      uint2* __restrict__ shadow, long long n4,
                                                      const float* __restrict__ hyper, float eps, float wd, float clip,
                                                      float gscale, int l2, int zero_g, const float* __restrict__ loss_src,
-                                                     float* __restrict__ loss_ring, int ring_n) {
+                                                     float* __restrict__ loss_ring, int ring_n,
+                                                     const float* __restrict__ norm_part) {
   const float lr = hyper[0], step = hyper[1], beta1 = hyper[3], beta2 = hyper[4];
   if (loss_src != nullptr && blockIdx.x == 0 && threadIdx.x == 0) loss_ring[(int)hyper[7] % ring_n] = *loss_src;
   const float bc1 = 1.f - powf(beta1, step), bc2 = 1.f - powf(beta2, step);
   float gs = gscale;
-  if (clip > 0.f) {
-    const float norm = sqrtf(hyper[2]) * gscale;
-    const float f = clip / (norm + 1e-6f);
-    if (f < 1.f) gs *= f;
-  }
+  if (clip > 0.f) gs *= adam_clip_scale(norm_part, clip, gscale);
   const float step_size = lr / bc1;
   const float bc2s = sqrtf(bc2);
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
@@ -395,10 +406,8 @@ void text_mask_launch(const int64_t* x, const bool* pad, int64_t* state, int64_t
   hipLaunchKernelGGL(text_mask_kernel, grid_for(n), dim3(256), 0, st, x, pad, state, xm, labels, n, unk_id, mask_id, p, lo,
                      range, advance);
 }
-void sumsq_launch(const float* g, long long n, float* out, hipStream_t st) {
-  long long b = (n + 4095) / 4096;
-  b = b > 2048 ? 2048 : (b < 1 ? 1 : b);
-  hipLaunchKernelGGL(sumsq_kernel, dim3((unsigned)b), dim3(256), 0, st, g, n, out);
+void sumsq_launch(const float* g, long long n, float* part, hipStream_t st) {
+  hipLaunchKernelGGL(sumsq_kernel, dim3(kSumsqBlocks), dim3(256), 0, st, g, n, part);
 }
 
 // dst[idx[r]][:] += src[r][:] — the backward of a row gather (rows of idx may repeat: fp32
@@ -499,7 +508,7 @@ void batch_sum2_launch(const float* a, const float* b, float* oa, float* ob, int
 }
 void adamw_launch(float* p, float* g, float* m, float* v, uint16_t* shadow, long long n, const float* hyper,
                   float eps, float wd, float clip, float gscale, int l2, int zero_g, const float* loss_src,
-                  float* loss_ring, int ring_n, hipStream_t st) {
+                  float* loss_ring, int ring_n, const float* norm_part, hipStream_t st) {
   const bool vec = n % 4 == 0 && ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) |
                                     reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v)) & 15) == 0 &&
                    (reinterpret_cast<uintptr_t>(shadow) & 7) == 0;
@@ -507,10 +516,10 @@ void adamw_launch(float* p, float* g, float* m, float* v, uint16_t* shadow, long
     hipLaunchKernelGGL(adamw4_kernel, grid_for(n / 4), dim3(256), 0, st, reinterpret_cast<float4*>(p),
                        reinterpret_cast<float4*>(g), reinterpret_cast<float4*>(m), reinterpret_cast<float4*>(v),
                        reinterpret_cast<uint2*>(shadow), n / 4, hyper, eps, wd, clip, gscale, l2, zero_g, loss_src,
-                       loss_ring, ring_n);
+                       loss_ring, ring_n, norm_part);
   else
     hipLaunchKernelGGL(adamw_kernel, grid_for(n), dim3(256), 0, st, p, g, m, v, shadow, n, hyper, eps, wd, clip, gscale,
-                       l2, zero_g, loss_src, loss_ring, ring_n);
+                       l2, zero_g, loss_src, loss_ring, ring_n, norm_part);
 }
 // grad[i] += Σ_r rep[r][i], rep[r][i] ← 0 (replicated gradient accumulators, see ops/optim.py)
 __global__ void fold_replicas_kernel(float* __restrict__ grad, float* __restrict__ rep, long long n, int nrep) {

@@ -61,15 +61,31 @@ def deterministic() -> bool:
 
 
 def check_device_errors(reset: bool = True) -> None:
-    """Checked builds (``PERCEIVER_CHECKED=1``): read the kernels' sticky index-validation words
-    (one host sync) and raise on any — token ids, gather rows and class labels outside their
-    tables (the kernels clamped / skipped the access).  Outside a graph capture every checked
-    launch raises at once (``checked_sync``); inside a replayed hipGraph nothing can, so the
-    Trainer calls this at every logging step and at the end of ``fit``, and ``bench.py`` after
-    its timed loop (SURVEY §5.3 failure detection).  A no-op in the regular build."""
+    """Read the kernels' sticky device error words (one host sync) and raise on any.
+
+    * ``csrc/persist.hip`` ``sa_block_fwd``: a bounded spin that timed out (bit 0: a tile gave up
+      waiting for its sample's next-layer Q/K/V rows and computed on whatever was there) or an
+      invalid tile ticket (bit 1).  The launch finishes either way (no GPU hang); this turns the
+      corrupted forward into an error instead of silent training on garbage.
+    * checked builds (``PERCEIVER_CHECKED=1``): the index-validation words — token ids, gather
+      rows and class labels outside their tables (the kernels clamped / skipped the access).
+      Outside a graph capture every checked launch raises at once (``checked_sync``); inside a
+      replayed hipGraph nothing can.
+
+    Called by the Trainer at every logging step and at the end of ``fit`` and by ``bench.py``
+    after its timed loop (SURVEY §5.3 failure detection)."""
     if not ext.available() or not torch.cuda.is_available() or not torch.cuda.is_initialized():
         return
     K = ext.require()
+    e = int(K.persist_errors(reset))
+    if e:
+        what = []
+        if e & 1:
+            what.append("a bounded spin timed out: a tile computed on rows its sample had not published")
+        if e & 2:
+            what.append("a workgroup drew a tile ticket outside the grid")
+        raise RuntimeError(f"sa_block_fwd_kernel (csrc/persist.hip) device error word {e:#x}: " + "; ".join(what)
+                           + ".  The persistent self-attention block forward's results of that step are invalid")
     if K.checked_build():
         c = int(K.check_errors(reset))
         if c:

@@ -264,6 +264,22 @@ def sa_layer_fwd(qkv, x, N, scale, wo, bo, g2, be2, eps, w1, b1, w2, b2, lnw=Non
                                                     site, p))
 
 
+def sa_block_fwd(qkv0, x0, N, scale, eps, wo, bo, g2, be2, w1, b1, w2, b2, lnw, lnb, wq, bq, seed=None, p=0.0):
+    """The persistent block forward (persist.hip sa_block_fwd_kernel): sa_layer_fwd of every layer
+    in one call, layer i's next projection from (lnw, lnb, wq, bq)[i] when present.  Returns the
+    per-layer outputs flattened ([o, lse, z, y, m2, r2, u] + [qkv_n, mean_n, rstd_n])."""
+    out, qkv, x = [], qkv0, x0
+    for i in range(len(wo)):
+        nx = i < len(wq)
+        r = sa_layer_fwd(qkv, x, N, scale, wo[i], bo[i], g2[i], be2[i], eps, w1[i], b1[i], w2[i], b2[i],
+                         lnw[i] if nx else None, lnb[i] if nx else None, wq[i] if nx else None,
+                         bq[i] if nx else None, seed=seed, site=i, p=p)
+        out += list(r)
+        x = r[2]
+        qkv = r[7] if nx else None
+    return out
+
+
 def post_attn_ln_linear_fwd(o, x, wo, bo, g2, be2, eps, w1, b1, w2, b2, lnw, lnb, wq, bq, seed=None, site=0, p=0.0):
     """post_attn_fwd of layer l, then ln_linear_fwd (LN1 + packed QKV) of layer l+1."""
     z, y, m2, r2, u = post_attn_fwd(o, x, wo, bo, g2, be2, eps, w1, b1, w2, b2, seed, site, p)
@@ -611,17 +627,20 @@ def text_mask(x, pad, state, unk, mask, p, lo, hi, advance=True):
     return xm, torch.where(sel, x, torch.full_like(x, -100))
 
 
-def sumsq(g, out):
-    out += (g.float() ** 2).sum()
+def sumsq(g, part):
+    """Σ g² as the kernel's partial buffer (csrc elementwise.hip sumsq_kernel): here one partial."""
+    part.zero_()
+    part[0] = (g.float() ** 2).sum()
 
 
-def adamw(p, g, m, v, shadow, hyper, eps, wd, clip, gscale, l2=False, zero_grad=False, loss_src=None, loss_ring=None):
+def adamw(p, g, m, v, shadow, hyper, eps, wd, clip, gscale, l2=False, zero_grad=False, loss_src=None, loss_ring=None,
+          norm_part=None):
     lr, step, b1, b2 = float(hyper[0]), float(hyper[1]), float(hyper[3]), float(hyper[4])
     if loss_src is not None:  # the step's loss into the engine's ring slot hyper[7]
         loss_ring.view(-1)[int(float(hyper[7])) % loss_ring.numel()] = loss_src.reshape(())
     gs = gscale
     if clip > 0:
-        norm = math.sqrt(float(hyper[2])) * gscale  # norm of the mean (all-reduced sum × 1/world)
+        norm = math.sqrt(float(norm_part.sum())) * gscale  # norm of the mean (all-reduced sum × 1/world)
         f = clip / (norm + 1e-6)
         if f < 1:
             gs *= f

@@ -934,6 +934,11 @@ SA_LAYER_FUSED = True
 PA_SIZES = lambda C: [C * C, C, C, C, C * C, C, C * C, C]  # noqa: E731  (Wo bo γ2 β2 W1 b1 W2 b2)
 LL_SIZES = lambda C: [C, C, 3 * C * C, 3 * C]                 # noqa: E731  (γ1 β1 Wqkv bqkv)
 SA_NP = 12  # parameters per self-attention layer (layer_spec_and_params order)
+# the fused C = 64 stacks with N <= 256 latents run every layer of a block in ONE persistent launch
+# (csrc/persist.hip); False: one launch per layer (chain.hip; the N = 512 path, and the reference the
+# persistent kernel is bitwise checked against in tests/test_persist_gpu.py).  Same-box A/B, round 6:
+# 1.342 / 1.346 ms per headline step against 1.372 / 1.373 with the per-layer launches
+PERSIST_BLOCK = True
 # channel widths run as one fused self-attention block node (PERCEIVER_SA_BLOCK_C128=0 keeps C = 128
 # stacks layer by layer)
 SA_BLOCK_CHANNELS = (32, 64, 128)
@@ -980,7 +985,33 @@ class _SABlockFn(torch.autograd.Function):
         # C = 64, H = 4 latent stacks, attention-probability dropout included (csrc/chain.hip
         # sa_layer_fwd_chain8_kernel: up to 512 latents)
         fused_layer = SA_LAYER_FUSED and C == 64 and H == 4 and N <= 512 and N % 64 == 0
-        for i in range(L):
+        res = None
+        if fused_layer and PERSIST_BLOCK and N <= 256 and hasattr(K, "sa_block_fwd"):
+            wantq = _LOOKAHEAD["want_q"]
+            nxt = [(P[i + 1][0], P[i + 1][1], bws[i + 1][0], P[i + 1][3]) for i in range(L - 1)]
+            if wantq is not None:  # the following cross-attention layer's LN + query projection
+                nxt.append(tuple(wantq[:4]))
+            res = K.sa_block_fwd(qkv, xl, N, scale, EPS, [b[2] for b in bws], [p[5] for p in P], [p[6] for p in P],
+                                 [p[7] for p in P], [b[3] for b in bws], [p[9] for p in P], [b[4] for b in bws],
+                                 [p[11] for p in P], [n[0] for n in nxt], [n[1] for n in nxt], [n[2] for n in nxt],
+                                 [n[3] for n in nxt], seed=seed, p=pdrop)
+        if res:
+            k = 0
+            for i in range(L):
+                o, lse, z, y, m2, r2, u = res[k:k + 7]
+                k += 7
+                qkv_n = mean_n = rstd_n = None
+                if i < len(nxt):
+                    qkv_n, mean_n, rstd_n = res[k:k + 3]
+                    k += 3
+                saved += [xl, qkv, mean1, rstd1, o, lse, y, m2, r2, u]
+                if i == L - 1 and wantq is not None:
+                    _LOOKAHEAD["want_q"] = None
+                    _LOOKAHEAD["have_q"] = (z, qkv_n, mean_n, rstd_n, wantq[0])
+                    ctx.out_ptr = z.data_ptr()
+                    qkv_n = mean_n = rstd_n = None
+                xl, qkv, mean1, rstd1 = z, qkv_n, mean_n, rstd_n
+        for i in range(L if not res else 0):
             p = P[i]
             _, _, wo, w1, w2 = bws[i]
             bo, g2, be2, b1, b2 = p[5], p[6], p[7], p[9], p[11]

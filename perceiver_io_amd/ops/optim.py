@@ -175,6 +175,9 @@ class FusedAdamW(torch.optim.Optimizer):
         self.exp_avg_sq = torch.zeros(self.flat.numel, dtype=torch.float32, device=dev)
         self.hyper = torch.zeros(8, dtype=torch.float32, device=dev)
         self.max_grad_norm = float(max_grad_norm)
+        # the gradient's sum of squares as fixed-order per-block partials (sumsq → adamw norm_part):
+        # no atomics, so the clip factor is bitwise reproducible in every mode
+        self.norm_part = torch.zeros(512, dtype=torch.float32, device=dev) if self.max_grad_norm > 0 else None
         self.l2 = False  # decoupled decay (AdamW); FusedAdam sets the coupled L2 form
         self._step = 0
         self._ring = _HostRing(8, 8, dev) if dev.type == "cuda" else None
@@ -232,19 +235,13 @@ class FusedAdamW(torch.optim.Optimizer):
         g = self.param_groups[0]
         self.flat.fold()
         if self.max_grad_norm > 0:
-            from . import deterministic
-
-            if deterministic():  # torch's tree reduction instead of per-block atomics
-                torch.sum(self.flat.grad * self.flat.grad, dim=0, keepdim=True, out=self.hyper[2:3])
-            else:
-                if not norm_staged:  # else the per-step staging (stage_step / stage_hyper) zeroed it
-                    self.hyper[2:3].zero_()
-                K.sumsq(self.flat.grad, self.hyper[2:3])
+            K.sumsq(self.flat.grad, self.norm_part)
         lo = self.loss_out
         K.adamw(self.flat.data, self.flat.grad, self.exp_avg, self.exp_avg_sq, self.flat.shadow, self.hyper,
                 g["eps"], g["weight_decay"], self.max_grad_norm, self.grad_scale, l2=self.l2,
                 zero_grad=zero_grad and self.flat.grad_rep is None,
-                loss_src=None if lo is None else lo[0], loss_ring=None if lo is None else lo[1])
+                loss_src=None if lo is None else lo[0], loss_ring=None if lo is None else lo[1],
+                norm_part=self.norm_part)
 
     @torch.no_grad()
     def step(self, closure=None, staged: bool = False):

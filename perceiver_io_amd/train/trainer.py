@@ -459,7 +459,7 @@ class Trainer:
                     self.callback_metrics.update(vals)
                     self.log_scalars(vals)
                     ops.mlm_head.check_overflow()  # fixed-capacity MLM rows: fail loudly, never truncate
-                    ops.check_device_errors()  # checked builds: index errors seen inside replayed graphs
+                    ops.check_device_errors()  # persistent-kernel spin timeouts, checked-build index errors
                     if self.terminate_on_nan and not all(math.isfinite(v) for v in vals.values()):
                         raise ValueError(f"non-finite metric at step {self.global_step}: {vals}")
                     if self.enable_progress_bar and self.is_global_zero:

@@ -98,3 +98,28 @@ def test_seq_clf_dropout_fused_under_graph(tmp_path, monkeypatch):
     assert tr.global_step == 2 * 6
     assert torch.isfinite(torch.tensor(tr.callback_metrics["train_loss"]))
 
+
+
+def test_persist_spin_timeout_raises_in_trainer(tmp_path):
+    """A bounded-spin timeout inside the persistent self-attention block forward (csrc/persist.hip
+    ``wait_count``) must stop training, not corrupt it silently: with a test-only spin bound of
+    0 polls the tiles that wait for their sample's next-layer rows give up, the kernel sets its
+    sticky error word, and the Trainer's logging-step check raises naming the kernel."""
+    from perceiver_io_amd.ops import ext
+
+    K = ext.require()
+    K.persist_errors(True)
+    K.persist_set_spin_limit(0)
+    try:
+        with pytest.raises(RuntimeError, match="sa_block_fwd_kernel"):
+            _run("mlm", ["fit", "--data=IMDBDataModule", "--data.synthetic=true", "--data.synthetic_size=64",
+                         "--data.vocab_size=500", "--data.max_seq_len=64", "--data.batch_size=16",
+                         "--data.num_workers=0", "--data.pad_to_max=true", "--model.num_latents=256",
+                         "--model.num_latent_channels=64", "--model.num_encoder_self_attention_heads=4",
+                         "--model.num_encoder_layers=2", "--model.num_encoder_self_attention_layers_per_block=4",
+                         "--optimizer.lr=0.003", "--trainer.accelerator=gpu", "--trainer.devices=1",
+                         "--trainer.max_steps=3", "--trainer.limit_val_batches=0",
+                         "--trainer.log_every_n_steps=1", "--model.masked_samples=null"], tmp_path)
+    finally:
+        K.persist_set_spin_limit(1 << 21)
+        K.persist_errors(True)
