@@ -120,6 +120,7 @@ void embed_fwd_launch(const int64_t*, const float*, const float*, float*, long l
 unsigned check_errors_elementwise(bool);
 unsigned check_errors_mlm_head(bool);
 unsigned check_errors_ce_head(bool);
+unsigned check_errors_rowgemm(bool);
 void embed_bwd_launch(const int64_t*, const float*, float*, float*, int, int, int, float, hipStream_t);
 void embed_bwd_sorted_launch(const int64_t*, const int64_t*, const float*, float*, long long, int, float, hipStream_t);
 bool embed_bwd_local_launch(const int64_t*, const float*, float*, float*, int, int, int, float, const SlabJob&,
@@ -175,7 +176,7 @@ hipStream_t stream() { return at::hip::getCurrentHIPStream(); }
 // outside [0, V) ∪ {-100}); reset clears them
 int64_t check_errors(bool reset) {
   return (int64_t)(pio::check_errors_elementwise(reset) | pio::check_errors_mlm_head(reset) |
-                   pio::check_errors_ce_head(reset));
+                   pio::check_errors_ce_head(reset) | pio::check_errors_rowgemm(reset));
 }
 bool checked_build() { return PIO_CHECKS != 0; }
 // checked builds, outside graph capture: wait for the kernel just launched and raise on any
@@ -188,7 +189,8 @@ void checked_sync(const char* what) {
   (void)hipStreamSynchronize(stream());
   const int64_t e = check_errors(true);
   TORCH_CHECK(e == 0, "checked build: ", what, " saw out-of-range indices (error bits ", e,
-              ": 1 token id >= vocab, 2 gather row out of range, 4 label outside [0, V) and != -100)");
+              ": 1 token id >= vocab, 2 gather row out of range, 4 label outside [0, V) and != -100, 8 PE row index outside "
+              "the position-encoding table)");
 }
 
 // deterministic mode (trainer flag ``deterministic``): every reduction that would
@@ -415,6 +417,7 @@ std::vector<Tensor> ln_linear_fwd(Tensor x, OptT lnw, OptT lnb, double eps, Tens
   pio::ln_linear_fwd_launch(x.data_ptr(), is_bf16(x), (int)x.stride(0), R, Kin, f32o(lnw), f32o(lnb), (float)eps, bfp(w),
                             (int)w.size(1), f32o(bias), N, (int)act, rptr, res_rs, y.data_ptr(), out_bf16, N, mp, rp, pp, prs, prows,
                             npix, pidx, stream());
+  if (pidx) checked_sync("ln_linear_fwd (pe_index)");
   std::vector<Tensor> out{y};
   if (mp) { out.push_back(mean); out.push_back(rstd); }
   return out;

@@ -23,7 +23,7 @@ namespace pio {
 #ifndef PIO_CHECKS
 #define PIO_CHECKS 0
 #endif
-enum : unsigned { kErrEmbedId = 1u, kErrGatherRow = 2u, kErrLabel = 4u };
+enum : unsigned { kErrEmbedId = 1u, kErrGatherRow = 2u, kErrLabel = 4u, kErrPeIndex = 8u };
 static __device__ unsigned pio_errors;
 __device__ __forceinline__ void pio_flag(unsigned bit) {
 #if PIO_CHECKS

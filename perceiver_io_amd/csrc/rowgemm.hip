@@ -196,9 +196,13 @@ struct PeSplit {
   int pe_rs, M, npix;
   const long long* idx;
 };
+// An index outside the table is clamped (no fault); the eager PyTorch path (index_select) raises
+// instead.  Checked builds flag it (kErrPeIndex: the launcher raises outside graph capture,
+// ops.check_device_errors() after replays); the sparse collator only produces in-range indices.
 __device__ __forceinline__ int pe_row(const PeSplit& ps, int gr) {
   if (ps.idx == nullptr) return gr % ps.M;
   const long long i = ps.idx[gr];
+  if (i < 0 || i >= ps.M) pio_flag(kErrPeIndex);
   return i < 0 ? 0 : (i >= ps.M ? ps.M - 1 : (int)i);
 }
 
@@ -1649,4 +1653,8 @@ void wgrad_launch(const void* G, bool g_bf16, int g_rs, int N, const void* A, bo
 #undef WG
 }
 
+}  // namespace pio
+
+namespace pio {
+unsigned check_errors_rowgemm(bool reset) { return pio_read_errors(reset); }
 }  // namespace pio

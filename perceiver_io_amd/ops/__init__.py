@@ -90,7 +90,8 @@ def check_device_errors(reset: bool = True) -> None:
         c = int(K.check_errors(reset))
         if c:
             raise RuntimeError(f"checked build: out-of-range indices seen on the device (error bits {c:#x}: "
-                               "1 token id >= vocab, 2 gather row out of range, 4 label outside [0, V) and != -100)")
+                               "1 token id >= vocab, 2 gather row out of range, 4 label outside [0, V) and != -100, "
+                               "8 PE row index outside the position-encoding table)")
 
 
 def use_hip(t: torch.Tensor) -> bool:

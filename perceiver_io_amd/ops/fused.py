@@ -1460,11 +1460,11 @@ _STATIC_SEEDS = {"on": False, "t": None, "n": 0}
 
 def begin_static_seeds(device) -> None:
     """Start a graph capture's static dropout seeds (train/engine.py StepEngine): every seeded
-    fused call captured until end_static_seeds() reads its own slot of one persistent int64
-    pool.  Call OUTSIDE the capture (the pool is allocated here on first use)."""
-    t = _STATIC_SEEDS["t"]
-    if t is None or t.device != torch.device(device):
-        t = torch.zeros(_STATIC_SEED_SLOTS, dtype=torch.int64, device=device)
+    fused call captured until end_static_seeds() reads its own slot of an int64 pool that belongs
+    to THIS capture only (a fresh tensor per captured graph: two engines — e.g. a train and an
+    eval model — or two graphs of one engine never share slots, so staging one graph's seeds can
+    not change what another graph reads).  Call OUTSIDE the capture (the pool is allocated here)."""
+    t = torch.zeros(_STATIC_SEED_SLOTS, dtype=torch.int64, device=device)
     _STATIC_SEEDS.update(on=True, t=t, n=0)
 
 
@@ -1472,7 +1472,9 @@ def end_static_seeds():
     """(pool, slots used) of the capture just ended; the engine stages slots [0, used) — fresh
     random values — in the launch before each replay (stage_step seed_dst / seeds)."""
     _STATIC_SEEDS["on"] = False
-    return _STATIC_SEEDS["t"], _STATIC_SEEDS["n"]
+    t, n = _STATIC_SEEDS["t"], _STATIC_SEEDS["n"]
+    _STATIC_SEEDS["t"] = None  # the captured graph keeps its pool (drop_seeds); the next capture gets a new one
+    return t, n
 _SEED_POOL = {"armed": False, "t": None, "i": 0}
 
 
@@ -1584,7 +1586,12 @@ def encode_inputs(encoder, x_in, pad_mask=None):
 def encode_sparse(encoder, values, index, pad_mask=None):
     """The encoder over a sparse image: ``values`` (B, K, C_img) pixel values at flat pixel
     positions ``index`` (B, K) int64; the K/V projections read the Fourier PE rows at ``index``
-    from the adapter's padded table inside their kernels (no gathered input rows)."""
+    from the adapter's padded table inside their kernels (no gathered input rows).
+
+    ``index`` must lie in [0, H·W) (``data/lartpc.py`` ``sparse_collate`` builds it from the
+    non-zero pixels).  The kernels clamp an index outside the table instead of faulting, where
+    the eager path's ``index_select`` raises; the checked build (``PERCEIVER_CHECKED=1``) flags
+    it and raises (``ops.check_device_errors``)."""
     ad = encoder.input_adapter
     pix = values.reshape(values.shape[0], values.shape[1], ad.num_image_channels).float().contiguous()
     idx = index if index.dtype == torch.int64 and index.is_contiguous() else index.long().contiguous()

@@ -837,7 +837,13 @@ for name, fn in (
                                    torch.randn(100, 64, device=dev).to(torch.bfloat16), torch.zeros(100, device=dev),
                                    torch.tensor([3.0], device=dev))),
         ("gather", lambda: K.index_add_rows(torch.zeros(10, 64, device=dev), torch.tensor([1, 12], device=dev),
-                                            torch.ones(2, 64, device=dev)))):
+                                            torch.ones(2, 64, device=dev))),
+        # a sparse image's PE row index past the table (rowgemm.hip pe_row)
+        ("pe_index", lambda: K.ln_linear_fwd(torch.randn(64, 1, device=dev), torch.ones(32, device=dev),
+                                             torch.zeros(32, device=dev), 1e-5,
+                                             torch.randn(64, 32, device=dev).to(torch.bfloat16), None, 0, None, True,
+                                             True, torch.randn(100, 32, device=dev), 32,
+                                             torch.tensor([3] * 63 + [100], device=dev)))):
     try:
         fn()
         out.append((name, "no error"))

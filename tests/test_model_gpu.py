@@ -322,6 +322,26 @@ def test_graph_replays_draw_fresh_dropout_masks():
             assert len(set(losses)) == 4, losses
 
 
+def test_two_engines_keep_private_dropout_seed_pools():
+    """Two step engines (e.g. two models trained in one process) capture dropout graphs: each
+    captured graph reads its OWN static seed slots, so staging one engine's seeds before its
+    replay cannot change the masks of the other's (interleaved replays, both still drawing fresh
+    masks every step)."""
+    ids = torch.randint(3, 500, (4, 96), device="cuda")
+    pad = torch.zeros(4, 96, dtype=torch.bool, device="cuda")
+    engs = []
+    for s in (6, 7):
+        torch.manual_seed(s)
+        engs.append(_fixed_mask_engine(_mlm_dropout(0.2), True, ids, pad, lr=0.0, warmup=0))
+    losses = [[], []]
+    for _ in range(3):
+        for k, e in enumerate(engs):
+            losses[k].append(e.step((None, ids, pad)).item())
+    pools = [next(iter(e._graphs.values())).drop_seeds[0] for e in engs]
+    assert pools[0].data_ptr() != pools[1].data_ptr()
+    assert all(len(set(ls)) == 3 for ls in losses), losses
+
+
 def _mlm_dropout(p, **kw):
     from perceiver_io_amd.tasks import LitMaskedLanguageModel
 

@@ -18,10 +18,13 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--which", default="both")
     ap.add_argument("--B", type=int, default=32)
+    ap.add_argument("--det", action="store_true", help="deterministic mode: per-key-block dQ slices, no atomics")
     a = ap.parse_args()
     from perceiver_io_amd.ops import emulation, ext
 
     K = ext.require()
+    if a.det:
+        K.set_deterministic(True)
     torch.manual_seed(0)
     B, M, Nq, H, nc, kin = a.B, 224 * 224, 32, 4, 3, 133
     C = 32 * H
