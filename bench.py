@@ -341,7 +341,7 @@ def main(argv=None):
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29517")
             tdist.init_process_group("nccl", rank=0, world_size=1, device_id=device)
-        reducer = FlatGradReducer(opt.flat, in_graph=True, force=True, overlap=args.overlap == "on")
+        reducer = FlatGradReducer(opt.flat, in_graph=args.overlap == "off", force=True, overlap=args.overlap == "on")
         reducer.plan(model)
     if world > 1:
         from perceiver_io_amd.ops.optim import FlatParameterSpace

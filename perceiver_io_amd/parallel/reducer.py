@@ -134,7 +134,11 @@ class FlatGradReducer:
         if in_graph is None:
             from .dist import graph_collectives_ok
 
-            in_graph = self.enabled and self.on_gpu and graph_collectives_ok(flat.device)
+            # the side-stream ready points are never captured (auto mode): a step graph holding
+            # RCCL work forked onto a second stream aborted at capture end, without a message,
+            # in one of several runs of the same test (rounds 5 and 6); the overlapped path keeps
+            # its collectives outside the graph, the default (inline) path is single-stream
+            in_graph = self.enabled and self.on_gpu and not self.overlap and graph_collectives_ok(flat.device)
         self.in_graph = bool(in_graph)
         if self.enabled:
             _ACTIVE.append(self)

@@ -123,10 +123,11 @@ def test_rccl_collectives_inside_the_step_graph():
     try:
         data = _data(0, STEPS)
         model = _setup()
-        opt, red, eng = _run(model, lambda f: FlatGradReducer(f, in_graph=True, force=True, overlap=True), True, data)
-        assert red.enabled and red.in_graph and eng.replays == STEPS - 2
-        # eager steps 1, 2 and the capture's backward (the replays run no Python)
-        assert red.launch_log == ["decoder", "layer_n", "layer_1_sa"] * 3
+        # the default data-parallel path: one all-reduce of the whole flat gradient after the
+        # backward, captured on the step's own stream (no fork), then one AdamW — all in the graph
+        opt, red, eng = _run(model, lambda f: FlatGradReducer(f, in_graph=True, force=True), True, data)
+        assert red.enabled and red.in_graph and not red.overlap and eng.replays == STEPS - 2
+        assert red.launch_log == [] and len(red.buckets) == 1
         red.close()
         ref_model = _setup()
         ref_opt, _, _ = _run(ref_model, None, True, data)
@@ -361,13 +362,13 @@ def test_graph_collectives_probe_capture_failure_fails_closed():
 
 
 def test_rccl_overlap_and_bucket_update_variants_bitwise():
-    """The data-parallel step's variants on a 1-rank RCCL group with the reducer forced on
-    (collectives inside the step graph), deterministic kernels: ready-point all-reduces on the
-    side stream or inline after the backward (overlap on / off), AdamW per bucket behind each
-    all-reduce or one pass after all of them (bucket_update on / off) — the final parameters
-    agree bit for bit (the slab reductions a ready point flushes run on the side stream only when
-    every destination lies inside the bucket; in deterministic mode all of them stay on the
-    compute stream)."""
+    """The data-parallel step's variants on a 1-rank RCCL group with the reducer forced on,
+    deterministic kernels: ready-point all-reduces on a side stream (overlap on: collectives
+    outside the step graph, after each replay) or one all-reduce inline after the backward inside
+    the graph (overlap off), AdamW per bucket behind each all-reduce or one pass after all of them
+    (bucket_update on / off) — the final parameters agree bit for bit (the slab reductions a
+    ready point flushes run on the side stream only when every destination lies inside the
+    bucket; in deterministic mode all of them stay on the compute stream)."""
     import torch.distributed as tdist
 
     from perceiver_io_amd import ops
@@ -384,7 +385,7 @@ def test_rccl_overlap_and_bucket_update_variants_bitwise():
             for bucket in (True, False):
                 model = _setup()
                 opt = FusedAdamW(model.parameters(), lr=1e-3, weight_decay=0.01)
-                red = FlatGradReducer(opt.flat, in_graph=True, force=True, overlap=overlap)
+                red = FlatGradReducer(opt.flat, in_graph=not overlap, force=True, overlap=overlap)
                 red.plan(model)
                 eng = StepEngine(lambda b, m=model: m.loss(b[0], b[1], labels=b[2], x_masked=b[3]), opt, reducer=red,
                                  device="cuda", graph=True, bucket_update=bucket)
