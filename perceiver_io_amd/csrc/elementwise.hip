@@ -224,9 +224,7 @@ __global__ void text_mask_kernel(const int64_t* __restrict__ x, const bool* __re
   }
 }
 
-// sum of squares of the flat gradient (for clip_grad_norm) → atomic into out[0]
-// 16-byte loads, four independent accumulation chains, ≈4 workgroups per CU
-// Σ g² in fixed order, no atomics: block b writes its partial to part[b] (kSumsqBlocks blocks,
+// sum of squares of the flat gradient (clip_grad_norm): Σ g² in fixed order, no atomics: block b writes its partial to part[b] (kSumsqBlocks blocks,
 // grid-stride, 8 independent 16-byte loads in flight per thread); the AdamW kernels sum the
 // partials themselves (adam_clip_scale).  The previous single-address atomic per block put
 // 2048 serialised adds at the end of an HBM-bound pass (36 µs for the 68 MB LArTPC gradient).
