@@ -85,7 +85,7 @@ bool ln_linear_post_attn_bwd_launch(int, const void*, bool, const uint16_t*, con
                                     const float*, const float*, const float*, const uint16_t*, const uint16_t*,
                                     const uint16_t*, const uint16_t*, const uint16_t*, const float*, const float*,
                                     float*, uint16_t*, float*, int, const PostAttnGrads&, int, const SlabJob&,
-                                    const DropCfg&, int, hipStream_t);
+                                    const DropCfg&, int, const uint16_t*, const float*, uint16_t*, float, hipStream_t);
 void post_attn_bwd_launch(int, const float*, const float*, const float*, const float*, const uint16_t*,
                           const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*, const float*,
                           const float*, float*, uint16_t*, float*, int, const PostAttnGrads&, int, const SlabJob&,
@@ -997,7 +997,8 @@ std::vector<Tensor> ln_linear_post_attn_bwd(Tensor g, Tensor wq, Tensor x, Tenso
                                             Tensor r2, Tensor u, Tensor o, Tensor wo, Tensor w1, Tensor w2, Tensor g2,
                                             Tensor be2, int64_t H, std::vector<Tensor> pa_grads, OptT job_slab,
                                             std::vector<Tensor> job_dsts, std::vector<int64_t> job_offs, OptT seed,
-                                            int64_t site, double p, OptT zero_out) {
+                                            int64_t site, double p, OptT zero_out, OptT att_qkv, OptT att_lse,
+                                            OptT att_out, double att_scale) {
   TORCH_CHECK(y.is_contiguous() && u.is_contiguous() && o.is_contiguous() && x.is_contiguous() && dres.is_contiguous(),
               "operands must be contiguous (R, C)");
   const int R = (int)y.size(0), C = (int)y.size(1);
@@ -1025,16 +1026,30 @@ std::vector<Tensor> ln_linear_post_attn_bwd(Tensor g, Tensor wq, Tensor x, Tenso
   Tensor delta = torch::empty({R, H}, f32);
   const auto job = with_zero_span(make_job(job_slab, job_dsts, job_offs), zero_out, y);
   const auto dr = make_drop(seed, site, p);
+  // att_*: the layer below's attention backward fused in (N = 64 latents per sample, the tile is
+  // the sample): its packed QKV rows and LSE in, its dQKV (R, 3C) bf16 out; dO / delta are then
+  // not produced (the returned tensors are unwritten)
+  const uint16_t* aq = nullptr; const float* al = nullptr; uint16_t* ao = nullptr;
+  if (att_out.has_value()) {
+    TORCH_CHECK(att_qkv.has_value() && att_lse.has_value(), "att_out needs att_qkv and att_lse");
+    CHECK_DT(*att_qkv, torch::kBFloat16); CHECK_DT(*att_out, torch::kBFloat16); CHECK_DT(*att_lse, torch::kFloat32);
+    TORCH_CHECK(C == 64 && H == 4 && R % 64 == 0, "fused attention backward: C = 64, H = 4, R % 64 == 0");
+    TORCH_CHECK(att_qkv->is_contiguous() && att_qkv->numel() == (int64_t)R * 3 * C && att_out->is_contiguous() &&
+                    att_out->numel() == (int64_t)R * 3 * C && att_lse->is_contiguous() && att_lse->numel() == (int64_t)R * H,
+                "fused attention backward: qkv / out (R, 3C), lse (R, H) contiguous");
+    aq = bfp(*att_qkv); al = f32p(*att_lse); ao = bfp_mut(*att_out);
+  }
   auto launch = [&](const Tensor& gg) {
     const bool gbf = gg.scalar_type() == torch::kBFloat16;
     return pio::ln_linear_post_attn_bwd_launch(
         C, gg.data_ptr(), gbf, bfp(wq), f32p(x), f32p(mean1), f32p(rstd1), f32p(lnw), f32p(lnb), f32p(dres), dg1, db1,
         dwq, dbq, f32p(y), f32p(m2), f32p(r2), bfp(u), bfp(o), bfp(wo), bfp(w1), bfp(w2), f32p(g2), f32p(be2),
-        dy.data_ptr<float>(), bfp_mut(dO), delta.data_ptr<float>(), (int)H, pg, R, job, dr, nq, stream());
+        dy.data_ptr<float>(), bfp_mut(dO), delta.data_ptr<float>(), (int)H, pg, R, job, dr, nq, aq, al, ao,
+        (float)att_scale, stream());
   };
   // a bf16 G (from attn_bwd's bf16 outputs) is taken by the chain-layout kernel; any other
   // kernel gets it widened to fp32 (same values)
-  if (!launch(g)) TORCH_CHECK(launch(g.to(torch::kFloat32)), "ln_linear_post_attn_bwd: launch failed");
+  if (!launch(g)) TORCH_CHECK(!ao && launch(g.to(torch::kFloat32)), "ln_linear_post_attn_bwd: launch failed");
   return {dy, dO, delta};
 }
 
@@ -1936,7 +1951,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("w2"), py::arg("g2"), py::arg("be2"), py::arg("H"), py::arg("pa_grads"),
         py::arg("job_slab") = py::none(), py::arg("job_dsts") = std::vector<Tensor>(),
         py::arg("job_offs") = std::vector<int64_t>(), py::arg("seed") = py::none(), py::arg("site") = 0,
-        py::arg("p") = 0.0, py::arg("zero_out") = py::none());
+        py::arg("p") = 0.0, py::arg("zero_out") = py::none(), py::arg("att_qkv") = py::none(),
+        py::arg("att_lse") = py::none(), py::arg("att_out") = py::none(), py::arg("att_scale") = 0.0);
   m.def("post_attn_bwd", &post_attn_bwd, py::arg("dz"), py::arg("y"), py::arg("m2"), py::arg("r2"), py::arg("u"),
         py::arg("o"), py::arg("wo"), py::arg("w1"), py::arg("w2"), py::arg("g2"), py::arg("be2"), py::arg("H"),
         py::arg("grads"), py::arg("slab") = false, py::arg("job_slab") = py::none(),

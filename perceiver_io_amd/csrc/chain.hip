@@ -281,7 +281,22 @@ __global__ __launch_bounds__(512) void sa_layer_fwd_chain8_kernel(
 //      staged.  Partials go to this tile's slab row (plain stores).
 // ------------------------------------------------------------------------------------
 
-template <int NQ, typename TG>
+// ATT (N = 64 latents per sample, one sample per tile): phase D appends the attention backward
+// of layer l itself — Q / K / V of layer l and its LSE are loaded in phase 0, dO and δ come
+// from phase B's registers — and the kernel stores dQKV of layer l (bf16) instead of dO / δ:
+// the separate attention-backward launch of the layer disappears.  Wave w = (head w & 3, keys
+// 32(w >> 2) .. + 31); per 32-query tile: S = Q·Kᵀ, dP = dO·Vᵀ, dS = P∘(dP − δ) (+ the
+// attention-probability dropout of the forward, same hash stream as attn_bwd), dV += Pᵀ·dO,
+// dK += dSᵀ·Q; the dS slabs of both key halves meet in LDS for dQ = dS·K; the dQKV tile leaves
+// through LDS as 16-byte rows.
+struct ChainAttn {
+  const uint16_t* qkv;  // layer l's packed Q | K | V rows (R, 3C) bf16
+  const float* lse;     // (R, H) log2-domain softmax statistics of the forward
+  uint16_t* dqkv;       // (R, 3C) bf16 out
+  float scale, scale_log2;
+};
+
+template <int NQ, typename TG, bool ATT>
 __global__ __launch_bounds__(512) void ln_linear_post_attn_bwd_chain8_kernel(
     const TG* __restrict__ G, const uint16_t* __restrict__ Wq, const float* __restrict__ X,
     const float* __restrict__ mean1, const float* __restrict__ rstd1, const float* __restrict__ lnw,
@@ -290,7 +305,7 @@ __global__ __launch_bounds__(512) void ln_linear_post_attn_bwd_chain8_kernel(
     const float* __restrict__ rstd2, const uint16_t* __restrict__ U, const uint16_t* __restrict__ O,
     const uint16_t* __restrict__ Wo, const uint16_t* __restrict__ W1, const uint16_t* __restrict__ W2,
     const float* __restrict__ g2, const float* __restrict__ be2, float* __restrict__ dY, uint16_t* __restrict__ dO,
-    float* __restrict__ delta, PostAttnGrads gr_out, int R, SlabJob job, DropCfg dr) {
+    float* __restrict__ delta, PostAttnGrads gr_out, int R, SlabJob job, DropCfg dr, ChainAttn at) {
   constexpr int C = 64, LD = 64, nq = NQ * C, LDG = nq, KT = nq / 32, NT = 512;  // swizzled images (swz8)
   constexpr int NWC = (3 * C + nq) * 8 / NT;  // 16-byte weight chunks per thread
   static_assert((3 * C + nq) * 8 % NT == 0 && KT % 2 == 0, "staging split");
@@ -370,6 +385,19 @@ __global__ __launch_bounds__(512) void ln_linear_post_attn_bwd_chain8_kernel(
     obv[i] = *reinterpret_cast<const uint2*>(O + (long long)gr * C + c);
   }
   const float mu1 = mean1[gr], rs1 = rstd1[gr], mu2 = mean2[gr], rs2 = rstd2[gr];
+  // phase D operands (ATT): this wave's K / V fragments (head w & 3, key 32hf + (l & 31)), one
+  // 16-byte chunk of the Q and K rows per thread, one LSE value per thread < 256
+  bf16x8 akf, avf, aq, ak;
+  float alse = 0.f;
+  if constexpr (ATT) {
+    const long long kr = (long long)(tile * 64 + 32 * hf + (l & 31)) * (3 * C) + (w & 3) * 16 + 8 * (l >> 5);
+    akf = *reinterpret_cast<const bf16x8*>(at.qkv + kr + C);
+    avf = *reinterpret_cast<const bf16x8*>(at.qkv + kr + 2 * C);
+    const long long qr = (long long)(tile * 64 + (threadIdx.x >> 3)) * (3 * C) + (threadIdx.x & 7) * 8;
+    aq = *reinterpret_cast<const bf16x8*>(at.qkv + qr);
+    ak = *reinterpret_cast<const bf16x8*>(at.qkv + qr + C);
+    alse = at.lse[(long long)tile * 256 + (threadIdx.x & 255)];
+  }
   PIO_TS(1);
   float pv;
   {
@@ -516,8 +544,9 @@ __global__ __launch_bounds__(512) void ln_linear_post_attn_bwd_chain8_kernel(
     cl2_gemm_t(sWo, LD, hf, bb, acc);  // dO
   }
   PIO_TS(8);
+  float dd[2];
   {
-    float ov[2][4], dd[2];
+    float ov[2][4];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       ov[i][0] = bf2f((uint16_t)(obv[i].x & 0xFFFF)); ov[i][1] = bf2f((uint16_t)(obv[i].x >> 16));
@@ -530,8 +559,10 @@ __global__ __launch_bounds__(512) void ln_linear_post_attn_bwd_chain8_kernel(
       }
       dd[i] = xor32_sum(xor16_sum(sacc));  // head 2hf + i = channels 16(2hf + i) .. + 15
     }
-    cl2_store_bf16(dO, C, gr, hf, t0);
-    if (g == 0) *reinterpret_cast<float2*>(delta + (long long)gr * 4 + 2 * hf) = make_float2(dd[0], dd[1]);
+    if constexpr (!ATT) {  // ATT: phase D consumes dO / δ from these registers
+      cl2_store_bf16(dO, C, gr, hf, t0);
+      if (g == 0) *reinterpret_cast<float2*>(delta + (long long)gr * 4 + 2 * hf) = make_float2(dd[0], dd[1]);
+    }
     cl2_tile_store(sOt, LD, lr, hf, ov);
   }
   PIO_TS(9);
@@ -557,6 +588,129 @@ __global__ __launch_bounds__(512) void ln_linear_post_attn_bwd_chain8_kernel(
     cl_ln_grads(sD1, sX1, LD, p4, sp(dlnw), sp(dlnb));
   }
   PIO_TS(11);
+  if constexpr (ATT) {
+    // ---- D: attention backward of layer l (N = 64: the tile is the sample) ----
+    constexpr int LDA = 40, LDS_ = 40;  // [row][d] tiles, d 16..31 zero; dS slabs [key][q]
+    uint16_t* sm16 = reinterpret_cast<uint16_t*>(smem);
+    uint16_t* sQa = sm16;                      // [4][64][LDA]  Q
+    uint16_t* sdOa = sQa + 4 * 64 * LDA;       // [4][64][LDA]  dO
+    uint16_t* sKa = sdOa + 4 * 64 * LDA;       // [4][64][LDA]  K
+    uint16_t* sdSa = sKa + 4 * 64 * LDA;       // [4 heads][2 query tiles][64 keys][LDS_]
+    float* sLa = reinterpret_cast<float*>(sdSa + 4 * 2 * 64 * LDS_);  // [4][64] LSE
+    float* sDa = sLa + 4 * 64;                 // [4][64] δ
+    uint16_t* sOut = sm16;                     // [64][3C] dQKV tile (over Q / dO, after they are consumed)
+    static_assert((4 * 3 * 64 * LDA + 4 * 2 * 64 * LDS_) * 2 + 2 * 4 * 64 * 4 <= lpb_chain8_smem<NQ>(), "phase D LDS");
+    static_assert(64 * 3 * C * 2 <= 2 * 4 * 64 * LDA * 2, "dQKV tile over the Q / dO tiles");
+    lds_sync();  // phase C's reads of the images are done
+    {
+      const int row = threadIdx.x >> 3, cc = (threadIdx.x & 7) * 8, hq = cc >> 4, d0 = cc & 15;
+      *reinterpret_cast<bf16x8*>(sQa + (hq * 64 + row) * LDA + d0) = aq;
+      *reinterpret_cast<bf16x8*>(sKa + (hq * 64 + row) * LDA + d0) = ak;
+      if (threadIdx.x < 256) {
+        const int zh = threadIdx.x >> 6, zr = threadIdx.x & 63;
+        const bf16x8 z8 = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        *reinterpret_cast<bf16x8*>(sQa + (zh * 64 + zr) * LDA + 16) = z8;
+        *reinterpret_cast<bf16x8*>(sQa + (zh * 64 + zr) * LDA + 24) = z8;
+        *reinterpret_cast<bf16x8*>(sdOa + (zh * 64 + zr) * LDA + 16) = z8;
+        *reinterpret_cast<bf16x8*>(sdOa + (zh * 64 + zr) * LDA + 24) = z8;
+        sLa[(threadIdx.x & 3) * 64 + (threadIdx.x >> 2)] = alse;
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {  // dO of row lr, head 2hf + i, dims 4g .. 4g + 3
+        uint2 pk;
+        pk.x = pack2(t0[i][0], t0[i][1]);
+        pk.y = pack2(t0[i][2], t0[i][3]);
+        *reinterpret_cast<uint2*>(sdOa + ((2 * hf + i) * 64 + lr) * LDA + 4 * g) = pk;
+        if (g == 0) sDa[(2 * hf + i) * 64 + lr] = dd[i];
+      }
+    }
+    lds_sync();
+    const int ah = w & 3, hh = l >> 5, r = l & 31;
+    const int b = tile;  // the sample (N = 64 rows)
+    const uint16_t* tQh = sQa + ah * 64 * LDA;
+    const uint16_t* tdOh = sdOa + ah * 64 * LDA;
+    const uint32_t dkey = dr.thresh ? drop_key(dr.seed, dr.site, 2u) : 0u;
+    const int key = 32 * hf + r;  // this lane's key (S / dP column)
+    f32x16 dKa = f32x16{}, dVa = f32x16{};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const uint16_t* tQ = tQh + 32 * j * LDA;
+      const uint16_t* tdO = tdOh + 32 * j * LDA;
+      const f32x16 S = mfma32(frag_kc(tQ, LDA, 0, 0), akf, f32x16{});
+      const f32x16 dP = mfma32(frag_kc(tdO, LDA, 0, 0), avf, f32x16{});
+      f32x4 lrow[4], drow[4];
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        lrow[gg] = *reinterpret_cast<const f32x4*>(sLa + ah * 64 + 32 * j + 8 * gg + 4 * hh);
+        drow[gg] = *reinterpret_cast<const f32x4*>(sDa + ah * 64 + 32 * j + 8 * gg + 4 * hh);
+      }
+      f32x16 P, dS;
+      if (!dr.thresh) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float p = fast_exp2(S[i] * at.scale_log2 - lrow[i >> 2][i & 3]);
+          P[i] = p;
+          dS[i] = p * (dP[i] - drow[i >> 2][i & 3]);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float p = fast_exp2(S[i] * at.scale_log2 - lrow[i >> 2][i & 3]);
+          const uint32_t idx = (uint32_t)(32 * j + acc_row(i, hh)) * 64u + (uint32_t)key;
+          const bool keep = keep_elem(dkey, (uint32_t)(b * 4 + ah), idx, dr.thresh);
+          P[i] = keep ? p * dr.scale : 0.f;
+          dS[i] = p * ((keep ? dP[i] * dr.scale : 0.f) - drow[i >> 2][i & 3]);
+        }
+      }
+      bf16x8 sa[2];
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        sa[ss] = pack_acc(dS, ss);
+        dVa = mfma32(pack_acc(P, ss), frag_ks_perm(tdO, LDA, 0, 16 * ss), dVa);
+        dKa = mfma32(sa[ss], frag_ks_perm(tQ, LDA, 0, 16 * ss), dKa);
+      }
+      uint16_t* slab = sdSa + ((ah * 2 + j) * 64 + 32 * hf) * LDS_;
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        const bf16x8& v = sa[gg >> 1];
+        const int o = 4 * (gg & 1);
+        const bf16x4 q4 = {v[o], v[o + 1], v[o + 2], v[o + 3]};
+        *reinterpret_cast<bf16x4*>(slab + r * LDS_ + 8 * gg + 4 * hh) = q4;
+      }
+    }
+    lds_sync();  // both key halves' dS slabs are in; Q / dO are consumed (sOut may overwrite them)
+    // dK (scaled) / dV rows: key 32hf + acc_row(i, hh), dim r (< 16)
+    if (r < 16) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int kk = 32 * hf + acc_row(i, hh);
+        sOut[kk * (3 * C) + C + ah * 16 + r] = f2bf(dKa[i] * at.scale);
+        sOut[kk * (3 * C) + 2 * C + ah * 16 + r] = f2bf(dVa[i]);
+      }
+    }
+    {  // dQ of query tile hf (both 16-row halves): Σ over the 64 keys of dS[key][q]·K[key][d]
+      const uint16_t* tS = sdSa + (ah * 2 + hf) * 64 * LDS_;
+      const uint16_t* tK = sKa + ah * 64 * LDA;
+      const int gq = l >> 4;
+#pragma unroll
+      for (int mh = 0; mh < 2; ++mh) {
+        f32x4 a0 = mfma16(frag16_tr(tS, LDS_, 16 * mh, 0), frag16_tr(tK, LDA, 0, 0), f32x4{0.f, 0.f, 0.f, 0.f});
+        f32x4 a1 = mfma16(frag16_tr(tS, LDS_, 16 * mh, 32), frag16_tr(tK, LDA, 0, 32), f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int qq = 32 * hf + 16 * mh + 4 * gq + i;
+          sOut[qq * (3 * C) + ah * 16 + (l & 15)] = f2bf((a0[i] + a1[i]) * at.scale);
+        }
+      }
+    }
+    lds_sync();
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {  // the dQKV tile: 64 rows × 24 16-byte chunks
+      const int c = threadIdx.x + NT * k, row = c / 24, col = (c % 24) * 8;
+      *reinterpret_cast<bf16x8*>(at.dqkv + (long long)(tile * 64 + row) * (3 * C) + col) =
+          *reinterpret_cast<const bf16x8*>(sOut + row * (3 * C) + col);
+    }
+  }
   };
   if (wave_id() >> 2) body(std::integral_constant<int, 1>{});
   else body(std::integral_constant<int, 0>{});
@@ -611,20 +765,29 @@ bool ln_linear_post_attn_bwd_chain_launch(const void* G, bool g_bf16, const uint
                                           const uint16_t* Wo, const uint16_t* W1, const uint16_t* W2, const float* g2,
                                           const float* be2, float* dY, uint16_t* dO, float* delta,
                                           const PostAttnGrads& grads, int R, const SlabJob& job, const DropCfg& dr,
-                                          int nq, hipStream_t st) {
+                                          int nq, const uint16_t* att_qkv, const float* att_lse, uint16_t* att_out,
+                                          float att_scale, hipStream_t st) {
   if (nq != 192 && nq != 64) return false;
+  // phase D (att): layer l is a self-attention layer in both forms — NQ = 3 (layer l+1 a
+  // self-attention layer too) and NQ = 1 (layer l+1 the next cross-attention layer's query path)
+  const bool att = att_out != nullptr;
   dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0));
-#define LPC(NQ, TG)                                                                                                    \
-  hipLaunchKernelGGL((ln_linear_post_attn_bwd_chain8_kernel<NQ, TG>), grid, dim3(512), 0, st, static_cast<const TG*>(G), \
-                     Wq, X, mean1, rstd1, lnw, lnb, dres, dlnw, dlnb, dWq, dbq, Ysave, mean2, rstd2, U, O, Wo, W1, W2,    \
-                     g2, be2, dY, dO, delta, grads, R, job, dr)
+  const ChainAttn at{att_qkv, att_lse, att_out, att_scale, att_scale * 1.4426950408889634f};
+#define LPC(NQ, TG, A)                                                                                                   \
+  hipLaunchKernelGGL((ln_linear_post_attn_bwd_chain8_kernel<NQ, TG, A>), grid, dim3(512), 0, st, static_cast<const TG*>(G), \
+                     Wq, X, mean1, rstd1, lnw, lnb, dres, dlnw, dlnb, dWq, dbq, Ysave, mean2, rstd2, U, O, Wo, W1, W2,       \
+                     g2, be2, dY, dO, delta, grads, R, job, dr, at)
   if (g_bf16) {
     if (nq != 192) return false;  // bf16 G only from the self-attention backward (nq = 3C)
-    LPC(3, uint16_t);
+    if (att) LPC(3, uint16_t, true);
+    else LPC(3, uint16_t, false);
   } else if (nq == 192) {
-    LPC(3, float);
+    if (att) LPC(3, float, true);
+    else LPC(3, float, false);
+  } else if (att) {
+    LPC(1, float, true);
   } else {
-    LPC(1, float);
+    LPC(1, float, false);
   }
 #undef LPC
   return true;

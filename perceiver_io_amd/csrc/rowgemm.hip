@@ -206,6 +206,34 @@ __device__ __forceinline__ int pe_row(const PeSplit& ps, int gr) {
   return i < 0 ? 0 : (i >= ps.M ? ps.M - 1 : (int)i);
 }
 
+// one fp32 vector of length K (an LN affine) at a 16-byte aligned base, K not a multiple of 8:
+// 16-byte loads for the whole 8-column chunks, scalar loads for the tail (zeros past K)
+template <int NCH>
+__device__ __forceinline__ void vec_load_mixed(float (&v)[NCH][8], const float* __restrict__ base, int K) {
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    const int c = rp_col(j);
+    if (c + 8 <= K) {
+      const float4 a = *reinterpret_cast<const float4*>(base + c), b = *reinterpret_cast<const float4*>(base + c + 4);
+      v[j][0] = a.x; v[j][1] = a.y; v[j][2] = a.z; v[j][3] = a.w;
+      v[j][4] = b.x; v[j][5] = b.y; v[j][6] = b.z; v[j][7] = b.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[j][e] = c + e < K ? ldf(base + c + e) : 0.f;
+    }
+  }
+}
+// per-operand vector-load flags of a launch whose operands do not all qualify (AV = false), e.g.
+// an odd input width (the LArTPC Fourier input, Kin = 131) with 8-aligned G / W rows
+constexpr int kVecG = 1;   // G rows: 16-byte aligned, g_rs and N multiples of 8
+constexpr int kVecW = 2;   // W rows: 16-byte aligned, w_rs a multiple of 8 and ≥ Kin
+constexpr int kVecLn = 4;  // LN affine vectors 16-byte aligned (whole chunks vectorised)
+template <int NCH>
+__device__ __forceinline__ void ln_vec_load(float (&v)[NCH][8], const float* __restrict__ base, int K, bool av, int vf) {
+  if (!av && (vf & kVecLn)) vec_load_mixed<NCH>(v, base, K);
+  else row_load<NCH>(v, base, 0, 0, 1, K, av);
+}
+
 template <int NCH, typename T>
 __device__ __forceinline__ void row_load_x(float (&v)[NCH][8], const T* __restrict__ X, long long x_rs, int gr, int R,
                                            int Kin, bool vec, const PeSplit& ps) {
@@ -417,7 +445,7 @@ __device__ __forceinline__ void ln_linear_fwd_tile(float (&xv)[NCH][8], bf16x8 (
                                                    const float* __restrict__ bias, int N, int act,
                                                    const float* __restrict__ res, int res_rs, TOut* __restrict__ Y,
                                                    int y_rs, float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                   uint16_t* smem, int part = 0, int nparts = 1) {
+                                                   uint16_t* smem, int part = 0, int nparts = 1, bool wv = false) {
   // nparts > 1: workgroups sharing the tile; this one forms output chunks part, part + nparts, …
   // (wb must hold chunk `part`), the row statistics are the last part's to store
   constexpr int KP = 32 * NCH, LD = KP + 8, LDO = 64 + 4;
@@ -426,7 +454,7 @@ __device__ __forceinline__ void ln_linear_fwd_tile(float (&xv)[NCH][8], bf16x8 (
   float* sO = reinterpret_cast<float*>(sW + 64 * LD);   // [64][LDO] output chunk
   const int gr = m0 + rp_row(), w = wave_id(), l = lane_id();
   // W rows are w_rs apart (≥ Kin, zero padded): a multiple of 8 keeps the staging vectorised
-  constexpr bool wvec = AV;
+  const bool wvec = AV || wv;
   const int wk = w_rs > Kin ? w_rs : Kin;
   const bool yvec = (N & 7) == 0 && (y_rs & 7) == 0 && aligned16(Y);
   if (has_ln) {
@@ -488,7 +516,7 @@ __global__ __launch_bounds__(256) void ln_linear_fwd_kernel(const TIn* __restric
                                                             const float* __restrict__ bias, int N, int act,
                                                             const float* __restrict__ res, int res_rs,
                                                             TOut* __restrict__ Y, int y_rs, float* __restrict__ mean_out,
-                                                            float* __restrict__ rstd_out, PeSplit ps) {
+                                                            float* __restrict__ rstd_out, PeSplit ps, int vf) {
   constexpr int KP = 32 * NCH;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   const int m0 = blockIdx.x * 64, gr = m0 + rp_row();
@@ -497,14 +525,14 @@ __global__ __launch_bounds__(256) void ln_linear_fwd_kernel(const TIn* __restric
   float xv[NCH][8];
   row_load_x<NCH>(xv, X, x_rs, gr, R, Kin, AV, ps);
   bf16x8 wb[NCH];
-  tile_fetch<NCH>(wb, W, w_rs, 64 * part, N, 64, w_rs > Kin ? w_rs : Kin, KP, AV);
+  tile_fetch<NCH>(wb, W, w_rs, 64 * part, N, 64, w_rs > Kin ? w_rs : Kin, KP, AV || (vf & kVecW));
   float gw[NCH][8], gb[NCH][8];
   if (lnw) {
-    row_load<NCH>(gw, lnw, 0, 0, 1, Kin, AV);
-    row_load<NCH>(gb, lnb, 0, 0, 1, Kin, AV);
+    ln_vec_load<NCH>(gw, lnw, Kin, AV, vf);
+    ln_vec_load<NCH>(gb, lnb, Kin, AV, vf);
   }
   ln_linear_fwd_tile<TOut, NCH, AV>(xv, wb, gw, gb, lnw != nullptr, m0, R, Kin, eps, W, w_rs, bias, N, act, res, res_rs, Y,
-                                y_rs, mean_out, rstd_out, smem, part, nparts);
+                                y_rs, mean_out, rstd_out, smem, part, nparts, (vf & kVecW) != 0);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1048,9 +1076,17 @@ __global__ __launch_bounds__(256) void post_attn_bwd_kernel(
 //   dXn = G·W (N streamed in 64-column chunks, double-buffered through registers),
 //   dW += Gᵀ·LN(X), db += Σ G (per chunk, atomics), dX = LN_bwd(dXn) (+ dres), dγ/dβ.
 // ------------------------------------------------------------------------------------
+// bytes: sG | sW | sXn during the chunk loop, the fp32 dXn tile sF over the same bytes after it,
+// then sPart | sPb (≈57 KB at 160 channels: two workgroups per CU)
+template <int NCH>
+constexpr int ln_linear_bwd_loop_smem() {
+  return 64 * 72 * 2 + 2 * 64 * (32 * NCH + 8) * 2 > 64 * (32 * NCH + 4) * 4
+             ? 64 * 72 * 2 + 2 * 64 * (32 * NCH + 8) * 2
+             : 64 * (32 * NCH + 4) * 4;
+}
 template <int NCH>
 constexpr int ln_linear_bwd_smem() {
-  return 64 * 72 * 2 + 2 * 64 * (32 * NCH + 8) * 2 + 64 * (32 * NCH + 4) * 4 + 8 * 32 * NCH * 4 + 4 * 64 * 4;
+  return ln_linear_bwd_loop_smem<NCH>() + 8 * 32 * NCH * 4 + 4 * 64 * 4;
 }
 
 // one 64-row tile; dX (incl. dres) is also left in dxo (row-pass registers) for a fused epilogue
@@ -1061,7 +1097,8 @@ __device__ __forceinline__ void ln_linear_bwd_body(
     int x_rs, const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ lnw,
     const float* __restrict__ lnb, const float* __restrict__ dres, int dres_rs, float* __restrict__ dX, int dx_rs,
     float* __restrict__ dlnw, float* __restrict__ dlnb, float* __restrict__ dW, float* __restrict__ db, int vrs,
-    int wrs, int slab, int R, PeSplit ps, uint16_t* smem, float (&dxo)[NCH][8], int part = 0, int nparts = 1) {
+    int wrs, int slab, int R, PeSplit ps, uint16_t* smem, float (&dxo)[NCH][8], int part = 0, int nparts = 1,
+    int vf = 0) {
   // nparts > 1: workgroups sharing the tile; the weight / bias gradient of 64-column chunk j is
   // part (j mod nparts)'s, the LN gradients and dX the row-output owner's (tile_part_owner)
   const bool own_rows = tile_part_owner(3, nparts) == part;
@@ -1069,12 +1106,13 @@ __device__ __forceinline__ void ln_linear_bwd_body(
   uint16_t* sG = smem;                                   // [64][LDG]  G chunk
   uint16_t* sW = sG + 64 * LDG;                          // [64][LD]   W chunk
   uint16_t* sXn = sW + 64 * LD;                          // [64][LD]   LN(X)
-  float* sF = reinterpret_cast<float*>(sXn + 64 * LD);   // [64][LDF]  dXn
-  float* sPart = sF + 64 * LDF;                          // [2][4][KP]
+  float* sF = reinterpret_cast<float*>(smem);            // [64][LDF]  dXn, after the loop (over sG | sW | sXn)
+  float* sPart = reinterpret_cast<float*>(smem + ln_linear_bwd_loop_smem<NCH>() / 2);  // [2][4][KP]
   float* sPb = sPart + 8 * KP;                           // [4][64]
   const int m0 = blockIdx.x * 64, gr = m0 + rp_row(), w = wave_id(), l = lane_id();
-  // AV: G, W, X, the LN affine and dres meet the vector-load preconditions (host-checked)
-  constexpr bool gvec = AV, wvec = AV;
+  // AV: G, W, X, the LN affine and dres meet the vector-load preconditions (host-checked);
+  // otherwise vf names the operands that still do (kVecG / kVecW / kVecLn)
+  const bool gvec = AV || (vf & kVecG), wvec = AV || (vf & kVecW);
   const int wk = w_rs > Kin ? w_rs : Kin;  // W rows zero padded to w_rs
   const bool kvec = (Kin & 7) == 0;
 
@@ -1083,7 +1121,7 @@ __device__ __forceinline__ void ln_linear_bwd_body(
   row_load_x<NCH>(xv, X, x_rs, gr, R, Kin, AV, ps);
   float mu = 0.f, rs = 1.f;
   if (lnw) {
-    row_load<NCH>(gw, lnw, 0, 0, 1, Kin, AV);
+    ln_vec_load<NCH>(gw, lnw, Kin, AV, vf);
     mu = *(gr < R ? mean + gr : kZero32B);  // address selects: no conditional loads
     rs = *(gr < R ? rstd + gr : kZero32B);
   }
@@ -1094,7 +1132,7 @@ __device__ __forceinline__ void ln_linear_bwd_body(
   if (dW) {  // LN(X), the forward GEMM's A operand, for the weight gradient
     float xn[NCH][8];
     if (lnw) {
-      row_load<NCH>(xn, lnb, 0, 0, 1, Kin, AV);
+      ln_vec_load<NCH>(xn, lnb, Kin, AV, vf);
 #pragma unroll
       for (int j = 0; j < NCH; ++j)
 #pragma unroll
@@ -1210,7 +1248,7 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
     int x_rs, const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ lnw,
     const float* __restrict__ lnb, const float* __restrict__ dres, int dres_rs, float* __restrict__ dX, int dx_rs,
     float* __restrict__ dlnw, float* __restrict__ dlnb, float* __restrict__ dW, float* __restrict__ db, int vrs,
-    int wrs, int slab, int R, PeSplit ps, SlabJob job) {
+    int wrs, int slab, int R, PeSplit ps, SlabJob job, int vf) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   if ((int)blockIdx.x >= (R + 63) / 64) {  // appended workgroups: the previous kernel's slab job
     {  // the appended job workgroups span every grid row: block (x − tiles)·gridDim.y + y
@@ -1222,7 +1260,7 @@ __global__ __launch_bounds__(256) void ln_linear_bwd_kernel(
   float dxo[NCH][8];
   ln_linear_bwd_body<TG, TX, NCH, AV>(G, g_rs, N, W, w_rs, Kin, X, x_rs, mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs,
                                   dlnw, dlnb, dW, db, vrs, wrs, slab, R, ps, smem, dxo, (int)blockIdx.y,
-                                  (int)gridDim.y);
+                                  (int)gridDim.y, vf);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1383,13 +1421,25 @@ bool ln_linear_post_attn_bwd_chain_launch(const void* G, bool g_bf16, const uint
                                           const uint16_t* Wo, const uint16_t* W1, const uint16_t* W2, const float* g2,
                                           const float* be2, float* dY, uint16_t* dO, float* delta,
                                           const PostAttnGrads& grads, int R, const SlabJob& job, const DropCfg& dr,
-                                          int nq, hipStream_t st);
+                                          int nq, const uint16_t* att_qkv, const float* att_lse, uint16_t* att_out,
+                                          float att_scale, hipStream_t st);
 static bool av_ok(std::initializer_list<const void*> ptrs, std::initializer_list<long long> widths) {
   for (const void* p : ptrs)
     if (!al16(p)) return false;
   for (long long w : widths)
     if (w & 7) return false;
   return true;
+}
+
+// kVecG / kVecW / kVecLn for the operands of an AV = false launch that still meet their
+// vector-load preconditions (G may be null: a forward)
+static int vec_flags(const void* G, int g_rs, int N, const void* W, int w_rs, int Kin, const float* lnw,
+                     const float* lnb) {
+  int vf = 0;
+  if (G && al16(G) && !(g_rs & 7) && !(N & 7)) vf |= kVecG;
+  if (al16(W) && !(w_rs & 7) && w_rs >= Kin) vf |= kVecW;
+  if (lnw && al16(lnw) && al16(lnb)) vf |= kVecLn;
+  return vf;
 }
 
 static int pick_nch(int K) {
@@ -1404,11 +1454,12 @@ static void ln_linear_fwd_t(const void* X, int x_rs, int R, int Kin, const float
   constexpr int KP = 32 * NCH;
   const size_t smem = ln_linear_fwd_smem<NCH>();
   const bool av = av_ok({X, W, lnw, lnb}, {Kin, x_rs, w_rs});
+  const int vf = av ? 0 : vec_flags(nullptr, 0, 0, W, w_rs, Kin, lnw, lnb);
   auto fn = av ? ln_linear_fwd_kernel<TI, TO, NCH, true> : ln_linear_fwd_kernel<TI, TO, NCH, false>;
   set_smem_once((const void*)fn);
   // few tiles: several workgroups per tile, each forming every split_tiles(R)-th 64-column chunk
   hipLaunchKernelGGL(fn, dim3((R + 63) / 64, split_tiles(R)), dim3(256), smem, st, (const TI*)X, x_rs, R, Kin, lnw, lnb,
-                     eps, W, w_rs, bias, N, act, res, res_rs, (TO*)Y, y_rs, mean, rstd, ps);
+                     eps, W, w_rs, bias, N, act, res, res_rs, (TO*)Y, y_rs, mean, rstd, ps, vf);
 }
 
 template <typename TI, typename TO>
@@ -1523,16 +1574,19 @@ bool ln_linear_post_attn_bwd_launch(int C, const void* Gv, bool g_bf16, const ui
                                     const uint16_t* Wo, const uint16_t* W1, const uint16_t* W2, const float* g2,
                                     const float* be2, float* dY, uint16_t* dO, float* delta, int H,
                                     const PostAttnGrads& grads, int R, const SlabJob& job, const DropCfg& dr,
-                                    int nq, hipStream_t st) {
+                                    int nq, const uint16_t* att_qkv, const float* att_lse, uint16_t* att_out,
+                                    float att_scale, hipStream_t st) {
   dim3 grid((R + 63) / 64 + (job.slab ? job.nblk : 0));
   const float* G = static_cast<const float*>(Gv);
   const bool av = av_ok({Gv, Wq, X, lnw, lnb, dres, Ysave, U, O, Wo, W1, W2, dY, dO}, {});
+  const bool att = att_out != nullptr;  // the fused attention backward (chain kernel only)
+  if (att && !(av && al16(att_qkv) && al16(att_out) && al16(att_lse))) return false;
   if (av && C == 64 && H == 4 && grads.slab && (R % 64) == 0 &&
       ln_linear_post_attn_bwd_chain_launch(Gv, g_bf16, Wq, X, mean1, rstd1, lnw, lnb, dres, dlnw, dlnb, dWq, dbq, Ysave,
                                            mean2, rstd2, U, O, Wo, W1, W2, g2, be2, dY, dO, delta, grads, R, job, dr, nq,
-                                           st))
+                                           att_qkv, att_lse, att_out, att_scale, st))
     return true;
-  if (g_bf16) return false;
+  if (g_bf16 || att) return false;
   grid.y = split_tiles(R);
   grid.x = (R + 63) / 64 + (job.slab ? (job.nblk + (int)grid.y - 1) / (int)grid.y : 0);
 #define LPB(CC, NQ)                                                                                               \
@@ -1560,13 +1614,14 @@ static void ln_linear_bwd_t(const void* G, int g_rs, int N, const uint16_t* W, i
   constexpr int KP = 32 * NCH;
   const size_t smem = ln_linear_bwd_smem<NCH>();
   const bool av = av_ok({G, W, X, lnw, lnb, dres}, {N, g_rs, w_rs, Kin, x_rs, dres ? dres_rs : 0});
+  const int vf = av ? 0 : vec_flags(G, g_rs, N, W, w_rs, Kin, lnw, lnb);
   auto fn = av ? ln_linear_bwd_kernel<TG, TX, NCH, true> : ln_linear_bwd_kernel<TG, TX, NCH, false>;
   set_smem_once((const void*)fn);
   // + the appended slab-job workgroups; few tiles: several workgroups per tile (split_tiles)
   const int spl = split_tiles(R);
   const dim3 grid((R + 63) / 64 + (job.slab ? (job.nblk + spl - 1) / spl : 0), spl);
   hipLaunchKernelGGL(fn, grid, dim3(256), smem, st, (const TG*)G, g_rs, N, W, w_rs, Kin, (const TX*)X, x_rs,
-                     mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, dlnw, dlnb, dW, db, vrs, wrs, slab, R, ps, job);
+                     mean, rstd, lnw, lnb, dres, dres_rs, dX, dx_rs, dlnw, dlnb, dW, db, vrs, wrs, slab, R, ps, job, vf);
 }
 
 template <typename TG, typename TX>

@@ -289,12 +289,24 @@ def post_attn_ln_linear_fwd(o, x, wo, bo, g2, be2, eps, w1, b1, w2, b2, lnw, lnb
 
 def ln_linear_post_attn_bwd(g, wq, x, mean1, rstd1, lnw, lnb, dres, ll_grads, y, m2, r2, u, o, wo, w1, w2, g2, be2,
                             H, pa_grads, job_slab=None, job_dsts=(), job_offs=(), seed=None, site=0, p=0.0,
-                            zero_out=None):
+                            zero_out=None, att_qkv=None, att_lse=None, att_out=None, att_scale=0.0):
     """ln_linear_bwd of layer l+1 (dX = dZ of layer l, incl. dres) → post_attn_bwd of layer l,
-    both into slab targets."""
+    both into slab targets.  att_out: layer l's attention backward too (64 latents per sample,
+    csrc/chain.hip phase D), its dQKV written into att_out (R, 3C) bf16."""
     _run_job(job_slab, job_dsts, job_offs)
     dz = ln_linear_bwd(g, wq, x, mean1, rstd1, lnw, lnb, dres, True, *ll_grads, slab=True)
-    return post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, be2, H, pa_grads, slab=True, seed=seed, site=site, p=p)
+    dy, do, delta = post_attn_bwd(dz, y, m2, r2, u, o, wo, w1, w2, g2, be2, H, pa_grads, slab=True, seed=seed,
+                                  site=site, p=p)
+    if att_out is not None:
+        R, C = y.shape
+        B, N = R // 64, 64
+        q3 = att_qkv.view(B, N, 3 * C)
+        d3 = torch.empty(B, N, 3 * C, device=y.device)
+        attn_bwd(q3[:, :, :C], q3[:, :, C:2 * C], q3[:, :, 2 * C:], None, o.view(B, N, C), do.view(B, N, C),
+                 att_lse.view(B, N, H), delta.view(B, N, H), H, C // H, att_scale, p, seed, d3[:, :, :C],
+                 d3[:, :, C:2 * C], d3[:, :, 2 * C:], site=site)
+        att_out.view(R, 3 * C).copy_(d3.view(R, 3 * C))
+    return dy, do, delta
 
 
 def _heads(x, H):

@@ -49,6 +49,10 @@ BF16_DQKV = True
 # the bf16 self-attention backward carries the pending slab reduction in appended workgroups
 # (1.429 → 1.377 ms on the headline step against the next chain kernel carrying it, r5)
 ATTN_SLAB = True
+# 64-latent blocks (one sample per 64-row tile): the boundary kernel of layers i → i-1 also runs
+# layer i-1's attention backward (csrc/chain.hip phase D) and hands its dQKV on as bf16 — one
+# launch per layer instead of two (tests/test_model_gpu.py compares both settings)
+CHAIN_ATT = True
 TALL_ROWS = 1 << 17  # kTallRows in csrc/binding.cpp: taller projections stream their dW (wgrad kernel)
 
 
@@ -1107,19 +1111,28 @@ class _SABlockFn(torch.autograd.Function):
             t_ = torch.empty((B, N, 3 * C), **f32)
             return t_, (dict(zero_out=t_) if zp else {})
 
+        # N = 64: layer i-1's attention backward runs inside the boundary kernel of layers i → i-1
+        fuse_att = (CHAIN_ATT and K is not emulation and zp == 0 and C == 64 and H == 4 and N == 64 and D == 16
+                    and R % 64 == 0 and hasattr(K, "ln_linear_post_attn_bwd"))
         dqkv_next, zkw = new_dqkv(L - 1)
         ho, _LOOKAHEAD["bwd_q"] = _LOOKAHEAD["bwd_q"], None
         if ho is not None and ho["key"] != getattr(ctx, "out_ptr", None):
             raise RuntimeError("fused encoder: a cross-attention layer handed its query-path backward to the wrong "
                                "self-attention block")
+        att_first = {}  # layer L-1's attention backward inside the first boundary kernel (fused)
         if ho is not None:
             # the next cross-attention layer's LN + query-projection backward (dX = this block's
             # dZ) fused with the last layer's post-attention backward
+            # (the chain kernel takes a query-projection hand-off: a C-row wq, fp32 G; a decoder's
+            # 2C-wide K|V hand-off runs on the row-pass kernel, without phase D)
+            if fuse_att and ho["g"].dtype == torch.float32 and ho["wq"].shape[0] in (C, 3 * C):
+                dqkv_next, zkw = torch.empty((B, N, 3 * C), device=dz.device, dtype=torch.bfloat16), {}
+                att_first = dict(att_qkv=S[L - 1][1], att_lse=S[L - 1][5], att_out=dqkv_next, att_scale=scale)
             sl = _GradSlab(R, [C, C, C * C, C] + PA_SIZES(C), dz2)
             tg = sl.targets()
             dy, do, delta = K.ln_linear_post_attn_bwd(ho["g"], ho["wq"], ho["x"], ho["mean1"], ho["rstd1"], ho["lnw"],
                                                       ho["lnb"], ho["dres"], tg[:4], *pa_args(L - 1), H, tg[4:],
-                                                      **_take_job(), **drop(L - 1), **zkw)
+                                                      **_take_job(), **drop(L - 1), **zkw, **att_first)
             sl.defer(K, ho["ll_dsts"] + pa_dsts(P[L - 1]))
         else:
             sl = _GradSlab(R, PA_SIZES(C), dz2)
@@ -1131,19 +1144,25 @@ class _SABlockFn(torch.autograd.Function):
             xl, qkv, mean1, rstd1, o, lse, y, m2, r2, u = S[i]
             qkv3 = qkv.view(B, N, 3 * C)
             dqkv = dqkv_next
-            # the bf16 variant carries the previous kernel's slab reduction on the CUs it shares with
-            # its tiles (two workgroups per CU); the chain kernel after it then carries none
-            K.attn_bwd(qkv3[:, :, :C], qkv3[:, :, C:2 * C], qkv3[:, :, 2 * C:], None, o, do.view(B, N, C), lse,
-                       delta.view(B, N, H), H, D, scale, ctx.p, ctx.seed, dqkv[:, :, :C], dqkv[:, :, C:2 * C],
-                       dqkv[:, :, 2 * C:], site=i, dq_zeroed=bool(zp & 1), kv_zeroed=bool(zp & 2),
-                       **(_take_job() if ATTN_SLAB and dqkv.dtype == torch.bfloat16 else {}))
+            if not (fuse_att and (i < L - 1 or att_first)):  # (fused: a boundary kernel already ran it)
+                # the bf16 variant carries the previous kernel's slab reduction on the CUs it shares
+                # with its tiles (two workgroups per CU); the chain kernel after it then carries none
+                K.attn_bwd(qkv3[:, :, :C], qkv3[:, :, C:2 * C], qkv3[:, :, 2 * C:], None, o, do.view(B, N, C), lse,
+                           delta.view(B, N, H), H, D, scale, ctx.p, ctx.seed, dqkv[:, :, :C], dqkv[:, :, C:2 * C],
+                           dqkv[:, :, 2 * C:], site=i, dq_zeroed=bool(zp & 1), kv_zeroed=bool(zp & 2),
+                           **(_take_job() if ATTN_SLAB and dqkv.dtype == torch.bfloat16 else {}))
             if i > 0:
-                dqkv_next, zkw = new_dqkv(i - 1)
+                att = {}
+                if fuse_att:  # layer i-1's attention backward in phase D: its dQKV out, bf16
+                    dqkv_next, zkw = torch.empty((B, N, 3 * C), device=dz.device, dtype=torch.bfloat16), {}
+                    att = dict(att_qkv=S[i - 1][1], att_lse=S[i - 1][5], att_out=dqkv_next, att_scale=scale)
+                else:
+                    dqkv_next, zkw = new_dqkv(i - 1)
                 sl = _GradSlab(R, LL_SIZES(C) + PA_SIZES(C), dz2)
                 tg = sl.targets()
                 dy, do, delta = K.ln_linear_post_attn_bwd(dqkv.view(R, 3 * C), bws[i][0], xl, mean1, rstd1, P[i][0],
                                                           P[i][1], dy, tg[:4], *pa_args(i - 1), H, tg[4:],
-                                                          **_take_job(), **drop(i - 1), **zkw)
+                                                          **_take_job(), **drop(i - 1), **zkw, **att)
                 sl.defer(K, ll_dsts(P[i]) + pa_dsts(P[i - 1]))
             elif getattr(ctx, "handoff", None) is not None:
                 # the producing cross-attention layer runs this LN1/QKV backward fused with its

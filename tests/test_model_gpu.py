@@ -532,3 +532,32 @@ def test_bf16_dqkv_handoff_is_bitwise_neutral(monkeypatch):
     assert a.keys() == b.keys()
     for n in a:
         assert torch.equal(a[n], b[n]), n
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_chain_fused_attention_backward_matches_separate(monkeypatch, p):
+    """64-latent blocks (``ops.fused.CHAIN_ATT``): the boundary kernel that also runs the layer
+    below's attention backward gives the gradients of the separate attention-backward launches
+    (same kernels' maths, bf16 dQKV hand-off), with and without dropout."""
+    from perceiver_io_amd import ops
+    from perceiver_io_amd.ops import fused
+
+    seed = torch.tensor([24681357], dtype=torch.int64, device="cuda")
+    monkeypatch.setattr(ops.fused, "_seed", lambda p_, device: seed if p_ > 0 else None)
+    res = []
+    for flag in (False, True):
+        monkeypatch.setattr(fused, "CHAIN_ATT", flag)
+        torch.manual_seed(6)
+        lit = _mlm_dropout(p)
+        m = lit.model.train()
+        ids = torch.randint(3, 500, (6, 96), device="cuda")
+        pad = torch.zeros(6, 96, dtype=torch.bool, device="cuda")
+        pad[2, 60:] = True
+        with torch.no_grad():
+            xm, lab = m.masking(ids, pad, generator=torch.Generator(device="cuda").manual_seed(2))
+        loss = m.loss(ids, pad, labels=lab, x_masked=xm)
+        loss.backward()
+        res.append((loss.item(), _grads(m)))
+    (l0, g0), (l1, g1) = res
+    assert l0 == l1
+    _check_grads(g1, g0, tol=2e-2)

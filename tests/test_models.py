@@ -274,6 +274,9 @@ def test_cross_self_attention_boundary_fusion(latents, monkeypatch):
     kernel's shape) a block's last kernel also computes the next cross layer's LN + query
     projection, whose backward comes back to the block.  Same outputs / gradients as unfused."""
     monkeypatch.setattr(ops.fused, "WGRAD_SLAB", True)
+    # the attention-backward fusion of 64-latent blocks changes which dQKV are bf16 (its own test:
+    # tests/test_models.py test_chain_fused_attention_plumbing_emulated)
+    monkeypatch.setattr(ops.fused, "CHAIN_ATT", False)
     torch.manual_seed(4)
     m = mlm_model(n=latents, layers=3, sa=2)
     enc = m.encoder
@@ -413,3 +416,50 @@ def test_classifier_loss_matches_logits_cross_entropy():
         if n in g:
             torch.testing.assert_close(p.grad, g[n], msg=n)
     assert isinstance(m.decoder.output_adapter, ClassificationOutputAdapter)
+
+
+def test_chain_fused_attention_plumbing_emulated(monkeypatch):
+    """64-latent blocks (``ops.fused.CHAIN_ATT``): the executor hands each boundary kernel the
+    layer below's Q|K|V, LSE and a bf16 dQKV buffer and skips that layer's attention-backward
+    launch (emulated kernels; the HIP kernel is compared in tests/test_attn_bwd_selfattn_gpu.py):
+    same forward, gradients within the bf16 rounding of the handed-on dQKV, and one
+    attention-backward launch per block instead of one per layer."""
+    monkeypatch.setattr(ops.fused, "WGRAD_SLAB", True)
+    torch.manual_seed(5)
+    m = mlm_model(n=64, layers=3, sa=3)
+    enc = m.encoder
+    x = torch.randint(3, 300, (2, 64))
+    pad = torch.zeros(2, 64, dtype=torch.bool)
+    pad[1, 40:] = True
+    emu = ops.emulation
+    calls = {}
+
+    class Counting:  # not the emulation module itself: the executor takes the kernel paths
+        def __getattr__(self, name):
+            calls[name] = calls.get(name, 0) + 1
+            return getattr(emu, name)
+
+    w = None
+    res = []
+    for flag in (False, True):
+        with monkeypatch.context() as mp:
+            mp.setattr(ops.fused, "kernels", lambda t: Counting())
+            mp.setattr(ops.fused, "CHAIN_ATT", flag)
+            calls.clear()
+            enc.zero_grad(set_to_none=True)
+            out = ops.fused.encoder_forward(enc, x, pad)
+            if w is None:
+                w = torch.randn_like(out)
+            (out * w).sum().backward()
+            res.append((out.detach(), {n: p.grad.clone() for n, p in enc.named_parameters() if p.grad is not None},
+                        dict(calls)))
+    (o0, g0, c0), (o1, g1, c1) = res
+    torch.testing.assert_close(o1, o0, rtol=0, atol=0)
+    # 3 blocks × 3 layers + 3 cross layers: 12 attention-backward launches unfused; fused, the 3
+    # cross layers' and one self-attention layer's (the decoder-side block's last layer, whose
+    # post-attention backward is not a chain kernel) remain
+    assert (c0["attn_bwd"], c1["attn_bwd"]) == (12, 4), (c0["attn_bwd"], c1["attn_bwd"])
+    assert set(g0) == set(g1)
+    for n in g0:
+        e = ((g1[n] - g0[n]).norm() / (g0[n].norm() + 1e-12)).item()
+        assert e < 2e-2, (n, e)
