@@ -36,7 +36,7 @@
 namespace pio {
 
 static __device__ unsigned pio_persist_err;  // sticky: bit 0 = a bounded spin timed out, bit 1 = bad ticket
-// polls before a wait gives up (≈1 s); tests lower it to force the timeout path
+// polls before a wait gives up (≈1 s); 0 (tests only) makes every wait time out at once
 static __device__ unsigned pio_persist_spin_limit = 1u << 21;
 
 void persist_set_spin_limit(unsigned n) {
@@ -78,6 +78,10 @@ typedef __attribute__((address_space(1))) unsigned gu32;  // shared words: globa
 // sticky error word and returns false (the caller stops waiting for the rest of the launch)
 __device__ __forceinline__ bool wait_count(unsigned* p, unsigned target) {
   const unsigned lim = pio_persist_spin_limit;
+  if (lim == 0) {  // test hook (persist_set_spin_limit(0)): every wait times out
+    atomicOr(&pio_persist_err, 1u);
+    return false;
+  }
   for (unsigned s = 0; __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++s) {
     if (s > lim) {
       atomicOr(&pio_persist_err, 1u);
@@ -115,7 +119,11 @@ __device__ __forceinline__ void publish_count(unsigned* p) {
 // KLDS: the sample's K rows are staged in LDS once per workgroup (as V is) and every wave reads
 // its head's fragments from there — the two query-block waves of a head no longer both fetch the
 // head's K through the memory system (64 → 32 KB of K loads per workgroup and layer)
-template <int MAXKT, bool KLDS, bool ADROP>
+// LOCAL (N = 64: the workgroup's tile is the whole sample): layer i + 1's Q, K and V rows are
+// also written into the workgroup's LDS images as layer i produces them, so layers ≥ 1 load
+// nothing from global memory before their attention and need no drain before the hand-off (the
+// rows still go to QKVn for the backward); MAXKT = 4 then (2 key tiles used).
+template <int MAXKT, bool KLDS, bool ADROP, bool LOCAL = false>
 __global__ __launch_bounds__(512) void sa_block_fwd_kernel(SABlockFwdArgs a) {
   constexpr int C = 64, H = 4, D = 16, LD = C + 8, LDV = C + 8, C3 = 3 * C, NT = 512;
   constexpr int NVI = MAXKT * 32 * 8 / NT;  // 16-byte V chunks per thread
@@ -130,7 +138,9 @@ __global__ __launch_bounds__(512) void sa_block_fwd_kernel(SABlockFwdArgs a) {
   __shared__ __attribute__((aligned(16))) bf16x8 sX[2][8 * 64];
   __shared__ __attribute__((aligned(16))) float2 sR[2][8 * 16];
   __shared__ __attribute__((aligned(16))) uint16_t sOnes[16 * 16];
+  __shared__ __attribute__((aligned(16))) uint16_t sQl[LOCAL ? 64 * LD : 8];  // LOCAL: the next layer's Q rows
   __shared__ int sTicket, sLast;
+  static_assert(!LOCAL || KLDS, "LOCAL keeps K in LDS");
   PIO_WG_BEGIN();
   if (threadIdx.x == 0)
     sTicket = (int)__hip_atomic_fetch_add((gu32*)(a.sync + kSyncTicket), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -196,22 +206,25 @@ __global__ __launch_bounds__(512) void sa_block_fwd_kernel(SABlockFwdArgs a) {
     }
     const __amdgpu_buffer_rsrc_t rq = pbuf(qkv, qkv_bytes);
     bf16x8 kf[MAXKT], qf, vr[NVI], kr[KLDS ? NVI : 1];
-    if constexpr (KLDS) {
+    const bool gload = !(LOCAL && i > 0);  // LOCAL layers ≥ 1: Q / K / V are already in LDS (uniform)
+    if (gload) {
+      if constexpr (KLDS) {
+#pragma unroll
+        for (int k = 0; k < NVI; ++k) {
+          const int c = threadIdx.x + NT * k, key = c >> 3, col = (c & 7) * 8;
+          kr[k] = ld16_sc1(rq, key < N ? ((rb + key) * C3 + C + col) * 2u : kOffNone);
+        }
+      } else {
+#pragma unroll
+        for (int kt = 0; kt < MAXKT; ++kt)
+          kf[kt] = ld16_sc1(rq, kt < nkt ? ((rb + 32 * kt + r) * C3 + C + h * D + 8 * hh) * 2u : kOffNone);
+      }
+      qf = ld16_sc1(rq, ((unsigned)(m0 + 32 * qb + r) * C3 + h * D + 8 * hh) * 2u);
 #pragma unroll
       for (int k = 0; k < NVI; ++k) {
         const int c = threadIdx.x + NT * k, key = c >> 3, col = (c & 7) * 8;
-        kr[k] = ld16_sc1(rq, key < N ? ((rb + key) * C3 + C + col) * 2u : kOffNone);
+        vr[k] = ld16_sc1(rq, key < N ? ((rb + key) * C3 + 2 * C + col) * 2u : kOffNone);
       }
-    } else {
-#pragma unroll
-      for (int kt = 0; kt < MAXKT; ++kt)
-        kf[kt] = ld16_sc1(rq, kt < nkt ? ((rb + 32 * kt + r) * C3 + C + h * D + 8 * hh) * 2u : kOffNone);
-    }
-    qf = ld16_sc1(rq, ((unsigned)(m0 + 32 * qb + r) * C3 + h * D + 8 * hh) * 2u);
-#pragma unroll
-    for (int k = 0; k < NVI; ++k) {
-      const int c = threadIdx.x + NT * k, key = c >> 3, col = (c & 7) * 8;
-      vr[k] = ld16_sc1(rq, key < N ? ((rb + key) * C3 + 2 * C + col) * 2u : kOffNone);
     }
     PTS(1);
     // ---- stage this layer's weights / vectors (prefetched) and the sample's V rows ----
@@ -222,15 +235,18 @@ __global__ __launch_bounds__(512) void sa_block_fwd_kernel(SABlockFwdArgs a) {
     }
     if ((int)threadIdx.x < 7 * C) sVec[threadIdx.x] = pv;
     if ((int)threadIdx.x < 3 * C) sVec[7 * C + threadIdx.x] = pq;
+    if (gload) {
 #pragma unroll
-    for (int k = 0; k < NVI; ++k) {
-      const int c = threadIdx.x + NT * k, key = c >> 3, col = (c & 7) * 8;
-      *reinterpret_cast<bf16x8*>(sV + key * LDV + col) = vr[k];
-      if constexpr (KLDS) *reinterpret_cast<bf16x8*>(sK + key * LDV + col) = kr[k];
+      for (int k = 0; k < NVI; ++k) {
+        const int c = threadIdx.x + NT * k, key = c >> 3, col = (c & 7) * 8;
+        *reinterpret_cast<bf16x8*>(sV + key * LDV + col) = vr[k];
+        if constexpr (KLDS) *reinterpret_cast<bf16x8*>(sK + key * LDV + col) = kr[k];
+      }
     }
     PTS(2);
     lds_sync();
     PTS(3);
+    if (!gload) qf = *reinterpret_cast<const bf16x8*>(sQl + (32 * qb + r) * LD + h * D + 8 * hh);
 
 
     // ---- attention: head h, query block qb (sa_layer_fwd_chain8_kernel) ----
@@ -376,6 +392,11 @@ __global__ __launch_bounds__(512) void sa_block_fwd_kernel(SABlockFwdArgs a) {
             pk.x = pack2(v[p][0], v[p][1]);
             pk.y = pack2(v[p][2], v[p][3]);
             st8_sc1(rn, ((unsigned)gr * (unsigned)nq + q * C + 16 * (2 * hf + p) + 4 * g) * 2u, pk);
+            if (LOCAL && i + 1 < a.L) {  // the next layer's row lr (= its key lr) into the LDS images;
+              // every wave's reads of this layer's sK / sV ended at the barrier after the attention
+              uint16_t* dst = q == 0 ? sQl + lr * LD : q == 1 ? sK + lr * LDV : sV + lr * LDV;
+              *reinterpret_cast<uint2*>(dst + 16 * (2 * hf + p) + 4 * g) = pk;
+            }
           }
         }
       }
@@ -383,8 +404,10 @@ __global__ __launch_bounds__(512) void sa_block_fwd_kernel(SABlockFwdArgs a) {
     PTS(9);
     if (i + 1 < a.L) {
       // publish the next layer's QKV rows to the sample; the barrier inside also ends every
-      // wave's reads of this layer's LDS images (the next layer overwrites them)
-      publish_count(cnt);
+      // wave's reads of this layer's LDS images (the next layer overwrites them).  LOCAL: no
+      // other workgroup reads them — the barrier only, no drain of the stores
+      if constexpr (LOCAL) lds_sync();
+      else publish_count(cnt);
       prefetch(i + 1);
     }
   }
@@ -405,8 +428,14 @@ bool sa_block_fwd_launch(const SABlockFwdArgs& a, hipStream_t st) {
     if (i + 1 < a.L && nq != 192) return false;  // layers before the last feed the next layer's QKV
   }
   const dim3 grid(a.R / 64);  // the sample's K rows staged in LDS (KLDS; profiles/r5_persist.md)
-  if (a.dr.thresh) hipLaunchKernelGGL((sa_block_fwd_kernel<8, true, true>), grid, dim3(512), 0, st, a);
-  else hipLaunchKernelGGL((sa_block_fwd_kernel<8, true, false>), grid, dim3(512), 0, st, a);
+  if (a.N == 64) {  // one tile per sample: the Q / K / V hand-off stays in the workgroup's LDS
+    if (a.dr.thresh) hipLaunchKernelGGL((sa_block_fwd_kernel<4, true, true, true>), grid, dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((sa_block_fwd_kernel<4, true, false, true>), grid, dim3(512), 0, st, a);
+  } else if (a.dr.thresh) {
+    hipLaunchKernelGGL((sa_block_fwd_kernel<8, true, true>), grid, dim3(512), 0, st, a);
+  } else {
+    hipLaunchKernelGGL((sa_block_fwd_kernel<8, true, false>), grid, dim3(512), 0, st, a);
+  }
   return true;
 }
 

@@ -626,7 +626,7 @@ class _LayerFn(torch.autograd.Function):
             P, pes, pesq, wt, kin = imp
             o, lse = K.attn_fwd_pe(q3, P, xkv2, pes, pesq, wt, H, scale, kin, EPS, 0)  # 0: one round of waves
         else:
-            nsplit = pick_splits(B, H, Nq, k3.shape[1])
+            nsplit = pick_splits(B, H, Nq, k3.shape[1], p_attn > 0)
             o, lse = K.attn_fwd(q3, k3, v3, kmask, H, D, scale, p_attn, seed, nsplit)
         o2 = o.view(B * Nq, C)
         # a batch-broadcast query stream (Bq = 1) is added as the residual without expanding it;
