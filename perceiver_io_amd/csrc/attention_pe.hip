@@ -83,7 +83,8 @@ template <int NC, int NS>
 __global__ __launch_bounds__(256, 2) void attn_fwd_pe_fact_kernel(PeFwdArgs a) {
   constexpr int LDT = PD + 8;       // augmentation tile row stride (bf16)
   constexpr int LKV = 2 * PD + 8;   // P' chunk row stride: K columns [0, 32), V columns [32, 64)
-  static_assert(NC + 2 <= 8, "augmentation rows live in accumulator registers 0..3 of both halves");
+  static_assert(NC + 4 <= 8, "augmentation rows live in accumulator registers 0..3 of both halves; "
+                            "score slots NC + 1..NC + 3 carry the folded softmax offset");
   __shared__ __attribute__((aligned(16))) uint16_t sKV[2][32 * LKV];
   __shared__ __attribute__((aligned(16))) uint16_t sA[4][NS][32 * LDT];  // [key][aug row], rows ≥ NC + 2 zero
   __shared__ __attribute__((aligned(16))) float sCL[4][NS][2][32];       // [key]: rσ·scale_log2, log2 rσ
@@ -162,9 +163,18 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pe_fact_kernel(PeFwdArgs a) {
   for (int s = 0; s < NS; ++s) {
     om[s] = f32x16{};
     oa[s] = f32x16{};
-    m_run[s] = -1e30f;
+    m_run[s] = 0.f;  // folded into the score MFMA (qa[s][2] slots NC + 1..NC + 3), set by chunk 0
   }
-  const float sl2 = a.scale_log2;
+  const float sl2 = a.scale_log2, isl2 = 1.f / sl2;
+  auto set_offset = [&](int s) {  // −m_run[s] → the query augmentation's offset slots
+    const float nm = -m_run[s];
+    const uint16_t mh = f2bf(nm);
+    if (hh == 0) {
+      qa[s][2][NC + 1] = (short)mh;
+      qa[s][2][NC + 2] = (short)f2bf(nm - bf2f(mh));
+      qa[s][2][NC + 3] = (short)mh;
+    }
+  };
   const int nch = kend > kbeg ? (kend - kbeg + 31) / 32 : 0;  // an empty split (kbeg ≥ M) has none
   auto chunk = [&](int ci, auto masked_t) {
     constexpr bool masked = decltype(masked_t)::value;
@@ -194,6 +204,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pe_fact_kernel(PeFwdArgs a) {
         vrow[NC + 1] = (short)f2bf(var * rs);    // 1/rσ: row NC + 1 of P̃ᵀ·A = the denominator l
         *reinterpret_cast<bf16x8*>(&sA[w][s][r * LDT]) = vrow;
       }
+      // score slots NC + 1..NC + 3: 1 / (rσ·scale_log2) as bf16 hi, hi, lo against the queries'
+      // −m_run as hi, lo, hi — the MFMA subtracts the softmax offset (to ~2^-16 relative)
+      const float icv = var * rs * isl2;
+      const uint16_t ih = f2bf(icv);
+      au[NC + 1] = (short)ih;
+      au[NC + 2] = (short)ih;
+      au[NC + 3] = (short)f2bf(icv - bf2f(ih));
       ka[s] = hh == 0 ? au : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
     }
     __syncthreads();  // the chunk and the tables are in LDS; buffer (ci + 1) & 1 is free
@@ -225,21 +242,29 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pe_fact_kernel(PeFwdArgs a) {
         }
       }
       mt = xor32_max(mt);
-      // lazy offset: moved only when a score exceeds it by more than 2^8 (p̃ ≤ 2^8 is exact in fp32
-      // and in range for bf16), so the accumulators are rescaled on a handful of chunks, not on
-      // nearly every one (a new maximum among 32 queries is the rule for the first ~50 chunks)
-      const float m_new = mt > m_run[s] + 8.f ? mt : m_run[s];
-      const float alpha = fast_exp2(m_run[s] - m_new);
+      // the scores come out of the MFMA relative to the lazy offset m_run (no per-element
+      // subtraction).  The offset moves only when a score exceeds it by more than 2^8 (p̃ ≤ 2^8 is
+      // exact in fp32 and in range for bf16) or on the split's first chunk, so the accumulators
+      // are rescaled on a handful of chunks, not on nearly every one (a new maximum among 32
+      // queries is the rule for the first ~50 chunks)
+      const bool mv = ci == 0 || mt > 8.f;
+      if (__ballot(mv)) {
+        const float dm = mv ? mt : 0.f;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) sc[s][i] = fast_exp2(sc[s][i] - m_new);
-      if (__ballot(m_new != m_run[s])) {  // some query's offset moved: rescale
+        for (int i = 0; i < 16; ++i) sc[s][i] -= dm;
+        if (ci > 0) {  // chunk 0: nothing accumulated yet (and exp2(−dm) may overflow)
+          const float alpha = fast_exp2(-dm);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          om[s][i] *= alpha;
-          oa[s][i] *= alpha;
+          for (int i = 0; i < 16; ++i) {
+            om[s][i] *= alpha;
+            oa[s][i] *= alpha;
+          }
         }
+        m_run[s] += dm;
+        set_offset(s);
       }
-      m_run[s] = m_new;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sc[s][i] = fast_exp2(sc[s][i]);
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
         const bf16x8 pb = pack_acc(sc[s], ss);
@@ -283,7 +308,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_pe_fact_kernel(PeFwdArgs a) {
       *reinterpret_cast<float4*>(op + 8 * g + 4 * hh) = make_float4(ov[0], ov[1], ov[2], ov[3]);
     }
     if (hh == 0) {
-      a.MLpart[row * 2] = m_run[s] + cq[s] * sl2;
+      a.MLpart[row * 2] = (nch > 0 ? m_run[s] : -1e30f) + cq[s] * sl2;  // an empty split: l = 0
       a.MLpart[row * 2 + 1] = lsum;
     }
   }
