@@ -47,6 +47,8 @@ def derived(d, cus):
     if d.get("GRBM_GUI_ACTIVE") and "SQ_VALU_MFMA_BUSY_CYCLES" in d:
         x["mfma_util_pct"] = 100.0 * d["SQ_VALU_MFMA_BUSY_CYCLES"] / (d["GRBM_GUI_ACTIVE"] / 8.0 * cus * 4)
     if d.get("SQ_WAVE_CYCLES"):
+        if d.get("GRBM_GUI_ACTIVE"):  # resident waves per CU, averaged over the dispatch
+            x["waves_per_cu"] = d["SQ_WAVE_CYCLES"] / (d["GRBM_GUI_ACTIVE"] / 8.0 * cus)
         if "SQ_ACTIVE_INST_VALU" in d:
             x["valu_active_pct"] = 100.0 * d["SQ_ACTIVE_INST_VALU"] / d["SQ_WAVE_CYCLES"]
         if "SQ_WAIT_INST_ANY" in d:

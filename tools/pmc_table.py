@@ -20,10 +20,10 @@ def main(argv=None):
     a = ap.parse_args(argv)
     res = ps.load(a.dirs, a.match)
     rows = sorted(((d.get("SQ_WAVE_CYCLES", 0.0), k, d, ps.derived(d, a.cus)) for k, d in res.items()), reverse=True)
-    print("| kernel | waves | MFMA busy % | VALU active % (per wave) | wait % | LDS bank-conflict % | VALU / MFMA instr |")
-    print("|---|---:|---:|---:|---:|---:|---:|")
+    print("| kernel | waves | waves / CU (mean resident) | MFMA busy % | VALU active % (per wave) | wait % | LDS bank-conflict % | VALU / MFMA instr |")
+    print("|---|---:|---:|---:|---:|---:|---:|---:|")
     for _, k, d, x in rows[:a.top]:
-        print(f"| `{k[:72]}` | {d.get('SQ_WAVES', 0):.0f} | {x.get('mfma_util_pct', 0):.1f} | "
+        print(f"| `{k[:72]}` | {d.get('SQ_WAVES', 0):.0f} | {x.get('waves_per_cu', 0):.1f} | {x.get('mfma_util_pct', 0):.1f} | "
               f"{x.get('valu_active_pct', 0):.1f} | {x.get('wait_pct', 0):.1f} | {x.get('lds_conflict_pct', 0):.1f} | "
               f"{x.get('valu_per_mfma', 0):.1f} |")
 
