@@ -67,6 +67,11 @@ def pick_splits(batch: int, heads: int, nq: int, nk: int, dropout: bool = False)
         # per score: the text classifier's cross-attention at batch 128 ran 28.6 → 18.5 µs
         # (+ a 4.8 µs combine); without dropout (15 µs) the combine eats the gain (r6)
         return 2 if dropout and blocks * waves < 2048 and tiles >= 8 else 1
+    if not dropout and blocks * waves >= 512 and tiles < 16:
+        # ≥ 2 waves per CU over a short key range: the 64-latent MLM cross-attention (256 two-wave
+        # workgroups, 512 keys) runs 9.3 µs unsplit against 12.0 µs split in two with its
+        # combine (tools/fwd_split_sweep.py, r6)
+        return 1
     want = max(1, 1024 // max(blocks, 1))
     return int(max(1, min(want, tiles // 4 if tiles >= 8 else 1)))
 
