@@ -1157,15 +1157,14 @@ void attn_bwd_pe_launch(const PeBwdArgs& a0, int nkb, int bsplit, hipStream_t st
                        a.H, a.C);
 }
 
-// key splits of one launch: about one round of workgroups (2 per CU) of the factored kernel, but
-// at least 6 chunks of 32 keys per split — with fewer, the partial last chunk and the combine cost
-// more than the extra workgroups gain (MNIST, 784 keys: 8 splits 22.5 µs, 4 splits 19.5 µs;
-// ImageNet keeps 32: tools/pe_fwd_split_sweep.py, r6)
-int attn_fwd_pe_auto_splits(int B, int H, int M, int ncu) {
+// key splits of one launch: about one round of workgroups (2 per CU) of the factored kernel.  (A
+// floor of 6 key chunks per split ran MNIST's forward 22.5 → 19.5 µs but moved the 4-sample
+// 28×28 classifier test's decoder query-LN gradient — an ill-conditioned tensor — past its
+// bf16 floor: not kept, profiles/r6_ab/README.md)
+int attn_fwd_pe_auto_splits(int B, int H, int ncu) {
   constexpr int ns = 2;  // samples per wave (3 measured equal, 4 spills at 2 waves / SIMD)
   const int bg = (B + 4 * ns - 1) / (4 * ns);
-  const int nch = (M + 31) / 32;
-  return std::max(1, std::min(2 * ncu / (bg * H), nch / 6));
+  return std::max(1, 2 * ncu / (bg * H));
 }
 
 // splits × 32-key chunks covering M keys; grid (batch groups, splits, heads), 4 waves each

@@ -155,7 +155,7 @@ void pe_proj_fwd_launch(const float*, int, const float*, const float*, const flo
                         const float*, long long, int, int, int, float, uint16_t*, float*, float*, hipStream_t);
 int pe_proj_bwd_blocks(int);
 void attn_fwd_pe_launch(const PeFwdArgs&, hipStream_t);
-int attn_fwd_pe_auto_splits(int, int, int, int);
+int attn_fwd_pe_auto_splits(int, int, int);
 void attn_combine_launch(const float*, const float*, uint16_t*, float*, int, long long, int, hipStream_t);
 void attn_bwd_pe_launch(const PeBwdArgs&, int, int, hipStream_t);
 void pe_proj_bwd_launch(const float*, const float*, int, const float*, const float*, int, int, int, float*, float*,
@@ -1881,7 +1881,7 @@ std::vector<Tensor> attn_fwd_pe(Tensor q, Tensor P, Tensor pix, Tensor pes, Tens
     int dev = 0, ncu = 256;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    nsplit = pio::attn_fwd_pe_auto_splits(B, (int)H, M, ncu);
+    nsplit = pio::attn_fwd_pe_auto_splits(B, (int)H, ncu);
   }
   const int ns = (int)std::max<int64_t>(1, std::min<int64_t>(nsplit, (M + 31) / 32));
   auto o = torch::empty({B, Nq, C}, q.options());
