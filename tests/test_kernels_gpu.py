@@ -689,6 +689,26 @@ def test_attention_pe_implicit_kv(B, Bq, Nq, M, H, nc, bsplit, nsplit):
         close(a, b, 2e-2, n)
 
 
+@pytest.mark.parametrize("qscale,nsplit", [(6.0, 1), (6.0, 4), (0.05, 1), (0.05, 0)])
+def test_attention_pe_folded_offset_extreme_scores(qscale, nsplit):
+    """The factored forward subtracts its lazy softmax offset inside the score MFMA (bf16 hi / lo
+    splits of 1 / (rσ·scale_log2) against −m), not per score.  Peaked scores (queries × 6: tens
+    of log2 units, the offset moving on many of the 94 chunks of a split) and near-flat ones
+    (× 0.05) — O and the LSE against the fp32 reference."""
+    torch.manual_seed(17)
+    H, nc, M, B, Nq = 4, 3, 3000, 3, 32
+    C = 32 * H
+    P, pes, pesq, wt, kin = _pe_implicit_operands(M, H, nc)
+    pix = torch.randn(B * M, nc, device=DEV)
+    q = bf(torch.randn(B, Nq, C, device=DEV) * qscale)
+    scale = 1 / math.sqrt(32)
+    o1, l1 = _ext().attn_fwd_pe(q, P, pix, pes, pesq, wt, H, scale, kin, 1e-5, nsplit)
+    o3, l3 = _pe_fwd_fp32(q, P, pix, pes, pesq, wt, H, scale, kin, 1e-5)
+    close(o1, o3, 2e-2, "O vs fp32")
+    err, top = (l1.float() - l3).abs().max().item(), l3.abs().max().item()
+    assert err <= 1e-3 * top + 5e-3, ("LSE", err, top)
+
+
 def test_index_add_rows_and_sumsq():
     torch.manual_seed(11)
     dst = torch.randn(1000, 64, device=DEV)
