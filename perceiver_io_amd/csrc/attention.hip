@@ -233,13 +233,16 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_kernel(AttnArgs a, uint16_t
           }
       }
       if (a.drop_thresh) {  // uniform: the element loop above stays branch-free
+        // element index qi·Nk + key0 + 4hh + (32kh + acc_row(i, 0)): base product once (keep_elem_m)
+        uint32_t cm0 = ((uint32_t)qi * (uint32_t)a.Nk + (uint32_t)(key0 + 4 * hh)) * kHashM1;
+        asm volatile("" : "+v"(cm0));
+        const uint32_t hs = hash3_seed(dkey, (uint32_t)(b * a.H + h));
 #pragma unroll
         for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
-            const int key = key0 + 32 * kh + acc_row(i, hh);
-            const uint32_t idx = (uint32_t)qi * (uint32_t)a.Nk + (uint32_t)key;
-            s[kh][i] = keep_elem(dkey, (uint32_t)(b * a.H + h), idx, a.drop_thresh) ? s[kh][i] * a.drop_scale : 0.f;
+            const uint32_t cm = cm0 + (uint32_t)(32 * kh + acc_row(i, 0)) * kHashM1;
+            s[kh][i] = keep_elem_m(hs, cm, a.drop_thresh) ? s[kh][i] * a.drop_scale : 0.f;
           }
       }
       l_run = l_run * alpha + ls;
@@ -574,11 +577,16 @@ __global__ __launch_bounds__(64 * NW, (QR == 2 && !DRP) ? 4 : 1) void attn_bwd_k
         // hoisted into the prologue of the dropout-free path
         uint32_t nk = (uint32_t)a.Nk;
         asm volatile("" : "+s"(nk));
+        // element index (q0 + 4hh)·Nk + key + acc_row(i, 0)·Nk: base product once, the offsets'
+        // products wave-uniform (keep_elem_m)
+        uint32_t cm0 = ((uint32_t)(q0 + 4 * hh) * nk + (uint32_t)key) * kHashM1;
+        asm volatile("" : "+v"(cm0));
+        const uint32_t nkm = nk * kHashM1;
+        const uint32_t hs = hash3_seed(dkey, (uint32_t)(b * a.H + h));
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const float p = fast_exp2(kpad ? -INFINITY : S[i] * a.scale_log2 - lrow[i >> 2][i & 3]);
-          const uint32_t idx = (uint32_t)(q0 + acc_row(i, hh)) * nk + (uint32_t)key;
-          const bool keep = keep_elem(dkey, (uint32_t)(b * a.H + h), idx, a.drop_thresh);
+          const bool keep = keep_elem_m(hs, cm0 + (uint32_t)acc_row(i, 0) * nkm, a.drop_thresh);
           P[i] = keep ? p * a.drop_scale : 0.f;
           dS[i] = p * ((keep ? dP[i] * a.drop_scale : 0.f) - drow[i >> 2][i & 3]);
         }

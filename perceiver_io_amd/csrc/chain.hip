@@ -151,12 +151,14 @@ __global__ __launch_bounds__(512) void sa_layer_fwd_chain8_kernel(
               // P·V product sees P∘mask/(1−p); masks as attn_bwd regenerates them (stream b·H + h,
               // element q·N + key of the sample)
               const uint32_t dkey = drop_key(dr.seed, dr.site, 2u);
+              // element index (row)·N + 32(4ch + k) + 4hh + acc_row(i, 0) (keep_elem_m)
+              uint32_t cm0 = ((uint32_t)(m0 - rb + 32 * qb + r) * (uint32_t)N + (uint32_t)(32 * (4 * ch + k) + 4 * hh)) * kHashM1;
+              asm volatile("" : "+v"(cm0));
+              const uint32_t hs = hash3_seed(dkey, (uint32_t)(b * H + h));
 #pragma unroll
               for (int i = 0; i < 16; ++i) {
                 l_run += sc[k][i];
-                const uint32_t key = 32 * (4 * ch + k) + acc_row(i, hh);
-                const uint32_t idx = (uint32_t)(m0 - rb + 32 * qb + r) * (uint32_t)N + key;
-                sc[k][i] = keep_elem(dkey, (uint32_t)(b * H + h), idx, dr.thresh) ? sc[k][i] * dr.scale : 0.f;
+                sc[k][i] = keep_elem_m(hs, cm0 + (uint32_t)acc_row(i, 0) * kHashM1, dr.thresh) ? sc[k][i] * dr.scale : 0.f;
               }
             }
           }
@@ -653,11 +655,14 @@ __global__ __launch_bounds__(512) void ln_linear_post_attn_bwd_chain8_kernel(
           dS[i] = p * (dP[i] - drow[i >> 2][i & 3]);
         }
       } else {
+        // element index (32j + 4hh)·64 + key + acc_row(i, 0)·64 (keep_elem_m)
+        uint32_t cm0 = ((uint32_t)(32 * j + 4 * hh) * 64u + (uint32_t)key) * kHashM1;
+        asm volatile("" : "+v"(cm0));
+        const uint32_t hs = hash3_seed(dkey, (uint32_t)(b * 4 + ah));
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const float p = fast_exp2(S[i] * at.scale_log2 - lrow[i >> 2][i & 3]);
-          const uint32_t idx = (uint32_t)(32 * j + acc_row(i, hh)) * 64u + (uint32_t)key;
-          const bool keep = keep_elem(dkey, (uint32_t)(b * 4 + ah), idx, dr.thresh);
+          const bool keep = keep_elem_m(hs, cm0 + (uint32_t)acc_row(i, 0) * 64u * kHashM1, dr.thresh);
           P[i] = keep ? p * dr.scale : 0.f;
           dS[i] = p * ((keep ? dP[i] * dr.scale : 0.f) - drow[i >> 2][i & 3]);
         }

@@ -457,6 +457,22 @@ __device__ __forceinline__ bool keep_elem(uint32_t seed, uint32_t stream, uint32
   return hash3(seed, stream, idx) >= thresh;
 }
 
+// The same hash with the per-element index product hoisted: hash3(a, b, c) ==
+// hash3_m(hash3_seed(a, b), c · kHashM1).  Callers whose indices are a runtime base plus
+// compile-time (or wave-uniform) offsets form c · kHashM1 as base · kHashM1 + offset · kHashM1
+// (mod 2^32, exact): one full-rate add per element instead of a quarter-rate v_mul_lo_u32, bit
+// for bit the same masks.  The caller makes the base opaque inside its dropout branch (as
+// keep_elem does with idx).
+constexpr uint32_t kHashM1 = 0x85EBCA77u;
+__device__ __forceinline__ uint32_t hash3_seed(uint32_t a, uint32_t b) { return a * 0x9E3779B1u ^ (b + 0x7F4A7C15u); }
+__device__ __forceinline__ bool keep_elem_m(uint32_t hs, uint32_t cm, uint32_t thresh) {
+  uint32_t h = hs ^ cm;
+  h ^= h >> 15; h *= 0x2C1B3C6Du;
+  h ^= h >> 12; h *= 0x297A2D39u;
+  h ^= h >> 15;
+  return h >= thresh;
+}
+
 // Dropout configuration of one fused call.  The 64-bit seed lives in DEVICE memory: it is
 // drawn per forward call by torch's graph-safe generator (a 1-element randint on the step's
 // stream), so a replayed hipGraph reads a fresh seed every step instead of a value frozen at

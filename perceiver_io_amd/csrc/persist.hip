@@ -282,12 +282,14 @@ __global__ __launch_bounds__(512) void sa_block_fwd_kernel(SABlockFwdArgs a) {
               for (int e = 0; e < 16; ++e) sc[k][e] = fast_exp2(fmaf(sc[k][e], a.scale_log2, -m_new));
               if constexpr (ADROP) {  // attention-probability dropout, as sa_layer_fwd_chain8_kernel
                 const uint32_t dkey = drop_key(a.dr.seed, (uint32_t)i, 2u);
+                // element index (row)·N + 32(4ch + k) + 4hh + acc_row(e, 0) (keep_elem_m)
+                uint32_t cm0 = ((uint32_t)(m0 - (int)rb + 32 * qb + r) * (uint32_t)N + (uint32_t)(32 * (4 * ch + k) + 4 * hh)) * kHashM1;
+                asm volatile("" : "+v"(cm0));
+                const uint32_t hs = hash3_seed(dkey, (uint32_t)(b * H + h));
 #pragma unroll
                 for (int e = 0; e < 16; ++e) {
                   l_run += sc[k][e];
-                  const uint32_t key = 32 * (4 * ch + k) + acc_row(e, hh);
-                  const uint32_t idx = (uint32_t)(m0 - (int)rb + 32 * qb + r) * (uint32_t)N + key;
-                  sc[k][e] = keep_elem(dkey, (uint32_t)(b * H + h), idx, a.dr.thresh) ? sc[k][e] * a.dr.scale : 0.f;
+                  sc[k][e] = keep_elem_m(hs, cm0 + (uint32_t)acc_row(e, 0) * kHashM1, a.dr.thresh) ? sc[k][e] * a.dr.scale : 0.f;
                 }
               }
             }
