@@ -139,13 +139,15 @@ __device__ __forceinline__ void cl2_drop(float (&v)[2][4], const DropCfg& d, uin
   if (d.thresh == 0u) return;
   const uint32_t key = drop_key(d.seed, d.site, sub);
   const int g = lane_id() >> 4;
+  // element index gr·64 + 32hf + 4g + (16i + j): base product once (keep_elem_m)
+  uint32_t cm0 = ((uint32_t)gr * 64u + (uint32_t)(32 * hf + 4 * g)) * kHashM1;
+  asm volatile("" : "+v"(cm0));
+  const uint32_t hs = hash3_seed(key, 0u);
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t idx = (uint32_t)gr * 64u + (uint32_t)(16 * (2 * hf + i) + 4 * g + j);
-      v[i][j] = keep_elem(key, 0u, idx, d.thresh) ? v[i][j] * d.scale : 0.f;
-    }
+    for (int j = 0; j < 4; ++j)
+      v[i][j] = keep_elem_m(hs, cm0 + (uint32_t)(16 * i + j) * kHashM1, d.thresh) ? v[i][j] * d.scale : 0.f;
 }
 __device__ __forceinline__ void cl2_store_f32(float* __restrict__ Y, int ld, int gr, int hf, const float (&v)[2][4]) {
   const int g = lane_id() >> 4;

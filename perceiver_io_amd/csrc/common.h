@@ -439,38 +439,29 @@ __device__ __forceinline__ void gelu_pair(float x, float& gelu, float& grad) {
 }
 
 // ---- counter-based RNG for dropout (regenerated in backward, no mask storage) -------
-__device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
-  // a few rounds of a murmur-style mixer over (seed, stream, index)
-  uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u);
-  h ^= c * 0x85EBCA77u;
+// hash3(a, b, c): a few rounds of a murmur-style mixer over (seed, stream, index); the text
+// masking kernel (elementwise.hip) and ops/emulation.py use it as is
+constexpr uint32_t kHashM1 = 0x85EBCA77u;
+__device__ __forceinline__ uint32_t hash3_seed(uint32_t a, uint32_t b) { return a * 0x9E3779B1u ^ (b + 0x7F4A7C15u); }
+__device__ __forceinline__ uint32_t hash3_mix(uint32_t h) {
   h ^= h >> 15; h *= 0x2C1B3C6Du;
   h ^= h >> 12; h *= 0x297A2D39u;
   h ^= h >> 15;
   return h;
 }
-// keep with probability (1-p): threshold = p * 2^32.  The empty asm makes idx opaque at the call
-// site: every caller sits inside a dropout-enabled branch, and without it the compiler hoists
-// the hash's per-element multiplies (hundreds of quarter-rate v_mul_lo_u32) out of the loops
-// and the branch into the kernel prologue, where they run even with dropout off.
-__device__ __forceinline__ bool keep_elem(uint32_t seed, uint32_t stream, uint32_t idx, uint32_t thresh) {
-  asm volatile("" : "+v"(idx));
-  return hash3(seed, stream, idx) >= thresh;
+__device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
+  return hash3_mix(hash3_seed(a, b) ^ c * kHashM1);
 }
-
-// The same hash with the per-element index product hoisted: hash3(a, b, c) ==
-// hash3_m(hash3_seed(a, b), c · kHashM1).  Callers whose indices are a runtime base plus
-// compile-time (or wave-uniform) offsets form c · kHashM1 as base · kHashM1 + offset · kHashM1
-// (mod 2^32, exact): one full-rate add per element instead of a quarter-rate v_mul_lo_u32, bit
-// for bit the same masks.  The caller makes the base opaque inside its dropout branch (as
-// keep_elem does with idx).
-constexpr uint32_t kHashM1 = 0x85EBCA77u;
-__device__ __forceinline__ uint32_t hash3_seed(uint32_t a, uint32_t b) { return a * 0x9E3779B1u ^ (b + 0x7F4A7C15u); }
+// dropout keep test (probability 1 − p, threshold p·2^32) of element c, called with
+// hs = hash3_seed(seed, stream) and cm = c·kHashM1: the dropout kernels form cm as
+// base·kHashM1 + offset·kHashM1 (mod 2^32, exact) with compile-time or wave-uniform offsets, so
+// each element costs one full-rate add instead of a quarter-rate v_mul_lo_u32 — bit for bit
+// hash3(seed, stream, c) >= thresh.  Each caller makes the base opaque (empty asm) inside its
+// dropout branch: otherwise the compiler hoists the per-element multiplies (hundreds of
+// quarter-rate v_mul_lo_u32) out of the loops and the branch into the kernel prologue, where
+// they run even with dropout off.
 __device__ __forceinline__ bool keep_elem_m(uint32_t hs, uint32_t cm, uint32_t thresh) {
-  uint32_t h = hs ^ cm;
-  h ^= h >> 15; h *= 0x2C1B3C6Du;
-  h ^= h >> 12; h *= 0x297A2D39u;
-  h ^= h >> 15;
-  return h >= thresh;
+  return hash3_mix(hs ^ cm) >= thresh;
 }
 
 // Dropout configuration of one fused call.  The 64-bit seed lives in DEVICE memory: it is
@@ -494,13 +485,15 @@ template <int NCH>
 __device__ __forceinline__ void drop_rows(float (&v)[NCH][8], const DropCfg& d, uint32_t sub, int gr, int C) {
   if (d.thresh == 0u) return;
   const uint32_t key = drop_key(d.seed, d.site, sub);
+  // element index gr·C + 8(t & 3) + (32j + e): base product once (keep_elem_m)
+  uint32_t cm0 = ((uint32_t)gr * (uint32_t)C + (uint32_t)(8 * (threadIdx.x & 3))) * kHashM1;
+  asm volatile("" : "+v"(cm0));
+  const uint32_t hs = hash3_seed(key, 0u);
 #pragma unroll
   for (int j = 0; j < NCH; ++j)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const uint32_t idx = (uint32_t)gr * (uint32_t)C + (uint32_t)(8 * ((threadIdx.x & 3) + 4 * j) + e);
-      v[j][e] = keep_elem(key, 0u, idx, d.thresh) ? v[j][e] * d.scale : 0.f;
-    }
+    for (int e = 0; e < 8; ++e)
+      v[j][e] = keep_elem_m(hs, cm0 + (uint32_t)(32 * j + e) * kHashM1, d.thresh) ? v[j][e] * d.scale : 0.f;
 }
 
 }  // namespace pio

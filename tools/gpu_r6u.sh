@@ -1,4 +1,4 @@
-# round-6 end evidence (after the PE offset fold and split rules): full GPU suite, smoke, every config's bench + step table
+# round-6 end evidence (after the PE offset fold, split rule and dropout hash hoist): full GPU suite, smoke, every config's bench + step table
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
