@@ -14,7 +14,8 @@
 //                     row block (second ticket) finalises the mean loss — no combine launch.
 //   pass 2 (backward) vocab × row split: logit tiles S = H·Wᵀ (vocab on the lane), p, dW += g·pᵀ·H
 //                     and db += g·Σ p, the one-hot terms dW[label] −= g·H[r], db[label] −= g of
-//                     each tile's few rows whose label the wave holds (a ballot scan per tile),
+//                     each tile's few rows whose label the wave holds (a ballot scan per tile;
+//                     a classifier-sized vocabulary subtracts it per logit in the tile instead),
 //                     partials stored into a slab row (or added); in appended workgroups the dH
 //                     rows g·u[r] with u[r] = Σ_v p·W − W[label] merged from pass 1's per-split
 //                     partials, scattered to their source positions.
@@ -38,6 +39,8 @@
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
 #error "this translation unit's sc1 hand-off protocol is validated on gfx950 (MI355X) only"
 #endif
+#include <algorithm>
+
 #include "common.h"
 
 namespace pio {
@@ -54,6 +57,11 @@ constexpr float kLN2 = 0.6931471805599453f;
 constexpr float kRescale = 8.f;  // lazy-rescale threshold (log2 units)
 constexpr float kRescaleSum = 256.f;  // 2^kRescale: a tile's Σ p above it takes the rescale branch
 constexpr int kCeMaxSplitsFwd = 16;  // ce2_num_splits caps the vocab splits of pass 1 here
+// pass 2 at a vocabulary this small (a classifier head: most tile rows' labels fall inside every
+// wave's 32 vocab entries) takes the one-hot term inside the tile, d = p − [label = v] (one
+// compare per logit), instead of the per-hit ballot scan, which would serialise on every row
+constexpr int kOneHotInTileMaxV = 256;
+constexpr int kDhRowsPerWg = 32;  // pass 2's appended dH workgroups: rows each (2 passes of 16)
 typedef float f2v __attribute__((ext_vector_type(2)));  // packed fp32 (v_pk_fma_f32 / v_pk_add_f32)
 
 // p = 2^(t·log2e − m) for the 16 logits of a tile (natural units) in packed pairs; returns Σ p
@@ -366,14 +374,16 @@ __global__ __launch_bounds__(256) void ce2_bwd_kernel(const uint16_t* __restrict
   using namespace ce2;
   __shared__ __attribute__((aligned(16))) uint16_t sH[2][HT * C];
   __shared__ __attribute__((aligned(16))) float sL[2][HT];  // lse·log2e; +inf for a row without a label
-  __shared__ int sLab[2][HT];                                  // the rows' labels (−1: none)
+  __shared__ __attribute__((aligned(16))) int sLab[2][HT];     // the rows' labels (−1: none)
   static_assert(HT == 64, "one tile row per lane in the one-hot scan");
   const int w = wave_id(), l = lane_id(), hh = l >> 5;
   const float g = gout[0] / fmaxf(count[0], 1.f);
-  if ((int)blockIdx.y == rsplit) {
+  if ((int)blockIdx.y >= rsplit) {
     // dH rows: u[r] = Σ_v p·W − W[label] merged from pass 1's split partials (a row per 16
-    // threads, 4 channels each), then dH[rowmap[r]] += g·u[r]
-    const int per = (M + gridDim.x - 1) / gridDim.x, r0 = blockIdx.x * per, r1 = min(M, r0 + per);
+    // threads, 4 channels each), then dH[rowmap[r]] += g·u[r]; the appended rows y ≥ rsplit of the
+    // grid, ≈ kDhRowsPerWg rows per workgroup
+    const int nb = (int)gridDim.x * ((int)gridDim.y - rsplit), bid = ((int)blockIdx.y - rsplit) * (int)gridDim.x + (int)blockIdx.x;
+    const int per = (M + nb - 1) / nb, r0 = bid * per, r1 = min(M, r0 + per);
     const int cq = threadIdx.x & 15;
     for (int r = r0 + (int)(threadIdx.x >> 4); r < r1; r += 16) {
       const int lab = (int)labels[r];
@@ -413,6 +423,7 @@ __global__ __launch_bounds__(256) void ce2_bwd_kernel(const uint16_t* __restrict
   }
   const int vl = 32 * w + (l & 31), vg = blockIdx.x * VB2 + vl;
   const bool vin = vg < V;
+  const bool small_v = V <= kOneHotInTileMaxV;
   // this lane's vocab row as the B operand (k = c = 16s + 8hh .. + 7)
   bf16x8 wb[4];
 #pragma unroll
@@ -484,6 +495,13 @@ __global__ __launch_bounds__(256) void ce2_bwd_kernel(const uint16_t* __restrict
         d[4 * q + 1] = fast_exp2(y0.y);
         d[4 * q + 2] = fast_exp2(y1.x);
         d[4 * q + 3] = fast_exp2(y1.y);
+        if (small_v) {  // uniform: the one-hot term in the tile (rows 32rb + 8q + 4hh + 0..3)
+          const int4 lb = *reinterpret_cast<const int4*>(&sLab[buf][32 * rb + 8 * q + 4 * hh]);
+          d[4 * q] -= lb.x == vg ? 1.f : 0.f;
+          d[4 * q + 1] -= lb.y == vg ? 1.f : 0.f;
+          d[4 * q + 2] -= lb.z == vg ? 1.f : 0.f;
+          d[4 * q + 3] -= lb.w == vg ? 1.f : 0.f;
+        }
         bs2 += f2v{d[4 * q], d[4 * q + 1]} + f2v{d[4 * q + 2], d[4 * q + 3]};
       }
       bsum += bs2.x + bs2.y;
@@ -498,7 +516,7 @@ __global__ __launch_bounds__(256) void ce2_bwd_kernel(const uint16_t* __restrict
     // the one-hot term of the tile's rows whose label is one of this wave's 32 vocab entries (on
     // average 64·32/V of them per tile: a ballot, rarely a hit): dW[label] −= H[r], db[label] −= 1
     // (g applied at the store), so the slab / accumulators hold the whole vocab gradient
-    {
+    if (!small_v) {
       const int v0w = blockIdx.x * VB2 + 32 * w;
       const int lb = sLab[buf][l];  // lane l: row l of the tile
       unsigned long long hits = __ballot(lb >= v0w && lb < v0w + 32);
@@ -592,7 +610,10 @@ void ce2_bwd_launch(const uint16_t* Hs, const int64_t* labels, const uint16_t* W
     (void)hipMemsetAsync(dW, 0, sizeof(float) * (size_t)V * ce2::C, st);
     (void)hipMemsetAsync(db, 0, sizeof(float) * (size_t)V, st);
   }
-  hipLaunchKernelGGL(ce2_bwd_kernel, dim3((V + ce2::VB2 - 1) / ce2::VB2, rsplit + 1), dim3(256), 0, st, Hs, labels, W, bias,
+  const int vb = (V + ce2::VB2 - 1) / ce2::VB2;
+  const int ndh = (M + ce2::kDhRowsPerWg - 1) / ce2::kDhRowsPerWg;  // dH workgroups wanted
+  const int ndy = std::max(1, (ndh + vb - 1) / vb);                   // appended grid rows
+  hipLaunchKernelGGL(ce2_bwd_kernel, dim3(vb, rsplit + ndy), dim3(256), 0, st, Hs, labels, W, bias,
                      lse, part_acc, part_ml, nsplit, gout, count, M, V, rsplit, tps, dW, db, slab, dH, rowmap, dh_rows);
 }
 
