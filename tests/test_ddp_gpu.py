@@ -8,6 +8,7 @@
   with the reducer forced on: the ready points fire during capture, their all-reduces run on the
   side stream inside the graph, and the replayed steps equal the plain single-GPU graph bitwise.
 """
+import gc
 import os
 import socket
 
@@ -128,6 +129,9 @@ def test_rccl_collectives_inside_the_step_graph():
         opt, red, eng = _run(model, lambda f: FlatGradReducer(f, in_graph=True, force=True), True, data)
         assert red.enabled and red.in_graph and not red.overlap and eng.replays == STEPS - 2
         assert red.launch_log == [] and len(red.buckets) == 1
+        eng = None
+        gc.collect()  # the captured graphs (with their collectives) before the reducer and the group
+        torch.cuda.synchronize()
         red.close()
         ref_model = _setup()
         ref_opt, _, _ = _run(ref_model, None, True, data)
@@ -136,6 +140,9 @@ def test_rccl_collectives_inside_the_step_graph():
         from perceiver_io_amd import ops
 
         ops.set_deterministic(False)
+        eng = None
+        gc.collect()
+        torch.cuda.synchronize()
         tdist.destroy_process_group()
 
 
