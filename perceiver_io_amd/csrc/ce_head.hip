@@ -362,6 +362,7 @@ __global__ __launch_bounds__(256) void ce2_fwd_kernel(const float* __restrict__ 
 // 64-row tiles (bf16 H, lse, labels) through LDS; dl = (2^(t − lse) − [label = v])·g;
 // dW[v] += dlᵀ·H, db[v] += Σ dl; partials stored into slab row y (or added atomically).
 // y = rsplit: dH[rowmap[r]] (+)= g·u[r] for the rows of slice x (appended workgroups).
+template <bool SMALLV>  // SMALLV: V ≤ kOneHotInTileMaxV, the one-hot term inside the tile
 __global__ __launch_bounds__(256) void ce2_bwd_kernel(const uint16_t* __restrict__ Hs, const int64_t* __restrict__ labels,
                                                       const uint16_t* __restrict__ W, const float* __restrict__ bias,
                                                       const float* __restrict__ lse, const float* __restrict__ part_acc,
@@ -423,7 +424,6 @@ __global__ __launch_bounds__(256) void ce2_bwd_kernel(const uint16_t* __restrict
   }
   const int vl = 32 * w + (l & 31), vg = blockIdx.x * VB2 + vl;
   const bool vin = vg < V;
-  const bool small_v = V <= kOneHotInTileMaxV;
   // this lane's vocab row as the B operand (k = c = 16s + 8hh .. + 7)
   bf16x8 wb[4];
 #pragma unroll
@@ -495,7 +495,7 @@ __global__ __launch_bounds__(256) void ce2_bwd_kernel(const uint16_t* __restrict
         d[4 * q + 1] = fast_exp2(y0.y);
         d[4 * q + 2] = fast_exp2(y1.x);
         d[4 * q + 3] = fast_exp2(y1.y);
-        if (small_v) {  // uniform: the one-hot term in the tile (rows 32rb + 8q + 4hh + 0..3)
+        if constexpr (SMALLV) {  // the one-hot term in the tile (rows 32rb + 8q + 4hh + 0..3)
           const int4 lb = *reinterpret_cast<const int4*>(&sLab[buf][32 * rb + 8 * q + 4 * hh]);
           d[4 * q] -= lb.x == vg ? 1.f : 0.f;
           d[4 * q + 1] -= lb.y == vg ? 1.f : 0.f;
@@ -516,7 +516,7 @@ __global__ __launch_bounds__(256) void ce2_bwd_kernel(const uint16_t* __restrict
     // the one-hot term of the tile's rows whose label is one of this wave's 32 vocab entries (on
     // average 64·32/V of them per tile: a ballot, rarely a hit): dW[label] −= H[r], db[label] −= 1
     // (g applied at the store), so the slab / accumulators hold the whole vocab gradient
-    if (!small_v) {
+    if constexpr (!SMALLV) {
       const int v0w = blockIdx.x * VB2 + 32 * w;
       const int lb = sLab[buf][l];  // lane l: row l of the tile
       unsigned long long hits = __ballot(lb >= v0w && lb < v0w + 32);
@@ -611,10 +611,16 @@ void ce2_bwd_launch(const uint16_t* Hs, const int64_t* labels, const uint16_t* W
     (void)hipMemsetAsync(db, 0, sizeof(float) * (size_t)V, st);
   }
   const int vb = (V + ce2::VB2 - 1) / ce2::VB2;
-  const int ndh = (M + ce2::kDhRowsPerWg - 1) / ce2::kDhRowsPerWg;  // dH workgroups wanted
-  const int ndy = std::max(1, (ndh + vb - 1) / vb);                   // appended grid rows
-  hipLaunchKernelGGL(ce2_bwd_kernel, dim3(vb, rsplit + ndy), dim3(256), 0, st, Hs, labels, W, bias,
-                     lse, part_acc, part_ml, nsplit, gout, count, M, V, rsplit, tps, dW, db, slab, dH, rowmap, dh_rows);
+  // appended dH grid rows: one row (vb workgroups) at a wide vocabulary — more cost the MLM head
+  // 3 µs (31.7 → 34.9 µs, r6) — and ≈ kDhRowsPerWg rows per workgroup at a classifier's few blocks
+  const int ndh = (M + ce2::kDhRowsPerWg - 1) / ce2::kDhRowsPerWg;
+  const int ndy = vb >= 16 ? 1 : std::max(1, (ndh + vb - 1) / vb);
+  if (V <= ce2::kOneHotInTileMaxV)
+    hipLaunchKernelGGL(ce2_bwd_kernel<true>, dim3(vb, rsplit + ndy), dim3(256), 0, st, Hs, labels, W, bias, lse, part_acc,
+                       part_ml, nsplit, gout, count, M, V, rsplit, tps, dW, db, slab, dH, rowmap, dh_rows);
+  else
+    hipLaunchKernelGGL(ce2_bwd_kernel<false>, dim3(vb, rsplit + ndy), dim3(256), 0, st, Hs, labels, W, bias, lse, part_acc,
+                       part_ml, nsplit, gout, count, M, V, rsplit, tps, dW, db, slab, dH, rowmap, dh_rows);
 }
 
 unsigned check_errors_ce_head(bool reset) { return pio_read_errors(reset); }
