@@ -1,4 +1,4 @@
-# round-6 end evidence (after the PE offset fold, split rule and dropout hash hoist): full GPU suite, smoke, every config's bench + step table
+# round-6 end evidence (after the PE offset fold, split rule, dropout hash hoist and CE small-vocab pass 2): full GPU suite, smoke, every config's bench + step table
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
